@@ -1,0 +1,138 @@
+/* include/plaincv_hip.h -- C ABI of libplaincv_hip.so (gfx950 / MI355X).
+ *
+ * The drop-in boundary for plainCV's transformer training hot path.  The
+ * reference (GeorgTirp/plainCV) is JAX/Flax/Optax: every op below replaces an
+ * XLA-emitted kernel behind one of its Python call sites (cited per entry).
+ *
+ * Conventions
+ *   - plain pointers + sizes; bf16 tensors are raw 16-bit words; "ld" = row
+ *     stride in elements (bf16 operands of GEMM/attention need ld % 8 == 0 and
+ *     16-byte aligned bases);
+ *   - every function returns int: 0 ok, <0 invalid argument (-1 EINVAL,
+ *     -2 alignment, -3 shape), >0 hipError_t;  pcv_last_error_string(code);
+ *   - every launch goes on the caller's `stream` (hipStream_t), with no host
+ *     synchronisation and no allocation, so a train step is hipGraph-capturable;
+ *   - the caller owns every buffer (kernels never allocate); accumulating
+ *     outputs ("+=") expect the caller to zero grads once per optimizer step.
+ */
+#ifndef PLAINCV_HIP_H
+#define PLAINCV_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- GEMM ----
+ * C = epi(alpha * op(A) . op(B)); A [M,K] (trans_a=0) or [K,M]; B [K,N]
+ * (trans_b=0) or [N,K].  Epilogue: +bias[N] -> act (1 GELU-tanh, writes the
+ * pre-activation to aux; 2 multiplies by gelu'(aux)) -> dropout -> +res_scale*res
+ * -> store (bf16, or fp32 with C = v + beta*C; split_k>1 = fp32 atomic accumulate).
+ * Replaces every flax nn.Dense / DenseGeneral / Conv(patch) contraction:
+ * models/vit_small.py:13-16,41-45,78-88,126; models/LM/transformer.py:194-201,
+ * 246-253,110-134,393-405 and their autodiff transposes. */
+int pcv_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
+                  int64_t lda, int64_t ldb, int64_t ldc, int trans_a, int trans_b,
+                  int64_t batch, int64_t stride_a, int64_t stride_b, int64_t stride_c,
+                  float alpha, float beta, int out_f32,
+                  const float* bias, const void* res, int64_t ldr, int64_t stride_r, int res_f32, float res_scale,
+                  void* aux, int64_t ldaux, int act,
+                  float dropout_rate, const uint32_t* seed, uint32_t site, int split_k, void* stream);
+
+/* ----------------------------------------------------------- attention ----
+ * Flash attention on the packed QKV activation (q/k/v = column blocks, head h
+ * at column h*head_dim); lse2[B,H,T] is log2-domain.  head_dim in {32,64,128}.
+ * Replaces flax SelfAttention's dot_product_attention (models/vit_small.py:41-45,
+ * broadcast dropout over batch/heads) and jax.nn.dot_product_attention(is_causal)
+ * (models/LM/transformer.py:233-240). */
+int pcv_attn_fwd(const void* q, const void* k, const void* v, int64_t ldq, void* out, int64_t ldo,
+                 float* lse2, int B, int T, int H, int head_dim, int causal,
+                 float dropout_rate, const uint32_t* seed, uint32_t site, void* stream);
+int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t ldq,
+                 const void* o, int64_t ldo, const void* dout, int64_t lddo,
+                 const float* lse2, float* delta_ws /* [B,H,T] */,
+                 void* dq, void* dk, void* dv, int64_t lddq,
+                 int B, int T, int H, int head_dim, int causal,
+                 float dropout_rate, const uint32_t* seed, uint32_t site, void* stream);
+
+/* --------------------------------------------------------------- norms ----
+ * flax LayerNorm (models/vit_small.py:38,52,124) on the fp32 residual stream,
+ * bf16 output; backward adds into dres (may alias dx) and accumulates dscale/dbias.
+ * flax RMSNorm (models/LM/transformer.py:41-47) on the bf16 residual stream. */
+int pcv_layernorm_fwd(const float* x, int64_t ldx, const float* scale, const float* bias, void* y,
+                      int64_t ldy, float* mean, float* rstd, int64_t R, int D, float eps, void* stream);
+int pcv_layernorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* scale,
+                      const float* mean, const float* rstd, const float* dres, int64_t ldres,
+                      float* dx, int64_t lddx, void* dx_bf16, int64_t lddxb, float* dscale, float* dbias,
+                      int64_t R, int D, void* stream);
+int pcv_rmsnorm_fwd(const void* x, int64_t ldx, const float* scale, void* y, int64_t ldy, float* rstd,
+                    int64_t R, int D, float eps, void* stream);
+int pcv_rmsnorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* scale,
+                    const float* rstd, const void* dres, int64_t ldres, void* dx, int64_t lddx,
+                    float* dscale, int64_t R, int D, void* stream);
+
+/* --------------------------------------------------------- elementwise ----
+ * RoPE, in place on the q|k column blocks (models/LM/embedding.py:28-66; backward = rotation by -theta). */
+int pcv_rope(void* qk, int64_t ld, int64_t R, int ncols, int T, int head_dim, const float* cos_tab,
+             const float* sin_tab, int backward, void* stream);
+/* SwiGLU h = silu(gate)*up on the packed [gate|up] activation (models/LM/transformer.py:110-134):
+ * gate at columns [0,F), up at [Fp, Fp+F) with Fp = F padded to 8; pad columns are written as 0. */
+int pcv_swiglu_fwd(const void* gu, int64_t ldgu, void* h, int64_t ldh, int64_t R, int F, int Fp, void* stream);
+int pcv_swiglu_bwd(const void* dh, int64_t lddh, const void* gu, int64_t ldgu, void* dgu, int64_t lddgu,
+                   int64_t R, int F, int Fp, void* stream);
+/* out = bf16(x * dropout_mask) (backward of an output dropout, models/vit_small.py:17). */
+int pcv_dropout_bwd_cast(const float* x, int64_t ldx, void* out, int64_t ldo, int64_t R, int N,
+                         float rate, const uint32_t* seed, uint32_t site, void* stream);
+int pcv_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+/* Advance the device-resident dropout seed (one per train step; hipGraph-replay safe). */
+int pcv_seed_next(uint32_t* seed, void* stream);
+/* out[c] += sum_r x[r,c]  (Dense bias gradients). */
+int pcv_colsum(const void* x, int64_t ld, int64_t R, int N, int x_f32, float* out, void* stream);
+/* ViT patch embedding input (models/vit_small.py:78-88, (kh,kw,c) flatten, /255) and token
+ * assembly cls|patches + pos_embedding + dropout (models/vit_small.py:95-109). */
+int pcv_vit_patchify(const uint8_t* img, void* out, int B, int H, int W, int C, int patch, void* stream);
+int pcv_vit_embed_fwd(const float* patch, const float* cls, const float* pos, float* x, void* x_bf16,
+                      int B, int T, int D, float rate, const uint32_t* seed, uint32_t site, void* stream);
+int pcv_vit_embed_bwd(const float* dx, void* dpatch, float* dcls, float* dpos, float* dbias,
+                      int B, int T, int D, float rate, const uint32_t* seed, uint32_t site, void* stream);
+/* nn.Embed gather / scatter-add (models/LM/transformer.py:361-369). */
+int pcv_embed_fwd(const int* ids, const void* table, int64_t ldt, void* out, int64_t ldo, int64_t R,
+                  int D, int V, int* oob_flag, void* stream);
+int pcv_embed_bwd(const int* ids, const void* dx, int64_t lddx, float* dtable, int64_t ldt, int64_t R,
+                  int D, int V, void* stream);
+
+/* ---------------------------------------------------------------- loss ----
+ * Softmax cross-entropy + argmax accuracy per row, gradient (softmax-onehot)*grad_scale
+ * (engine/flax_engine.py:13-22; train_lm.py:181-186).  pcv_mean2: deterministic means. */
+int pcv_xent_fwd_bwd(const void* logits, int64_t ld, int logits_f32, const int* labels, int64_t R, int V,
+                     float* row_loss, float* row_correct, void* dlogits, int64_t ldd, float grad_scale,
+                     void* stream);
+int pcv_mean2(const float* x, const float* y, int64_t n, float scale, float* out, void* stream);
+
+/* ----------------------------------------------------------- optimizer ----
+ * Multi-tensor AdamW over chunk tables {int64 start, int64 len} of the flat fp32
+ * buffers (optax.adamw at optim/factory.py:199-205; nesterov = the adam branch of
+ * optax.contrib.muon, factory.py:464-484).  step/gscale are device scalars. */
+int pcv_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, float* upd,
+                   const void* chunks, int nchunks, float lr, float b1, float b2, float eps,
+                   float eps_root, float wd, int nesterov, int apply, const int* step,
+                   const float* gscale, void* stream);
+/* gscale = min(1, clip/(||g/accum||+1e-6))/accum  (train_lm.py:173-178, 664). */
+int pcv_grad_scale(const float* g, const void* chunks, int nchunks, float* partial_ws, float inv_accum,
+                   float clip, float* gscale, float* gnorm, void* stream);
+int pcv_step_bump(int* step, void* stream);
+/* Muon (optax.contrib.muon scale_by_muon): momentum + nesterov + Frobenius normalisation
+ * into NS workspaces, and the shape-scaled weight-decayed update; descriptors are
+ * pcv_muon_mat_size()-byte records (see optim.hip MuonMat). */
+int pcv_muon_prep(const void* mats, int nmats, int64_t max_elems, float beta, int nesterov, float eps,
+                  const int* step, const float* gscale, void* stream);
+int pcv_muon_apply(const void* mats, int nmats, int64_t max_elems, float lr, float wd, int shape_scale,
+                   int apply, void* stream);
+int pcv_muon_mat_size(void);
+int pcv_chunk_size(void);
+const char* pcv_last_error_string(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLAINCV_HIP_H */

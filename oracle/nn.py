@@ -1,0 +1,62 @@
+"""Flax/JAX layer semantics restated in PyTorch CPU (TEST INFRASTRUCTURE ONLY).
+
+Each helper cites the flax/jax behaviour the reference relies on (SURVEY.md
+§8a "parity-critical third-party defaults").
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import rng as _rng
+
+
+def rnd(x, bf16: bool):
+    """Round to bf16 and back (models a bf16 GEMM operand) when bf16 placement is on."""
+    if bf16 and x.dtype != torch.float64:
+        return x.to(torch.bfloat16).to(x.dtype)
+    return x
+
+
+def mm(x, w, bf16: bool = False):
+    """Dense contraction x @ w; in bf16 placement both operands are rounded to
+    bf16 and accumulated in fp32 (the MFMA bf16 contract)."""
+    return rnd(x, bf16) @ rnd(w, bf16)
+
+
+def layernorm(x, scale, bias, eps=1e-6):
+    """flax.linen.LayerNorm: fast variance E[x^2]-E[x]^2 (clipped at 0), eps 1e-6
+    (used at models/vit_small.py:38,52,124)."""
+    mean = x.mean(-1, keepdim=True)
+    mean2 = (x * x).mean(-1, keepdim=True)
+    var = torch.clamp(mean2 - mean * mean, min=0.0)
+    return (x - mean) * torch.rsqrt(var + eps) * scale + bias
+
+
+def rmsnorm(x, scale, eps=1e-6, out_dtype=None):
+    """flax.linen.RMSNorm (models/LM/transformer.py:41-47): stats in fp32,
+    y = x * rsqrt(mean(x^2) + eps) * scale, cast once to the compute dtype."""
+    xf = x.float() if x.dtype in (torch.bfloat16, torch.float16) else x
+    mean2 = (xf * xf).mean(-1, keepdim=True)
+    y = xf * torch.rsqrt(mean2 + eps) * scale.to(xf.dtype)
+    return y.to(out_dtype or x.dtype)
+
+
+def gelu_tanh(x):
+    """flax.linen.gelu default approximate=True (models/vit_small.py:14)."""
+    c = math.sqrt(2.0 / math.pi)
+    return 0.5 * x * (1.0 + torch.tanh(c * (x + 0.044715 * x * x * x)))
+
+
+def dropout(x, rate, seed, site, train, mask_shape=None):
+    """flax.linen.Dropout: inverted dropout, keep ~ Bernoulli(1-rate), x*keep/(1-rate).
+    The keep bits come from the shared counter hash (oracle.rng)."""
+    if not train or rate == 0.0:
+        return x
+    shape = tuple(mask_shape) if mask_shape is not None else tuple(x.shape)
+    keep = torch.from_numpy(_rng.keep_mask(seed, site, shape, rate))
+    return torch.where(keep, x / (1.0 - rate), torch.zeros((), dtype=x.dtype))
+
+
+def silu(x):
+    return x * torch.sigmoid(x)

@@ -1,0 +1,143 @@
+"""ViT-small forward, restated from models/vit_small.py (TEST INFRASTRUCTURE ONLY).
+
+Parameters are a flat dict keyed by the Flax pytree path joined with "/",
+with Flax shapes (Conv kernel HWIO, DenseGeneral q/k/v kernels (D,H,Dh),
+out kernel (H,Dh,D)), exactly as ``plaincv_amd.models.vit_small`` stores them.
+"""
+from dataclasses import dataclass
+
+import torch
+
+from .nn import dropout, gelu_tanh, layernorm, mm, rnd
+
+# dropout site ids shared with plaincv_amd.models.vit_small (the kernel side)
+SITE_EMBED = 1
+
+
+def site_attn(i):
+    return 16 + 4 * i
+
+
+def site_mlp_hidden(i):
+    return 16 + 4 * i + 1
+
+
+def site_mlp_out(i):
+    return 16 + 4 * i + 2
+
+
+@dataclass
+class ViTConfig:
+    """VisionTransformer fields (models/vit_small.py:59-69; defaults train.py:105-115)."""
+    num_classes: int = 10
+    patch_size: int = 4
+    hidden_size: int = 128
+    mlp_dim: int = 256
+    num_layers: int = 4
+    num_heads: int = 4
+    dropout_rate: float = 0.1
+    use_layernorm: bool = True
+    use_batchnorm: bool = False
+
+
+def self_attention(params, pre, y, cfg: ViTConfig, train, seed, layer, bf16):
+    """flax.linen.SelfAttention (MultiHeadDotProductAttention) as used at
+    models/vit_small.py:41-45: q/k/v DenseGeneral(D->H,Dh)+bias, q scaled by
+    1/sqrt(Dh) before the einsum, fp32 softmax, dropout on the weights with
+    broadcast_dropout=True (mask shape (1,1,T,T)), out DenseGeneral(H,Dh->D)+bias."""
+    B, T, D = y.shape
+    H = cfg.num_heads
+    Dh = D // H
+    q = mm(y, params[f"{pre}/query/kernel"].reshape(D, H * Dh), bf16) + params[f"{pre}/query/bias"].reshape(-1)
+    k = mm(y, params[f"{pre}/key/kernel"].reshape(D, H * Dh), bf16) + params[f"{pre}/key/bias"].reshape(-1)
+    v = mm(y, params[f"{pre}/value/kernel"].reshape(D, H * Dh), bf16) + params[f"{pre}/value/bias"].reshape(-1)
+    q = q.reshape(B, T, H, Dh)
+    k = k.reshape(B, T, H, Dh)
+    v = v.reshape(B, T, H, Dh)
+    scale = 1.0 / (Dh ** 0.5)
+    logits = torch.einsum("bqhd,bkhd->bhqk", rnd(q, bf16), rnd(k, bf16)) * scale
+    w = torch.softmax(logits, dim=-1)
+    if train and cfg.dropout_rate > 0.0:
+        w = dropout(w, cfg.dropout_rate, seed, site_attn(layer), train, mask_shape=(T, T))
+    o = torch.einsum("bhqk,bkhd->bqhd", rnd(w, bf16), rnd(v, bf16)).reshape(B, T, H * Dh)
+    out = mm(o, params[f"{pre}/out/kernel"].reshape(H * Dh, D), bf16) + params[f"{pre}/out/bias"]
+    return out
+
+
+def mlp_block(params, pre, y, cfg: ViTConfig, train, seed, layer, bf16):
+    """MlpBlock (models/vit_small.py:6-18): Dense -> gelu(tanh) -> Dropout -> Dense -> Dropout."""
+    h = mm(y, params[f"{pre}/Dense_0/kernel"], bf16) + params[f"{pre}/Dense_0/bias"]
+    h = gelu_tanh(h)
+    h = dropout(h, cfg.dropout_rate, seed, site_mlp_hidden(layer), train)
+    o = mm(h, params[f"{pre}/Dense_1/kernel"], bf16) + params[f"{pre}/Dense_1/bias"]
+    return dropout(o, cfg.dropout_rate, seed, site_mlp_out(layer), train)
+
+
+def vit_apply(params, images, cfg: ViTConfig, train: bool = True, seed: int = 0,
+              bf16: bool = False, dtype=torch.float32):
+    """VisionTransformer.__call__ (models/vit_small.py:94-127).
+
+    images: uint8 (B,H,W,C) NHWC.  Returns logits (B, num_classes)."""
+    if cfg.use_batchnorm:
+        raise NotImplementedError("use_batchnorm ViT variant is SURVEY §8f-3 'next'")
+    x = images.to(dtype) / 255.0
+    B, Hh, Ww, C = x.shape
+    ps = cfg.patch_size
+    gh, gw = Hh // ps, Ww // ps
+    x = x[:, : gh * ps, : gw * ps, :]
+    # VALID conv with kernel=stride=patch == GEMM over (kh,kw,c)-flattened patches
+    patches = x.reshape(B, gh, ps, gw, ps, C).permute(0, 1, 3, 2, 4, 5).reshape(B, gh * gw, ps * ps * C)
+    D = cfg.hidden_size
+    x = mm(patches, params["Conv_0/kernel"].reshape(ps * ps * C, D), bf16) + params["Conv_0/bias"]
+    cls = params["cls_token"].expand(B, 1, D)
+    x = torch.cat([cls, x], dim=1) + params["pos_embedding"]
+    x = dropout(x, cfg.dropout_rate, seed, SITE_EMBED, train)
+    for i in range(cfg.num_layers):
+        pre = f"EncoderBlock_{i}"
+        y = layernorm(x, params[f"{pre}/LayerNorm_0/scale"], params[f"{pre}/LayerNorm_0/bias"]) \
+            if cfg.use_layernorm else x
+        x = x + self_attention(params, f"{pre}/SelfAttention_0", y, cfg, train, seed, i, bf16)
+        y = layernorm(x, params[f"{pre}/LayerNorm_1/scale"], params[f"{pre}/LayerNorm_1/bias"]) \
+            if cfg.use_layernorm else x
+        x = x + mlp_block(params, f"{pre}/MlpBlock_0", y, cfg, train, seed, i, bf16)
+    if cfg.use_layernorm:
+        x = layernorm(x, params["LayerNorm_0/scale"], params["LayerNorm_0/bias"])
+    cls_repr = x[:, 0]
+    return mm(cls_repr, params["Dense_0/kernel"], bf16) + params["Dense_0/bias"]
+
+
+def vit_param_shapes(cfg: ViTConfig, image_size: int, channels: int):
+    """Flax param pytree shapes (names as Flax auto-naming produces them)."""
+    D, M, H = cfg.hidden_size, cfg.mlp_dim, cfg.num_heads
+    Dh = D // H
+    ps = cfg.patch_size
+    T = (image_size // ps) ** 2 + 1
+    shapes = {
+        "Conv_0/kernel": (ps, ps, channels, D),
+        "Conv_0/bias": (D,),
+        "cls_token": (1, 1, D),
+        "pos_embedding": (1, T, D),
+    }
+    for i in range(cfg.num_layers):
+        pre = f"EncoderBlock_{i}"
+        if cfg.use_layernorm:
+            shapes[f"{pre}/LayerNorm_0/scale"] = (D,)
+            shapes[f"{pre}/LayerNorm_0/bias"] = (D,)
+        for n in ("query", "key", "value"):
+            shapes[f"{pre}/SelfAttention_0/{n}/kernel"] = (D, H, Dh)
+            shapes[f"{pre}/SelfAttention_0/{n}/bias"] = (H, Dh)
+        shapes[f"{pre}/SelfAttention_0/out/kernel"] = (H, Dh, D)
+        shapes[f"{pre}/SelfAttention_0/out/bias"] = (D,)
+        if cfg.use_layernorm:
+            shapes[f"{pre}/LayerNorm_1/scale"] = (D,)
+            shapes[f"{pre}/LayerNorm_1/bias"] = (D,)
+        shapes[f"{pre}/MlpBlock_0/Dense_0/kernel"] = (D, M)
+        shapes[f"{pre}/MlpBlock_0/Dense_0/bias"] = (M,)
+        shapes[f"{pre}/MlpBlock_0/Dense_1/kernel"] = (M, D)
+        shapes[f"{pre}/MlpBlock_0/Dense_1/bias"] = (D,)
+    if cfg.use_layernorm:
+        shapes["LayerNorm_0/scale"] = (D,)
+        shapes["LayerNorm_0/bias"] = (D,)
+    shapes["Dense_0/kernel"] = (D, cfg.num_classes)
+    shapes["Dense_0/bias"] = (cfg.num_classes,)
+    return shapes

@@ -1,0 +1,470 @@
+// plaincv_amd/csrc/attention.hip -- flash attention forward/backward for gfx950.
+//
+// Replaces flax SelfAttention's dot_product_attention (ViT, models/vit_small.py:41-45:
+// non-causal, Dh=32, T=257, dropout on the weights broadcast over batch+heads)
+// and jax.nn.dot_product_attention(is_causal=True) (LM, models/LM/transformer.py:233-240:
+// Dh=64, fp32 logits/softmax, probs cast to bf16).
+//
+// Layout: q/k/v are column blocks of the packed QKV activation [B*T, ld]
+// (head h at columns h*DH of each block), o is [B*T, ldo]; nothing is transposed.
+// LSE is stored per (b,h,q) in the log2 domain: lse2 = m2 + log2(l), where
+// m2/l are the running max/sum of s*scale*log2(e).
+//
+// MFMA v_mfma_f32_16x16x32_bf16 with the key on the MFMA row and the query on the
+// lane ("swapped" S^T = K.Q^T): the P accumulator then already holds, per lane,
+// 4+4 keys of one query, which is the A fragment of P.V once the k order of the
+// 32-key step is permuted kappa(g,j) = 32s + (j<4 ? 4g+j : 16+4g+j-4); V (or K, dO, Q)
+// rows are fetched in that same order with the transposing ds_read_b64_tr_b16.
+// Three kernels: fwd; bwd_dkdv (workgroup = 64 keys, loop over queries);
+// bwd_dq (workgroup = 64 queries, loop over keys) -- deterministic, no atomics.
+#include "common.h"
+
+namespace pcv {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float NEG_BIG = -1.0e30f;
+
+struct AttnArgs {
+  const bf16 *q, *k, *v; int64_t ldq;     // q/k/v row stride (same packed buffer)
+  const bf16* o; int64_t ldo;             // fwd out / bwd in
+  bf16* out; int64_t ldout;               // fwd: O
+  const bf16* dout; int64_t lddo;         // bwd: dO
+  bf16 *dq, *dk, *dv; int64_t lddq;       // bwd outputs (row stride lddq)
+  float* lse2; float* delta;              // [B,H,T]
+  int B, T, H;
+  float scale;                            // 1/sqrt(DH)
+  uint32_t drop_thresh; float drop_scale; const uint32_t* seedp; uint32_t site;
+};
+
+template <int DH>
+struct Tile {
+  static constexpr int LD = DH + 8;  // padded row (elements), 16-B aligned rows
+};
+
+// Cooperative load of 64 rows x DH of a column block into a padded LDS image.
+template <int DH>
+__device__ __forceinline__ void load_rows(bf16* lds, const bf16* base, int64_t ld, int row0, int T,
+                                          int64_t bT) {
+  constexpr int CPR = DH / 8;
+  constexpr int LD = Tile<DH>::LD;
+  for (int idx = threadIdx.x; idx < 64 * CPR; idx += 256) {
+    const int r = idx / CPR, c = idx % CPR;
+    const int gr = row0 + r;
+    u32x4 v = u32x4{0u, 0u, 0u, 0u};
+    if (gr < T) v = *reinterpret_cast<const u32x4*>(base + (bT + gr) * ld + c * 8);
+    *reinterpret_cast<u32x4*>(lds + r * LD + c * 8) = v;
+  }
+}
+
+// A/B fragment of 16 rows x 32 k from a row-major padded image (k contiguous)
+template <int DH>
+__device__ __forceinline__ bf16x8 row_frag(const bf16* lds, int rbase, int ks) {
+  const int l = threadIdx.x & 63;
+  return *reinterpret_cast<const bf16x8*>(lds + (rbase + (l & 15)) * Tile<DH>::LD + ks * 32 + 8 * (l >> 4));
+}
+// fragment whose k index runs over ROWS in kappa order (32-row step s), columns cbase..+15
+template <int DH>
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* lds, int s, int cbase) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, w = l & 15, q = w >> 2, p = w & 3;
+  const bf16* a0 = lds + (32 * s + 4 * g + q) * Tile<DH>::LD + cbase + 4 * p;
+  const bf16* a1 = a0 + 16 * Tile<DH>::LD;
+  bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
+  bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a1));
+  return bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+}
+// per-lane global fragment: row `row`, k = ks*32 + 8*(lane>>4) .. +8
+__device__ __forceinline__ bf16x8 glob_frag(const bf16* base, int64_t ld, int64_t row, bool valid, int ks) {
+  const int l = threadIdx.x & 63;
+  if (!valid) return bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  return *reinterpret_cast<const bf16x8*>(base + row * ld + ks * 32 + 8 * (l >> 4));
+}
+__device__ __forceinline__ bf16x8 pack8(f32x4 a, f32x4 b) {
+  return bf16x8{f2bf(a[0]), f2bf(a[1]), f2bf(a[2]), f2bf(a[3]), f2bf(b[0]), f2bf(b[1]), f2bf(b[2]), f2bf(b[3])};
+}
+
+// ------------------------------------------------------------------ forward
+template <int DH, bool CAUSAL, bool DROP>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  const uint32_t seed = DROP ? *a.seedp : 0u;
+  constexpr int LD = Tile<DH>::LD;
+  constexpr int KS = DH / 32, DT = DH / 16;
+  __shared__ __attribute__((aligned(16))) bf16 Ks[64 * LD];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[64 * LD];
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int T = a.T;
+  const int64_t bT = (int64_t)b * T;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+  const int q0 = qb * 64 + wave * 16;
+  const int myq = q0 + (lane & 15);
+  const bf16* Q = a.q + h * DH;
+  const bf16* Kp = a.k + h * DH;
+  const bf16* Vp = a.v + h * DH;
+
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) qf[ks] = glob_frag(Q, a.ldq, bT + myq, myq < T, ks);
+
+  const float c2 = a.scale * LOG2E;
+  float m2 = NEG_BIG, lsum = 0.f;
+  f32x4 acc[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int nkb = (T + 63) / 64;
+  if (CAUSAL) nkb = min(nkb, (qb * 64 + 63) / 64 + 1);
+  for (int kb = 0; kb < nkb; ++kb) {
+    __syncthreads();
+    load_rows<DH>(Ks, Kp, a.ldq, kb * 64, T, bT);
+    load_rows<DH>(Vs, Vp, a.ldq, kb * 64, T, bT);
+    __syncthreads();
+    f32x4 s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Ks, 16 * t, ks), qf[ks], s[t], 0, 0, 0);
+    }
+    float bmax = NEG_BIG;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kb * 64 + 16 * t + 4 * g + r;
+        bool ok = key < T;
+        if (CAUSAL) ok = ok && key <= myq;
+        s[t][r] = ok ? s[t][r] * c2 : NEG_BIG;
+        bmax = fmaxf(bmax, s[t][r]);
+      }
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+    const float mnew = fmaxf(m2, bmax);
+    const float alpha = exp2f(m2 - mnew);
+    float rs = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float p = s[t][r] > 0.5f * NEG_BIG ? exp2f(s[t][r] - mnew) : 0.f;
+        rs += p;
+        if (DROP) {
+          const int key = kb * 64 + 16 * t + 4 * g + r;
+          const uint32_t hh = hash3(seed, a.site, (uint32_t)myq * (uint32_t)T + (uint32_t)key);
+          p = hh >= a.drop_thresh ? p * a.drop_scale : 0.f;
+        }
+        s[t][r] = p;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    lsum = lsum * alpha + rs;
+    m2 = mnew;
+    // rescale O rows: acc row = query (lane>>4)*4 + r; alpha lives on lane == query
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float al = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+      for (int d = 0; d < DT; ++d) acc[d][r] *= al;
+    }
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16x8 pa = pack8(s[2 * st], s[2 * st + 1]);
+#pragma unroll
+      for (int d = 0; d < DT; ++d)
+        acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_frag<DH>(Vs, st, 16 * d), acc[d], 0, 0, 0);
+    }
+  }
+  // normalise + store
+  const float inv = 1.f / lsum;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float iv = __shfl(inv, 4 * g + r, 64);
+    const int qq = q0 + 4 * g + r;
+    if (qq < T) {
+#pragma unroll
+      for (int d = 0; d < DT; ++d)
+        a.out[(bT + qq) * a.ldout + h * DH + 16 * d + (lane & 15)] = f2bf(acc[d][r] * iv);
+    }
+  }
+  if (g == 0 && myq < T) a.lse2[((int64_t)b * a.H + h) * T + myq] = m2 + log2f(lsum);
+}
+
+// ------------------------------------------------------------- bwd: delta
+// delta[b,h,q] = sum_d dO[q,d] * O[q,d]
+template <int DH>
+__global__ void attn_bwd_delta_kernel(AttnArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over B*T*H
+  const int64_t n = (int64_t)a.B * a.T * a.H;
+  if (i >= n) return;
+  const int h = (int)(i % a.H);
+  const int64_t row = i / a.H;  // b*T + t
+  const bf16* o = a.o + row * a.ldo + h * DH;
+  const bf16* d = a.dout + row * a.lddo + h * DH;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < DH; c += 8) {
+    bf16x8 x = *reinterpret_cast<const bf16x8*>(o + c);
+    bf16x8 y = *reinterpret_cast<const bf16x8*>(d + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += bf2f(x[j]) * bf2f(y[j]);
+  }
+  const int64_t b = row / a.T, t = row % a.T;
+  a.delta[(b * a.H + h) * a.T + t] = s;
+}
+
+// --------------------------------------------------------- bwd: dK, dV
+template <int DH, bool CAUSAL, bool DROP>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
+  const uint32_t seed = DROP ? *a.seedp : 0u;
+  constexpr int LD = Tile<DH>::LD;
+  constexpr int KS = DH / 32, DT = DH / 16;
+  __shared__ __attribute__((aligned(16))) bf16 Qs[64 * LD];
+  __shared__ __attribute__((aligned(16))) bf16 Ds[64 * LD];
+  __shared__ float Ls[64], Dl[64];
+  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int T = a.T;
+  const int64_t bT = (int64_t)b * T;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+  const int k0 = kb * 64 + wave * 16;
+  const int mykey = k0 + (lane & 15);
+  const bool kval = mykey < T;
+  const bf16* Qp = a.q + h * DH;
+  const bf16* Kp = a.k + h * DH;
+  const bf16* Vp = a.v + h * DH;
+  const bf16* dOp = a.dout + h * DH;
+  const float* lse = a.lse2 + ((int64_t)b * a.H + h) * T;
+  const float* del = a.delta + ((int64_t)b * a.H + h) * T;
+
+  bf16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    kf[ks] = glob_frag(Kp, a.ldq, bT + mykey, kval, ks);
+    vf[ks] = glob_frag(Vp, a.ldq, bT + mykey, kval, ks);
+  }
+  const float c2 = a.scale * LOG2E;
+  f32x4 dv[DT], dk[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) { dv[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+  const int nqb = (T + 63) / 64;
+  const int qb0 = CAUSAL ? kb : 0;
+  for (int qb = qb0; qb < nqb; ++qb) {
+    __syncthreads();
+    load_rows<DH>(Qs, Qp, a.ldq, qb * 64, T, bT);
+    load_rows<DH>(Ds, dOp, a.lddo, qb * 64, T, bT);
+    if (threadIdx.x < 64) {
+      const int qq = qb * 64 + threadIdx.x;
+      Ls[threadIdx.x] = qq < T ? lse[qq] : 0.f;
+      Dl[threadIdx.x] = qq < T ? del[qq] : 0.f;
+    }
+    __syncthreads();
+    f32x4 p[4], ds[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Qs, 16 * t, ks), kf[ks], sv, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Ds, 16 * t, ks), vf[ks], dp, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = 16 * t + 4 * g + r;
+        const int qq = qb * 64 + ql;
+        bool ok = kval && qq < T;
+        if (CAUSAL) ok = ok && mykey <= qq;
+        float pv = ok ? exp2f(sv[r] * c2 - Ls[ql]) : 0.f;
+        float dpv = dp[r];
+        float pd = pv;
+        if (DROP) {
+          const uint32_t hh = hash3(seed, a.site, (uint32_t)qq * (uint32_t)T + (uint32_t)mykey);
+          const float km = hh >= a.drop_thresh ? a.drop_scale : 0.f;
+          pd = pv * km;
+          dpv *= km;
+        }
+        p[t][r] = pd;
+        ds[t][r] = pv * (dpv - Dl[ql]);
+      }
+    }
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16x8 pb = pack8(p[2 * st], p[2 * st + 1]);
+      const bf16x8 sb = pack8(ds[2 * st], ds[2 * st + 1]);
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag<DH>(Ds, st, 16 * d), pb, dv[d], 0, 0, 0);
+        dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag<DH>(Qs, st, 16 * d), sb, dk[d], 0, 0, 0);
+      }
+    }
+  }
+  if (kval) {
+#pragma unroll
+    for (int d = 0; d < DT; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int dd = 16 * d + 4 * g + r;
+        a.dv[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(dv[d][r]);
+        a.dk[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(dk[d][r] * a.scale);
+      }
+  }
+}
+
+// --------------------------------------------------------------- bwd: dQ
+template <int DH, bool CAUSAL, bool DROP>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
+  const uint32_t seed = DROP ? *a.seedp : 0u;
+  constexpr int LD = Tile<DH>::LD;
+  constexpr int KS = DH / 32, DT = DH / 16;
+  __shared__ __attribute__((aligned(16))) bf16 Ks[64 * LD];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[64 * LD];
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int T = a.T;
+  const int64_t bT = (int64_t)b * T;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+  const int q0 = qb * 64 + wave * 16;
+  const int myq = q0 + (lane & 15);
+  const bool qval = myq < T;
+  const bf16* Qp = a.q + h * DH;
+  const bf16* Kp = a.k + h * DH;
+  const bf16* Vp = a.v + h * DH;
+  const bf16* dOp = a.dout + h * DH;
+  const int64_t bh = (int64_t)b * a.H + h;
+  const float myl = qval ? a.lse2[bh * T + myq] : 0.f;
+  const float myd = qval ? a.delta[bh * T + myq] : 0.f;
+
+  bf16x8 qf[KS], of[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    qf[ks] = glob_frag(Qp, a.ldq, bT + myq, qval, ks);
+    of[ks] = glob_frag(dOp, a.lddo, bT + myq, qval, ks);
+  }
+  const float c2 = a.scale * LOG2E;
+  f32x4 acc[DT];
+#pragma unroll
+  for (int d = 0; d < DT; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int nkb = (T + 63) / 64;
+  if (CAUSAL) nkb = min(nkb, (qb * 64 + 63) / 64 + 1);
+  for (int kb = 0; kb < nkb; ++kb) {
+    __syncthreads();
+    load_rows<DH>(Ks, Kp, a.ldq, kb * 64, T, bT);
+    load_rows<DH>(Vs, Vp, a.ldq, kb * 64, T, bT);
+    __syncthreads();
+    f32x4 ds[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Ks, 16 * t, ks), qf[ks], sv, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Vs, 16 * t, ks), of[ks], dp, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kb * 64 + 16 * t + 4 * g + r;
+        bool ok = qval && key < T;
+        if (CAUSAL) ok = ok && key <= myq;
+        const float pv = ok ? exp2f(sv[r] * c2 - myl) : 0.f;
+        float dpv = dp[r];
+        if (DROP) {
+          const uint32_t hh = hash3(seed, a.site, (uint32_t)myq * (uint32_t)T + (uint32_t)key);
+          dpv *= hh >= a.drop_thresh ? a.drop_scale : 0.f;
+        }
+        ds[t][r] = pv * (dpv - myd);
+      }
+    }
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const bf16x8 sa = pack8(ds[2 * st], ds[2 * st + 1]);
+#pragma unroll
+      for (int d = 0; d < DT; ++d)
+        acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, tr_frag<DH>(Ks, st, 16 * d), acc[d], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int qq = q0 + 4 * g + r;
+    if (qq < T) {
+#pragma unroll
+      for (int d = 0; d < DT; ++d)
+        a.dq[(bT + qq) * a.lddq + h * DH + 16 * d + (lane & 15)] = f2bf(acc[d][r] * a.scale);
+    }
+  }
+}
+
+template <int DH, bool C, bool D>
+static void launch_fwd(const AttnArgs& a, hipStream_t s) {
+  dim3 grid((a.T + 63) / 64, a.H, a.B);
+  hipLaunchKernelGGL((attn_fwd_kernel<DH, C, D>), grid, dim3(256), 0, s, a);
+}
+template <int DH, bool C, bool D>
+static void launch_bwd(const AttnArgs& a, hipStream_t s) {
+  const int64_t n = (int64_t)a.B * a.T * a.H;
+  hipLaunchKernelGGL((attn_bwd_delta_kernel<DH>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+  dim3 grid((a.T + 63) / 64, a.H, a.B);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH, C, D>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, C, D>), grid, dim3(256), 0, s, a);
+}
+
+template <bool FWD>
+static int dispatch(const AttnArgs& a, int dh, int causal, int drop, hipStream_t s) {
+#define PCV_ATT(DHV, CV, DV) \
+  if (dh == DHV && causal == CV && drop == DV) { FWD ? launch_fwd<DHV, CV, DV>(a, s) : launch_bwd<DHV, CV, DV>(a, s); return pcv_launch_status(); }
+  PCV_ATT(32, 0, 0) PCV_ATT(32, 0, 1) PCV_ATT(32, 1, 0) PCV_ATT(32, 1, 1)
+  PCV_ATT(64, 0, 0) PCV_ATT(64, 0, 1) PCV_ATT(64, 1, 0) PCV_ATT(64, 1, 1)
+  PCV_ATT(128, 0, 0) PCV_ATT(128, 1, 0)
+#undef PCV_ATT
+  return PCV_EINVAL;
+}
+
+static void set_drop(AttnArgs& a, float rate, const uint32_t* seed, uint32_t site) {
+  a.seedp = seed; a.site = site; a.drop_thresh = 0; a.drop_scale = 1.f;
+  if (rate > 0.f) {
+    double t = (double)rate * 4294967296.0;
+    a.drop_thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+    a.drop_scale = 1.f / (1.f - rate);
+  }
+}
+
+}  // namespace pcv
+
+using namespace pcv;
+
+extern "C" int pcv_attn_fwd(const void* q, const void* k, const void* v, int64_t ldq,
+                            void* out, int64_t ldo, float* lse2,
+                            int B, int T, int H, int head_dim, int causal,
+                            float dropout_rate, const uint32_t* seed, uint32_t site, void* stream) {
+  if (B <= 0 || T <= 0 || H <= 0) return PCV_EINVAL;
+  if (dropout_rate > 0.f && !seed) return PCV_EINVAL;
+  if ((ldq & 7) || (ldo & 7) || !pcv_aligned16(q) || !pcv_aligned16(k) || !pcv_aligned16(v)) return PCV_EALIGN;
+  AttnArgs a{};
+  a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.ldq = ldq;
+  a.out = (bf16*)out; a.ldout = ldo; a.lse2 = lse2;
+  a.B = B; a.T = T; a.H = H; a.scale = 1.f / sqrtf((float)head_dim);
+  set_drop(a, dropout_rate, seed, site);
+  return dispatch<true>(a, head_dim, causal ? 1 : 0, a.drop_thresh ? 1 : 0, (hipStream_t)stream);
+}
+
+extern "C" int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t ldq,
+                            const void* o, int64_t ldo, const void* dout, int64_t lddo,
+                            const float* lse2, float* delta_ws,
+                            void* dq, void* dk, void* dv, int64_t lddq,
+                            int B, int T, int H, int head_dim, int causal,
+                            float dropout_rate, const uint32_t* seed, uint32_t site, void* stream) {
+  if (B <= 0 || T <= 0 || H <= 0) return PCV_EINVAL;
+  if (dropout_rate > 0.f && !seed) return PCV_EINVAL;
+  if ((ldq & 7) || (ldo & 7) || (lddo & 7) || !pcv_aligned16(q) || !pcv_aligned16(k) || !pcv_aligned16(v) ||
+      !pcv_aligned16(o) || !pcv_aligned16(dout))
+    return PCV_EALIGN;
+  AttnArgs a{};
+  a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.ldq = ldq;
+  a.o = (const bf16*)o; a.ldo = ldo; a.dout = (const bf16*)dout; a.lddo = lddo;
+  a.dq = (bf16*)dq; a.dk = (bf16*)dk; a.dv = (bf16*)dv; a.lddq = lddq;
+  a.lse2 = (float*)lse2; a.delta = delta_ws;
+  a.B = B; a.T = T; a.H = H; a.scale = 1.f / sqrtf((float)head_dim);
+  set_drop(a, dropout_rate, seed, site);
+  return dispatch<false>(a, head_dim, causal ? 1 : 0, a.drop_thresh ? 1 : 0, (hipStream_t)stream);
+}

@@ -1,0 +1,82 @@
+// plaincv_amd/csrc/common.h -- shared device helpers for the gfx950 kernels.
+//
+// Conventions:
+//   * bf16 tensors are stored as raw 16-bit words (uint16_t in the C ABI);
+//     arithmetic is fp32, conversion by the hardware v_cvt_pk_bf16_f32 (RNE).
+//   * every entry point returns int: 0 ok, <0 invalid argument, >0 hipError_t.
+//   * all launches go on the caller's stream, no host sync, no allocation, so
+//     a whole train step can be captured into one hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+#define PCV_EINVAL (-1)
+#define PCV_EALIGN (-2)
+#define PCV_ESHAPE (-3)
+
+namespace pcv {
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+// 32-bit lowbias hash of (seed, site, idx); restated in oracle/rng.py.
+__device__ __forceinline__ uint32_t hash3(uint32_t seed, uint32_t site, uint32_t idx) {
+  uint32_t x = idx * 0x9E3779B1u + site * 0x85EBCA77u + seed * 0xC2B2AE3Du;
+  x ^= x >> 16; x *= 0x7FEB352Du;
+  x ^= x >> 15; x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x a multiple of 64 (<= 1024); `red` must hold
+// blockDim.x/64 floats of LDS.  Result is broadcast to every thread.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < nw; ++i) s += red[i];
+  return s;
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float c = 0.7978845608028654f;  // sqrt(2/pi)
+  float u = c * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float c = 0.7978845608028654f;
+  float x2 = x * x;
+  float u = c * (x + 0.044715f * x2 * x);
+  float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * c * (1.f + 3.f * 0.044715f * x2);
+}
+
+}  // namespace pcv
+
+static inline int pcv_launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+static inline bool pcv_aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }

@@ -1,0 +1,208 @@
+// plaincv_amd/csrc/optim.hip -- optimizer kernels (multi-tensor over the flat buffers).
+//
+//   AdamW   optim/factory.py:193-205 -> optax.adamw (also the Muon/SOAP/Shampoo
+//           fallback branches, optional nesterov = optax.contrib.muon's adam branch)
+//   Muon    optim/factory.py:441-484 -> optax.contrib.muon: momentum + nesterov
+//           bias correction (muon_prep), Frobenius normalisation, and the final
+//           shape-scaled, weight-decayed update (muon_apply).  The Newton-Schulz
+//           iterations themselves are batched MFMA GEMMs (gemm.hip).
+//   grad clipping (train_lm.py:173-178) + accumulation mean: deterministic
+//   per-chunk sum-of-squares partials, then one tiny kernel derives the device
+//   scalar gscale = clip_factor / accum that every optimizer kernel multiplies in.
+// Step counters, gscale and norms live in device memory so the whole optimizer
+// step replays correctly from a captured hipGraph.
+#include "common.h"
+
+namespace pcv {
+
+struct Chunk { int64_t start; int64_t len; };
+
+struct AdamHyper {
+  float lr, b1, b2, eps, eps_root, wd;
+  int nesterov, apply;
+};
+
+__global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, float* m, float* v, bf16* pb, float* upd,
+                                                    const Chunk* chunks, AdamHyper h, const int* step,
+                                                    const float* gscale) {
+  const Chunk ck = chunks[blockIdx.x];
+  const float t = (float)(*step + 1);
+  const float bc1 = 1.f - powf(h.b1, t), bc2 = 1.f - powf(h.b2, t);
+  const float bc1n = 1.f - powf(h.b1, t + 1.f);
+  const float gs = gscale ? *gscale : 1.f;
+  for (int64_t i = ck.start + threadIdx.x; i < ck.start + ck.len; i += 256) {
+    const float gi = g[i] * gs;
+    const float mi = h.b1 * m[i] + (1.f - h.b1) * gi;
+    const float vi = h.b2 * v[i] + (1.f - h.b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float mh = h.nesterov ? h.b1 * mi / bc1n + (1.f - h.b1) * gi / bc1 : mi / bc1;
+    const float vh = vi / bc2;
+    const float pi = p[i];
+    const float u = -h.lr * (mh / (sqrtf(vh + h.eps_root) + h.eps) + h.wd * pi);
+    if (upd) upd[i] = u;
+    if (h.apply) {
+      const float pn = pi + u;
+      p[i] = pn;
+      if (pb) pb[i] = f2bf(pn);
+    }
+  }
+}
+
+// per-chunk sum of squares (deterministic partials)
+__global__ __launch_bounds__(256) void sqnorm_kernel(const float* x, const Chunk* chunks, float* partial) {
+  __shared__ float red[4];
+  const Chunk ck = chunks[blockIdx.x];
+  float s = 0.f;
+  for (int64_t i = ck.start + threadIdx.x; i < ck.start + ck.len; i += 256) s += x[i] * x[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+// gscale = min(1, clip/(||g/accum||+1e-6)) / accum   (clip <= 0: no clipping)
+__global__ __launch_bounds__(1024) void gscale_kernel(const float* partial, int n, float inv_accum, float clip,
+                                                      float* gscale, float* gnorm) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 1024) s += partial[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) {
+    const float nrm = sqrtf(s) * inv_accum;
+    float f = 1.f;
+    if (clip > 0.f) f = fminf(1.f, clip / (nrm + 1e-6f));
+    *gscale = f * inv_accum;
+    if (gnorm) *gnorm = nrm;
+  }
+}
+
+__global__ void bump_kernel(int* step) { *step += 1; }
+
+// ------------------------------------------------------------------- Muon
+struct MuonMat {
+  float* p; const float* g; float* mu; bf16* pb; float* upd;
+  int64_t rows, cols, ld, ldx;  // param view (fan_in x fan_out) row stride ld; X row stride ldx
+  float* x32;                  // workspace [r', c'] (transposed if rows > cols)
+  bf16* xb;                    // bf16 copy of the normalised X (NS input)
+  const bf16* xo;              // NS output [r', c'] (bf16)
+  float* norm2;                // sum of squares of x32
+};
+
+struct MuonHyper {
+  float beta, lr, wd, eps, shape_scale;
+  int nesterov, apply;
+};
+
+// mu = beta*mu + (1-beta)*g*gs; X = nesterov-corrected mu_hat, stored transposed when rows > cols
+__global__ __launch_bounds__(256) void muon_prep_kernel(const MuonMat* mats, MuonHyper h, const int* step,
+                                                        const float* gscale) {
+  __shared__ float red[4];
+  const MuonMat M = mats[blockIdx.y];
+  const int64_t n = M.rows * M.cols;
+  const float t = (float)(*step + 1);
+  const float bc = 1.f - powf(h.beta, t), bcn = 1.f - powf(h.beta, t + 1.f);
+  const float gs = gscale ? *gscale : 1.f;
+  const bool tr = M.rows > M.cols;
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / M.cols, c = i % M.cols;
+    const int64_t off = r * M.ld + c;
+    const float gi = M.g[off] * gs;
+    const float mi = h.beta * M.mu[off] + (1.f - h.beta) * gi;
+    M.mu[off] = mi;
+    const float xh = h.nesterov ? h.beta * mi / bcn + (1.f - h.beta) * gi / bc : mi / bc;
+    M.x32[tr ? c * M.ldx + r : r * M.ldx + c] = xh;
+    s += xh * xh;
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) atomicAdd(M.norm2, s);
+}
+
+__global__ __launch_bounds__(256) void muon_norm_kernel(const MuonMat* mats, float eps) {
+  const MuonMat M = mats[blockIdx.y];
+  const int64_t n = M.rows * M.cols;
+  const float inv = 1.f / (sqrtf(*M.norm2) + eps);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    { const int64_t cx = M.rows > M.cols ? M.rows : M.cols; const int64_t j = (i / cx) * M.ldx + i % cx; M.xb[j] = f2bf(M.x32[j] * inv); }
+}
+
+// u = -lr*(O*shape_scale + wd*p); p += u
+__global__ __launch_bounds__(256) void muon_apply_kernel(const MuonMat* mats, MuonHyper h) {
+  const MuonMat M = mats[blockIdx.y];
+  const int64_t n = M.rows * M.cols;
+  const bool tr = M.rows > M.cols;
+  const float ss = h.shape_scale > 0.f ? sqrtf(fmaxf(1.f, (float)M.cols / (float)M.rows)) : 1.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / M.cols, c = i % M.cols;
+    const int64_t off = r * M.ld + c;
+    const float o = bf2f(M.xo[tr ? c * M.ldx + r : r * M.ldx + c]);
+    const float pi = M.p[off];
+    const float u = -h.lr * (o * ss + h.wd * pi);
+    if (M.upd) M.upd[off] = u;
+    if (h.apply) {
+      const float pn = pi + u;
+      M.p[off] = pn;
+      if (M.pb) M.pb[off] = f2bf(pn);
+    }
+  }
+}
+
+}  // namespace pcv
+
+using namespace pcv;
+
+extern "C" int pcv_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, float* upd,
+                              const void* chunks, int nchunks, float lr, float b1, float b2, float eps, float eps_root,
+                              float wd, int nesterov, int apply, const int* step, const float* gscale, void* stream) {
+  if (nchunks < 0 || !step) return PCV_EINVAL;
+  if (nchunks == 0) return 0;
+  AdamHyper h{lr, b1, b2, eps, eps_root, wd, nesterov, apply};
+  hipLaunchKernelGGL(adamw_kernel, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (bf16*)p_bf16, upd,
+                     (const Chunk*)chunks, h, step, gscale);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_grad_scale(const float* g, const void* chunks, int nchunks, float* partial_ws, float inv_accum,
+                              float clip, float* gscale, float* gnorm, void* stream) {
+  if (nchunks <= 0) return PCV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(nchunks), dim3(256), 0, s, g, (const Chunk*)chunks, partial_ws);
+  hipLaunchKernelGGL(gscale_kernel, dim3(1), dim3(1024), 0, s, partial_ws, nchunks, inv_accum, clip, gscale, gnorm);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_step_bump(int* step, void* stream) {
+  hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_muon_prep(const void* mats, int nmats, int64_t max_elems, float beta, int nesterov, float eps,
+                             const int* step, const float* gscale, void* stream) {
+  if (nmats <= 0) return PCV_EINVAL;
+  MuonHyper h{beta, 0.f, 0.f, eps, 0.f, nesterov, 0};
+  int gx = (int)((max_elems + 256 * 8 - 1) / (256 * 8));
+  gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(muon_prep_kernel, dim3(gx, nmats), dim3(256), 0, s, (const MuonMat*)mats, h, step, gscale);
+  hipLaunchKernelGGL(muon_norm_kernel, dim3(gx, nmats), dim3(256), 0, s, (const MuonMat*)mats, eps);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_muon_apply(const void* mats, int nmats, int64_t max_elems, float lr, float wd, int shape_scale,
+                              int apply, void* stream) {
+  if (nmats <= 0) return PCV_EINVAL;
+  MuonHyper h{0.f, lr, wd, 0.f, shape_scale ? 1.f : 0.f, 0, apply};
+  int gx = (int)((max_elems + 256 * 8 - 1) / (256 * 8));
+  gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
+  hipLaunchKernelGGL(muon_apply_kernel, dim3(gx, nmats), dim3(256), 0, (hipStream_t)stream, (const MuonMat*)mats, h);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_muon_mat_size(void) { return (int)sizeof(MuonMat); }
+extern "C" int pcv_chunk_size(void) { return (int)sizeof(Chunk); }
+
+extern "C" const char* pcv_last_error_string(int code) {
+  if (code == PCV_EINVAL) return "invalid argument";
+  if (code == PCV_EALIGN) return "misaligned pointer or leading dimension";
+  if (code == PCV_ESHAPE) return "shape mismatch";
+  return hipGetErrorString((hipError_t)code);
+}

@@ -1,0 +1,102 @@
+"""Data parallelism: one process per GPU, gradient mean over RCCL/xGMI.
+
+Replaces the reference's single-process ``jax.pmap`` + ``lax.pmean(grads)``
+(train_lm.py:195-210, 256-271) and its collective probe with fallback
+(train_lm.py:442-462, 485-492).  Each rank computes its own micro-batches; the
+only exchange is the mean of the flat fp32 gradient buffer, done ONCE per
+optimizer step (the reference reduces every micro-step; mean-of-sums equals
+sum-of-means up to fp rounding), in contiguous buckets walked from the end of
+the buffer (= the order the backward produces them).  Params/optimizer state
+stay replicated; every rank runs the identical optimizer update.
+``torch.distributed`` backend "nccl" is RCCL on ROCm; "gloo" is used for the
+CPU multi-process tests.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+DEFAULT_BUCKET_BYTES = 128 << 20
+
+
+def is_initialized():
+    return dist.is_available() and dist.is_initialized()
+
+
+def world_size():
+    return dist.get_world_size() if is_initialized() else 1
+
+
+def rank():
+    return dist.get_rank() if is_initialized() else 0
+
+
+def init_from_env(backend=None):
+    """torchrun-style env (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR/PORT).  Returns
+    (rank, local_rank, world_size, device)."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    lr = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1 and not is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(lr)
+            dist.init_process_group(backend=backend, device_id=torch.device("cuda", lr))
+        else:
+            dist.init_process_group(backend=backend)
+    dev = torch.device("cuda", lr) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    return rank(), lr, world_size(), dev
+
+
+def probe_collectives(device):
+    """psum(arange(n)) health check (train_lm.py:442-462).  Returns (ok, err)."""
+    n = world_size()
+    if n <= 1:
+        return False, None
+    try:
+        x = torch.arange(n, dtype=torch.float32, device=device)
+        dist.all_reduce(x)
+        ok = torch.allclose(x.cpu(), torch.arange(n, dtype=torch.float32) * n)
+        return bool(ok), None if ok else "psum mismatch"
+    except Exception as exc:  # pragma: no cover - depends on the fabric
+        return False, str(exc)
+
+
+def _avg_supported(t):
+    return t.is_cuda and dist.get_backend() == "nccl"
+
+
+def all_reduce_mean_(t, bucket_bytes=DEFAULT_BUCKET_BYTES):
+    """In-place mean of a flat tensor across ranks, bucketed back to front."""
+    n = world_size()
+    if n <= 1:
+        return t
+    per = max(1, bucket_bytes // t.element_size())
+    total = t.numel()
+    end = total
+    use_avg = _avg_supported(t)
+    while end > 0:
+        start = max(0, end - per)
+        chunk = t[start:end]
+        if use_avg:
+            dist.all_reduce(chunk, op=dist.ReduceOp.AVG)
+        else:
+            dist.all_reduce(chunk, op=dist.ReduceOp.SUM)
+            chunk.div_(n)
+        end = start
+    return t
+
+
+def all_reduce_grads(store, bucket_bytes=DEFAULT_BUCKET_BYTES):
+    if world_size() > 1:
+        all_reduce_mean_(store.grad_flat[: store.layout.size], bucket_bytes)
+
+
+def all_reduce_metrics(m):
+    """pmean of the [loss, acc] scalars (train_lm.py:208-209)."""
+    if world_size() > 1:
+        all_reduce_mean_(m)
+    return m

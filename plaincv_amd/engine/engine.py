@@ -1,0 +1,211 @@
+"""Train/eval step engine (mirrors engine/flax_engine.py:13-134).
+
+Same public names and call shapes as the reference:
+
+    state = create_train_state(rng, model_def, learning_rate, image_shape, num_classes, cfg, curvature_batch)
+    train_step = make_train_step(return_updates=False)
+    state, metrics = train_step(state, (images, labels), rng)        # metrics: {'loss', 'accuracy'}
+    eval_step = make_eval_step();  metrics = eval_step(state, (images, labels))
+
+Differences that are MI355X design, not semantics: ``state`` is mutated in
+place (and returned) instead of rebuilt; the reference's redundant second
+forward (flax_engine.py:107-109, same rng -> same metrics) is skipped; the
+whole step (forward, backward, optimizer) can be captured into one hipGraph
+(``GraphedTrainStep``) because every kernel runs on the current stream with
+device-resident seeds/counters.
+"""
+from dataclasses import dataclass, field
+from typing import Any, Dict, Optional
+
+import torch
+
+from .. import kernels as K
+from ..optim.adamw import AdamW
+from ..optim.base import apply_updates
+from ..optim.factory import get_optimizer
+from ..params import ParamStore
+from . import data_parallel as dp
+
+
+def _seed_of(rng, step):
+    if rng is None:
+        return None
+    if isinstance(rng, torch.Generator):
+        return int(torch.randint(0, 2 ** 31 - 1, (1,), generator=rng).item())
+    if isinstance(rng, torch.Tensor):
+        return int(rng.reshape(-1)[-1].item()) & 0x7FFFFFFF
+    try:
+        return int(rng) & 0x7FFFFFFF
+    except TypeError:
+        return (hash(rng) + step) & 0x7FFFFFFF
+
+
+def cross_entropy_loss(logits, labels):
+    """flax_engine.py:13-16 on the GPU kernel (mean softmax CE)."""
+    return compute_metrics(logits, labels)["loss"]
+
+
+def compute_metrics(logits, labels) -> Dict[str, torch.Tensor]:
+    """flax_engine.py:19-22: {'loss': mean CE, 'accuracy': mean(argmax == label)}."""
+    R = logits.shape[0]
+    lg = logits if logits.stride(-1) == 1 else logits.contiguous()
+    rl = torch.empty(R, dtype=torch.float32, device=lg.device)
+    rc = torch.empty(R, dtype=torch.float32, device=lg.device)
+    out = torch.empty(2, dtype=torch.float32, device=lg.device)
+    K.xent(lg, labels.to(torch.int32), rl, rc)
+    K.mean2(rl, rc, R, 1.0 / R, out)
+    return {"loss": out[0], "accuracy": out[1]}
+
+
+@dataclass
+class TrainState:
+    """flax TrainState (+ batch_stats) with the MI355X runtime attached."""
+    step: int
+    params: ParamStore
+    opt_state: Any
+    tx: Any
+    apply_fn: Any                       # the model definition (bind() -> runner)
+    batch_stats: Any = None
+    runners: Dict[tuple, Any] = field(default_factory=dict)
+    gscale: Optional[torch.Tensor] = None
+
+    def runner_for(self, image_shape):
+        key = tuple(int(s) for s in image_shape)
+        r = self.runners.get(key)
+        if r is None:
+            r = self.apply_fn.bind(self.params, key, self.params.device)
+            self.runners[key] = r
+        return r
+
+    def replace(self, **kw):
+        for k, v in kw.items():
+            setattr(self, k, v)
+        return self
+
+
+def create_train_state(rng, model_def, learning_rate: float, image_shape, num_classes: int, cfg=None,
+                       curvature_batch=None, device="cuda", init_params=None):
+    """flax_engine.py:30-66.  ``init_params`` ({name: tensor}) overrides the
+    initialiser (parity tests inject the oracle's params)."""
+    seed = _seed_of(rng, 0) or 0
+    layout = model_def.layout(image_shape)
+    store = ParamStore(layout, device)
+    store.load(init_params if init_params is not None else model_def.init(seed, image_shape))
+    if cfg is None:
+        tx = AdamW(learning_rate, weight_decay=1e-4)   # optax.adamw default weight_decay
+    else:
+        tx = get_optimizer(cfg, model_def=model_def, curvature_batch=curvature_batch, batch_stats=None)
+    opt_state = tx.init(store)
+    st = TrainState(step=0, params=store, opt_state=opt_state, tx=tx, apply_fn=model_def)
+    st.runner_for(image_shape)
+    return st
+
+
+def _prepare(runner, images, labels):
+    if images.device != runner.labels.device:
+        images = images.to(runner.labels.device, non_blocking=True)
+    if labels is not None and (labels.device != runner.labels.device or labels.dtype != torch.int32):
+        labels = labels.to(device=runner.labels.device, dtype=torch.int32, non_blocking=True)
+    return images.contiguous(), labels
+
+
+def make_train_step(return_updates: bool = False):
+    """flax_engine.py:95-123."""
+
+    def train_step(state: TrainState, batch, rng=None):
+        images, labels = batch
+        runner = state.runner_for(images.shape)
+        images, labels = _prepare(runner, images, labels)
+        seed = _seed_of(rng, state.step)
+        if seed is None:
+            K.seed_next(runner.seed)
+        else:
+            runner.seed.fill_(seed)
+        store = state.params
+        store.zero_grad()
+        metrics = runner.forward(images, labels, train=True, need_grad=True)
+        runner.backward(train=True)
+        dp.all_reduce_grads(store)
+        if return_updates:
+            grads = {k: v.clone() for k, v in store.grads.items()}
+            updates, state.opt_state = state.tx.update(store.grads, state.opt_state, store)
+            updates = {k: v.clone() for k, v in updates.items()}
+            apply_updates(store, updates)
+            state.step += 1
+            return state, {"loss": metrics[0], "accuracy": metrics[1]}, grads, updates
+        state.tx.step_(store, state.opt_state)
+        state.step += 1
+        return state, {"loss": metrics[0], "accuracy": metrics[1]}
+
+    return train_step
+
+
+def make_eval_step():
+    """flax_engine.py:126-134 (deterministic forward, no dropout)."""
+
+    def eval_step(state: TrainState, batch):
+        images, labels = batch
+        runner = state.runner_for(images.shape)
+        images, labels = _prepare(runner, images, labels)
+        m = runner.forward(images, labels, train=False, need_grad=False)
+        return {"loss": m[0].clone(), "accuracy": m[1].clone()}
+
+    return eval_step
+
+
+class GraphedTrainStep:
+    """One hipGraph per step: seed advance, zero-grad, forward, backward,
+    (all-reduce outside the graph when world_size > 1), optimizer.
+
+    Inputs are copied into static buffers before each replay."""
+
+    def __init__(self, state: TrainState, image_shape, warmup=2):
+        self.state = state
+        self.runner = state.runner_for(image_shape)
+        dev = state.params.device
+        self.images = torch.zeros(tuple(image_shape), dtype=torch.uint8, device=dev)
+        self.labels = torch.zeros(image_shape[0], dtype=torch.int32, device=dev)
+        self.distributed = dp.world_size() > 1
+        self.stream = torch.cuda.Stream(device=dev)
+        self.g_fb = torch.cuda.CUDAGraph()
+        self.g_opt = torch.cuda.CUDAGraph() if self.distributed else None
+        s = self.stream
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._fb()
+                self._opt()
+            torch.cuda.synchronize()
+            if self.distributed:
+                with torch.cuda.graph(self.g_fb, stream=s):
+                    self._fb()
+                with torch.cuda.graph(self.g_opt, stream=s):
+                    self._opt()
+            else:
+                with torch.cuda.graph(self.g_fb, stream=s):
+                    self._fb()
+                    self._opt()
+        torch.cuda.current_stream().wait_stream(s)
+        self.metrics = self.runner.metrics
+
+    def _fb(self):
+        K.seed_next(self.runner.seed)
+        self.state.params.zero_grad()
+        self.runner.forward(self.images, self.labels, train=True, need_grad=True)
+        self.runner.backward(train=True)
+
+    def _opt(self):
+        self.state.tx.step_(self.state.params, self.state.opt_state)
+
+    def __call__(self, images=None, labels=None):
+        if images is not None:
+            self.images.copy_(images, non_blocking=True)
+        if labels is not None:
+            self.labels.copy_(labels, non_blocking=True)
+        self.runner.labels.copy_(self.labels)
+        self.g_fb.replay()
+        if self.distributed:
+            dp.all_reduce_grads(self.state.params)
+            self.g_opt.replay()
+        self.state.step += 1
+        return self.metrics

@@ -1,0 +1,89 @@
+"""LM train-step functions (mirrors train_lm.py:173-353).
+
+    compute_grads, eval_step = make_train_fns(state, use_doc_mask=False)
+    for micro in range(accum):  compute_grads(state, input_ids)      # grads (+)= g/accum
+    apply_grads = make_apply_grads_fn(grad_clip)
+    state, gnorm = apply_grads(state)                               # clip, DP mean, optimizer, zero
+
+Gradients accumulate in the flat fp32 buffer with the 1/accum mean folded
+into the cross-entropy gradient scale, so after the last micro-step the buffer
+holds exactly the reference's ``grads_accum / grad_accum_steps``
+(train_lm.py:658-664).  ``apply_grads`` then all-reduces it ONCE across ranks
+(the reference pmeans every micro-step; equal up to rounding), derives the
+clip factor on the device (train_lm.py:173-178) and runs the optimizer.
+"""
+from dataclasses import dataclass, field
+from typing import Any
+
+import torch
+
+from .. import kernels as K
+from ..optim.factory import get_optimizer
+from ..params import ParamStore
+from . import data_parallel as dp
+
+
+@dataclass
+class LMTrainState:
+    step: int
+    params: ParamStore
+    opt_state: Any
+    tx: Any
+    model: Any
+    runner: Any
+    accum: int = 1
+    gscale: torch.Tensor = None
+    gnorm: torch.Tensor = None
+    chunks: torch.Tensor = None
+    partial: torch.Tensor = None
+    loss_sum: torch.Tensor = None
+
+
+def create_lm_state(cfg, model, variables, micro_batch, device, accum=1):
+    store = ParamStore(model.layout(), device)
+    store.load(variables["params"])
+    tx = get_optimizer(cfg, model_def=model)
+    opt_state = tx.init(store)
+    R = micro_batch * int(cfg.seq_len)
+    runner = model.bind(store, micro_batch, int(cfg.seq_len), device, grad_scale=1.0 / (R * accum))
+    chunks = store.chunks()
+    st = LMTrainState(step=0, params=store, opt_state=opt_state, tx=tx, model=model, runner=runner, accum=accum,
+                      gscale=torch.ones(1, device=device), gnorm=torch.zeros(1, device=device), chunks=chunks,
+                      partial=torch.zeros(int(chunks.shape[0]), device=device),
+                      loss_sum=torch.zeros(2, device=device))
+    return st
+
+
+def make_train_fns(use_doc_mask=False):
+    if use_doc_mask:
+        raise NotImplementedError("intra_doc_masking is SURVEY §8f-1 'next' (segment ids in the attention kernel)")
+
+    def compute_grads(state: LMTrainState, input_ids):
+        r = state.runner
+        r.set_batch(input_ids)
+        m = r.forward(need_grad=True)
+        r.backward()
+        state.loss_sum.add_(m)
+        return m
+
+    def eval_step(state: LMTrainState, input_ids):
+        r = state.runner
+        r.set_batch(input_ids)
+        m = r.forward(need_grad=False).clone()
+        return dp.all_reduce_metrics(m)
+
+    return compute_grads, eval_step
+
+
+def make_apply_grads_fn(grad_clip=None):
+    def apply_grads(state: LMTrainState):
+        store = state.params
+        dp.all_reduce_grads(store)
+        K.grad_scale(store.grad_flat, state.chunks, state.partial, 1.0, grad_clip if grad_clip else 0.0,
+                     state.gscale, state.gnorm)
+        state.tx.step_(store, state.opt_state, gscale=state.gscale if grad_clip else None)
+        store.zero_grad()
+        state.step += 1
+        return state, state.gnorm
+
+    return apply_grads

@@ -1,0 +1,111 @@
+"""ctypes binding of libplaincv_hip.so (the C-ABI declared in include/plaincv_hip.h).
+
+The product path has no fallback: if the library is missing or fails to load,
+every op raises.  Arguments are plain pointers / sizes / the caller's HIP
+stream, exactly as a ctypes/cgo/JNI consumer would bind them.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PLAINCV_HIP_LIB", os.path.join(_HERE, "libplaincv_hip.so"))
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int
+U32 = ctypes.c_uint32
+I64 = ctypes.c_int64
+F32 = ctypes.c_float
+
+# name -> argtypes (return type is always int status)
+SIGNATURES = {
+    "pcv_gemm_bf16": [P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, I64, I64, I64, I64,
+                      F32, F32, I32, P, P, I64, I64, I32, F32, P, I64, I32, F32, P, U32, I32, P],
+    "pcv_attn_fwd": [P, P, P, I64, P, I64, P, I32, I32, I32, I32, I32, F32, P, U32, P],
+    "pcv_attn_bwd": [P, P, P, I64, P, I64, P, I64, P, P, P, P, P, I64, I32, I32, I32, I32, I32,
+                     F32, P, U32, P],
+    "pcv_layernorm_fwd": [P, I64, P, P, P, I64, P, P, I64, I32, F32, P],
+    "pcv_layernorm_bwd": [P, I64, P, I64, P, P, P, P, I64, P, I64, P, I64, P, P, I64, I32, P],
+    "pcv_rmsnorm_fwd": [P, I64, P, P, I64, P, I64, I32, F32, P],
+    "pcv_rmsnorm_bwd": [P, I64, P, I64, P, P, P, I64, P, I64, P, I64, I32, P],
+    "pcv_rope": [P, I64, I64, I32, I32, I32, P, P, I32, P],
+    "pcv_swiglu_fwd": [P, I64, P, I64, I64, I32, I32, P],
+    "pcv_swiglu_bwd": [P, I64, P, I64, P, I64, I64, I32, I32, P],
+    "pcv_dropout_bwd_cast": [P, I64, P, I64, I64, I32, F32, P, U32, P],
+    "pcv_cast_f32_bf16": [P, P, I64, P],
+    "pcv_colsum": [P, I64, I64, I32, I32, P, P],
+    "pcv_vit_patchify": [P, P, I32, I32, I32, I32, I32, P],
+    "pcv_vit_embed_fwd": [P, P, P, P, P, I32, I32, I32, F32, P, U32, P],
+    "pcv_vit_embed_bwd": [P, P, P, P, P, I32, I32, I32, F32, P, U32, P],
+    "pcv_seed_next": [P, P],
+    "pcv_embed_fwd": [P, P, I64, P, I64, I64, I32, I32, P, P],
+    "pcv_embed_bwd": [P, P, I64, P, I64, I64, I32, I32, P],
+    "pcv_xent_fwd_bwd": [P, I64, I32, P, I64, I32, P, P, P, I64, F32, P],
+    "pcv_mean2": [P, P, I64, F32, P, P],
+    "pcv_adamw_step": [P, P, P, P, P, P, P, I32, F32, F32, F32, F32, F32, F32, I32, I32, P, P, P],
+    "pcv_grad_scale": [P, P, I32, P, F32, F32, P, P, P],
+    "pcv_step_bump": [P, P],
+    "pcv_muon_prep": [P, I32, I64, F32, I32, F32, P, P, P],
+    "pcv_muon_apply": [P, I32, I64, F32, F32, I32, I32, P],
+    "pcv_muon_mat_size": [],
+    "pcv_chunk_size": [],
+}
+
+_lib = None
+_err = None
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the library once (torch must already be imported so the process
+    shares torch's HIP runtime: both resolve the soname libamdhip64.so.7)."""
+    global _lib, _err
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HipLibraryError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(make -C plaincv_amd/csrc). The product path has no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, argt in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argt
+        fn.restype = ctypes.c_int
+    if hasattr(lib, "pcv_last_error_string"):
+        lib.pcv_last_error_string.argtypes = [ctypes.c_int]
+        lib.pcv_last_error_string.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+_ERRS = {-1: "invalid argument", -2: "misaligned pointer or leading dimension", -3: "shape mismatch"}
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        if rc < 0:
+            msg = _ERRS.get(rc, "error")
+        elif hasattr(lib, "pcv_last_error_string"):
+            msg = lib.pcv_last_error_string(rc).decode()
+        else:
+            msg = f"hipError {rc}"
+        raise RuntimeError(f"{name} failed: {msg} (rc={rc})")
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())

@@ -1,0 +1,289 @@
+"""Thin typed wrappers over the C-ABI kernels (torch tensors in, raw pointers out).
+
+Each wrapper validates shapes/dtypes/strides on the host before launching
+(a wrong shape must never reach a kernel) and launches on the current stream.
+"""
+import math
+
+import torch
+
+from . import hip
+from .hip import ptr, stream_ptr
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+EPI_NONE, EPI_GELU, EPI_GELU_BWD = 0, 1, 2
+
+
+def _ld(t):
+    if t.dim() < 2:
+        raise ValueError("expected a >=2-D tensor")
+    if t.stride(-1) != 1:
+        raise ValueError(f"innermost stride must be 1, got {t.stride()}")
+    return t.stride(-2)
+
+
+def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=None, res_scale=1.0, aux=None,
+         act=EPI_NONE, drop_rate=0.0, seed=None, site=0, split_k=None):
+    """out[M,N] = epi(alpha * op(a) @ op(b)).
+
+    a: [M,K] (ta=False) or [K,M] (ta=True); b: [K,N] (tb=False) or [N,K] (tb=True).
+    Optional leading batch dim on a, b, out (same batch size).  bf16 inputs,
+    bf16 or fp32 output (fp32: out = v + beta*out).  Epilogue order:
+    +bias -> [gelu (aux<-preact) | *gelu'(aux)] -> dropout -> +res."""
+    batched = a.dim() == 3
+    if batched:
+        nb = a.shape[0]
+        if b.dim() != 3 or out.dim() != 3 or b.shape[0] != nb or out.shape[0] != nb:
+            raise ValueError("batched gemm needs 3-D a, b, out with equal batch")
+        sa, sb, sc = a.stride(0), b.stride(0), out.stride(0)
+        a2, b2, o2 = a[0], b[0], out[0]
+    else:
+        nb, sa, sb, sc = 1, 0, 0, 0
+        a2, b2, o2 = a, b, out
+    if ta:
+        K, M = a2.shape
+    else:
+        M, K = a2.shape
+    if tb:
+        N, K2 = b2.shape
+    else:
+        K2, N = b2.shape
+    if K != K2:
+        raise ValueError(f"gemm contraction mismatch {K} vs {K2}")
+    if tuple(o2.shape) != (M, N):
+        raise ValueError(f"gemm out shape {tuple(o2.shape)} != {(M, N)}")
+    if a.dtype != BF16 or b.dtype != BF16:
+        raise ValueError("gemm operands must be bf16")
+    if out.dtype not in (BF16, F32):
+        raise ValueError("gemm out must be bf16 or fp32")
+    if not (a.is_cuda and b.is_cuda and out.is_cuda):
+        raise ValueError("gemm tensors must be on the GPU")
+    out_f32 = int(out.dtype == F32)
+    if bias is not None and (bias.dtype != F32 or bias.numel() != N or not bias.is_contiguous()):
+        raise ValueError("bias must be contiguous fp32 [N]")
+    ldr, res_f32, sr = 0, 0, 0
+    if res is not None:
+        if tuple(res.shape[-2:]) != (M, N):
+            raise ValueError("residual shape mismatch")
+        ldr, res_f32 = _ld(res), int(res.dtype == F32)
+        if batched:
+            if res.dim() != 3 or res.shape[0] != nb:
+                raise ValueError("batched gemm needs a batched residual")
+            sr = res.stride(0)
+    ldaux = 0
+    if batched and (bias is not None or act != EPI_NONE or drop_rate > 0.0):
+        raise ValueError("batched gemm supports only the residual epilogue")
+    if act != EPI_NONE:
+        if aux is None or aux.dtype != BF16 or tuple(aux.shape[-2:]) != (M, N):
+            raise ValueError("gelu epilogue needs bf16 aux [M,N]")
+        ldaux = _ld(aux)
+    if split_k is None:
+        split_k = 1
+        plain = out_f32 and beta == 1.0 and bias is None and res is None and act == EPI_NONE and drop_rate == 0.0
+        if plain and K >= 1024:
+            t64 = math.ceil(M / 64) * math.ceil(N / 64) * nb
+            if t64 < 512:
+                split_k = max(1, min(math.ceil(1024 / t64), K // 512))
+    hip.call("pcv_gemm_bf16", ptr(a2), ptr(b2), ptr(o2), M, N, K, _ld(a2), _ld(b2), _ld(o2),
+             int(ta), int(tb), nb, sa, sb, sc, float(alpha), float(beta), out_f32,
+             ptr(bias), ptr(res), ldr, sr, res_f32, float(res_scale), ptr(aux), ldaux, int(act),
+             float(drop_rate), ptr(seed), int(site) & 0xFFFFFFFF, int(split_k), stream_ptr())
+    return out
+
+
+def _chk(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("tensor must live on the GPU")
+
+
+def attn_fwd(qkv, out, lse2, B, T, H, Dh, causal, drop_rate=0.0, seed=None, site=0, q_off=0, k_off=None, v_off=None):
+    """Flash attention forward on packed qkv [B*T, ld] (q|k|v column blocks)."""
+    D = H * Dh
+    k_off = D if k_off is None else k_off
+    v_off = 2 * D if v_off is None else v_off
+    _chk(qkv.dtype == BF16 and out.dtype == BF16 and lse2.dtype == F32, "attn dtypes")
+    _chk(qkv.shape[0] == B * T and out.shape[0] == B * T and lse2.numel() >= B * H * T, "attn shapes")
+    _dev(qkv, out, lse2)
+    base = qkv.data_ptr()
+    es = qkv.element_size()
+    hip.call("pcv_attn_fwd", base + q_off * es, base + k_off * es, base + v_off * es, _ld(qkv),
+             ptr(out), _ld(out), ptr(lse2), B, T, H, Dh, int(causal), float(drop_rate),
+             ptr(seed), int(site), stream_ptr())
+
+
+def attn_bwd(qkv, o, dout, lse2, delta_ws, dqkv, B, T, H, Dh, causal, drop_rate=0.0, seed=None, site=0):
+    D = H * Dh
+    _chk(qkv.dtype == BF16 and dqkv.dtype == BF16 and dout.dtype == BF16 and o.dtype == BF16, "attn bwd dtypes")
+    _chk(dqkv.shape[0] == B * T and dqkv.shape[1] >= 3 * D and delta_ws.numel() >= B * H * T, "attn bwd shapes")
+    _dev(qkv, o, dout, lse2, delta_ws, dqkv)
+    base, es = qkv.data_ptr(), qkv.element_size()
+    dbase = dqkv.data_ptr()
+    hip.call("pcv_attn_bwd", base, base + D * es, base + 2 * D * es, _ld(qkv), ptr(o), _ld(o), ptr(dout),
+             _ld(dout), ptr(lse2), ptr(delta_ws), dbase, dbase + D * es, dbase + 2 * D * es, _ld(dqkv),
+             B, T, H, Dh, int(causal), float(drop_rate), ptr(seed), int(site), stream_ptr())
+
+
+def layernorm_fwd(x, scale, bias, y, mean, rstd, eps=1e-6):
+    R, D = x.shape
+    _chk(x.dtype == F32 and y.dtype == BF16 and tuple(y.shape) == (R, D), "layernorm fwd")
+    _dev(x, scale, bias, y, mean, rstd)
+    hip.call("pcv_layernorm_fwd", ptr(x), _ld(x), ptr(scale), ptr(bias), ptr(y), _ld(y), ptr(mean), ptr(rstd),
+             R, D, float(eps), stream_ptr())
+
+
+def layernorm_bwd(dy, x, scale, mean, rstd, dres, dx, dx_bf16, dscale, dbias):
+    R, D = x.shape
+    _chk(dy.dtype == F32 and dx.dtype == F32 and tuple(dy.shape) == (R, D), "layernorm bwd")
+    _dev(dy, x, scale, mean, rstd, dres, dx, dx_bf16, dscale, dbias)
+    hip.call("pcv_layernorm_bwd", ptr(dy), _ld(dy), ptr(x), _ld(x), ptr(scale), ptr(mean), ptr(rstd),
+             ptr(dres), _ld(dres) if dres is not None else 0, ptr(dx), _ld(dx), ptr(dx_bf16),
+             _ld(dx_bf16) if dx_bf16 is not None else 0, ptr(dscale), ptr(dbias), R, D, stream_ptr())
+
+
+def rmsnorm_fwd(x, scale, y, rstd, eps=1e-6):
+    R, D = x.shape
+    _chk(x.dtype == BF16 and y.dtype == BF16 and tuple(y.shape) == (R, D), "rmsnorm fwd")
+    _dev(x, scale, y, rstd)
+    hip.call("pcv_rmsnorm_fwd", ptr(x), _ld(x), ptr(scale), ptr(y), _ld(y), ptr(rstd), R, D, float(eps),
+             stream_ptr())
+
+
+def rmsnorm_bwd(dy, x, scale, rstd, dres, dx, dscale):
+    R, D = x.shape
+    _chk(dy.dtype == BF16 and dx.dtype == BF16 and tuple(dy.shape) == (R, D), "rmsnorm bwd")
+    _dev(dy, x, scale, rstd, dres, dx, dscale)
+    hip.call("pcv_rmsnorm_bwd", ptr(dy), _ld(dy), ptr(x), _ld(x), ptr(scale), ptr(rstd), ptr(dres),
+             _ld(dres) if dres is not None else 0, ptr(dx), _ld(dx), ptr(dscale), R, D, stream_ptr())
+
+
+def rope(qk, T, Dh, cos_tab, sin_tab, backward=False, ncols=None):
+    R = qk.shape[0]
+    ncols = qk.shape[1] if ncols is None else ncols
+    _chk(qk.dtype == BF16 and cos_tab.dtype == F32, "rope dtypes")
+    _dev(qk, cos_tab, sin_tab)
+    hip.call("pcv_rope", ptr(qk), _ld(qk), R, ncols, T, Dh, ptr(cos_tab), ptr(sin_tab), int(backward),
+             stream_ptr())
+
+
+def swiglu_fwd(gu, h, F=None):
+    """gu [R, 2*Fp] = gate|up halves (Fp = F padded to 8), h [R, >=Fp]."""
+    R = h.shape[0]
+    Fp = gu.shape[1] // 2
+    F = Fp if F is None else F
+    _chk(gu.shape[0] == R and gu.shape[1] == 2 * Fp and Fp % 8 == 0 and gu.dtype == BF16 and h.dtype == BF16,
+         "swiglu fwd")
+    _chk(_ld(h) >= Fp, "swiglu fwd h ld")
+    _dev(gu, h)
+    hip.call("pcv_swiglu_fwd", ptr(gu), _ld(gu), ptr(h), _ld(h), R, F, Fp, stream_ptr())
+
+
+def swiglu_bwd(dh, gu, dgu, F=None):
+    R = dh.shape[0]
+    Fp = gu.shape[1] // 2
+    F = Fp if F is None else F
+    _chk(gu.shape[0] == R and dgu.shape[0] == R and tuple(dgu.shape) == tuple(gu.shape), "swiglu bwd")
+    _chk(_ld(dh) >= Fp, "swiglu bwd dh ld")
+    _dev(dh, gu, dgu)
+    hip.call("pcv_swiglu_bwd", ptr(dh), _ld(dh), ptr(gu), _ld(gu), ptr(dgu), _ld(dgu), R, F, Fp, stream_ptr())
+
+
+def dropout_bwd_cast(x, out, rate=0.0, seed=None, site=0):
+    R, N = x.shape
+    _chk(x.dtype == F32 and out.dtype == BF16 and tuple(out.shape) == (R, N), "dropout_bwd_cast")
+    _dev(x, out)
+    hip.call("pcv_dropout_bwd_cast", ptr(x), _ld(x), ptr(out), _ld(out), R, N, float(rate),
+             ptr(seed), int(site), stream_ptr())
+
+
+def cast_f32_bf16(x, y):
+    _chk(x.is_contiguous() and y.is_contiguous() and x.numel() == y.numel(), "cast")
+    _dev(x, y)
+    hip.call("pcv_cast_f32_bf16", ptr(x), ptr(y), x.numel(), stream_ptr())
+
+
+def colsum(x, out):
+    R, N = x.shape
+    _chk(out.dtype == F32 and out.numel() == N and out.is_contiguous(), "colsum out")
+    _dev(x, out)
+    hip.call("pcv_colsum", ptr(x), _ld(x), R, N, int(x.dtype == F32), ptr(out), stream_ptr())
+
+
+def vit_patchify(images, out, patch):
+    B, H, W, C = images.shape
+    _chk(images.dtype == torch.uint8 and images.is_contiguous() and out.dtype == BF16 and out.is_contiguous(),
+         "patchify")
+    _chk(out.numel() == B * (H // patch) * (W // patch) * patch * patch * C, "patchify out size")
+    _dev(images, out)
+    hip.call("pcv_vit_patchify", ptr(images), ptr(out), B, H, W, C, patch, stream_ptr())
+
+
+def vit_embed_fwd(patch_out, cls, pos, x, x_bf16, B, T, D, rate=0.0, seed=None, site=0):
+    _chk(patch_out.numel() == B * (T - 1) * D and x.numel() == B * T * D and pos.numel() == T * D, "embed fwd")
+    _dev(patch_out, cls, pos, x, x_bf16)
+    hip.call("pcv_vit_embed_fwd", ptr(patch_out), ptr(cls), ptr(pos), ptr(x), ptr(x_bf16), B, T, D, float(rate),
+             ptr(seed), int(site), stream_ptr())
+
+
+def vit_embed_bwd(dx, dpatch, dcls, dpos, dbias, B, T, D, rate=0.0, seed=None, site=0):
+    _chk(dx.numel() == B * T * D and dpatch.numel() == B * (T - 1) * D, "embed bwd")
+    _dev(dx, dpatch, dcls, dpos, dbias)
+    hip.call("pcv_vit_embed_bwd", ptr(dx), ptr(dpatch), ptr(dcls), ptr(dpos), ptr(dbias), B, T, D, float(rate),
+             ptr(seed), int(site), stream_ptr())
+
+
+def embed_fwd(ids, table, out, oob=None):
+    R = ids.numel()
+    V, D = table.shape
+    _chk(ids.dtype == torch.int32 and table.dtype == BF16 and tuple(out.shape) == (R, D), "embed fwd")
+    _dev(ids, table, out, oob)
+    hip.call("pcv_embed_fwd", ptr(ids), ptr(table), _ld(table), ptr(out), _ld(out), R, D, V, ptr(oob),
+             stream_ptr())
+
+
+def embed_bwd(ids, dx, dtable):
+    R = ids.numel()
+    V, D = dtable.shape
+    _chk(dtable.dtype == F32 and tuple(dx.shape) == (R, D), "embed bwd")
+    _dev(ids, dx, dtable)
+    hip.call("pcv_embed_bwd", ptr(ids), ptr(dx), _ld(dx), ptr(dtable), _ld(dtable), R, D, V, stream_ptr())
+
+
+def xent(logits, labels, row_loss, row_correct, dlogits=None, grad_scale=1.0):
+    R, V = logits.shape
+    _chk(labels.dtype == torch.int32 and labels.numel() == R and row_loss.numel() >= R, "xent")
+    _chk(dlogits is None or (dlogits.dtype == logits.dtype and tuple(dlogits.shape) == (R, V)), "xent dlogits")
+    _dev(logits, labels, row_loss, row_correct, dlogits)
+    hip.call("pcv_xent_fwd_bwd", ptr(logits), _ld(logits), int(logits.dtype == F32), ptr(labels), R, V,
+             ptr(row_loss), ptr(row_correct), ptr(dlogits), _ld(dlogits) if dlogits is not None else 0,
+             float(grad_scale), stream_ptr())
+
+
+def mean2(x, y, n, scale, out):
+    _dev(x, y, out)
+    hip.call("pcv_mean2", ptr(x), ptr(y), int(n), float(scale), ptr(out), stream_ptr())
+
+
+def seed_next(seed_buf):
+    """Advance the device dropout seed (uint32 stored in an int32 tensor)."""
+    _dev(seed_buf)
+    hip.call("pcv_seed_next", ptr(seed_buf), stream_ptr())
+
+
+def step_bump(count):
+    _dev(count)
+    hip.call("pcv_step_bump", ptr(count), stream_ptr())
+
+
+def grad_scale(grad_flat, chunks, partial_ws, inv_accum, clip, gscale, gnorm=None):
+    """gscale <- min(1, clip/(||g*inv_accum||+1e-6)) * inv_accum (clip<=0: no clip)."""
+    _dev(grad_flat, chunks, partial_ws, gscale, gnorm)
+    hip.call("pcv_grad_scale", ptr(grad_flat), ptr(chunks), int(chunks.shape[0]), ptr(partial_ws),
+             float(inv_accum), float(clip if clip is not None else 0.0), ptr(gscale), ptr(gnorm), stream_ptr())

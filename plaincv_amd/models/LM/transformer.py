@@ -1,0 +1,256 @@
+"""Causal LM (RoPE + SwiGLU + RMSNorm) on the MI355X kernels.
+
+Mirrors models/LM/transformer.py:13-407 and embedding.py:8-66: same
+``ModelConfig`` fields, the same Flax parameter names/shapes
+(``embed_tokens/embedding``, ``layers_{i}/attn/w_qkv/kernel`` ...) and the
+reference's bf16 placement (lm_adam.yaml ``dtype: bfloat16``): fp32 master
+params, bf16 Dense/Embed outputs, fp32 RMSNorm statistics with a bf16 output,
+RoPE in fp32 rounded back, fp32 logits-softmax in attention with bf16 P, a bf16
+residual stream and fp32 cross-entropy.
+
+``Transformer.bind(store, micro_batch, seq_len, device)`` returns an
+``LMRunner`` (fixed-shape forward/backward executor, no autograd).  Storage
+choices: fc_gate|fc_up are one interleaved [d, 2F] operand (one GEMM), the
+vocab axis of lm_head and the hidden axis are padded to multiples of 8, the
+logits buffer is overwritten in place by dlogits.
+"""
+import math
+from dataclasses import dataclass
+from typing import Literal
+
+import torch
+
+from ... import kernels as K
+from ...params import Layout
+
+
+@dataclass
+class ModelConfig:
+    vocab_size: int
+    seq_len: int
+    dim: int
+    expand: float
+    n_layers: int
+    n_heads: int
+    mlp: Literal["mlp", "glu", "mlp_relu_sq"] = "mlp"
+    rmsnorm_eps: float = 1e-6
+    tie_embeddings: bool = False
+    rope_theta: float = 500000.0
+    dtype: torch.dtype = torch.float32
+    param_dtype: torch.dtype = torch.float32
+
+    @property
+    def hidden_dim(self):
+        return int(self.expand * self.dim)
+
+
+def _pad8(n):
+    return (n + 7) // 8 * 8
+
+
+def precompute_freqs_cis(dim, end, theta=10000.0):
+    """embedding.py:8-26 -> cos, sin (end, dim/2) fp32 (host, like the reference's jnp fp32)."""
+    inv = 1.0 / (theta ** (torch.arange(0, dim, 2, dtype=torch.float32) / dim))
+    t = torch.arange(end, dtype=torch.float32)
+    f = torch.outer(t, inv)
+    return torch.cos(f), torch.sin(f)
+
+
+class Transformer:
+    def __init__(self, cfg: ModelConfig, normtype="rmsnorm"):
+        if normtype != "rmsnorm":
+            raise NotImplementedError("only the rmsnorm Block is on the hot path")
+        if cfg.mlp != "glu":
+            raise NotImplementedError(f"mlp={cfg.mlp!r}: only the GLU (SwiGLU) block is on the hot path")
+        if cfg.dim % cfg.n_heads:
+            raise ValueError("dim must be divisible by n_heads")
+        self.cfg = cfg
+
+    def layout(self):
+        c = self.cfg
+        d, F, V = c.dim, c.hidden_dim, c.vocab_size
+        L = Layout()
+        L.add("embed_tokens/embedding", (V, d))
+        for i in range(c.n_layers):
+            p = f"layers_{i}"
+            L.add(f"{p}/attn_norm/RMSNorm_0/scale", (d,))
+            L.add(f"{p}/attn/w_qkv/kernel", (d, 3 * d))
+            L.add(f"{p}/attn/w_out/kernel", (d, d))
+            L.add(f"{p}/mlp_norm/RMSNorm_0/scale", (d,))
+            L.add_fused(f"{p}/mlp/gate_up", [f"{p}/mlp/fc_gate/kernel", f"{p}/mlp/fc_up/kernel"], (d, F),
+                        pad_each=True)
+            L.add(f"{p}/mlp/fc2/kernel", (F, d))
+        L.add("out_norm/RMSNorm_0/scale", (d,))
+        if not c.tie_embeddings:
+            L.add("lm_head/kernel", (d, V))
+        return L
+
+    def init(self, seed):
+        """normal(0.02) embed/w_qkv/fc_gate/fc_up/lm_head, normal(0.02/sqrt(2L)) w_out/fc2,
+        ones norms (transformer.py:188-191, 296-298, 358-368)."""
+        c = self.cfg
+        gen = torch.Generator().manual_seed(int(seed))
+        resid = 0.02 / math.sqrt(2 * c.n_layers)
+        out = {}
+        for name, leaf in self.layout().leaves.items():
+            if name.endswith("/scale"):
+                out[name] = torch.ones(leaf.shape)
+            elif name.endswith("w_out/kernel") or name.endswith("fc2/kernel"):
+                out[name] = torch.randn(leaf.shape, generator=gen) * resid
+            else:
+                out[name] = torch.randn(leaf.shape, generator=gen) * 0.02
+        return out
+
+    def bind(self, store, micro_batch, seq_len, device, grad_scale=None):
+        return LMRunner(self, store, micro_batch, seq_len, device, grad_scale)
+
+    def num_params(self, non_embedding=False):
+        n = 0
+        for name, leaf in self.layout().leaves.items():
+            if non_embedding and name.startswith("embed_tokens/"):
+                continue
+            n += int(math.prod(leaf.shape))
+        return n
+
+    def flops_per_token(self, seq_len=None):
+        """PaLM convention 6*N_matmul + 12*L*T*d, full attention counted."""
+        c = self.cfg
+        T = seq_len or c.seq_len
+        n_mat = self.num_params(non_embedding=True) - (2 * c.n_layers + 1) * c.dim
+        return 6 * n_mat + 12 * c.n_layers * T * c.dim
+
+
+class LMRunner:
+    def __init__(self, model: Transformer, store, b, T, device, grad_scale=None):
+        c = model.cfg
+        self.m, self.s, self.c = model, store, c
+        self.b, self.T = b, T
+        self.R = R = b * T
+        self.d, self.H = c.dim, c.n_heads
+        self.Dh = c.dim // c.n_heads
+        self.F = c.hidden_dim
+        self.Fp = _pad8(self.F)
+        self.V = c.vocab_size
+        self.Vp = _pad8(self.V)
+        if self.Dh not in (32, 64, 128) or self.d % 8:
+            raise ValueError("head_dim must be 32/64/128 and d_model a multiple of 8")
+        dev = torch.device(device)
+        bf, f32 = torch.bfloat16, torch.float32
+        e = lambda *s, dt=bf: torch.empty(*s, dtype=dt, device=dev)  # noqa: E731
+        L = c.n_layers
+        d = self.d
+        self.inputs = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.labels = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.x = [e(R, d) for _ in range(L + 1)]
+        self.x1 = [e(R, d) for _ in range(L)]
+        self.y0 = [e(R, d) for _ in range(L)]
+        self.y1 = [e(R, d) for _ in range(L)]
+        self.r0 = [e(R, dt=f32) for _ in range(L)]
+        self.r1 = [e(R, dt=f32) for _ in range(L)]
+        self.qkv = [e(R, 3 * d) for _ in range(L)]
+        self.o = [e(R, d) for _ in range(L)]
+        self.lse = [e(b * self.H * T, dt=f32) for _ in range(L)]
+        # [gate | up] halves of Fp columns each (pads are zero after swiglu)
+        self.gu = [e(R, 2 * self.Fp) for _ in range(L)]
+        self.hm = [e(R, self.Fp)[:, : self.F] for _ in range(L)]
+        self.yf = e(R, d)
+        self.rf = e(R, dt=f32)
+        self.logits = e(R, self.Vp)[:, : self.V]
+        self.row_loss = e(R, dt=f32)
+        self.row_correct = e(R, dt=f32)
+        self.metrics = torch.zeros(2, dtype=f32, device=dev)
+        # backward workspaces
+        self.dx = e(R, d)
+        self.dy = e(R, d)
+        self.dh = e(R, self.Fp)[:, : self.F]
+        self.dgu = e(R, 2 * self.Fp)
+        self.do = e(R, d)
+        self.dqkv = e(R, 3 * d)
+        self.delta = e(b * self.H * T, dt=f32)
+        cos, sin = precompute_freqs_cis(self.Dh, c.seq_len, c.rope_theta)
+        self.cos = cos[:T].contiguous().to(dev)
+        self.sin = sin[:T].contiguous().to(dev)
+        self.grad_scale = 1.0 / R if grad_scale is None else grad_scale
+        self._views()
+
+    def _views(self):
+        s, c = self.s, self.c
+        P, G, W = s.params, s.grads, s.bf16
+        self.w = []
+        for i in range(c.n_layers):
+            p = f"layers_{i}"
+            self.w.append({
+                "s0": P[f"{p}/attn_norm/RMSNorm_0/scale"], "gs0": G[f"{p}/attn_norm/RMSNorm_0/scale"],
+                "Wqkv": W[f"{p}/attn/w_qkv/kernel"], "gWqkv": G[f"{p}/attn/w_qkv/kernel"],
+                "Wo": W[f"{p}/attn/w_out/kernel"], "gWo": G[f"{p}/attn/w_out/kernel"],
+                "s1": P[f"{p}/mlp_norm/RMSNorm_0/scale"], "gs1": G[f"{p}/mlp_norm/RMSNorm_0/scale"],
+                "Wgu": s.group_view(s.shadow, f"{p}/mlp/gate_up"),
+                "gWgu": s.group_view(s.grad_flat, f"{p}/mlp/gate_up"),
+                "W2": W[f"{p}/mlp/fc2/kernel"], "gW2": G[f"{p}/mlp/fc2/kernel"],
+            })
+        self.Wemb, self.gWemb = W["embed_tokens/embedding"], G["embed_tokens/embedding"]
+        self.sf, self.gsf = P["out_norm/RMSNorm_0/scale"], G["out_norm/RMSNorm_0/scale"]
+        if not c.tie_embeddings:
+            self.Wh, self.gWh = W["lm_head/kernel"], G["lm_head/kernel"]
+
+    def set_batch(self, input_ids):
+        """input_ids (b, T+1) int on the GPU -> inputs/labels (train_lm.py:141-142)."""
+        b, T = self.b, self.T
+        if tuple(input_ids.shape) != (b, T + 1):
+            raise ValueError(f"Expected input_ids of shape {(b, T + 1)}, got {tuple(input_ids.shape)}")
+        self.inputs.view(b, T).copy_(input_ids[:, :-1])
+        self.labels.view(b, T).copy_(input_ids[:, 1:])
+
+    def forward(self, need_grad=True):
+        c = self.c
+        b, T, d, H, Dh = self.b, self.T, self.d, self.H, self.Dh
+        eps = c.rmsnorm_eps
+        K.embed_fwd(self.inputs, self.Wemb, self.x[0])
+        for i in range(c.n_layers):
+            w = self.w[i]
+            K.rmsnorm_fwd(self.x[i], w["s0"], self.y0[i], self.r0[i], eps)
+            K.gemm(self.y0[i], w["Wqkv"], self.qkv[i])
+            K.rope(self.qkv[i], T, Dh, self.cos, self.sin, ncols=2 * d)
+            K.attn_fwd(self.qkv[i], self.o[i], self.lse[i], b, T, H, Dh, causal=True)
+            K.gemm(self.o[i], w["Wo"], self.x1[i], res=self.x[i])
+            K.rmsnorm_fwd(self.x1[i], w["s1"], self.y1[i], self.r1[i], eps)
+            K.gemm(self.y1[i], w["Wgu"], self.gu[i])
+            K.swiglu_fwd(self.gu[i], self.hm[i], F=self.F)
+            K.gemm(self.hm[i], w["W2"], self.x[i + 1], res=self.x1[i])
+        K.rmsnorm_fwd(self.x[-1], self.sf, self.yf, self.rf, eps)
+        if c.tie_embeddings:
+            K.gemm(self.yf, self.Wemb, self.logits, tb=True)
+        else:
+            K.gemm(self.yf, self.Wh, self.logits)
+        K.xent(self.logits, self.labels, self.row_loss, self.row_correct,
+               self.logits if need_grad else None, grad_scale=self.grad_scale)
+        K.mean2(self.row_loss, self.row_correct, self.R, 1.0 / self.R, self.metrics)
+        return self.metrics
+
+    def backward(self):
+        c = self.c
+        b, T, d, H, Dh = self.b, self.T, self.d, self.H, self.Dh
+        dl = self.logits  # dlogits (in place)
+        if c.tie_embeddings:
+            K.gemm(dl, self.yf, self.gWemb, ta=True, beta=1.0)
+            K.gemm(dl, self.Wemb, self.dy, tb=False)
+        else:
+            K.gemm(self.yf, dl, self.gWh, ta=True, beta=1.0)
+            K.gemm(dl, self.Wh, self.dy, tb=True)
+        K.rmsnorm_bwd(self.dy, self.x[-1], self.sf, self.rf, None, self.dx, self.gsf)
+        for i in reversed(range(c.n_layers)):
+            w = self.w[i]
+            K.gemm(self.hm[i], self.dx, w["gW2"], ta=True, beta=1.0)
+            K.gemm(self.dx, w["W2"], self.dh, tb=True)
+            K.swiglu_bwd(self.dh, self.gu[i], self.dgu, F=self.F)
+            K.gemm(self.y1[i], self.dgu, w["gWgu"], ta=True, beta=1.0)
+            K.gemm(self.dgu, w["Wgu"], self.dy, tb=True)
+            K.rmsnorm_bwd(self.dy, self.x1[i], w["s1"], self.r1[i], self.dx, self.dx, w["gs1"])
+            K.gemm(self.o[i], self.dx, w["gWo"], ta=True, beta=1.0)
+            K.gemm(self.dx, w["Wo"], self.do, tb=True)
+            K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, self.dqkv, b, T, H, Dh, causal=True)
+            K.rope(self.dqkv, T, Dh, self.cos, self.sin, backward=True, ncols=2 * d)
+            K.gemm(self.y0[i], self.dqkv, w["gWqkv"], ta=True, beta=1.0)
+            K.gemm(self.dqkv, w["Wqkv"], self.dy, tb=True)
+            K.rmsnorm_bwd(self.dy, self.x[i], w["s0"], self.r0[i], self.dx, self.dx, w["gs0"])
+        K.embed_bwd(self.inputs, self.dx, self.gWemb)

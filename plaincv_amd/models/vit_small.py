@@ -1,0 +1,341 @@
+"""ViT-small on the MI355X kernels (mirrors models/vit_small.py:6-127).
+
+``VisionTransformer`` keeps the reference constructor fields and the Flax
+parameter pytree (names + shapes), and adds ``bind()`` which returns a
+``ViTRunner``: a fixed-shape executor that owns every activation buffer and
+runs the hand-written forward and backward as a straight sequence of C-ABI
+launches (no autograd, no allocation after the first call, hipGraph-capturable).
+
+Numerics: bf16 MFMA operands with fp32 accumulation; the residual stream, the
+LayerNorm statistics, softmax and every gradient reduction stay fp32
+(the reference ViT is fp32: the bf16 operands are BASELINE.json config 2's
+"bf16").  Dropout uses the counter hash shared with oracle/rng.py.
+"""
+import math
+
+import torch
+
+from .. import kernels as K
+from ..params import Layout, ParamStore
+
+SITE_EMBED = 1
+
+
+def site_attn(i):
+    return 16 + 4 * i
+
+
+def site_mlp_hidden(i):
+    return 16 + 4 * i + 1
+
+
+def site_mlp_out(i):
+    return 16 + 4 * i + 2
+
+
+def _pad8(n):
+    return (n + 7) // 8 * 8
+
+
+def _lecun_normal(shape, fan_in, gen):
+    """flax lecun_normal = variance_scaling(1, fan_in, truncated_normal)."""
+    std = math.sqrt(1.0 / fan_in) / 0.87962566103423978
+    t = torch.empty(shape, dtype=torch.float32)
+    torch.nn.init.trunc_normal_(t, mean=0.0, std=1.0, a=-2.0, b=2.0, generator=gen)
+    return t * std
+
+
+class VisionTransformer:
+    """Reference signature: VisionTransformer(num_classes, patch_size, hidden_size,
+    mlp_dim, num_layers, num_heads, dropout_rate, use_layernorm, use_batchnorm)."""
+
+    def __init__(self, num_classes=10, patch_size=4, hidden_size=128, mlp_dim=256, num_layers=4, num_heads=4,
+                 dropout_rate=0.1, use_layernorm=True, use_batchnorm=False):
+        if use_batchnorm and use_layernorm:
+            raise ValueError("use_batchnorm and use_layernorm cannot both be True.")
+        if use_batchnorm:
+            raise NotImplementedError("use_batchnorm ViT is SURVEY.md §8f-3 'next' (needs batch_stats)")
+        self.num_classes = num_classes
+        self.patch_size = patch_size
+        self.hidden_size = hidden_size
+        self.mlp_dim = mlp_dim
+        self.num_layers = num_layers
+        self.num_heads = num_heads
+        self.dropout_rate = float(dropout_rate)
+        self.use_layernorm = use_layernorm
+        self.use_batchnorm = use_batchnorm
+        if hidden_size % num_heads:
+            raise ValueError("hidden_size must be divisible by num_heads")
+
+    # ------------------------------------------------------------ params
+    def layout(self, image_shape):
+        """Flat layout for images of shape (B, H, W, C) (B unused)."""
+        _, Hh, Ww, C = image_shape
+        D, M, H = self.hidden_size, self.mlp_dim, self.num_heads
+        Dh = D // H
+        ps = self.patch_size
+        T = (Hh // ps) * (Ww // ps) + 1
+        L = Layout()
+        L.add("Conv_0/kernel", (ps, ps, C, D))
+        L.add("Conv_0/bias", (D,))
+        L.add("cls_token", (1, 1, D))
+        L.add("pos_embedding", (1, T, D))
+        for i in range(self.num_layers):
+            pre = f"EncoderBlock_{i}"
+            if self.use_layernorm:
+                L.add(f"{pre}/LayerNorm_0/scale", (D,))
+                L.add(f"{pre}/LayerNorm_0/bias", (D,))
+            a = f"{pre}/SelfAttention_0"
+            L.add_fused(f"{a}/qkv_kernel", [f"{a}/{n}/kernel" for n in ("query", "key", "value")], (D, H, Dh))
+            L.add_concat(f"{a}/qkv_bias", [f"{a}/{n}/bias" for n in ("query", "key", "value")], (H, Dh))
+            L.add(f"{a}/out/kernel", (H, Dh, D))
+            L.add(f"{a}/out/bias", (D,))
+            if self.use_layernorm:
+                L.add(f"{pre}/LayerNorm_1/scale", (D,))
+                L.add(f"{pre}/LayerNorm_1/bias", (D,))
+            L.add(f"{pre}/MlpBlock_0/Dense_0/kernel", (D, M))
+            L.add(f"{pre}/MlpBlock_0/Dense_0/bias", (M,))
+            L.add(f"{pre}/MlpBlock_0/Dense_1/kernel", (M, D))
+            L.add(f"{pre}/MlpBlock_0/Dense_1/bias", (D,))
+        if self.use_layernorm:
+            L.add("LayerNorm_0/scale", (D,))
+            L.add("LayerNorm_0/bias", (D,))
+        L.add("Dense_0/kernel", (D, self.num_classes))
+        L.add("Dense_0/bias", (self.num_classes,))
+        return L
+
+    def init(self, seed, image_shape):
+        """Flax initialisers (lecun_normal kernels, zero biases, zero cls token,
+        normal(0.02) pos embedding, LayerNorm ones/zeros) -> {name: cpu tensor}.
+        The stream differs from JAX's threefry, so parity tests inject params."""
+        gen = torch.Generator().manual_seed(int(seed))
+        out = {}
+        D, M, H = self.hidden_size, self.mlp_dim, self.num_heads
+        for name, leaf in self.layout(image_shape).leaves.items():
+            shp = leaf.shape
+            if name.endswith("/bias") or name == "cls_token":
+                out[name] = torch.zeros(shp)
+            elif name.endswith("/scale"):
+                out[name] = torch.ones(shp)
+            elif name == "pos_embedding":
+                out[name] = torch.randn(shp, generator=gen) * 0.02
+            elif name == "Conv_0/kernel":
+                out[name] = _lecun_normal(shp, shp[0] * shp[1] * shp[2], gen)
+            elif name.endswith("out/kernel"):
+                out[name] = _lecun_normal(shp, shp[0] * shp[1], gen)
+            else:
+                out[name] = _lecun_normal(shp, shp[0], gen)
+        return out
+
+    def bind(self, store, image_shape, device):
+        return ViTRunner(self, store, image_shape, device)
+
+
+class ViTRunner:
+    """Fixed-shape forward/backward executor for one batch geometry."""
+
+    def __init__(self, model: VisionTransformer, store: ParamStore, image_shape, device):
+        self.m = model
+        self.s = store
+        B, Hh, Ww, C = image_shape
+        ps = model.patch_size
+        self.B, self.C, self.Hh, self.Ww = B, C, Hh, Ww
+        self.gh, self.gw = Hh // ps, Ww // ps
+        self.hw = self.gh * self.gw
+        self.T = self.hw + 1
+        D, M, H = model.hidden_size, model.mlp_dim, model.num_heads
+        self.D, self.M, self.H, self.Dh = D, M, H, D // H
+        self.Kp = ps * ps * C
+        self.Kc = model.num_classes
+        if self.Kp % 8 or D % 8 or M % 8 or self.Dh not in (32, 64, 128):
+            raise ValueError("ViT geometry must have patch*patch*C, hidden, mlp multiples of 8 and head_dim 32/64/128")
+        R = B * self.T
+        self.R = R
+        dev = torch.device(device)
+        f32, bf = torch.float32, torch.bfloat16
+        e = lambda *s, dt=f32: torch.empty(*s, dtype=dt, device=dev)  # noqa: E731
+        Lc = model.num_layers
+        self.patches = e(B * self.hw, self.Kp, dt=bf)
+        self.patch_out = e(B * self.hw, D)
+        self.xs = [e(R, D) for _ in range(Lc + 1)]   # block inputs (fp32 residual stream)
+        self.x1s = [e(R, D) for _ in range(Lc)]      # mid-block residual
+        self.x0b = e(R, D, dt=bf) if not model.use_layernorm else None
+        self.y0 = [e(R, D, dt=bf) for _ in range(Lc)]
+        self.y1 = [e(R, D, dt=bf) for _ in range(Lc)]
+        self.st0 = [(e(R), e(R)) for _ in range(Lc)]
+        self.st1 = [(e(R), e(R)) for _ in range(Lc)]
+        self.qkv = [e(R, 3 * D, dt=bf) for _ in range(Lc)]
+        self.o = [e(R, D, dt=bf) for _ in range(Lc)]
+        self.lse = [e(B * H * self.T) for _ in range(Lc)]
+        self.h = [e(R, M, dt=bf) for _ in range(Lc)]
+        self.a = [e(R, M, dt=bf) for _ in range(Lc)]
+        self.yf = e(B, D, dt=bf)
+        self.stf = (e(B), e(B))
+        self.Kcp = _pad8(self.Kc)
+        self.logits = e(B, self.Kcp)[:, : self.Kc]
+        self.dlogits = e(B, self.Kcp)[:, : self.Kc]
+        self.dlogits_b = torch.zeros(B, self.Kcp, dtype=bf, device=dev)[:, : self.Kc]
+        self.row_loss = e(B)
+        self.row_correct = e(B)
+        self.metrics = torch.zeros(2, dtype=f32, device=dev)  # [loss, accuracy]
+        # backward workspaces
+        self.dx = e(R, D)
+        self.dxb = e(R, D, dt=bf)
+        self.dym = e(R, D, dt=bf)
+        self.dh = e(R, M, dt=bf)
+        self.dy = e(R, D)
+        self.do = e(R, D, dt=bf)
+        self.dqkv = e(R, 3 * D, dt=bf)
+        self.delta = e(B * H * self.T)
+        self.dyf = e(B, D)
+        self.dpatch = e(B * self.hw, D, dt=bf)
+        self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.seed = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._views()
+
+    # ------------------------------------------------------------ views
+    def _views(self):
+        s, m = self.s, self.m
+        D, M, H, Dh = self.D, self.M, self.H, self.Dh
+        P, G, W = s.params, s.grads, s.bf16
+        self.w = []
+        for i in range(m.num_layers):
+            pre = f"EncoderBlock_{i}"
+            a = f"{pre}/SelfAttention_0"
+            d = {
+                "Wqkv": s.group_view(s.shadow, f"{a}/qkv_kernel"),
+                "bqkv": s.group_view(s.flat, f"{a}/qkv_bias"),
+                "gWqkv": s.group_view(s.grad_flat, f"{a}/qkv_kernel"),
+                "gbqkv": s.group_view(s.grad_flat, f"{a}/qkv_bias"),
+                "Wo": W[f"{a}/out/kernel"].reshape(H * Dh, D),
+                "bo": P[f"{a}/out/bias"], "gWo": G[f"{a}/out/kernel"].reshape(H * Dh, D),
+                "gbo": G[f"{a}/out/bias"],
+                "W0": W[f"{pre}/MlpBlock_0/Dense_0/kernel"], "b0": P[f"{pre}/MlpBlock_0/Dense_0/bias"],
+                "gW0": G[f"{pre}/MlpBlock_0/Dense_0/kernel"], "gb0": G[f"{pre}/MlpBlock_0/Dense_0/bias"],
+                "W1": W[f"{pre}/MlpBlock_0/Dense_1/kernel"], "b1": P[f"{pre}/MlpBlock_0/Dense_1/bias"],
+                "gW1": G[f"{pre}/MlpBlock_0/Dense_1/kernel"], "gb1": G[f"{pre}/MlpBlock_0/Dense_1/bias"],
+            }
+            if m.use_layernorm:
+                for j in (0, 1):
+                    d[f"s{j}"] = P[f"{pre}/LayerNorm_{j}/scale"]
+                    d[f"c{j}"] = P[f"{pre}/LayerNorm_{j}/bias"]
+                    d[f"gs{j}"] = G[f"{pre}/LayerNorm_{j}/scale"]
+                    d[f"gc{j}"] = G[f"{pre}/LayerNorm_{j}/bias"]
+            self.w.append(d)
+        self.Wconv = W["Conv_0/kernel"].reshape(self.Kp, D)
+        self.gWconv = G["Conv_0/kernel"].reshape(self.Kp, D)
+        self.bconv, self.gbconv = P["Conv_0/bias"], G["Conv_0/bias"]
+        self.cls, self.gcls = P["cls_token"].reshape(D), G["cls_token"].reshape(D)
+        self.pos, self.gpos = P["pos_embedding"].reshape(self.T, D), G["pos_embedding"].reshape(self.T, D)
+        if m.use_layernorm:
+            self.sf, self.cf = P["LayerNorm_0/scale"], P["LayerNorm_0/bias"]
+            self.gsf, self.gcf = G["LayerNorm_0/scale"], G["LayerNorm_0/bias"]
+        self.Wh, self.bh = W["Dense_0/kernel"], P["Dense_0/bias"]
+        self.gWh, self.gbh = G["Dense_0/kernel"], G["Dense_0/bias"]
+
+    # ---------------------------------------------------------- forward
+    def forward(self, images, labels=None, train=True, need_grad=True):
+        """images: uint8 (B,H,W,C) on the GPU; labels int32 (B,).  Leaves
+        [loss, accuracy] in self.metrics and dlogits (if need_grad)."""
+        m = self.m
+        B, T, D, H, Dh = self.B, self.T, self.D, self.H, self.Dh
+        rate = m.dropout_rate if train else 0.0
+        seed = self.seed
+        if labels is not None:
+            self.labels.copy_(labels, non_blocking=True)
+        K.vit_patchify(images, self.patches, m.patch_size)
+        K.gemm(self.patches, self.Wconv, self.patch_out, bias=self.bconv)
+        K.vit_embed_fwd(self.patch_out, self.cls, self.pos, self.xs[0], None, B, T, D, rate, seed, SITE_EMBED)
+        for i in range(m.num_layers):
+            w = self.w[i]
+            x = self.xs[i]
+            if m.use_layernorm:
+                K.layernorm_fwd(x, w["s0"], w["c0"], self.y0[i], *self.st0[i])
+            else:
+                K.dropout_bwd_cast(x, self.y0[i])
+            K.gemm(self.y0[i], w["Wqkv"], self.qkv[i], bias=w["bqkv"])
+            K.attn_fwd(self.qkv[i], self.o[i], self.lse[i], B, T, H, Dh, causal=False, drop_rate=rate,
+                       seed=seed, site=site_attn(i))
+            K.gemm(self.o[i], w["Wo"], self.x1s[i], bias=w["bo"], res=x)
+            if m.use_layernorm:
+                K.layernorm_fwd(self.x1s[i], w["s1"], w["c1"], self.y1[i], *self.st1[i])
+            else:
+                K.dropout_bwd_cast(self.x1s[i], self.y1[i])
+            K.gemm(self.y1[i], w["W0"], self.a[i], bias=w["b0"], aux=self.h[i], act=K.EPI_GELU,
+                   drop_rate=rate, seed=seed, site=site_mlp_hidden(i))
+            K.gemm(self.a[i], w["W1"], self.xs[i + 1], bias=w["b1"], res=self.x1s[i], drop_rate=rate, seed=seed,
+                   site=site_mlp_out(i))
+        xcls = self.xs[-1].view(B, T * D)[:, :D]   # cls rows (row stride T*D)
+        if m.use_layernorm:
+            K.layernorm_fwd(xcls, self.sf, self.cf, self.yf, *self.stf)
+        else:
+            K.dropout_bwd_cast(xcls, self.yf)
+        K.gemm(self.yf, self.Wh, self.logits, bias=self.bh)
+        K.xent(self.logits, self.labels, self.row_loss, self.row_correct,
+               self.dlogits if need_grad else None, grad_scale=1.0 / B)
+        K.mean2(self.row_loss, self.row_correct, B, 1.0 / B, self.metrics)
+        return self.metrics
+
+    # --------------------------------------------------------- backward
+    def backward(self, train=True):
+        """Accumulates parameter gradients (+=) into the store's grad buffer."""
+        m = self.m
+        B, T, D, H, Dh = self.B, self.T, self.D, self.H, self.Dh
+        rate = m.dropout_rate if train else 0.0
+        seed = self.seed
+        # head
+        K.dropout_bwd_cast(self.dlogits, self.dlogits_b) if self.Kc % 4 == 0 else self.dlogits_b.copy_(self.dlogits)
+        K.gemm(self.yf, self.dlogits_b, self.gWh, ta=True, beta=1.0)
+        K.colsum(self.dlogits, self.gbh)
+        K.gemm(self.dlogits_b, self.Wh, self.dyf, tb=True)
+        self.dx.zero_()
+        self.dxb.zero_()
+        dxc = self.dx.view(B, T * D)[:, :D]
+        dxbc = self.dxb.view(B, T * D)[:, :D]
+        xcls = self.xs[-1].view(B, T * D)[:, :D]
+        if m.use_layernorm:
+            K.layernorm_bwd(self.dyf, xcls, self.sf, *self.stf, None, dxc, dxbc, self.gsf, self.gcf)
+        else:
+            dxc.copy_(self.dyf)
+            dxbc.copy_(self.dyf)
+        for i in reversed(range(m.num_layers)):
+            w = self.w[i]
+            # MLP: x2 = x1 + drop(D1(drop(gelu(D0(ln1(x1))))))
+            K.dropout_bwd_cast(self.dx, self.dym, rate, seed, site_mlp_out(i))
+            K.colsum(self.dym, w["gb1"])
+            K.gemm(self.a[i], self.dym, w["gW1"], ta=True, beta=1.0)
+            K.gemm(self.dym, w["W1"], self.dh, tb=True, aux=self.h[i], act=K.EPI_GELU_BWD, drop_rate=rate,
+                   seed=seed, site=site_mlp_hidden(i))
+            K.colsum(self.dh, w["gb0"])
+            K.gemm(self.y1[i], self.dh, w["gW0"], ta=True, beta=1.0)
+            if m.use_layernorm:
+                K.gemm(self.dh, w["W0"], self.dy, tb=True)
+                K.layernorm_bwd(self.dy, self.x1s[i], w["s1"], *self.st1[i], self.dx, self.dx, self.dxb,
+                                w["gs1"], w["gc1"])
+            else:
+                K.gemm(self.dh, w["W0"], self.dx, tb=True, beta=1.0)
+                K.dropout_bwd_cast(self.dx, self.dxb)
+            # attention: x1 = x + out(attn(qkv(ln0(x))))
+            K.gemm(self.o[i], self.dxb, w["gWo"], ta=True, beta=1.0)
+            K.colsum(self.dx, w["gbo"])
+            K.gemm(self.dxb, w["Wo"], self.do, tb=True)
+            K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, self.dqkv, B, T, H, Dh,
+                       causal=False, drop_rate=rate, seed=seed, site=site_attn(i))
+            K.gemm(self.y0[i], self.dqkv, w["gWqkv"], ta=True, beta=1.0)
+            K.colsum(self.dqkv, w["gbqkv"])
+            if m.use_layernorm:
+                K.gemm(self.dqkv, w["Wqkv"], self.dy, tb=True)
+                K.layernorm_bwd(self.dy, self.xs[i], w["s0"], *self.st0[i], self.dx, self.dx, self.dxb,
+                                w["gs0"], w["gc0"])
+            else:
+                K.gemm(self.dqkv, w["Wqkv"], self.dx, tb=True, beta=1.0)
+                K.dropout_bwd_cast(self.dx, self.dxb)
+        K.vit_embed_bwd(self.dx, self.dpatch, self.gcls, self.gpos, self.gbconv, B, T, D, rate, seed, SITE_EMBED)
+        K.gemm(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
+
+    def flops_per_step(self):
+        """Algorithmic fwd+bwd matmul FLOPs (3x forward; SURVEY §8d counting)."""
+        B, T, D, M, Kc = self.B, self.T, self.D, self.M, self.Kc
+        per_layer = 2 * B * T * D * 3 * D + 2 * B * T * D * D + 2 * 2 * B * T * T * D + 2 * 2 * B * T * D * M
+        fwd = self.m.num_layers * per_layer + 2 * B * self.hw * self.Kp * D + 2 * B * D * Kc
+        return 3 * fwd

@@ -1,0 +1,81 @@
+"""GEMM kernel vs a torch fp32 reference on bf16-rounded operands."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _padded(rows, cols, dev, g):
+    """bf16 [rows, cols] view of a buffer whose leading dimension is padded to 8."""
+    ld = (cols + 7) // 8 * 8
+    return torch.randn(rows, ld, device=dev, generator=g).to(torch.bfloat16)[:, :cols]
+
+
+def _ref(a, b, ta, tb):
+    A = a.float().t() if ta else a.float()
+    B = b.float().t() if tb else b.float()
+    return A @ B
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (257, 200, 48), (1000, 384, 128), (64, 50257 % 1000, 130),
+                                   (16448, 128, 256), (33, 2730, 1024), (512, 512, 4096)])
+def test_gemm_layouts(dev, ta, tb, M, N, K):
+    from plaincv_amd import kernels as k
+    g = torch.Generator(device=dev).manual_seed(M * 7 + N + K)
+    a = _padded(*((K, M) if ta else (M, K)), dev, g)
+    b = _padded(*((N, K) if tb else (K, N)), dev, g)
+    out = torch.empty(M, N, device=dev, dtype=torch.float32)
+    k.gemm(a, b, out, ta=ta, tb=tb)
+    ref = _ref(a, b, ta, tb)
+    err = (out - ref).abs().max().item()
+    assert err <= 1e-3 * (K ** 0.5) * 4, err
+
+
+def test_gemm_padded_ld_and_bf16_out(dev):
+    from plaincv_amd import kernels as k
+    M, N, K = 300, 2730, 768
+    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    wbuf = torch.randn(K, 2736, device=dev).to(torch.bfloat16)
+    w = wbuf[:, :N]
+    obuf = torch.zeros(M, 2736, device=dev, dtype=torch.bfloat16)
+    out = obuf[:, :N]
+    k.gemm(a, w, out)
+    ref = a.float() @ w.float()
+    assert torch.allclose(out.float(), ref, rtol=2e-2, atol=2e-1)
+    assert obuf[:, N:].abs().max().item() == 0.0
+
+
+def test_gemm_epilogues(dev):
+    from plaincv_amd import kernels as k
+    M, N, K = 513, 256, 128
+    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (0.1 * torch.randn(K, N, device=dev)).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev)
+    aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    out = torch.empty(M, N, device=dev, dtype=torch.float32)
+    k.gemm(a, w, out, bias=bias, aux=aux, act=k.EPI_GELU, res=res)
+    h = a.float() @ w.float() + bias
+    ref = torch.nn.functional.gelu(h, approximate="tanh") + res
+    assert torch.allclose(aux.float(), h, rtol=1e-2, atol=1e-2)
+    assert torch.allclose(out, ref, rtol=1e-3, atol=1e-3)
+    # accumulate (beta=1) and split-K
+    c = torch.randn(128, 384, device=dev)
+    c0 = c.clone()
+    x = torch.randn(16448, 128, device=dev).to(torch.bfloat16)
+    dy = torch.randn(16448, 384, device=dev).to(torch.bfloat16)
+    k.gemm(x, dy, c, ta=True, beta=1.0)
+    ref = c0 + x.float().t() @ dy.float()
+    assert torch.allclose(c, ref, rtol=1e-3, atol=5e-2), (c - ref).abs().max()
+
+
+def test_gemm_batched(dev):
+    from plaincv_amd import kernels as k
+    B, M, N, K = 5, 128, 256, 256
+    a = torch.randn(B, M, K, device=dev).to(torch.bfloat16)
+    b = torch.randn(B, N, K, device=dev).to(torch.bfloat16)
+    out = torch.empty(B, M, N, device=dev)
+    k.gemm(a, b, out, tb=True)
+    ref = a.float() @ b.float().transpose(1, 2)
+    assert torch.allclose(out, ref, rtol=1e-3, atol=1e-2)

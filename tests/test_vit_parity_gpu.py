@@ -1,0 +1,91 @@
+"""ViT forward/backward/optimizer on the HIP path vs the CPU oracle (bf16 placement).
+
+Tolerances (bf16 MFMA operands vs an oracle that rounds the same GEMM operands):
+loss abs <= 2e-2, every gradient leaf rel-L2 <= 5e-2, updated params after one
+AdamW/Muon step max|dp| <= 2e-3 (lr 1e-3, Adam direction ~O(1)).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _small_model(rate, use_ln=True, classes=10):
+    from plaincv_amd.models.vit_small import VisionTransformer
+    return VisionTransformer(num_classes=classes, patch_size=4, hidden_size=64, mlp_dim=128, num_layers=2,
+                             num_heads=2, dropout_rate=rate, use_layernorm=use_ln)
+
+
+def _oracle_cfg(m):
+    from oracle.vit import ViTConfig
+    return ViTConfig(num_classes=m.num_classes, patch_size=m.patch_size, hidden_size=m.hidden_size,
+                     mlp_dim=m.mlp_dim, num_layers=m.num_layers, num_heads=m.num_heads,
+                     dropout_rate=m.dropout_rate, use_layernorm=m.use_layernorm)
+
+
+def _rel(a, b, floor=1e-2):
+    """relative L2 error with an absolute floor (some leaves, e.g. the attention
+    key bias, have an exactly-zero true gradient: softmax shift invariance)."""
+    return (a - b).norm().item() / max(b.norm().item(), floor)
+
+
+@pytest.mark.parametrize("rate,use_ln,shape", [(0.0, True, (4, 16, 16, 3)), (0.1, True, (4, 16, 16, 3)),
+                                               (0.0, False, (4, 16, 16, 3)), (0.1, True, (3, 28, 28, 1))])
+def test_vit_grads_match_oracle(dev, rate, use_ln, shape):
+    from oracle.engine import cross_entropy_loss, value_and_grad
+    from oracle.vit import vit_apply
+    from plaincv_amd.engine import create_train_state, make_train_step
+    m = _small_model(rate, use_ln)
+    init = m.init(0, shape)
+    g = torch.Generator().manual_seed(1)
+    images = torch.randint(0, 256, shape, generator=g, dtype=torch.uint8)
+    labels = torch.randint(0, m.num_classes, (shape[0],), generator=g, dtype=torch.int32)
+    st = create_train_state(0, m, 1e-3, shape, m.num_classes, init_params=init)
+    runner = st.runner_for(shape)
+    runner.seed.fill_(77)
+    st.params.zero_grad()
+    met = runner.forward(images.to(dev), labels.to(dev), train=True)
+    runner.backward(train=True)
+    torch.cuda.synchronize()
+    gpu_grads = st.params.grads_dict()
+    oc = _oracle_cfg(m)
+    (loss, _), grads = value_and_grad(
+        lambda p: (cross_entropy_loss(vit_apply(p, images, oc, True, 77, bf16=True), labels), None), init)
+    assert abs(met[0].item() - loss.item()) < 2e-2, (met[0].item(), loss.item())
+    for k in init:
+        r = _rel(gpu_grads[k], grads[k])
+        assert r < 5e-2, (k, r)
+
+
+@pytest.mark.parametrize("optim", ["adamw", "muon"])
+def test_vit_train_step_matches_oracle(dev, optim):
+    from oracle import optim as oopt
+    from oracle.engine import apply_updates, cross_entropy_loss, value_and_grad
+    from oracle.vit import vit_apply
+    from plaincv_amd.engine import create_train_state, make_train_step
+    from utils import Config
+    m = _small_model(0.0)
+    shape = (4, 16, 16, 3)
+    cfg = Config(optim=optim, lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9)
+    init = m.init(3, shape)
+    st = create_train_state(0, m, 1e-3, shape, m.num_classes, cfg=cfg, init_params=init)
+    step = make_train_step()
+    tx = oopt.get_optimizer(cfg)
+    ostate = tx.init(init)
+    params = dict(init)
+    oc = _oracle_cfg(m)
+    gen = torch.Generator().manual_seed(5)
+    for it in range(3):
+        images = torch.randint(0, 256, shape, generator=gen, dtype=torch.uint8)
+        labels = torch.randint(0, 10, (shape[0],), generator=gen, dtype=torch.int32)
+        st, met = step(st, (images.to(dev), labels.to(dev)), it)
+        _, grads = value_and_grad(
+            lambda p: (cross_entropy_loss(vit_apply(p, images, oc, True, it, bf16=True), labels), None), params)
+        upd, ostate = tx.update(grads, ostate, params)
+        params = apply_updates(params, upd)
+    torch.cuda.synchronize()
+    got = st.params.to_dict()
+    for k in params:
+        d = (got[k] - params[k]).abs().max().item()
+        assert d < 3e-3 * 3, (k, d)
