@@ -1,0 +1,267 @@
+"""Benchmark: plainCV training hot path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload vit_c2|lm124m] [--no-cpu-baseline]
+
+Default workload (N=1): BASELINE.json configs[1] -- ViT-small on Tiny-ImageNet-
+shaped synthetic data (uint8 64x64x3, 200 classes, per-GPU batch 64, dropout 0.1,
+LayerNorm), Muon optimizer, bf16 MFMA compute with fp32 master params.  One
+"step" = one full optimizer step (forward + backward + Muon/AdamW update) on
+one batch per GPU, replayed from a hipGraph; inputs are resident in HBM.
+With N>1 each rank runs the same per-GPU batch (weak scaling) and gradients
+are averaged over RCCL once per step.  ``value`` = images/s over all ranks.
+
+Also reported: the roofline of the dominant kernel (timed live with HIP
+events on its own stream, algorithmic FLOPs per launch) and the CPU baseline
+(the oracle/ restatement timed on this host's cores on a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from plaincv_amd.engine import GraphedTrainStep, create_train_state  # noqa: E402
+from plaincv_amd.engine import data_parallel as dp  # noqa: E402
+from plaincv_amd.models.vit_small import VisionTransformer  # noqa: E402
+from utils import Config  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+
+# config/config_vit.yaml + BASELINE.json configs[1] overrides
+VIT_C2 = dict(dataset="tiny_imagenet_synthetic", batch_size=64, image_size=64, num_channels=3, num_classes=200,
+              model="vit_small", vit_patch_size=4, vit_hidden_size=128, vit_mlp_dim=256, vit_layers=4, vit_heads=4,
+              vit_dropout=0.1, vit_use_layernorm=True, optim="muon", lr=0.001, weight_decay=0.01, beta1=0.9,
+              beta2=0.9, muon_beta=0.95, muon_ns_steps=5, muon_ns_coeffs=[3.4445, -4.7750, 2.0315],
+              muon_nesterov=True, eigen_tracking_enabled=False, seed=0)
+
+
+def vit_model(cfg):
+    return VisionTransformer(num_classes=cfg.num_classes, patch_size=cfg.vit_patch_size,
+                             hidden_size=cfg.vit_hidden_size, mlp_dim=cfg.vit_mlp_dim, num_layers=cfg.vit_layers,
+                             num_heads=cfg.vit_heads, dropout_rate=cfg.vit_dropout,
+                             use_layernorm=cfg.vit_use_layernorm)
+
+
+def timed_kernel(fn, iters=50):
+    """Average duration of fn() (one kernel launch) with HIP events on a
+    dedicated stream (torch.cuda.Event only sees the stream it records on)."""
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for _ in range(5):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(iters):
+            fn()
+        e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def vit_roofline(state, image_shape):
+    """Dominant kernel of the ViT step (rocprof: the per-layer MLP/QKV GEMMs and
+    flash attention); we time the largest-FLOP GEMM (MLP Dense_0 forward,
+    [B*T,128]x[128,256] + bias + GELU + dropout epilogue) live."""
+    from plaincv_amd import kernels as K
+    r = state.runner_for(image_shape)
+    w = r.w[0]
+    fn = lambda: K.gemm(r.y1[0], w["W0"], r.a[0], bias=w["b0"], aux=r.h[0], act=K.EPI_GELU,  # noqa: E731
+                        drop_rate=r.m.dropout_rate, seed=r.seed, site=17)
+    dt = timed_kernel(fn)
+    flops = 2.0 * r.R * r.D * r.M
+    achieved = flops / dt / 1e12
+    return {"kernel": "gemm_bf16_kernel (MLP Dense_0 fwd, M=%d N=%d K=%d)" % (r.R, r.M, r.D), "bound": "mfma",
+            "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None, "launch_us": round(dt * 1e6, 2),
+            "flops_per_launch": flops}
+
+
+def cpu_baseline_vit(cfg, seconds=12.0):
+    """oracle/ (PyTorch CPU fp32 restatement) timed on this host: the same
+    workload (B=64 TI-shaped, Muon), bounded to ~`seconds` of CPU work."""
+    from oracle import optim as oopt
+    from oracle.engine import apply_updates, cross_entropy_loss, value_and_grad
+    from oracle.vit import ViTConfig, vit_apply
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    m = vit_model(cfg)
+    shape = (cfg.batch_size, cfg.image_size, cfg.image_size, cfg.num_channels)
+    params = m.init(0, shape)
+    oc = ViTConfig(num_classes=cfg.num_classes, patch_size=cfg.vit_patch_size, hidden_size=cfg.vit_hidden_size,
+                   mlp_dim=cfg.vit_mlp_dim, num_layers=cfg.vit_layers, num_heads=cfg.vit_heads,
+                   dropout_rate=cfg.vit_dropout)
+    tx = oopt.get_optimizer(cfg)
+    st = tx.init(params)
+    g = torch.Generator().manual_seed(0)
+    imgs = torch.randint(0, 256, shape, generator=g, dtype=torch.uint8)
+    labels = torch.randint(0, cfg.num_classes, (cfg.batch_size,), generator=g, dtype=torch.int32)
+
+    def step(i):
+        nonlocal params, st
+        _, grads = value_and_grad(lambda p: (cross_entropy_loss(vit_apply(p, imgs, oc, True, i), labels), None),
+                                  params)
+        upd, st = tx.update(grads, st, params)
+        params = apply_updates(params, upd)
+
+    step(0)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step(n + 1)
+        n += 1
+        if time.perf_counter() - t0 > seconds or n >= 50:
+            break
+    dt = (time.perf_counter() - t0) / n
+    model_name = "unknown"
+    try:
+        model_name = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(" :\t")
+    except Exception:
+        pass
+    return {"value": round(cfg.batch_size / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "steps_per_sec": round(1.0 / dt, 4),
+            "sample": f"{n} timed oracle ViT-small Muon train steps (fp32, B={cfg.batch_size}, 64x64x3, 200 classes) "
+                      f"after 1 warmup; CPU {model_name}"}
+
+
+def bench_vit(args):
+    rank, local_rank, world, dev = dp.init_from_env()
+    cfg = Config(VIT_C2)
+    m = vit_model(cfg)
+    B = cfg.batch_size
+    shape = (B, cfg.image_size, cfg.image_size, cfg.num_channels)
+    state = create_train_state(cfg.seed, m, cfg.lr, shape, cfg.num_classes, cfg=cfg, device=dev)
+    if world > 1:   # identical replicas: broadcast rank 0's params
+        torch.distributed.broadcast(state.params.flat, 0)
+        state.params.sync_shadow()
+    gen = torch.Generator().manual_seed(1234 + rank)
+    nb = 4
+    pool_x = torch.randint(0, 256, (nb,) + shape, generator=gen, dtype=torch.uint8).to(dev)
+    pool_y = torch.randint(0, cfg.num_classes, (nb, B), generator=gen, dtype=torch.int32).to(dev)
+    step = GraphedTrainStep(state, shape, warmup=2)
+    for i in range(args.warmup):
+        step(pool_x[i % nb], pool_y[i % nb])
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(pool_x[i % nb], pool_y[i % nb])
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(t.item())
+    loss = float(step.metrics[0].item())
+    flops = state.runner_for(shape).flops_per_step()
+    out = None
+    if rank == 0:
+        sps = args.steps / dt
+        out = {"metric": METRIC, "value": round(world * B * sps, 2), "unit": "images/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+               "data": "synthetic (uint8 images U[0,255], labels U[0,200), seeded, resident in HBM)",
+               "config": {"workload": "vit_small_tinyimagenet_muon (BASELINE configs[1])", "global_batch": world * B,
+                          "per_gpu_batch": B, "image": [64, 64, 3], "classes": 200, "tokens": 257,
+                          "optimizer": "muon", "parallelism": f"dp{world}"},
+               "steps_per_sec": round(sps, 3), "tflops_per_gpu": round(flops * sps / 1e12, 3),
+               "final_loss": round(loss, 4)}
+        out["roofline"] = vit_roofline(state, shape)
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_vit(cfg, args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+    return out
+
+
+def bench_lm(args):
+    """124M causal LM (BASELINE configs[2] shape, AdamW, seq 1024, micro-batch 16)."""
+    from plaincv_amd.engine.lm import create_lm_state, make_apply_grads_fn, make_train_fns
+    from plaincv_amd.models.LM.constructor import construct_model
+    rank, local_rank, world, dev = dp.init_from_env()
+    cfg = Config(model="transformer", vocab_size=50257, d_model=768, expand="8/3", n_layers=12, n_heads=12,
+                 mlp_class="glu", seq_len=1024, tie_embeddings=False, rope_theta=500000.0, dtype="bfloat16",
+                 optim="adamw", lr=3e-4, weight_decay=0.1, beta1=0.9, beta2=0.95, seed=0)
+    mb, accum = args.lm_micro_batch, args.lm_accum
+    model, mc, variables = construct_model(cfg)
+    st = create_lm_state(cfg, model, variables, mb, dev, accum=accum)
+    compute_grads, _ = make_train_fns()
+    apply_grads = make_apply_grads_fn(None)
+    gen = torch.Generator().manual_seed(99 + rank)
+    pool = torch.randint(0, cfg.vocab_size, (4, mb, cfg.seq_len + 1), generator=gen, dtype=torch.int32).to(dev)
+
+    def one_step(i):
+        for a in range(accum):
+            compute_grads(st, pool[(i * accum + a) % 4])
+        apply_grads(st)
+
+    for i in range(args.warmup):
+        one_step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        one_step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(t.item())
+    tokens = world * mb * accum * cfg.seq_len * args.steps
+    fpt = model.flops_per_token(cfg.seq_len)
+    if rank != 0:
+        return None
+    return {"metric": METRIC, "value": round(tokens / dt, 1), "unit": "tokens/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic token ids U[0,50257), resident in HBM",
+            "config": {"workload": "lm124m_adamw (BASELINE configs[2] shape)", "micro_batch": mb, "accum": accum,
+                       "seq_len": cfg.seq_len, "global_batch_tokens": world * mb * accum * cfg.seq_len,
+                       "parallelism": f"dp{world}"},
+            "steps_per_sec": round(args.steps / dt, 4),
+            "tflops_per_gpu": round(tokens / world / dt * fpt / 1e12, 2),
+            "roofline": None, "cpu_baseline": None}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="vit_c2", choices=["vit_c2", "lm124m"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--lm-micro-batch", type=int, default=16)
+    ap.add_argument("--lm-accum", type=int, default=1)
+    ap.add_argument("--with-lm", action="store_true", help="also run the 124M LM and attach it as 'lm124m'")
+    args = ap.parse_args()
+    if args.workload == "lm124m":
+        out = bench_lm(args)
+    else:
+        out = bench_vit(args)
+        if args.with_lm and out is not None:
+            a2 = argparse.Namespace(**vars(args))
+            a2.steps, a2.warmup = 3, 1
+            out["lm124m"] = bench_lm(a2)
+    if out is not None:
+        print(json.dumps(out), flush=True)
+    if dp.is_initialized():
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,93 @@
+"""Committed golden vectors: the oracle must keep reproducing them (CPU), and the
+HIP path must match them within the bf16 tolerances (GPU)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden.make_golden import LM_CFG, VIT_CFG, lm_params, vit_params
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    return np.load(os.path.join(HERE, name), allow_pickle=False)
+
+
+def test_wikitext_fixture_shape():
+    z = _load("wikitext_ctx128_rows0-7.npz")
+    ids = z["input_ids"]
+    assert ids.shape == (8, 129) and ids.dtype == np.int32
+    assert ids.min() >= 0 and ids.max() < 50257
+    assert z["docs_lengths_len"].sum() == z["docs_lengths_flat"].size
+
+
+def test_oracle_reproduces_vit_golden():
+    from oracle.engine import cross_entropy_loss
+    from oracle.vit import vit_apply
+    z = _load("vit_tiny.npz")
+    cfg, p = vit_params()
+    for k in p:
+        assert np.array_equal(p[k].numpy(), z["param:" + k])
+    logits = vit_apply(p, torch.from_numpy(z["images"]), cfg, True, int(z["seed"]), bf16=True)
+    assert np.allclose(logits.detach().numpy(), z["logits"], atol=1e-5)
+    assert abs(cross_entropy_loss(logits, torch.from_numpy(z["labels"])).item() - float(z["loss"])) < 1e-5
+
+
+def test_oracle_reproduces_lm_golden():
+    from oracle.engine import lm_loss_and_acc
+    from oracle.lm import transformer_apply
+    z = _load("lm_tiny.npz")
+    mc, p = lm_params()
+    ids = torch.from_numpy(z["input_ids"].astype(np.int64))
+    logits = transformer_apply(p, ids[:, :-1], mc, torch.bfloat16)
+    loss, acc = lm_loss_and_acc(logits, ids[:, 1:])
+    assert abs(loss.item() - float(z["loss"])) < 1e-4
+    assert np.allclose(logits[0, :4].float().numpy(), z["logits_row0_pos0-3"], atol=1e-2)
+
+
+@pytest.mark.gpu
+def test_hip_vit_matches_golden(dev):
+    from plaincv_amd.engine import create_train_state
+    from plaincv_amd.models.vit_small import VisionTransformer
+    z = _load("vit_tiny.npz")
+    cfg, p = vit_params()
+    m = VisionTransformer(**VIT_CFG)
+    shape = tuple(z["images"].shape)
+    st = create_train_state(0, m, 1e-3, shape, 10, init_params=p)
+    r = st.runner_for(shape)
+    r.seed.fill_(int(z["seed"]))
+    st.params.zero_grad()
+    met = r.forward(torch.from_numpy(z["images"]).to(dev), torch.from_numpy(z["labels"]).to(dev), train=True)
+    r.backward()
+    torch.cuda.synchronize()
+    assert abs(met[0].item() - float(z["loss"])) < 2e-2
+    assert np.allclose(r.logits.float().cpu().numpy(), z["logits"], atol=5e-2)
+    for k in ("Conv_0/kernel", "EncoderBlock_1/MlpBlock_0/Dense_0/kernel", "Dense_0/kernel", "pos_embedding"):
+        g = st.params.grads[k].cpu().numpy()
+        ref = z["grad:" + k]
+        assert np.linalg.norm(g - ref) <= 5e-2 * max(np.linalg.norm(ref), 1e-2), k
+
+
+@pytest.mark.gpu
+def test_hip_lm_matches_golden(dev):
+    from plaincv_amd.models.LM.transformer import ModelConfig, Transformer
+    from plaincv_amd.params import ParamStore
+    z = _load("lm_tiny.npz")
+    mc, p = lm_params()
+    model = Transformer(ModelConfig(mlp="glu", **LM_CFG))
+    store = ParamStore(model.layout(), dev)
+    store.load(p)
+    ids = torch.from_numpy(z["input_ids"]).to(dev)
+    run = model.bind(store, ids.shape[0], ids.shape[1] - 1, dev)
+    run.set_batch(ids)
+    store.zero_grad()
+    met = run.forward()
+    run.backward()
+    torch.cuda.synchronize()
+    assert abs(met[0].item() - float(z["loss"])) < 2e-2
+    for k in ("layers_0/attn/w_qkv/kernel", "layers_1/mlp/fc2/kernel"):
+        g = store.grads[k].cpu().numpy()
+        ref = z["grad:" + k]
+        assert np.linalg.norm(g - ref) <= 6e-2 * np.linalg.norm(ref), k
