@@ -84,110 +84,184 @@ __device__ __forceinline__ bf16x8 pack8(f32x4 a, f32x4 b) {
 }
 
 // ------------------------------------------------------------------ forward
+// Prefetch of one 64-row K/V tile into registers (issued a tile ahead; written to
+// the other LDS buffer after the current tile's MFMAs -- "issue early, write late").
+template <int DH>
+struct TileRegs {
+  static constexpr int N = 64 * DH / 8 / 256;   // 16-B chunks per thread per matrix
+  u32x4 k[N], v[N];
+};
+template <int DH>
+__device__ __forceinline__ void tile_load(TileRegs<DH>& t, const bf16* Kp, const bf16* Vp, int64_t ld, int row0,
+                                          int T, int64_t bT) {
+  constexpr int CPR = DH / 8;
+#pragma unroll
+  for (int i = 0; i < TileRegs<DH>::N; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    const int r = idx / CPR, c = idx % CPR;
+    const int gr = row0 + r;
+    if (gr < T) {
+      t.k[i] = *reinterpret_cast<const u32x4*>(Kp + (bT + gr) * ld + c * 8);
+      t.v[i] = *reinterpret_cast<const u32x4*>(Vp + (bT + gr) * ld + c * 8);
+    } else {
+      t.k[i] = u32x4{0u, 0u, 0u, 0u};
+      t.v[i] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+}
+template <int DH>
+__device__ __forceinline__ void tile_store(const TileRegs<DH>& t, bf16* Ks, bf16* Vs) {
+  constexpr int CPR = DH / 8;
+  constexpr int LD = Tile<DH>::LD;
+#pragma unroll
+  for (int i = 0; i < TileRegs<DH>::N; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    const int r = idx / CPR, c = idx % CPR;
+    *reinterpret_cast<u32x4*>(Ks + r * LD + c * 8) = t.k[i];
+    *reinterpret_cast<u32x4*>(Vs + r * LD + c * 8) = t.v[i];
+  }
+}
+
+// Workgroup = 4 waves x 32 queries (two 16-query groups per wave share every K/V
+// fragment read from LDS); K/V tiles of 64 keys double-buffered in LDS.
 template <int DH, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnArgs a) {
   const uint32_t seed = DROP ? *a.seedp : 0u;
   constexpr int LD = Tile<DH>::LD;
-  constexpr int KS = DH / 32, DT = DH / 16;
-  __shared__ __attribute__((aligned(16))) bf16 Ks[64 * LD];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[64 * LD];
+  constexpr int KS = DH / 32, DT = DH / 16, QG = 2;
+  __shared__ __attribute__((aligned(16))) bf16 KVs[2][2][64 * LD];
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int T = a.T;
   const int64_t bT = (int64_t)b * T;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4;
-  const int q0 = qb * 64 + wave * 16;
-  const int myq = q0 + (lane & 15);
+  const int qw = qb * 128 + wave * 32;          // first query of this wave
   const bf16* Q = a.q + h * DH;
   const bf16* Kp = a.k + h * DH;
   const bf16* Vp = a.v + h * DH;
 
-  bf16x8 qf[KS];
+  bf16x8 qf[QG][KS];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) qf[ks] = glob_frag(Q, a.ldq, bT + myq, myq < T, ks);
-
+  for (int gq = 0; gq < QG; ++gq) {
+    const int myq = qw + gq * 16 + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[gq][ks] = glob_frag(Q, a.ldq, bT + myq, myq < T, ks);
+  }
   const float c2 = a.scale * LOG2E;
-  float m2 = NEG_BIG, lsum = 0.f;
-  f32x4 acc[DT];
+  float m2[QG], lsum[QG];
+  f32x4 acc[QG][DT];
 #pragma unroll
-  for (int d = 0; d < DT; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int gq = 0; gq < QG; ++gq) {
+    m2[gq] = NEG_BIG;
+    lsum[gq] = 0.f;
+#pragma unroll
+    for (int d = 0; d < DT; ++d) acc[gq][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   int nkb = (T + 63) / 64;
-  if (CAUSAL) nkb = min(nkb, (qb * 64 + 63) / 64 + 1);
+  if (CAUSAL) nkb = min(nkb, (qb * 128 + 127) / 64 + 1);
+  TileRegs<DH> pre;
+  tile_load<DH>(pre, Kp, Vp, a.ldq, 0, T, bT);
+  tile_store<DH>(pre, KVs[0][0], KVs[0][1]);
+  __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
-    __syncthreads();
-    load_rows<DH>(Ks, Kp, a.ldq, kb * 64, T, bT);
-    load_rows<DH>(Vs, Vp, a.ldq, kb * 64, T, bT);
-    __syncthreads();
-    f32x4 s[4];
+    const bf16* Ks = KVs[kb & 1][0];
+    const bf16* Vs = KVs[kb & 1][1];
+    const bool more = kb + 1 < nkb;
+    if (more) tile_load<DH>(pre, Kp, Vp, a.ldq, (kb + 1) * 64, T, bT);
+    const bool active = !CAUSAL || kb * 64 <= qw + 31;   // wave-uniform causal skip
+    if (active) {
+      f32x4 s[QG][4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < 4; ++t) {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Ks, 16 * t, ks), qf[ks], s[t], 0, 0, 0);
-    }
-    float bmax = NEG_BIG;
+        for (int gq = 0; gq < QG; ++gq) s[gq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 kf = row_frag<DH>(Ks, 16 * t, ks);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb * 64 + 16 * t + 4 * g + r;
-        bool ok = key < T;
-        if (CAUSAL) ok = ok && key <= myq;
-        s[t][r] = ok ? s[t][r] * c2 : NEG_BIG;
-        bmax = fmaxf(bmax, s[t][r]);
-      }
-    bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
-    bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
-    const float mnew = fmaxf(m2, bmax);
-    const float alpha = exp2f(m2 - mnew);
-    float rs = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float p = s[t][r] > 0.5f * NEG_BIG ? exp2f(s[t][r] - mnew) : 0.f;
-        rs += p;
-        if (DROP) {
-          const int key = kb * 64 + 16 * t + 4 * g + r;
-          const uint32_t hh = hash3(seed, a.site, (uint32_t)myq * (uint32_t)T + (uint32_t)key);
-          p = hh >= a.drop_thresh ? p * a.drop_scale : 0.f;
+          for (int gq = 0; gq < QG; ++gq)
+            s[gq][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[gq][ks], s[gq][t], 0, 0, 0);
         }
-        s[t][r] = p;
       }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    lsum = lsum * alpha + rs;
-    m2 = mnew;
-    // rescale O rows: acc row = query (lane>>4)*4 + r; alpha lives on lane == query
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float al = __shfl(alpha, 4 * g + r, 64);
+      for (int gq = 0; gq < QG; ++gq) {
+        const int myq = qw + gq * 16 + (lane & 15);
+        float bmax = NEG_BIG;
 #pragma unroll
-      for (int d = 0; d < DT; ++d) acc[d][r] *= al;
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kb * 64 + 16 * t + 4 * g + r;
+            bool ok = key < T;
+            if (CAUSAL) ok = ok && key <= myq;
+            s[gq][t][r] = ok ? s[gq][t][r] * c2 : NEG_BIG;
+            bmax = fmaxf(bmax, s[gq][t][r]);
+          }
+        bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
+        bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+        const float mnew = fmaxf(m2[gq], bmax);
+        const float alpha = exp2f(m2[gq] - mnew);
+        float rs = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float p = s[gq][t][r] > 0.5f * NEG_BIG ? exp2f(s[gq][t][r] - mnew) : 0.f;
+            rs += p;
+            if (DROP) {
+              const int key = kb * 64 + 16 * t + 4 * g + r;
+              const uint32_t hh = hash3(seed, a.site, (uint32_t)myq * (uint32_t)T + (uint32_t)key);
+              p = hh >= a.drop_thresh ? p * a.drop_scale : 0.f;
+            }
+            s[gq][t][r] = p;
+          }
+        rs += __shfl_xor(rs, 16, 64);
+        rs += __shfl_xor(rs, 32, 64);
+        lsum[gq] = lsum[gq] * alpha + rs;
+        m2[gq] = mnew;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float al = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+          for (int d = 0; d < DT; ++d) acc[gq][d][r] *= al;
+        }
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8 pa[QG];
+#pragma unroll
+        for (int gq = 0; gq < QG; ++gq) pa[gq] = pack8(s[gq][2 * st], s[gq][2 * st + 1]);
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+          const bf16x8 vf = tr_frag<DH>(Vs, st, 16 * d);
+#pragma unroll
+          for (int gq = 0; gq < QG; ++gq)
+            acc[gq][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[gq], vf, acc[gq][d], 0, 0, 0);
+        }
+      }
     }
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const bf16x8 pa = pack8(s[2 * st], s[2 * st + 1]);
-#pragma unroll
-      for (int d = 0; d < DT; ++d)
-        acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_frag<DH>(Vs, st, 16 * d), acc[d], 0, 0, 0);
-    }
+    if (more) tile_store<DH>(pre, KVs[(kb + 1) & 1][0], KVs[(kb + 1) & 1][1]);
+    __syncthreads();
   }
   // normalise + store
-  const float inv = 1.f / lsum;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float iv = __shfl(inv, 4 * g + r, 64);
-    const int qq = q0 + 4 * g + r;
-    if (qq < T) {
+  for (int gq = 0; gq < QG; ++gq) {
+    const int q0 = qw + gq * 16;
+    const float inv = 1.f / lsum[gq];
 #pragma unroll
-      for (int d = 0; d < DT; ++d)
-        a.out[(bT + qq) * a.ldout + h * DH + 16 * d + (lane & 15)] = f2bf(acc[d][r] * iv);
+    for (int r = 0; r < 4; ++r) {
+      const float iv = __shfl(inv, 4 * g + r, 64);
+      const int qq = q0 + 4 * g + r;
+      if (qq < T) {
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+          a.out[(bT + qq) * a.ldout + h * DH + 16 * d + (lane & 15)] = f2bf(acc[gq][d][r] * iv);
+      }
     }
+    const int myq = q0 + (lane & 15);
+    if (g == 0 && myq < T) a.lse2[((int64_t)b * a.H + h) * T + myq] = m2[gq] + log2f(lsum[gq]);
   }
-  if (g == 0 && myq < T) a.lse2[((int64_t)b * a.H + h) * T + myq] = m2 + log2f(lsum);
 }
 
 // ------------------------------------------------------------- bwd: delta
@@ -214,22 +288,29 @@ __global__ void attn_bwd_delta_kernel(AttnArgs a) {
 }
 
 // --------------------------------------------------------- bwd: dK, dV
+// Workgroup = 4 waves x 32 keys (two 16-key groups per wave share every Q/dO
+// fragment); loops over 64-query tiles (Q, dO, lse2, delta) prefetched into
+// registers one tile ahead and double-buffered in LDS.
+template <int DH>
+struct QTileRegs {
+  static constexpr int N = 64 * DH / 8 / 256;
+  u32x4 q[N], o[N];
+  float l, d;
+};
+
 template <int DH, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(AttnArgs a) {
   const uint32_t seed = DROP ? *a.seedp : 0u;
   constexpr int LD = Tile<DH>::LD;
-  constexpr int KS = DH / 32, DT = DH / 16;
-  __shared__ __attribute__((aligned(16))) bf16 Qs[64 * LD];
-  __shared__ __attribute__((aligned(16))) bf16 Ds[64 * LD];
-  __shared__ float Ls[64], Dl[64];
+  constexpr int KS = DH / 32, DT = DH / 16, KG = 2, CPR = DH / 8;
+  __shared__ __attribute__((aligned(16))) bf16 QOs[2][2][64 * LD];
+  __shared__ float LDl[2][2][64];
   const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int T = a.T;
   const int64_t bT = (int64_t)b * T;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4;
-  const int k0 = kb * 64 + wave * 16;
-  const int mykey = k0 + (lane & 15);
-  const bool kval = mykey < T;
+  const int kw = kb * 128 + wave * 32;
   const bf16* Qp = a.q + h * DH;
   const bf16* Kp = a.k + h * DH;
   const bf16* Vp = a.v + h * DH;
@@ -237,174 +318,277 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs a) {
   const float* lse = a.lse2 + ((int64_t)b * a.H + h) * T;
   const float* del = a.delta + ((int64_t)b * a.H + h) * T;
 
-  bf16x8 kf[KS], vf[KS];
+  bf16x8 kf[KG][KS], vf[KG][KS];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    kf[ks] = glob_frag(Kp, a.ldq, bT + mykey, kval, ks);
-    vf[ks] = glob_frag(Vp, a.ldq, bT + mykey, kval, ks);
+  for (int gk = 0; gk < KG; ++gk) {
+    const int key = kw + gk * 16 + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[gk][ks] = glob_frag(Kp, a.ldq, bT + key, key < T, ks);
+      vf[gk][ks] = glob_frag(Vp, a.ldq, bT + key, key < T, ks);
+    }
   }
   const float c2 = a.scale * LOG2E;
-  f32x4 dv[DT], dk[DT];
+  f32x4 dv[KG][DT], dk[KG][DT];
 #pragma unroll
-  for (int d = 0; d < DT; ++d) { dv[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+  for (int gk = 0; gk < KG; ++gk)
+#pragma unroll
+    for (int d = 0; d < DT; ++d) { dv[gk][d] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[gk][d] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+  auto qload = [&](QTileRegs<DH>& t, int q0) {
+#pragma unroll
+    for (int i = 0; i < QTileRegs<DH>::N; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      const int r = idx / CPR, c = idx % CPR;
+      const int gr = q0 + r;
+      if (gr < T) {
+        t.q[i] = *reinterpret_cast<const u32x4*>(Qp + (bT + gr) * a.ldq + c * 8);
+        t.o[i] = *reinterpret_cast<const u32x4*>(dOp + (bT + gr) * a.lddo + c * 8);
+      } else {
+        t.q[i] = u32x4{0u, 0u, 0u, 0u};
+        t.o[i] = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+    if (threadIdx.x < 64) {
+      const int qq = q0 + threadIdx.x;
+      t.l = qq < T ? lse[qq] : 0.f;
+      t.d = qq < T ? del[qq] : 0.f;
+    }
+  };
+  auto qstore = [&](const QTileRegs<DH>& t, int buf) {
+#pragma unroll
+    for (int i = 0; i < QTileRegs<DH>::N; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      const int r = idx / CPR, c = idx % CPR;
+      *reinterpret_cast<u32x4*>(QOs[buf][0] + r * LD + c * 8) = t.q[i];
+      *reinterpret_cast<u32x4*>(QOs[buf][1] + r * LD + c * 8) = t.o[i];
+    }
+    if (threadIdx.x < 64) { LDl[buf][0][threadIdx.x] = t.l; LDl[buf][1][threadIdx.x] = t.d; }
+  };
 
   const int nqb = (T + 63) / 64;
-  const int qb0 = CAUSAL ? kb : 0;
+  const int qb0 = CAUSAL ? (kb * 128) / 64 : 0;
+  QTileRegs<DH> pre;
+  if (qb0 < nqb) { qload(pre, qb0 * 64); qstore(pre, 0); }
+  __syncthreads();
   for (int qb = qb0; qb < nqb; ++qb) {
-    __syncthreads();
-    load_rows<DH>(Qs, Qp, a.ldq, qb * 64, T, bT);
-    load_rows<DH>(Ds, dOp, a.lddo, qb * 64, T, bT);
-    if (threadIdx.x < 64) {
-      const int qq = qb * 64 + threadIdx.x;
-      Ls[threadIdx.x] = qq < T ? lse[qq] : 0.f;
-      Dl[threadIdx.x] = qq < T ? del[qq] : 0.f;
-    }
-    __syncthreads();
-    f32x4 p[4], ds[4];
+    const int buf = (qb - qb0) & 1;
+    const bf16* Qs = QOs[buf][0];
+    const bf16* Ds = QOs[buf][1];
+    const float* Ls = LDl[buf][0];
+    const float* Dl = LDl[buf][1];
+    const bool more = qb + 1 < nqb;
+    if (more) qload(pre, (qb + 1) * 64);
+    const bool active = !CAUSAL || qb * 64 + 63 >= kw;
+    if (active) {
+      f32x4 p[KG][4], ds[KG][4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < 4; ++t) {
+        f32x4 sv[KG], dp[KG];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Qs, 16 * t, ks), kf[ks], sv, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Ds, 16 * t, ks), vf[ks], dp, 0, 0, 0);
-      }
+        for (int gk = 0; gk < KG; ++gk) { sv[gk] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[gk] = f32x4{0.f, 0.f, 0.f, 0.f}; }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = 16 * t + 4 * g + r;
-        const int qq = qb * 64 + ql;
-        bool ok = kval && qq < T;
-        if (CAUSAL) ok = ok && mykey <= qq;
-        float pv = ok ? exp2f(sv[r] * c2 - Ls[ql]) : 0.f;
-        float dpv = dp[r];
-        float pd = pv;
-        if (DROP) {
-          const uint32_t hh = hash3(seed, a.site, (uint32_t)qq * (uint32_t)T + (uint32_t)mykey);
-          const float km = hh >= a.drop_thresh ? a.drop_scale : 0.f;
-          pd = pv * km;
-          dpv *= km;
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 qa = row_frag<DH>(Qs, 16 * t, ks);
+          const bf16x8 oa = row_frag<DH>(Ds, 16 * t, ks);
+#pragma unroll
+          for (int gk = 0; gk < KG; ++gk) {
+            sv[gk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[gk][ks], sv[gk], 0, 0, 0);
+            dp[gk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[gk][ks], dp[gk], 0, 0, 0);
+          }
         }
-        p[t][r] = pd;
-        ds[t][r] = pv * (dpv - Dl[ql]);
+#pragma unroll
+        for (int gk = 0; gk < KG; ++gk) {
+          const int mykey = kw + gk * 16 + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ql = 16 * t + 4 * g + r;
+            const int qq = qb * 64 + ql;
+            bool ok = mykey < T && qq < T;
+            if (CAUSAL) ok = ok && mykey <= qq;
+            const float pv = ok ? exp2f(sv[gk][r] * c2 - Ls[ql]) : 0.f;
+            float dpv = dp[gk][r];
+            float pd = pv;
+            if (DROP) {
+              const uint32_t hh = hash3(seed, a.site, (uint32_t)qq * (uint32_t)T + (uint32_t)mykey);
+              const float km = hh >= a.drop_thresh ? a.drop_scale : 0.f;
+              pd = pv * km;
+              dpv *= km;
+            }
+            p[gk][t][r] = pd;
+            ds[gk][t][r] = pv * (dpv - Dl[ql]);
+          }
+        }
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8 pb[KG], sb[KG];
+#pragma unroll
+        for (int gk = 0; gk < KG; ++gk) {
+          pb[gk] = pack8(p[gk][2 * st], p[gk][2 * st + 1]);
+          sb[gk] = pack8(ds[gk][2 * st], ds[gk][2 * st + 1]);
+        }
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+          const bf16x8 oT = tr_frag<DH>(Ds, st, 16 * d);
+          const bf16x8 qT = tr_frag<DH>(Qs, st, 16 * d);
+#pragma unroll
+          for (int gk = 0; gk < KG; ++gk) {
+            dv[gk][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oT, pb[gk], dv[gk][d], 0, 0, 0);
+            dk[gk][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qT, sb[gk], dk[gk][d], 0, 0, 0);
+          }
+        }
       }
     }
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const bf16x8 pb = pack8(p[2 * st], p[2 * st + 1]);
-      const bf16x8 sb = pack8(ds[2 * st], ds[2 * st + 1]);
-#pragma unroll
-      for (int d = 0; d < DT; ++d) {
-        dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag<DH>(Ds, st, 16 * d), pb, dv[d], 0, 0, 0);
-        dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag<DH>(Qs, st, 16 * d), sb, dk[d], 0, 0, 0);
-      }
-    }
+    if (more) qstore(pre, buf ^ 1);
+    __syncthreads();
   }
-  if (kval) {
 #pragma unroll
-    for (int d = 0; d < DT; ++d)
+  for (int gk = 0; gk < KG; ++gk) {
+    const int mykey = kw + gk * 16 + (lane & 15);
+    if (mykey < T) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int dd = 16 * d + 4 * g + r;
-        a.dv[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(dv[d][r]);
-        a.dk[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(dk[d][r] * a.scale);
-      }
+      for (int d = 0; d < DT; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int dd = 16 * d + 4 * g + r;
+          a.dv[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(dv[gk][d][r]);
+          a.dk[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(dk[gk][d][r] * a.scale);
+        }
+    }
   }
 }
 
 // --------------------------------------------------------------- bwd: dQ
+// Workgroup = 4 waves x 32 queries; loops over prefetched, double-buffered K/V tiles.
 template <int DH, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(AttnArgs a) {
   const uint32_t seed = DROP ? *a.seedp : 0u;
   constexpr int LD = Tile<DH>::LD;
-  constexpr int KS = DH / 32, DT = DH / 16;
-  __shared__ __attribute__((aligned(16))) bf16 Ks[64 * LD];
-  __shared__ __attribute__((aligned(16))) bf16 Vs[64 * LD];
+  constexpr int KS = DH / 32, DT = DH / 16, QG = 2;
+  __shared__ __attribute__((aligned(16))) bf16 KVs[2][2][64 * LD];
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int T = a.T;
   const int64_t bT = (int64_t)b * T;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4;
-  const int q0 = qb * 64 + wave * 16;
-  const int myq = q0 + (lane & 15);
-  const bool qval = myq < T;
+  const int qw = qb * 128 + wave * 32;
   const bf16* Qp = a.q + h * DH;
   const bf16* Kp = a.k + h * DH;
   const bf16* Vp = a.v + h * DH;
   const bf16* dOp = a.dout + h * DH;
   const int64_t bh = (int64_t)b * a.H + h;
-  const float myl = qval ? a.lse2[bh * T + myq] : 0.f;
-  const float myd = qval ? a.delta[bh * T + myq] : 0.f;
 
-  bf16x8 qf[KS], of[KS];
+  bf16x8 qf[QG][KS], of[QG][KS];
+  float myl[QG], myd[QG];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    qf[ks] = glob_frag(Qp, a.ldq, bT + myq, qval, ks);
-    of[ks] = glob_frag(dOp, a.lddo, bT + myq, qval, ks);
+  for (int gq = 0; gq < QG; ++gq) {
+    const int myq = qw + gq * 16 + (lane & 15);
+    const bool qv = myq < T;
+    myl[gq] = qv ? a.lse2[bh * T + myq] : 0.f;
+    myd[gq] = qv ? a.delta[bh * T + myq] : 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      qf[gq][ks] = glob_frag(Qp, a.ldq, bT + myq, qv, ks);
+      of[gq][ks] = glob_frag(dOp, a.lddo, bT + myq, qv, ks);
+    }
   }
   const float c2 = a.scale * LOG2E;
-  f32x4 acc[DT];
+  f32x4 acc[QG][DT];
 #pragma unroll
-  for (int d = 0; d < DT; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int gq = 0; gq < QG; ++gq)
+#pragma unroll
+    for (int d = 0; d < DT; ++d) acc[gq][d] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   int nkb = (T + 63) / 64;
-  if (CAUSAL) nkb = min(nkb, (qb * 64 + 63) / 64 + 1);
+  if (CAUSAL) nkb = min(nkb, (qb * 128 + 127) / 64 + 1);
+  TileRegs<DH> pre;
+  tile_load<DH>(pre, Kp, Vp, a.ldq, 0, T, bT);
+  tile_store<DH>(pre, KVs[0][0], KVs[0][1]);
+  __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
-    __syncthreads();
-    load_rows<DH>(Ks, Kp, a.ldq, kb * 64, T, bT);
-    load_rows<DH>(Vs, Vp, a.ldq, kb * 64, T, bT);
-    __syncthreads();
-    f32x4 ds[4];
+    const bf16* Ks = KVs[kb & 1][0];
+    const bf16* Vs = KVs[kb & 1][1];
+    const bool more = kb + 1 < nkb;
+    if (more) tile_load<DH>(pre, Kp, Vp, a.ldq, (kb + 1) * 64, T, bT);
+    const bool active = !CAUSAL || kb * 64 <= qw + 31;
+    if (active) {
+      f32x4 ds[QG][4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < 4; ++t) {
+        f32x4 sv[QG], dp[QG];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Ks, 16 * t, ks), qf[ks], sv, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Vs, 16 * t, ks), of[ks], dp, 0, 0, 0);
-      }
+        for (int gq = 0; gq < QG; ++gq) { sv[gq] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[gq] = f32x4{0.f, 0.f, 0.f, 0.f}; }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kb * 64 + 16 * t + 4 * g + r;
-        bool ok = qval && key < T;
-        if (CAUSAL) ok = ok && key <= myq;
-        const float pv = ok ? exp2f(sv[r] * c2 - myl) : 0.f;
-        float dpv = dp[r];
-        if (DROP) {
-          const uint32_t hh = hash3(seed, a.site, (uint32_t)myq * (uint32_t)T + (uint32_t)key);
-          dpv *= hh >= a.drop_thresh ? a.drop_scale : 0.f;
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 ka = row_frag<DH>(Ks, 16 * t, ks);
+          const bf16x8 va = row_frag<DH>(Vs, 16 * t, ks);
+#pragma unroll
+          for (int gq = 0; gq < QG; ++gq) {
+            sv[gq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[gq][ks], sv[gq], 0, 0, 0);
+            dp[gq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, of[gq][ks], dp[gq], 0, 0, 0);
+          }
         }
-        ds[t][r] = pv * (dpv - myd);
+#pragma unroll
+        for (int gq = 0; gq < QG; ++gq) {
+          const int myq = qw + gq * 16 + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kb * 64 + 16 * t + 4 * g + r;
+            bool ok = myq < T && key < T;
+            if (CAUSAL) ok = ok && key <= myq;
+            const float pv = ok ? exp2f(sv[gq][r] * c2 - myl[gq]) : 0.f;
+            float dpv = dp[gq][r];
+            if (DROP) {
+              const uint32_t hh = hash3(seed, a.site, (uint32_t)myq * (uint32_t)T + (uint32_t)key);
+              dpv *= hh >= a.drop_thresh ? a.drop_scale : 0.f;
+            }
+            ds[gq][t][r] = pv * (dpv - myd[gq]);
+          }
+        }
+      }
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8 sa[QG];
+#pragma unroll
+        for (int gq = 0; gq < QG; ++gq) sa[gq] = pack8(ds[gq][2 * st], ds[gq][2 * st + 1]);
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+          const bf16x8 kt = tr_frag<DH>(Ks, st, 16 * d);
+#pragma unroll
+          for (int gq = 0; gq < QG; ++gq)
+            acc[gq][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa[gq], kt, acc[gq][d], 0, 0, 0);
+        }
       }
     }
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const bf16x8 sa = pack8(ds[2 * st], ds[2 * st + 1]);
-#pragma unroll
-      for (int d = 0; d < DT; ++d)
-        acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, tr_frag<DH>(Ks, st, 16 * d), acc[d], 0, 0, 0);
-    }
+    if (more) tile_store<DH>(pre, KVs[(kb + 1) & 1][0], KVs[(kb + 1) & 1][1]);
+    __syncthreads();
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int qq = q0 + 4 * g + r;
-    if (qq < T) {
+  for (int gq = 0; gq < QG; ++gq) {
+    const int q0 = qw + gq * 16;
 #pragma unroll
-      for (int d = 0; d < DT; ++d)
-        a.dq[(bT + qq) * a.lddq + h * DH + 16 * d + (lane & 15)] = f2bf(acc[d][r] * a.scale);
+    for (int r = 0; r < 4; ++r) {
+      const int qq = q0 + 4 * g + r;
+      if (qq < T) {
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+          a.dq[(bT + qq) * a.lddq + h * DH + 16 * d + (lane & 15)] = f2bf(acc[gq][d][r] * a.scale);
+      }
     }
   }
 }
 
 template <int DH, bool C, bool D>
 static void launch_fwd(const AttnArgs& a, hipStream_t s) {
-  dim3 grid((a.T + 63) / 64, a.H, a.B);
+  dim3 grid((a.T + 127) / 128, a.H, a.B);
   hipLaunchKernelGGL((attn_fwd_kernel<DH, C, D>), grid, dim3(256), 0, s, a);
 }
 template <int DH, bool C, bool D>
 static void launch_bwd(const AttnArgs& a, hipStream_t s) {
   const int64_t n = (int64_t)a.B * a.T * a.H;
   hipLaunchKernelGGL((attn_bwd_delta_kernel<DH>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
-  dim3 grid((a.T + 63) / 64, a.H, a.B);
+  dim3 grid((a.T + 127) / 128, a.H, a.B);
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH, C, D>), grid, dim3(256), 0, s, a);
   hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, C, D>), grid, dim3(256), 0, s, a);
 }

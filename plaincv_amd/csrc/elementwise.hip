@@ -108,8 +108,10 @@ __global__ void colsum_kernel(const T* x, int64_t ld, int64_t R, int N, float* o
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  if (c < N)
+  if (c < N) {
+#pragma unroll 4
     for (int64_t r = (int64_t)blockIdx.y * 4 + rl; r < R; r += (int64_t)gridDim.y * 4) s += (float)x[r * ld + c];
+  }
   red[rl][cl] = s;
   __syncthreads();
   if (rl == 0 && c < N) atomicAdd(out + c, red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
@@ -154,20 +156,22 @@ __global__ void vit_embed_bwd_kernel(const float* dx, bf16* dpatch, float* dcls,
                                      uint32_t site) {
   const uint32_t seed = thresh ? *seedp : 0u;
   const int64_t n = (int64_t)T * D;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int d = (int)(i % D), t = (int)(i / D);
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) {
-      const int64_t idx = ((int64_t)b * T + t) * D + d;
-      float g = dx[idx];
-      if (thresh) g = hash3(seed, site, (uint32_t)idx) >= thresh ? g * scale : 0.f;
-      s += g;
-      if (t > 0) dpatch[((int64_t)b * (T - 1) + t - 1) * D + d] = f2bf(g);
-    }
-    dpos[i] += s;
-    if (t == 0) dcls[d] += s;
-    else atomicAdd(dbias + d, s);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int d = (int)(i % D), t = (int)(i / D);
+  const int b0 = blockIdx.y * 8, b1 = min(B, b0 + 8);
+  float s = 0.f;
+#pragma unroll 4
+  for (int b = b0; b < b1; ++b) {
+    const int64_t idx = ((int64_t)b * T + t) * D + d;
+    float g = dx[idx];
+    if (thresh) g = hash3(seed, site, (uint32_t)idx) >= thresh ? g * scale : 0.f;
+    s += g;
+    if (t > 0) dpatch[((int64_t)b * (T - 1) + t - 1) * D + d] = f2bf(g);
   }
+  atomicAdd(dpos + i, s);
+  if (t == 0) atomicAdd(dcls + d, s);
+  else if (dbias) atomicAdd(dbias + d, s);  // high contention: callers prefer colsum(dpatch)
 }
 
 // --------------------------------------------------------------- embedding
@@ -262,8 +266,8 @@ extern "C" int pcv_cast_f32_bf16(const float* x, void* y, int64_t n, void* strea
 
 extern "C" int pcv_colsum(const void* x, int64_t ld, int64_t R, int N, int x_f32, float* out, void* stream) {
   if (R <= 0 || N <= 0) return PCV_EINVAL;
-  int gy = (int)((R + 255) / 256);
-  if (gy > 64) gy = 64;
+  int gy = (int)((R + 31) / 32);
+  if (gy > 128) gy = 128;
   dim3 grid((N + 63) / 64, gy);
   if (x_f32)
     hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)x, ld, R, N, out);
@@ -300,7 +304,8 @@ extern "C" int pcv_vit_embed_bwd(const float* dx, void* dpatch, float* dcls, flo
   uint32_t th; float sc;
   drop_params(rate, &th, &sc);
   const int64_t n = (int64_t)T * D;
-  hipLaunchKernelGGL(vit_embed_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dx, (bf16*)dpatch,
+  dim3 grid((unsigned)((n + 255) / 256), (unsigned)((B + 7) / 8));
+  hipLaunchKernelGGL(vit_embed_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, dx, (bf16*)dpatch,
                      dcls, dpos, dbias, B, T, D, th, sc, seed, site);
   return pcv_launch_status();
 }

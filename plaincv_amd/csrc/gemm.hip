@@ -35,6 +35,8 @@ struct GemmArgs {
   uint32_t drop_thresh; float drop_scale; const uint32_t* seedp; uint32_t site;  // dropout on activation (thresh 0 = off)
   int split_k; int64_t k_per_split;
   int tiles_m, tiles_n;
+  int vec_ok;                    // C/aux/res/bias bases and row strides allow 16-B access
+  int glds_ok;                   // A/B bases and row strides allow 16-B LDS-DMA pieces
 };
 
 template <int R>
@@ -132,6 +134,54 @@ __device__ __forceinline__ bf16x8 mc_frag(const char* lds, int cbase, int ks) {
   return bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
 }
 
+// ---- direct global->LDS (global_load_lds_dwordx4) staging of FULL 64-deep k-tiles.
+// The LDS destination of one wave-instruction is 1 KiB, lane-linear (base + 16*lane),
+// so the swizzled images above are produced by permuting each lane's SOURCE chunk
+// (the XOR maps are involutions).  Rows/columns past the matrix edge are clamped to
+// a valid address: they only feed output rows/cols that are never stored.
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void glds16(const bf16* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int R>
+__device__ __forceinline__ void kc_glds(char* lds, const bf16* base, int64_t ld, int64_t rows, int64_t row0,
+                                        int64_t k0) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int PER_WAVE = R * 128 / 1024 / 4;  // 1-KiB pieces per wave
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int piece = wave * PER_WAVE + i;
+    const int r = piece * 8 + (lane >> 3);
+    const int kc = (lane & 7) ^ ((r >> 1) & 7);
+    int64_t gr = row0 + r;
+    gr = gr < rows ? gr : rows - 1;
+    glds16(base + gr * ld + k0 + kc * 8, lds + piece * 1024);
+  }
+}
+
+template <int R>
+__device__ __forceinline__ void mc_glds(char* lds, const bf16* base, int64_t ld, int64_t cols, int64_t c0,
+                                        int64_t k0) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int RB = R * 2;                    // bytes per k-row
+  constexpr int KR_PER_PIECE = 1024 / RB;      // k-rows per 1-KiB piece
+  constexpr int SLOTS = RB / 16;               // 16-B slots per k-row
+  constexpr int PER_WAVE = 64 * RB / 1024 / 4;
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int piece = wave * PER_WAVE + i;
+    const int kr = piece * KR_PER_PIECE + lane / SLOTS;
+    const int sl = lane % SLOTS;
+    const int cb = mc_blk<R>(sl >> 1, kr);     // involution: physical block -> logical block
+    int64_t gc = c0 + (cb * 2 + (sl & 1)) * 8;
+    const int64_t last = ((cols - 1) >> 3) << 3;
+    gc = gc <= last ? gc : last;
+    glds16(base + (k0 + kr) * ld + gc, lds + piece * 1024);
+  }
+}
+
 template <bool A_KC, bool B_KC, int WM, int WN>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   constexpr int BM = 32 * WM, BN = 32 * WN;
@@ -187,16 +237,31 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     if (B_KC) kc_store<BN>(stB, lb); else mc_store<BN>(stB, lb);
   };
 
+  // full k-tiles: async glds straight into LDS; the ragged last tile (and
+  // tiles when a leading dimension breaks 16-B alignment) via registers + zero fill
+  auto issue = [&](int64_t k0, int buf) -> bool {
+    if (g.glds_ok && k0 + 64 <= kend) {
+      char* la = smem + buf * STAGE;
+      char* lb = la + A_BYTES;
+      if (A_KC) kc_glds<BM>(la, A, g.lda, g.M, m0, k0); else mc_glds<BM>(la, A, g.lda, g.M, m0, k0);
+      if (B_KC) kc_glds<BN>(lb, B, g.ldb, g.N, n0, k0); else mc_glds<BN>(lb, B, g.ldb, g.N, n0, k0);
+      return false;
+    }
+    gload(k0);
+    return true;
+  };
+
   if (nk > 0) {
-    gload(kbeg);
-    lstore(0);
+    if (issue(kbeg, 0)) lstore(0);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     const char* la = smem + buf * STAGE;
     const char* lb = la + A_BYTES;
-    if (kt + 1 < nk) gload(kbeg + (int64_t)(kt + 1) * 64);
+    bool pend = false;
+    if (kt + 1 < nk) pend = issue(kbeg + (int64_t)(kt + 1) * 64, buf ^ 1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[WM], bfr[WN];
@@ -216,44 +281,148 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
         for (int j = 0; j < WN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) lstore(buf ^ 1);
+    if (pend) lstore(buf ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
   // ---------------- epilogue ----------------
+  // Stage the fp32 tile through LDS ([BM][BN+4], conflict-free ds_write_b32), then
+  // every thread owns 8 consecutive columns of a row: 16-B loads of bias/aux/res
+  // and 16-B stores of the output (the MFMA C layout would otherwise store 2-4 B
+  // per lane, which made the small-K ViT GEMMs epilogue-bound).
+  constexpr int CLD = BN + 4;
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ct[(wr * (BM / 2) + i * 16 + (lane >> 4) * 4 + r) * CLD + wc * (BN / 2) + j * 16 + (lane & 15)] =
+            acc[i][j][r];
+  __syncthreads();
   char* Cb = (char*)g.C + bz * g.sC * (g.out_f32 ? 4 : 2);
+  if (g.split_k > 1) {
+    // split-K partial: fp32 atomics shaped as 64 consecutive floats (256 B) per
+    // wave-instruction -- the full-rate atomic shape (MI355X_MICROARCH "Global float atomics")
+    float* C = (float*)Cb;
+    for (int idx = threadIdx.x; idx < BM * BN; idx += 256) {
+      const int rr = idx / BN, c = idx % BN;
+      const int64_t row = m0 + rr, col = n0 + c;
+      if (row < g.M && col < g.N) atomicAdd(C + row * g.ldc + col, g.alpha * ct[rr * CLD + c]);
+    }
+    return;
+  }
+  constexpr int CPR = BN / 8;            // 8-column chunks per row
+  constexpr int RPP = 256 / CPR;         // rows per pass
+  const int cc = threadIdx.x % CPR;
+  const int64_t col = n0 + cc * 8;
+  if (col < g.N) {
+    const bool vec = g.vec_ok && col + 8 <= g.N;
+    float bv[8];
 #pragma unroll
-  for (int i = 0; i < WM; ++i) {
+    for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+    if (g.bias) {
+      if (vec) {
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(g.bias + col);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(g.bias + col + 4);
 #pragma unroll
-    for (int j = 0; j < WN; ++j) {
-      const int64_t col = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
-      if (col >= g.N) continue;
-      const float bcol = g.bias ? g.bias[col] : 0.f;
+        for (int e = 0; e < 4; ++e) { bv[e] = b0[e]; bv[e + 4] = b1[e]; }
+      } else {
+        for (int e = 0; e < 8; ++e) bv[e] = (col + e < g.N) ? g.bias[col + e] : 0.f;
+      }
+    }
+    const uint32_t seed = g.drop_thresh ? *g.seedp : 0u;
+    for (int rr = threadIdx.x / CPR; rr < BM; rr += RPP) {
+      const int64_t row = m0 + rr;
+      if (row >= g.M) break;
+      float v[8];
+      const f32x4 c0 = *reinterpret_cast<const f32x4*>(ct + rr * CLD + cc * 8);
+      const f32x4 c1 = *reinterpret_cast<const f32x4*>(ct + rr * CLD + cc * 8 + 4);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wr * (BM / 2) + i * 16 + (lane >> 4) * 4 + r;
-        if (row >= g.M) continue;
-        float v = g.alpha * acc[i][j][r] + bcol;
+      for (int e = 0; e < 4; ++e) { v[e] = g.alpha * c0[e] + bv[e]; v[e + 4] = g.alpha * c1[e] + bv[e + 4]; }
+      if (g.act != EPI_NONE) {
+        bf16* ap = g.aux + row * g.ldaux + col;
         if (g.act == EPI_GELU) {
-          g.aux[row * g.ldaux + col] = f2bf(v);
-          v = gelu_tanh(v);
-        } else if (g.act == EPI_GELU_BWD) {
-          v *= gelu_tanh_grad(bf2f(g.aux[row * g.ldaux + col]));
-        }
-        if (g.drop_thresh) {
-          const uint32_t h = hash3(*g.seedp, g.site, (uint32_t)(row * g.N + col));
-          v = (h >= g.drop_thresh) ? v * g.drop_scale : 0.f;
-        }
-        if (g.res) {
-          v += g.res_scale * (g.res_f32 ? ((const float*)g.res)[bz * g.sR + row * g.ldr + col]
-                                        : bf2f(((const bf16*)g.res)[bz * g.sR + row * g.ldr + col]));
-        }
-        if (g.out_f32) {
-          float* cp = (float*)Cb + row * g.ldc + col;
-          if (g.split_k > 1) atomicAdd(cp, v);
-          else *cp = (g.beta != 0.f) ? v + g.beta * *cp : v;
+          if (vec) {
+            bf16x8 hv;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) hv[e] = f2bf(v[e]);
+            *reinterpret_cast<bf16x8*>(ap) = hv;
+          } else {
+            for (int e = 0; e < 8; ++e) if (col + e < g.N) ap[e] = f2bf(v[e]);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
         } else {
-          ((bf16*)Cb)[row * g.ldc + col] = f2bf(v);
+          float hv[8];
+          if (vec) {
+            const bf16x8 h8 = *reinterpret_cast<const bf16x8*>(ap);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) hv[e] = bf2f(h8[e]);
+          } else {
+            for (int e = 0; e < 8; ++e) hv[e] = (col + e < g.N) ? bf2f(ap[e]) : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad(hv[e]);
+        }
+      }
+      if (g.drop_thresh) {
+        const uint32_t base = (uint32_t)(row * g.N + col);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          v[e] = (hash3(seed, g.site, base + e) >= g.drop_thresh) ? v[e] * g.drop_scale : 0.f;
+      }
+      if (g.res) {
+        if (g.res_f32) {
+          const float* rp = (const float*)g.res + bz * g.sR + row * g.ldr + col;
+          if (vec) {
+            const f32x4 r0 = *reinterpret_cast<const f32x4*>(rp);
+            const f32x4 r1 = *reinterpret_cast<const f32x4*>(rp + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { v[e] += g.res_scale * r0[e]; v[e + 4] += g.res_scale * r1[e]; }
+          } else {
+            for (int e = 0; e < 8; ++e) if (col + e < g.N) v[e] += g.res_scale * rp[e];
+          }
+        } else {
+          const bf16* rp = (const bf16*)g.res + bz * g.sR + row * g.ldr + col;
+          if (vec) {
+            const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(rp);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += g.res_scale * bf2f(r8[e]);
+          } else {
+            for (int e = 0; e < 8; ++e) if (col + e < g.N) v[e] += g.res_scale * bf2f(rp[e]);
+          }
+        }
+      }
+      if (g.out_f32) {
+        float* cp = (float*)Cb + row * g.ldc + col;
+        if (g.split_k > 1) {
+          for (int e = 0; e < 8; ++e) if (col + e < g.N) atomicAdd(cp + e, v[e]);
+        } else if (vec) {
+          f32x4 o0{v[0], v[1], v[2], v[3]}, o1{v[4], v[5], v[6], v[7]};
+          if (g.beta != 0.f) {
+            const f32x4 p0 = *reinterpret_cast<const f32x4*>(cp);
+            const f32x4 p1 = *reinterpret_cast<const f32x4*>(cp + 4);
+            o0 += g.beta * p0;
+            o1 += g.beta * p1;
+          }
+          *reinterpret_cast<f32x4*>(cp) = o0;
+          *reinterpret_cast<f32x4*>(cp + 4) = o1;
+        } else {
+          for (int e = 0; e < 8; ++e)
+            if (col + e < g.N) cp[e] = (g.beta != 0.f) ? v[e] + g.beta * cp[e] : v[e];
+        }
+      } else {
+        bf16* cp = (bf16*)Cb + row * g.ldc + col;
+        if (vec) {
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+          *reinterpret_cast<bf16x8*>(cp) = o;
+        } else {
+          for (int e = 0; e < 8; ++e) if (col + e < g.N) cp[e] = f2bf(v[e]);
         }
       }
     }
@@ -266,8 +435,15 @@ static hipError_t launch_t(const GemmArgs& a, int batch, hipStream_t s) {
   GemmArgs g = a;
   g.tiles_m = (int)((g.M + BM - 1) / BM);
   g.tiles_n = (int)((g.N + BN - 1) / BN);
-  const size_t lds = 2 * (size_t)(BM + BN) * 64 * 2;
+  const size_t stage = 2 * (size_t)(BM + BN) * 64 * 2, ctile = (size_t)BM * (BN + 4) * 4;
+  const size_t lds = stage > ctile ? stage : ctile;
   dim3 grid(g.tiles_m * g.tiles_n, batch, g.split_k > 1 ? g.split_k : 1);
+  static bool attr = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<AK, BK, WM, WN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)lds);
+    attr = true;
+  }
   hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, WM, WN>), grid, dim3(256), lds, s, g);
   return hipGetLastError();
 }
@@ -315,6 +491,16 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
     g.drop_thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
     if (g.drop_thresh == 0) g.drop_thresh = 1;
     g.drop_scale = 1.f / (1.f - drop_rate);
+  }
+  {
+    const int es = out_f32 ? 4 : 2;
+    bool ok = pcv_aligned16(C) && ((ldc * es) % 16 == 0) && ((stride_c * es) % 16 == 0);
+    if (bias) ok = ok && pcv_aligned16(bias);
+    if (res) ok = ok && pcv_aligned16(res) && ((ldr * (res_f32 ? 4 : 2)) % 16 == 0) &&
+                   ((stride_r * (res_f32 ? 4 : 2)) % 16 == 0);
+    if (aux) ok = ok && pcv_aligned16(aux) && ((ldaux * 2) % 16 == 0);
+    g.vec_ok = ok ? 1 : 0;
+    g.glds_ok = 1;  // lda/ldb % 8 == 0 and 16-B aligned bases are required above
   }
   g.split_k = 1;
   if (split_k > 1) {

@@ -13,47 +13,81 @@ namespace pcv {
 template <typename T>
 __device__ __forceinline__ float ldv(const T* p) { return (float)*p; }
 
+// Block reduce of (max, argmax-first), 512 threads.
+__device__ __forceinline__ void reduce_max_arg(float& m, int& a, float* sm, int* si) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64);
+    const int a2 = __shfl_xor(a, o, 64);
+    if (m2 > m || (m2 == m && a2 < a)) { m = m2; a = a2; }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sm[w] = m; si[w] = a; }
+  __syncthreads();
+  m = sm[0]; a = si[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); ++i)
+    if (sm[i] > m || (sm[i] == m && si[i] < a)) { m = sm[i]; a = si[i]; }
+}
+
+// Row cached in LDS (dynamic shared memory, V*sizeof(T) bytes): HBM is read once
+// and the gradient written once.  512 threads per row.
 template <typename T>
-__global__ __launch_bounds__(256) void xent_kernel(const T* logits, int64_t ld, const int* labels, int64_t R, int V,
+__global__ __launch_bounds__(512) void xent_kernel(const T* logits, int64_t ld, const int* labels, int64_t R, int V,
                                                    float* row_loss, float* row_correct, T* dlogits, int64_t ldd,
-                                                   float grad_scale) {
-  __shared__ float sm[256], ss[256];
-  __shared__ int si[256];
+                                                   float grad_scale, int vec) {
+  extern __shared__ __attribute__((aligned(16))) char smem_x[];
+  T* zs = reinterpret_cast<T*>(smem_x);
+  __shared__ float sm[8];
+  __shared__ int si[8];
+  __shared__ float red[8];
   const int64_t row = blockIdx.x;
   const T* z = logits + row * ld;
-  float m = -3.0e38f, s = 0.f;
+  constexpr int VE = 16 / sizeof(T);
+  float m = -3.0e38f;
   int am = 0x7fffffff;
-  for (int j = threadIdx.x; j < V; j += 256) {
-    const float v = ldv(z + j);
-    if (v > m) { s = s * __expf(m - v) + 1.f; m = v; am = j; }
-    else { s += __expf(v - m); if (v == m && j < am) am = j; }
-  }
-  sm[threadIdx.x] = m; ss[threadIdx.x] = s; si[threadIdx.x] = am;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) {
-      const float m1 = sm[threadIdx.x], m2 = sm[threadIdx.x + o];
-      const float s1 = ss[threadIdx.x], s2 = ss[threadIdx.x + o];
-      const int i1 = si[threadIdx.x], i2 = si[threadIdx.x + o];
-      const float mm = fmaxf(m1, m2);
-      ss[threadIdx.x] = (s1 > 0.f ? s1 * __expf(m1 - mm) : 0.f) + (s2 > 0.f ? s2 * __expf(m2 - mm) : 0.f);
-      sm[threadIdx.x] = mm;
-      si[threadIdx.x] = (m1 > m2) ? i1 : (m2 > m1 ? i2 : min(i1, i2));
+  const int Vv = vec ? V / VE * VE : 0;
+  for (int j = threadIdx.x * VE; j < Vv; j += 512 * VE) {
+    const u32x4 w = *reinterpret_cast<const u32x4*>(z + j);
+    *reinterpret_cast<u32x4*>(zs + j) = w;
+    const T* e = reinterpret_cast<const T*>(&w);
+#pragma unroll
+    for (int q = 0; q < VE; ++q) {
+      const float v = (float)e[q];
+      if (v > m) { m = v; am = j + q; }
     }
-    __syncthreads();
   }
-  const float mx = sm[0];
-  const float lse = mx + __logf(ss[0]);
-  int y = labels[row];
+  for (int j = Vv + threadIdx.x; j < V; j += 512) {
+    const T t = z[j];
+    zs[j] = t;
+    const float v = (float)t;
+    if (v > m) { m = v; am = j; }
+  }
+  __syncthreads();
+  reduce_max_arg(m, am, sm, si);
+  float s = 0.f;
+  for (int j = threadIdx.x; j < V; j += 512) s += __expf((float)zs[j] - m);
+  s = block_sum(s, red);
+  const float lse = m + __logf(s);
+  const int y = labels[row];
   const bool yok = y >= 0 && y < V;
   if (threadIdx.x == 0) {
-    row_loss[row] = yok ? lse - ldv(z + y) : 0.f;
-    row_correct[row] = (yok && si[0] == y) ? 1.f : 0.f;
+    row_loss[row] = yok ? lse - (float)zs[y] : 0.f;
+    row_correct[row] = (yok && am == y) ? 1.f : 0.f;
   }
   if (dlogits) {
     T* d = dlogits + row * ldd;
-    for (int j = threadIdx.x; j < V; j += 256) {
-      float p = __expf(ldv(z + j) - lse);
+    for (int j = threadIdx.x * VE; j < Vv; j += 512 * VE) {
+      union { u32x4 w; T e[VE]; } o;
+#pragma unroll
+      for (int q = 0; q < VE; ++q) {
+        float p = __expf((float)zs[j + q] - lse);
+        if (j + q == y) p -= 1.f;
+        o.e[q] = (T)(p * grad_scale);
+      }
+      *reinterpret_cast<u32x4*>(d + j) = o.w;
+    }
+    for (int j = Vv + threadIdx.x; j < V; j += 512) {
+      float p = __expf((float)zs[j] - lse);
       if (j == y) p -= 1.f;
       d[j] = (T)(p * grad_scale);
     }
@@ -80,12 +114,23 @@ extern "C" int pcv_xent_fwd_bwd(const void* logits, int64_t ld, int logits_f32, 
                                 void* stream) {
   if (R <= 0 || V <= 0) return PCV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
+  const size_t es = logits_f32 ? 4 : 2;
+  const size_t lds = ((size_t)V * es + 15) / 16 * 16;
+  if (lds > 150 * 1024) return PCV_EINVAL;  // row must fit in LDS (V <= ~76k bf16 / 38k fp32)
+  const int vec = pcv_aligned16(logits) && ((ld * es) % 16 == 0) &&
+                  (!dlogits || (pcv_aligned16(dlogits) && (ldd * es) % 16 == 0));
+  static bool attr = false;  // > 64 KiB of dynamic LDS must be opted into once
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)xent_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    (void)hipFuncSetAttribute((const void*)xent_kernel<bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    attr = true;
+  }
   if (logits_f32)
-    hipLaunchKernelGGL(xent_kernel<float>, dim3((unsigned)R), dim3(256), 0, s, (const float*)logits, ld, labels, R, V,
-                       row_loss, row_correct, (float*)dlogits, ldd, grad_scale);
+    hipLaunchKernelGGL(xent_kernel<float>, dim3((unsigned)R), dim3(512), lds, s, (const float*)logits, ld, labels, R,
+                       V, row_loss, row_correct, (float*)dlogits, ldd, grad_scale, vec);
   else
-    hipLaunchKernelGGL(xent_kernel<bf16>, dim3((unsigned)R), dim3(256), 0, s, (const bf16*)logits, ld, labels, R, V,
-                       row_loss, row_correct, (bf16*)dlogits, ldd, grad_scale);
+    hipLaunchKernelGGL(xent_kernel<bf16>, dim3((unsigned)R), dim3(512), lds, s, (const bf16*)logits, ld, labels, R, V,
+                       row_loss, row_correct, (bf16*)dlogits, ldd, grad_scale, vec);
   return pcv_launch_status();
 }
 

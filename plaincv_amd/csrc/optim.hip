@@ -30,6 +30,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, fl
   const float bc1 = 1.f - powf(h.b1, t), bc2 = 1.f - powf(h.b2, t);
   const float bc1n = 1.f - powf(h.b1, t + 1.f);
   const float gs = gscale ? *gscale : 1.f;
+#pragma unroll 4
   for (int64_t i = ck.start + threadIdx.x; i < ck.start + ck.len; i += 256) {
     const float gi = g[i] * gs;
     const float mi = h.b1 * m[i] + (1.f - h.b1) * gi;
@@ -54,6 +55,7 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const float* x, const Chunk
   __shared__ float red[4];
   const Chunk ck = chunks[blockIdx.x];
   float s = 0.f;
+#pragma unroll 4
   for (int64_t i = ck.start + threadIdx.x; i < ck.start + ck.len; i += 256) s += x[i] * x[i];
   s = block_sum(s, red);
   if (threadIdx.x == 0) partial[blockIdx.x] = s;

@@ -37,6 +37,7 @@ class LMTrainState:
     chunks: torch.Tensor = None
     partial: torch.Tensor = None
     loss_sum: torch.Tensor = None
+    track_norm: bool = False          # compute ||g|| every step even without clipping
 
 
 def create_lm_state(cfg, model, variables, micro_batch, device, accum=1):
@@ -79,8 +80,9 @@ def make_apply_grads_fn(grad_clip=None):
     def apply_grads(state: LMTrainState):
         store = state.params
         dp.all_reduce_grads(store)
-        K.grad_scale(store.grad_flat, state.chunks, state.partial, 1.0, grad_clip if grad_clip else 0.0,
-                     state.gscale, state.gnorm)
+        if grad_clip or state.track_norm:
+            K.grad_scale(store.grad_flat, state.chunks, state.partial, 1.0, grad_clip if grad_clip else 0.0,
+                         state.gscale, state.gnorm)
         state.tx.step_(store, state.opt_state, gscale=state.gscale if grad_clip else None)
         store.zero_grad()
         state.step += 1

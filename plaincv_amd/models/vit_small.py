@@ -330,7 +330,8 @@ class ViTRunner:
             else:
                 K.gemm(self.dqkv, w["Wqkv"], self.dx, tb=True, beta=1.0)
                 K.dropout_bwd_cast(self.dx, self.dxb)
-        K.vit_embed_bwd(self.dx, self.dpatch, self.gcls, self.gpos, self.gbconv, B, T, D, rate, seed, SITE_EMBED)
+        K.vit_embed_bwd(self.dx, self.dpatch, self.gcls, self.gpos, None, B, T, D, rate, seed, SITE_EMBED)
+        K.colsum(self.dpatch, self.gbconv)
         K.gemm(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
 
     def flops_per_step(self):

@@ -156,7 +156,7 @@ class ParamStore:
     def zero_grad(self):
         self.grad_flat.zero_()
 
-    def chunks(self, names=None, chunk=65536):
+    def chunks(self, names=None, chunk=4096):
         """Chunk table {start, len} covering the storage of `names` (all leaves by default)."""
         spans = []
         if names is None:

@@ -24,7 +24,7 @@ def _oracle_cfg(m):
                      dropout_rate=m.dropout_rate, use_layernorm=m.use_layernorm)
 
 
-def _rel(a, b, floor=1e-2):
+def _rel(a, b, floor=2e-2):
     """relative L2 error with an absolute floor (some leaves, e.g. the attention
     key bias, have an exactly-zero true gradient: softmax shift invariance)."""
     return (a - b).norm().item() / max(b.norm().item(), floor)
@@ -54,6 +54,12 @@ def test_vit_grads_match_oracle(dev, rate, use_ln, shape):
         lambda p: (cross_entropy_loss(vit_apply(p, images, oc, True, 77, bf16=True), labels), None), init)
     assert abs(met[0].item() - loss.item()) < 2e-2, (met[0].item(), loss.item())
     for k in init:
+        if k.endswith("key/bias"):
+            # true gradient is exactly 0 (softmax shift invariance); the kernel's
+            # value is bf16 noise -> bound it against the query-bias gradient
+            q = gpu_grads[k.replace("key/bias", "query/bias")].norm().item()
+            assert gpu_grads[k].norm().item() < 0.1 * q + 1e-6, k
+            continue
         r = _rel(gpu_grads[k], grads[k])
         assert r < 5e-2, (k, r)
 
