@@ -47,13 +47,21 @@ int pcv_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, i
  * (models/LM/transformer.py:233-240). */
 int pcv_attn_fwd(const void* q, const void* k, const void* v, int64_t ldq, void* out, int64_t ldo,
                  float* lse2, int B, int T, int H, int head_dim, int causal,
-                 float dropout_rate, const uint32_t* seed, uint32_t site, void* stream);
+                 float dropout_rate, const uint16_t* drop_mask, void* stream);
 int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t ldq,
                  const void* o, int64_t ldo, const void* dout, int64_t lddo,
                  const float* lse2, float* delta_ws /* [B,H,T] */,
                  void* dq, void* dk, void* dv, int64_t lddq,
                  int B, int T, int H, int head_dim, int causal,
-                 float dropout_rate, const uint32_t* seed, uint32_t site, void* stream);
+                 float dropout_rate, const uint16_t* drop_mask, void* stream);
+/* Attention-weight dropout mask: flax draws ONE [T,T] keep mask per layer and
+ * broadcasts it over batch and heads (models/vit_small.py:41-45, nn.Dropout with
+ * broadcast_dims (0,1) inside dot_product_attention).  Drawn once per step for
+ * `layers` consecutive layers (site = site + l*site_stride) into packed bits,
+ * pcv_attn_mask_words(T) uint16 words per layer; read by pcv_attn_fwd/bwd. */
+int64_t pcv_attn_mask_words(int T);
+int pcv_attn_drop_mask(const uint32_t* seed, uint32_t site, uint32_t site_stride, int layers, int T,
+                       float dropout_rate, uint16_t* mask, void* stream);
 
 /* --------------------------------------------------------------- norms ----
  * flax LayerNorm (models/vit_small.py:38,52,124) on the fp32 residual stream,
@@ -70,6 +78,12 @@ int pcv_rmsnorm_fwd(const void* x, int64_t ldx, const float* scale, void* y, int
 int pcv_rmsnorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* scale,
                     const float* rstd, const void* dres, int64_t ldres, void* dx, int64_t lddx,
                     float* dscale, int64_t R, int D, void* stream);
+/* Parameter gradients alone (the *_bwd entries skip them when dscale is NULL), so a
+ * caller can run them on a side stream beside the data-gradient chain. */
+int pcv_layernorm_param_grad(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* mean,
+                             const float* rstd, float* dscale, float* dbias, int64_t R, int D, void* stream);
+int pcv_rmsnorm_param_grad(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* rstd,
+                           float* dscale, int64_t R, int D, void* stream);
 
 /* --------------------------------------------------------- elementwise ----
  * RoPE, in place on the q|k column blocks (models/LM/embedding.py:28-66; backward = rotation by -theta). */

@@ -33,8 +33,25 @@ struct AttnArgs {
   float* lse2; float* delta;              // [B,H,T]
   int B, T, H;
   float scale;                            // 1/sqrt(DH)
-  uint32_t drop_thresh; float drop_scale; const uint32_t* seedp; uint32_t site;
+  int drop; float drop_scale;             // dropout on the weights (broadcast over batch and heads)
+  const uint16_t* mask;                   // packed keep bits, see drop_word()
+  int n64;                                // key-tile count of the mask (2*ceil(T/128))
 };
+
+// Dropout keep-mask layout.  flax SelfAttention broadcasts one [T,T] mask over batch
+// and heads (models/vit_small.py:41-45, broadcast_dropout=True), so the bits are drawn
+// once per step by attn_mask_kernel and read by all three kernels.  A 16-bit word
+// holds a 4x4 (query x key) block, bit (q&3)*4 + (k&3); the words are ordered
+//   [q/16][k/64][(q&15)>>2][(k&15)>>2][(k&63)>>4]
+// so a lane of the fwd/dq kernels (one query, keys 16t+4g+r) reads its 4 words of a
+// 64-key tile as one 8-byte load, and a dkdv lane (one key) reads 4 single words.
+__host__ __device__ __forceinline__ int64_t drop_word(int q, int k, int n64) {
+  return (((int64_t)(q >> 4) * n64 + (k >> 6)) * 4 + ((q & 15) >> 2)) * 16 + ((k & 15) >> 2) * 4 + ((k & 63) >> 4);
+}
+__host__ __device__ __forceinline__ int drop_n64(int T) { return 2 * ((T + 127) / 128); }
+__host__ __device__ __forceinline__ int64_t drop_words(int T) {
+  return (int64_t)(8 * ((T + 127) / 128)) * drop_n64(T) * 64;
+}
 
 template <int DH>
 struct Tile {
@@ -126,7 +143,6 @@ __device__ __forceinline__ void tile_store(const TileRegs<DH>& t, bf16* Ks, bf16
 // fragment read from LDS); K/V tiles of 64 keys double-buffered in LDS.
 template <int DH, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnArgs a) {
-  const uint32_t seed = DROP ? *a.seedp : 0u;
   constexpr int LD = Tile<DH>::LD;
   constexpr int KS = DH / 32, DT = DH / 16, QG = 2;
   __shared__ __attribute__((aligned(16))) bf16 KVs[2][2][64 * LD];
@@ -169,7 +185,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
     const bf16* Vs = KVs[kb & 1][1];
     const bool more = kb + 1 < nkb;
     if (more) tile_load<DH>(pre, Kp, Vp, a.ldq, (kb + 1) * 64, T, bT);
-    const bool active = !CAUSAL || kb * 64 <= qw + 31;   // wave-uniform causal skip
+    const bool active = qw < T && (!CAUSAL || kb * 64 <= qw + 31);   // wave-uniform skip
     if (active) {
       f32x4 s[QG][4];
 #pragma unroll
@@ -187,33 +203,46 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
 #pragma unroll
       for (int gq = 0; gq < QG; ++gq) {
         const int myq = qw + gq * 16 + (lane & 15);
+        // Interior tile (every key valid for every query of the group) needs no mask.
+        // Masked scores become NEG_BIG in the raw domain; the scale is folded into
+        // the exp2 argument (max commutes with the positive scale).  The first key
+        // tile always holds a valid key for every row, so m2 is finite from then on.
+        const bool interior = kb * 64 + 63 < T && (!CAUSAL || kb * 64 + 63 <= qw + gq * 16);
+        if (!interior) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int key = kb * 64 + 16 * t + 4 * g + r;
+              bool ok = key < T;
+              if (CAUSAL) ok = ok && key <= myq;
+              s[gq][t][r] = ok ? s[gq][t][r] : NEG_BIG;
+            }
+        }
         float bmax = NEG_BIG;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = kb * 64 + 16 * t + 4 * g + r;
-            bool ok = key < T;
-            if (CAUSAL) ok = ok && key <= myq;
-            s[gq][t][r] = ok ? s[gq][t][r] * c2 : NEG_BIG;
-            bmax = fmaxf(bmax, s[gq][t][r]);
-          }
+          for (int r = 0; r < 4; ++r) bmax = fmaxf(bmax, s[gq][t][r]);
         bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
         bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
-        const float mnew = fmaxf(m2[gq], bmax);
-        const float alpha = exp2f(m2[gq] - mnew);
+        const float mnew = fmaxf(m2[gq], bmax * c2);
+        const float alpha = __builtin_amdgcn_exp2f(m2[gq] - mnew);
+        uint32_t wt[4] = {0u, 0u, 0u, 0u};
+        if (DROP) {
+          const uint64_t mw = *reinterpret_cast<const uint64_t*>(a.mask + drop_word(myq, kb * 64 + 4 * g, a.n64));
+#pragma unroll
+          for (int t = 0; t < 4; ++t) wt[t] = (uint32_t)(mw >> (16 * t)) >> (4 * (myq & 3));
+        }
         float rs = 0.f;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float p = s[gq][t][r] > 0.5f * NEG_BIG ? exp2f(s[gq][t][r] - mnew) : 0.f;
+            float p = __builtin_amdgcn_exp2f(fmaf(s[gq][t][r], c2, -mnew));
             rs += p;
-            if (DROP) {
-              const int key = kb * 64 + 16 * t + 4 * g + r;
-              const uint32_t hh = hash3(seed, a.site, (uint32_t)myq * (uint32_t)T + (uint32_t)key);
-              p = hh >= a.drop_thresh ? p * a.drop_scale : 0.f;
-            }
+            // dropped weights -> 0 (bit select); the 1/keep scale is applied at the end
+            if (DROP) p = __uint_as_float(__float_as_uint(p) & (uint32_t)__builtin_amdgcn_sbfe((int)wt[t], r, 1));
             s[gq][t][r] = p;
           }
         rs += __shfl_xor(rs, 16, 64);
@@ -248,7 +277,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
 #pragma unroll
   for (int gq = 0; gq < QG; ++gq) {
     const int q0 = qw + gq * 16;
-    const float inv = 1.f / lsum[gq];
+    const float inv = (DROP ? a.drop_scale : 1.f) / lsum[gq];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float iv = __shfl(inv, 4 * g + r, 64);
@@ -300,7 +329,6 @@ struct QTileRegs {
 
 template <int DH, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(AttnArgs a) {
-  const uint32_t seed = DROP ? *a.seedp : 0u;
   constexpr int LD = Tile<DH>::LD;
   constexpr int KS = DH / 32, DT = DH / 16, KG = 2, CPR = DH / 8;
   __shared__ __attribute__((aligned(16))) bf16 QOs[2][2][64 * LD];
@@ -379,7 +407,9 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
     const float* Dl = LDl[buf][1];
     const bool more = qb + 1 < nqb;
     if (more) qload(pre, (qb + 1) * 64);
-    const bool active = !CAUSAL || qb * 64 + 63 >= kw;
+    const bool active = kw < T && (!CAUSAL || qb * 64 + 63 >= kw);
+    // every (query, key) pair of this wave's 64x32 block valid: skip per-element masks
+    const bool interior = qb * 64 + 63 < T && kw + 31 < T && (!CAUSAL || kw + 31 <= qb * 64);
     if (active) {
       f32x4 p[KG][4], ds[KG][4];
 #pragma unroll
@@ -400,20 +430,24 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
 #pragma unroll
         for (int gk = 0; gk < KG; ++gk) {
           const int mykey = kw + gk * 16 + (lane & 15);
+          uint32_t wt = 0;
+          if (DROP) wt = (uint32_t)a.mask[drop_word(qb * 64 + 16 * t + 4 * g, mykey, a.n64)] >> (mykey & 3);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int ql = 16 * t + 4 * g + r;
-            const int qq = qb * 64 + ql;
-            bool ok = mykey < T && qq < T;
-            if (CAUSAL) ok = ok && mykey <= qq;
-            const float pv = ok ? exp2f(sv[gk][r] * c2 - Ls[ql]) : 0.f;
+            float pv = __builtin_amdgcn_exp2f(fmaf(sv[gk][r], c2, -Ls[ql]));
+            if (!interior) {
+              const int qq = qb * 64 + ql;
+              bool ok = mykey < T && qq < T;
+              if (CAUSAL) ok = ok && mykey <= qq;
+              pv = ok ? pv : 0.f;
+            }
             float dpv = dp[gk][r];
             float pd = pv;
-            if (DROP) {
-              const uint32_t hh = hash3(seed, a.site, (uint32_t)qq * (uint32_t)T + (uint32_t)mykey);
-              const float km = hh >= a.drop_thresh ? a.drop_scale : 0.f;
-              pd = pv * km;
-              dpv *= km;
+            if (DROP) {   // keep bit as an all-ones/zero mask; dV's 1/keep scale is applied at the store
+              const uint32_t km = (uint32_t)__builtin_amdgcn_sbfe((int)wt, 4 * r, 1);
+              pd = __uint_as_float(__float_as_uint(pv) & km);
+              dpv = __uint_as_float(__float_as_uint(dpv) & km) * a.drop_scale;
             }
             p[gk][t][r] = pd;
             ds[gk][t][r] = pv * (dpv - Dl[ql]);
@@ -452,7 +486,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int dd = 16 * d + 4 * g + r;
-          a.dv[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(dv[gk][d][r]);
+          a.dv[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(DROP ? dv[gk][d][r] * a.drop_scale : dv[gk][d][r]);
           a.dk[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(dk[gk][d][r] * a.scale);
         }
     }
@@ -463,7 +497,6 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
 // Workgroup = 4 waves x 32 queries; loops over prefetched, double-buffered K/V tiles.
 template <int DH, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(AttnArgs a) {
-  const uint32_t seed = DROP ? *a.seedp : 0u;
   constexpr int LD = Tile<DH>::LD;
   constexpr int KS = DH / 32, DT = DH / 16, QG = 2;
   __shared__ __attribute__((aligned(16))) bf16 KVs[2][2][64 * LD];
@@ -511,7 +544,8 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
     const bf16* Vs = KVs[kb & 1][1];
     const bool more = kb + 1 < nkb;
     if (more) tile_load<DH>(pre, Kp, Vp, a.ldq, (kb + 1) * 64, T, bT);
-    const bool active = !CAUSAL || kb * 64 <= qw + 31;
+    const bool active = qw < T && (!CAUSAL || kb * 64 <= qw + 31);
+    const bool interior = kb * 64 + 63 < T && qw + 31 < T && (!CAUSAL || kb * 64 + 63 <= qw);
     if (active) {
       f32x4 ds[QG][4];
 #pragma unroll
@@ -532,17 +566,21 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
 #pragma unroll
         for (int gq = 0; gq < QG; ++gq) {
           const int myq = qw + gq * 16 + (lane & 15);
+          uint32_t wt = 0;
+          if (DROP) wt = (uint32_t)a.mask[drop_word(myq, kb * 64 + 16 * t + 4 * g, a.n64)] >> (4 * (myq & 3));
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int key = kb * 64 + 16 * t + 4 * g + r;
-            bool ok = myq < T && key < T;
-            if (CAUSAL) ok = ok && key <= myq;
-            const float pv = ok ? exp2f(sv[gq][r] * c2 - myl[gq]) : 0.f;
-            float dpv = dp[gq][r];
-            if (DROP) {
-              const uint32_t hh = hash3(seed, a.site, (uint32_t)myq * (uint32_t)T + (uint32_t)key);
-              dpv *= hh >= a.drop_thresh ? a.drop_scale : 0.f;
+            float pv = __builtin_amdgcn_exp2f(fmaf(sv[gq][r], c2, -myl[gq]));
+            if (!interior) {
+              const int key = kb * 64 + 16 * t + 4 * g + r;
+              bool ok = myq < T && key < T;
+              if (CAUSAL) ok = ok && key <= myq;
+              pv = ok ? pv : 0.f;
             }
+            float dpv = dp[gq][r];
+            if (DROP)
+              dpv = __uint_as_float(__float_as_uint(dpv) & (uint32_t)__builtin_amdgcn_sbfe((int)wt, r, 1)) *
+                    a.drop_scale;
             ds[gq][t][r] = pv * (dpv - myd[gq]);
           }
         }
@@ -604,13 +642,34 @@ static int dispatch(const AttnArgs& a, int dh, int causal, int drop, hipStream_t
   return PCV_EINVAL;
 }
 
-static void set_drop(AttnArgs& a, float rate, const uint32_t* seed, uint32_t site) {
-  a.seedp = seed; a.site = site; a.drop_thresh = 0; a.drop_scale = 1.f;
-  if (rate > 0.f) {
-    double t = (double)rate * 4294967296.0;
-    a.drop_thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
-    a.drop_scale = 1.f / (1.f - rate);
-  }
+static void set_drop(AttnArgs& a, float rate, const uint16_t* mask) {
+  a.mask = mask; a.n64 = drop_n64(a.T); a.drop = 0; a.drop_scale = 1.f;
+  if (rate > 0.f) { a.drop = 1; a.drop_scale = 1.f / (1.f - rate); }
+}
+
+// One thread per mask word: 16 hash3 draws (the oracle's keep_mask over the flat
+// q*T+k index, oracle/rng.py), padding queries/keys get 0.  blockIdx.y = layer.
+__global__ __launch_bounds__(256) void attn_mask_kernel(const uint32_t* seedp, uint32_t site0, uint32_t site_stride,
+                                                        int T, uint32_t thresh, int64_t words, uint16_t* mask) {
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= words) return;
+  const uint32_t seed = *seedp;
+  const uint32_t site = site0 + site_stride * blockIdx.y;
+  const int n64 = drop_n64(T);
+  const int sub = (int)(w & 63);
+  const int64_t blk = w >> 6;
+  const int q0 = (int)(blk / n64) * 16 + (sub >> 4) * 4;
+  const int k0 = (int)(blk % n64) * 64 + (sub & 3) * 16 + ((sub >> 2) & 3) * 4;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int qr = 0; qr < 4; ++qr)
+#pragma unroll
+    for (int kr = 0; kr < 4; ++kr) {
+      const int q = q0 + qr, k = k0 + kr;
+      if (q < T && k < T && hash3(seed, site, (uint32_t)q * (uint32_t)T + (uint32_t)k) >= thresh)
+        bits |= 1u << (qr * 4 + kr);
+    }
+  mask[(int64_t)blockIdx.y * words + w] = (uint16_t)bits;
 }
 
 }  // namespace pcv
@@ -620,16 +679,16 @@ using namespace pcv;
 extern "C" int pcv_attn_fwd(const void* q, const void* k, const void* v, int64_t ldq,
                             void* out, int64_t ldo, float* lse2,
                             int B, int T, int H, int head_dim, int causal,
-                            float dropout_rate, const uint32_t* seed, uint32_t site, void* stream) {
+                            float dropout_rate, const uint16_t* drop_mask, void* stream) {
   if (B <= 0 || T <= 0 || H <= 0) return PCV_EINVAL;
-  if (dropout_rate > 0.f && !seed) return PCV_EINVAL;
+  if (dropout_rate > 0.f && (!drop_mask || ((uintptr_t)drop_mask & 7))) return PCV_EINVAL;
   if ((ldq & 7) || (ldo & 7) || !pcv_aligned16(q) || !pcv_aligned16(k) || !pcv_aligned16(v)) return PCV_EALIGN;
   AttnArgs a{};
   a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.ldq = ldq;
   a.out = (bf16*)out; a.ldout = ldo; a.lse2 = lse2;
   a.B = B; a.T = T; a.H = H; a.scale = 1.f / sqrtf((float)head_dim);
-  set_drop(a, dropout_rate, seed, site);
-  return dispatch<true>(a, head_dim, causal ? 1 : 0, a.drop_thresh ? 1 : 0, (hipStream_t)stream);
+  set_drop(a, dropout_rate, drop_mask);
+  return dispatch<true>(a, head_dim, causal ? 1 : 0, a.drop, (hipStream_t)stream);
 }
 
 extern "C" int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t ldq,
@@ -637,9 +696,9 @@ extern "C" int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t
                             const float* lse2, float* delta_ws,
                             void* dq, void* dk, void* dv, int64_t lddq,
                             int B, int T, int H, int head_dim, int causal,
-                            float dropout_rate, const uint32_t* seed, uint32_t site, void* stream) {
+                            float dropout_rate, const uint16_t* drop_mask, void* stream) {
   if (B <= 0 || T <= 0 || H <= 0) return PCV_EINVAL;
-  if (dropout_rate > 0.f && !seed) return PCV_EINVAL;
+  if (dropout_rate > 0.f && (!drop_mask || ((uintptr_t)drop_mask & 7))) return PCV_EINVAL;
   if ((ldq & 7) || (ldo & 7) || (lddo & 7) || !pcv_aligned16(q) || !pcv_aligned16(k) || !pcv_aligned16(v) ||
       !pcv_aligned16(o) || !pcv_aligned16(dout))
     return PCV_EALIGN;
@@ -649,6 +708,20 @@ extern "C" int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t
   a.dq = (bf16*)dq; a.dk = (bf16*)dk; a.dv = (bf16*)dv; a.lddq = lddq;
   a.lse2 = (float*)lse2; a.delta = delta_ws;
   a.B = B; a.T = T; a.H = H; a.scale = 1.f / sqrtf((float)head_dim);
-  set_drop(a, dropout_rate, seed, site);
-  return dispatch<false>(a, head_dim, causal ? 1 : 0, a.drop_thresh ? 1 : 0, (hipStream_t)stream);
+  set_drop(a, dropout_rate, drop_mask);
+  return dispatch<false>(a, head_dim, causal ? 1 : 0, a.drop, (hipStream_t)stream);
+}
+
+extern "C" int64_t pcv_attn_mask_words(int T) { return T > 0 ? drop_words(T) : 0; }
+
+extern "C" int pcv_attn_drop_mask(const uint32_t* seed, uint32_t site, uint32_t site_stride, int layers, int T,
+                                  float dropout_rate, uint16_t* mask, void* stream) {
+  if (T <= 0 || layers <= 0 || !seed || !mask || !(dropout_rate > 0.f && dropout_rate < 1.f)) return PCV_EINVAL;
+  const double t = (double)dropout_rate * 4294967296.0;
+  const uint32_t thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  const int64_t words = drop_words(T);
+  dim3 grid((unsigned)((words + 255) / 256), (unsigned)layers);
+  hipLaunchKernelGGL(attn_mask_kernel, grid, dim3(256), 0, (hipStream_t)stream, seed, site, site_stride, T, thresh,
+                     words, mask);
+  return pcv_launch_status();
 }

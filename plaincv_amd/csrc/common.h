@@ -60,17 +60,20 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return s;
 }
 
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float c = 0.7978845608028654f;  // sqrt(2/pi)
-  float u = c * (x + 0.044715f * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+// tanh-approximate GELU (flax.linen.gelu, approximate=True) in sigmoid form:
+// 0.5*(1 + tanh(u)) = sigmoid(2u), u = sqrt(2/pi)*(x + 0.044715 x^3) -> one v_exp + one v_rcp.
+constexpr float GELU_K = 1.5957691216057308f;        // 2*sqrt(2/pi)
+constexpr float GELU_KL = GELU_K * 1.4426950408889634f;
+constexpr float GELU_A = 0.044715f;
+__device__ __forceinline__ float gelu_sig(float x, float x2) {
+  const float zl = x * fmaf(GELU_KL * GELU_A, x2, GELU_KL);
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-zl));
 }
+__device__ __forceinline__ float gelu_tanh(float x) { return x * gelu_sig(x, x * x); }
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
-  const float c = 0.7978845608028654f;
-  float x2 = x * x;
-  float u = c * (x + 0.044715f * x2 * x);
-  float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * c * (1.f + 3.f * 0.044715f * x2);
+  const float x2 = x * x;
+  const float s = gelu_sig(x, x2);
+  return fmaf(x * s * (1.f - s), fmaf(3.f * GELU_A * GELU_K, x2, GELU_K), s);
 }
 
 }  // namespace pcv

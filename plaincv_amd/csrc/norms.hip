@@ -249,9 +249,11 @@ extern "C" int pcv_layernorm_bwd(const float* dy, int64_t lddy, const float* x, 
                                  int D, void* stream) {
   if (R <= 0 || D <= 0 || D > 4096 || (D & 3)) return PCV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  // parameter grads first: they read dy and x before dx (which may alias dres) is written
-  hipLaunchKernelGGL((norm_param_grad_kernel<float, float, true>), grid_cols(R, D), dim3(256), 0, s, dy, lddy, x,
-                     ldx, mean, rstd, dscale, dbias, R, D);
+  // parameter grads first: they read dy and x before dx (which may alias dres) is written.
+  // dscale == nullptr: the caller launches pcv_layernorm_param_grad itself (e.g. on a side stream)
+  if (dscale)
+    hipLaunchKernelGGL((norm_param_grad_kernel<float, float, true>), grid_cols(R, D), dim3(256), 0, s, dy, lddy, x,
+                       ldx, mean, rstd, dscale, dbias, R, D);
   PCV_NV_DISPATCH(D, hipLaunchKernelGGL(ln_bwd_kernel<NV>, grid_rows(R), dim3(256), 0, s, dy, lddy, x, ldx,
                                         scale, mean, rstd, dres, ldres, dx, lddx, (bf16*)dx_bf16, lddxb, R, D));
   return pcv_launch_status();
@@ -271,11 +273,32 @@ extern "C" int pcv_rmsnorm_bwd(const void* dy, int64_t lddy, const void* x, int6
                                float* dscale, int64_t R, int D, void* stream) {
   if (R <= 0 || D <= 0 || D > 4096 || (D & 3)) return PCV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL((norm_param_grad_kernel<bf16, bf16, false>), grid_cols(R, D), dim3(256), 0, s,
-                     (const bf16*)dy, lddy, (const bf16*)x, ldx, (const float*)nullptr, rstd, dscale,
-                     (float*)nullptr, R, D);
+  if (dscale)
+    hipLaunchKernelGGL((norm_param_grad_kernel<bf16, bf16, false>), grid_cols(R, D), dim3(256), 0, s,
+                       (const bf16*)dy, lddy, (const bf16*)x, ldx, (const float*)nullptr, rstd, dscale,
+                       (float*)nullptr, R, D);
   PCV_NV_DISPATCH(D, hipLaunchKernelGGL(rms_bwd_kernel<NV>, grid_rows(R), dim3(256), 0, s, (const bf16*)dy,
                                         lddy, (const bf16*)x, ldx, scale, rstd, (const bf16*)dres, ldres, (bf16*)dx,
                                         lddx, R, D));
+  return pcv_launch_status();
+}
+
+// Parameter gradients alone (dscale += sum_r dy*xhat, dbias += sum_r dy), for callers that
+// run them off the critical path; same kernel pcv_layernorm_bwd / pcv_rmsnorm_bwd launch.
+extern "C" int pcv_layernorm_param_grad(const float* dy, int64_t lddy, const float* x, int64_t ldx,
+                                        const float* mean, const float* rstd, float* dscale, float* dbias,
+                                        int64_t R, int D, void* stream) {
+  if (R <= 0 || D <= 0 || D > 4096 || (D & 3) || !dscale || !dbias) return PCV_EINVAL;
+  hipLaunchKernelGGL((norm_param_grad_kernel<float, float, true>), grid_cols(R, D), dim3(256), 0,
+                     (hipStream_t)stream, dy, lddy, x, ldx, mean, rstd, dscale, dbias, R, D);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_rmsnorm_param_grad(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* rstd,
+                                      float* dscale, int64_t R, int D, void* stream) {
+  if (R <= 0 || D <= 0 || D > 4096 || (D & 3) || !dscale) return PCV_EINVAL;
+  hipLaunchKernelGGL((norm_param_grad_kernel<bf16, bf16, false>), grid_cols(R, D), dim3(256), 0,
+                     (hipStream_t)stream, (const bf16*)dy, lddy, (const bf16*)x, ldx, (const float*)nullptr, rstd,
+                     dscale, (float*)nullptr, R, D);
   return pcv_launch_status();
 }

@@ -22,13 +22,17 @@ F32 = ctypes.c_float
 SIGNATURES = {
     "pcv_gemm_bf16": [P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, I64, I64, I64, I64,
                       F32, F32, I32, P, P, I64, I64, I32, F32, P, I64, I32, F32, P, U32, I32, P],
-    "pcv_attn_fwd": [P, P, P, I64, P, I64, P, I32, I32, I32, I32, I32, F32, P, U32, P],
+    "pcv_attn_fwd": [P, P, P, I64, P, I64, P, I32, I32, I32, I32, I32, F32, P, P],
     "pcv_attn_bwd": [P, P, P, I64, P, I64, P, I64, P, P, P, P, P, I64, I32, I32, I32, I32, I32,
-                     F32, P, U32, P],
+                     F32, P, P],
+    "pcv_attn_mask_words": [I32],
+    "pcv_attn_drop_mask": [P, U32, U32, I32, I32, F32, P, P],
     "pcv_layernorm_fwd": [P, I64, P, P, P, I64, P, P, I64, I32, F32, P],
     "pcv_layernorm_bwd": [P, I64, P, I64, P, P, P, P, I64, P, I64, P, I64, P, P, I64, I32, P],
     "pcv_rmsnorm_fwd": [P, I64, P, P, I64, P, I64, I32, F32, P],
     "pcv_rmsnorm_bwd": [P, I64, P, I64, P, P, P, I64, P, I64, P, I64, I32, P],
+    "pcv_layernorm_param_grad": [P, I64, P, I64, P, P, P, P, I64, I32, P],
+    "pcv_rmsnorm_param_grad": [P, I64, P, I64, P, P, I64, I32, P],
     "pcv_rope": [P, I64, I64, I32, I32, I32, P, P, I32, P],
     "pcv_swiglu_fwd": [P, I64, P, I64, I64, I32, I32, P],
     "pcv_swiglu_bwd": [P, I64, P, I64, P, I64, I64, I32, I32, P],
@@ -52,6 +56,9 @@ SIGNATURES = {
     "pcv_chunk_size": [],
 }
 
+# non-status return types (everything else returns an int status)
+RESTYPES = {"pcv_attn_mask_words": I64}
+
 _lib = None
 _err = None
 
@@ -74,7 +81,7 @@ def load():
     for name, argt in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argt
-        fn.restype = ctypes.c_int
+        fn.restype = RESTYPES.get(name, ctypes.c_int)
     if hasattr(lib, "pcv_last_error_string"):
         lib.pcv_last_error_string.argtypes = [ctypes.c_int]
         lib.pcv_last_error_string.restype = ctypes.c_char_p

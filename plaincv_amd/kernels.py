@@ -83,9 +83,11 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
         split_k = 1
         plain = out_f32 and beta == 1.0 and bias is None and res is None and act == EPI_NONE and drop_rate == 0.0
         if plain and K >= 1024:
-            t64 = math.ceil(M / 64) * math.ceil(N / 64) * nb
-            if t64 < 512:
-                split_k = max(1, min(math.ceil(1024 / t64), K // 512))
+            # weight-gradient shape (small MxN, long K): split K until the 128x128-tile grid
+            # covers the 256 CUs; the device side then picks the 128x128 tile (t128*split >= 240)
+            t128 = math.ceil(M / 128) * math.ceil(N / 128) * nb
+            if t128 < 256:
+                split_k = max(1, min(math.ceil(256 / t128), K // 512))
     hip.call("pcv_gemm_bf16", ptr(a2), ptr(b2), ptr(o2), M, N, K, _ld(a2), _ld(b2), _ld(o2),
              int(ta), int(tb), nb, sa, sb, sc, float(alpha), float(beta), out_f32,
              ptr(bias), ptr(res), ldr, sr, res_f32, float(res_scale), ptr(aux), ldaux, int(act),
@@ -104,8 +106,20 @@ def _dev(*ts):
             raise ValueError("tensor must live on the GPU")
 
 
-def attn_fwd(qkv, out, lse2, B, T, H, Dh, causal, drop_rate=0.0, seed=None, site=0, q_off=0, k_off=None, v_off=None):
-    """Flash attention forward on packed qkv [B*T, ld] (q|k|v column blocks)."""
+def attn_mask_words(T):
+    return int(hip.load().pcv_attn_mask_words(int(T)))
+
+
+def attn_drop_mask(seed, site, T, drop_rate, mask, layers=1, site_stride=0):
+    """Draw the broadcast [T,T] attention-dropout keep bits of `layers` layers (site + l*site_stride)."""
+    _chk(mask.dtype == torch.int16 and mask.numel() >= layers * attn_mask_words(T), "attn mask buffer")
+    _dev(seed, mask)
+    hip.call("pcv_attn_drop_mask", ptr(seed), int(site) & 0xFFFFFFFF, int(site_stride), int(layers), int(T),
+             float(drop_rate), ptr(mask), stream_ptr())
+
+
+def attn_fwd(qkv, out, lse2, B, T, H, Dh, causal, drop_rate=0.0, mask=None, q_off=0, k_off=None, v_off=None):
+    """Flash attention forward on packed qkv [B*T, ld] (q|k|v column blocks); `mask` = attn_drop_mask bits."""
     D = H * Dh
     k_off = D if k_off is None else k_off
     v_off = 2 * D if v_off is None else v_off
@@ -116,10 +130,10 @@ def attn_fwd(qkv, out, lse2, B, T, H, Dh, causal, drop_rate=0.0, seed=None, site
     es = qkv.element_size()
     hip.call("pcv_attn_fwd", base + q_off * es, base + k_off * es, base + v_off * es, _ld(qkv),
              ptr(out), _ld(out), ptr(lse2), B, T, H, Dh, int(causal), float(drop_rate),
-             ptr(seed), int(site), stream_ptr())
+             ptr(mask), stream_ptr())
 
 
-def attn_bwd(qkv, o, dout, lse2, delta_ws, dqkv, B, T, H, Dh, causal, drop_rate=0.0, seed=None, site=0):
+def attn_bwd(qkv, o, dout, lse2, delta_ws, dqkv, B, T, H, Dh, causal, drop_rate=0.0, mask=None):
     D = H * Dh
     _chk(qkv.dtype == BF16 and dqkv.dtype == BF16 and dout.dtype == BF16 and o.dtype == BF16, "attn bwd dtypes")
     _chk(dqkv.shape[0] == B * T and dqkv.shape[1] >= 3 * D and delta_ws.numel() >= B * H * T, "attn bwd shapes")
@@ -128,7 +142,7 @@ def attn_bwd(qkv, o, dout, lse2, delta_ws, dqkv, B, T, H, Dh, causal, drop_rate=
     dbase = dqkv.data_ptr()
     hip.call("pcv_attn_bwd", base, base + D * es, base + 2 * D * es, _ld(qkv), ptr(o), _ld(o), ptr(dout),
              _ld(dout), ptr(lse2), ptr(delta_ws), dbase, dbase + D * es, dbase + 2 * D * es, _ld(dqkv),
-             B, T, H, Dh, int(causal), float(drop_rate), ptr(seed), int(site), stream_ptr())
+             B, T, H, Dh, int(causal), float(drop_rate), ptr(mask), stream_ptr())
 
 
 def layernorm_fwd(x, scale, bias, y, mean, rstd, eps=1e-6):
@@ -146,6 +160,22 @@ def layernorm_bwd(dy, x, scale, mean, rstd, dres, dx, dx_bf16, dscale, dbias):
     hip.call("pcv_layernorm_bwd", ptr(dy), _ld(dy), ptr(x), _ld(x), ptr(scale), ptr(mean), ptr(rstd),
              ptr(dres), _ld(dres) if dres is not None else 0, ptr(dx), _ld(dx), ptr(dx_bf16),
              _ld(dx_bf16) if dx_bf16 is not None else 0, ptr(dscale), ptr(dbias), R, D, stream_ptr())
+
+
+def layernorm_param_grad(dy, x, mean, rstd, dscale, dbias):
+    R, D = x.shape
+    _chk(dy.dtype == F32 and x.dtype == F32 and tuple(dy.shape) == (R, D), "layernorm param grad")
+    _dev(dy, x, mean, rstd, dscale, dbias)
+    hip.call("pcv_layernorm_param_grad", ptr(dy), _ld(dy), ptr(x), _ld(x), ptr(mean), ptr(rstd), ptr(dscale),
+             ptr(dbias), R, D, stream_ptr())
+
+
+def rmsnorm_param_grad(dy, x, rstd, dscale):
+    R, D = x.shape
+    _chk(dy.dtype == BF16 and x.dtype == BF16 and tuple(dy.shape) == (R, D), "rmsnorm param grad")
+    _dev(dy, x, rstd, dscale)
+    hip.call("pcv_rmsnorm_param_grad", ptr(dy), _ld(dy), ptr(x), _ld(x), ptr(rstd), ptr(dscale), R, D,
+             stream_ptr())
 
 
 def rmsnorm_fwd(x, scale, y, rstd, eps=1e-6):

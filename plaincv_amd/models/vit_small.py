@@ -11,6 +11,7 @@ LayerNorm statistics, softmax and every gradient reduction stay fp32
 (the reference ViT is fp32: the bf16 operands are BASELINE.json config 2's
 "bf16").  Dropout uses the counter hash shared with oracle/rng.py.
 """
+import contextlib
 import math
 
 import torch
@@ -127,14 +128,14 @@ class VisionTransformer:
                 out[name] = _lecun_normal(shp, shp[0], gen)
         return out
 
-    def bind(self, store, image_shape, device):
-        return ViTRunner(self, store, image_shape, device)
+    def bind(self, store, image_shape, device, side_stream=False):
+        return ViTRunner(self, store, image_shape, device, side_stream=side_stream)
 
 
 class ViTRunner:
     """Fixed-shape forward/backward executor for one batch geometry."""
 
-    def __init__(self, model: VisionTransformer, store: ParamStore, image_shape, device):
+    def __init__(self, model: VisionTransformer, store: ParamStore, image_shape, device, side_stream=False):
         self.m = model
         self.s = store
         B, Hh, Ww, C = image_shape
@@ -167,6 +168,9 @@ class ViTRunner:
         self.qkv = [e(R, 3 * D, dt=bf) for _ in range(Lc)]
         self.o = [e(R, D, dt=bf) for _ in range(Lc)]
         self.lse = [e(B * H * self.T) for _ in range(Lc)]
+        # broadcast attention-dropout keep bits, drawn once per step for all layers
+        self.mask_words = K.attn_mask_words(self.T)
+        self.attn_mask = torch.zeros(Lc * self.mask_words, dtype=torch.int16, device=dev)
         self.h = [e(R, M, dt=bf) for _ in range(Lc)]
         self.a = [e(R, M, dt=bf) for _ in range(Lc)]
         self.yf = e(B, D, dt=bf)
@@ -178,14 +182,24 @@ class ViTRunner:
         self.row_loss = e(B)
         self.row_correct = e(B)
         self.metrics = torch.zeros(2, dtype=f32, device=dev)  # [loss, accuracy]
-        # backward workspaces
-        self.dx = e(R, D)
-        self.dxb = e(R, D, dt=bf)
-        self.dym = e(R, D, dt=bf)
-        self.dh = e(R, M, dt=bf)
-        self.dy = e(R, D)
+        # backward workspaces.  Weight/bias/norm-parameter gradients may run on a side stream
+        # beside the data-gradient chain (side_stream=True), so every activation gradient they
+        # read has its own per-layer buffer (nothing is overwritten while the side stream may
+        # still read it).  Off by default: a captured graph spreads two-stream work over
+        # several hardware queues and every cross-queue edge cost 5-12 us on MI355X
+        # (profiles/r01_vit_side_stream_timeline.txt), more than the overlap returns at ViT-small size.
+        self.side = torch.cuda.Stream(device=dev) if (side_stream and dev.type == "cuda") else None
+        self.dx = e(R, D)                              # top-of-stack residual gradient
+        self.dym = [e(R, D, dt=bf) for _ in range(Lc)]
+        self.dh = [e(R, M, dt=bf) for _ in range(Lc)]
+        self.dy_m = [e(R, D) for _ in range(Lc)]
+        self.dx_mid = [e(R, D) for _ in range(Lc)]
+        self.dxb_mid = [e(R, D, dt=bf) for _ in range(Lc)]
+        self.dqkv = [e(R, 3 * D, dt=bf) for _ in range(Lc)]
+        self.dy_a = [e(R, D) for _ in range(Lc)]
+        self.dx_out = [e(R, D) for _ in range(Lc)]
+        self.dxb_out = [e(R, D, dt=bf) for _ in range(Lc)]
         self.do = e(R, D, dt=bf)
-        self.dqkv = e(R, 3 * D, dt=bf)
         self.delta = e(B * H * self.T)
         self.dyf = e(B, D)
         self.dpatch = e(B * self.hw, D, dt=bf)
@@ -233,6 +247,10 @@ class ViTRunner:
         self.Wh, self.bh = W["Dense_0/kernel"], P["Dense_0/bias"]
         self.gWh, self.gbh = G["Dense_0/kernel"], G["Dense_0/bias"]
 
+    def _mask(self, i):
+        w = self.mask_words
+        return self.attn_mask[i * w:(i + 1) * w]
+
     # ---------------------------------------------------------- forward
     def forward(self, images, labels=None, train=True, need_grad=True):
         """images: uint8 (B,H,W,C) on the GPU; labels int32 (B,).  Leaves
@@ -246,6 +264,9 @@ class ViTRunner:
         K.vit_patchify(images, self.patches, m.patch_size)
         K.gemm(self.patches, self.Wconv, self.patch_out, bias=self.bconv)
         K.vit_embed_fwd(self.patch_out, self.cls, self.pos, self.xs[0], None, B, T, D, rate, seed, SITE_EMBED)
+        if rate > 0.0:
+            K.attn_drop_mask(seed, site_attn(0), T, rate, self.attn_mask, layers=m.num_layers,
+                             site_stride=site_attn(1) - site_attn(0))
         for i in range(m.num_layers):
             w = self.w[i]
             x = self.xs[i]
@@ -255,7 +276,7 @@ class ViTRunner:
                 K.dropout_bwd_cast(x, self.y0[i])
             K.gemm(self.y0[i], w["Wqkv"], self.qkv[i], bias=w["bqkv"])
             K.attn_fwd(self.qkv[i], self.o[i], self.lse[i], B, T, H, Dh, causal=False, drop_rate=rate,
-                       seed=seed, site=site_attn(i))
+                       mask=self._mask(i))
             K.gemm(self.o[i], w["Wo"], self.x1s[i], bias=w["bo"], res=x)
             if m.use_layernorm:
                 K.layernorm_fwd(self.x1s[i], w["s1"], w["c1"], self.y1[i], *self.st1[i])
@@ -277,62 +298,87 @@ class ViTRunner:
         return self.metrics
 
     # --------------------------------------------------------- backward
+    def _fork(self):
+        """Side stream waits for everything issued on the main stream so far; returns its context."""
+        if self.side is None:
+            return contextlib.nullcontext()
+        self.side.wait_stream(torch.cuda.current_stream())
+        return torch.cuda.stream(self.side)
+
     def backward(self, train=True):
-        """Accumulates parameter gradients (+=) into the store's grad buffer."""
+        """Accumulates parameter gradients (+=) into the store's grad buffer.
+
+        The data-gradient chain (dgrad GEMMs, attention, norm backward) runs on the
+        caller's stream; weight-gradient GEMMs, bias column sums and norm-parameter
+        gradients are forked onto self.side as soon as their inputs exist and joined
+        back at the end (a graph capture turns this into parallel branches)."""
         m = self.m
         B, T, D, H, Dh = self.B, self.T, self.D, self.H, self.Dh
         rate = m.dropout_rate if train else 0.0
         seed = self.seed
         # head
         K.dropout_bwd_cast(self.dlogits, self.dlogits_b) if self.Kc % 4 == 0 else self.dlogits_b.copy_(self.dlogits)
-        K.gemm(self.yf, self.dlogits_b, self.gWh, ta=True, beta=1.0)
-        K.colsum(self.dlogits, self.gbh)
+        with self._fork():
+            K.gemm(self.yf, self.dlogits_b, self.gWh, ta=True, beta=1.0)
+            K.colsum(self.dlogits, self.gbh)
         K.gemm(self.dlogits_b, self.Wh, self.dyf, tb=True)
         self.dx.zero_()
-        self.dxb.zero_()
         dxc = self.dx.view(B, T * D)[:, :D]
-        dxbc = self.dxb.view(B, T * D)[:, :D]
         xcls = self.xs[-1].view(B, T * D)[:, :D]
         if m.use_layernorm:
-            K.layernorm_bwd(self.dyf, xcls, self.sf, *self.stf, None, dxc, dxbc, self.gsf, self.gcf)
+            K.layernorm_bwd(self.dyf, xcls, self.sf, *self.stf, None, dxc, None, self.gsf, self.gcf)
         else:
             dxc.copy_(self.dyf)
-            dxbc.copy_(self.dyf)
+        dx_in = self.dx
         for i in reversed(range(m.num_layers)):
             w = self.w[i]
+            dym, dh, dqkv = self.dym[i], self.dh[i], self.dqkv[i]
+            dx_mid, dxb_mid, dx_out, dxb_out = self.dx_mid[i], self.dxb_mid[i], self.dx_out[i], self.dxb_out[i]
             # MLP: x2 = x1 + drop(D1(drop(gelu(D0(ln1(x1))))))
-            K.dropout_bwd_cast(self.dx, self.dym, rate, seed, site_mlp_out(i))
-            K.colsum(self.dym, w["gb1"])
-            K.gemm(self.a[i], self.dym, w["gW1"], ta=True, beta=1.0)
-            K.gemm(self.dym, w["W1"], self.dh, tb=True, aux=self.h[i], act=K.EPI_GELU_BWD, drop_rate=rate,
+            K.dropout_bwd_cast(dx_in, dym, rate, seed, site_mlp_out(i))
+            with self._fork():
+                K.colsum(dym, w["gb1"])
+                K.gemm(self.a[i], dym, w["gW1"], ta=True, beta=1.0)
+            K.gemm(dym, w["W1"], dh, tb=True, aux=self.h[i], act=K.EPI_GELU_BWD, drop_rate=rate,
                    seed=seed, site=site_mlp_hidden(i))
-            K.colsum(self.dh, w["gb0"])
-            K.gemm(self.y1[i], self.dh, w["gW0"], ta=True, beta=1.0)
+            with self._fork():
+                K.colsum(dh, w["gb0"])
+                K.gemm(self.y1[i], dh, w["gW0"], ta=True, beta=1.0)
             if m.use_layernorm:
-                K.gemm(self.dh, w["W0"], self.dy, tb=True)
-                K.layernorm_bwd(self.dy, self.x1s[i], w["s1"], *self.st1[i], self.dx, self.dx, self.dxb,
-                                w["gs1"], w["gc1"])
+                K.gemm(dh, w["W0"], self.dy_m[i], tb=True)
+                K.layernorm_bwd(self.dy_m[i], self.x1s[i], w["s1"], *self.st1[i], dx_in, dx_mid, dxb_mid,
+                                None, None)
+                with self._fork():
+                    K.layernorm_param_grad(self.dy_m[i], self.x1s[i], *self.st1[i], w["gs1"], w["gc1"])
             else:
-                K.gemm(self.dh, w["W0"], self.dx, tb=True, beta=1.0)
-                K.dropout_bwd_cast(self.dx, self.dxb)
+                K.gemm(dh, w["W0"], dx_mid, tb=True, res=dx_in)
+                K.dropout_bwd_cast(dx_mid, dxb_mid)
             # attention: x1 = x + out(attn(qkv(ln0(x))))
-            K.gemm(self.o[i], self.dxb, w["gWo"], ta=True, beta=1.0)
-            K.colsum(self.dx, w["gbo"])
-            K.gemm(self.dxb, w["Wo"], self.do, tb=True)
-            K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, self.dqkv, B, T, H, Dh,
-                       causal=False, drop_rate=rate, seed=seed, site=site_attn(i))
-            K.gemm(self.y0[i], self.dqkv, w["gWqkv"], ta=True, beta=1.0)
-            K.colsum(self.dqkv, w["gbqkv"])
+            with self._fork():
+                K.gemm(self.o[i], dxb_mid, w["gWo"], ta=True, beta=1.0)
+                K.colsum(dx_mid, w["gbo"])
+            K.gemm(dxb_mid, w["Wo"], self.do, tb=True)
+            K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
+                       causal=False, drop_rate=rate, mask=self._mask(i))
+            with self._fork():
+                K.gemm(self.y0[i], dqkv, w["gWqkv"], ta=True, beta=1.0)
+                K.colsum(dqkv, w["gbqkv"])
             if m.use_layernorm:
-                K.gemm(self.dqkv, w["Wqkv"], self.dy, tb=True)
-                K.layernorm_bwd(self.dy, self.xs[i], w["s0"], *self.st0[i], self.dx, self.dx, self.dxb,
-                                w["gs0"], w["gc0"])
+                K.gemm(dqkv, w["Wqkv"], self.dy_a[i], tb=True)
+                K.layernorm_bwd(self.dy_a[i], self.xs[i], w["s0"], *self.st0[i], dx_mid, dx_out, dxb_out,
+                                None, None)
+                with self._fork():
+                    K.layernorm_param_grad(self.dy_a[i], self.xs[i], *self.st0[i], w["gs0"], w["gc0"])
             else:
-                K.gemm(self.dqkv, w["Wqkv"], self.dx, tb=True, beta=1.0)
-                K.dropout_bwd_cast(self.dx, self.dxb)
-        K.vit_embed_bwd(self.dx, self.dpatch, self.gcls, self.gpos, None, B, T, D, rate, seed, SITE_EMBED)
-        K.colsum(self.dpatch, self.gbconv)
-        K.gemm(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
+                K.gemm(dqkv, w["Wqkv"], dx_out, tb=True, res=dx_mid)
+                K.dropout_bwd_cast(dx_out, dxb_out)
+            dx_in = dx_out
+        K.vit_embed_bwd(dx_in, self.dpatch, self.gcls, self.gpos, None, B, T, D, rate, seed, SITE_EMBED)
+        with self._fork():
+            K.colsum(self.dpatch, self.gbconv)
+            K.gemm(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
 
     def flops_per_step(self):
         """Algorithmic fwd+bwd matmul FLOPs (3x forward; SURVEY §8d counting)."""

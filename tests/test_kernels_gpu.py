@@ -21,9 +21,34 @@ def _attn_ref(qkv, B, T, H, Dh, causal, keep=None, rate=0.0):
     return torch.einsum("bhqk,bkhd->bqhd", p, v).reshape(B * T, D)
 
 
+def _unpack_attn_mask(words, T):
+    """Decode pcv_attn_drop_mask's packed layout (attention.hip drop_word) into a [T,T] bool mask."""
+    n64 = 2 * ((T + 127) // 128)
+    q = np.arange(T)[:, None]
+    k = np.arange(T)[None, :]
+    w = ((((q >> 4) * n64 + (k >> 6)) * 4 + ((q & 15) >> 2)) * 16 + ((k & 15) >> 2) * 4 + ((k & 63) >> 4))
+    bit = (q & 3) * 4 + (k & 3)
+    return ((words.astype(np.int64)[w] >> bit) & 1).astype(bool)
+
+
+@pytest.mark.parametrize("T,rate", [(257, 0.1), (100, 0.5), (1030, 0.2)])
+def test_attn_drop_mask_bits(dev, T, rate):
+    from oracle import rng
+    from plaincv_amd import kernels as K
+    seed = torch.tensor([4321], dtype=torch.int32, device=dev)
+    W = K.attn_mask_words(T)
+    mask = torch.zeros(3 * W, dtype=torch.int16, device=dev)
+    K.attn_drop_mask(seed, 20, T, rate, mask, layers=3, site_stride=4)
+    words = mask.cpu().numpy().view(np.uint16)
+    for layer in range(3):
+        got = _unpack_attn_mask(words[layer * W:(layer + 1) * W], T)
+        assert np.array_equal(got, rng.keep_mask(4321, 20 + 4 * layer, (T, T), rate))
+
+
 @pytest.mark.parametrize("B,T,H,Dh,causal,rate", [(2, 257, 4, 32, False, 0.0), (2, 100, 2, 64, True, 0.0),
                                                   (1, 1024, 2, 64, True, 0.0), (2, 257, 4, 32, False, 0.1),
-                                                  (3, 70, 3, 32, True, 0.0)])
+                                                  (3, 70, 3, 32, True, 0.0), (2, 100, 2, 64, True, 0.2),
+                                                  (1, 300, 2, 32, False, 0.3)])
 def test_attention_fwd_bwd(dev, B, T, H, Dh, causal, rate):
     from oracle import rng
     from plaincv_amd import kernels as K
@@ -33,7 +58,12 @@ def test_attention_fwd_bwd(dev, B, T, H, Dh, causal, rate):
     out = torch.empty(B * T, D, device=dev, dtype=torch.bfloat16)
     lse = torch.empty(B * H * T, device=dev)
     seed = torch.tensor([1234], dtype=torch.int32, device=dev)
-    K.attn_fwd(qkv, out, lse, B, T, H, Dh, causal, drop_rate=rate, seed=seed, site=7)
+    mask = None
+    if rate > 0:
+        mask = torch.zeros(2 * K.attn_mask_words(T), dtype=torch.int16, device=dev)
+        K.attn_drop_mask(seed, 3, T, rate, mask, layers=2, site_stride=4)   # layer 1 -> site 7
+        mask = mask[K.attn_mask_words(T):]
+    K.attn_fwd(qkv, out, lse, B, T, H, Dh, causal, drop_rate=rate, mask=mask)
     keep = None
     if rate > 0:
         keep = torch.from_numpy(rng.keep_mask(1234, 7, (T, T), rate)).to(dev)
@@ -44,7 +74,7 @@ def test_attention_fwd_bwd(dev, B, T, H, Dh, causal, rate):
     ref.backward(do.float())
     dqkv = torch.zeros(B * T, 3 * D, device=dev, dtype=torch.bfloat16)
     delta = torch.empty(B * H * T, device=dev)
-    K.attn_bwd(qkv, out, do, lse, delta, dqkv, B, T, H, Dh, causal, drop_rate=rate, seed=seed, site=7)
+    K.attn_bwd(qkv, out, do, lse, delta, dqkv, B, T, H, Dh, causal, drop_rate=rate, mask=mask)
     g = qf.grad
     err = (dqkv.float() - g).abs().max().item()
     scale = g.abs().max().item()
