@@ -138,11 +138,17 @@ int pcv_step_bump(int* step, void* stream);
 /* Muon (optax.contrib.muon scale_by_muon): momentum + nesterov + Frobenius normalisation
  * into NS workspaces, and the shape-scaled weight-decayed update; descriptors are
  * pcv_muon_mat_size()-byte records (see optim.hip MuonMat). */
-int pcv_muon_prep(const void* mats, int nmats, int64_t max_elems, float beta, int nesterov, float eps,
+int pcv_muon_prep(const void* mats, int nmats, int nnorm, int64_t max_elems, float beta, int nesterov, float eps,
                   const int* step, const float* gscale, void* stream);
 int pcv_muon_apply(const void* mats, int nmats, int64_t max_elems, float lr, float wd, int shape_scale,
                    int apply, void* stream);
 int pcv_muon_mat_size(void);
+/* Newton-Schulz of matrices whose NS operand is at most 128 x 256, entirely in one
+ * workgroup's LDS (csrc/muon_fused.hip): reads each record's x32 (un-normalised, from
+ * pcv_muon_prep) and norm2, writes xo.  pcv_muon_fused_ok(rows, cols) says which shapes qualify. */
+int pcv_muon_fused_ok(int64_t rows, int64_t cols);
+int pcv_muon_ns_fused(const void* mats, int nmats, float eps, float ns_a, float ns_b, float ns_c, int ns_steps,
+                      void* stream);
 int pcv_chunk_size(void);
 const char* pcv_last_error_string(int code);
 

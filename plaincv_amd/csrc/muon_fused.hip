@@ -1,0 +1,259 @@
+// plaincv_amd/csrc/muon_fused.hip -- Newton-Schulz of a small matrix in ONE workgroup.
+//
+// optax.contrib.muon (optim/factory.py:441-484, routing optim/muon.py:120-129) orthogonalises
+// each routed update with five Newton-Schulz iterations.  The general path runs them as three
+// batched GEMM launches per iteration (optim/muon.py _newton_schulz); for matrices whose NS
+// operand X (min x max of the kernel shape) fits in LDS -- r' <= 128, c' <= 256, every
+// ViT-small routed kernel -- one 512-thread workgroup per matrix runs all iterations with X,
+// A and B resident in LDS: one launch instead of 3 * ns_steps.
+//
+// Input: the un-normalised fp32 X written by muon_prep_kernel (x32, [r'][ldx]) and its
+// squared Frobenius norm; output: bf16 X_ns (xo, [r'][ldx]) read by muon_apply_kernel.
+// Numerics follow the general path: X, A' = b X X^T and B = (c/b^2) A'A' + A' are bf16
+// (fp32 MFMA accumulation) and X' = B X + a X is rounded to bf16 each iteration.
+//
+// A' and B are symmetric, which the kernel uses three ways: their B-operand fragments are
+// read as rows (k contiguous); a 16x16 result tile is stored transposed (4 consecutive
+// elements per lane, one 8-byte LDS write); and X' is computed as X'^T = X^T B so that its
+// tiles, too, store 4 consecutive elements of an X row per lane.  Every block is computed
+// whole on zero-padded images (no per-tile guards inside the MFMA loops).
+#include "common.h"
+#include "optim_types.h"
+
+namespace pcv {
+namespace {
+
+constexpr int MF_THREADS = 512, MF_WAVES = 8;
+constexpr int MF_RMAX = 128, MF_CMAX = 256;
+constexpr int MF_LDX = MF_CMAX + 8, MF_LDA = MF_RMAX + 8;   // padded rows (elements)
+constexpr size_t MF_LDS = (size_t)MF_RMAX * MF_LDX * 2 + 2 * (size_t)MF_RMAX * MF_LDA * 2;
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// 16 rows x 32 k (row-major image, k contiguous): lane l -> row l&15, k = 8*(l>>4) .. +8
+__device__ __forceinline__ bf16x8 frag_rows(const bf16* lds, int ld, int row0, int ks) {
+  const int l = threadIdx.x & 63;
+  return *reinterpret_cast<const bf16x8*>(lds + (row0 + (l & 15)) * ld + ks * 32 + 8 * (l >> 4));
+}
+// same rows, k in the kappa order of frag_tr: k = 32s + 4g + j (j<4), 32s + 16 + 4g + j-4 (j>=4)
+__device__ __forceinline__ bf16x8 frag_rows_kappa(const bf16* lds, int ld, int row0, int s) {
+  const int l = threadIdx.x & 63, g = l >> 4;
+  const bf16* p = lds + (row0 + (l & 15)) * ld + 32 * s + 4 * g;
+  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(p);
+  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(p + 16);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+// k running over ROWS of a row-major image (kappa order), the 16 columns c0.. on the lane,
+// via the transposing ds_read_b64_tr_b16 (same construction as attention.hip tr_frag)
+__device__ __forceinline__ bf16x8 frag_tr(const bf16* lds, int ld, int s, int c0) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, w = l & 15, q = w >> 2, p = w & 3;
+  const bf16* a0 = lds + (32 * s + 4 * g + q) * ld + c0 + 4 * p;
+  const bf16* a1 = a0 + 16 * ld;
+  const bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
+  const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a1));
+  return bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+}
+
+#define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0)
+
+// C(4x2 tiles) = L[rows rt0*16..+64) . L[rows ct0*16..+32)^T over k = 0 .. 32*ksteps
+__device__ __forceinline__ void gram_block(const bf16* L, int ld, int rt0, int ct0, int ksteps, f32x4 (&acc)[4][2]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a[4], b[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a[i] = frag_rows(L, ld, (rt0 + i) * 16, 0);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b[j] = frag_rows(L, ld, (ct0 + j) * 16, 0);
+  for (int ks = 0; ks < ksteps; ++ks) {
+    bf16x8 an[4], bn[2];
+    const int kn = ks + 1 < ksteps ? ks + 1 : ks;     // last step re-reads (harmless, keeps the loop branch-free)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) an[i] = frag_rows(L, ld, (rt0 + i) * 16, kn);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bn[j] = frag_rows(L, ld, (ct0 + j) * 16, kn);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = MFMA16(a[i], b[j], acc[i][j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = an[i];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b[j] = bn[j];
+  }
+}
+
+// C(4x2 tiles) = X^T[rows ct0*16..+64) . Bm[.., cols rt0*16..+32) over k = 0 .. 32*ssteps  (= (Bm X)^T)
+__device__ __forceinline__ void xtb_block(const bf16* X, const bf16* Bm, int ct0, int rt0, int ssteps,
+                                          f32x4 (&acc)[4][2]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a[4], b[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a[i] = frag_tr(X, MF_LDX, 0, (ct0 + i) * 16);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b[j] = frag_rows_kappa(Bm, MF_LDA, (rt0 + j) * 16, 0);
+  for (int s = 0; s < ssteps; ++s) {
+    bf16x8 an[4], bn[2];
+    const int sn = s + 1 < ssteps ? s + 1 : s;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) an[i] = frag_tr(X, MF_LDX, sn, (ct0 + i) * 16);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bn[j] = frag_rows_kappa(Bm, MF_LDA, (rt0 + j) * 16, sn);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = MFMA16(a[i], b[j], acc[i][j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = an[i];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) b[j] = bn[j];
+  }
+}
+
+__device__ __forceinline__ void st4(bf16* p, float a, float b, float c, float d) {
+  *reinterpret_cast<bf16x4*>(p) = bf16x4{f2bf(a), f2bf(b), f2bf(c), f2bf(d)};
+}
+
+__global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats, float eps, float ns_a, float ns_b,
+                                                             float ns_c, int ns_steps) {
+  extern __shared__ __attribute__((aligned(16))) char smem_m[];
+  bf16* X = reinterpret_cast<bf16*>(smem_m);                       // [128][MF_LDX]
+  bf16* A = X + MF_RMAX * MF_LDX;                                  // [128][MF_LDA]
+  bf16* Bm = A + MF_RMAX * MF_LDA;                                 // [128][MF_LDA]
+  const MuonMat M = mats[blockIdx.x];
+  const int rx = (int)(M.rows < M.cols ? M.rows : M.cols), cx = (int)(M.rows < M.cols ? M.cols : M.rows);
+  const int ldx = (int)M.ldx;
+  const int rp = (rx + 31) / 32 * 32, cp = (cx + 31) / 32 * 32;    // zero-padded to the MFMA k step
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4;
+
+  // X = x32 / (||x32||_F + eps) -> bf16; padding rows/columns of all images zero
+  const float inv = 1.f / (sqrtf(*M.norm2) + eps);
+  for (int i = tid; i < MF_RMAX * MF_LDX / 4; i += MF_THREADS) {
+    const int r = i / (MF_LDX / 4), c4 = (i % (MF_LDX / 4)) * 4;
+    f32x4v v = f32x4v{0.f, 0.f, 0.f, 0.f};
+    if (r < rx && c4 < cx) {
+      v = *reinterpret_cast<const f32x4v*>(M.x32 + (int64_t)r * ldx + c4);
+      // x32 rows are padded to ldx >= cx with unspecified values: keep only real columns
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (c4 + e >= cx) v[e] = 0.f;
+    }
+    st4(X + r * MF_LDX + c4, v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
+  }
+  for (int i = tid; i < 2 * MF_RMAX * MF_LDA / 8; i += MF_THREADS)
+    reinterpret_cast<u32x4*>(A)[i] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+
+  const int nrt = rp / 16, nct = cp / 16;
+  const int bcols_sq = (nrt + 1) / 2, nblk_sq = ((nrt + 3) / 4) * bcols_sq;
+  const int bcols_x = (nrt + 1) / 2, nblk_x = ((nct + 3) / 4) * bcols_x;
+  const float cb2 = ns_c / (ns_b * ns_b);
+  for (int it = 0; it < ns_steps; ++it) {
+    // A' = b X X^T, then B = (c/b^2) A'A' + A'   (symmetric: tiles stored transposed)
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const bf16* L = pass == 0 ? X : A;
+      const int ld = pass == 0 ? MF_LDX : MF_LDA;
+      bf16* out = pass == 0 ? A : Bm;
+      for (int blk = wave; blk < nblk_sq; blk += MF_WAVES) {
+        const int rt0 = (blk / bcols_sq) * 4, ct0 = (blk % bcols_sq) * 2;
+        f32x4 acc[4][2];
+        gram_block(L, ld, rt0, ct0, (pass == 0 ? cp : rp) / 32, acc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            // lane holds C[(rt0+i)*16 + 4g + r][(ct0+j)*16 + (l&15)], r = 0..3 -> write C^T
+            const int trow = (ct0 + j) * 16 + (lane & 15), tcol = (rt0 + i) * 16 + 4 * g;
+            bf16* dst = out + trow * MF_LDA + tcol;
+            if (pass == 0) {
+              st4(dst, ns_b * acc[i][j][0], ns_b * acc[i][j][1], ns_b * acc[i][j][2], ns_b * acc[i][j][3]);
+            } else {
+              const bf16x4 a4 = *reinterpret_cast<const bf16x4*>(A + trow * MF_LDA + tcol);
+              st4(dst, fmaf(cb2, acc[i][j][0], bf2f(a4[0])), fmaf(cb2, acc[i][j][1], bf2f(a4[1])),
+                  fmaf(cb2, acc[i][j][2], bf2f(a4[2])), fmaf(cb2, acc[i][j][3], bf2f(a4[3])));
+            }
+          }
+      }
+      __syncthreads();
+    }
+    // X'^T = X^T B + a X^T : tiles of X'^T (cp x rp); lane holds X'[row (rt0+j)*16 + (l&15)]
+    // [cols (ct0+i)*16 + 4g .. +3]; at most 2 blocks per wave, kept in registers until every
+    // wave has finished reading X
+    f32x4 acc[2][4][2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int blk = wave + q * MF_WAVES;
+      if (blk < nblk_x) xtb_block(X, Bm, (blk / bcols_x) * 4, (blk % bcols_x) * 2, rp / 32, acc[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int blk = wave + q * MF_WAVES;
+      if (blk >= nblk_x) continue;
+      const int ct0 = (blk / bcols_x) * 4, rt0 = (blk % bcols_x) * 2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const bf16x4 x4 =
+              *reinterpret_cast<const bf16x4*>(X + ((rt0 + j) * 16 + (lane & 15)) * MF_LDX + (ct0 + i) * 16 + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[q][i][j][r] = fmaf(ns_a, bf2f(x4[r]), acc[q][i][j][r]);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int blk = wave + q * MF_WAVES;
+      if (blk >= nblk_x) continue;
+      const int ct0 = (blk / bcols_x) * 4, rt0 = (blk % bcols_x) * 2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int row = (rt0 + j) * 16 + (lane & 15), col = (ct0 + i) * 16 + 4 * g;
+          // rows >= rp / columns >= cp of the padded image must stay zero
+          if (row < rp && col < cp)
+            st4(X + row * MF_LDX + col, acc[q][i][j][0], acc[q][i][j][1], acc[q][i][j][2], acc[q][i][j][3]);
+        }
+    }
+    __syncthreads();
+  }
+
+  // X_ns -> xo [rx][ldx] (real rows/columns only)
+  bf16* xo = const_cast<bf16*>(M.xo);
+  for (int i = tid; i < rx * (ldx / 4); i += MF_THREADS) {
+    const int r = i / (ldx / 4), c4 = (i % (ldx / 4)) * 4;
+    if (c4 < cx) *reinterpret_cast<bf16x4*>(xo + (int64_t)r * ldx + c4) = *reinterpret_cast<const bf16x4*>(X + r * MF_LDX + c4);
+  }
+}
+
+}  // namespace
+}  // namespace pcv
+
+using namespace pcv;
+
+// Whether pcv_muon_ns_fused handles a (rows x cols) kernel: NS operand min x max within 128 x 256.
+extern "C" int pcv_muon_fused_ok(int64_t rows, int64_t cols) {
+  const int64_t r = rows < cols ? rows : cols, c = rows < cols ? cols : rows;
+  return r > 0 && r <= MF_RMAX && c <= MF_CMAX;
+}
+
+extern "C" int pcv_muon_ns_fused(const void* mats, int nmats, float eps, float ns_a, float ns_b, float ns_c,
+                                 int ns_steps, void* stream) {
+  if (nmats <= 0 || ns_steps < 0 || ns_b == 0.f) return PCV_EINVAL;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)muon_ns_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)MF_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(muon_ns_kernel, dim3(nmats), dim3(MF_THREADS), MF_LDS, (hipStream_t)stream,
+                     (const MuonMat*)mats, eps, ns_a, ns_b, ns_c, ns_steps);
+  return pcv_launch_status();
+}

@@ -12,6 +12,7 @@
 // Step counters, gscale and norms live in device memory so the whole optimizer
 // step replays correctly from a captured hipGraph.
 #include "common.h"
+#include "optim_types.h"
 
 namespace pcv {
 
@@ -80,20 +81,6 @@ __global__ __launch_bounds__(1024) void gscale_kernel(const float* partial, int 
 __global__ void bump_kernel(int* step) { *step += 1; }
 
 // ------------------------------------------------------------------- Muon
-struct MuonMat {
-  float* p; const float* g; float* mu; bf16* pb; float* upd;
-  int64_t rows, cols, ld, ldx;  // param view (fan_in x fan_out) row stride ld; X row stride ldx
-  float* x32;                  // workspace [r', c'] (transposed if rows > cols)
-  bf16* xb;                    // bf16 copy of the normalised X (NS input)
-  const bf16* xo;              // NS output [r', c'] (bf16)
-  float* norm2;                // sum of squares of x32
-};
-
-struct MuonHyper {
-  float beta, lr, wd, eps, shape_scale;
-  int nesterov, apply;
-};
-
 // mu = beta*mu + (1-beta)*g*gs; X = nesterov-corrected mu_hat, stored transposed when rows > cols
 __global__ __launch_bounds__(256) void muon_prep_kernel(const MuonMat* mats, MuonHyper h, const int* step,
                                                         const float* gscale) {
@@ -177,15 +164,17 @@ extern "C" int pcv_step_bump(int* step, void* stream) {
   return pcv_launch_status();
 }
 
-extern "C" int pcv_muon_prep(const void* mats, int nmats, int64_t max_elems, float beta, int nesterov, float eps,
-                             const int* step, const float* gscale, void* stream) {
-  if (nmats <= 0) return PCV_EINVAL;
+// nnorm: the leading records whose bf16 NS input the norm kernel writes (the others are
+// normalised by pcv_muon_ns_fused while it loads x32)
+extern "C" int pcv_muon_prep(const void* mats, int nmats, int nnorm, int64_t max_elems, float beta, int nesterov,
+                             float eps, const int* step, const float* gscale, void* stream) {
+  if (nmats <= 0 || nnorm < 0 || nnorm > nmats) return PCV_EINVAL;
   MuonHyper h{beta, 0.f, 0.f, eps, 0.f, nesterov, 0};
   int gx = (int)((max_elems + 256 * 8 - 1) / (256 * 8));
   gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(muon_prep_kernel, dim3(gx, nmats), dim3(256), 0, s, (const MuonMat*)mats, h, step, gscale);
-  hipLaunchKernelGGL(muon_norm_kernel, dim3(gx, nmats), dim3(256), 0, s, (const MuonMat*)mats, eps);
+  if (nnorm > 0) hipLaunchKernelGGL(muon_norm_kernel, dim3(gx, nnorm), dim3(256), 0, s, (const MuonMat*)mats, eps);
   return pcv_launch_status();
 }
 

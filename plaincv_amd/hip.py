@@ -50,8 +50,10 @@ SIGNATURES = {
     "pcv_adamw_step": [P, P, P, P, P, P, P, I32, F32, F32, F32, F32, F32, F32, I32, I32, P, P, P],
     "pcv_grad_scale": [P, P, I32, P, F32, F32, P, P, P],
     "pcv_step_bump": [P, P],
-    "pcv_muon_prep": [P, I32, I64, F32, I32, F32, P, P, P],
+    "pcv_muon_prep": [P, I32, I32, I64, F32, I32, F32, P, P, P],
     "pcv_muon_apply": [P, I32, I64, F32, F32, I32, I32, P],
+    "pcv_muon_ns_fused": [P, I32, F32, F32, F32, F32, I32, P],
+    "pcv_muon_fused_ok": [I64, I64],
     "pcv_muon_mat_size": [],
     "pcv_chunk_size": [],
 }

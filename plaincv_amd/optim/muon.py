@@ -14,7 +14,10 @@ Newton-Schulz chain runs as batched bf16 MFMA GEMMs over each group (three
 GEMMs per iteration: A' = b X X^T; B = (c/b^2) A'A' + A'; X' = B X + a X, the
 scalars folded into the GEMM epilogues), ping-ponging two bf16 X buffers.
 Momentum/normalisation (pcv_muon_prep) and the final update (pcv_muon_apply)
-are one launch each over all routed matrices.
+are one launch each over all routed matrices.  Matrices whose NS operand fits
+one workgroup's LDS (min <= 128, max <= 256: every ViT-small kernel) skip
+the GEMM chain: pcv_muon_ns_fused runs all iterations for each of them in one
+workgroup with X, A, B resident in LDS -- one launch for all such matrices.
 """
 from collections import OrderedDict
 
@@ -49,7 +52,7 @@ class _Group:
 class Muon(GradientTransformation):
     def __init__(self, learning_rate, ns_coeffs=(3.4445, -4.7750, 2.0315), ns_steps=5, beta=0.95, eps=1e-8,
                  weight_decay=0.0, nesterov=True, adaptive=False, adam_b1=0.9, adam_b2=0.999, adam_eps_root=0.0,
-                 adam_weight_decay=0.0, shape_scale=True):
+                 adam_weight_decay=0.0, shape_scale=True, fused=True):
         if adaptive:
             raise NotImplementedError("muon_adaptive=True (dual-norm scaling) is not on the hot path")
         self.lr = float(learning_rate)
@@ -59,6 +62,7 @@ class Muon(GradientTransformation):
         self.nesterov = bool(nesterov)
         self.adam = (float(adam_b1), float(adam_b2), float(adam_eps_root), float(adam_weight_decay))
         self.shape_scale = bool(shape_scale)
+        self.fused = bool(fused)     # False: every routed matrix takes the batched-GEMM chain
 
     def init(self, store):
         dev = store.device
@@ -71,45 +75,53 @@ class Muon(GradientTransformation):
         b1, b2, eps_root, awd = self.adam
         st.branch = AdamBranch(store, rest, b1, b2, self.eps, eps_root, awd, self.nesterov)
         st.routed = routed
-        # group routed matrices by NS shape (min, max)
+        # Group routed matrices by NS shape (min, max).  Groups whose operand fits one
+        # workgroup's LDS (csrc/muon_fused.hip) run Newton-Schulz in a single launch; the
+        # rest run the batched-GEMM chain.  Records: general groups first (the prep launch
+        # normalises those into bf16), then the fused ones (normalised by the NS kernel).
+        lib = hip.load()
         groups = OrderedDict()
         for k in routed:
             r, c = store.params[k].shape
-            key = (min(r, c), max(r, c))
-            groups.setdefault(key, []).append(k)
-        st.groups = [_Group(r, c, names, dev) for (r, c), names in groups.items()]
+            groups.setdefault((min(r, c), max(r, c)), []).append(k)
+        gl = [_Group(r, c, names, dev) for (r, c), names in groups.items()]
+        for g in gl:
+            g.fused = self.fused and bool(lib.pcv_muon_fused_ok(g.r, g.c))
+        st.groups = [g for g in gl if not g.fused] + [g for g in gl if g.fused]
+        st.n_general = sum(len(g.names) for g in st.groups if not g.fused)
+        st.n_fused = len(routed) - st.n_general
         st.norm2 = torch.zeros(max(1, len(routed)), dtype=torch.float32, device=dev)
         st.max_elems = max([store.params[k].numel() for k in routed], default=1)
         final = self.ns_steps % 2
         mu = st.tensors["mu"]
+        size = lib.pcv_muon_mat_size()
+        assert size == 13 * 8, size
         recs_apply, recs_upd = [], []
         idx = 0
-        esz4, esz2 = 4, 2
         for g in st.groups:
             for j, k in enumerate(g.names):
                 leaf = store.leaf(k)
                 rows, cols = leaf.shape
-                ld = leaf.strides[0]
                 off = leaf.offset
-                base = [store.flat.data_ptr() + off * esz4, store.grad_flat.data_ptr() + off * esz4,
-                        mu.data_ptr() + off * esz4, store.shadow.data_ptr() + off * esz2]
-                tail = [rows, cols, ld, g.ldx, g.x32[j].data_ptr(), g.xb[0][j].data_ptr(),
-                        g.xb[final][j].data_ptr(), st.norm2.data_ptr() + idx * 4]
+                xo = g.xb[0 if g.fused else final][j]
+                base = [store.flat.data_ptr() + off * 4, store.grad_flat.data_ptr() + off * 4,
+                        mu.data_ptr() + off * 4, store.shadow.data_ptr() + off * 2]
+                tail = [rows, cols, leaf.strides[0], g.ldx, g.x32[j].data_ptr(), g.xb[0][j].data_ptr(),
+                        xo.data_ptr(), st.norm2.data_ptr() + idx * 4]
                 recs_apply.append(base + [0] + tail)
-                recs_upd.append(base + [st.upd.data_ptr() + off * esz4] + tail)
+                recs_upd.append(base + [st.upd.data_ptr() + off * 4] + tail)
                 idx += 1
-        size = hip.load().pcv_muon_mat_size()
-        assert size == 13 * 8, size
-        st.mats_apply = torch.tensor(np.array(recs_apply, dtype=np.uint64).view(np.int64), device=dev) \
-            if routed else None
-        st.mats_upd = torch.tensor(np.array(recs_upd, dtype=np.uint64).view(np.int64), device=dev) \
-            if routed else None
+        tab = lambda recs: torch.tensor(np.array(recs, dtype=np.uint64).view(np.int64), device=dev)  # noqa: E731
+        st.mats_apply = tab(recs_apply) if routed else None
+        st.mats_upd = tab(recs_upd) if routed else None
         return st
 
     # ------------------------------------------------------------------
     def _newton_schulz(self, st):
         a, b, c = self.a, self.b, self.c
         for g in st.groups:
+            if g.fused:
+                continue
             cur = 0
             for _ in range(self.ns_steps):
                 X, Xn = g.xb[cur], g.xb[cur ^ 1]
@@ -117,12 +129,15 @@ class Muon(GradientTransformation):
                 K.gemm(g.A, g.A, g.B, alpha=c / (b * b), res=g.A)          # B = c/b^2 A'A' + A'
                 K.gemm(g.B, X, Xn, res=X, res_scale=a)                     # X = B X + a X
                 cur ^= 1
+        if st.n_fused:
+            fused_recs = st.mats_apply[st.n_general:]
+            hip.call("pcv_muon_ns_fused", ptr(fused_recs), st.n_fused, self.eps, a, b, c, self.ns_steps,
+                     stream_ptr())
 
     def _run(self, store, st, gscale, apply):
-        ensure = st.routed
-        if ensure:
+        if st.routed:
             st.norm2.zero_()
-            hip.call("pcv_muon_prep", ptr(st.mats_apply), len(st.routed), st.max_elems, self.beta,
+            hip.call("pcv_muon_prep", ptr(st.mats_apply), len(st.routed), st.n_general, st.max_elems, self.beta,
                      int(self.nesterov), self.eps, ptr(st.count), ptr(gscale), stream_ptr())
             self._newton_schulz(st)
             mats = st.mats_apply if apply else st.mats_upd

@@ -204,3 +204,37 @@ def test_gemm_dropout_matches_oracle_hash(dev):
     assert torch.allclose(out, ref, atol=1e-2, rtol=1e-3)
     frac = keep.float().mean().item()
     assert abs(frac - 0.75) < 0.02
+
+
+@pytest.mark.parametrize("shapes", [[(128, 256), (256, 128), (128, 200), (48, 100), (128, 128)],
+                                    [(96, 256), (7, 33), (200, 64)]])
+def test_muon_fused_matches_batched_chain(dev, shapes):
+    """pcv_muon_fused (one workgroup per matrix, NS in LDS) vs the batched-GEMM NS chain:
+    same momentum, same bf16 NS numerics (up to A'A' vs A'A'^T on a symmetric A'), so the
+    updates agree to bf16 rounding of the orthogonalised direction (|du| <= 2e-2 * lr)."""
+    from plaincv_amd.optim.muon import Muon
+    from plaincv_amd.params import Layout, ParamStore
+    lay = Layout()
+    for i, s in enumerate(shapes):
+        lay.add(f"Dense_{i}/kernel", s)
+    lay.add("Dense_0/bias", (shapes[0][1],))
+    g = torch.Generator().manual_seed(7)
+    init = {k: torch.randn(*l.shape, generator=g) * 0.1 for k, l in lay.leaves.items()}
+    grads = [{k: torch.randn(*l.shape, generator=g) for k, l in lay.leaves.items()} for _ in range(3)]
+    ups = []
+    for fused in (True, False):
+        store = ParamStore(lay, dev)
+        store.load(init)
+        tx = Muon(1e-3, weight_decay=0.1, fused=fused)
+        st = tx.init(store)
+        assert (st.n_fused > 0) == fused
+        for gr in grads:
+            store.zero_grad()
+            for k, v in gr.items():
+                store.grads[k].copy_(v.to(dev))
+            tx.step_(store, st)
+        torch.cuda.synchronize()
+        ups.append({k: (store.params[k].cpu() - init[k]) for k in init})
+    for k in init:
+        d = (ups[0][k] - ups[1][k]).abs().max().item()
+        assert d <= 3 * 2e-2 * 1e-3, (k, d)
