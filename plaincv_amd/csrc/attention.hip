@@ -53,10 +53,26 @@ __host__ __device__ __forceinline__ int64_t drop_words(int T) {
   return (int64_t)(8 * ((T + 127) / 128)) * drop_n64(T) * 64;
 }
 
+// LDS tile images are unpadded [rows][DH] with the 16-B chunks of row r XOR-permuted
+// by tswz(r) (a function of r mod 16).  The masks were found by exhaustive search
+// over XOR-linear maps so that all three access shapes are bank-conflict-free:
+// row fragments (ds_read_b128, 16 rows x one chunk), transposing fragments
+// (ds_read_b64_tr_b16, 8 rows x 32 B) and the tile stores (ds_write_b128).
 template <int DH>
 struct Tile {
-  static constexpr int LD = DH + 8;  // padded row (elements), 16-B aligned rows
+  static constexpr int LD = DH;
 };
+template <int DH>
+__device__ __forceinline__ int tswz(int r) {
+  if constexpr (DH == 32) return (((r >> 2) & 1) << 1) ^ ((r >> 3) & 1);
+  else if constexpr (DH == 64) return (((r >> 1) & 1) << 1) ^ (((r >> 2) & 1) << 2) ^ ((r >> 3) & 1);
+  else return ((r & 1) << 1) ^ (((r >> 1) & 1) << 2) ^ (((r >> 2) & 1) << 3) ^ ((r >> 3) & 1);
+}
+// element offset of 16-B chunk `c` of row `r`
+template <int DH>
+__device__ __forceinline__ int toff(int r, int c) {
+  return r * DH + ((c ^ tswz<DH>(r)) << 3);
+}
 
 // Cooperative load of 64 rows x DH of a column block into a padded LDS image.
 template <int DH>
@@ -69,7 +85,7 @@ __device__ __forceinline__ void load_rows(bf16* lds, const bf16* base, int64_t l
     const int gr = row0 + r;
     u32x4 v = u32x4{0u, 0u, 0u, 0u};
     if (gr < T) v = *reinterpret_cast<const u32x4*>(base + (bT + gr) * ld + c * 8);
-    *reinterpret_cast<u32x4*>(lds + r * LD + c * 8) = v;
+    *reinterpret_cast<u32x4*>(lds + toff<DH>(r, c)) = v;
   }
 }
 
@@ -77,15 +93,15 @@ __device__ __forceinline__ void load_rows(bf16* lds, const bf16* base, int64_t l
 template <int DH>
 __device__ __forceinline__ bf16x8 row_frag(const bf16* lds, int rbase, int ks) {
   const int l = threadIdx.x & 63;
-  return *reinterpret_cast<const bf16x8*>(lds + (rbase + (l & 15)) * Tile<DH>::LD + ks * 32 + 8 * (l >> 4));
+  return *reinterpret_cast<const bf16x8*>(lds + toff<DH>(rbase + (l & 15), ks * 4 + (l >> 4)));
 }
 // fragment whose k index runs over ROWS in kappa order (32-row step s), columns cbase..+15
 template <int DH>
 __device__ __forceinline__ bf16x8 tr_frag(const bf16* lds, int s, int cbase) {
   const int l = threadIdx.x & 63;
   const int g = l >> 4, w = l & 15, q = w >> 2, p = w & 3;
-  const bf16* a0 = lds + (32 * s + 4 * g + q) * Tile<DH>::LD + cbase + 4 * p;
-  const bf16* a1 = a0 + 16 * Tile<DH>::LD;
+  const bf16* a0 = lds + toff<DH>(32 * s + 4 * g + q, (cbase >> 3) + (p >> 1)) + 4 * (p & 1);
+  const bf16* a1 = a0 + 16 * DH;   // row +16: same swizzle
   bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
   bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a1));
   return bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
@@ -134,8 +150,8 @@ __device__ __forceinline__ void tile_store(const TileRegs<DH>& t, bf16* Ks, bf16
   for (int i = 0; i < TileRegs<DH>::N; ++i) {
     const int idx = threadIdx.x + 256 * i;
     const int r = idx / CPR, c = idx % CPR;
-    *reinterpret_cast<u32x4*>(Ks + r * LD + c * 8) = t.k[i];
-    *reinterpret_cast<u32x4*>(Vs + r * LD + c * 8) = t.v[i];
+    *reinterpret_cast<u32x4*>(Ks + toff<DH>(r, c)) = t.k[i];
+    *reinterpret_cast<u32x4*>(Vs + toff<DH>(r, c)) = t.v[i];
   }
 }
 
@@ -143,9 +159,9 @@ __device__ __forceinline__ void tile_store(const TileRegs<DH>& t, bf16* Ks, bf16
 // fragment read from LDS); K/V tiles of 64 keys double-buffered in LDS.
 template <int DH, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnArgs a) {
-  constexpr int LD = Tile<DH>::LD;
   constexpr int KS = DH / 32, DT = DH / 16, QG = 2;
-  __shared__ __attribute__((aligned(16))) bf16 KVs[2][2][64 * LD];
+  constexpr int TILE = 64 * DH;
+  __shared__ __attribute__((aligned(16))) bf16 kv_smem[2 * 2 * TILE];   // [buffer][K|V][TILE]
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int T = a.T;
   const int64_t bT = (int64_t)b * T;
@@ -178,11 +194,11 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
   if (CAUSAL) nkb = min(nkb, (qb * 128 + 127) / 64 + 1);
   TileRegs<DH> pre;
   tile_load<DH>(pre, Kp, Vp, a.ldq, 0, T, bT);
-  tile_store<DH>(pre, KVs[0][0], KVs[0][1]);
+  tile_store<DH>(pre, kv_smem, kv_smem + TILE);
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
-    const bf16* Ks = KVs[kb & 1][0];
-    const bf16* Vs = KVs[kb & 1][1];
+    const bf16* Ks = kv_smem + 2 * (kb & 1) * TILE;
+    const bf16* Vs = Ks + TILE;
     const bool more = kb + 1 < nkb;
     if (more) tile_load<DH>(pre, Kp, Vp, a.ldq, (kb + 1) * 64, T, bT);
     const bool active = qw < T && (!CAUSAL || kb * 64 <= qw + 31);   // wave-uniform skip
@@ -270,7 +286,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
         }
       }
     }
-    if (more) tile_store<DH>(pre, KVs[(kb + 1) & 1][0], KVs[(kb + 1) & 1][1]);
+    if (more) tile_store<DH>(pre, kv_smem + 2 * ((kb + 1) & 1) * TILE, kv_smem + (2 * ((kb + 1) & 1) + 1) * TILE);
     __syncthreads();
   }
   // normalise + store
@@ -329,10 +345,10 @@ struct QTileRegs {
 
 template <int DH, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(AttnArgs a) {
-  constexpr int LD = Tile<DH>::LD;
   constexpr int KS = DH / 32, DT = DH / 16, KG = 2, CPR = DH / 8;
-  __shared__ __attribute__((aligned(16))) bf16 QOs[2][2][64 * LD];
-  __shared__ float LDl[2][2][64];
+  constexpr int TILE = 64 * DH;
+  __shared__ __attribute__((aligned(16))) bf16 qo_smem[2 * 2 * TILE];   // [buffer][Q|dO][TILE]
+  __shared__ float ld_smem[2 * 128];                                    // [buffer][lse|delta][64]
   const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int T = a.T;
   const int64_t bT = (int64_t)b * T;
@@ -383,28 +399,28 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
       t.d = qq < T ? del[qq] : 0.f;
     }
   };
+  const int nqb = (T + 63) / 64;
+  const int qb0 = CAUSAL ? (kb * 128) / 64 : 0;
   auto qstore = [&](const QTileRegs<DH>& t, int buf) {
 #pragma unroll
     for (int i = 0; i < QTileRegs<DH>::N; ++i) {
       const int idx = threadIdx.x + 256 * i;
       const int r = idx / CPR, c = idx % CPR;
-      *reinterpret_cast<u32x4*>(QOs[buf][0] + r * LD + c * 8) = t.q[i];
-      *reinterpret_cast<u32x4*>(QOs[buf][1] + r * LD + c * 8) = t.o[i];
+      *reinterpret_cast<u32x4*>(qo_smem + 2 * buf * TILE + toff<DH>(r, c)) = t.q[i];
+      *reinterpret_cast<u32x4*>(qo_smem + (2 * buf + 1) * TILE + toff<DH>(r, c)) = t.o[i];
     }
-    if (threadIdx.x < 64) { LDl[buf][0][threadIdx.x] = t.l; LDl[buf][1][threadIdx.x] = t.d; }
+    if (threadIdx.x < 64) { ld_smem[buf * 128 + threadIdx.x] = t.l; ld_smem[buf * 128 + 64 + threadIdx.x] = t.d; }
   };
 
-  const int nqb = (T + 63) / 64;
-  const int qb0 = CAUSAL ? (kb * 128) / 64 : 0;
   QTileRegs<DH> pre;
   if (qb0 < nqb) { qload(pre, qb0 * 64); qstore(pre, 0); }
   __syncthreads();
   for (int qb = qb0; qb < nqb; ++qb) {
     const int buf = (qb - qb0) & 1;
-    const bf16* Qs = QOs[buf][0];
-    const bf16* Ds = QOs[buf][1];
-    const float* Ls = LDl[buf][0];
-    const float* Dl = LDl[buf][1];
+    const bf16* Qs = qo_smem + 2 * buf * TILE;
+    const bf16* Ds = Qs + TILE;
+    const float* Ls = ld_smem + buf * 128;
+    const float* Dl = Ls + 64;
     const bool more = qb + 1 < nqb;
     if (more) qload(pre, (qb + 1) * 64);
     const bool active = kw < T && (!CAUSAL || qb * 64 + 63 >= kw);
@@ -497,9 +513,9 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
 // Workgroup = 4 waves x 32 queries; loops over prefetched, double-buffered K/V tiles.
 template <int DH, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(AttnArgs a) {
-  constexpr int LD = Tile<DH>::LD;
+  constexpr int TILE = 64 * DH;
   constexpr int KS = DH / 32, DT = DH / 16, QG = 2;
-  __shared__ __attribute__((aligned(16))) bf16 KVs[2][2][64 * LD];
+  __shared__ __attribute__((aligned(16))) bf16 kv_smem[2 * 2 * TILE];   // [buffer][K|V][TILE]
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int T = a.T;
   const int64_t bT = (int64_t)b * T;
@@ -537,11 +553,11 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
   if (CAUSAL) nkb = min(nkb, (qb * 128 + 127) / 64 + 1);
   TileRegs<DH> pre;
   tile_load<DH>(pre, Kp, Vp, a.ldq, 0, T, bT);
-  tile_store<DH>(pre, KVs[0][0], KVs[0][1]);
+  tile_store<DH>(pre, kv_smem, kv_smem + TILE);
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
-    const bf16* Ks = KVs[kb & 1][0];
-    const bf16* Vs = KVs[kb & 1][1];
+    const bf16* Ks = kv_smem + 2 * (kb & 1) * TILE;
+    const bf16* Vs = Ks + TILE;
     const bool more = kb + 1 < nkb;
     if (more) tile_load<DH>(pre, Kp, Vp, a.ldq, (kb + 1) * 64, T, bT);
     const bool active = qw < T && (!CAUSAL || kb * 64 <= qw + 31);
@@ -599,7 +615,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
         }
       }
     }
-    if (more) tile_store<DH>(pre, KVs[(kb + 1) & 1][0], KVs[(kb + 1) & 1][1]);
+    if (more) tile_store<DH>(pre, kv_smem + 2 * ((kb + 1) & 1) * TILE, kv_smem + (2 * ((kb + 1) & 1) + 1) * TILE);
     __syncthreads();
   }
 #pragma unroll

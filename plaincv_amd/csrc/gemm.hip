@@ -37,6 +37,16 @@ struct GemmArgs {
   int tiles_m, tiles_n;
   int vec_ok;                    // C/aux/res/bias bases and row strides allow 16-B access
   int glds_ok;                   // A/B bases and row strides allow 16-B LDS-DMA pieces
+  // Row-complete LayerNorm epilogues (pcv_gemm_ln; the 64x128 tile holds whole rows, N <= 128):
+  //  ln_mode 1: C = x1 = alpha*acc + bias (+dropout) + res;  ln_y = LN(x1) (bf16), ln_mean/ln_rstd out
+  //  ln_mode 2: dy = alpha*acc;  C = dx = res + LN_bwd(dy; ln_x, ln_mean, ln_rstd, ln_scale),
+  //             ln_y = bf16(dx); ln_dscale += sum dy*xhat, ln_dbias += sum dy, colsum += sum dx
+  int ln_mode;
+  const float* ln_scale; const float* ln_bias; float ln_eps;
+  bf16* ln_y; int64_t ld_lny;
+  float* ln_mean; float* ln_rstd;
+  const float* ln_x; int64_t ld_lnx;
+  float* ln_dscale; float* ln_dbias; float* colsum;
 };
 
 template <int R>
@@ -182,12 +192,154 @@ __device__ __forceinline__ void mc_glds(char* lds, const bf16* base, int64_t ld,
   }
 }
 
+// LayerNorm epilogue over whole rows of a BM x 128 fp32 tile staged in LDS (ct, row
+// stride 132).  16 consecutive lanes own one row (8 columns each), so the row
+// statistics are 4 xor-shuffles; per-column parameter gradients and column sums are
+// reduced over the workgroup's rows and added with one atomic per column.
+template <int BM>
+__device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0) {
+  constexpr int CLD = 128 + 4;
+  const int tid = threadIdx.x, cc = tid & 15, wave = tid >> 6, lane = tid & 63;
+  const int col = cc * 8;
+  const bool colok = col < g.N;          // N % 8 == 0: a chunk is all in or all out
+  const float invN = 1.f / (float)g.N;
+  float bv[8], sc[8], sh[8], cs[8], dsc[8], dbi[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { bv[e] = 0.f; sc[e] = 0.f; sh[e] = 0.f; cs[e] = 0.f; dsc[e] = 0.f; dbi[e] = 0.f; }
+  if (colok) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (g.bias) bv[e] = g.bias[col + e];
+      sc[e] = g.ln_scale[col + e];
+      if (g.ln_mode == 1) sh[e] = g.ln_bias[col + e];
+    }
+  }
+  const uint32_t seed = g.drop_thresh ? *g.seedp : 0u;
+  for (int rr = tid >> 4; rr < BM; rr += 16) {
+    const int64_t row = m0 + rr;
+    if (row >= g.M) break;                // uniform over the row's 16 lanes
+    float v[8];
+    const f32x4 c0 = *reinterpret_cast<const f32x4*>(ct + rr * CLD + col);
+    const f32x4 c1 = *reinterpret_cast<const f32x4*>(ct + rr * CLD + col + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = g.alpha * c0[e] + bv[e]; v[e + 4] = g.alpha * c1[e] + bv[e + 4]; }
+    if (g.drop_thresh) {
+      const uint32_t base = (uint32_t)(row * g.N + col);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] = (hash3(seed, g.site, base + e) >= g.drop_thresh) ? v[e] * g.drop_scale : 0.f;
+    }
+    float rv[8];
+    if (colok) {
+      const float* rp = (const float*)g.res + row * g.ldr + col;
+      const f32x4 r0 = *reinterpret_cast<const f32x4*>(rp), r1 = *reinterpret_cast<const f32x4*>(rp + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { rv[e] = r0[e]; rv[e + 4] = r1[e]; }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { rv[e] = 0.f; v[e] = 0.f; }
+    }
+    float* cp = (float*)g.C + row * g.ldc + col;
+    bf16* yp = g.ln_y ? g.ln_y + row * g.ld_lny + col : nullptr;
+    if (g.ln_mode == 1) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { v[e] += rv[e]; s1 += v[e]; s2 += v[e] * v[e]; }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      const float mean = s1 * invN;
+      const float rs = rsqrtf(fmaxf(s2 * invN - mean * mean, 0.f) + g.ln_eps);
+      if (colok) {
+        *reinterpret_cast<f32x4*>(cp) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(cp + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        bf16x8 y;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) y[e] = f2bf((v[e] - mean) * rs * sc[e] + sh[e]);
+        *reinterpret_cast<bf16x8*>(yp) = y;
+      }
+      if (cc == 0) { g.ln_mean[row] = mean; g.ln_rstd[row] = rs; }
+    } else {
+      const float mean = g.ln_mean[row], rs = g.ln_rstd[row];
+      float xh[8], gx[8], s1 = 0.f, s2 = 0.f;
+      if (colok) {
+        const float* xp = g.ln_x + row * g.ld_lnx + col;
+        const f32x4 x0 = *reinterpret_cast<const f32x4*>(xp), x1 = *reinterpret_cast<const f32x4*>(xp + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { xh[e] = (x0[e] - mean) * rs; xh[e + 4] = (x1[e] - mean) * rs; }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xh[e] = 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        gx[e] = v[e] * sc[e];
+        s1 += gx[e];
+        s2 += gx[e] * xh[e];
+        dsc[e] += v[e] * xh[e];
+        dbi[e] += v[e];
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      s1 *= invN;
+      s2 *= invN;
+      float dx[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { dx[e] = rv[e] + rs * (gx[e] - s1 - xh[e] * s2); cs[e] += dx[e]; }
+      if (colok) {
+        *reinterpret_cast<f32x4*>(cp) = f32x4{dx[0], dx[1], dx[2], dx[3]};
+        *reinterpret_cast<f32x4*>(cp + 4) = f32x4{dx[4], dx[5], dx[6], dx[7]};
+        if (g.ln_y) {
+          bf16x8 y;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) y[e] = f2bf(dx[e]);
+          *reinterpret_cast<bf16x8*>(yp) = y;
+        }
+      }
+    }
+  }
+  if (g.ln_mode != 2) return;
+  // column reductions: 4 row-groups per wave by shuffle, 4 waves through LDS, one atomic per column
+  __syncthreads();                        // ct is no longer read; reuse the LDS behind it
+  float* red = const_cast<float*>(ct) + BM * CLD;   // [3][4 waves][128]
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float a = dsc[e], b = dbi[e], c = cs[e];
+    a += __shfl_xor(a, 16, 64); a += __shfl_xor(a, 32, 64);
+    b += __shfl_xor(b, 16, 64); b += __shfl_xor(b, 32, 64);
+    c += __shfl_xor(c, 16, 64); c += __shfl_xor(c, 32, 64);
+    if (lane < 16) {
+      red[(0 * 4 + wave) * 128 + col + e] = a;
+      red[(1 * 4 + wave) * 128 + col + e] = b;
+      red[(2 * 4 + wave) * 128 + col + e] = c;
+    }
+  }
+  __syncthreads();
+  if (tid < 128 && tid < g.N) {
+    float a = 0.f, b = 0.f, c = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { a += red[w * 128 + tid]; b += red[(4 + w) * 128 + tid]; c += red[(8 + w) * 128 + tid]; }
+    if (g.ln_dscale) atomicAdd(g.ln_dscale + tid, a);
+    if (g.ln_dbias) atomicAdd(g.ln_dbias + tid, b);
+    if (g.colsum) atomicAdd(g.colsum + tid, c);
+  }
+}
+
+// k-tiles in flight: the 64x64 tile has little MFMA work per k-tile, so more of them
+// must be in flight to cover load latency (4 x 16 KiB ring); 128x128 keeps 2 x 32 KiB.
+#ifndef PCV_GEMM_STAGES_SMALL
+#define PCV_GEMM_STAGES_SMALL 2
+#endif
+template <int WM, int WN>
+struct GemmStages { static constexpr int S = WM * WN <= 4 ? PCV_GEMM_STAGES_SMALL : 2; };
+
 template <bool A_KC, bool B_KC, int WM, int WN>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   constexpr int BM = 32 * WM, BN = 32 * WN;
   constexpr int A_BYTES = BM * 64 * 2, B_BYTES = BN * 64 * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int S = GemmStages<WM, WN>::S;
+  constexpr int PIECES = (BM + BN) / 32;   // global_load_lds instructions per wave per k-tile
 
   // XCD-aware bijective remap, then GROUP_M=8 ordering
   const int nwg = g.tiles_m * g.tiles_n;
@@ -237,31 +389,45 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     if (B_KC) kc_store<BN>(stB, lb); else mc_store<BN>(stB, lb);
   };
 
-  // full k-tiles: async glds straight into LDS; the ragged last tile (and
-  // tiles when a leading dimension breaks 16-B alignment) via registers + zero fill
-  auto issue = [&](int64_t k0, int buf) -> bool {
+  // Full k-tiles go global->LDS asynchronously (global_load_lds) into an S-deep ring;
+  // the ragged last tile (and every tile when a leading dimension breaks 16-B
+  // alignment) goes through registers with zero fill, synchronously.
+  // Loads complete in order, so "tile kt landed" = at most PIECES*(tiles issued after
+  // kt) of this wave's vector-memory ops outstanding; a synchronous tile drains all.
+  auto issue = [&](int kt) {
+    if (kt >= nk) return;
+    const int64_t k0 = kbeg + (int64_t)kt * 64;
+    char* la = smem + (kt % S) * STAGE;
+    char* lb = la + A_BYTES;
     if (g.glds_ok && k0 + 64 <= kend) {
-      char* la = smem + buf * STAGE;
-      char* lb = la + A_BYTES;
       if (A_KC) kc_glds<BM>(la, A, g.lda, g.M, m0, k0); else mc_glds<BM>(la, A, g.lda, g.M, m0, k0);
       if (B_KC) kc_glds<BN>(lb, B, g.ldb, g.N, n0, k0); else mc_glds<BN>(lb, B, g.ldb, g.N, n0, k0);
-      return false;
+      return;
     }
     gload(k0);
-    return true;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lstore(kt % S);
   };
 
-  if (nk > 0) {
-    if (issue(kbeg, 0)) lstore(0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < S - 1; ++i) issue(i);
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    const char* la = smem + buf * STAGE;
+    // tile kt landed (this wave's pieces), then the barrier makes every wave's visible
+    // and frees the slot of tile kt-1 for tile kt+S-1
+    if constexpr (S == 4) {
+      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PIECES) : "memory");
+      else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PIECES) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (S == 3) {
+      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PIECES) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    issue(kt + S - 1);
+    const char* la = smem + (kt % S) * STAGE;
     const char* lb = la + A_BYTES;
-    bool pend = false;
-    if (kt + 1 < nk) pend = issue(kbeg + (int64_t)(kt + 1) * 64, buf ^ 1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[WM], bfr[WN];
@@ -281,10 +447,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
         for (int j = 0; j < WN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (pend) lstore(buf ^ 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();   // every wave done with the ring before the epilogue reuses the LDS
 
   // ---------------- epilogue ----------------
   // Stage the fp32 tile through LDS ([BM][BN+4], conflict-free ds_write_b32), then
@@ -313,6 +478,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
       if (row < g.M && col < g.N) atomicAdd(C + row * g.ldc + col, g.alpha * ct[rr * CLD + c]);
     }
     return;
+  }
+  if constexpr (BN == 128) {
+    if (g.ln_mode) { ln_epilogue<BM>(g, ct, m0); return; }
   }
   constexpr int CPR = BN / 8;            // 8-column chunks per row
   constexpr int RPP = 256 / CPR;         // rows per pass
@@ -435,7 +603,8 @@ static hipError_t launch_t(const GemmArgs& a, int batch, hipStream_t s) {
   GemmArgs g = a;
   g.tiles_m = (int)((g.M + BM - 1) / BM);
   g.tiles_n = (int)((g.N + BN - 1) / BN);
-  const size_t stage = 2 * (size_t)(BM + BN) * 64 * 2, ctile = (size_t)BM * (BN + 4) * 4;
+  const size_t stage = GemmStages<WM, WN>::S * (size_t)(BM + BN) * 64 * 2;
+  const size_t ctile = (size_t)BM * (BN + 4) * 4 + (BN == 128 ? 3 * 4 * 128 * 4 : 0);   // + LN reductions
   const size_t lds = stage > ctile ? stage : ctile;
   dim3 grid(g.tiles_m * g.tiles_n, batch, g.split_k > 1 ? g.split_k : 1);
   static bool attr = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
@@ -512,5 +681,48 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
   const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128);
   hipError_t e = (t128 * batch * g.split_k >= 240) ? launch_sz<4, 4>(g, trans_a, trans_b, (int)batch, s)
                                                     : launch_sz<2, 2>(g, trans_a, trans_b, (int)batch, s);
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+// GEMM whose epilogue finishes a LayerNorm over each complete output row (ViT: the
+// residual-stream GEMMs have N = hidden <= 128, so one 64 x 128 tile holds whole rows).
+// ln_mode 1 (forward): C = x1 = alpha*op(A).op(B) + bias (+dropout) + res  (fp32), and
+//   ln_y = bf16(LN(x1)*ln_scale + ln_bias), ln_mean/ln_rstd per row  -- replaces gemm + ln_fwd.
+// ln_mode 2 (backward): dy = alpha*op(A).op(B);  C = dx = res + LN_bwd(dy) (fp32),
+//   ln_y = bf16(dx), ln_dscale/ln_dbias/colsum accumulate (+=) over rows  -- replaces
+//   gemm + ln_bwd + the parameter-gradient and bias column-sum kernels.
+extern "C" int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                           int64_t ldb, int64_t ldc, int trans_a, int trans_b, float alpha, const float* bias,
+                           const float* res, int64_t ldr, float dropout_rate, const uint32_t* seed, uint32_t site,
+                           int ln_mode, const float* ln_scale, const float* ln_bias, float ln_eps, void* ln_y,
+                           int64_t ld_lny, float* ln_mean, float* ln_rstd, const float* ln_x, int64_t ld_lnx,
+                           float* ln_dscale, float* ln_dbias, float* colsum, void* stream) {
+  if (M < 0 || N <= 0 || K < 0 || N > 128 || (N & 7) || (ln_mode != 1 && ln_mode != 2)) return PCV_EINVAL;
+  if (!res || !ln_scale || !ln_mean || !ln_rstd) return PCV_EINVAL;
+  if (ln_mode == 1 && (!ln_bias || !ln_y)) return PCV_EINVAL;
+  if (ln_mode == 2 && (!ln_x || bias || dropout_rate > 0.f)) return PCV_EINVAL;
+  if (dropout_rate > 0.f && !seed) return PCV_EINVAL;
+  if (M == 0) return 0;
+  if ((lda & 7) || (ldb & 7) || !pcv_aligned16(A) || !pcv_aligned16(B)) return PCV_EALIGN;
+  if (!pcv_aligned16(C) || (ldc & 3) || !pcv_aligned16(res) || (ldr & 3) || (ln_y && (!pcv_aligned16(ln_y) || (ld_lny & 7))) ||
+      (ln_x && (!pcv_aligned16(ln_x) || (ld_lnx & 3))))
+    return PCV_EALIGN;
+  GemmArgs g{};
+  g.A = (const bf16*)A; g.B = (const bf16*)B; g.C = C;
+  g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.alpha = alpha; g.beta = 0.f; g.out_f32 = 1;
+  g.bias = bias; g.res = res; g.ldr = ldr; g.res_f32 = 1; g.res_scale = 1.f;
+  g.drop_thresh = 0; g.drop_scale = 1.f; g.seedp = seed; g.site = site;
+  if (dropout_rate > 0.f) {
+    double t = (double)dropout_rate * 4294967296.0;
+    g.drop_thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+    if (g.drop_thresh == 0) g.drop_thresh = 1;
+    g.drop_scale = 1.f / (1.f - dropout_rate);
+  }
+  g.vec_ok = 1; g.glds_ok = 1; g.split_k = 1;
+  g.ln_mode = ln_mode; g.ln_scale = ln_scale; g.ln_bias = ln_bias; g.ln_eps = ln_eps;
+  g.ln_y = (bf16*)ln_y; g.ld_lny = ld_lny; g.ln_mean = ln_mean; g.ln_rstd = ln_rstd;
+  g.ln_x = ln_x; g.ld_lnx = ld_lnx; g.ln_dscale = ln_dscale; g.ln_dbias = ln_dbias; g.colsum = colsum;
+  hipError_t e = launch_sz<2, 4>(g, trans_a, trans_b, 1, (hipStream_t)stream);
   return e == hipSuccess ? 0 : (int)e;
 }

@@ -95,6 +95,34 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
     return out
 
 
+def gemm_ln(a, b, out, *, ln_mode, res, ln_scale, ln_y, ln_mean, ln_rstd, ta=False, tb=False, alpha=1.0, bias=None,
+            drop_rate=0.0, seed=None, site=0, ln_bias=None, ln_eps=1e-6, ln_x=None, ln_dscale=None, ln_dbias=None,
+            colsum=None):
+    """GEMM whose epilogue completes a LayerNorm over each output row (pcv_gemm_ln, N <= 128).
+
+    ln_mode 1: out = x1 = op(a)@op(b)*alpha + bias (+dropout) + res;  ln_y = LN(x1) (bf16), stats out.
+    ln_mode 2: dy = op(a)@op(b)*alpha;  out = dx = res + LN_bwd(dy; ln_x, stats, ln_scale); ln_y = bf16(dx);
+               ln_dscale / ln_dbias / colsum accumulate."""
+    M, K = (a.shape[1], a.shape[0]) if ta else tuple(a.shape)
+    N, K2 = tuple(b.shape) if tb else (b.shape[1], b.shape[0])
+    _chk(K == K2 and tuple(out.shape) == (M, N) and tuple(res.shape) == (M, N), "gemm_ln shapes")
+    _chk(a.dtype == BF16 and b.dtype == BF16 and out.dtype == F32 and res.dtype == F32, "gemm_ln dtypes")
+    _chk(ln_y is not None or ln_mode == 2, "gemm_ln forward needs ln_y")
+    if ln_y is not None:
+        _chk(tuple(ln_y.shape) == (M, N) and ln_y.dtype == BF16, "gemm_ln ln_y")
+    _chk(ln_mode in (1, 2) and N <= 128 and N % 8 == 0, "gemm_ln mode / N")
+    if ln_mode == 2:
+        _chk(ln_x is not None and tuple(ln_x.shape) == (M, N) and ln_x.dtype == F32, "gemm_ln ln_x")
+    _dev(a, b, out, res, ln_scale, ln_y, ln_mean, ln_rstd, bias, ln_bias, ln_x, ln_dscale, ln_dbias, colsum)
+    hip.call("pcv_gemm_ln", ptr(a), ptr(b), ptr(out), M, N, K, _ld(a), _ld(b), _ld(out), int(ta), int(tb),
+             float(alpha), ptr(bias), ptr(res), _ld(res), float(drop_rate), ptr(seed), int(site) & 0xFFFFFFFF,
+             int(ln_mode), ptr(ln_scale), ptr(ln_bias), float(ln_eps), ptr(ln_y),
+             _ld(ln_y) if ln_y is not None else 0, ptr(ln_mean),
+             ptr(ln_rstd), ptr(ln_x), _ld(ln_x) if ln_x is not None else 0, ptr(ln_dscale), ptr(ln_dbias),
+             ptr(colsum), stream_ptr())
+    return out
+
+
 def _chk(cond, msg):
     if not cond:
         raise ValueError(msg)

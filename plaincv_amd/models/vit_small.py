@@ -192,11 +192,13 @@ class ViTRunner:
         self.dx = e(R, D)                              # top-of-stack residual gradient
         self.dym = [e(R, D, dt=bf) for _ in range(Lc)]
         self.dh = [e(R, M, dt=bf) for _ in range(Lc)]
-        self.dy_m = [e(R, D) for _ in range(Lc)]
+        # LayerNorm fused into the residual-stream GEMM epilogues (pcv_gemm_ln) when rows fit one tile
+        self.fuse_ln = bool(model.use_layernorm) and D <= 128 and D % 8 == 0
+        self.dy_m = [e(R, D) for _ in range(Lc)] if not self.fuse_ln else None
         self.dx_mid = [e(R, D) for _ in range(Lc)]
         self.dxb_mid = [e(R, D, dt=bf) for _ in range(Lc)]
         self.dqkv = [e(R, 3 * D, dt=bf) for _ in range(Lc)]
-        self.dy_a = [e(R, D) for _ in range(Lc)]
+        self.dy_a = [e(R, D) for _ in range(Lc)] if not self.fuse_ln else None
         self.dx_out = [e(R, D) for _ in range(Lc)]
         self.dxb_out = [e(R, D, dt=bf) for _ in range(Lc)]
         self.do = e(R, D, dt=bf)
@@ -267,25 +269,39 @@ class ViTRunner:
         if rate > 0.0:
             K.attn_drop_mask(seed, site_attn(0), T, rate, self.attn_mask, layers=m.num_layers,
                              site_stride=site_attn(1) - site_attn(0))
-        for i in range(m.num_layers):
+        L = m.num_layers
+        for i in range(L):
             w = self.w[i]
             x = self.xs[i]
-            if m.use_layernorm:
-                K.layernorm_fwd(x, w["s0"], w["c0"], self.y0[i], *self.st0[i])
-            else:
-                K.dropout_bwd_cast(x, self.y0[i])
+            if not self.fuse_ln:
+                if m.use_layernorm:
+                    K.layernorm_fwd(x, w["s0"], w["c0"], self.y0[i], *self.st0[i])
+                else:
+                    K.dropout_bwd_cast(x, self.y0[i])
+            elif i == 0:
+                K.layernorm_fwd(x, w["s0"], w["c0"], self.y0[0], *self.st0[0])
             K.gemm(self.y0[i], w["Wqkv"], self.qkv[i], bias=w["bqkv"])
             K.attn_fwd(self.qkv[i], self.o[i], self.lse[i], B, T, H, Dh, causal=False, drop_rate=rate,
                        mask=self._mask(i))
-            K.gemm(self.o[i], w["Wo"], self.x1s[i], bias=w["bo"], res=x)
-            if m.use_layernorm:
-                K.layernorm_fwd(self.x1s[i], w["s1"], w["c1"], self.y1[i], *self.st1[i])
+            if self.fuse_ln:   # out projection + residual + LayerNorm_1 in one launch
+                K.gemm_ln(self.o[i], w["Wo"], self.x1s[i], ln_mode=1, bias=w["bo"], res=x, ln_scale=w["s1"],
+                          ln_bias=w["c1"], ln_y=self.y1[i], ln_mean=self.st1[i][0], ln_rstd=self.st1[i][1])
             else:
-                K.dropout_bwd_cast(self.x1s[i], self.y1[i])
+                K.gemm(self.o[i], w["Wo"], self.x1s[i], bias=w["bo"], res=x)
+                if m.use_layernorm:
+                    K.layernorm_fwd(self.x1s[i], w["s1"], w["c1"], self.y1[i], *self.st1[i])
+                else:
+                    K.dropout_bwd_cast(self.x1s[i], self.y1[i])
             K.gemm(self.y1[i], w["W0"], self.a[i], bias=w["b0"], aux=self.h[i], act=K.EPI_GELU,
                    drop_rate=rate, seed=seed, site=site_mlp_hidden(i))
-            K.gemm(self.a[i], w["W1"], self.xs[i + 1], bias=w["b1"], res=self.x1s[i], drop_rate=rate, seed=seed,
-                   site=site_mlp_out(i))
+            if self.fuse_ln and i + 1 < L:   # MLP out + dropout + residual + next block's LayerNorm_0
+                wn = self.w[i + 1]
+                K.gemm_ln(self.a[i], w["W1"], self.xs[i + 1], ln_mode=1, bias=w["b1"], res=self.x1s[i],
+                          drop_rate=rate, seed=seed, site=site_mlp_out(i), ln_scale=wn["s0"], ln_bias=wn["c0"],
+                          ln_y=self.y0[i + 1], ln_mean=self.st0[i + 1][0], ln_rstd=self.st0[i + 1][1])
+            else:
+                K.gemm(self.a[i], w["W1"], self.xs[i + 1], bias=w["b1"], res=self.x1s[i], drop_rate=rate,
+                       seed=seed, site=site_mlp_out(i))
         xcls = self.xs[-1].view(B, T * D)[:, :D]   # cls rows (row stride T*D)
         if m.use_layernorm:
             K.layernorm_fwd(xcls, self.sf, self.cf, self.yf, *self.stf)
@@ -344,7 +360,11 @@ class ViTRunner:
             with self._fork():
                 K.colsum(dh, w["gb0"])
                 K.gemm(self.y1[i], dh, w["gW0"], ta=True, beta=1.0)
-            if m.use_layernorm:
+            if self.fuse_ln:   # dgrad + LayerNorm_1 backward + residual + its parameter and bias grads
+                K.gemm_ln(dh, w["W0"], dx_mid, tb=True, ln_mode=2, res=dx_in, ln_scale=w["s1"], ln_y=dxb_mid,
+                          ln_mean=self.st1[i][0], ln_rstd=self.st1[i][1], ln_x=self.x1s[i], ln_dscale=w["gs1"],
+                          ln_dbias=w["gc1"], colsum=w["gbo"])
+            elif m.use_layernorm:
                 K.gemm(dh, w["W0"], self.dy_m[i], tb=True)
                 K.layernorm_bwd(self.dy_m[i], self.x1s[i], w["s1"], *self.st1[i], dx_in, dx_mid, dxb_mid,
                                 None, None)
@@ -356,14 +376,19 @@ class ViTRunner:
             # attention: x1 = x + out(attn(qkv(ln0(x))))
             with self._fork():
                 K.gemm(self.o[i], dxb_mid, w["gWo"], ta=True, beta=1.0)
-                K.colsum(dx_mid, w["gbo"])
+                if not self.fuse_ln:
+                    K.colsum(dx_mid, w["gbo"])
             K.gemm(dxb_mid, w["Wo"], self.do, tb=True)
             K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
                        causal=False, drop_rate=rate, mask=self._mask(i))
             with self._fork():
                 K.gemm(self.y0[i], dqkv, w["gWqkv"], ta=True, beta=1.0)
                 K.colsum(dqkv, w["gbqkv"])
-            if m.use_layernorm:
+            if self.fuse_ln:
+                K.gemm_ln(dqkv, w["Wqkv"], dx_out, tb=True, ln_mode=2, res=dx_mid, ln_scale=w["s0"], ln_y=None,
+                          ln_mean=self.st0[i][0], ln_rstd=self.st0[i][1], ln_x=self.xs[i], ln_dscale=w["gs0"],
+                          ln_dbias=w["gc0"])
+            elif m.use_layernorm:
                 K.gemm(dqkv, w["Wqkv"], self.dy_a[i], tb=True)
                 K.layernorm_bwd(self.dy_a[i], self.xs[i], w["s0"], *self.st0[i], dx_mid, dx_out, dxb_out,
                                 None, None)

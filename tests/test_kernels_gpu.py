@@ -238,3 +238,61 @@ def test_muon_fused_matches_batched_chain(dev, shapes):
     for k in init:
         d = (ups[0][k] - ups[1][k]).abs().max().item()
         assert d <= 3 * 2e-2 * 1e-3, (k, d)
+
+
+@pytest.mark.parametrize("M,N,K,rate", [(1000, 128, 256, 0.0), (777, 128, 128, 0.1), (300, 96, 64, 0.0)])
+def test_gemm_ln_forward(dev, M, N, K, rate):
+    """pcv_gemm_ln mode 1 (GEMM + bias + dropout + residual, then LayerNorm of each row) vs fp32 torch."""
+    from oracle import rng
+    from plaincv_amd import kernels as K_
+    torch.manual_seed(3)
+    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    b = (torch.randn(K, N, device=dev) * 0.1).to(torch.bfloat16)
+    bias, res = torch.randn(N, device=dev), torch.randn(M, N, device=dev)
+    sc, sh = torch.rand(N, device=dev) + 0.5, torch.randn(N, device=dev)
+    out = torch.empty(M, N, device=dev)
+    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    mean, rstd = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    seed = torch.tensor([21], dtype=torch.int32, device=dev)
+    K_.gemm_ln(a, b, out, ln_mode=1, res=res, ln_scale=sc, ln_bias=sh, ln_y=y, ln_mean=mean, ln_rstd=rstd,
+               bias=bias, drop_rate=rate, seed=seed, site=9)
+    v = a.float() @ b.float() + bias
+    if rate > 0:
+        keep = torch.from_numpy(rng.keep_mask(21, 9, (M, N), rate)).to(dev)
+        v = torch.where(keep, v / (1 - rate), torch.zeros((), device=dev))
+    x1 = v + res
+    assert torch.allclose(out, x1, atol=2e-3, rtol=1e-3)
+    ref = torch.nn.functional.layer_norm(x1, (N,), sc, sh, eps=1e-6)
+    assert (y.float() - ref).abs().max().item() < 3e-2
+    assert torch.allclose(mean, x1.mean(-1), atol=1e-4)
+    assert torch.allclose(rstd, 1 / torch.sqrt(x1.var(-1, unbiased=False) + 1e-6), rtol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 128, 256), (513, 64, 128)])
+def test_gemm_ln_backward(dev, M, N, K):
+    """pcv_gemm_ln mode 2 (dgrad GEMM, LayerNorm backward, residual add, parameter grads, column sum)."""
+    from plaincv_amd import kernels as K_
+    torch.manual_seed(4)
+    dh = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) * 0.1).to(torch.bfloat16)     # dy = dh @ w^T  (tb=True)
+    x = torch.randn(M, N, device=dev) * 2 + 0.5
+    sc = torch.rand(N, device=dev) + 0.5
+    mean = x.mean(-1)
+    rstd = 1 / torch.sqrt(x.var(-1, unbiased=False) + 1e-6)
+    dres = torch.randn(M, N, device=dev)
+    dx = torch.empty(M, N, device=dev)
+    dxb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ds, db, cs = (torch.full((N,), 0.5, device=dev) for _ in range(3))
+    K_.gemm_ln(dh, w, dx, tb=True, ln_mode=2, res=dres, ln_scale=sc, ln_y=dxb, ln_mean=mean, ln_rstd=rstd,
+               ln_x=x, ln_dscale=ds, ln_dbias=db, colsum=cs)
+    dy = dh.float() @ w.float().t()
+    xr = x.clone().requires_grad_(True)
+    scr = sc.clone().requires_grad_(True)
+    shr = torch.zeros(N, device=dev, requires_grad=True)
+    torch.nn.functional.layer_norm(xr, (N,), scr, shr, eps=1e-6).backward(dy)
+    ref = xr.grad + dres
+    assert torch.allclose(dx, ref, atol=2e-3, rtol=2e-3), (dx - ref).abs().max().item()
+    assert (dxb.float() - ref).abs().max().item() < 3e-2
+    assert torch.allclose(ds - 0.5, scr.grad, atol=5e-2, rtol=2e-3)
+    assert torch.allclose(db - 0.5, shr.grad, atol=5e-2, rtol=2e-3)
+    assert torch.allclose(cs - 0.5, ref.sum(0), atol=5e-2, rtol=2e-3)
