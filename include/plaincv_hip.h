@@ -37,13 +37,14 @@ int pcv_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, i
                   float alpha, float beta, int out_f32,
                   const float* bias, const void* res, int64_t ldr, int64_t stride_r, int res_f32, float res_scale,
                   void* aux, int64_t ldaux, int act,
-                  float dropout_rate, const uint32_t* seed, uint32_t site, int split_k, void* stream);
+                  float dropout_rate, const uint32_t* seed, uint32_t site, float* colsum, int split_k, void* stream);
 
 /* GEMM + LayerNorm over each complete output row (N <= 128, N % 8 == 0; ViT residual stream).
  * ln_mode 1: C = x1 = alpha*op(A)op(B) + bias (+dropout) + res (fp32); ln_y = bf16 LN(x1),
  *            ln_mean / ln_rstd written (flax LayerNorm fwd, models/vit_small.py:38,52).
  * ln_mode 2: dy = alpha*op(A)op(B); C = dx = res + LN_bwd(dy; ln_x, ln_mean, ln_rstd, ln_scale);
- *            ln_y = bf16(dx); ln_dscale += sum dy*xhat, ln_dbias += sum dy, colsum += sum dx. */
+ *            y = dropout_bwd(dx) (site/seed/rate of the sublayer below; rate 0: y = dx):
+ *            ln_y = bf16(y) (optional), colsum += sum y; ln_dscale += sum dy*xhat, ln_dbias += sum dy. */
 int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, int trans_a, int trans_b, float alpha, const float* bias, const float* res, int64_t ldr,
                 float dropout_rate, const uint32_t* seed, uint32_t site, int ln_mode, const float* ln_scale,

@@ -40,7 +40,9 @@ struct GemmArgs {
   // Row-complete LayerNorm epilogues (pcv_gemm_ln; the 64x128 tile holds whole rows, N <= 128):
   //  ln_mode 1: C = x1 = alpha*acc + bias (+dropout) + res;  ln_y = LN(x1) (bf16), ln_mean/ln_rstd out
   //  ln_mode 2: dy = alpha*acc;  C = dx = res + LN_bwd(dy; ln_x, ln_mean, ln_rstd, ln_scale),
-  //             ln_y = bf16(dx); ln_dscale += sum dy*xhat, ln_dbias += sum dy, colsum += sum dx
+  //             y = dropout_bwd(dx) (or dx): ln_y = bf16(y), colsum += sum y;
+  //             ln_dscale += sum dy*xhat, ln_dbias += sum dy
+  //  (generic epilogue) colsum += column sums of the stored output
   int ln_mode;
   const float* ln_scale; const float* ln_bias; float ln_eps;
   bf16* ln_y; int64_t ld_lny;
@@ -223,7 +225,7 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0) {
     const f32x4 c1 = *reinterpret_cast<const f32x4*>(ct + rr * CLD + col + 4);
 #pragma unroll
     for (int e = 0; e < 4; ++e) { v[e] = g.alpha * c0[e] + bv[e]; v[e + 4] = g.alpha * c1[e] + bv[e + 4]; }
-    if (g.drop_thresh) {
+    if (g.drop_thresh && g.ln_mode == 1) {
       const uint32_t base = (uint32_t)(row * g.N + col);
 #pragma unroll
       for (int e = 0; e < 8; ++e)
@@ -282,16 +284,24 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0) {
       for (int o = 1; o < 16; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
       s1 *= invN;
       s2 *= invN;
-      float dx[8];
+      float dx[8], yv[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { dx[e] = rv[e] + rs * (gx[e] - s1 - xh[e] * s2); cs[e] += dx[e]; }
+      for (int e = 0; e < 8; ++e) { dx[e] = rv[e] + rs * (gx[e] - s1 - xh[e] * s2); yv[e] = dx[e]; }
+      if (g.drop_thresh) {   // ln_y / colsum carry the dropout backward of dx (the producer's dropout)
+        const uint32_t base = (uint32_t)(row * g.N + col);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          yv[e] = (hash3(seed, g.site, base + e) >= g.drop_thresh) ? yv[e] * g.drop_scale : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[e] += colok ? yv[e] : 0.f;
       if (colok) {
         *reinterpret_cast<f32x4*>(cp) = f32x4{dx[0], dx[1], dx[2], dx[3]};
         *reinterpret_cast<f32x4*>(cp + 4) = f32x4{dx[4], dx[5], dx[6], dx[7]};
         if (g.ln_y) {
           bf16x8 y;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) y[e] = f2bf(dx[e]);
+          for (int e = 0; e < 8; ++e) y[e] = f2bf(yv[e]);
           *reinterpret_cast<bf16x8*>(yp) = y;
         }
       }
@@ -486,6 +496,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   constexpr int RPP = 256 / CPR;         // rows per pass
   const int cc = threadIdx.x % CPR;
   const int64_t col = n0 + cc * 8;
+  float csum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) csum[e] = 0.f;
   if (col < g.N) {
     const bool vec = g.vec_ok && col + 8 <= g.N;
     float bv[8];
@@ -564,6 +577,10 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
           }
         }
       }
+      if (g.colsum) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[e] += (col + e < g.N) ? v[e] : 0.f;
+      }
       if (g.out_f32) {
         float* cp = (float*)Cb + row * g.ldc + col;
         if (g.split_k > 1) {
@@ -593,6 +610,20 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
           for (int e = 0; e < 8; ++e) if (col + e < g.N) cp[e] = f2bf(v[e]);
         }
       }
+    }
+  }
+  if (g.colsum) {
+    // column sums of this tile's rows: the RPP threads sharing a column chunk reduce through
+    // LDS (the staged tile is no longer read), then one atomic per column
+    __syncthreads();
+    float* red = ct;                       // [RPP][BN]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[(threadIdx.x / CPR) * BN + cc * 8 + e] = csum[e];
+    __syncthreads();
+    if (threadIdx.x < BN && n0 + threadIdx.x < g.N) {
+      float t = 0.f;
+      for (int q = 0; q < RPP; ++q) t += red[q * BN + threadIdx.x];
+      atomicAdd(g.colsum + n0 + threadIdx.x, t);
     }
   }
 }
@@ -639,8 +670,9 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
                              const float* bias, const void* res, int64_t ldr, int64_t stride_r, int res_f32, float res_scale,
                              void* aux, int64_t ldaux, int act,
                              float drop_rate, const uint32_t* seed, uint32_t site,
-                             int split_k, void* stream) {
+                             float* colsum, int split_k, void* stream) {
   if (M < 0 || N < 0 || K < 0 || batch < 1) return PCV_EINVAL;
+  if (colsum && (batch > 1 || split_k > 1)) return PCV_EINVAL;
   if (M == 0 || N == 0) return 0;
   if ((lda & 7) || (ldb & 7) || !pcv_aligned16(A) || !pcv_aligned16(B)) return PCV_EALIGN;
   if ((stride_a & 7) || (stride_b & 7)) return PCV_EALIGN;
@@ -653,6 +685,7 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
   g.alpha = alpha; g.beta = beta; g.out_f32 = out_f32;
   g.bias = bias; g.res = res; g.ldr = ldr; g.sR = stride_r; g.res_f32 = res_f32; g.res_scale = res_scale;
   g.aux = (bf16*)aux; g.ldaux = ldaux; g.act = act;
+  g.colsum = colsum;
   g.drop_thresh = 0; g.drop_scale = 1.f; g.seedp = seed; g.site = site;
   if (drop_rate > 0.f && !seed) return PCV_EINVAL;
   if (drop_rate > 0.f) {
@@ -688,9 +721,11 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
 // residual-stream GEMMs have N = hidden <= 128, so one 64 x 128 tile holds whole rows).
 // ln_mode 1 (forward): C = x1 = alpha*op(A).op(B) + bias (+dropout) + res  (fp32), and
 //   ln_y = bf16(LN(x1)*ln_scale + ln_bias), ln_mean/ln_rstd per row  -- replaces gemm + ln_fwd.
-// ln_mode 2 (backward): dy = alpha*op(A).op(B);  C = dx = res + LN_bwd(dy) (fp32),
-//   ln_y = bf16(dx), ln_dscale/ln_dbias/colsum accumulate (+=) over rows  -- replaces
-//   gemm + ln_bwd + the parameter-gradient and bias column-sum kernels.
+// ln_mode 2 (backward): dy = alpha*op(A).op(B);  C = dx = res + LN_bwd(dy) (fp32);
+//   ln_y = bf16(y), y = dropout_bwd(dx) with (seed, site, dropout_rate) or dx itself;
+//   ln_dscale/ln_dbias/colsum (+= column sums of y) accumulate over rows  -- replaces
+//   gemm + ln_bwd + the parameter-gradient kernel + the dropout-backward cast and the
+//   bias column sum of the sublayer below.
 extern "C" int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                            int64_t ldb, int64_t ldc, int trans_a, int trans_b, float alpha, const float* bias,
                            const float* res, int64_t ldr, float dropout_rate, const uint32_t* seed, uint32_t site,
@@ -700,7 +735,7 @@ extern "C" int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, in
   if (M < 0 || N <= 0 || K < 0 || N > 128 || (N & 7) || (ln_mode != 1 && ln_mode != 2)) return PCV_EINVAL;
   if (!res || !ln_scale || !ln_mean || !ln_rstd) return PCV_EINVAL;
   if (ln_mode == 1 && (!ln_bias || !ln_y)) return PCV_EINVAL;
-  if (ln_mode == 2 && (!ln_x || bias || dropout_rate > 0.f)) return PCV_EINVAL;
+  if (ln_mode == 2 && (!ln_x || bias)) return PCV_EINVAL;
   if (dropout_rate > 0.f && !seed) return PCV_EINVAL;
   if (M == 0) return 0;
   if ((lda & 7) || (ldb & 7) || !pcv_aligned16(A) || !pcv_aligned16(B)) return PCV_EALIGN;

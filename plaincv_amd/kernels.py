@@ -25,13 +25,14 @@ def _ld(t):
 
 
 def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=None, res_scale=1.0, aux=None,
-         act=EPI_NONE, drop_rate=0.0, seed=None, site=0, split_k=None):
+         act=EPI_NONE, drop_rate=0.0, seed=None, site=0, split_k=None, colsum=None):
     """out[M,N] = epi(alpha * op(a) @ op(b)).
 
     a: [M,K] (ta=False) or [K,M] (ta=True); b: [K,N] (tb=False) or [N,K] (tb=True).
     Optional leading batch dim on a, b, out (same batch size).  bf16 inputs,
     bf16 or fp32 output (fp32: out = v + beta*out).  Epilogue order:
-    +bias -> [gelu (aux<-preact) | *gelu'(aux)] -> dropout -> +res."""
+    +bias -> [gelu (aux<-preact) | *gelu'(aux)] -> dropout -> +res.  colsum (fp32 [N]) += column sums
+    of the stored values (not with split-K or batches)."""
     batched = a.dim() == 3
     if batched:
         nb = a.shape[0]
@@ -79,6 +80,9 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
         if aux is None or aux.dtype != BF16 or tuple(aux.shape[-2:]) != (M, N):
             raise ValueError("gelu epilogue needs bf16 aux [M,N]")
         ldaux = _ld(aux)
+    if colsum is not None:
+        _chk(not batched and colsum.dtype == F32 and colsum.numel() >= N and colsum.is_cuda, "gemm colsum")
+        split_k = 1
     if split_k is None:
         split_k = 1
         plain = out_f32 and beta == 1.0 and bias is None and res is None and act == EPI_NONE and drop_rate == 0.0
@@ -91,7 +95,7 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
     hip.call("pcv_gemm_bf16", ptr(a2), ptr(b2), ptr(o2), M, N, K, _ld(a2), _ld(b2), _ld(o2),
              int(ta), int(tb), nb, sa, sb, sc, float(alpha), float(beta), out_f32,
              ptr(bias), ptr(res), ldr, sr, res_f32, float(res_scale), ptr(aux), ldaux, int(act),
-             float(drop_rate), ptr(seed), int(site) & 0xFFFFFFFF, int(split_k), stream_ptr())
+             float(drop_rate), ptr(seed), int(site) & 0xFFFFFFFF, ptr(colsum), int(split_k), stream_ptr())
     return out
 
 

@@ -351,14 +351,18 @@ class ViTRunner:
             dym, dh, dqkv = self.dym[i], self.dh[i], self.dqkv[i]
             dx_mid, dxb_mid, dx_out, dxb_out = self.dx_mid[i], self.dxb_mid[i], self.dx_out[i], self.dxb_out[i]
             # MLP: x2 = x1 + drop(D1(drop(gelu(D0(ln1(x1))))))
-            K.dropout_bwd_cast(dx_in, dym, rate, seed, site_mlp_out(i))
-            with self._fork():
+            # (fused path: below the top block, dym and its bias column sum were produced by the
+            # LayerNorm_0 backward epilogue of the block above)
+            if not (self.fuse_ln and i + 1 < m.num_layers):
+                K.dropout_bwd_cast(dx_in, dym, rate, seed, site_mlp_out(i))
                 K.colsum(dym, w["gb1"])
+            with self._fork():
                 K.gemm(self.a[i], dym, w["gW1"], ta=True, beta=1.0)
             K.gemm(dym, w["W1"], dh, tb=True, aux=self.h[i], act=K.EPI_GELU_BWD, drop_rate=rate,
-                   seed=seed, site=site_mlp_hidden(i))
+                   seed=seed, site=site_mlp_hidden(i), colsum=w["gb0"] if self.side is None else None)
             with self._fork():
-                K.colsum(dh, w["gb0"])
+                if self.side is not None:
+                    K.colsum(dh, w["gb0"])
                 K.gemm(self.y1[i], dh, w["gW0"], ta=True, beta=1.0)
             if self.fuse_ln:   # dgrad + LayerNorm_1 backward + residual + its parameter and bias grads
                 K.gemm_ln(dh, w["W0"], dx_mid, tb=True, ln_mode=2, res=dx_in, ln_scale=w["s1"], ln_y=dxb_mid,
@@ -384,10 +388,13 @@ class ViTRunner:
             with self._fork():
                 K.gemm(self.y0[i], dqkv, w["gWqkv"], ta=True, beta=1.0)
                 K.colsum(dqkv, w["gbqkv"])
-            if self.fuse_ln:
-                K.gemm_ln(dqkv, w["Wqkv"], dx_out, tb=True, ln_mode=2, res=dx_mid, ln_scale=w["s0"], ln_y=None,
-                          ln_mean=self.st0[i][0], ln_rstd=self.st0[i][1], ln_x=self.xs[i], ln_dscale=w["gs0"],
-                          ln_dbias=w["gc0"])
+            if self.fuse_ln:   # + the dropout backward / bias column sum of the block below's MLP output
+                below = i > 0
+                K.gemm_ln(dqkv, w["Wqkv"], dx_out, tb=True, ln_mode=2, res=dx_mid, ln_scale=w["s0"],
+                          ln_y=self.dym[i - 1] if below else None, drop_rate=rate if below else 0.0, seed=seed,
+                          site=site_mlp_out(i - 1) if below else 0, ln_mean=self.st0[i][0],
+                          ln_rstd=self.st0[i][1], ln_x=self.xs[i], ln_dscale=w["gs0"], ln_dbias=w["gc0"],
+                          colsum=self.w[i - 1]["gb1"] if below else None)
             elif m.use_layernorm:
                 K.gemm(dqkv, w["Wqkv"], self.dy_a[i], tb=True)
                 K.layernorm_bwd(self.dy_a[i], self.xs[i], w["s0"], *self.st0[i], dx_mid, dx_out, dxb_out,

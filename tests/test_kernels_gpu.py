@@ -268,9 +268,11 @@ def test_gemm_ln_forward(dev, M, N, K, rate):
     assert torch.allclose(rstd, 1 / torch.sqrt(x1.var(-1, unbiased=False) + 1e-6), rtol=1e-3)
 
 
-@pytest.mark.parametrize("M,N,K", [(1000, 128, 256), (513, 64, 128)])
-def test_gemm_ln_backward(dev, M, N, K):
-    """pcv_gemm_ln mode 2 (dgrad GEMM, LayerNorm backward, residual add, parameter grads, column sum)."""
+@pytest.mark.parametrize("M,N,K,rate", [(1000, 128, 256, 0.0), (513, 64, 128, 0.0), (700, 128, 384, 0.1)])
+def test_gemm_ln_backward(dev, M, N, K, rate):
+    """pcv_gemm_ln mode 2 (dgrad GEMM, LayerNorm backward, residual add, parameter grads, and the
+    dropout-backward bf16 copy + column sum consumed by the sublayer below)."""
+    from oracle import rng
     from plaincv_amd import kernels as K_
     torch.manual_seed(4)
     dh = torch.randn(M, K, device=dev).to(torch.bfloat16)
@@ -283,8 +285,9 @@ def test_gemm_ln_backward(dev, M, N, K):
     dx = torch.empty(M, N, device=dev)
     dxb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     ds, db, cs = (torch.full((N,), 0.5, device=dev) for _ in range(3))
+    seed = torch.tensor([5], dtype=torch.int32, device=dev)
     K_.gemm_ln(dh, w, dx, tb=True, ln_mode=2, res=dres, ln_scale=sc, ln_y=dxb, ln_mean=mean, ln_rstd=rstd,
-               ln_x=x, ln_dscale=ds, ln_dbias=db, colsum=cs)
+               ln_x=x, ln_dscale=ds, ln_dbias=db, colsum=cs, drop_rate=rate, seed=seed, site=11)
     dy = dh.float() @ w.float().t()
     xr = x.clone().requires_grad_(True)
     scr = sc.clone().requires_grad_(True)
@@ -292,7 +295,30 @@ def test_gemm_ln_backward(dev, M, N, K):
     torch.nn.functional.layer_norm(xr, (N,), scr, shr, eps=1e-6).backward(dy)
     ref = xr.grad + dres
     assert torch.allclose(dx, ref, atol=2e-3, rtol=2e-3), (dx - ref).abs().max().item()
-    assert (dxb.float() - ref).abs().max().item() < 3e-2
+    yref = ref
+    if rate > 0:
+        keep = torch.from_numpy(rng.keep_mask(5, 11, (M, N), rate)).to(dev)
+        yref = torch.where(keep, ref / (1 - rate), torch.zeros((), device=dev))
+    assert (dxb.float() - yref).abs().max().item() < 3e-2
     assert torch.allclose(ds - 0.5, scr.grad, atol=5e-2, rtol=2e-3)
     assert torch.allclose(db - 0.5, shr.grad, atol=5e-2, rtol=2e-3)
-    assert torch.allclose(cs - 0.5, ref.sum(0), atol=5e-2, rtol=2e-3)
+    assert torch.allclose(cs - 0.5, yref.sum(0), atol=5e-2, rtol=2e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 256, 128), (777, 200, 64)])
+def test_gemm_colsum_epilogue(dev, M, N, K):
+    """Generic GEMM epilogue column sum (bias gradient of the layer that produced the output)."""
+    from plaincv_amd import kernels as K_
+    torch.manual_seed(6)
+    a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev) * 0.1).to(torch.bfloat16)
+    aux = torch.randn(M, N, device=dev).to(torch.bfloat16)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    cs = torch.ones(N, device=dev)
+    K_.gemm(a, w, out, tb=True, aux=aux, act=K_.EPI_GELU_BWD, colsum=cs)
+    xa = aux.float().requires_grad_(True)
+    gl = torch.nn.functional.gelu(xa, approximate="tanh")
+    (gd,) = torch.autograd.grad(gl, xa, torch.ones_like(gl))
+    ref = (a.float() @ w.float().t()) * gd
+    assert (out.float() - ref).abs().max().item() < 5e-2
+    assert torch.allclose(cs - 1.0, ref.sum(0), atol=5e-2, rtol=1e-2)
