@@ -11,8 +11,8 @@ With N>1 each rank runs the same per-GPU batch (weak scaling) and gradients
 are averaged over RCCL once per step.  ``value`` = images/s over all ranks.
 
 Also reported: the roofline of the dominant kernel (timed live with HIP
-events on its own stream, algorithmic FLOPs per launch) and the CPU baseline
-(the oracle/ restatement timed on this host's cores on a bounded sample).
+events on its own stream, algorithmic bytes or FLOPs per launch) and the CPU
+baseline (the oracle/ restatement timed on this host's cores on a bounded sample).
 """
 import argparse
 import json
@@ -66,22 +66,51 @@ def timed_kernel(fn, iters=50):
     return e0.elapsed_time(e1) / iters * 1e-3
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/r*_pmc_traffic.json, FETCH_SIZE/WRITE_SIZE passes made by tools/gpu_full.sh)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k.get("mean_hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def vit_roofline(state, image_shape):
-    """Dominant kernel of the ViT step (rocprof: the per-layer MLP/QKV GEMMs and
-    flash attention); we time the largest-FLOP GEMM (MLP Dense_0 forward,
-    [B*T,128]x[128,256] + bias + GELU + dropout epilogue) live."""
+    """Dominant kernel of the ViT step by rocprof time: gemm_bf16_kernel<true,true,2,4>, the
+    dgrad GEMM + LayerNorm-backward epilogue (pcv_gemm_ln mode 2), launched twice per layer
+    (MLP Dense_0 dgrad -> LN_1 bwd; QKV dgrad -> LN_0 bwd).  It is HBM-bound (arithmetic
+    intensity ~10 flop/B), so the roofline is algorithmic bytes per launch / launch time,
+    both launch shapes of layer 1 timed live with HIP events on their stream."""
     from plaincv_amd import kernels as K
     r = state.runner_for(image_shape)
-    w = r.w[0]
-    fn = lambda: K.gemm(r.y1[0], w["W0"], r.a[0], bias=w["b0"], aux=r.h[0], act=K.EPI_GELU,  # noqa: E731
-                        drop_rate=r.m.dropout_rate, seed=r.seed, site=17)
-    dt = timed_kernel(fn)
-    flops = 2.0 * r.R * r.D * r.M
-    achieved = flops / dt / 1e12
-    return {"kernel": "gemm_bf16_kernel (MLP Dense_0 fwd, M=%d N=%d K=%d)" % (r.R, r.M, r.D), "bound": "mfma",
-            "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None, "launch_us": round(dt * 1e6, 2),
-            "flops_per_launch": flops}
+    i = 1
+    w, wb = r.w[i], r.w[i - 1]
+    R, D, M = r.R, r.D, r.M
+    f_mlp = lambda: K.gemm_ln(r.dh[i], w["W0"], r.dx_mid[i], tb=True, ln_mode=2, res=r.dx_out[i],  # noqa: E731
+                              ln_scale=w["s1"], ln_y=r.dxb_mid[i], ln_mean=r.st1[i][0], ln_rstd=r.st1[i][1],
+                              ln_x=r.x1s[i], ln_dscale=w["gs1"], ln_dbias=w["gc1"], colsum=w["gbo"])
+    f_qkv = lambda: K.gemm_ln(r.dqkv[i], w["Wqkv"], r.dx_out[i], tb=True, ln_mode=2, res=r.dx_mid[i],  # noqa: E731
+                              ln_scale=w["s0"], ln_y=r.dym[i - 1], drop_rate=r.m.dropout_rate, seed=r.seed,
+                              site=16 + 4 * (i - 1) + 2, ln_mean=r.st0[i][0], ln_rstd=r.st0[i][1], ln_x=r.xs[i],
+                              ln_dscale=w["gs0"], ln_dbias=w["gc0"], colsum=wb["gb1"])
+    t1, t2 = timed_kernel(f_mlp), timed_kernel(f_qkv)
+    # algorithmic bytes: A + W (bf16) + residual, LN input, dx out (fp32) + row stats + bf16 copy
+    rows = R * D * 4 * 3 + R * 8 + R * D * 2
+    b1 = R * M * 2 + D * M * 2 + rows
+    b2 = R * 3 * D * 2 + D * 3 * D * 2 + rows
+    achieved = (b1 + b2) / (t1 + t2) / 1e9
+    traffic, tsrc = pmc_traffic("gemm_bf16_kernel<true,true,2,4>")   # mean HBM bytes per launch (PMC)
+    return {"kernel": "gemm_bf16_kernel<true,true,2,4> = pcv_gemm_ln mode 2 (dgrad GEMM + LayerNorm backward "
+                      f"epilogue; MLP M={R} N={D} K={M} and QKV M={R} N={D} K={3 * D})", "bound": "hbm",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+            "launch_us": round((t1 + t2) / 2 * 1e6, 2), "launch_us_by_shape": [round(t1 * 1e6, 2), round(t2 * 1e6, 2)],
+            "bytes_per_launch": [b1, b2]}
 
 
 def cpu_baseline_vit(cfg, seconds=12.0):
@@ -233,7 +262,23 @@ def bench_lm(args):
                        "parallelism": f"dp{world}"},
             "steps_per_sec": round(args.steps / dt, 4),
             "tflops_per_gpu": round(tokens / world / dt * fpt / 1e12, 2),
-            "roofline": None, "cpu_baseline": None}
+            "roofline": lm_roofline(st), "cpu_baseline": None}
+
+
+def lm_roofline(st):
+    """Largest MFMA-bound kernel of the LM step: the lm_head GEMM (logits = y . W_head,
+    M = micro_batch*T, N = vocab, K = d_model), timed live with HIP events."""
+    from plaincv_amd import kernels as K
+    r = st.runner
+    M, Kd = r.yf.shape
+    N = r.logits.shape[1]
+    dt = timed_kernel(lambda: K.gemm(r.yf, r.Wh, r.logits), iters=10)
+    flops = 2.0 * M * N * Kd
+    achieved = flops / dt / 1e12
+    return {"kernel": f"gemm_bf16_kernel<true,false,4,4> (lm_head fwd, M={M} N={N} K={Kd})", "bound": "mfma",
+            "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None, "launch_us": round(dt * 1e6, 2),
+            "flops_per_launch": flops}
 
 
 def main():

@@ -198,8 +198,37 @@ __device__ __forceinline__ void mc_glds(char* lds, const bf16* base, int64_t ld,
 // stride 132).  16 consecutive lanes own one row (8 columns each), so the row
 // statistics are 4 xor-shuffles; per-column parameter gradients and column sums are
 // reduced over the workgroup's rows and added with one atomic per column.
+// Row operands of the LN epilogue (residual, LN input, row statistics) for this thread's
+// BM/16 rows, loaded before the GEMM main loop so their latency hides behind it.
 template <int BM>
-__device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0) {
+struct LnPre {
+  f32x4 r[BM / 16][2], x[BM / 16][2];
+  float mean[BM / 16], rstd[BM / 16];
+};
+template <int BM>
+__device__ __forceinline__ void ln_prefetch(const GemmArgs& g, int64_t m0, LnPre<BM>& p) {
+  const int tid = threadIdx.x, col = (tid & 15) * 8;
+  const bool colok = col < g.N;
+#pragma unroll
+  for (int q = 0; q < BM / 16; ++q) {
+    const int64_t row = m0 + (tid >> 4) + 16 * q;
+    const bool ok = row < g.M && colok;
+    const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* rp = (const float*)g.res + row * g.ldr + col;
+    p.r[q][0] = ok ? *reinterpret_cast<const f32x4*>(rp) : z;
+    p.r[q][1] = ok ? *reinterpret_cast<const f32x4*>(rp + 4) : z;
+    if (g.ln_mode == 2) {
+      const float* xp = g.ln_x + row * g.ld_lnx + col;
+      p.x[q][0] = ok ? *reinterpret_cast<const f32x4*>(xp) : z;
+      p.x[q][1] = ok ? *reinterpret_cast<const f32x4*>(xp + 4) : z;
+      p.mean[q] = row < g.M ? g.ln_mean[row] : 0.f;
+      p.rstd[q] = row < g.M ? g.ln_rstd[row] : 0.f;
+    }
+  }
+}
+
+template <int BM>
+__device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, const LnPre<BM>& pre) {
   constexpr int CLD = 128 + 4;
   const int tid = threadIdx.x, cc = tid & 15, wave = tid >> 6, lane = tid & 63;
   const int col = cc * 8;
@@ -217,7 +246,9 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0) {
     }
   }
   const uint32_t seed = g.drop_thresh ? *g.seedp : 0u;
-  for (int rr = tid >> 4; rr < BM; rr += 16) {
+#pragma unroll
+  for (int q = 0; q < BM / 16; ++q) {
+    const int rr = (tid >> 4) + 16 * q;
     const int64_t row = m0 + rr;
     if (row >= g.M) break;                // uniform over the row's 16 lanes
     float v[8];
@@ -232,14 +263,11 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0) {
         v[e] = (hash3(seed, g.site, base + e) >= g.drop_thresh) ? v[e] * g.drop_scale : 0.f;
     }
     float rv[8];
-    if (colok) {
-      const float* rp = (const float*)g.res + row * g.ldr + col;
-      const f32x4 r0 = *reinterpret_cast<const f32x4*>(rp), r1 = *reinterpret_cast<const f32x4*>(rp + 4);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { rv[e] = r0[e]; rv[e + 4] = r1[e]; }
-    } else {
+    for (int e = 0; e < 4; ++e) { rv[e] = pre.r[q][0][e]; rv[e + 4] = pre.r[q][1][e]; }
+    if (!colok) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { rv[e] = 0.f; v[e] = 0.f; }
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
     }
     float* cp = (float*)g.C + row * g.ldc + col;
     bf16* yp = g.ln_y ? g.ln_y + row * g.ld_lny + col : nullptr;
@@ -261,16 +289,12 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0) {
       }
       if (cc == 0) { g.ln_mean[row] = mean; g.ln_rstd[row] = rs; }
     } else {
-      const float mean = g.ln_mean[row], rs = g.ln_rstd[row];
+      const float mean = pre.mean[q], rs = pre.rstd[q];
       float xh[8], gx[8], s1 = 0.f, s2 = 0.f;
-      if (colok) {
-        const float* xp = g.ln_x + row * g.ld_lnx + col;
-        const f32x4 x0 = *reinterpret_cast<const f32x4*>(xp), x1 = *reinterpret_cast<const f32x4*>(xp + 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { xh[e] = (x0[e] - mean) * rs; xh[e + 4] = (x1[e] - mean) * rs; }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) xh[e] = 0.f;
+      for (int e = 0; e < 4; ++e) {     // zero-filled for columns >= N (prefetch)
+        xh[e] = colok ? (pre.x[q][0][e] - mean) * rs : 0.f;
+        xh[e + 4] = colok ? (pre.x[q][1][e] - mean) * rs : 0.f;
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -339,8 +363,13 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0) {
 #ifndef PCV_GEMM_STAGES_SMALL
 #define PCV_GEMM_STAGES_SMALL 2
 #endif
+#ifndef PCV_GEMM_STAGES_LN
+#define PCV_GEMM_STAGES_LN 2
+#endif
 template <int WM, int WN>
-struct GemmStages { static constexpr int S = WM * WN <= 4 ? PCV_GEMM_STAGES_SMALL : 2; };
+struct GemmStages {
+  static constexpr int S = (WM == 2 && WN == 4) ? PCV_GEMM_STAGES_LN : (WM * WN <= 4 ? PCV_GEMM_STAGES_SMALL : 2);
+};
 
 template <bool A_KC, bool B_KC, int WM, int WN>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
@@ -384,6 +413,13 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   for (int i = 0; i < WM; ++i)
 #pragma unroll
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // the 64 x 128 tile (pcv_gemm_ln) prefetches its LN row operands before the main loop
+  constexpr bool LN_TILE = BM == 64 && BN == 128;
+  LnPre<LN_TILE ? BM : 16> lnpre;
+  if constexpr (LN_TILE) {
+    if (g.ln_mode) ln_prefetch<BM>(g, m0, lnpre);
+  }
 
   u32x4 stA[BM * 8 / 256], stB[BN * 8 / 256];
   auto gload = [&](int64_t k0) {
@@ -489,8 +525,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     }
     return;
   }
-  if constexpr (BN == 128) {
-    if (g.ln_mode) { ln_epilogue<BM>(g, ct, m0); return; }
+  if constexpr (LN_TILE) {
+    if (g.ln_mode) { ln_epilogue<BM>(g, ct, m0, lnpre); return; }
   }
   constexpr int CPR = BN / 8;            // 8-column chunks per row
   constexpr int RPP = 256 / CPR;         // rows per pass
@@ -635,7 +671,7 @@ static hipError_t launch_t(const GemmArgs& a, int batch, hipStream_t s) {
   g.tiles_m = (int)((g.M + BM - 1) / BM);
   g.tiles_n = (int)((g.N + BN - 1) / BN);
   const size_t stage = GemmStages<WM, WN>::S * (size_t)(BM + BN) * 64 * 2;
-  const size_t ctile = (size_t)BM * (BN + 4) * 4 + (BN == 128 ? 3 * 4 * 128 * 4 : 0);   // + LN reductions
+  const size_t ctile = (size_t)BM * (BN + 4) * 4 + (BM == 64 && BN == 128 ? 3 * 4 * 128 * 4 : 0);   // + LN reductions
   const size_t lds = stage > ctile ? stage : ctile;
   dim3 grid(g.tiles_m * g.tiles_n, batch, g.split_k > 1 ? g.split_k : 1);
   static bool attr = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel

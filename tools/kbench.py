@@ -53,6 +53,18 @@ CASES = {
     "dW_fc2    256 x 128 x R": lambda: K.gemm(a, y0, gW1, ta=True, beta=1.0),
     "dW_qkv    128 x 384 x R": lambda: K.gemm(y0, qkv, gWqkv, ta=True, beta=1.0),
     "colsum    R x 256 bf16": lambda: K.colsum(dh, gb),
+    "lnfwd_proj R x 128 x 128 +res+LN": lambda: K.gemm_ln(o, Wo, out_f, ln_mode=1, bias=b1, res=x32, ln_scale=sc,
+                                                          ln_bias=bi, ln_y=y0, ln_mean=mean, ln_rstd=rstd),
+    "lnfwd_fc2 R x 128 x 256 +drop+res+LN": lambda: K.gemm_ln(a, W1, out_f, ln_mode=1, bias=b1, res=x32,
+                                                              drop_rate=0.1, seed=seed, site=4, ln_scale=sc,
+                                                              ln_bias=bi, ln_y=y0, ln_mean=mean, ln_rstd=rstd),
+    "lnbwd_fc1 R x 128 x 256 LNbwd": lambda: K.gemm_ln(dh, W0, dx, tb=True, ln_mode=2, res=out_f, ln_scale=sc,
+                                                        ln_y=dxb, ln_mean=mean, ln_rstd=rstd, ln_x=x32,
+                                                        ln_dscale=gs, ln_dbias=gc, colsum=b1),
+    "lnbwd_qkv R x 128 x 384 LNbwd+drop": lambda: K.gemm_ln(qkv, Wqkv, dx, tb=True, ln_mode=2, res=out_f,
+                                                             ln_scale=sc, ln_y=dxb, ln_mean=mean, ln_rstd=rstd,
+                                                             ln_x=x32, ln_dscale=gs, ln_dbias=gc, colsum=b1,
+                                                             drop_rate=0.1, seed=seed, site=5),
     **{f"dWsplit{sk:<3d} 128 x 256 x R": (lambda sk=sk: K.gemm(y0, dh, gW0, ta=True, beta=1.0, split_k=sk))
        for sk in (4, 8, 16, 32, 64, 128)},
     "ln_fwd    R x 128": lambda: K.layernorm_fwd(x32, sc, bi, y0, mean, rstd),
