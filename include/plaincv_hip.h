@@ -155,6 +155,11 @@ int pcv_muon_prep(const void* mats, int nmats, int nnorm, int64_t max_elems, flo
 int pcv_muon_apply(const void* mats, int nmats, int64_t max_elems, float lr, float wd, int shape_scale,
                    int apply, void* stream);
 int pcv_muon_mat_size(void);
+/* Batched bf16 transpose (64x64 tiles, many matrices per launch): records
+ * {src, dst, rows, cols, ld_src, ld_dst, first_tile} (pcv_transpose_rec_size() bytes),
+ * dst[c][r] = src[r][c].  Keeps K-contiguous copies of the forward-GEMM weights. */
+int pcv_transpose_bf16_batch(const void* recs, int nrec, int64_t total_tiles, void* stream);
+int pcv_transpose_rec_size(void);
 /* Newton-Schulz of matrices whose NS operand is at most 128 x 256, entirely in one
  * workgroup's LDS (csrc/muon_fused.hip): reads each record's x32 (un-normalised, from
  * pcv_muon_prep) and norm2, writes xo.  pcv_muon_fused_ok(rows, cols) says which shapes qualify. */

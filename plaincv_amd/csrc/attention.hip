@@ -55,18 +55,20 @@ __host__ __device__ __forceinline__ int64_t drop_words(int T) {
 
 // LDS tile images are unpadded [rows][DH] with the 16-B chunks of row r XOR-permuted
 // by tswz(r) (a function of r mod 16).  The masks were found by exhaustive search
-// over XOR-linear maps so that all three access shapes are bank-conflict-free:
-// row fragments (ds_read_b128, 16 rows x one chunk), transposing fragments
-// (ds_read_b64_tr_b16, 8 rows x 32 B) and the tile stores (ds_write_b128).
+// over XOR-linear maps, against the gfx950 LDS lane groups of each instruction
+// (MI355X_MICROARCH.md LDS table), so that all three access shapes are
+// bank-conflict-free: row fragments (ds_read_b128), transposing fragments
+// (ds_read_b64_tr_b16, two 32-lane groups) and the tile stores (ds_write_b128,
+// 8-lane groups over 32 banks).
 template <int DH>
 struct Tile {
   static constexpr int LD = DH;
 };
 template <int DH>
 __device__ __forceinline__ int tswz(int r) {
-  if constexpr (DH == 32) return (((r >> 2) & 1) << 1) ^ ((r >> 3) & 1);
-  else if constexpr (DH == 64) return (((r >> 1) & 1) << 1) ^ (((r >> 2) & 1) << 2) ^ ((r >> 3) & 1);
-  else return ((r & 1) << 1) ^ (((r >> 1) & 1) << 2) ^ (((r >> 2) & 1) << 3) ^ ((r >> 3) & 1);
+  if constexpr (DH == 32) return ((r >> 2) & 1) << 1;
+  else if constexpr (DH == 64) return (((r >> 1) & 1) << 1) ^ (((r >> 2) & 1) << 2);
+  else return ((r & 1) << 1) ^ (((r >> 1) & 1) << 2) ^ (((r >> 2) & 1) << 3);
 }
 // element offset of 16-B chunk `c` of row `r`
 template <int DH>

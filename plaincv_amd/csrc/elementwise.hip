@@ -331,3 +331,55 @@ extern "C" int pcv_seed_next(uint32_t* seed, void* stream) {
   hipLaunchKernelGGL(seed_next_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, seed);
   return pcv_launch_status();
 }
+
+// ------------------------------------------------------- batched transpose
+// Row-major bf16 matrices src [rows][lds] -> dst [cols][ldd], one 64x64 tile per workgroup,
+// many matrices per launch (record table with prefix tile counts).  Keeps a K-contiguous
+// copy of each forward-GEMM weight (Flax kernels are [in][out] = [K][N]) so the forward
+// GEMMs read both operands with plain ds_read_b128 instead of the transposing path.
+namespace pcv {
+struct TrRec {
+  const bf16* src; bf16* dst;
+  int64_t rows, cols, lds, ldd, tile0;
+};
+
+__global__ __launch_bounds__(256) void transpose_batch_kernel(const TrRec* recs, int n) {
+  __shared__ bf16 t[64][66];
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {                      // last record with tile0 <= blockIdx.x
+    const int mid = (lo + hi + 1) >> 1;
+    if (recs[mid].tile0 <= (int64_t)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const TrRec R = recs[lo];
+  const int64_t tile = (int64_t)blockIdx.x - R.tile0;
+  const int64_t tcs = (R.cols + 63) / 64;
+  const int64_t r0 = (tile / tcs) * 64, c0 = (tile % tcs) * 64;
+  const int tid = threadIdx.x, lr = tid >> 2, lc = (tid & 3) * 16;
+  {
+    const int64_t r = r0 + lr;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int64_t c = c0 + lc + j;
+      t[lr][lc + j] = (r < R.rows && c < R.cols) ? R.src[r * R.lds + c] : (bf16)0.f;
+    }
+  }
+  __syncthreads();
+  const int64_t dr = c0 + lr;            // destination row = source column
+  if (dr < R.cols) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int64_t dc = r0 + lc + j;    // destination column = source row
+      if (dc < R.rows) R.dst[dr * R.ldd + dc] = t[lc + j][lr];
+    }
+  }
+}
+}  // namespace pcv
+
+extern "C" int pcv_transpose_bf16_batch(const void* recs, int nrec, int64_t total_tiles, void* stream) {
+  if (nrec <= 0 || total_tiles <= 0) return PCV_EINVAL;
+  hipLaunchKernelGGL(pcv::transpose_batch_kernel, dim3((unsigned)total_tiles), dim3(256), 0, (hipStream_t)stream,
+                     (const pcv::TrRec*)recs, nrec);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_transpose_rec_size(void) { return (int)sizeof(pcv::TrRec); }

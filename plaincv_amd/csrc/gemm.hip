@@ -366,9 +366,13 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
 #ifndef PCV_GEMM_STAGES_LN
 #define PCV_GEMM_STAGES_LN 2
 #endif
+#ifndef PCV_GEMM_STAGES_BIG
+#define PCV_GEMM_STAGES_BIG 2
+#endif
 template <int WM, int WN>
 struct GemmStages {
-  static constexpr int S = (WM == 2 && WN == 4) ? PCV_GEMM_STAGES_LN : (WM * WN <= 4 ? PCV_GEMM_STAGES_SMALL : 2);
+  static constexpr int S =
+      (WM == 2 && WN == 4) ? PCV_GEMM_STAGES_LN : (WM * WN <= 4 ? PCV_GEMM_STAGES_SMALL : PCV_GEMM_STAGES_BIG);
 };
 
 template <bool A_KC, bool B_KC, int WM, int WN>

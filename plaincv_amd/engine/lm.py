@@ -84,6 +84,7 @@ def make_apply_grads_fn(grad_clip=None):
             K.grad_scale(store.grad_flat, state.chunks, state.partial, 1.0, grad_clip if grad_clip else 0.0,
                          state.gscale, state.gnorm)
         state.tx.step_(store, state.opt_state, gscale=state.gscale if grad_clip else None)
+        store.version += 1
         store.zero_grad()
         state.step += 1
         return state, state.gnorm

@@ -56,6 +56,8 @@ SIGNATURES = {
     "pcv_muon_apply": [P, I32, I64, F32, F32, I32, I32, P],
     "pcv_muon_ns_fused": [P, I32, F32, F32, F32, F32, I32, P],
     "pcv_muon_fused_ok": [I64, I64],
+    "pcv_transpose_bf16_batch": [P, I32, I64, P],
+    "pcv_transpose_rec_size": [],
     "pcv_muon_mat_size": [],
     "pcv_chunk_size": [],
 }

@@ -127,6 +127,25 @@ def gemm_ln(a, b, out, *, ln_mode, res, ln_scale, ln_y, ln_mean, ln_rstd, ta=Fal
     return out
 
 
+class TransposeBatch:
+    """dst[c][r] = src[r][c] for a fixed list of (src, dst) bf16 2-D views, one launch."""
+
+    def __init__(self, pairs, device):
+        import numpy as np
+        recs, tiles = [], 0
+        for src, dst in pairs:
+            rows, cols = src.shape
+            _chk(src.dtype == BF16 and dst.dtype == BF16 and tuple(dst.shape) == (cols, rows), "transpose pair")
+            recs.append([src.data_ptr(), dst.data_ptr(), rows, cols, _ld(src), _ld(dst), tiles])
+            tiles += math.ceil(rows / 64) * math.ceil(cols / 64)
+        _chk(hip.load().pcv_transpose_rec_size() == 56, "transpose record size")
+        self.n, self.tiles = len(recs), tiles
+        self.table = torch.tensor(np.array(recs, dtype=np.uint64).view(np.int64), device=device)
+
+    def __call__(self):
+        hip.call("pcv_transpose_bf16_batch", ptr(self.table), self.n, self.tiles, stream_ptr())
+
+
 def _chk(cond, msg):
     if not cond:
         raise ValueError(msg)

@@ -172,6 +172,7 @@ class LMRunner:
         self.sin = sin[:T].contiguous().to(dev)
         self.grad_scale = 1.0 / R if grad_scale is None else grad_scale
         self._views()
+        self._transposed_weights(dev)
 
     def _views(self):
         s, c = self.s, self.c
@@ -193,6 +194,33 @@ class LMRunner:
         if not c.tie_embeddings:
             self.Wh, self.gWh = W["lm_head/kernel"], G["lm_head/kernel"]
 
+    def _transposed_weights(self, dev):
+        """K-contiguous ([out][in]) bf16 copies of the forward-GEMM weights, so every forward
+        GEMM reads both operands with ds_read_b128 (the [in][out] Flax layout needs the
+        transposing LDS path, measured ~25 % slower at these shapes).  Refreshed from the
+        bf16 shadow by one batched transpose launch whenever the store's version changes."""
+        def t(rows, cols):
+            ld = (cols + 7) // 8 * 8
+            return torch.zeros(rows, ld, dtype=torch.bfloat16, device=dev)[:, :cols]
+        pairs = []
+        for w in self.w:
+            for k in ("Wqkv", "Wo", "Wgu", "W2"):
+                src = w[k]
+                dst = t(src.shape[1], src.shape[0])
+                w[k + "T"] = dst
+                pairs.append((src, dst))
+        self.WhT = None
+        if not self.c.tie_embeddings:
+            self.WhT = t(self.Wh.shape[1], self.Wh.shape[0])
+            pairs.append((self.Wh, self.WhT))
+        self._tr = K.TransposeBatch(pairs, dev)
+        self._wt_version = -1
+
+    def _refresh_weights(self):
+        if self._wt_version != self.s.version:
+            self._tr()
+            self._wt_version = self.s.version
+
     def set_batch(self, input_ids):
         """input_ids (b, T+1) int on the GPU -> inputs/labels (train_lm.py:141-142)."""
         b, T = self.b, self.T
@@ -205,23 +233,24 @@ class LMRunner:
         c = self.c
         b, T, d, H, Dh = self.b, self.T, self.d, self.H, self.Dh
         eps = c.rmsnorm_eps
+        self._refresh_weights()
         K.embed_fwd(self.inputs, self.Wemb, self.x[0])
         for i in range(c.n_layers):
             w = self.w[i]
             K.rmsnorm_fwd(self.x[i], w["s0"], self.y0[i], self.r0[i], eps)
-            K.gemm(self.y0[i], w["Wqkv"], self.qkv[i])
+            K.gemm(self.y0[i], w["WqkvT"], self.qkv[i], tb=True)
             K.rope(self.qkv[i], T, Dh, self.cos, self.sin, ncols=2 * d)
             K.attn_fwd(self.qkv[i], self.o[i], self.lse[i], b, T, H, Dh, causal=True)
-            K.gemm(self.o[i], w["Wo"], self.x1[i], res=self.x[i])
+            K.gemm(self.o[i], w["WoT"], self.x1[i], tb=True, res=self.x[i])
             K.rmsnorm_fwd(self.x1[i], w["s1"], self.y1[i], self.r1[i], eps)
-            K.gemm(self.y1[i], w["Wgu"], self.gu[i])
+            K.gemm(self.y1[i], w["WguT"], self.gu[i], tb=True)
             K.swiglu_fwd(self.gu[i], self.hm[i], F=self.F)
-            K.gemm(self.hm[i], w["W2"], self.x[i + 1], res=self.x1[i])
+            K.gemm(self.hm[i], w["W2T"], self.x[i + 1], tb=True, res=self.x1[i])
         K.rmsnorm_fwd(self.x[-1], self.sf, self.yf, self.rf, eps)
         if c.tie_embeddings:
             K.gemm(self.yf, self.Wemb, self.logits, tb=True)
         else:
-            K.gemm(self.yf, self.Wh, self.logits)
+            K.gemm(self.yf, self.WhT, self.logits, tb=True)
         K.xent(self.logits, self.labels, self.row_loss, self.row_correct,
                self.logits if need_grad else None, grad_scale=self.grad_scale)
         K.mean2(self.row_loss, self.row_correct, self.R, 1.0 / self.R, self.metrics)

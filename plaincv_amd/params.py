@@ -123,6 +123,9 @@ class ParamStore:
         self.grads = OrderedDict((k, self._view(self.grad_flat, l)) for k, l in layout.leaves.items()) \
             if with_grads else None
         self.bf16 = OrderedDict((k, self._view(self.shadow, l)) for k, l in layout.leaves.items())
+        # bumped whenever the bf16 shadow changes (load, optimizer step), so derived
+        # copies (e.g. the LM runner's transposed forward weights) know to refresh
+        self.version = 0
 
     @staticmethod
     def _view(buf, leaf):
@@ -146,6 +149,7 @@ class ParamStore:
     def sync_shadow(self):
         from . import kernels
         kernels.cast_f32_bf16(self.flat, self.shadow)
+        self.version += 1
 
     def to_dict(self):
         return OrderedDict((k, v.detach().clone().cpu()) for k, v in self.params.items())

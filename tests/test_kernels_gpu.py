@@ -322,3 +322,19 @@ def test_gemm_colsum_epilogue(dev, M, N, K):
     ref = (a.float() @ w.float().t()) * gd
     assert (out.float() - ref).abs().max().item() < 5e-2
     assert torch.allclose(cs - 1.0, ref.sum(0), atol=5e-2, rtol=1e-2)
+
+
+def test_transpose_batch(dev):
+    from plaincv_amd import kernels as K_
+    torch.manual_seed(8)
+    shapes = [(768, 2304), (100, 37), (64, 64), (130, 1000)]
+    pairs, srcs = [], []
+    for r, c in shapes:
+        base = torch.randn(r, (c + 7) // 8 * 8, device=dev).to(torch.bfloat16)
+        src = base[:, :c]
+        dst = torch.zeros(c, (r + 7) // 8 * 8, device=dev, dtype=torch.bfloat16)[:, :r]
+        pairs.append((src, dst))
+        srcs.append(src)
+    K_.TransposeBatch(pairs, dev)()
+    for src, dst in pairs:
+        assert torch.equal(dst, src.t())

@@ -1,0 +1,55 @@
+"""GEMM throughput at the LM shapes: pcv_gemm_bf16 vs torch.matmul (hipBLASLt) on the same operands.
+
+    python tools/gemm_bench.py
+"""
+import time
+
+import torch
+
+import plaincv_amd.kernels as K
+
+dev = torch.device("cuda")
+
+
+def tm(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+# (name, M, N, K, mode) mode: fwd = A[M,K] B[K,N]; dgrad = A[M,K] B[N,K]^T; wgrad = A[K,M]^T B[K,N] (fp32 += )
+SHAPES = [("lm_head fwd", 16384, 50304, 768, "fwd"), ("qkv fwd", 16384, 2304, 768, "fwd"),
+          ("gate|up fwd", 16384, 4096, 768, "fwd"), ("fc2 fwd", 16384, 768, 2048, "fwd"),
+          ("out fwd", 16384, 768, 768, "fwd"), ("lm_head dgrad", 16384, 768, 50304, "dgrad"),
+          ("gate|up dgrad", 16384, 768, 4096, "dgrad"), ("lm_head wgrad", 768, 50304, 16384, "wgrad"),
+          ("gate|up wgrad", 768, 4096, 16384, "wgrad"), ("qkv wgrad", 768, 2304, 16384, "wgrad")]
+
+for name, M, N, Kd, mode in SHAPES:
+    bf = torch.bfloat16
+    if mode == "fwd":
+        a, b = torch.randn(M, Kd, device=dev, dtype=bf), torch.randn(Kd, N, device=dev, dtype=bf)
+        c = torch.empty(M, N, device=dev, dtype=bf)
+        ours = lambda: K.gemm(a, b, c)  # noqa: E731
+        ref = lambda: torch.matmul(a, b, out=c)  # noqa: E731
+    elif mode == "dgrad":
+        a, b = torch.randn(M, Kd, device=dev, dtype=bf), torch.randn(N, Kd, device=dev, dtype=bf)
+        c = torch.empty(M, N, device=dev, dtype=bf)
+        ours = lambda: K.gemm(a, b, c, tb=True)  # noqa: E731
+        ref = lambda: torch.matmul(a, b.t(), out=c)  # noqa: E731
+    else:
+        a, b = torch.randn(Kd, M, device=dev, dtype=bf), torch.randn(Kd, N, device=dev, dtype=bf)
+        c = torch.zeros(M, N, device=dev, dtype=torch.float32)
+        cb = torch.empty(M, N, device=dev, dtype=bf)
+        ours = lambda: K.gemm(a, b, c, ta=True, beta=1.0)  # noqa: E731
+        ref = lambda: torch.matmul(a.t(), b, out=cb)  # noqa: E731
+    fl = 2.0 * M * N * Kd
+    t1, t2 = tm(ours), tm(ref)
+    print(f"{name:16s} M={M:6d} N={N:6d} K={Kd:6d}  pcv {fl / t1 / 1e12:7.1f} TF/s ({t1 * 1e6:8.1f} us)   "
+          f"torch/hipBLASLt {fl / t2 / 1e12:7.1f} TF/s ({t2 * 1e6:8.1f} us)", flush=True)
