@@ -198,6 +198,71 @@ __device__ __forceinline__ void mc_glds(char* lds, const bf16* base, int64_t ld,
 // stride 132).  16 consecutive lanes own one row (8 columns each), so the row
 // statistics are 4 xor-shuffles; per-column parameter gradients and column sums are
 // reduced over the workgroup's rows and added with one atomic per column.
+// ---- loop-invariant addressing for the main loop
+// LDS byte offsets (within one operand image of a stage) of this lane's fragment for
+// rows/cols rbase..+15 and k-step ks; the transposing (M/N-contiguous) form needs two.
+template <bool KC, int R>
+__device__ __forceinline__ void frag_offsets(int rbase, int ks, int (&off)[2]) {
+  const int l = threadIdx.x & 63;
+  if constexpr (KC) {
+    const int r = rbase + (l & 15);
+    const int c = ks * 4 + (l >> 4);
+    off[0] = r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
+    off[1] = 0;
+  } else {
+    const int g = l >> 4, w = l & 15, q = w >> 2, p = w & 3;
+    const int kr0 = ks * 32 + 8 * g + q, kr1 = kr0 + 4;
+    const int cb = rbase >> 4;
+    off[0] = kr0 * (R * 2) + (mc_blk<R>(cb, kr0) << 5) + p * 8;
+    off[1] = kr1 * (R * 2) + (mc_blk<R>(cb, kr1) << 5) + p * 8;
+  }
+}
+template <bool KC>
+__device__ __forceinline__ bf16x8 read_frag(const char* img, const int (&off)[2]) {
+  if constexpr (KC) {
+    return *reinterpret_cast<const bf16x8*>(img + off[0]);
+  } else {
+    const bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + off[0]));
+    const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + off[1]));
+    return bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+  }
+}
+// Per-lane global source pointers of the LDS-DMA pieces (same maps as kc_glds/mc_glds),
+// at k = kbeg; advanced by 64 k per tile.
+template <int R>
+__device__ __forceinline__ void kc_piece_ptrs(const bf16** out, const bf16* base, int64_t ld, int64_t rows,
+                                              int64_t row0, int64_t kbeg) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int PER_WAVE = R * 128 / 1024 / 4;
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int piece = wave * PER_WAVE + i;
+    const int r = piece * 8 + (lane >> 3);
+    const int kc = (lane & 7) ^ ((r >> 1) & 7);
+    int64_t gr = row0 + r;
+    gr = gr < rows ? gr : rows - 1;
+    out[i] = base + gr * ld + kbeg + kc * 8;
+  }
+}
+template <int R>
+__device__ __forceinline__ void mc_piece_ptrs(const bf16** out, const bf16* base, int64_t ld, int64_t cols,
+                                              int64_t c0, int64_t kbeg) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int RB = R * 2, KR_PER_PIECE = 1024 / RB, SLOTS = RB / 16;
+  constexpr int PER_WAVE = 64 * RB / 1024 / 4;
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int piece = wave * PER_WAVE + i;
+    const int kr = piece * KR_PER_PIECE + lane / SLOTS;
+    const int sl = lane % SLOTS;
+    const int cb = mc_blk<R>(sl >> 1, kr);
+    int64_t gc = c0 + (cb * 2 + (sl & 1)) * 8;
+    const int64_t last = ((cols - 1) >> 3) << 3;
+    gc = gc <= last ? gc : last;
+    out[i] = base + (kbeg + kr) * ld + gc;
+  }
+}
+
 // Row operands of the LN epilogue (residual, LN input, row statistics) for this thread's
 // BM/16 rows, loaded before the GEMM main loop so their latency hides behind it.
 template <int BM>
@@ -439,66 +504,90 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
     if (B_KC) kc_store<BN>(stB, lb); else mc_store<BN>(stB, lb);
   };
 
-  // Full k-tiles go global->LDS asynchronously (global_load_lds) into an S-deep ring;
-  // the ragged last tile (and every tile when a leading dimension breaks 16-B
-  // alignment) goes through registers with zero fill, synchronously.
-  // Loads complete in order, so "tile kt landed" = at most PIECES*(tiles issued after
-  // kt) of this wave's vector-memory ops outstanding; a synchronous tile drains all.
-  auto issue = [&](int kt) {
-    if (kt >= nk) return;
-    const int64_t k0 = kbeg + (int64_t)kt * 64;
-    char* la = smem + (kt % S) * STAGE;
-    char* lb = la + A_BYTES;
-    if (g.glds_ok && k0 + 64 <= kend) {
-      if (A_KC) kc_glds<BM>(la, A, g.lda, g.M, m0, k0); else mc_glds<BM>(la, A, g.lda, g.M, m0, k0);
-      if (B_KC) kc_glds<BN>(lb, B, g.ldb, g.N, n0, k0); else mc_glds<BN>(lb, B, g.ldb, g.N, n0, k0);
-      return;
-    }
-    gload(k0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lstore(kt % S);
-  };
-
+  // LDS byte offsets of this lane's fragments within a stage (loop-invariant)
+  int offA[WM][2][2], offB[WN][2][2];
 #pragma unroll
-  for (int i = 0; i < S - 1; ++i) issue(i);
-  for (int kt = 0; kt < nk; ++kt) {
-    // tile kt landed (this wave's pieces), then the barrier makes every wave's visible
-    // and frees the slot of tile kt-1 for tile kt+S-1
-    if constexpr (S == 4) {
-      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PIECES) : "memory");
-      else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PIECES) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if constexpr (S == 3) {
-      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PIECES) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    issue(kt + S - 1);
-    const char* la = smem + (kt % S) * STAGE;
+  for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+    for (int i = 0; i < WM; ++i) frag_offsets<A_KC, BM>(wr * (BM / 2) + i * 16, ks, offA[i][ks]);
+#pragma unroll
+    for (int j = 0; j < WN; ++j) frag_offsets<B_KC, BN>(wc * (BN / 2) + j * 16, ks, offB[j][ks]);
+  }
+  auto compute = [&](const char* la) {
     const char* lb = la + A_BYTES;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 af[WM], bfr[WN];
 #pragma unroll
-      for (int i = 0; i < WM; ++i) {
-        const int rb = wr * (BM / 2) + i * 16;
-        af[i] = A_KC ? kc_frag(la, rb, ks) : mc_frag<BM>(la, rb, ks);
-      }
+      for (int i = 0; i < WM; ++i) af[i] = read_frag<A_KC>(la, offA[i][ks]);
 #pragma unroll
-      for (int j = 0; j < WN; ++j) {
-        const int cb = wc * (BN / 2) + j * 16;
-        bfr[j] = B_KC ? kc_frag(lb, cb, ks) : mc_frag<BN>(lb, cb, ks);
-      }
+      for (int j = 0; j < WN; ++j) bfr[j] = read_frag<B_KC>(lb, offB[j][ks]);
 #pragma unroll
       for (int i = 0; i < WM; ++i)
 #pragma unroll
         for (int j = 0; j < WN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+  };
+
+  if (g.glds_ok) {
+    // Full k-tiles: global -> LDS by DMA (global_load_lds) into an S-deep ring from
+    // per-lane source pointers computed once and advanced by a constant per tile.
+    // Loads complete in order: "tile kt landed" = at most PIECES*(tiles issued after
+    // kt) of this wave's vector-memory ops outstanding.
+    constexpr int PA = BM / 32, PB = BN / 32;   // pieces per wave per operand
+    const bf16* pa[PA];
+    const bf16* pb[PB];
+    if (A_KC) kc_piece_ptrs<BM>(pa, A, g.lda, g.M, m0, kbeg); else mc_piece_ptrs<BM>(pa, A, g.lda, g.M, m0, kbeg);
+    if (B_KC) kc_piece_ptrs<BN>(pb, B, g.ldb, g.N, n0, kbeg); else mc_piece_ptrs<BN>(pb, B, g.ldb, g.N, n0, kbeg);
+    const int64_t stepA = A_KC ? 64 : 64 * g.lda, stepB = B_KC ? 64 : 64 * g.ldb;
+    const int nfull = (int)((kend - kbeg) / 64);
+    const int wave_piece0A = wave * PA, wave_piece0B = wave * PB;
+    auto issue = [&](int kt) {
+      if (kt >= nfull) return;
+      char* la = smem + (kt % S) * STAGE;
+      char* lb = la + A_BYTES;
+#pragma unroll
+      for (int i = 0; i < PA; ++i) { glds16(pa[i], la + (wave_piece0A + i) * 1024); pa[i] += stepA; }
+#pragma unroll
+      for (int i = 0; i < PB; ++i) { glds16(pb[i], lb + (wave_piece0B + i) * 1024); pb[i] += stepB; }
+    };
+#pragma unroll
+    for (int i = 0; i < S - 1; ++i) issue(i);
+    for (int kt = 0; kt < nfull; ++kt) {
+      if constexpr (S == 4) {
+        if (kt + 2 < nfull) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PIECES) : "memory");
+        else if (kt + 1 < nfull) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PIECES) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if constexpr (S == 3) {
+        if (kt + 1 < nfull) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PIECES) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      issue(kt + S - 1);
+      compute(smem + (kt % S) * STAGE);
+    }
+    if (kbeg + (int64_t)nfull * 64 < kend) {   // ragged last k-tile: registers with zero fill
+      gload(kbeg + (int64_t)nfull * 64);
+      __syncthreads();                            // every wave is done with the ring
+      lstore(0);
+      __syncthreads();
+      compute(smem);
+    }
+  } else {
+    // a leading dimension breaks 16-B alignment: every tile through registers, double-buffered
+    if (nk > 0) { gload(kbeg); lstore(0); }
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) gload(kbeg + (int64_t)(kt + 1) * 64);
+      compute(smem + (kt & 1) * STAGE);
+      if (more) lstore((kt + 1) & 1);
+      __syncthreads();
+    }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();   // every wave done with the ring before the epilogue reuses the LDS
 
   // ---------------- epilogue ----------------
