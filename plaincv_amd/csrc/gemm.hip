@@ -441,7 +441,7 @@ struct GemmStages {
 };
 
 template <bool A_KC, bool B_KC, int WM, int WN>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256, (WM * WN >= 64) ? 1 : 2) void gemm_bf16_kernel(GemmArgs g) {
   constexpr int BM = 32 * WM, BN = 32 * WN;
   constexpr int A_BYTES = BM * 64 * 2, B_BYTES = BN * 64 * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -513,21 +513,42 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < WN; ++j) frag_offsets<B_KC, BN>(wc * (BN / 2) + j * 16, ks, offB[j][ks]);
   }
+  // both k-steps' fragments are read before the first MFMA, so the second half's LDS
+  // latency hides under the first half's MFMAs (the 256x256 tile, whose 8x8 blocking
+  // already hides it and has no registers to spare, reads one k-step at a time)
   auto compute = [&](const char* la) {
     const char* lb = la + A_BYTES;
+    if constexpr (WM * WN >= 64) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[WM], bfr[WN];
+#pragma unroll
+        for (int i = 0; i < WM; ++i) af[i] = read_frag<A_KC>(la, offA[i][ks]);
+#pragma unroll
+        for (int j = 0; j < WN; ++j) bfr[j] = read_frag<B_KC>(lb, offB[j][ks]);
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      return;
+    }
+    bf16x8 af[2][WM], bfr[2][WN];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[WM], bfr[WN];
 #pragma unroll
-      for (int i = 0; i < WM; ++i) af[i] = read_frag<A_KC>(la, offA[i][ks]);
+      for (int i = 0; i < WM; ++i) af[ks][i] = read_frag<A_KC>(la, offA[i][ks]);
 #pragma unroll
-      for (int j = 0; j < WN; ++j) bfr[j] = read_frag<B_KC>(lb, offB[j][ks]);
+      for (int j = 0; j < WN; ++j) bfr[ks][j] = read_frag<B_KC>(lb, offB[j][ks]);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < WM; ++i)
 #pragma unroll
         for (int j = 0; j < WN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
   };
 
   if (g.glds_ok) {
@@ -591,36 +612,15 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   __syncthreads();   // every wave done with the ring before the epilogue reuses the LDS
 
   // ---------------- epilogue ----------------
-  // Stage the fp32 tile through LDS ([BM][BN+4], conflict-free ds_write_b32), then
-  // every thread owns 8 consecutive columns of a row: 16-B loads of bias/aux/res
-  // and 16-B stores of the output (the MFMA C layout would otherwise store 2-4 B
-  // per lane, which made the small-K ViT GEMMs epilogue-bound).
+  // Stage the fp32 tile through LDS ([CH][BN+4] rows at a time, conflict-free
+  // ds_write_b32), then every thread owns 8 consecutive columns of a row: 16-B loads of
+  // bias/aux/res and 16-B stores of the output (the MFMA C layout would otherwise store
+  // 2-4 B per lane, which made the small-K ViT GEMMs epilogue-bound).  The 256x256 tile
+  // does not fit LDS at once and is staged in 64-row chunks.
   constexpr int CLD = BN + 4;
+  constexpr int CH = BM * CLD * 4 <= 96 * 1024 ? BM : 64;
   float* ct = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int i = 0; i < WM; ++i)
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        ct[(wr * (BM / 2) + i * 16 + (lane >> 4) * 4 + r) * CLD + wc * (BN / 2) + j * 16 + (lane & 15)] =
-            acc[i][j][r];
-  __syncthreads();
   char* Cb = (char*)g.C + bz * g.sC * (g.out_f32 ? 4 : 2);
-  if (g.split_k > 1) {
-    // split-K partial: fp32 atomics shaped as 64 consecutive floats (256 B) per
-    // wave-instruction -- the full-rate atomic shape (MI355X_MICROARCH "Global float atomics")
-    float* C = (float*)Cb;
-    for (int idx = threadIdx.x; idx < BM * BN; idx += 256) {
-      const int rr = idx / BN, c = idx % BN;
-      const int64_t row = m0 + rr, col = n0 + c;
-      if (row < g.M && col < g.N) atomicAdd(C + row * g.ldc + col, g.alpha * ct[rr * CLD + c]);
-    }
-    return;
-  }
-  if constexpr (LN_TILE) {
-    if (g.ln_mode) { ln_epilogue<BM>(g, ct, m0, lnpre); return; }
-  }
   constexpr int CPR = BN / 8;            // 8-column chunks per row
   constexpr int RPP = 256 / CPR;         // rows per pass
   const int cc = threadIdx.x % CPR;
@@ -628,24 +628,51 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
   float csum[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) csum[e] = 0.f;
-  if (col < g.N) {
-    const bool vec = g.vec_ok && col + 8 <= g.N;
-    float bv[8];
+  const bool vec = g.vec_ok && col + 8 <= g.N;
+  float bv[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) bv[e] = 0.f;
-    if (g.bias) {
-      if (vec) {
-        const f32x4 b0 = *reinterpret_cast<const f32x4*>(g.bias + col);
-        const f32x4 b1 = *reinterpret_cast<const f32x4*>(g.bias + col + 4);
+  for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+  if (g.bias && col < g.N) {
+    if (vec) {
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(g.bias + col);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(g.bias + col + 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { bv[e] = b0[e]; bv[e + 4] = b1[e]; }
-      } else {
-        for (int e = 0; e < 8; ++e) bv[e] = (col + e < g.N) ? g.bias[col + e] : 0.f;
-      }
+      for (int e = 0; e < 4; ++e) { bv[e] = b0[e]; bv[e + 4] = b1[e]; }
+    } else {
+      for (int e = 0; e < 8; ++e) bv[e] = (col + e < g.N) ? g.bias[col + e] : 0.f;
     }
-    const uint32_t seed = g.drop_thresh ? *g.seedp : 0u;
-    for (int rr = threadIdx.x / CPR; rr < BM; rr += RPP) {
-      const int64_t row = m0 + rr;
+  }
+  const uint32_t seed = g.drop_thresh ? *g.seedp : 0u;
+  for (int rc = 0; rc < BM; rc += CH) {
+    if (rc) __syncthreads();             // the previous chunk is fully consumed
+#pragma unroll
+    for (int i = 0; i < WM; ++i) {
+      const int rt = wr * (BM / 2) + i * 16;
+      if (rt < rc || rt >= rc + CH) continue;   // wave-uniform
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ct[(rt - rc + (lane >> 4) * 4 + r) * CLD + wc * (BN / 2) + j * 16 + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (g.split_k > 1) {
+      // split-K partial: fp32 atomics shaped as 64 consecutive floats (256 B) per
+      // wave-instruction -- the full-rate atomic shape (MI355X_MICROARCH "Global float atomics")
+      float* C = (float*)Cb;
+      for (int idx = threadIdx.x; idx < CH * BN; idx += 256) {
+        const int rr = idx / BN, c = idx % BN;
+        const int64_t row = m0 + rc + rr, cl = n0 + c;
+        if (row < g.M && cl < g.N) atomicAdd(C + row * g.ldc + cl, g.alpha * ct[rr * CLD + c]);
+      }
+      continue;
+    }
+    if constexpr (LN_TILE) {
+      if (g.ln_mode) { ln_epilogue<BM>(g, ct, m0, lnpre); return; }
+    }
+    if (col >= g.N) continue;
+    for (int rr = threadIdx.x / CPR; rr < CH; rr += RPP) {
+      const int64_t row = m0 + rc + rr;
       if (row >= g.M) break;
       float v[8];
       const f32x4 c0 = *reinterpret_cast<const f32x4*>(ct + rr * CLD + cc * 8);
@@ -739,8 +766,9 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmArgs g) {
           for (int e = 0; e < 8; ++e) if (col + e < g.N) cp[e] = f2bf(v[e]);
         }
       }
-    }
+        }
   }
+  if (g.split_k > 1) return;
   if (g.colsum) {
     // column sums of this tile's rows: the RPP threads sharing a column chunk reduce through
     // LDS (the staged tile is no longer read), then one atomic per column
@@ -764,7 +792,8 @@ static hipError_t launch_t(const GemmArgs& a, int batch, hipStream_t s) {
   g.tiles_m = (int)((g.M + BM - 1) / BM);
   g.tiles_n = (int)((g.N + BN - 1) / BN);
   const size_t stage = GemmStages<WM, WN>::S * (size_t)(BM + BN) * 64 * 2;
-  const size_t ctile = (size_t)BM * (BN + 4) * 4 + (BM == 64 && BN == 128 ? 3 * 4 * 128 * 4 : 0);   // + LN reductions
+  constexpr int CH = BM * (BN + 4) * 4 <= 96 * 1024 ? BM : 64;   // epilogue staging rows (as in the kernel)
+  const size_t ctile = (size_t)CH * (BN + 4) * 4 + (BM == 64 && BN == 128 ? 3 * 4 * 128 * 4 : 0);   // + LN reductions
   const size_t lds = stage > ctile ? stage : ctile;
   dim3 grid(g.tiles_m * g.tiles_n, batch, g.split_k > 1 ? g.split_k : 1);
   static bool attr = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
@@ -840,9 +869,12 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
     g.k_per_split = kps;
   }
   hipStream_t s = (hipStream_t)stream;
-  const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128);
-  hipError_t e = (t128 * batch * g.split_k >= 240) ? launch_sz<4, 4>(g, trans_a, trans_b, (int)batch, s)
-                                                    : launch_sz<2, 2>(g, trans_a, trans_b, (int)batch, s);
+  // tile: 128x128 when that grid covers the chip, else 64x64.  (A 256x256 tile with
+  // one 128x128 block per wave was measured 15-45 % slower at the LM shapes: it needs
+  // all 512 registers, spills, and runs one wave per SIMD.)
+  const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128) * batch * g.split_k;
+  hipError_t e = t128 >= 240 ? launch_sz<4, 4>(g, trans_a, trans_b, (int)batch, s)
+                             : launch_sz<2, 2>(g, trans_a, trans_b, (int)batch, s);
   return e == hipSuccess ? 0 : (int)e;
 }
 
