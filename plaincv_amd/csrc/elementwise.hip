@@ -344,7 +344,7 @@ struct TrRec {
 };
 
 __global__ __launch_bounds__(256) void transpose_batch_kernel(const TrRec* recs, int n) {
-  __shared__ bf16 t[64][66];
+  __shared__ bf16 t[64][72];             // 144-B rows: 16-B aligned, rotating banks
   int lo = 0, hi = n - 1;
   while (lo < hi) {                      // last record with tile0 <= blockIdx.x
     const int mid = (lo + hi + 1) >> 1;
@@ -354,22 +354,43 @@ __global__ __launch_bounds__(256) void transpose_batch_kernel(const TrRec* recs,
   const int64_t tile = (int64_t)blockIdx.x - R.tile0;
   const int64_t tcs = (R.cols + 63) / 64;
   const int64_t r0 = (tile / tcs) * 64, c0 = (tile % tcs) * 64;
-  const int tid = threadIdx.x, lr = tid >> 2, lc = (tid & 3) * 16;
-  {
-    const int64_t r = r0 + lr;
+  const int tid = threadIdx.x;
+  // load: 64 rows x 8 chunks of 8; thread -> (row tid>>3 + 32*h, chunk tid&7)
+  const bool full_c = c0 + 64 <= R.cols && (R.lds & 7) == 0 && (((uintptr_t)R.src) & 15) == 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int64_t c = c0 + lc + j;
-      t[lr][lc + j] = (r < R.rows && c < R.cols) ? R.src[r * R.lds + c] : (bf16)0.f;
+  for (int h = 0; h < 2; ++h) {
+    const int lr = (tid >> 3) + 32 * h, ch = tid & 7;
+    const int64_t r = r0 + lr;
+    u32x4 v = u32x4{0u, 0u, 0u, 0u};
+    if (r < R.rows) {
+      const bf16* p = R.src + r * R.lds + c0 + ch * 8;
+      if (full_c) {
+        v = *reinterpret_cast<const u32x4*>(p);
+      } else {
+        union { u32x4 w; bf16 e[8]; } u;
+        u.w = v;
+        for (int j = 0; j < 8; ++j) if (c0 + ch * 8 + j < R.cols) u.e[j] = p[j];
+        v = u.w;
+      }
     }
+    *reinterpret_cast<u32x4*>(&t[lr][ch * 8]) = v;
   }
   __syncthreads();
-  const int64_t dr = c0 + lr;            // destination row = source column
-  if (dr < R.cols) {
+  // store: destination row c0 + (tid>>3) + 32*h (a source column), 8 consecutive source rows
+  const bool full_r = r0 + 64 <= R.rows && (R.ldd & 7) == 0 && (((uintptr_t)R.dst) & 15) == 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int64_t dc = r0 + lc + j;    // destination column = source row
-      if (dc < R.rows) R.dst[dr * R.ldd + dc] = t[lc + j][lr];
+  for (int h = 0; h < 2; ++h) {
+    const int lc = (tid >> 3) + 32 * h, ch = tid & 7;
+    const int64_t dr = c0 + lc;
+    if (dr >= R.cols) continue;
+    union { u32x4 w; bf16 e[8]; } u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) u.e[j] = t[ch * 8 + j][lc];
+    bf16* q = R.dst + dr * R.ldd + r0 + ch * 8;
+    if (full_r) {
+      *reinterpret_cast<u32x4*>(q) = u.w;
+    } else {
+      for (int j = 0; j < 8; ++j) if (r0 + ch * 8 + j < R.rows) q[j] = u.e[j];
     }
   }
 }

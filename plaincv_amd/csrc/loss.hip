@@ -94,6 +94,115 @@ __global__ __launch_bounds__(512) void xent_kernel(const T* logits, int64_t ld, 
   }
 }
 
+// Large-vocabulary rows (LM, V ~ 50k): no LDS copy of the row, so many rows are in flight
+// per CU.  Pass 1 streams the row once (16-B loads, 4 in flight per thread) keeping an
+// online max / rescaled sum-exp / first argmax per thread; pass 2 re-reads the row (an
+// L2 hit for the rows in flight) and writes d = (softmax - onehot) * grad_scale.
+template <typename T>
+__global__ __launch_bounds__(256) void xent_stream_kernel(const T* logits, int64_t ld, const int* labels, int64_t R,
+                                                          int V, float* row_loss, float* row_correct, T* dlogits,
+                                                          int64_t ldd, float grad_scale) {
+  constexpr int VE = 16 / sizeof(T);
+  __shared__ float sm[4], ss[4];
+  __shared__ int si[4];
+  const int64_t row = blockIdx.x;
+  const T* z = logits + row * ld;
+  const int nv = V / VE;                 // full 16-B chunks (row base and stride are 16-B aligned)
+  float m = -3.0e38f, s = 0.f;
+  int am = 0x7fffffff;
+  auto absorb = [&](float v, int j) {
+    if (v > m) { s = s * __expf(m - v) + 1.f; m = v; am = j; }
+    else s += __expf(v - m);
+  };
+  int c = threadIdx.x;
+  for (; c + 3 * 256 < nv; c += 4 * 256) {
+    u32x4 w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) w[u] = *reinterpret_cast<const u32x4*>(z + (int64_t)(c + u * 256) * VE);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const T* e = reinterpret_cast<const T*>(&w[u]);
+#pragma unroll
+      for (int q = 0; q < VE; ++q) absorb((float)e[q], (c + u * 256) * VE + q);
+    }
+  }
+  for (; c < nv; c += 256) {
+    const u32x4 w = *reinterpret_cast<const u32x4*>(z + (int64_t)c * VE);
+    const T* e = reinterpret_cast<const T*>(&w);
+#pragma unroll
+    for (int q = 0; q < VE; ++q) absorb((float)e[q], c * VE + q);
+  }
+  for (int j = nv * VE + threadIdx.x; j < V; j += 256) absorb((float)z[j], j);
+  // block reduce: max, then sum rescaled to the block max, first argmax
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    const int a2 = __shfl_xor(am, o, 64);
+    const float mn = fmaxf(m, m2);
+    s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+    if (m2 > m || (m2 == m && a2 < am)) am = a2;
+    m = mn;
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sm[w] = m; ss[w] = s; si[w] = am; }
+  __syncthreads();
+  float M = sm[0];
+  int A = si[0];
+  for (int i = 1; i < 4; ++i) {
+    if (sm[i] > M || (sm[i] == M && si[i] < A)) A = si[i];
+    M = fmaxf(M, sm[i]);
+  }
+  float S = 0.f;
+  for (int i = 0; i < 4; ++i) S += ss[i] * __expf(sm[i] - M);
+  const float lse = M + __logf(S);
+  const int y = labels[row];
+  const bool yok = y >= 0 && y < V;
+  if (threadIdx.x == 0) {
+    row_loss[row] = yok ? lse - (float)z[y] : 0.f;
+    row_correct[row] = (yok && A == y) ? 1.f : 0.f;
+  }
+  if (!dlogits) return;
+  __syncthreads();                       // z[y] read above before an in-place overwrite
+  T* d = dlogits + row * ldd;
+  c = threadIdx.x;
+  for (; c + 3 * 256 < nv; c += 4 * 256) {
+    u32x4 wv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) wv[u] = *reinterpret_cast<const u32x4*>(z + (int64_t)(c + u * 256) * VE);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const T* e = reinterpret_cast<const T*>(&wv[u]);
+      union { u32x4 w; T e[VE]; } o;
+#pragma unroll
+      for (int q = 0; q < VE; ++q) {
+        const int j = (c + u * 256) * VE + q;
+        float p = __expf((float)e[q] - lse);
+        if (j == y) p -= 1.f;
+        o.e[q] = (T)(p * grad_scale);
+      }
+      *reinterpret_cast<u32x4*>(d + (int64_t)(c + u * 256) * VE) = o.w;
+    }
+  }
+  for (; c < nv; c += 256) {
+    const u32x4 wv = *reinterpret_cast<const u32x4*>(z + (int64_t)c * VE);
+    const T* e = reinterpret_cast<const T*>(&wv);
+    union { u32x4 w; T e[VE]; } o;
+#pragma unroll
+    for (int q = 0; q < VE; ++q) {
+      const int j = c * VE + q;
+      float p = __expf((float)e[q] - lse);
+      if (j == y) p -= 1.f;
+      o.e[q] = (T)(p * grad_scale);
+    }
+    *reinterpret_cast<u32x4*>(d + (int64_t)c * VE) = o.w;
+  }
+  for (int j = nv * VE + threadIdx.x; j < V; j += 256) {
+    float p = __expf((float)z[j] - lse);
+    if (j == y) p -= 1.f;
+    d[j] = (T)(p * grad_scale);
+  }
+}
+
 // out[0] = scale * sum(x[0..n)), out[1] = scale2 * sum(y[0..n)) (y optional); one block, deterministic
 __global__ __launch_bounds__(1024) void mean2_kernel(const float* x, const float* y, int64_t n, float scale,
                                                      float* out) {
@@ -115,6 +224,17 @@ extern "C" int pcv_xent_fwd_bwd(const void* logits, int64_t ld, int logits_f32, 
   if (R <= 0 || V <= 0) return PCV_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const size_t es = logits_f32 ? 4 : 2;
+  const bool aligned = pcv_aligned16(logits) && ((ld * es) % 16 == 0) &&
+                       (!dlogits || (pcv_aligned16(dlogits) && (ldd * es) % 16 == 0));
+  if (V >= 4096 && aligned) {   // streaming kernel (large vocabulary)
+    if (logits_f32)
+      hipLaunchKernelGGL(xent_stream_kernel<float>, dim3((unsigned)R), dim3(256), 0, s, (const float*)logits, ld,
+                         labels, R, V, row_loss, row_correct, (float*)dlogits, ldd, grad_scale);
+    else
+      hipLaunchKernelGGL(xent_stream_kernel<bf16>, dim3((unsigned)R), dim3(256), 0, s, (const bf16*)logits, ld,
+                         labels, R, V, row_loss, row_correct, (bf16*)dlogits, ldd, grad_scale);
+    return pcv_launch_status();
+  }
   const size_t lds = ((size_t)V * es + 15) / 16 * 16;
   if (lds > 150 * 1024) return PCV_EINVAL;  // row must fit in LDS (V <= ~76k bf16 / 38k fp32)
   const int vec = pcv_aligned16(logits) && ((ld * es) % 16 == 0) &&

@@ -161,8 +161,14 @@ def test_rope_swiglu_xent_embed(dev):
     lg = buf[:, :V]
     lab = torch.randint(0, V, (R,), device=dev, dtype=torch.int32)
     rl, rc = torch.empty(R, device=dev), torch.empty(R, device=dev)
-    K.xent(lg, lab, rl, rc, lg, grad_scale=1.0 / R)
-    lf = buf[:, :V].float()  # now overwritten with grads: recompute reference from a copy
+    lcopy = lg.float().clone()
+    K.xent(lg, lab, rl, rc, lg, grad_scale=1.0 / R)     # in place: logits -> dlogits
+    lr_ = lcopy.requires_grad_(True)
+    lref = torch.nn.functional.cross_entropy(lr_, lab.long(), reduction="none")
+    assert torch.allclose(rl, lref.detach(), atol=1e-3, rtol=1e-4)
+    lref.mean().backward()
+    assert torch.allclose(lg.float(), lr_.grad, atol=1e-4)
+    assert torch.equal(rc, (lcopy.argmax(-1) == lab.long()).float())
     torch.manual_seed(2)
     # reference on fresh data
     buf2 = torch.randn(R, 50264, device=dev).to(torch.bfloat16)
