@@ -19,10 +19,13 @@
 // bwd_dq (workgroup = 64 queries, loop over keys) -- deterministic, no atomics.
 #include "common.h"
 
+#include <type_traits>
+
 namespace pcv {
 
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1.0e30f;
+constexpr f32x4 kZero4 = {0.f, 0.f, 0.f, 0.f};
 
 struct AttnArgs {
   const bf16 *q, *k, *v; int64_t ldq;     // q/k/v row stride (same packed buffer)
@@ -157,6 +160,30 @@ __device__ __forceinline__ void tile_store(const TileRegs<DH>& t, bf16* Ks, bf16
   }
 }
 
+// Workgroup order.  Dispatch follows the linear block id, so under a causal mask the
+// heaviest blocks (late query blocks for fwd/dQ, early key blocks for dK/dV) are mapped
+// to the lowest ids: they start first and the grid's tail is made of light blocks.
+template <bool CAUSAL>
+__device__ __forceinline__ void heavy_first(int& qb, int& h, int& b) {
+  if (!CAUSAL) { qb = blockIdx.x; h = blockIdx.y; b = blockIdx.z; return; }
+  const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int nbh = gridDim.y * gridDim.z;
+  qb = gridDim.x - 1 - lin / nbh;
+  const int bh = lin % nbh;
+  h = bh % gridDim.y;
+  b = bh / gridDim.y;
+}
+template <bool CAUSAL>
+__device__ __forceinline__ void light_last(int& kb, int& h, int& b) {
+  if (!CAUSAL) { kb = blockIdx.x; h = blockIdx.y; b = blockIdx.z; return; }
+  const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int nbh = gridDim.y * gridDim.z;
+  kb = lin / nbh;
+  const int bh = lin % nbh;
+  h = bh % gridDim.y;
+  b = bh / gridDim.y;
+}
+
 // Workgroup = 4 waves x 32 queries (two 16-query groups per wave share every K/V
 // fragment read from LDS); K/V tiles of 64 keys double-buffered in LDS.
 template <int DH, bool CAUSAL, bool DROP>
@@ -164,7 +191,8 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
   constexpr int KS = DH / 32, DT = DH / 16, QG = 2;
   constexpr int TILE = 64 * DH;
   __shared__ __attribute__((aligned(16))) bf16 kv_smem[2 * 2 * TILE];   // [buffer][K|V][TILE]
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  int qb, h, b;
+  heavy_first<CAUSAL>(qb, h, b);
   const int T = a.T;
   const int64_t bT = (int64_t)b * T;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -209,24 +237,23 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
 #pragma unroll
-        for (int gq = 0; gq < QG; ++gq) s[gq][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const bf16x8 kf = row_frag<DH>(Ks, 16 * t, ks);
 #pragma unroll
-          for (int gq = 0; gq < QG; ++gq)
-            s[gq][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[gq][ks], s[gq][t], 0, 0, 0);
+          for (int gq = 0; gq < QG; ++gq)   // first k-step: inline-zero accumulator
+            s[gq][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[gq][ks], ks ? s[gq][t] : kZero4, 0, 0, 0);
         }
       }
-#pragma unroll
-      for (int gq = 0; gq < QG; ++gq) {
+      // Online softmax per 16-query group.  Masked scores (ragged tail, causal diagonal)
+      // become NEG_BIG in the raw domain -- only on boundary tiles, in their own code path.
+      // The running max is updated lazily: it is raised only when some score exceeds it by
+      // more than 2^8 (log2 domain), so steady-state tiles skip the rescale of the output
+      // accumulators; exp2 arguments stay <= 8, which bf16 P and the fp32 sums absorb.
+      // The first key tile always holds a valid key for every row, so m2 is finite after it.
+      auto softmax = [&](auto maskc, int gq) {
+        constexpr bool MASK = decltype(maskc)::value;
         const int myq = qw + gq * 16 + (lane & 15);
-        // Interior tile (every key valid for every query of the group) needs no mask.
-        // Masked scores become NEG_BIG in the raw domain; the scale is folded into
-        // the exp2 argument (max commutes with the positive scale).  The first key
-        // tile always holds a valid key for every row, so m2 is finite from then on.
-        const bool interior = kb * 64 + 63 < T && (!CAUSAL || kb * 64 + 63 <= qw + gq * 16);
-        if (!interior) {
+        if constexpr (MASK) {
 #pragma unroll
           for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -244,20 +271,32 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
           for (int r = 0; r < 4; ++r) bmax = fmaxf(bmax, s[gq][t][r]);
         bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
         bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
-        const float mnew = fmaxf(m2[gq], bmax * c2);
-        const float alpha = __builtin_amdgcn_exp2f(m2[gq] - mnew);
+        const float cand = bmax * c2;
+        if (__ballot(cand > m2[gq] + 8.f) != 0) {   // some row's max moved: rescale (wave-uniform branch)
+          const float mnew = fmaxf(m2[gq], cand);
+          const float alpha = __builtin_amdgcn_exp2f(m2[gq] - mnew);
+          lsum[gq] *= alpha;
+          m2[gq] = mnew;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float al = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+            for (int d = 0; d < DT; ++d) acc[gq][d][r] *= al;
+          }
+        }
         uint32_t wt[4] = {0u, 0u, 0u, 0u};
         if (DROP) {
           const uint64_t mw = *reinterpret_cast<const uint64_t*>(a.mask + drop_word(myq, kb * 64 + 4 * g, a.n64));
 #pragma unroll
           for (int t = 0; t < 4; ++t) wt[t] = (uint32_t)(mw >> (16 * t)) >> (4 * (myq & 3));
         }
+        const float mneg = -m2[gq];
         float rs = 0.f;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float p = __builtin_amdgcn_exp2f(fmaf(s[gq][t][r], c2, -mnew));
+            float p = __builtin_amdgcn_exp2f(fmaf(s[gq][t][r], c2, mneg));
             rs += p;
             // dropped weights -> 0 (bit select); the 1/keep scale is applied at the end
             if (DROP) p = __uint_as_float(__float_as_uint(p) & (uint32_t)__builtin_amdgcn_sbfe((int)wt[t], r, 1));
@@ -265,14 +304,13 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
           }
         rs += __shfl_xor(rs, 16, 64);
         rs += __shfl_xor(rs, 32, 64);
-        lsum[gq] = lsum[gq] * alpha + rs;
-        m2[gq] = mnew;
+        lsum[gq] += rs;
+      };
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float al = __shfl(alpha, 4 * g + r, 64);
-#pragma unroll
-          for (int d = 0; d < DT; ++d) acc[gq][d][r] *= al;
-        }
+      for (int gq = 0; gq < QG; ++gq) {
+        const bool interior = kb * 64 + 63 < T && (!CAUSAL || kb * 64 + 63 <= qw + gq * 16);
+        if (interior) softmax(std::false_type{}, gq);
+        else softmax(std::true_type{}, gq);
       }
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
@@ -351,7 +389,8 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
   constexpr int TILE = 64 * DH;
   __shared__ __attribute__((aligned(16))) bf16 qo_smem[2 * 2 * TILE];   // [buffer][Q|dO][TILE]
   __shared__ float ld_smem[2 * 128];                                    // [buffer][lse|delta][64]
-  const int kb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  int kb, h, b;
+  light_last<CAUSAL>(kb, h, b);
   const int T = a.T;
   const int64_t bT = (int64_t)b * T;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -434,15 +473,13 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
       for (int t = 0; t < 4; ++t) {
         f32x4 sv[KG], dp[KG];
 #pragma unroll
-        for (int gk = 0; gk < KG; ++gk) { sv[gk] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[gk] = f32x4{0.f, 0.f, 0.f, 0.f}; }
-#pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const bf16x8 qa = row_frag<DH>(Qs, 16 * t, ks);
           const bf16x8 oa = row_frag<DH>(Ds, 16 * t, ks);
 #pragma unroll
           for (int gk = 0; gk < KG; ++gk) {
-            sv[gk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[gk][ks], sv[gk], 0, 0, 0);
-            dp[gk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[gk][ks], dp[gk], 0, 0, 0);
+            sv[gk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[gk][ks], ks ? sv[gk] : kZero4, 0, 0, 0);
+            dp[gk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[gk][ks], ks ? dp[gk] : kZero4, 0, 0, 0);
           }
         }
 #pragma unroll
@@ -518,7 +555,8 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
   constexpr int TILE = 64 * DH;
   constexpr int KS = DH / 32, DT = DH / 16, QG = 2;
   __shared__ __attribute__((aligned(16))) bf16 kv_smem[2 * 2 * TILE];   // [buffer][K|V][TILE]
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  int qb, h, b;
+  heavy_first<CAUSAL>(qb, h, b);
   const int T = a.T;
   const int64_t bT = (int64_t)b * T;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -570,15 +608,13 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
       for (int t = 0; t < 4; ++t) {
         f32x4 sv[QG], dp[QG];
 #pragma unroll
-        for (int gq = 0; gq < QG; ++gq) { sv[gq] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[gq] = f32x4{0.f, 0.f, 0.f, 0.f}; }
-#pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const bf16x8 ka = row_frag<DH>(Ks, 16 * t, ks);
           const bf16x8 va = row_frag<DH>(Vs, 16 * t, ks);
 #pragma unroll
           for (int gq = 0; gq < QG; ++gq) {
-            sv[gq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[gq][ks], sv[gq], 0, 0, 0);
-            dp[gq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, of[gq][ks], dp[gq], 0, 0, 0);
+            sv[gq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[gq][ks], ks ? sv[gq] : kZero4, 0, 0, 0);
+            dp[gq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, of[gq][ks], ks ? dp[gq] : kZero4, 0, 0, 0);
           }
         }
 #pragma unroll

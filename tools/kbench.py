@@ -36,6 +36,12 @@ gb = t(M, dt=f32)
 seed = torch.zeros(1, dtype=torch.int32, device=dev)
 lse, delta = t(B * H * T, dt=f32), t(B * H * T, dt=f32)
 mw = K.attn_mask_words(T)
+# LM attention shapes (124M: b=16, T=1024, H=12, Dh=64, causal)
+Bl, Tl, Hl, Dl = 16, 1024, 12, 64
+qkv_l = t(Bl * Tl, 3 * Hl * Dl)
+o_l, do_l = t(Bl * Tl, Hl * Dl), t(Bl * Tl, Hl * Dl)
+dqkv_l = t(Bl * Tl, 3 * Hl * Dl)
+lse_l, delta_l = t(Bl * Hl * Tl, dt=f32), t(Bl * Hl * Tl, dt=f32)
 mask = torch.zeros(mw, dtype=torch.int16, device=dev)
 
 CASES = {
@@ -72,6 +78,9 @@ CASES = {
     "attn_fwd  64x4x257x32 drop": lambda: K.attn_fwd(qkv, o, lse, B, T, H, 32, False, drop_rate=0.1, mask=mask),
     "attn_bwd  64x4x257x32 drop": lambda: K.attn_bwd(qkv, o, o, lse, delta, qkv, B, T, H, 32, False, drop_rate=0.1,
                                                      mask=mask),
+    "lmattn_fwd 16x12x1024x64 causal": lambda: K.attn_fwd(qkv_l, o_l, lse_l, Bl, Tl, Hl, Dl, True),
+    "lmattn_bwd 16x12x1024x64 causal": lambda: K.attn_bwd(qkv_l, o_l, do_l, lse_l, delta_l, dqkv_l, Bl, Tl, Hl, Dl,
+                                                          True),
 }
 
 
