@@ -51,6 +51,19 @@ int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, int64_t N, in
                 const float* ln_bias, float ln_eps, void* ln_y, int64_t ld_lny, float* ln_mean, float* ln_rstd,
                 const float* ln_x, int64_t ld_lnx, float* ln_dscale, float* ln_dbias, float* colsum, void* stream);
 
+/* Grouped weight-gradient GEMM: n independent C_i[M,N] (fp32) += alpha_i * A_i^T B_i with
+ * A_i [K][M], B_i [K][N] bf16 (row strides lda/ldb % 8 == 0, 16-B aligned bases), each split
+ * split_k_i ways over K (fp32 atomics), ONE launch for all of them -- the flax autodiff
+ * kernel gradients of every Dense in a backward pass (models/vit_small.py:41-45,78-88).
+ * Descriptor (pcv_gemm_desc_size() bytes): {A, B, C, M, N, K, lda, ldb, ldc, alpha, split_k}.
+ * plan: host descriptors -> device plan buffer (pcv_gemm_grouped_plan_size(n) bytes, caller
+ * owned, synchronous copy); run: stream-ordered, graph-capturable.  No two descriptors of a
+ * plan may share a C. */
+int64_t pcv_gemm_grouped_plan_size(int n);
+int pcv_gemm_desc_size(void);
+int pcv_gemm_grouped_plan(const void* descs, int n, int tile /* 64 | 128 */, void* plan_dev, int64_t* total_blocks);
+int pcv_gemm_grouped_run(const void* plan_dev, int n, int tile /* as planned */, int64_t total_blocks, void* stream);
+
 /* ----------------------------------------------------------- attention ----
  * Flash attention on the packed QKV activation (q/k/v = column blocks, head h
  * at column h*head_dim); lse2[B,H,T] is log2-domain.  head_dim in {32,64,128}.

@@ -19,6 +19,8 @@
 // remapped so each XCD gets a contiguous run of tiles, grouped 8 along M.
 #include "common.h"
 
+#include <vector>
+
 namespace pcv {
 
 enum { EPI_NONE = 0, EPI_GELU = 1, EPI_GELU_BWD = 2 };
@@ -440,8 +442,9 @@ struct GemmStages {
       (WM == 2 && WN == 4) ? PCV_GEMM_STAGES_LN : (WM * WN <= 4 ? PCV_GEMM_STAGES_SMALL : PCV_GEMM_STAGES_BIG);
 };
 
+// One output tile (bid = tile index, bz = batch index, kz = split-K slice) of the GEMM g.
 template <bool A_KC, bool B_KC, int WM, int WN>
-__global__ __launch_bounds__(256, (WM * WN >= 64) ? 1 : 2) void gemm_bf16_kernel(GemmArgs g) {
+__device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz, int kz, bool remap) {
   constexpr int BM = 32 * WM, BN = 32 * WN;
   constexpr int A_BYTES = BM * 64 * 2, B_BYTES = BN * 64 * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -449,11 +452,11 @@ __global__ __launch_bounds__(256, (WM * WN >= 64) ? 1 : 2) void gemm_bf16_kernel
   constexpr int S = GemmStages<WM, WN>::S;
   constexpr int PIECES = (BM + BN) / 32;   // global_load_lds instructions per wave per k-tile
 
-  // XCD-aware bijective remap, then GROUP_M=8 ordering
+  // XCD-aware bijective remap (block ids are dealt round-robin to the 8 XCDs, so each XCD
+  // gets a contiguous run of tiles), then GROUP_M=8 ordering
   const int nwg = g.tiles_m * g.tiles_n;
-  const int bid = blockIdx.x;
   const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
-  const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int wgid = remap ? (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3) : bid;
   const int GROUP = 8;
   const int per_group = GROUP * g.tiles_n;
   const int gid = wgid / per_group;
@@ -463,13 +466,12 @@ __global__ __launch_bounds__(256, (WM * WN >= 64) ? 1 : 2) void gemm_bf16_kernel
   const int tn = (wgid % per_group) / gsz;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
 
-  const int64_t bz = blockIdx.y;
   const bf16* A = g.A + bz * g.sA;
   const bf16* B = g.B + bz * g.sB;
 
   int64_t kbeg = 0, kend = g.K;
   if (g.split_k > 1) {
-    kbeg = (int64_t)blockIdx.z * g.k_per_split;
+    kbeg = (int64_t)kz * g.k_per_split;
     kend = min(g.K, kbeg + g.k_per_split);
   }
   const int nk = (int)((kend - kbeg + 63) / 64);
@@ -785,16 +787,50 @@ __global__ __launch_bounds__(256, (WM * WN >= 64) ? 1 : 2) void gemm_bf16_kernel
   }
 }
 
+template <bool A_KC, bool B_KC, int WM, int WN>
+__global__ __launch_bounds__(256, (WM * WN >= 64) ? 1 : 2) void gemm_bf16_kernel(GemmArgs g) {
+  gemm_tile<A_KC, B_KC, WM, WN>(g, blockIdx.x, blockIdx.y, blockIdx.z, true);
+}
+
+// Grouped GEMM: many independent GEMMs of one operand form and tile shape in one launch
+// (ViT weight gradients: every layer's dW = X^T dY shares K = rows of the batch, and one
+// launch of all of them fills the chip where each alone ran one latency-bound wave of
+// workgroups).  prefix[i] = first block of GEMM i (tiles_m * tiles_n * split_k blocks each).
+template <bool A_KC, bool B_KC, int WM, int WN>
+__global__ __launch_bounds__(256, (WM * WN >= 64) ? 1 : 2) void gemm_grouped_kernel(const GemmArgs* gs, const int* prefix,
+                                                                                   int n) {
+  // XCD-aware: blocks are dealt round-robin to the 8 XCDs; give each XCD a contiguous run of
+  // logical blocks so the output tiles of one K slice (which read the same A/B rows) share an L2.
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int blk = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (prefix[mid] <= blk) lo = mid; else hi = mid - 1;
+  }
+  const GemmArgs& g = gs[lo];
+  const int local = blk - prefix[lo];
+  const int tiles = g.tiles_m * g.tiles_n;
+  gemm_tile<A_KC, B_KC, WM, WN>(g, local % tiles, 0, local / tiles, false);
+}
+
+template <int WM, int WN>
+static constexpr size_t gemm_lds() {   // dynamic LDS of one workgroup (k-tile ring vs epilogue staging)
+  constexpr int BM = 32 * WM, BN = 32 * WN;
+  constexpr size_t stage = GemmStages<WM, WN>::S * (size_t)(BM + BN) * 64 * 2;
+  constexpr int CH = BM * (BN + 4) * 4 <= 96 * 1024 ? BM : 64;   // epilogue staging rows (as in the kernel)
+  constexpr size_t ctile = (size_t)CH * (BN + 4) * 4 + (BM == 64 && BN == 128 ? 3 * 4 * 128 * 4 : 0);   // + LN reductions
+  return stage > ctile ? stage : ctile;
+}
+
 template <bool AK, bool BK, int WM, int WN>
 static hipError_t launch_t(const GemmArgs& a, int batch, hipStream_t s) {
   constexpr int BM = 32 * WM, BN = 32 * WN;
   GemmArgs g = a;
   g.tiles_m = (int)((g.M + BM - 1) / BM);
   g.tiles_n = (int)((g.N + BN - 1) / BN);
-  const size_t stage = GemmStages<WM, WN>::S * (size_t)(BM + BN) * 64 * 2;
-  constexpr int CH = BM * (BN + 4) * 4 <= 96 * 1024 ? BM : 64;   // epilogue staging rows (as in the kernel)
-  const size_t ctile = (size_t)CH * (BN + 4) * 4 + (BM == 64 && BN == 128 ? 3 * 4 * 128 * 4 : 0);   // + LN reductions
-  const size_t lds = stage > ctile ? stage : ctile;
+  constexpr size_t lds = gemm_lds<WM, WN>();
   dim3 grid(g.tiles_m * g.tiles_n, batch, g.split_k > 1 ? g.split_k : 1);
   static bool attr = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
   if (!attr) {
@@ -921,4 +957,76 @@ extern "C" int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, in
   g.ln_x = ln_x; g.ld_lnx = ld_lnx; g.ln_dscale = ln_dscale; g.ln_dbias = ln_dbias; g.colsum = colsum;
   hipError_t e = launch_sz<2, 4>(g, trans_a, trans_b, 1, (hipStream_t)stream);
   return e == hipSuccess ? 0 : (int)e;
+}
+
+// ------------------------------------------------------------- grouped GEMM
+// Plan (host, once): descriptors -> GemmArgs + block prefix in a caller-owned device buffer;
+// run (stream-ordered, graph-capturable): one launch.  Weight-gradient form only:
+// C[M,N] (fp32) += alpha * A^T B with A [K][M] and B [K][N] (both M/N-contiguous), split-K
+// fp32 atomics (split_k > 1) or read-add-write (split_k == 1), 64 x 64 or 128 x 128 tiles.  No two
+// descriptors of one plan may write the same C.
+struct PcvGemmDesc {
+  const void* A; const void* B; float* C;
+  int64_t M, N, K, lda, ldb, ldc;
+  float alpha; int split_k;
+};
+
+extern "C" int64_t pcv_gemm_grouped_plan_size(int n) {
+  return n <= 0 ? 0 : (int64_t)((n * sizeof(GemmArgs) + 255) / 256 * 256 + (n + 1) * sizeof(int));
+}
+extern "C" int pcv_gemm_desc_size(void) { return (int)sizeof(PcvGemmDesc); }
+
+extern "C" int pcv_gemm_grouped_plan(const void* descs, int n, int tile, void* plan_dev, int64_t* total_blocks) {
+  if (n <= 0 || !descs || !plan_dev || !total_blocks || (tile != 64 && tile != 128)) return PCV_EINVAL;
+  const PcvGemmDesc* d = (const PcvGemmDesc*)descs;
+  std::vector<GemmArgs> gs(n);
+  std::vector<int> prefix(n + 1);
+  int64_t tot = 0;
+  for (int i = 0; i < n; ++i) {
+    const PcvGemmDesc& e = d[i];
+    if (e.M <= 0 || e.N <= 0 || e.K <= 0 || (e.lda & 7) || (e.ldb & 7) || !pcv_aligned16(e.A) || !pcv_aligned16(e.B))
+      return PCV_EALIGN;
+    GemmArgs g{};
+    g.A = (const bf16*)e.A; g.B = (const bf16*)e.B; g.C = e.C;
+    g.M = e.M; g.N = e.N; g.K = e.K; g.lda = e.lda; g.ldb = e.ldb; g.ldc = e.ldc;
+    g.alpha = e.alpha; g.beta = 1.f; g.out_f32 = 1; g.res_scale = 1.f;
+    g.drop_scale = 1.f; g.glds_ok = 1;
+    g.vec_ok = pcv_aligned16(e.C) && (e.ldc % 4 == 0);
+    int split = e.split_k < 1 ? 1 : e.split_k;
+    const int64_t kps = ((e.K + split - 1) / split + 63) / 64 * 64;
+    g.split_k = (int)((e.K + kps - 1) / kps);
+    g.k_per_split = kps;
+    g.tiles_m = (int)((e.M + tile - 1) / tile);
+    g.tiles_n = (int)((e.N + tile - 1) / tile);
+    prefix[i] = (int)tot;
+    tot += (int64_t)g.tiles_m * g.tiles_n * g.split_k;
+    gs[i] = g;
+  }
+  prefix[n] = (int)tot;
+  const size_t off = (n * sizeof(GemmArgs) + 255) / 256 * 256;
+  hipError_t e = hipMemcpy(plan_dev, gs.data(), n * sizeof(GemmArgs), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy((char*)plan_dev + off, prefix.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice);
+  *total_blocks = tot;
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+template <int W>
+static void grouped_launch(const void* plan_dev, int n, int64_t total_blocks, hipStream_t s) {
+  constexpr size_t lds = gemm_lds<W, W>();
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_grouped_kernel<false, false, W, W>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const size_t off = (n * sizeof(GemmArgs) + 255) / 256 * 256;
+  hipLaunchKernelGGL((gemm_grouped_kernel<false, false, W, W>), dim3((unsigned)total_blocks), dim3(256), lds, s,
+                     (const GemmArgs*)plan_dev, (const int*)((const char*)plan_dev + off), n);
+}
+
+extern "C" int pcv_gemm_grouped_run(const void* plan_dev, int n, int tile, int64_t total_blocks, void* stream) {
+  if (n <= 0 || total_blocks <= 0 || !plan_dev || (tile != 64 && tile != 128)) return PCV_EINVAL;
+  if (tile == 64) grouped_launch<2>(plan_dev, n, total_blocks, (hipStream_t)stream);
+  else grouped_launch<4>(plan_dev, n, total_blocks, (hipStream_t)stream);
+  return pcv_launch_status();
 }

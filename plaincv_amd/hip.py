@@ -24,6 +24,10 @@ SIGNATURES = {
                       F32, F32, I32, P, P, I64, I64, I32, F32, P, I64, I32, F32, P, U32, P, I32, P],
     "pcv_gemm_ln": [P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, F32, P, P, I64, F32, P, U32, I32, P, P, F32,
                     P, I64, P, P, P, I64, P, P, P, P],
+    "pcv_gemm_grouped_plan_size": [I32],
+    "pcv_gemm_desc_size": [],
+    "pcv_gemm_grouped_plan": [P, I32, I32, P, P],
+    "pcv_gemm_grouped_run": [P, I32, I32, I64, P],
     "pcv_attn_fwd": [P, P, P, I64, P, I64, P, I32, I32, I32, I32, I32, F32, P, P],
     "pcv_attn_bwd": [P, P, P, I64, P, I64, P, I64, P, P, P, P, P, I64, I32, I32, I32, I32, I32,
                      F32, P, P],
@@ -63,7 +67,7 @@ SIGNATURES = {
 }
 
 # non-status return types (everything else returns an int status)
-RESTYPES = {"pcv_attn_mask_words": I64}
+RESTYPES = {"pcv_attn_mask_words": I64, "pcv_gemm_grouped_plan_size": I64}
 
 _lib = None
 _err = None

@@ -127,6 +127,49 @@ def gemm_ln(a, b, out, *, ln_mode, res, ln_scale, ln_y, ln_mean, ln_rstd, ta=Fal
     return out
 
 
+class GroupedWGrad:
+    """Deferred weight gradients: C += alpha * A^T B for a fixed list of (A [K,M], B [K,N], C fp32 [M,N])
+    views, all in ONE launch (pcv_gemm_grouped_run).  split_k: per-GEMM K split (fp32 atomics);
+    None picks a split so the whole launch holds ~target_blocks workgroups.  tile: 64 or 128
+    (output tile edge; env PCV_WGRAD_TILE overrides)."""
+
+    def __init__(self, items, device, split_k=None, target_blocks=None, tile=None):
+        import os
+        import ctypes
+        import numpy as np
+        lib = hip.load()
+        _chk(lib.pcv_gemm_desc_size() == 80, "gemm desc size")
+        tile = int(os.environ.get("PCV_WGRAD_TILE", tile or 64))
+        if target_blocks is None:
+            target_blocks = int(os.environ.get("PCV_WGRAD_BLOCKS", 1024 if tile == 64 else 512))
+        self.tile = tile
+        tiles = [math.ceil(a.shape[1] / tile) * math.ceil(b.shape[1] / tile) for a, b, _, _ in items]
+        if split_k is None:
+            split_k = max(1, round(target_blocks / max(1, sum(tiles))))
+        raw = bytearray()
+        self._keep = []
+        for (a, b, c, alpha), t in zip(items, tiles):
+            K_, M = a.shape
+            K2, N = b.shape
+            _chk(K_ == K2 and tuple(c.shape) == (M, N) and a.dtype == BF16 and b.dtype == BF16 and c.dtype == F32,
+                 "grouped wgrad operand shapes")
+            _chk(c.stride(1) == 1, "grouped wgrad C must be row-contiguous")
+            s = max(1, min(split_k, K_ // 256))
+            raw += np.array([a.data_ptr(), b.data_ptr(), c.data_ptr()], dtype=np.uint64).tobytes()
+            raw += np.array([M, N, K_, _ld(a), _ld(b), c.stride(0)], dtype=np.int64).tobytes()
+            raw += np.array([alpha], dtype=np.float32).tobytes() + np.array([s], dtype=np.int32).tobytes()
+            self._keep += [a, b, c]
+        self.n = len(items)
+        self.plan = torch.empty(lib.pcv_gemm_grouped_plan_size(self.n), dtype=torch.uint8, device=device)
+        buf = ctypes.create_string_buffer(bytes(raw), len(raw))
+        total = ctypes.c_int64(0)
+        hip.call("pcv_gemm_grouped_plan", ctypes.addressof(buf), self.n, self.tile, ptr(self.plan), ctypes.addressof(total))
+        self.blocks = total.value
+
+    def __call__(self):
+        hip.call("pcv_gemm_grouped_run", ptr(self.plan), self.n, self.tile, self.blocks, stream_ptr())
+
+
 class TransposeBatch:
     """dst[c][r] = src[r][c] for a fixed list of (src, dst) bf16 2-D views, one launch."""
 

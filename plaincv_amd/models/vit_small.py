@@ -128,14 +128,14 @@ class VisionTransformer:
                 out[name] = _lecun_normal(shp, shp[0], gen)
         return out
 
-    def bind(self, store, image_shape, device, side_stream=False):
-        return ViTRunner(self, store, image_shape, device, side_stream=side_stream)
+    def bind(self, store, image_shape, device, side_stream=False, grouped_wgrad=True):
+        return ViTRunner(self, store, image_shape, device, side_stream=side_stream, grouped_wgrad=grouped_wgrad)
 
 
 class ViTRunner:
     """Fixed-shape forward/backward executor for one batch geometry."""
 
-    def __init__(self, model: VisionTransformer, store: ParamStore, image_shape, device, side_stream=False):
+    def __init__(self, model: VisionTransformer, store: ParamStore, image_shape, device, side_stream=False, grouped_wgrad=True):
         self.m = model
         self.s = store
         B, Hh, Ww, C = image_shape
@@ -208,6 +208,16 @@ class ViTRunner:
         self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
         self.seed = torch.zeros(1, dtype=torch.int32, device=dev)
         self._views()
+        # Weight gradients deferred to ONE grouped launch at the end of backward: each dW GEMM
+        # alone is a few dozen 64x64 output tiles over K = B*T rows, a latency-bound partial
+        # wave; all of them together fill the chip (csrc/gemm.hip gemm_grouped_kernel).
+        self.wgrad = None
+        if grouped_wgrad and self.side is None and dev.type == "cuda":
+            items = [(self.yf, self.dlogits_b, self.gWh, 1.0), (self.patches, self.dpatch, self.gWconv, 1.0)]
+            for i, w in enumerate(self.w):
+                items += [(self.a[i], self.dym[i], w["gW1"], 1.0), (self.y1[i], self.dh[i], w["gW0"], 1.0),
+                          (self.o[i], self.dxb_mid[i], w["gWo"], 1.0), (self.y0[i], self.dqkv[i], w["gWqkv"], 1.0)]
+            self.wgrad = K.GroupedWGrad(items, dev)
 
     # ------------------------------------------------------------ views
     def _views(self):
@@ -335,7 +345,8 @@ class ViTRunner:
         # head
         K.dropout_bwd_cast(self.dlogits, self.dlogits_b) if self.Kc % 4 == 0 else self.dlogits_b.copy_(self.dlogits)
         with self._fork():
-            K.gemm(self.yf, self.dlogits_b, self.gWh, ta=True, beta=1.0)
+            if self.wgrad is None:
+                K.gemm(self.yf, self.dlogits_b, self.gWh, ta=True, beta=1.0)
             K.colsum(self.dlogits, self.gbh)
         K.gemm(self.dlogits_b, self.Wh, self.dyf, tb=True)
         self.dx.zero_()
@@ -357,13 +368,15 @@ class ViTRunner:
                 K.dropout_bwd_cast(dx_in, dym, rate, seed, site_mlp_out(i))
                 K.colsum(dym, w["gb1"])
             with self._fork():
-                K.gemm(self.a[i], dym, w["gW1"], ta=True, beta=1.0)
+                if self.wgrad is None:
+                    K.gemm(self.a[i], dym, w["gW1"], ta=True, beta=1.0)
             K.gemm(dym, w["W1"], dh, tb=True, aux=self.h[i], act=K.EPI_GELU_BWD, drop_rate=rate,
                    seed=seed, site=site_mlp_hidden(i), colsum=w["gb0"] if self.side is None else None)
             with self._fork():
                 if self.side is not None:
                     K.colsum(dh, w["gb0"])
-                K.gemm(self.y1[i], dh, w["gW0"], ta=True, beta=1.0)
+                if self.wgrad is None:
+                    K.gemm(self.y1[i], dh, w["gW0"], ta=True, beta=1.0)
             if self.fuse_ln:   # dgrad + LayerNorm_1 backward + residual + its parameter and bias grads
                 K.gemm_ln(dh, w["W0"], dx_mid, tb=True, ln_mode=2, res=dx_in, ln_scale=w["s1"], ln_y=dxb_mid,
                           ln_mean=self.st1[i][0], ln_rstd=self.st1[i][1], ln_x=self.x1s[i], ln_dscale=w["gs1"],
@@ -379,14 +392,16 @@ class ViTRunner:
                 K.dropout_bwd_cast(dx_mid, dxb_mid)
             # attention: x1 = x + out(attn(qkv(ln0(x))))
             with self._fork():
-                K.gemm(self.o[i], dxb_mid, w["gWo"], ta=True, beta=1.0)
+                if self.wgrad is None:
+                    K.gemm(self.o[i], dxb_mid, w["gWo"], ta=True, beta=1.0)
                 if not self.fuse_ln:
                     K.colsum(dx_mid, w["gbo"])
             K.gemm(dxb_mid, w["Wo"], self.do, tb=True)
             K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
                        causal=False, drop_rate=rate, mask=self._mask(i))
             with self._fork():
-                K.gemm(self.y0[i], dqkv, w["gWqkv"], ta=True, beta=1.0)
+                if self.wgrad is None:
+                    K.gemm(self.y0[i], dqkv, w["gWqkv"], ta=True, beta=1.0)
                 K.colsum(dqkv, w["gbqkv"])
             if self.fuse_ln:   # + the dropout backward / bias column sum of the block below's MLP output
                 below = i > 0
@@ -408,7 +423,10 @@ class ViTRunner:
         K.vit_embed_bwd(dx_in, self.dpatch, self.gcls, self.gpos, None, B, T, D, rate, seed, SITE_EMBED)
         with self._fork():
             K.colsum(self.dpatch, self.gbconv)
-            K.gemm(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
+            if self.wgrad is None:
+                K.gemm(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
+        if self.wgrad is not None:
+            self.wgrad()
         if self.side is not None:
             torch.cuda.current_stream().wait_stream(self.side)
 

@@ -330,6 +330,36 @@ def test_gemm_colsum_epilogue(dev, M, N, K):
     assert torch.allclose(cs - 1.0, ref.sum(0), atol=5e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("tile", [64, 128])
+def test_grouped_wgrad(dev, tile):
+    """One grouped launch of weight-gradient GEMMs == separate fp32 A^T B accumulations."""
+    from plaincv_amd import kernels as K_
+    torch.manual_seed(9)
+    shapes = [(16640, 128, 384), (16640, 128, 128), (16640, 128, 512), (16640, 512, 128), (300, 72, 40),
+              (64, 8, 8)]
+    items, refs = [], []
+    for Kd, M, N in shapes:
+        a = torch.randn(Kd, M, device=dev).to(torch.bfloat16)
+        b = torch.randn(Kd, N, device=dev).to(torch.bfloat16)
+        c = torch.randn(M, N, device=dev)
+        refs.append(c + 0.5 * (a.float().t() @ b.float()))
+        items.append((a, b, c, 0.5))
+    g = K_.GroupedWGrad(items, dev, tile=tile)
+    g()
+    torch.cuda.synchronize()
+    for (a, b, c, _), ref in zip(items, refs):
+        err = (c - ref).abs().max().item()
+        assert err < 2e-3 * max(1.0, ref.abs().max().item()), err
+    # a second run accumulates again (beta = 1 semantics)
+    for (a, b, c, _), ref in zip(items, refs):
+        c.copy_(ref)
+    g()
+    torch.cuda.synchronize()
+    for (a, b, c, _), ref in zip(items, refs):
+        ref2 = ref + 0.5 * (a.float().t() @ b.float())
+        assert (c - ref2).abs().max().item() < 2e-3 * max(1.0, ref2.abs().max().item())
+
+
 def test_transpose_batch(dev):
     from plaincv_amd import kernels as K_
     torch.manual_seed(8)
