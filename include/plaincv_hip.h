@@ -28,6 +28,10 @@ extern "C" {
  * (trans_b=0) or [N,K].  Epilogue: +bias[N] -> act (1 GELU-tanh, writes the
  * pre-activation to aux; 2 multiplies by gelu'(aux)) -> dropout -> +res_scale*res
  * -> store (bf16, or fp32 with C = v + beta*C; split_k>1 = fp32 atomic accumulate).
+ * colsum (optional, fp32) += column sums of the stored tile.  col_reps > 1: colsum (and
+ * pcv_gemm_ln's ln_dscale / ln_dbias) is a [col_reps][N] block and workgroup b adds into row
+ * b % col_reps (spreads the float atomics of hundreds of workgroups over several rows); the
+ * caller folds the rows, e.g. with a zero_after column-sum job of pcv_gemm_grouped.
  * Replaces every flax nn.Dense / DenseGeneral / Conv(patch) contraction:
  * models/vit_small.py:13-16,41-45,78-88,126; models/LM/transformer.py:194-201,
  * 246-253,110-134,393-405 and their autodiff transposes. */
@@ -37,7 +41,8 @@ int pcv_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, i
                   float alpha, float beta, int out_f32,
                   const float* bias, const void* res, int64_t ldr, int64_t stride_r, int res_f32, float res_scale,
                   void* aux, int64_t ldaux, int act,
-                  float dropout_rate, const uint32_t* seed, uint32_t site, float* colsum, int split_k, void* stream);
+                  float dropout_rate, const uint32_t* seed, uint32_t site, float* colsum, int col_reps, int split_k,
+                  void* stream);
 
 /* GEMM + LayerNorm over each complete output row (N <= 128, N % 8 == 0; ViT residual stream).
  * ln_mode 1: C = x1 = alpha*op(A)op(B) + bias (+dropout) + res (fp32); ln_y = bf16 LN(x1),
@@ -49,13 +54,18 @@ int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, int64_t N, in
                 int64_t ldc, int trans_a, int trans_b, float alpha, const float* bias, const float* res, int64_t ldr,
                 float dropout_rate, const uint32_t* seed, uint32_t site, int ln_mode, const float* ln_scale,
                 const float* ln_bias, float ln_eps, void* ln_y, int64_t ld_lny, float* ln_mean, float* ln_rstd,
-                const float* ln_x, int64_t ld_lnx, float* ln_dscale, float* ln_dbias, float* colsum, void* stream);
+                const float* ln_x, int64_t ld_lnx, float* ln_dscale, float* ln_dbias, float* colsum, int col_reps,
+                void* stream);
 
 /* Grouped weight-gradient GEMM: n independent C_i[M,N] (fp32) += alpha_i * A_i^T B_i with
  * A_i [K][M], B_i [K][N] bf16 (row strides lda/ldb % 8 == 0, 16-B aligned bases), each split
  * split_k_i ways over K (fp32 atomics), ONE launch for all of them -- the flax autodiff
  * kernel gradients of every Dense in a backward pass (models/vit_small.py:41-45,78-88).
- * Descriptor (pcv_gemm_desc_size() bytes): {A, B, C, M, N, K, lda, ldb, ldc, alpha, split_k}.
+ * Descriptor (pcv_gemm_desc_size() bytes): {A, B, C, M, N, K, lda, ldb, ldc, alpha, split_k, kind, a_f32,
+ * zero_after, pad}.
+ * kind 1 = column-sum job in the same launch (bias gradients): C[c] += sum_r A[r, c] over A
+ * [M][N] (bf16, or fp32 if a_f32; N % 8 == 0), rows split split_k ways; zero_after (fp32 only)
+ * resets A after reading it (the fold of col_reps replica rows, below).
  * plan: host descriptors -> device plan buffer (pcv_gemm_grouped_plan_size(n) bytes, caller
  * owned, synchronous copy); run: stream-ordered, graph-capturable.  No two descriptors of a
  * plan may share a C. */

@@ -353,23 +353,28 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
 // delta[b,h,q] = sum_d dO[q,d] * O[q,d]
 template <int DH>
 __global__ void attn_bwd_delta_kernel(AttnArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // over B*T*H
-  const int64_t n = (int64_t)a.B * a.T * a.H;
-  if (i >= n) return;
+  // delta[b,h,t] = <o, dO> over one head: DH/8 lanes per (row, head), 16 B each (coalesced
+  // across the row), reduced by lane shuffles
+  constexpr int LPR = DH / 8;
+  const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = (int64_t)a.B * a.T * a.H * LPR;
+  const int64_t i = gi / LPR;
+  const int c = (int)(gi % LPR) * 8;
   const int h = (int)(i % a.H);
   const int64_t row = i / a.H;  // b*T + t
-  const bf16* o = a.o + row * a.ldo + h * DH;
-  const bf16* d = a.dout + row * a.lddo + h * DH;
   float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < DH; c += 8) {
-    bf16x8 x = *reinterpret_cast<const bf16x8*>(o + c);
-    bf16x8 y = *reinterpret_cast<const bf16x8*>(d + c);
+  if (gi < n) {
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(a.o + row * a.ldo + h * DH + c);
+    const bf16x8 y = *reinterpret_cast<const bf16x8*>(a.dout + row * a.lddo + h * DH + c);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += bf2f(x[j]) * bf2f(y[j]);
   }
-  const int64_t b = row / a.T, t = row % a.T;
-  a.delta[(b * a.H + h) * a.T + t] = s;
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (gi < n && c == 0) {
+    const int64_t b = row / a.T, t = row % a.T;
+    a.delta[(b * a.H + h) * a.T + t] = s;
+  }
 }
 
 // --------------------------------------------------------- bwd: dK, dV
@@ -679,7 +684,8 @@ static void launch_fwd(const AttnArgs& a, hipStream_t s) {
 template <int DH, bool C, bool D>
 static void launch_bwd(const AttnArgs& a, hipStream_t s) {
   const int64_t n = (int64_t)a.B * a.T * a.H;
-  hipLaunchKernelGGL((attn_bwd_delta_kernel<DH>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+  const int64_t nd = n * (DH / 8);
+  hipLaunchKernelGGL((attn_bwd_delta_kernel<DH>), dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a);
   dim3 grid((a.T + 127) / 128, a.H, a.B);
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH, C, D>), grid, dim3(256), 0, s, a);
   hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, C, D>), grid, dim3(256), 0, s, a);

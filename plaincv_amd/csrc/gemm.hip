@@ -51,7 +51,40 @@ struct GemmArgs {
   float* ln_mean; float* ln_rstd;
   const float* ln_x; int64_t ld_lnx;
   float* ln_dscale; float* ln_dbias; float* colsum;
+  // column accumulators (colsum, ln_dscale, ln_dbias) replicated over col_reps rows of N:
+  // workgroup b adds into row b % col_reps, so no single row takes every workgroup's atomics
+  // (one contended row runs ~14x below the chip's float-atomic rate); the caller folds the
+  // replicas (pcv_gemm_grouped column-sum jobs with zero_after)
+  int col_reps;
 };
+
+__device__ __forceinline__ int64_t col_rep_off(const GemmArgs& g) {
+  return g.col_reps > 1 ? (int64_t)(blockIdx.x % g.col_reps) * g.N : 0;
+}
+
+#ifdef PCV_GEMM_TIMING
+// debug builds only: per-workgroup phase timestamps (s_memrealtime, 100 MHz) + HW_ID / XCC_ID
+__device__ uint64_t* pcv_gemm_timing_buf;
+#define PCV_TREC(slot)                                                                        \
+  do {                                                                                        \
+    if (threadIdx.x == 0 && pcv_gemm_timing_buf)                                              \
+      pcv_gemm_timing_buf[(size_t)(blockIdx.x + gridDim.x * blockIdx.z) * 8 + (slot)] =       \
+          (slot) == 7 ? ((uint64_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |                \
+                         ((uint64_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32))         \
+                      : __builtin_amdgcn_s_memrealtime();                                     \
+  } while (0)
+extern "C" int pcv_debug_gemm_timing(void* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(pcv_gemm_timing_buf), &buf, sizeof(buf));
+}
+__device__ int pcv_dbg_nostore;
+#define PCV_DBG_STORE (!pcv_dbg_nostore)
+extern "C" int pcv_debug_gemm_nostore(int v) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(pcv_dbg_nostore), &v, sizeof(v));
+}
+#else
+#define PCV_TREC(slot) do {} while (0)
+#define PCV_DBG_STORE true
+#endif
 
 template <int R>
 struct KCTile {  // R rows x 64 k, image [R][64] bf16, 128-B rows, chunk swizzle
@@ -60,10 +93,17 @@ struct KCTile {  // R rows x 64 k, image [R][64] bf16, 128-B rows, chunk swizzle
 
 __device__ __forceinline__ u32x4 load_chunk8(const bf16* p, int nvalid) {
   if (nvalid >= 8) return *reinterpret_cast<const u32x4*>(p);
-  union { u32x4 v; bf16 h[8]; } u;
-  u.v = u32x4{0u, 0u, 0u, 0u};
-  for (int i = 0; i < nvalid; ++i) u.h[i] = p[i];
-  return u.v;
+  // ragged edge: element-wise, assembled in registers (a union indexed by a runtime count
+  // would live in scratch)
+  const uint16_t* q = reinterpret_cast<const uint16_t*>(p);
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t lo = (2 * i < nvalid) ? q[2 * i] : 0u;
+    const uint32_t hi = (2 * i + 1 < nvalid) ? q[2 * i + 1] : 0u;
+    w[i] = lo | (hi << 16);
+  }
+  return u32x4{w[0], w[1], w[2], w[3]};
 }
 
 // K-contiguous operand: rows [row0,row0+R) of a [rows][K] matrix, k in [k0,k0+64)
@@ -271,6 +311,8 @@ template <int BM>
 struct LnPre {
   f32x4 r[BM / 16][2], x[BM / 16][2];
   float mean[BM / 16], rstd[BM / 16];
+  f32x4 bias[2], scale[2], shift[2];   // this lane's 8 columns
+  uint32_t seed;
 };
 template <int BM>
 __device__ __forceinline__ void ln_prefetch(const GemmArgs& g, int64_t m0, LnPre<BM>& p) {
@@ -292,6 +334,25 @@ __device__ __forceinline__ void ln_prefetch(const GemmArgs& g, int64_t m0, LnPre
       p.rstd[q] = row < g.M ? g.ln_rstd[row] : 0.f;
     }
   }
+  // per-column parameters (N % 8 == 0 and 16-B aligned: checked by pcv_gemm_ln)
+  const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    p.bias[h] = (colok && g.bias) ? *reinterpret_cast<const f32x4*>(g.bias + col + 4 * h) : z;
+    p.scale[h] = colok ? *reinterpret_cast<const f32x4*>(g.ln_scale + col + 4 * h) : z;
+    p.shift[h] = (colok && g.ln_mode == 1) ? *reinterpret_cast<const f32x4*>(g.ln_bias + col + 4 * h) : z;
+  }
+  p.seed = g.drop_thresh ? *g.seedp : 0u;
+}
+
+// sum over the 16 lanes of a DPP row (all 16 receive it): quad butterflies, then the half-row
+// and row mirrors pair the remaining partial sums -- VALU only, no LDS round trips
+__device__ __forceinline__ float dpp_row_sum16(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));  // row_mirror
+  return v;
 }
 
 template <int BM>
@@ -303,16 +364,20 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
   const float invN = 1.f / (float)g.N;
   float bv[8], sc[8], sh[8], cs[8], dsc[8], dbi[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { bv[e] = 0.f; sc[e] = 0.f; sh[e] = 0.f; cs[e] = 0.f; dsc[e] = 0.f; dbi[e] = 0.f; }
-  if (colok) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (g.bias) bv[e] = g.bias[col + e];
-      sc[e] = g.ln_scale[col + e];
-      if (g.ln_mode == 1) sh[e] = g.ln_bias[col + e];
-    }
+  for (int e = 0; e < 4; ++e) {
+    bv[e] = pre.bias[0][e]; bv[e + 4] = pre.bias[1][e];
+    sc[e] = pre.scale[0][e]; sc[e + 4] = pre.scale[1][e];
+    sh[e] = pre.shift[0][e]; sh[e + 4] = pre.shift[1][e];
   }
-  const uint32_t seed = g.drop_thresh ? *g.seedp : 0u;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { cs[e] = 0.f; dsc[e] = 0.f; dbi[e] = 0.f; }
+  const uint32_t seed = pre.seed;
+  // Every global load of this epilogue was prefetched before the main loop and only stores
+  // follow.  One explicit wait here: left to the compiler, the runtime ln_mode branches merge
+  // conservatively and a row iteration could wait for ALL outstanding memory ops, i.e. for
+  // the previous rows' stores (vmcnt counts stores too on gfx9).
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
+  PCV_TREC(6);
 #pragma unroll
   for (int q = 0; q < BM / 16; ++q) {
     const int rr = (tid >> 4) + 16 * q;
@@ -342,11 +407,11 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) { v[e] += rv[e]; s1 += v[e]; s2 += v[e] * v[e]; }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      s1 = dpp_row_sum16(s1);
+      s2 = dpp_row_sum16(s2);
       const float mean = s1 * invN;
       const float rs = rsqrtf(fmaxf(s2 * invN - mean * mean, 0.f) + g.ln_eps);
-      if (colok) {
+      if (colok && PCV_DBG_STORE) {
         *reinterpret_cast<f32x4*>(cp) = f32x4{v[0], v[1], v[2], v[3]};
         *reinterpret_cast<f32x4*>(cp + 4) = f32x4{v[4], v[5], v[6], v[7]};
         bf16x8 y;
@@ -371,10 +436,8 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
         dsc[e] += v[e] * xh[e];
         dbi[e] += v[e];
       }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
-      s1 *= invN;
-      s2 *= invN;
+      s1 = dpp_row_sum16(s1) * invN;
+      s2 = dpp_row_sum16(s2) * invN;
       float dx[8], yv[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) { dx[e] = rv[e] + rs * (gx[e] - s1 - xh[e] * s2); yv[e] = dx[e]; }
@@ -386,7 +449,7 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) cs[e] += colok ? yv[e] : 0.f;
-      if (colok) {
+      if (colok && PCV_DBG_STORE) {
         *reinterpret_cast<f32x4*>(cp) = f32x4{dx[0], dx[1], dx[2], dx[3]};
         *reinterpret_cast<f32x4*>(cp + 4) = f32x4{dx[4], dx[5], dx[6], dx[7]};
         if (g.ln_y) {
@@ -398,30 +461,40 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
       }
     }
   }
+  PCV_TREC(3);
   if (g.ln_mode != 2) return;
-  // column reductions: 4 row-groups per wave by shuffle, 4 waves through LDS, one atomic per column
-  __syncthreads();                        // ct is no longer read; reuse the LDS behind it
-  float* red = const_cast<float*>(ct) + BM * CLD;   // [3][4 waves][128]
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    float a = dsc[e], b = dbi[e], c = cs[e];
-    a += __shfl_xor(a, 16, 64); a += __shfl_xor(a, 32, 64);
-    b += __shfl_xor(b, 16, 64); b += __shfl_xor(b, 32, 64);
-    c += __shfl_xor(c, 16, 64); c += __shfl_xor(c, 32, 64);
-    if (lane < 16) {
-      red[(0 * 4 + wave) * 128 + col + e] = a;
-      red[(1 * 4 + wave) * 128 + col + e] = b;
-      red[(2 * 4 + wave) * 128 + col + e] = c;
-    }
+  // column reductions: every lane's 8-column partials (16 row-groups: 4 per wave) through LDS,
+  // summed per column by one thread, one atomic per column and array
+  __syncthreads();                        // ct is no longer read; reuse its LDS
+  float* red = const_cast<float*>(ct);    // [3][16 partials][128]
+  {
+    const int part = wave * 4 + (lane >> 4);
+    float* r0 = red + part * 128 + col;
+    *reinterpret_cast<f32x4*>(r0) = f32x4{dsc[0], dsc[1], dsc[2], dsc[3]};
+    *reinterpret_cast<f32x4*>(r0 + 4) = f32x4{dsc[4], dsc[5], dsc[6], dsc[7]};
+    *reinterpret_cast<f32x4*>(r0 + 16 * 128) = f32x4{dbi[0], dbi[1], dbi[2], dbi[3]};
+    *reinterpret_cast<f32x4*>(r0 + 16 * 128 + 4) = f32x4{dbi[4], dbi[5], dbi[6], dbi[7]};
+    *reinterpret_cast<f32x4*>(r0 + 32 * 128) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+    *reinterpret_cast<f32x4*>(r0 + 32 * 128 + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
   }
   __syncthreads();
-  if (tid < 128 && tid < g.N) {
-    float a = 0.f, b = 0.f, c = 0.f;
+  PCV_TREC(4);
+  {
+    const int c = tid & 127;
+    if (c < g.N) {
+      auto colsum16 = [&](int arr) {
+        float v = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) { a += red[w * 128 + tid]; b += red[(4 + w) * 128 + tid]; c += red[(8 + w) * 128 + tid]; }
-    if (g.ln_dscale) atomicAdd(g.ln_dscale + tid, a);
-    if (g.ln_dbias) atomicAdd(g.ln_dbias + tid, b);
-    if (g.colsum) atomicAdd(g.colsum + tid, c);
+        for (int p = 0; p < 16; ++p) v += red[(arr * 16 + p) * 128 + c];
+        return v;
+      };
+      if (tid < 128) {
+        if (g.ln_dscale) atomicAdd(g.ln_dscale + col_rep_off(g) + c, colsum16(0));
+        if (g.colsum) atomicAdd(g.colsum + col_rep_off(g) + c, colsum16(2));
+      } else if (g.ln_dbias) {
+        atomicAdd(g.ln_dbias + col_rep_off(g) + c, colsum16(1));
+      }
+    }
   }
 }
 
@@ -442,14 +515,27 @@ struct GemmStages {
       (WM == 2 && WN == 4) ? PCV_GEMM_STAGES_LN : (WM * WN <= 4 ? PCV_GEMM_STAGES_SMALL : PCV_GEMM_STAGES_BIG);
 };
 
+// s_waitcnt until at most P * min(n, N) vector-memory ops of this wave are outstanding
+// (vmcnt needs an immediate: unrolled over the possible counts)
+template <int P, int N>
+__device__ __forceinline__ void wait_tiles(int n) {
+  if constexpr (N <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    static_assert(P * N <= 63, "vmcnt is 6 bits");
+    if (n >= N) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(P * N) : "memory");
+    else wait_tiles<P, N - 1>(n);
+  }
+}
+
+
 // One output tile (bid = tile index, bz = batch index, kz = split-K slice) of the GEMM g.
-template <bool A_KC, bool B_KC, int WM, int WN>
+template <bool A_KC, bool B_KC, int WM, int WN, int S = GemmStages<WM, WN>::S>
 __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz, int kz, bool remap) {
   constexpr int BM = 32 * WM, BN = 32 * WN;
   constexpr int A_BYTES = BM * 64 * 2, B_BYTES = BN * 64 * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int S = GemmStages<WM, WN>::S;
   constexpr int PIECES = (BM + BN) / 32;   // global_load_lds instructions per wave per k-tile
 
   // XCD-aware bijective remap (block ids are dealt round-robin to the 8 XCDs, so each XCD
@@ -485,8 +571,10 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
 #pragma unroll
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  PCV_TREC(0);
+  PCV_TREC(7);
   // the 64 x 128 tile (pcv_gemm_ln) prefetches its LN row operands before the main loop
-  constexpr bool LN_TILE = BM == 64 && BN == 128;
+  constexpr bool LN_TILE = BM <= 64 && BN == 128;   // 64x128 / 32x128: pcv_gemm_ln tiles (whole rows)
   LnPre<LN_TILE ? BM : 16> lnpre;
   if constexpr (LN_TILE) {
     if (g.ln_mode) ln_prefetch<BM>(g, m0, lnpre);
@@ -578,16 +666,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
 #pragma unroll
     for (int i = 0; i < S - 1; ++i) issue(i);
     for (int kt = 0; kt < nfull; ++kt) {
-      if constexpr (S == 4) {
-        if (kt + 2 < nfull) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PIECES) : "memory");
-        else if (kt + 1 < nfull) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PIECES) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else if constexpr (S == 3) {
-        if (kt + 1 < nfull) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PIECES) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      wait_tiles<PIECES, S - 2>(nfull - 1 - kt);   // tile kt landed: later tiles may stay in flight
       __syncthreads();
       issue(kt + S - 1);
       compute(smem + (kt % S) * STAGE);
@@ -612,6 +691,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
     }
   }
   __syncthreads();   // every wave done with the ring before the epilogue reuses the LDS
+  PCV_TREC(1);
 
   // ---------------- epilogue ----------------
   // Stage the fp32 tile through LDS ([CH][BN+4] rows at a time, conflict-free
@@ -670,7 +750,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
       continue;
     }
     if constexpr (LN_TILE) {
-      if (g.ln_mode) { ln_epilogue<BM>(g, ct, m0, lnpre); return; }
+      if (g.ln_mode) { PCV_TREC(2); ln_epilogue<BM>(g, ct, m0, lnpre); PCV_TREC(5); return; }
     }
     if (col >= g.N) continue;
     for (int rr = threadIdx.x / CPR; rr < CH; rr += RPP) {
@@ -782,7 +862,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
     if (threadIdx.x < BN && n0 + threadIdx.x < g.N) {
       float t = 0.f;
       for (int q = 0; q < RPP; ++q) t += red[q * BN + threadIdx.x];
-      atomicAdd(g.colsum + n0 + threadIdx.x, t);
+      atomicAdd(g.colsum + col_rep_off(g) + n0 + threadIdx.x, t);
     }
   }
 }
@@ -796,6 +876,85 @@ __global__ __launch_bounds__(256, (WM * WN >= 64) ? 1 : 2) void gemm_bf16_kernel
 // (ViT weight gradients: every layer's dW = X^T dY shares K = rows of the batch, and one
 // launch of all of them fills the chip where each alone ran one latency-bound wave of
 // workgroups).  prefix[i] = first block of GEMM i (tiles_m * tiles_n * split_k blocks each).
+// k-tiles in flight for the grouped (weight-gradient) launch: long K slices, so deeper rings
+#ifndef PCV_GROUPED_STAGES_64
+#define PCV_GROUPED_STAGES_64 2
+#endif
+#ifndef PCV_GROUPED_STAGES_128
+#define PCV_GROUPED_STAGES_128 2
+#endif
+template <int W>
+struct GroupedStages {
+  static constexpr int S = W == 2 ? PCV_GROUPED_STAGES_64 : PCV_GROUPED_STAGES_128;
+};
+
+// Column-sum job of the grouped launch (bias gradients): out[c] += sum_r x[r, c] over one
+// slice of rows and 64 columns.  256 threads = 8 column groups (16 B each) x 32 row lanes,
+// four rows in flight per lane, reduced through LDS, one atomic per column and block.
+constexpr int GROUPED_JOB_COLSUM = 1;
+
+__device__ __forceinline__ void colsum_job(const GemmArgs& g, int local) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int cb = local % g.tiles_n, slice = local / g.tiles_n;
+  const int tid = threadIdx.x, cg = tid & 7, rl = tid >> 3;
+  const int c0 = cb * 64 + cg * 8;
+  const int64_t r0 = (int64_t)slice * g.k_per_split;
+  const int64_t r1 = min(g.M, r0 + g.k_per_split);
+  f32x4 s0{0.f, 0.f, 0.f, 0.f}, s1{0.f, 0.f, 0.f, 0.f};
+  if (c0 < g.N) {   // N % 8 == 0 (checked at plan time)
+    if (g.res_f32) {
+      const float* x = (const float*)g.A + c0;
+      int64_t r = r0 + rl;
+      for (; r + 96 < r1; r += 128) {
+        f32x4 v[4][2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[u][0] = *reinterpret_cast<const f32x4*>(x + (r + 32 * u) * g.lda);
+          v[u][1] = *reinterpret_cast<const f32x4*>(x + (r + 32 * u) * g.lda + 4);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { s0 += v[u][0]; s1 += v[u][1]; }
+      }
+      for (; r < r1; r += 32) {
+        s0 += *reinterpret_cast<const f32x4*>(x + r * g.lda);
+        s1 += *reinterpret_cast<const f32x4*>(x + r * g.lda + 4);
+      }
+    } else {
+      const bf16* x = g.A + c0;
+      auto acc8 = [&](const bf16x8& v) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { s0[e] += bf2f(v[e]); s1[e] += bf2f(v[e + 4]); }
+      };
+      int64_t r = r0 + rl;
+      for (; r + 96 < r1; r += 128) {
+        bf16x8 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const bf16x8*>(x + (r + 32 * u) * g.lda);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc8(v[u]);
+      }
+      for (; r < r1; r += 32) acc8(*reinterpret_cast<const bf16x8*>(x + r * g.lda));
+    }
+  }
+  if (g.ln_mode && g.res_f32 && c0 < g.N) {   // zero_after: fp32 replica rows are reset for the next pass
+    float* x = (float*)g.A + c0;
+    for (int64_t r = r0 + rl; r < r1; r += 32) {
+      *reinterpret_cast<f32x4*>(x + r * g.lda) = f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(x + r * g.lda + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  float* red = (float*)smem;   // [32 row lanes][64 columns]
+  *reinterpret_cast<f32x4*>(red + rl * 64 + cg * 8) = s0;
+  *reinterpret_cast<f32x4*>(red + rl * 64 + cg * 8 + 4) = s1;
+  __syncthreads();
+  if (tid < 64 && cb * 64 + tid < g.N) {
+    float v = 0.f;
+#pragma unroll 8
+    for (int q = 0; q < 32; ++q) v += red[q * 64 + tid];
+    atomicAdd((float*)g.C + cb * 64 + tid, v);
+  }
+}
+
 template <bool A_KC, bool B_KC, int WM, int WN>
 __global__ __launch_bounds__(256, (WM * WN >= 64) ? 1 : 2) void gemm_grouped_kernel(const GemmArgs* gs, const int* prefix,
                                                                                    int n) {
@@ -811,16 +970,21 @@ __global__ __launch_bounds__(256, (WM * WN >= 64) ? 1 : 2) void gemm_grouped_ker
   }
   const GemmArgs& g = gs[lo];
   const int local = blk - prefix[lo];
+  if (g.act == GROUPED_JOB_COLSUM) {
+    colsum_job(g, local);
+    return;
+  }
   const int tiles = g.tiles_m * g.tiles_n;
-  gemm_tile<A_KC, B_KC, WM, WN>(g, local % tiles, 0, local / tiles, false);
+  gemm_tile<A_KC, B_KC, WM, WN, GroupedStages<WM>::S>(g, local % tiles, 0, local / tiles, false);
 }
 
-template <int WM, int WN>
+template <int WM, int WN, int S = GemmStages<WM, WN>::S>
 static constexpr size_t gemm_lds() {   // dynamic LDS of one workgroup (k-tile ring vs epilogue staging)
   constexpr int BM = 32 * WM, BN = 32 * WN;
-  constexpr size_t stage = GemmStages<WM, WN>::S * (size_t)(BM + BN) * 64 * 2;
+  constexpr size_t stage = S * (size_t)(BM + BN) * 64 * 2;
   constexpr int CH = BM * (BN + 4) * 4 <= 96 * 1024 ? BM : 64;   // epilogue staging rows (as in the kernel)
-  constexpr size_t ctile = (size_t)CH * (BN + 4) * 4 + (BM == 64 && BN == 128 ? 3 * 4 * 128 * 4 : 0);   // + LN reductions
+  constexpr size_t ctile0 = (size_t)CH * (BN + 4) * 4;
+  constexpr size_t ctile = (BN == 128 && ctile0 < 3 * 16 * 128 * 4) ? 3 * 16 * 128 * 4 : ctile0;   // + LN column reductions
   return stage > ctile ? stage : ctile;
 }
 
@@ -864,7 +1028,7 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
                              const float* bias, const void* res, int64_t ldr, int64_t stride_r, int res_f32, float res_scale,
                              void* aux, int64_t ldaux, int act,
                              float drop_rate, const uint32_t* seed, uint32_t site,
-                             float* colsum, int split_k, void* stream) {
+                             float* colsum, int col_reps, int split_k, void* stream) {
   if (M < 0 || N < 0 || K < 0 || batch < 1) return PCV_EINVAL;
   if (colsum && (batch > 1 || split_k > 1)) return PCV_EINVAL;
   if (M == 0 || N == 0) return 0;
@@ -880,6 +1044,7 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
   g.bias = bias; g.res = res; g.ldr = ldr; g.sR = stride_r; g.res_f32 = res_f32; g.res_scale = res_scale;
   g.aux = (bf16*)aux; g.ldaux = ldaux; g.act = act;
   g.colsum = colsum;
+  g.col_reps = col_reps;
   g.drop_thresh = 0; g.drop_scale = 1.f; g.seedp = seed; g.site = site;
   if (drop_rate > 0.f && !seed) return PCV_EINVAL;
   if (drop_rate > 0.f) {
@@ -928,7 +1093,7 @@ extern "C" int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, in
                            const float* res, int64_t ldr, float dropout_rate, const uint32_t* seed, uint32_t site,
                            int ln_mode, const float* ln_scale, const float* ln_bias, float ln_eps, void* ln_y,
                            int64_t ld_lny, float* ln_mean, float* ln_rstd, const float* ln_x, int64_t ld_lnx,
-                           float* ln_dscale, float* ln_dbias, float* colsum, void* stream) {
+                           float* ln_dscale, float* ln_dbias, float* colsum, int col_reps, void* stream) {
   if (M < 0 || N <= 0 || K < 0 || N > 128 || (N & 7) || (ln_mode != 1 && ln_mode != 2)) return PCV_EINVAL;
   if (!res || !ln_scale || !ln_mean || !ln_rstd) return PCV_EINVAL;
   if (ln_mode == 1 && (!ln_bias || !ln_y)) return PCV_EINVAL;
@@ -955,6 +1120,8 @@ extern "C" int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, in
   g.ln_mode = ln_mode; g.ln_scale = ln_scale; g.ln_bias = ln_bias; g.ln_eps = ln_eps;
   g.ln_y = (bf16*)ln_y; g.ld_lny = ld_lny; g.ln_mean = ln_mean; g.ln_rstd = ln_rstd;
   g.ln_x = ln_x; g.ld_lnx = ld_lnx; g.ln_dscale = ln_dscale; g.ln_dbias = ln_dbias; g.colsum = colsum;
+  g.col_reps = col_reps;
+  // 64 x 128 tiles (a 32-row tile doubles every workgroup's weight traffic: measured slower)
   hipError_t e = launch_sz<2, 4>(g, trans_a, trans_b, 1, (hipStream_t)stream);
   return e == hipSuccess ? 0 : (int)e;
 }
@@ -969,6 +1136,10 @@ struct PcvGemmDesc {
   const void* A; const void* B; float* C;
   int64_t M, N, K, lda, ldb, ldc;
   float alpha; int split_k;
+  int kind;      // 0: C += alpha A^T B;  1: column sum C[c] += sum_r A[r, c] (A: M x N, row stride lda, B unused)
+  int a_f32;     // kind 1: A holds fp32 (else bf16)
+  int zero_after;   // kind 1, fp32 A: A is reset to 0 after it is read (replicated accumulators)
+  int pad_;
 };
 
 extern "C" int64_t pcv_gemm_grouped_plan_size(int n) {
@@ -984,6 +1155,24 @@ extern "C" int pcv_gemm_grouped_plan(const void* descs, int n, int tile, void* p
   int64_t tot = 0;
   for (int i = 0; i < n; ++i) {
     const PcvGemmDesc& e = d[i];
+    if (e.kind == GROUPED_JOB_COLSUM) {   // rows split into split_k slices of whole 32-row steps
+      if (e.M <= 0 || e.N <= 0 || (e.N & 7) || !pcv_aligned16(e.A) || !e.C || (e.lda & (e.a_f32 ? 3 : 7)))
+        return PCV_EALIGN;
+      GemmArgs g{};
+      g.A = (const bf16*)e.A; g.C = e.C; g.M = e.M; g.N = e.N; g.lda = e.lda;
+      g.act = GROUPED_JOB_COLSUM; g.res_f32 = e.a_f32 ? 1 : 0;
+      g.ln_mode = (e.zero_after && e.a_f32) ? 1 : 0;
+      const int split = e.split_k < 1 ? 1 : e.split_k;
+      g.k_per_split = ((e.M + split - 1) / split + 31) / 32 * 32;
+      g.split_k = (int)((e.M + g.k_per_split - 1) / g.k_per_split);
+      g.tiles_m = 1;
+      g.tiles_n = (int)((e.N + 63) / 64);
+      prefix[i] = (int)tot;
+      tot += (int64_t)g.tiles_n * g.split_k;
+      gs[i] = g;
+      continue;
+    }
+    if (e.kind != 0) return PCV_EINVAL;
     if (e.M <= 0 || e.N <= 0 || e.K <= 0 || (e.lda & 7) || (e.ldb & 7) || !pcv_aligned16(e.A) || !pcv_aligned16(e.B))
       return PCV_EALIGN;
     GemmArgs g{};
@@ -1012,7 +1201,7 @@ extern "C" int pcv_gemm_grouped_plan(const void* descs, int n, int tile, void* p
 
 template <int W>
 static void grouped_launch(const void* plan_dev, int n, int64_t total_blocks, hipStream_t s) {
-  constexpr size_t lds = gemm_lds<W, W>();
+  constexpr size_t lds = gemm_lds<W, W, GroupedStages<W>::S>();
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_grouped_kernel<false, false, W, W>,

@@ -21,9 +21,9 @@ F32 = ctypes.c_float
 # name -> argtypes (return type is always int status)
 SIGNATURES = {
     "pcv_gemm_bf16": [P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, I64, I64, I64, I64,
-                      F32, F32, I32, P, P, I64, I64, I32, F32, P, I64, I32, F32, P, U32, P, I32, P],
+                      F32, F32, I32, P, P, I64, I64, I32, F32, P, I64, I32, F32, P, U32, P, I32, I32, P],
     "pcv_gemm_ln": [P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, F32, P, P, I64, F32, P, U32, I32, P, P, F32,
-                    P, I64, P, P, P, I64, P, P, P, P],
+                    P, I64, P, P, P, I64, P, P, P, I32, P],
     "pcv_gemm_grouped_plan_size": [I32],
     "pcv_gemm_desc_size": [],
     "pcv_gemm_grouped_plan": [P, I32, I32, P, P],

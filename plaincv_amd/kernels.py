@@ -25,14 +25,15 @@ def _ld(t):
 
 
 def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=None, res_scale=1.0, aux=None,
-         act=EPI_NONE, drop_rate=0.0, seed=None, site=0, split_k=None, colsum=None):
+         act=EPI_NONE, drop_rate=0.0, seed=None, site=0, split_k=None, colsum=None, col_reps=1):
     """out[M,N] = epi(alpha * op(a) @ op(b)).
 
     a: [M,K] (ta=False) or [K,M] (ta=True); b: [K,N] (tb=False) or [N,K] (tb=True).
     Optional leading batch dim on a, b, out (same batch size).  bf16 inputs,
     bf16 or fp32 output (fp32: out = v + beta*out).  Epilogue order:
     +bias -> [gelu (aux<-preact) | *gelu'(aux)] -> dropout -> +res.  colsum (fp32 [N]) += column sums
-    of the stored values (not with split-K or batches)."""
+    of the stored values (not with split-K or batches); col_reps > 1: colsum is [col_reps, N] and
+    workgroup b adds into row b % col_reps (the caller folds the rows)."""
     batched = a.dim() == 3
     if batched:
         nb = a.shape[0]
@@ -81,7 +82,8 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
             raise ValueError("gelu epilogue needs bf16 aux [M,N]")
         ldaux = _ld(aux)
     if colsum is not None:
-        _chk(not batched and colsum.dtype == F32 and colsum.numel() >= N and colsum.is_cuda, "gemm colsum")
+        _chk(not batched and colsum.dtype == F32 and colsum.numel() >= N * max(1, col_reps) and colsum.is_cuda and
+             colsum.is_contiguous(), "gemm colsum")
         split_k = 1
     if split_k is None:
         split_k = 1
@@ -95,18 +97,19 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
     hip.call("pcv_gemm_bf16", ptr(a2), ptr(b2), ptr(o2), M, N, K, _ld(a2), _ld(b2), _ld(o2),
              int(ta), int(tb), nb, sa, sb, sc, float(alpha), float(beta), out_f32,
              ptr(bias), ptr(res), ldr, sr, res_f32, float(res_scale), ptr(aux), ldaux, int(act),
-             float(drop_rate), ptr(seed), int(site) & 0xFFFFFFFF, ptr(colsum), int(split_k), stream_ptr())
+             float(drop_rate), ptr(seed), int(site) & 0xFFFFFFFF, ptr(colsum), int(col_reps), int(split_k),
+             stream_ptr())
     return out
 
 
 def gemm_ln(a, b, out, *, ln_mode, res, ln_scale, ln_y, ln_mean, ln_rstd, ta=False, tb=False, alpha=1.0, bias=None,
             drop_rate=0.0, seed=None, site=0, ln_bias=None, ln_eps=1e-6, ln_x=None, ln_dscale=None, ln_dbias=None,
-            colsum=None):
+            colsum=None, col_reps=1):
     """GEMM whose epilogue completes a LayerNorm over each output row (pcv_gemm_ln, N <= 128).
 
     ln_mode 1: out = x1 = op(a)@op(b)*alpha + bias (+dropout) + res;  ln_y = LN(x1) (bf16), stats out.
     ln_mode 2: dy = op(a)@op(b)*alpha;  out = dx = res + LN_bwd(dy; ln_x, stats, ln_scale); ln_y = bf16(dx);
-               ln_dscale / ln_dbias / colsum accumulate."""
+               ln_dscale / ln_dbias / colsum accumulate ([col_reps, N] replica rows when col_reps > 1)."""
     M, K = (a.shape[1], a.shape[0]) if ta else tuple(a.shape)
     N, K2 = tuple(b.shape) if tb else (b.shape[1], b.shape[0])
     _chk(K == K2 and tuple(out.shape) == (M, N) and tuple(res.shape) == (M, N), "gemm_ln shapes")
@@ -123,32 +126,51 @@ def gemm_ln(a, b, out, *, ln_mode, res, ln_scale, ln_y, ln_mean, ln_rstd, ta=Fal
              int(ln_mode), ptr(ln_scale), ptr(ln_bias), float(ln_eps), ptr(ln_y),
              _ld(ln_y) if ln_y is not None else 0, ptr(ln_mean),
              ptr(ln_rstd), ptr(ln_x), _ld(ln_x) if ln_x is not None else 0, ptr(ln_dscale), ptr(ln_dbias),
-             ptr(colsum), stream_ptr())
+             ptr(colsum), int(col_reps), stream_ptr())
     return out
 
 
 class GroupedWGrad:
-    """Deferred weight gradients: C += alpha * A^T B for a fixed list of (A [K,M], B [K,N], C fp32 [M,N])
-    views, all in ONE launch (pcv_gemm_grouped_run).  split_k: per-GEMM K split (fp32 atomics);
-    None picks a split so the whole launch holds ~target_blocks workgroups.  tile: 64 or 128
-    (output tile edge; env PCV_WGRAD_TILE overrides)."""
+    """Deferred weight/bias gradients in ONE launch (pcv_gemm_grouped_run) for a fixed list of views:
+    GEMM items (A [K,M], B [K,N], C fp32 [M,N], alpha): C += alpha * A^T B, split over K (fp32 atomics);
+    column-sum items ("colsum", X [R,N] bf16|fp32, out fp32 [N]): out += X.sum(0);
+    ("fold", X fp32 [reps,N], out): the same, then X = 0 (replicated column accumulators).
+    split_k None picks a GEMM split so the GEMM jobs hold ~target_blocks workgroups; column sums
+    take ~colsum_rows rows per workgroup.  tile: 64 or 128 (env PCV_WGRAD_TILE overrides)."""
 
-    def __init__(self, items, device, split_k=None, target_blocks=None, tile=None):
+    def __init__(self, items, device, split_k=None, target_blocks=None, tile=None, colsum_rows=512):
         import os
         import ctypes
         import numpy as np
         lib = hip.load()
-        _chk(lib.pcv_gemm_desc_size() == 80, "gemm desc size")
+        _chk(lib.pcv_gemm_desc_size() == 96, "gemm desc size")
         tile = int(os.environ.get("PCV_WGRAD_TILE", tile or 64))
         if target_blocks is None:
             target_blocks = int(os.environ.get("PCV_WGRAD_BLOCKS", 1024 if tile == 64 else 512))
         self.tile = tile
-        tiles = [math.ceil(a.shape[1] / tile) * math.ceil(b.shape[1] / tile) for a, b, _, _ in items]
+        gemms = [it for it in items if not isinstance(it[0], str)]
+        tiles = sum(math.ceil(a.shape[1] / tile) * math.ceil(b.shape[1] / tile) for a, b, _, _ in gemms)
         if split_k is None:
-            split_k = max(1, round(target_blocks / max(1, sum(tiles))))
+            split_k = max(1, round(target_blocks / max(1, tiles)))
         raw = bytearray()
         self._keep = []
-        for (a, b, c, alpha), t in zip(items, tiles):
+        for it in items:
+            if isinstance(it[0], str):
+                _chk(it[0] in ("colsum", "fold"), f"unknown grouped job {it[0]}")
+                kind, x, out = it
+                fold = kind == "fold"
+                _chk(not fold or x.dtype == F32, "fold needs fp32 replicas")
+                R, N = x.shape
+                _chk(x.dtype in (BF16, F32) and out.dtype == F32 and out.is_contiguous() and out.numel() == N and
+                     x.stride(1) == 1 and N % 8 == 0, "grouped colsum operands")
+                raw += np.array([x.data_ptr(), 0, out.data_ptr()], dtype=np.uint64).tobytes()
+                raw += np.array([R, N, 0, x.stride(0), 0, 0], dtype=np.int64).tobytes()
+                raw += np.array([1.0], dtype=np.float32).tobytes()
+                raw += np.array([max(1, math.ceil(R / colsum_rows)), 1, int(x.dtype == F32), int(fold), 0],
+                                dtype=np.int32).tobytes()
+                self._keep += [x, out]
+                continue
+            a, b, c, alpha = it
             K_, M = a.shape
             K2, N = b.shape
             _chk(K_ == K2 and tuple(c.shape) == (M, N) and a.dtype == BF16 and b.dtype == BF16 and c.dtype == F32,
@@ -157,7 +179,7 @@ class GroupedWGrad:
             s = max(1, min(split_k, K_ // 256))
             raw += np.array([a.data_ptr(), b.data_ptr(), c.data_ptr()], dtype=np.uint64).tobytes()
             raw += np.array([M, N, K_, _ld(a), _ld(b), c.stride(0)], dtype=np.int64).tobytes()
-            raw += np.array([alpha], dtype=np.float32).tobytes() + np.array([s], dtype=np.int32).tobytes()
+            raw += np.array([alpha], dtype=np.float32).tobytes() + np.array([s, 0, 0, 0, 0], dtype=np.int32).tobytes()
             self._keep += [a, b, c]
         self.n = len(items)
         self.plan = torch.empty(lib.pcv_gemm_grouped_plan_size(self.n), dtype=torch.uint8, device=device)

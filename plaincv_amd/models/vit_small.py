@@ -212,11 +212,38 @@ class ViTRunner:
         # alone is a few dozen 64x64 output tiles over K = B*T rows, a latency-bound partial
         # wave; all of them together fill the chip (csrc/gemm.hip gemm_grouped_kernel).
         self.wgrad = None
+        self.rep_ws, self.reps = {}, 1
         if grouped_wgrad and self.side is None and dev.type == "cuda":
             items = [(self.yf, self.dlogits_b, self.gWh, 1.0), (self.patches, self.dpatch, self.gWconv, 1.0)]
             for i, w in enumerate(self.w):
                 items += [(self.a[i], self.dym[i], w["gW1"], 1.0), (self.y1[i], self.dh[i], w["gW0"], 1.0),
                           (self.o[i], self.dxb_mid[i], w["gWo"], 1.0), (self.y0[i], self.dqkv[i], w["gWqkv"], 1.0)]
+            # bias gradients that are plain column sums ride along as column-sum jobs
+            items += [("colsum", self.dqkv[i], w["gbqkv"]) for i, w in enumerate(self.w)]
+            items.append(("colsum", self.dpatch, self.gbconv))
+            # MLP-out bias of the blocks whose dym is not produced by a fused LayerNorm backward
+            for i, w in enumerate(self.w):
+                if not (self.fuse_ln and i + 1 < len(self.w)):
+                    items.append(("colsum", self.dym[i], w["gb1"]))
+            self.head_bias_grouped = self.Kc % 8 == 0
+            if self.head_bias_grouped:
+                items.append(("colsum", self.dlogits, self.gbh))
+            # Column accumulators written by every row tile of a GEMM epilogue (bias and LayerNorm
+            # parameter gradients) go to 32 replica rows, folded into the gradients by the same launch
+            self.reps = 32
+
+            def replicate(key, target):
+                ws = torch.zeros(self.reps, target.numel(), dtype=f32, device=dev)
+                self.rep_ws[key] = ws
+                items.append(("fold", ws, target.view(-1)))
+
+            for i, w in enumerate(self.w):
+                replicate(("gb0", i), w["gb0"])
+                if self.fuse_ln:
+                    for k in ("gs1", "gc1", "gbo", "gs0", "gc0"):
+                        replicate((k, i), w[k])
+                    if i + 1 < len(self.w):
+                        replicate(("gb1", i), w["gb1"])   # produced by the LayerNorm_0 backward of block i+1
             self.wgrad = K.GroupedWGrad(items, dev)
 
     # ------------------------------------------------------------ views
@@ -258,6 +285,11 @@ class ViTRunner:
             self.gsf, self.gcf = G["LayerNorm_0/scale"], G["LayerNorm_0/bias"]
         self.Wh, self.bh = W["Dense_0/kernel"], P["Dense_0/bias"]
         self.gWh, self.gbh = G["Dense_0/kernel"], G["Dense_0/bias"]
+
+    def _acc(self, key, target):
+        """Column-accumulator destination: the replica block when one exists, else the gradient itself."""
+        ws = self.rep_ws.get(key)
+        return (target, 1) if ws is None else (ws, self.reps)
 
     def _mask(self, i):
         w = self.mask_words
@@ -347,7 +379,8 @@ class ViTRunner:
         with self._fork():
             if self.wgrad is None:
                 K.gemm(self.yf, self.dlogits_b, self.gWh, ta=True, beta=1.0)
-            K.colsum(self.dlogits, self.gbh)
+            if self.wgrad is None or not self.head_bias_grouped:
+                K.colsum(self.dlogits, self.gbh)
         K.gemm(self.dlogits_b, self.Wh, self.dyf, tb=True)
         self.dx.zero_()
         dxc = self.dx.view(B, T * D)[:, :D]
@@ -366,21 +399,24 @@ class ViTRunner:
             # LayerNorm_0 backward epilogue of the block above)
             if not (self.fuse_ln and i + 1 < m.num_layers):
                 K.dropout_bwd_cast(dx_in, dym, rate, seed, site_mlp_out(i))
-                K.colsum(dym, w["gb1"])
+                if self.wgrad is None:
+                    K.colsum(dym, w["gb1"])
             with self._fork():
                 if self.wgrad is None:
                     K.gemm(self.a[i], dym, w["gW1"], ta=True, beta=1.0)
+            gb0, reps = self._acc(("gb0", i), w["gb0"])
             K.gemm(dym, w["W1"], dh, tb=True, aux=self.h[i], act=K.EPI_GELU_BWD, drop_rate=rate,
-                   seed=seed, site=site_mlp_hidden(i), colsum=w["gb0"] if self.side is None else None)
+                   seed=seed, site=site_mlp_hidden(i), colsum=gb0 if self.side is None else None, col_reps=reps)
             with self._fork():
                 if self.side is not None:
                     K.colsum(dh, w["gb0"])
                 if self.wgrad is None:
                     K.gemm(self.y1[i], dh, w["gW0"], ta=True, beta=1.0)
             if self.fuse_ln:   # dgrad + LayerNorm_1 backward + residual + its parameter and bias grads
+                (gs1, reps), (gc1, _), (gbo, _) = (self._acc((k, i), w[k]) for k in ("gs1", "gc1", "gbo"))
                 K.gemm_ln(dh, w["W0"], dx_mid, tb=True, ln_mode=2, res=dx_in, ln_scale=w["s1"], ln_y=dxb_mid,
-                          ln_mean=self.st1[i][0], ln_rstd=self.st1[i][1], ln_x=self.x1s[i], ln_dscale=w["gs1"],
-                          ln_dbias=w["gc1"], colsum=w["gbo"])
+                          ln_mean=self.st1[i][0], ln_rstd=self.st1[i][1], ln_x=self.x1s[i], ln_dscale=gs1,
+                          ln_dbias=gc1, colsum=gbo, col_reps=reps)
             elif m.use_layernorm:
                 K.gemm(dh, w["W0"], self.dy_m[i], tb=True)
                 K.layernorm_bwd(self.dy_m[i], self.x1s[i], w["s1"], *self.st1[i], dx_in, dx_mid, dxb_mid,
@@ -402,14 +438,17 @@ class ViTRunner:
             with self._fork():
                 if self.wgrad is None:
                     K.gemm(self.y0[i], dqkv, w["gWqkv"], ta=True, beta=1.0)
-                K.colsum(dqkv, w["gbqkv"])
+                if self.wgrad is None:
+                    K.colsum(dqkv, w["gbqkv"])
             if self.fuse_ln:   # + the dropout backward / bias column sum of the block below's MLP output
                 below = i > 0
+                (gs0, reps), (gc0, _) = (self._acc((k, i), w[k]) for k in ("gs0", "gc0"))
+                gb1 = self._acc(("gb1", i - 1), self.w[i - 1]["gb1"])[0] if below else None
                 K.gemm_ln(dqkv, w["Wqkv"], dx_out, tb=True, ln_mode=2, res=dx_mid, ln_scale=w["s0"],
                           ln_y=self.dym[i - 1] if below else None, drop_rate=rate if below else 0.0, seed=seed,
                           site=site_mlp_out(i - 1) if below else 0, ln_mean=self.st0[i][0],
-                          ln_rstd=self.st0[i][1], ln_x=self.xs[i], ln_dscale=w["gs0"], ln_dbias=w["gc0"],
-                          colsum=self.w[i - 1]["gb1"] if below else None)
+                          ln_rstd=self.st0[i][1], ln_x=self.xs[i], ln_dscale=gs0, ln_dbias=gc0,
+                          colsum=gb1, col_reps=reps)
             elif m.use_layernorm:
                 K.gemm(dqkv, w["Wqkv"], self.dy_a[i], tb=True)
                 K.layernorm_bwd(self.dy_a[i], self.xs[i], w["s0"], *self.st0[i], dx_mid, dx_out, dxb_out,
@@ -422,7 +461,8 @@ class ViTRunner:
             dx_in = dx_out
         K.vit_embed_bwd(dx_in, self.dpatch, self.gcls, self.gpos, None, B, T, D, rate, seed, SITE_EMBED)
         with self._fork():
-            K.colsum(self.dpatch, self.gbconv)
+            if self.wgrad is None:
+                K.colsum(self.dpatch, self.gbconv)
             if self.wgrad is None:
                 K.gemm(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
         if self.wgrad is not None:

@@ -274,8 +274,9 @@ def test_gemm_ln_forward(dev, M, N, K, rate):
     assert torch.allclose(rstd, 1 / torch.sqrt(x1.var(-1, unbiased=False) + 1e-6), rtol=1e-3)
 
 
-@pytest.mark.parametrize("M,N,K,rate", [(1000, 128, 256, 0.0), (513, 64, 128, 0.0), (700, 128, 384, 0.1)])
-def test_gemm_ln_backward(dev, M, N, K, rate):
+@pytest.mark.parametrize("M,N,K,rate,reps", [(1000, 128, 256, 0.0, 1), (513, 64, 128, 0.0, 1), (700, 128, 384, 0.1, 1),
+                                             (1000, 128, 256, 0.1, 32)])
+def test_gemm_ln_backward(dev, M, N, K, rate, reps):
     """pcv_gemm_ln mode 2 (dgrad GEMM, LayerNorm backward, residual add, parameter grads, and the
     dropout-backward bf16 copy + column sum consumed by the sublayer below)."""
     from oracle import rng
@@ -292,8 +293,17 @@ def test_gemm_ln_backward(dev, M, N, K, rate):
     dxb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     ds, db, cs = (torch.full((N,), 0.5, device=dev) for _ in range(3))
     seed = torch.tensor([5], dtype=torch.int32, device=dev)
-    K_.gemm_ln(dh, w, dx, tb=True, ln_mode=2, res=dres, ln_scale=sc, ln_y=dxb, ln_mean=mean, ln_rstd=rstd,
-               ln_x=x, ln_dscale=ds, ln_dbias=db, colsum=cs, drop_rate=rate, seed=seed, site=11)
+    if reps > 1:   # replica rows [reps, N], folded afterwards
+        wss = [torch.zeros(reps, N, device=dev) for _ in range(3)]
+        K_.gemm_ln(dh, w, dx, tb=True, ln_mode=2, res=dres, ln_scale=sc, ln_y=dxb, ln_mean=mean, ln_rstd=rstd,
+                   ln_x=x, ln_dscale=wss[0], ln_dbias=wss[1], colsum=wss[2], col_reps=reps, drop_rate=rate,
+                   seed=seed, site=11)
+        K_.GroupedWGrad([("fold", ws, t) for ws, t in zip(wss, (ds, db, cs))], dev)()
+        torch.cuda.synchronize()
+        assert all(ws.abs().max().item() == 0.0 for ws in wss)   # fold resets the replicas
+    else:
+        K_.gemm_ln(dh, w, dx, tb=True, ln_mode=2, res=dres, ln_scale=sc, ln_y=dxb, ln_mean=mean, ln_rstd=rstd,
+                   ln_x=x, ln_dscale=ds, ln_dbias=db, colsum=cs, drop_rate=rate, seed=seed, site=11)
     dy = dh.float() @ w.float().t()
     xr = x.clone().requires_grad_(True)
     scr = sc.clone().requires_grad_(True)
@@ -344,15 +354,24 @@ def test_grouped_wgrad(dev, tile):
         c = torch.randn(M, N, device=dev)
         refs.append(c + 0.5 * (a.float().t() @ b.float()))
         items.append((a, b, c, 0.5))
-    g = K_.GroupedWGrad(items, dev, tile=tile)
+    # column-sum jobs in the same launch (bf16 and fp32 inputs, ragged row counts, strided rows)
+    xs = [torch.randn(16640, 392, device=dev)[:, :384].to(torch.bfloat16), torch.randn(1001, 136, device=dev)[:, :128],
+          torch.randn(7, 8, device=dev).to(torch.bfloat16)]
+    outs = [torch.randn(x.shape[1], device=dev) for x in xs]
+    cref = [o + x.float().sum(0) for x, o in zip(xs, outs)]
+    g = K_.GroupedWGrad(items + [("colsum", x, o) for x, o in zip(xs, outs)], dev, tile=tile)
     g()
     torch.cuda.synchronize()
+    for o, r in zip(outs, cref):
+        assert torch.allclose(o, r, atol=2e-2, rtol=1e-4), (o - r).abs().max().item()
     for (a, b, c, _), ref in zip(items, refs):
         err = (c - ref).abs().max().item()
         assert err < 2e-3 * max(1.0, ref.abs().max().item()), err
     # a second run accumulates again (beta = 1 semantics)
     for (a, b, c, _), ref in zip(items, refs):
         c.copy_(ref)
+    for o, r in zip(outs, cref):
+        o.copy_(r)
     g()
     torch.cuda.synchronize()
     for (a, b, c, _), ref in zip(items, refs):
