@@ -164,7 +164,7 @@ class GraphedTrainStep:
         self.runner = state.runner_for(image_shape)
         dev = state.params.device
         self.images = torch.zeros(tuple(image_shape), dtype=torch.uint8, device=dev)
-        self.labels = torch.zeros(image_shape[0], dtype=torch.int32, device=dev)
+        self.labels = self.runner.labels   # the runner's static label buffer (no second copy)
         self.distributed = dp.world_size() > 1
         self.stream = torch.cuda.Stream(device=dev)
         self.g_fb = torch.cuda.CUDAGraph()
@@ -191,7 +191,7 @@ class GraphedTrainStep:
     def _fb(self):
         K.seed_next(self.runner.seed)
         self.state.params.zero_grad()
-        self.runner.forward(self.images, self.labels, train=True, need_grad=True)
+        self.runner.forward(self.images, None, train=True, need_grad=True)
         self.runner.backward(train=True)
 
     def _opt(self):
@@ -202,7 +202,6 @@ class GraphedTrainStep:
             self.images.copy_(images, non_blocking=True)
         if labels is not None:
             self.labels.copy_(labels, non_blocking=True)
-        self.runner.labels.copy_(self.labels)
         self.g_fb.replay()
         if self.distributed:
             dp.all_reduce_grads(self.state.params)
