@@ -78,6 +78,13 @@ CASES = {
     "attn_fwd  64x4x257x32 drop": lambda: K.attn_fwd(qkv, o, lse, B, T, H, 32, False, drop_rate=0.1, mask=mask),
     "attn_bwd  64x4x257x32 drop": lambda: K.attn_bwd(qkv, o, o, lse, delta, qkv, B, T, H, 32, False, drop_rate=0.1,
                                                      mask=mask),
+    "attn_fwd  64x4x256x32 drop (no ragged tail)": lambda: K.attn_fwd(qkv[:B * 256], o[:B * 256], lse, B, 256, H, 32,
+                                                                     False, drop_rate=0.1, mask=mask),
+    "attn_bwd  64x4x256x32 drop (no ragged tail)": lambda: K.attn_bwd(qkv[:B * 256], o[:B * 256], o[:B * 256], lse,
+                                                                     delta, qkv[:B * 256], B, 256, H, 32, False,
+                                                                     drop_rate=0.1, mask=mask),
+    "attn_fwd  64x4x257x32 nodrop": lambda: K.attn_fwd(qkv, o, lse, B, T, H, 32, False),
+    "attn_bwd  64x4x257x32 nodrop": lambda: K.attn_bwd(qkv, o, o, lse, delta, qkv, B, T, H, 32, False),
     "lmattn_fwd 16x12x1024x64 causal": lambda: K.attn_fwd(qkv_l, o_l, lse_l, Bl, Tl, Hl, Dl, True),
     "lmattn_bwd 16x12x1024x64 causal": lambda: K.attn_bwd(qkv_l, o_l, do_l, lse_l, delta_l, dqkv_l, Bl, Tl, Hl, Dl,
                                                           True),
