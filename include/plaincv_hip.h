@@ -135,6 +135,10 @@ int pcv_dropout_bwd_cast(const float* x, int64_t ldx, void* out, int64_t ldo, in
 int pcv_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 /* Advance the device-resident dropout seed (one per train step; hipGraph-replay safe). */
 int pcv_seed_next(uint32_t* seed, void* stream);
+/* Step prologue: x[0:n) = 0 (the flat gradient buffer, 16-B aligned) and, if seed is given,
+ * the dropout seed advanced as pcv_seed_next -- one launch (flax_engine.py:95-123's fresh
+ * gradients and per-step dropout rng). */
+int pcv_zero_seed(float* x, int64_t n, uint32_t* seed, void* stream);
 /* out[c] += sum_r x[r,c]  (Dense bias gradients). */
 int pcv_colsum(const void* x, int64_t ld, int64_t R, int N, int x_f32, float* out, void* stream);
 /* ViT patch embedding input (models/vit_small.py:78-88, (kh,kw,c) flatten, /255) and token

@@ -201,6 +201,16 @@ __global__ void embed_bwd_kernel(const int* ids, const bf16* dx, int64_t lddx, f
 
 __global__ void seed_next_kernel(uint32_t* seed) { *seed = hash3(*seed, 0x5EEDu, 0x9E37u); }
 
+// step prologue in one launch: grad[0:n) = 0 (16-B stores) and the dropout seed advanced
+__global__ void zero_seed_kernel(float* x, int64_t n, uint32_t* seed) {
+  if (seed && blockIdx.x == 0 && threadIdx.x == 0) *seed = hash3(*seed, 0x5EEDu, 0x9E37u);
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+    reinterpret_cast<f32x4*>(x)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = 0.f;
+}
+
 static int grid_for(int64_t n, int block = 256) {
   int64_t g = (n + block - 1) / block;
   if (g > 4096) g = 4096;
@@ -323,6 +333,12 @@ extern "C" int pcv_embed_bwd(const int* ids, const void* dx, int64_t lddx, float
   if (R <= 0 || D <= 0) return PCV_EINVAL;
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(grid_for(R * D)), dim3(256), 0, (hipStream_t)stream, ids, (const bf16*)dx,
                      lddx, dtable, ldt, R, D, V);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_zero_seed(float* x, int64_t n, uint32_t* seed, void* stream) {
+  if ((!x && n > 0) || n < 0 || !pcv_aligned16(x)) return PCV_EINVAL;
+  hipLaunchKernelGGL(zero_seed_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, n, seed);
   return pcv_launch_status();
 }
 

@@ -189,8 +189,7 @@ class GraphedTrainStep:
         self.metrics = self.runner.metrics
 
     def _fb(self):
-        K.seed_next(self.runner.seed)
-        self.state.params.zero_grad()
+        K.zero_seed(self.state.params.grad_flat, self.runner.seed)   # zero grads + advance seed
         self.runner.forward(self.images, None, train=True, need_grad=True)
         self.runner.backward(train=True)
 

@@ -423,6 +423,13 @@ def seed_next(seed_buf):
     hip.call("pcv_seed_next", ptr(seed_buf), stream_ptr())
 
 
+def zero_seed(grad_flat, seed_buf=None):
+    """grad_flat = 0 and (optionally) advance the dropout seed, one launch."""
+    _dev(grad_flat, seed_buf)
+    _chk(grad_flat.dtype == F32 and grad_flat.is_contiguous(), "zero_seed buffer")
+    hip.call("pcv_zero_seed", ptr(grad_flat), grad_flat.numel(), ptr(seed_buf), stream_ptr())
+
+
 def step_bump(count):
     _dev(count)
     hip.call("pcv_step_bump", ptr(count), stream_ptr())

@@ -189,7 +189,9 @@ class ViTRunner:
         # several hardware queues and every cross-queue edge cost 5-12 us on MI355X
         # (profiles/r01_vit_side_stream_timeline.txt), more than the overlap returns at ViT-small size.
         self.side = torch.cuda.Stream(device=dev) if (side_stream and dev.type == "cuda") else None
-        self.dx = e(R, D)                              # top-of-stack residual gradient
+        # top-of-stack residual gradient: only the cls rows are ever written (the head reads the
+        # cls token alone), so the other rows stay zero from here on -- no per-step memset
+        self.dx = torch.zeros(R, D, dtype=f32, device=dev)
         self.dym = [e(R, D, dt=bf) for _ in range(Lc)]
         self.dh = [e(R, M, dt=bf) for _ in range(Lc)]
         # LayerNorm fused into the residual-stream GEMM epilogues (pcv_gemm_ln) when rows fit one tile
@@ -382,7 +384,6 @@ class ViTRunner:
             if self.wgrad is None or not self.head_bias_grouped:
                 K.colsum(self.dlogits, self.gbh)
         K.gemm(self.dlogits_b, self.Wh, self.dyf, tb=True)
-        self.dx.zero_()
         dxc = self.dx.view(B, T * D)[:, :D]
         xcls = self.xs[-1].view(B, T * D)[:, :D]
         if m.use_layernorm:
