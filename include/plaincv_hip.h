@@ -32,6 +32,9 @@ extern "C" {
  * pcv_gemm_ln's ln_dscale / ln_dbias) is a [col_reps][N] block and workgroup b adds into row
  * b % col_reps (spreads the float atomics of hundreds of workgroups over several rows); the
  * caller folds the rows, e.g. with a zero_after column-sum job of pcv_gemm_grouped.
+ * attn_delta (optional; bf16 C whose N columns are attn_H heads of 32 or 64, rows b*attn_T + t):
+ * attn_delta[(b*attn_H + h)*attn_T + t] = <bf16 C row head h, attn_o row head h> -- the
+ * attention-backward row constant computed where dO is produced (see pcv_attn_bwd delta_ready).
  * Replaces every flax nn.Dense / DenseGeneral / Conv(patch) contraction:
  * models/vit_small.py:13-16,41-45,78-88,126; models/LM/transformer.py:194-201,
  * 246-253,110-134,393-405 and their autodiff transposes. */
@@ -41,7 +44,8 @@ int pcv_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, i
                   float alpha, float beta, int out_f32,
                   const float* bias, const void* res, int64_t ldr, int64_t stride_r, int res_f32, float res_scale,
                   void* aux, int64_t ldaux, int act,
-                  float dropout_rate, const uint32_t* seed, uint32_t site, float* colsum, int col_reps, int split_k,
+                  float dropout_rate, const uint32_t* seed, uint32_t site, float* colsum, int col_reps,
+                  const void* attn_o, int64_t ld_attn_o, float* attn_delta, int attn_T, int attn_H, int split_k,
                   void* stream);
 
 /* GEMM + LayerNorm over each complete output row (N <= 128, N % 8 == 0; ViT residual stream).
@@ -88,8 +92,10 @@ int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t ldq,
                  const float* lse2, float* delta_ws /* [B,H,T] */,
                  void* dq, void* dk, void* dv, int64_t lddq,
                  int B, int T, int H, int head_dim, int causal,
-                 float dropout_rate, const uint16_t* drop_mask, void* stream);
-/* Attention-weight dropout mask: flax draws ONE [T,T] keep mask per layer and
+                 float dropout_rate, const uint16_t* drop_mask, int delta_ready, void* stream);
+/* (delta_ready: delta_ws already holds rowsum(dO * O) per (b, h, t) -- pcv_gemm_bf16's
+ * attention-delta epilogue on the GEMM that produced dO -- so its kernel is skipped.)
+ * Attention-weight dropout mask: flax draws ONE [T,T] keep mask per layer and
  * broadcasts it over batch and heads (models/vit_small.py:41-45, nn.Dropout with
  * broadcast_dims (0,1) inside dot_product_attention).  Drawn once per step for
  * `layers` consecutive layers (site = site + l*site_stride) into packed bits,

@@ -39,6 +39,7 @@ struct AttnArgs {
   int drop; float drop_scale;             // dropout on the weights (broadcast over batch and heads)
   const uint16_t* mask;                   // packed keep bits, see drop_word()
   int n64;                                // key-tile count of the mask (2*ceil(T/128))
+  int delta_ready;                        // bwd: delta already computed (fused into the dO producer)
 };
 
 // Dropout keep-mask layout.  flax SelfAttention broadcasts one [T,T] mask over batch
@@ -685,7 +686,8 @@ template <int DH, bool C, bool D>
 static void launch_bwd(const AttnArgs& a, hipStream_t s) {
   const int64_t n = (int64_t)a.B * a.T * a.H;
   const int64_t nd = n * (DH / 8);
-  hipLaunchKernelGGL((attn_bwd_delta_kernel<DH>), dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a);
+  if (!a.delta_ready)
+    hipLaunchKernelGGL((attn_bwd_delta_kernel<DH>), dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a);
   dim3 grid((a.T + 127) / 128, a.H, a.B);
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH, C, D>), grid, dim3(256), 0, s, a);
   hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, C, D>), grid, dim3(256), 0, s, a);
@@ -756,7 +758,7 @@ extern "C" int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t
                             const float* lse2, float* delta_ws,
                             void* dq, void* dk, void* dv, int64_t lddq,
                             int B, int T, int H, int head_dim, int causal,
-                            float dropout_rate, const uint16_t* drop_mask, void* stream) {
+                            float dropout_rate, const uint16_t* drop_mask, int delta_ready, void* stream) {
   if (B <= 0 || T <= 0 || H <= 0) return PCV_EINVAL;
   if (dropout_rate > 0.f && (!drop_mask || ((uintptr_t)drop_mask & 7))) return PCV_EINVAL;
   if ((ldq & 7) || (ldo & 7) || (lddo & 7) || !pcv_aligned16(q) || !pcv_aligned16(k) || !pcv_aligned16(v) ||
@@ -766,7 +768,7 @@ extern "C" int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t
   a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.ldq = ldq;
   a.o = (const bf16*)o; a.ldo = ldo; a.dout = (const bf16*)dout; a.lddo = lddo;
   a.dq = (bf16*)dq; a.dk = (bf16*)dk; a.dv = (bf16*)dv; a.lddq = lddq;
-  a.lse2 = (float*)lse2; a.delta = delta_ws;
+  a.lse2 = (float*)lse2; a.delta = delta_ws; a.delta_ready = delta_ready;
   a.B = B; a.T = T; a.H = H; a.scale = 1.f / sqrtf((float)head_dim);
   set_drop(a, dropout_rate, drop_mask);
   return dispatch<false>(a, head_dim, causal ? 1 : 0, a.drop, (hipStream_t)stream);

@@ -56,6 +56,10 @@ struct GemmArgs {
   // (one contended row runs ~14x below the chip's float-atomic rate); the caller folds the
   // replicas (pcv_gemm_grouped column-sum jobs with zero_after)
   int col_reps;
+  // attention-backward row constant fused into a bf16 epilogue (the out-projection dgrad
+  // produces dO): delta[(b H + h) T + t] = <bf16(C[row, h dh : (h+1) dh]), dl_o[row, same]>,
+  // row = b T + t -- replaces attn_bwd_delta_kernel
+  const bf16* dl_o; int64_t ld_dlo; float* dl_delta; int dl_T, dl_H, dl_dh;
 };
 
 __device__ __forceinline__ int64_t col_rep_off(const GemmArgs& g) {
@@ -844,6 +848,20 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
           *reinterpret_cast<bf16x8*>(cp) = o;
+          if (g.dl_delta) {   // lanes of one head are dh/8 consecutive lanes (a quad or an octet)
+            const bf16x8 ov = *reinterpret_cast<const bf16x8*>(g.dl_o + row * g.ld_dlo + col);
+            float d = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) d += bf2f(o[e]) * bf2f(ov[e]);
+            d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0xB1, 0xF, 0xF, false));
+            d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x4E, 0xF, 0xF, false));
+            if (g.dl_dh == 64)
+              d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x141, 0xF, 0xF, false));
+            if (col % g.dl_dh == 0) {
+              const int64_t b = row / g.dl_T, t = row % g.dl_T;
+              g.dl_delta[(b * g.dl_H + col / g.dl_dh) * g.dl_T + t] = d;
+            }
+          }
         } else {
           for (int e = 0; e < 8; ++e) if (col + e < g.N) cp[e] = f2bf(v[e]);
         }
@@ -1028,7 +1046,8 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
                              const float* bias, const void* res, int64_t ldr, int64_t stride_r, int res_f32, float res_scale,
                              void* aux, int64_t ldaux, int act,
                              float drop_rate, const uint32_t* seed, uint32_t site,
-                             float* colsum, int col_reps, int split_k, void* stream) {
+                             float* colsum, int col_reps, const void* attn_o, int64_t ld_attn_o,
+                             float* attn_delta, int attn_T, int attn_H, int split_k, void* stream) {
   if (M < 0 || N < 0 || K < 0 || batch < 1) return PCV_EINVAL;
   if (colsum && (batch > 1 || split_k > 1)) return PCV_EINVAL;
   if (M == 0 || N == 0) return 0;
@@ -1045,6 +1064,15 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
   g.aux = (bf16*)aux; g.ldaux = ldaux; g.act = act;
   g.colsum = colsum;
   g.col_reps = col_reps;
+  if (attn_delta) {
+    // whole heads per lane group: dh in {32, 64} dividing N, bf16 out, vectorised, one tile row
+    // per 8-column lane chunk (no split-K / batch)
+    if (!attn_o || out_f32 || split_k > 1 || batch > 1 || attn_T <= 0 || attn_H <= 0 || N % attn_H) return PCV_EINVAL;
+    const int64_t dh = N / attn_H;
+    if ((dh != 32 && dh != 64) || (ld_attn_o & 7) || !pcv_aligned16(attn_o) || M % attn_T) return PCV_EINVAL;
+    g.dl_o = (const bf16*)attn_o; g.ld_dlo = ld_attn_o; g.dl_delta = attn_delta;
+    g.dl_T = attn_T; g.dl_H = attn_H; g.dl_dh = (int)dh;
+  }
   g.drop_thresh = 0; g.drop_scale = 1.f; g.seedp = seed; g.site = site;
   if (drop_rate > 0.f && !seed) return PCV_EINVAL;
   if (drop_rate > 0.f) {
@@ -1061,6 +1089,7 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
                    ((stride_r * (res_f32 ? 4 : 2)) % 16 == 0);
     if (aux) ok = ok && pcv_aligned16(aux) && ((ldaux * 2) % 16 == 0);
     g.vec_ok = ok ? 1 : 0;
+    if (attn_delta && !ok) return PCV_EALIGN;
     g.glds_ok = 1;  // lda/ldb % 8 == 0 and 16-B aligned bases are required above
   }
   g.split_k = 1;

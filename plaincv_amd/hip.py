@@ -21,7 +21,8 @@ F32 = ctypes.c_float
 # name -> argtypes (return type is always int status)
 SIGNATURES = {
     "pcv_gemm_bf16": [P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, I64, I64, I64, I64,
-                      F32, F32, I32, P, P, I64, I64, I32, F32, P, I64, I32, F32, P, U32, P, I32, I32, P],
+                      F32, F32, I32, P, P, I64, I64, I32, F32, P, I64, I32, F32, P, U32, P, I32, P, I64, P, I32, I32,
+                      I32, P],
     "pcv_gemm_ln": [P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, F32, P, P, I64, F32, P, U32, I32, P, P, F32,
                     P, I64, P, P, P, I64, P, P, P, I32, P],
     "pcv_gemm_grouped_plan_size": [I32],
@@ -30,7 +31,7 @@ SIGNATURES = {
     "pcv_gemm_grouped_run": [P, I32, I32, I64, P],
     "pcv_attn_fwd": [P, P, P, I64, P, I64, P, I32, I32, I32, I32, I32, F32, P, P],
     "pcv_attn_bwd": [P, P, P, I64, P, I64, P, I64, P, P, P, P, P, I64, I32, I32, I32, I32, I32,
-                     F32, P, P],
+                     F32, P, I32, P],
     "pcv_attn_mask_words": [I32],
     "pcv_attn_drop_mask": [P, U32, U32, I32, I32, F32, P, P],
     "pcv_layernorm_fwd": [P, I64, P, P, P, I64, P, P, I64, I32, F32, P],

@@ -25,7 +25,7 @@ def _ld(t):
 
 
 def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=None, res_scale=1.0, aux=None,
-         act=EPI_NONE, drop_rate=0.0, seed=None, site=0, split_k=None, colsum=None, col_reps=1):
+         act=EPI_NONE, drop_rate=0.0, seed=None, site=0, split_k=None, colsum=None, col_reps=1, attn_delta=None):
     """out[M,N] = epi(alpha * op(a) @ op(b)).
 
     a: [M,K] (ta=False) or [K,M] (ta=True); b: [K,N] (tb=False) or [N,K] (tb=True).
@@ -33,7 +33,8 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
     bf16 or fp32 output (fp32: out = v + beta*out).  Epilogue order:
     +bias -> [gelu (aux<-preact) | *gelu'(aux)] -> dropout -> +res.  colsum (fp32 [N]) += column sums
     of the stored values (not with split-K or batches); col_reps > 1: colsum is [col_reps, N] and
-    workgroup b adds into row b % col_reps (the caller folds the rows)."""
+    workgroup b adds into row b % col_reps (the caller folds the rows).  attn_delta=(o, delta, T, H):
+    with bf16 out = dO, also delta[(b H + h) T + t] = <out[b T + t, head h], o[b T + t, head h]>."""
     batched = a.dim() == 3
     if batched:
         nb = a.shape[0]
@@ -85,6 +86,13 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
         _chk(not batched and colsum.dtype == F32 and colsum.numel() >= N * max(1, col_reps) and colsum.is_cuda and
              colsum.is_contiguous(), "gemm colsum")
         split_k = 1
+    dl_o, dl_ld, dl, dl_T, dl_H = None, 0, None, 0, 0
+    if attn_delta is not None:
+        dl_o, dl, dl_T, dl_H = attn_delta
+        _chk(not batched and out.dtype == BF16 and dl_o.dtype == BF16 and tuple(dl_o.shape) == (M, N) and
+             dl.dtype == F32 and dl.numel() >= M * dl_H, "gemm attn_delta")
+        dl_ld = _ld(dl_o)
+        split_k = 1
     if split_k is None:
         split_k = 1
         plain = out_f32 and beta == 1.0 and bias is None and res is None and act == EPI_NONE and drop_rate == 0.0
@@ -97,8 +105,8 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
     hip.call("pcv_gemm_bf16", ptr(a2), ptr(b2), ptr(o2), M, N, K, _ld(a2), _ld(b2), _ld(o2),
              int(ta), int(tb), nb, sa, sb, sc, float(alpha), float(beta), out_f32,
              ptr(bias), ptr(res), ldr, sr, res_f32, float(res_scale), ptr(aux), ldaux, int(act),
-             float(drop_rate), ptr(seed), int(site) & 0xFFFFFFFF, ptr(colsum), int(col_reps), int(split_k),
-             stream_ptr())
+             float(drop_rate), ptr(seed), int(site) & 0xFFFFFFFF, ptr(colsum), int(col_reps), ptr(dl_o), dl_ld,
+             ptr(dl), int(dl_T), int(dl_H), int(split_k), stream_ptr())
     return out
 
 
@@ -249,7 +257,7 @@ def attn_fwd(qkv, out, lse2, B, T, H, Dh, causal, drop_rate=0.0, mask=None, q_of
              ptr(mask), stream_ptr())
 
 
-def attn_bwd(qkv, o, dout, lse2, delta_ws, dqkv, B, T, H, Dh, causal, drop_rate=0.0, mask=None):
+def attn_bwd(qkv, o, dout, lse2, delta_ws, dqkv, B, T, H, Dh, causal, drop_rate=0.0, mask=None, delta_ready=False):
     D = H * Dh
     _chk(qkv.dtype == BF16 and dqkv.dtype == BF16 and dout.dtype == BF16 and o.dtype == BF16, "attn bwd dtypes")
     _chk(dqkv.shape[0] == B * T and dqkv.shape[1] >= 3 * D and delta_ws.numel() >= B * H * T, "attn bwd shapes")
@@ -258,7 +266,7 @@ def attn_bwd(qkv, o, dout, lse2, delta_ws, dqkv, B, T, H, Dh, causal, drop_rate=
     dbase = dqkv.data_ptr()
     hip.call("pcv_attn_bwd", base, base + D * es, base + 2 * D * es, _ld(qkv), ptr(o), _ld(o), ptr(dout),
              _ld(dout), ptr(lse2), ptr(delta_ws), dbase, dbase + D * es, dbase + 2 * D * es, _ld(dqkv),
-             B, T, H, Dh, int(causal), float(drop_rate), ptr(mask), stream_ptr())
+             B, T, H, Dh, int(causal), float(drop_rate), ptr(mask), int(delta_ready), stream_ptr())
 
 
 def layernorm_fwd(x, scale, bias, y, mean, rstd, eps=1e-6):

@@ -276,8 +276,9 @@ class LMRunner:
             K.gemm(self.dgu, w["Wgu"], self.dy, tb=True)
             K.rmsnorm_bwd(self.dy, self.x1[i], w["s1"], self.r1[i], self.dx, self.dx, w["gs1"])
             K.gemm(self.o[i], self.dx, w["gWo"], ta=True, beta=1.0)
-            K.gemm(self.dx, w["Wo"], self.do, tb=True)
-            K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, self.dqkv, b, T, H, Dh, causal=True)
+            K.gemm(self.dx, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H))   # + delta
+            K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, self.dqkv, b, T, H, Dh, causal=True,
+                       delta_ready=True)
             K.rope(self.dqkv, T, Dh, self.cos, self.sin, backward=True, ncols=2 * d)
             K.gemm(self.y0[i], self.dqkv, w["gWqkv"], ta=True, beta=1.0)
             K.gemm(self.dqkv, w["Wqkv"], self.dy, tb=True)

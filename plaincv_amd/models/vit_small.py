@@ -433,9 +433,10 @@ class ViTRunner:
                     K.gemm(self.o[i], dxb_mid, w["gWo"], ta=True, beta=1.0)
                 if not self.fuse_ln:
                     K.colsum(dx_mid, w["gbo"])
-            K.gemm(dxb_mid, w["Wo"], self.do, tb=True)
+            # dO = dy Wo^T; its epilogue also forms the attention-backward row constant delta
+            K.gemm(dxb_mid, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H))
             K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
-                       causal=False, drop_rate=rate, mask=self._mask(i))
+                       causal=False, drop_rate=rate, mask=self._mask(i), delta_ready=True)
             with self._fork():
                 if self.wgrad is None:
                     K.gemm(self.y0[i], dqkv, w["gWqkv"], ta=True, beta=1.0)

@@ -4,7 +4,7 @@ import sqlite3
 import sys
 
 
-def main(db, marker="seed_next_kernel", which=-2):
+def main(db, marker="zero_seed_kernel", which=-2):
     con = sqlite3.connect(db)
     rows = con.execute("select name, start, end, grid_x, grid_y, grid_z, workgroup_x from kernels "
                        "order by start").fetchall()

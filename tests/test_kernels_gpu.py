@@ -379,6 +379,24 @@ def test_grouped_wgrad(dev, tile):
         assert (c - ref2).abs().max().item() < 2e-3 * max(1.0, ref2.abs().max().item())
 
 
+@pytest.mark.parametrize("B,T,H,Dh", [(4, 257, 4, 32), (2, 128, 12, 64)])
+def test_gemm_attn_delta_epilogue(dev, B, T, H, Dh):
+    """dO GEMM epilogue computing the attention-backward delta = rowsum per head of dO * O."""
+    from plaincv_amd import kernels as K_
+    torch.manual_seed(12)
+    R, D = B * T, H * Dh
+    dy = torch.randn(R, D, device=dev).to(torch.bfloat16)
+    w = (torch.randn(D, D, device=dev) * 0.1).to(torch.bfloat16)
+    o = torch.randn(R, D, device=dev).to(torch.bfloat16)
+    do = torch.empty(R, D, device=dev, dtype=torch.bfloat16)
+    delta = torch.full((B * H * T,), 7.0, device=dev)
+    K_.gemm(dy, w, do, tb=True, attn_delta=(o, delta, T, H))
+    ref_do = (dy.float() @ w.float().t())
+    assert (do.float() - ref_do).abs().max().item() < 5e-2 * max(1.0, ref_do.abs().max().item())
+    ref = (do.float() * o.float()).reshape(B, T, H, Dh).sum(-1).permute(0, 2, 1).reshape(-1)
+    assert torch.allclose(delta, ref, atol=1e-3, rtol=1e-3), (delta - ref).abs().max().item()
+
+
 def test_transpose_batch(dev):
     from plaincv_amd import kernels as K_
     torch.manual_seed(8)
