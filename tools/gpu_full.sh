@@ -6,7 +6,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
-timeout -k 10 600 python -m pytest tests -m gpu -x -q --tb=short > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --tb=short --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 timeout -k 10 400 python bench.py > $O/bench_vit.json 2> $O/bench_vit.err
 cat $O/bench_vit.json

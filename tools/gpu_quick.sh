@@ -3,7 +3,7 @@
 set -e
 TAG=${1:-x}
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q --tb=short > gpurun_out/tests_$TAG.log 2>&1 || { tail -30 gpurun_out/tests_$TAG.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --tb=short --timeout 120 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1 || { tail -30 gpurun_out/tests_$TAG.log; exit 1; }
 tail -3 gpurun_out/tests_$TAG.log
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_vit_$TAG.json 2> gpurun_out/bench_vit_$TAG.err
 cat gpurun_out/bench_vit_$TAG.json
