@@ -200,6 +200,46 @@ int pcv_muon_fused_ok(int64_t rows, int64_t cols);
 int pcv_muon_ns_fused(const void* mats, int nmats, float eps, float ns_a, float ns_b, float ns_c, int ns_steps,
                       void* stream);
 int pcv_chunk_size(void);
+
+/* ------------------------------------------------- matrix preconditioners ----
+ * SOAP (optim/soap.py:136-368) and Shampoo (optim/shampoo.py:81-296): the per-leaf
+ * jnp matmuls, jnp.linalg.eigh (soap.py:100-105, shampoo.py:205-206) and jnp.linalg.qr
+ * (soap.py:125,131) of the reference, batched over every routed matrix (csrc/precond.hip).
+ * Job records are plain 8-byte fields (pointers, int64, double), sizes from pcv_*_job_size().
+ *
+ * Grouped fp32 GEMM (v_mfma_f32_16x16x4_f32, exact fp32), one launch for all jobs:
+ *   C = alpha * (*alpha_dev)^apow * op(A) diag(kscale) op(B) + beta * C + rscale * R; Cb = bf16(C)
+ *   record {A, B, C, kscale, R, Cb, alpha_dev, M, N, K, lda, ldb, ldc, ldr, ldcb, ta, tb, apow,
+ *           tiles_n, first_tile, alpha, beta, rscale} (64x64 tiles, first_tile = prefix sum). */
+int pcv_f32_job_size(void);
+int pcv_gemm_f32_grouped(const void* jobs, int njobs, int64_t total_tiles, void* stream);
+/* Symmetric eigendecomposition, n <= 256, one workgroup per matrix (cyclic Jacobi, packed upper
+ * triangle in LDS, round-robin parallel rotations, rotation log for the vectors pass):
+ *   record {A, w, wpow, perm, log, nrounds, lda, n, shift}: eigenvalues of A + shift*I into w
+ *   (descending if sort_desc, else in Jacobi order), wpow = max(w, pow_floor)^(-pow_expo) (optional),
+ *   perm = source column of each output; log holds pcv_eigh_log_floats(n, max_sweeps) floats.
+ * pcv_eigh_vectors replays the log: Vout = V0 (identity if NULL) x rotations, columns in w's order;
+ *   record {V0, Vout, perm, log, nrounds, ld0, ldo, n}; Vout may alias V0. */
+int pcv_eigh_job_size(void);
+int pcv_vec_job_size(void);
+int64_t pcv_eigh_log_floats(int64_t n, int max_sweeps);
+int pcv_eigh_jacobi(const void* jobs, int njobs, int max_n, int max_sweeps, float tol_rel, float tol_abs_rel,
+                    int sort_desc, float pow_floor, float pow_expo, void* stream);
+int pcv_eigh_vectors(const void* jobs, int njobs, int max_n, void* stream);
+/* Householder QR (LAPACK geqrf/orgqr sign convention), Q of A[:, perm] (perm optional), n <= 1024:
+ *   record {A, perm, Q, W, Qt, lda, ldq, n}; W and Qt are n*n fp32 workspaces. */
+int pcv_qr_job_size(void);
+int pcv_householder_qr(const void* jobs, int njobs, int max_n, void* stream);
+/* SOAP Adam in the rotated basis over flat arenas (soap.py:249-268), step = device int from 1. */
+int pcv_soap_adam(const float* g_rot, float* m, float* v, float* n_rot, int64_t n, float b1, float b2, float eps,
+                  const int* step, int correct_bias, void* stream);
+/* SOAP refresh order (soap.py:115-126): perm = stable argsort(-diag(Q^T T)), T = M Q;
+ * record {Q, T, perm, ldq, ldt, n}.  Re-index: dst[i][j] = src[pl[i]][pr[j]];
+ * record {src, dst, pl, pr, rows, cols, first_block} (256-element blocks). */
+int pcv_sort_job_size(void);
+int pcv_soap_est_sort(const void* jobs, int njobs, void* stream);
+int pcv_perm_job_size(void);
+int pcv_permute_rc(const void* jobs, int njobs, int64_t total_blocks, void* stream);
 const char* pcv_last_error_string(int code);
 
 #ifdef __cplusplus

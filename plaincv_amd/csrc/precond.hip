@@ -1,0 +1,550 @@
+// plaincv_amd/csrc/precond.hip -- matrix-preconditioner kernels for SOAP and Shampoo.
+//
+//   SOAP     optim/soap.py:136-368  (Kronecker second moments L, R; eigenbases QL, QR from
+//            eigh at the first step, soap.py:100-105; Adam in the rotated basis; one QR power
+//            step + v re-index every precondition_frequency steps, soap.py:108-133)
+//   Shampoo  optim/shampoo.py:81-296 (L += g g^T, R += g^T g; P = U max(lambda, eps)^(-p) U^T
+//            from eigh(L + eps I), shampoo.py:195-215; update P_L g P_R)
+//
+// The reference runs these through XLA's fp32 dot + cuSOLVER syevd/geqrf per leaf.  Here:
+//   * every product (Gram updates, basis rotations g' = QL^T g QR, back-projections, the
+//     warm-start rotation U^T L U, P = U diag(d) U^T) is a job of ONE grouped fp32 MFMA GEMM
+//     launch (v_mfma_f32_16x16x4_f32: exact fp32, the chip's fp32 matrix path) per phase, for
+//     all routed matrices at once;
+//   * the symmetric eigendecomposition is a cyclic Jacobi method, one 1024-thread workgroup per
+//     matrix with the packed upper triangle RESIDENT in LDS (n <= 256: 129 KiB), parallel
+//     round-robin ordering (n/2 disjoint rotations per round, applied as independent 2x2 blocks),
+//     threshold skipping and a per-sweep convergence flag.  The rotations are logged (c, s per
+//     pair per round) and a second kernel replays the log on the eigenvector rows (rows are
+//     independent, so it is parallel over row blocks), starting from identity or from a previous
+//     basis U (Shampoo warm start: Jacobi on U^T (L + eps I) U converges in a few sweeps);
+//   * the QR of SOAP's refresh is Householder (LAPACK geqrf/orgqr convention, so the column
+//     signs match jnp.linalg.qr), one workgroup per matrix, on a column-major workspace;
+//   * SOAP's Adam-in-the-rotated-basis is one flat elementwise launch over every routed
+//     matrix (m, v, g', n' live in flat arenas).
+// All launches are stream-ordered with no host sync and no allocation.
+#include "common.h"
+
+namespace pcv {
+
+// ------------------------------------------------------------------ fp32 grouped GEMM ----
+// C = alpha * adev^apow * op(A) diag(kscale) op(B) + beta * C + rscale * R;  Cb = bf16(C).
+struct F32Job {
+  const float* A; const float* B; float* C;
+  const float* kscale; const float* R; bf16* Cb; const float* alpha_dev;
+  int64_t M, N, K, lda, ldb, ldc, ldr, ldcb;
+  int64_t ta, tb, apow, tiles_n, first_tile;
+  double alpha, beta, rscale;
+};
+static_assert(sizeof(F32Job) == 23 * 8, "F32Job layout");
+
+constexpr int FG_T = 64, FG_K = 16, FG_LD = FG_T + 16;   // +16: the 4 k-rows of a read hit 4 bank groups
+
+__global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __restrict__ jobs, int njobs) {
+  __shared__ float As[FG_K][FG_LD];
+  __shared__ float Bs[FG_K][FG_LD];
+  const int64_t bid = blockIdx.x;
+  int j = 0;
+  while (j + 1 < njobs && jobs[j + 1].first_tile <= bid) ++j;
+  const F32Job& jb = jobs[j];
+  const int64_t t = bid - jb.first_tile;
+  const int64_t m0 = (t / jb.tiles_n) * FG_T, n0 = (t % jb.tiles_n) * FG_T;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int64_t M = jb.M, N = jb.N, K = jb.K;
+  const float* __restrict__ A = jb.A;
+  const float* __restrict__ B = jb.B;
+  const float* __restrict__ ks = jb.kscale;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int64_t k0 = 0; k0 < K; k0 += FG_K) {
+    float ra[4], rb[4];
+    int am[4], ak[4], bn[4], bk[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (jb.ta) { am[i] = tid & 63; ak[i] = (tid >> 6) + 4 * i; }      // A stored [K][M]
+      else { ak[i] = tid & 15; am[i] = (tid >> 4) + 16 * i; }            // A stored [M][K]
+      const int64_t gm = m0 + am[i], gk = k0 + ak[i];
+      float x = 0.f;
+      if (gm < M && gk < K) {
+        x = jb.ta ? A[gk * jb.lda + gm] : A[gm * jb.lda + gk];
+        if (ks) x *= ks[gk];
+      }
+      ra[i] = x;
+      if (jb.tb) { bk[i] = tid & 15; bn[i] = (tid >> 4) + 16 * i; }      // B stored [N][K]
+      else { bn[i] = tid & 63; bk[i] = (tid >> 6) + 4 * i; }             // B stored [K][N]
+      const int64_t gn = n0 + bn[i], gk2 = k0 + bk[i];
+      float y = 0.f;
+      if (gn < N && gk2 < K) y = jb.tb ? B[gn * jb.ldb + gk2] : B[gk2 * jb.ldb + gn];
+      rb[i] = y;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      As[ak[i]][am[i]] = ra[i];
+      Bs[bk[i]][bn[i]] = rb[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < FG_K; kk += 4) {
+      const int kr = kk + (lane >> 4);
+      float fa[2], fb[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) fa[a] = As[kr][wm * 32 + a * 16 + (lane & 15)];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) fb[b] = Bs[kr][wn * 32 + b * 16 + (lane & 15)];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a], fb[b], acc[a][b], 0, 0, 0);
+    }
+  }
+  float alpha = (float)jb.alpha;
+  if (jb.alpha_dev) {
+    const float s = *jb.alpha_dev;
+    alpha *= jb.apow == 2 ? s * s : s;
+  }
+  const float beta = (float)jb.beta, rscale = (float)jb.rscale;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 32 + a * 16 + (lane >> 4) * 4 + r;
+        const int64_t col = n0 + wn * 32 + b * 16 + (lane & 15);
+        if (row < M && col < N) {
+          float v = alpha * acc[a][b][r];
+          float* c = jb.C + row * jb.ldc + col;
+          if (beta != 0.f) v += beta * *c;
+          if (jb.R) v += rscale * jb.R[row * jb.ldr + col];
+          *c = v;
+          if (jb.Cb) jb.Cb[row * jb.ldcb + col] = f2bf(v);
+        }
+      }
+}
+
+// ------------------------------------------------------------------ Jacobi eigh ----
+// Packed upper triangle of the padded (np = n rounded up to 4) symmetric matrix in LDS.
+struct EighJob {
+  const float* A; float* w; float* wpow; int* perm; float2* log; int* nrounds;
+  int64_t lda, n;
+  double shift;
+};
+static_assert(sizeof(EighJob) == 9 * 8, "EighJob layout");
+
+constexpr int EJ_MAXN = 256, EJ_THREADS = 1024;
+
+__device__ __forceinline__ int tri_idx(int i, int j, int np) {   // i <= j
+  return i * np - ((i * (i - 1)) >> 1) + (j - i);
+}
+__device__ __forceinline__ int tri_at(int i, int j, int np) { return i <= j ? tri_idx(i, j, np) : tri_idx(j, i, np); }
+// Round-robin (circle) schedule: round s of m = np-1 rounds; pair 0 = (s, m), pair k = (s+k, s-k) mod m.
+__device__ __forceinline__ void rr_pair(int s, int k, int np, int& p, int& q) {
+  const int m = np - 1;
+  if (k == 0) { p = s; q = m; }
+  else { p = s + k; if (p >= m) p -= m; q = s - k; if (q < 0) q += m; }
+}
+
+__device__ __forceinline__ float wpow_of(float x, float floor_, float expo) {
+  return powf(fmaxf(x, floor_), -expo);
+}
+
+__global__ __launch_bounds__(EJ_THREADS) void eigh_jacobi_kernel(const EighJob* __restrict__ jobs, int max_sweeps,
+                                                                  float tol_rel, float tol_abs_rel, int sort_desc,
+                                                                  float pow_floor, float pow_expo) {
+  extern __shared__ __attribute__((aligned(16))) float tri[];
+  const EighJob jb = jobs[blockIdx.x];
+  const int n = (int)jb.n, np = (n + 3) & ~3, P = np >> 1, m = np - 1;
+  const int ntri = np * (np + 1) / 2;
+  float* cs_c = tri + ntri;          // [P]
+  float* cs_s = cs_c + EJ_MAXN / 2;  // [P]
+  float* cs_t = cs_s + EJ_MAXN / 2;  // [P] tangent (diagonal update)
+  int* pp = (int*)(cs_t + EJ_MAXN / 2);   // [P] p | q << 16
+  __shared__ float red[EJ_THREADS / 64];
+  __shared__ int flag[2];
+  const int tid = threadIdx.x;
+  // load: packed upper triangle, diagonal shifted; pads are zero
+  for (int i = tid; i < ntri; i += EJ_THREADS) tri[i] = 0.f;
+  __syncthreads();
+  float dmax = 0.f;
+  for (int e = tid; e < n * n; e += EJ_THREADS) {
+    const int r = e / n, c = e - r * n;
+    if (r <= c) {
+      float x = jb.A[(int64_t)r * jb.lda + c];
+      if (r == c) { x += (float)jb.shift; dmax = fmaxf(dmax, fabsf(x)); }
+      tri[tri_idx(r, c, np)] = x;
+    }
+  }
+  if (tid < 2) flag[tid] = 0;
+  // ||A|| proxy: max |a_ii| (for a PSD matrix every |a_ij| <= max diag)
+  dmax = wave_max(dmax);
+  if ((tid & 63) == 0) red[tid >> 6] = dmax;
+  __syncthreads();
+  float anorm = 0.f;
+  for (int i = 0; i < EJ_THREADS / 64; ++i) anorm = fmaxf(anorm, red[i]);
+  const float tol_abs = tol_abs_rel * anorm;
+  const int nhalf = P >> 1;            // P even (np % 4 == 0)
+  const int nblk = nhalf * (P + 1);    // P(P+1)/2 pair blocks (K1 <= K2)
+  int round = 0, sweep = 0;
+  for (; sweep < max_sweeps; ++sweep) {
+    for (int s = 0; s < m; ++s) {
+      // phase 1: one thread per pair -> rotation (c, s, t)
+      if (tid < P) {
+        int p, q;
+        rr_pair(s, tid, np, p, q);
+        const float app = tri[tri_idx(p, p, np)], aqq = tri[tri_idx(q, q, np)], apq = tri[tri_at(p, q, np)];
+        float c = 1.f, sn = 0.f, tt = 0.f;
+        if (fabsf(apq) > fmaxf(tol_rel * sqrtf(fabsf(app * aqq)), tol_abs)) {
+          const float tau = (aqq - app) / (2.f * apq);
+          tt = (tau >= 0.f ? 1.f : -1.f) / (fabsf(tau) + sqrtf(1.f + tau * tau));
+          c = rsqrtf(1.f + tt * tt);
+          sn = tt * c;
+          flag[sweep & 1] = 1;
+        }
+        cs_c[tid] = c; cs_s[tid] = sn; cs_t[tid] = tt;
+        pp[tid] = p | (q << 16);
+        jb.log[(int64_t)round * P + tid] = make_float2(c, sn);
+      }
+      __syncthreads();
+      if (s == 0 && tid == 0) flag[(sweep + 1) & 1] = 0;   // read by everyone at the end of sweep-1
+      // phase 2: independent 2x2 blocks B' = R1^T B R2 (R = [[c, s], [-s, c]])
+      for (int b = tid; b < nblk; b += EJ_THREADS) {
+        const int r = b / (P + 1), ci = b - r * (P + 1);
+        int k1, k2;
+        if (ci < P - r) { k1 = r; k2 = r + ci; }
+        else { k1 = P - 1 - r; k2 = k1 + (ci - (P - r)); }
+        const int pq1 = pp[k1];
+        const int p1 = pq1 & 0xffff, q1 = pq1 >> 16;
+        if (k1 == k2) {
+          const float tt = cs_t[k1];
+          if (tt != 0.f) {
+            const int ipq = tri_at(p1, q1, np), ipp = tri_idx(p1, p1, np), iqq = tri_idx(q1, q1, np);
+            const float apq = tri[ipq];
+            tri[ipp] -= tt * apq;
+            tri[iqq] += tt * apq;
+            tri[ipq] = 0.f;
+          }
+          continue;
+        }
+        const float c1 = cs_c[k1], s1 = cs_s[k1], c2 = cs_c[k2], s2 = cs_s[k2];
+        if (s1 == 0.f && s2 == 0.f) continue;
+        const int pq2 = pp[k2];
+        const int p2 = pq2 & 0xffff, q2 = pq2 >> 16;
+        const int i11 = tri_at(p1, p2, np), i12 = tri_at(p1, q2, np), i21 = tri_at(q1, p2, np),
+                  i22 = tri_at(q1, q2, np);
+        const float b11 = tri[i11], b12 = tri[i12], b21 = tri[i21], b22 = tri[i22];
+        // B R2
+        const float x11 = c2 * b11 - s2 * b12, x12 = s2 * b11 + c2 * b12;
+        const float x21 = c2 * b21 - s2 * b22, x22 = s2 * b21 + c2 * b22;
+        // R1^T (B R2)
+        tri[i11] = c1 * x11 - s1 * x21;
+        tri[i12] = c1 * x12 - s1 * x22;
+        tri[i21] = s1 * x11 + c1 * x21;
+        tri[i22] = s1 * x12 + c1 * x22;
+      }
+      __syncthreads();
+      ++round;
+    }
+    if (flag[sweep & 1] == 0) { round -= m; ++sweep; break; }   // a sweep with no rotation: not logged
+  }
+  // eigenvalues = diagonal; rank sort (stable) over the n real indices
+  if (tid < n) {
+    const float wi = tri[tri_idx(tid, tid, np)];
+    int rank = tid;
+    if (sort_desc) {
+      rank = 0;
+      for (int j2 = 0; j2 < n; ++j2) {
+        const float wj = tri[tri_idx(j2, j2, np)];
+        rank += (wj > wi) || (wj == wi && j2 < tid);
+      }
+    }
+    jb.w[rank] = wi;
+    if (jb.wpow) jb.wpow[rank] = wpow_of(wi, pow_floor, pow_expo);
+    jb.perm[rank] = tid;
+  }
+  if (tid == 0) *jb.nrounds = round;
+}
+
+// Replay the rotation log on rows of V (V = V0 * J_1 * J_2 * ...), V0 = identity or a given
+// basis; output columns in the eigh_jacobi_kernel's sorted order.  In place (Vout == V0) is fine:
+// a workgroup reads all of its rows before it writes them.
+struct VecJob {
+  const float* V0; float* Vout; const int* perm; const float2* log; const int* nrounds;
+  int64_t ld0, ldo, n;
+};
+static_assert(sizeof(VecJob) == 8 * 8, "VecJob layout");
+
+constexpr int EV_ROWS = 32, EV_LD = EJ_MAXN + 4;
+
+__global__ __launch_bounds__(256) void eigh_vectors_kernel(const VecJob* __restrict__ jobs) {
+  __shared__ float Vs[EV_ROWS][EV_LD];
+  const VecJob jb = jobs[blockIdx.y];
+  const int n = (int)jb.n, np = (n + 3) & ~3, P = np >> 1, m = np - 1;
+  const int row0 = blockIdx.x * EV_ROWS;
+  if (row0 >= n) return;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < EV_ROWS * np; e += 256) {
+    const int r = e / np, c = e - r * np, gr = row0 + r;
+    float x = 0.f;
+    if (gr < n && c < n) x = jb.V0 ? jb.V0[(int64_t)gr * jb.ld0 + c] : (gr == c ? 1.f : 0.f);
+    Vs[r][c] = x;
+  }
+  const int nr = *jb.nrounds;
+  const int k = tid & 127, rsub = tid >> 7;   // pair k, rows rsub + 2j
+  const bool act = k < P;
+  float2 cur = make_float2(1.f, 0.f), nxt = make_float2(1.f, 0.f);
+  if (act && nr > 0) cur = jb.log[k];
+  __syncthreads();
+  for (int rd = 0; rd < nr; ++rd) {
+    if (act && rd + 1 < nr) nxt = jb.log[(int64_t)(rd + 1) * P + k];
+    if (act && cur.y != 0.f) {
+      int p, q;
+      rr_pair(rd % m, k, np, p, q);
+#pragma unroll 4
+      for (int j = 0; j < EV_ROWS / 2; ++j) {
+        const int r = rsub + 2 * j;
+        const float vp = Vs[r][p], vq = Vs[r][q];
+        Vs[r][p] = cur.x * vp - cur.y * vq;
+        Vs[r][q] = cur.y * vp + cur.x * vq;
+      }
+    }
+    cur = nxt;
+    __syncthreads();
+  }
+  for (int e = tid; e < EV_ROWS * n; e += 256) {
+    const int r = e / n, c = e - r * n, gr = row0 + r;
+    if (gr < n) jb.Vout[(int64_t)gr * jb.ldo + c] = Vs[r][jb.perm[c]];
+  }
+}
+
+// ------------------------------------------------------------------ Householder QR ----
+// Q of A[:, perm] (LAPACK sgeqrf + sorgqr conventions: H_j = I - tau v v^T, v_0 = 1,
+// beta = -sign(alpha) ||x||; tau = 0 when the sub-column is already zero).  Working copies are
+// column-major (W[k*n + i] = element (i, k)) so every column sweep is contiguous.
+struct QrJob {
+  const float* A; const int* perm; float* Q; float* W; float* Qt;
+  int64_t lda, ldq, n;
+};
+static_assert(sizeof(QrJob) == 8 * 8, "QrJob layout");
+
+constexpr int QR_THREADS = 1024, QR_MAXN = 1024;
+
+__global__ __launch_bounds__(QR_THREADS) void householder_qr_kernel(const QrJob* __restrict__ jobs) {
+  __shared__ float vsh[QR_MAXN];
+  __shared__ float tau_sh[QR_MAXN];
+  __shared__ float red[QR_THREADS / 64];
+  __shared__ float sc[2];
+  const QrJob jb = jobs[blockIdx.x];
+  const int n = (int)jb.n, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = QR_THREADS / 64;
+  float* W = jb.W;
+  float* Qt = jb.Qt;
+  for (int e = tid; e < n * n; e += QR_THREADS) {
+    const int k = e / n, i = e - k * n;
+    const int src = jb.perm ? jb.perm[k] : k;
+    W[e] = jb.A[(int64_t)i * jb.lda + src];
+  }
+  __syncthreads();
+  for (int j = 0; j < n; ++j) {
+    float* col = W + (int64_t)j * n;
+    // ||x[1:]||^2 of x = W[j:, j]
+    float s2 = 0.f;
+    for (int i = j + 1 + tid; i < n; i += QR_THREADS) s2 += col[i] * col[i];
+    s2 = block_sum(s2, red);
+    if (tid == 0) {
+      const float alpha = col[j];
+      float tau = 0.f, scale = 0.f, beta = alpha;
+      if (s2 > 0.f) {
+        beta = -copysignf(sqrtf(alpha * alpha + s2), alpha);
+        tau = (beta - alpha) / beta;
+        scale = 1.f / (alpha - beta);
+      }
+      tau_sh[j] = tau;
+      sc[0] = scale;
+      sc[1] = beta;
+    }
+    __syncthreads();
+    const float tau = tau_sh[j], scale = sc[0];
+    for (int i = j + tid; i < n; i += QR_THREADS) {
+      const float v = i == j ? 1.f : col[i] * scale;
+      vsh[i] = v;
+      if (i > j) col[i] = v;          // keep v below the diagonal (Q formation reads it back)
+    }
+    __syncthreads();
+    if (tau != 0.f) {
+      // trailing columns k > j: one wave per column, lanes over rows
+      for (int k = j + 1 + wv; k < n; k += nw) {
+        float* ck = W + (int64_t)k * n;
+        float d = 0.f;
+        for (int i = j + lane; i < n; i += 64) d += vsh[i] * ck[i];
+        d = wave_sum(d) * tau;
+        for (int i = j + lane; i < n; i += 64) ck[i] -= d * vsh[i];
+      }
+    }
+    __syncthreads();
+  }
+  // Q = H_0 ... H_{n-1} I, accumulated backwards on column-major Qt
+  for (int e = tid; e < n * n; e += QR_THREADS) {
+    const int k = e / n, i = e - k * n;
+    Qt[e] = i == k ? 1.f : 0.f;
+  }
+  __syncthreads();
+  for (int j = n - 1; j >= 0; --j) {
+    const float tau = tau_sh[j];
+    if (tau == 0.f) continue;   // uniform across the block
+    const float* col = W + (int64_t)j * n;
+    for (int i = j + tid; i < n; i += QR_THREADS) vsh[i] = i == j ? 1.f : col[i];
+    __syncthreads();
+    for (int k = j + wv; k < n; k += nw) {
+      float* ck = Qt + (int64_t)k * n;
+      float d = 0.f;
+      for (int i = j + lane; i < n; i += 64) d += vsh[i] * ck[i];
+      d = wave_sum(d) * tau;
+      for (int i = j + lane; i < n; i += 64) ck[i] -= d * vsh[i];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < n * n; e += QR_THREADS) {
+    const int i = e / n, k = e - i * n;
+    jb.Q[(int64_t)i * jb.ldq + k] = Qt[(int64_t)k * n + i];
+  }
+}
+
+// ------------------------------------------------------------------ SOAP helpers ----
+// Adam in the rotated basis (soap.py:249-268): m = b1 m + (1-b1) g'; v = b2 v + (1-b2) g'^2;
+// n' = (m / bc1) / (sqrt(v / bc2) + eps), step t = *step (device, counted from 1).
+__global__ __launch_bounds__(256) void soap_adam_kernel(const float* __restrict__ g, float* __restrict__ m,
+                                                        float* __restrict__ v, float* __restrict__ nrot, int64_t n,
+                                                        float b1, float b2, float eps, const int* step,
+                                                        int correct_bias) {
+  const float t = (float)(*step);
+  const float bc1 = correct_bias ? 1.f - powf(b1, t) : 1.f;
+  const float bc2 = correct_bias ? 1.f - powf(b2, t) : 1.f;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float gi = g[i];
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    nrot[i] = (mi / bc1) / (sqrtf(vi / bc2) + eps);
+  }
+}
+
+// Refresh ordering (soap.py:115-126): est_i = (Q^T M Q)_ii = sum_r Q[r,i] * T[r,i] with T = M Q;
+// perm = stable argsort(-est).  One workgroup per matrix.
+struct SortJob { const float* Q; const float* T; int* perm; int64_t ldq, ldt, n; };
+static_assert(sizeof(SortJob) == 6 * 8, "SortJob layout");
+
+__global__ __launch_bounds__(256) void soap_est_sort_kernel(const SortJob* __restrict__ jobs) {
+  __shared__ float est[QR_MAXN];
+  const SortJob jb = jobs[blockIdx.x];
+  const int n = (int)jb.n;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    float s = 0.f;
+    for (int r = 0; r < n; ++r) s += jb.Q[(int64_t)r * jb.ldq + i] * jb.T[(int64_t)r * jb.ldt + i];
+    est[i] = s;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const float e = est[i];
+    int rank = 0;
+    for (int j = 0; j < n; ++j) rank += (est[j] > e) || (est[j] == e && j < i);
+    jb.perm[rank] = i;
+  }
+}
+
+// v_new[i][j] = v[perm_l[i]][perm_r[j]] into tmp, one launch over all routed matrices.
+struct PermJob { const float* src; float* dst; const int* pl; const int* pr; int64_t rows, cols, first_block; };
+static_assert(sizeof(PermJob) == 7 * 8, "PermJob layout");
+
+__global__ __launch_bounds__(256) void permute_rc_kernel(const PermJob* __restrict__ jobs, int njobs) {
+  const int64_t bid = blockIdx.x;
+  int j = 0;
+  while (j + 1 < njobs && jobs[j + 1].first_block <= bid) ++j;
+  const PermJob& jb = jobs[j];
+  const int64_t e = (bid - jb.first_block) * 256 + threadIdx.x;
+  if (e >= jb.rows * jb.cols) return;
+  const int64_t r = e / jb.cols, c = e - r * jb.cols;
+  jb.dst[e] = jb.src[(int64_t)jb.pl[r] * jb.cols + jb.pr[c]];
+}
+
+}  // namespace pcv
+
+using namespace pcv;
+
+extern "C" int pcv_f32_job_size(void) { return (int)sizeof(F32Job); }
+extern "C" int pcv_eigh_job_size(void) { return (int)sizeof(EighJob); }
+extern "C" int pcv_vec_job_size(void) { return (int)sizeof(VecJob); }
+extern "C" int pcv_qr_job_size(void) { return (int)sizeof(QrJob); }
+extern "C" int pcv_sort_job_size(void) { return (int)sizeof(SortJob); }
+extern "C" int pcv_perm_job_size(void) { return (int)sizeof(PermJob); }
+
+extern "C" int pcv_gemm_f32_grouped(const void* jobs_dev, int njobs, int64_t total_tiles, void* stream) {
+  if (!jobs_dev || njobs <= 0 || total_tiles <= 0) return PCV_EINVAL;
+  hipLaunchKernelGGL(gemm_f32_grouped_kernel, dim3((unsigned)total_tiles), dim3(256), 0, (hipStream_t)stream,
+                     (const F32Job*)jobs_dev, njobs);
+  return pcv_launch_status();
+}
+
+extern "C" int64_t pcv_eigh_log_floats(int64_t n, int max_sweeps) {
+  const int64_t np = (n + 3) & ~3ll;
+  return 2 * (int64_t)max_sweeps * (np - 1) * (np / 2);
+}
+
+extern "C" int pcv_eigh_jacobi(const void* jobs_dev, int njobs, int max_n, int max_sweeps, float tol_rel,
+                               float tol_abs_rel, int sort_desc, float pow_floor, float pow_expo, void* stream) {
+  if (!jobs_dev || njobs <= 0 || max_n <= 1 || max_n > EJ_MAXN || max_sweeps <= 0) return PCV_EINVAL;
+  const int np = (max_n + 3) & ~3;
+  const size_t lds = (size_t)(np * (np + 1) / 2 + 3 * (EJ_MAXN / 2) + EJ_MAXN / 2) * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)eigh_jacobi_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)((size_t)(EJ_MAXN * (EJ_MAXN + 1) / 2 + 2 * EJ_MAXN) * 4));
+    attr = true;
+  }
+  hipLaunchKernelGGL(eigh_jacobi_kernel, dim3(njobs), dim3(EJ_THREADS), lds, (hipStream_t)stream,
+                     (const EighJob*)jobs_dev, max_sweeps, tol_rel, tol_abs_rel, sort_desc, pow_floor, pow_expo);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_eigh_vectors(const void* jobs_dev, int njobs, int max_n, void* stream) {
+  if (!jobs_dev || njobs <= 0 || max_n <= 1 || max_n > EJ_MAXN) return PCV_EINVAL;
+  hipLaunchKernelGGL(eigh_vectors_kernel, dim3((max_n + EV_ROWS - 1) / EV_ROWS, njobs), dim3(256), 0,
+                     (hipStream_t)stream, (const VecJob*)jobs_dev);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_householder_qr(const void* jobs_dev, int njobs, int max_n, void* stream) {
+  if (!jobs_dev || njobs <= 0 || max_n <= 0 || max_n > QR_MAXN) return PCV_EINVAL;
+  hipLaunchKernelGGL(householder_qr_kernel, dim3(njobs), dim3(QR_THREADS), 0, (hipStream_t)stream,
+                     (const QrJob*)jobs_dev);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_soap_adam(const float* g, float* m, float* v, float* nrot, int64_t n, float b1, float b2,
+                             float eps, const int* step, int correct_bias, void* stream) {
+  if (!g || !m || !v || !nrot || !step || n < 0) return PCV_EINVAL;
+  if (n == 0) return 0;
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(soap_adam_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0,
+                     (hipStream_t)stream, g, m, v, nrot, n, b1, b2, eps, step, correct_bias);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_soap_est_sort(const void* jobs_dev, int njobs, void* stream) {
+  if (!jobs_dev || njobs <= 0) return PCV_EINVAL;
+  hipLaunchKernelGGL(soap_est_sort_kernel, dim3(njobs), dim3(256), 0, (hipStream_t)stream,
+                     (const SortJob*)jobs_dev);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_permute_rc(const void* jobs_dev, int njobs, int64_t total_blocks, void* stream) {
+  if (!jobs_dev || njobs <= 0 || total_blocks <= 0) return PCV_EINVAL;
+  hipLaunchKernelGGL(permute_rc_kernel, dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const PermJob*)jobs_dev, njobs);
+  return pcv_launch_status();
+}

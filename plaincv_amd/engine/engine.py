@@ -166,9 +166,12 @@ class GraphedTrainStep:
         self.images = torch.zeros(tuple(image_shape), dtype=torch.uint8, device=dev)
         self.labels = self.runner.labels   # the runner's static label buffer (no second copy)
         self.distributed = dp.world_size() > 1
+        # SOAP/Shampoo steps are host-driven (first step, refreshes, basis restarts): they run
+        # eagerly after the captured forward/backward.
+        self.opt_graphed = bool(getattr(state.tx, "graphable", True))
         self.stream = torch.cuda.Stream(device=dev)
         self.g_fb = torch.cuda.CUDAGraph()
-        self.g_opt = torch.cuda.CUDAGraph() if self.distributed else None
+        self.g_opt = torch.cuda.CUDAGraph() if (self.distributed and self.opt_graphed) else None
         s = self.stream
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -176,11 +179,12 @@ class GraphedTrainStep:
                 self._fb()
                 self._opt()
             torch.cuda.synchronize()
-            if self.distributed:
+            if self.distributed or not self.opt_graphed:
                 with torch.cuda.graph(self.g_fb, stream=s):
                     self._fb()
-                with torch.cuda.graph(self.g_opt, stream=s):
-                    self._opt()
+                if self.g_opt is not None:
+                    with torch.cuda.graph(self.g_opt, stream=s):
+                        self._opt()
             else:
                 with torch.cuda.graph(self.g_fb, stream=s):
                     self._fb()
@@ -204,6 +208,9 @@ class GraphedTrainStep:
         self.g_fb.replay()
         if self.distributed:
             dp.all_reduce_grads(self.state.params)
+        if self.g_opt is not None:
             self.g_opt.replay()
+        elif self.distributed or not self.opt_graphed:
+            self._opt()
         self.state.step += 1
         return self.metrics

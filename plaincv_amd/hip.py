@@ -66,10 +66,24 @@ SIGNATURES = {
     "pcv_transpose_rec_size": [],
     "pcv_muon_mat_size": [],
     "pcv_chunk_size": [],
+    "pcv_f32_job_size": [],
+    "pcv_eigh_job_size": [],
+    "pcv_vec_job_size": [],
+    "pcv_qr_job_size": [],
+    "pcv_sort_job_size": [],
+    "pcv_perm_job_size": [],
+    "pcv_gemm_f32_grouped": [P, I32, I64, P],
+    "pcv_eigh_log_floats": [I64, I32],
+    "pcv_eigh_jacobi": [P, I32, I32, I32, F32, F32, I32, F32, F32, P],
+    "pcv_eigh_vectors": [P, I32, I32, P],
+    "pcv_householder_qr": [P, I32, I32, P],
+    "pcv_soap_adam": [P, P, P, P, I64, F32, F32, F32, P, I32, P],
+    "pcv_soap_est_sort": [P, I32, P],
+    "pcv_permute_rc": [P, I32, I64, P],
 }
 
 # non-status return types (everything else returns an int status)
-RESTYPES = {"pcv_attn_mask_words": I64, "pcv_gemm_grouped_plan_size": I64}
+RESTYPES = {"pcv_attn_mask_words": I64, "pcv_gemm_grouped_plan_size": I64, "pcv_eigh_log_floats": I64}
 
 _lib = None
 _err = None

@@ -1,0 +1,235 @@
+"""Host-side plans for the matrix-preconditioner kernels (csrc/precond.hip).
+
+Each plan packs its job records once (plain 8-byte fields: pointers, int64, double) into a
+device tensor, so a step is a fixed sequence of stream-ordered launches with no host work
+beyond the launch itself.  Shapes are validated here, before anything reaches a kernel.
+"""
+import struct
+
+import torch
+
+from .. import hip
+from ..hip import ptr, stream_ptr
+
+TILE = 64
+EIGH_MAX_N = 256
+
+
+def _addr(t):
+    return 0 if t is None else int(t.data_ptr())
+
+
+def _pack(records, fmt):
+    raw = b"".join(struct.pack(fmt, *r) for r in records)
+    return torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+
+
+def _ld(t):
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"expected a row-major 2-D fp32 matrix, got shape {tuple(t.shape)} strides {t.stride()}")
+    if t.dtype != torch.float32:
+        raise ValueError("fp32 operand expected")
+    return t.stride(0)
+
+
+class GemmF32:
+    """One grouped launch of C = alpha*adev^apow * op(A) diag(kscale) op(B) + beta*C + rscale*R
+    (+ bf16 copy Cb).  ``add(...)`` jobs, then ``finalize(device)``; ``run()`` per step."""
+
+    FMT = "<7Q13q3d"
+
+    def __init__(self):
+        self.jobs = []
+        self.dev = None
+
+    def add(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, kscale=None, r=None, rscale=0.0, cb=None,
+            alpha_dev=None, apow=1):
+        M, K = (a.shape[1], a.shape[0]) if ta else (a.shape[0], a.shape[1])
+        K2, N = (b.shape[1], b.shape[0]) if tb else (b.shape[0], b.shape[1])
+        if K != K2 or tuple(c.shape) != (M, N):
+            raise ValueError(f"gemm_f32 shapes: op(A) {M}x{K}, op(B) {K2}x{N}, C {tuple(c.shape)}")
+        if kscale is not None and kscale.numel() < K:
+            raise ValueError("kscale shorter than K")
+        if r is not None and tuple(r.shape) != (M, N):
+            raise ValueError("residual shape")
+        if cb is not None and (tuple(cb.shape) != (M, N) or cb.dtype != torch.bfloat16 or cb.stride(1) != 1):
+            raise ValueError("bf16 copy shape")
+        tiles_n = (N + TILE - 1) // TILE
+        self.jobs.append(dict(A=a, B=b, C=c, ks=kscale, R=r, Cb=cb, ad=alpha_dev, M=M, N=N, K=K, lda=_ld(a),
+                              ldb=_ld(b), ldc=_ld(c), ldr=_ld(r) if r is not None else 0,
+                              ldcb=cb.stride(0) if cb is not None else 0, ta=int(ta), tb=int(tb), apow=int(apow),
+                              tiles=((M + TILE - 1) // TILE) * tiles_n, tiles_n=tiles_n, alpha=float(alpha),
+                              beta=float(beta), rscale=float(rscale)))
+        return self
+
+    def finalize(self, device):
+        lib = hip.load()
+        assert lib.pcv_f32_job_size() == struct.calcsize(self.FMT)
+        recs, first = [], 0
+        for j in self.jobs:
+            recs.append((_addr(j["A"]), _addr(j["B"]), _addr(j["C"]), _addr(j["ks"]), _addr(j["R"]),
+                         _addr(j["Cb"]), _addr(j["ad"]), j["M"], j["N"], j["K"], j["lda"], j["ldb"], j["ldc"],
+                         j["ldr"], j["ldcb"], j["ta"], j["tb"], j["apow"], j["tiles_n"], first, j["alpha"],
+                         j["beta"], j["rscale"]))
+            first += j["tiles"]
+        self.total = first
+        self.dev = _pack(recs, self.FMT).to(device) if recs else None
+        return self
+
+    def run(self):
+        if self.dev is not None and self.total > 0:
+            hip.call("pcv_gemm_f32_grouped", ptr(self.dev), len(self.jobs), self.total, stream_ptr())
+
+
+class Eigh:
+    """Batched symmetric eigendecomposition (cyclic Jacobi, csrc/precond.hip) of n <= 256
+    matrices: eigenvalues w (descending if sort_desc), optional wpow = max(w, floor)^(-expo),
+    eigenvectors written to vout (starting from basis v0 when given: vout = v0 @ eigvecs(A))."""
+
+    FMT_E = "<6Q2qd"
+    FMT_V = "<5Q3q"
+
+    def __init__(self, device, max_sweeps=15, tol_rel=2e-7, tol_abs_rel=1e-9, sort_desc=True, pow_floor=0.0,
+                 pow_expo=0.0):
+        self.device = torch.device(device)
+        self.max_sweeps, self.tol_rel, self.tol_abs_rel = int(max_sweeps), float(tol_rel), float(tol_abs_rel)
+        self.sort_desc, self.pow_floor, self.pow_expo = int(bool(sort_desc)), float(pow_floor), float(pow_expo)
+        self.items = []
+
+    def add(self, a, vout, v0=None, shift=0.0, want_pow=False):
+        n = a.shape[0]
+        if a.shape != (n, n) or vout.shape != (n, n) or (v0 is not None and v0.shape != (n, n)):
+            raise ValueError("eigh: square matrices of one size per job")
+        if n > EIGH_MAX_N or n < 2:
+            raise NotImplementedError(f"eigh kernel handles 2 <= n <= {EIGH_MAX_N} (got {n})")
+        _ld(a), _ld(vout)
+        lib = hip.load()
+        it = dict(a=a, vout=vout, v0=v0, shift=float(shift), n=n,
+                  w=torch.zeros(n, dtype=torch.float32, device=self.device),
+                  wpow=torch.zeros(n, dtype=torch.float32, device=self.device) if want_pow else None,
+                  perm=torch.zeros(n, dtype=torch.int32, device=self.device),
+                  log=torch.zeros(int(lib.pcv_eigh_log_floats(n, self.max_sweeps)), dtype=torch.float32,
+                                  device=self.device),
+                  nrounds=torch.zeros(1, dtype=torch.int32, device=self.device))
+        self.items.append(it)
+        return it
+
+    def finalize(self):
+        lib = hip.load()
+        assert lib.pcv_eigh_job_size() == struct.calcsize(self.FMT_E)
+        assert lib.pcv_vec_job_size() == struct.calcsize(self.FMT_V)
+        e, v = [], []
+        for it in self.items:
+            e.append((_addr(it["a"]), _addr(it["w"]), _addr(it["wpow"]), _addr(it["perm"]), _addr(it["log"]),
+                      _addr(it["nrounds"]), it["a"].stride(0), it["n"], it["shift"]))
+            v.append((_addr(it["v0"]), _addr(it["vout"]), _addr(it["perm"]), _addr(it["log"]), _addr(it["nrounds"]),
+                      it["v0"].stride(0) if it["v0"] is not None else 0, it["vout"].stride(0), it["n"]))
+        self.max_n = max([it["n"] for it in self.items], default=0)
+        self.e_dev = _pack(e, self.FMT_E).to(self.device) if e else None
+        self.v_dev = _pack(v, self.FMT_V).to(self.device) if v else None
+        return self
+
+    def run(self):
+        if not self.items:
+            return
+        s = stream_ptr()
+        hip.call("pcv_eigh_jacobi", ptr(self.e_dev), len(self.items), self.max_n, self.max_sweeps, self.tol_rel,
+                 self.tol_abs_rel, self.sort_desc, self.pow_floor, self.pow_expo, s)
+        hip.call("pcv_eigh_vectors", ptr(self.v_dev), len(self.items), self.max_n, s)
+
+
+class HouseholderQR:
+    """Q of A[:, perm] for a batch of square matrices (one workgroup each)."""
+
+    FMT = "<5Q3q"
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.items = []
+
+    def add(self, a, q, perm=None):
+        n = a.shape[0]
+        if a.shape != (n, n) or q.shape != (n, n):
+            raise ValueError("qr: square matrices expected")
+        if n > 1024:
+            raise NotImplementedError("householder_qr handles n <= 1024")
+        _ld(a), _ld(q)
+        self.items.append(dict(a=a, q=q, perm=perm, n=n,
+                               w=torch.zeros(n * n, dtype=torch.float32, device=self.device),
+                               qt=torch.zeros(n * n, dtype=torch.float32, device=self.device)))
+
+    def finalize(self):
+        lib = hip.load()
+        assert lib.pcv_qr_job_size() == struct.calcsize(self.FMT)
+        recs = [(_addr(it["a"]), _addr(it["perm"]), _addr(it["q"]), _addr(it["w"]), _addr(it["qt"]),
+                 it["a"].stride(0), it["q"].stride(0), it["n"]) for it in self.items]
+        self.max_n = max([it["n"] for it in self.items], default=0)
+        self.dev = _pack(recs, self.FMT).to(self.device) if recs else None
+        return self
+
+    def run(self):
+        if self.items:
+            hip.call("pcv_householder_qr", ptr(self.dev), len(self.items), self.max_n, stream_ptr())
+
+
+class EstSort:
+    """perm = stable argsort(-diag(Q^T M Q)) given T = M Q (soap.py:115-126)."""
+
+    FMT = "<3Q3q"
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.recs = []
+
+    def add(self, q, t, perm):
+        n = q.shape[0]
+        if q.shape != (n, n) or t.shape != (n, n) or perm.numel() != n:
+            raise ValueError("est_sort shapes")
+        self.recs.append((_addr(q), _addr(t), _addr(perm), _ld(q), _ld(t), n))
+
+    def finalize(self):
+        assert hip.load().pcv_sort_job_size() == struct.calcsize(self.FMT)
+        self.dev = _pack(self.recs, self.FMT).to(self.device) if self.recs else None
+        return self
+
+    def run(self):
+        if self.recs:
+            hip.call("pcv_soap_est_sort", ptr(self.dev), len(self.recs), stream_ptr())
+
+
+class PermuteRC:
+    """dst[i, j] = src[pl[i], pr[j]] for contiguous [rows, cols] matrices, one launch."""
+
+    FMT = "<4Q3q"
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.recs = []
+        self.total = 0
+
+    def add(self, src, dst, pl, pr):
+        rows, cols = src.shape
+        if not (src.is_contiguous() and dst.is_contiguous()) or dst.shape != src.shape:
+            raise ValueError("permute_rc needs contiguous equal-shape matrices")
+        if pl.numel() != rows or pr.numel() != cols:
+            raise ValueError("permute_rc permutation sizes")
+        self.recs.append((_addr(src), _addr(dst), _addr(pl), _addr(pr), rows, cols, self.total))
+        self.total += (rows * cols + 255) // 256
+
+    def finalize(self):
+        assert hip.load().pcv_perm_job_size() == struct.calcsize(self.FMT)
+        self.dev = _pack(self.recs, self.FMT).to(self.device) if self.recs else None
+        return self
+
+    def run(self):
+        if self.recs:
+            hip.call("pcv_permute_rc", ptr(self.dev), len(self.recs), self.total, stream_ptr())
+
+
+def soap_adam(g, m, v, nrot, b1, b2, eps, step_dev, correct_bias=True):
+    n = g.numel()
+    for t in (m, v, nrot):
+        if t.numel() != n or not t.is_contiguous():
+            raise ValueError("soap_adam arenas must be contiguous and equal-sized")
+    hip.call("pcv_soap_adam", ptr(g), ptr(m), ptr(v), ptr(nrot), n, float(b1), float(b2), float(eps), ptr(step_dev),
+             int(bool(correct_bias)), stream_ptr())

@@ -1,46 +1,36 @@
-"""SOAP (optim/soap.py:136-368) on the GPU.
+"""SOAP (optim/soap.py:136-368) on the GPU through the preconditioner kernels.
 
-Routed (``should_use_matrix_preconditioner``) leaves keep m, v (param shape),
-L, R (Kronecker second moments), QL, QR; step -1 = first step initialises the
-eigenbases with a ZERO update (soap.py:201-229); later steps run Adam in the
-rotated basis, project back, EMA L/R with the raw gradient and refresh the
-bases by one QR power step every ``precondition_frequency`` steps with the v
-re-index (soap.py:108-133).  Non-routed leaves use AdamW with coupled weight
-decay (soap.py:310-335) through the multi-tensor kernel.
+Routed (``should_use_matrix_preconditioner``) leaves keep m, v (param shape, in the
+rotated basis), L, R (Kronecker second moments), QL, QR.  Per step (soap.py:201-300):
 
-Round-1 status: the per-matrix products, eigh and QR run as fp32 torch GPU
-ops (rocBLAS/rocSOLVER) on the step's stream; moving them onto the pcv MFMA
-GEMM + a HIP Jacobi eigh is listed in DESIGN.md §7.
+    L = b2s L + (1-b2s) g g^T;  R = b2s R + (1-b2s) g^T g                 (grouped fp32 GEMM)
+    first step:  QL, QR = eigh_desc(L), eigh_desc(R); update = 0            (Jacobi eigh)
+    otherwise:   g' = QL^T g QR                                             (2 grouped GEMMs)
+                 m, v = Adam moments of g';  n' = m^/(sqrt(v^)+eps)         (1 flat launch)
+                 u = -lr (QL n' QR^T + wd p)  -> applied to p and its bf16 shadow in the
+                 last GEMM's epilogue;  m_orig = QL m QR^T
+                 every f steps: est = diag(Q^T M Q), stable argsort desc, v re-indexed,
+                 Q = qr(M Q[:, perm])                                       (sort, permute, Householder QR)
+                 m = QL^T m_orig QR
+Non-routed leaves: AdamW with coupled weight decay (soap.py:310-335) via the multi-tensor kernel.
+Every matrix product runs as one grouped launch over all routed matrices (csrc/precond.hip).
 """
-from types import SimpleNamespace
-
 import torch
 
 from .. import kernels as K
 from .adamw import AdamBranch, _views
 from .base import GradientTransformation, OptState, ensure_grads
 from .matrix_routing import should_use_matrix_preconditioner
+from .precond import Eigh, EstSort, GemmF32, HouseholderQR, PermuteRC, soap_adam
 
 
-def _eigh_desc(mat):
-    m = 0.5 * (mat + mat.t())
-    _, q = torch.linalg.eigh(m + 1e-30 * torch.eye(m.shape[0], dtype=m.dtype, device=m.device))
-    return torch.flip(q, dims=[1])
-
-
-def _refresh(L, R, QL, QR, v):
-    est_l = torch.diag(QL.t() @ L @ QL)
-    il = torch.argsort(-est_l, stable=True)
-    v = v[il, :]
-    QLn, _ = torch.linalg.qr(L @ QL[:, il], mode="reduced")
-    est_r = torch.diag(QR.t() @ R @ QR)
-    ir = torch.argsort(-est_r, stable=True)
-    v = v[:, ir]
-    QRn, _ = torch.linalg.qr(R @ QR[:, ir], mode="reduced")
-    return QLn, QRn, v
+class _Mat:
+    pass
 
 
 class Soap(GradientTransformation):
+    graphable = False      # first step / refresh steps change the launch sequence (host-driven)
+
     def __init__(self, learning_rate, b1=0.95, b2=0.95, eps=1e-8, weight_decay=0.01, precondition_frequency=10,
                  shampoo_beta2=None, correct_bias=True):
         self.lr = float(learning_rate)
@@ -50,61 +40,119 @@ class Soap(GradientTransformation):
         self.correct_bias = bool(correct_bias)
 
     def init(self, store):
-        st = OptState(store.device)
+        dev = store.device
+        st = OptState(dev)
         st.tensors["mu"] = torch.zeros_like(store.flat)
         st.tensors["nu"] = torch.zeros_like(store.flat)
         st.upd = torch.zeros_like(store.flat)
         routed = [k for k, p in store.params.items() if should_use_matrix_preconditioner(k, p)]
         rest = [k for k in store.params if k not in routed]
-        if not self.correct_bias:
-            raise NotImplementedError("correct_bias=False")
         st.branch = AdamBranch(store, rest, self.b1, self.b2, self.eps, 0.0, self.wd, False)
-        st.mats = {}
-        for k in routed:
+        st.routed = routed
+        st.host_step = -1
+        st.t_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        sizes = [store.params[k].numel() for k in routed]
+        tot = max(1, sum(sizes))
+        for name in ("m", "v", "grot", "nrot", "vtmp"):
+            st.tensors["soap_" + name] = torch.zeros(tot, dtype=torch.float32, device=dev)
+        st.mats = []
+        off = 0
+        for k, sz in zip(routed, sizes):
             r, c = store.params[k].shape
-            dev = store.device
-            st.mats[k] = SimpleNamespace(
-                m=torch.zeros(r, c, device=dev), v=torch.zeros(r, c, device=dev),
-                L=torch.zeros(r, r, device=dev), R=torch.zeros(c, c, device=dev),
-                QL=torch.eye(r, device=dev), QR=torch.eye(c, device=dev), step=-1)
+            s = _Mat()
+            s.name, s.r, s.c = k, r, c
+            for name in ("m", "v", "grot", "nrot", "vtmp"):
+                setattr(s, name, st.tensors["soap_" + name][off:off + sz].view(r, c))
+            off += sz
+            z = lambda a, b: torch.zeros(a, b, dtype=torch.float32, device=dev)  # noqa: E731
+            s.L, s.R = z(r, r), z(c, c)
+            s.QL = torch.eye(r, dtype=torch.float32, device=dev)
+            s.QR = torch.eye(c, dtype=torch.float32, device=dev)
+            s.T1, s.X1, s.Y1, s.morig, s.Z = z(r, c), z(r, c), z(r, c), z(r, c), z(r, c)
+            s.TL, s.TR = z(r, r), z(c, c)
+            s.perm_l = torch.zeros(r, dtype=torch.int32, device=dev)
+            s.perm_r = torch.zeros(c, dtype=torch.int32, device=dev)
+            st.mats.append(s)
+        st.plans = {}
         return st
 
-    def _run(self, store, st, gscale, apply):
-        gs = gscale if gscale is not None else None
-        for k, s in st.mats.items():
-            g = store.grads[k]
-            if gs is not None:
-                g = g * gs
-            p = store.params[k]
-            L = self.sb2 * s.L + (1.0 - self.sb2) * (g @ g.t())
-            R = self.sb2 * s.R + (1.0 - self.sb2) * (g.t() @ g)
-            if s.step < 0:
-                s.L, s.R, s.QL, s.QR, s.step = L, R, _eigh_desc(L), _eigh_desc(R), 0
-                u = torch.zeros_like(g)
-            else:
-                s.step += 1
-                t = s.step
-                g_rot = s.QL.t() @ g @ s.QR
-                s.m = self.b1 * s.m + (1.0 - self.b1) * g_rot
-                s.v = self.b2 * s.v + (1.0 - self.b2) * g_rot * g_rot
-                n_rot = (s.m / (1.0 - self.b1 ** t)) / (torch.sqrt(s.v / (1.0 - self.b2 ** t)) + self.eps)
-                n = s.QL @ n_rot @ s.QR.t()
-                if self.wd != 0.0:
-                    n = n + self.wd * p
-                m_orig = s.QL @ s.m @ s.QR.t()
-                if self.f > 0 and t % self.f == 0:
-                    s.QL, s.QR, s.v = _refresh(L, R, s.QL, s.QR, s.v)
-                s.m = s.QL.t() @ m_orig @ s.QR
-                s.L, s.R = L, R
-                u = -self.lr * n
+    # ------------------------------------------------------------------
+    def _plans(self, store, st, gscale, apply):
+        key = (int(gscale.data_ptr()) if gscale is not None else 0, bool(apply))
+        if key in st.plans:
+            return st.plans[key]
+        dev = store.device
+        pl = {}
+        gram, init = GemmF32(), Eigh(dev, sort_desc=True)
+        rot1, rot2, back1, back2 = GemmF32(), GemmF32(), GemmF32(), GemmF32()
+        ref1, srt, perm, qr = GemmF32(), EstSort(dev), PermuteRC(dev), HouseholderQR(dev)
+        rep1, rep2 = GemmF32(), GemmF32()
+        for s in st.mats:
+            g, p = store.grads[s.name], store.params[s.name]
+            gram.add(g, g, s.L, tb=True, alpha=1.0 - self.sb2, beta=self.sb2, alpha_dev=gscale, apow=2)
+            gram.add(g, g, s.R, ta=True, alpha=1.0 - self.sb2, beta=self.sb2, alpha_dev=gscale, apow=2)
+            init.add(s.L, s.QL)
+            init.add(s.R, s.QR)
+            rot1.add(s.QL, g, s.T1, ta=True, alpha_dev=gscale, apow=1)
+            rot2.add(s.T1, s.QR, s.grot)
+            back1.add(s.QL, s.nrot, s.X1)
+            back1.add(s.QL, s.m, s.Y1)
             if apply:
-                p.add_(u)
-                store.bf16[k].copy_(p)
+                back2.add(s.X1, s.QR, p, tb=True, alpha=-self.lr, beta=1.0 - self.lr * self.wd,
+                          cb=store.bf16[s.name])
             else:
-                store._view(st.upd, store.leaf(k)).copy_(u)
+                back2.add(s.X1, s.QR, store._view(st.upd, store.leaf(s.name)), tb=True, alpha=-self.lr, r=p,
+                          rscale=-self.lr * self.wd)
+            back2.add(s.Y1, s.QR, s.morig, tb=True)
+            ref1.add(s.L, s.QL, s.TL)
+            ref1.add(s.R, s.QR, s.TR)
+            srt.add(s.QL, s.TL, s.perm_l)
+            srt.add(s.QR, s.TR, s.perm_r)
+            perm.add(s.v, s.vtmp, s.perm_l, s.perm_r)
+            qr.add(s.TL, s.QL, s.perm_l)
+            qr.add(s.TR, s.QR, s.perm_r)
+            rep1.add(s.QL, s.morig, s.Z, ta=True)
+            rep2.add(s.Z, s.QR, s.m)
+        for name, obj in (("gram", gram), ("rot1", rot1), ("rot2", rot2), ("back1", back1), ("back2", back2),
+                          ("ref1", ref1), ("rep1", rep1), ("rep2", rep2)):
+            pl[name] = obj.finalize(dev)
+        pl["init"] = init.finalize()
+        pl["sort"], pl["perm"], pl["qr"] = srt.finalize(), perm.finalize(), qr.finalize()
+        st.plans[key] = pl
+        return pl
+
+    def _run(self, store, st, gscale, apply):
+        if st.mats:
+            pl = self._plans(store, st, gscale, apply)
+            pl["gram"].run()
+            if st.host_step < 0:
+                pl["init"].run()
+                st.host_step = 0
+                if not apply:
+                    for s in st.mats:
+                        store._view(st.upd, store.leaf(s.name)).zero_()
+            else:
+                st.host_step += 1
+                K.step_bump(st.t_dev)
+                pl["rot1"].run()
+                pl["rot2"].run()
+                soap_adam(st.tensors["soap_grot"], st.tensors["soap_m"], st.tensors["soap_v"],
+                          st.tensors["soap_nrot"], self.b1, self.b2, self.eps, st.t_dev, self.correct_bias)
+                pl["back1"].run()
+                pl["back2"].run()
+                if self.f > 0 and st.host_step % self.f == 0:
+                    pl["ref1"].run()
+                    pl["sort"].run()
+                    pl["perm"].run()
+                    st.tensors["soap_v"].copy_(st.tensors["soap_vtmp"])
+                    pl["qr"].run()
+                pl["rep1"].run()
+                pl["rep2"].run()
         st.branch.run(store, st.tensors["mu"], st.tensors["nu"], st.count, self.lr, gscale=gscale,
                       upd=None if apply else st.upd, apply=apply)
         K.step_bump(st.count)
+        if apply:
+            store.version += 1
 
     def update(self, grads, state, params=None):
         ensure_grads(params, grads)

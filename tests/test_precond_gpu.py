@@ -1,0 +1,284 @@
+"""SOAP / Shampoo preconditioner kernels (csrc/precond.hip) on the GPU.
+
+Kernel level (vs torch fp64 on the same device, a checker only):
+  grouped fp32 GEMM  max|err| <= 2e-5 * sum|a||b|-scale (exact-fp32 MFMA chain)
+  Jacobi eigh        eigenvalues within 2e-5 * ||A||, ||A V - V diag(w)|| <= 5e-5 ||A||, ||V^T V - I|| <= 5e-5
+  Householder QR     Q within 1e-4 of LAPACK's Q (same sign convention) for full-rank inputs;
+                     orthonormal and A[:, perm] = Q (Q^T A[:, perm]) with upper-triangular R otherwise
+Optimizer level (vs the CPU oracle, oracle/optim.py, fp32):
+  Shampoo  updates after 6 steps (rectangular + square routed leaves): max|du| <= 2e-3 * lr-scale
+  SOAP     square full-rank leaves over 12 steps incl. two QR refreshes (f = 5): max|du| <= 5e-3 * lr-scale;
+           step 0 routed update exactly 0.  (Rectangular SOAP factors are rank deficient, so their
+           eigenbasis inside the null space is arbitrary in ANY eigh -- jax's and torch's differ too --
+           and trajectories there are compared through invariants only.)
+"""
+from collections import OrderedDict
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _gemm_case(dev, M, N, K, ta, tb, ks=False, beta=0.0, res=False, cb=False, adev=None, apow=1):
+    from plaincv_amd.optim.precond import GemmF32
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 3 + K + ta * 2 + tb)
+    a = torch.randn((K, M) if ta else (M, K), generator=g).to(dev)
+    b = torch.randn((N, K) if tb else (K, N), generator=g).to(dev)
+    c = torch.randn(M, N, generator=g).to(dev)
+    c0 = c.clone()
+    kv = torch.rand(K, generator=g).to(dev) if ks else None
+    r = torch.randn(M, N, generator=g).to(dev) if res else None
+    cbt = torch.zeros(M, N, dtype=torch.bfloat16, device=dev) if cb else None
+    plan = GemmF32().add(a, b, c, ta=ta, tb=tb, alpha=0.7, beta=beta, kscale=kv, r=r, rscale=-0.3, cb=cbt,
+                         alpha_dev=adev, apow=apow).finalize(dev)
+    plan.run()
+    torch.cuda.synchronize()
+    A = (a.t() if ta else a).double()
+    B = (b.t() if tb else b).double()
+    if kv is not None:
+        A = A * kv.double()[None, :]
+    s = 0.7 * (adev.item() ** apow if adev is not None else 1.0)
+    ref = s * A @ B + beta * c0.double() + (-0.3 * r.double() if res else 0.0)
+    scale = (A.abs() @ B.abs()).max().item() + 1.0
+    err = (c.double() - ref).abs().max().item()
+    assert err <= 2e-5 * scale, (M, N, K, ta, tb, err, scale)
+    if cb:
+        assert (cbt.float() - c).abs().max().item() <= 1e-2 * c.abs().max().item()
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 64, 64), (37, 50, 29), (200, 128, 256), (1, 300, 5)])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (1, 0), (0, 1), (1, 1)])
+def test_gemm_f32_grouped_shapes(dev, M, N, K, ta, tb):
+    _gemm_case(dev, M, N, K, ta, tb)
+
+
+def test_gemm_f32_epilogue_and_grouping(dev):
+    from plaincv_amd.optim.precond import GemmF32
+    _gemm_case(dev, 70, 90, 33, 1, 1, ks=True, beta=0.5, res=True, cb=True,
+               adev=torch.tensor([1.5], device=dev), apow=2)
+    # several jobs of different shapes in ONE launch
+    g = torch.Generator().manual_seed(3)
+    plan, refs = GemmF32(), []
+    for (M, N, K) in [(13, 17, 19), (128, 64, 200), (65, 129, 3)]:
+        a, b = torch.randn(M, K, generator=g).to(dev), torch.randn(K, N, generator=g).to(dev)
+        c = torch.zeros(M, N, device=dev)
+        plan.add(a, b, c)
+        refs.append((c, a.double() @ b.double()))
+    plan.finalize(dev).run()
+    torch.cuda.synchronize()
+    for c, ref in refs:
+        assert (c.double() - ref).abs().max().item() < 1e-4
+
+
+def _spd(n, rank, g, dev, scale=1.0):
+    x = torch.randn(n, rank, generator=g, dtype=torch.float64) * scale
+    return (x @ x.t()).float().to(dev)
+
+
+@pytest.mark.parametrize("n,rank", [(2, 2), (37, 50), (128, 400), (200, 200), (256, 300), (256, 100), (64, 1)])
+def test_eigh_jacobi(dev, n, rank):
+    from plaincv_amd.optim.precond import Eigh
+    g = torch.Generator().manual_seed(n + rank)
+    A = _spd(n, rank, g, dev)
+    V = torch.zeros(n, n, device=dev)
+    e = Eigh(dev, sort_desc=True)
+    it = e.add(A, V)
+    e.finalize().run()
+    torch.cuda.synchronize()
+    Ad = A.double()
+    w_ref = torch.linalg.eigvalsh(Ad).flip(0)
+    an = w_ref.abs().max().item()
+    w, Vd = it["w"].double(), V.double()
+    assert (w - w_ref).abs().max().item() <= 2e-5 * an
+    assert torch.all(w[:-1] >= w[1:])
+    assert (Ad @ Vd - Vd * w[None, :]).norm().item() <= 5e-5 * an * n ** 0.5
+    assert (Vd.t() @ Vd - torch.eye(n, device=dev, dtype=torch.float64)).abs().max().item() <= 5e-5
+    assert int(it["nrounds"].item()) > 0
+
+
+def test_eigh_warm_start_and_inverse_root(dev):
+    """Shampoo's use: eigh of U^T L U + eps I from a previous basis U gives the same
+    P = U' max(w, eps)^(-1/4) U'^T as a cold eigh of L + eps I, in fewer rounds."""
+    from plaincv_amd.optim.precond import Eigh, GemmF32
+    n, eps = 96, 1e-4
+    g = torch.Generator().manual_seed(9)
+    L0 = _spd(n, 40, g, dev, 0.1) + eps * torch.eye(n, device=dev)
+    dL = _spd(n, 3, g, dev, 0.02)
+    U = torch.zeros(n, n, device=dev)
+    cold = Eigh(dev, sort_desc=False, pow_floor=eps, pow_expo=0.25)
+    c_it = cold.add(L0, U, shift=eps, want_pow=True)
+    cold.finalize().run()
+    L1 = L0 + dL
+    T, A = torch.zeros(n, n, device=dev), torch.zeros(n, n, device=dev)
+    GemmF32().add(L1, U, T).finalize(dev).run()
+    GemmF32().add(U, T, A, ta=True).finalize(dev).run()
+    warm = Eigh(dev, sort_desc=False, pow_floor=eps, pow_expo=0.25)
+    w_it = warm.add(A, U, v0=U, shift=eps, want_pow=True)
+    warm.finalize().run()
+    P = torch.zeros(n, n, device=dev)
+    GemmF32().add(U, U, P, tb=True, kscale=w_it["wpow"]).finalize(dev).run()
+    torch.cuda.synchronize()
+    w, Q = torch.linalg.eigh(L1.double() + eps * torch.eye(n, device=dev, dtype=torch.float64))
+    P_ref = (Q * w.clamp(min=eps) ** -0.25) @ Q.t()
+    rel = (P.double() - P_ref).norm().item() / P_ref.norm().item()
+    assert rel < 2e-4, rel
+    assert int(w_it["nrounds"].item()) < int(c_it["nrounds"].item())
+
+
+@pytest.mark.parametrize("n,rank,use_perm", [(5, 5, False), (128, 128, True), (256, 256, True), (200, 60, True)])
+def test_householder_qr(dev, n, rank, use_perm):
+    from plaincv_amd.optim.precond import HouseholderQR
+    g = torch.Generator().manual_seed(n)
+    A = (torch.randn(n, rank, generator=g, dtype=torch.float64) @ torch.randn(rank, n, generator=g,
+                                                                              dtype=torch.float64)).float().to(dev)
+    perm = torch.randperm(n, generator=g).to(torch.int32).to(dev) if use_perm else None
+    Q = torch.zeros(n, n, device=dev)
+    qr = HouseholderQR(dev)
+    qr.add(A, Q, perm)
+    qr.finalize().run()
+    torch.cuda.synchronize()
+    Ap = (A[:, perm.long()] if use_perm else A).double()
+    Qd = Q.double()
+    I = torch.eye(n, device=dev, dtype=torch.float64)
+    assert (Qd.t() @ Qd - I).abs().max().item() < 5e-5
+    R = Qd.t() @ Ap
+    assert (torch.tril(R, -1)).abs().max().item() < 5e-5 * Ap.abs().max().item() * n ** 0.5
+    if rank == n:
+        Q_ref, _ = torch.linalg.qr(Ap)
+        assert (Qd - Q_ref).abs().max().item() < 1e-3
+
+
+# ----------------------------------------------------------------------------------- optimizers
+def _store(dev, shapes):
+    from plaincv_amd.params import Layout, ParamStore
+    lay = Layout()
+    for k, s in shapes.items():
+        lay.add(k, s)
+    st = ParamStore(lay, dev)
+    g = torch.Generator().manual_seed(0)
+    init = OrderedDict((k, torch.randn(s, generator=g) * 0.1) for k, s in shapes.items())
+    st.load(init)
+    return st, init
+
+
+def _run_pair(dev, shapes, gpu_tx, oracle_tx, steps, seed=1):
+    store, params = _store(dev, shapes)
+    gst = gpu_tx.init(store)
+    ost = oracle_tx.init(params)
+    g = torch.Generator().manual_seed(seed)
+    per_step = []
+    for _ in range(steps):
+        grads = OrderedDict((k, torch.randn(s, generator=g)) for k, s in shapes.items())
+        upd, gst = gpu_tx.update(OrderedDict((k, v.to(dev)) for k, v in grads.items()), gst, store)
+        upd = OrderedDict((k, v.clone().cpu()) for k, v in upd.items())
+        oupd, ost = oracle_tx.update(grads, ost, params)
+        for k in shapes:
+            store.params[k].add_(upd[k].to(dev))
+            params[k] = params[k] + oupd[k]
+        per_step.append((upd, oupd))
+    torch.cuda.synchronize()
+    return per_step
+
+
+def test_shampoo_matches_oracle(dev):
+    from oracle import optim as oopt
+    from plaincv_amd.optim.shampoo import Shampoo
+    shapes = OrderedDict([("Dense_0/kernel", (48, 96)), ("Dense_0/bias", (96,)), ("head/kernel", (96, 40)),
+                          ("sq/kernel", (64, 64))])
+    lr = 1e-2
+    steps = _run_pair(dev, shapes, Shampoo(lr, eps=1e-4, weight_decay=0.01),
+                      oopt.shampoo(lr, eps=1e-4, weight_decay=0.01), 6)
+    for i, (u, o) in enumerate(steps):
+        for k in shapes:
+            d = (u[k] - o[k]).abs().max().item()
+            assert d <= 2e-3 * max(o[k].abs().max().item(), lr), (i, k, d)
+
+
+def test_soap_matches_oracle(dev):
+    from oracle import optim as oopt
+    from plaincv_amd.optim.soap import Soap
+    shapes = OrderedDict([("a/kernel", (64, 64)), ("b/kernel", (96, 96)), ("a/bias", (64,)),
+                          ("embed/embedding", (10, 16))])
+    lr = 1e-2
+    steps = _run_pair(dev, shapes, Soap(lr, b1=0.9, b2=0.9, weight_decay=0.01, precondition_frequency=5),
+                      oopt.soap(lr, b1=0.9, b2=0.9, weight_decay=0.01, precondition_frequency=5), 12)
+    for k in ("a/kernel", "b/kernel"):
+        assert steps[0][0][k].abs().max().item() == 0.0
+    for i, (u, o) in enumerate(steps):
+        for k in shapes:
+            d = (u[k] - o[k]).abs().max().item()
+            assert d <= 5e-3 * max(o[k].abs().max().item(), lr), (i, k, d)
+
+
+def test_soap_rectangular_invariants(dev):
+    """Rank-deficient factors: after the first step QL/QR diagonalise L/R; after a refresh they
+    stay orthonormal and QL^T L QL has a descending-sorted diagonal up to the QR power step."""
+    from plaincv_amd.optim.soap import Soap
+    shapes = OrderedDict([("k/kernel", (32, 80))])
+    store, _ = _store(dev, shapes)
+    tx = Soap(1e-2, precondition_frequency=2)
+    st = tx.init(store)
+    g = torch.Generator().manual_seed(4)
+    for i in range(5):
+        store.grads["k/kernel"].copy_(torch.randn(32, 80, generator=g).to(dev))
+        tx.step_(store, st)
+        torch.cuda.synchronize()
+        s = st.mats[0]
+        for Q, M in ((s.QL, s.L), (s.QR, s.R)):
+            n = Q.shape[0]
+            assert (Q.t() @ Q - torch.eye(n, device=dev)).abs().max().item() < 1e-4
+            if i == 0:
+                D = Q.t() @ M @ Q
+                off = D - torch.diag(torch.diag(D))
+                assert off.abs().max().item() < 1e-4 * M.abs().max().item()
+                dg = torch.diag(D)
+                assert torch.all(dg[:-1] >= dg[1:] - 1e-5 * dg.abs().max())
+        assert torch.isfinite(store.params["k/kernel"]).all()
+
+
+@pytest.mark.parametrize("optim", ["soap", "shampoo"])
+def test_vit_train_step_preconditioned(dev, optim):
+    """ViT-small-shaped model (hidden 64) through the engine with SOAP/Shampoo: step 0 matches
+    the oracle for every leaf (SOAP: routed leaves untouched), later steps stay finite and
+    Shampoo (basis-invariant) tracks the oracle for 3 steps."""
+    from oracle import optim as oopt
+    from oracle.engine import apply_updates, cross_entropy_loss, value_and_grad
+    from oracle.vit import ViTConfig, vit_apply
+    from plaincv_amd.engine import create_train_state, make_train_step
+    from plaincv_amd.models.vit_small import VisionTransformer
+    from utils import Config
+    m = VisionTransformer(num_classes=10, patch_size=4, hidden_size=64, mlp_dim=128, num_layers=2, num_heads=2,
+                          dropout_rate=0.0)
+    shape = (4, 16, 16, 3)
+    cfg = Config(optim=optim, lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9)
+    init = m.init(3, shape)
+    st = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=init)
+    step = make_train_step()
+    tx = oopt.get_optimizer(cfg)
+    ostate = tx.init(init)
+    params = dict(init)
+    oc = ViTConfig(num_classes=10, patch_size=4, hidden_size=64, mlp_dim=128, num_layers=2, num_heads=2,
+                   dropout_rate=0.0)
+    gen = torch.Generator().manual_seed(5)
+    nsteps = 3 if optim == "shampoo" else 1
+    for it in range(nsteps):
+        images = torch.randint(0, 256, shape, generator=gen, dtype=torch.uint8)
+        labels = torch.randint(0, 10, (shape[0],), generator=gen, dtype=torch.int32)
+        st, met = step(st, (images.to(dev), labels.to(dev)), it)
+        _, grads = value_and_grad(
+            lambda p: (cross_entropy_loss(vit_apply(p, images, oc, True, it, bf16=True), labels), None), params)
+        upd, ostate = tx.update(grads, ostate, params)
+        params = apply_updates(params, upd)
+    torch.cuda.synchronize()
+    got = st.params.to_dict()
+    for k in params:
+        d = (got[k] - params[k]).abs().max().item()
+        assert d < 3e-3 * nsteps, (k, d)
+    for it in range(3):
+        images = torch.randint(0, 256, shape, generator=gen, dtype=torch.uint8)
+        labels = torch.randint(0, 10, (shape[0],), generator=gen, dtype=torch.int32)
+        st, met = step(st, (images.to(dev), labels.to(dev)), 10 + it)
+    torch.cuda.synchronize()
+    assert torch.isfinite(met["loss"]).item()
+    assert all(torch.isfinite(v).all() for v in st.params.params.values())
