@@ -1,6 +1,6 @@
 """Benchmark: plainCV training hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload vit_c2|lm124m] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload vit_c2|vit_c4_soap|vit_c4_shampoo|lm124m] [--no-cpu-baseline]
 
 Default workload (N=1): BASELINE.json configs[1] -- ViT-small on Tiny-ImageNet-
 shaped synthetic data (uint8 64x64x3, 200 classes, per-GPU batch 64, dropout 0.1,
@@ -41,6 +41,16 @@ VIT_C2 = dict(dataset="tiny_imagenet_synthetic", batch_size=64, image_size=64, n
               vit_dropout=0.1, vit_use_layernorm=True, optim="muon", lr=0.001, weight_decay=0.01, beta1=0.9,
               beta2=0.9, muon_beta=0.95, muon_ns_steps=5, muon_ns_coeffs=[3.4445, -4.7750, 2.0315],
               muon_nesterov=True, eigen_tracking_enabled=False, seed=0)
+
+
+# BASELINE.json configs[3]: the same ViT/TI-synthetic workload with SOAP or Shampoo
+# (exp/run_soap_vit_small/config.yaml: b1 .9, b2 .9, eps 1e-8, wd .01, precondition_frequency 10;
+# Shampoo factory.py:657-673 defaults: eps 1e-4, exponent .25, adam b1 .9 / b2 cfg, adam_eps 1e-8)
+VIT_C4 = {"soap": dict(VIT_C2, optim="soap", eps=1e-8, precondition_frequency=10),
+          "shampoo": dict(VIT_C2, optim="shampoo", eps=1e-4, shampoo_exponent=0.25, adam_eps=1e-8)}
+WORKLOAD_NAMES = {"vit_c2": "vit_small_tinyimagenet_muon (BASELINE configs[1])",
+                  "vit_c4_soap": "vit_small_tinyimagenet_soap (BASELINE configs[3] optimizer)",
+                  "vit_c4_shampoo": "vit_small_tinyimagenet_shampoo (BASELINE configs[3] optimizer)"}
 
 
 def vit_model(cfg):
@@ -155,13 +165,13 @@ def cpu_baseline_vit(cfg, seconds=12.0):
         pass
     return {"value": round(cfg.batch_size / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
             "steps_per_sec": round(1.0 / dt, 4),
-            "sample": f"{n} timed oracle ViT-small Muon train steps (fp32, B={cfg.batch_size}, 64x64x3, 200 classes) "
+            "sample": f"{n} timed oracle ViT-small {cfg.optim} train steps (fp32, B={cfg.batch_size}, 64x64x3, 200 classes) "
                       f"after 1 warmup; CPU {model_name}"}
 
 
 def bench_vit(args):
     rank, local_rank, world, dev = dp.init_from_env()
-    cfg = Config(VIT_C2)
+    cfg = Config(VIT_C2 if args.workload == "vit_c2" else VIT_C4[args.workload.split("_")[-1]])
     m = vit_model(cfg)
     B = cfg.batch_size
     shape = (B, cfg.image_size, cfg.image_size, cfg.num_channels)
@@ -199,9 +209,9 @@ def bench_vit(args):
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
                "data": "synthetic (uint8 images U[0,255], labels U[0,200), seeded, resident in HBM)",
-               "config": {"workload": "vit_small_tinyimagenet_muon (BASELINE configs[1])", "global_batch": world * B,
+               "config": {"workload": WORKLOAD_NAMES[args.workload], "global_batch": world * B,
                           "per_gpu_batch": B, "image": [64, 64, 3], "classes": 200, "tokens": 257,
-                          "optimizer": "muon", "parallelism": f"dp{world}"},
+                          "optimizer": cfg.optim, "parallelism": f"dp{world}"},
                "steps_per_sec": round(sps, 3), "tflops_per_gpu": round(flops * sps / 1e12, 3),
                "final_loss": round(loss, 4)}
         out["roofline"] = vit_roofline(state, shape)
@@ -287,7 +297,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="vit_c2", choices=["vit_c2", "lm124m"])
+    ap.add_argument("--workload", default="vit_c2", choices=["vit_c2", "vit_c4_soap", "vit_c4_shampoo", "lm124m"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--lm-micro-batch", type=int, default=16)

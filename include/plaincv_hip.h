@@ -208,18 +208,33 @@ int pcv_chunk_size(void);
  * Job records are plain 8-byte fields (pointers, int64, double), sizes from pcv_*_job_size().
  *
  * Grouped fp32 GEMM (v_mfma_f32_16x16x4_f32, exact fp32), one launch for all jobs:
- *   C = alpha * (*alpha_dev)^apow * op(A) diag(kscale) op(B) + beta * C + rscale * R; Cb = bf16(C)
- *   record {A, B, C, kscale, R, Cb, alpha_dev, M, N, K, lda, ldb, ldc, ldr, ldcb, ta, tb, apow,
- *           tiles_n, first_tile, alpha, beta, rscale} (64x64 tiles, first_tile = prefix sum). */
+ *   C = alpha * (*alpha_dev)^apow * op(A) diag(kscale) op(B) + beta * C + rscale * R; Cb = bf16(C),
+ *   op(A) = a_mul * A + a_diag * I (likewise B) -- the Newton iteration's T = aI + bM unmaterialised;
+ *   conv_in: the job is skipped when *conv_in <= conv_tol; conv_out: atomic max of |C - I|.
+ *   record {A, B, C, kscale, R, Cb, alpha_dev, conv_in, conv_out, M, N, K, lda, ldb, ldc, ldr, ldcb,
+ *           ta, tb, apow, tiles_n, first_tile, alpha, beta, rscale, a_diag, a_mul, b_diag, b_mul,
+ *           conv_tol} (64x64 tiles, first_tile = prefix sum; apow bit 4 marks a float4-aligned job).
+ * vec = 1: every job is float4-aligned (16-B bases, ld % 4, M, N, K % 4) -> vector staging. */
 int pcv_f32_job_size(void);
-int pcv_gemm_f32_grouped(const void* jobs, int njobs, int64_t total_tiles, void* stream);
+int pcv_gemm_f32_grouped(const void* jobs, int njobs, int64_t total_tiles, int vec, void* stream);
+/* Shampoo inverse p-th root (shampoo.py:195-215) by the coupled Newton iteration on the grouped
+ * GEMM above: pcv_newton_init (record {L, M0, X0, conv[iters], X1, P, ldl, n, shift}; M0 = zA,
+ * X0 = z^(1/p) I with A = L + shift I, z = (1+p)/(2||A||_F)), the per-iteration GEMM jobs, and
+ * pcv_newton_select (P = X of the first iteration whose max|M - I| <= tol; record field status =
+ * 0 converged / 1 not, read by the exact-eigh fallback jobs' skip field).  Record {L, M0, X0, conv,
+ * X1, P, status, ldl, n, shift}. */
+int pcv_newton_job_size(void);
+/* conv[iters + 1]: conv[0] = 1 if ||A||_F / shift <= kappa_max (else the chain is skipped and status = 1). */
+int pcv_newton_init(const void* jobs, int njobs, float p, int iters, float kappa_max, void* stream);
+int pcv_newton_select(const void* jobs, int njobs, int iters, float tol, int64_t max_n, void* stream);
 /* Symmetric eigendecomposition, n <= 256, one workgroup per matrix (cyclic Jacobi, packed upper
  * triangle in LDS, round-robin parallel rotations, rotation log for the vectors pass):
- *   record {A, w, wpow, perm, log, nrounds, lda, n, shift}: eigenvalues of A + shift*I into w
+ *   record {A, w, wpow, perm, log, nrounds, skip, lda, n, shift}: eigenvalues of A + shift*I into w
  *   (descending if sort_desc, else in Jacobi order), wpow = max(w, pow_floor)^(-pow_expo) (optional),
  *   perm = source column of each output; log holds pcv_eigh_log_floats(n, max_sweeps) floats.
  * pcv_eigh_vectors replays the log: Vout = V0 (identity if NULL) x rotations, columns in w's order;
- *   record {V0, Vout, perm, log, nrounds, ld0, ldo, n}; Vout may alias V0. */
+ *   record {V0, Vout, perm, log, nrounds, skip, ld0, ldo, n}; Vout may alias V0.  skip (optional
+ *   device float): the job is skipped when *skip <= 0.5. */
 int pcv_eigh_job_size(void);
 int pcv_vec_job_size(void);
 int64_t pcv_eigh_log_floats(int64_t n, int max_sweeps);

@@ -29,113 +29,259 @@ namespace pcv {
 
 // ------------------------------------------------------------------ fp32 grouped GEMM ----
 // C = alpha * adev^apow * op(A) diag(kscale) op(B) + beta * C + rscale * R;  Cb = bf16(C).
+// Affine operands (the Newton iteration's T = a I + b M without materialising T):
+//   op(A)[m][k] = a_mul * A[m][k] + a_diag * (m == k), op(B) likewise with b_mul / b_diag.
+// conv_in: skip the whole job when *conv_in <= conv_tol (matrix already converged);
+// conv_out: atomic max over the tile of |C - I| (the next iteration's conv_in).
 struct F32Job {
   const float* A; const float* B; float* C;
   const float* kscale; const float* R; bf16* Cb; const float* alpha_dev;
+  const float* conv_in; float* conv_out;
   int64_t M, N, K, lda, ldb, ldc, ldr, ldcb;
   int64_t ta, tb, apow, tiles_n, first_tile;
-  double alpha, beta, rscale;
+  double alpha, beta, rscale, a_diag, a_mul, b_diag, b_mul, conv_tol;
 };
-static_assert(sizeof(F32Job) == 23 * 8, "F32Job layout");
+static_assert(sizeof(F32Job) == 30 * 8, "F32Job layout");
 
-constexpr int FG_T = 64, FG_K = 16, FG_LD = FG_T + 16;   // +16: the 4 k-rows of a read hit 4 bank groups
+constexpr int FG_T = 64, FG_K = 128;
+constexpr int LD_KX = FG_T + 16;    // k-major image [k][x]: fragment reads of 4 k-rows hit 4 bank groups
+constexpr int LD_XK = FG_K + 4;     // k-contiguous image [x][k]: 16 rows x 4 k of a read hit 64 banks
+constexpr int FG_NPER = FG_T * FG_K / 256;   // elements per thread per operand per k-chunk (32)
 
-__global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __restrict__ jobs, int njobs) {
-  __shared__ float As[FG_K][FG_LD];
-  __shared__ float Bs[FG_K][FG_LD];
-  const int64_t bid = blockIdx.x;
-  int j = 0;
-  while (j + 1 < njobs && jobs[j + 1].first_tile <= bid) ++j;
-  const F32Job& jb = jobs[j];
-  const int64_t t = bid - jb.first_tile;
-  const int64_t m0 = (t / jb.tiles_n) * FG_T, n0 = (t % jb.tiles_n) * FG_T;
+// One operand's k-chunk staging.  ROWK: element (x, k) at base[x*ld + k] (A with ta=0, B with
+// tb=1), kept in LDS as [x][k]; otherwise element (x, k) at base[k*ld + x], kept as [k][x] -- so
+// every LDS store is row-contiguous (no transposed writes).  x is the tile's M (or N) index.
+// Offsets are int32 (the host checks every matrix has < 2^31 elements).
+template <bool ROWK, bool VEC>
+struct Stager {
+  static constexpr int NL = VEC ? FG_NPER / 4 : FG_NPER;   // loads per thread
+  int off0;                  // element offset of this thread's first load at k = 0
+  int xs, ks;                // first load's tile coordinates
+  int dx, dk;                // per-load step in tile coordinates
+  int ld;
+  __device__ void init(int tid, int x0, int ld_) {
+    ld = ld_;
+    if (VEC) {
+      if (ROWK) { xs = tid >> 5; ks = (tid & 31) * 4; dx = 8; dk = 0; }    // float4 along k
+      else { ks = tid >> 4; xs = (tid & 15) * 4; dk = 16; dx = 0; }         // float4 along x
+    } else {
+      if (ROWK) { xs = tid >> 7; ks = tid & 127; dx = 2; dk = 0; }
+      else { ks = tid >> 6; xs = tid & 63; dk = 4; dx = 0; }
+    }
+    off0 = ROWK ? (x0 + xs) * ld + ks : ks * ld + x0 + xs;
+  }
+  __device__ __forceinline__ float xform(float v, int gx, int gk, int X, int K, float mul, float diag,
+                                         const float* __restrict__ ksc) const {
+    if (gx >= X || gk >= K) return 0.f;
+    float y = mul * v;
+    if (gx == gk) y += diag;
+    if (ksc) y *= ksc[gk];
+    return y;
+  }
+  __device__ void load(const float* __restrict__ base, int k0, int x0, int X, int K, float mul, float diag,
+                       const float* __restrict__ ksc, float (&r)[FG_NPER]) const {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int x = xs + dx * i, k = ks + dk * i, gx = x0 + x, gk = k0 + k;
+      const int o = off0 + (ROWK ? dx * i * ld + k0 : (dk * i + k0) * ld);
+      if (VEC) {
+        // VEC jobs: K % 4 == 0 and X % 4 == 0, so each float4 is all in range or all out
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gx < X && gk < K) v = *(const float4*)(base + o);
+        const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          r[4 * i + q] = xform(e[q], gx + (ROWK ? 0 : q), gk + (ROWK ? q : 0), X, K, mul, diag, ksc);
+      } else {
+        r[i] = (gx < X && gk < K) ? xform(base[o], gx, gk, X, K, mul, diag, ksc) : 0.f;
+      }
+    }
+  }
+  __device__ void store(float* S, const float (&r)[FG_NPER]) const {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int x = xs + dx * i, k = ks + dk * i;
+      if (VEC) {
+        float* d = ROWK ? S + x * LD_XK + k : S + k * LD_KX + x;
+        *(float4*)d = make_float4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+      } else {
+        S[ROWK ? x * LD_XK + k : k * LD_KX + x] = r[i];
+      }
+    }
+  }
+  // MFMA 16x16x4 operand: element (x, k) of the staged chunk
+  __device__ __forceinline__ float frag(const float* S, int x, int k) const {
+    return ROWK ? S[x * LD_XK + k] : S[k * LD_KX + x];
+  }
+};
+
+constexpr int FG_LDS_FLOATS = (FG_T * LD_XK > FG_K * LD_KX ? FG_T * LD_XK : FG_K * LD_KX);
+
+template <bool TA, bool TB, bool VEC>
+__device__ __forceinline__ void f32_tile(const F32Job& jb, int m0, int n0, float* As, float* Bs,
+                                         f32x4 (&acc)[2][2]) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
-  const int64_t M = jb.M, N = jb.N, K = jb.K;
+  const int M = (int)jb.M, N = (int)jb.N, K = (int)jb.K;
+  Stager<!TA, VEC> sa;     // A row-major [M][K] when !TA
+  Stager<TB, VEC> sb;      // B stored [N][K] when TB (row-major along k)
+  sa.init(tid, m0, (int)jb.lda);
+  sb.init(tid, n0, (int)jb.ldb);
+  const float amul = (float)jb.a_mul, adiag = (float)jb.a_diag, bmul = (float)jb.b_mul, bdiag = (float)jb.b_diag;
   const float* __restrict__ A = jb.A;
   const float* __restrict__ B = jb.B;
-  const float* __restrict__ ks = jb.kscale;
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int64_t k0 = 0; k0 < K; k0 += FG_K) {
-    float ra[4], rb[4];
-    int am[4], ak[4], bn[4], bk[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (jb.ta) { am[i] = tid & 63; ak[i] = (tid >> 6) + 4 * i; }      // A stored [K][M]
-      else { ak[i] = tid & 15; am[i] = (tid >> 4) + 16 * i; }            // A stored [M][K]
-      const int64_t gm = m0 + am[i], gk = k0 + ak[i];
-      float x = 0.f;
-      if (gm < M && gk < K) {
-        x = jb.ta ? A[gk * jb.lda + gm] : A[gm * jb.lda + gk];
-        if (ks) x *= ks[gk];
-      }
-      ra[i] = x;
-      if (jb.tb) { bk[i] = tid & 15; bn[i] = (tid >> 4) + 16 * i; }      // B stored [N][K]
-      else { bn[i] = tid & 63; bk[i] = (tid >> 6) + 4 * i; }             // B stored [K][N]
-      const int64_t gn = n0 + bn[i], gk2 = k0 + bk[i];
-      float y = 0.f;
-      if (gn < N && gk2 < K) y = jb.tb ? B[gn * jb.ldb + gk2] : B[gk2 * jb.ldb + gn];
-      rb[i] = y;
-    }
+  const float* __restrict__ ksc = jb.kscale;
+  float ra[FG_NPER], rb[FG_NPER];
+  sa.load(A, 0, m0, M, K, amul, adiag, ksc, ra);
+  sb.load(B, 0, n0, N, K, bmul, bdiag, nullptr, rb);
+  for (int k0 = 0; k0 < K; k0 += FG_K) {
+    sa.store(As, ra);
+    sb.store(Bs, rb);
     __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      As[ak[i]][am[i]] = ra[i];
-      Bs[bk[i]][bn[i]] = rb[i];
+    if (k0 + FG_K < K) {     // next chunk's loads in flight under this chunk's MFMAs
+      sa.load(A, k0 + FG_K, m0, M, K, amul, adiag, ksc, ra);
+      sb.load(B, k0 + FG_K, n0, N, K, bmul, bdiag, nullptr, rb);
     }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < FG_K; kk += 4) {
+    const int kend = K - k0 < FG_K ? ((K - k0 + 3) & ~3) : FG_K;
+#pragma unroll 8
+    for (int kk = 0; kk < kend; kk += 4) {
       const int kr = kk + (lane >> 4);
       float fa[2], fb[2];
 #pragma unroll
-      for (int a = 0; a < 2; ++a) fa[a] = As[kr][wm * 32 + a * 16 + (lane & 15)];
+      for (int a = 0; a < 2; ++a) fa[a] = sa.frag(As, wm * 32 + a * 16 + (lane & 15), kr);
 #pragma unroll
-      for (int b = 0; b < 2; ++b) fb[b] = Bs[kr][wn * 32 + b * 16 + (lane & 15)];
+      for (int b = 0; b < 2; ++b) fb[b] = sb.frag(Bs, wn * 32 + b * 16 + (lane & 15), kr);
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a], fb[b], acc[a][b], 0, 0, 0);
     }
+    __syncthreads();
   }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __restrict__ jobs, int njobs) {
+  __shared__ __attribute__((aligned(16))) float As[FG_LDS_FLOATS];
+  __shared__ __attribute__((aligned(16))) float Bs[FG_LDS_FLOATS];
+  const int bid = blockIdx.x;
+  int j = 0;
+  while (j + 1 < njobs && jobs[j + 1].first_tile <= bid) ++j;
+  const F32Job jb = jobs[j];
+  if (jb.conv_in && *jb.conv_in <= (float)jb.conv_tol) return;
+  const int t = bid - (int)jb.first_tile;
+  const int m0 = (t / (int)jb.tiles_n) * FG_T, n0 = (t % (int)jb.tiles_n) * FG_T;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // (every job of a VEC launch is float4-aligned: the host splits aligned and unaligned jobs)
+  switch ((int)jb.ta * 2 + (int)jb.tb) {
+    case 0: f32_tile<false, false, VEC>(jb, m0, n0, As, Bs, acc); break;
+    case 1: f32_tile<false, true, VEC>(jb, m0, n0, As, Bs, acc); break;
+    case 2: f32_tile<true, false, VEC>(jb, m0, n0, As, Bs, acc); break;
+    default: f32_tile<true, true, VEC>(jb, m0, n0, As, Bs, acc); break;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+  const int M = (int)jb.M, N = (int)jb.N;
   float alpha = (float)jb.alpha;
   if (jb.alpha_dev) {
     const float s = *jb.alpha_dev;
-    alpha *= jb.apow == 2 ? s * s : s;
+    alpha *= (jb.apow & 15) == 2 ? s * s : s;
   }
   const float beta = (float)jb.beta, rscale = (float)jb.rscale;
+  float dev_max = 0.f;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * 32 + a * 16 + (lane >> 4) * 4 + r;
-        const int64_t col = n0 + wn * 32 + b * 16 + (lane & 15);
+        const int row = m0 + wm * 32 + a * 16 + (lane >> 4) * 4 + r;
+        const int col = n0 + wn * 32 + b * 16 + (lane & 15);
         if (row < M && col < N) {
           float v = alpha * acc[a][b][r];
-          float* c = jb.C + row * jb.ldc + col;
+          float* c = jb.C + (int64_t)row * jb.ldc + col;
           if (beta != 0.f) v += beta * *c;
-          if (jb.R) v += rscale * jb.R[row * jb.ldr + col];
+          if (jb.R) v += rscale * jb.R[(int64_t)row * jb.ldr + col];
           *c = v;
-          if (jb.Cb) jb.Cb[row * jb.ldcb + col] = f2bf(v);
+          if (jb.Cb) jb.Cb[(int64_t)row * jb.ldcb + col] = f2bf(v);
+          const float d = fabsf(v - (row == col ? 1.f : 0.f));
+          dev_max = (d == d) ? fmaxf(dev_max, d) : __builtin_inff();   // NaN -> never converged
         }
       }
+  if (jb.conv_out) {
+    dev_max = wave_max(dev_max);
+    if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)jb.conv_out, __float_as_uint(dev_max));
+  }
+}
+
+// Coupled Newton iteration for A^(-1/p) (A = L + shift I, symmetric positive definite), setup:
+//   z = (1 + p) / (2 ||A||_F);  M0 = z A;  X0 = z^(1/p) I;  conv[1..iters] = 0.
+// Then per iteration i (grouped GEMMs above, skipped while conv[i] <= tol):
+//   T = ((p+1) I - M)/p;  X <- X T;  M <- T^p M;  conv[i+1] = max|M - I|.
+// M -> I and X -> A^(-1/p) (Guo & Higham 2006; the Shampoo inverse root of shampoo.py:195-215).
+// conv[0] gates the whole chain: 1 (run) when ||A||_F / shift <= kappa_max, else 0 -- past that
+// bound fp32 rounding can leave A indefinite, where only the eigh path with the reference's clamp
+// max(lambda, eps) is meaningful (the caller's fallback jobs run when status = 1).
+struct NewtonJob {
+  const float* L; float* M0; float* X0; float* conv; float* X1; float* P; float* status;
+  int64_t ldl, n;
+  double shift;
+};
+static_assert(sizeof(NewtonJob) == 10 * 8, "NewtonJob layout");
+
+__global__ __launch_bounds__(1024) void newton_init_kernel(const NewtonJob* __restrict__ jobs, float p, int iters,
+                                                           float kappa_max) {
+  __shared__ float red[16];
+  const NewtonJob jb = jobs[blockIdx.x];
+  const int n = (int)jb.n;
+  const float sh = (float)jb.shift;
+  float s = 0.f;
+  for (int e = threadIdx.x; e < n * n; e += 1024) {
+    const int r = e / n, c = e - r * n;
+    const float x = jb.L[(int64_t)r * jb.ldl + c] + (r == c ? sh : 0.f);
+    s += x * x;
+  }
+  s = block_sum(s, red);
+  const float fro = sqrtf(s);
+  const float z = (1.f + p) / (2.f * fro);
+  const float xz = powf(z, 1.f / p);
+  for (int e = threadIdx.x; e < n * n; e += 1024) {
+    const int r = e / n, c = e - r * n;
+    jb.M0[e] = z * (jb.L[(int64_t)r * jb.ldl + c] + (r == c ? sh : 0.f));
+    jb.X0[e] = r == c ? xz : 0.f;
+  }
+  for (int i = threadIdx.x; i <= iters; i += 1024)
+    jb.conv[i] = i > 0 ? 0.f : ((fro <= kappa_max * sh && fro == fro) ? 1.f : 0.f);
+}
+
+// P = the X of the first converged iteration (X buffers ping-pong: iteration i writes X[(i+1)&1]);
+// status = 0 if the chain ran and some iteration reached tol, else 1 (not attempted, not converged
+// or NaN: the caller's exact eigh fallback jobs run for exactly these matrices).
+__global__ __launch_bounds__(256) void newton_select_kernel(const NewtonJob* __restrict__ jobs, int iters,
+                                                            float tol) {
+  const NewtonJob jb = jobs[blockIdx.y];
+  int done = -1;
+  if (jb.conv[0] > tol)
+    for (int i = 1; i <= iters; ++i)
+      if (jb.conv[i] <= tol) { done = i; break; }
+  if (jb.status && blockIdx.x == 0 && threadIdx.x == 0) *jb.status = done < 0 ? 1.f : 0.f;
+  if (done < 0) return;
+  const float* X = (done & 1) ? jb.X1 : jb.X0;
+  const int64_t nn = jb.n * jb.n;
+  for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < nn; e += (int64_t)gridDim.x * 256) jb.P[e] = X[e];
 }
 
 // ------------------------------------------------------------------ Jacobi eigh ----
 // Packed upper triangle of the padded (np = n rounded up to 4) symmetric matrix in LDS.
 struct EighJob {
-  const float* A; float* w; float* wpow; int* perm; float2* log; int* nrounds;
+  const float* A; float* w; float* wpow; int* perm; float2* log; int* nrounds; const float* skip;
   int64_t lda, n;
   double shift;
 };
-static_assert(sizeof(EighJob) == 9 * 8, "EighJob layout");
+static_assert(sizeof(EighJob) == 10 * 8, "EighJob layout");
 
 constexpr int EJ_MAXN = 256, EJ_THREADS = 1024;
 
@@ -159,6 +305,7 @@ __global__ __launch_bounds__(EJ_THREADS) void eigh_jacobi_kernel(const EighJob* 
                                                                   float pow_floor, float pow_expo) {
   extern __shared__ __attribute__((aligned(16))) float tri[];
   const EighJob jb = jobs[blockIdx.x];
+  if (jb.skip && *jb.skip <= 0.5f) return;   // e.g. the Newton root of this matrix converged
   const int n = (int)jb.n, np = (n + 3) & ~3, P = np >> 1, m = np - 1;
   const int ntri = np * (np + 1) / 2;
   float* cs_c = tri + ntri;          // [P]
@@ -274,16 +421,17 @@ __global__ __launch_bounds__(EJ_THREADS) void eigh_jacobi_kernel(const EighJob* 
 // basis; output columns in the eigh_jacobi_kernel's sorted order.  In place (Vout == V0) is fine:
 // a workgroup reads all of its rows before it writes them.
 struct VecJob {
-  const float* V0; float* Vout; const int* perm; const float2* log; const int* nrounds;
+  const float* V0; float* Vout; const int* perm; const float2* log; const int* nrounds; const float* skip;
   int64_t ld0, ldo, n;
 };
-static_assert(sizeof(VecJob) == 8 * 8, "VecJob layout");
+static_assert(sizeof(VecJob) == 9 * 8, "VecJob layout");
 
 constexpr int EV_ROWS = 32, EV_LD = EJ_MAXN + 4;
 
 __global__ __launch_bounds__(256) void eigh_vectors_kernel(const VecJob* __restrict__ jobs) {
   __shared__ float Vs[EV_ROWS][EV_LD];
   const VecJob jb = jobs[blockIdx.y];
+  if (jb.skip && *jb.skip <= 0.5f) return;
   const int n = (int)jb.n, np = (n + 3) & ~3, P = np >> 1, m = np - 1;
   const int row0 = blockIdx.x * EV_ROWS;
   if (row0 >= n) return;
@@ -477,16 +625,38 @@ __global__ __launch_bounds__(256) void permute_rc_kernel(const PermJob* __restri
 using namespace pcv;
 
 extern "C" int pcv_f32_job_size(void) { return (int)sizeof(F32Job); }
+extern "C" int pcv_newton_job_size(void) { return (int)sizeof(NewtonJob); }
+
+extern "C" int pcv_newton_init(const void* jobs_dev, int njobs, float p, int iters, float kappa_max,
+                               void* stream) {
+  if (!jobs_dev || njobs <= 0 || p <= 0.f || iters <= 0) return PCV_EINVAL;
+  hipLaunchKernelGGL(newton_init_kernel, dim3(njobs), dim3(1024), 0, (hipStream_t)stream,
+                     (const NewtonJob*)jobs_dev, p, iters, kappa_max);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_newton_select(const void* jobs_dev, int njobs, int iters, float tol, int64_t max_n,
+                                 void* stream) {
+  if (!jobs_dev || njobs <= 0 || iters <= 0 || max_n <= 0) return PCV_EINVAL;
+  const int64_t blocks = (max_n * max_n + 255) / 256;
+  hipLaunchKernelGGL(newton_select_kernel, dim3((unsigned)(blocks < 64 ? blocks : 64), njobs), dim3(256), 0,
+                     (hipStream_t)stream, (const NewtonJob*)jobs_dev, iters, tol);
+  return pcv_launch_status();
+}
 extern "C" int pcv_eigh_job_size(void) { return (int)sizeof(EighJob); }
 extern "C" int pcv_vec_job_size(void) { return (int)sizeof(VecJob); }
 extern "C" int pcv_qr_job_size(void) { return (int)sizeof(QrJob); }
 extern "C" int pcv_sort_job_size(void) { return (int)sizeof(SortJob); }
 extern "C" int pcv_perm_job_size(void) { return (int)sizeof(PermJob); }
 
-extern "C" int pcv_gemm_f32_grouped(const void* jobs_dev, int njobs, int64_t total_tiles, void* stream) {
-  if (!jobs_dev || njobs <= 0 || total_tiles <= 0) return PCV_EINVAL;
-  hipLaunchKernelGGL(gemm_f32_grouped_kernel, dim3((unsigned)total_tiles), dim3(256), 0, (hipStream_t)stream,
-                     (const F32Job*)jobs_dev, njobs);
+extern "C" int pcv_gemm_f32_grouped(const void* jobs_dev, int njobs, int64_t total_tiles, int vec, void* stream) {
+  if (!jobs_dev || njobs <= 0 || total_tiles <= 0 || total_tiles >= (1ll << 31)) return PCV_EINVAL;
+  if (vec)
+    hipLaunchKernelGGL(gemm_f32_grouped_kernel<true>, dim3((unsigned)total_tiles), dim3(256), 0, (hipStream_t)stream,
+                       (const F32Job*)jobs_dev, njobs);
+  else
+    hipLaunchKernelGGL(gemm_f32_grouped_kernel<false>, dim3((unsigned)total_tiles), dim3(256), 0,
+                       (hipStream_t)stream, (const F32Job*)jobs_dev, njobs);
   return pcv_launch_status();
 }
 

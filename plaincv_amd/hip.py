@@ -67,12 +67,15 @@ SIGNATURES = {
     "pcv_muon_mat_size": [],
     "pcv_chunk_size": [],
     "pcv_f32_job_size": [],
+    "pcv_newton_job_size": [],
+    "pcv_newton_init": [P, I32, F32, I32, F32, P],
+    "pcv_newton_select": [P, I32, I32, F32, I64, P],
     "pcv_eigh_job_size": [],
     "pcv_vec_job_size": [],
     "pcv_qr_job_size": [],
     "pcv_sort_job_size": [],
     "pcv_perm_job_size": [],
-    "pcv_gemm_f32_grouped": [P, I32, I64, P],
+    "pcv_gemm_f32_grouped": [P, I32, I64, I32, P],
     "pcv_eigh_log_floats": [I64, I32],
     "pcv_eigh_jacobi": [P, I32, I32, I32, F32, F32, I32, F32, F32, P],
     "pcv_eigh_vectors": [P, I32, I32, P],

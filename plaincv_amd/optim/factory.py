@@ -7,7 +7,8 @@ keeps the reference's signature, config keys and defaults:
 * muon           factory.py:441-484  (muon_beta .95, muon_ns_steps 5, ns coeffs
                  (3.4445,-4.7750,2.0315), muon_nesterov True, adam_eps_root 0)
 * soap           factory.py:632-652  (beta1/beta2 .95, eps 1e-8, wd .01, precondition_frequency 10)
-* shampoo        factory.py:657-673  (eps 1e-4, shampoo_exponent .25, adam_eps 1e-8)
+* shampoo        factory.py:657-673  (eps 1e-4, shampoo_exponent .25, adam_eps 1e-8; build-only key
+                 shampoo_root: "newton" (default) | "eigh", the inverse-root method)
 
 Any other name raises ``ValueError(f"Unknown optimizer name: {cfg.optim}")``
 (factory.py:797-798); the research optimizers of the reference (PN-S, Sophia,
@@ -45,5 +46,6 @@ def get_optimizer(cfg, model_def=None, curvature_batch=None, batch_stats=None):
     if name == "shampoo":
         return Shampoo(lr, eps=_g(cfg, "eps", 1e-4), exponent=_g(cfg, "shampoo_exponent", 0.25),
                        weight_decay=_g(cfg, "weight_decay", 0.0), adam_b1=_g(cfg, "beta1", 0.9),
-                       adam_b2=_g(cfg, "beta2", 0.999), adam_eps=_g(cfg, "adam_eps", 1e-8))
+                       adam_b2=_g(cfg, "beta2", 0.999), adam_eps=_g(cfg, "adam_eps", 1e-8),
+                       root_method=str(_g(cfg, "shampoo_root", "newton")))
     raise ValueError(f"Unknown optimizer name: {_g(cfg, 'optim', name)}")

@@ -36,14 +36,17 @@ class GemmF32:
     """One grouped launch of C = alpha*adev^apow * op(A) diag(kscale) op(B) + beta*C + rscale*R
     (+ bf16 copy Cb).  ``add(...)`` jobs, then ``finalize(device)``; ``run()`` per step."""
 
-    FMT = "<7Q13q3d"
+    FMT = "<9Q13q8d"
 
     def __init__(self):
         self.jobs = []
         self.dev = None
 
     def add(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, kscale=None, r=None, rscale=0.0, cb=None,
-            alpha_dev=None, apow=1):
+            alpha_dev=None, apow=1, a_affine=(1.0, 0.0), b_affine=(1.0, 0.0), conv_in=None, conv_out=None,
+            conv_tol=0.0):
+        """a_affine = (mul, diag): op(A) -> mul * op(A) + diag * I (b_affine likewise);
+        conv_in: skip this job when *conv_in <= conv_tol; conv_out: atomic max of |C - I|."""
         M, K = (a.shape[1], a.shape[0]) if ta else (a.shape[0], a.shape[1])
         K2, N = (b.shape[1], b.shape[0]) if tb else (b.shape[0], b.shape[1])
         if K != K2 or tuple(c.shape) != (M, N):
@@ -55,30 +58,114 @@ class GemmF32:
         if cb is not None and (tuple(cb.shape) != (M, N) or cb.dtype != torch.bfloat16 or cb.stride(1) != 1):
             raise ValueError("bf16 copy shape")
         tiles_n = (N + TILE - 1) // TILE
+        for t in (a, b, c, r):
+            if t is not None and t.shape[0] * t.stride(0) >= 2 ** 31:
+                raise ValueError("gemm_f32 operands must have < 2^31 elements (int32 offsets)")
+        # float4 staging: 16-B aligned bases, row strides % 4, K and the operand x-extents % 4
+        vec = (K % 4 == 0 and M % 4 == 0 and N % 4 == 0 and all(
+            t.data_ptr() % 16 == 0 and t.stride(0) % 4 == 0 for t in (a, b)))
         self.jobs.append(dict(A=a, B=b, C=c, ks=kscale, R=r, Cb=cb, ad=alpha_dev, M=M, N=N, K=K, lda=_ld(a),
                               ldb=_ld(b), ldc=_ld(c), ldr=_ld(r) if r is not None else 0,
-                              ldcb=cb.stride(0) if cb is not None else 0, ta=int(ta), tb=int(tb), apow=int(apow),
+                              ldcb=cb.stride(0) if cb is not None else 0, ta=int(ta), tb=int(tb), apow=int(apow) | (16 if vec else 0),
                               tiles=((M + TILE - 1) // TILE) * tiles_n, tiles_n=tiles_n, alpha=float(alpha),
-                              beta=float(beta), rscale=float(rscale)))
+                              beta=float(beta), rscale=float(rscale), aff=(float(a_affine[1]), float(a_affine[0]),
+                                                                           float(b_affine[1]), float(b_affine[0])),
+                              ci=conv_in, co=conv_out, tol=float(conv_tol)))
         return self
 
     def finalize(self, device):
+        """Two device tables: float4-aligned jobs (vector staging kernel) and the rest."""
         lib = hip.load()
         assert lib.pcv_f32_job_size() == struct.calcsize(self.FMT)
-        recs, first = [], 0
-        for j in self.jobs:
-            recs.append((_addr(j["A"]), _addr(j["B"]), _addr(j["C"]), _addr(j["ks"]), _addr(j["R"]),
-                         _addr(j["Cb"]), _addr(j["ad"]), j["M"], j["N"], j["K"], j["lda"], j["ldb"], j["ldc"],
-                         j["ldr"], j["ldcb"], j["ta"], j["tb"], j["apow"], j["tiles_n"], first, j["alpha"],
-                         j["beta"], j["rscale"]))
-            first += j["tiles"]
-        self.total = first
-        self.dev = _pack(recs, self.FMT).to(device) if recs else None
+        self.groups = []
+        for vec in (True, False):
+            recs, first = [], 0
+            for j in self.jobs:
+                if bool(j["apow"] & 16) != vec:
+                    continue
+                recs.append((_addr(j["A"]), _addr(j["B"]), _addr(j["C"]), _addr(j["ks"]), _addr(j["R"]),
+                             _addr(j["Cb"]), _addr(j["ad"]), _addr(j["ci"]), _addr(j["co"]), j["M"], j["N"], j["K"],
+                             j["lda"], j["ldb"], j["ldc"], j["ldr"], j["ldcb"], j["ta"], j["tb"], j["apow"],
+                             j["tiles_n"], first, j["alpha"], j["beta"], j["rscale"]) + j["aff"] + (j["tol"],))
+                first += j["tiles"]
+            if recs:
+                self.groups.append((_pack(recs, self.FMT).to(device), len(recs), first, int(vec)))
         return self
 
     def run(self):
-        if self.dev is not None and self.total > 0:
-            hip.call("pcv_gemm_f32_grouped", ptr(self.dev), len(self.jobs), self.total, stream_ptr())
+        s = stream_ptr()
+        for dev, n, total, vec in self.groups:
+            hip.call("pcv_gemm_f32_grouped", ptr(dev), n, total, vec, s)
+
+
+class NewtonRoot:
+    """P = (L + shift I)^(-1/p) for a batch of symmetric positive definite matrices by the coupled
+    Newton iteration (csrc/precond.hip), p in {1, 2, 4}: one init launch, then per iteration
+    T = ((p+1) I - M)/p (folded into the GEMM operand loads), X <- X T, M <- T^p M as grouped fp32
+    MFMA GEMMs; a matrix whose max|M - I| fell to ``tol`` skips its remaining iterations; one
+    select launch copies each matrix's converged X into P."""
+
+    FMT = "<7Q2qd"
+
+    def __init__(self, device, p=4, iters=30, tol=4e-6, kappa_max=2e7):
+        """kappa_max bounds ||L + shift I||_F / shift: past it fp32 Newton is no longer as accurate as
+        fp32 eigh (measured), so the matrix is left to the eigh fallback (status 1)."""
+        if p not in (1, 2, 4):
+            raise NotImplementedError("coupled Newton inverse root implemented for p in {1, 2, 4}")
+        self.device, self.p, self.iters, self.tol = torch.device(device), int(p), int(iters), float(tol)
+        self.kappa_max = float(kappa_max)
+        self.items = []
+
+    def add(self, L, P, shift):
+        n = L.shape[0]
+        if L.shape != (n, n) or P.shape != (n, n) or not P.is_contiguous():
+            raise ValueError("newton root: square L and contiguous square P")
+        _ld(L)
+        z = lambda: torch.zeros(n, n, dtype=torch.float32, device=self.device)  # noqa: E731
+        it = dict(L=L, P=P, shift=float(shift), n=n, M=[z(), z()], X=[z(), z()], T2=z(), Y=z(),
+                  conv=torch.zeros(self.iters + 1, dtype=torch.float32, device=self.device),
+                  status=torch.zeros(1, dtype=torch.float32, device=self.device))
+        self.items.append(it)
+        return it
+
+    def finalize(self):
+        lib = hip.load()
+        assert lib.pcv_newton_job_size() == struct.calcsize(self.FMT)
+        recs = [(_addr(it["L"]), _addr(it["M"][0]), _addr(it["X"][0]), _addr(it["conv"]), _addr(it["X"][1]),
+                 _addr(it["P"]), _addr(it["status"]), it["L"].stride(0), it["n"], it["shift"]) for it in self.items]
+        self.max_n = max([it["n"] for it in self.items], default=0)
+        self.dev = _pack(recs, self.FMT).to(self.device) if recs else None
+        p = float(self.p)
+        T = ((-1.0 / p), (p + 1.0) / p)     # T = -M/p + (p+1)/p I
+        self.launches = []
+        for i in range(self.iters):
+            cur, nxt = i & 1, (i + 1) & 1
+            l1, l2, l3 = GemmF32(), GemmF32(), GemmF32()
+            for it in self.items:
+                cin, cout = it["conv"][i:i + 1], it["conv"][i + 1:i + 2]
+                M, X = it["M"], it["X"]
+                kw = dict(conv_in=cin, conv_tol=self.tol)
+                l1.add(X[cur], M[cur], X[nxt], b_affine=T, **kw)                              # X' = X T
+                if self.p == 1:
+                    l1.add(M[cur], M[cur], M[nxt], a_affine=T, conv_out=cout, **kw)           # M' = T M
+                elif self.p == 2:
+                    l1.add(M[cur], M[cur], it["T2"], a_affine=T, b_affine=T, **kw)           # T^2
+                    l2.add(it["T2"], M[cur], M[nxt], conv_out=cout, **kw)                    # M' = T^2 M
+                else:
+                    l1.add(M[cur], M[cur], it["T2"], a_affine=T, b_affine=T, **kw)           # T^2
+                    l2.add(it["T2"], M[cur], it["Y"], **kw)                                   # Y = T^2 M
+                    l3.add(it["T2"], it["Y"], M[nxt], conv_out=cout, **kw)                   # M' = T^2 Y
+            self.launches += [g.finalize(self.device) for g in (l1, l2, l3) if g.jobs]
+        return self
+
+    def run(self):
+        if not self.items:
+            return
+        s = stream_ptr()
+        hip.call("pcv_newton_init", ptr(self.dev), len(self.items), float(self.p), self.iters, self.kappa_max, s)
+        for g in self.launches:
+            g.run()
+        hip.call("pcv_newton_select", ptr(self.dev), len(self.items), self.iters, self.tol, self.max_n, s)
 
 
 class Eigh:
@@ -86,8 +173,8 @@ class Eigh:
     matrices: eigenvalues w (descending if sort_desc), optional wpow = max(w, floor)^(-expo),
     eigenvectors written to vout (starting from basis v0 when given: vout = v0 @ eigvecs(A))."""
 
-    FMT_E = "<6Q2qd"
-    FMT_V = "<5Q3q"
+    FMT_E = "<7Q2qd"
+    FMT_V = "<6Q3q"
 
     def __init__(self, device, max_sweeps=15, tol_rel=2e-7, tol_abs_rel=1e-9, sort_desc=True, pow_floor=0.0,
                  pow_expo=0.0):
@@ -96,7 +183,8 @@ class Eigh:
         self.sort_desc, self.pow_floor, self.pow_expo = int(bool(sort_desc)), float(pow_floor), float(pow_expo)
         self.items = []
 
-    def add(self, a, vout, v0=None, shift=0.0, want_pow=False):
+    def add(self, a, vout, v0=None, shift=0.0, want_pow=False, skip=None):
+        """skip: device float; the job (eigenvalues and vectors) is skipped when *skip <= 0.5."""
         n = a.shape[0]
         if a.shape != (n, n) or vout.shape != (n, n) or (v0 is not None and v0.shape != (n, n)):
             raise ValueError("eigh: square matrices of one size per job")
@@ -104,7 +192,7 @@ class Eigh:
             raise NotImplementedError(f"eigh kernel handles 2 <= n <= {EIGH_MAX_N} (got {n})")
         _ld(a), _ld(vout)
         lib = hip.load()
-        it = dict(a=a, vout=vout, v0=v0, shift=float(shift), n=n,
+        it = dict(a=a, vout=vout, v0=v0, shift=float(shift), n=n, skip=skip,
                   w=torch.zeros(n, dtype=torch.float32, device=self.device),
                   wpow=torch.zeros(n, dtype=torch.float32, device=self.device) if want_pow else None,
                   perm=torch.zeros(n, dtype=torch.int32, device=self.device),
@@ -121,9 +209,10 @@ class Eigh:
         e, v = [], []
         for it in self.items:
             e.append((_addr(it["a"]), _addr(it["w"]), _addr(it["wpow"]), _addr(it["perm"]), _addr(it["log"]),
-                      _addr(it["nrounds"]), it["a"].stride(0), it["n"], it["shift"]))
+                      _addr(it["nrounds"]), _addr(it["skip"]), it["a"].stride(0), it["n"], it["shift"]))
             v.append((_addr(it["v0"]), _addr(it["vout"]), _addr(it["perm"]), _addr(it["log"]), _addr(it["nrounds"]),
-                      it["v0"].stride(0) if it["v0"] is not None else 0, it["vout"].stride(0), it["n"]))
+                      _addr(it["skip"]), it["v0"].stride(0) if it["v0"] is not None else 0, it["vout"].stride(0),
+                      it["n"]))
         self.max_n = max([it["n"] for it in self.items], default=0)
         self.e_dev = _pack(e, self.FMT_E).to(self.device) if e else None
         self.v_dev = _pack(v, self.FMT_V).to(self.device) if v else None

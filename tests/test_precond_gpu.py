@@ -181,13 +181,47 @@ def _run_pair(dev, shapes, gpu_tx, oracle_tx, steps, seed=1):
     return per_step
 
 
-def test_shampoo_matches_oracle(dev):
+@pytest.mark.parametrize("n,rank,scale", [(64, 64, 1.0), (256, 128, 1.0), (200, 3, 10.0), (128, 1, 100.0)])
+def test_shampoo_inverse_root(dev, n, rank, scale):
+    """Shampoo's P = (L + eps I)^(-1/4) (clamped eigenvalues) from the Newton chain with its exact
+    Jacobi fallback vs fp64 eigh of the same fp32 L.  Bar: within 2x the error of the reference's
+    own fp32 algorithm (torch fp32 eigh + clamp on this device) + 1e-5.  The last two cases have
+    kappa ~ 1e7-1e8, where fp32 rounding makes L + eps I indefinite: Newton cannot converge there
+    and the fallback must take over (status 1)."""
+    from plaincv_amd.optim.shampoo import Shampoo
+    from collections import OrderedDict as OD
+    eps = 1e-4
+    g = torch.Generator().manual_seed(n + rank)
+    x = torch.randn(n, rank, generator=g, dtype=torch.float64) * (scale / rank ** 0.5)
+    L = (x @ x.t()).float().to(dev) + eps * torch.eye(n, device=dev)
+    store, _ = _store(dev, OD([("k/kernel", (n, 8))]))
+    tx = Shampoo(1e-3, eps=eps)
+    st = tx.init(store)
+    s = st.mats[0]
+    pl = tx._plans(store, st, None, True)
+    s.L.copy_(L)
+    pl["root"].run(), pl["eig"].run(), pl["pmat"].run()
+    torch.cuda.synchronize()
+    def ref(Lm, dt):
+        w, Q = torch.linalg.eigh(Lm.to(dt) + eps * torch.eye(n, device=dev, dtype=dt))
+        return ((Q * w.clamp(min=eps) ** -0.25) @ Q.t()).double()
+    P64 = ref(L, torch.float64)
+    rel = lambda P: (P.double() - P64).norm().item() / P64.norm().item()  # noqa: E731
+    got, base = rel(s.PL), rel(ref(L, torch.float32))
+    assert got <= 2 * base + 1e-5, (got, base)
+    status = pl["root"].items[0]["status"].item()
+    if rank < 5:
+        assert status == 1.0
+
+
+@pytest.mark.parametrize("root", ["newton", "eigh"])
+def test_shampoo_matches_oracle(dev, root):
     from oracle import optim as oopt
     from plaincv_amd.optim.shampoo import Shampoo
     shapes = OrderedDict([("Dense_0/kernel", (48, 96)), ("Dense_0/bias", (96,)), ("head/kernel", (96, 40)),
                           ("sq/kernel", (64, 64))])
     lr = 1e-2
-    steps = _run_pair(dev, shapes, Shampoo(lr, eps=1e-4, weight_decay=0.01),
+    steps = _run_pair(dev, shapes, Shampoo(lr, eps=1e-4, weight_decay=0.01, root_method=root),
                       oopt.shampoo(lr, eps=1e-4, weight_decay=0.01), 6)
     for i, (u, o) in enumerate(steps):
         for k in shapes:
