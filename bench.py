@@ -1,6 +1,6 @@
 """Benchmark: plainCV training hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload vit_c2|vit_c4_soap|vit_c4_shampoo|lm124m] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload vit_c2|vit_c4_soap|vit_c4_shampoo|lm124m|lm420m] [--no-cpu-baseline]
 
 Default workload (N=1): BASELINE.json configs[1] -- ViT-small on Tiny-ImageNet-
 shaped synthetic data (uint8 64x64x3, 200 classes, per-GPU batch 64, dropout 0.1,
@@ -222,19 +222,83 @@ def bench_vit(args):
     return out
 
 
+def cpu_baseline_lm(cfg, variables, clip, seconds=12.0):
+    """oracle/ (PyTorch CPU fp32 restatement) timed on this host: the same LM and optimizer at
+    micro-batch 1 x seq_len tokens, bounded to ~`seconds` of CPU work."""
+    from oracle import optim as oopt
+    from oracle.engine import apply_updates, clip_grads, lm_loss_and_acc, value_and_grad
+    from oracle.lm import model_config_from_cfg, transformer_apply
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    mc = model_config_from_cfg(cfg)
+    params = {k: v.clone() for k, v in variables["params"].items()}
+    tx = oopt.get_optimizer(cfg)
+    st = tx.init(params)
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(0, cfg.vocab_size, (1, cfg.seq_len + 1), generator=g, dtype=torch.int64)
+
+    def step():
+        nonlocal params, st
+        _, grads = value_and_grad(lambda p: lm_loss_and_acc(transformer_apply(p, ids[:, :-1], mc), ids[:, 1:]),
+                                  params)
+        if clip:
+            grads = clip_grads(grads, clip)
+        upd, st = tx.update(grads, st, params)
+        params = apply_updates(params, upd)
+
+    step()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        n += 1
+        if time.perf_counter() - t0 > seconds or n >= 20:
+            break
+    dt = (time.perf_counter() - t0) / n
+    model_name = "unknown"
+    try:
+        model_name = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(" :\t")
+    except Exception:
+        pass
+    return {"value": round(cfg.seq_len / dt, 2), "unit": "tokens/s", "cores": threads, "kind": "port",
+            "steps_per_sec": round(1.0 / dt, 4),
+            "sample": f"{n} timed oracle {cfg.optim} train steps of 1 x {cfg.seq_len} tokens (fp32) after 1 warmup; "
+                      f"CPU {model_name}"}
+
+
+LM_CFGS = {
+    # BASELINE configs[2]: 124M causal LM (config/lm_adam.yaml shape), AdamW, seq 1024, micro-batch 16
+    "lm124m": dict(cfg=dict(model="transformer", vocab_size=50257, d_model=768, expand="8/3", n_layers=12, n_heads=12,
+                            mlp_class="glu", seq_len=1024, tie_embeddings=False, rope_theta=500000.0,
+                            dtype="bfloat16", optim="adamw", lr=3e-4, weight_decay=0.1, beta1=0.9, beta2=0.95,
+                            seed=0),
+                   mb=16, accum=1, clip=None, name="lm124m_adamw (BASELINE configs[2] shape)"),
+    # BASELINE configs[4]: 420M LM (config/tr_420M_x8gpu.yaml: d 1024, L 24, H 16, V 50280, T 2048,
+    # micro-batch 8, accum 4, grad_clip 1.0) with Muon (config/lm_muon.yaml muon_* keys)
+    "lm420m": dict(cfg=dict(model="transformer", vocab_size=50280, d_model=1024, expand="8/3", n_layers=24,
+                            n_heads=16, mlp_class="glu", seq_len=2048, tie_embeddings=False, rope_theta=500000.0,
+                            dtype="bfloat16", optim="muon", lr=3e-3, weight_decay=0.1, beta1=0.9, beta2=0.95,
+                            muon_beta=0.95, muon_ns_steps=5, muon_ns_coeffs=[3.4445, -4.7750, 2.0315],
+                            muon_nesterov=True, seed=100),
+                   mb=8, accum=4, clip=1.0, name="lm420m_muon (BASELINE configs[4] shape, tr_420M_x8gpu.yaml)"),
+}
+
+
 def bench_lm(args):
-    """124M causal LM (BASELINE configs[2] shape, AdamW, seq 1024, micro-batch 16)."""
+    """Causal LM train step: `accum` micro-steps (forward + backward) + grad clip + optimizer."""
     from plaincv_amd.engine.lm import create_lm_state, make_apply_grads_fn, make_train_fns
     from plaincv_amd.models.LM.constructor import construct_model
     rank, local_rank, world, dev = dp.init_from_env()
-    cfg = Config(model="transformer", vocab_size=50257, d_model=768, expand="8/3", n_layers=12, n_heads=12,
-                 mlp_class="glu", seq_len=1024, tie_embeddings=False, rope_theta=500000.0, dtype="bfloat16",
-                 optim="adamw", lr=3e-4, weight_decay=0.1, beta1=0.9, beta2=0.95, seed=0)
+    spec = LM_CFGS[args.workload]
+    cfg = Config(spec["cfg"])
+    if args.lm_micro_batch is None:
+        args.lm_micro_batch = spec["mb"]
+    if args.lm_accum is None:
+        args.lm_accum = spec["accum"]
     mb, accum = args.lm_micro_batch, args.lm_accum
     model, mc, variables = construct_model(cfg)
     st = create_lm_state(cfg, model, variables, mb, dev, accum=accum)
     compute_grads, _ = make_train_fns()
-    apply_grads = make_apply_grads_fn(None)
+    apply_grads = make_apply_grads_fn(spec["clip"])
     gen = torch.Generator().manual_seed(99 + rank)
     pool = torch.randint(0, cfg.vocab_size, (4, mb, cfg.seq_len + 1), generator=gen, dtype=torch.int32).to(dev)
 
@@ -266,13 +330,15 @@ def bench_lm(args):
     return {"metric": METRIC, "value": round(tokens / dt, 1), "unit": "tokens/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic token ids U[0,50257), resident in HBM",
-            "config": {"workload": "lm124m_adamw (BASELINE configs[2] shape)", "micro_batch": mb, "accum": accum,
+            "data": f"synthetic token ids U[0,{cfg.vocab_size}), resident in HBM",
+            "config": {"workload": spec["name"], "micro_batch": mb, "accum": accum, "grad_clip": spec["clip"],
                        "seq_len": cfg.seq_len, "global_batch_tokens": world * mb * accum * cfg.seq_len,
                        "parallelism": f"dp{world}"},
             "steps_per_sec": round(args.steps / dt, 4),
             "tflops_per_gpu": round(tokens / world / dt * fpt / 1e12, 2),
-            "roofline": lm_roofline(st), "cpu_baseline": None}
+            "roofline": lm_roofline(st),
+            "cpu_baseline": (cpu_baseline_lm(cfg, variables, spec["clip"], args.cpu_seconds)
+                             if world == 1 and not args.no_cpu_baseline else None)}
 
 
 def lm_roofline(st):
@@ -297,20 +363,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="vit_c2", choices=["vit_c2", "vit_c4_soap", "vit_c4_shampoo", "lm124m"])
+    ap.add_argument("--workload", default="vit_c2", choices=["vit_c2", "vit_c4_soap", "vit_c4_shampoo", "lm124m", "lm420m"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--lm-micro-batch", type=int, default=16)
-    ap.add_argument("--lm-accum", type=int, default=1)
+    ap.add_argument("--lm-micro-batch", type=int, default=None, help="default: the workload's config")
+    ap.add_argument("--lm-accum", type=int, default=None, help="default: the workload's config")
     ap.add_argument("--with-lm", action="store_true", help="also run the 124M LM and attach it as 'lm124m'")
     args = ap.parse_args()
-    if args.workload == "lm124m":
+    if args.workload.startswith("lm"):
         out = bench_lm(args)
     else:
         out = bench_vit(args)
         if args.with_lm and out is not None:
             a2 = argparse.Namespace(**vars(args))
-            a2.steps, a2.warmup = 3, 1
+            a2.steps, a2.warmup, a2.workload = 3, 1, "lm124m"
             out["lm124m"] = bench_lm(a2)
     if out is not None:
         print(json.dumps(out), flush=True)

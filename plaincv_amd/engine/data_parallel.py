@@ -8,6 +8,12 @@ optimizer step (the reference reduces every micro-step; mean-of-sums equals
 sum-of-means up to fp rounding), in contiguous buckets walked from the end of
 the buffer (= the order the backward produces them).  Params/optimizer state
 stay replicated; every rank runs the identical optimizer update.
+
+Overlap (:class:`OverlappedReducer`): during the LAST micro-step's backward the runner reports,
+layer by layer, the offset above which the flat gradient is final; once a bucket's worth is
+final it is all-reduced on a side stream (RCCL over xGMI) while the backward continues on the
+compute stream, ordered by HIP events -- so only the last bucket (the embedding's rows) is
+exposed after the backward.
 ``torch.distributed`` backend "nccl" is RCCL on ROCm; "gloo" is used for the
 CPU multi-process tests.
 """
@@ -100,3 +106,54 @@ def all_reduce_metrics(m):
     if world_size() > 1:
         all_reduce_mean_(m)
     return m
+
+
+class OverlappedReducer:
+    """Bucketed gradient mean overlapped with the backward that produces the gradients.
+
+    ``ready(offset)``: flat[offset:] is final (the backward walks the layout back to front);
+    buckets of >= ``bucket_bytes`` are launched immediately on the communication stream after an
+    event recorded on the compute stream.  ``finish()`` reduces the rest and makes the compute
+    stream wait for every launched reduction.  With one rank it does nothing; on CPU (gloo tests)
+    the reductions run synchronously with the same bucketing."""
+
+    def __init__(self, flat, bucket_bytes=32 << 20):
+        self.flat = flat
+        self.bucket = max(1, bucket_bytes // flat.element_size())
+        self.active = world_size() > 1
+        self.cuda = flat.is_cuda
+        self.comm = torch.cuda.Stream(device=flat.device) if (self.active and self.cuda) else None
+        self.pending_end = None
+        self.launched = 0
+
+    def begin(self, end=None):
+        self.pending_end = self.flat.numel() if end is None else int(end)
+        self.launched = 0
+
+    def _launch(self, start, end):
+        chunk = self.flat[start:end]
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.flat.device))
+            self.comm.wait_event(ev)
+            with torch.cuda.stream(self.comm):
+                all_reduce_mean_(chunk, bucket_bytes=(end - start) * self.flat.element_size())
+        else:
+            all_reduce_mean_(chunk, bucket_bytes=(end - start) * self.flat.element_size())
+        self.launched += 1
+
+    def ready(self, offset):
+        if not self.active or self.pending_end is None:
+            return
+        if self.pending_end - offset >= self.bucket:
+            self._launch(int(offset), self.pending_end)
+            self.pending_end = int(offset)
+
+    def finish(self):
+        if not self.active or self.pending_end is None:
+            return
+        if self.pending_end > 0:
+            self._launch(0, self.pending_end)
+        self.pending_end = None
+        if self.cuda:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.comm)

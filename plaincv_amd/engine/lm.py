@@ -38,6 +38,8 @@ class LMTrainState:
     partial: torch.Tensor = None
     loss_sum: torch.Tensor = None
     track_norm: bool = False          # compute ||g|| every step even without clipping
+    micro: int = 0                    # micro-steps accumulated since the last optimizer step
+    reducer: Any = None               # data_parallel.OverlappedReducer (world > 1)
 
 
 def create_lm_state(cfg, model, variables, micro_batch, device, accum=1):
@@ -52,6 +54,7 @@ def create_lm_state(cfg, model, variables, micro_batch, device, accum=1):
                       gscale=torch.ones(1, device=device), gnorm=torch.zeros(1, device=device), chunks=chunks,
                       partial=torch.zeros(int(chunks.shape[0]), device=device),
                       loss_sum=torch.zeros(2, device=device))
+    st.reducer = dp.OverlappedReducer(store.grad_flat[: store.layout.size])
     return st
 
 
@@ -60,10 +63,18 @@ def make_train_fns(use_doc_mask=False):
         raise NotImplementedError("intra_doc_masking is SURVEY §8f-1 'next' (segment ids in the attention kernel)")
 
     def compute_grads(state: LMTrainState, input_ids):
+        """One micro-step (train_lm.py:189-210).  On the last micro-step of an optimizer step the
+        gradient all-reduce is overlapped with this backward (data_parallel.OverlappedReducer);
+        apply_grads finishes it."""
         r = state.runner
         r.set_batch(input_ids)
         m = r.forward(need_grad=True)
-        r.backward()
+        last = state.micro == state.accum - 1
+        red = state.reducer if (last and state.reducer is not None and state.reducer.active) else None
+        if red is not None:
+            red.begin()
+        r.backward(on_ready=red.ready if red is not None else None)
+        state.micro = (state.micro + 1) % state.accum
         state.loss_sum.add_(m)
         return m
 
@@ -79,7 +90,11 @@ def make_train_fns(use_doc_mask=False):
 def make_apply_grads_fn(grad_clip=None):
     def apply_grads(state: LMTrainState):
         store = state.params
-        dp.all_reduce_grads(store)
+        if state.reducer is not None and state.reducer.pending_end is not None:
+            state.reducer.finish()          # reductions launched during the last backward
+        else:
+            dp.all_reduce_grads(store)
+        state.micro = 0
         if grad_clip or state.track_norm:
             K.grad_scale(store.grad_flat, state.chunks, state.partial, 1.0, grad_clip if grad_clip else 0.0,
                          state.gscale, state.gnorm)

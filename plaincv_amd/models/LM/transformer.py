@@ -173,6 +173,11 @@ class LMRunner:
         self.grad_scale = 1.0 / R if grad_scale is None else grad_scale
         self._views()
         self._transposed_weights(dev)
+        # flat-gradient offsets above which the backward has finished (overlapped DP reduction)
+        lv = store.layout.leaves
+        first = lambda pre: min(l.offset for k, l in lv.items() if k.startswith(pre))  # noqa: E731
+        self._ready_off = {i: first(f"layers_{i}/") for i in range(L)}
+        self._ready_off["head"] = first("out_norm/")
 
     def _views(self):
         s, c = self.s, self.c
@@ -256,7 +261,10 @@ class LMRunner:
         K.mean2(self.row_loss, self.row_correct, self.R, 1.0 / self.R, self.metrics)
         return self.metrics
 
-    def backward(self):
+    def backward(self, on_ready=None):
+        """on_ready(offset): called (host side, in stream order) whenever the flat gradient above
+        `offset` is final -- after the head, after each layer, after the embedding -- so a data-
+        parallel reducer can overlap the all-reduce of those rows with the rest of the backward."""
         c = self.c
         b, T, d, H, Dh = self.b, self.T, self.d, self.H, self.Dh
         dl = self.logits  # dlogits (in place)
@@ -267,6 +275,8 @@ class LMRunner:
             K.gemm(self.yf, dl, self.gWh, ta=True, beta=1.0)
             K.gemm(dl, self.Wh, self.dy, tb=True)
         K.rmsnorm_bwd(self.dy, self.x[-1], self.sf, self.rf, None, self.dx, self.gsf)
+        if on_ready is not None:
+            on_ready(self._ready_off["head"])
         for i in reversed(range(c.n_layers)):
             w = self.w[i]
             K.gemm(self.hm[i], self.dx, w["gW2"], ta=True, beta=1.0)
@@ -283,4 +293,8 @@ class LMRunner:
             K.gemm(self.y0[i], self.dqkv, w["gWqkv"], ta=True, beta=1.0)
             K.gemm(self.dqkv, w["Wqkv"], self.dy, tb=True)
             K.rmsnorm_bwd(self.dy, self.x[i], w["s0"], self.r0[i], self.dx, self.dx, w["gs0"])
+            if on_ready is not None and i > 0:
+                on_ready(self._ready_off[i])
         K.embed_bwd(self.inputs, self.dx, self.gWemb)
+        if on_ready is not None:
+            on_ready(0)

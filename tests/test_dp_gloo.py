@@ -56,3 +56,38 @@ def test_gloo_world2_grad_mean():
     for r in range(world):
         ok, mean_ok, sem_ok, ws = out[r]
         assert ok and mean_ok and sem_ok and ws == world, out[r]
+
+
+def _overlap_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from plaincv_amd.engine import data_parallel as dp
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 10_000
+        flat = torch.arange(n, dtype=torch.float32) * (rank + 1)
+        red = dp.OverlappedReducer(flat, bucket_bytes=4 * 1500)
+        red.begin()
+        # the LM backward's ready points: head, layers top to bottom, embedding (offset 0)
+        for off in (9_000, 7_700, 6_000, 5_900, 3_000, 1_200, 0):
+            red.ready(off)
+        launched_before_finish = red.launched
+        red.finish()
+        ok = torch.allclose(flat, torch.arange(n, dtype=torch.float32) * (world + 1) / 2)
+        out[rank] = (ok, launched_before_finish, red.pending_end)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_overlapped_reducer():
+    """OverlappedReducer: buckets launched as the backward reports final regions, the rest at
+    finish(); the result is the exact mean of every element."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_overlap_worker, args=(world, _port(), out), nprocs=world, join=True)
+    for r in range(world):
+        ok, launched, pend = out[r]
+        assert ok and launched >= 3 and pend is None, out[r]
