@@ -48,6 +48,16 @@ int pcv_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, i
                   const void* attn_o, int64_t ld_attn_o, float* attn_delta, int attn_T, int attn_H, int split_k,
                   void* stream);
 
+/* 256x256 8-wave ping-pong GEMM (csrc/gemm_big.hip) for large products with BOTH operands
+ * K-contiguous: C[M,N] (bf16) = alpha * A[M,K] . B[N,K]^T (+ res_scale * res (bf16)).  pcv_gemm_bf16
+ * dispatches to it by itself when pcv_gemm_big_ok() (eligible shape, >= 512 tiles, enabled);
+ * pcv_gemm_big_enable(on) toggles that dispatch (on < 0: query) and returns the previous state.
+ * Replaces the same flax Dense contractions as pcv_gemm_bf16 (the LM forward and dgrad GEMMs). */
+int pcv_gemm_big_enable(int on);
+int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb);
+int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                 int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale, void* stream);
+
 /* GEMM + LayerNorm over each complete output row (N <= 128, N % 8 == 0; ViT residual stream).
  * ln_mode 1: C = x1 = alpha*op(A)op(B) + bias (+dropout) + res (fp32); ln_y = bf16 LN(x1),
  *            ln_mean / ln_rstd written (flax LayerNorm fwd, models/vit_small.py:38,52).

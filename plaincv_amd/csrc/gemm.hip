@@ -19,6 +19,12 @@
 // remapped so each XCD gets a contiguous run of tiles, grouped 8 along M.
 #include "common.h"
 
+extern "C" int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                               int64_t ldb);
+extern "C" int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                            int64_t ldb, int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale,
+                            void* stream);
+
 #include <vector>
 
 namespace pcv {
@@ -513,6 +519,9 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
 #ifndef PCV_GEMM_STAGES_BIG
 #define PCV_GEMM_STAGES_BIG 2
 #endif
+#ifndef PCV_GEMM_RAW_BARRIER
+#define PCV_GEMM_RAW_BARRIER 0
+#endif
 template <int WM, int WN>
 struct GemmStages {
   static constexpr int S =
@@ -671,7 +680,17 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
     for (int i = 0; i < S - 1; ++i) issue(i);
     for (int kt = 0; kt < nfull; ++kt) {
       wait_tiles<PIECES, S - 2>(nfull - 1 - kt);   // tile kt landed: later tiles may stay in flight
+#if PCV_GEMM_RAW_BARRIER
+      // raw s_barrier: __syncthreads() would add a vmcnt(0) and drain the deeper ring's later
+      // tiles at every k-step.  RAW: each wave's counted vmcnt above + this barrier order the
+      // LDS-DMA data for every reader; WAR: a stage is re-issued only after all waves passed this
+      // barrier, i.e. finished the MFMAs (and so the ds_reads) of the tile it held.
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#else
       __syncthreads();
+#endif
       issue(kt + S - 1);
       compute(smem + (kt % S) * STAGE);
     }
@@ -1099,6 +1118,12 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
     g.k_per_split = kps;
   }
   hipStream_t s = (hipStream_t)stream;
+  // large products with both operands K-contiguous and a plain (or residual) bf16 epilogue:
+  // the 256x256 8-wave ping-pong kernel (gemm_big.hip)
+  if (!trans_a && trans_b && !out_f32 && batch == 1 && g.split_k == 1 && !bias && !aux && act == EPI_NONE &&
+      g.drop_thresh == 0 && !colsum && !attn_delta && (!res || !res_f32) &&
+      pcv_gemm_big_ok(M, N, K, A, lda, B, ldb))
+    return pcv_gemm_big(A, B, C, M, N, K, lda, ldb, ldc, alpha, res, ldr, res_scale, stream);
   // tile: 128x128 when that grid covers the chip, else 64x64.  (A 256x256 tile with
   // one 128x128 block per wave was measured 15-45 % slower at the LM shapes: it needs
   // all 512 registers, spills, and runs one wave per SIMD.)

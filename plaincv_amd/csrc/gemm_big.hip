@@ -1,0 +1,267 @@
+// plaincv_amd/csrc/gemm_big.hip -- 256x256 bf16 GEMM for the large K-contiguous LM products.
+//
+// C[M,N] (bf16) = alpha * A[M,K] . B[N,K]^T (+ res_scale * res), A and B both K-contiguous:
+// every LM forward GEMM (activations x K-contiguous weight copies: qkv, out, gate|up, fc2,
+// lm_head) and the data-gradient GEMMs (dY x W^T) of models/LM/transformer.py:194-201,
+// 246-253, 110-134, 393-405.  Dispatched from pcv_gemm_bf16 when the product has enough
+// 256x256 tiles to fill the chip and no fused epilogue beyond a residual.
+//
+// Structure (MI355X: 2 waves per SIMD, the two halves of the workgroup ping-pong):
+//   * 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns a 128 x 64 output block,
+//     8 x 4 accumulators of v_mfma_f32_16x16x32_bf16 (128 VGPRs);
+//   * K advances in 32-wide steps through a 4-slot LDS ring (A and B images of one step,
+//     32 KiB per slot, 128 KiB total), filled by global_load_lds (LDS-DMA) 3 steps ahead;
+//     the images are 64-byte rows with the 16-byte k-chunks XOR-swizzled by 2 * ((row >> 3) & 1),
+//     applied on the SOURCE address (the DMA writes lane-linear): every ds_read_b128 lane group
+//     of gfx950 ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...) then covers the 64 banks exactly
+//     once (found by exhaustive search over XOR maps), so fragment reads are conflict free;
+//   * the two wave groups (M halves) run one barrier apart, so at every moment one group
+//     issues its MFMAs while the other issues its loads and LDS reads;
+//   * synchronisation (per step s, both groups): issue step s+3 -> read slot s -> lgkmcnt(0)
+//     -> [group 1: vmcnt retiring step s+1] -> barrier -> MFMAs -> [group 0: vmcnt retiring
+//     step s+1] -> barrier.  Barrier i of group 0 is barrier i-1 of group 1, which gives:
+//       RAW: a slot is read only after every wave's counted vmcnt retired its DMA and a barrier
+//            both groups passed afterwards;
+//       WAR: slot (s-1)&3 is re-filled (step s+3) only after both groups' reads of step s-1
+//            were retired by their lgkmcnt(0) before a barrier the issuer has passed.
+//     No __syncthreads() in the loop (it would add vmcnt(0) and drain the prefetch).
+//   * a ragged K tail (K % 32) goes through registers with zero fill after the ring drains;
+//   * the bf16 tile is staged through LDS and stored as 16-byte rows (+ residual).
+#include "common.h"
+
+namespace pcv {
+
+struct BigArgs {
+  const bf16* A; const bf16* B; bf16* C; const bf16* res;
+  int64_t lda, ldb, ldc, ldr;
+  int M, N, K, tiles_m, tiles_n;
+  float alpha, res_scale;
+};
+
+constexpr int GB_T = 256;                 // tile
+constexpr int GB_IMG = GB_T * 64;         // one operand image of a 32-k step: 256 rows x 64 B
+constexpr int GB_SLOT = 2 * GB_IMG;       // A + B
+constexpr int GB_SLOTS = 4;
+constexpr int GB_CLD = GB_T * 2 + 16;     // epilogue staging row (bytes): +16 B breaks 4-row bank aliasing
+constexpr int GB_LDS = (GB_SLOTS * GB_SLOT > GB_T * GB_CLD) ? GB_SLOTS * GB_SLOT : GB_T * GB_CLD;
+
+typedef __attribute__((address_space(3))) void gb_lds_void;
+
+__device__ __forceinline__ void gb_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// retire this wave's loads of step s+1: at most 4 * min(2, remaining) DMA ops may stay in flight
+__device__ __forceinline__ void gb_wait_next(int steps_after) {
+  if (steps_after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (steps_after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // XCD-aware bijective remap, then 8-row groups along M (as gemm.hip)
+  const int bid = blockIdx.x, nwg = g.tiles_m * g.tiles_n;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int per_group = 8 * g.tiles_n;
+  const int first_m = (wgid / per_group) * 8;
+  const int gsz = min(g.tiles_m - first_m, 8);
+  const int tm = first_m + (wgid % per_group) % gsz, tn = (wgid % per_group) / gsz;
+  const int m0 = tm * GB_T, n0 = tn * GB_T;
+
+  // DMA sources: this wave fills 1-KiB pieces (wave*2 + i) of each image = rows 16*(wave*2+i) ..
+  // lane -> row (lane >> 2), stored chunk (lane & 3) <- source k-chunk (lane & 3) ^ 2*((row >> 3) & 1)
+  const bf16* srcA[2];
+  const bf16* srcB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 16 + (lane >> 2);
+    const int kc = (lane & 3) ^ (((row >> 3) & 1) << 1);
+    const int ra = min(m0 + row, g.M - 1), rb = min(n0 + row, g.N - 1);   // clamped rows feed only masked outputs
+    srcA[i] = g.A + (int64_t)ra * g.lda + kc * 8;
+    srcB[i] = g.B + (int64_t)rb * g.ldb + kc * 8;
+  }
+  const int nsteps = g.K / 32;
+  auto issue = [&](int s) {
+    char* slot = smem + (s & 3) * GB_SLOT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(srcA[i] + s * 32), (gb_lds_void*)(slot + (wave * 2 + i) * 1024),
+                                       16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(srcB[i] + s * 32),
+                                       (gb_lds_void*)(slot + GB_IMG + (wave * 2 + i) * 1024), 16, 0, 0);
+  };
+
+  // fragment offsets within an image (the swizzle depends only on lane & 15)
+  const int fsw = (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) << 4);
+  int offA[8], offB[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) offA[i] = (wr * 128 + i * 16 + (lane & 15)) * 64 + fsw;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) offB[j] = GB_IMG + (wc * 64 + j * 16 + (lane & 15)) * 64 + fsw;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto mfmas = [&](const bf16x8 (&a)[8], const bf16x8 (&b)[4]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  };
+
+  if (nsteps > 0) {
+    for (int s = 0; s < 3 && s < nsteps; ++s) issue(s);
+    gb_wait_next(min(2, nsteps - 1));   // step 0 retired (loads of steps 1, 2 may fly)
+    gb_barrier();
+    if (wr == 1) gb_barrier();          // stagger: group 1 runs one barrier behind
+    for (int s = 0; s < nsteps; ++s) {
+      if (s + 3 < nsteps) issue(s + 3);
+      const char* slot = smem + (s & 3) * GB_SLOT;
+      bf16x8 a[8], b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(slot + offB[j]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(slot + offA[i]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const int after = min(nsteps - 1, s + 3) - (s + 1);   // steps issued after step s+1
+      if (wr == 1 && s + 1 < nsteps) gb_wait_next(after);
+      gb_barrier();
+      __builtin_amdgcn_s_setprio(1);
+      mfmas(a, b);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (wr == 0 && s + 1 < nsteps) gb_wait_next(after);
+      gb_barrier();
+    }
+    if (wr == 0) gb_barrier();          // equal barrier counts for both groups
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // ragged K tail through registers, zero-filled: 256 rows x 4 chunks per operand, 2 chunks per thread
+  const int ktail = g.K - nsteps * 32;
+  if (ktail > 0) {
+    const int k0 = nsteps * 32;
+#pragma unroll
+    for (int op = 0; op < 2; ++op) {
+      const bf16* base = op ? g.B : g.A;
+      const int64_t ld = op ? g.ldb : g.lda;
+      const int r0 = op ? n0 : m0, rows = op ? g.N : g.M;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int idx = tid + h * 512, row = idx >> 2, kc = idx & 3;
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = k0 + kc * 8 + e;
+          v[e] = (r0 + row < rows && k < g.K) ? base[(int64_t)(r0 + row) * ld + k] : f2bf(0.f);
+        }
+        *reinterpret_cast<bf16x8*>(smem + op * GB_IMG + row * 64 + ((kc ^ (((row >> 3) & 1) << 1)) << 4)) = v;
+      }
+    }
+    __syncthreads();
+    bf16x8 a[8], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(smem + offB[j]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(smem + offA[i]);
+    mfmas(a, b);
+    __syncthreads();
+  }
+
+  // epilogue: bf16 tile staged in LDS ([256][CLD bytes]), then 16-B row chunks (+ residual)
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 128 + i * 16 + (lane >> 4) * 4 + r, col = wc * 64 + j * 16 + (lane & 15);
+        *reinterpret_cast<bf16*>(smem + row * GB_CLD + col * 2) = f2bf(g.alpha * acc[i][j][r]);
+      }
+  __syncthreads();
+  const bool vec = ((g.ldc & 7) == 0) && ((uintptr_t)g.C & 15) == 0 &&
+                   (!g.res || (((g.ldr & 7) == 0) && ((uintptr_t)g.res & 15) == 0));
+#pragma unroll 4
+  for (int e = tid; e < GB_T * 32; e += 512) {
+    const int row = e >> 5, cc = (e & 31) * 8;
+    const int gr = m0 + row, gc = n0 + cc;
+    if (gr >= g.M || gc >= g.N) continue;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + row * GB_CLD + cc * 2);
+    bf16* dst = g.C + (int64_t)gr * g.ldc + gc;
+    if (vec && gc + 8 <= g.N) {
+      if (g.res) {
+        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(g.res + (int64_t)gr * g.ldr + gc);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + g.res_scale * bf2f(rv[q]));
+      }
+      *reinterpret_cast<bf16x8*>(dst) = v;
+    } else {
+      for (int q = 0; q < 8 && gc + q < g.N; ++q) {
+        float x = bf2f(v[q]);
+        if (g.res) x += g.res_scale * bf2f(g.res[(int64_t)gr * g.ldr + gc + q]);
+        dst[q] = f2bf(x);
+      }
+    }
+  }
+}
+
+}  // namespace pcv
+
+using namespace pcv;
+
+static int g_big_enabled = 1;
+
+extern "C" int pcv_gemm_big_enable(int on) {
+  const int old = g_big_enabled;
+  if (on >= 0) g_big_enabled = on ? 1 : 0;
+  return old;
+}
+
+static bool big_shape_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb) {
+  if (M <= 0 || N <= 0 || K < 32 * 4 || M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return false;
+  return !((lda & 7) || (ldb & 7) || !pcv_aligned16(A) || !pcv_aligned16(B));
+}
+
+// Dispatch test used by pcv_gemm_bf16 (which falls back to the 128x128 family otherwise): both
+// operands K-contiguous with 16-B aligned rows, bf16 output, and enough 256x256 tiles to fill
+// every CU twice (smaller grids leave CUs idle at one 128-KiB workgroup per CU).
+extern "C" int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                               int64_t ldb) {
+  if (!g_big_enabled || !big_shape_ok(M, N, K, A, lda, B, ldb)) return 0;
+  const int64_t tiles = ((M + GB_T - 1) / GB_T) * ((N + GB_T - 1) / GB_T);
+  return tiles >= 512 ? 1 : 0;
+}
+
+extern "C" int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                            int64_t ldb, int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale,
+                            void* stream) {
+  if (!big_shape_ok(M, N, K, A, lda, B, ldb) || !C) return PCV_EINVAL;
+  BigArgs g{};
+  g.A = (const bf16*)A; g.B = (const bf16*)B; g.C = (bf16*)C; g.res = (const bf16*)res;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldr = ldr;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.tiles_m = (int)((M + GB_T - 1) / GB_T);
+  g.tiles_n = (int)((N + GB_T - 1) / GB_T);
+  g.alpha = alpha; g.res_scale = res_scale;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(gemm_big_kernel, dim3(g.tiles_m * g.tiles_n), dim3(512), GB_LDS, (hipStream_t)stream, g);
+  return pcv_launch_status();
+}

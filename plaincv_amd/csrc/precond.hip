@@ -143,7 +143,6 @@ __device__ __forceinline__ void f32_tile(const F32Job& jb, int m0, int n0, float
       sb.load(B, k0 + FG_K, n0, N, K, bmul, bdiag, nullptr, rb);
     }
     const int kend = K - k0 < FG_K ? ((K - k0 + 3) & ~3) : FG_K;
-#pragma unroll 8
     for (int kk = 0; kk < kend; kk += 4) {
       const int kr = kk + (lane >> 4);
       float fa[2], fb[2];

@@ -79,3 +79,36 @@ def test_gemm_batched(dev):
     k.gemm(a, b, out, tb=True)
     ref = a.float() @ b.float().transpose(1, 2)
     assert torch.allclose(out, ref, rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("M,N,K,res", [(16384, 50257, 768, False), (8192, 4096, 1000, True), (16384, 2304, 128, False),
+                                       (6000, 5472, 2736, True), (4100, 8200, 200, False)])
+def test_gemm_big_kernel(dev, M, N, K, res):
+    """256x256 8-wave ping-pong kernel (gemm_big.hip) through pcv_gemm_bf16's dispatch (both operands
+    K-contiguous, bf16 out, >= 512 tiles): ragged M/N (clamped DMA rows), ragged K (register tail),
+    padded row strides, residual epilogue; and the same call with the big path disabled."""
+    from plaincv_amd import hip
+    from plaincv_amd import kernels as k
+    lib = hip.load()
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    a = _padded(M, K, dev, g)
+    b = _padded(N, K, dev, g)
+    r = _padded(M, N, dev, g) if res else None
+    assert lib.pcv_gemm_big_ok(M, N, K, hip.ptr(a), a.stride(0), hip.ptr(b), b.stride(0)) == 1
+    outs = []
+    for on in (1, 0):
+        prev = lib.pcv_gemm_big_enable(on)
+        try:
+            out = torch.empty(M, (N + 7) // 8 * 8, device=dev, dtype=torch.bfloat16)[:, :N]
+            k.gemm(a, b, out, tb=True, alpha=0.5, res=r)
+            torch.cuda.synchronize()
+        finally:
+            lib.pcv_gemm_big_enable(prev)
+        outs.append(out.float())
+    ref = 0.5 * (a.float() @ b.float().t())
+    if res:
+        ref = ref + r.float()
+    tol = 1e-3 * (K ** 0.5) * 4 + 1e-2 * ref.abs().max().item()   # bf16 output rounding
+    for out in outs:
+        assert (out - ref).abs().max().item() <= tol
+    assert (outs[0] - outs[1]).abs().max().item() <= tol
