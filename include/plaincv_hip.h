@@ -96,15 +96,21 @@ int pcv_gemm_grouped_run(const void* plan_dev, int n, int tile /* as planned */,
  * (models/LM/transformer.py:233-240). */
 int pcv_attn_fwd(const void* q, const void* k, const void* v, int64_t ldq, void* out, int64_t ldo,
                  float* lse2, int B, int T, int H, int head_dim, int causal,
-                 float dropout_rate, const uint16_t* drop_mask, void* stream);
+                 float dropout_rate, const uint16_t* drop_mask, const int* doc_start, const int* doc_end,
+                 void* stream);
 int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t ldq,
                  const void* o, int64_t ldo, const void* dout, int64_t lddo,
                  const float* lse2, float* delta_ws /* [B,H,T] */,
                  void* dq, void* dk, void* dv, int64_t lddq,
                  int B, int T, int H, int head_dim, int causal,
-                 float dropout_rate, const uint16_t* drop_mask, int delta_ready, void* stream);
+                 float dropout_rate, const uint16_t* drop_mask, int delta_ready, const int* doc_start,
+                 const int* doc_end, void* stream);
 /* (delta_ready: delta_ws already holds rowsum(dO * O) per (b, h, t) -- pcv_gemm_bf16's
  * attention-delta epilogue on the GEMM that produced dO -- so its kernel is skipped.)
+ * doc_start/doc_end (optional, causal only): int32 [B*T], the intra-document causal mask of
+ * train_lm.py:107-131 / data_prep_utils.py:14-43 -- key k is visible to query t iff
+ * doc_start[t] <= k <= t; doc_end[t] = end (exclusive) of t's document.  Key/query tiles outside
+ * a block's documents are skipped, so short documents cost proportionally less. */
  * Attention-weight dropout mask: flax draws ONE [T,T] keep mask per layer and
  * broadcasts it over batch and heads (models/vit_small.py:41-45, nn.Dropout with
  * broadcast_dims (0,1) inside dot_product_attention).  Drawn once per step for
@@ -145,6 +151,13 @@ int pcv_rope(void* qk, int64_t ld, int64_t R, int ncols, int T, int head_dim, co
 int pcv_swiglu_fwd(const void* gu, int64_t ldgu, void* h, int64_t ldh, int64_t R, int F, int Fp, void* stream);
 int pcv_swiglu_bwd(const void* dh, int64_t lddh, const void* gu, int64_t ldgu, void* dgu, int64_t lddgu,
                    int64_t R, int F, int Fp, void* stream);
+/* Non-gated LM MLPs: h = act(a) on the fc1 output a [R][Fp] (kind 1 silu: MLP,
+ * models/LM/transformer.py:70-97; kind 2 relu^2: MLPReluSquared, 138-165); backward da = dh * act'(a)
+ * (da may alias dh).  Pad columns [F, Fp) are written as 0. */
+int pcv_mlp_act_fwd(const void* a, int64_t lda, void* h, int64_t ldh, int64_t R, int F, int Fp, int kind,
+                    void* stream);
+int pcv_mlp_act_bwd(const void* dh, int64_t lddh, const void* a, int64_t lda, void* da, int64_t ldda, int64_t R,
+                    int F, int Fp, int kind, void* stream);
 /* out = bf16(x * dropout_mask) (backward of an output dropout, models/vit_small.py:17). */
 int pcv_dropout_bwd_cast(const float* x, int64_t ldx, void* out, int64_t ldo, int64_t R, int N,
                          float rate, const uint32_t* seed, uint32_t site, void* stream);

@@ -60,3 +60,25 @@ def value_and_grad(loss_fn, params):
 def apply_updates(params, updates):
     """optax.apply_updates: (p + u).astype(p.dtype)."""
     return {k: (p + updates[k]).to(p.dtype) for k, p in params.items()}
+
+
+def intra_doc_causal_mask(doc_boundaries, max_seq_length):
+    """data/datasets/data_prep_utils.py:14-43: block-diagonal causal bool mask [T, T]."""
+    if sum(doc_boundaries) != max_seq_length:
+        raise ValueError("Sum of doc_boundaries does not match max_seq_length.")
+    return torch.block_diag(*[torch.tril(torch.ones(n, n, dtype=torch.bool)) for n in doc_boundaries])
+
+
+def build_attn_mask(docs_lengths, seq_len):
+    """train_lm.py:97-131 (_trim_last_token + _build_attn_mask): (B, T, T) bool."""
+    masks = []
+    for boundaries in docs_lengths:
+        b = [int(x) for x in boundaries]
+        if b:
+            b[-1] -= 1
+            if b[-1] <= 0:
+                b.pop()
+        if sum(b) != seq_len:
+            raise ValueError(f"Sum(doc_boundaries)={sum(b)} != seq_len={seq_len}.")
+        masks.append(intra_doc_causal_mask(b, seq_len))
+    return torch.stack(masks, 0)

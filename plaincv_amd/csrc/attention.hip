@@ -40,6 +40,11 @@ struct AttnArgs {
   const uint16_t* mask;                   // packed keep bits, see drop_word()
   int n64;                                // key-tile count of the mask (2*ceil(T/128))
   int delta_ready;                        // bwd: delta already computed (fused into the dO producer)
+  // intra-document causal mask (train_lm.py:107-131, data_prep_utils.py:14-43): key k is visible to
+  // query q iff dstart[q] <= k <= q, i.e. same document; [B*T] int32, nullptr = plain causal.
+  // dend[t] = end (exclusive) of t's document.  Documents are contiguous, so dstart/dend are
+  // non-decreasing in t and a tile's extreme values are those of its first/last row.
+  const int* dstart; const int* dend;
 };
 
 // Dropout keep-mask layout.  flax SelfAttention broadcasts one [T,T] mask over batch
@@ -223,16 +228,28 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
 
   int nkb = (T + 63) / 64;
   if (CAUSAL) nkb = min(nkb, (qb * 128 + 127) / 64 + 1);
+  // document mask: keys below the block's first document start are never visible
+  const bool doc = CAUSAL && a.dstart != nullptr;
+  int kb0 = 0, wds = 0, gds[QG], myds[QG];
+  if (doc) {
+    kb0 = a.dstart[bT + min(qb * 128, T - 1)] / 64;
+    wds = a.dstart[bT + min(qw, T - 1)];
+#pragma unroll
+    for (int gq = 0; gq < QG; ++gq) {
+      gds[gq] = a.dstart[bT + min(qw + gq * 16 + 15, T - 1)];
+      myds[gq] = a.dstart[bT + min(qw + gq * 16 + (lane & 15), T - 1)];
+    }
+  }
   TileRegs<DH> pre;
-  tile_load<DH>(pre, Kp, Vp, a.ldq, 0, T, bT);
+  tile_load<DH>(pre, Kp, Vp, a.ldq, kb0 * 64, T, bT);
   tile_store<DH>(pre, kv_smem, kv_smem + TILE);
   __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
-    const bf16* Ks = kv_smem + 2 * (kb & 1) * TILE;
+  for (int kb = kb0; kb < nkb; ++kb) {
+    const bf16* Ks = kv_smem + 2 * ((kb - kb0) & 1) * TILE;
     const bf16* Vs = Ks + TILE;
     const bool more = kb + 1 < nkb;
     if (more) tile_load<DH>(pre, Kp, Vp, a.ldq, (kb + 1) * 64, T, bT);
-    const bool active = qw < T && (!CAUSAL || kb * 64 <= qw + 31);   // wave-uniform skip
+    const bool active = qw < T && (!CAUSAL || kb * 64 <= qw + 31) && (!doc || kb * 64 + 63 >= wds);   // wave-uniform
     if (active) {
       f32x4 s[QG][4];
 #pragma unroll
@@ -254,7 +271,9 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
       auto softmax = [&](auto maskc, int gq) {
         constexpr bool MASK = decltype(maskc)::value;
         const int myq = qw + gq * 16 + (lane & 15);
+        uint32_t okbits = 0xFFFFu;
         if constexpr (MASK) {
+          okbits = 0u;
 #pragma unroll
           for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -262,7 +281,9 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
               const int key = kb * 64 + 16 * t + 4 * g + r;
               bool ok = key < T;
               if (CAUSAL) ok = ok && key <= myq;
+              if (doc) ok = ok && key >= myds[gq];
               s[gq][t][r] = ok ? s[gq][t][r] : NEG_BIG;
+              okbits |= (ok ? 1u : 0u) << (4 * t + r);
             }
         }
         float bmax = NEG_BIG;
@@ -298,6 +319,9 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float p = __builtin_amdgcn_exp2f(fmaf(s[gq][t][r], c2, mneg));
+            // masked keys contribute exactly 0 (under a document mask a row can see no valid key in
+            // a tile while its running max is still the initial value)
+            if (MASK) p = ((okbits >> (4 * t + r)) & 1u) ? p : 0.f;
             rs += p;
             // dropped weights -> 0 (bit select); the 1/keep scale is applied at the end
             if (DROP) p = __uint_as_float(__float_as_uint(p) & (uint32_t)__builtin_amdgcn_sbfe((int)wt[t], r, 1));
@@ -309,7 +333,8 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
       };
 #pragma unroll
       for (int gq = 0; gq < QG; ++gq) {
-        const bool interior = kb * 64 + 63 < T && (!CAUSAL || kb * 64 + 63 <= qw + gq * 16);
+        const bool interior = kb * 64 + 63 < T && (!CAUSAL || kb * 64 + 63 <= qw + gq * 16) &&
+                              (!doc || kb * 64 >= gds[gq]);
         if (interior) softmax(std::false_type{}, gq);
         else softmax(std::true_type{}, gq);
       }
@@ -327,7 +352,10 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
         }
       }
     }
-    if (more) tile_store<DH>(pre, kv_smem + 2 * ((kb + 1) & 1) * TILE, kv_smem + (2 * ((kb + 1) & 1) + 1) * TILE);
+    if (more) {
+      const int nb = (kb + 1 - kb0) & 1;
+      tile_store<DH>(pre, kv_smem + 2 * nb * TILE, kv_smem + (2 * nb + 1) * TILE);
+    }
     __syncthreads();
   }
   // normalise + store
@@ -446,8 +474,18 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
       t.d = qq < T ? del[qq] : 0.f;
     }
   };
-  const int nqb = (T + 63) / 64;
+  int nqb = (T + 63) / 64;
   const int qb0 = CAUSAL ? (kb * 128) / 64 : 0;
+  // document mask: queries at or past the end of the block's last document never see its keys
+  const bool doc = CAUSAL && a.dstart != nullptr;
+  int wde_lo = 0, wde_hi = 0, myde[KG];
+  if (doc) {
+    nqb = min(nqb, (a.dend[bT + min(kb * 128 + 127, T - 1)] + 63) / 64);
+    wde_lo = a.dend[bT + min(kw, T - 1)];
+    wde_hi = a.dend[bT + min(kw + 31, T - 1)];
+#pragma unroll
+    for (int gk = 0; gk < KG; ++gk) myde[gk] = a.dend[bT + min(kw + gk * 16 + (lane & 15), T - 1)];
+  }
   auto qstore = [&](const QTileRegs<DH>& t, int buf) {
 #pragma unroll
     for (int i = 0; i < QTileRegs<DH>::N; ++i) {
@@ -470,9 +508,10 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
     const float* Dl = Ls + 64;
     const bool more = qb + 1 < nqb;
     if (more) qload(pre, (qb + 1) * 64);
-    const bool active = kw < T && (!CAUSAL || qb * 64 + 63 >= kw);
+    const bool active = kw < T && (!CAUSAL || qb * 64 + 63 >= kw) && (!doc || qb * 64 < wde_hi);
     // every (query, key) pair of this wave's 64x32 block valid: skip per-element masks
-    const bool interior = qb * 64 + 63 < T && kw + 31 < T && (!CAUSAL || kw + 31 <= qb * 64);
+    const bool interior = qb * 64 + 63 < T && kw + 31 < T && (!CAUSAL || kw + 31 <= qb * 64) &&
+                          (!doc || qb * 64 + 63 < wde_lo);
     if (active) {
       f32x4 p[KG][4], ds[KG][4];
 #pragma unroll
@@ -501,6 +540,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
               const int qq = qb * 64 + ql;
               bool ok = mykey < T && qq < T;
               if (CAUSAL) ok = ok && mykey <= qq;
+              if (doc) ok = ok && qq < myde[gk];
               pv = ok ? pv : 0.f;
             }
             float dpv = dp[gk][r];
@@ -597,17 +637,27 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
 
   int nkb = (T + 63) / 64;
   if (CAUSAL) nkb = min(nkb, (qb * 128 + 127) / 64 + 1);
+  const bool doc = CAUSAL && a.dstart != nullptr;
+  int kb0 = 0, wds_lo = 0, wds_hi = 0, myds[QG];
+  if (doc) {
+    kb0 = a.dstart[bT + min(qb * 128, T - 1)] / 64;
+    wds_lo = a.dstart[bT + min(qw, T - 1)];
+    wds_hi = a.dstart[bT + min(qw + 31, T - 1)];
+#pragma unroll
+    for (int gq = 0; gq < QG; ++gq) myds[gq] = a.dstart[bT + min(qw + gq * 16 + (lane & 15), T - 1)];
+  }
   TileRegs<DH> pre;
-  tile_load<DH>(pre, Kp, Vp, a.ldq, 0, T, bT);
+  tile_load<DH>(pre, Kp, Vp, a.ldq, kb0 * 64, T, bT);
   tile_store<DH>(pre, kv_smem, kv_smem + TILE);
   __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
-    const bf16* Ks = kv_smem + 2 * (kb & 1) * TILE;
+  for (int kb = kb0; kb < nkb; ++kb) {
+    const bf16* Ks = kv_smem + 2 * ((kb - kb0) & 1) * TILE;
     const bf16* Vs = Ks + TILE;
     const bool more = kb + 1 < nkb;
     if (more) tile_load<DH>(pre, Kp, Vp, a.ldq, (kb + 1) * 64, T, bT);
-    const bool active = qw < T && (!CAUSAL || kb * 64 <= qw + 31);
-    const bool interior = kb * 64 + 63 < T && qw + 31 < T && (!CAUSAL || kb * 64 + 63 <= qw);
+    const bool active = qw < T && (!CAUSAL || kb * 64 <= qw + 31) && (!doc || kb * 64 + 63 >= wds_lo);
+    const bool interior = kb * 64 + 63 < T && qw + 31 < T && (!CAUSAL || kb * 64 + 63 <= qw) &&
+                          (!doc || kb * 64 >= wds_hi);
     if (active) {
       f32x4 ds[QG][4];
 #pragma unroll
@@ -635,6 +685,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
               const int key = kb * 64 + 16 * t + 4 * g + r;
               bool ok = myq < T && key < T;
               if (CAUSAL) ok = ok && key <= myq;
+              if (doc) ok = ok && key >= myds[gq];
               pv = ok ? pv : 0.f;
             }
             float dpv = dp[gq][r];
@@ -659,7 +710,10 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
         }
       }
     }
-    if (more) tile_store<DH>(pre, kv_smem + 2 * ((kb + 1) & 1) * TILE, kv_smem + (2 * ((kb + 1) & 1) + 1) * TILE);
+    if (more) {
+      const int nb = (kb + 1 - kb0) & 1;
+      tile_store<DH>(pre, kv_smem + 2 * nb * TILE, kv_smem + (2 * nb + 1) * TILE);
+    }
     __syncthreads();
   }
 #pragma unroll
@@ -741,14 +795,17 @@ using namespace pcv;
 extern "C" int pcv_attn_fwd(const void* q, const void* k, const void* v, int64_t ldq,
                             void* out, int64_t ldo, float* lse2,
                             int B, int T, int H, int head_dim, int causal,
-                            float dropout_rate, const uint16_t* drop_mask, void* stream) {
+                            float dropout_rate, const uint16_t* drop_mask, const int* doc_start,
+                            const int* doc_end, void* stream) {
   if (B <= 0 || T <= 0 || H <= 0) return PCV_EINVAL;
+  if ((doc_start != nullptr) != (doc_end != nullptr) || (doc_start && !causal)) return PCV_EINVAL;
   if (dropout_rate > 0.f && (!drop_mask || ((uintptr_t)drop_mask & 7))) return PCV_EINVAL;
   if ((ldq & 7) || (ldo & 7) || !pcv_aligned16(q) || !pcv_aligned16(k) || !pcv_aligned16(v)) return PCV_EALIGN;
   AttnArgs a{};
   a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.ldq = ldq;
   a.out = (bf16*)out; a.ldout = ldo; a.lse2 = lse2;
   a.B = B; a.T = T; a.H = H; a.scale = 1.f / sqrtf((float)head_dim);
+  a.dstart = doc_start; a.dend = doc_end;
   set_drop(a, dropout_rate, drop_mask);
   return dispatch<true>(a, head_dim, causal ? 1 : 0, a.drop, (hipStream_t)stream);
 }
@@ -758,8 +815,10 @@ extern "C" int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t
                             const float* lse2, float* delta_ws,
                             void* dq, void* dk, void* dv, int64_t lddq,
                             int B, int T, int H, int head_dim, int causal,
-                            float dropout_rate, const uint16_t* drop_mask, int delta_ready, void* stream) {
+                            float dropout_rate, const uint16_t* drop_mask, int delta_ready,
+                            const int* doc_start, const int* doc_end, void* stream) {
   if (B <= 0 || T <= 0 || H <= 0) return PCV_EINVAL;
+  if ((doc_start != nullptr) != (doc_end != nullptr) || (doc_start && !causal)) return PCV_EINVAL;
   if (dropout_rate > 0.f && (!drop_mask || ((uintptr_t)drop_mask & 7))) return PCV_EINVAL;
   if ((ldq & 7) || (ldo & 7) || (lddo & 7) || !pcv_aligned16(q) || !pcv_aligned16(k) || !pcv_aligned16(v) ||
       !pcv_aligned16(o) || !pcv_aligned16(dout))
@@ -770,6 +829,7 @@ extern "C" int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t
   a.dq = (bf16*)dq; a.dk = (bf16*)dk; a.dv = (bf16*)dv; a.lddq = lddq;
   a.lse2 = (float*)lse2; a.delta = delta_ws; a.delta_ready = delta_ready;
   a.B = B; a.T = T; a.H = H; a.scale = 1.f / sqrtf((float)head_dim);
+  a.dstart = doc_start; a.dend = doc_end;
   set_drop(a, dropout_rate, drop_mask);
   return dispatch<false>(a, head_dim, causal ? 1 : 0, a.drop, (hipStream_t)stream);
 }

@@ -51,6 +51,47 @@ __global__ void swiglu_fwd_kernel(const bf16* gu, int64_t ldgu, bf16* h, int64_t
   }
 }
 
+// Non-gated MLP activations (models/LM/transformer.py:70-97 MLP: silu; 138-165 MLPReluSquared:
+// relu(x)^2) on the fc1 output a [R][Fp] (pad columns written as 0).  kind 1 = silu, 2 = relu^2.
+__device__ __forceinline__ float mlp_act(float x, int kind) {
+  return kind == 1 ? silu(x) : (x > 0.f ? x * x : 0.f);
+}
+__device__ __forceinline__ float mlp_act_grad(float x, int kind) {
+  if (kind == 1) {
+    const float sg = 1.f / (1.f + __expf(-x));
+    return sg * (1.f + x * (1.f - sg));
+  }
+  return x > 0.f ? 2.f * x : 0.f;
+}
+__global__ void mlp_act_fwd_kernel(const bf16* a, int64_t lda, bf16* h, int64_t ldh, int64_t R, int F, int Fp,
+                                   int kind) {
+  const int64_t n8 = R * (Fp / 8);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / (Fp / 8);
+    const int c = (int)(i % (Fp / 8)) * 8;
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(a + row * lda + c);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(c + j < F ? mlp_act(bf2f(x[j]), kind) : 0.f);
+    *reinterpret_cast<bf16x8*>(h + row * ldh + c) = o;
+  }
+}
+// da = dh * act'(a) (may alias dh)
+__global__ void mlp_act_bwd_kernel(const bf16* dh, int64_t lddh, const bf16* a, int64_t lda, bf16* da, int64_t ldda,
+                                   int64_t R, int F, int Fp, int kind) {
+  const int64_t n8 = R * (Fp / 8);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / (Fp / 8);
+    const int c = (int)(i % (Fp / 8)) * 8;
+    const bf16x8 d = *reinterpret_cast<const bf16x8*>(dh + row * lddh + c);
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(a + row * lda + c);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(c + j < F ? bf2f(d[j]) * mlp_act_grad(bf2f(x[j]), kind) : 0.f);
+    *reinterpret_cast<bf16x8*>(da + row * ldda + c) = o;
+  }
+}
+
 __global__ void swiglu_bwd_kernel(const bf16* dh, int64_t lddh, const bf16* gu, int64_t ldgu, bf16* dgu,
                                   int64_t lddgu, int64_t R, int F, int Fp) {
   const int64_t n8 = R * (Fp / 8);
@@ -253,6 +294,26 @@ extern "C" int pcv_swiglu_bwd(const void* dh, int64_t lddh, const void* gu, int6
     return PCV_EINVAL;
   hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(R * (Fp / 8))), dim3(256), 0, (hipStream_t)stream,
                      (const bf16*)dh, lddh, (const bf16*)gu, ldgu, (bf16*)dgu, lddgu, R, F, Fp);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_mlp_act_fwd(const void* a, int64_t lda, void* h, int64_t ldh, int64_t R, int F, int Fp, int kind,
+                               void* stream) {
+  if (R <= 0 || F <= 0 || (Fp & 7) || Fp < F || (lda & 7) || (ldh & 7) || lda < Fp || ldh < Fp ||
+      (kind != 1 && kind != 2) || !pcv_aligned16(a) || !pcv_aligned16(h))
+    return PCV_EINVAL;
+  hipLaunchKernelGGL(mlp_act_fwd_kernel, dim3(grid_for(R * (Fp / 8))), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)a, lda, (bf16*)h, ldh, R, F, Fp, kind);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_mlp_act_bwd(const void* dh, int64_t lddh, const void* a, int64_t lda, void* da, int64_t ldda,
+                               int64_t R, int F, int Fp, int kind, void* stream) {
+  if (R <= 0 || F <= 0 || (Fp & 7) || Fp < F || (lda & 7) || (lddh & 7) || (ldda & 7) || lddh < Fp ||
+      lda < Fp || ldda < Fp || (kind != 1 && kind != 2))
+    return PCV_EINVAL;
+  hipLaunchKernelGGL(mlp_act_bwd_kernel, dim3(grid_for(R * (Fp / 8))), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)dh, lddh, (const bf16*)a, lda, (bf16*)da, ldda, R, F, Fp, kind);
   return pcv_launch_status();
 }
 

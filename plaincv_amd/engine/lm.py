@@ -15,6 +15,7 @@ clip factor on the device (train_lm.py:173-178) and runs the optimizer.
 from dataclasses import dataclass, field
 from typing import Any
 
+import numpy as np
 import torch
 
 from .. import kernels as K
@@ -58,16 +59,50 @@ def create_lm_state(cfg, model, variables, micro_batch, device, accum=1):
     return st
 
 
-def make_train_fns(use_doc_mask=False):
-    if use_doc_mask:
-        raise NotImplementedError("intra_doc_masking is SURVEY §8f-1 'next' (segment ids in the attention kernel)")
+def trim_last_token(doc_boundaries):
+    """train_lm.py:97-104: the last document loses the token dropped by inputs = ids[:, :-1]."""
+    trimmed = [int(x) for x in doc_boundaries]
+    if not trimmed:
+        return trimmed
+    trimmed[-1] -= 1
+    if trimmed[-1] <= 0:
+        trimmed.pop()
+    return trimmed
 
-    def compute_grads(state: LMTrainState, input_ids):
+
+def doc_bounds(docs_lengths, seq_len):
+    """Per-token document bounds for the intra-document causal mask (train_lm.py:107-131 with
+    data_prep_utils.intra_doc_causal_mask): row i's documents are trim_last_token(docs_lengths[i]),
+    which must sum to seq_len (ValueError otherwise, as the reference).  Returns (doc_start, doc_end)
+    int32 [B, seq_len]: token t sees keys k with doc_start[t] <= k <= t; doc_end is exclusive.
+    The block-diagonal causal [T, T] mask is never materialised -- the attention kernels read these."""
+    if docs_lengths is None:
+        raise ValueError("intra_doc_masking=True but docs_lengths not found in batch.")
+    B = len(docs_lengths)
+    ds = np.zeros((B, seq_len), dtype=np.int32)
+    de = np.zeros((B, seq_len), dtype=np.int32)
+    for i, boundaries in enumerate(docs_lengths):
+        bl = trim_last_token(boundaries)
+        if sum(bl) != seq_len:
+            raise ValueError(f"Sum(doc_boundaries)={sum(bl)} != seq_len={seq_len}.")
+        start = 0
+        for n in bl:
+            ds[i, start:start + n] = start
+            de[i, start:start + n] = start + n
+            start += n
+    return ds, de
+
+
+def make_train_fns(use_doc_mask=False):
+    """train_lm.py:189-313 (both the pmap and single-device variants: data parallelism is one
+    process per GPU here).  With use_doc_mask the step functions take the batch's docs_lengths."""
+
+    def compute_grads(state: LMTrainState, input_ids, docs_lengths=None):
         """One micro-step (train_lm.py:189-210).  On the last micro-step of an optimizer step the
         gradient all-reduce is overlapped with this backward (data_parallel.OverlappedReducer);
         apply_grads finishes it."""
         r = state.runner
-        r.set_batch(input_ids)
+        r.set_batch(input_ids, doc=doc_bounds(docs_lengths, r.T) if use_doc_mask else None)
         m = r.forward(need_grad=True)
         last = state.micro == state.accum - 1
         red = state.reducer if (last and state.reducer is not None and state.reducer.active) else None
@@ -78,9 +113,9 @@ def make_train_fns(use_doc_mask=False):
         state.loss_sum.add_(m)
         return m
 
-    def eval_step(state: LMTrainState, input_ids):
+    def eval_step(state: LMTrainState, input_ids, docs_lengths=None):
         r = state.runner
-        r.set_batch(input_ids)
+        r.set_batch(input_ids, doc=doc_bounds(docs_lengths, r.T) if use_doc_mask else None)
         m = r.forward(need_grad=False).clone()
         return dp.all_reduce_metrics(m)
 

@@ -29,9 +29,9 @@ SIGNATURES = {
     "pcv_gemm_desc_size": [],
     "pcv_gemm_grouped_plan": [P, I32, I32, P, P],
     "pcv_gemm_grouped_run": [P, I32, I32, I64, P],
-    "pcv_attn_fwd": [P, P, P, I64, P, I64, P, I32, I32, I32, I32, I32, F32, P, P],
+    "pcv_attn_fwd": [P, P, P, I64, P, I64, P, I32, I32, I32, I32, I32, F32, P, P, P, P],
     "pcv_attn_bwd": [P, P, P, I64, P, I64, P, I64, P, P, P, P, P, I64, I32, I32, I32, I32, I32,
-                     F32, P, I32, P],
+                     F32, P, I32, P, P, P],
     "pcv_attn_mask_words": [I32],
     "pcv_attn_drop_mask": [P, U32, U32, I32, I32, F32, P, P],
     "pcv_layernorm_fwd": [P, I64, P, P, P, I64, P, P, I64, I32, F32, P],
@@ -43,6 +43,8 @@ SIGNATURES = {
     "pcv_rope": [P, I64, I64, I32, I32, I32, P, P, I32, P],
     "pcv_swiglu_fwd": [P, I64, P, I64, I64, I32, I32, P],
     "pcv_swiglu_bwd": [P, I64, P, I64, P, I64, I64, I32, I32, P],
+    "pcv_mlp_act_fwd": [P, I64, P, I64, I64, I32, I32, I32, P],
+    "pcv_mlp_act_bwd": [P, I64, P, I64, P, I64, I64, I32, I32, I32, P],
     "pcv_dropout_bwd_cast": [P, I64, P, I64, I64, I32, F32, P, U32, P],
     "pcv_cast_f32_bf16": [P, P, I64, P],
     "pcv_colsum": [P, I64, I64, I32, I32, P, P],

@@ -242,31 +242,48 @@ def attn_drop_mask(seed, site, T, drop_rate, mask, layers=1, site_stride=0):
              float(drop_rate), ptr(mask), stream_ptr())
 
 
-def attn_fwd(qkv, out, lse2, B, T, H, Dh, causal, drop_rate=0.0, mask=None, q_off=0, k_off=None, v_off=None):
-    """Flash attention forward on packed qkv [B*T, ld] (q|k|v column blocks); `mask` = attn_drop_mask bits."""
+def _doc_arrays(doc, B, T, causal):
+    """doc = (doc_start, doc_end) int32 [B*T] (intra-document causal mask) or None."""
+    if doc is None:
+        return None, None
+    ds, de = doc
+    _chk(causal, "document mask needs causal attention")
+    _chk(ds.dtype == torch.int32 and de.dtype == torch.int32 and ds.numel() == B * T and de.numel() == B * T
+         and ds.is_contiguous() and de.is_contiguous(), "doc_start/doc_end: contiguous int32 [B*T]")
+    return ds, de
+
+
+def attn_fwd(qkv, out, lse2, B, T, H, Dh, causal, drop_rate=0.0, mask=None, q_off=0, k_off=None, v_off=None,
+             doc=None):
+    """Flash attention forward on packed qkv [B*T, ld] (q|k|v column blocks); `mask` = attn_drop_mask bits;
+    doc = (doc_start, doc_end) per-token document bounds for the intra-document causal mask."""
     D = H * Dh
     k_off = D if k_off is None else k_off
     v_off = 2 * D if v_off is None else v_off
     _chk(qkv.dtype == BF16 and out.dtype == BF16 and lse2.dtype == F32, "attn dtypes")
     _chk(qkv.shape[0] == B * T and out.shape[0] == B * T and lse2.numel() >= B * H * T, "attn shapes")
     _dev(qkv, out, lse2)
+    ds, de = _doc_arrays(doc, B, T, causal)
     base = qkv.data_ptr()
     es = qkv.element_size()
     hip.call("pcv_attn_fwd", base + q_off * es, base + k_off * es, base + v_off * es, _ld(qkv),
              ptr(out), _ld(out), ptr(lse2), B, T, H, Dh, int(causal), float(drop_rate),
-             ptr(mask), stream_ptr())
+             ptr(mask), ptr(ds), ptr(de), stream_ptr())
 
 
-def attn_bwd(qkv, o, dout, lse2, delta_ws, dqkv, B, T, H, Dh, causal, drop_rate=0.0, mask=None, delta_ready=False):
+def attn_bwd(qkv, o, dout, lse2, delta_ws, dqkv, B, T, H, Dh, causal, drop_rate=0.0, mask=None, delta_ready=False,
+             doc=None):
     D = H * Dh
     _chk(qkv.dtype == BF16 and dqkv.dtype == BF16 and dout.dtype == BF16 and o.dtype == BF16, "attn bwd dtypes")
     _chk(dqkv.shape[0] == B * T and dqkv.shape[1] >= 3 * D and delta_ws.numel() >= B * H * T, "attn bwd shapes")
     _dev(qkv, o, dout, lse2, delta_ws, dqkv)
+    ds, de = _doc_arrays(doc, B, T, causal)
     base, es = qkv.data_ptr(), qkv.element_size()
     dbase = dqkv.data_ptr()
     hip.call("pcv_attn_bwd", base, base + D * es, base + 2 * D * es, _ld(qkv), ptr(o), _ld(o), ptr(dout),
              _ld(dout), ptr(lse2), ptr(delta_ws), dbase, dbase + D * es, dbase + 2 * D * es, _ld(dqkv),
-             B, T, H, Dh, int(causal), float(drop_rate), ptr(mask), int(delta_ready), stream_ptr())
+             B, T, H, Dh, int(causal), float(drop_rate), ptr(mask), int(delta_ready), ptr(ds), ptr(de),
+             stream_ptr())
 
 
 def layernorm_fwd(x, scale, bias, y, mean, rstd, eps=1e-6):
@@ -325,6 +342,26 @@ def rope(qk, T, Dh, cos_tab, sin_tab, backward=False, ncols=None):
     _dev(qk, cos_tab, sin_tab)
     hip.call("pcv_rope", ptr(qk), _ld(qk), R, ncols, T, Dh, ptr(cos_tab), ptr(sin_tab), int(backward),
              stream_ptr())
+
+
+MLP_ACT = {"mlp": 1, "mlp_relu_sq": 2}
+
+
+def mlp_act_fwd(a, h, F, kind):
+    """h[:, :F] = act(a) (silu for 'mlp', relu^2 for 'mlp_relu_sq'); a/h padded to Fp columns."""
+    Fp = (F + 7) // 8 * 8
+    _chk(a.dtype == BF16 and h.dtype == BF16 and a.shape[0] == h.shape[0], "mlp_act_fwd")
+    _dev(a, h)
+    hip.call("pcv_mlp_act_fwd", ptr(a), _ld(a), ptr(h), _ld(h), a.shape[0], int(F), Fp, MLP_ACT[kind], stream_ptr())
+
+
+def mlp_act_bwd(dh, a, da, F, kind):
+    Fp = (F + 7) // 8 * 8
+    _chk(dh.dtype == BF16 and a.dtype == BF16 and da.dtype == BF16 and dh.shape[0] == a.shape[0] == da.shape[0],
+         "mlp_act_bwd")
+    _dev(dh, a, da)
+    hip.call("pcv_mlp_act_bwd", ptr(dh), _ld(dh), ptr(a), _ld(a), ptr(da), _ld(da), a.shape[0], int(F), Fp,
+             MLP_ACT[kind], stream_ptr())
 
 
 def swiglu_fwd(gu, h, F=None):

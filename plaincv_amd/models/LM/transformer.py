@@ -60,8 +60,8 @@ class Transformer:
     def __init__(self, cfg: ModelConfig, normtype="rmsnorm"):
         if normtype != "rmsnorm":
             raise NotImplementedError("only the rmsnorm Block is on the hot path")
-        if cfg.mlp != "glu":
-            raise NotImplementedError(f"mlp={cfg.mlp!r}: only the GLU (SwiGLU) block is on the hot path")
+        if cfg.mlp not in ("glu", "mlp", "mlp_relu_sq"):
+            raise ValueError(f"Unknown mlp type: {cfg.mlp}")   # transformer.py:331-332
         if cfg.dim % cfg.n_heads:
             raise ValueError("dim must be divisible by n_heads")
         self.cfg = cfg
@@ -77,8 +77,11 @@ class Transformer:
             L.add(f"{p}/attn/w_qkv/kernel", (d, 3 * d))
             L.add(f"{p}/attn/w_out/kernel", (d, d))
             L.add(f"{p}/mlp_norm/RMSNorm_0/scale", (d,))
-            L.add_fused(f"{p}/mlp/gate_up", [f"{p}/mlp/fc_gate/kernel", f"{p}/mlp/fc_up/kernel"], (d, F),
-                        pad_each=True)
+            if c.mlp == "glu":
+                L.add_fused(f"{p}/mlp/gate_up", [f"{p}/mlp/fc_gate/kernel", f"{p}/mlp/fc_up/kernel"], (d, F),
+                            pad_each=True)
+            else:   # MLP (silu) / MLPReluSquared: fc1 -> act -> fc2 (transformer.py:70-97, 138-165)
+                L.add(f"{p}/mlp/fc1/kernel", (d, F))
             L.add(f"{p}/mlp/fc2/kernel", (F, d))
         L.add("out_norm/RMSNorm_0/scale", (d,))
         if not c.tie_embeddings:
@@ -150,8 +153,10 @@ class LMRunner:
         self.qkv = [e(R, 3 * d) for _ in range(L)]
         self.o = [e(R, d) for _ in range(L)]
         self.lse = [e(b * self.H * T, dt=f32) for _ in range(L)]
-        # [gate | up] halves of Fp columns each (pads are zero after swiglu)
-        self.gu = [e(R, 2 * self.Fp) for _ in range(L)]
+        # glu: [gate | up] halves of Fp columns each (pads are zero after swiglu); else the fc1 output
+        self.glu = c.mlp == "glu"
+        nmlp = 2 * self.Fp if self.glu else self.Fp
+        self.gu = [e(R, nmlp) for _ in range(L)]
         self.hm = [e(R, self.Fp)[:, : self.F] for _ in range(L)]
         self.yf = e(R, d)
         self.rf = e(R, dt=f32)
@@ -163,7 +168,7 @@ class LMRunner:
         self.dx = e(R, d)
         self.dy = e(R, d)
         self.dh = e(R, self.Fp)[:, : self.F]
-        self.dgu = e(R, 2 * self.Fp)
+        self.dgu = e(R, nmlp)
         self.do = e(R, d)
         self.dqkv = e(R, 3 * d)
         self.delta = e(b * self.H * T, dt=f32)
@@ -171,6 +176,7 @@ class LMRunner:
         self.cos = cos[:T].contiguous().to(dev)
         self.sin = sin[:T].contiguous().to(dev)
         self.grad_scale = 1.0 / R if grad_scale is None else grad_scale
+        self.doc = None
         self._views()
         self._transposed_weights(dev)
         # flat-gradient offsets above which the backward has finished (overlapped DP reduction)
@@ -190,8 +196,9 @@ class LMRunner:
                 "Wqkv": W[f"{p}/attn/w_qkv/kernel"], "gWqkv": G[f"{p}/attn/w_qkv/kernel"],
                 "Wo": W[f"{p}/attn/w_out/kernel"], "gWo": G[f"{p}/attn/w_out/kernel"],
                 "s1": P[f"{p}/mlp_norm/RMSNorm_0/scale"], "gs1": G[f"{p}/mlp_norm/RMSNorm_0/scale"],
-                "Wgu": s.group_view(s.shadow, f"{p}/mlp/gate_up"),
-                "gWgu": s.group_view(s.grad_flat, f"{p}/mlp/gate_up"),
+                # first MLP matrix: the fused [gate | up] operand (glu) or fc1
+                "Wgu": s.group_view(s.shadow, f"{p}/mlp/gate_up") if self.glu else W[f"{p}/mlp/fc1/kernel"],
+                "gWgu": s.group_view(s.grad_flat, f"{p}/mlp/gate_up") if self.glu else G[f"{p}/mlp/fc1/kernel"],
                 "W2": W[f"{p}/mlp/fc2/kernel"], "gW2": G[f"{p}/mlp/fc2/kernel"],
             })
         self.Wemb, self.gWemb = W["embed_tokens/embedding"], G["embed_tokens/embedding"]
@@ -226,13 +233,28 @@ class LMRunner:
             self._tr()
             self._wt_version = self.s.version
 
-    def set_batch(self, input_ids):
-        """input_ids (b, T+1) int on the GPU -> inputs/labels (train_lm.py:141-142)."""
+    def set_batch(self, input_ids, doc=None):
+        """input_ids (b, T+1) int on the GPU -> inputs/labels (train_lm.py:141-142).  doc = per-token
+        (doc_start, doc_end) int32 [b, T] for the intra-document causal mask (train_lm.py:107-131,
+        engine.lm.doc_bounds), or None for plain causal attention."""
         b, T = self.b, self.T
         if tuple(input_ids.shape) != (b, T + 1):
             raise ValueError(f"Expected input_ids of shape {(b, T + 1)}, got {tuple(input_ids.shape)}")
         self.inputs.view(b, T).copy_(input_ids[:, :-1])
         self.labels.view(b, T).copy_(input_ids[:, 1:])
+        if doc is None:
+            self.doc = None
+        else:
+            if not hasattr(self, "_doc_bufs"):
+                dev = self.inputs.device
+                self._doc_bufs = (torch.zeros(b * T, dtype=torch.int32, device=dev),
+                                  torch.zeros(b * T, dtype=torch.int32, device=dev))
+            for buf, src in zip(self._doc_bufs, doc):
+                src = torch.as_tensor(src, dtype=torch.int32)
+                if tuple(src.shape) != (b, T):
+                    raise ValueError(f"doc bounds must be ({b}, {T}), got {tuple(src.shape)}")
+                buf.view(b, T).copy_(src, non_blocking=True)
+            self.doc = self._doc_bufs
 
     def forward(self, need_grad=True):
         c = self.c
@@ -245,11 +267,15 @@ class LMRunner:
             K.rmsnorm_fwd(self.x[i], w["s0"], self.y0[i], self.r0[i], eps)
             K.gemm(self.y0[i], w["WqkvT"], self.qkv[i], tb=True)
             K.rope(self.qkv[i], T, Dh, self.cos, self.sin, ncols=2 * d)
-            K.attn_fwd(self.qkv[i], self.o[i], self.lse[i], b, T, H, Dh, causal=True)
+            K.attn_fwd(self.qkv[i], self.o[i], self.lse[i], b, T, H, Dh, causal=True, doc=self.doc)
             K.gemm(self.o[i], w["WoT"], self.x1[i], tb=True, res=self.x[i])
             K.rmsnorm_fwd(self.x1[i], w["s1"], self.y1[i], self.r1[i], eps)
-            K.gemm(self.y1[i], w["WguT"], self.gu[i], tb=True)
-            K.swiglu_fwd(self.gu[i], self.hm[i], F=self.F)
+            if self.glu:
+                K.gemm(self.y1[i], w["WguT"], self.gu[i], tb=True)
+                K.swiglu_fwd(self.gu[i], self.hm[i], F=self.F)
+            else:
+                K.gemm(self.y1[i], w["WguT"], self.gu[i][:, : self.F], tb=True)
+                K.mlp_act_fwd(self.gu[i], self.hm[i], self.F, c.mlp)
             K.gemm(self.hm[i], w["W2T"], self.x[i + 1], tb=True, res=self.x1[i])
         K.rmsnorm_fwd(self.x[-1], self.sf, self.yf, self.rf, eps)
         if c.tie_embeddings:
@@ -281,13 +307,19 @@ class LMRunner:
             w = self.w[i]
             K.gemm(self.hm[i], self.dx, w["gW2"], ta=True, beta=1.0)
             K.gemm(self.dx, w["W2"], self.dh, tb=True)
-            K.swiglu_bwd(self.dh, self.gu[i], self.dgu, F=self.F)
-            K.gemm(self.y1[i], self.dgu, w["gWgu"], ta=True, beta=1.0)
-            K.gemm(self.dgu, w["Wgu"], self.dy, tb=True)
+            if self.glu:
+                K.swiglu_bwd(self.dh, self.gu[i], self.dgu, F=self.F)
+                dgu = self.dgu
+            else:
+                K.mlp_act_bwd(self.dh, self.gu[i], self.dgu, self.F, c.mlp)
+                dgu = self.dgu[:, : self.F]
+            K.gemm(self.y1[i], dgu, w["gWgu"], ta=True, beta=1.0)
+            K.gemm(dgu, w["Wgu"], self.dy, tb=True)
             K.rmsnorm_bwd(self.dy, self.x1[i], w["s1"], self.r1[i], self.dx, self.dx, w["gs1"])
             K.gemm(self.o[i], self.dx, w["gWo"], ta=True, beta=1.0)
             K.gemm(self.dx, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H))   # + delta
             K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, self.dqkv, b, T, H, Dh, causal=True,
+                       doc=self.doc,
                        delta_ready=True)
             K.rope(self.dqkv, T, Dh, self.cos, self.sin, backward=True, ncols=2 * d)
             K.gemm(self.y0[i], self.dqkv, w["gWqkv"], ta=True, beta=1.0)

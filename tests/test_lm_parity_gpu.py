@@ -8,23 +8,25 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _tiny(vocab=512, d=128, L=2, H=2, T=64, tie=False, expand="8/3"):
+def _tiny(vocab=512, d=128, L=2, H=2, T=64, tie=False, expand="8/3", mlp="glu"):
     from utils import Config
     return Config(model="transformer", vocab_size=vocab, d_model=d, expand=expand, n_layers=L, n_heads=H,
-                  mlp_class="glu", seq_len=T, tie_embeddings=tie, rope_theta=500000.0, dtype="bfloat16", seed=0)
+                  mlp_class=mlp, seq_len=T, tie_embeddings=tie, rope_theta=500000.0, dtype="bfloat16", seed=0)
 
 
 def _rel(a, b, floor=1e-3):
     return (a - b).norm().item() / max(b.norm().item(), floor)
 
 
-@pytest.mark.parametrize("tie,b,T", [(False, 2, 64), (True, 2, 64), (False, 1, 200)])
-def test_lm_grads_match_oracle(dev, tie, b, T):
+@pytest.mark.parametrize("tie,b,T,mlp", [(False, 2, 64, "glu"), (True, 2, 64, "glu"), (False, 1, 200, "glu"),
+                                         (False, 2, 64, "mlp"), (False, 2, 100, "mlp_relu_sq")])
+def test_lm_grads_match_oracle(dev, tie, b, T, mlp):
+    """incl. the non-gated MLP variants (MLP silu, MLPReluSquared: transformer.py:70-97, 138-165)"""
     from oracle.engine import lm_loss_and_acc, value_and_grad
     from oracle.lm import model_config_from_cfg, transformer_apply
     from plaincv_amd.models.LM.constructor import construct_model
     from plaincv_amd.params import ParamStore
-    cfg = _tiny(tie=tie, T=T)
+    cfg = _tiny(tie=tie, T=T, mlp=mlp)
     model, mc, variables = construct_model(cfg)
     init = variables["params"]
     store = ParamStore(model.layout(), dev)
