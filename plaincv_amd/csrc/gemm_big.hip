@@ -38,12 +38,18 @@ struct BigArgs {
   float alpha, res_scale;
 };
 
-constexpr int GB_T = 256;                 // tile
-constexpr int GB_IMG = GB_T * 64;         // one operand image of a 32-k step: 256 rows x 64 B
-constexpr int GB_SLOT = 2 * GB_IMG;       // A + B
+constexpr int GB_T = 256;                 // tile rows (M); the N width BN is a template parameter
+constexpr int GB_IMG = GB_T * 64;         // the A image of a 32-k step: 256 rows x 64 B
 constexpr int GB_SLOTS = 4;
-constexpr int GB_CLD = GB_T * 2 + 16;     // epilogue staging row (bytes): +16 B breaks 4-row bank aliasing
-constexpr int GB_LDS = (GB_SLOTS * GB_SLOT > GB_T * GB_CLD) ? GB_SLOTS * GB_SLOT : GB_T * GB_CLD;
+template <int BN>
+struct GbCfg {
+  static constexpr int SLOT = GB_IMG + BN * 64;          // A + B images of one step
+  static constexpr int CLD = BN * 2 + 16;                // epilogue staging row (bytes): +16 B breaks 4-row bank aliasing
+  static constexpr int LDS = (GB_SLOTS * SLOT > GB_T * CLD) ? GB_SLOTS * SLOT : GB_T * CLD;
+  static constexpr int WN = BN / 4;                      // per-wave columns (64 | 48)
+  static constexpr int NJ = WN / 16;                     // 16-col blocks per wave
+  static constexpr int BPIECES = BN / 16;                // 1-KiB B pieces per step (16 | 12)
+};
 
 typedef __attribute__((address_space(3))) void gb_lds_void;
 
@@ -53,14 +59,22 @@ __device__ __forceinline__ void gb_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// retire this wave's loads of step s+1: at most 4 * min(2, remaining) DMA ops may stay in flight
-__device__ __forceinline__ void gb_wait_next(int steps_after) {
-  if (steps_after >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (steps_after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+// retire this wave's loads of step s+1: at most L * min(2, remaining) DMA ops (L = this wave's
+// loads per step, 3 or 4) may stay in flight
+template <int L>
+__device__ __forceinline__ void gb_wait_n(int steps_after) {
+  if (steps_after >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * L) : "memory");
+  else if (steps_after == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(L) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
+__device__ __forceinline__ void gb_wait_next(int steps_after, bool three) {
+  if (three) gb_wait_n<3>(steps_after);
+  else gb_wait_n<4>(steps_after);
+}
 
+template <int BN>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
+  using C = GbCfg<BN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave >> 2, wc = wave & 3;
@@ -73,77 +87,89 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
   const int first_m = (wgid / per_group) * 8;
   const int gsz = min(g.tiles_m - first_m, 8);
   const int tm = first_m + (wgid % per_group) % gsz, tn = (wgid % per_group) / gsz;
-  const int m0 = tm * GB_T, n0 = tn * GB_T;
+  const int m0 = tm * GB_T, n0 = tn * BN;
 
-  // DMA sources: this wave fills 1-KiB pieces (wave*2 + i) of each image = rows 16*(wave*2+i) ..
+  // DMA sources: A pieces (16 per step) two per wave; B pieces (BN/16 per step) two per wave, or for
+  // BN = 192 two for waves 0-3 and one for waves 4-7.  Piece p = image rows 16p .. 16p+15;
   // lane -> row (lane >> 2), stored chunk (lane & 3) <- source k-chunk (lane & 3) ^ 2*((row >> 3) & 1)
+  constexpr bool B3 = C::BPIECES == 12;
+  const int nbp = (!B3 || wave < 4) ? 2 : 1;
+  const bool three = nbp == 1;   // this wave's loads per step: 2 A + nbp B
+  int bpiece[2];
+  if (!B3) { bpiece[0] = wave * 2; bpiece[1] = wave * 2 + 1; }
+  else { bpiece[0] = wave < 4 ? wave * 2 : 8 + (wave - 4); bpiece[1] = wave < 4 ? wave * 2 + 1 : bpiece[0]; }
   const bf16* srcA[2];
   const bf16* srcB[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = (wave * 2 + i) * 16 + (lane >> 2);
     const int kc = (lane & 3) ^ (((row >> 3) & 1) << 1);
-    const int ra = min(m0 + row, g.M - 1), rb = min(n0 + row, g.N - 1);   // clamped rows feed only masked outputs
+    const int ra = min(m0 + row, g.M - 1);   // clamped rows feed only masked outputs
     srcA[i] = g.A + (int64_t)ra * g.lda + kc * 8;
-    srcB[i] = g.B + (int64_t)rb * g.ldb + kc * 8;
+    const int rowb = bpiece[i] * 16 + (lane >> 2);
+    const int kcb = (lane & 3) ^ (((rowb >> 3) & 1) << 1);
+    const int rb = min(n0 + rowb, g.N - 1);
+    srcB[i] = g.B + (int64_t)rb * g.ldb + kcb * 8;
   }
   const int nsteps = g.K / 32;
   auto issue = [&](int s) {
-    char* slot = smem + (s & 3) * GB_SLOT;
+    char* slot = smem + (s & 3) * C::SLOT;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(srcA[i] + s * 32), (gb_lds_void*)(slot + (wave * 2 + i) * 1024),
                                        16, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(srcB[i] + s * 32),
-                                       (gb_lds_void*)(slot + GB_IMG + (wave * 2 + i) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(srcB[0] + s * 32),
+                                     (gb_lds_void*)(slot + GB_IMG + bpiece[0] * 1024), 16, 0, 0);
+    if (nbp == 2)
+      __builtin_amdgcn_global_load_lds((const void*)(srcB[1] + s * 32),
+                                       (gb_lds_void*)(slot + GB_IMG + bpiece[1] * 1024), 16, 0, 0);
   };
 
   // fragment offsets within an image (the swizzle depends only on lane & 15)
   const int fsw = (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) << 4);
-  int offA[8], offB[4];
+  constexpr int NJ = C::NJ;
+  int offA[8], offB[NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i) offA[i] = (wr * 128 + i * 16 + (lane & 15)) * 64 + fsw;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) offB[j] = GB_IMG + (wc * 64 + j * 16 + (lane & 15)) * 64 + fsw;
+  for (int j = 0; j < NJ; ++j) offB[j] = GB_IMG + (wc * C::WN + j * 16 + (lane & 15)) * 64 + fsw;
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto mfmas = [&](const bf16x8 (&a)[8], const bf16x8 (&b)[4]) {
+  auto mfmas = [&](const bf16x8 (&a)[8], const bf16x8 (&b)[NJ]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
   };
 
   if (nsteps > 0) {
     for (int s = 0; s < 3 && s < nsteps; ++s) issue(s);
-    gb_wait_next(min(2, nsteps - 1));   // step 0 retired (loads of steps 1, 2 may fly)
+    gb_wait_next(min(2, nsteps - 1), three);   // step 0 retired (loads of steps 1, 2 may fly)
     gb_barrier();
     if (wr == 1) gb_barrier();          // stagger: group 1 runs one barrier behind
     for (int s = 0; s < nsteps; ++s) {
       if (s + 3 < nsteps) issue(s + 3);
-      const char* slot = smem + (s & 3) * GB_SLOT;
-      bf16x8 a[8], b[4];
+      const char* slot = smem + (s & 3) * C::SLOT;
+      bf16x8 a[8], b[NJ];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(slot + offB[j]);
+      for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(slot + offB[j]);
 #pragma unroll
       for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(slot + offA[i]);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       const int after = min(nsteps - 1, s + 3) - (s + 1);   // steps issued after step s+1
-      if (wr == 1 && s + 1 < nsteps) gb_wait_next(after);
+      if (wr == 1 && s + 1 < nsteps) gb_wait_next(after, three);
       gb_barrier();
       __builtin_amdgcn_s_setprio(1);
       mfmas(a, b);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
-      if (wr == 0 && s + 1 < nsteps) gb_wait_next(after);
+      if (wr == 0 && s + 1 < nsteps) gb_wait_next(after, three);
       gb_barrier();
     }
     if (wr == 0) gb_barrier();          // equal barrier counts for both groups
@@ -160,9 +186,11 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
       const bf16* base = op ? g.B : g.A;
       const int64_t ld = op ? g.ldb : g.lda;
       const int r0 = op ? n0 : m0, rows = op ? g.N : g.M;
+      const int nrows = op ? BN : GB_T;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int idx = tid + h * 512, row = idx >> 2, kc = idx & 3;
+        if (row >= nrows) continue;
         bf16x8 v;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -173,9 +201,9 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
       }
     }
     __syncthreads();
-    bf16x8 a[8], b[4];
+    bf16x8 a[8], b[NJ];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(smem + offB[j]);
+    for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(smem + offB[j]);
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(smem + offA[i]);
     mfmas(a, b);
@@ -186,21 +214,22 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = wr * 128 + i * 16 + (lane >> 4) * 4 + r, col = wc * 64 + j * 16 + (lane & 15);
-        *reinterpret_cast<bf16*>(smem + row * GB_CLD + col * 2) = f2bf(g.alpha * acc[i][j][r]);
+        const int row = wr * 128 + i * 16 + (lane >> 4) * 4 + r, col = wc * C::WN + j * 16 + (lane & 15);
+        *reinterpret_cast<bf16*>(smem + row * C::CLD + col * 2) = f2bf(g.alpha * acc[i][j][r]);
       }
   __syncthreads();
   const bool vec = ((g.ldc & 7) == 0) && ((uintptr_t)g.C & 15) == 0 &&
                    (!g.res || (((g.ldr & 7) == 0) && ((uintptr_t)g.res & 15) == 0));
+  constexpr int CPR = BN / 8;   // 8-column chunks per row
 #pragma unroll 4
-  for (int e = tid; e < GB_T * 32; e += 512) {
-    const int row = e >> 5, cc = (e & 31) * 8;
+  for (int e = tid; e < GB_T * CPR; e += 512) {
+    const int row = e / CPR, cc = (e % CPR) * 8;
     const int gr = m0 + row, gc = n0 + cc;
     if (gr >= g.M || gc >= g.N) continue;
-    bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + row * GB_CLD + cc * 2);
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + row * C::CLD + cc * 2);
     bf16* dst = g.C + (int64_t)gr * g.ldc + gc;
     if (vec && gc + 8 <= g.N) {
       if (g.res) {
@@ -236,14 +265,38 @@ static bool big_shape_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t
   return !((lda & 7) || (ldb & 7) || !pcv_aligned16(A) || !pcv_aligned16(B));
 }
 
+static int big_bn(int64_t M, int64_t N) {
+  // N width per tile (one 128-KiB workgroup per CU, 256 CUs): 256 when that grid has >= 512 tiles
+  // or whole rounds of 256; else 192 when N % 192 == 0 gives whole rounds (N = 768: the LM's
+  // d-wide products, 256 tiles instead of 192); 0 = leave it to the 128x128 family
+  const int64_t tm = (M + GB_T - 1) / GB_T;
+  const int64_t t256 = tm * ((N + 255) / 256);
+  if (t256 >= 512) return 256;
+  if (N % 192 == 0) {
+    const int64_t t192 = tm * (N / 192);
+    if (t192 >= 256 && t192 % 256 == 0) return 192;
+  }
+  if (t256 >= 256 && t256 % 256 == 0) return 256;
+  return 0;
+}
+
 // Dispatch test used by pcv_gemm_bf16 (which falls back to the 128x128 family otherwise): both
-// operands K-contiguous with 16-B aligned rows, bf16 output, and enough 256x256 tiles to fill
-// every CU twice (smaller grids leave CUs idle at one 128-KiB workgroup per CU).
+// operands K-contiguous with 16-B aligned rows, bf16 output, and a grid that fills the chip.
 extern "C" int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
                                int64_t ldb) {
   if (!g_big_enabled || !big_shape_ok(M, N, K, A, lda, B, ldb)) return 0;
-  const int64_t tiles = ((M + GB_T - 1) / GB_T) * ((N + GB_T - 1) / GB_T);
-  return tiles >= 512 ? 1 : 0;
+  return big_bn(M, N) ? 1 : 0;
+}
+
+template <int BN>
+static void launch_big(const BigArgs& g, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_big_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              GbCfg<BN>::LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(gemm_big_kernel<BN>, dim3(g.tiles_m * g.tiles_n), dim3(512), GbCfg<BN>::LDS, s, g);
 }
 
 extern "C" int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
@@ -254,14 +307,11 @@ extern "C" int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, in
   g.A = (const bf16*)A; g.B = (const bf16*)B; g.C = (bf16*)C; g.res = (const bf16*)res;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldr = ldr;
   g.M = (int)M; g.N = (int)N; g.K = (int)K;
-  g.tiles_m = (int)((M + GB_T - 1) / GB_T);
-  g.tiles_n = (int)((N + GB_T - 1) / GB_T);
   g.alpha = alpha; g.res_scale = res_scale;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS);
-    attr = true;
-  }
-  hipLaunchKernelGGL(gemm_big_kernel, dim3(g.tiles_m * g.tiles_n), dim3(512), GB_LDS, (hipStream_t)stream, g);
+  const int bn = big_bn(M, N) == 192 ? 192 : 256;
+  g.tiles_m = (int)((M + GB_T - 1) / GB_T);
+  g.tiles_n = (int)((N + bn - 1) / bn);
+  if (bn == 192) launch_big<192>(g, (hipStream_t)stream);
+  else launch_big<256>(g, (hipStream_t)stream);
   return pcv_launch_status();
 }

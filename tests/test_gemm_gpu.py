@@ -82,9 +82,10 @@ def test_gemm_batched(dev):
 
 
 @pytest.mark.parametrize("M,N,K,res", [(16384, 50257, 768, False), (8192, 4096, 1000, True), (16384, 2304, 128, False),
-                                       (6000, 5472, 2736, True), (4100, 8200, 200, False)])
+                                       (6000, 5472, 2736, True), (4100, 8200, 200, False),
+                                       (16384, 768, 2304, True), (16384, 768, 4100, False), (16384, 1024, 1024, True)])
 def test_gemm_big_kernel(dev, M, N, K, res):
-    """256x256 8-wave ping-pong kernel (gemm_big.hip) through pcv_gemm_bf16's dispatch (both operands
+    """256x256 / 256x192 8-wave ping-pong kernel (gemm_big.hip) through pcv_gemm_bf16's dispatch (both operands
     K-contiguous, bf16 out, >= 512 tiles): ragged M/N (clamped DMA rows), ragged K (register tail),
     padded row strides, residual epilogue; and the same call with the big path disabled."""
     from plaincv_amd import hip

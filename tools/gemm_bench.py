@@ -34,7 +34,8 @@ SHAPES = [("lm_head fwd", 16384, 50304, 768, "fwd"), ("qkv fwd", 16384, 2304, 76
           ("gate|up wgrad", 768, 4096, 16384, "wgrad"), ("qkv wgrad", 768, 2304, 16384, "wgrad"),
           # 420M (d 1024, F 2730 -> gate|up 2 x 2736, V 50280, 16384 rows)
           ("420M lm_head fwd", 16384, 50280, 1024, "fwd"), ("420M qkv fwd", 16384, 3072, 1024, "fwd"),
-          ("420M gate|up fwd", 16384, 5472, 1024, "fwd")]
+          ("420M gate|up fwd", 16384, 5472, 1024, "fwd"), ("qkv dgrad", 16384, 768, 2304, "dgrad"),
+          ("420M out fwd", 16384, 1024, 1024, "fwd"), ("420M gate|up dgrad", 16384, 1024, 5472, "dgrad")]
 
 FLT = sys.argv[1] if len(sys.argv) > 1 else ""
 REF = "--no-ref" not in sys.argv
