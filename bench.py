@@ -344,6 +344,7 @@ def bench_lm(args):
 def lm_roofline(st):
     """Largest MFMA-bound kernel of the LM step: the lm_head GEMM (logits = y . W_head,
     M = micro_batch*T, N = vocab, K = d_model), timed live with HIP events."""
+    from plaincv_amd import hip
     from plaincv_amd import kernels as K
     r = st.runner
     M, Kd = r.yf.shape
@@ -351,7 +352,10 @@ def lm_roofline(st):
     dt = timed_kernel(lambda: K.gemm(r.yf, r.WhT, r.logits, tb=True), iters=10)
     flops = 2.0 * M * N * Kd
     achieved = flops / dt / 1e12
-    return {"kernel": f"gemm_bf16_kernel<true,true,4,4> (lm_head fwd on the K-contiguous weight copy, "
+    lib = hip.load()
+    big = lib.pcv_gemm_big_ok(M, N, Kd, hip.ptr(r.yf), r.yf.stride(0), hip.ptr(r.WhT), r.WhT.stride(0))
+    name = "gemm_big_kernel<256>" if big else "gemm_bf16_kernel<true,true,4,4>"
+    return {"kernel": f"{name} (lm_head fwd on the K-contiguous weight copy, "
                       f"M={M} N={N} K={Kd})", "bound": "mfma",
             "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None, "launch_us": round(dt * 1e6, 2),

@@ -57,6 +57,14 @@ int pcv_gemm_big_enable(int on);
 int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb);
 int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                  int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale, void* stream);
+/* Weight-gradient form of the same kernel: C[M,N] (fp32) += alpha * A[K,M]^T . B[K,N] with A and B
+ * K-major (M-/N-contiguous rows), K split over the grid and added with fp32 atomics (K % 32 == 0).
+ * pcv_gemm_bf16 dispatches trans_a, !trans_b, fp32-out, beta == 1 products without epilogue here.
+ * Replaces the kernel cotangents X^T dY of the LM's flax Dense layers (transformer.py:194-201,
+ * 246-253, 110-134, 393-405 VJPs). */
+int pcv_gemm_big_wgrad_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb);
+int pcv_gemm_big_wgrad(const void* A, const void* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                       int64_t ldb, int64_t ldc, float alpha, void* stream);
 
 /* GEMM + LayerNorm over each complete output row (N <= 128, N % 8 == 0; ViT residual stream).
  * ln_mode 1: C = x1 = alpha*op(A)op(B) + bias (+dropout) + res (fp32); ln_y = bf16 LN(x1),

@@ -24,6 +24,10 @@ extern "C" int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, i
 extern "C" int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                             int64_t ldb, int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale,
                             void* stream);
+extern "C" int pcv_gemm_big_wgrad_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                                     int64_t ldb);
+extern "C" int pcv_gemm_big_wgrad(const void* A, const void* B, float* C, int64_t M, int64_t N, int64_t K,
+                                  int64_t lda, int64_t ldb, int64_t ldc, float alpha, void* stream);
 
 #include <vector>
 
@@ -1124,6 +1128,11 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
       g.drop_thresh == 0 && !colsum && !attn_delta && (!res || !res_f32) &&
       pcv_gemm_big_ok(M, N, K, A, lda, B, ldb))
     return pcv_gemm_big(A, B, C, M, N, K, lda, ldb, ldc, alpha, res, ldr, res_scale, stream);
+  // weight gradients accumulated into fp32 (C += alpha A^T B, both operands K-major): the 256x256
+  // split-K / atomic form of the same kernel; it picks its own split count
+  if (trans_a && !trans_b && out_f32 && beta == 1.f && batch == 1 && !bias && !res && !aux && act == EPI_NONE &&
+      g.drop_thresh == 0 && !colsum && !attn_delta && pcv_aligned16(C) && pcv_gemm_big_wgrad_ok(M, N, K, A, lda, B, ldb))
+    return pcv_gemm_big_wgrad(A, B, (float*)C, M, N, K, lda, ldb, ldc, alpha, stream);
   // tile: 128x128 when that grid covers the chip, else 64x64.  (A 256x256 tile with
   // one 128x128 block per wave was measured 15-45 % slower at the LM shapes: it needs
   // all 512 registers, spills, and runs one wave per SIMD.)

@@ -28,6 +28,7 @@
 //   * a ragged K tail (K % 32) goes through registers with zero fill after the ring drains;
 //   * the bf16 tile is staged through LDS and stored as 16-byte rows (+ residual).
 #include "common.h"
+#include <cstdlib>
 
 namespace pcv {
 
@@ -248,6 +249,184 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
   }
 }
 
+// ------------------------------------------------------------------ weight-gradient form ----
+// C[M,N] (fp32) += alpha * A[K,M]^T . B[K,N] with A and B stored K-major (M- / N-contiguous): the
+// flax Dense kernel cotangents dW = X^T dY of the LM (models/LM/transformer.py Dense call sites).
+// Same 8-wave ping-pong schedule and 4-slot LDS-DMA ring as gemm_big_kernel; the images are
+// [32 k-rows][256 cols] (512 B rows) with 32-B blocks XOR-swizzled by mc_blk (as gemm.hip's
+// M/N-contiguous images) and read with ds_read_tr16_b64 into the MFMA operand layout.  K is split
+// over blockIdx.y (each split a multiple of 32) and the fp32 tile is added with atomics, staged
+// through LDS 64 rows at a time so every wave-instruction adds 64 consecutive floats (256 B).
+struct WgArgs {
+  const bf16* A; const bf16* B; float* C;
+  int64_t lda, ldb, ldc;
+  int M, N, K, tiles_m, tiles_n, kps;
+  float alpha;
+};
+
+constexpr int GW_IMG = 32 * 512;          // one operand image of a 32-k step
+constexpr int GW_SLOT = 2 * GW_IMG;
+constexpr int GW_CLD = 256 + 4;           // epilogue staging row (floats)
+constexpr int GW_LDS = (GB_SLOTS * GW_SLOT > 64 * GW_CLD * 4) ? GB_SLOTS * GW_SLOT : 64 * GW_CLD * 4;
+
+__device__ __forceinline__ int gw_blk(int cb, int k) { return cb ^ ((k & 3) | (((k >> 3) & 1) << 2)); }
+typedef __attribute__((address_space(3))) char gw_lds_char;
+
+// two transposing 8-B reads at k-rows kr and kr + 4 (same swizzle block, +4 rows = +2048 B)
+__device__ __forceinline__ void gw_tr2(uint32_t addr, bf16x4& lo, bf16x4& hi) {
+  asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:2048"
+               : "=&v"(lo), "=v"(hi) : "v"(addr));
+}
+
+// lgkmcnt(0) that the compiler sees as producing the 24 read results (nothing reads them earlier)
+__device__ __forceinline__ void gw_wait12(bf16x4 (&lo)[12], bf16x4 (&hi)[12]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(lo[0]), "+v"(lo[1]), "+v"(lo[2]), "+v"(lo[3]), "+v"(lo[4]), "+v"(lo[5]), "+v"(lo[6]),
+                 "+v"(lo[7]), "+v"(lo[8]), "+v"(lo[9]), "+v"(lo[10]), "+v"(lo[11]), "+v"(hi[0]), "+v"(hi[1]),
+                 "+v"(hi[2]), "+v"(hi[3]), "+v"(hi[4]), "+v"(hi[5]), "+v"(hi[6]), "+v"(hi[7]), "+v"(hi[8]),
+                 "+v"(hi[9]), "+v"(hi[10]), "+v"(hi[11])
+               :
+               : "memory");
+}
+
+__global__ __launch_bounds__(512, 1) void gemm_big_wgrad_kernel(WgArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int bid = blockIdx.x, nwg = g.tiles_m * g.tiles_n;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int per_group = 8 * g.tiles_n;
+  const int first_m = (wgid / per_group) * 8;
+  const int gsz = min(g.tiles_m - first_m, 8);
+  const int tm = first_m + (wgid % per_group) % gsz, tn = (wgid % per_group) / gsz;
+  const int m0 = tm * GB_T, n0 = tn * GB_T;
+  const int kbeg = blockIdx.y * g.kps;
+  const int kend = min(g.K, kbeg + g.kps);
+  const int nsteps = (kend - kbeg) / 32;
+  if (nsteps <= 0) return;   // uniform over the workgroup, before any barrier
+
+  // DMA: piece p (16 per image and step) = k-rows 2p, 2p+1; this wave fills pieces 2*wave, 2*wave+1
+  // of both images.  lane -> k-row (lane >> 5), physical 16-B slot (lane & 31) of block sl >> 1,
+  // holding logical block gw_blk(sl >> 1, kr) (an involution), clamped to the last valid 8 columns.
+  const bf16* srcA[2];
+  const bf16* srcB[2];
+  const int lastA = ((g.M - 1) >> 3) << 3, lastB = ((g.N - 1) >> 3) << 3;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int kr = (wave * 2 + i) * 2 + (lane >> 5);
+    const int sl = lane & 31;
+    const int cb = gw_blk(sl >> 1, kr);
+    const int ca = min(m0 + (cb * 2 + (sl & 1)) * 8, lastA);
+    const int cbb = min(n0 + (cb * 2 + (sl & 1)) * 8, lastB);
+    srcA[i] = g.A + (int64_t)(kbeg + kr) * g.lda + ca;
+    srcB[i] = g.B + (int64_t)(kbeg + kr) * g.ldb + cbb;
+  }
+  const int64_t stepA = 32 * g.lda, stepB = 32 * g.ldb;
+  auto issue = [&](int s) {
+    char* slot = smem + (s & 3) * GW_SLOT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(srcA[i] + s * stepA), (gb_lds_void*)(slot + (wave * 2 + i) * 1024),
+                                       16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(srcB[i] + s * stepB),
+                                       (gb_lds_void*)(slot + GW_IMG + (wave * 2 + i) * 1024), 16, 0, 0);
+  };
+  // transposing fragment reads: lane (g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3) reads 8 B
+  // of k-rows 8g + q and 8g + q + 4 at its 16-column block
+  const int fg = lane >> 4, fq = (lane & 15) >> 2, fp = lane & 3;
+  const int kr0 = 8 * fg + fq, kr1 = kr0 + 4;
+  int offA[8][2], offB[4][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int cb = wr * 8 + i;
+    offA[i][0] = kr0 * 512 + (gw_blk(cb, kr0) << 5) + fp * 8;
+    offA[i][1] = kr1 * 512 + (gw_blk(cb, kr1) << 5) + fp * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int cb = wc * 4 + j;
+    offB[j][0] = GW_IMG + kr0 * 512 + (gw_blk(cb, kr0) << 5) + fp * 8;
+    offB[j][1] = GW_IMG + kr1 * 512 + (gw_blk(cb, kr1) << 5) + fp * 8;
+  }
+  // The reads are inline asm: the compiler treats the ds_read_tr builtin as aliasing every LDS-DMA
+  // in flight and puts a vmcnt(0) in front of it, which would drain the 3-step prefetch each step.
+  // The asm outputs are only consumed after the explicit lgkmcnt(0) that names them (gw_wait12).
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(gw_lds_char*)smem;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int s = 0; s < 3 && s < nsteps; ++s) issue(s);
+  gb_wait_n<4>(min(2, nsteps - 1));
+  gb_barrier();
+  if (wr == 1) gb_barrier();
+  for (int s = 0; s < nsteps; ++s) {
+    if (s + 3 < nsteps) issue(s + 3);
+    const char* slot = smem + (s & 3) * GW_SLOT;
+    const uint32_t sb = lds0 + (uint32_t)((s & 3) * GW_SLOT);
+    bf16x4 lo[12], hi[12];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gw_tr2(sb + offB[j][0], lo[8 + j], hi[8 + j]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gw_tr2(sb + offA[i][0], lo[i], hi[i]);
+    gw_wait12(lo, hi);
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 a[8], b[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = __builtin_shufflevector(lo[i], hi[i], 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = __builtin_shufflevector(lo[8 + j], hi[8 + j], 0, 1, 2, 3, 4, 5, 6, 7);
+    const int after = min(nsteps - 1, s + 3) - (s + 1);
+    if (wr == 1 && s + 1 < nsteps) gb_wait_n<4>(after);
+    gb_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (wr == 0 && s + 1 < nsteps) gb_wait_n<4>(after);
+    gb_barrier();
+  }
+  if (wr == 0) gb_barrier();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // epilogue: 4 chunks of 64 rows through LDS, then coalesced fp32 atomics
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    __syncthreads();
+    if (wr == (c >> 1)) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = (c & 1) * 4 + ii;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ct[(ii * 16 + (lane >> 4) * 4 + r) * GW_CLD + wc * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < 64 * 256; e += 512) {
+      const int row = e >> 8, col = e & 255;
+      const int gr = m0 + c * 64 + row, gc = n0 + col;
+      if (gr < g.M && gc < g.N) {
+        float* dst = g.C + (int64_t)gr * g.ldc + gc;
+        if (gridDim.y == 1) *dst += g.alpha * ct[row * GW_CLD + col];   // sole writer of this tile
+        else atomicAdd(dst, g.alpha * ct[row * GW_CLD + col]);
+      }
+    }
+  }
+}
+
 }  // namespace pcv
 
 using namespace pcv;
@@ -313,5 +492,60 @@ extern "C" int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, in
   g.tiles_n = (int)((N + bn - 1) / bn);
   if (bn == 192) launch_big<192>(g, (hipStream_t)stream);
   else launch_big<256>(g, (hipStream_t)stream);
+  return pcv_launch_status();
+}
+
+// ---------------------------------------------------------------- weight-gradient entry ----
+static bool wgrad_shape_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb) {
+  if (M < 256 || N < 256 || K < 32 * 16 || (K & 31) || M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31))
+    return false;
+  // fewer than 20 output tiles (d x d products): the 128x128 split-K family wins (measured 56 vs 70 us at 768^2)
+  if (((M + GB_T - 1) / GB_T) * ((N + GB_T - 1) / GB_T) < 20) return false;
+  return !((lda & 7) || (ldb & 7) || !pcv_aligned16(A) || !pcv_aligned16(B));
+}
+
+// split count: minimise rounds x (32-k steps per split + epilogue), every split a multiple of 32
+// deep and >= 512 (s > 1).  The epilogue (pipeline fill + 256 KB of fp32 atomics per tile) costs
+// about 40 steps (measured: 0.87 us per step and 36 us per tile on the full chip).
+static int wgrad_splits(int64_t tiles, int64_t K) {
+  constexpr int64_t kEpi = 40;
+  int best = 1;
+  int64_t best_cost = -1;
+  for (int s = 1; s <= 64; ++s) {
+    const int64_t kps = ((K + s - 1) / s + 31) / 32 * 32;
+    if (s > 1 && kps < 512) break;
+    const int64_t wgs = tiles * ((K + kps - 1) / kps);
+    const int64_t cost = ((wgs + 255) / 256) * (kps / 32 + kEpi);
+    if (best_cost < 0 || cost < best_cost) { best_cost = cost; best = s; }
+  }
+  return best;
+}
+
+extern "C" int pcv_gemm_big_wgrad_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                                     int64_t ldb) {
+  return (g_big_enabled && wgrad_shape_ok(M, N, K, A, lda, B, ldb)) ? 1 : 0;
+}
+
+// C (fp32, [M][ldc]) += alpha * A^T B with A [K][lda >= M] and B [K][ldb >= N] bf16
+extern "C" int pcv_gemm_big_wgrad(const void* A, const void* B, float* C, int64_t M, int64_t N, int64_t K,
+                                  int64_t lda, int64_t ldb, int64_t ldc, float alpha, void* stream) {
+  if (!wgrad_shape_ok(M, N, K, A, lda, B, ldb) || !C) return PCV_EINVAL;
+  WgArgs g{};
+  g.A = (const bf16*)A; g.B = (const bf16*)B; g.C = C;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K; g.alpha = alpha;
+  g.tiles_m = (int)((M + GB_T - 1) / GB_T);
+  g.tiles_n = (int)((N + GB_T - 1) / GB_T);
+  static const int forced = getenv("PCV_WGRAD_SPLITS") ? atoi(getenv("PCV_WGRAD_SPLITS")) : 0;
+  const int s = forced > 0 ? forced : wgrad_splits((int64_t)g.tiles_m * g.tiles_n, K);
+  g.kps = (int)(((K + s - 1) / s + 31) / 32 * 32);
+  const int nsplit = (int)((K + g.kps - 1) / g.kps);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_big_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, GW_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(gemm_big_wgrad_kernel, dim3(g.tiles_m * g.tiles_n, nsplit), dim3(512), GW_LDS,
+                     (hipStream_t)stream, g);
   return pcv_launch_status();
 }

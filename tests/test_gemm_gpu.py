@@ -70,6 +70,37 @@ def test_gemm_epilogues(dev):
     assert torch.allclose(c, ref, rtol=1e-3, atol=5e-2), (c - ref).abs().max()
 
 
+@pytest.mark.parametrize("M,N,K", [(768, 50257, 16384), (1280, 1280, 16384), (768, 4608, 16384), (2304, 768, 16384),
+                                   (1100, 1300, 4096), (1300, 1000, 544), (50257, 768, 16384)])
+def test_gemm_big_wgrad(dev, M, N, K):
+    """Split-K / fp32-atomic weight-gradient form of the 256x256 kernel (C += alpha X^T dY, both operands
+    K-major) through pcv_gemm_bf16's dispatch: ragged M/N (clamped DMA columns, masked atomics), padded
+    row strides, K not a multiple of the split; compared with the 128x128 path (big kernel disabled)."""
+    from plaincv_amd import hip
+    from plaincv_amd import kernels as k
+    lib = hip.load()
+    g = torch.Generator(device=dev).manual_seed(M * 7 + N + K)
+    a = _padded(K, M, dev, g)
+    b = _padded(K, N, dev, g)
+    assert lib.pcv_gemm_big_wgrad_ok(M, N, K, hip.ptr(a), a.stride(0), hip.ptr(b), b.stride(0)) == 1
+    c0 = torch.randn(M, N, device=dev, generator=g)
+    outs = []
+    for on in (1, 0):
+        prev = lib.pcv_gemm_big_enable(on)
+        try:
+            c = c0.clone()
+            k.gemm(a, b, c, ta=True, alpha=0.25, beta=1.0)
+            torch.cuda.synchronize()
+        finally:
+            lib.pcv_gemm_big_enable(prev)
+        outs.append(c)
+    ref = c0 + 0.25 * (a.float().t() @ b.float())
+    tol = 2e-5 * K + 1e-4 * ref.abs().max().item()   # fp32 accumulation-order differences only
+    for out in outs:
+        assert (out - ref).abs().max().item() <= tol
+    assert (outs[0] - outs[1]).abs().max().item() <= tol
+
+
 def test_gemm_batched(dev):
     from plaincv_amd import kernels as k
     B, M, N, K = 5, 128, 256, 256

@@ -35,7 +35,11 @@ SHAPES = [("lm_head fwd", 16384, 50304, 768, "fwd"), ("qkv fwd", 16384, 2304, 76
           # 420M (d 1024, F 2730 -> gate|up 2 x 2736, V 50280, 16384 rows)
           ("420M lm_head fwd", 16384, 50280, 1024, "fwd"), ("420M qkv fwd", 16384, 3072, 1024, "fwd"),
           ("420M gate|up fwd", 16384, 5472, 1024, "fwd"), ("qkv dgrad", 16384, 768, 2304, "dgrad"),
-          ("420M out fwd", 16384, 1024, 1024, "fwd"), ("420M gate|up dgrad", 16384, 1024, 5472, "dgrad")]
+          ("420M out fwd", 16384, 1024, 1024, "fwd"), ("420M gate|up dgrad", 16384, 1024, 5472, "dgrad"),
+          ("fc2 wgrad", 2048, 768, 16384, "wgrad"), ("out wgrad", 768, 768, 16384, "wgrad"),
+          ("420M lm_head wgrad", 1024, 50280, 16384, "wgrad"), ("420M gate|up wgrad", 1024, 5472, 16384, "wgrad"),
+          ("420M fc2 wgrad", 2736, 1024, 16384, "wgrad"), ("420M qkv wgrad", 1024, 3072, 16384, "wgrad"),
+          ("420M out wgrad", 1024, 1024, 16384, "wgrad")]
 
 FLT = sys.argv[1] if len(sys.argv) > 1 else ""
 REF = "--no-ref" not in sys.argv
