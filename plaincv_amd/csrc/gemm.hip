@@ -208,6 +208,7 @@ __device__ __forceinline__ bf16x8 mc_frag(const char* lds, int cbase, int ks) {
 // (the XOR maps are involutions).  Rows/columns past the matrix edge are clamped to
 // a valid address: they only feed output rows/cols that are never stored.
 typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) char gemm_lds_char;
 
 __device__ __forceinline__ void glds16(const bf16* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)lds_wave_base, 16, 0, 0);
@@ -273,6 +274,25 @@ __device__ __forceinline__ void frag_offsets(int rbase, int ks, int (&off)[2]) {
     off[1] = kr1 * (R * 2) + (mc_blk<R>(cb, kr1) << 5) + p * 8;
   }
 }
+// Transposing fragment read as inline asm.  The ds_read_tr builtin is treated by the compiler as
+// aliasing every LDS-DMA in flight, so it would put a vmcnt(0) in front of it and drain the DMA of
+// the NEXT k-tile before this one is read (no load/compute overlap at all for M/N-contiguous
+// operands).  The asm results are consumed only after tr_wait() + tr_touch(); k and k + 4 share the
+// swizzle block (k = 8g + q, q < 4), so the second read is the first + 4 rows (= 8R bytes).
+template <int R>
+__device__ __forceinline__ void tr_read(const char* img, int off, bf16x4& lo, bf16x4& hi) {
+  const uint32_t a = (uint32_t)(uintptr_t)(gemm_lds_char*)(img + off);
+  asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %2 offset:%3"
+               : "=&v"(lo), "=v"(hi) : "v"(a), "i"(8 * R) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void tr_wait() { asm volatile("s_waitcnt lgkmcnt(%0)" :: "i"(N) : "memory"); }
+// ties a read result to a point after the wait: nothing may read the register earlier
+__device__ __forceinline__ void tr_touch(bf16x4& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ bf16x8 tr_join(const bf16x4& lo, const bf16x4& hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 template <bool KC>
 __device__ __forceinline__ bf16x8 read_frag(const char* img, const int (&off)[2]) {
   if constexpr (KC) {
@@ -625,37 +645,62 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
   // already hides it and has no registers to spare, reads one k-step at a time)
   auto compute = [&](const char* la) {
     const char* lb = la + A_BYTES;
-    if constexpr (WM * WN >= 64) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 af[WM], bfr[WN];
-#pragma unroll
-        for (int i = 0; i < WM; ++i) af[i] = read_frag<A_KC>(la, offA[i][ks]);
-#pragma unroll
-        for (int j = 0; j < WN; ++j) bfr[j] = read_frag<B_KC>(lb, offB[j][ks]);
-#pragma unroll
-        for (int i = 0; i < WM; ++i)
-#pragma unroll
-          for (int j = 0; j < WN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      }
-      return;
-    }
+    // K-contiguous fragments: plain ds_read_b128 (the compiler counts their lgkmcnt);
+    // M/N-contiguous ones: tr_read pairs, waited for explicitly (N1 = LDS ops of one k-step)
+    constexpr int N1 = WM * (A_KC ? 1 : 2) + WN * (B_KC ? 1 : 2);
     bf16x8 af[2][WM], bfr[2][WN];
+    bf16x4 alo[2][WM], ahi[2][WM], blo[2][WN], bhi[2][WN];
+    auto reads = [&](int ks) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+      for (int i = 0; i < WM; ++i) {
+        if constexpr (A_KC) af[ks][i] = read_frag<true>(la, offA[i][ks]);
+        else tr_read<BM>(la, offA[i][ks][0], alo[ks][i], ahi[ks][i]);
+      }
 #pragma unroll
-      for (int i = 0; i < WM; ++i) af[ks][i] = read_frag<A_KC>(la, offA[i][ks]);
+      for (int j = 0; j < WN; ++j) {
+        if constexpr (B_KC) bfr[ks][j] = read_frag<true>(lb, offB[j][ks]);
+        else tr_read<BN>(lb, offB[j][ks][0], blo[ks][j], bhi[ks][j]);
+      }
+    };
+    auto join = [&](int ks) {
 #pragma unroll
-      for (int j = 0; j < WN; ++j) bfr[ks][j] = read_frag<B_KC>(lb, offB[j][ks]);
-    }
+      for (int i = 0; i < WM; ++i)
+        if constexpr (!A_KC) { tr_touch(alo[ks][i]); tr_touch(ahi[ks][i]); af[ks][i] = tr_join(alo[ks][i], ahi[ks][i]); }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int j = 0; j < WN; ++j)
+        if constexpr (!B_KC) { tr_touch(blo[ks][j]); tr_touch(bhi[ks][j]); bfr[ks][j] = tr_join(blo[ks][j], bhi[ks][j]); }
+    };
+    auto mfmas = [&](int ks) {
 #pragma unroll
       for (int i = 0; i < WM; ++i)
 #pragma unroll
         for (int j = 0; j < WN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][i], bfr[ks][j], acc[i][j], 0, 0, 0);
+    };
+    if constexpr (WM * WN >= 64) {
+      // both k-steps' fragments are read before the first MFMA, so the second half's LDS
+      // latency hides under the first half's MFMAs, except for the 256x256 tile (8x8 blocking,
+      // no registers to spare): one k-step at a time
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        reads(ks);
+        if constexpr (!A_KC || !B_KC) tr_wait<0>();
+        join(ks);
+        mfmas(ks);
+      }
+    } else {
+      reads(0);
+      reads(1);
+      if constexpr (!A_KC || !B_KC) tr_wait<(N1 < 15 ? N1 : 15)>();   // k-step 0 landed (in-order; 4-bit count)
+      join(0);
+      mfmas(0);
+      if constexpr (!A_KC || !B_KC) {
+        __builtin_amdgcn_sched_barrier(0);   // keep k-step 0's MFMAs ahead of the second wait
+        tr_wait<0>();
+      }
+      join(1);
+      mfmas(1);
+    }
   };
 
   if (g.glds_ok) {

@@ -70,8 +70,8 @@ def test_gemm_epilogues(dev):
     assert torch.allclose(c, ref, rtol=1e-3, atol=5e-2), (c - ref).abs().max()
 
 
-@pytest.mark.parametrize("M,N,K", [(768, 50257, 16384), (1280, 1280, 16384), (768, 4608, 16384), (2304, 768, 16384),
-                                   (1100, 1300, 4096), (1300, 1000, 544), (50257, 768, 16384)])
+@pytest.mark.parametrize("M,N,K", [(768, 50257, 16384), (4100, 4100, 16384), (1024, 50280, 4096), (50257, 1000, 544),
+                                   (50257, 768, 16384)])
 def test_gemm_big_wgrad(dev, M, N, K):
     """Split-K / fp32-atomic weight-gradient form of the 256x256 kernel (C += alpha X^T dY, both operands
     K-major) through pcv_gemm_bf16's dispatch: ragged M/N (clamped DMA columns, masked atomics), padded
