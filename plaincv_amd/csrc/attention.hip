@@ -19,6 +19,7 @@
 // bwd_dq (workgroup = 64 queries, loop over keys) -- deterministic, no atomics.
 #include "common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace pcv {
@@ -731,6 +732,388 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
   }
 }
 
+// ------------------------------------------------------- short sequences (ViT)
+// Dh = 32, T <= 320, no causal / document mask (the ViT: 257 tokens, flax SelfAttention,
+// models/vit_small.py:41-45).  One workgroup of 16 waves per (batch, head) holds the head's whole
+// Q, K, V (and, backward, dO) in LDS, loaded once: the tiled kernels above run 1.5 rounds of
+// 3-query-block workgroups (the third holding one query) through a 5-tile loop whose load latency
+// is not hidden at this length.  Rows are padded to TP = ceil(T / 32) * 32 with zeros; scores of
+// padded keys are masked, padded queries are never stored.  Same math, masks and LSE convention
+// as attn_fwd_kernel / attn_bwd_*.  16 waves (4 per SIMD, <= 128 VGPRs): these kernels are
+// latency-bound chains (MFMA -> row max -> exp -> MFMA), so occupancy is what hides them
+// (measured: 8 waves spent 58 % of wave-cycles parked in s_waitcnt).
+constexpr int SH_TMAX = 320, SH_DH = 32, SH_THREADS = 1024, SH_WAVES = SH_THREADS / 64;
+
+// Cooperative load of rows [0, TP) of N column blocks into swizzled LDS images: all of a thread's
+// 16-B loads are issued before the first LDS store (one HBM latency for the whole prologue).
+template <int N>
+__device__ __forceinline__ void sh_load_images(bf16* const (&img)[N], const bf16* const (&src)[N],
+                                               const int64_t (&ld)[N], int T, int TP, int64_t bT) {
+  constexpr int CPR = SH_DH / 8, ITER = (SH_TMAX * CPR + SH_THREADS - 1) / SH_THREADS;
+  u32x4 v[ITER][N];
+#pragma unroll
+  for (int i = 0; i < ITER; ++i) {
+    const int idx = threadIdx.x + SH_THREADS * i;
+    const int r = idx / CPR, c = idx % CPR;
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      v[i][n] = u32x4{0u, 0u, 0u, 0u};
+      if (r < T) v[i][n] = *reinterpret_cast<const u32x4*>(src[n] + (bT + r) * ld[n] + c * 8);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < ITER; ++i) {
+    const int idx = threadIdx.x + SH_THREADS * i;
+    const int r = idx / CPR, c = idx % CPR;
+    if (r < TP) {
+#pragma unroll
+      for (int n = 0; n < N; ++n) *reinterpret_cast<u32x4*>(img[n] + toff<SH_DH>(r, c)) = v[i][n];
+    }
+  }
+}
+
+// The layer's packed [T,T] dropout keep words (drop_word layout, shared by every batch and head)
+// staged into LDS once per workgroup: read per score element, a global 2-byte load each time
+// serialised a few microseconds of latency into every score chain.
+constexpr int SH_MASK_WORDS = 8 * ((SH_TMAX + 127) / 128) * (2 * ((SH_TMAX + 127) / 128)) * 64;
+__device__ __forceinline__ void sh_load_mask(uint16_t* dst, const uint16_t* src, int T) {
+  const int n = (int)drop_words(T) / 8;   // 16-B chunks (the word count is a multiple of 64)
+  for (int i = threadIdx.x; i < n; i += blockDim.x)
+    reinterpret_cast<u32x4*>(dst)[i] = reinterpret_cast<const u32x4*>(src)[i];
+}
+
+// Forward: 16-query groups dealt round-robin to the waves (17 at T = 257); per group an online
+// softmax over 64-key chunks (lazy rescale as attn_fwd_kernel), K and V fragments from LDS.
+// NT = TP / 16 key blocks (compile time: the chunk loop unrolls).
+template <int NT>
+__host__ __device__ constexpr size_t sh_fwd_lds(bool drop) {
+  return 3 * (size_t)NT * 16 * SH_DH * sizeof(bf16) + (drop ? SH_MASK_WORDS * sizeof(uint16_t) : 0);
+}
+template <int NT, bool DROP>
+__global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs a) {
+  constexpr int DH = SH_DH, DT = DH / 16, TP = NT * 16, NC = (NT + 3) / 4;
+  extern __shared__ __attribute__((aligned(16))) char shf_smem[];
+  bf16* Qs = reinterpret_cast<bf16*>(shf_smem);
+  bf16* Ks = Qs + TP * DH;
+  bf16* Vs = Ks + TP * DH;
+  uint16_t* mk = reinterpret_cast<uint16_t*>(Vs + TP * DH);
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int T = a.T;
+  const int64_t bT = (int64_t)b * T;
+  {
+    bf16* const img[3] = {Qs, Ks, Vs};
+    const bf16* const src[3] = {a.q + h * DH, a.k + h * DH, a.v + h * DH};
+    const int64_t ld[3] = {a.ldq, a.ldq, a.ldq};
+    sh_load_images<3>(img, src, ld, T, TP, bT);
+  }
+  if (DROP) sh_load_mask(mk, a.mask, T);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4;
+  const float c2 = a.scale * LOG2E;
+  const int NG = (T + 15) / 16;
+  for (int gq = wave; gq < NG; gq += SH_WAVES) {
+    const int myq = gq * 16 + (lane & 15);
+    const bool qv = myq < T;
+    int Tl = T;   // opaque: keeps the bounds tests of the tail chunk inside the loop
+    asm volatile("" : "+s"(Tl));
+    const bf16x8 qf = row_frag<DH>(Qs, gq * 16, 0);
+    float m2 = NEG_BIG, l = 0.f;
+    f32x4 acc[DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) acc[d] = kZero4;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int nt = (4 * c + 4 <= NT) ? 4 : NT - 4 * c;   // key blocks in this chunk (4 or 2)
+      uint64_t mw = 0;
+      if (DROP) mw = *reinterpret_cast<const uint64_t*>(mk + drop_word(myq, 64 * c + 4 * g, a.n64));
+      f32x4 s[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (t < nt) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Ks, 64 * c + 16 * t, 0), qf, kZero4, 0, 0, 0);
+      if (64 * c + 16 * nt > Tl) {   // chunk reaches past T: padded keys -> NEG_BIG
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          if (t < nt) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[t][r] = 64 * c + 16 * t + 4 * g + r < Tl ? s[t][r] : NEG_BIG;
+          }
+      }
+      float bmax = NEG_BIG;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (t < nt) bmax = fmaxf(bmax, fmaxf(fmaxf(s[t][0], s[t][1]), fmaxf(s[t][2], s[t][3])));
+      bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
+      bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+      const float cand = bmax * c2;
+      if (__ballot(cand > m2 + 8.f) != 0) {   // a row's max moved by > 2^8: rescale (wave-uniform)
+        const float mnew = fmaxf(m2, cand);
+        const float alpha = __builtin_amdgcn_exp2f(m2 - mnew);
+        l *= alpha;
+        m2 = mnew;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float al = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+          for (int d = 0; d < DT; ++d) acc[d][r] *= al;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < nt) {
+          uint32_t wt = 0;
+          if (DROP) wt = (uint32_t)(mw >> (16 * t)) >> (4 * (myq & 3));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            // padded keys hold NEG_BIG: exp2 of it underflows to exactly 0
+            float p = __builtin_amdgcn_exp2f(fmaf(s[t][r], c2, -m2));
+            l += p;
+            if (DROP) p = __uint_as_float(__float_as_uint(p) & (uint32_t)__builtin_amdgcn_sbfe((int)wt, r, 1));
+            s[t][r] = p;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (2 * u < nt) {
+          const bf16x8 pa = pack8(s[2 * u], s[2 * u + 1]);
+#pragma unroll
+          for (int d = 0; d < DT; ++d)
+            acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_frag<DH>(Vs, 2 * c + u, 16 * d), acc[d], 0, 0, 0);
+        }
+      }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = (DROP ? a.drop_scale : 1.f) / l;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float iv = __shfl(inv, 4 * g + r, 64);
+      const int qq = gq * 16 + 4 * g + r;
+      if (qq < T) {
+#pragma unroll
+        for (int d = 0; d < DT; ++d) a.out[(bT + qq) * a.ldout + h * DH + 16 * d + (lane & 15)] = f2bf(acc[d][r] * iv);
+      }
+    }
+    if (g == 0 && qv) a.lse2[((int64_t)b * a.H + h) * T + myq] = m2 + log2f(l);
+  }
+}
+
+// Backward: waves 0-7 own key blocks (dK, dV of 16 keys over all queries, k = queries in the
+// MFMAs), waves 8-15 own query groups (dQ of 16 queries over all keys, k = keys) -- the two
+// products need opposite MFMA orientations of the recomputed scores, and splitting the waves
+// keeps both in registers with no cross-wave sum and no barrier after the prologue.
+// delta = rowsum(dO o O) is formed in-kernel unless the dO producer already wrote it.
+constexpr size_t SH_BWD_LDS = 4 * SH_TMAX * SH_DH * sizeof(bf16) + 2 * SH_TMAX * sizeof(float) +
+                              SH_MASK_WORDS * sizeof(uint16_t);
+
+template <bool DROP>
+__global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs a) {
+  constexpr int DH = SH_DH, DT = DH / 16;
+  extern __shared__ __attribute__((aligned(16))) char sh_smem[];
+  bf16* Qs = reinterpret_cast<bf16*>(sh_smem);
+  bf16* Ks = Qs + SH_TMAX * DH;
+  bf16* Vs = Ks + SH_TMAX * DH;
+  bf16* Os = Vs + SH_TMAX * DH;   // dO
+  float* Ls = reinterpret_cast<float*>(Os + SH_TMAX * DH);
+  float* Dl = Ls + SH_TMAX;
+  uint16_t* mk = reinterpret_cast<uint16_t*>(Dl + SH_TMAX);
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int T = a.T, TP = (T + 31) & ~31, NT = TP / 16;
+  const int64_t bT = (int64_t)b * T, bh = (int64_t)b * a.H + h;
+  {
+    bf16* const img[4] = {Qs, Ks, Vs, Os};
+    const bf16* const src[4] = {a.q + h * DH, a.k + h * DH, a.v + h * DH, a.dout + h * DH};
+    const int64_t ld[4] = {a.ldq, a.ldq, a.ldq, a.lddo};
+    sh_load_images<4>(img, src, ld, T, TP, bT);
+  }
+  if (DROP) sh_load_mask(mk, a.mask, T);
+  if (a.delta_ready) {
+    for (int r = threadIdx.x; r < TP; r += blockDim.x) {
+      Ls[r] = r < T ? a.lse2[bh * T + r] : 0.f;
+      Dl[r] = r < T ? a.delta[bh * T + r] : 0.f;
+    }
+  } else {
+    // delta = rowsum(dO o O): 4 lanes x 8 columns per row, all loads issued first
+    constexpr int ITER = (SH_TMAX * 4 + SH_THREADS - 1) / SH_THREADS;
+    bf16x8 xo[ITER], xd[ITER];
+    float lv[ITER];
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int idx = threadIdx.x + SH_THREADS * i;
+      const int r = idx >> 2, c = (idx & 3) * 8;
+      xo[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      xd[i] = xo[i];
+      lv[i] = 0.f;
+      if (r < T) {
+        xo[i] = *reinterpret_cast<const bf16x8*>(a.o + (bT + r) * a.ldo + h * DH + c);
+        xd[i] = *reinterpret_cast<const bf16x8*>(a.dout + (bT + r) * a.lddo + h * DH + c);
+        lv[i] = a.lse2[bh * T + r];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+      const int idx = threadIdx.x + SH_THREADS * i;
+      const int r = idx >> 2;
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += bf2f(xo[i][j]) * bf2f(xd[i][j]);
+      sum += __shfl_xor(sum, 1, 64);
+      sum += __shfl_xor(sum, 2, 64);
+      if ((idx & 3) == 0 && r < TP) {
+        Dl[r] = sum;
+        Ls[r] = lv[i];
+        if (r < T) a.delta[bh * T + r] = sum;
+      }
+    }
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4;
+  const float c2 = a.scale * LOG2E;
+  const int NB = (T + 15) / 16;
+  if (wave < 8) {
+    // ---- dK, dV of keys 16*kb .. +15 (lane & 15), over all queries
+    for (int kb = wave; kb < NB; kb += 8) {
+      const int mykey = kb * 16 + (lane & 15);
+      const bf16x8 kf = row_frag<DH>(Ks, kb * 16, 0);
+      const bf16x8 vf = row_frag<DH>(Vs, kb * 16, 0);
+      f32x4 dv[DT], dk[DT];
+#pragma unroll
+      for (int d = 0; d < DT; ++d) { dv[d] = kZero4; dk[d] = kZero4; }
+      for (int st = 0; st < NT / 2; ++st) {
+        const bool interior = kb * 16 + 16 <= T && 32 * st + 32 <= T;   // wave-uniform: no bounds tests
+        f32x4 p[2], ds[2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const int t = 2 * st + tt;
+          const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Qs, 16 * t, 0), kf, kZero4, 0, 0, 0);
+          const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Os, 16 * t, 0), vf, kZero4, 0, 0, 0);
+          uint32_t wt = 0;
+          if (DROP) wt = (uint32_t)mk[drop_word(16 * t + 4 * g, mykey, a.n64)] >> (mykey & 3);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ql = 16 * t + 4 * g + r;
+            float pv = __builtin_amdgcn_exp2f(fmaf(sv[r], c2, -Ls[ql]));
+            if (!interior) pv = (mykey < T && ql < T) ? pv : 0.f;
+            float dpv = dp[r];
+            float pd = pv;
+            if (DROP) {
+              const uint32_t km = (uint32_t)__builtin_amdgcn_sbfe((int)wt, 4 * r, 1);
+              pd = __uint_as_float(__float_as_uint(pv) & km);
+              dpv = __uint_as_float(__float_as_uint(dpv) & km) * a.drop_scale;
+            }
+            p[tt][r] = pd;
+            ds[tt][r] = pv * (dpv - Dl[ql]);
+          }
+        }
+        const bf16x8 pb = pack8(p[0], p[1]), sb = pack8(ds[0], ds[1]);
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+          dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag<DH>(Os, st, 16 * d), pb, dv[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag<DH>(Qs, st, 16 * d), sb, dk[d], 0, 0, 0);
+        }
+      }
+      if (mykey < T) {
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int dd = 16 * d + 4 * g + r;
+            a.dv[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(DROP ? dv[d][r] * a.drop_scale : dv[d][r]);
+            a.dk[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(dk[d][r] * a.scale);
+          }
+      }
+    }
+  } else {
+    // ---- dQ of queries 16*gq .. +15 (lane & 15), over all keys
+    for (int gq = wave - 8; gq < NB; gq += 8) {
+      const int q0 = gq * 16;
+      const int myq = q0 + (lane & 15);
+      const bf16x8 qf = row_frag<DH>(Qs, q0, 0);
+      const bf16x8 of = row_frag<DH>(Os, q0, 0);
+      const float myl = Ls[myq], myd = Dl[myq];
+      f32x4 acc[DT];
+#pragma unroll
+      for (int d = 0; d < DT; ++d) acc[d] = kZero4;
+      for (int st = 0; st < NT / 2; ++st) {
+        const bool interior = q0 + 16 <= T && 32 * st + 32 <= T;
+        f32x4 ds[2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const int t = 2 * st + tt;
+          const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Ks, 16 * t, 0), qf, kZero4, 0, 0, 0);
+          const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Vs, 16 * t, 0), of, kZero4, 0, 0, 0);
+          uint32_t wt = 0;
+          if (DROP) wt = (uint32_t)mk[drop_word(myq, 16 * t + 4 * g, a.n64)] >> (4 * (myq & 3));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = 16 * t + 4 * g + r;
+            float pv = __builtin_amdgcn_exp2f(fmaf(sv[r], c2, -myl));
+            if (!interior) pv = (myq < T && key < T) ? pv : 0.f;
+            float dpv = dp[r];
+            if (DROP)
+              dpv = __uint_as_float(__float_as_uint(dpv) & (uint32_t)__builtin_amdgcn_sbfe((int)wt, r, 1)) *
+                    a.drop_scale;
+            ds[tt][r] = pv * (dpv - myd);
+          }
+        }
+        const bf16x8 sa = pack8(ds[0], ds[1]);
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+          acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, tr_frag<DH>(Ks, st, 16 * d), acc[d], 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = q0 + 4 * g + r;
+        if (qq < T) {
+#pragma unroll
+          for (int d = 0; d < DT; ++d)
+            a.dq[(bT + qq) * a.lddq + h * DH + 16 * d + (lane & 15)] = f2bf(acc[d][r] * a.scale);
+        }
+      }
+    }
+  }
+}
+
+static bool short_ok(const AttnArgs& a, int dh, int causal, bool) {
+  return dh == SH_DH && !causal && a.T >= 1 && a.T <= SH_TMAX && a.dstart == nullptr &&
+         getenv("PCV_ATTN_NO_SHORT") == nullptr;
+}
+template <int NT, bool D>
+static void launch_short_fwd_nt(const AttnArgs& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)attn_short_fwd_kernel<NT, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sh_fwd_lds<NT>(D));
+    attr = true;
+  }
+  hipLaunchKernelGGL((attn_short_fwd_kernel<NT, D>), dim3(a.H, a.B), dim3(SH_THREADS), sh_fwd_lds<NT>(D), s, a);
+}
+template <bool D>
+static void launch_short_fwd(const AttnArgs& a, hipStream_t s) {
+  switch ((a.T + 31) / 32) {
+    case 1: launch_short_fwd_nt<2, D>(a, s); break;
+    case 2: launch_short_fwd_nt<4, D>(a, s); break;
+    case 3: launch_short_fwd_nt<6, D>(a, s); break;
+    case 4: launch_short_fwd_nt<8, D>(a, s); break;
+    case 5: launch_short_fwd_nt<10, D>(a, s); break;
+    case 6: launch_short_fwd_nt<12, D>(a, s); break;
+    case 7: launch_short_fwd_nt<14, D>(a, s); break;
+    case 8: launch_short_fwd_nt<16, D>(a, s); break;
+    case 9: launch_short_fwd_nt<18, D>(a, s); break;
+    default: launch_short_fwd_nt<20, D>(a, s); break;
+  }
+}
+template <bool D>
+static void launch_short_bwd(const AttnArgs& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)attn_short_bwd_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)SH_BWD_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((attn_short_bwd_kernel<D>), dim3(a.H, a.B), dim3(SH_THREADS), SH_BWD_LDS, s, a);
+}
+
 template <int DH, bool C, bool D>
 static void launch_fwd(const AttnArgs& a, hipStream_t s) {
   dim3 grid((a.T + 127) / 128, a.H, a.B);
@@ -749,6 +1132,11 @@ static void launch_bwd(const AttnArgs& a, hipStream_t s) {
 
 template <bool FWD>
 static int dispatch(const AttnArgs& a, int dh, int causal, int drop, hipStream_t s) {
+  if (short_ok(a, dh, causal, FWD)) {
+    if (FWD) { drop ? launch_short_fwd<true>(a, s) : launch_short_fwd<false>(a, s); }
+    else { drop ? launch_short_bwd<true>(a, s) : launch_short_bwd<false>(a, s); }
+    return pcv_launch_status();
+  }
 #define PCV_ATT(DHV, CV, DV) \
   if (dh == DHV && causal == CV && drop == DV) { FWD ? launch_fwd<DHV, CV, DV>(a, s) : launch_bwd<DHV, CV, DV>(a, s); return pcv_launch_status(); }
   PCV_ATT(32, 0, 0) PCV_ATT(32, 0, 1) PCV_ATT(32, 1, 0) PCV_ATT(32, 1, 1)

@@ -81,6 +81,59 @@ def test_attention_fwd_bwd(dev, B, T, H, Dh, causal, rate):
     assert err < 3e-2 * max(1.0, scale), (err, scale)
 
 
+@pytest.mark.parametrize("B,T,H,rate,delta_ready", [(2, 257, 4, 0.1, False), (3, 17, 2, 0.0, False),
+                                                     (1, 320, 3, 0.2, True), (2, 1, 2, 0.0, False),
+                                                     (2, 64, 4, 0.1, True), (4, 257, 4, 0.0, True)])
+def test_attention_short_path(dev, B, T, H, rate, delta_ready, monkeypatch):
+    """One-workgroup-per-(batch, head) kernels for Dh = 32, T <= 320, non-causal (the ViT):
+    against the fp32 reference, and against the tiled kernels (PCV_ATTN_NO_SHORT) on the same inputs."""
+    from oracle import rng
+    from plaincv_amd import kernels as K
+    Dh = 32
+    D = H * Dh
+    g = torch.Generator(device=dev).manual_seed(T + B)
+    qkv = torch.randn(B * T, 3 * D, device=dev, generator=g).to(torch.bfloat16)
+    do = torch.randn(B * T, D, device=dev, generator=g).to(torch.bfloat16)
+    seed = torch.tensor([99], dtype=torch.int32, device=dev)
+    mask = None
+    if rate > 0:
+        mask = torch.zeros(K.attn_mask_words(T), dtype=torch.int16, device=dev)
+        K.attn_drop_mask(seed, 5, T, rate, mask)
+    res = {}
+    for short in (True, False):
+        if short:
+            monkeypatch.delenv("PCV_ATTN_NO_SHORT", raising=False)
+        else:
+            monkeypatch.setenv("PCV_ATTN_NO_SHORT", "1")
+        out = torch.empty(B * T, D, device=dev, dtype=torch.bfloat16)
+        lse = torch.empty(B * H * T, device=dev)
+        K.attn_fwd(qkv, out, lse, B, T, H, Dh, False, drop_rate=rate, mask=mask)
+        delta = torch.empty(B * H * T, device=dev)
+        if delta_ready:
+            o4, d4 = out.float().reshape(B, T, H, Dh), do.float().reshape(B, T, H, Dh)
+            delta.copy_((o4 * d4).sum(-1).permute(0, 2, 1).reshape(-1))
+        dqkv = torch.zeros(B * T, 3 * D, device=dev, dtype=torch.bfloat16)
+        K.attn_bwd(qkv, out, do, lse, delta, dqkv, B, T, H, Dh, False, drop_rate=rate, mask=mask,
+                   delta_ready=delta_ready)
+        torch.cuda.synchronize()
+        res[short] = (out.float(), lse.clone(), dqkv.float(), delta.clone())
+    monkeypatch.delenv("PCV_ATTN_NO_SHORT", raising=False)
+    keep = torch.from_numpy(rng.keep_mask(99, 5, (T, T), rate)).to(dev) if rate > 0 else None
+    qf = qkv.float().requires_grad_(True)
+    ref = _attn_ref(qf, B, T, H, Dh, False, keep, rate)
+    ref.backward(do.float())
+    for short in (True, False):
+        out, lse, dqkv, delta = res[short]
+        assert (out - ref).abs().max().item() < 2e-2
+        err, scale = (dqkv - qf.grad).abs().max().item(), qf.grad.abs().max().item()
+        assert err < 3e-2 * max(1.0, scale), (short, err, scale)
+    a, b = res[True], res[False]
+    assert (a[0] - b[0]).abs().max().item() <= 1e-2
+    assert (a[1] - b[1]).abs().max().item() <= 1e-4
+    assert (a[2] - b[2]).abs().max().item() <= 2e-2 * max(1.0, b[2].abs().max().item())
+    assert (a[3] - b[3]).abs().max().item() <= 1e-2 * max(1.0, b[3].abs().max().item())   # from each path's bf16 O
+
+
 def test_layernorm_rmsnorm(dev):
     from plaincv_amd import kernels as K
     torch.manual_seed(1)

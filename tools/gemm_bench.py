@@ -16,6 +16,19 @@ def tm(fn, iters=20):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
+    if "--graph" in sys.argv:   # replay a captured graph of `iters` calls: kernel time without host launch cost
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(iters):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / iters * 1e-3
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
@@ -39,7 +52,11 @@ SHAPES = [("lm_head fwd", 16384, 50304, 768, "fwd"), ("qkv fwd", 16384, 2304, 76
           ("fc2 wgrad", 2048, 768, 16384, "wgrad"), ("out wgrad", 768, 768, 16384, "wgrad"),
           ("420M lm_head wgrad", 1024, 50280, 16384, "wgrad"), ("420M gate|up wgrad", 1024, 5472, 16384, "wgrad"),
           ("420M fc2 wgrad", 2736, 1024, 16384, "wgrad"), ("420M qkv wgrad", 1024, 3072, 16384, "wgrad"),
-          ("420M out wgrad", 1024, 1024, 16384, "wgrad")]
+          ("420M out wgrad", 1024, 1024, 16384, "wgrad"),
+          # ViT-small (B=64 x 257 tokens, d 128, mlp 256): weights [K][N] (N-contiguous), fp32 bias
+          ("vit qkv fwd", 16448, 384, 128, "fwdkn"), ("vit qkv fwd+bias", 16448, 384, 128, "fwdknb"),
+          ("vit fc1 fwd", 16448, 256, 128, "fwdkn"), ("vit fc2 fwd", 16448, 128, 256, "fwdkn"),
+          ("vit out fwd", 16448, 128, 128, "fwdkn")]
 
 FLT = sys.argv[1] if len(sys.argv) > 1 else ""
 REF = "--no-ref" not in sys.argv
@@ -47,7 +64,13 @@ for name, M, N, Kd, mode in SHAPES:
     if FLT not in name:
         continue
     bf = torch.bfloat16
-    if mode in ("fwd", "dgrad"):
+    if mode in ("fwdkn", "fwdknb"):
+        a, b = torch.randn(M, Kd, device=dev, dtype=bf), torch.randn(Kd, N, device=dev, dtype=bf)
+        c = torch.empty(M, N, device=dev, dtype=bf)
+        bias = torch.randn(N, device=dev) if mode == "fwdknb" else None
+        ours = lambda: K.gemm(a, b, c, bias=bias)  # noqa: E731
+        ref = lambda: torch.matmul(a, b, out=c)  # noqa: E731
+    elif mode in ("fwd", "dgrad"):
         a, b = torch.randn(M, Kd, device=dev, dtype=bf), torch.randn(N, Kd, device=dev, dtype=bf)
         c = torch.empty(M, N, device=dev, dtype=bf)
         ours = lambda: K.gemm(a, b, c, tb=True)  # noqa: E731
