@@ -295,7 +295,9 @@ def bench_lm(args):
     if args.lm_accum is None:
         args.lm_accum = spec["accum"]
     mb, accum = args.lm_micro_batch, args.lm_accum
-    model, mc, variables = construct_model(cfg)
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):   # stdout carries only the JSON line
+        model, mc, variables = construct_model(cfg)
     st = create_lm_state(cfg, model, variables, mb, dev, accum=accum)
     compute_grads, _ = make_train_fns()
     apply_grads = make_apply_grads_fn(spec["clip"])

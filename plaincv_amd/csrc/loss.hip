@@ -7,6 +7,7 @@
 // in the logits dtype (may alias the logits).  Per-row loss / correctness go to
 // [R] buffers reduced by a deterministic single-block sum (no float atomics).
 #include "common.h"
+#include <cstdlib>
 
 namespace pcv {
 
@@ -115,15 +116,38 @@ __global__ __launch_bounds__(256) void xent_stream_kernel(const T* logits, int64
     else s += __expf(v - m);
   };
   int c = threadIdx.x;
+  // main body per 4 x 16 B: the chunk max first (v_max only), then one rescale per chunk when it
+  // raises the running max (with its first position for the argmax), then one exp per element --
+  // the per-element absorb() branch diverged on every new maximum and cost a second exp
   for (; c + 3 * 256 < nv; c += 4 * 256) {
     u32x4 w[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) w[u] = *reinterpret_cast<const u32x4*>(z + (int64_t)(c + u * 256) * VE);
+    float cm = -3.0e38f;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const T* e = reinterpret_cast<const T*>(&w[u]);
 #pragma unroll
-      for (int q = 0; q < VE; ++q) absorb((float)e[q], (c + u * 256) * VE + q);
+      for (int q = 0; q < VE; ++q) cm = fmaxf(cm, (float)e[q]);
+    }
+    if (cm > m) {
+      s *= __expf(m - cm);
+      m = cm;
+      int pos = 0x7fffffff;
+#pragma unroll
+      for (int u = 3; u >= 0; --u) {
+        const T* e = reinterpret_cast<const T*>(&w[u]);
+#pragma unroll
+        for (int q = VE - 1; q >= 0; --q)
+          if ((float)e[q] == cm) pos = (c + u * 256) * VE + q;
+      }
+      am = pos;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const T* e = reinterpret_cast<const T*>(&w[u]);
+#pragma unroll
+      for (int q = 0; q < VE; ++q) s += __expf((float)e[q] - m);
     }
   }
   for (; c < nv; c += 256) {
@@ -203,6 +227,109 @@ __global__ __launch_bounds__(256) void xent_stream_kernel(const T* logits, int64
   }
 }
 
+// LM vocabulary rows (bf16, V <= 8 * 1024 * XR_CH): one 1024-thread block per row holds the whole
+// row in registers (<= XR_CH 16-B chunks per thread), so the row is read from HBM once and written
+// once (3.3 GB per 124M step instead of 5: the two-pass stream kernel's second read missed L2 at
+// ~25 MB of rows in flight per XCD).  Max + first argmax, then sum exp(z - max), then the
+// gradient, each over registers; block reductions through LDS.
+constexpr int XR_CH = 7;
+__global__ __launch_bounds__(1024, 1) void xent_reg_kernel(const bf16* logits, int64_t ld, const int* labels, int V,
+                                                           float* row_loss, float* row_correct, bf16* dlogits,
+                                                           int64_t ldd, float grad_scale) {
+  __shared__ float rm[16], rs[16];
+  __shared__ int ri[16];
+  const int64_t row = blockIdx.x;
+  const bf16* z = logits + row * ld;
+  const int nv = V / 8;
+  const int tid = threadIdx.x, w = tid >> 6;
+  bf16x8 x[XR_CH];
+#pragma unroll
+  for (int i = 0; i < XR_CH; ++i) {
+    const int c = tid + 1024 * i;
+    if (c < nv) x[i] = *reinterpret_cast<const bf16x8*>(z + (int64_t)c * 8);
+  }
+  // tail elements (V % 8) belong to thread 0
+  const int tail0 = nv * 8;
+  float m = -3.0e38f;
+  int am = 0x7fffffff;
+#pragma unroll
+  for (int i = 0; i < XR_CH; ++i) {
+    const int c = tid + 1024 * i;
+    if (c < nv) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float v = bf2f(x[i][q]);
+        if (v > m) { m = v; am = c * 8 + q; }   // increasing index order: strict > keeps the first
+      }
+    }
+  }
+  if (tid == 0)
+    for (int j = tail0; j < V; ++j) {
+      const float v = bf2f(z[j]);
+      if (v > m) { m = v; am = j; }
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64);
+    const int a2 = __shfl_xor(am, o, 64);
+    if (m2 > m || (m2 == m && a2 < am)) { m = m2; am = a2; }
+  }
+  if ((tid & 63) == 0) { rm[w] = m; ri[w] = am; }
+  __syncthreads();
+  float M = rm[0];
+  int A = ri[0];
+#pragma unroll
+  for (int i = 1; i < 16; ++i)
+    if (rm[i] > M || (rm[i] == M && ri[i] < A)) { M = rm[i]; A = ri[i]; }
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < XR_CH; ++i) {
+    const int c = tid + 1024 * i;
+    if (c < nv) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sum += __expf(bf2f(x[i][q]) - M);
+    }
+  }
+  if (tid == 0)
+    for (int j = tail0; j < V; ++j) sum += __expf(bf2f(z[j]) - M);
+  sum = wave_sum(sum);
+  if ((tid & 63) == 0) rs[w] = sum;
+  __syncthreads();
+  float S = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) S += rs[i];
+  const float lse = M + __logf(S);
+  const int y = labels[row];
+  const bool yok = y >= 0 && y < V;
+  if (tid == 0) {
+    row_loss[row] = yok ? lse - bf2f(z[y]) : 0.f;
+    row_correct[row] = (yok && A == y) ? 1.f : 0.f;
+  }
+  if (!dlogits) return;
+  __syncthreads();   // z[y] and the tail read above before an in-place overwrite
+  bf16* d = dlogits + row * ldd;
+#pragma unroll
+  for (int i = 0; i < XR_CH; ++i) {
+    const int c = tid + 1024 * i;
+    if (c < nv) {
+      bf16x8 o;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float p = __expf(bf2f(x[i][q]) - lse);
+        if (c * 8 + q == y) p -= 1.f;
+        o[q] = f2bf(p * grad_scale);
+      }
+      *reinterpret_cast<bf16x8*>(d + (int64_t)c * 8) = o;
+    }
+  }
+  if (tid == 0)
+    for (int j = tail0; j < V; ++j) {
+      float p = __expf(bf2f(z[j]) - lse);
+      if (j == y) p -= 1.f;
+      d[j] = f2bf(p * grad_scale);
+    }
+}
+
 // out[0] = scale * sum(x[0..n)), out[1] = scale2 * sum(y[0..n)) (y optional); one block, deterministic
 __global__ __launch_bounds__(1024) void mean2_kernel(const float* x, const float* y, int64_t n, float scale,
                                                      float* out) {
@@ -226,6 +353,11 @@ extern "C" int pcv_xent_fwd_bwd(const void* logits, int64_t ld, int logits_f32, 
   const size_t es = logits_f32 ? 4 : 2;
   const bool aligned = pcv_aligned16(logits) && ((ld * es) % 16 == 0) &&
                        (!dlogits || (pcv_aligned16(dlogits) && (ldd * es) % 16 == 0));
+  if (V >= 4096 && V <= 8 * 1024 * XR_CH && aligned && !logits_f32 && getenv("PCV_XENT_STREAM") == nullptr) {
+    hipLaunchKernelGGL(xent_reg_kernel, dim3((unsigned)R), dim3(1024), 0, s, (const bf16*)logits, ld, labels, (int)V,
+                       row_loss, row_correct, (bf16*)dlogits, ldd, grad_scale);
+    return pcv_launch_status();
+  }
   if (V >= 4096 && aligned) {   // streaming kernel (large vocabulary)
     if (logits_f32)
       hipLaunchKernelGGL(xent_stream_kernel<float>, dim3((unsigned)R), dim3(256), 0, s, (const float*)logits, ld,

@@ -235,6 +235,20 @@ def test_rope_swiglu_xent_embed(dev):
     loss.mean().backward()
     assert torch.allclose(d2.float(), lf.grad, atol=1e-4)
     assert torch.equal(rc2, (lf.argmax(-1) == lab.long()).float())
+    # planted ties: accuracy counts the FIRST maximal index (torch.argmax / jnp.argmax)
+    buf3 = torch.randn(R, 50264, device=dev).to(torch.bfloat16)
+    lg3 = buf3[:, :V]
+    j1 = torch.randint(0, V // 2, (R,), device=dev)
+    j2 = j1 + torch.randint(1, V // 2, (R,), device=dev)
+    rows = torch.arange(R, device=dev)
+    lg3[rows, j1] = 8.0
+    lg3[rows, j2] = 8.0
+    lab3 = torch.where(rows % 2 == 0, j1, j2).to(torch.int32)
+    rl3, rc3 = torch.empty(R, device=dev), torch.empty(R, device=dev)
+    K.xent(lg3, lab3, rl3, rc3, None, grad_scale=1.0)
+    assert torch.equal(rc3, (rows % 2 == 0).float())
+    assert torch.allclose(rl3, torch.nn.functional.cross_entropy(lg3.float(), lab3.long(), reduction="none"),
+                          atol=1e-3, rtol=1e-4)
     # embedding
     Vv, Dd = 1000, 64
     tab = torch.randn(Vv, Dd, device=dev).to(torch.bfloat16)
