@@ -18,6 +18,7 @@
 // Ragged M/N/K are zero-filled on load and masked on store.  blockIdx.x is
 // remapped so each XCD gets a contiguous run of tiles, grouped 8 along M.
 #include "common.h"
+#include <cstdlib>
 
 extern "C" int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
                                int64_t ldb);
@@ -1178,12 +1179,17 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
   if (trans_a && !trans_b && out_f32 && beta == 1.f && batch == 1 && !bias && !res && !aux && act == EPI_NONE &&
       g.drop_thresh == 0 && !colsum && !attn_delta && pcv_aligned16(C) && pcv_gemm_big_wgrad_ok(M, N, K, A, lda, B, ldb))
     return pcv_gemm_big_wgrad(A, B, (float*)C, M, N, K, lda, ldb, ldc, alpha, stream);
-  // tile: 128x128 when that grid covers the chip, else 64x64.  (A 256x256 tile with
+  // tile: 128x128 when that grid covers the chip and K is deep, else 64x64.  (A 256x256 tile with
   // one 128x128 block per wave was measured 15-45 % slower at the LM shapes: it needs
   // all 512 registers, spills, and runs one wave per SIMD.)
   const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128) * batch * g.split_k;
-  hipError_t e = t128 >= 240 ? launch_sz<4, 4>(g, trans_a, trans_b, (int)batch, s)
-                             : launch_sz<2, 2>(g, trans_a, trans_b, (int)batch, s);
+  static const int tile_env = getenv("PCV_GEMM_TILE") ? atoi(getenv("PCV_GEMM_TILE")) : 0;   // 64 / 128: A/B runs
+  // 128x128 only for deep products: at K <= 384 (every ViT GEMM) a 128x128 tile is 2-6 k-tiles of
+  // prologue/epilogue-bound work at 2 workgroups per CU; the 64x64 tile runs 4 per CU (ViT C2 step
+  // 0.899 -> 0.863 ms with every GEMM on 64x64)
+  const bool big_tile = tile_env ? tile_env == 128 : (t128 >= 240 && K >= 512);
+  hipError_t e = big_tile ? launch_sz<4, 4>(g, trans_a, trans_b, (int)batch, s)
+                          : launch_sz<2, 2>(g, trans_a, trans_b, (int)batch, s);
   return e == hipSuccess ? 0 : (int)e;
 }
 
