@@ -1024,8 +1024,10 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
       }
     }
   } else {
-    // ---- dQ of queries 16*gq .. +15 (lane & 15), over all keys
-    for (int gq = wave - 8; gq < NB; gq += 8) {
+    // ---- dQ of queries 16*gq .. +15 (lane & 15), over all keys.  Query group gq goes to wave
+    // 8 + ((gq + 1) & 7): with NB = 17 the third item lands on wave 9 (SIMD of wave 1), not on
+    // wave 8, which shares a SIMD with wave 0 that already holds the third key block
+    for (int gq = (wave - 9) & 7; gq < NB; gq += 8) {
       const int q0 = gq * 16;
       const int myq = q0 + (lane & 15);
       const bf16x8 qf = row_frag<DH>(Qs, q0, 0);
