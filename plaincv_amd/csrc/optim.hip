@@ -117,6 +117,9 @@ __global__ __launch_bounds__(256) void muon_norm_kernel(const MuonMat* mats, flo
 // u = -lr*(O*shape_scale + wd*p); p += u
 __global__ __launch_bounds__(256) void muon_apply_kernel(const MuonMat* mats, MuonHyper h) {
   const MuonMat M = mats[blockIdx.y];
+  // the matrix's sum of squares was last read by the NS normalisation: reset it for the next step
+  // here instead of a separate fill launch (muon_prep accumulates into it with atomics)
+  if (blockIdx.x == 0 && threadIdx.x == 0) *M.norm2 = 0.f;
   const int64_t n = M.rows * M.cols;
   const bool tr = M.rows > M.cols;
   const float ss = h.shape_scale > 0.f ? sqrtf(fmaxf(1.f, (float)M.cols / (float)M.rows)) : 1.f;

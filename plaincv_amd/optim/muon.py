@@ -135,8 +135,7 @@ class Muon(GradientTransformation):
                      stream_ptr())
 
     def _run(self, store, st, gscale, apply):
-        if st.routed:
-            st.norm2.zero_()
+        if st.routed:   # st.norm2 is zero here: created zeroed, reset by pcv_muon_apply after use
             hip.call("pcv_muon_prep", ptr(st.mats_apply), len(st.routed), st.n_general, st.max_elems, self.beta,
                      int(self.nesterov), self.eps, ptr(st.count), ptr(gscale), stream_ptr())
             self._newton_schulz(st)
