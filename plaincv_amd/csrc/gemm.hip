@@ -1236,7 +1236,12 @@ extern "C" int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, in
   g.ln_x = ln_x; g.ld_lnx = ld_lnx; g.ln_dscale = ln_dscale; g.ln_dbias = ln_dbias; g.colsum = colsum;
   g.col_reps = col_reps;
   // 64 x 128 tiles (a 32-row tile doubles every workgroup's weight traffic: measured slower)
-  hipError_t e = launch_sz<2, 4>(g, trans_a, trans_b, 1, (hipStream_t)stream);
+  // PCV_LN_TILE=32: 32x128 tiles (514 workgroups at the ViT's 16448 rows instead of 257).  Measured:
+  // ViT C2 step 0.858 -> 0.852 ms, but each launch alone 16.9 -> 21.7 us back to back (the per-column
+  // LN-parameter atomics double), so the 64x128 tile stays the default.
+  static const int ln32 = getenv("PCV_LN_TILE") ? atoi(getenv("PCV_LN_TILE")) == 32 : 0;
+  hipError_t e = ln32 ? launch_sz<1, 4>(g, trans_a, trans_b, 1, (hipStream_t)stream)
+                      : launch_sz<2, 4>(g, trans_a, trans_b, 1, (hipStream_t)stream);
   return e == hipSuccess ? 0 : (int)e;
 }
 
