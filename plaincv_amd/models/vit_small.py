@@ -13,6 +13,7 @@ LayerNorm statistics, softmax and every gradient reduction stay fp32
 """
 import contextlib
 import math
+import os
 
 import torch
 
@@ -232,7 +233,7 @@ class ViTRunner:
                 items.append(("colsum", self.dlogits, self.gbh))
             # Column accumulators written by every row tile of a GEMM epilogue (bias and LayerNorm
             # parameter gradients) go to 32 replica rows, folded into the gradients by the same launch
-            self.reps = 32
+            self.reps = int(os.environ.get("PCV_COL_REPS", "32"))
 
             def replicate(key, target):
                 ws = torch.zeros(self.reps, target.numel(), dtype=f32, device=dev)
