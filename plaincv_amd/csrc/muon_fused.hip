@@ -25,22 +25,33 @@ namespace {
 
 constexpr int MF_THREADS = 512, MF_WAVES = 8;
 constexpr int MF_RMAX = 128, MF_CMAX = 256;
-constexpr int MF_LDX = MF_CMAX + 8, MF_LDA = MF_RMAX + 8;   // padded rows (elements)
+constexpr int MF_LDX = MF_CMAX, MF_LDA = MF_RMAX;   // unpadded rows (elements); XOR-swizzled, see mf_off
 constexpr size_t MF_LDS = (size_t)MF_RMAX * MF_LDX * 2 + 2 * (size_t)MF_RMAX * MF_LDA * 2;
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
+// Images are unpadded [rows][ld] with the 16-B chunks of row r XOR-permuted by h(r mod 16), h
+// linear over GF(2) with h(1,2,4,8) = (2,4,8,9), found by exhaustive search so that all access
+// shapes are bank-conflict-free on the gfx950 LDS lane groups: 16-B row fragments
+// (ds_read_b128), 8-B k-permuted row fragments, transposing 8-B reads (ds_read_b64_tr_b16) and
+// the transposed 8-B tile stores (16 consecutive rows, one column).  The padded-row layout it
+// replaces could not satisfy all of them (48 % of LDS cycles in bank conflicts, rocprofv3).
+__device__ __forceinline__ int mf_h(int r) { return ((r & 7) << 1) ^ ((r & 8) ? 9 : 0); }
+__device__ __forceinline__ int mf_off(int r, int c, int ld) {
+  return r * ld + ((((c >> 3) ^ mf_h(r & 15))) << 3) + (c & 7);
+}
+
 // 16 rows x 32 k (row-major image, k contiguous): lane l -> row l&15, k = 8*(l>>4) .. +8
 __device__ __forceinline__ bf16x8 frag_rows(const bf16* lds, int ld, int row0, int ks) {
   const int l = threadIdx.x & 63;
-  return *reinterpret_cast<const bf16x8*>(lds + (row0 + (l & 15)) * ld + ks * 32 + 8 * (l >> 4));
+  return *reinterpret_cast<const bf16x8*>(lds + mf_off(row0 + (l & 15), ks * 32 + 8 * (l >> 4), ld));
 }
 // same rows, k in the kappa order of frag_tr: k = 32s + 4g + j (j<4), 32s + 16 + 4g + j-4 (j>=4)
 __device__ __forceinline__ bf16x8 frag_rows_kappa(const bf16* lds, int ld, int row0, int s) {
   const int l = threadIdx.x & 63, g = l >> 4;
-  const bf16* p = lds + (row0 + (l & 15)) * ld + 32 * s + 4 * g;
-  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(p);
-  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(p + 16);
+  const int r = row0 + (l & 15);
+  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(lds + mf_off(r, 32 * s + 4 * g, ld));
+  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(lds + mf_off(r, 32 * s + 4 * g + 16, ld));
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 // k running over ROWS of a row-major image (kappa order), the 16 columns c0.. on the lane,
@@ -48,8 +59,8 @@ __device__ __forceinline__ bf16x8 frag_rows_kappa(const bf16* lds, int ld, int r
 __device__ __forceinline__ bf16x8 frag_tr(const bf16* lds, int ld, int s, int c0) {
   const int l = threadIdx.x & 63;
   const int g = l >> 4, w = l & 15, q = w >> 2, p = w & 3;
-  const bf16* a0 = lds + (32 * s + 4 * g + q) * ld + c0 + 4 * p;
-  const bf16* a1 = a0 + 16 * ld;
+  const bf16* a0 = lds + mf_off(32 * s + 4 * g + q, c0 + 4 * p, ld);
+  const bf16* a1 = a0 + 16 * ld;   // row + 16: same swizzle
   const bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
   const bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a1));
   return bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
@@ -144,7 +155,7 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
       for (int e = 0; e < 4; ++e)
         if (c4 + e >= cx) v[e] = 0.f;
     }
-    st4(X + r * MF_LDX + c4, v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
+    st4(X + mf_off(r, c4, MF_LDX), v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
   }
   for (int i = tid; i < 2 * MF_RMAX * MF_LDA / 8; i += MF_THREADS)
     reinterpret_cast<u32x4*>(A)[i] = u32x4{0u, 0u, 0u, 0u};
@@ -171,11 +182,11 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
           for (int j = 0; j < 2; ++j) {
             // lane holds C[(rt0+i)*16 + 4g + r][(ct0+j)*16 + (l&15)], r = 0..3 -> write C^T
             const int trow = (ct0 + j) * 16 + (lane & 15), tcol = (rt0 + i) * 16 + 4 * g;
-            bf16* dst = out + trow * MF_LDA + tcol;
+            bf16* dst = out + mf_off(trow, tcol, MF_LDA);
             if (pass == 0) {
               st4(dst, ns_b * acc[i][j][0], ns_b * acc[i][j][1], ns_b * acc[i][j][2], ns_b * acc[i][j][3]);
             } else {
-              const bf16x4 a4 = *reinterpret_cast<const bf16x4*>(A + trow * MF_LDA + tcol);
+              const bf16x4 a4 = *reinterpret_cast<const bf16x4*>(A + mf_off(trow, tcol, MF_LDA));
               st4(dst, fmaf(cb2, acc[i][j][0], bf2f(a4[0])), fmaf(cb2, acc[i][j][1], bf2f(a4[1])),
                   fmaf(cb2, acc[i][j][2], bf2f(a4[2])), fmaf(cb2, acc[i][j][3], bf2f(a4[3])));
             }
@@ -202,7 +213,7 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const bf16x4 x4 =
-              *reinterpret_cast<const bf16x4*>(X + ((rt0 + j) * 16 + (lane & 15)) * MF_LDX + (ct0 + i) * 16 + 4 * g);
+              *reinterpret_cast<const bf16x4*>(X + mf_off((rt0 + j) * 16 + (lane & 15), (ct0 + i) * 16 + 4 * g, MF_LDX));
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[q][i][j][r] = fmaf(ns_a, bf2f(x4[r]), acc[q][i][j][r]);
         }
@@ -220,7 +231,7 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
           const int row = (rt0 + j) * 16 + (lane & 15), col = (ct0 + i) * 16 + 4 * g;
           // rows >= rp / columns >= cp of the padded image must stay zero
           if (row < rp && col < cp)
-            st4(X + row * MF_LDX + col, acc[q][i][j][0], acc[q][i][j][1], acc[q][i][j][2], acc[q][i][j][3]);
+            st4(X + mf_off(row, col, MF_LDX), acc[q][i][j][0], acc[q][i][j][1], acc[q][i][j][2], acc[q][i][j][3]);
         }
     }
     __syncthreads();
@@ -230,7 +241,8 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
   bf16* xo = const_cast<bf16*>(M.xo);
   for (int i = tid; i < rx * (ldx / 4); i += MF_THREADS) {
     const int r = i / (ldx / 4), c4 = (i % (ldx / 4)) * 4;
-    if (c4 < cx) *reinterpret_cast<bf16x4*>(xo + (int64_t)r * ldx + c4) = *reinterpret_cast<const bf16x4*>(X + r * MF_LDX + c4);
+    if (c4 < cx)
+      *reinterpret_cast<bf16x4*>(xo + (int64_t)r * ldx + c4) = *reinterpret_cast<const bf16x4*>(X + mf_off(r, c4, MF_LDX));
   }
 }
 
