@@ -1081,39 +1081,33 @@ static bool short_ok(const AttnArgs& a, int dh, int causal, bool) {
          getenv("PCV_ATTN_NO_SHORT") == nullptr;
 }
 template <int NT, bool D>
-static void launch_short_fwd_nt(const AttnArgs& a, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_short_fwd_kernel<NT, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sh_fwd_lds<NT>(D));
-    attr = true;
-  }
+static int launch_short_fwd_nt(const AttnArgs& a, hipStream_t s) {
+  static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
+  if (const int e = optin.ensure((const void*)attn_short_fwd_kernel<NT, D>, (int)((int)sh_fwd_lds<NT>(D)))) return e;
   hipLaunchKernelGGL((attn_short_fwd_kernel<NT, D>), dim3(a.H, a.B), dim3(SH_THREADS), sh_fwd_lds<NT>(D), s, a);
+  return 0;
 }
 template <bool D>
-static void launch_short_fwd(const AttnArgs& a, hipStream_t s) {
+static int launch_short_fwd(const AttnArgs& a, hipStream_t s) {
   switch ((a.T + 31) / 32) {
-    case 1: launch_short_fwd_nt<2, D>(a, s); break;
-    case 2: launch_short_fwd_nt<4, D>(a, s); break;
-    case 3: launch_short_fwd_nt<6, D>(a, s); break;
-    case 4: launch_short_fwd_nt<8, D>(a, s); break;
-    case 5: launch_short_fwd_nt<10, D>(a, s); break;
-    case 6: launch_short_fwd_nt<12, D>(a, s); break;
-    case 7: launch_short_fwd_nt<14, D>(a, s); break;
-    case 8: launch_short_fwd_nt<16, D>(a, s); break;
-    case 9: launch_short_fwd_nt<18, D>(a, s); break;
-    default: launch_short_fwd_nt<20, D>(a, s); break;
+    case 1: return launch_short_fwd_nt<2, D>(a, s);
+    case 2: return launch_short_fwd_nt<4, D>(a, s);
+    case 3: return launch_short_fwd_nt<6, D>(a, s);
+    case 4: return launch_short_fwd_nt<8, D>(a, s);
+    case 5: return launch_short_fwd_nt<10, D>(a, s);
+    case 6: return launch_short_fwd_nt<12, D>(a, s);
+    case 7: return launch_short_fwd_nt<14, D>(a, s);
+    case 8: return launch_short_fwd_nt<16, D>(a, s);
+    case 9: return launch_short_fwd_nt<18, D>(a, s);
+    default: return launch_short_fwd_nt<20, D>(a, s);
   }
 }
 template <bool D>
-static void launch_short_bwd(const AttnArgs& a, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_short_bwd_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)SH_BWD_LDS);
-    attr = true;
-  }
+static int launch_short_bwd(const AttnArgs& a, hipStream_t s) {
+  static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
+  if (const int e = optin.ensure((const void*)attn_short_bwd_kernel<D>, (int)((int)SH_BWD_LDS))) return e;
   hipLaunchKernelGGL((attn_short_bwd_kernel<D>), dim3(a.H, a.B), dim3(SH_THREADS), SH_BWD_LDS, s, a);
+  return 0;
 }
 
 template <int DH, bool C, bool D>
@@ -1135,9 +1129,9 @@ static void launch_bwd(const AttnArgs& a, hipStream_t s) {
 template <bool FWD>
 static int dispatch(const AttnArgs& a, int dh, int causal, int drop, hipStream_t s) {
   if (short_ok(a, dh, causal, FWD)) {
-    if (FWD) { drop ? launch_short_fwd<true>(a, s) : launch_short_fwd<false>(a, s); }
-    else { drop ? launch_short_bwd<true>(a, s) : launch_short_bwd<false>(a, s); }
-    return pcv_launch_status();
+    const int e = FWD ? (drop ? launch_short_fwd<true>(a, s) : launch_short_fwd<false>(a, s))
+                      : (drop ? launch_short_bwd<true>(a, s) : launch_short_bwd<false>(a, s));
+    return e ? e : pcv_launch_status();
   }
 #define PCV_ATT(DHV, CV, DV) \
   if (dh == DHV && causal == CV && drop == DV) { FWD ? launch_fwd<DHV, CV, DV>(a, s) : launch_bwd<DHV, CV, DV>(a, s); return pcv_launch_status(); }

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -83,3 +85,22 @@ static inline int pcv_launch_status() {
   return e == hipSuccess ? 0 : (int)e;
 }
 static inline bool pcv_aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// Opt-in to > 64 KiB of dynamic LDS for one kernel, once per device (std::call_once per device
+// slot: thread-safe, and a process driving several GPUs sets the attribute on each).  Returns 0
+// or the hipError_t of hipFuncSetAttribute, which the entry point returns to its caller instead
+// of letting the launch fail later with an opaque error.  Call sites hold one static instance
+// per kernel (function-template statics are per instantiation).
+struct PcvLdsOptIn {
+  static constexpr int kMaxDev = 64;
+  std::once_flag once[kMaxDev];
+  int err[kMaxDev] = {};
+  int ensure(const void* fn, int bytes) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return (int)hipErrorInvalidDevice;
+    std::call_once(once[dev], [&] {
+      err[dev] = (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    });
+    return err[dev];
+  }
+};

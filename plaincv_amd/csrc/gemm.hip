@@ -1083,12 +1083,8 @@ static hipError_t launch_t(const GemmArgs& a, int batch, hipStream_t s) {
   g.tiles_n = (int)((g.N + BN - 1) / BN);
   constexpr size_t lds = gemm_lds<WM, WN>();
   dim3 grid(g.tiles_m * g.tiles_n, batch, g.split_k > 1 ? g.split_k : 1);
-  static bool attr = false;  // > 64 KiB of dynamic LDS must be opted into once per kernel
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<AK, BK, WM, WN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
-    attr = true;
-  }
+  static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
+  if (const int e = optin.ensure((const void*)gemm_bf16_kernel<AK, BK, WM, WN>, (int)((int)lds))) return (hipError_t)e;
   hipLaunchKernelGGL((gemm_bf16_kernel<AK, BK, WM, WN>), grid, dim3(256), lds, s, g);
   return hipGetLastError();
 }
@@ -1319,22 +1315,19 @@ extern "C" int pcv_gemm_grouped_plan(const void* descs, int n, int tile, void* p
 }
 
 template <int W>
-static void grouped_launch(const void* plan_dev, int n, int64_t total_blocks, hipStream_t s) {
+static int grouped_launch(const void* plan_dev, int n, int64_t total_blocks, hipStream_t s) {
   constexpr size_t lds = gemm_lds<W, W, GroupedStages<W>::S>();
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_grouped_kernel<false, false, W, W>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
+  static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
+  if (const int e = optin.ensure((const void*)gemm_grouped_kernel<false, false, W, W>, (int)((int)lds))) return e;
   const size_t off = (n * sizeof(GemmArgs) + 255) / 256 * 256;
   hipLaunchKernelGGL((gemm_grouped_kernel<false, false, W, W>), dim3((unsigned)total_blocks), dim3(256), lds, s,
                      (const GemmArgs*)plan_dev, (const int*)((const char*)plan_dev + off), n);
+  return 0;
 }
 
 extern "C" int pcv_gemm_grouped_run(const void* plan_dev, int n, int tile, int64_t total_blocks, void* stream) {
   if (n <= 0 || total_blocks <= 0 || !plan_dev || (tile != 64 && tile != 128)) return PCV_EINVAL;
-  if (tile == 64) grouped_launch<2>(plan_dev, n, total_blocks, (hipStream_t)stream);
-  else grouped_launch<4>(plan_dev, n, total_blocks, (hipStream_t)stream);
-  return pcv_launch_status();
+  const int e = tile == 64 ? grouped_launch<2>(plan_dev, n, total_blocks, (hipStream_t)stream)
+                           : grouped_launch<4>(plan_dev, n, total_blocks, (hipStream_t)stream);
+  return e ? e : pcv_launch_status();
 }

@@ -468,14 +468,11 @@ extern "C" int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, i
 }
 
 template <int BN>
-static void launch_big(const BigArgs& g, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_big_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              GbCfg<BN>::LDS);
-    attr = true;
-  }
+static int launch_big(const BigArgs& g, hipStream_t s) {
+  static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
+  if (const int e = optin.ensure((const void*)gemm_big_kernel<BN>, (int)(GbCfg<BN>::LDS))) return e;
   hipLaunchKernelGGL(gemm_big_kernel<BN>, dim3(g.tiles_m * g.tiles_n), dim3(512), GbCfg<BN>::LDS, s, g);
+  return 0;
 }
 
 extern "C" int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
@@ -490,9 +487,8 @@ extern "C" int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, in
   const int bn = big_bn(M, N) == 192 ? 192 : 256;
   g.tiles_m = (int)((M + GB_T - 1) / GB_T);
   g.tiles_n = (int)((N + bn - 1) / bn);
-  if (bn == 192) launch_big<192>(g, (hipStream_t)stream);
-  else launch_big<256>(g, (hipStream_t)stream);
-  return pcv_launch_status();
+  const int e = bn == 192 ? launch_big<192>(g, (hipStream_t)stream) : launch_big<256>(g, (hipStream_t)stream);
+  return e ? e : pcv_launch_status();
 }
 
 // ---------------------------------------------------------------- weight-gradient entry ----
@@ -542,11 +538,8 @@ extern "C" int pcv_gemm_big_wgrad(const void* A, const void* B, float* C, int64_
   const int s = forced > 0 ? forced : wgrad_splits((int64_t)g.tiles_m * g.tiles_n, K);
   g.kps = (int)(((K + s - 1) / s + 31) / 32 * 32);
   const int nsplit = (int)((K + g.kps - 1) / g.kps);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_big_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, GW_LDS);
-    attr = true;
-  }
+  static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
+  if (const int e = optin.ensure((const void*)gemm_big_wgrad_kernel, (int)(GW_LDS))) return e;
   hipLaunchKernelGGL(gemm_big_wgrad_kernel, dim3(g.tiles_m * g.tiles_n, nsplit), dim3(512), GW_LDS,
                      (hipStream_t)stream, g);
   return pcv_launch_status();

@@ -371,12 +371,10 @@ extern "C" int pcv_xent_fwd_bwd(const void* logits, int64_t ld, int logits_f32, 
   if (lds > 150 * 1024) return PCV_EINVAL;  // row must fit in LDS (V <= ~76k bf16 / 38k fp32)
   const int vec = pcv_aligned16(logits) && ((ld * es) % 16 == 0) &&
                   (!dlogits || (pcv_aligned16(dlogits) && (ldd * es) % 16 == 0));
-  static bool attr = false;  // > 64 KiB of dynamic LDS must be opted into once
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)xent_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    (void)hipFuncSetAttribute((const void*)xent_kernel<bf16>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    attr = true;
-  }
+  static PcvLdsOptIn optin_f32, optin_bf16;  // > 64 KiB of dynamic LDS: opt in once per device
+  if (const int e = logits_f32 ? optin_f32.ensure((const void*)xent_kernel<float>, 150 * 1024)
+                               : optin_bf16.ensure((const void*)xent_kernel<bf16>, 150 * 1024))
+    return e;
   if (logits_f32)
     hipLaunchKernelGGL(xent_kernel<float>, dim3((unsigned)R), dim3(512), lds, s, (const float*)logits, ld, labels, R,
                        V, row_loss, row_correct, (float*)dlogits, ldd, grad_scale, vec);

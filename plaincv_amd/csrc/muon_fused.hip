@@ -9,8 +9,18 @@
 //
 // Input: the un-normalised fp32 X written by muon_prep_kernel (x32, [r'][ldx]) and its
 // squared Frobenius norm; output: bf16 X_ns (xo, [r'][ldx]) read by muon_apply_kernel.
-// Numerics follow the general path: X, A' = b X X^T and B = (c/b^2) A'A' + A' are bf16
-// (fp32 MFMA accumulation) and X' = B X + a X is rounded to bf16 each iteration.
+// Numerics (same as the general path): the MFMA operands X, A' = b X X^T and
+// B = (c/b^2) A'A' + A' are bf16 with fp32 accumulation, but X itself is CARRIED in fp32
+// across iterations: X' = B bf16(X) + a X with the a X term in fp32.  Rounding X to bf16
+// every iteration (the round-1 numerics) was measured to dominate the error against fp32
+// NS5 on real gradients (4-17 % rel-Frobenius; carrying X: 0.3-1.3 %, inside SURVEY §8c's
+// 2e-2).  The fp32 X is held as hi (the bf16 LDS image, the MFMA operand)
+// plus lo = bf16(X - hi) in registers of the lane that produces that element of X' (the
+// block-to-wave assignment is fixed across iterations): +32 VGPRs, no extra LDS.  B, the
+// other operand of X' = B X, is likewise stored as hi + lo images and X' takes two MFMAs
+// per fragment pair (+40 % MFMA work, within the launch's latency); A' stays bf16.
+// Measured vs fp32 NS5 (tests/test_optim_parity_gpu.py): round-1 numerics 2.2-5.6 % on
+// the test cases, carry + B hi/lo <= 1.3 %.
 //
 // A' and B are symmetric, which the kernel uses three ways: their B-operand fragments are
 // read as rows (k contiguous); a 16x16 result tile is stored transposed (4 consecutive
@@ -26,7 +36,8 @@ namespace {
 constexpr int MF_THREADS = 512, MF_WAVES = 8;
 constexpr int MF_RMAX = 128, MF_CMAX = 256;
 constexpr int MF_LDX = MF_CMAX, MF_LDA = MF_RMAX;   // unpadded rows (elements); XOR-swizzled, see mf_off
-constexpr size_t MF_LDS = (size_t)MF_RMAX * MF_LDX * 2 + 2 * (size_t)MF_RMAX * MF_LDA * 2;
+// X + A' + B (hi) + B (lo) = 64 + 3 x 32 KiB = 160 KiB: the whole LDS of a CU (one workgroup may declare it)
+constexpr size_t MF_LDS = (size_t)MF_RMAX * MF_LDX * 2 + 3 * (size_t)MF_RMAX * MF_LDA * 2;
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
@@ -97,33 +108,46 @@ __device__ __forceinline__ void gram_block(const bf16* L, int ld, int rt0, int c
   }
 }
 
-// C(4x2 tiles) = X^T[rows ct0*16..+64) . Bm[.., cols rt0*16..+32) over k = 0 .. 32*ssteps  (= (Bm X)^T)
-__device__ __forceinline__ void xtb_block(const bf16* X, const bf16* Bm, int ct0, int rt0, int ssteps,
+// C(4x2 tiles) = X^T[rows ct0*16..+64) . (Bh + Bl)[.., cols rt0*16..+32) over k = 0 .. 32*ssteps
+// (= (B X)^T with B = Bh + Bl carried at ~16 mantissa bits: two MFMAs per fragment pair)
+__device__ __forceinline__ void xtb_block(const bf16* X, const bf16* Bh, const bf16* Bl, int ct0, int rt0, int ssteps,
                                           f32x4 (&acc)[4][2]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 a[4], b[2];
+  bf16x8 a[4], b[2], bl[2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) a[i] = frag_tr(X, MF_LDX, 0, (ct0 + i) * 16);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) b[j] = frag_rows_kappa(Bm, MF_LDA, (rt0 + j) * 16, 0);
+  for (int j = 0; j < 2; ++j) {
+    b[j] = frag_rows_kappa(Bh, MF_LDA, (rt0 + j) * 16, 0);
+    bl[j] = frag_rows_kappa(Bl, MF_LDA, (rt0 + j) * 16, 0);
+  }
   for (int s = 0; s < ssteps; ++s) {
-    bf16x8 an[4], bn[2];
+    bf16x8 an[4], bn[2], bln[2];
     const int sn = s + 1 < ssteps ? s + 1 : s;
 #pragma unroll
     for (int i = 0; i < 4; ++i) an[i] = frag_tr(X, MF_LDX, sn, (ct0 + i) * 16);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bn[j] = frag_rows_kappa(Bm, MF_LDA, (rt0 + j) * 16, sn);
+    for (int j = 0; j < 2; ++j) {
+      bn[j] = frag_rows_kappa(Bh, MF_LDA, (rt0 + j) * 16, sn);
+      bln[j] = frag_rows_kappa(Bl, MF_LDA, (rt0 + j) * 16, sn);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = MFMA16(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < 2; ++j) {
+        acc[i][j] = MFMA16(a[i], b[j], acc[i][j]);
+        acc[i][j] = MFMA16(a[i], bl[j], acc[i][j]);
+      }
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = an[i];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) b[j] = bn[j];
+    for (int j = 0; j < 2; ++j) {
+      b[j] = bn[j];
+      bl[j] = bln[j];
+    }
   }
 }
 
@@ -136,7 +160,8 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
   extern __shared__ __attribute__((aligned(16))) char smem_m[];
   bf16* X = reinterpret_cast<bf16*>(smem_m);                       // [128][MF_LDX]
   bf16* A = X + MF_RMAX * MF_LDX;                                  // [128][MF_LDA]
-  bf16* Bm = A + MF_RMAX * MF_LDA;                                 // [128][MF_LDA]
+  bf16* Bm = A + MF_RMAX * MF_LDA;                                 // [128][MF_LDA]  B (hi)
+  bf16* Bl = Bm + MF_RMAX * MF_LDA;                                // [128][MF_LDA]  B - hi (lo)
   const MuonMat M = mats[blockIdx.x];
   const int rx = (int)(M.rows < M.cols ? M.rows : M.cols), cx = (int)(M.rows < M.cols ? M.cols : M.rows);
   const int ldx = (int)M.ldx;
@@ -157,13 +182,39 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
     }
     st4(X + mf_off(r, c4, MF_LDX), v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv);
   }
-  for (int i = tid; i < 2 * MF_RMAX * MF_LDA / 8; i += MF_THREADS)
+  for (int i = tid; i < 3 * MF_RMAX * MF_LDA / 8; i += MF_THREADS)
     reinterpret_cast<u32x4*>(A)[i] = u32x4{0u, 0u, 0u, 0u};
-  __syncthreads();
 
   const int nrt = rp / 16, nct = cp / 16;
   const int bcols_sq = (nrt + 1) / 2, nblk_sq = ((nrt + 3) / 4) * bcols_sq;
   const int bcols_x = (nrt + 1) / 2, nblk_x = ((nct + 3) / 4) * bcols_x;
+  // lo part of this lane's X' elements: X'[row (rt0+j)*16 + (l&15)][cols (ct0+i)*16 + 4g .. +3]
+  // of its blocks blk = wave + 8q (<= 2 per wave: nblk_x <= 16 at 128 x 256)
+  bf16x4 xlo[2][4][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int blk = wave + q * MF_WAVES;
+    const int ct0 = (blk / bcols_x) * 4, rt0 = (blk % bcols_x) * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = (rt0 + j) * 16 + (lane & 15), col = (ct0 + i) * 16 + 4 * g;
+        f32x4v v = f32x4v{0.f, 0.f, 0.f, 0.f};
+        if (blk < nblk_x && row < rx && col < cx) {
+          v = *reinterpret_cast<const f32x4v*>(M.x32 + (int64_t)row * ldx + col);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (col + e >= cx) v[e] = 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = v[e] * inv;
+          xlo[q][i][j][e] = f2bf(x - bf2f(f2bf(x)));
+        }
+      }
+  }
+  __syncthreads();
   const float cb2 = ns_c / (ns_b * ns_b);
   for (int it = 0; it < ns_steps; ++it) {
     // A' = b X X^T, then B = (c/b^2) A'A' + A'   (symmetric: tiles stored transposed)
@@ -186,9 +237,17 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
             if (pass == 0) {
               st4(dst, ns_b * acc[i][j][0], ns_b * acc[i][j][1], ns_b * acc[i][j][2], ns_b * acc[i][j][3]);
             } else {
-              const bf16x4 a4 = *reinterpret_cast<const bf16x4*>(A + mf_off(trow, tcol, MF_LDA));
-              st4(dst, fmaf(cb2, acc[i][j][0], bf2f(a4[0])), fmaf(cb2, acc[i][j][1], bf2f(a4[1])),
-                  fmaf(cb2, acc[i][j][2], bf2f(a4[2])), fmaf(cb2, acc[i][j][3], bf2f(a4[3])));
+              const int o = mf_off(trow, tcol, MF_LDA);
+              const bf16x4 a4 = *reinterpret_cast<const bf16x4*>(A + o);
+              bf16x4 h4, l4;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float v = fmaf(cb2, acc[i][j][r], bf2f(a4[r]));
+                h4[r] = f2bf(v);
+                l4[r] = f2bf(v - bf2f(h4[r]));
+              }
+              *reinterpret_cast<bf16x4*>(dst) = h4;
+              *reinterpret_cast<bf16x4*>(Bl + o) = l4;
             }
           }
       }
@@ -201,7 +260,7 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int blk = wave + q * MF_WAVES;
-      if (blk < nblk_x) xtb_block(X, Bm, (blk / bcols_x) * 4, (blk % bcols_x) * 2, rp / 32, acc[q]);
+      if (blk < nblk_x) xtb_block(X, Bm, Bl, (blk / bcols_x) * 4, (blk % bcols_x) * 2, rp / 32, acc[q]);
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -215,7 +274,7 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
           const bf16x4 x4 =
               *reinterpret_cast<const bf16x4*>(X + mf_off((rt0 + j) * 16 + (lane & 15), (ct0 + i) * 16 + 4 * g, MF_LDX));
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[q][i][j][r] = fmaf(ns_a, bf2f(x4[r]), acc[q][i][j][r]);
+          for (int r = 0; r < 4; ++r) acc[q][i][j][r] = fmaf(ns_a, bf2f(x4[r]) + bf2f(xlo[q][i][j][r]), acc[q][i][j][r]);
         }
     }
     __syncthreads();
@@ -229,9 +288,15 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int row = (rt0 + j) * 16 + (lane & 15), col = (ct0 + i) * 16 + 4 * g;
-          // rows >= rp / columns >= cp of the padded image must stay zero
-          if (row < rp && col < cp)
-            st4(X + mf_off(row, col, MF_LDX), acc[q][i][j][0], acc[q][i][j][1], acc[q][i][j][2], acc[q][i][j][3]);
+          bf16x4 h4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            h4[r] = f2bf(acc[q][i][j][r]);
+            xlo[q][i][j][r] = f2bf(acc[q][i][j][r] - bf2f(h4[r]));
+          }
+          // rows >= rp / columns >= cp of the padded image must stay zero (rows >= rx / columns
+          // >= cx inside it stay zero by themselves: zero rows/columns of X, A', B and lo)
+          if (row < rp && col < cp) *reinterpret_cast<bf16x4*>(X + mf_off(row, col, MF_LDX)) = h4;
         }
     }
     __syncthreads();
@@ -260,11 +325,8 @@ extern "C" int pcv_muon_fused_ok(int64_t rows, int64_t cols) {
 extern "C" int pcv_muon_ns_fused(const void* mats, int nmats, float eps, float ns_a, float ns_b, float ns_c,
                                  int ns_steps, void* stream) {
   if (nmats <= 0 || ns_steps < 0 || ns_b == 0.f) return PCV_EINVAL;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)muon_ns_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)MF_LDS);
-    attr = true;
-  }
+  static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
+  if (const int e = optin.ensure((const void*)muon_ns_kernel, (int)((int)MF_LDS))) return e;
   hipLaunchKernelGGL(muon_ns_kernel, dim3(nmats), dim3(MF_THREADS), MF_LDS, (hipStream_t)stream,
                      (const MuonMat*)mats, eps, ns_a, ns_b, ns_c, ns_steps);
   return pcv_launch_status();

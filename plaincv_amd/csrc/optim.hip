@@ -111,7 +111,13 @@ __global__ __launch_bounds__(256) void muon_norm_kernel(const MuonMat* mats, flo
   const int64_t n = M.rows * M.cols;
   const float inv = 1.f / (sqrtf(*M.norm2) + eps);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    { const int64_t cx = M.rows > M.cols ? M.rows : M.cols; const int64_t j = (i / cx) * M.ldx + i % cx; M.xb[j] = f2bf(M.x32[j] * inv); }
+  {
+    const int64_t cx = M.rows > M.cols ? M.rows : M.cols;
+    const int64_t j = (i / cx) * M.ldx + i % cx;
+    const float x = M.x32[j] * inv;
+    M.x32[j] = x;          // the fp32 X the NS chain carries across iterations
+    M.xb[j] = f2bf(x);     // its bf16 MFMA operand
+  }
 }
 
 // u = -lr*(O*shape_scale + wd*p); p += u

@@ -669,12 +669,8 @@ extern "C" int pcv_eigh_jacobi(const void* jobs_dev, int njobs, int max_n, int m
   if (!jobs_dev || njobs <= 0 || max_n <= 1 || max_n > EJ_MAXN || max_sweeps <= 0) return PCV_EINVAL;
   const int np = (max_n + 3) & ~3;
   const size_t lds = (size_t)(np * (np + 1) / 2 + 3 * (EJ_MAXN / 2) + EJ_MAXN / 2) * 4;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)eigh_jacobi_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)((size_t)(EJ_MAXN * (EJ_MAXN + 1) / 2 + 2 * EJ_MAXN) * 4));
-    attr = true;
-  }
+  static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
+  if (const int e = optin.ensure((const void*)eigh_jacobi_kernel, (int)((int)((size_t)(EJ_MAXN * (EJ_MAXN + 1) / 2 + 2 * EJ_MAXN) * 4)))) return e;
   hipLaunchKernelGGL(eigh_jacobi_kernel, dim3(njobs), dim3(EJ_THREADS), lds, (hipStream_t)stream,
                      (const EighJob*)jobs_dev, max_sweeps, tol_rel, tol_abs_rel, sort_desc, pow_floor, pow_expo);
   return pcv_launch_status();

@@ -12,7 +12,10 @@ adam branch.
 MI355X mapping: routed matrices are grouped by their (min, max) shape and the
 Newton-Schulz chain runs as batched bf16 MFMA GEMMs over each group (three
 GEMMs per iteration: A' = b X X^T; B = (c/b^2) A'A' + A'; X' = B X + a X, the
-scalars folded into the GEMM epilogues), ping-ponging two bf16 X buffers.
+scalars folded into the GEMM epilogues).  X is carried in fp32 across iterations
+(X' = B bf16(X) + a X, the a X term in the fp32 epilogue, then re-rounded into the bf16
+operand): rounding X itself every iteration dominated the bf16-NS error against fp32 NS5 on
+real gradients (tests/test_optim_parity_gpu.py holds it to 2e-2).
 Momentum/normalisation (pcv_muon_prep) and the final update (pcv_muon_apply)
 are one launch each over all routed matrices.  Matrices whose NS operand fits
 one workgroup's LDS (min <= 128, max <= 256: every ViT-small kernel) skip
@@ -43,8 +46,10 @@ class _Group:
         n = len(names)
         # row strides padded to 8 elements (16-B aligned bf16 GEMM operands)
         self.ldx, ldr = (c + 7) // 8 * 8, (r + 7) // 8 * 8
-        self.x32 = torch.zeros(n, r, self.ldx, dtype=torch.float32, device=device)
-        self.xb = [torch.zeros(n, r, self.ldx, dtype=torch.bfloat16, device=device)[:, :, :c] for _ in range(2)]
+        self.x32 = torch.zeros(n, r, self.ldx, dtype=torch.float32, device=device)   # fp32 X (carried)
+        self.x32v = self.x32[:, :, :c]
+        self.xb_full = torch.zeros(n, r, self.ldx, dtype=torch.bfloat16, device=device)
+        self.xb = self.xb_full[:, :, :c]                                               # bf16(X): MFMA operand
         self.A = torch.zeros(n, r, ldr, dtype=torch.bfloat16, device=device)[:, :, :r]
         self.B = torch.zeros(n, r, ldr, dtype=torch.bfloat16, device=device)[:, :, :r]
 
@@ -92,7 +97,6 @@ class Muon(GradientTransformation):
         st.n_fused = len(routed) - st.n_general
         st.norm2 = torch.zeros(max(1, len(routed)), dtype=torch.float32, device=dev)
         st.max_elems = max([store.params[k].numel() for k in routed], default=1)
-        final = self.ns_steps % 2
         mu = st.tensors["mu"]
         size = lib.pcv_muon_mat_size()
         assert size == 13 * 8, size
@@ -103,10 +107,10 @@ class Muon(GradientTransformation):
                 leaf = store.leaf(k)
                 rows, cols = leaf.shape
                 off = leaf.offset
-                xo = g.xb[0 if g.fused else final][j]
+                xo = g.xb[j]
                 base = [store.flat.data_ptr() + off * 4, store.grad_flat.data_ptr() + off * 4,
                         mu.data_ptr() + off * 4, store.shadow.data_ptr() + off * 2]
-                tail = [rows, cols, leaf.strides[0], g.ldx, g.x32[j].data_ptr(), g.xb[0][j].data_ptr(),
+                tail = [rows, cols, leaf.strides[0], g.ldx, g.x32[j].data_ptr(), g.xb[j].data_ptr(),
                         xo.data_ptr(), st.norm2.data_ptr() + idx * 4]
                 recs_apply.append(base + [0] + tail)
                 recs_upd.append(base + [st.upd.data_ptr() + off * 4] + tail)
@@ -122,13 +126,12 @@ class Muon(GradientTransformation):
         for g in st.groups:
             if g.fused:
                 continue
-            cur = 0
+            X = g.xb
             for _ in range(self.ns_steps):
-                X, Xn = g.xb[cur], g.xb[cur ^ 1]
                 K.gemm(X, X, g.A, tb=True, alpha=b)                       # A' = b X X^T
                 K.gemm(g.A, g.A, g.B, alpha=c / (b * b), res=g.A)          # B = c/b^2 A'A' + A'
-                K.gemm(g.B, X, Xn, res=X, res_scale=a)                     # X = B X + a X
-                cur ^= 1
+                K.gemm(g.B, X, g.x32v, beta=a)                             # X32 = B bf16(X) + a X32
+                K.cast_f32_bf16(g.x32, g.xb_full)                          # next MFMA operand
         if st.n_fused:
             fused_recs = st.mats_apply[st.n_general:]
             hip.call("pcv_muon_ns_fused", ptr(fused_recs), st.n_fused, self.eps, a, b, c, self.ns_steps,

@@ -91,3 +91,69 @@ def test_hip_lm_matches_golden(dev):
         g = store.grads[k].cpu().numpy()
         ref = z["grad:" + k]
         assert np.linalg.norm(g - ref) <= 6e-2 * np.linalg.norm(ref), k
+
+
+def _move_rel(got, p0, ref):
+    d_h = got.astype(np.float64) - p0.astype(np.float64)
+    d_o = ref.astype(np.float64) - p0.astype(np.float64)
+    return np.linalg.norm(d_h - d_o) / max(np.linalg.norm(d_o), 1e-30)
+
+
+@pytest.mark.gpu
+def test_hip_vit_golden_muon3(dev):
+    """3 Muon steps (lr 1e-3, wd 0.01, Adam b1/b2 0.9) on the golden batch without dropout vs the
+    committed oracle trajectory ``muon3:*``: rel-L2 of each leaf's movement (key biases excluded:
+    their true gradient is exactly 0, the bf16 one is noise that Adam normalises)."""
+    from plaincv_amd.engine import create_train_state, make_train_step
+    from plaincv_amd.models.vit_small import VisionTransformer
+    from utils import Config
+    z = _load("vit_tiny.npz")
+    _, p = vit_params()
+    m = VisionTransformer(**dict(VIT_CFG, dropout_rate=0.0))
+    shape = tuple(z["images"].shape)
+    cfg = Config(optim="muon", lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9)
+    st = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=p)
+    step = make_train_step()
+    imgs, labels = torch.from_numpy(z["images"]).to(dev), torch.from_numpy(z["labels"]).to(dev)
+    for it in range(3):
+        st, _ = step(st, (imgs, labels), it)
+    torch.cuda.synchronize()
+    got = st.params.to_dict()
+    for k in p:
+        if k.endswith("key/bias"):
+            continue
+        r = _move_rel(got[k].numpy(), p[k].numpy(), z["muon3:" + k])
+        print(f"GOLDEN_MUON3 {k} {r:.4f}")
+        assert r < 0.5, (k, r)
+
+
+@pytest.mark.gpu
+def test_hip_lm_golden_adamw3(dev):
+    """3 AdamW steps (lr 3e-4, b2 0.95, wd 0.1) on the reference's wikitext rows vs the committed
+    oracle trajectory ``adamw3:*`` (vocabulary-sized leaves through their stored samples)."""
+    from plaincv_amd.engine.lm import create_lm_state, make_apply_grads_fn, make_train_fns
+    from plaincv_amd.models.LM.transformer import ModelConfig, Transformer
+    from utils import Config
+    z = _load("lm_tiny.npz")
+    _, p = lm_params()
+    model = Transformer(ModelConfig(mlp="glu", **LM_CFG))
+    cfg = Config(optim="adamw", lr=3e-4, beta1=0.9, beta2=0.95, weight_decay=0.1, seq_len=LM_CFG["seq_len"])
+    ids = torch.from_numpy(z["input_ids"]).to(dev)
+    st = create_lm_state(cfg, model, {"params": p}, ids.shape[0], dev)
+    compute_grads, _ = make_train_fns()
+    apply_grads = make_apply_grads_fn(None)
+    for _ in range(3):
+        compute_grads(st, ids)
+        apply_grads(st)
+    torch.cuda.synchronize()
+    got = st.params.to_dict()
+    sample = np.random.default_rng(0).integers(0, 50257 * LM_CFG["dim"], 2048)
+    for k in p:
+        g, p0 = got[k].reshape(-1).numpy(), p[k].reshape(-1).numpy()
+        if "adamw3:" + k in z:
+            r = _move_rel(g, p0, z["adamw3:" + k].reshape(-1))
+        else:
+            idx = sample % g.size
+            r = _move_rel(g[idx], p0[idx], z["adamw3_sample:" + k])
+        print(f"GOLDEN_ADAMW3 {k} {r:.4f}")
+        assert r < 0.5, (k, r)

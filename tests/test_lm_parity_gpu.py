@@ -1,7 +1,8 @@
 """Causal LM on the HIP path vs the CPU oracle in the reference's bf16 placement.
 
-Tolerances (SURVEY §8c bf16 mode): loss abs <= 2e-2, gradient leaves rel-L2 <= 5e-2
-(floor 1e-3), params after 3 AdamW / Muon steps max|dp| <= 1e-2 (lr 1e-3)."""
+Tolerances (SURVEY §8c bf16 mode): loss abs <= 2e-2, gradient leaves rel-L2 <= 6e-2 (floor 1e-3),
+grad norm rel 3e-2; the optimizer step given the HIP gradients within tests/parity_util's
+bounds (AdamW 1e-5, bf16-NS Muon 2e-2 relative to the update)."""
 import pytest
 import torch
 
@@ -49,13 +50,22 @@ def test_lm_grads_match_oracle(dev, tie, b, T, mlp):
         assert r < 6e-2, (k, r)
 
 
-@pytest.mark.parametrize("optim,clip", [("adamw", None), ("muon", 1.0)])
+@pytest.mark.parametrize("optim,clip", [("adamw", None), ("muon", 1.0), ("adamw", 0.05), ("muon", 0.05)])
 def test_lm_train_steps_match_oracle(dev, optim, clip):
+    """Three optimizer steps of 2 accumulated micro-steps through compute_grads / apply_grads.
+    Each step checks, against the oracle at the same params:
+      (1) the accumulated mean gradient, every leaf rel <= 6e-2;
+      (2) the clip: gnorm equals ||g_hip|| (rel 1e-4) and the oracle's ||g|| (rel 3e-2), and the
+          device clip factor equals min(1, c / (||g|| + 1e-6)) (train_lm.py:173-178); clip 0.05
+          must engage;
+      (3) the applied update against the oracle optimizer fed clip(g_hip) (step_rel: AdamW 1e-5,
+          Muon routed 2e-2)."""
     from oracle import optim as oopt
-    from oracle.engine import apply_updates, clip_grads, lm_loss_and_acc, value_and_grad
+    from oracle.engine import clip_grads, lm_loss_and_acc, value_and_grad
     from oracle.lm import model_config_from_cfg, transformer_apply
     from plaincv_amd.engine.lm import create_lm_state, make_apply_grads_fn, make_train_fns
     from plaincv_amd.models.LM.constructor import construct_model
+    from tests.parity_util import global_norm, step_bound, step_rel
     cfg = _tiny()
     cfg.update(optim=optim, lr=1e-3, weight_decay=0.1, beta1=0.9, beta2=0.95)
     model, mc, variables = construct_model(cfg)
@@ -64,26 +74,35 @@ def test_lm_train_steps_match_oracle(dev, optim, clip):
     compute_grads, _ = make_train_fns()
     apply_grads = make_apply_grads_fn(clip)
     tx = oopt.get_optimizer(cfg)
-    params = dict(variables["params"])
-    ostate = tx.init(params)
+    ostate = tx.init(dict(variables["params"]))
     omc = model_config_from_cfg(cfg)
     gen = torch.Generator().manual_seed(11)
     for it in range(3):
-        acc_g = None
+        p0 = st.params.to_dict()
+        g_or = None
         for _ in range(accum):
             ids = torch.randint(0, cfg.vocab_size, (b, T + 1), generator=gen, dtype=torch.int32)
             compute_grads(st, ids.to(dev))
             _, gr = value_and_grad(
-                lambda p: lm_loss_and_acc(transformer_apply(p, ids[:, :-1], omc, torch.bfloat16), ids[:, 1:]),
-                params)
-            acc_g = gr if acc_g is None else {k: acc_g[k] + gr[k] for k in gr}
-        acc_g = {k: v / accum for k, v in acc_g.items()}
+                lambda p: lm_loss_and_acc(transformer_apply(p, ids[:, :-1], omc, torch.bfloat16), ids[:, 1:]), p0)
+            g_or = gr if g_or is None else {k: g_or[k] + gr[k] for k in gr}
+        g_or = {k: v / accum for k, v in g_or.items()}
+        torch.cuda.synchronize()
+        g_hip = st.params.grads_dict()
+        for k in p0:
+            assert _rel(g_hip[k], g_or[k]) < 6e-2, (it, k, _rel(g_hip[k], g_or[k]))
         st, gnorm = apply_grads(st)
-        acc_g = clip_grads(acc_g, clip)
-        upd, ostate = tx.update(acc_g, ostate, params)
-        params = apply_updates(params, upd)
-    torch.cuda.synchronize()
-    got = st.params.to_dict()
-    for k in params:
-        d = (got[k] - params[k]).abs().max().item()
-        assert d < 1e-2, (k, d)
+        torch.cuda.synchronize()
+        p1 = st.params.to_dict()
+        if clip is not None:
+            n_hip, n_or = global_norm(g_hip), global_norm(g_or)
+            assert abs(gnorm.item() - n_hip) <= 1e-4 * n_hip, (gnorm.item(), n_hip)
+            assert abs(gnorm.item() - n_or) <= 3e-2 * n_or, (gnorm.item(), n_or)
+            want = min(1.0, clip / (n_hip + 1e-6))
+            assert abs(st.gscale.item() - want) <= 1e-5 * want, (st.gscale.item(), want)
+            if clip < 0.1:
+                assert want < 1.0
+        u, ostate = tx.update(clip_grads(g_hip, clip), ostate, p0)
+        for k in p0:
+            e = step_rel(p0[k], p1[k], u[k])
+            assert e <= step_bound(optim, k, p0[k]), (it, k, e)

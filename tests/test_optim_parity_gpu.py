@@ -1,0 +1,210 @@
+"""Optimizer-step parity: the HIP optimizers vs the CPU oracle on IDENTICAL gradients.
+
+The engine-level tests compare whole training steps, where bf16 GEMM gradients already differ
+from the oracle's by a few per cent; an optimizer error smaller than that would hide inside
+them.  Here the optimizer is isolated: both sides get the same fp32 gradients and the same
+starting state, and every step's UPDATE is compared relative to the oracle's update
+(rel = ||u_hip - u_oracle||_F / ||u_oracle||_F per leaf), in both entry points:
+
+  * ``tx.update(grads, state, params)`` -- the functional facade (optax's sign convention);
+  * ``tx.step_(store, state, gscale)``  -- the fused in-place step the engines run, with a
+    device grad scale (clip x 1/accum) and the bf16 GEMM shadow it refreshes.
+
+Bounds:
+  AdamW (and Muon's Adam branch)   rel <= 1e-5   (fp32 both sides; the step_ delta also carries
+                                                  the fp32 rounding of p + u, ~1e-7 relative)
+  Muon routed leaves, bf16 NS5     rel <= 2e-2   (bf16 MFMA Newton-Schulz vs fp32 NS5)
+Shapes are the real layouts: ViT-small C2 (Tiny-ImageNet 64x64x3, D 128, 4 layers, 200
+classes -- fused q|k|v groups, 3-D attention kernels, 4-D patch conv; the routed 128x256,
+256x128, 128x200 kernels take the one-workgroup fused NS kernel) and a 124M-width LM block
+(d 768: w_qkv 768x2304, fused gate|up 768x2048, fc2 2048x768 -- the batched-GEMM NS chain).
+
+``test_parity_check_catches_broken_steps`` runs deliberately broken optimizer steps (Nesterov
+off, NS skipped, shape factor dropped, bias correction off by one step, no-op step) through the
+same comparison and requires it to FAIL, so the bounds above are known to have teeth.
+Gradients are momentum-like (a shared rank-one direction plus full-rank noise): NS5 in bf16 is
+within the bound there; for nearly rank-deficient momenta the NS polynomial amplifies bf16
+rounding in the null space, which is a property of bf16 NS, not of this build.
+"""
+from collections import OrderedDict
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from tests.parity_util import ADAM_TOL, MUON_TOL, rel as _rel, routed as _routed, step_rel
+
+
+def _vit_layout():
+    from plaincv_amd.models.vit_small import VisionTransformer
+    m = VisionTransformer(num_classes=200, patch_size=4, hidden_size=128, mlp_dim=256, num_layers=4, num_heads=4)
+    return m.layout((64, 64, 64, 3))
+
+
+def _lm_layout():
+    from plaincv_amd.models.LM.transformer import ModelConfig, Transformer
+    mc = ModelConfig(vocab_size=1000, dim=768, expand=8 / 3, n_layers=1, n_heads=12, mlp="glu", seq_len=64)
+    return Transformer(mc).layout()
+
+
+LAYOUTS = {"vit_c2": _vit_layout, "lm768": _lm_layout}
+
+
+def _grads(layout, gen, scale_by_leaf):
+    out = OrderedDict()
+    for k, l in layout.leaves.items():
+        s = scale_by_leaf[k]
+        g = torch.randn(l.shape, generator=gen)
+        if len(l.shape) >= 2:   # momentum-like: a shared rank-one direction plus noise
+            u = torch.randn(l.shape[0], 1, generator=gen)
+            v = torch.randn(1, int(torch.tensor(l.shape[1:]).prod()), generator=gen)
+            g = g + 2.0 * (u @ v).reshape(l.shape)
+        out[k] = (s * g).contiguous()
+    return out
+
+
+def run_pair(dev, layout, gpu_tx, oracle_tx, steps, mode, gscale=1.0, seed=0, mutate_state=None):
+    """Per-step (hip_update, oracle_update) dicts (CPU fp32) for identical gradients.
+    mode "update": tx.update; mode "step_": tx.step_ with a device gscale, update = p_after - p_before."""
+    from plaincv_amd.params import ParamStore
+    gen = torch.Generator().manual_seed(seed)
+    store = ParamStore(layout, dev)
+    init = OrderedDict((k, 0.1 * torch.randn(l.shape, generator=gen)) for k, l in layout.leaves.items())
+    store.load(init)
+    params = OrderedDict((k, v.clone()) for k, v in init.items())
+    scale = {k: float(10.0 ** torch.empty(1).uniform_(-3, 0, generator=gen).item()) for k in layout.leaves}
+    gst = gpu_tx.init(store)
+    if mutate_state is not None:
+        mutate_state(gst)
+    ost = oracle_tx.init(params)
+    gs = torch.full((1,), float(gscale), device=dev)
+    out = []
+    for _ in range(steps):
+        grads = _grads(layout, gen, scale)
+        store.zero_grad()
+        for k, v in grads.items():
+            store.grads[k].copy_(v.to(dev))
+        before = after = None
+        if mode == "update":
+            upd, gst = gpu_tx.update(store.grads, gst, store)
+            hip = OrderedDict((k, v.detach().cpu().clone()) for k, v in upd.items())
+            for k in hip:
+                store.params[k].add_(upd[k])
+            store.sync_shadow()
+        else:
+            before = store.to_dict()
+            gpu_tx.step_(store, gst, gscale=gs if gscale != 1.0 else None)
+            after = store.to_dict()
+            hip = OrderedDict((k, after[k].double() - before[k].double()) for k in before)
+            # the fused step refreshes the bf16 GEMM shadow from the new fp32 master
+            for k in before:
+                sh = store.bf16[k].float().cpu()
+                assert torch.equal(sh, after[k].to(torch.bfloat16).float()), ("shadow", k)
+        og = OrderedDict((k, v * gscale) for k, v in grads.items())
+        oupd, ost = oracle_tx.update(og, ost, params)
+        for k in params:
+            params[k] = params[k] + oupd[k]
+        out.append((hip, oupd, before, after))
+    torch.cuda.synchronize()
+    return out
+
+
+def worst(steps, routed_pred):
+    """(worst rel over routed leaves, worst rel over the rest)."""
+    wr, wa = 0.0, 0.0
+    for hip, ora, p0, p1 in steps:
+        for k in ora:
+            r = _rel(hip[k], ora[k]) if p0 is None else step_rel(p0[k], p1[k], ora[k])
+            if routed_pred(k, ora[k]):
+                wr = max(wr, r)
+            else:
+                wa = max(wa, r)
+    return wr, wa
+
+
+@pytest.mark.parametrize("which", ["vit_c2", "lm768"])
+@pytest.mark.parametrize("mode,gscale", [("update", 1.0), ("step_", 1.0), ("step_", 0.37)])
+def test_adamw_update_parity(dev, which, mode, gscale):
+    from oracle import optim as oopt
+    from plaincv_amd.optim.adamw import AdamW
+    lr, hp = 1e-2, dict(b1=0.9, b2=0.95, eps=1e-8, weight_decay=0.1)
+    steps = run_pair(dev, LAYOUTS[which](), AdamW(lr, **hp), oopt.adamw(lr, **hp), 4, mode, gscale)
+    _, wa = worst(steps, lambda k, p: False)
+    assert wa <= ADAM_TOL, wa
+
+
+@pytest.mark.parametrize("which", ["vit_c2", "lm768"])
+@pytest.mark.parametrize("mode,gscale", [("update", 1.0), ("step_", 0.37)])
+def test_muon_update_parity(dev, which, mode, gscale):
+    """Routed leaves through the fused one-workgroup NS kernel (ViT) and the batched-GEMM chain
+    (LM); the Adam branch (Nesterov, as optax.contrib.muon) on everything else."""
+    from oracle import optim as oopt
+    from plaincv_amd.optim.muon import Muon
+    lr, wd = 1e-2, 0.1
+    gpu = Muon(lr, weight_decay=wd, adam_b1=0.9, adam_b2=0.95, adam_weight_decay=wd)
+    ora = oopt.muon(lr, weight_decay=wd, adam_b1=0.9, adam_b2=0.95, adam_weight_decay=wd)
+    steps = run_pair(dev, LAYOUTS[which](), gpu, ora, 3, mode, gscale)
+    wr, wa = worst(steps, _routed)
+    assert wr <= MUON_TOL, wr
+    assert wa <= ADAM_TOL, wa
+
+
+def test_muon_ragged_fused_shapes(dev):
+    """Fused NS kernel on ragged routed shapes (7x33, 48x100, 200x64) vs fp32 NS5."""
+    from oracle import optim as oopt
+    from plaincv_amd.optim.muon import Muon
+    from plaincv_amd.params import Layout
+    lay = Layout()
+    for i, s in enumerate([(7, 33), (48, 100), (200, 64), (96, 256)]):
+        lay.add(f"Dense_{i}/kernel", s)
+    lay.add("Dense_0/bias", (33,))
+    gpu = Muon(1e-2, weight_decay=0.05, adam_weight_decay=0.05)
+    ora = oopt.muon(1e-2, weight_decay=0.05, adam_weight_decay=0.05)
+    steps = run_pair(dev, lay, gpu, ora, 3, "step_")
+    wr, wa = worst(steps, _routed)
+    assert wr <= MUON_TOL, wr
+    assert wa <= ADAM_TOL, wa
+
+
+def _mutations():
+    from oracle import optim as oopt
+    from plaincv_amd.optim.adamw import AdamW
+    from plaincv_amd.optim.muon import Muon
+    hp = dict(b1=0.9, b2=0.95, eps=1e-8, weight_decay=0.1)
+    mk = dict(weight_decay=0.1, adam_b1=0.9, adam_b2=0.95, adam_weight_decay=0.1)
+
+    class NoOp:
+        def __init__(self, tx):
+            self.tx = tx
+
+        def init(self, store):
+            return self.tx.init(store)
+
+        def step_(self, store, state, gscale=None):
+            pass
+
+    def count_plus_one(st):
+        st.count.fill_(1)
+
+    return {
+        # name: (hip tx, oracle tx, state mutation, which error must exceed its bound)
+        "adamw_bias_correction_off_by_one": (AdamW(1e-2, **hp), oopt.adamw(1e-2, **hp), count_plus_one, "adam"),
+        "adamw_noop": (NoOp(AdamW(1e-2, **hp)), oopt.adamw(1e-2, **hp), None, "adam"),
+        "muon_nesterov_off": (Muon(1e-2, nesterov=False, **mk), oopt.muon(1e-2, **mk), None, "both"),
+        "muon_ns_skipped": (Muon(1e-2, ns_steps=0, **mk), oopt.muon(1e-2, **mk), None, "routed"),
+        "muon_no_shape_factor": (Muon(1e-2, shape_scale=False, **mk), oopt.muon(1e-2, **mk), None, "routed"),
+        "muon_bias_correction_off_by_one": (Muon(1e-2, **mk), oopt.muon(1e-2, **mk), count_plus_one, "both"),
+    }
+
+
+@pytest.mark.parametrize("name", ["adamw_bias_correction_off_by_one", "adamw_noop", "muon_nesterov_off",
+                                  "muon_ns_skipped", "muon_no_shape_factor", "muon_bias_correction_off_by_one"])
+def test_parity_check_catches_broken_steps(dev, name):
+    gpu, ora, mut, which = _mutations()[name]
+    steps = run_pair(dev, _vit_layout(), gpu, ora, 2, "step_", mutate_state=mut)
+    wr, wa = worst(steps, _routed if "muon" in name else (lambda k, p: False))
+    if which in ("routed", "both"):
+        assert wr > MUON_TOL, (name, wr)
+    if which in ("adam", "both"):
+        assert wa > ADAM_TOL * 100, (name, wa)

@@ -1,8 +1,9 @@
 """ViT forward/backward/optimizer on the HIP path vs the CPU oracle (bf16 placement).
 
 Tolerances (bf16 MFMA operands vs an oracle that rounds the same GEMM operands):
-loss abs <= 2e-2, every gradient leaf rel-L2 <= 5e-2, updated params after one
-AdamW/Muon step max|dp| <= 2e-3 (lr 1e-3, Adam direction ~O(1)).
+loss abs <= 2e-2, every gradient leaf rel-L2 <= 5e-2; the optimizer step, given the HIP
+gradients, within tests/parity_util's bounds (AdamW 1e-5, bf16-NS Muon 2e-2 relative to the
+update, not to the parameter).
 """
 import numpy as np
 import pytest
@@ -66,32 +67,57 @@ def test_vit_grads_match_oracle(dev, rate, use_ln, shape):
 
 @pytest.mark.parametrize("optim", ["adamw", "muon"])
 def test_vit_train_step_matches_oracle(dev, optim):
+    """Three engine steps (make_train_step: fused q|k|v groups, dropout 0.1 on, the in-place
+    ``step_``).  Each step checks, against the oracle:
+      (1) loss (abs 2e-2) and every gradient leaf (rel 5e-2) at the same params;
+      (2) the applied update against the oracle optimizer fed the HIP step's own gradients
+          (tests/parity_util.step_rel: AdamW leaves 1e-5, Muon routed leaves 2e-2), so an
+          optimizer error cannot hide inside the bf16 gradient differences;
+    and after the 3 steps (3) the parameter movement against an independent oracle trajectory
+    (rel-L2 of the movement; key biases excluded: their true gradient is exactly 0).
+    B = 16: the 10-class head gradient is then full rank (see test_optim_parity_gpu)."""
     from oracle import optim as oopt
     from oracle.engine import apply_updates, cross_entropy_loss, value_and_grad
     from oracle.vit import vit_apply
     from plaincv_amd.engine import create_train_state, make_train_step
+    from tests.parity_util import step_bound, step_rel
     from utils import Config
-    m = _small_model(0.0)
-    shape = (4, 16, 16, 3)
+    m = _small_model(0.1)
+    shape = (16, 16, 16, 3)
     cfg = Config(optim=optim, lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9)
     init = m.init(3, shape)
     st = create_train_state(0, m, 1e-3, shape, m.num_classes, cfg=cfg, init_params=init)
     step = make_train_step()
-    tx = oopt.get_optimizer(cfg)
-    ostate = tx.init(init)
-    params = dict(init)
+    tx_h, tx_o = oopt.get_optimizer(cfg), oopt.get_optimizer(cfg)
+    s_h, s_o = tx_h.init(init), tx_o.init(init)
+    po = dict(init)
     oc = _oracle_cfg(m)
     gen = torch.Generator().manual_seed(5)
     for it in range(3):
         images = torch.randint(0, 256, shape, generator=gen, dtype=torch.uint8)
         labels = torch.randint(0, 10, (shape[0],), generator=gen, dtype=torch.int32)
+        p0 = st.params.to_dict()
         st, met = step(st, (images.to(dev), labels.to(dev)), it)
-        _, grads = value_and_grad(
-            lambda p: (cross_entropy_loss(vit_apply(p, images, oc, True, it, bf16=True), labels), None), params)
-        upd, ostate = tx.update(grads, ostate, params)
-        params = apply_updates(params, upd)
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        p1, g_hip = st.params.to_dict(), st.params.grads_dict()
+        f = lambda p: (cross_entropy_loss(vit_apply(p, images, oc, True, it, bf16=True), labels), None)  # noqa: E731
+        (loss, _), g_or = value_and_grad(f, p0)
+        assert abs(met["loss"].item() - loss.item()) < 2e-2, (it, met["loss"].item(), loss.item())
+        for k in init:
+            if not k.endswith("key/bias"):
+                assert _rel(g_hip[k], g_or[k]) < 5e-2, (it, k, _rel(g_hip[k], g_or[k]))
+        u, s_h = tx_h.update(g_hip, s_h, p0)
+        for k in init:
+            e = step_rel(p0[k], p1[k], u[k])
+            assert e <= step_bound(optim, k, p0[k]), (it, k, e)
+        _, go = value_and_grad(lambda p: (cross_entropy_loss(vit_apply(p, images, oc, True, it, bf16=True),
+                                                             labels), None), po)
+        uo, s_o = tx_o.update(go, s_o, po)
+        po = apply_updates(po, uo)
     got = st.params.to_dict()
-    for k in params:
-        d = (got[k] - params[k]).abs().max().item()
-        assert d < 3e-3 * 3, (k, d)
+    for k in init:
+        if k.endswith("key/bias"):
+            continue
+        r = _rel(got[k] - init[k], po[k] - init[k])
+        print(f"VIT_MOVE {optim} {k} {r:.4f}")
+        assert r < 0.5, (k, r)
