@@ -1,6 +1,12 @@
 """Benchmark: plainCV training hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload vit_c2|vit_c4_soap|vit_c4_shampoo|lm124m|lm420m] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload vit_c2|vit_c4_soap|vit_c4_shampoo|lm124m|lm420m]
+                    [--no-cpu-baseline] [--no-lm]
+
+``--gpus N`` (N > 1) without a torchrun environment: the parent process spawns N ranks of this
+script (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1/MASTER_PORT, one GPU each) BEFORE
+anything touches the GPU, relays rank 0's JSON line and exits with the worst rank's status.
+Under torchrun (WORLD_SIZE set) it runs as the given rank, and --gpus must equal WORLD_SIZE.
 
 Default workload (N=1): BASELINE.json configs[1] -- ViT-small on Tiny-ImageNet-
 shaped synthetic data (uint8 64x64x3, 200 classes, per-GPU batch 64, dropout 0.1,
@@ -9,6 +15,9 @@ LayerNorm), Muon optimizer, bf16 MFMA compute with fp32 master params.  One
 one batch per GPU, replayed from a hipGraph; inputs are resident in HBM.
 With N>1 each rank runs the same per-GPU batch (weak scaling) and gradients
 are averaged over RCCL once per step.  ``value`` = images/s over all ranks.
+The line also carries ``lm124m``: BASELINE configs[2] at its exact shape (124M LM, AdamW,
+seq 1024, micro-batch 16, grad accumulation 8, DDP over the same ranks) with its own
+roofline and CPU baseline (``--no-lm`` skips it).
 
 Also reported: the roofline of the dominant kernel (timed live with HIP
 events on its own stream, algorithmic bytes or FLOPs per launch) and the CPU
@@ -58,6 +67,38 @@ def vit_model(cfg):
                              hidden_size=cfg.vit_hidden_size, mlp_dim=cfg.vit_mlp_dim, num_layers=cfg.vit_layers,
                              num_heads=cfg.vit_heads, dropout_rate=cfg.vit_dropout,
                              use_layernorm=cfg.vit_use_layernorm)
+
+
+def cpu_threads():
+    """Host threads for the CPU baseline (the whole affinity set), capped by
+    the cgroup CPU quota when one is set (the GPU box gives each GPU a share of a larger
+    machine; more threads than the quota only time-slice)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = max(1, min(n, -(-int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        return open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(" :\t")
+    except Exception:
+        return "unknown"
+
+
+def timed_loop(step, min_steps=5, max_steps=50, seconds=12.0, warmup=2):
+    """2 warm-up steps, then >= min_steps timed steps (more while under `seconds`)."""
+    for i in range(warmup):
+        step(i)
+    n, t0 = 0, time.perf_counter()
+    while n < min_steps or (time.perf_counter() - t0 < seconds and n < max_steps):
+        step(warmup + n)
+        n += 1
+    return n, (time.perf_counter() - t0) / n
 
 
 def timed_kernel(fn, iters=50):
@@ -131,7 +172,7 @@ def cpu_baseline_vit(cfg, seconds=12.0):
     from oracle import optim as oopt
     from oracle.engine import apply_updates, cross_entropy_loss, value_and_grad
     from oracle.vit import ViTConfig, vit_apply
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     m = vit_model(cfg)
     shape = (cfg.batch_size, cfg.image_size, cfg.image_size, cfg.num_channels)
@@ -152,23 +193,31 @@ def cpu_baseline_vit(cfg, seconds=12.0):
         upd, st = tx.update(grads, st, params)
         params = apply_updates(params, upd)
 
-    step(0)
-    n, t0 = 0, time.perf_counter()
-    while True:
-        step(n + 1)
-        n += 1
-        if time.perf_counter() - t0 > seconds or n >= 50:
-            break
-    dt = (time.perf_counter() - t0) / n
-    model_name = "unknown"
-    try:
-        model_name = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(" :\t")
-    except Exception:
-        pass
+    n, dt = timed_loop(step, seconds=seconds)
     return {"value": round(cfg.batch_size / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
             "steps_per_sec": round(1.0 / dt, 4),
-            "sample": f"{n} timed oracle ViT-small {cfg.optim} train steps (fp32, B={cfg.batch_size}, 64x64x3, 200 classes) "
-                      f"after 1 warmup; CPU {model_name}"}
+            "sample": f"{n} timed oracle ViT-small {cfg.optim} train steps (fp32, B={cfg.batch_size}, 64x64x3, "
+                      f"200 classes) after 2 warm-up steps, {threads} threads (affinity set "
+                      f"{len(os.sched_getaffinity(0))}, cgroup-capped); CPU {cpu_model()}"}
+
+
+def allreduce_busbw(buf, iters=10):
+    """RCCL all-reduce of the gradient buffer (the step's one exchange): bus bandwidth
+    2 (n-1)/n S / t (nccl-tests convention)."""
+    n = dp.world_size()
+    if n <= 1:
+        return None
+    for _ in range(2):
+        dp.all_reduce_mean_(buf)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dp.all_reduce_mean_(buf)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / iters
+    S = buf.numel() * buf.element_size()
+    return {"bytes": S, "us": round(t * 1e6, 1), "busbw_GBs": round(2 * (n - 1) / n * S / t / 1e9, 2),
+            "world": n, "backend": torch.distributed.get_backend()}
 
 
 def bench_vit(args):
@@ -217,10 +266,15 @@ def bench_vit(args):
                "steps_per_sec": round(sps, 3), "tflops_per_gpu": round(flops * sps / 1e12, 3),
                "final_loss": round(loss, 4)}
         out["roofline"] = vit_roofline(state, shape)
+        if world > 1:
+            out["grad_allreduce"] = None   # filled below (collective: every rank takes part)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_vit(cfg, args.cpu_seconds)
         else:
             out["cpu_baseline"] = None
+    ar = allreduce_busbw(state.params.grad_flat[: state.params.layout.size]) if world > 1 else None
+    if out is not None and world > 1:
+        out["grad_allreduce"] = ar
     return out
 
 
@@ -230,7 +284,7 @@ def cpu_baseline_lm(cfg, variables, clip, seconds=12.0):
     from oracle import optim as oopt
     from oracle.engine import apply_updates, clip_grads, lm_loss_and_acc, value_and_grad
     from oracle.lm import model_config_from_cfg, transformer_apply
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     mc = model_config_from_cfg(cfg)
     params = {k: v.clone() for k, v in variables["params"].items()}
@@ -239,7 +293,7 @@ def cpu_baseline_lm(cfg, variables, clip, seconds=12.0):
     g = torch.Generator().manual_seed(0)
     ids = torch.randint(0, cfg.vocab_size, (1, cfg.seq_len + 1), generator=g, dtype=torch.int64)
 
-    def step():
+    def step(i):
         nonlocal params, st
         _, grads = value_and_grad(lambda p: lm_loss_and_acc(transformer_apply(p, ids[:, :-1], mc), ids[:, 1:]),
                                   params)
@@ -248,23 +302,12 @@ def cpu_baseline_lm(cfg, variables, clip, seconds=12.0):
         upd, st = tx.update(grads, st, params)
         params = apply_updates(params, upd)
 
-    step()
-    n, t0 = 0, time.perf_counter()
-    while True:
-        step()
-        n += 1
-        if time.perf_counter() - t0 > seconds or n >= 20:
-            break
-    dt = (time.perf_counter() - t0) / n
-    model_name = "unknown"
-    try:
-        model_name = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(" :\t")
-    except Exception:
-        pass
+    n, dt = timed_loop(step, seconds=seconds, max_steps=20)
     return {"value": round(cfg.seq_len / dt, 2), "unit": "tokens/s", "cores": threads, "kind": "port",
             "steps_per_sec": round(1.0 / dt, 4),
-            "sample": f"{n} timed oracle {cfg.optim} train steps of 1 x {cfg.seq_len} tokens (fp32) after 1 warmup; "
-                      f"CPU {model_name}"}
+            "sample": f"{n} timed oracle {cfg.optim} train steps of 1 x {cfg.seq_len} tokens (fp32) after 2 warm-up "
+                      f"steps, {threads} threads (affinity set {len(os.sched_getaffinity(0))}, cgroup-capped); "
+                      f"CPU {cpu_model()}"}
 
 
 LM_CFGS = {
@@ -273,7 +316,7 @@ LM_CFGS = {
                             mlp_class="glu", seq_len=1024, tie_embeddings=False, rope_theta=500000.0,
                             dtype="bfloat16", optim="adamw", lr=3e-4, weight_decay=0.1, beta1=0.9, beta2=0.95,
                             seed=0),
-                   mb=16, accum=1, clip=None, name="lm124m_adamw (BASELINE configs[2] shape)"),
+                   mb=16, accum=8, clip=None, name="lm124m_adamw (BASELINE configs[2]: micro-batch 16, accum 8)"),
     # BASELINE configs[4]: 420M LM (config/tr_420M_x8gpu.yaml: d 1024, L 24, H 16, V 50280, T 2048,
     # micro-batch 8, accum 4, grad_clip 1.0) with Muon (config/lm_muon.yaml muon_* keys)
     "lm420m": dict(cfg=dict(model="transformer", vocab_size=50280, d_model=1024, expand="8/3", n_layers=24,
@@ -329,6 +372,7 @@ def bench_lm(args):
     dt = float(t.item())
     tokens = world * mb * accum * cfg.seq_len * args.steps
     fpt = model.flops_per_token(cfg.seq_len)
+    ar = allreduce_busbw(st.params.grad_flat[: st.params.layout.size], iters=3) if world > 1 else None
     if rank != 0:
         return None
     return {"metric": METRIC, "value": round(tokens / dt, 1), "unit": "tokens/s", "n_gpus": world,
@@ -341,6 +385,7 @@ def bench_lm(args):
             "steps_per_sec": round(args.steps / dt, 4),
             "tflops_per_gpu": round(tokens / world / dt * fpt / 1e12, 2),
             "roofline": lm_roofline(st),
+            "grad_allreduce": ar,
             "cpu_baseline": (cpu_baseline_lm(cfg, variables, spec["clip"], args.cpu_seconds)
                              if world == 1 and not args.no_cpu_baseline else None)}
 
@@ -366,26 +411,105 @@ def lm_roofline(st):
             "flops_per_launch": flops}
 
 
+def bench_dp_stub(args):
+    """CPU stand-in for the launcher test (tests/test_bench_launcher.py): the same rank
+    bootstrap, barrier / max-over-ranks timing and JSON line, with a gloo all-reduce of a
+    rank-dependent vector as the 'step' (no GPU)."""
+    rank, _, world, _ = dp.init_from_env(backend="gloo")
+    if os.environ.get("PCV_BENCH_FAIL_RANK") == str(rank):
+        raise RuntimeError(f"rank {rank}: injected failure (launcher test)")
+    x = torch.full((1024,), float(rank + 1))
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        y = x.clone()
+        dp.all_reduce_mean_(y)
+    if world > 1:
+        torch.distributed.barrier()
+    t = torch.tensor([time.perf_counter() - t0])
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    if rank != 0:
+        return None
+    return {"metric": "dp_stub", "value": round(world * args.steps / float(t.item()), 2), "unit": "steps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "mean": float(y[0].item()),
+            "config": {"workload": "dp_stub", "parallelism": f"dp{world}"}}
+
+
+def launch_ranks(n, argv):
+    """Spawn n ranks of this script (one GPU each) before the parent touches the GPU; relay
+    rank 0's stdout; return the worst exit status (every rank is stopped if one fails)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    import tempfile
+    procs = []
+    out0 = tempfile.TemporaryFile()
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=out0 if r == 0 else sys.stderr, start_new_session=True))
+    # poll every rank: the first failure stops the others (a rank blocked in a collective on a
+    # dead peer would otherwise wait for the communicator timeout)
+    failed = None
+    while failed is None and any(p.poll() is None for p in procs):
+        failed = next((p.returncode for p in procs if p.poll() is not None and p.returncode != 0), None)
+        time.sleep(0.2)
+    if failed is None:
+        failed = next((p.returncode for p in procs if p.returncode != 0), None)
+    for p in procs:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGTERM)
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+    out0.seek(0)
+    sys.stdout.write(out0.read().decode())
+    sys.stdout.flush()
+    return 0 if failed is None else (failed if failed > 0 else 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="vit_c2", choices=["vit_c2", "vit_c4_soap", "vit_c4_shampoo", "lm124m", "lm420m"])
+    ap.add_argument("--workload", default="vit_c2",
+                    choices=["vit_c2", "vit_c4_soap", "vit_c4_shampoo", "lm124m", "lm420m", "dp_stub"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--lm-micro-batch", type=int, default=None, help="default: the workload's config")
     ap.add_argument("--lm-accum", type=int, default=None, help="default: the workload's config")
-    ap.add_argument("--with-lm", action="store_true", help="also run the 124M LM and attach it as 'lm124m'")
+    ap.add_argument("--no-lm", action="store_true", help="skip the attached 124M LM (configs[2]) line")
+    ap.add_argument("--lm-steps", type=int, default=10)
+    ap.add_argument("--lm-warmup", type=int, default=2)
     args = ap.parse_args()
-    if args.workload.startswith("lm"):
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={env_world}")
+    if args.workload == "dp_stub":
+        out = bench_dp_stub(args)
+    elif args.workload.startswith("lm"):
         out = bench_lm(args)
     else:
         out = bench_vit(args)
-        if args.with_lm and out is not None:
+        if not args.no_lm:   # every rank: the LM line is a DDP run over the same ranks
             a2 = argparse.Namespace(**vars(args))
-            a2.steps, a2.warmup, a2.workload = 3, 1, "lm124m"
-            out["lm124m"] = bench_lm(a2)
+            a2.steps, a2.warmup, a2.workload = args.lm_steps, args.lm_warmup, "lm124m"
+            lm = bench_lm(a2)
+            if out is not None:
+                out["lm124m"] = lm
     if out is not None:
         print(json.dumps(out), flush=True)
     if dp.is_initialized():

@@ -153,11 +153,43 @@ def make_eval_step():
     return eval_step
 
 
+def _device_storages(objs, depth=6):
+    """Every device storage reachable from objs (tensors, dicts, lists, plain objects)."""
+    found, seen = {}, set()
+
+    def walk(o, d):
+        if isinstance(o, torch.Tensor):
+            if o.is_cuda:
+                st = o.untyped_storage()
+                found.setdefault(st.data_ptr(), st)
+            return
+        if d <= 0 or id(o) in seen or isinstance(o, (str, bytes, int, float, bool, type(None))):
+            return
+        seen.add(id(o))
+        if isinstance(o, dict):
+            vals = o.values()
+        elif isinstance(o, (list, tuple)):
+            vals = o
+        elif hasattr(o, "__dict__"):
+            vals = vars(o).values()
+        else:
+            return
+        for v in vals:
+            walk(v, d - 1)
+
+    for o in objs:
+        walk(o, depth)
+    return list(found.values())
+
+
 class GraphedTrainStep:
     """One hipGraph per step: seed advance, zero-grad, forward, backward,
     (all-reduce outside the graph when world_size > 1), optimizer.
 
-    Inputs are copied into static buffers before each replay."""
+    Inputs are copied into static buffers before each replay.  The warm-up launches that
+    precede capture (lazy library setup) run on zero images; the params, optimizer state and
+    seed they touch are snapshotted and restored, so construction does not train the model,
+    and under data parallelism the warm-up gradients are all-reduced like a real step."""
 
     def __init__(self, state: TrainState, image_shape, warmup=2):
         self.state = state
@@ -174,11 +206,22 @@ class GraphedTrainStep:
         self.g_opt = torch.cuda.CUDAGraph() if (self.distributed and self.opt_graphed) else None
         s = self.stream
         s.wait_stream(torch.cuda.current_stream())
+        store = state.params
+        saved = [(st, st.clone()) for st in _device_storages([store.flat, store.shadow, self.runner.seed,
+                                                              state.opt_state])]
+        host = {k: v for k, v in vars(state.opt_state).items() if isinstance(v, (int, float, bool))}  # e.g. host_step
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self._fb()
+                if self.distributed:
+                    dp.all_reduce_grads(store)
                 self._opt()
             torch.cuda.synchronize()
+            for st, copy in saved:
+                st.copy_(copy)
+            torch.cuda.synchronize()
+            for k, v in host.items():
+                setattr(state.opt_state, k, v)
             if self.distributed or not self.opt_graphed:
                 with torch.cuda.graph(self.g_fb, stream=s):
                     self._fb()

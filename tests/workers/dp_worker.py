@@ -1,0 +1,121 @@
+"""One rank of the 2-process data-parallel GPU test (tests/test_dp_gpu.py).  Both ranks share
+cuda:0 and talk over gloo (RCCL refuses two ranks on one device); the code under test is the
+same DP path the RCCL run takes (GraphedTrainStep's reduce branch, OverlappedReducer).
+
+Each rank: (1) its LOCAL gradient with the reducer off, (2) gathers the peers' local gradients
+-> expected mean, (3) one data-parallel step, then checks on the GPU results: the reduced
+gradient (ViT: still in the grad buffer after the step) equals the mean; the applied update
+equals the oracle optimizer fed that mean (tests/parity_util bounds); and writes its params'
+checksum so the parent can check the replicas are bit-identical.  Writes a JSON report."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def gather_mean(local):
+    outs = [torch.zeros_like(local) for _ in range(dist.get_world_size())]
+    dist.all_gather(outs, local)
+    return sum(outs) / len(outs)
+
+
+def vit(rep, dev):
+    from oracle import optim as oopt
+    from plaincv_amd.engine import GraphedTrainStep, create_train_state
+    from plaincv_amd.models.vit_small import VisionTransformer
+    from tests.parity_util import step_bound, step_rel
+    from utils import Config
+    rank = dist.get_rank()
+    m = VisionTransformer(num_classes=10, patch_size=4, hidden_size=64, mlp_dim=128, num_layers=2, num_heads=2,
+                          dropout_rate=0.0)
+    shape = (8, 16, 16, 3)
+    cfg = Config(optim="muon", lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9)
+    init = m.init(3, shape)
+    st = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=init)
+    g = torch.Generator().manual_seed(100 + rank)
+    imgs = torch.randint(0, 256, shape, generator=g, dtype=torch.uint8).to(dev)
+    labels = torch.randint(0, 10, (shape[0],), generator=g, dtype=torch.int32).to(dev)
+    r = st.runner_for(shape)
+    st.params.zero_grad()
+    r.forward(imgs, labels, train=True)
+    r.backward(train=True)
+    torch.cuda.synchronize()
+    local = st.params.grad_flat.cpu().clone()
+    mean = gather_mean(local)
+    step = GraphedTrainStep(st, shape, warmup=2)
+    # construction's warm-up steps must leave params (and optimizer state) as they were
+    rep["warmup_restored"] = all(torch.equal(st.params.params[k].cpu(), init[k]) for k in init)
+    p0 = st.params.to_dict()
+    step(imgs, labels)
+    torch.cuda.synchronize()
+    red = st.params.grad_flat.cpu()
+    rep["grad_mean_err"] = float((red - mean).abs().max() / mean.abs().max())
+    p1 = st.params.to_dict()
+    gm = {k: st.params._view(mean, st.params.leaf(k)).clone() for k in init}
+    tx = oopt.get_optimizer(cfg)
+    u, _ = tx.update(gm, tx.init(p0), p0)
+    rep["step_excess"] = max(step_rel(p0[k], p1[k], u[k]) / step_bound("muon", k, p0[k]) for k in init)
+    rep["checksum"] = float(sum(v.double().sum() * (i + 1) for i, v in enumerate(p1.values())))
+
+
+def lm(rep, dev):
+    from oracle import optim as oopt
+    from plaincv_amd.engine.lm import create_lm_state, make_apply_grads_fn, make_train_fns
+    from plaincv_amd.models.LM.constructor import construct_model
+    from tests.parity_util import step_bound, step_rel
+    from utils import Config
+    rank = dist.get_rank()
+    cfg = Config(model="transformer", vocab_size=512, d_model=128, expand="8/3", n_layers=2, n_heads=2,
+                 mlp_class="glu", seq_len=64, tie_embeddings=False, rope_theta=500000.0, dtype="bfloat16", seed=0,
+                 optim="adamw", lr=1e-3, weight_decay=0.1, beta1=0.9, beta2=0.95)
+    model, _, variables = construct_model(cfg)
+    b, T, accum = 2, 64, 2
+    g = torch.Generator().manual_seed(200 + rank)
+    batches = [torch.randint(0, 512, (b, T + 1), generator=g, dtype=torch.int32).to(dev) for _ in range(accum)]
+    compute_grads, _ = make_train_fns()
+    # (1) local accumulated gradient: a second state with the reducer switched off
+    loc = create_lm_state(cfg, model, variables, b, dev, accum=accum)
+    loc.reducer = None
+    for x in batches:
+        compute_grads(loc, x)
+    torch.cuda.synchronize()
+    mean = gather_mean(loc.params.grad_flat.cpu().clone())
+    # (2) the DP step: reductions overlapped with the last micro-step's backward
+    st = create_lm_state(cfg, model, variables, b, dev, accum=accum)
+    # the reducer's bucket: small enough that the tiny model's backward launches several
+    st.reducer.bucket = 4096
+    p0 = st.params.to_dict()
+    for x in batches:
+        compute_grads(st, x)
+    rep["buckets_during_backward"] = st.reducer.launched
+    apply_grads = make_apply_grads_fn(None)
+    st, _ = apply_grads(st)
+    torch.cuda.synchronize()
+    p1 = st.params.to_dict()
+    gm = {k: st.params._view(mean, st.params.leaf(k)).clone() for k in p0}
+    tx = oopt.get_optimizer(cfg)
+    u, _ = tx.update(gm, tx.init(p0), p0)
+    rep["step_excess"] = max(step_rel(p0[k], p1[k], u[k]) / step_bound("adamw", k, p0[k]) for k in p0)
+    rep["checksum"] = float(sum(v.double().sum() * (i + 1) for i, v in enumerate(p1.values())))
+
+
+def main():
+    which, out = sys.argv[1], sys.argv[2]
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo")
+    rep = {"rank": dist.get_rank()}
+    (vit if which == "vit" else lm)(rep, dev)
+    dist.barrier()
+    with open(out, "w") as f:
+        json.dump(rep, f)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
