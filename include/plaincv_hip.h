@@ -105,14 +105,20 @@ int pcv_gemm_grouped_run(const void* plan_dev, int n, int tile /* as planned */,
 int pcv_attn_fwd(const void* q, const void* k, const void* v, int64_t ldq, void* out, int64_t ldo,
                  float* lse2, int B, int T, int H, int head_dim, int causal,
                  float dropout_rate, const uint16_t* drop_mask, const int* doc_start, const int* doc_end,
-                 void* stream);
+                 void* out_lo, void* stream);
 int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t ldq,
                  const void* o, int64_t ldo, const void* dout, int64_t lddo,
                  const float* lse2, float* delta_ws /* [B,H,T] */,
                  void* dq, void* dk, void* dv, int64_t lddq,
                  int B, int T, int H, int head_dim, int causal,
                  float dropout_rate, const uint16_t* drop_mask, int delta_ready, const int* doc_start,
-                 const int* doc_end, void* stream);
+                 const int* doc_end, const void* o_lo, void* stream);
+/* out_lo / o_lo (optional, short-sequence path only -- pcv_attn_short_ok): the forward also
+ * writes O's bf16 rounding residual O - bf16(O) (row stride ldo, P.V accumulated with P split
+ * into bf16 hi + lo), and the backward forms delta = <dO, O_hi + O_lo> from it, so delta
+ * matches the backward's own fp32 softmax P.  Required for deep-layer dQ accuracy when keys
+ * share a large common component (DESIGN.md §3).  PCV_EINVAL elsewhere, or with delta_ready. */
+int pcv_attn_short_ok(int T, int head_dim, int causal);
 /* (delta_ready: delta_ws already holds rowsum(dO * O) per (b, h, t) -- pcv_gemm_bf16's
  * attention-delta epilogue on the GEMM that produced dO -- so its kernel is skipped.)
  * doc_start/doc_end (optional, causal only): int32 [B*T], the intra-document causal mask of

@@ -41,6 +41,13 @@ struct AttnArgs {
   const uint16_t* mask;                   // packed keep bits, see drop_word()
   int n64;                                // key-tile count of the mask (2*ceil(T/128))
   int delta_ready;                        // bwd: delta already computed (fused into the dO producer)
+  // short (ViT) path: O's bf16 rounding residual O - bf16(O) (fwd writes it, bwd reads it; row
+  // strides ldout / ldo).  The backward's softmax row constant delta = <dO, O> must be formed
+  // from the O the backward's own P reproduces (fp32 P, not the bf16-rounded P of the P.V
+  // MFMA, not bf16(O)): a mismatch eps breaks sum_k dS = 0 and lands in dQ as -eps * (mean
+  // key), which deep ViT layers (keys sharing a component 2-7x their spread) amplified to
+  // 5-30 % dQ error (tools/attn_layer_diag.py).  nullptr: hi only.
+  bf16* out_lo; const bf16* o_lo;
   // intra-document causal mask (train_lm.py:107-131, data_prep_utils.py:14-43): key k is visible to
   // query q iff dstart[q] <= k <= q, i.e. same document; [B*T] int32, nullptr = plain causal.
   // dend[t] = end (exclusive) of t's document.  Documents are contiguous, so dstart/dend are
@@ -875,10 +882,22 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         if (2 * u < nt) {
+          // P = hi + lo (bf16 each): O accumulates P.V at ~16 mantissa bits of P, so the
+          // backward's delta = <dO, O> matches its own fp32 P (see AttnArgs::out_lo)
           const bf16x8 pa = pack8(s[2 * u], s[2 * u + 1]);
+          f32x4 r0, r1;
 #pragma unroll
-          for (int d = 0; d < DT; ++d)
-            acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_frag<DH>(Vs, 2 * c + u, 16 * d), acc[d], 0, 0, 0);
+          for (int r = 0; r < 4; ++r) {
+            r0[r] = s[2 * u][r] - bf2f(pa[r]);
+            r1[r] = s[2 * u + 1][r] - bf2f(pa[4 + r]);
+          }
+          const bf16x8 pl = pack8(r0, r1);
+#pragma unroll
+          for (int d = 0; d < DT; ++d) {
+            const bf16x8 vt = tr_frag<DH>(Vs, 2 * c + u, 16 * d);
+            acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vt, acc[d], 0, 0, 0);
+            acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vt, acc[d], 0, 0, 0);
+          }
         }
       }
     }
@@ -891,7 +910,12 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
       const int qq = gq * 16 + 4 * g + r;
       if (qq < T) {
 #pragma unroll
-        for (int d = 0; d < DT; ++d) a.out[(bT + qq) * a.ldout + h * DH + 16 * d + (lane & 15)] = f2bf(acc[d][r] * iv);
+        for (int d = 0; d < DT; ++d) {
+          const float o = acc[d][r] * iv;
+          const bf16 oh = f2bf(o);
+          a.out[(bT + qq) * a.ldout + h * DH + 16 * d + (lane & 15)] = oh;
+          if (a.out_lo) a.out_lo[(bT + qq) * a.ldout + h * DH + 16 * d + (lane & 15)] = f2bf(o - bf2f(oh));
+        }
       }
     }
     if (g == 0 && qv) a.lse2[((int64_t)b * a.H + h) * T + myq] = m2 + log2f(l);
@@ -935,17 +959,19 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
   } else {
     // delta = rowsum(dO o O): 4 lanes x 8 columns per row, all loads issued first
     constexpr int ITER = (SH_TMAX * 4 + SH_THREADS - 1) / SH_THREADS;
-    bf16x8 xo[ITER], xd[ITER];
+    bf16x8 xo[ITER], xl[ITER], xd[ITER];
     float lv[ITER];
 #pragma unroll
     for (int i = 0; i < ITER; ++i) {
       const int idx = threadIdx.x + SH_THREADS * i;
       const int r = idx >> 2, c = (idx & 3) * 8;
       xo[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      xl[i] = xo[i];
       xd[i] = xo[i];
       lv[i] = 0.f;
       if (r < T) {
         xo[i] = *reinterpret_cast<const bf16x8*>(a.o + (bT + r) * a.ldo + h * DH + c);
+        if (a.o_lo) xl[i] = *reinterpret_cast<const bf16x8*>(a.o_lo + (bT + r) * a.ldo + h * DH + c);
         xd[i] = *reinterpret_cast<const bf16x8*>(a.dout + (bT + r) * a.lddo + h * DH + c);
         lv[i] = a.lse2[bh * T + r];
       }
@@ -956,7 +982,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
       const int r = idx >> 2;
       float sum = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sum += bf2f(xo[i][j]) * bf2f(xd[i][j]);
+      for (int j = 0; j < 8; ++j) sum += (bf2f(xo[i][j]) + bf2f(xl[i][j])) * bf2f(xd[i][j]);
       sum += __shfl_xor(sum, 1, 64);
       sum += __shfl_xor(sum, 2, 64);
       if ((idx & 3) == 0 && r < TP) {
@@ -1128,6 +1154,8 @@ static void launch_bwd(const AttnArgs& a, hipStream_t s) {
 
 template <bool FWD>
 static int dispatch(const AttnArgs& a, int dh, int causal, int drop, hipStream_t s) {
+  if ((a.out_lo || a.o_lo) && !short_ok(a, dh, causal, FWD)) return PCV_EINVAL;   // short path only
+  if (a.o_lo && a.delta_ready) return PCV_EINVAL;                                 // delta is formed here
   if (short_ok(a, dh, causal, FWD)) {
     const int e = FWD ? (drop ? launch_short_fwd<true>(a, s) : launch_short_fwd<false>(a, s))
                       : (drop ? launch_short_bwd<true>(a, s) : launch_short_bwd<false>(a, s));
@@ -1180,14 +1208,15 @@ extern "C" int pcv_attn_fwd(const void* q, const void* k, const void* v, int64_t
                             void* out, int64_t ldo, float* lse2,
                             int B, int T, int H, int head_dim, int causal,
                             float dropout_rate, const uint16_t* drop_mask, const int* doc_start,
-                            const int* doc_end, void* stream) {
+                            const int* doc_end, void* out_lo, void* stream) {
   if (B <= 0 || T <= 0 || H <= 0) return PCV_EINVAL;
+  if (out_lo && !pcv_aligned16(out_lo)) return PCV_EALIGN;
   if ((doc_start != nullptr) != (doc_end != nullptr) || (doc_start && !causal)) return PCV_EINVAL;
   if (dropout_rate > 0.f && (!drop_mask || ((uintptr_t)drop_mask & 7))) return PCV_EINVAL;
   if ((ldq & 7) || (ldo & 7) || !pcv_aligned16(q) || !pcv_aligned16(k) || !pcv_aligned16(v)) return PCV_EALIGN;
   AttnArgs a{};
   a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.ldq = ldq;
-  a.out = (bf16*)out; a.ldout = ldo; a.lse2 = lse2;
+  a.out = (bf16*)out; a.ldout = ldo; a.lse2 = lse2; a.out_lo = (bf16*)out_lo;
   a.B = B; a.T = T; a.H = H; a.scale = 1.f / sqrtf((float)head_dim);
   a.dstart = doc_start; a.dend = doc_end;
   set_drop(a, dropout_rate, drop_mask);
@@ -1200,8 +1229,9 @@ extern "C" int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t
                             void* dq, void* dk, void* dv, int64_t lddq,
                             int B, int T, int H, int head_dim, int causal,
                             float dropout_rate, const uint16_t* drop_mask, int delta_ready,
-                            const int* doc_start, const int* doc_end, void* stream) {
+                            const int* doc_start, const int* doc_end, const void* o_lo, void* stream) {
   if (B <= 0 || T <= 0 || H <= 0) return PCV_EINVAL;
+  if (o_lo && !pcv_aligned16(o_lo)) return PCV_EALIGN;
   if ((doc_start != nullptr) != (doc_end != nullptr) || (doc_start && !causal)) return PCV_EINVAL;
   if (dropout_rate > 0.f && (!drop_mask || ((uintptr_t)drop_mask & 7))) return PCV_EINVAL;
   if ((ldq & 7) || (ldo & 7) || (lddo & 7) || !pcv_aligned16(q) || !pcv_aligned16(k) || !pcv_aligned16(v) ||
@@ -1209,7 +1239,7 @@ extern "C" int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t
     return PCV_EALIGN;
   AttnArgs a{};
   a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.ldq = ldq;
-  a.o = (const bf16*)o; a.ldo = ldo; a.dout = (const bf16*)dout; a.lddo = lddo;
+  a.o = (const bf16*)o; a.ldo = ldo; a.dout = (const bf16*)dout; a.lddo = lddo; a.o_lo = (const bf16*)o_lo;
   a.dq = (bf16*)dq; a.dk = (bf16*)dk; a.dv = (bf16*)dv; a.lddq = lddq;
   a.lse2 = (float*)lse2; a.delta = delta_ws; a.delta_ready = delta_ready;
   a.B = B; a.T = T; a.H = H; a.scale = 1.f / sqrtf((float)head_dim);
@@ -1219,6 +1249,14 @@ extern "C" int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t
 }
 
 extern "C" int64_t pcv_attn_mask_words(int T) { return T > 0 ? drop_words(T) : 0; }
+
+// Whether (T, head_dim, causal) takes the one-workgroup short-sequence kernels (the only path
+// that writes / reads the O residual out_lo / o_lo).
+extern "C" int pcv_attn_short_ok(int T, int head_dim, int causal) {
+  AttnArgs a{};
+  a.T = T;
+  return short_ok(a, head_dim, causal, true) ? 1 : 0;
+}
 
 extern "C" int pcv_attn_drop_mask(const uint32_t* seed, uint32_t site, uint32_t site_stride, int layers, int T,
                                   float dropout_rate, uint16_t* mask, void* stream) {

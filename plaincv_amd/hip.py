@@ -29,9 +29,10 @@ SIGNATURES = {
     "pcv_gemm_desc_size": [],
     "pcv_gemm_grouped_plan": [P, I32, I32, P, P],
     "pcv_gemm_grouped_run": [P, I32, I32, I64, P],
-    "pcv_attn_fwd": [P, P, P, I64, P, I64, P, I32, I32, I32, I32, I32, F32, P, P, P, P],
+    "pcv_attn_fwd": [P, P, P, I64, P, I64, P, I32, I32, I32, I32, I32, F32, P, P, P, P, P],
     "pcv_attn_bwd": [P, P, P, I64, P, I64, P, I64, P, P, P, P, P, I64, I32, I32, I32, I32, I32,
-                     F32, P, I32, P, P, P],
+                     F32, P, I32, P, P, P, P],
+    "pcv_attn_short_ok": [I32, I32, I32],
     "pcv_attn_mask_words": [I32],
     "pcv_attn_drop_mask": [P, U32, U32, I32, I32, F32, P, P],
     "pcv_layernorm_fwd": [P, I64, P, P, P, I64, P, P, I64, I32, F32, P],

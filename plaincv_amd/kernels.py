@@ -253,37 +253,50 @@ def _doc_arrays(doc, B, T, causal):
     return ds, de
 
 
+def attn_short_ok(T, Dh, causal):
+    """Whether (T, Dh, causal) runs the one-workgroup short-sequence kernels (out_lo / o_lo support)."""
+    return bool(hip.load().pcv_attn_short_ok(int(T), int(Dh), int(causal)))
+
+
 def attn_fwd(qkv, out, lse2, B, T, H, Dh, causal, drop_rate=0.0, mask=None, q_off=0, k_off=None, v_off=None,
-             doc=None):
+             doc=None, out_lo=None):
     """Flash attention forward on packed qkv [B*T, ld] (q|k|v column blocks); `mask` = attn_drop_mask bits;
-    doc = (doc_start, doc_end) per-token document bounds for the intra-document causal mask."""
+    doc = (doc_start, doc_end) per-token document bounds for the intra-document causal mask;
+    out_lo (short path only): O's bf16 rounding residual, same shape/stride as out, for attn_bwd's o_lo."""
     D = H * Dh
     k_off = D if k_off is None else k_off
     v_off = 2 * D if v_off is None else v_off
     _chk(qkv.dtype == BF16 and out.dtype == BF16 and lse2.dtype == F32, "attn dtypes")
     _chk(qkv.shape[0] == B * T and out.shape[0] == B * T and lse2.numel() >= B * H * T, "attn shapes")
     _dev(qkv, out, lse2)
+    if out_lo is not None:
+        _chk(out_lo.dtype == BF16 and out_lo.shape == out.shape and out_lo.stride() == out.stride(), "attn out_lo")
+        _dev(out_lo)
     ds, de = _doc_arrays(doc, B, T, causal)
     base = qkv.data_ptr()
     es = qkv.element_size()
     hip.call("pcv_attn_fwd", base + q_off * es, base + k_off * es, base + v_off * es, _ld(qkv),
              ptr(out), _ld(out), ptr(lse2), B, T, H, Dh, int(causal), float(drop_rate),
-             ptr(mask), ptr(ds), ptr(de), stream_ptr())
+             ptr(mask), ptr(ds), ptr(de), ptr(out_lo), stream_ptr())
 
 
 def attn_bwd(qkv, o, dout, lse2, delta_ws, dqkv, B, T, H, Dh, causal, drop_rate=0.0, mask=None, delta_ready=False,
-             doc=None):
+             doc=None, o_lo=None):
     D = H * Dh
     _chk(qkv.dtype == BF16 and dqkv.dtype == BF16 and dout.dtype == BF16 and o.dtype == BF16, "attn bwd dtypes")
     _chk(dqkv.shape[0] == B * T and dqkv.shape[1] >= 3 * D and delta_ws.numel() >= B * H * T, "attn bwd shapes")
     _dev(qkv, o, dout, lse2, delta_ws, dqkv)
+    if o_lo is not None:
+        _chk(o_lo.dtype == BF16 and o_lo.shape == o.shape and o_lo.stride() == o.stride() and not delta_ready,
+             "attn o_lo")
+        _dev(o_lo)
     ds, de = _doc_arrays(doc, B, T, causal)
     base, es = qkv.data_ptr(), qkv.element_size()
     dbase = dqkv.data_ptr()
     hip.call("pcv_attn_bwd", base, base + D * es, base + 2 * D * es, _ld(qkv), ptr(o), _ld(o), ptr(dout),
              _ld(dout), ptr(lse2), ptr(delta_ws), dbase, dbase + D * es, dbase + 2 * D * es, _ld(dqkv),
              B, T, H, Dh, int(causal), float(drop_rate), ptr(mask), int(delta_ready), ptr(ds), ptr(de),
-             stream_ptr())
+             ptr(o_lo), stream_ptr())
 
 
 def layernorm_fwd(x, scale, bias, y, mean, rstd, eps=1e-6):

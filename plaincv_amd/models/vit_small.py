@@ -168,6 +168,10 @@ class ViTRunner:
         self.st1 = [(e(R), e(R)) for _ in range(Lc)]
         self.qkv = [e(R, 3 * D, dt=bf) for _ in range(Lc)]
         self.o = [e(R, D, dt=bf) for _ in range(Lc)]
+        # O's bf16 rounding residual: the attention backward forms its softmax row constant from
+        # O_hi + O_lo so that it matches its own fp32 P (AttnArgs::out_lo)
+        self.short_attn = K.attn_short_ok(self.T, D // H, False)
+        self.o_lo = [e(R, D, dt=bf) for _ in range(Lc)] if self.short_attn else [None] * Lc
         self.lse = [e(B * H * self.T) for _ in range(Lc)]
         # broadcast attention-dropout keep bits, drawn once per step for all layers
         self.mask_words = K.attn_mask_words(self.T)
@@ -327,7 +331,7 @@ class ViTRunner:
                 K.layernorm_fwd(x, w["s0"], w["c0"], self.y0[0], *self.st0[0])
             K.gemm(self.y0[i], w["Wqkv"], self.qkv[i], bias=w["bqkv"])
             K.attn_fwd(self.qkv[i], self.o[i], self.lse[i], B, T, H, Dh, causal=False, drop_rate=rate,
-                       mask=self._mask(i))
+                       mask=self._mask(i), out_lo=self.o_lo[i])
             if self.fuse_ln:   # out projection + residual + LayerNorm_1 in one launch
                 K.gemm_ln(self.o[i], w["Wo"], self.x1s[i], ln_mode=1, bias=w["bo"], res=x, ln_scale=w["s1"],
                           ln_bias=w["c1"], ln_y=self.y1[i], ln_mean=self.st1[i][0], ln_rstd=self.st1[i][1])
@@ -434,10 +438,16 @@ class ViTRunner:
                     K.gemm(self.o[i], dxb_mid, w["gWo"], ta=True, beta=1.0)
                 if not self.fuse_ln:
                     K.colsum(dx_mid, w["gbo"])
-            # dO = dy Wo^T; its epilogue also forms the attention-backward row constant delta
-            K.gemm(dxb_mid, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H))
-            K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
-                       causal=False, drop_rate=rate, mask=self._mask(i), delta_ready=True)
+            if self.short_attn:
+                # dO = dy Wo^T; the short backward forms delta = <dO, O_hi + O_lo> in its prologue
+                K.gemm(dxb_mid, w["Wo"], self.do, tb=True)
+                K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
+                           causal=False, drop_rate=rate, mask=self._mask(i), o_lo=self.o_lo[i])
+            else:
+                # dO = dy Wo^T; its epilogue also forms the attention-backward row constant delta
+                K.gemm(dxb_mid, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H))
+                K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
+                           causal=False, drop_rate=rate, mask=self._mask(i), delta_ready=True)
             with self._fork():
                 if self.wgrad is None:
                     K.gemm(self.y0[i], dqkv, w["gWqkv"], ta=True, beta=1.0)
