@@ -1,17 +1,21 @@
-"""ViT training driver on the MI355X hot path (mirrors train.py:93-125, 330-509 of the reference).
+"""ViT training driver on the MI355X hot path (mirrors train.py:93-134, 330-529 of the reference).
 
-    python train.py --config config_vit.yaml [--job_idx N]
-    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 train.py --config config_vit.yaml
+    python train.py --config=config/config_vit.yaml [--exp_name=NAME] [--job_idx=N] [--job_cluster=C]
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 train.py --config=config/config_vit.yaml
 
-Config keys as the reference (dataset, batch_size, num_epochs, image_size, seed, model=vit_small,
-vit_patch_size/hidden_size/mlp_dim/layers/heads/dropout/use_layernorm, optim + its keys,
-data_root) and the per-epoch log line {epoch, train_loss, train_accuracy, eval_loss,
-eval_accuracy, epoch_time}.  Every epoch gets fresh iterators with seed + epoch
-(train.py:369-374).  One process per GPU: rank r trains on batches r, r + world, ... of the
-epoch's stream with the gradient mean over RCCL; eval metrics are averaged over ranks.
-Out of scope: wandb, eigen tracking, curvature CSVs, PN-S/Sophia/HF.
+Same flags as the reference (train.py:49-55, utils.py:60-70).  ``model: transformer`` configs are
+handed to ``train_lm.run`` exactly as the reference does (train.py:132-134).  Config keys as the
+reference (dataset, batch_size, num_epochs, image_size, num_channels, num_classes, seed,
+model in {vit, vit_small, vision_transformer}, vit_patch_size/hidden_size/mlp_dim/layers/heads/
+dropout/use_layernorm/use_batchnorm, optim + its keys, data_root) and the same outputs: the
+per-epoch log line {epoch, train_loss, train_accuracy, eval_loss, eval_accuracy, epoch_time}, the
+``Epoch NNN | ...`` summary line, the experiment dir with config.yaml, and the
+``{optim}_metrics.csv`` + eval-loss PNG curves at the end (train.py:407-520).  Every epoch gets
+fresh iterators with seed + epoch (train.py:369-374).  One process per GPU: rank r trains on
+batches r, r + world, ... of the epoch's stream with the gradient mean over RCCL; metrics are
+averaged over ranks.  Out of scope: ResNet/MLP models, wandb, TensorBoard, eigen
+tracking, curvature CSVs, PN-S/Sophia/HF.
 """
-import argparse
 import time
 
 import torch
@@ -20,40 +24,58 @@ from plaincv_amd.data.images import get_datasets
 from plaincv_amd.engine import create_train_state, make_eval_step, make_train_step
 from plaincv_amd.engine import data_parallel as dp
 from plaincv_amd.models.vit_small import VisionTransformer
-from utils import load_config, log_scalar_dict
+from utils import load_config, log_scalar_dict, maybe_make_dir, parse_flags, save_loss_curves
 
 NUM_CLASSES = {"fashion_mnist": 10, "tiny_imagenet": 200, "tiny_imagenet_synthetic": 200}
 CHANNELS = {"fashion_mnist": 1, "tiny_imagenet": 3, "tiny_imagenet_synthetic": 3}
+VIT_NAMES = {"vit", "vit_small", "vision_transformer"}
+
+
+def num_classes(cfg):
+    return int(getattr(cfg, "num_classes", None) or NUM_CLASSES[cfg.dataset])
 
 
 def construct_model(cfg):
-    """train.py:367-405 (vit_* keys and defaults)."""
-    if not str(cfg.model).startswith("vit"):
-        raise ValueError(f"only the ViT models are on the MI355X hot path, got model={cfg.model!r}")
+    """train.py:93-125: the ViT branch (vit_* keys and defaults)."""
+    if cfg.model not in VIT_NAMES:
+        raise ValueError(f"Unknown model: {cfg.model} (the MI355X hot path builds the ViT: "
+                         f"{sorted(VIT_NAMES)}; ResNet/MLP are out of scope)")
     g = lambda k, d: getattr(cfg, k, d)  # noqa: E731
-    if g("vit_use_batchnorm", False):
-        raise NotImplementedError("vit_use_batchnorm=True is SURVEY §8f-3 'next'")
-    return VisionTransformer(num_classes=NUM_CLASSES[cfg.dataset], patch_size=g("vit_patch_size", 4),
+    return VisionTransformer(num_classes=num_classes(cfg), patch_size=g("vit_patch_size", 4),
                              hidden_size=g("vit_hidden_size", 128), mlp_dim=g("vit_mlp_dim", 256),
                              num_layers=g("vit_layers", 4), num_heads=g("vit_heads", 4),
-                             dropout_rate=g("vit_dropout", 0.1), use_layernorm=g("vit_use_layernorm", True))
+                             dropout_rate=g("vit_dropout", 0.1), use_layernorm=g("vit_use_layernorm", True),
+                             use_batchnorm=g("vit_use_batchnorm", False))
+
+
+def image_shape(cfg):
+    size = int(getattr(cfg, "image_size", None) or (28 if cfg.dataset == "fashion_mnist" else 64))
+    ch = int(getattr(cfg, "num_channels", None) or CHANNELS[cfg.dataset])
+    return (int(cfg.batch_size), size, size, ch)
 
 
 def run(cfg):
+    if cfg.model == "transformer" or str(cfg.model).startswith("pythia"):
+        from train_lm import run as run_lm       # train.py:132-134
+        return run_lm(cfg)
     rank, _, world, dev = dp.init_from_env()
+    maybe_make_dir(cfg, rank=rank)
+    if getattr(cfg, "eigen_tracking_enabled", False) and rank == 0:
+        print("note: eigen_tracking_enabled is ignored (eigen tracking is outside the MI355X hot path)")
     model = construct_model(cfg)
-    size = int(getattr(cfg, "image_size", None) or (28 if cfg.dataset == "fashion_mnist" else 64))
-    shape = (int(cfg.batch_size), size, size, CHANNELS[cfg.dataset])
-    state = create_train_state(int(getattr(cfg, "seed", 0)), model, float(cfg.lr), shape,
-                               NUM_CLASSES[cfg.dataset], cfg=cfg, device=dev)
+    shape = image_shape(cfg)
+    seed = int(getattr(cfg, "seed", 0))
+    state = create_train_state(seed, model, float(cfg.lr), shape, num_classes(cfg), cfg=cfg, device=dev)
     if world > 1:
         torch.distributed.broadcast(state.params.flat, 0)
         state.params.sync_shadow()
     train_step, eval_step = make_train_step(), make_eval_step()
+    wall_times, iters, train_losses, eval_losses, train_accs, eval_accs = [], [], [], [], [], []
+    training_start = time.time()
     step = 0
     for epoch in range(1, int(cfg.num_epochs) + 1):
         t0 = time.time()
-        train_ds, test_ds = get_datasets(cfg.dataset, int(cfg.batch_size), seed=int(getattr(cfg, "seed", 0)) + epoch,
+        train_ds, test_ds = get_datasets(cfg.dataset, int(cfg.batch_size), seed=seed + epoch,
                                          image_size=getattr(cfg, "image_size", None),
                                          data_root=getattr(cfg, "data_root", None))
         tr = torch.zeros(2, device=dev)
@@ -77,18 +99,27 @@ def run(cfg):
         evm = dp.all_reduce_metrics(ev / max(1, nev))
         tl, ta = (float(x) for x in trm.tolist())
         el, ea = (float(x) for x in evm.tolist())
+        epoch_time = time.time() - t0
+        wall_times.append(time.time() - training_start)
+        iters.append(epoch)
+        train_losses.append(tl)
+        eval_losses.append(el)
+        train_accs.append(ta)
+        eval_accs.append(ea)
         log_scalar_dict(cfg, {"epoch": epoch, "train_loss": tl, "train_accuracy": ta, "eval_loss": el,
-                              "eval_accuracy": ea, "epoch_time": time.time() - t0}, rank=rank)
+                              "eval_accuracy": ea, "epoch_time": epoch_time}, rank=rank)
+        if rank == 0:
+            print(f"Epoch {epoch:03d} | train loss {tl:.4f}, train acc {ta:.4f} | "
+                  f"eval loss {el:.4f}, eval acc {ea:.4f} | time {epoch_time:.2f}s", flush=True)
+    if rank == 0:
+        save_loss_curves(cfg, cfg.optim, wall_times, iters, train_losses, eval_losses, train_accs, eval_accs)
     return state
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--config", required=True)
-    ap.add_argument("--job_idx", type=int, default=None)
-    a = ap.parse_args()
-    cfg, _ = load_config(a.config, job_idx=a.job_idx)
-    run(cfg)
+def main(argv=None):
+    flags = parse_flags(argv, default_config="config/config.yaml")
+    cfg, _ = load_config(flags.config)
+    return run(cfg)
 
 
 if __name__ == "__main__":

@@ -1,7 +1,10 @@
 """LM training driver on the MI355X hot path (mirrors train_lm.py:465-731 of the reference).
 
-    python train_lm.py --config config.yaml [--job_idx N]                      # one GPU
-    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 train_lm.py --config config.yaml
+    python train_lm.py --config=config/lm.yaml [--exp_name=NAME] [--job_idx=N]     # one GPU
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 train_lm.py --config=config/lm.yaml
+
+Flags as the reference (train_lm.py:76-88 + utils.py:60-70: --config, --exp_name, --job_idx,
+--job_cluster); the experiment dir is created with the resolved config.yaml (train_lm.py:508).
 
 Same config keys as the reference (model/d_model/expand/n_layers/n_heads/mlp_class/seq_len/
 vocab_size/tie_embeddings/rope_theta, trainset_path/validset_path/valid_tokens, sampler/
@@ -13,7 +16,6 @@ takes its own micro-batches of the shared index stream (data.lm_datasampler.Rank
 and the gradient mean is overlapped with the last micro-step's backward.  Out of scope here
 (SURVEY §2): wandb, eigen tracking, curvature batches for PN-S/Sophia/HF.
 """
-import argparse
 import math
 import time
 
@@ -23,7 +25,7 @@ from plaincv_amd.data.lm_loader import get_dataloaders, next_batch
 from plaincv_amd.engine import data_parallel as dp
 from plaincv_amd.engine.lm import create_lm_state, make_apply_grads_fn, make_train_fns
 from plaincv_amd.models.LM.constructor import construct_model
-from utils import load_config, log_scalar_dict
+from utils import load_config, log_scalar_dict, maybe_make_dir, parse_flags
 
 
 def run(cfg):
@@ -34,6 +36,7 @@ def run(cfg):
         ok, err = dp.probe_collectives(dev)          # train_lm.py:442-462
         if not ok:
             raise RuntimeError(f"data-parallel collectives unavailable: {err}")
+    maybe_make_dir(cfg, rank=rank)
     use_doc_mask = bool(getattr(cfg, "intra_doc_masking", False))
     trainloader, validloader = get_dataloaders(cfg, rank=rank, world=world)
     model, _, variables = construct_model(cfg)
@@ -85,13 +88,10 @@ def run(cfg):
     return state
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--config", required=True)
-    ap.add_argument("--job_idx", type=int, default=None)
-    a = ap.parse_args()
-    cfg, _ = load_config(a.config, job_idx=a.job_idx)
-    run(cfg)
+def main(argv=None):
+    flags = parse_flags(argv, default_config="config/lm.yaml")
+    cfg, _ = load_config(flags.config)
+    return run(cfg)
 
 
 if __name__ == "__main__":
