@@ -17,6 +17,7 @@
  */
 #ifndef PLAINCV_HIP_H
 #define PLAINCV_HIP_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -155,6 +156,24 @@ int pcv_layernorm_param_grad(const float* dy, int64_t lddy, const float* x, int6
                              const float* rstd, float* dscale, float* dbias, int64_t R, int D, void* stream);
 int pcv_rmsnorm_param_grad(const void* dy, int64_t lddy, const void* x, int64_t ldx, const float* rstd,
                            float* dscale, int64_t R, int D, void* stream);
+
+/* flax BatchNorm (models/vit_small.py:35-36,49-50,121-122; use_batchnorm=True): momentum 0.99,
+ * eps 1e-5, column statistics over all R rows.  stats: train -> batch mean/rstd (fast variance) and
+ * the running averages updated in place (flax_engine.py:74-85 mutable batch_stats); eval -> mean /
+ * rstd from the running averages (ws unused).  apply: y = (x-mean)*rstd*scale+bias (bf16), any rows
+ * of the same columns (the final norm normalises only the cls rows with the full-batch stats).
+ * bwd (train mode): dx = dres + scale*rstd*(dy - mean(dy) - xhat*mean(dy*xhat)); dscale/dbias +=.
+ * Deterministic (fixed-order partial reduction, no float atomics).  ws: workspace_size(R, D) bytes. */
+size_t pcv_batchnorm_workspace_size(int64_t R, int D);
+int pcv_batchnorm_stats(const float* x, int64_t ldx, int64_t R, int D, int train, float momentum, float eps,
+                        float* ra_mean, float* ra_var, float* mean, float* rstd, void* ws, size_t ws_bytes,
+                        void* stream);
+int pcv_batchnorm_apply(const float* x, int64_t ldx, int64_t R, int D, const float* mean, const float* rstd,
+                        const float* scale, const float* bias, void* y, int64_t ldy, void* stream);
+int pcv_batchnorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, int64_t R, int D,
+                      const float* mean, const float* rstd, const float* scale, const float* dres, int64_t ldres,
+                      float* dx, int64_t lddx, void* dx_bf16, int64_t lddxb, float* dscale, float* dbias,
+                      void* ws, size_t ws_bytes, void* stream);
 
 /* --------------------------------------------------------- elementwise ----
  * RoPE, in place on the q|k column blocks (models/LM/embedding.py:28-66; backward = rotation by -theta). */

@@ -33,6 +33,22 @@ def layernorm(x, scale, bias, eps=1e-6):
     return (x - mean) * torch.rsqrt(var + eps) * scale + bias
 
 
+def batchnorm(x, scale, bias, ra_mean, ra_var, train, momentum=0.99, eps=1e-5):
+    """flax.linen.BatchNorm (models/vit_small.py:35-36,49-50,121-122; defaults momentum 0.99,
+    epsilon 1e-5, axis -1, use_fast_variance): train -> statistics over every axis but the last,
+    var = max(E[x^2]-E[x]^2, 0), running averages ra <- m*ra + (1-m)*stat; eval -> running averages.
+    Returns (y, new_mean, new_var) (the unchanged running averages in eval)."""
+    if train:
+        red = tuple(range(x.dim() - 1))
+        mean = x.mean(red)
+        var = torch.clamp((x * x).mean(red) - mean * mean, min=0.0)
+        new_mean = momentum * ra_mean + (1.0 - momentum) * mean.detach()
+        new_var = momentum * ra_var + (1.0 - momentum) * var.detach()
+    else:
+        mean, var, new_mean, new_var = ra_mean, ra_var, ra_mean, ra_var
+    return (x - mean) * torch.rsqrt(var + eps) * scale + bias, new_mean, new_var
+
+
 def rmsnorm(x, scale, eps=1e-6, out_dtype=None):
     """flax.linen.RMSNorm (models/LM/transformer.py:41-47): stats in fp32,
     y = x * rsqrt(mean(x^2) + eps) * scale, cast once to the compute dtype."""

@@ -8,7 +8,7 @@ from dataclasses import dataclass
 
 import torch
 
-from .nn import dropout, gelu_tanh, layernorm, mm, rnd
+from .nn import batchnorm, dropout, gelu_tanh, layernorm, mm, rnd
 
 # dropout site ids shared with plaincv_amd.models.vit_small (the kernel side)
 SITE_EMBED = 1
@@ -73,13 +73,29 @@ def mlp_block(params, pre, y, cfg: ViTConfig, train, seed, layer, bf16):
     return dropout(o, cfg.dropout_rate, seed, site_mlp_out(layer), train)
 
 
+def _prenorm(params, name, x, cfg, train, batch_stats, new_stats):
+    """EncoderBlock / VisionTransformer pre-norm choice (models/vit_small.py:31-40,46-52,121-124)."""
+    if cfg.use_batchnorm and cfg.use_layernorm:
+        raise ValueError("use_batchnorm and use_layernorm cannot both be True.")
+    if cfg.use_batchnorm:
+        y, m, v = batchnorm(x, params[f"{name}/scale"], params[f"{name}/bias"], batch_stats[f"{name}/mean"],
+                            batch_stats[f"{name}/var"], train)
+        if new_stats is not None:
+            new_stats[f"{name}/mean"], new_stats[f"{name}/var"] = m, v
+        return y
+    if cfg.use_layernorm:
+        return layernorm(x, params[f"{name}/scale"], params[f"{name}/bias"])
+    return x
+
+
 def vit_apply(params, images, cfg: ViTConfig, train: bool = True, seed: int = 0,
-              bf16: bool = False, dtype=torch.float32):
+              bf16: bool = False, dtype=torch.float32, batch_stats=None, new_batch_stats=None):
     """VisionTransformer.__call__ (models/vit_small.py:94-127).
 
-    images: uint8 (B,H,W,C) NHWC.  Returns logits (B, num_classes)."""
-    if cfg.use_batchnorm:
-        raise NotImplementedError("use_batchnorm ViT variant is SURVEY §8f-3 'next'")
+    images: uint8 (B,H,W,C) NHWC.  Returns logits (B, num_classes).  BatchNorm variant:
+    ``batch_stats`` holds the running averages ({"<module path>/mean|var"}); in train mode the
+    updated averages are written into ``new_batch_stats`` (flax mutable=["batch_stats"])."""
+    norm = "BatchNorm" if cfg.use_batchnorm else "LayerNorm"
     x = images.to(dtype) / 255.0
     B, Hh, Ww, C = x.shape
     ps = cfg.patch_size
@@ -94,14 +110,11 @@ def vit_apply(params, images, cfg: ViTConfig, train: bool = True, seed: int = 0,
     x = dropout(x, cfg.dropout_rate, seed, SITE_EMBED, train)
     for i in range(cfg.num_layers):
         pre = f"EncoderBlock_{i}"
-        y = layernorm(x, params[f"{pre}/LayerNorm_0/scale"], params[f"{pre}/LayerNorm_0/bias"]) \
-            if cfg.use_layernorm else x
+        y = _prenorm(params, f"{pre}/{norm}_0", x, cfg, train, batch_stats, new_batch_stats)
         x = x + self_attention(params, f"{pre}/SelfAttention_0", y, cfg, train, seed, i, bf16)
-        y = layernorm(x, params[f"{pre}/LayerNorm_1/scale"], params[f"{pre}/LayerNorm_1/bias"]) \
-            if cfg.use_layernorm else x
+        y = _prenorm(params, f"{pre}/{norm}_1", x, cfg, train, batch_stats, new_batch_stats)
         x = x + mlp_block(params, f"{pre}/MlpBlock_0", y, cfg, train, seed, i, bf16)
-    if cfg.use_layernorm:
-        x = layernorm(x, params["LayerNorm_0/scale"], params["LayerNorm_0/bias"])
+    x = _prenorm(params, f"{norm}_0", x, cfg, train, batch_stats, new_batch_stats)
     cls_repr = x[:, 0]
     return mm(cls_repr, params["Dense_0/kernel"], bf16) + params["Dense_0/bias"]
 
@@ -112,6 +125,7 @@ def vit_param_shapes(cfg: ViTConfig, image_size: int, channels: int):
     Dh = D // H
     ps = cfg.patch_size
     T = (image_size // ps) ** 2 + 1
+    norm = "BatchNorm" if cfg.use_batchnorm else ("LayerNorm" if cfg.use_layernorm else None)
     shapes = {
         "Conv_0/kernel": (ps, ps, channels, D),
         "Conv_0/bias": (D,),
@@ -120,24 +134,24 @@ def vit_param_shapes(cfg: ViTConfig, image_size: int, channels: int):
     }
     for i in range(cfg.num_layers):
         pre = f"EncoderBlock_{i}"
-        if cfg.use_layernorm:
-            shapes[f"{pre}/LayerNorm_0/scale"] = (D,)
-            shapes[f"{pre}/LayerNorm_0/bias"] = (D,)
+        if norm:
+            shapes[f"{pre}/{norm}_0/scale"] = (D,)
+            shapes[f"{pre}/{norm}_0/bias"] = (D,)
         for n in ("query", "key", "value"):
             shapes[f"{pre}/SelfAttention_0/{n}/kernel"] = (D, H, Dh)
             shapes[f"{pre}/SelfAttention_0/{n}/bias"] = (H, Dh)
         shapes[f"{pre}/SelfAttention_0/out/kernel"] = (H, Dh, D)
         shapes[f"{pre}/SelfAttention_0/out/bias"] = (D,)
-        if cfg.use_layernorm:
-            shapes[f"{pre}/LayerNorm_1/scale"] = (D,)
-            shapes[f"{pre}/LayerNorm_1/bias"] = (D,)
+        if norm:
+            shapes[f"{pre}/{norm}_1/scale"] = (D,)
+            shapes[f"{pre}/{norm}_1/bias"] = (D,)
         shapes[f"{pre}/MlpBlock_0/Dense_0/kernel"] = (D, M)
         shapes[f"{pre}/MlpBlock_0/Dense_0/bias"] = (M,)
         shapes[f"{pre}/MlpBlock_0/Dense_1/kernel"] = (M, D)
         shapes[f"{pre}/MlpBlock_0/Dense_1/bias"] = (D,)
-    if cfg.use_layernorm:
-        shapes["LayerNorm_0/scale"] = (D,)
-        shapes["LayerNorm_0/bias"] = (D,)
+    if norm:
+        shapes[f"{norm}_0/scale"] = (D,)
+        shapes[f"{norm}_0/bias"] = (D,)
     shapes["Dense_0/kernel"] = (D, cfg.num_classes)
     shapes["Dense_0/bias"] = (cfg.num_classes,)
     return shapes

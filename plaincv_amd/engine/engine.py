@@ -23,6 +23,7 @@ from .. import kernels as K
 from ..optim.adamw import AdamW
 from ..optim.base import apply_updates
 from ..optim.factory import get_optimizer
+from ..models.vit_small import BatchStats
 from ..params import ParamStore
 from . import data_parallel as dp
 
@@ -73,7 +74,8 @@ class TrainState:
         key = tuple(int(s) for s in image_shape)
         r = self.runners.get(key)
         if r is None:
-            r = self.apply_fn.bind(self.params, key, self.params.device)
+            kw = {} if self.batch_stats is None else {"batch_stats": self.batch_stats}
+            r = self.apply_fn.bind(self.params, key, self.params.device, **kw)
             self.runners[key] = r
         return r
 
@@ -84,19 +86,25 @@ class TrainState:
 
 
 def create_train_state(rng, model_def, learning_rate: float, image_shape, num_classes: int, cfg=None,
-                       curvature_batch=None, device="cuda", init_params=None):
+                       curvature_batch=None, device="cuda", init_params=None, init_batch_stats=None):
     """flax_engine.py:30-66.  ``init_params`` ({name: tensor}) overrides the
-    initialiser (parity tests inject the oracle's params)."""
+    initialiser (parity tests inject the oracle's params); ``init_batch_stats`` likewise for the
+    BatchNorm variant's running averages (default: flax's zeros / ones)."""
     seed = _seed_of(rng, 0) or 0
     layout = model_def.layout(image_shape)
     store = ParamStore(layout, device)
     store.load(init_params if init_params is not None else model_def.init(seed, image_shape))
+    batch_stats = None
+    shapes = getattr(model_def, "batch_stats_shapes", lambda: {})()
+    if shapes:   # variables.get("batch_stats") (flax_engine.py:46-47)
+        batch_stats = BatchStats(shapes, store.device)
+        batch_stats.load(init_batch_stats if init_batch_stats is not None else model_def.init_batch_stats())
     if cfg is None:
         tx = AdamW(learning_rate, weight_decay=1e-4)   # optax.adamw default weight_decay
     else:
-        tx = get_optimizer(cfg, model_def=model_def, curvature_batch=curvature_batch, batch_stats=None)
+        tx = get_optimizer(cfg, model_def=model_def, curvature_batch=curvature_batch, batch_stats=batch_stats)
     opt_state = tx.init(store)
-    st = TrainState(step=0, params=store, opt_state=opt_state, tx=tx, apply_fn=model_def)
+    st = TrainState(step=0, params=store, opt_state=opt_state, tx=tx, apply_fn=model_def, batch_stats=batch_stats)
     st.runner_for(image_shape)
     return st
 
@@ -107,6 +115,13 @@ def _prepare(runner, images, labels):
     if labels is not None and (labels.device != runner.labels.device or labels.dtype != torch.int32):
         labels = labels.to(device=runner.labels.device, dtype=torch.int32, non_blocking=True)
     return images.contiguous(), labels
+
+
+def _reduce_batch_stats(state):
+    """Under data parallelism every rank's BatchNorm sees its own micro-batch; the running averages
+    (linear EMAs) are averaged over ranks once per step so the replicas stay identical."""
+    if state.batch_stats is not None and dp.world_size() > 1:
+        dp.all_reduce_mean_(state.batch_stats.flat)
 
 
 def make_train_step(return_updates: bool = False):
@@ -126,6 +141,7 @@ def make_train_step(return_updates: bool = False):
         metrics = runner.forward(images, labels, train=True, need_grad=True)
         runner.backward(train=True)
         dp.all_reduce_grads(store)
+        _reduce_batch_stats(state)
         if return_updates:
             grads = {k: v.clone() for k, v in store.grads.items()}
             updates, state.opt_state = state.tx.update(store.grads, state.opt_state, store)
@@ -208,13 +224,14 @@ class GraphedTrainStep:
         s.wait_stream(torch.cuda.current_stream())
         store = state.params
         saved = [(st, st.clone()) for st in _device_storages([store.flat, store.shadow, self.runner.seed,
-                                                              state.opt_state])]
+                                                              state.opt_state, state.batch_stats])]
         host = {k: v for k, v in vars(state.opt_state).items() if isinstance(v, (int, float, bool))}  # e.g. host_step
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self._fb()
                 if self.distributed:
                     dp.all_reduce_grads(store)
+                    _reduce_batch_stats(state)
                 self._opt()
             torch.cuda.synchronize()
             for st, copy in saved:
@@ -251,6 +268,7 @@ class GraphedTrainStep:
         self.g_fb.replay()
         if self.distributed:
             dp.all_reduce_grads(self.state.params)
+            _reduce_batch_stats(self.state)
         if self.g_opt is not None:
             self.g_opt.replay()
         elif self.distributed or not self.opt_graphed:

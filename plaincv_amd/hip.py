@@ -17,6 +17,7 @@ I32 = ctypes.c_int
 U32 = ctypes.c_uint32
 I64 = ctypes.c_int64
 F32 = ctypes.c_float
+SZ = ctypes.c_size_t
 
 # name -> argtypes (return type is always int status)
 SIGNATURES = {
@@ -41,6 +42,10 @@ SIGNATURES = {
     "pcv_rmsnorm_bwd": [P, I64, P, I64, P, P, P, I64, P, I64, P, I64, I32, P],
     "pcv_layernorm_param_grad": [P, I64, P, I64, P, P, P, P, I64, I32, P],
     "pcv_rmsnorm_param_grad": [P, I64, P, I64, P, P, I64, I32, P],
+    "pcv_batchnorm_workspace_size": [I64, I32],
+    "pcv_batchnorm_stats": [P, I64, I64, I32, I32, F32, F32, P, P, P, P, P, SZ, P],
+    "pcv_batchnorm_apply": [P, I64, I64, I32, P, P, P, P, P, I64, P],
+    "pcv_batchnorm_bwd": [P, I64, P, I64, I64, I32, P, P, P, P, I64, P, I64, P, I64, P, P, P, SZ, P],
     "pcv_rope": [P, I64, I64, I32, I32, I32, P, P, I32, P],
     "pcv_swiglu_fwd": [P, I64, P, I64, I64, I32, I32, P],
     "pcv_swiglu_bwd": [P, I64, P, I64, P, I64, I64, I32, I32, P],
@@ -94,7 +99,7 @@ SIGNATURES = {
 }
 
 # non-status return types (everything else returns an int status)
-RESTYPES = {"pcv_attn_mask_words": I64, "pcv_gemm_grouped_plan_size": I64, "pcv_eigh_log_floats": I64}
+RESTYPES = {"pcv_attn_mask_words": I64, "pcv_batchnorm_workspace_size": SZ, "pcv_gemm_grouped_plan_size": I64, "pcv_eigh_log_floats": I64}
 
 _lib = None
 _err = None

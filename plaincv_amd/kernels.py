@@ -316,6 +316,45 @@ def layernorm_bwd(dy, x, scale, mean, rstd, dres, dx, dx_bf16, dscale, dbias):
              _ld(dx_bf16) if dx_bf16 is not None else 0, ptr(dscale), ptr(dbias), R, D, stream_ptr())
 
 
+def batchnorm_workspace_bytes(R, D):
+    return int(hip.load().pcv_batchnorm_workspace_size(int(R), int(D)))
+
+
+def batchnorm_stats(x, ra_mean, ra_var, mean, rstd, ws, train, momentum=0.99, eps=1e-5):
+    """flax BatchNorm statistics over all rows of x [R, D] (fp32): train -> batch stats + running
+    averages updated in place; eval -> stats from the running averages."""
+    R, D = x.shape
+    _chk(x.dtype == F32 and all(t.dtype == F32 and t.numel() == D and t.is_contiguous()
+                                for t in (ra_mean, ra_var, mean, rstd)), "batchnorm stats")
+    _chk(ws.dtype == F32 and ws.numel() * 4 >= batchnorm_workspace_bytes(R, D), "batchnorm stats workspace")
+    _dev(x, ra_mean, ra_var, mean, rstd, ws)
+    hip.call("pcv_batchnorm_stats", ptr(x), _ld(x), R, D, int(bool(train)), float(momentum), float(eps),
+             ptr(ra_mean), ptr(ra_var), ptr(mean), ptr(rstd), ptr(ws), ws.numel() * 4, stream_ptr())
+
+
+def batchnorm_apply(x, mean, rstd, scale, bias, y):
+    R, D = x.shape
+    _chk(x.dtype == F32 and y.dtype == BF16 and tuple(y.shape) == (R, D), "batchnorm apply")
+    _dev(x, mean, rstd, scale, bias, y)
+    hip.call("pcv_batchnorm_apply", ptr(x), _ld(x), R, D, ptr(mean), ptr(rstd), ptr(scale), ptr(bias), ptr(y),
+             _ld(y), stream_ptr())
+
+
+def batchnorm_bwd(dy, x, mean, rstd, scale, dres, dx, dx_bf16, dscale, dbias, ws):
+    """Train-mode BatchNorm VJP (through the batch statistics); dres may alias dx."""
+    R, D = x.shape
+    _chk(dy.dtype == F32 and dx.dtype == F32 and tuple(dy.shape) == (R, D) and tuple(dx.shape) == (R, D),
+         "batchnorm bwd")
+    _chk(dx_bf16 is None or (dx_bf16.dtype == BF16 and tuple(dx_bf16.shape) == (R, D)), "batchnorm bwd bf16 copy")
+    _chk(dres is None or (dres.dtype == F32 and tuple(dres.shape) == (R, D)), "batchnorm bwd dres")
+    _chk(ws.dtype == F32 and ws.numel() * 4 >= batchnorm_workspace_bytes(R, D), "batchnorm bwd workspace")
+    _dev(dy, x, mean, rstd, scale, dres, dx, dx_bf16, dscale, dbias, ws)
+    hip.call("pcv_batchnorm_bwd", ptr(dy), _ld(dy), ptr(x), _ld(x), R, D, ptr(mean), ptr(rstd), ptr(scale),
+             ptr(dres), _ld(dres) if dres is not None else 0, ptr(dx), _ld(dx), ptr(dx_bf16),
+             _ld(dx_bf16) if dx_bf16 is not None else 0, ptr(dscale), ptr(dbias), ptr(ws), ws.numel() * 4,
+             stream_ptr())
+
+
 def layernorm_param_grad(dy, x, mean, rstd, dscale, dbias):
     R, D = x.shape
     _chk(dy.dtype == F32 and x.dtype == F32 and tuple(dy.shape) == (R, D), "layernorm param grad")

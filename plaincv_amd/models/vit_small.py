@@ -7,7 +7,7 @@ runs the hand-written forward and backward as a straight sequence of C-ABI
 launches (no autograd, no allocation after the first call, hipGraph-capturable).
 
 Numerics: bf16 MFMA operands with fp32 accumulation; the residual stream, the
-LayerNorm statistics, softmax and every gradient reduction stay fp32
+LayerNorm / BatchNorm statistics, softmax and every gradient reduction stay fp32
 (the reference ViT is fp32: the bf16 operands are BASELINE.json config 2's
 "bf16").  Dropout uses the counter hash shared with oracle/rng.py.
 """
@@ -55,8 +55,6 @@ class VisionTransformer:
                  dropout_rate=0.1, use_layernorm=True, use_batchnorm=False):
         if use_batchnorm and use_layernorm:
             raise ValueError("use_batchnorm and use_layernorm cannot both be True.")
-        if use_batchnorm:
-            raise NotImplementedError("use_batchnorm ViT is SURVEY.md §8f-3 'next' (needs batch_stats)")
         self.num_classes = num_classes
         self.patch_size = patch_size
         self.hidden_size = hidden_size
@@ -70,6 +68,26 @@ class VisionTransformer:
             raise ValueError("hidden_size must be divisible by num_heads")
 
     # ------------------------------------------------------------ params
+    def _norm(self):
+        """Flax module name of the pre-norms: LayerNorm, BatchNorm or none (vit_small.py:31-40)."""
+        return "BatchNorm" if self.use_batchnorm else ("LayerNorm" if self.use_layernorm else None)
+
+    def batch_stats_shapes(self):
+        """flax 'batch_stats' collection of the BatchNorm variant: {name: (D,)} for the running
+        mean / var of every BatchNorm (vit_small.py:35,49,121), in forward order; {} otherwise."""
+        if not self.use_batchnorm:
+            return {}
+        D = self.hidden_size
+        names = [f"EncoderBlock_{i}/BatchNorm_{j}" for i in range(self.num_layers) for j in (0, 1)]
+        names.append("BatchNorm_0")
+        return {f"{n}/{k}": (D,) for n in names for k in ("mean", "var")}
+
+    def init_batch_stats(self):
+        """flax BatchNorm initialisers: running mean zeros, running var ones (and init does not update
+        them: flax skips the running-average update while initialising)."""
+        return {k: (torch.zeros if k.endswith("/mean") else torch.ones)(shp)
+                for k, shp in self.batch_stats_shapes().items()}
+
     def layout(self, image_shape):
         """Flat layout for images of shape (B, H, W, C) (B unused)."""
         _, Hh, Ww, C = image_shape
@@ -82,26 +100,27 @@ class VisionTransformer:
         L.add("Conv_0/bias", (D,))
         L.add("cls_token", (1, 1, D))
         L.add("pos_embedding", (1, T, D))
+        norm = self._norm()
         for i in range(self.num_layers):
             pre = f"EncoderBlock_{i}"
-            if self.use_layernorm:
-                L.add(f"{pre}/LayerNorm_0/scale", (D,))
-                L.add(f"{pre}/LayerNorm_0/bias", (D,))
+            if norm:
+                L.add(f"{pre}/{norm}_0/scale", (D,))
+                L.add(f"{pre}/{norm}_0/bias", (D,))
             a = f"{pre}/SelfAttention_0"
             L.add_fused(f"{a}/qkv_kernel", [f"{a}/{n}/kernel" for n in ("query", "key", "value")], (D, H, Dh))
             L.add_concat(f"{a}/qkv_bias", [f"{a}/{n}/bias" for n in ("query", "key", "value")], (H, Dh))
             L.add(f"{a}/out/kernel", (H, Dh, D))
             L.add(f"{a}/out/bias", (D,))
-            if self.use_layernorm:
-                L.add(f"{pre}/LayerNorm_1/scale", (D,))
-                L.add(f"{pre}/LayerNorm_1/bias", (D,))
+            if norm:
+                L.add(f"{pre}/{norm}_1/scale", (D,))
+                L.add(f"{pre}/{norm}_1/bias", (D,))
             L.add(f"{pre}/MlpBlock_0/Dense_0/kernel", (D, M))
             L.add(f"{pre}/MlpBlock_0/Dense_0/bias", (M,))
             L.add(f"{pre}/MlpBlock_0/Dense_1/kernel", (M, D))
             L.add(f"{pre}/MlpBlock_0/Dense_1/bias", (D,))
-        if self.use_layernorm:
-            L.add("LayerNorm_0/scale", (D,))
-            L.add("LayerNorm_0/bias", (D,))
+        if norm:
+            L.add(f"{norm}_0/scale", (D,))
+            L.add(f"{norm}_0/bias", (D,))
         L.add("Dense_0/kernel", (D, self.num_classes))
         L.add("Dense_0/bias", (self.num_classes,))
         return L
@@ -129,16 +148,46 @@ class VisionTransformer:
                 out[name] = _lecun_normal(shp, shp[0], gen)
         return out
 
-    def bind(self, store, image_shape, device, side_stream=False, grouped_wgrad=True):
-        return ViTRunner(self, store, image_shape, device, side_stream=side_stream, grouped_wgrad=grouped_wgrad)
+    def bind(self, store, image_shape, device, side_stream=False, grouped_wgrad=True, batch_stats=None):
+        return ViTRunner(self, store, image_shape, device, side_stream=side_stream, grouped_wgrad=grouped_wgrad,
+                         batch_stats=batch_stats)
+
+
+class BatchStats:
+    """The mutable flax 'batch_stats' collection (flax_engine.py:25-27, 69-92): one flat fp32 device
+    buffer (one all-reduce under data parallelism) with a view per running mean / var."""
+
+    def __init__(self, shapes, device):
+        n = sum(math.prod(s) for s in shapes.values())
+        self.flat = torch.zeros(max(n, 1), dtype=torch.float32, device=device)
+        self.views, off = {}, 0
+        for k, shp in shapes.items():
+            c = math.prod(shp)
+            self.views[k] = self.flat[off:off + c].view(shp)
+            off += c
+
+    def __getitem__(self, k):
+        return self.views[k]
+
+    def load(self, d):
+        for k, v in self.views.items():
+            v.copy_(torch.as_tensor(d[k], dtype=torch.float32).reshape(v.shape))
+
+    def to_dict(self):
+        return {k: v.detach().cpu().clone() for k, v in self.views.items()}
 
 
 class ViTRunner:
     """Fixed-shape forward/backward executor for one batch geometry."""
 
-    def __init__(self, model: VisionTransformer, store: ParamStore, image_shape, device, side_stream=False, grouped_wgrad=True):
+    def __init__(self, model: VisionTransformer, store: ParamStore, image_shape, device, side_stream=False,
+                 grouped_wgrad=True, batch_stats=None):
         self.m = model
         self.s = store
+        self.bn = bool(model.use_batchnorm)
+        if self.bn and batch_stats is None:
+            raise ValueError("the BatchNorm ViT needs its batch_stats (TrainState.batch_stats)")
+        self.bs = batch_stats
         B, Hh, Ww, C = image_shape
         ps = model.patch_size
         self.B, self.C, self.Hh, self.Ww = B, C, Hh, Ww
@@ -210,7 +259,18 @@ class ViTRunner:
         self.dxb_out = [e(R, D, dt=bf) for _ in range(Lc)]
         self.do = e(R, D, dt=bf)
         self.delta = e(B * H * self.T)
-        self.dyf = e(B, D)
+        if self.bn:
+            # BatchNorm statistics are per column over all rows: [mean, rstd] of D each per norm, one
+            # reduction workspace, and a dense top-of-stack dy (the final norm's VJP spreads the cls
+            # rows' gradient to every row through the batch statistics)
+            self.bst0 = [(e(D), e(D)) for _ in range(Lc)]
+            self.bst1 = [(e(D), e(D)) for _ in range(Lc)]
+            self.bstf = (e(D), e(D))
+            self.bn_ws = e((K.batchnorm_workspace_bytes(R, D) + 3) // 4)
+            self.dy_top = torch.zeros(R, D, dtype=f32, device=dev)
+            self.dyf = self.dy_top.view(B, self.T * D)[:, :D]
+        else:
+            self.dyf = e(B, D)
         self.dpatch = e(B * self.hw, D, dt=bf)
         self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
         self.seed = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -275,21 +335,28 @@ class ViTRunner:
                 "W1": W[f"{pre}/MlpBlock_0/Dense_1/kernel"], "b1": P[f"{pre}/MlpBlock_0/Dense_1/bias"],
                 "gW1": G[f"{pre}/MlpBlock_0/Dense_1/kernel"], "gb1": G[f"{pre}/MlpBlock_0/Dense_1/bias"],
             }
-            if m.use_layernorm:
+            norm = m._norm()
+            if norm:
                 for j in (0, 1):
-                    d[f"s{j}"] = P[f"{pre}/LayerNorm_{j}/scale"]
-                    d[f"c{j}"] = P[f"{pre}/LayerNorm_{j}/bias"]
-                    d[f"gs{j}"] = G[f"{pre}/LayerNorm_{j}/scale"]
-                    d[f"gc{j}"] = G[f"{pre}/LayerNorm_{j}/bias"]
+                    d[f"s{j}"] = P[f"{pre}/{norm}_{j}/scale"]
+                    d[f"c{j}"] = P[f"{pre}/{norm}_{j}/bias"]
+                    d[f"gs{j}"] = G[f"{pre}/{norm}_{j}/scale"]
+                    d[f"gc{j}"] = G[f"{pre}/{norm}_{j}/bias"]
+            if self.bn:
+                for j in (0, 1):
+                    d[f"ra{j}"] = (self.bs[f"{pre}/BatchNorm_{j}/mean"], self.bs[f"{pre}/BatchNorm_{j}/var"])
             self.w.append(d)
         self.Wconv = W["Conv_0/kernel"].reshape(self.Kp, D)
         self.gWconv = G["Conv_0/kernel"].reshape(self.Kp, D)
         self.bconv, self.gbconv = P["Conv_0/bias"], G["Conv_0/bias"]
         self.cls, self.gcls = P["cls_token"].reshape(D), G["cls_token"].reshape(D)
         self.pos, self.gpos = P["pos_embedding"].reshape(self.T, D), G["pos_embedding"].reshape(self.T, D)
-        if m.use_layernorm:
-            self.sf, self.cf = P["LayerNorm_0/scale"], P["LayerNorm_0/bias"]
-            self.gsf, self.gcf = G["LayerNorm_0/scale"], G["LayerNorm_0/bias"]
+        norm = m._norm()
+        if norm:
+            self.sf, self.cf = P[f"{norm}_0/scale"], P[f"{norm}_0/bias"]
+            self.gsf, self.gcf = G[f"{norm}_0/scale"], G[f"{norm}_0/bias"]
+        if self.bn:
+            self.raf = (self.bs["BatchNorm_0/mean"], self.bs["BatchNorm_0/var"])
         self.Wh, self.bh = W["Dense_0/kernel"], P["Dense_0/bias"]
         self.gWh, self.gbh = G["Dense_0/kernel"], G["Dense_0/bias"]
 
@@ -322,7 +389,9 @@ class ViTRunner:
         for i in range(L):
             w = self.w[i]
             x = self.xs[i]
-            if not self.fuse_ln:
+            if self.bn:
+                self._bn_fwd(x, w["ra0"], self.bst0[i], w["s0"], w["c0"], self.y0[i], train)
+            elif not self.fuse_ln:
                 if m.use_layernorm:
                     K.layernorm_fwd(x, w["s0"], w["c0"], self.y0[i], *self.st0[i])
                 else:
@@ -337,7 +406,9 @@ class ViTRunner:
                           ln_bias=w["c1"], ln_y=self.y1[i], ln_mean=self.st1[i][0], ln_rstd=self.st1[i][1])
             else:
                 K.gemm(self.o[i], w["Wo"], self.x1s[i], bias=w["bo"], res=x)
-                if m.use_layernorm:
+                if self.bn:
+                    self._bn_fwd(self.x1s[i], w["ra1"], self.bst1[i], w["s1"], w["c1"], self.y1[i], train)
+                elif m.use_layernorm:
                     K.layernorm_fwd(self.x1s[i], w["s1"], w["c1"], self.y1[i], *self.st1[i])
                 else:
                     K.dropout_bwd_cast(self.x1s[i], self.y1[i])
@@ -352,7 +423,10 @@ class ViTRunner:
                 K.gemm(self.a[i], w["W1"], self.xs[i + 1], bias=w["b1"], res=self.x1s[i], drop_rate=rate,
                        seed=seed, site=site_mlp_out(i))
         xcls = self.xs[-1].view(B, T * D)[:, :D]   # cls rows (row stride T*D)
-        if m.use_layernorm:
+        if self.bn:   # statistics over every row, normalise the cls rows only (vit_small.py:121-125)
+            K.batchnorm_stats(self.xs[-1], *self.raf, *self.bstf, self.bn_ws, train)
+            K.batchnorm_apply(xcls, *self.bstf, self.sf, self.cf, self.yf)
+        elif m.use_layernorm:
             K.layernorm_fwd(xcls, self.sf, self.cf, self.yf, *self.stf)
         else:
             K.dropout_bwd_cast(xcls, self.yf)
@@ -361,6 +435,10 @@ class ViTRunner:
                self.dlogits if need_grad else None, grad_scale=1.0 / B)
         K.mean2(self.row_loss, self.row_correct, B, 1.0 / B, self.metrics)
         return self.metrics
+
+    def _bn_fwd(self, x, ra, st, scale, bias, y, train):
+        K.batchnorm_stats(x, *ra, *st, self.bn_ws, train)
+        K.batchnorm_apply(x, *st, scale, bias, y)
 
     # --------------------------------------------------------- backward
     def _fork(self):
@@ -391,7 +469,10 @@ class ViTRunner:
         K.gemm(self.dlogits_b, self.Wh, self.dyf, tb=True)
         dxc = self.dx.view(B, T * D)[:, :D]
         xcls = self.xs[-1].view(B, T * D)[:, :D]
-        if m.use_layernorm:
+        if self.bn:   # dense: every row's dx goes through the batch statistics
+            K.batchnorm_bwd(self.dy_top, self.xs[-1], *self.bstf, self.sf, None, self.dx, None, self.gsf, self.gcf,
+                            self.bn_ws)
+        elif m.use_layernorm:
             K.layernorm_bwd(self.dyf, xcls, self.sf, *self.stf, None, dxc, None, self.gsf, self.gcf)
         else:
             dxc.copy_(self.dyf)
@@ -423,6 +504,10 @@ class ViTRunner:
                 K.gemm_ln(dh, w["W0"], dx_mid, tb=True, ln_mode=2, res=dx_in, ln_scale=w["s1"], ln_y=dxb_mid,
                           ln_mean=self.st1[i][0], ln_rstd=self.st1[i][1], ln_x=self.x1s[i], ln_dscale=gs1,
                           ln_dbias=gc1, colsum=gbo, col_reps=reps)
+            elif self.bn:
+                K.gemm(dh, w["W0"], self.dy_m[i], tb=True)
+                K.batchnorm_bwd(self.dy_m[i], self.x1s[i], *self.bst1[i], w["s1"], dx_in, dx_mid, dxb_mid,
+                                w["gs1"], w["gc1"], self.bn_ws)
             elif m.use_layernorm:
                 K.gemm(dh, w["W0"], self.dy_m[i], tb=True)
                 K.layernorm_bwd(self.dy_m[i], self.x1s[i], w["s1"], *self.st1[i], dx_in, dx_mid, dxb_mid,
@@ -462,6 +547,10 @@ class ViTRunner:
                           site=site_mlp_out(i - 1) if below else 0, ln_mean=self.st0[i][0],
                           ln_rstd=self.st0[i][1], ln_x=self.xs[i], ln_dscale=gs0, ln_dbias=gc0,
                           colsum=gb1, col_reps=reps)
+            elif self.bn:
+                K.gemm(dqkv, w["Wqkv"], self.dy_a[i], tb=True)
+                K.batchnorm_bwd(self.dy_a[i], self.xs[i], *self.bst0[i], w["s0"], dx_mid, dx_out, dxb_out,
+                                w["gs0"], w["gc0"], self.bn_ws)
             elif m.use_layernorm:
                 K.gemm(dqkv, w["Wqkv"], self.dy_a[i], tb=True)
                 K.layernorm_bwd(self.dy_a[i], self.xs[i], w["s0"], *self.st0[i], dx_mid, dx_out, dxb_out,

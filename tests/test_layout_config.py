@@ -103,3 +103,19 @@ def test_routing_matches_oracle():
     for n, s in cases:
         t = torch.empty(s)
         assert should_use_matrix_preconditioner(n, t) == oracle_route(n, t), n
+
+
+def test_vit_batchnorm_names_and_init():
+    from plaincv_amd.models.vit_small import VisionTransformer
+    m = VisionTransformer(num_classes=10, patch_size=4, hidden_size=64, mlp_dim=128, num_layers=2, num_heads=2,
+                          use_layernorm=False, use_batchnorm=True)
+    with pytest.raises(ValueError, match="cannot both be True"):
+        VisionTransformer(use_layernorm=True, use_batchnorm=True)
+    lay = m.layout((2, 16, 16, 3))
+    assert "EncoderBlock_1/BatchNorm_1/scale" in lay.leaves and "BatchNorm_0/bias" in lay.leaves
+    assert not any("LayerNorm" in k for k in lay.leaves)
+    bs = m.init_batch_stats()
+    assert sorted(bs) == sorted(f"{p}/{k}" for p in ("EncoderBlock_0/BatchNorm_0", "EncoderBlock_0/BatchNorm_1",
+                                                     "EncoderBlock_1/BatchNorm_0", "EncoderBlock_1/BatchNorm_1",
+                                                     "BatchNorm_0") for k in ("mean", "var"))
+    assert all((v == 0).all() if k.endswith("mean") else (v == 1).all() for k, v in bs.items())

@@ -13,7 +13,7 @@ from oracle import rng
 from oracle.engine import (apply_updates, clip_grads, cross_entropy_loss, global_norm, lm_loss_and_acc,
                            value_and_grad)
 from oracle.lm import ModelConfig, apply_rotary, attention, lm_param_shapes, precompute_freqs_cis, transformer_apply
-from oracle.nn import gelu_tanh, layernorm, rmsnorm
+from oracle.nn import batchnorm, gelu_tanh, layernorm, rmsnorm
 from oracle.vit import ViTConfig, vit_apply, vit_param_shapes
 
 
@@ -50,6 +50,31 @@ def test_layernorm_fast_variance_and_gelu():
     assert torch.allclose(y, ref, atol=1e-10)
     z = torch.linspace(-5, 5, 101, dtype=torch.float64)
     assert torch.allclose(gelu_tanh(z), torch.nn.functional.gelu(z, approximate="tanh"))
+
+
+def test_batchnorm_flax_semantics():
+    """flax BatchNorm: column stats over all leading axes (biased variance), eps 1e-5, running
+    averages ra <- 0.99 ra + 0.01 stat; eval uses the running averages; the train-mode VJP goes
+    through the batch statistics (sum over rows of dx is 0, dx orthogonal to xhat per column)."""
+    x = torch.randn(3, 7, 5, dtype=torch.float64) * 2 + 1
+    sc, bi = torch.linspace(0.5, 2, 5, dtype=torch.float64), torch.linspace(-1, 1, 5, dtype=torch.float64)
+    ra_m, ra_v = torch.zeros(5, dtype=torch.float64), torch.ones(5, dtype=torch.float64)
+    y, m, v = batchnorm(x, sc, bi, ra_m, ra_v, True)
+    ref = torch.nn.functional.batch_norm(x.reshape(-1, 5), None, None, sc, bi, training=True, eps=1e-5)
+    assert torch.allclose(y.reshape(-1, 5), ref, atol=1e-10)
+    flat = x.reshape(-1, 5)
+    assert torch.allclose(m, 0.01 * flat.mean(0)) and torch.allclose(v, 0.99 + 0.01 * flat.var(0, unbiased=False))
+    ye, me, ve = batchnorm(x, sc, bi, m, v, False)
+    assert me is m and ve is v
+    assert torch.allclose(ye, (x - m) / torch.sqrt(v + 1e-5) * sc + bi)
+    xr = x.clone().requires_grad_(True)
+    out = batchnorm(xr, sc, bi, ra_m, ra_v, True)[0]
+    dy = torch.randn_like(out)
+    (dx,) = torch.autograd.grad(out, xr, dy)
+    xh = (flat - flat.mean(0)) / torch.sqrt(flat.var(0, unbiased=False) + 1e-5)
+    assert torch.allclose(dx.reshape(-1, 5).sum(0), torch.zeros(5, dtype=torch.float64), atol=1e-9)
+    assert torch.allclose((dx.reshape(-1, 5) * xh).sum(0), torch.zeros(5, dtype=torch.float64), atol=1e-4)
+    assert torch.autograd.gradcheck(lambda t: batchnorm(t, sc, bi, ra_m, ra_v, True)[0], (xr,))
 
 
 def test_adamw_first_step_closed_form():
