@@ -232,6 +232,19 @@ int pcv_adamw_step(float* p, const float* g, float* m, float* v, void* p_bf16, f
                    const void* chunks, int nchunks, float lr, float b1, float b2, float eps,
                    float eps_root, float wd, int nesterov, int apply, const int* step,
                    const float* gscale, void* stream);
+/* Signum (optim/signum.py:14-66): m = mom*m + (1-mom)*g*gscale; d = nesterov ? (1-mom)*g + mom*m : m;
+ * u = -lr*(sign(d) + wd*p) (sign(0) = 0, wd term only when wd > 0).  apply: p += u and the bf16
+ * shadow; else u -> upd (the functional update() facade / a schedule-free base). */
+int pcv_signum_step(float* p, const float* g, float* m, void* p_bf16, float* upd, const void* chunks, int nchunks,
+                    float lr, float momentum, float wd, int nesterov, int apply, const float* gscale, void* stream);
+/* Schedule-free wrapper (optim/factory.py:82-99 -> optax.contrib.schedule_free): given the base
+ * optimizer's update u (base_upd) at y = params, z <- z + u, x = (1-ck)(y-(1-b1)z_old)/b1 + ck z,
+ * y' = b1 x + (1-b1) z; apply: y += (y' - y) (+ bf16 shadow), else y' - y -> upd_out.
+ * sf_scalars = device [weight_sum, max_lr, ck] (zeros at init), step_count device int (1 at init):
+ * ck = max_lr^p / (weight_sum + max_lr^p) is formed on the device, so the step replays from a graph. */
+int pcv_schedule_free_step(float* y, float* z, const float* base_upd, void* y_bf16, float* upd_out,
+                           const void* chunks, int nchunks, float b1, float lr, float weight_lr_power,
+                           float* sf_scalars, int* step_count, int apply, void* stream);
 /* gscale = min(1, clip/(||g/accum||+1e-6))/accum  (train_lm.py:173-178, 664). */
 int pcv_grad_scale(const float* g, const void* chunks, int nchunks, float* partial_ws, float inv_accum,
                    float clip, float* gscale, float* gnorm, void* stream);

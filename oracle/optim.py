@@ -287,27 +287,105 @@ def shampoo(learning_rate, eps=1e-4, exponent=0.25, weight_decay=0.0, adam_b1=0.
     return SimpleNamespace(init=init, update=update)
 
 
+# ----------------------------------------------------------------------------
+# Signum (optim/signum.py:14-66)
+# ----------------------------------------------------------------------------
+def signum(learning_rate, momentum=0.9, nesterov=False, weight_decay=0.0):
+    """m = mom m + (1-mom) g; d = (1-mom) g + mom m (nesterov) or m; u = -lr (sign(d) + wd p)."""
+    if learning_rate < 0.0:
+        raise ValueError(f"learning_rate must be >= 0, got {learning_rate}.")
+    if momentum < 0.0 or momentum >= 1.0:
+        raise ValueError(f"momentum must be in [0, 1), got {momentum}.")
+    if weight_decay < 0.0:
+        raise ValueError(f"weight_decay must be >= 0, got {weight_decay}.")
+
+    def init(params):
+        return SimpleNamespace(momentum_buffer={k: torch.zeros_like(p) for k, p in params.items()})
+
+    def update(grads, state, params=None):
+        buf, upd = {}, {}
+        for k, g in grads.items():
+            m = momentum * state.momentum_buffer[k] + (1.0 - momentum) * g
+            buf[k] = m
+            d = (1.0 - momentum) * g + momentum * m if nesterov else m
+            u = torch.sign(d)
+            if weight_decay > 0.0:
+                if params is None:
+                    raise ValueError("Signum with weight_decay requires current params.")
+                u = u + weight_decay * params[k]
+            upd[k] = -learning_rate * u
+        return upd, SimpleNamespace(momentum_buffer=buf)
+
+    return SimpleNamespace(init=init, update=update)
+
+
+# ----------------------------------------------------------------------------
+# schedule-free wrapper (optim/factory.py:82-99 -> optax.contrib.schedule_free, optax 0.2.6)
+# ----------------------------------------------------------------------------
+def schedule_free(base, learning_rate, b1=0.9, weight_lr_power=2.0):
+    """optax.contrib.schedule_free (Defazio et al. 2024), restated: params are y (where gradients
+    are taken); z (init = params) takes the base optimizer's steps; x is the weighted average with
+    c_k = w_k / sum w, w_k = max_lr^weight_lr_power; y = b1 x + (1-b1) z.  x is recomputed from
+    y and the old z each step: x_prev = (y - (1-b1) z_old) / b1.  Scalars in fp32 as optax keeps them."""
+    if b1 == 0:
+        raise ValueError("The current implementation of schedule_free requires b1 > 0.")
+    f32 = torch.float32
+
+    def init(params):
+        return SimpleNamespace(b1=torch.tensor(b1, dtype=f32), weight_sum=torch.zeros((), dtype=f32),
+                               step_count=1, max_lr=torch.zeros((), dtype=f32), base_state=base.init(params),
+                               z={k: p.clone() for k, p in params.items()})
+
+    def update(grads, state, params):
+        lr = torch.tensor(learning_rate, dtype=f32)
+        max_lr = torch.maximum(state.max_lr, lr)
+        weight = max_lr ** weight_lr_power
+        total = state.weight_sum + weight
+        ck = torch.nan_to_num(weight / total, nan=0.0)
+        if torch.isnan(weight) or torch.isnan(total):
+            ck = torch.tensor(float("nan"), dtype=f32)
+        base_upd, base_state = base.update(grads, state.base_state, params)
+        z_new = {k: (state.z[k] + base_upd[k]).to(state.z[k].dtype) for k in params}
+        upd = {}
+        for k, y in params.items():
+            prev_x = (y - (1.0 - state.b1) * state.z[k]) / state.b1
+            x = (1.0 - ck) * prev_x + ck * z_new[k]
+            upd[k] = (state.b1 * x + (1.0 - state.b1) * z_new[k]) - y
+        return upd, SimpleNamespace(b1=state.b1, weight_sum=total, step_count=state.step_count + 1, max_lr=max_lr,
+                                    base_state=base_state, z=z_new)
+
+    return SimpleNamespace(init=init, update=update)
+
+
 def get_optimizer(cfg):
-    """optim/factory.py:180-802 restricted to the hot-path branches."""
+    """optim/factory.py:180-802 restricted to the hot-path branches (+ the schedule-free wrapper)."""
     name = str(getattr(cfg, "optim", "adamw")).lower()
     lr = float(cfg.lr)
     g = lambda k, d: getattr(cfg, k, d)  # noqa: E731
     if name in {"adam", "adamw"}:
-        return adamw(lr, b1=g("beta1", 0.9), b2=g("beta2", 0.999), eps=g("eps", 1e-8),
-                     weight_decay=g("weight_decay", 0.0))
-    if name == "muon":
+        tx = adamw(lr, b1=g("beta1", 0.9), b2=g("beta2", 0.999), eps=g("eps", 1e-8),
+                   weight_decay=g("weight_decay", 0.0))
+    elif name == "muon":
         wd = g("weight_decay", 0.0)
-        return muon(lr, ns_coeffs=tuple(g("muon_ns_coeffs", (3.4445, -4.7750, 2.0315))),
-                    ns_steps=g("muon_ns_steps", 5), beta=g("muon_beta", 0.95), eps=g("eps", 1e-8),
-                    weight_decay=wd, nesterov=g("muon_nesterov", True), adam_b1=g("beta1", 0.9),
-                    adam_b2=g("beta2", 0.999), adam_eps_root=g("adam_eps_root", 0.0),
-                    adam_weight_decay=wd, adam_nesterov=g("muon_nesterov", True))
-    if name == "soap":
-        return soap(lr, b1=g("beta1", 0.95), b2=g("beta2", 0.95), eps=g("eps", 1e-8),
-                    weight_decay=g("weight_decay", 0.01), precondition_frequency=g("precondition_frequency", 10),
-                    shampoo_beta2=g("shampoo_beta2", None), correct_bias=g("correct_bias", True))
-    if name == "shampoo":
-        return shampoo(lr, eps=g("eps", 1e-4), exponent=g("shampoo_exponent", 0.25),
-                       weight_decay=g("weight_decay", 0.0), adam_b1=g("beta1", 0.9), adam_b2=g("beta2", 0.999),
-                       adam_eps=g("adam_eps", 1e-8))
-    raise ValueError(f"Unknown optimizer name: {cfg.optim}")
+        tx = muon(lr, ns_coeffs=tuple(g("muon_ns_coeffs", (3.4445, -4.7750, 2.0315))),
+                  ns_steps=g("muon_ns_steps", 5), beta=g("muon_beta", 0.95), eps=g("eps", 1e-8),
+                  weight_decay=wd, nesterov=g("muon_nesterov", True), adam_b1=g("beta1", 0.9),
+                  adam_b2=g("beta2", 0.999), adam_eps_root=g("adam_eps_root", 0.0),
+                  adam_weight_decay=wd, adam_nesterov=g("muon_nesterov", True))
+    elif name == "soap":
+        tx = soap(lr, b1=g("beta1", 0.95), b2=g("beta2", 0.95), eps=g("eps", 1e-8),
+                  weight_decay=g("weight_decay", 0.01), precondition_frequency=g("precondition_frequency", 10),
+                  shampoo_beta2=g("shampoo_beta2", None), correct_bias=g("correct_bias", True))
+    elif name == "shampoo":
+        tx = shampoo(lr, eps=g("eps", 1e-4), exponent=g("shampoo_exponent", 0.25),
+                     weight_decay=g("weight_decay", 0.0), adam_b1=g("beta1", 0.9), adam_b2=g("beta2", 0.999),
+                     adam_eps=g("adam_eps", 1e-8))
+    elif name in {"signum", "sign_sgd", "sign-sgd", "signsgd"}:
+        tx = signum(lr, momentum=g("signum_momentum", g("beta1", 0.9)), nesterov=g("signum_nesterov", False),
+                    weight_decay=g("weight_decay", 0.0))
+    else:
+        raise ValueError(f"Unknown optimizer name: {cfg.optim}")
+    if g("schedule_free", False):       # factory.py:82-99, 801
+        tx = schedule_free(tx, g("schedule_free_lr", cfg.lr), b1=g("schedule_free_b1", 0.9),
+                           weight_lr_power=g("schedule_free_weight_lr_power", 2.0))
+    return tx

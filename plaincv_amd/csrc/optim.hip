@@ -6,6 +6,10 @@
 //           bias correction (muon_prep), Frobenius normalisation, and the final
 //           shape-scaled, weight-decayed update (muon_apply).  The Newton-Schulz
 //           iterations themselves are batched MFMA GEMMs (gemm.hip).
+//   Signum  optim/signum.py:14-66: sign of the (optionally Nesterov) momentum + decoupled wd
+//   schedule-free  optim/factory.py:82-99 -> optax.contrib.schedule_free wrapped around any of
+//           the above: the base step is written to an update buffer, then one elementwise pass
+//           advances z, re-forms x from y and the old z, and writes y (params + bf16 shadow).
 //   grad clipping (train_lm.py:173-178) + accumulation mean: deterministic
 //   per-chunk sum-of-squares partials, then one tiny kernel derives the device
 //   scalar gscale = clip_factor / accum that every optimizer kernel multiplies in.
@@ -47,6 +51,74 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, fl
       const float pn = pi + u;
       p[i] = pn;
       if (pb) pb[i] = f2bf(pn);
+    }
+  }
+}
+
+struct SignumHyper {
+  float lr, momentum, wd;
+  int nesterov, apply;
+};
+
+// m = mom m + (1-mom) g;  d = (1-mom) g + mom m (nesterov) | m;  u = -lr (sign(d) + wd p)
+__global__ __launch_bounds__(256) void signum_kernel(float* p, const float* g, float* m, bf16* pb, float* upd,
+                                                     const Chunk* chunks, SignumHyper h, const float* gscale) {
+  const Chunk ck = chunks[blockIdx.x];
+  const float gs = gscale ? *gscale : 1.f;
+#pragma unroll 4
+  for (int64_t i = ck.start + threadIdx.x; i < ck.start + ck.len; i += 256) {
+    const float gi = g[i] * gs;
+    const float mi = h.momentum * m[i] + (1.f - h.momentum) * gi;
+    m[i] = mi;
+    const float d = h.nesterov ? (1.f - h.momentum) * gi + h.momentum * mi : mi;
+    float u = (float)((d > 0.f) - (d < 0.f));   // jnp.sign (sign(0) = 0)
+    const float pi = p[i];
+    if (h.wd > 0.f) u += h.wd * pi;
+    u = -h.lr * u;
+    if (upd) upd[i] = u;
+    if (h.apply) {
+      const float pn = pi + u;
+      p[i] = pn;
+      if (pb) pb[i] = f2bf(pn);
+    }
+  }
+}
+
+// schedule-free scalars sf = [weight_sum, max_lr, ck]: max_lr = max(max_lr, lr), w = max_lr^power,
+// total = weight_sum + w, ck = w / total (nan -> 0, nan if w or total is nan), step_count += 1
+__global__ void sf_prep_kernel(float* sf, int* step_count, float lr, float power) {
+  const float max_lr = fmaxf(sf[1], lr);
+  const float w = powf(max_lr, power);
+  const float total = sf[0] + w;
+  float ck = w / total;
+  if (isnan(ck)) ck = 0.f;
+  if (isnan(w) || isnan(total)) ck = __builtin_nanf("");
+  sf[0] = total;
+  sf[1] = max_lr;
+  sf[2] = ck;
+  *step_count += 1;
+}
+
+// z' = z + u;  x = (1-ck) (y - (1-b1) z)/b1 + ck z';  y' = b1 x + (1-b1) z';  update = y' - y
+// apply: y <- y + update (= optax.apply_updates) and the bf16 shadow; else update -> out
+__global__ __launch_bounds__(256) void sf_apply_kernel(float* y, float* z, const float* u, bf16* pb, float* out,
+                                                       const Chunk* chunks, float b1, const float* sf, int apply) {
+  const Chunk c = chunks[blockIdx.x];
+  const float ck = sf[2];
+#pragma unroll 4
+  for (int64_t i = c.start + threadIdx.x; i < c.start + c.len; i += 256) {
+    const float yi = y[i], zi = z[i];
+    const float zn = zi + u[i];
+    const float xp = (yi - (1.f - b1) * zi) / b1;
+    const float x = (1.f - ck) * xp + ck * zn;
+    const float d = (b1 * x + (1.f - b1) * zn) - yi;
+    z[i] = zn;
+    if (apply) {
+      const float yn = yi + d;
+      y[i] = yn;
+      if (pb) pb[i] = f2bf(yn);
+    } else {
+      out[i] = d;
     }
   }
 }
@@ -156,6 +228,29 @@ extern "C" int pcv_adamw_step(float* p, const float* g, float* m, float* v, void
   AdamHyper h{lr, b1, b2, eps, eps_root, wd, nesterov, apply};
   hipLaunchKernelGGL(adamw_kernel, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (bf16*)p_bf16, upd,
                      (const Chunk*)chunks, h, step, gscale);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_signum_step(float* p, const float* g, float* m, void* p_bf16, float* upd, const void* chunks,
+                               int nchunks, float lr, float momentum, float wd, int nesterov, int apply,
+                               const float* gscale, void* stream) {
+  if (nchunks < 0 || !p || !g || !m || (!apply && !upd)) return PCV_EINVAL;
+  if (nchunks == 0) return 0;
+  SignumHyper h{lr, momentum, wd, nesterov, apply};
+  hipLaunchKernelGGL(signum_kernel, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, p, g, m, (bf16*)p_bf16, upd,
+                     (const Chunk*)chunks, h, gscale);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_schedule_free_step(float* y, float* z, const float* base_upd, void* y_bf16, float* upd_out,
+                                      const void* chunks, int nchunks, float b1, float lr, float weight_lr_power,
+                                      float* sf_scalars, int* step_count, int apply, void* stream) {
+  if (nchunks <= 0 || !y || !z || !base_upd || !sf_scalars || !step_count || (!apply && !upd_out) || b1 == 0.f)
+    return PCV_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(sf_prep_kernel, dim3(1), dim3(1), 0, s, sf_scalars, step_count, lr, weight_lr_power);
+  hipLaunchKernelGGL(sf_apply_kernel, dim3(nchunks), dim3(256), 0, s, y, z, base_upd, (bf16*)y_bf16, upd_out,
+                     (const Chunk*)chunks, b1, (const float*)sf_scalars, apply);
   return pcv_launch_status();
 }
 

@@ -64,6 +64,8 @@ SIGNATURES = {
     "pcv_xent_fwd_bwd": [P, I64, I32, P, I64, I32, P, P, P, I64, F32, P],
     "pcv_mean2": [P, P, I64, F32, P, P],
     "pcv_adamw_step": [P, P, P, P, P, P, P, I32, F32, F32, F32, F32, F32, F32, I32, I32, P, P, P],
+    "pcv_signum_step": [P, P, P, P, P, P, I32, F32, F32, F32, I32, I32, P, P],
+    "pcv_schedule_free_step": [P, P, P, P, P, P, I32, F32, F32, F32, P, P, I32, P],
     "pcv_grad_scale": [P, P, I32, P, F32, F32, P, P, P],
     "pcv_step_bump": [P, P],
     "pcv_muon_prep": [P, I32, I32, I64, F32, I32, F32, P, P, P],

@@ -61,6 +61,13 @@ class AdamW(GradientTransformation):
         K.step_bump(state.count)
         return _views(store, state.upd), state
 
+    def update_into_(self, store, state, gscale=None):
+        state.branch.run(store, state.tensors["mu"], state.tensors["nu"], state.count, self.lr, gscale=gscale,
+                         upd=state.upd, apply=False)
+        from .. import kernels as K
+        K.step_bump(state.count)
+        return state.upd
+
     def step_(self, store, state, gscale=None):
         state.branch.run(store, state.tensors["mu"], state.tensors["nu"], state.count, self.lr, gscale=gscale)
         from .. import kernels as K

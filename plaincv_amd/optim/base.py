@@ -26,6 +26,12 @@ class GradientTransformation:
     def step_(self, store, state, gscale=None):
         raise NotImplementedError
 
+    def update_into_(self, store, state, gscale=None):
+        """Advance ``state`` by one step on the store's gradients (x gscale) and write the update
+        (already scaled by -lr) into the flat buffer ``state.upd`` without applying it; returns
+        that buffer.  The schedule-free wrapper drives its base optimizer through this."""
+        raise NotImplementedError
+
 
 class OptState:
     """Device-resident optimizer state; ``count`` is an int32 device scalar so

@@ -9,14 +9,20 @@ keeps the reference's signature, config keys and defaults:
 * soap           factory.py:632-652  (beta1/beta2 .95, eps 1e-8, wd .01, precondition_frequency 10)
 * shampoo        factory.py:657-673  (eps 1e-4, shampoo_exponent .25, adam_eps 1e-8; build-only key
                  shampoo_root: "newton" (default) | "eigh", the inverse-root method)
+* signum / sign_sgd / sign-sgd / signsgd   factory.py:210-219 (signum_momentum -> beta1 -> .9,
+                 signum_nesterov False, weight_decay 0)
+* schedule_free: True wraps any of them (factory.py:82-99, 801: schedule_free_lr -> lr,
+                 schedule_free_b1 .9, schedule_free_weight_lr_power 2.0)
 
 Any other name raises ``ValueError(f"Unknown optimizer name: {cfg.optim}")``
 (factory.py:797-798); the research optimizers of the reference (PN-S, Sophia,
-HF, Signum) are out of scope.
+HF) are out of scope.
 """
 from .adamw import AdamW
 from .muon import Muon
+from .schedule_free import ScheduleFree
 from .shampoo import Shampoo
+from .signum import Signum
 from .soap import Soap
 
 
@@ -25,6 +31,15 @@ def _g(cfg, k, d):
 
 
 def get_optimizer(cfg, model_def=None, curvature_batch=None, batch_stats=None):
+    tx = _base_optimizer(cfg)
+    if _g(cfg, "schedule_free", False):
+        tx = ScheduleFree(tx, float(_g(cfg, "schedule_free_lr", _g(cfg, "lr", 1e-3))),
+                          b1=float(_g(cfg, "schedule_free_b1", 0.9)),
+                          weight_lr_power=float(_g(cfg, "schedule_free_weight_lr_power", 2.0)))
+    return tx
+
+
+def _base_optimizer(cfg):
     name = str(_g(cfg, "optim", "adamw")).lower()
     lr = float(_g(cfg, "lr", 1e-3))
     if name in {"adam", "adamw"}:
@@ -48,4 +63,7 @@ def get_optimizer(cfg, model_def=None, curvature_batch=None, batch_stats=None):
                        weight_decay=_g(cfg, "weight_decay", 0.0), adam_b1=_g(cfg, "beta1", 0.9),
                        adam_b2=_g(cfg, "beta2", 0.999), adam_eps=_g(cfg, "adam_eps", 1e-8),
                        root_method=str(_g(cfg, "shampoo_root", "newton")))
+    if name in {"signum", "sign_sgd", "sign-sgd", "signsgd"}:
+        return Signum(lr, momentum=float(_g(cfg, "signum_momentum", _g(cfg, "beta1", 0.9))),
+                      nesterov=bool(_g(cfg, "signum_nesterov", False)), weight_decay=float(_g(cfg, "weight_decay", 0.0)))
     raise ValueError(f"Unknown optimizer name: {_g(cfg, 'optim', name)}")

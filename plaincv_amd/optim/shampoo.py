@@ -152,5 +152,9 @@ class Shampoo(GradientTransformation):
         self._run(params, state, None, apply=False)
         return _views(params, state.upd), state
 
+    def update_into_(self, store, state, gscale=None):
+        self._run(store, state, gscale, apply=False)
+        return state.upd
+
     def step_(self, store, state, gscale=None):
         self._run(store, state, gscale, apply=True)

@@ -119,3 +119,23 @@ def test_vit_batchnorm_names_and_init():
                                                      "EncoderBlock_1/BatchNorm_0", "EncoderBlock_1/BatchNorm_1",
                                                      "BatchNorm_0") for k in ("mean", "var"))
     assert all((v == 0).all() if k.endswith("mean") else (v == 1).all() for k, v in bs.items())
+
+
+def test_factory_signum_and_schedule_free_keys():
+    """factory.py:210-219 (signum aliases, signum_momentum -> beta1 -> 0.9) and 82-99, 801
+    (schedule_free wraps any optimizer; schedule_free_lr defaults to lr)."""
+    from plaincv_amd.optim import ScheduleFree, Signum, get_optimizer
+    for name in ("signum", "sign_sgd", "sign-sgd", "signsgd", "SIGNUM"):
+        tx = get_optimizer(Config(optim=name, lr=3e-4, beta1=0.8, weight_decay=0.1))
+        assert isinstance(tx, Signum) and tx.momentum == 0.8 and tx.wd == 0.1 and not tx.nesterov
+    tx = get_optimizer(Config(optim="signum", lr=3e-4, signum_momentum=0.95, signum_nesterov=True))
+    assert tx.momentum == 0.95 and tx.nesterov
+    tx = get_optimizer(Config(optim="muon", lr=1e-3, schedule_free=True))
+    assert isinstance(tx, ScheduleFree) and tx.lr == 1e-3 and tx.b1 == 0.9 and tx.power == 2.0
+    tx = get_optimizer(Config(optim="soap", lr=1e-3, schedule_free=True, schedule_free_lr=0.01, schedule_free_b1=0.8))
+    assert tx.lr == 0.01 and tx.b1 == 0.8 and tx.graphable is False
+    assert not isinstance(get_optimizer(Config(optim="adamw", lr=1e-3, schedule_free=False)), ScheduleFree)
+    with pytest.raises(ValueError, match="Unknown optimizer name"):
+        get_optimizer(Config(optim="lion", lr=1e-3))
+    with pytest.raises(ValueError):
+        get_optimizer(Config(optim="signum", lr=1e-3, signum_momentum=1.0))

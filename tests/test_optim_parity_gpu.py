@@ -208,3 +208,102 @@ def test_parity_check_catches_broken_steps(dev, name):
         assert wr > MUON_TOL, (name, wr)
     if which in ("adam", "both"):
         assert wa > ADAM_TOL * 100, (name, wa)
+
+
+def _sign_tolerant_worst(steps, lr, wd_max=0.1):
+    """Signum updates are -lr (sign(d) + wd p): equal to fp32 rounding except where the momentum
+    direction d is within rounding of 0 and the two sides' last-ulp differences pick different
+    signs.  Returns (fraction of such sign ties, worst rel error over the other elements)."""
+    ties, n, worst_rel = 0, 0, 0.0
+    for hip, ora, p0, p1 in steps:
+        for k in ora:
+            h = hip[k].double() if p0 is None else p1[k].double() - p0[k].double()
+            o = ora[k].double()
+            tie = (h - o).abs() > 0.5 * lr        # a sign flip moves the element by >= lr
+            ties += int(tie.sum())
+            n += o.numel()
+            keep = ~tie
+            if keep.any():
+                err = (h[keep] - o[keep]).norm().item()
+                if p0 is not None:   # fp32 rounding of p + u, as step_rel
+                    p1f = p1[k][keep].float()
+                    ulp = (torch.nextafter(p1f.abs(), torch.full_like(p1f, float("inf"))) - p1f.abs()).double()
+                    err = max(0.0, err - 0.5 * ulp.norm().item())
+                worst_rel = max(worst_rel, err / max(o[keep].norm().item(), 1e-30))
+    return ties / max(n, 1), worst_rel
+
+
+@pytest.mark.parametrize("which", ["vit_c2", "lm768"])
+@pytest.mark.parametrize("mode,gscale", [("update", 1.0), ("step_", 0.37)])
+@pytest.mark.parametrize("nesterov", [False, True])
+def test_signum_update_parity(dev, which, mode, gscale, nesterov):
+    """optim/signum.py:14-66 on identical gradients: sign ties (|d| at rounding level) at most 1e-5
+    of the elements, every other element within 1e-5 relative."""
+    from oracle import optim as oopt
+    from plaincv_amd.optim.signum import Signum
+    lr, mom, wd = 1e-2, 0.9, 0.1
+    steps = run_pair(dev, LAYOUTS[which](), Signum(lr, mom, nesterov, wd), oopt.signum(lr, mom, nesterov, wd),
+                     4, mode, gscale)
+    tie_frac, wr = _sign_tolerant_worst(steps, lr)
+    assert tie_frac <= 1e-5, tie_frac
+    assert wr <= ADAM_TOL, wr
+
+
+@pytest.mark.parametrize("base", ["adamw", "muon", "signum"])
+@pytest.mark.parametrize("mode,gscale", [("update", 1.0), ("step_", 0.37)])
+def test_schedule_free_update_parity(dev, base, mode, gscale):
+    """optax.contrib.schedule_free (factory.py:82-99) around each base on the ViT-small layout,
+    5 steps (c_k = 1, 1/2, ... so x, y and z all separate); schedule_free_lr != lr as in the
+    reference configs (0.01 vs 1e-3)."""
+    from oracle import optim as oopt
+    from plaincv_amd.optim.factory import get_optimizer
+    from utils import Config
+    cfg = Config(optim=base, lr=1e-2, weight_decay=0.1, beta1=0.9, beta2=0.95, schedule_free=True,
+                 schedule_free_lr=0.03, schedule_free_b1=0.9, schedule_free_weight_lr_power=2.0)
+    steps = run_pair(dev, _vit_layout(), get_optimizer(cfg), oopt.get_optimizer(cfg), 5, mode, gscale)
+    if base == "signum":
+        tie_frac, wr = _sign_tolerant_worst(steps, 1e-2)
+        assert tie_frac <= 1e-5 and wr <= ADAM_TOL, (tie_frac, wr)
+        return
+    wr, wa = worst(steps, _routed if base == "muon" else (lambda k, p: False))
+    assert wa <= ADAM_TOL, wa
+    if base == "muon":
+        assert wr <= MUON_TOL, wr
+
+
+def _sf_mutations():
+    from oracle import optim as oopt
+    from plaincv_amd.optim.adamw import AdamW
+    from plaincv_amd.optim.schedule_free import ScheduleFree
+    from plaincv_amd.optim.signum import Signum
+    hp = dict(b1=0.9, b2=0.95, eps=1e-8, weight_decay=0.1)
+
+    def weight_sum_preset(st):       # c_k no longer 1/k
+        st.sf[0] = 5e-4
+
+    def z_shift(st):                 # z not initialised to the params
+        st.tensors["z"].mul_(1.01)
+
+    sf = lambda b: oopt.schedule_free(b, 0.03, 0.9, 2.0)  # noqa: E731
+    return {
+        "sf_weight_sum": (ScheduleFree(AdamW(1e-2, **hp), 0.03, 0.9), sf(oopt.adamw(1e-2, **hp)), weight_sum_preset),
+        "sf_z_init": (ScheduleFree(AdamW(1e-2, **hp), 0.03, 0.9), sf(oopt.adamw(1e-2, **hp)), z_shift),
+        "sf_b1": (ScheduleFree(AdamW(1e-2, **hp), 0.03, 0.8), sf(oopt.adamw(1e-2, **hp)), None),
+        # (weight_lr_power alone cannot be caught with a constant lr: c_k = 1/k for every power)
+        "sf_zero_lr": (ScheduleFree(AdamW(1e-2, **hp), 0.0, 0.9), sf(oopt.adamw(1e-2, **hp)), None),
+        "signum_nesterov_flipped": (Signum(1e-2, 0.9, True, 0.1), oopt.signum(1e-2, 0.9, False, 0.1), None),
+        "signum_no_wd": (Signum(1e-2, 0.9, False, 0.0), oopt.signum(1e-2, 0.9, False, 0.1), None),
+    }
+
+
+@pytest.mark.parametrize("name", ["sf_weight_sum", "sf_z_init", "sf_b1", "sf_zero_lr", "signum_nesterov_flipped",
+                                  "signum_no_wd"])
+def test_sf_signum_checks_catch_broken_steps(dev, name):
+    gpu, ora, mut = _sf_mutations()[name]
+    steps = run_pair(dev, _vit_layout(), gpu, ora, 3, "step_", mutate_state=mut)
+    if name.startswith("signum"):
+        tie_frac, wr = _sign_tolerant_worst(steps, 1e-2)
+        assert tie_frac > 1e-3 or wr > ADAM_TOL * 100, (name, tie_frac, wr)
+    else:
+        _, wa = worst(steps, lambda k, p: False)
+        assert wa > ADAM_TOL * 100, (name, wa)

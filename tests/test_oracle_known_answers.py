@@ -3,6 +3,7 @@
 The reference ships no tests or golden vectors for this path and JAX/Flax/Optax
 are absent, so these closed forms are what anchors the restatement."""
 import math
+from types import SimpleNamespace
 
 import numpy as np
 import pytest
@@ -243,3 +244,34 @@ def test_dropout_hash_rate_and_determinism():
     assert not np.array_equal(m1, rng.keep_mask(4, 17, (300, 300), 0.1))
     assert not np.array_equal(m1, rng.keep_mask(3, 18, (300, 300), 0.1))
     assert rng.keep_mask(3, 17, (10,), 0.0).all()
+
+
+def test_signum_and_schedule_free_closed_forms():
+    """Signum (optim/signum.py): step 1 is -lr (sign(g) + wd p) with or without Nesterov; factory
+    validation errors.  Schedule-free (optax.contrib.schedule_free): with a constant lr c_k = 1/k,
+    the first update equals the base update (x = z_1, y = z_1), and x_k is the running mean of the
+    z iterates (checked with a fixed-step base, where z_k = z_0 + k u)."""
+    p = {"w": torch.randn(4, 3, dtype=torch.float64)}
+    g = {"w": torch.randn(4, 3, dtype=torch.float64)}
+    for nest in (False, True):
+        tx = oopt.signum(0.1, 0.9, nest, 0.01)
+        u, _ = tx.update(g, tx.init(p), p)
+        assert torch.allclose(u["w"], -0.1 * (torch.sign(g["w"]) + 0.01 * p["w"]))
+    for bad in (dict(learning_rate=-1.0), dict(learning_rate=1.0, momentum=1.0), dict(learning_rate=1.0, weight_decay=-1)):
+        with pytest.raises(ValueError):
+            oopt.signum(**bad)
+    fixed = SimpleNamespace(init=lambda params: None,
+                            update=lambda grads, st, params: ({k: torch.full_like(v, 0.5) for k, v in grads.items()}, st))
+    b1 = 0.9
+    sf = oopt.schedule_free(fixed, 0.01, b1=b1)
+    st = sf.init(p)
+    y = dict(p)
+    z0 = p["w"].clone()
+    for k in range(1, 6):
+        u, st = sf.update(g, st, y)
+        y = apply_updates(y, u)
+        zk = z0 + 0.5 * k
+        xk = torch.stack([z0 + 0.5 * j for j in range(1, k + 1)]).mean(0)     # c_k = 1/k: running mean
+        assert torch.allclose(st.z["w"], zk) and torch.allclose(y["w"], b1 * xk + (1 - b1) * zk, atol=1e-6), k
+    with pytest.raises(ValueError):
+        oopt.schedule_free(fixed, 0.01, b1=0.0)

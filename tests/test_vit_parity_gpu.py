@@ -65,7 +65,7 @@ def test_vit_grads_match_oracle(dev, rate, use_ln, shape):
         assert r < 5e-2, (k, r)
 
 
-@pytest.mark.parametrize("optim", ["adamw", "muon"])
+@pytest.mark.parametrize("optim", ["adamw", "muon", "signum", "adamw+schedule_free"])
 def test_vit_train_step_matches_oracle(dev, optim):
     """Three engine steps (make_train_step: fused q|k|v groups, dropout 0.1 on, the in-place
     ``step_``).  Each step checks, against the oracle:
@@ -84,7 +84,9 @@ def test_vit_train_step_matches_oracle(dev, optim):
     from utils import Config
     m = _small_model(0.1)
     shape = (16, 16, 16, 3)
-    cfg = Config(optim=optim, lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9)
+    name, _, wrap = optim.partition("+")
+    cfg = Config(optim=name, lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9, schedule_free=bool(wrap),
+                 schedule_free_lr=0.01)
     init = m.init(3, shape)
     st = create_train_state(0, m, 1e-3, shape, m.num_classes, cfg=cfg, init_params=init)
     step = make_train_step()
@@ -108,8 +110,12 @@ def test_vit_train_step_matches_oracle(dev, optim):
                 assert _rel(g_hip[k], g_or[k]) < 5e-2, (it, k, _rel(g_hip[k], g_or[k]))
         u, s_h = tx_h.update(g_hip, s_h, p0)
         for k in init:
+            if name == "signum":   # elements whose momentum sign is a rounding-level tie may flip
+                d = (p1[k].double() - p0[k].double() - u[k].double()).abs()
+                assert (d > 0.5e-3).double().mean().item() <= 1e-3, (it, k)
+                continue
             e = step_rel(p0[k], p1[k], u[k])
-            assert e <= step_bound(optim, k, p0[k]), (it, k, e)
+            assert e <= step_bound(name, k, p0[k]), (it, k, e)
         _, go = value_and_grad(lambda p: (cross_entropy_loss(vit_apply(p, images, oc, True, it, bf16=True),
                                                              labels), None), po)
         uo, s_o = tx_o.update(go, s_o, po)
