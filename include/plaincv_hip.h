@@ -310,10 +310,24 @@ int64_t pcv_eigh_log_floats(int64_t n, int max_sweeps);
 int pcv_eigh_jacobi(const void* jobs, int njobs, int max_n, int max_sweeps, float tol_rel, float tol_abs_rel,
                     int sort_desc, float pow_floor, float pow_expo, void* stream);
 int pcv_eigh_vectors(const void* jobs, int njobs, int max_n, void* stream);
-/* Householder QR (LAPACK geqrf/orgqr sign convention), Q of A[:, perm] (perm optional), n <= 1024:
+/* Householder QR (LAPACK geqrf/orgqr sign convention), Q of A[:, perm] (perm optional), n <= 4096:
  *   record {A, perm, Q, W, Qt, lda, ldq, n}; W and Qt are n*n fp32 workspaces. */
 int pcv_qr_job_size(void);
 int pcv_householder_qr(const void* jobs, int njobs, int max_n, void* stream);
+int pcv_soap_sort_max_n(void);   /* largest n of pcv_householder_qr / pcv_soap_est_sort (4096) */
+/* Batched symmetric eigendecomposition for 256 < n <= 4096 (LM-sized SOAP / Shampoo factors;
+ * jnp.linalg.eigh at optim/soap.py:100-105, shampoo.py:205-206): one-sided (Hestenes) Jacobi on
+ * the rows of A + shift I in HBM, one workgroup per rotation, a round of np/2 disjoint rotations per
+ * launch (round-robin schedule), rotation flags per sweep [64] for the host's convergence test.
+ * Jobs: pcv_eigh_big_job_size() bytes each {A, At, Vt, w, wpow, perm, flags, skip, vout, lda, ldv,
+ * ldo, n, shift}; finish writes w (descending when sort_desc), wpow = max(w, floor)^-expo, perm and
+ * the eigenvectors as the columns of vout. */
+int pcv_eigh_big_job_size(void);
+int pcv_eigh_big_init(const void* jobs_dev, int njobs, int max_n, int64_t max_ldv, void* stream);
+int pcv_eigh_big_round(const void* jobs_dev, int njobs, int max_n, int round, int sweep, float tol, float tiny,
+                       void* stream);
+int pcv_eigh_big_finish(const void* jobs_dev, int njobs, int max_n, int sort_desc, float pow_floor, float pow_expo,
+                        void* stream);
 /* SOAP Adam in the rotated basis over flat arenas (soap.py:249-268), step = device int from 1. */
 int pcv_soap_adam(const float* g_rot, float* m, float* v, float* n_rot, int64_t n, float b1, float b2, float eps,
                   const int* step, int correct_bias, void* stream);

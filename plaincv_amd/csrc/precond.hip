@@ -479,7 +479,7 @@ struct QrJob {
 };
 static_assert(sizeof(QrJob) == 8 * 8, "QrJob layout");
 
-constexpr int QR_THREADS = 1024, QR_MAXN = 1024;
+constexpr int QR_THREADS = 1024, QR_MAXN = 4096;   // W / Qt live in HBM; LDS holds v and tau only
 
 __global__ __launch_bounds__(QR_THREADS) void householder_qr_kernel(const QrJob* __restrict__ jobs) {
   __shared__ float vsh[QR_MAXN];
@@ -643,6 +643,7 @@ extern "C" int pcv_newton_select(const void* jobs_dev, int njobs, int iters, flo
   return pcv_launch_status();
 }
 extern "C" int pcv_eigh_job_size(void) { return (int)sizeof(EighJob); }
+extern "C" int pcv_soap_sort_max_n(void) { return QR_MAXN; }
 extern "C" int pcv_vec_job_size(void) { return (int)sizeof(VecJob); }
 extern "C" int pcv_qr_job_size(void) { return (int)sizeof(QrJob); }
 extern "C" int pcv_sort_job_size(void) { return (int)sizeof(SortJob); }
@@ -701,7 +702,7 @@ extern "C" int pcv_soap_adam(const float* g, float* m, float* v, float* nrot, in
 }
 
 extern "C" int pcv_soap_est_sort(const void* jobs_dev, int njobs, void* stream) {
-  if (!jobs_dev || njobs <= 0) return PCV_EINVAL;
+  if (!jobs_dev || njobs <= 0) return PCV_EINVAL;   // host plan checks n <= pcv_soap_sort_max_n()
   hipLaunchKernelGGL(soap_est_sort_kernel, dim3(njobs), dim3(256), 0, (hipStream_t)stream,
                      (const SortJob*)jobs_dev);
   return pcv_launch_status();

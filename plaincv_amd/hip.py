@@ -95,6 +95,11 @@ SIGNATURES = {
     "pcv_eigh_jacobi": [P, I32, I32, I32, F32, F32, I32, F32, F32, P],
     "pcv_eigh_vectors": [P, I32, I32, P],
     "pcv_householder_qr": [P, I32, I32, P],
+    "pcv_soap_sort_max_n": [],
+    "pcv_eigh_big_job_size": [],
+    "pcv_eigh_big_init": [P, I32, I32, I64, P],
+    "pcv_eigh_big_round": [P, I32, I32, I32, I32, F32, F32, P],
+    "pcv_eigh_big_finish": [P, I32, I32, I32, F32, F32, P],
     "pcv_soap_adam": [P, P, P, P, I64, F32, F32, F32, P, I32, P],
     "pcv_soap_est_sort": [P, I32, P],
     "pcv_permute_rc": [P, I32, I64, P],

@@ -12,7 +12,9 @@ from .. import hip
 from ..hip import ptr, stream_ptr
 
 TILE = 64
-EIGH_MAX_N = 256
+EIGH_MAX_N = 256          # two-sided LDS Jacobi (one CU per matrix)
+EIGH_BIG_MAX_N = 4096     # one-sided Jacobi in HBM (csrc/eigh_big.hip)
+QR_MAX_N = 4096
 
 
 def _addr(t):
@@ -169,36 +171,47 @@ class NewtonRoot:
 
 
 class Eigh:
-    """Batched symmetric eigendecomposition (cyclic Jacobi, csrc/precond.hip) of n <= 256
-    matrices: eigenvalues w (descending if sort_desc), optional wpow = max(w, floor)^(-expo),
-    eigenvectors written to vout (starting from basis v0 when given: vout = v0 @ eigvecs(A))."""
+    """Batched symmetric eigendecomposition: eigenvalues w (descending if sort_desc), optional
+    wpow = max(w, floor)^(-expo), eigenvectors written to vout (starting from basis v0 when given:
+    vout = v0 @ eigvecs(A)).  n <= 256: cyclic two-sided Jacobi with the packed triangle in one CU's
+    LDS (csrc/precond.hip); 256 < n <= 4096 (LM factors): one-sided Jacobi over HBM, a round of
+    independent rotations per launch (csrc/eigh_big.hip), sweeps until a sweep rotates nothing."""
 
     FMT_E = "<7Q2qd"
     FMT_V = "<6Q3q"
+    FMT_B = "<9Q4qd"
 
     def __init__(self, device, max_sweeps=15, tol_rel=2e-7, tol_abs_rel=1e-9, sort_desc=True, pow_floor=0.0,
-                 pow_expo=0.0):
+                 pow_expo=0.0, big_max_sweeps=30, big_tol=2e-6):
         self.device = torch.device(device)
         self.max_sweeps, self.tol_rel, self.tol_abs_rel = int(max_sweeps), float(tol_rel), float(tol_abs_rel)
         self.sort_desc, self.pow_floor, self.pow_expo = int(bool(sort_desc)), float(pow_floor), float(pow_expo)
+        self.big_max_sweeps, self.big_tol = int(big_max_sweeps), float(big_tol)
         self.items = []
+        self.big = []
+        self.sweeps_run = 0
 
     def add(self, a, vout, v0=None, shift=0.0, want_pow=False, skip=None):
         """skip: device float; the job (eigenvalues and vectors) is skipped when *skip <= 0.5."""
         n = a.shape[0]
         if a.shape != (n, n) or vout.shape != (n, n) or (v0 is not None and v0.shape != (n, n)):
             raise ValueError("eigh: square matrices of one size per job")
-        if n > EIGH_MAX_N or n < 2:
-            raise NotImplementedError(f"eigh kernel handles 2 <= n <= {EIGH_MAX_N} (got {n})")
+        if n > EIGH_BIG_MAX_N or n < 2:
+            raise NotImplementedError(f"eigh handles 2 <= n <= {EIGH_BIG_MAX_N} (got {n})")
         _ld(a), _ld(vout)
+        z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=self.device)  # noqa: E731
+        if n > EIGH_MAX_N:
+            np_, ldv = n + (n & 1), (n + 3) // 4 * 4
+            it = dict(a=a, vout=vout, v0=v0, shift=float(shift), n=n, skip=skip, ldv=ldv,
+                      At=z(np_, ldv), Vt=z(np_, ldv), w=z(n), wpow=z(n) if want_pow else None,
+                      perm=z(n, dt=torch.int32), flags=z(64, dt=torch.int32),
+                      tmp=z(n, n) if v0 is not None else None)
+            self.big.append(it)
+            return it
         lib = hip.load()
         it = dict(a=a, vout=vout, v0=v0, shift=float(shift), n=n, skip=skip,
-                  w=torch.zeros(n, dtype=torch.float32, device=self.device),
-                  wpow=torch.zeros(n, dtype=torch.float32, device=self.device) if want_pow else None,
-                  perm=torch.zeros(n, dtype=torch.int32, device=self.device),
-                  log=torch.zeros(int(lib.pcv_eigh_log_floats(n, self.max_sweeps)), dtype=torch.float32,
-                                  device=self.device),
-                  nrounds=torch.zeros(1, dtype=torch.int32, device=self.device))
+                  w=z(n), wpow=z(n) if want_pow else None, perm=z(n, dt=torch.int32),
+                  log=z(int(lib.pcv_eigh_log_floats(n, self.max_sweeps))), nrounds=z(1, dt=torch.int32))
         self.items.append(it)
         return it
 
@@ -206,6 +219,7 @@ class Eigh:
         lib = hip.load()
         assert lib.pcv_eigh_job_size() == struct.calcsize(self.FMT_E)
         assert lib.pcv_vec_job_size() == struct.calcsize(self.FMT_V)
+        assert lib.pcv_eigh_big_job_size() == struct.calcsize(self.FMT_B)
         e, v = [], []
         for it in self.items:
             e.append((_addr(it["a"]), _addr(it["w"]), _addr(it["wpow"]), _addr(it["perm"]), _addr(it["log"]),
@@ -216,15 +230,51 @@ class Eigh:
         self.max_n = max([it["n"] for it in self.items], default=0)
         self.e_dev = _pack(e, self.FMT_E).to(self.device) if e else None
         self.v_dev = _pack(v, self.FMT_V).to(self.device) if v else None
+        b = []
+        self.big_v0 = GemmF32()
+        for it in self.big:
+            out = it["tmp"] if it["v0"] is not None else it["vout"]
+            b.append((_addr(it["a"]), _addr(it["At"]), _addr(it["Vt"]), _addr(it["w"]), _addr(it["wpow"]),
+                      _addr(it["perm"]), _addr(it["flags"]), _addr(it["skip"]), _addr(out), it["a"].stride(0),
+                      it["ldv"], out.stride(0), it["n"], it["shift"]))
+            if it["v0"] is not None:
+                self.big_v0.add(it["v0"], it["tmp"], it["vout"], conv_in=it["skip"], conv_tol=0.5) \
+                    if it["skip"] is not None else self.big_v0.add(it["v0"], it["tmp"], it["vout"])
+        self.big_n = max([it["n"] for it in self.big], default=0)
+        self.big_ldv = max([it["ldv"] for it in self.big], default=0)
+        self.b_dev = _pack(b, self.FMT_B).to(self.device) if b else None
+        if self.big_v0.jobs:
+            self.big_v0.finalize(self.device)
         return self
 
     def run(self):
-        if not self.items:
-            return
         s = stream_ptr()
-        hip.call("pcv_eigh_jacobi", ptr(self.e_dev), len(self.items), self.max_n, self.max_sweeps, self.tol_rel,
-                 self.tol_abs_rel, self.sort_desc, self.pow_floor, self.pow_expo, s)
-        hip.call("pcv_eigh_vectors", ptr(self.v_dev), len(self.items), self.max_n, s)
+        if self.items:
+            hip.call("pcv_eigh_jacobi", ptr(self.e_dev), len(self.items), self.max_n, self.max_sweeps, self.tol_rel,
+                     self.tol_abs_rel, self.sort_desc, self.pow_floor, self.pow_expo, s)
+            hip.call("pcv_eigh_vectors", ptr(self.v_dev), len(self.items), self.max_n, s)
+        if self.big:
+            self._run_big(s)
+
+    def _run_big(self, s):
+        """Host-driven sweeps (one sync per sweep): SOAP's one-off initial basis and Shampoo's
+        fallback; skipped jobs (Newton converged) are checked once up front."""
+        skips = [it["skip"] for it in self.big if it["skip"] is not None]
+        if len(skips) == len(self.big) and all(float(x.item()) <= 0.5 for x in skips):
+            return
+        nb, n_max = len(self.big), self.big_n
+        hip.call("pcv_eigh_big_init", ptr(self.b_dev), nb, n_max, self.big_ldv, s)
+        rounds = n_max + (n_max & 1) - 1
+        self.sweeps_run = 0
+        for sweep in range(min(self.big_max_sweeps, 64)):
+            for r in range(rounds):
+                hip.call("pcv_eigh_big_round", ptr(self.b_dev), nb, n_max, r, sweep, self.big_tol, 1e-30, s)
+            self.sweeps_run = sweep + 1
+            if int(torch.stack([it["flags"][sweep] for it in self.big]).max().item()) == 0:
+                break
+        hip.call("pcv_eigh_big_finish", ptr(self.b_dev), nb, n_max, self.sort_desc, self.pow_floor, self.pow_expo, s)
+        if self.big_v0.jobs:
+            self.big_v0.run()
 
 
 class HouseholderQR:
@@ -240,8 +290,8 @@ class HouseholderQR:
         n = a.shape[0]
         if a.shape != (n, n) or q.shape != (n, n):
             raise ValueError("qr: square matrices expected")
-        if n > 1024:
-            raise NotImplementedError("householder_qr handles n <= 1024")
+        if n > QR_MAX_N:
+            raise NotImplementedError(f"householder_qr handles n <= {QR_MAX_N}")
         _ld(a), _ld(q)
         self.items.append(dict(a=a, q=q, perm=perm, n=n,
                                w=torch.zeros(n * n, dtype=torch.float32, device=self.device),
@@ -274,6 +324,8 @@ class EstSort:
         n = q.shape[0]
         if q.shape != (n, n) or t.shape != (n, n) or perm.numel() != n:
             raise ValueError("est_sort shapes")
+        if n > QR_MAX_N:
+            raise NotImplementedError(f"est_sort handles n <= {QR_MAX_N}")
         self.recs.append((_addr(q), _addr(t), _addr(perm), _ld(q), _ld(t), n))
 
     def finalize(self):

@@ -48,7 +48,8 @@ def test_attn_drop_mask_bits(dev, T, rate):
 @pytest.mark.parametrize("B,T,H,Dh,causal,rate", [(2, 257, 4, 32, False, 0.0), (2, 100, 2, 64, True, 0.0),
                                                   (1, 1024, 2, 64, True, 0.0), (2, 257, 4, 32, False, 0.1),
                                                   (3, 70, 3, 32, True, 0.0), (2, 100, 2, 64, True, 0.2),
-                                                  (1, 300, 2, 32, False, 0.3)])
+                                                  (1, 300, 2, 32, False, 0.3),
+                                                  (1, 2048, 2, 64, True, 0.0)])   # C5: T = 2048, Dh = 64
 def test_attention_fwd_bwd(dev, B, T, H, Dh, causal, rate):
     from oracle import rng
     from plaincv_amd import kernels as K

@@ -3,6 +3,8 @@
 Kernel level (vs torch fp64 on the same device, a checker only):
   grouped fp32 GEMM  max|err| <= 2e-5 * sum|a||b|-scale (exact-fp32 MFMA chain)
   Jacobi eigh        eigenvalues within 2e-5 * ||A||, ||A V - V diag(w)|| <= 5e-5 ||A||, ||V^T V - I|| <= 5e-5
+  one-sided eigh     (256 < n <= 4096, LM factors) eigenvalues within 1e-4 * ||A||, same residual / 1e-4
+                     orthogonality bounds scaled by sqrt(n / 256)
   Householder QR     Q within 1e-4 of LAPACK's Q (same sign convention) for full-rank inputs;
                      orthonormal and A[:, perm] = Q (Q^T A[:, perm]) with upper-triangular R otherwise
 Optimizer level (vs the CPU oracle, oracle/optim.py, fp32):
@@ -97,6 +99,80 @@ def test_eigh_jacobi(dev, n, rank):
     assert int(it["nrounds"].item()) > 0
 
 
+@pytest.mark.parametrize("n,rank", [(300, 300), (513, 100), (768, 768), (1031, 1031), (2304, 768)])
+def test_eigh_big_one_sided(dev, n, rank):
+    """LM-sized factors (768 = d of the 124M model, 2304 = its w_qkv fan-out, rank 768 = a
+    rank-deficient R = g^T g) through the one-sided Jacobi path."""
+    from plaincv_amd.optim.precond import Eigh
+    g = torch.Generator().manual_seed(n + rank)
+    A = _spd(n, rank, g, dev, 1.0 / rank ** 0.5)
+    V = torch.zeros(n, n, device=dev)
+    e = Eigh(dev, sort_desc=True)
+    it = e.add(A, V)
+    e.finalize().run()
+    torch.cuda.synchronize()
+    Ad = A.double()
+    w_ref = torch.linalg.eigvalsh(Ad).flip(0)
+    an = w_ref.abs().max().item()
+    w, Vd = it["w"].double(), V.double()
+    sc = max(1.0, (n / 256) ** 0.5)
+    print(f"EIGH_BIG n={n} rank={rank} sweeps={e.sweeps_run} werr={(w - w_ref).abs().max().item() / an:.2e}")
+    assert (w - w_ref).abs().max().item() <= 1e-4 * an
+    assert torch.all(w[:-1] >= w[1:])
+    assert (Ad @ Vd - Vd * w[None, :]).norm().item() <= 5e-5 * sc * an * n ** 0.5
+    assert (Vd.t() @ Vd - torch.eye(n, device=dev, dtype=torch.float64)).abs().max().item() <= 1e-4 * sc
+    assert 1 <= e.sweeps_run < e.big_max_sweeps
+
+
+def test_eigh_big_batched_warm_start_and_skip(dev):
+    """One Eigh plan mixing the LDS path (n <= 256) and two one-sided sizes; a warm-started big job
+    (vout = v0 @ eigvecs(v0^T L v0 + eps I)) reproduces the cold inverse root; a skipped job is left
+    untouched."""
+    from plaincv_amd.optim.precond import Eigh, GemmF32
+    g = torch.Generator().manual_seed(11)
+    eps = 1e-4
+    mats = [_spd(n, r, g, dev, 1.0 / r ** 0.5) for n, r in ((200, 100), (400, 400), (600, 300))]
+    outs = [torch.zeros_like(m) for m in mats]
+    e = Eigh(dev, sort_desc=False, pow_floor=eps, pow_expo=0.25)
+    its = [e.add(m, o, shift=eps, want_pow=True) for m, o in zip(mats, outs)]
+    skipped = torch.full((500, 500), 7.0, device=dev)
+    sk_flag = torch.zeros(1, device=dev)
+    e.add(_spd(500, 500, g, dev), skipped, skip=sk_flag)
+    e.finalize().run()
+    torch.cuda.synchronize()
+    assert torch.all(skipped == 7.0)
+    def root(Lm, dt):
+        n = Lm.shape[0]
+        w, Q = torch.linalg.eigh(Lm.to(dt) + eps * torch.eye(n, device=dev, dtype=dt))
+        return ((Q * w.clamp(min=eps) ** -0.25) @ Q.t()).double()
+
+    # bar: a multiple of the error of fp32 eigh (+1e-5), as test_shampoo_inverse_root -- 2x for the
+    # one-sided path, 3x for the two-sided LDS path on the rank-deficient 200 (null-space eigenvalues
+    # clamp to eps, where an absolute eigenvalue error of ~1e-6 ||A|| moves (w + eps)^-1/4 by %)
+    for m, o, it in zip(mats, outs, its):
+        P = (o.double() * it["wpow"].double()[None, :]) @ o.double().t()
+        P64 = root(m, torch.float64)
+        rel = lambda X: (X - P64).norm().item() / P64.norm().item()  # noqa: E731
+        k = 3 if m.shape[0] <= 256 else 2
+        assert rel(P) <= k * rel(root(m, torch.float32)) + 1e-5, (m.shape[0], rel(P))
+    # warm start from the previous basis on a perturbed L (Shampoo eigh mode at LM sizes)
+    L0, U = mats[1], outs[1]
+    L1 = L0 + _spd(400, 4, g, dev, 0.05)
+    T, A = torch.zeros_like(L0), torch.zeros_like(L0)
+    GemmF32().add(L1, U, T).finalize(dev).run()
+    GemmF32().add(U, T, A, ta=True).finalize(dev).run()
+    U2 = torch.zeros_like(U)
+    warm = Eigh(dev, sort_desc=False, pow_floor=eps, pow_expo=0.25)
+    w_it = warm.add(A, U2, v0=U, shift=eps, want_pow=True)
+    warm.finalize().run()
+    torch.cuda.synchronize()
+    P = (U2.double() * w_it["wpow"].double()[None, :]) @ U2.double().t()
+    P64 = root(L1, torch.float64)
+    rel = lambda X: (X - P64).norm().item() / P64.norm().item()  # noqa: E731
+    assert rel(P) <= 2 * rel(root(L1, torch.float32)) + 1e-5
+    assert warm.sweeps_run <= e.sweeps_run
+
+
 def test_eigh_warm_start_and_inverse_root(dev):
     """Shampoo's use: eigh of U^T L U + eps I from a previous basis U gives the same
     P = U' max(w, eps)^(-1/4) U'^T as a cold eigh of L + eps I, in fewer rounds."""
@@ -126,7 +202,8 @@ def test_eigh_warm_start_and_inverse_root(dev):
     assert int(w_it["nrounds"].item()) < int(c_it["nrounds"].item())
 
 
-@pytest.mark.parametrize("n,rank,use_perm", [(5, 5, False), (128, 128, True), (256, 256, True), (200, 60, True)])
+@pytest.mark.parametrize("n,rank,use_perm", [(5, 5, False), (128, 128, True), (256, 256, True), (200, 60, True),
+                                             (1100, 1100, True), (1500, 400, True)])
 def test_householder_qr(dev, n, rank, use_perm):
     from plaincv_amd.optim.precond import HouseholderQR
     g = torch.Generator().manual_seed(n)
@@ -243,6 +320,53 @@ def test_soap_matches_oracle(dev):
         for k in shapes:
             d = (u[k] - o[k]).abs().max().item()
             assert d <= 5e-3 * max(o[k].abs().max().item(), lr), (i, k, d)
+
+
+def test_soap_lm_sized_square_matches_oracle(dev):
+    """A square routed leaf past the LDS eigh (n = 320: one-sided Jacobi basis at step 0, QR
+    refreshes at f = 4) plus a small one, 9 steps.  A square gradient's factors are ill-conditioned
+    (L = g g^T spans ~1e5), so eigenvectors inside clusters differ between ANY two fp32 eighs: the
+    bar is the reference algorithm's own fp32 error -- the HIP update is compared with the oracle
+    run in fp64 and must be within 2x the fp32 oracle's distance to it (+ 1e-4 of the update)."""
+    from oracle import optim as oopt
+    from plaincv_amd.optim.soap import Soap
+    shapes = OrderedDict([("big/kernel", (320, 320)), ("a/kernel", (64, 64)), ("a/bias", (64,))])
+    lr = 1e-2
+    kw = dict(b1=0.9, b2=0.9, weight_decay=0.01, precondition_frequency=4)
+    store, p32 = _store(dev, shapes)
+    p64 = OrderedDict((k, v.double()) for k, v in p32.items())
+    tx, o32, o64 = Soap(lr, **kw), oopt.soap(lr, **kw), oopt.soap(lr, **kw)
+    gst, s32, s64 = tx.init(store), o32.init(p32), o64.init(p64)
+    g = torch.Generator().manual_seed(1)
+    for i in range(9):
+        grads = OrderedDict((k, torch.randn(sh, generator=g)) for k, sh in shapes.items())
+        u, gst = tx.update(OrderedDict((k, v.to(dev)) for k, v in grads.items()), gst, store)
+        u = OrderedDict((k, v.clone().cpu().double()) for k, v in u.items())
+        u32, s32 = o32.update(grads, s32, p32)
+        u64, s64 = o64.update(OrderedDict((k, v.double()) for k, v in grads.items()), s64, p64)
+        for k in shapes:
+            store.params[k].add_(u[k].float().to(dev))
+            p32[k] = p32[k] + u32[k]
+            p64[k] = p64[k] + u64[k]
+            if i == 0 and k.endswith("kernel"):
+                assert u[k].abs().max().item() == 0.0
+                continue
+            err, base = (u[k] - u64[k]).norm().item(), (u32[k].double() - u64[k]).norm().item()
+            assert err <= 2 * base + 1e-4 * u64[k].norm().item(), (i, k, err, base)
+
+
+def test_shampoo_eigh_root_lm_sized(dev):
+    """Shampoo's eigh root mode on a 300 x 520 leaf (both factors past the LDS eigh) vs the oracle."""
+    from oracle import optim as oopt
+    from plaincv_amd.optim.shampoo import Shampoo
+    shapes = OrderedDict([("w/kernel", (300, 520)), ("w/bias", (520,))])
+    lr = 1e-2
+    steps = _run_pair(dev, shapes, Shampoo(lr, eps=1e-4, weight_decay=0.01, root_method="eigh"),
+                      oopt.shampoo(lr, eps=1e-4, weight_decay=0.01), 3)
+    for i, (u, o) in enumerate(steps):
+        for k in shapes:
+            d = (u[k] - o[k]).abs().max().item()
+            assert d <= 2e-3 * max(o[k].abs().max().item(), lr), (i, k, d)
 
 
 def test_soap_rectangular_invariants(dev):

@@ -34,7 +34,9 @@ def tm(fn, iters=20):
 
 
 CASES = [("vit drop", 64, 257, 4, 32, False, 0.1), ("vit nodrop", 64, 257, 4, 32, False, 0.0),
-         ("vit T256 nodrop", 64, 256, 4, 32, False, 0.0),
+         ("vit T256 nodrop", 64, 256, 4, 32, False, 0.0), ("vit T256 drop", 64, 256, 4, 32, False, 0.1),
+         ("vit T241 nodrop", 64, 241, 4, 32, False, 0.0), ("vit T272 nodrop", 64, 272, 4, 32, False, 0.0),
+         ("vit T128x2 nodrop", 128, 128, 4, 32, False, 0.0),
          ("lm124m", 16, 1024, 12, 64, True, 0.0), ("lm420m", 8, 2048, 16, 64, True, 0.0),
          ("vitT32", 64, 32, 4, 32, False, 0.0), ("vitT64", 64, 64, 4, 32, False, 0.0),
          ("vitT128", 64, 128, 4, 32, False, 0.0), ("vitT192", 64, 192, 4, 32, False, 0.0)]
