@@ -266,6 +266,19 @@ int pcv_transpose_rec_size(void);
  * workgroup's LDS (csrc/muon_fused.hip): reads each record's x32 (un-normalised, from
  * pcv_muon_prep) and norm2, writes xo.  pcv_muon_fused_ok(rows, cols) says which shapes qualify. */
 int pcv_muon_fused_ok(int64_t rows, int64_t cols);
+/* The whole Muon step in ONE launch when every routed matrix fits pcv_muon_ns_fused (ViT-small):
+ * nmats workgroups run momentum/Nesterov prep, the in-block Frobenius norm, NS and the update of one
+ * matrix each (records as pcv_muon_prep / pcv_muon_apply: p/pb or upd per record), nchunks more run
+ * the Adam branch (chunk table as pcv_adamw_step) over the flat p, g, mu, nu; the last block to finish
+ * bumps *step (ticket: a zeroed device int the call leaves zeroed).  apply = 0: updates to the
+ * records' upd and to the flat upd (functional update()).  in_block = 0: the matrix workgroups run
+ * NS only (x32 / norm2 from pcv_muon_prep before, xo for pcv_muon_apply after: the streaming
+ * parts stay wide), the Adam branch and the bump still ride in this launch. */
+int pcv_muon_step_fused(const void* mats, int nmats, const void* chunks, int nchunks, float* p, const float* g,
+                        float* mu, float* nu, void* p_bf16, float* upd, float lr, float wd, float beta, int nesterov,
+                        float eps, int shape_scale, float ns_a, float ns_b, float ns_c, int ns_steps, float adam_b1,
+                        float adam_b2, float adam_eps_root, float adam_wd, int apply, int* step, const float* gscale,
+                        int* ticket, int in_block, void* stream);
 int pcv_muon_ns_fused(const void* mats, int nmats, float eps, float ns_a, float ns_b, float ns_c, int ns_steps,
                       void* stream);
 int pcv_chunk_size(void);

@@ -20,39 +20,10 @@
 
 namespace pcv {
 
-struct Chunk { int64_t start; int64_t len; };
-
-struct AdamHyper {
-  float lr, b1, b2, eps, eps_root, wd;
-  int nesterov, apply;
-};
-
 __global__ __launch_bounds__(256) void adamw_kernel(float* p, const float* g, float* m, float* v, bf16* pb, float* upd,
                                                     const Chunk* chunks, AdamHyper h, const int* step,
                                                     const float* gscale) {
-  const Chunk ck = chunks[blockIdx.x];
-  const float t = (float)(*step + 1);
-  const float bc1 = 1.f - powf(h.b1, t), bc2 = 1.f - powf(h.b2, t);
-  const float bc1n = 1.f - powf(h.b1, t + 1.f);
-  const float gs = gscale ? *gscale : 1.f;
-#pragma unroll 4
-  for (int64_t i = ck.start + threadIdx.x; i < ck.start + ck.len; i += 256) {
-    const float gi = g[i] * gs;
-    const float mi = h.b1 * m[i] + (1.f - h.b1) * gi;
-    const float vi = h.b2 * v[i] + (1.f - h.b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    const float mh = h.nesterov ? h.b1 * mi / bc1n + (1.f - h.b1) * gi / bc1 : mi / bc1;
-    const float vh = vi / bc2;
-    const float pi = p[i];
-    const float u = -h.lr * (mh / (sqrtf(vh + h.eps_root) + h.eps) + h.wd * pi);
-    if (upd) upd[i] = u;
-    if (h.apply) {
-      const float pn = pi + u;
-      p[i] = pn;
-      if (pb) pb[i] = f2bf(pn);
-    }
-  }
+  adamw_chunk(p, g, m, v, pb, upd, chunks[blockIdx.x], h, *step, gscale ? *gscale : 1.f);
 }
 
 struct SignumHyper {

@@ -20,4 +20,38 @@ struct MuonHyper {
   int nesterov, apply;
 };
 
+struct Chunk { int64_t start; int64_t len; };
+
+struct AdamHyper {
+  float lr, b1, b2, eps, eps_root, wd;
+  int nesterov, apply;
+};
+
+// optax.adamw over one chunk of the flat buffers (count-from-1 bias correction, step = the
+// device counter before this step's bump; optional Nesterov = optax.contrib.muon's adam branch)
+__device__ __forceinline__ void adamw_chunk(float* p, const float* g, float* m, float* v, bf16* pb, float* upd,
+                                            const Chunk ck, const AdamHyper& h, int step, float gs) {
+  const float t = (float)(step + 1);
+  const float bc1 = 1.f - powf(h.b1, t), bc2 = 1.f - powf(h.b2, t);
+  const float bc1n = 1.f - powf(h.b1, t + 1.f);
+#pragma unroll 4
+  for (int64_t i = ck.start + threadIdx.x; i < ck.start + ck.len; i += blockDim.x) {
+    const float gi = g[i] * gs;
+    const float mi = h.b1 * m[i] + (1.f - h.b1) * gi;
+    const float vi = h.b2 * v[i] + (1.f - h.b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float mh = h.nesterov ? h.b1 * mi / bc1n + (1.f - h.b1) * gi / bc1 : mi / bc1;
+    const float vh = vi / bc2;
+    const float pi = p[i];
+    const float u = -h.lr * (mh / (sqrtf(vh + h.eps_root) + h.eps) + h.wd * pi);
+    if (upd) upd[i] = u;
+    if (h.apply) {
+      const float pn = pi + u;
+      p[i] = pn;
+      if (pb) pb[i] = f2bf(pn);
+    }
+  }
+}
+
 }  // namespace pcv

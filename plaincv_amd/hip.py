@@ -70,6 +70,8 @@ SIGNATURES = {
     "pcv_step_bump": [P, P],
     "pcv_muon_prep": [P, I32, I32, I64, F32, I32, F32, P, P, P],
     "pcv_muon_apply": [P, I32, I64, F32, F32, I32, I32, P],
+    "pcv_muon_step_fused": [P, I32, P, I32, P, P, P, P, P, P, F32, F32, F32, I32, F32, I32, F32, F32, F32, I32, F32,
+                            F32, F32, F32, I32, P, P, P, I32, P],
     "pcv_muon_ns_fused": [P, I32, F32, F32, F32, F32, I32, P],
     "pcv_muon_fused_ok": [I64, I64],
     "pcv_transpose_bf16_batch": [P, I32, I64, P],

@@ -24,6 +24,8 @@ workgroup with X, A, B resident in LDS -- one launch for all such matrices.
 """
 from collections import OrderedDict
 
+import os
+
 import numpy as np
 import torch
 
@@ -68,6 +70,9 @@ class Muon(GradientTransformation):
         self.adam = (float(adam_b1), float(adam_b2), float(adam_eps_root), float(adam_weight_decay))
         self.shape_scale = bool(shape_scale)
         self.fused = bool(fused)     # False: every routed matrix takes the batched-GEMM chain
+        # all-fused models run the whole step as one launch (PCV_MUON_ONE_LAUNCH=0: the 5-launch form)
+        self.one_launch = os.environ.get("PCV_MUON_ONE_LAUNCH", "1") != "0"
+        self.in_block = os.environ.get("PCV_MUON_IN_BLOCK", "0") == "1"
 
     def init(self, store):
         dev = store.device
@@ -96,6 +101,10 @@ class Muon(GradientTransformation):
         st.n_general = sum(len(g.names) for g in st.groups if not g.fused)
         st.n_fused = len(routed) - st.n_general
         st.norm2 = torch.zeros(max(1, len(routed)), dtype=torch.float32, device=dev)
+        st.ticket = torch.zeros(1, dtype=torch.int32, device=dev)   # last-block counter of the one-launch step
+        # the one-launch step moves 4 consecutive columns per lane (16-B accesses of p, g, mu)
+        st.vec4 = all(store.params[k].shape[1] % 4 == 0 and store.leaf(k).offset % 4 == 0 and
+                      store.leaf(k).strides[0] % 4 == 0 for k in routed)
         st.max_elems = max([store.params[k].numel() for k in routed], default=1)
         mu = st.tensors["mu"]
         size = lib.pcv_muon_mat_size()
@@ -138,6 +147,25 @@ class Muon(GradientTransformation):
                      stream_ptr())
 
     def _run(self, store, st, gscale, apply):
+        if st.routed and st.n_general == 0 and self.one_launch and st.vec4:
+            # every routed matrix fits the one-workgroup NS: the NS workgroups, the Adam branch and the
+            # step bump share one launch (csrc/muon_fused.hip muon_step_kernel); prep and apply stay
+            # wide launches around it (PCV_MUON_IN_BLOCK=1 moves them into the NS workgroups)
+            b1, b2, eps_root, awd = self.adam
+            br = st.branch
+            mats = st.mats_apply if apply else st.mats_upd
+            if not self.in_block:
+                hip.call("pcv_muon_prep", ptr(st.mats_apply), len(st.routed), 0, st.max_elems, self.beta,
+                         int(self.nesterov), self.eps, ptr(st.count), ptr(gscale), stream_ptr())
+            hip.call("pcv_muon_step_fused", ptr(mats), len(st.routed), ptr(br.chunks) if br.nchunks else None,
+                     br.nchunks, ptr(store.flat), ptr(store.grad_flat), ptr(st.tensors["mu"]), ptr(st.tensors["nu"]),
+                     ptr(store.shadow), ptr(st.upd), self.lr, self.wd, self.beta, int(self.nesterov), self.eps,
+                     int(self.shape_scale), self.a, self.b, self.c, self.ns_steps, b1, b2, eps_root, awd, int(apply),
+                     ptr(st.count), ptr(gscale), ptr(st.ticket), int(self.in_block), stream_ptr())
+            if not self.in_block:
+                hip.call("pcv_muon_apply", ptr(mats), len(st.routed), st.max_elems, self.lr, self.wd,
+                         int(self.shape_scale), int(apply), stream_ptr())
+            return
         if st.routed:   # st.norm2 is zero here: created zeroed, reset by pcv_muon_apply after use
             hip.call("pcv_muon_prep", ptr(st.mats_apply), len(st.routed), st.n_general, st.max_elems, self.beta,
                      int(self.nesterov), self.eps, ptr(st.count), ptr(gscale), stream_ptr())
