@@ -216,6 +216,21 @@ int pcv_embed_fwd(const int* ids, const void* table, int64_t ldt, void* out, int
 int pcv_embed_bwd(const int* ids, const void* dx, int64_t lddx, float* dtable, int64_t ldt, int64_t R,
                   int D, int V, void* stream);
 
+/* The ViT classifier head in ONE workgroup (models/vit_small.py:123-127, flax_engine.py:13-22):
+ * y = LayerNorm(x cls rows) -> yf (bf16), logits = y W + bias (fp32, [B][ldl]), metrics = [mean CE,
+ * mean accuracy]; with dlogits != NULL also dlogits = (softmax - onehot) * grad_scale (fp32 + bf16),
+ * dx (cls rows) = LayerNorm VJP of dlogits W^T, dscale / dbias += its parameter gradients, dhead_bias
+ * (optional) += the column sums of dlogits, and dym
+ * (cls rows) = bf16 dropout VJP of dx (index (b * row_stride) * D + c, the top block's MLP-out site).
+ * x / dx / dym rows: stride ldx / lddx / lddym (T * D for the cls rows).  pcv_vit_head_ok(B, D, K):
+ * B <= 64, D <= 128 multiple of 32, K <= 256. */
+int pcv_vit_head_ok(int B, int D, int K);
+int pcv_vit_head(const float* x, int64_t ldx, const float* ln_scale, const float* ln_bias, float eps, const void* W,
+                 int64_t ldw, const float* bias, const int* labels, int B, int D, int K, void* yf, int64_t ldy,
+                 float* logits, int64_t ldl, float* metrics, float grad_scale, float* dlogits, void* dlogits_b,
+                 int64_t ldd, float* dx, int64_t lddx, float* dscale, float* dbias, float* dhead_bias, void* dym,
+                 int64_t lddym, float drop_rate, const uint32_t* seed, uint32_t site, int64_t row_stride,
+                 void* stream);
 /* ---------------------------------------------------------------- loss ----
  * Softmax cross-entropy + argmax accuracy per row, gradient (softmax-onehot)*grad_scale
  * (engine/flax_engine.py:13-22; train_lm.py:181-186).  pcv_mean2: deterministic means. */

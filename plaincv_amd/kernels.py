@@ -509,6 +509,35 @@ def xent(logits, labels, row_loss, row_correct, dlogits=None, grad_scale=1.0):
              float(grad_scale), stream_ptr())
 
 
+def vit_head_ok(B, D, K):
+    return bool(hip.load().pcv_vit_head_ok(int(B), int(D), int(K)))
+
+
+def vit_head(x, ln_scale, ln_bias, W, bias, labels, yf, logits, metrics, grad_scale=1.0, dlogits=None,
+             dlogits_b=None, dx=None, dscale=None, dbias=None, dym=None, drop_rate=0.0, seed=None, site=0,
+             row_stride=1, eps=1e-6, dhead_bias=None):
+    """Fused ViT head (pcv_vit_head): final LayerNorm of the cls rows x [B, D] (strided), logits, CE
+    metrics and, with dlogits given, the whole head backward down to the top block's dropout VJP."""
+    B, D = x.shape
+    Kc = bias.numel()
+    _chk(vit_head_ok(B, D, Kc), "vit_head shape")
+    _chk(x.dtype == F32 and W.dtype == BF16 and tuple(W.shape[:1]) == (D,) and W.shape[1] >= Kc, "vit_head W")
+    _chk(tuple(yf.shape) == (B, D) and yf.dtype == BF16 and tuple(logits.shape) == (B, Kc), "vit_head outputs")
+    _chk(labels.dtype == torch.int32 and labels.numel() == B, "vit_head labels")
+    grad = dlogits is not None
+    if grad:
+        _chk(tuple(dlogits.shape) == (B, Kc) and tuple(dlogits_b.shape) == (B, Kc) and _ld(dlogits) == _ld(dlogits_b) and
+             tuple(dx.shape) == (B, D) and tuple(dym.shape) == (B, D) and dx.dtype == F32 and dym.dtype == BF16,
+             "vit_head grads")
+    _dev(x, ln_scale, ln_bias, W, bias, labels, yf, logits, metrics, dlogits, dlogits_b, dx, dscale, dbias, dym, seed,
+         dhead_bias)
+    hip.call("pcv_vit_head", ptr(x), _ld(x), ptr(ln_scale), ptr(ln_bias), float(eps), ptr(W), _ld(W), ptr(bias),
+             ptr(labels), B, D, Kc, ptr(yf), _ld(yf), ptr(logits), _ld(logits), ptr(metrics), float(grad_scale),
+             ptr(dlogits), ptr(dlogits_b), _ld(dlogits) if grad else 0, ptr(dx), _ld(dx) if grad else 0,
+             ptr(dscale), ptr(dbias), ptr(dhead_bias), ptr(dym), _ld(dym) if grad else 0, float(drop_rate), ptr(seed),
+             int(site) & 0xFFFFFFFF, int(row_stride), stream_ptr())
+
+
 def mean2(x, y, n, scale, out):
     _dev(x, y, out)
     hip.call("pcv_mean2", ptr(x), ptr(y), int(n), float(scale), ptr(out), stream_ptr())

@@ -247,6 +247,11 @@ class ViTRunner:
         # cls token alone), so the other rows stay zero from here on -- no per-step memset
         self.dx = torch.zeros(R, D, dtype=f32, device=dev)
         self.dym = [e(R, D, dt=bf) for _ in range(Lc)]
+        # the final LayerNorm, head, CE and the head's whole backward in one workgroup (csrc/vit_head.hip)
+        self.fused_head = (bool(model.use_layernorm) and not self.bn and K.vit_head_ok(B, D, self.Kc) and
+                           os.environ.get("PCV_VIT_FUSED_HEAD", "1") != "0")
+        if self.fused_head:   # only the cls rows of the top block's dropout-VJP operand are ever written
+            self.dym[Lc - 1] = torch.zeros(R, D, dtype=bf, device=dev)
         self.dh = [e(R, M, dt=bf) for _ in range(Lc)]
         # LayerNorm fused into the residual-stream GEMM epilogues (pcv_gemm_ln) when rows fit one tile
         self.fuse_ln = bool(model.use_layernorm) and D <= 128 and D % 8 == 0
@@ -292,7 +297,7 @@ class ViTRunner:
             for i, w in enumerate(self.w):
                 if not (self.fuse_ln and i + 1 < len(self.w)):
                     items.append(("colsum", self.dym[i], w["gb1"]))
-            self.head_bias_grouped = self.Kc % 8 == 0
+            self.head_bias_grouped = self.Kc % 8 == 0 and not self.fused_head   # fused head: its own column sums
             if self.head_bias_grouped:
                 items.append(("colsum", self.dlogits, self.gbh))
             # Column accumulators written by every row tile of a GEMM epilogue (bias and LayerNorm
@@ -423,6 +428,15 @@ class ViTRunner:
                 K.gemm(self.a[i], w["W1"], self.xs[i + 1], bias=w["b1"], res=self.x1s[i], drop_rate=rate,
                        seed=seed, site=site_mlp_out(i))
         xcls = self.xs[-1].view(B, T * D)[:, :D]   # cls rows (row stride T*D)
+        if self.fused_head:
+            g = need_grad
+            K.vit_head(xcls, self.sf, self.cf, self.Wh, self.bh, self.labels, self.yf, self.logits, self.metrics,
+                       grad_scale=1.0 / B, dlogits=self.dlogits if g else None, dlogits_b=self.dlogits_b if g else None,
+                       dx=self.dx.view(B, T * D)[:, :D] if g else None, dscale=self.gsf if g else None,
+                       dbias=self.gcf if g else None, dym=self.dym[L - 1].view(B, T * D)[:, :D] if g else None,
+                       drop_rate=rate, seed=seed, site=site_mlp_out(L - 1), row_stride=T,
+                       dhead_bias=self.gbh if g else None)
+            return self.metrics
         if self.bn:   # statistics over every row, normalise the cls rows only (vit_small.py:121-125)
             K.batchnorm_stats(self.xs[-1], *self.raf, *self.bstf, self.bn_ws, train)
             K.batchnorm_apply(xcls, *self.bstf, self.sf, self.cf, self.yf)
@@ -459,7 +473,38 @@ class ViTRunner:
         B, T, D, H, Dh = self.B, self.T, self.D, self.H, self.Dh
         rate = m.dropout_rate if train else 0.0
         seed = self.seed
-        # head
+        # head (fused head: already done by the forward's vit_head launch, down to the top block's dym)
+        if not self.fused_head:
+            self._head_backward()
+        elif self.wgrad is None:   # no grouped launch: the head weight gradient on its own
+            with self._fork():
+                K.gemm(self.yf, self.dlogits_b, self.gWh, ta=True, beta=1.0)
+        dx_in = self.dx
+        for i in reversed(range(m.num_layers)):
+            w, dym = self.w[i], self.dym[i]
+            # MLP: x2 = x1 + drop(D1(drop(gelu(D0(ln1(x1))))))
+            # (fused path: below the top block, dym and its bias column sum were produced by the
+            # LayerNorm_0 backward epilogue of the block above; the top block's by the fused head)
+            if not (self.fuse_ln and i + 1 < m.num_layers) and not (self.fused_head and i + 1 == m.num_layers):
+                K.dropout_bwd_cast(dx_in, dym, rate, seed, site_mlp_out(i))
+                if self.wgrad is None:
+                    K.colsum(dym, w["gb1"])
+            self._block_backward(i, dx_in, rate, seed)
+            dx_in = self.dx_out[i]
+        K.vit_embed_bwd(dx_in, self.dpatch, self.gcls, self.gpos, None, B, T, D, rate, seed, SITE_EMBED)
+        with self._fork():
+            if self.wgrad is None:
+                K.colsum(self.dpatch, self.gbconv)
+            if self.wgrad is None:
+                K.gemm(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
+        if self.wgrad is not None:
+            self.wgrad()
+        if self.side is not None:
+            torch.cuda.current_stream().wait_stream(self.side)
+
+    def _head_backward(self):
+        m = self.m
+        B, T, D = self.B, self.T, self.D
         K.dropout_bwd_cast(self.dlogits, self.dlogits_b) if self.Kc % 4 == 0 else self.dlogits_b.copy_(self.dlogits)
         with self._fork():
             if self.wgrad is None:
@@ -476,101 +521,86 @@ class ViTRunner:
             K.layernorm_bwd(self.dyf, xcls, self.sf, *self.stf, None, dxc, None, self.gsf, self.gcf)
         else:
             dxc.copy_(self.dyf)
-        dx_in = self.dx
-        for i in reversed(range(m.num_layers)):
-            w = self.w[i]
-            dym, dh, dqkv = self.dym[i], self.dh[i], self.dqkv[i]
-            dx_mid, dxb_mid, dx_out, dxb_out = self.dx_mid[i], self.dxb_mid[i], self.dx_out[i], self.dxb_out[i]
-            # MLP: x2 = x1 + drop(D1(drop(gelu(D0(ln1(x1))))))
-            # (fused path: below the top block, dym and its bias column sum were produced by the
-            # LayerNorm_0 backward epilogue of the block above)
-            if not (self.fuse_ln and i + 1 < m.num_layers):
-                K.dropout_bwd_cast(dx_in, dym, rate, seed, site_mlp_out(i))
-                if self.wgrad is None:
-                    K.colsum(dym, w["gb1"])
-            with self._fork():
-                if self.wgrad is None:
-                    K.gemm(self.a[i], dym, w["gW1"], ta=True, beta=1.0)
-            gb0, reps = self._acc(("gb0", i), w["gb0"])
-            K.gemm(dym, w["W1"], dh, tb=True, aux=self.h[i], act=K.EPI_GELU_BWD, drop_rate=rate,
-                   seed=seed, site=site_mlp_hidden(i), colsum=gb0 if self.side is None else None, col_reps=reps)
-            with self._fork():
-                if self.side is not None:
-                    K.colsum(dh, w["gb0"])
-                if self.wgrad is None:
-                    K.gemm(self.y1[i], dh, w["gW0"], ta=True, beta=1.0)
-            if self.fuse_ln:   # dgrad + LayerNorm_1 backward + residual + its parameter and bias grads
-                (gs1, reps), (gc1, _), (gbo, _) = (self._acc((k, i), w[k]) for k in ("gs1", "gc1", "gbo"))
-                K.gemm_ln(dh, w["W0"], dx_mid, tb=True, ln_mode=2, res=dx_in, ln_scale=w["s1"], ln_y=dxb_mid,
-                          ln_mean=self.st1[i][0], ln_rstd=self.st1[i][1], ln_x=self.x1s[i], ln_dscale=gs1,
-                          ln_dbias=gc1, colsum=gbo, col_reps=reps)
-            elif self.bn:
-                K.gemm(dh, w["W0"], self.dy_m[i], tb=True)
-                K.batchnorm_bwd(self.dy_m[i], self.x1s[i], *self.bst1[i], w["s1"], dx_in, dx_mid, dxb_mid,
-                                w["gs1"], w["gc1"], self.bn_ws)
-            elif m.use_layernorm:
-                K.gemm(dh, w["W0"], self.dy_m[i], tb=True)
-                K.layernorm_bwd(self.dy_m[i], self.x1s[i], w["s1"], *self.st1[i], dx_in, dx_mid, dxb_mid,
-                                None, None)
-                with self._fork():
-                    K.layernorm_param_grad(self.dy_m[i], self.x1s[i], *self.st1[i], w["gs1"], w["gc1"])
-            else:
-                K.gemm(dh, w["W0"], dx_mid, tb=True, res=dx_in)
-                K.dropout_bwd_cast(dx_mid, dxb_mid)
-            # attention: x1 = x + out(attn(qkv(ln0(x))))
-            with self._fork():
-                if self.wgrad is None:
-                    K.gemm(self.o[i], dxb_mid, w["gWo"], ta=True, beta=1.0)
-                if not self.fuse_ln:
-                    K.colsum(dx_mid, w["gbo"])
-            if self.short_attn:
-                # dO = dy Wo^T; the short backward forms delta = <dO, O_hi + O_lo> in its prologue
-                K.gemm(dxb_mid, w["Wo"], self.do, tb=True)
-                K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
-                           causal=False, drop_rate=rate, mask=self._mask(i), o_lo=self.o_lo[i])
-            else:
-                # dO = dy Wo^T; its epilogue also forms the attention-backward row constant delta
-                K.gemm(dxb_mid, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H))
-                K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
-                           causal=False, drop_rate=rate, mask=self._mask(i), delta_ready=True)
-            with self._fork():
-                if self.wgrad is None:
-                    K.gemm(self.y0[i], dqkv, w["gWqkv"], ta=True, beta=1.0)
-                if self.wgrad is None:
-                    K.colsum(dqkv, w["gbqkv"])
-            if self.fuse_ln:   # + the dropout backward / bias column sum of the block below's MLP output
-                below = i > 0
-                (gs0, reps), (gc0, _) = (self._acc((k, i), w[k]) for k in ("gs0", "gc0"))
-                gb1 = self._acc(("gb1", i - 1), self.w[i - 1]["gb1"])[0] if below else None
-                K.gemm_ln(dqkv, w["Wqkv"], dx_out, tb=True, ln_mode=2, res=dx_mid, ln_scale=w["s0"],
-                          ln_y=self.dym[i - 1] if below else None, drop_rate=rate if below else 0.0, seed=seed,
-                          site=site_mlp_out(i - 1) if below else 0, ln_mean=self.st0[i][0],
-                          ln_rstd=self.st0[i][1], ln_x=self.xs[i], ln_dscale=gs0, ln_dbias=gc0,
-                          colsum=gb1, col_reps=reps)
-            elif self.bn:
-                K.gemm(dqkv, w["Wqkv"], self.dy_a[i], tb=True)
-                K.batchnorm_bwd(self.dy_a[i], self.xs[i], *self.bst0[i], w["s0"], dx_mid, dx_out, dxb_out,
-                                w["gs0"], w["gc0"], self.bn_ws)
-            elif m.use_layernorm:
-                K.gemm(dqkv, w["Wqkv"], self.dy_a[i], tb=True)
-                K.layernorm_bwd(self.dy_a[i], self.xs[i], w["s0"], *self.st0[i], dx_mid, dx_out, dxb_out,
-                                None, None)
-                with self._fork():
-                    K.layernorm_param_grad(self.dy_a[i], self.xs[i], *self.st0[i], w["gs0"], w["gc0"])
-            else:
-                K.gemm(dqkv, w["Wqkv"], dx_out, tb=True, res=dx_mid)
-                K.dropout_bwd_cast(dx_out, dxb_out)
-            dx_in = dx_out
-        K.vit_embed_bwd(dx_in, self.dpatch, self.gcls, self.gpos, None, B, T, D, rate, seed, SITE_EMBED)
+
+    def _block_backward(self, i, dx_in, rate, seed):
+        """One encoder block's backward below its MLP-output dropout VJP (dym already formed)."""
+        m = self.m
+        B, T, D, H, Dh = self.B, self.T, self.D, self.H, self.Dh
+        w = self.w[i]
+        dym, dh, dqkv = self.dym[i], self.dh[i], self.dqkv[i]
+        dx_mid, dxb_mid, dx_out, dxb_out = self.dx_mid[i], self.dxb_mid[i], self.dx_out[i], self.dxb_out[i]
         with self._fork():
             if self.wgrad is None:
-                K.colsum(self.dpatch, self.gbconv)
+                K.gemm(self.a[i], dym, w["gW1"], ta=True, beta=1.0)
+        gb0, reps = self._acc(("gb0", i), w["gb0"])
+        K.gemm(dym, w["W1"], dh, tb=True, aux=self.h[i], act=K.EPI_GELU_BWD, drop_rate=rate,
+               seed=seed, site=site_mlp_hidden(i), colsum=gb0 if self.side is None else None, col_reps=reps)
+        with self._fork():
+            if self.side is not None:
+                K.colsum(dh, w["gb0"])
             if self.wgrad is None:
-                K.gemm(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
-        if self.wgrad is not None:
-            self.wgrad()
-        if self.side is not None:
-            torch.cuda.current_stream().wait_stream(self.side)
+                K.gemm(self.y1[i], dh, w["gW0"], ta=True, beta=1.0)
+        if self.fuse_ln:   # dgrad + LayerNorm_1 backward + residual + its parameter and bias grads
+            (gs1, reps), (gc1, _), (gbo, _) = (self._acc((k, i), w[k]) for k in ("gs1", "gc1", "gbo"))
+            K.gemm_ln(dh, w["W0"], dx_mid, tb=True, ln_mode=2, res=dx_in, ln_scale=w["s1"], ln_y=dxb_mid,
+                      ln_mean=self.st1[i][0], ln_rstd=self.st1[i][1], ln_x=self.x1s[i], ln_dscale=gs1,
+                      ln_dbias=gc1, colsum=gbo, col_reps=reps)
+        elif self.bn:
+            K.gemm(dh, w["W0"], self.dy_m[i], tb=True)
+            K.batchnorm_bwd(self.dy_m[i], self.x1s[i], *self.bst1[i], w["s1"], dx_in, dx_mid, dxb_mid,
+                            w["gs1"], w["gc1"], self.bn_ws)
+        elif m.use_layernorm:
+            K.gemm(dh, w["W0"], self.dy_m[i], tb=True)
+            K.layernorm_bwd(self.dy_m[i], self.x1s[i], w["s1"], *self.st1[i], dx_in, dx_mid, dxb_mid,
+                            None, None)
+            with self._fork():
+                K.layernorm_param_grad(self.dy_m[i], self.x1s[i], *self.st1[i], w["gs1"], w["gc1"])
+        else:
+            K.gemm(dh, w["W0"], dx_mid, tb=True, res=dx_in)
+            K.dropout_bwd_cast(dx_mid, dxb_mid)
+        # attention: x1 = x + out(attn(qkv(ln0(x))))
+        with self._fork():
+            if self.wgrad is None:
+                K.gemm(self.o[i], dxb_mid, w["gWo"], ta=True, beta=1.0)
+            if not self.fuse_ln:
+                K.colsum(dx_mid, w["gbo"])
+        if self.short_attn:
+            # dO = dy Wo^T; the short backward forms delta = <dO, O_hi + O_lo> in its prologue
+            K.gemm(dxb_mid, w["Wo"], self.do, tb=True)
+            K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
+                       causal=False, drop_rate=rate, mask=self._mask(i), o_lo=self.o_lo[i])
+        else:
+            # dO = dy Wo^T; its epilogue also forms the attention-backward row constant delta
+            K.gemm(dxb_mid, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H))
+            K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
+                       causal=False, drop_rate=rate, mask=self._mask(i), delta_ready=True)
+        with self._fork():
+            if self.wgrad is None:
+                K.gemm(self.y0[i], dqkv, w["gWqkv"], ta=True, beta=1.0)
+            if self.wgrad is None:
+                K.colsum(dqkv, w["gbqkv"])
+        if self.fuse_ln:   # + the dropout backward / bias column sum of the block below's MLP output
+            below = i > 0
+            (gs0, reps), (gc0, _) = (self._acc((k, i), w[k]) for k in ("gs0", "gc0"))
+            gb1 = self._acc(("gb1", i - 1), self.w[i - 1]["gb1"])[0] if below else None
+            K.gemm_ln(dqkv, w["Wqkv"], dx_out, tb=True, ln_mode=2, res=dx_mid, ln_scale=w["s0"],
+                      ln_y=self.dym[i - 1] if below else None, drop_rate=rate if below else 0.0, seed=seed,
+                      site=site_mlp_out(i - 1) if below else 0, ln_mean=self.st0[i][0],
+                      ln_rstd=self.st0[i][1], ln_x=self.xs[i], ln_dscale=gs0, ln_dbias=gc0,
+                      colsum=gb1, col_reps=reps)
+        elif self.bn:
+            K.gemm(dqkv, w["Wqkv"], self.dy_a[i], tb=True)
+            K.batchnorm_bwd(self.dy_a[i], self.xs[i], *self.bst0[i], w["s0"], dx_mid, dx_out, dxb_out,
+                            w["gs0"], w["gc0"], self.bn_ws)
+        elif m.use_layernorm:
+            K.gemm(dqkv, w["Wqkv"], self.dy_a[i], tb=True)
+            K.layernorm_bwd(self.dy_a[i], self.xs[i], w["s0"], *self.st0[i], dx_mid, dx_out, dxb_out,
+                            None, None)
+            with self._fork():
+                K.layernorm_param_grad(self.dy_a[i], self.xs[i], *self.st0[i], w["gs0"], w["gc0"])
+        else:
+            K.gemm(dqkv, w["Wqkv"], dx_out, tb=True, res=dx_mid)
+            K.dropout_bwd_cast(dx_out, dxb_out)
 
     def flops_per_step(self):
         """Algorithmic fwd+bwd matmul FLOPs (3x forward; SURVEY §8d counting)."""

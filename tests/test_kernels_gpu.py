@@ -5,6 +5,8 @@ import numpy as np
 import pytest
 import torch
 
+from tests.parity_util import rel
+
 pytestmark = pytest.mark.gpu
 
 
@@ -479,3 +481,66 @@ def test_transpose_batch(dev):
     K_.TransposeBatch(pairs, dev)()
     for src, dst in pairs:
         assert torch.equal(dst, src.t())
+
+
+@pytest.mark.parametrize("B,D,Kc,rate", [(64, 128, 200, 0.1), (4, 64, 10, 0.0), (33, 96, 256, 0.3), (1, 32, 1, 0.0)])
+def test_vit_head_fused(dev, B, D, Kc, rate):
+    """csrc/vit_head.hip vs torch fp32 on the same bf16-rounded GEMM operands: LayerNorm of strided cls
+    rows, logits, CE metrics, dlogits, the head bias / LN parameter gradients, dx and the dropout-VJP
+    bf16 rows (dropout bits from oracle.rng at the flat index (b * T) * D + c)."""
+    from oracle import rng
+    from plaincv_amd import kernels as K
+    T = 5
+    g = torch.Generator().manual_seed(B + D + Kc)
+    X = torch.randn(B * T, D, generator=g).to(dev)
+    x = X.view(B, T * D)[:, :D]
+    s, c = (torch.rand(D, generator=g) + 0.5).to(dev), (0.1 * torch.randn(D, generator=g)).to(dev)
+    Kp = (Kc + 7) // 8 * 8
+    Wfull = torch.zeros(D, Kp, dtype=torch.bfloat16, device=dev)
+    Wfull[:, :Kc] = (0.1 * torch.randn(D, Kc, generator=g)).to(torch.bfloat16).to(dev)
+    W = Wfull[:, :Kc]
+    bias = (0.1 * torch.randn(Kc, generator=g)).to(dev)
+    labels = torch.randint(0, Kc, (B,), generator=g, dtype=torch.int32).to(dev)
+    yf = torch.empty(B, D, dtype=torch.bfloat16, device=dev)
+    logits = torch.empty(B, Kp, device=dev)[:, :Kc]
+    met = torch.empty(2, device=dev)
+    dl = torch.empty(B, Kp, device=dev)[:, :Kc]
+    dlb = torch.zeros(B, Kp, dtype=torch.bfloat16, device=dev)[:, :Kc]
+    DX = torch.zeros(B * T, D, device=dev)
+    DYM = torch.zeros(B * T, D, dtype=torch.bfloat16, device=dev)
+    gs, gc, gb = torch.full((D,), 0.5, device=dev), torch.full((D,), -0.25, device=dev), torch.full((Kc,), 1.0, device=dev)
+    seed = torch.tensor([99], dtype=torch.int32, device=dev)
+    K.vit_head(x, s, c, W, bias, labels, yf, logits, met, grad_scale=1.0 / B, dlogits=dl, dlogits_b=dlb,
+               dx=DX.view(B, T * D)[:, :D], dscale=gs, dbias=gc, dym=DYM.view(B, T * D)[:, :D], drop_rate=rate,
+               seed=seed, site=13, row_stride=T, dhead_bias=gb)
+    torch.cuda.synchronize()
+    # torch reference with the same bf16 operand rounding
+    xr = x.clone().requires_grad_(True)
+    sr, cr = s.clone().requires_grad_(True), c.clone().requires_grad_(True)
+    mu = xr.mean(-1, keepdim=True)
+    var = ((xr * xr).mean(-1, keepdim=True) - mu * mu).clamp(min=0)
+    y = (xr - mu) * torch.rsqrt(var + 1e-6) * sr + cr
+    yb = y.to(torch.bfloat16).float()
+    z = yb @ W.float() + bias
+    assert rel(logits, z.detach()) < 1e-5
+    assert rel(yf.float(), y.detach()) < 4e-3                # bf16 rounding of the LN output
+    lse = torch.logsumexp(z, -1)
+    loss = (lse - z.gather(1, labels.long()[:, None])[:, 0]).mean()
+    acc = (z.argmax(-1) == labels.long()).float().mean()
+    assert abs(met[0].item() - loss.item()) < 1e-5 and abs(met[1].item() - acc.item()) < 1e-6
+    d_ref = (torch.softmax(z, -1) - torch.nn.functional.one_hot(labels.long(), Kc).float()) / B
+    assert rel(dl, d_ref.detach()) < 1e-5
+    assert rel(gb - 1.0, d_ref.detach().sum(0)) < 1e-5
+    dy = dlb.float() @ W.float().t()                         # the bf16 dlogits operand, as the GEMM
+    gx, gsr, gcr = torch.autograd.grad(y, (xr, sr, cr), dy)
+    got_dx = DX.view(B, T * D)[:, :D]
+    assert rel(got_dx, gx) < 1e-4
+    assert rel(gs - 0.5, gsr) < 1e-4 and rel(gc + 0.25, gcr) < 1e-4
+    keep = torch.ones(B, D, dtype=torch.bool)
+    if rate > 0:
+        km = rng.keep_mask(99, 13, (B * T, D), rate)
+        keep = torch.from_numpy(km).view(B, T * D)[:, :D]
+    want = torch.where(keep.to(dev), gx / (1 - rate), torch.zeros((), device=dev)).to(torch.bfloat16).float()
+    assert rel(DYM.view(B, T * D)[:, :D].float(), want) < 4e-3
+    others = DYM.view(B, T, D)[:, 1:]
+    assert (others == 0).all()
