@@ -42,6 +42,7 @@ from utils import Config  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+F32_PEAK_TFLOPS = 157.3     # MI355X fp32 MFMA (= vector peak)
 HBM_PEAK_GBS = 8000.0
 
 # config/config_vit.yaml + BASELINE.json configs[1] overrides
@@ -49,14 +50,16 @@ VIT_C2 = dict(dataset="tiny_imagenet_synthetic", batch_size=64, image_size=64, n
               model="vit_small", vit_patch_size=4, vit_hidden_size=128, vit_mlp_dim=256, vit_layers=4, vit_heads=4,
               vit_dropout=0.1, vit_use_layernorm=True, optim="muon", lr=0.001, weight_decay=0.01, beta1=0.9,
               beta2=0.9, muon_beta=0.95, muon_ns_steps=5, muon_ns_coeffs=[3.4445, -4.7750, 2.0315],
-              muon_nesterov=True, eigen_tracking_enabled=False, seed=0)
+              muon_nesterov=True, eigen_tracking_enabled=False, seed=0, vit_dtype="bfloat16")
 
 
 # BASELINE.json configs[3]: the same ViT/TI-synthetic workload with SOAP or Shampoo
 # (exp/run_soap_vit_small/config.yaml: b1 .9, b2 .9, eps 1e-8, wd .01, precondition_frequency 10;
 # Shampoo factory.py:657-673 defaults: eps 1e-4, exponent .25, adam b1 .9 / b2 cfg, adam_eps 1e-8)
-VIT_C4 = {"soap": dict(VIT_C2, optim="soap", eps=1e-8, precondition_frequency=10),
-          "shampoo": dict(VIT_C2, optim="shampoo", eps=1e-4, shampoo_exponent=0.25, adam_eps=1e-8)}
+# configs[3] names no bf16, so it runs in the reference ViT's own precision: fp32 (models/vit_f32.py)
+VIT_C4 = {"soap": dict(VIT_C2, optim="soap", eps=1e-8, precondition_frequency=10, vit_dtype="float32"),
+          "shampoo": dict(VIT_C2, optim="shampoo", eps=1e-4, shampoo_exponent=0.25, adam_eps=1e-8,
+                          vit_dtype="float32")}
 WORKLOAD_NAMES = {"vit_c2": "vit_small_tinyimagenet_muon (BASELINE configs[1])",
                   "vit_c4_soap": "vit_small_tinyimagenet_soap (BASELINE configs[3] optimizer)",
                   "vit_c4_shampoo": "vit_small_tinyimagenet_shampoo (BASELINE configs[3] optimizer)"}
@@ -66,7 +69,7 @@ def vit_model(cfg):
     return VisionTransformer(num_classes=cfg.num_classes, patch_size=cfg.vit_patch_size,
                              hidden_size=cfg.vit_hidden_size, mlp_dim=cfg.vit_mlp_dim, num_layers=cfg.vit_layers,
                              num_heads=cfg.vit_heads, dropout_rate=cfg.vit_dropout,
-                             use_layernorm=cfg.vit_use_layernorm)
+                             use_layernorm=cfg.vit_use_layernorm, dtype=cfg.get("vit_dtype", "float32"))
 
 
 def cpu_threads():
@@ -166,6 +169,22 @@ def vit_roofline(state, image_shape):
             "bytes_per_launch": [b1, b2]}
 
 
+def vit_roofline_f32(state, image_shape):
+    """fp32 ViT path: the weight-gradient launch (every dW = X^T dY of the step, K = B*T rows, one
+    grouped exact-fp32 MFMA launch) -- the largest single launch of the fp32 step -- against the
+    fp32 MFMA peak; FLOPs = 2 K sum(M N) over its jobs, timed live on its stream."""
+    r = state.runner_for(image_shape)
+    t = timed_kernel(lambda: r.g_wgrad.run())
+    flops = 0
+    for j in r.g_wgrad.jobs:
+        flops += 2 * j["M"] * j["N"] * j["K"]
+    ach = flops / t / 1e12
+    return {"kernel": "gemm_f32_grouped (all weight gradients of the fp32 step, one launch)", "bound": "mfma",
+            "achieved": round(ach, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / F32_PEAK_TFLOPS, 4), "traffic": None, "launch_us": round(t * 1e6, 2),
+            "flops_per_launch": flops}
+
+
 def cpu_baseline_vit(cfg, seconds=12.0):
     """oracle/ (PyTorch CPU fp32 restatement) timed on this host: the same
     workload (B=64 TI-shaped, Muon), bounded to ~`seconds` of CPU work."""
@@ -258,14 +277,15 @@ def bench_vit(args):
         sps = args.steps / dt
         out = {"metric": METRIC, "value": round(world * B * sps, 2), "unit": "images/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
-               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "f32" if cfg.vit_dtype == "float32" else "bf16",
                "data": "synthetic (uint8 images U[0,255], labels U[0,200), seeded, resident in HBM)",
                "config": {"workload": WORKLOAD_NAMES[args.workload], "global_batch": world * B,
                           "per_gpu_batch": B, "image": [64, 64, 3], "classes": 200, "tokens": 257,
                           "optimizer": cfg.optim, "parallelism": f"dp{world}"},
                "steps_per_sec": round(sps, 3), "tflops_per_gpu": round(flops * sps / 1e12, 3),
                "final_loss": round(loss, 4)}
-        out["roofline"] = vit_roofline(state, shape)
+        out["roofline"] = vit_roofline_f32(state, shape) if cfg.vit_dtype == "float32" else vit_roofline(state, shape)
         if world > 1:
             out["grad_allreduce"] = None   # filled below (collective: every rank takes part)
         if world == 1 and not args.no_cpu_baseline:

@@ -216,6 +216,28 @@ int pcv_embed_fwd(const int* ids, const void* table, int64_t ldt, void* out, int
 int pcv_embed_bwd(const int* ids, const void* dx, int64_t lddx, float* dtable, int64_t ldt, int64_t R,
                   int D, int V, void* stream);
 
+/* fp32 ViT path (VisionTransformer(dtype="float32"): the reference ViT's own precision; every
+ * contraction on the exact-fp32 MFMA via pcv_gemm_f32_grouped).  patchify: uint8 NHWC -> fp32/255
+ * patches (models/vit_small.py:78-95); LayerNorm with fp32 output; the Dense epilogue out =
+ * dropout(act(x + bias)) + res_scale * res (act 1 = tanh-GELU, aux = pre-activation) and its VJP;
+ * attention softmax over materialised scores S [rows = B*H*T][T] -> P and the weight-dropped Pd
+ * (packed keep bits of pcv_attn_drop_mask), its VJP dS = P o (dP - rowsum(dP o P)) in place of dPd;
+ * the embedding VJP with an fp32 patch gradient.  Dropout index = flat output index, as everywhere. */
+int pcv_vit_patchify_f32(const uint8_t* img, float* out, int B, int H, int W, int C, int patch, void* stream);
+int pcv_layernorm_fwd_f32(const float* x, int64_t ldx, const float* scale, const float* bias, float* y, int64_t ldy,
+                          float* mean, float* rstd, int64_t R, int D, float eps, void* stream);
+int pcv_f32_epilogue(const float* x, int64_t ldx, const float* bias, const float* res, int64_t ldr, float res_scale,
+                     float* aux, int64_t ldaux, float* out, int64_t ldo, int64_t R, int N, int act, float rate,
+                     const uint32_t* seed, uint32_t site, void* stream);
+int pcv_f32_epilogue_bwd(const float* dy, int64_t lddy, const float* aux, int64_t ldaux, float* dx, int64_t lddx,
+                         int64_t R, int N, int act, float rate, const uint32_t* seed, uint32_t site, void* stream);
+int pcv_attn_softmax_f32(const float* S, float* P, float* Pd, int64_t rows, int T, const uint16_t* mask, float rate,
+                         void* stream);
+int pcv_attn_softmax_bwd_f32(const float* P, float* dPd, int64_t rows, int T, const uint16_t* mask, float rate,
+                             void* stream);
+int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls, float* dpos, int B, int T, int D, float rate,
+                          const uint32_t* seed, uint32_t site, void* stream);
+
 /* The ViT classifier head in ONE workgroup (models/vit_small.py:123-127, flax_engine.py:13-22):
  * y = LayerNorm(x cls rows) -> yf (bf16), logits = y W + bias (fp32, [B][ldl]), metrics = [mean CE,
  * mean accuracy]; with dlogits != NULL also dlogits = (softmax - onehot) * grad_scale (fp32 + bf16),

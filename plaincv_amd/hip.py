@@ -61,6 +61,13 @@ SIGNATURES = {
     "pcv_zero_seed": [P, I64, P, P],
     "pcv_embed_fwd": [P, P, I64, P, I64, I64, I32, I32, P, P],
     "pcv_embed_bwd": [P, P, I64, P, I64, I64, I32, I32, P],
+    "pcv_vit_patchify_f32": [P, P, I32, I32, I32, I32, I32, P],
+    "pcv_layernorm_fwd_f32": [P, I64, P, P, P, I64, P, P, I64, I32, F32, P],
+    "pcv_f32_epilogue": [P, I64, P, P, I64, F32, P, I64, P, I64, I64, I32, I32, F32, P, U32, P],
+    "pcv_f32_epilogue_bwd": [P, I64, P, I64, P, I64, I64, I32, I32, F32, P, U32, P],
+    "pcv_attn_softmax_f32": [P, P, P, I64, I32, P, F32, P],
+    "pcv_attn_softmax_bwd_f32": [P, P, I64, I32, P, F32, P],
+    "pcv_vit_embed_bwd_f32": [P, P, P, P, I32, I32, I32, F32, P, U32, P],
     "pcv_vit_head_ok": [I32, I32, I32],
     "pcv_vit_head": [P, I64, P, P, F32, P, I64, P, P, I32, I32, I32, P, I64, P, I64, P, F32, P, P, I64, P, I64, P, P,
                      P, P, I64, F32, P, U32, I64, P],

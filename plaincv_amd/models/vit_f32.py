@@ -1,0 +1,301 @@
+"""fp32 ViT executor (VisionTransformer(dtype="float32")): the reference's own precision.
+
+The reference ViT computes in fp32 (models/vit_small.py:95; BASELINE configs[0] and [3] name no
+bf16).  Same forward / backward as ``ViTRunner`` (bf16 MFMA operands), but every contraction runs on
+the exact-fp32 MFMA through the grouped fp32 GEMM of csrc/precond.hip (``GemmF32``: each call site
+is one pre-planned launch; the per-(batch, head) attention products are jobs of one launch), with
+the elementwise epilogues, LayerNorm, attention softmax / weight dropout over materialised
+[B*H, T, T] scores and the embedding VJP in csrc/vit_f32.hip.  Dropout bits and sites are those
+of the bf16 path (shared with oracle/rng.py), so the two runners draw identical masks.
+Supported: LayerNorm or no norm (use_batchnorm is bf16-path only).
+"""
+import math
+
+import torch
+
+from .. import hip
+from .. import kernels as K
+from ..hip import ptr, stream_ptr
+from ..optim.precond import GemmF32
+
+SITE_EMBED = 1
+
+
+def site_attn(i):
+    return 16 + 4 * i
+
+
+def site_mlp_hidden(i):
+    return 16 + 4 * i + 1
+
+
+def site_mlp_out(i):
+    return 16 + 4 * i + 2
+
+
+def _epi(x, out, bias=None, res=None, aux=None, act=0, rate=0.0, seed=None, site=0, res_scale=1.0):
+    R, N = out.shape
+    hip.call("pcv_f32_epilogue", ptr(x), x.stride(0), ptr(bias), ptr(res), res.stride(0) if res is not None else 0,
+             float(res_scale), ptr(aux), aux.stride(0) if aux is not None else 0, ptr(out), out.stride(0), R, N,
+             int(act), float(rate), ptr(seed), int(site), stream_ptr())
+
+
+def _epi_bwd(dy, dx, aux=None, act=0, rate=0.0, seed=None, site=0):
+    R, N = dx.shape
+    hip.call("pcv_f32_epilogue_bwd", ptr(dy), dy.stride(0), ptr(aux), aux.stride(0) if aux is not None else 0, ptr(dx),
+             dx.stride(0), R, N, int(act), float(rate), ptr(seed), int(site), stream_ptr())
+
+
+def _gemm(a, b, c, **kw):
+    return GemmF32().add(a, b, c, **kw)
+
+
+class ViTRunnerF32:
+    """Fixed-shape fp32 forward/backward executor (graph-capturable, no allocation after init)."""
+
+    def __init__(self, model, store, image_shape, device):
+        if model.use_batchnorm:
+            raise NotImplementedError("the fp32 ViT path supports LayerNorm or no norm (use_batchnorm: bf16 path)")
+        self.m, self.s = model, store
+        B, Hh, Ww, C = image_shape
+        ps = model.patch_size
+        self.B, self.C, self.Hh, self.Ww = B, C, Hh, Ww
+        self.hw = (Hh // ps) * (Ww // ps)
+        self.T = T = self.hw + 1
+        D, M, H = model.hidden_size, model.mlp_dim, model.num_heads
+        self.D, self.M, self.H, self.Dh = D, M, H, D // H
+        self.Kp, self.Kc = ps * ps * C, model.num_classes
+        self.R = R = B * T
+        L = model.num_layers
+        dev = torch.device(device)
+        z = lambda *sh: torch.zeros(*sh, dtype=torch.float32, device=dev)  # noqa: E731
+        BH = B * H
+        self.patches, self.patch_out = z(B * self.hw, self.Kp), z(B * self.hw, D)
+        self.xs = [z(R, D) for _ in range(L + 1)]
+        self.x1s = [z(R, D) for _ in range(L)]
+        ln = model.use_layernorm
+        self.y0 = [z(R, D) for _ in range(L)] if ln else self.xs[:L]
+        self.y1 = [z(R, D) for _ in range(L)] if ln else self.x1s
+        self.st0 = [(z(R), z(R)) for _ in range(L)]
+        self.st1 = [(z(R), z(R)) for _ in range(L)]
+        self.qkv = [z(R, 3 * D) for _ in range(L)]
+        self.S = z(BH * T, T)                               # scores (scratch), later dPd / dS
+        self.P = [z(BH * T, T) for _ in range(L)]
+        self.Pd = [z(BH * T, T) for _ in range(L)] if model.dropout_rate > 0 else self.P
+        self.o = [z(R, D) for _ in range(L)]
+        self.pre = [z(R, M) for _ in range(L)]
+        self.a = [z(R, M) for _ in range(L)]
+        self.tD, self.tM = z(R, D), z(R, M)
+        self.yf, self.stf = z(B, D), (z(B), z(B))
+        self.logits, self.dlogits = z(B, self.Kc), z(B, self.Kc)
+        self.row_loss, self.row_correct = z(B), z(B)
+        self.metrics = z(2)
+        self.labels = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.seed = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.mask_words = K.attn_mask_words(T)
+        self.attn_mask = torch.zeros(L * self.mask_words, dtype=torch.int16, device=dev)
+        # backward
+        self.dx = z(R, D)                                   # only the cls rows are written
+        self.dyf = z(B, D)
+        self.dmo, self.da = z(R, D), z(R, M)
+        self.dy1, self.dx1, self.dO = z(R, D), z(R, D), z(R, D)
+        self.dqkv, self.dy0 = z(R, 3 * D), z(R, D)
+        self.dxo = [z(R, D) for _ in range(L)]
+        self.dpatch = z(B * self.hw, D)
+        self._views()
+        self._plan()
+
+    def _views(self):
+        s, m = self.s, self.m
+        D, H, Dh = self.D, self.H, self.Dh
+        P, G = s.params, s.grads
+        self.w = []
+        for i in range(m.num_layers):
+            pre, a = f"EncoderBlock_{i}", f"EncoderBlock_{i}/SelfAttention_0"
+            d = {"Wqkv": s.group_view(s.flat, f"{a}/qkv_kernel"), "bqkv": s.group_view(s.flat, f"{a}/qkv_bias"),
+                 "gWqkv": s.group_view(s.grad_flat, f"{a}/qkv_kernel"),
+                 "gbqkv": s.group_view(s.grad_flat, f"{a}/qkv_bias"),
+                 "Wo": P[f"{a}/out/kernel"].reshape(H * Dh, D), "bo": P[f"{a}/out/bias"],
+                 "gWo": G[f"{a}/out/kernel"].reshape(H * Dh, D), "gbo": G[f"{a}/out/bias"]}
+            for j, n in ((0, "Dense_0"), (1, "Dense_1")):
+                d[f"W{j}"], d[f"b{j}"] = P[f"{pre}/MlpBlock_0/{n}/kernel"], P[f"{pre}/MlpBlock_0/{n}/bias"]
+                d[f"gW{j}"], d[f"gb{j}"] = G[f"{pre}/MlpBlock_0/{n}/kernel"], G[f"{pre}/MlpBlock_0/{n}/bias"]
+            if m.use_layernorm:
+                for j in (0, 1):
+                    d[f"s{j}"], d[f"c{j}"] = P[f"{pre}/LayerNorm_{j}/scale"], P[f"{pre}/LayerNorm_{j}/bias"]
+                    d[f"gs{j}"], d[f"gc{j}"] = G[f"{pre}/LayerNorm_{j}/scale"], G[f"{pre}/LayerNorm_{j}/bias"]
+            self.w.append(d)
+        self.Wconv, self.gWconv = P["Conv_0/kernel"].reshape(self.Kp, D), G["Conv_0/kernel"].reshape(self.Kp, D)
+        self.bconv, self.gbconv = P["Conv_0/bias"], G["Conv_0/bias"]
+        self.cls, self.gcls = P["cls_token"].reshape(D), G["cls_token"].reshape(D)
+        self.pos, self.gpos = P["pos_embedding"].reshape(self.T, D), G["pos_embedding"].reshape(self.T, D)
+        if m.use_layernorm:
+            self.sf, self.cf = P["LayerNorm_0/scale"], P["LayerNorm_0/bias"]
+            self.gsf, self.gcf = G["LayerNorm_0/scale"], G["LayerNorm_0/bias"]
+        self.Wh, self.bh, self.gWh, self.gbh = P["Dense_0/kernel"], P["Dense_0/bias"], G["Dense_0/kernel"], G["Dense_0/bias"]
+
+    def _heads(self, t, col0, i_b, i_h):
+        """[T, Dh] view of head i_h of batch i_b in the column block starting at col0 of t [R, *]."""
+        T, Dh = self.T, self.Dh
+        return t[i_b * T:(i_b + 1) * T, col0 + i_h * Dh: col0 + (i_h + 1) * Dh]
+
+    def _plan(self):
+        """Every fp32 GEMM of the step as a finalized grouped launch (fixed pointers)."""
+        dev = self.s.device
+        B, H, T, D = self.B, self.H, self.T, self.D
+        sc = 1.0 / math.sqrt(self.Dh)
+        f = lambda g: g.finalize(dev)  # noqa: E731
+        self.g_patch = f(_gemm(self.patches, self.Wconv, self.patch_out))
+        self.g_head = f(_gemm(self.yf, self.Wh, self.logits))
+        self.g_head_d = f(_gemm(self.dlogits, self.Wh, self.dyf, tb=True))
+        L = self.m.num_layers
+        # per-layer activation gradients (operands of the weight gradients, run once at the end)
+        self.dmo_l = [torch.zeros_like(self.dmo) for _ in range(L)]
+        self.da_l = [torch.zeros_like(self.da) for _ in range(L)]
+        self.dx1_l = [torch.zeros_like(self.dx1) for _ in range(L)]
+        self.dqkv_l = [torch.zeros_like(self.dqkv) for _ in range(L)]
+        self.gf, self.gb = [], []
+        for i in range(L):
+            w = self.w[i]
+            qkv, Pd, o, dqkv = self.qkv[i], self.Pd[i], self.o[i], self.dqkv_l[i]
+            s_g, pv, dpv, dqk = GemmF32(), GemmF32(), GemmF32(), GemmF32()
+            for b in range(B):
+                for h in range(H):
+                    q, k, v = (self._heads(qkv, c0, b, h) for c0 in (0, D, 2 * D))
+                    dq, dk, dv = (self._heads(dqkv, c0, b, h) for c0 in (0, D, 2 * D))
+                    dob = self._heads(self.dO, 0, b, h)
+                    rows = slice((b * H + h) * T, (b * H + h + 1) * T)
+                    s_g.add(q, k, self.S[rows], tb=True, alpha=sc)          # S = scale Q K^T
+                    pv.add(Pd[rows], v, self._heads(o, 0, b, h))             # O = Pd V
+                    dpv.add(dob, v, self.S[rows], tb=True)                   # dPd = dO V^T
+                    dpv.add(Pd[rows], dob, dv, ta=True)                      # dV = Pd^T dO
+                    dqk.add(self.S[rows], k, dq, alpha=sc)                   # dQ = scale dS K
+                    dqk.add(self.S[rows], q, dk, ta=True, alpha=sc)          # dK = scale dS^T Q
+            self.gf.append(dict(qkv=f(_gemm(self.y0[i], w["Wqkv"], qkv)), s=f(s_g), pv=f(pv),
+                                out=f(_gemm(o, w["Wo"], self.tD)), fc1=f(_gemm(self.y1[i], w["W0"], self.tM)),
+                                fc2=f(_gemm(self.a[i], w["W1"], self.tD))))
+            self.gb.append(dict(fc2_d=f(_gemm(self.dmo_l[i], w["W1"], self.da, tb=True)),
+                                fc1_d=f(_gemm(self.da_l[i], w["W0"], self.dy1, tb=True)),
+                                out_d=f(_gemm(self.dx1_l[i], w["Wo"], self.dO, tb=True)), dpv=f(dpv), dqk=f(dqk),
+                                qkv_d=f(_gemm(dqkv, w["Wqkv"], self.dy0, tb=True))))
+        # every weight gradient (K = B*T rows) in one grouped launch at the end of backward
+        wg = GemmF32()
+        wg.add(self.yf, self.dlogits, self.gWh, ta=True, beta=1.0)
+        wg.add(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
+        for i in range(L):
+            w = self.w[i]
+            wg.add(self.a[i], self.dmo_l[i], w["gW1"], ta=True, beta=1.0)
+            wg.add(self.y1[i], self.da_l[i], w["gW0"], ta=True, beta=1.0)
+            wg.add(self.o[i], self.dx1_l[i], w["gWo"], ta=True, beta=1.0)
+            wg.add(self.y0[i], self.dqkv_l[i], w["gWqkv"], ta=True, beta=1.0)
+        self.g_wgrad = f(wg)
+
+    def _mask(self, i):
+        w = self.mask_words
+        return self.attn_mask[i * w:(i + 1) * w]
+
+    # ---------------------------------------------------------- forward
+    def forward(self, images, labels=None, train=True, need_grad=True):
+        m = self.m
+        B, T, D = self.B, self.T, self.D
+        rate = m.dropout_rate if train else 0.0
+        seed = self.seed
+        if labels is not None:
+            self.labels.copy_(labels, non_blocking=True)
+        hip.call("pcv_vit_patchify_f32", ptr(images), ptr(self.patches), B, self.Hh, self.Ww, self.C, m.patch_size,
+                 stream_ptr())
+        self.g_patch.run()
+        _epi(self.patch_out, self.patch_out, bias=self.bconv)
+        K.vit_embed_fwd(self.patch_out, self.cls, self.pos, self.xs[0], None, B, T, D, rate, seed, SITE_EMBED)
+        if rate > 0.0:
+            K.attn_drop_mask(seed, site_attn(0), T, rate, self.attn_mask, layers=m.num_layers,
+                             site_stride=site_attn(1) - site_attn(0))
+        for i in range(m.num_layers):
+            w, x = self.w[i], self.xs[i]
+            if m.use_layernorm:
+                self._ln(x, w["s0"], w["c0"], self.y0[i], self.st0[i])
+            g = self.gf[i]
+            g["qkv"].run()
+            _epi(self.qkv[i], self.qkv[i], bias=w["bqkv"])
+            g["s"].run()
+            hip.call("pcv_attn_softmax_f32", ptr(self.S), ptr(self.P[i]), ptr(self.Pd[i]),
+                     self.S.shape[0], T, ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
+            g["pv"].run()
+            g["out"].run()
+            _epi(self.tD, self.x1s[i], bias=w["bo"], res=x)
+            if m.use_layernorm:
+                self._ln(self.x1s[i], w["s1"], w["c1"], self.y1[i], self.st1[i])
+            g["fc1"].run()
+            _epi(self.tM, self.a[i], bias=w["b0"], aux=self.pre[i], act=1, rate=rate, seed=seed,
+                 site=site_mlp_hidden(i))
+            g["fc2"].run()
+            _epi(self.tD, self.xs[i + 1], bias=w["b1"], res=self.x1s[i], rate=rate, seed=seed, site=site_mlp_out(i))
+        xcls = self.xs[-1].view(B, T * D)[:, :D]
+        if m.use_layernorm:
+            self._ln(xcls, self.sf, self.cf, self.yf, self.stf)
+        else:
+            _epi(xcls, self.yf)
+        self.g_head.run()
+        _epi(self.logits, self.logits, bias=self.bh)
+        K.xent(self.logits, self.labels, self.row_loss, self.row_correct, self.dlogits if need_grad else None,
+               grad_scale=1.0 / B)
+        K.mean2(self.row_loss, self.row_correct, B, 1.0 / B, self.metrics)
+        return self.metrics
+
+    def _ln(self, x, s, c, y, st):
+        R, D = x.shape
+        hip.call("pcv_layernorm_fwd_f32", ptr(x), x.stride(0), ptr(s), ptr(c), ptr(y), y.stride(0), ptr(st[0]),
+                 ptr(st[1]), R, D, 1e-6, stream_ptr())
+
+    # --------------------------------------------------------- backward
+    def backward(self, train=True):
+        m = self.m
+        B, T, D = self.B, self.T, self.D
+        rate = m.dropout_rate if train else 0.0
+        seed = self.seed
+        K.colsum(self.dlogits, self.gbh)
+        self.g_head_d.run()
+        dxc = self.dx.view(B, T * D)[:, :D]
+        xcls = self.xs[-1].view(B, T * D)[:, :D]
+        if m.use_layernorm:
+            K.layernorm_bwd(self.dyf, xcls, self.sf, *self.stf, None, dxc, None, self.gsf, self.gcf)
+        else:
+            _epi(self.dyf, dxc)
+        dx_in = self.dx
+        for i in reversed(range(m.num_layers)):
+            w, g = self.w[i], self.gb[i]
+            dmo, da, dx1, dqkv = self.dmo_l[i], self.da_l[i], self.dx1_l[i], self.dqkv_l[i]
+            _epi_bwd(dx_in, dmo, rate=rate, seed=seed, site=site_mlp_out(i))            # MLP-out dropout VJP
+            K.colsum(dmo, w["gb1"])
+            g["fc2_d"].run()                                                           # self.da = dmo W1^T
+            _epi_bwd(self.da, da, aux=self.pre[i], act=1, rate=rate, seed=seed, site=site_mlp_hidden(i))
+            K.colsum(da, w["gb0"])
+            g["fc1_d"].run()                                                           # self.dy1 = da W0^T
+            if m.use_layernorm:
+                K.layernorm_bwd(self.dy1, self.x1s[i], w["s1"], *self.st1[i], dx_in, dx1, None, w["gs1"], w["gc1"])
+            else:
+                _epi(self.dy1, dx1, res=dx_in)
+            K.colsum(dx1, w["gbo"])
+            g["out_d"].run()                                                           # self.dO = dx1 Wo^T
+            g["dpv"].run()                                                             # dPd -> S, dV
+            hip.call("pcv_attn_softmax_bwd_f32", ptr(self.P[i]), ptr(self.S), self.S.shape[0], T,
+                     ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
+            g["dqk"].run()                                                             # dQ, dK
+            K.colsum(dqkv, w["gbqkv"])
+            g["qkv_d"].run()                                                           # self.dy0 = dqkv Wqkv^T
+            if m.use_layernorm:
+                K.layernorm_bwd(self.dy0, self.xs[i], w["s0"], *self.st0[i], dx1, self.dxo[i], None, w["gs0"],
+                                w["gc0"])
+            else:
+                _epi(self.dy0, self.dxo[i], res=dx1)
+            dx_in = self.dxo[i]
+        hip.call("pcv_vit_embed_bwd_f32", ptr(dx_in), ptr(self.dpatch), ptr(self.gcls), ptr(self.gpos), B, T, D,
+                 float(rate), ptr(seed), SITE_EMBED, stream_ptr())
+        K.colsum(self.dpatch, self.gbconv)
+        self.g_wgrad.run()
+
+    def flops_per_step(self):
+        B, T, D, M, Kc = self.B, self.T, self.D, self.M, self.Kc
+        per_layer = 2 * B * T * D * 3 * D + 2 * B * T * D * D + 2 * 2 * B * T * T * D + 2 * 2 * B * T * D * M
+        fwd = self.m.num_layers * per_layer + 2 * B * self.hw * self.Kp * D + 2 * B * D * Kc
+        return 3 * fwd

@@ -52,9 +52,15 @@ class VisionTransformer:
     mlp_dim, num_layers, num_heads, dropout_rate, use_layernorm, use_batchnorm)."""
 
     def __init__(self, num_classes=10, patch_size=4, hidden_size=128, mlp_dim=256, num_layers=4, num_heads=4,
-                 dropout_rate=0.1, use_layernorm=True, use_batchnorm=False):
+                 dropout_rate=0.1, use_layernorm=True, use_batchnorm=False, dtype="bfloat16"):
+        """dtype (build-only): "bfloat16" -- bf16 MFMA operands, fp32 accumulation / residual stream
+        (BASELINE configs[1]); "float32" -- every contraction in exact fp32, the reference ViT's
+        precision (models/vit_f32.py)."""
         if use_batchnorm and use_layernorm:
             raise ValueError("use_batchnorm and use_layernorm cannot both be True.")
+        if str(dtype) not in ("bfloat16", "float32"):
+            raise ValueError(f"ViT dtype must be 'bfloat16' or 'float32', got {dtype!r}")
+        self.dtype = str(dtype)
         self.num_classes = num_classes
         self.patch_size = patch_size
         self.hidden_size = hidden_size
@@ -149,6 +155,9 @@ class VisionTransformer:
         return out
 
     def bind(self, store, image_shape, device, side_stream=False, grouped_wgrad=True, batch_stats=None):
+        if self.dtype == "float32":
+            from .vit_f32 import ViTRunnerF32
+            return ViTRunnerF32(self, store, image_shape, device)
         return ViTRunner(self, store, image_shape, device, side_stream=side_stream, grouped_wgrad=grouped_wgrad,
                          batch_stats=batch_stats)
 

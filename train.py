@@ -7,7 +7,7 @@ Same flags as the reference (train.py:49-55, utils.py:60-70).  ``model: transfor
 handed to ``train_lm.run`` exactly as the reference does (train.py:132-134).  Config keys as the
 reference (dataset, batch_size, num_epochs, image_size, num_channels, num_classes, seed,
 model in {vit, vit_small, vision_transformer}, vit_patch_size/hidden_size/mlp_dim/layers/heads/
-dropout/use_layernorm/use_batchnorm, optim + its keys, data_root) and the same outputs: the
+dropout/use_layernorm/use_batchnorm/dtype, optim + its keys, data_root) and the same outputs: the
 per-epoch log line {epoch, train_loss, train_accuracy, eval_loss, eval_accuracy, epoch_time}, the
 ``Epoch NNN | ...`` summary line, the experiment dir with config.yaml, and the
 ``{optim}_metrics.csv`` + eval-loss PNG curves at the end (train.py:407-520).  Every epoch gets
@@ -41,11 +41,16 @@ def construct_model(cfg):
         raise ValueError(f"Unknown model: {cfg.model} (the MI355X hot path builds the ViT: "
                          f"{sorted(VIT_NAMES)}; ResNet/MLP are out of scope)")
     g = lambda k, d: getattr(cfg, k, d)  # noqa: E731
+    # vit_dtype: the reference ViT computes in fp32 (models/vit_small.py:95), so that is the CLI
+    # default; "bfloat16" selects the bf16-MFMA runner (BASELINE configs[1]).  BatchNorm runs on
+    # the bf16 runner only.
+    bn = g("vit_use_batchnorm", False)
+    dtype = g("vit_dtype", "bfloat16" if bn else "float32")
     return VisionTransformer(num_classes=num_classes(cfg), patch_size=g("vit_patch_size", 4),
                              hidden_size=g("vit_hidden_size", 128), mlp_dim=g("vit_mlp_dim", 256),
                              num_layers=g("vit_layers", 4), num_heads=g("vit_heads", 4),
                              dropout_rate=g("vit_dropout", 0.1), use_layernorm=g("vit_use_layernorm", True),
-                             use_batchnorm=g("vit_use_batchnorm", False))
+                             use_batchnorm=bn, dtype=dtype)
 
 
 def image_shape(cfg):
