@@ -237,6 +237,27 @@ int pcv_attn_softmax_bwd_f32(const float* P, float* dPd, int64_t rows, int T, co
                              void* stream);
 int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls, float* dpos, int B, int T, int D, float rate,
                           const uint32_t* seed, uint32_t site, void* stream);
+/* Exact-fp32 row-panel GEMM with the Dense epilogue fused (csrc/gemm_f32.hip): C[M][N] =
+ * dropout(act(A[M][K] op(B) + bias)) + res_scale * res, op(B) = B [K][N] (tb = 0) or B^T with B
+ * stored [N][K] (tb = 1); aux = the pre-activation when act = 1 (GELU tanh); dropout index row * N +
+ * col (as pcv_f32_epilogue).  ok: N % 128 == 0, K % 64 == 0, 16-B aligned A / B, lda / ldb % 4 == 0. */
+int pcv_gemm_f32_rows_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb,
+                         int tb);
+int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C, int64_t ldc,
+                      int64_t M, int64_t N, int64_t K, const float* bias, float* aux, int64_t ldaux, const float* res,
+                      int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed, uint32_t site,
+                      void* stream);
+/* Fused fp32 self-attention of one layer (flax MultiHeadDotProductAttention at
+ * models/vit_small.py:41-45, fp32): qkv [B*T][ldqkv] holds q | k | v column blocks of width D = H * 32;
+ * out [B*T][ldo] = softmax(q k^T / sqrt(32)) (weight dropout: packed keep words `mask`, rate) v;
+ * mrow / linv [B*H*T] = each query's row max and 1/sum.  The backward writes dq | dk | dv into
+ * dqkv's column blocks from qkv, out, dout and those stats.  ok: head_dim 32, 1 <= T <= 272. */
+int pcv_attn_fused_f32_ok(int T, int head_dim);
+int pcv_attn_fwd_f32(const float* qkv, int64_t ldqkv, float* out, int64_t ldo, float* mrow, float* linv, int B, int T,
+                     int H, int D, const uint16_t* mask, float rate, void* stream);
+int pcv_attn_bwd_f32(const float* qkv, int64_t ldqkv, const float* o, int64_t ldo, const float* dout, int64_t lddo,
+                     const float* mrow, const float* linv, float* dqkv, int64_t lddqkv, int B, int T, int H, int D,
+                     const uint16_t* mask, float rate, void* stream);
 
 /* The ViT classifier head in ONE workgroup (models/vit_small.py:123-127, flax_engine.py:13-22):
  * y = LayerNorm(x cls rows) -> yf (bf16), logits = y W + bias (fp32, [B][ldl]), metrics = [mean CE,
@@ -331,7 +352,7 @@ int pcv_chunk_size(void);
  *   op(A) = a_mul * A + a_diag * I (likewise B) -- the Newton iteration's T = aI + bM unmaterialised;
  *   conv_in: the job is skipped when *conv_in <= conv_tol; conv_out: atomic max of |C - I|.
  *   record {A, B, C, kscale, R, Cb, alpha_dev, conv_in, conv_out, M, N, K, lda, ldb, ldc, ldr, ldcb,
- *           ta, tb, apow, tiles_n, first_tile, alpha, beta, rscale, a_diag, a_mul, b_diag, b_mul,
+ *           ta, tb, apow, tiles_n, first_tile, ksplit, kchunk, alpha, beta, rscale, a_diag, a_mul, b_diag, b_mul,
  *           conv_tol} (64x64 tiles, first_tile = prefix sum; apow bit 4 marks a float4-aligned job).
  * vec = 1: every job is float4-aligned (16-B bases, ld % 4, M, N, K % 4) -> vector staging. */
 int pcv_f32_job_size(void);

@@ -33,15 +33,18 @@ namespace pcv {
 //   op(A)[m][k] = a_mul * A[m][k] + a_diag * (m == k), op(B) likewise with b_mul / b_diag.
 // conv_in: skip the whole job when *conv_in <= conv_tol (matrix already converged);
 // conv_out: atomic max over the tile of |C - I| (the next iteration's conv_in).
+// ksplit > 1 (split-K, for long-K jobs such as weight gradients with K = B*T): the job's tiles are
+// ksplit x (M/64 x N/64), each summing a kchunk-long slice of K and adding alpha * partial to C
+// with fp32 atomics -- only for C += alpha op(A) op(B) (beta = 1, no R / Cb / conv_out).
 struct F32Job {
   const float* A; const float* B; float* C;
   const float* kscale; const float* R; bf16* Cb; const float* alpha_dev;
   const float* conv_in; float* conv_out;
   int64_t M, N, K, lda, ldb, ldc, ldr, ldcb;
-  int64_t ta, tb, apow, tiles_n, first_tile;
+  int64_t ta, tb, apow, tiles_n, first_tile, ksplit, kchunk;
   double alpha, beta, rscale, a_diag, a_mul, b_diag, b_mul, conv_tol;
 };
-static_assert(sizeof(F32Job) == 30 * 8, "F32Job layout");
+static_assert(sizeof(F32Job) == 32 * 8, "F32Job layout");
 
 constexpr int FG_T = 64, FG_K = 128;
 constexpr int LD_KX = FG_T + 16;    // k-major image [k][x]: fragment reads of 4 k-rows hit 4 bank groups
@@ -118,11 +121,12 @@ struct Stager {
 constexpr int FG_LDS_FLOATS = (FG_T * LD_XK > FG_K * LD_KX ? FG_T * LD_XK : FG_K * LD_KX);
 
 template <bool TA, bool TB, bool VEC>
-__device__ __forceinline__ void f32_tile(const F32Job& jb, int m0, int n0, float* As, float* Bs,
+__device__ __forceinline__ void f32_tile(const F32Job& jb, int m0, int n0, int kbeg, int K, float* As, float* Bs,
                                          f32x4 (&acc)[2][2]) {
+  // sums k in [kbeg, K): K is the job's K, or the end of this tile's split-K slice
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
-  const int M = (int)jb.M, N = (int)jb.N, K = (int)jb.K;
+  const int M = (int)jb.M, N = (int)jb.N;
   Stager<!TA, VEC> sa;     // A row-major [M][K] when !TA
   Stager<TB, VEC> sb;      // B stored [N][K] when TB (row-major along k)
   sa.init(tid, m0, (int)jb.lda);
@@ -132,9 +136,9 @@ __device__ __forceinline__ void f32_tile(const F32Job& jb, int m0, int n0, float
   const float* __restrict__ B = jb.B;
   const float* __restrict__ ksc = jb.kscale;
   float ra[FG_NPER], rb[FG_NPER];
-  sa.load(A, 0, m0, M, K, amul, adiag, ksc, ra);
-  sb.load(B, 0, n0, N, K, bmul, bdiag, nullptr, rb);
-  for (int k0 = 0; k0 < K; k0 += FG_K) {
+  sa.load(A, kbeg, m0, M, K, amul, adiag, ksc, ra);
+  sb.load(B, kbeg, n0, N, K, bmul, bdiag, nullptr, rb);
+  for (int k0 = kbeg; k0 < K; k0 += FG_K) {
     sa.store(As, ra);
     sb.store(Bs, rb);
     __syncthreads();
@@ -168,7 +172,15 @@ __global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __r
   while (j + 1 < njobs && jobs[j + 1].first_tile <= bid) ++j;
   const F32Job jb = jobs[j];
   if (jb.conv_in && *jb.conv_in <= (float)jb.conv_tol) return;
-  const int t = bid - (int)jb.first_tile;
+  int t = bid - (int)jb.first_tile;
+  int kbeg = 0, kend = (int)jb.K;
+  if (jb.ksplit > 1) {   // tile t = slice * (tiles of C) + C tile
+    const int ntile = (int)(((jb.M + FG_T - 1) / FG_T) * jb.tiles_n);
+    const int sl = t / ntile;
+    t -= sl * ntile;
+    kbeg = sl * (int)jb.kchunk;
+    kend = min(kend, kbeg + (int)jb.kchunk);
+  }
   const int m0 = (t / (int)jb.tiles_n) * FG_T, n0 = (t % (int)jb.tiles_n) * FG_T;
   f32x4 acc[2][2];
 #pragma unroll
@@ -177,10 +189,10 @@ __global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __r
     for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   // (every job of a VEC launch is float4-aligned: the host splits aligned and unaligned jobs)
   switch ((int)jb.ta * 2 + (int)jb.tb) {
-    case 0: f32_tile<false, false, VEC>(jb, m0, n0, As, Bs, acc); break;
-    case 1: f32_tile<false, true, VEC>(jb, m0, n0, As, Bs, acc); break;
-    case 2: f32_tile<true, false, VEC>(jb, m0, n0, As, Bs, acc); break;
-    default: f32_tile<true, true, VEC>(jb, m0, n0, As, Bs, acc); break;
+    case 0: f32_tile<false, false, VEC>(jb, m0, n0, kbeg, kend, As, Bs, acc); break;
+    case 1: f32_tile<false, true, VEC>(jb, m0, n0, kbeg, kend, As, Bs, acc); break;
+    case 2: f32_tile<true, false, VEC>(jb, m0, n0, kbeg, kend, As, Bs, acc); break;
+    default: f32_tile<true, true, VEC>(jb, m0, n0, kbeg, kend, As, Bs, acc); break;
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
   const int M = (int)jb.M, N = (int)jb.N;
@@ -190,6 +202,19 @@ __global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __r
     alpha *= (jb.apow & 15) == 2 ? s * s : s;
   }
   const float beta = (float)jb.beta, rscale = (float)jb.rscale;
+  if (jb.ksplit > 1) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * 32 + a * 16 + (lane >> 4) * 4 + r;
+          const int col = n0 + wn * 32 + b * 16 + (lane & 15);
+          if (row < M && col < N) atomicAdd(jb.C + (int64_t)row * jb.ldc + col, alpha * acc[a][b][r]);
+        }
+    return;
+  }
   float dev_max = 0.f;
 #pragma unroll
   for (int a = 0; a < 2; ++a)

@@ -172,6 +172,318 @@ __global__ void vit_embed_bwd_f32_kernel(const float* dx, float* dpatch, float* 
   if (t == 0) dcls[d] += s;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused fp32 attention for the ViT shapes (head_dim 32, T <= 272): one workgroup of 16 waves per
+// (batch, head), Q/K/V (and dO) of the head staged once in swizzled LDS images, every product on
+// v_mfma_f32_16x16x4_f32.  No [B*H, T, T] score tensor: the forward keeps the row max m and
+// 1/sum of its online softmax per query, the backward recomputes P = exp(s - m) / sum
+// from them and forms delta = rowsum(dO o O) = rowsum(dPd o Pd) in its prologue.
+// MFMA orientation: a 16x16x4 MFMA sums over k = 4 lane groups x steps; the contraction index of
+// (step s, lane group g) is chosen per product so that the scores land in the lanes and
+// registers the next product reads them from: with the scores computed transposed
+// (S^T = K Q^T: lane = query, register r = key 4g + r), O^T = V^T Pd^T and dQ^T = K^T dS^T take
+// them as their B operand directly; with S = Q K^T (lane = key, r = query 4g + r) so do
+// dV^T = dO^T Pd and dK^T = Q^T dS.  No cross-lane transposes.
+constexpr int FA_DH = 32, FA_TMAX = 272, FA_THREADS = 1024, FA_WAVES = FA_THREADS / 64;
+
+struct FaArgs {
+  const float* qkv; const float* o; const float* dout; float* out; float* dqkv;
+  float* mrow; float* linv; const uint16_t* mask;
+  int64_t ldqkv, ldo, lddo, lddqkv;
+  int T, H, D, n64;
+  float scale, dscale;
+};
+
+// element (r, c) of a swizzled [TP][32] fp32 image: 16-B slot (c >> 2) XOR ((r >> 1) & 7), so
+// the 16 rows of a fragment read hit 16 distinct (row parity, slot) bank groups
+__device__ __forceinline__ int fa_off(int r, int c) { return r * FA_DH + ((((c >> 2) ^ ((r >> 1) & 7))) << 2) + (c & 3); }
+
+__device__ __forceinline__ void fa_load(float* dst, const float* src, int64_t ld, int T, int TP) {
+  for (int i = threadIdx.x; i < TP * (FA_DH / 4); i += FA_THREADS) {
+    const int r = i >> 3, c = (i & 7) * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (r < T) v = *reinterpret_cast<const f32x4*>(src + (int64_t)r * ld + c);
+    *reinterpret_cast<f32x4*>(dst + fa_off(r, c)) = v;
+  }
+}
+
+// x[0..7] = X[r][8g .. 8g+7]: the operand of the 8 steps of a 32-long contraction over d
+__device__ __forceinline__ void fa_row8(const float* X, int r, int g, float (&x)[8]) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(X + fa_off(r, 8 * g));
+  const f32x4 b = *reinterpret_cast<const f32x4*>(X + fa_off(r, 8 * g + 4));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { x[j] = a[j]; x[4 + j] = b[j]; }
+}
+
+// the keep words of query rows [0, 16 * ceil(T/16)) (drop_word layout, shared by batch and heads)
+__host__ __device__ __forceinline__ int fa_mask_words(int T) { return ((T + 15) / 16) * 2 * ((T + 127) / 128) * 64; }
+__device__ __forceinline__ void fa_load_mask(uint16_t* dst, const uint16_t* src, int T) {
+  const int n = fa_mask_words(T) / 8;
+  for (int i = threadIdx.x; i < n; i += FA_THREADS)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+}
+
+__host__ __device__ constexpr size_t fa_fwd_lds(int NB) { return 2 * (size_t)NB * 16 * FA_DH * 4 + 17 * 6 * 64 * 2; }
+constexpr size_t FA_BWD_LDS = 4 * (size_t)FA_TMAX * FA_DH * 4 + 3 * FA_TMAX * 4 + 17 * 6 * 64 * 2;
+static_assert(FA_BWD_LDS <= 160 * 1024, "fp32 attention backward LDS");
+
+// Forward: 16-query groups dealt round-robin to the waves; per group an online softmax over
+// 64-key chunks.  O^T = V^T Pd^T keeps the query in the lane (o[d][r] = O^T[16d + 4g + r][q]), so
+// the per-query rescale is a lane-local multiply.  The final row max m and 1/sum are stored.
+template <bool DROP>
+__global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  const int h = blockIdx.x, b = blockIdx.y, T = a.T;
+  const int NB = (T + 15) / 16, TP = NB * 16;
+  float* Ks = reinterpret_cast<float*>(fa_smem);
+  float* Vs = Ks + TP * FA_DH;
+  uint16_t* mk = reinterpret_cast<uint16_t*>(Vs + TP * FA_DH);
+  const int64_t bT = (int64_t)b * T, bh = (int64_t)b * a.H + h;
+  fa_load(Ks, a.qkv + bT * a.ldqkv + a.D + h * FA_DH, a.ldqkv, T, TP);
+  fa_load(Vs, a.qkv + bT * a.ldqkv + 2 * a.D + h * FA_DH, a.ldqkv, T, TP);
+  if (DROP) fa_load_mask(mk, a.mask, T);
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  for (int gq = wave; gq < NB; gq += FA_WAVES) {
+    const int q = gq * 16 + c16;
+    const bool qv = q < T;
+    float qf[8];
+    {
+      f32x4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = x0;
+      if (qv) {
+        const float* src = a.qkv + (bT + q) * a.ldqkv + h * FA_DH + 8 * g;
+        x0 = *reinterpret_cast<const f32x4*>(src);
+        x1 = *reinterpret_cast<const f32x4*>(src + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { qf[j] = x0[j]; qf[4 + j] = x1[j]; }
+    }
+    float m = -__builtin_inff(), l = 0.f;
+    f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    for (int k0 = 0; k0 < NB; k0 += 4) {
+      f32x4 st[4];
+      float cmax = -__builtin_inff();
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (k0 + t < NB) {
+          float kf[8];
+          fa_row8(Ks, (k0 + t) * 16 + c16, g, kf);
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s], qf[s], acc, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {   // (K Q^T)[key (k0+t)*16 + 4g + r][query q] * scale
+            const float v = ((k0 + t) * 16 + 4 * g + r < T) ? acc[r] * a.scale : -__builtin_inff();
+            st[t][r] = v;
+            cmax = fmaxf(cmax, v);
+          }
+        }
+      }
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+      const float mnew = fmaxf(m, cmax);
+      const float alpha = expf(m - mnew);   // 0 on the first chunk (m = -inf)
+      m = mnew;
+      l *= alpha;
+      o[0] *= alpha;
+      o[1] *= alpha;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (k0 + t < NB) {
+          uint32_t w = 0;
+          if (DROP && qv) w = mk[f32_drop_word(q, (k0 + t) * 16 + 4 * g, a.n64)] >> ((q & 3) * 4);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            float p = expf(st[t][s] - m);
+            l += p;
+            if (DROP) p = ((w >> s) & 1u) ? p : 0.f;
+            const int key = (k0 + t) * 16 + 4 * g + s;
+#pragma unroll
+            for (int d = 0; d < 2; ++d)
+              o[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(Vs[fa_off(key, 16 * d + c16)], p, o[d], 0, 0, 0);
+          }
+        }
+      }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.f / l;
+    const float os = DROP ? inv * a.dscale : inv;
+    if (qv) {
+#pragma unroll
+      for (int d = 0; d < 2; ++d)   // o[d][r] = O^T[16d + 4g + r][q]
+        *reinterpret_cast<f32x4*>(a.out + (bT + q) * a.ldo + h * FA_DH + 16 * d + 4 * g) = o[d] * os;
+      if (g == 0) {
+        a.mrow[bh * T + q] = m;
+        a.linv[bh * T + q] = inv;
+      }
+    }
+  }
+}
+
+// Backward: waves 0-7 own key blocks (dK, dV of 16 keys over all queries: S = Q K^T orientation),
+// waves 8-15 own query groups (dQ of 16 queries over all keys: S^T orientation); both recompute
+// the scores and dPd = dO V^T for their orientation.  dQ / dK / dV are written to the q / k / v
+// column blocks of dqkv [B*T][3D].
+template <bool DROP>
+__global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char fb_smem[];
+  const int h = blockIdx.x, b = blockIdx.y, T = a.T;
+  const int NB = (T + 15) / 16, TP = NB * 16;
+  float* Qs = reinterpret_cast<float*>(fb_smem);
+  float* Ks = Qs + TP * FA_DH;
+  float* Vs = Ks + TP * FA_DH;
+  float* Os = Vs + TP * FA_DH;   // dO
+  float* Ms = Os + TP * FA_DH;
+  float* Is = Ms + TP;
+  float* Dl = Is + TP;
+  uint16_t* mk = reinterpret_cast<uint16_t*>(Dl + TP);
+  const int64_t bT = (int64_t)b * T, bh = (int64_t)b * a.H + h;
+  const float* base = a.qkv + bT * a.ldqkv + h * FA_DH;
+  fa_load(Qs, base, a.ldqkv, T, TP);
+  fa_load(Ks, base + a.D, a.ldqkv, T, TP);
+  fa_load(Vs, base + 2 * a.D, a.ldqkv, T, TP);
+  fa_load(Os, a.dout + bT * a.lddo + h * FA_DH, a.lddo, T, TP);
+  if (DROP) fa_load_mask(mk, a.mask, T);
+  for (int r = threadIdx.x; r < TP; r += FA_THREADS) {
+    Ms[r] = r < T ? a.mrow[bh * T + r] : 0.f;
+    Is[r] = r < T ? a.linv[bh * T + r] : 0.f;   // 0: padded queries get P = 0
+  }
+  // delta = rowsum(dO o O), 4 lanes x 8 columns per row (a quad never straddles a wave)
+  for (int i = threadIdx.x; i < TP * 4; i += FA_THREADS) {
+    const int r = i >> 2, c = (i & 3) * 8;
+    float sum = 0.f;
+    if (r < T) {
+      const float* op = a.o + (bT + r) * a.ldo + h * FA_DH + c;
+      const float* dp = a.dout + (bT + r) * a.lddo + h * FA_DH + c;
+      const f32x4 o0 = *reinterpret_cast<const f32x4*>(op), o1 = *reinterpret_cast<const f32x4*>(op + 4);
+      const f32x4 d0 = *reinterpret_cast<const f32x4*>(dp), d1 = *reinterpret_cast<const f32x4*>(dp + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sum += o0[j] * d0[j] + o1[j] * d1[j];
+    }
+    sum += __shfl_xor(sum, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    if ((i & 3) == 0) Dl[r] = sum;
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  if (wave < 8) {
+    for (int kb = wave; kb < NB; kb += 8) {
+      const int key = kb * 16 + c16;
+      float kf[8], vf[8];
+      fa_row8(Ks, key, g, kf);
+      fa_row8(Vs, key, g, vf);
+      f32x4 dv[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, dk[2] = {dv[0], dv[0]};
+      for (int qb = 0; qb < NB; ++qb) {
+        float qa[8], oa[8];
+        fa_row8(Qs, qb * 16 + c16, g, qa);
+        fa_row8(Os, qb * 16 + c16, g, oa);
+        f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = sv;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          sv = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[s], kf[s], sv, 0, 0, 0);   // S[q 4g+r][key]
+          dp = __builtin_amdgcn_mfma_f32_16x16x4f32(oa[s], vf[s], dp, 0, 0, 0);   // dPd[q][key]
+        }
+        uint32_t w = 0xFFFFu;
+        if (DROP && key < T) w = mk[f32_drop_word(qb * 16 + 4 * g, key, a.n64)] >> (key & 3);
+        float pd[4], ds[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ql = qb * 16 + 4 * g + r;
+          const float p = expf(sv[r] * a.scale - Ms[ql]) * Is[ql];
+          float pdv = p, dpv = dp[r];
+          if (DROP) {
+            const bool keep = (w >> (4 * r)) & 1u;
+            pdv = keep ? p * a.dscale : 0.f;
+            dpv = keep ? dpv * a.dscale : 0.f;
+          }
+          pd[r] = pdv;
+          ds[r] = p * (dpv - Dl[ql]);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int ql = qb * 16 + 4 * g + s;
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            dv[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(Os[fa_off(ql, 16 * d + c16)], pd[s], dv[d], 0, 0, 0);
+            dk[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(Qs[fa_off(ql, 16 * d + c16)], ds[s], dk[d], 0, 0, 0);
+          }
+        }
+      }
+      if (key < T) {
+        float* dst = a.dqkv + (bT + key) * a.lddqkv + h * FA_DH;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {   // dv[d][r] = dV^T[16d + 4g + r][key]
+          *reinterpret_cast<f32x4*>(dst + 2 * a.D + 16 * d + 4 * g) = dv[d];
+          *reinterpret_cast<f32x4*>(dst + a.D + 16 * d + 4 * g) = dk[d] * a.scale;
+        }
+      }
+    }
+  } else {
+    // query group gq -> wave 8 + ((gq + 1) & 7): the 17th group (T = 257) lands on wave 9, whose
+    // SIMD holds no third key block
+    for (int gq = (wave - 9) & 7; gq < NB; gq += 8) {
+      const int q = gq * 16 + c16;
+      float qf[8], of[8];
+      fa_row8(Qs, q, g, qf);
+      fa_row8(Os, q, g, of);
+      const float mq = Ms[q], iq = Is[q], dq = Dl[q];
+      f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      for (int kb = 0; kb < NB; ++kb) {
+        float ka[8], va[8];
+        fa_row8(Ks, kb * 16 + c16, g, ka);
+        fa_row8(Vs, kb * 16 + c16, g, va);
+        f32x4 st = {0.f, 0.f, 0.f, 0.f}, dpt = st;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          st = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[s], qf[s], st, 0, 0, 0);    // S^T[key 4g+r][q]
+          dpt = __builtin_amdgcn_mfma_f32_16x16x4f32(va[s], of[s], dpt, 0, 0, 0);  // dPd^T
+        }
+        uint32_t w = 0xFFFFu;
+        if (DROP && q < T) w = mk[f32_drop_word(q, kb * 16 + 4 * g, a.n64)] >> ((q & 3) * 4);
+        float ds[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kb * 16 + 4 * g + r;
+          const float p = key < T ? expf(st[r] * a.scale - mq) * iq : 0.f;
+          float dpv = dpt[r];
+          if (DROP) dpv = ((w >> r) & 1u) ? dpv * a.dscale : 0.f;
+          ds[r] = p * (dpv - dq);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int key = kb * 16 + 4 * g + s;
+#pragma unroll
+          for (int d = 0; d < 2; ++d)
+            acc[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ks[fa_off(key, 16 * d + c16)], ds[s], acc[d], 0, 0, 0);
+        }
+      }
+      if (q < T) {
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+          *reinterpret_cast<f32x4*>(a.dqkv + (bT + q) * a.lddqkv + h * FA_DH + 16 * d + 4 * g) = acc[d] * a.scale;
+      }
+    }
+  }
+}
+
+template <bool D>
+static int fa_fwd_launch(const FaArgs& a, int B, hipStream_t s) {
+  static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
+  if (const int e = optin.ensure((const void*)attn_fwd_f32_kernel<D>, (int)fa_fwd_lds(FA_TMAX / 16))) return e;
+  hipLaunchKernelGGL((attn_fwd_f32_kernel<D>), dim3(a.H, B), dim3(FA_THREADS), fa_fwd_lds((a.T + 15) / 16), s, a);
+  return 0;
+}
+template <bool D>
+static int fa_bwd_launch(const FaArgs& a, int B, hipStream_t s) {
+  static PcvLdsOptIn optin;
+  if (const int e = optin.ensure((const void*)attn_bwd_f32_kernel<D>, (int)FA_BWD_LDS)) return e;
+  hipLaunchKernelGGL((attn_bwd_f32_kernel<D>), dim3(a.H, B), dim3(FA_THREADS), FA_BWD_LDS, s, a);
+  return 0;
+}
+
+static bool fa_aligned(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
 static unsigned f32_grid(int64_t n) {
   int64_t g = (n + 255) / 256;
   return (unsigned)(g < 1 ? 1 : (g > 16384 ? 16384 : g));
@@ -256,4 +568,42 @@ extern "C" int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls
   hipLaunchKernelGGL(vit_embed_bwd_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      dx, dpatch, dcls, dpos, B, T, D, th, sc, seed, site);
   return pcv_launch_status();
+}
+
+// ---- fused fp32 attention (head_dim 32, T <= 272) ----
+extern "C" int pcv_attn_fused_f32_ok(int T, int head_dim) { return T >= 1 && T <= FA_TMAX && head_dim == FA_DH; }
+
+extern "C" int pcv_attn_fwd_f32(const float* qkv, int64_t ldqkv, float* out, int64_t ldo, float* mrow, float* linv,
+                                int B, int T, int H, int D, const uint16_t* mask, float rate, void* stream) {
+  if (!qkv || !out || !mrow || !linv || B <= 0 || H <= 0 || !pcv_attn_fused_f32_ok(T, D / H) || D != H * FA_DH ||
+      ldqkv < 3 * D || ldo < D || (ldqkv & 3) || (ldo & 3) || !fa_aligned(qkv) || !fa_aligned(out) ||
+      (rate > 0.f && (!mask || !fa_aligned(mask))) || rate < 0.f || rate >= 1.f)
+    return PCV_EINVAL;
+  FaArgs a = {};
+  a.qkv = qkv; a.out = out; a.mrow = mrow; a.linv = linv; a.mask = mask;
+  a.ldqkv = ldqkv; a.ldo = ldo; a.T = T; a.H = H; a.D = D; a.n64 = 2 * ((T + 127) / 128);
+  a.scale = 1.f / sqrtf((float)FA_DH);
+  a.dscale = rate > 0.f ? 1.f / (1.f - rate) : 1.f;
+  const int e = rate > 0.f ? fa_fwd_launch<true>(a, B, (hipStream_t)stream)
+                           : fa_fwd_launch<false>(a, B, (hipStream_t)stream);
+  return e ? e : pcv_launch_status();
+}
+
+extern "C" int pcv_attn_bwd_f32(const float* qkv, int64_t ldqkv, const float* o, int64_t ldo, const float* dout,
+                                int64_t lddo, const float* mrow, const float* linv, float* dqkv, int64_t lddqkv, int B,
+                                int T, int H, int D, const uint16_t* mask, float rate, void* stream) {
+  if (!qkv || !o || !dout || !mrow || !linv || !dqkv || B <= 0 || H <= 0 || !pcv_attn_fused_f32_ok(T, D / H) ||
+      D != H * FA_DH || ldqkv < 3 * D || lddqkv < 3 * D || ldo < D || lddo < D ||
+      ((ldqkv | ldo | lddo | lddqkv) & 3) || !fa_aligned(qkv) || !fa_aligned(o) || !fa_aligned(dout) ||
+      !fa_aligned(dqkv) || (rate > 0.f && (!mask || !fa_aligned(mask))) || rate < 0.f || rate >= 1.f)
+    return PCV_EINVAL;
+  FaArgs a = {};
+  a.qkv = qkv; a.o = o; a.dout = dout; a.dqkv = dqkv; a.mrow = const_cast<float*>(mrow);
+  a.linv = const_cast<float*>(linv); a.mask = mask;
+  a.ldqkv = ldqkv; a.ldo = ldo; a.lddo = lddo; a.lddqkv = lddqkv;
+  a.T = T; a.H = H; a.D = D; a.n64 = 2 * ((T + 127) / 128);
+  a.scale = 1.f / sqrtf((float)FA_DH);
+  a.dscale = rate > 0.f ? 1.f / (1.f - rate) : 1.f;
+  const int e = rate > 0.f ? fa_bwd_launch<true>(a, B, (hipStream_t)stream) : fa_bwd_launch<false>(a, B, (hipStream_t)stream);
+  return e ? e : pcv_launch_status();
 }

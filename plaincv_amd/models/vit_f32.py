@@ -4,12 +4,15 @@ The reference ViT computes in fp32 (models/vit_small.py:95; BASELINE configs[0] 
 bf16).  Same forward / backward as ``ViTRunner`` (bf16 MFMA operands), but every contraction runs on
 the exact-fp32 MFMA through the grouped fp32 GEMM of csrc/precond.hip (``GemmF32``: each call site
 is one pre-planned launch; the per-(batch, head) attention products are jobs of one launch), with
-the elementwise epilogues, LayerNorm, attention softmax / weight dropout over materialised
-[B*H, T, T] scores and the embedding VJP in csrc/vit_f32.hip.  Dropout bits and sites are those
+the elementwise epilogues, LayerNorm, the fused fp32 attention (head_dim 32, T <= 272: one
+workgroup per (batch, head), scores never leave the CU; other shapes: per-head GEMM jobs around a
+softmax / weight-dropout kernel over materialised [B*H, T, T] scores) and the embedding VJP in
+csrc/vit_f32.hip.  Dropout bits and sites are those
 of the bf16 path (shared with oracle/rng.py), so the two runners draw identical masks.
 Supported: LayerNorm or no norm (use_batchnorm is bf16-path only).
 """
 import math
+import os
 
 import torch
 
@@ -50,6 +53,36 @@ def _gemm(a, b, c, **kw):
     return GemmF32().add(a, b, c, **kw)
 
 
+class _Dense:
+    """One token-row product c = epi(a op(b)) of the step: the fused row-panel GEMM of
+    csrc/gemm_f32.hip when the shape fits it (N % 128, K % 64), else a planned grouped-GEMM launch
+    followed by the standalone epilogue kernel (same element order and dropout index)."""
+
+    def __init__(self, a, b, c, tb=False, bias=None, res=None, aux=None, act=0, site=0, dropout=False):
+        self.a, self.b, self.c, self.tb = a, b, c, bool(tb)
+        self.bias, self.res, self.aux, self.act, self.site, self.dropout = bias, res, aux, act, site, dropout
+        M, K = a.shape
+        self.M, self.N, self.K = M, c.shape[1], K
+        self.fused = bool(hip.load().pcv_gemm_f32_rows_ok(M, self.N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
+                                                          int(tb)))
+        self.plan = None if self.fused else GemmF32().add(a, b, c, tb=tb).finalize(c.device)
+        self.epi = bias is not None or res is not None or act or dropout
+
+    def run(self, rate=0.0, seed=None):
+        rate = rate if self.dropout else 0.0
+        if self.fused:
+            hip.call("pcv_gemm_f32_rows", ptr(self.a), self.a.stride(0), ptr(self.b), self.b.stride(0), int(self.tb),
+                     ptr(self.c), self.c.stride(0), self.M, self.N, self.K, ptr(self.bias), ptr(self.aux),
+                     self.aux.stride(0) if self.aux is not None else 0, ptr(self.res),
+                     self.res.stride(0) if self.res is not None else 0, 1.0, int(self.act), float(rate), ptr(seed),
+                     int(self.site), stream_ptr())
+            return
+        self.plan.run()
+        if self.epi:
+            _epi(self.c, self.c, bias=self.bias, res=self.res, aux=self.aux, act=self.act, rate=rate, seed=seed,
+                 site=self.site)
+
+
 class ViTRunnerF32:
     """Fixed-shape fp32 forward/backward executor (graph-capturable, no allocation after init)."""
 
@@ -79,13 +112,18 @@ class ViTRunnerF32:
         self.st0 = [(z(R), z(R)) for _ in range(L)]
         self.st1 = [(z(R), z(R)) for _ in range(L)]
         self.qkv = [z(R, 3 * D) for _ in range(L)]
-        self.S = z(BH * T, T)                               # scores (scratch), later dPd / dS
-        self.P = [z(BH * T, T) for _ in range(L)]
-        self.Pd = [z(BH * T, T) for _ in range(L)] if model.dropout_rate > 0 else self.P
+        self.fused_attn = (bool(hip.load().pcv_attn_fused_f32_ok(T, self.Dh))
+                           and os.environ.get("PCV_F32_FUSED_ATTN", "1") != "0")
+        if self.fused_attn:   # per-query softmax row max and 1/sum, read back by the backward
+            self.mrow = [z(BH * T) for _ in range(L)]
+            self.linv = [z(BH * T) for _ in range(L)]
+        else:
+            self.S = z(BH * T, T)                           # scores (scratch), later dPd / dS
+            self.P = [z(BH * T, T) for _ in range(L)]
+            self.Pd = [z(BH * T, T) for _ in range(L)] if model.dropout_rate > 0 else self.P
         self.o = [z(R, D) for _ in range(L)]
         self.pre = [z(R, M) for _ in range(L)]
         self.a = [z(R, M) for _ in range(L)]
-        self.tD, self.tM = z(R, D), z(R, M)
         self.yf, self.stf = z(B, D), (z(B), z(B))
         self.logits, self.dlogits = z(B, self.Kc), z(B, self.Kc)
         self.row_loss, self.row_correct = z(B), z(B)
@@ -157,9 +195,10 @@ class ViTRunnerF32:
         self.gf, self.gb = [], []
         for i in range(L):
             w = self.w[i]
-            qkv, Pd, o, dqkv = self.qkv[i], self.Pd[i], self.o[i], self.dqkv_l[i]
+            qkv, o, dqkv = self.qkv[i], self.o[i], self.dqkv_l[i]
             s_g, pv, dpv, dqk = GemmF32(), GemmF32(), GemmF32(), GemmF32()
-            for b in range(B):
+            for b in range(B if not self.fused_attn else 0):
+                Pd = self.Pd[i]
                 for h in range(H):
                     q, k, v = (self._heads(qkv, c0, b, h) for c0 in (0, D, 2 * D))
                     dq, dk, dv = (self._heads(dqkv, c0, b, h) for c0 in (0, D, 2 * D))
@@ -171,23 +210,32 @@ class ViTRunnerF32:
                     dpv.add(Pd[rows], dob, dv, ta=True)                      # dV = Pd^T dO
                     dqk.add(self.S[rows], k, dq, alpha=sc)                   # dQ = scale dS K
                     dqk.add(self.S[rows], q, dk, ta=True, alpha=sc)          # dK = scale dS^T Q
-            self.gf.append(dict(qkv=f(_gemm(self.y0[i], w["Wqkv"], qkv)), s=f(s_g), pv=f(pv),
-                                out=f(_gemm(o, w["Wo"], self.tD)), fc1=f(_gemm(self.y1[i], w["W0"], self.tM)),
-                                fc2=f(_gemm(self.a[i], w["W1"], self.tD))))
-            self.gb.append(dict(fc2_d=f(_gemm(self.dmo_l[i], w["W1"], self.da, tb=True)),
-                                fc1_d=f(_gemm(self.da_l[i], w["W0"], self.dy1, tb=True)),
-                                out_d=f(_gemm(self.dx1_l[i], w["Wo"], self.dO, tb=True)), dpv=f(dpv), dqk=f(dqk),
-                                qkv_d=f(_gemm(dqkv, w["Wqkv"], self.dy0, tb=True))))
+            att = {} if self.fused_attn else dict(s=f(s_g), pv=f(pv), dpv=f(dpv), dqk=f(dqk))
+            self.gf.append(dict(
+                qkv=_Dense(self.y0[i], w["Wqkv"], qkv, bias=w["bqkv"]), s=att.get("s"), pv=att.get("pv"),
+                out=_Dense(o, w["Wo"], self.x1s[i], bias=w["bo"], res=self.xs[i]),
+                fc1=_Dense(self.y1[i], w["W0"], self.a[i], bias=w["b0"], aux=self.pre[i], act=1,
+                           site=site_mlp_hidden(i), dropout=True),
+                fc2=_Dense(self.a[i], w["W1"], self.xs[i + 1], bias=w["b1"], res=self.x1s[i], site=site_mlp_out(i),
+                           dropout=True)))
+            self.gb.append(dict(fc2_d=_Dense(self.dmo_l[i], w["W1"], self.da, tb=True),
+                                fc1_d=_Dense(self.da_l[i], w["W0"], self.dy1, tb=True),
+                                out_d=_Dense(self.dx1_l[i], w["Wo"], self.dO, tb=True), dpv=att.get("dpv"),
+                                dqk=att.get("dqk"),
+                                qkv_d=_Dense(dqkv, w["Wqkv"], self.dy0, tb=True)))
         # every weight gradient (K = B*T rows) in one grouped launch at the end of backward
+        # (split-K: a [D, N] gradient is only a few 64x64 tiles, so each tile's K = B*T sum is cut
+        # into ~1024-long slices accumulated with fp32 atomics -- ~2k workgroups instead of 138)
         wg = GemmF32()
-        wg.add(self.yf, self.dlogits, self.gWh, ta=True, beta=1.0)
-        wg.add(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
+        ks = lambda t: max(1, t.shape[0] // 1024)  # noqa: E731
+        wg.add(self.yf, self.dlogits, self.gWh, ta=True, beta=1.0, ksplit=ks(self.yf))
+        wg.add(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0, ksplit=ks(self.patches))
         for i in range(L):
             w = self.w[i]
-            wg.add(self.a[i], self.dmo_l[i], w["gW1"], ta=True, beta=1.0)
-            wg.add(self.y1[i], self.da_l[i], w["gW0"], ta=True, beta=1.0)
-            wg.add(self.o[i], self.dx1_l[i], w["gWo"], ta=True, beta=1.0)
-            wg.add(self.y0[i], self.dqkv_l[i], w["gWqkv"], ta=True, beta=1.0)
+            wg.add(self.a[i], self.dmo_l[i], w["gW1"], ta=True, beta=1.0, ksplit=ks(self.a[i]))
+            wg.add(self.y1[i], self.da_l[i], w["gW0"], ta=True, beta=1.0, ksplit=ks(self.y1[i]))
+            wg.add(self.o[i], self.dx1_l[i], w["gWo"], ta=True, beta=1.0, ksplit=ks(self.o[i]))
+            wg.add(self.y0[i], self.dqkv_l[i], w["gWqkv"], ta=True, beta=1.0, ksplit=ks(self.y0[i]))
         self.g_wgrad = f(wg)
 
     def _mask(self, i):
@@ -216,20 +264,20 @@ class ViTRunnerF32:
                 self._ln(x, w["s0"], w["c0"], self.y0[i], self.st0[i])
             g = self.gf[i]
             g["qkv"].run()
-            _epi(self.qkv[i], self.qkv[i], bias=w["bqkv"])
-            g["s"].run()
-            hip.call("pcv_attn_softmax_f32", ptr(self.S), ptr(self.P[i]), ptr(self.Pd[i]),
-                     self.S.shape[0], T, ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
-            g["pv"].run()
+            if self.fused_attn:
+                hip.call("pcv_attn_fwd_f32", ptr(self.qkv[i]), 3 * D, ptr(self.o[i]), D, ptr(self.mrow[i]),
+                         ptr(self.linv[i]), B, T, self.H, D, ptr(self._mask(i)) if rate > 0 else None, float(rate),
+                         stream_ptr())
+            else:
+                g["s"].run()
+                hip.call("pcv_attn_softmax_f32", ptr(self.S), ptr(self.P[i]), ptr(self.Pd[i]),
+                         self.S.shape[0], T, ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
+                g["pv"].run()
             g["out"].run()
-            _epi(self.tD, self.x1s[i], bias=w["bo"], res=x)
             if m.use_layernorm:
                 self._ln(self.x1s[i], w["s1"], w["c1"], self.y1[i], self.st1[i])
-            g["fc1"].run()
-            _epi(self.tM, self.a[i], bias=w["b0"], aux=self.pre[i], act=1, rate=rate, seed=seed,
-                 site=site_mlp_hidden(i))
-            g["fc2"].run()
-            _epi(self.tD, self.xs[i + 1], bias=w["b1"], res=self.x1s[i], rate=rate, seed=seed, site=site_mlp_out(i))
+            g["fc1"].run(rate, seed)
+            g["fc2"].run(rate, seed)
         xcls = self.xs[-1].view(B, T * D)[:, :D]
         if m.use_layernorm:
             self._ln(xcls, self.sf, self.cf, self.yf, self.stf)
@@ -277,10 +325,15 @@ class ViTRunnerF32:
                 _epi(self.dy1, dx1, res=dx_in)
             K.colsum(dx1, w["gbo"])
             g["out_d"].run()                                                           # self.dO = dx1 Wo^T
-            g["dpv"].run()                                                             # dPd -> S, dV
-            hip.call("pcv_attn_softmax_bwd_f32", ptr(self.P[i]), ptr(self.S), self.S.shape[0], T,
-                     ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
-            g["dqk"].run()                                                             # dQ, dK
+            if self.fused_attn:                                                        # dQ, dK, dV
+                hip.call("pcv_attn_bwd_f32", ptr(self.qkv[i]), 3 * D, ptr(self.o[i]), D, ptr(self.dO), D,
+                         ptr(self.mrow[i]), ptr(self.linv[i]), ptr(dqkv), 3 * D, B, T, self.H, D,
+                         ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
+            else:
+                g["dpv"].run()                                                         # dPd -> S, dV
+                hip.call("pcv_attn_softmax_bwd_f32", ptr(self.P[i]), ptr(self.S), self.S.shape[0], T,
+                         ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
+                g["dqk"].run()                                                         # dQ, dK
             K.colsum(dqkv, w["gbqkv"])
             g["qkv_d"].run()                                                           # self.dy0 = dqkv Wqkv^T
             if m.use_layernorm:

@@ -38,7 +38,7 @@ class GemmF32:
     """One grouped launch of C = alpha*adev^apow * op(A) diag(kscale) op(B) + beta*C + rscale*R
     (+ bf16 copy Cb).  ``add(...)`` jobs, then ``finalize(device)``; ``run()`` per step."""
 
-    FMT = "<9Q13q8d"
+    FMT = "<9Q15q8d"
 
     def __init__(self):
         self.jobs = []
@@ -46,9 +46,11 @@ class GemmF32:
 
     def add(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, kscale=None, r=None, rscale=0.0, cb=None,
             alpha_dev=None, apow=1, a_affine=(1.0, 0.0), b_affine=(1.0, 0.0), conv_in=None, conv_out=None,
-            conv_tol=0.0):
+            conv_tol=0.0, ksplit=1):
         """a_affine = (mul, diag): op(A) -> mul * op(A) + diag * I (b_affine likewise);
-        conv_in: skip this job when *conv_in <= conv_tol; conv_out: atomic max of |C - I|."""
+        conv_in: skip this job when *conv_in <= conv_tol; conv_out: atomic max of |C - I|;
+        ksplit > 1: split K over that many tiles per C tile, accumulated with fp32 atomics (only
+        C += alpha op(A) op(B): beta 1, no r / cb / conv_out)."""
         M, K = (a.shape[1], a.shape[0]) if ta else (a.shape[0], a.shape[1])
         K2, N = (b.shape[1], b.shape[0]) if tb else (b.shape[0], b.shape[1])
         if K != K2 or tuple(c.shape) != (M, N):
@@ -60,6 +62,14 @@ class GemmF32:
         if cb is not None and (tuple(cb.shape) != (M, N) or cb.dtype != torch.bfloat16 or cb.stride(1) != 1):
             raise ValueError("bf16 copy shape")
         tiles_n = (N + TILE - 1) // TILE
+        ksplit = max(1, int(ksplit))
+        kchunk = K
+        if ksplit > 1:
+            if beta != 1.0 or r is not None or cb is not None or conv_out is not None:
+                raise ValueError("split-K jobs accumulate into C: beta must be 1 with no r / cb / conv_out")
+            kchunk = -(-K // ksplit)
+            kchunk = -(-kchunk // 128) * 128          # whole 128-long k chunks per slice
+            ksplit = -(-K // kchunk)
         for t in (a, b, c, r):
             if t is not None and t.shape[0] * t.stride(0) >= 2 ** 31:
                 raise ValueError("gemm_f32 operands must have < 2^31 elements (int32 offsets)")
@@ -69,7 +79,8 @@ class GemmF32:
         self.jobs.append(dict(A=a, B=b, C=c, ks=kscale, R=r, Cb=cb, ad=alpha_dev, M=M, N=N, K=K, lda=_ld(a),
                               ldb=_ld(b), ldc=_ld(c), ldr=_ld(r) if r is not None else 0,
                               ldcb=cb.stride(0) if cb is not None else 0, ta=int(ta), tb=int(tb), apow=int(apow) | (16 if vec else 0),
-                              tiles=((M + TILE - 1) // TILE) * tiles_n, tiles_n=tiles_n, alpha=float(alpha),
+                              tiles=((M + TILE - 1) // TILE) * tiles_n * ksplit, tiles_n=tiles_n, ksplit=ksplit,
+                              kchunk=kchunk, alpha=float(alpha),
                               beta=float(beta), rscale=float(rscale), aff=(float(a_affine[1]), float(a_affine[0]),
                                                                            float(b_affine[1]), float(b_affine[0])),
                               ci=conv_in, co=conv_out, tol=float(conv_tol)))
@@ -88,7 +99,8 @@ class GemmF32:
                 recs.append((_addr(j["A"]), _addr(j["B"]), _addr(j["C"]), _addr(j["ks"]), _addr(j["R"]),
                              _addr(j["Cb"]), _addr(j["ad"]), _addr(j["ci"]), _addr(j["co"]), j["M"], j["N"], j["K"],
                              j["lda"], j["ldb"], j["ldc"], j["ldr"], j["ldcb"], j["ta"], j["tb"], j["apow"],
-                             j["tiles_n"], first, j["alpha"], j["beta"], j["rscale"]) + j["aff"] + (j["tol"],))
+                             j["tiles_n"], first, j["ksplit"], j["kchunk"], j["alpha"], j["beta"], j["rscale"]) + j["aff"]
+                            + (j["tol"],))
                 first += j["tiles"]
             if recs:
                 self.groups.append((_pack(recs, self.FMT).to(device), len(recs), first, int(vec)))

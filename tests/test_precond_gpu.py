@@ -73,6 +73,31 @@ def test_gemm_f32_epilogue_and_grouping(dev):
         assert (c.double() - ref).abs().max().item() < 1e-4
 
 
+@pytest.mark.parametrize("M,N,K,ks,ta,tb", [(128, 384, 5000, 5, 1, 0), (48, 128, 16384, 16, 1, 0), (37, 50, 700, 3, 0, 1),
+                                             (64, 64, 130, 2, 1, 1)])
+def test_gemm_f32_split_k(dev, M, N, K, ks, ta, tb):
+    """split-K jobs (fp32 atomics into C, beta 1) beside an unsplit job in one launch"""
+    from plaincv_amd.optim.precond import GemmF32
+    g = torch.Generator().manual_seed(M + N + K)
+    a = torch.randn((K, M) if ta else (M, K), generator=g).to(dev)
+    b = torch.randn((N, K) if tb else (K, N), generator=g).to(dev)
+    c = torch.randn(M, N, generator=g).to(dev)
+    c0 = c.clone()
+    a2, b2, c2 = torch.randn(33, 20, generator=g).to(dev), torch.randn(20, 70, generator=g).to(dev), torch.zeros(33, 70, device=dev)
+    plan = GemmF32().add(a, b, c, ta=bool(ta), tb=bool(tb), alpha=0.5, beta=1.0, ksplit=ks).add(a2, b2, c2)
+    assert plan.jobs[0]["ksplit"] > 1
+    plan.finalize(dev).run()
+    torch.cuda.synchronize()
+    A = (a.t() if ta else a).double()
+    B = (b.t() if tb else b).double()
+    ref = 0.5 * A @ B + c0.double()
+    scale = (A.abs() @ B.abs()).max().item() + 1.0
+    assert (c.double() - ref).abs().max().item() <= 2e-5 * scale
+    assert (c2.double() - a2.double() @ b2.double()).abs().max().item() < 1e-4
+    with pytest.raises(ValueError):
+        GemmF32().add(a, b, c, ta=bool(ta), tb=bool(tb), beta=0.0, ksplit=ks)
+
+
 def _spd(n, rank, g, dev, scale=1.0):
     x = torch.randn(n, rank, generator=g, dtype=torch.float64) * scale
     return (x @ x.t()).float().to(dev)

@@ -135,3 +135,29 @@ def test_vit_f32_graphed_step(dev):
         gsc(images, labels)
     torch.cuda.synchronize()
     assert torch.isfinite(sc.params.flat).all()
+
+
+def test_vit_f32_unfused_attention_matches_fused(dev, monkeypatch):
+    """The general attention path (per-head GEMM jobs around the materialised-score softmax, used
+    past T = 272 or head_dim != 32) and the fused kernels give the same step (rel 1e-5)."""
+    from plaincv_amd.engine import create_train_state
+    m = _model(0.1)
+    shape = (4, 16, 16, 3)
+    init = m.init(5, shape)
+    g = torch.Generator().manual_seed(6)
+    images = torch.randint(0, 256, shape, generator=g, dtype=torch.uint8).to(dev)
+    labels = torch.randint(0, 10, (4,), generator=g, dtype=torch.int32).to(dev)
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PCV_F32_FUSED_ATTN", flag)
+        st = create_train_state(0, m, 1e-3, shape, 10, init_params=init)
+        r = st.runner_for(shape)
+        assert r.fused_attn == (flag == "1")
+        r.seed.fill_(9)
+        st.params.zero_grad()
+        met = r.forward(images, labels, train=True)
+        r.backward(train=True)
+        torch.cuda.synchronize()
+        out.append((met[0].item(), st.params.grad_flat.clone()))
+    assert abs(out[0][0] - out[1][0]) <= 1e-6 * abs(out[1][0])
+    assert rel(out[0][1], out[1][1]) < 1e-5
