@@ -38,6 +38,7 @@ sys.path.insert(0, ROOT)
 from plaincv_amd.engine import GraphedTrainStep, create_train_state  # noqa: E402
 from plaincv_amd.engine import data_parallel as dp  # noqa: E402
 from plaincv_amd.models.vit_small import VisionTransformer  # noqa: E402
+from plaincv_amd.optim.precond import GemmF32  # noqa: E402
 from utils import Config  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
@@ -174,12 +175,15 @@ def vit_roofline_f32(state, image_shape):
     grouped exact-fp32 MFMA launch) -- the largest single launch of the fp32 step -- against the
     fp32 MFMA peak; FLOPs = 2 K sum(M N) over its jobs, timed live on its stream."""
     r = state.runner_for(image_shape)
-    t = timed_kernel(lambda: r.g_wgrad.run())
+    g = r.g_wgrad
+    t = timed_kernel(lambda: g.run())
     flops = 0
-    for j in r.g_wgrad.jobs:
-        flops += 2 * j["M"] * j["N"] * j["K"]
+    for j in g.jobs:   # GemmF32 job dicts or WgradF32 (A [K][M], B [K][N], C) triples
+        flops += 2 * j["M"] * j["N"] * j["K"] if isinstance(j, dict) else 2 * j[0].shape[1] * j[1].shape[1] * j[0].shape[0]
     ach = flops / t / 1e12
-    return {"kernel": "gemm_f32_grouped (all weight gradients of the fp32 step, one launch)", "bound": "mfma",
+    name = ("gemm_f32_grouped (weight gradients of the fp32 step, one launch)" if isinstance(g, GemmF32) else
+            "gemm_f32_wgrad_kernel<128> (the layer weight gradients of the fp32 step, one launch, split-K)")
+    return {"kernel": name, "bound": "mfma",
             "achieved": round(ach, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / F32_PEAK_TFLOPS, 4), "traffic": None, "launch_us": round(t * 1e6, 2),
             "flops_per_launch": flops}

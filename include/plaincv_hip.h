@@ -247,6 +247,13 @@ int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, int64_t ldb, 
                       int64_t M, int64_t N, int64_t K, const float* bias, float* aux, int64_t ldaux, const float* res,
                       int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed, uint32_t site,
                       void* stream);
+/* Every fp32 weight gradient of a step in one launch (csrc/gemm_f32.hip): jobs_dev holds njobs
+ * records (pcv_gemm_f32_wgrad_job_size() bytes) {A, B, C, lda, ldb, ldc, M, N, K, tiles_n, tiles,
+ * ksplit, kchunk, first}: C[M][N] += A^T B with A [K][M], B [K][N] (K-major token rows), 64 x bn
+ * panels x ksplit K slices added with fp32 atomics; first = prefix sum of tiles * ksplit.
+ * Requires M % 64, N % bn, K % 64, kchunk % 64 == 0, 16-B aligned operands, ld % 4 == 0. */
+int pcv_gemm_f32_wgrad_job_size(void);
+int pcv_gemm_f32_wgrad(const void* jobs_dev, int njobs, int64_t total_blocks, int bn, void* stream);
 /* Fused fp32 self-attention of one layer (flax MultiHeadDotProductAttention at
  * models/vit_small.py:41-45, fp32): qkv [B*T][ldqkv] holds q | k | v column blocks of width D = H * 32;
  * out [B*T][ldo] = softmax(q k^T / sqrt(32)) (weight dropout: packed keep words `mask`, rate) v;

@@ -20,7 +20,7 @@
 
 namespace pcv {
 
-constexpr int GR_BM = 64, GR_BN = 128, GR_BK = 64, GR_LDK = GR_BK + 4;
+constexpr int GR_BM = 64, GR_BN = 128, GR_BK = 64, GR_LDK = GR_BK + 4;   // GR_BN: the widest panel
 
 struct GrArgs {
   const float* A; const float* B; float* C;
@@ -37,47 +37,57 @@ __device__ __forceinline__ float gr_gelu(float x) {
   return 0.5f * x * (1.f + tanhf(k * (x + 0.044715f * x * x * x)));
 }
 
-template <bool TB, bool EPI>
-__global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
-  // one LDS image per operand; the next 64-long k chunk waits in registers (its global loads are
-  // issued before this chunk's MFMAs, ~1.7 us of MFMA work per chunk covers their latency)
-  __shared__ __attribute__((aligned(16))) float As[GR_BM * GR_LDK];
-  __shared__ __attribute__((aligned(16))) float Bs[GR_BN * GR_LDK];
-  constexpr int C4 = GR_BK / 4;                       // float4 per k-row of a chunk
-  constexpr int NA = GR_BM * C4 / 256, NB = GR_BN * C4 / 256;
+// Main loop shared by the row GEMM and the weight-gradient GEMM: acc += op(A)[m0.., kbeg:kend] .
+// op(B)[kbeg:kend, n0..] for one 64 x BN tile (waves 2 x 2, each 32 x BN/2).  Operand layouts:
+//   A: !TA [M][K] (k-contiguous rows, float4 staged as is) / TA [K][M] (lanes along m for
+//      coalesced loads, transposed into the [m][k] image by scalar LDS stores);
+//   B:  TB [N][K] / !TB [K][N] (transposed likewise).
+// (kend - kbeg) % 64 == 0; with TA, M % 64 == 0; B's n-range is always in bounds (N % BN == 0).
+// The next chunk's global loads are issued before this chunk's MFMAs; inside a chunk the next
+// 16-long slice's fragments are read from LDS while the current slice's MFMAs issue.
+template <bool TA, bool TB, int BN>
+__device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
+                                            int64_t ldb, int M, int m0, int n0, int kbeg, int kend, float* As,
+                                            float* Bs, f32x4 (&acc)[2][BN / 32]) {
+  constexpr int C4 = GR_BK / 4;                          // float4 per 64-long k row
+  constexpr int NA = GR_BM * C4 / 256, NB = BN * C4 / 256;
+  constexpr int WN = BN / 2, NJ = WN / 16;               // wave tile 32 x WN
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
   const int g4 = lane >> 4, c16 = lane & 15;
-  const int tn = blockIdx.x % g.tiles_n, tm = blockIdx.x / g.tiles_n;
-  const int m0 = tm * GR_BM, n0 = tn * GR_BN;
-  // A chunk: 64 rows x C4 float4; rows past M read row M-1 (their C rows are dropped)
   const float* ap[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
-    const int idx = tid + 256 * i, r = idx / C4, c4 = idx % C4;
-    ap[i] = g.A + (int64_t)min(m0 + r, g.M - 1) * g.lda + c4 * 4;
+    const int idx = tid + 256 * i;
+    if (TA) ap[i] = A + (int64_t)(kbeg + idx / (GR_BM / 4)) * lda + m0 + (idx % (GR_BM / 4)) * 4;
+    else ap[i] = A + (int64_t)min(m0 + idx / C4, M - 1) * lda + kbeg + (idx % C4) * 4;
   }
-  // B chunk: TB -- 128 n-rows x C4 float4 along k; !TB -- GR_BK k-rows x 32 float4 along n, lanes
-  // walking k so that the transposing LDS stores are bank-consecutive
   const float* bp[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const int idx = tid + 256 * i;
-    if (TB) bp[i] = g.B + (int64_t)(n0 + idx / C4) * g.ldb + (idx % C4) * 4;
-    else bp[i] = g.B + (int64_t)(idx % GR_BK) * g.ldb + n0 + (idx / GR_BK) * 4;
+    if (TB) bp[i] = B + (int64_t)(n0 + idx / C4) * ldb + kbeg + (idx % C4) * 4;
+    else bp[i] = B + (int64_t)(kbeg + idx / (BN / 4)) * ldb + n0 + (idx % (BN / 4)) * 4;
   }
   f32x4 ra[NA], rb[NB];
-  auto gload = [&](int k0) {
+  auto gload = [&](int kc) {   // chunk kc (relative to kbeg)
 #pragma unroll
-    for (int i = 0; i < NA; ++i) ra[i] = *reinterpret_cast<const f32x4*>(ap[i] + k0);
+    for (int i = 0; i < NA; ++i)
+      ra[i] = *reinterpret_cast<const f32x4*>(ap[i] + (TA ? (int64_t)kc * GR_BK * lda : (int64_t)kc * GR_BK));
 #pragma unroll
     for (int i = 0; i < NB; ++i)
-      rb[i] = *reinterpret_cast<const f32x4*>(bp[i] + (TB ? (int64_t)k0 : (int64_t)k0 * g.ldb));
+      rb[i] = *reinterpret_cast<const f32x4*>(bp[i] + (TB ? (int64_t)kc * GR_BK : (int64_t)kc * GR_BK * ldb));
   };
   auto lstore = [&]() {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int idx = tid + 256 * i;
-      *reinterpret_cast<f32x4*>(&As[(idx / C4) * GR_LDK + (idx % C4) * 4]) = ra[i];
+      if (TA) {
+        const int kr = idx / (GR_BM / 4), m = (idx % (GR_BM / 4)) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) As[(m + j) * GR_LDK + kr] = ra[i][j];
+      } else {
+        *reinterpret_cast<f32x4*>(&As[(idx / C4) * GR_LDK + (idx % C4) * 4]) = ra[i];
+      }
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
@@ -85,38 +95,39 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
       if (TB) {
         *reinterpret_cast<f32x4*>(&Bs[(idx / C4) * GR_LDK + (idx % C4) * 4]) = rb[i];
       } else {
-        const int kr = idx % GR_BK, n = (idx / GR_BK) * 4;
+        const int kr = idx / (BN / 4), n = (idx % (BN / 4)) * 4;
 #pragma unroll
         for (int j = 0; j < 4; ++j) Bs[(n + j) * GR_LDK + kr] = rb[i][j];
       }
     }
   };
-  f32x4 acc[2][4];
+  auto fload = [&](int kk, f32x4 (&fa)[2], f32x4 (&fb)[NJ]) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
+      fa[i] = *reinterpret_cast<const f32x4*>(&As[(wm * 32 + i * 16 + c16) * GR_LDK + kk + 4 * g4]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = g.K / GR_BK;
+    for (int j = 0; j < NJ; ++j)
+      fb[j] = *reinterpret_cast<const f32x4*>(&Bs[(wn * WN + j * 16 + c16) * GR_LDK + kk + 4 * g4]);
+  };
+  const int nk = (kend - kbeg) / GR_BK;
   gload(0);
   lstore();
   __syncthreads();
   for (int kc = 0; kc < nk; ++kc) {
-    if (kc + 1 < nk) gload((kc + 1) * GR_BK);
+    if (kc + 1 < nk) gload(kc + 1);
+    f32x4 fa[2][2], fb[2][NJ];
+    fload(0, fa[0], fb[0]);
 #pragma unroll
-    for (int kk = 0; kk < GR_BK; kk += 16) {
-      f32x4 fa[2], fb[4];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        fa[i] = *reinterpret_cast<const f32x4*>(&As[(wm * 32 + i * 16 + c16) * GR_LDK + kk + 4 * g4]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        fb[j] = *reinterpret_cast<const f32x4*>(&Bs[(wn * 64 + j * 16 + c16) * GR_LDK + kk + 4 * g4]);
+    for (int sl = 0; sl < GR_BK / 16; ++sl) {
+      const int cur = sl & 1;
+      if (sl + 1 < GR_BK / 16) fload((sl + 1) * 16, fa[cur ^ 1], fb[cur ^ 1]);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[cur][i][s], fb[cur][j][s], acc[i][j], 0, 0, 0);
     }
     if (kc + 1 < nk) {
       __syncthreads();
@@ -124,6 +135,23 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
       __syncthreads();
     }
   }
+}
+
+template <bool TB, bool EPI, int BN>
+__global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
+  __shared__ __attribute__((aligned(16))) float As[GR_BM * GR_LDK];
+  __shared__ __attribute__((aligned(16))) float Bs[BN * GR_LDK];
+  constexpr int WN = BN / 2, NJ = WN / 16;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+  const int g4 = lane >> 4, c16 = lane & 15;
+  const int tn = blockIdx.x % g.tiles_n, tm = blockIdx.x / g.tiles_n;
+  const int m0 = tm * GR_BM, n0 = tn * BN;
+  f32x4 acc[2][NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gr_mainloop<false, TB, BN>(g.A, g.lda, g.B, g.ldb, g.M, m0, n0, 0, g.K, As, Bs, acc);
   const uint32_t seed = (EPI && g.thresh) ? *g.seed : 0u;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -132,8 +160,8 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
       const int row = m0 + wm * 32 + i * 16 + 4 * g4 + r;
       if (row >= g.M) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wn * 64 + j * 16 + c16;
+      for (int j = 0; j < NJ; ++j) {
+        const int col = n0 + wn * WN + j * 16 + c16;
         float v = acc[i][j][r];
         if (EPI) {
           if (g.bias) v += g.bias[col];
@@ -146,6 +174,49 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
         }
         g.C[(int64_t)row * g.ldc + col] = v;
       }
+    }
+}
+
+// Weight gradients dW[M][N] += A^T B (A = activations [K][M], B = output gradients [K][N], K = B*T
+// rows) for every weight of the step in one launch: a table of jobs, each M/64 x N/BN tiles x
+// ksplit slices of K; slice partial sums are added with fp32 atomics (dW is zeroed per step).
+struct WgJob {
+  const float* A; const float* B; float* C;
+  int64_t lda, ldb, ldc;
+  int32_t M, N, K, tiles_n, tiles, ksplit, kchunk, first;
+};
+static_assert(sizeof(WgJob) == 6 * 8 + 8 * 4, "WgJob layout");
+
+template <int BN>
+__global__ __launch_bounds__(256) void gemm_f32_wgrad_kernel(const WgJob* __restrict__ jobs, int njobs) {
+  __shared__ __attribute__((aligned(16))) float As[GR_BM * GR_LDK];
+  __shared__ __attribute__((aligned(16))) float Bs[BN * GR_LDK];
+  constexpr int WN = BN / 2, NJ = WN / 16;
+  const int bid = blockIdx.x;
+  int j = 0;
+  while (j + 1 < njobs && jobs[j + 1].first <= bid) ++j;
+  const WgJob jb = jobs[j];
+  int t = bid - jb.first;
+  const int sl = t / jb.tiles;   // slice-major: the blocks of one slice cover every tile of the job
+  t -= sl * jb.tiles;
+  const int m0 = (t / jb.tiles_n) * GR_BM, n0 = (t % jb.tiles_n) * BN;
+  const int kbeg = sl * jb.kchunk, kend = min(jb.K, kbeg + jb.kchunk);
+  f32x4 acc[2][NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < NJ; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gr_mainloop<true, false, BN>(jb.A, jb.lda, jb.B, jb.ldb, jb.M, m0, n0, kbeg, kend, As, Bs, acc);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+  const int g4 = lane >> 4, c16 = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wm * 32 + i * 16 + 4 * g4 + r;
+#pragma unroll
+      for (int q = 0; q < NJ; ++q)
+        atomicAdd(jb.C + (int64_t)row * jb.ldc + n0 + wn * WN + q * 16 + c16, acc[i][q][r]);
     }
 }
 
@@ -171,7 +242,7 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
   GrArgs g = {};
   g.A = A; g.B = B; g.C = C; g.bias = bias; g.res = res; g.aux = aux; g.seed = seed;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldr = ldr; g.ldaux = ldaux;
-  g.M = (int)M; g.N = (int)N; g.K = (int)K; g.act = act; g.site = (int)site; g.tiles_n = (int)(N / GR_BN);
+  g.M = (int)M; g.N = (int)N; g.K = (int)K; g.act = act; g.site = (int)site;
   g.thresh = 0; g.dscale = 1.f; g.res_scale = res_scale;
   if (rate > 0.f) {   // as drop_params (elementwise.hip)
     const double t = (double)rate * 4294967296.0;
@@ -179,14 +250,38 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
     g.dscale = 1.f / (1.f - rate);
   }
   const bool epi = bias || act || res || g.thresh;
-  const unsigned blocks = (unsigned)(((M + GR_BM - 1) / GR_BM) * g.tiles_n);
+  // 64 x 128 panels, or 64 x 64 when the 128-wide grid would leave fewer than two workgroups per
+  // CU (the N = 128 products: one workgroup per CU cannot hide its own load / epilogue latency)
+  const int64_t mt = (M + GR_BM - 1) / GR_BM;
+  const bool narrow = mt * (N / 128) < 512;
+  g.tiles_n = (int)(N / (narrow ? 64 : 128));
+  const unsigned blocks = (unsigned)(mt * g.tiles_n);
   hipStream_t s = (hipStream_t)stream;
-  if (tb) {
-    if (epi) hipLaunchKernelGGL((gemm_f32_rows_kernel<true, true>), dim3(blocks), dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((gemm_f32_rows_kernel<true, false>), dim3(blocks), dim3(256), 0, s, g);
+#define GR_LAUNCH(TBv, EPv, BNv) hipLaunchKernelGGL((gemm_f32_rows_kernel<TBv, EPv, BNv>), dim3(blocks), dim3(256), 0, s, g)
+  if (narrow) {
+    if (tb) { if (epi) GR_LAUNCH(true, true, 64); else GR_LAUNCH(true, false, 64); }
+    else { if (epi) GR_LAUNCH(false, true, 64); else GR_LAUNCH(false, false, 64); }
   } else {
-    if (epi) hipLaunchKernelGGL((gemm_f32_rows_kernel<false, true>), dim3(blocks), dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((gemm_f32_rows_kernel<false, false>), dim3(blocks), dim3(256), 0, s, g);
+    if (tb) { if (epi) GR_LAUNCH(true, true, 128); else GR_LAUNCH(true, false, 128); }
+    else { if (epi) GR_LAUNCH(false, true, 128); else GR_LAUNCH(false, false, 128); }
   }
+#undef GR_LAUNCH
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_gemm_f32_wgrad_job_size(void) { return (int)sizeof(WgJob); }
+
+// jobs_dev: njobs WgJob records (host-packed; first = prefix sum of tiles * ksplit, every job with
+// M % 64 == 0, N % 64 == 0, K % 64 == 0, kchunk % 64 == 0, 16-B aligned operands, ld % 4 == 0),
+// all of one panel width bn (64 or 128; N % bn == 0)
+extern "C" int pcv_gemm_f32_wgrad(const void* jobs_dev, int njobs, int64_t total_blocks, int bn, void* stream) {
+  if (!jobs_dev || njobs <= 0 || total_blocks <= 0 || total_blocks >= (1ll << 31) || (bn != 64 && bn != 128))
+    return PCV_EINVAL;
+  if (bn == 64)
+    hipLaunchKernelGGL((gemm_f32_wgrad_kernel<64>), dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const WgJob*)jobs_dev, njobs);
+  else
+    hipLaunchKernelGGL((gemm_f32_wgrad_kernel<128>), dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const WgJob*)jobs_dev, njobs);
   return pcv_launch_status();
 }

@@ -70,6 +70,8 @@ SIGNATURES = {
     "pcv_vit_embed_bwd_f32": [P, P, P, P, I32, I32, I32, F32, P, U32, P],
     "pcv_gemm_f32_rows_ok": [I64, I64, I64, P, I64, P, I64, I32],
     "pcv_gemm_f32_rows": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32, P],
+    "pcv_gemm_f32_wgrad_job_size": [],
+    "pcv_gemm_f32_wgrad": [P, I32, I64, I32, P],
     "pcv_attn_fused_f32_ok": [I32, I32],
     "pcv_attn_fwd_f32": [P, I64, P, I64, P, P, I32, I32, I32, I32, P, F32, P],
     "pcv_attn_bwd_f32": [P, I64, P, I64, P, I64, P, P, P, I64, I32, I32, I32, I32, P, F32, P],

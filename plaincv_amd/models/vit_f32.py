@@ -19,7 +19,7 @@ import torch
 from .. import hip
 from .. import kernels as K
 from ..hip import ptr, stream_ptr
-from ..optim.precond import GemmF32
+from ..optim.precond import GemmF32, WgradF32
 
 SITE_EMBED = 1
 
@@ -226,17 +226,22 @@ class ViTRunnerF32:
         # every weight gradient (K = B*T rows) in one grouped launch at the end of backward
         # (split-K: a [D, N] gradient is only a few 64x64 tiles, so each tile's K = B*T sum is cut
         # into ~1024-long slices accumulated with fp32 atomics -- ~2k workgroups instead of 138)
-        wg = GemmF32()
-        ks = lambda t: max(1, t.shape[0] // 1024)  # noqa: E731
-        wg.add(self.yf, self.dlogits, self.gWh, ta=True, beta=1.0, ksplit=ks(self.yf))
-        wg.add(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0, ksplit=ks(self.patches))
+        # The layer weights go to the row-panel wgrad kernel (csrc/gemm_f32.hip) when their shapes fit,
+        # the rest (head, patch conv, odd widths) to the grouped fp32 GEMM
+        wg, wr = GemmF32(), WgradF32()
+        ks = lambda t: max(1, t.shape[0] // 256)  # noqa: E731   (few tiles: a deep K split)
+        prods = [(self.yf, self.dlogits, self.gWh), (self.patches, self.dpatch, self.gWconv)]
         for i in range(L):
             w = self.w[i]
-            wg.add(self.a[i], self.dmo_l[i], w["gW1"], ta=True, beta=1.0, ksplit=ks(self.a[i]))
-            wg.add(self.y1[i], self.da_l[i], w["gW0"], ta=True, beta=1.0, ksplit=ks(self.y1[i]))
-            wg.add(self.o[i], self.dx1_l[i], w["gWo"], ta=True, beta=1.0, ksplit=ks(self.o[i]))
-            wg.add(self.y0[i], self.dqkv_l[i], w["gWqkv"], ta=True, beta=1.0, ksplit=ks(self.y0[i]))
-        self.g_wgrad = f(wg)
+            prods += [(self.a[i], self.dmo_l[i], w["gW1"]), (self.y1[i], self.da_l[i], w["gW0"]),
+                      (self.o[i], self.dx1_l[i], w["gWo"]), (self.y0[i], self.dqkv_l[i], w["gWqkv"])]
+        for a, b, c in prods:
+            if WgradF32.fits(a, b, c) and os.environ.get("PCV_F32_WGRAD_ROWS", "1") != "0":
+                wr.add(a, b, c)
+            else:
+                wg.add(a, b, c, ta=True, beta=1.0, ksplit=ks(a))
+        self.g_wgrad_parts = [f(x) for x in (wg, wr) if x.jobs]
+        self.g_wgrad = self.g_wgrad_parts[-1]
 
     def _mask(self, i):
         w = self.mask_words
@@ -345,7 +350,8 @@ class ViTRunnerF32:
         hip.call("pcv_vit_embed_bwd_f32", ptr(dx_in), ptr(self.dpatch), ptr(self.gcls), ptr(self.gpos), B, T, D,
                  float(rate), ptr(seed), SITE_EMBED, stream_ptr())
         K.colsum(self.dpatch, self.gbconv)
-        self.g_wgrad.run()
+        for part in self.g_wgrad_parts:
+            part.run()
 
     def flops_per_step(self):
         B, T, D, M, Kc = self.B, self.T, self.D, self.M, self.Kc

@@ -112,6 +112,53 @@ class GemmF32:
             hip.call("pcv_gemm_f32_grouped", ptr(dev), n, total, vec, s)
 
 
+class WgradF32:
+    """One launch of every fp32 weight gradient C += A^T B (A [K][M] activations, B [K][N] output
+    gradients, K = token rows) on the row-panel kernel of csrc/gemm_f32.hip: 64 x 128 panels, K
+    split into slices accumulated with fp32 atomics (``target_blocks`` workgroups in total).
+    ``fits(a, b, c)`` says whether a product can join (M, N % 64 / 128, K % 64, 16-B aligned)."""
+
+    FMT = "<3Q3q8i"
+    BN = 128
+
+    def __init__(self, target_blocks=2048):
+        self.jobs, self.target = [], int(target_blocks)
+
+    @classmethod
+    def fits(cls, a, b, c):
+        K, M = a.shape
+        N = b.shape[1]
+        return (b.shape[0] == K and tuple(c.shape) == (M, N) and M % 64 == 0 and N % cls.BN == 0 and K % 64 == 0
+                and all(t.dtype == torch.float32 and t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
+                        for t in (a, b, c)))
+
+    def add(self, a, b, c):
+        if not self.fits(a, b, c):
+            raise ValueError(f"wgrad_f32 job does not fit: A {tuple(a.shape)} B {tuple(b.shape)} C {tuple(c.shape)}")
+        self.jobs.append((a, b, c))
+        return self
+
+    def finalize(self, device):
+        lib = hip.load()
+        assert lib.pcv_gemm_f32_wgrad_job_size() == struct.calcsize(self.FMT)
+        tiles = [(a.shape[1] // 64) * (b.shape[1] // self.BN) for a, b, _ in self.jobs]
+        chunks = max(1, -(-sum(tiles) * max(a.shape[0] // 64 for a, _, _ in self.jobs) // self.target))
+        recs, first = [], 0
+        for (a, b, c), t in zip(self.jobs, tiles):
+            K = a.shape[0]
+            kchunk = 64 * min(chunks, K // 64)
+            ksplit = -(-K // kchunk)
+            recs.append((a.data_ptr(), b.data_ptr(), c.data_ptr(), a.stride(0), b.stride(0), c.stride(0),
+                         a.shape[1], b.shape[1], K, b.shape[1] // self.BN, t, ksplit, kchunk, first))
+            first += t * ksplit
+        self.total = first
+        self.table = _pack(recs, self.FMT).to(device)
+        return self
+
+    def run(self):
+        hip.call("pcv_gemm_f32_wgrad", ptr(self.table), len(self.jobs), self.total, self.BN, stream_ptr())
+
+
 class NewtonRoot:
     """P = (L + shift I)^(-1/p) for a batch of symmetric positive definite matrices by the coupled
     Newton iteration (csrc/precond.hip), p in {1, 2, 4}: one init launch, then per iteration

@@ -98,6 +98,25 @@ def test_gemm_f32_split_k(dev, M, N, K, ks, ta, tb):
         GemmF32().add(a, b, c, ta=bool(ta), tb=bool(tb), beta=0.0, ksplit=ks)
 
 
+def test_wgrad_f32_grouped(dev):
+    """row-panel weight-gradient launch (csrc/gemm_f32.hip): several C += A^T B jobs with K = 16448
+    token rows, split-K slices added with atomics, vs fp64"""
+    from plaincv_amd.optim.precond import WgradF32
+    g = torch.Generator().manual_seed(11)
+    plan, refs = WgradF32(target_blocks=700), []
+    for (M, N, K) in [(128, 384, 16448), (256, 128, 16448), (64, 128, 640), (128, 256, 1024)]:
+        a = torch.randn(K, M, generator=g).to(dev)
+        b = torch.randn(K, N, generator=g).to(dev)
+        c = torch.randn(M, N, generator=g).to(dev)
+        refs.append((c, c.double() + a.double().t() @ b.double(), (a.abs().double().t() @ b.abs().double()).max().item()))
+        plan.add(a, b, c)
+    assert not WgradF32.fits(torch.zeros(64, 48, device=dev), torch.zeros(64, 128, device=dev), torch.zeros(48, 128, device=dev))
+    plan.finalize(dev).run()
+    torch.cuda.synchronize()
+    for c, ref, scale in refs:
+        assert (c.double() - ref).abs().max().item() <= 2e-6 * scale
+
+
 def _spd(n, rank, g, dev, scale=1.0):
     x = torch.randn(n, rank, generator=g, dtype=torch.float64) * scale
     return (x @ x.t()).float().to(dev)
