@@ -32,9 +32,12 @@ struct GrArgs {
   float dscale, res_scale;
 };
 
+// GELU (tanh form): 0.5 x (1 + tanh(u)) = x / (1 + exp(-2u)), u = sqrt(2/pi) (x + 0.044715 x^3) --
+// one exp and one division instead of tanhf's polynomial (the same function; the sigmoid form
+// also avoids the 1 + tanh(u) cancellation for very negative x)
 __device__ __forceinline__ float gr_gelu(float x) {
-  const float k = 0.7978845608028654f;   // sqrt(2/pi); as f32_epilogue_kernel (vit_f32.hip)
-  return 0.5f * x * (1.f + tanhf(k * (x + 0.044715f * x * x * x)));
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return x / (1.f + expf(-2.f * u));
 }
 
 // Main loop shared by the row GEMM and the weight-gradient GEMM: acc += op(A)[m0.., kbeg:kend] .
@@ -139,8 +142,11 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
 
 template <bool TB, bool EPI, int BN>
 __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
-  __shared__ __attribute__((aligned(16))) float As[GR_BM * GR_LDK];
-  __shared__ __attribute__((aligned(16))) float Bs[BN * GR_LDK];
+  // operand images during the main loop; the C tile [64][BN + 4] for the epilogue afterwards
+  __shared__ __attribute__((aligned(16))) float smem[(GR_BM + BN) * GR_LDK];
+  static_assert(GR_BM * (BN + 4) <= (GR_BM + BN) * GR_LDK, "C tile fits the operand images");
+  float* As = smem;
+  float* Bs = smem + GR_BM * GR_LDK;
   constexpr int WN = BN / 2, NJ = WN / 16;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
   const int g4 = lane >> 4, c16 = lane & 15;
@@ -152,29 +158,41 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   gr_mainloop<false, TB, BN>(g.A, g.lda, g.B, g.ldb, g.M, m0, n0, 0, g.K, As, Bs, acc);
-  const uint32_t seed = (EPI && g.thresh) ? *g.seed : 0u;
+  // C tile through LDS, so the epilogue streams rows as float4: 16-B loads of bias / residual and
+  // 16-B stores of C (and of the GELU pre-activation)
+  constexpr int LDC = BN + 4;
+  __syncthreads();
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = m0 + wm * 32 + i * 16 + 4 * g4 + r;
-      if (row >= g.M) continue;
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int col = n0 + wn * WN + j * 16 + c16;
-        float v = acc[i][j][r];
-        if (EPI) {
-          if (g.bias) v += g.bias[col];
-          if (g.act) {
-            if (g.aux) g.aux[(int64_t)row * g.ldaux + col] = v;
-            v = gr_gelu(v);
-          }
-          if (g.thresh) v = hash3(seed, (uint32_t)g.site, (uint32_t)((int64_t)row * g.N + col)) >= g.thresh ? v * g.dscale : 0.f;
-          if (g.res) v += g.res_scale * g.res[(int64_t)row * g.ldr + col];
-        }
-        g.C[(int64_t)row * g.ldc + col] = v;
+      for (int j = 0; j < NJ; ++j) smem[(wm * 32 + i * 16 + 4 * g4 + r) * LDC + wn * WN + j * 16 + c16] = acc[i][j][r];
+  __syncthreads();
+  const uint32_t seed = (EPI && g.thresh) ? *g.seed : 0u;
+  constexpr int Q = BN / 4;
+#pragma unroll
+  for (int it = 0; it < GR_BM * Q / 256; ++it) {
+    const int idx = threadIdx.x + 256 * it, rl = idx / Q, cl = (idx % Q) * 4;
+    const int row = m0 + rl, col = n0 + cl;
+    if (row >= g.M) continue;
+    f32x4 v = *reinterpret_cast<const f32x4*>(&smem[rl * LDC + cl]);
+    if (EPI) {
+      if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + col);
+      if (g.act) {
+        if (g.aux) *reinterpret_cast<f32x4*>(g.aux + (int64_t)row * g.ldaux + col) = v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gr_gelu(v[e]);
       }
+      if (g.thresh) {
+        const uint32_t base = (uint32_t)((int64_t)row * g.N + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = hash3(seed, (uint32_t)g.site, base + e) >= g.thresh ? v[e] * g.dscale : 0.f;
+      }
+      if (g.res) v += g.res_scale * *reinterpret_cast<const f32x4*>(g.res + (int64_t)row * g.ldr + col);
     }
+    *reinterpret_cast<f32x4*>(g.C + (int64_t)row * g.ldc + col) = v;
+  }
 }
 
 // Weight gradients dW[M][N] += A^T B (A = activations [K][M], B = output gradients [K][N], K = B*T
@@ -239,6 +257,10 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
   if (!A || !B || !C || !pcv_gemm_f32_rows_ok(M, N, K, A, lda, B, ldb, tb) || ldc < N || (act && aux && ldaux < N) ||
       (res && ldr < N) || rate < 0.f || rate >= 1.f || (rate > 0.f && !seed))
     return PCV_EINVAL;
+  // the epilogue moves float4 rows: 16-B aligned C / aux / res / bias and row strides % 4
+  if (!gr_al(C) || (ldc & 3) || (aux && (!gr_al(aux) || (ldaux & 3))) || (res && (!gr_al(res) || (ldr & 3))) ||
+      (bias && !gr_al(bias)))
+    return PCV_EALIGN;
   GrArgs g = {};
   g.A = A; g.B = B; g.C = C; g.bias = bias; g.res = res; g.aux = aux; g.seed = seed;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldr = ldr; g.ldaux = ldaux;

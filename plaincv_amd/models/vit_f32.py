@@ -63,8 +63,10 @@ class _Dense:
         self.bias, self.res, self.aux, self.act, self.site, self.dropout = bias, res, aux, act, site, dropout
         M, K = a.shape
         self.M, self.N, self.K = M, c.shape[1], K
-        self.fused = bool(hip.load().pcv_gemm_f32_rows_ok(M, self.N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
-                                                          int(tb)))
+        al = all(t is None or (t.data_ptr() % 16 == 0 and (t.dim() == 1 or t.stride(0) % 4 == 0))
+                 for t in (c, aux, res, bias))
+        self.fused = al and bool(hip.load().pcv_gemm_f32_rows_ok(M, self.N, K, ptr(a), a.stride(0), ptr(b),
+                                                                 b.stride(0), int(tb)))
         self.plan = None if self.fused else GemmF32().add(a, b, c, tb=tb).finalize(c.device)
         self.epi = bias is not None or res is not None or act or dropout
 
