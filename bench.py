@@ -38,7 +38,6 @@ sys.path.insert(0, ROOT)
 from plaincv_amd.engine import GraphedTrainStep, create_train_state  # noqa: E402
 from plaincv_amd.engine import data_parallel as dp  # noqa: E402
 from plaincv_amd.models.vit_small import VisionTransformer  # noqa: E402
-from plaincv_amd.optim.precond import GemmF32  # noqa: E402
 from utils import Config  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
@@ -170,20 +169,18 @@ def vit_roofline(state, image_shape):
             "bytes_per_launch": [b1, b2]}
 
 
-def vit_roofline_f32(state, image_shape):
-    """fp32 ViT path: the weight-gradient launch (every dW = X^T dY of the step, K = B*T rows, one
-    grouped exact-fp32 MFMA launch) -- the largest single launch of the fp32 step -- against the
-    fp32 MFMA peak; FLOPs = 2 K sum(M N) over its jobs, timed live on its stream."""
+def vit_roofline_f32(state, image_shape, rate):
+    """fp32 ViT path: the dominant kernel of the step is the fused fp32 attention backward
+    (attn_bwd_f32_kernel, one launch per layer): its algorithmic FLOPs are the five T x T x Dh
+    products of a (batch, head) -- the score recompute, dPd = dO V^T, dV, dK, dQ -- 5 * 2 * T^2 * Dh
+    per (batch, head), timed live on layer 0 against the fp32 MFMA peak (157.3 TF/s)."""
     r = state.runner_for(image_shape)
-    g = r.g_wgrad
-    t = timed_kernel(lambda: g.run())
-    flops = 0
-    for j in g.jobs:   # GemmF32 job dicts or WgradF32 (A [K][M], B [K][N], C) triples
-        flops += 2 * j["M"] * j["N"] * j["K"] if isinstance(j, dict) else 2 * j[0].shape[1] * j[1].shape[1] * j[0].shape[0]
+    if not getattr(r, "fused_attn", False):
+        return None
+    t = timed_kernel(lambda: r.attn_bwd(0, rate))
+    flops = 5 * 2 * r.B * r.H * r.T * r.T * r.Dh
     ach = flops / t / 1e12
-    name = ("gemm_f32_grouped (weight gradients of the fp32 step, one launch)" if isinstance(g, GemmF32) else
-            "gemm_f32_wgrad_kernel<128> (the layer weight gradients of the fp32 step, one launch, split-K)")
-    return {"kernel": name, "bound": "mfma",
+    return {"kernel": "attn_bwd_f32_kernel<dropout> (fused fp32 attention backward of one layer)", "bound": "mfma",
             "achieved": round(ach, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / F32_PEAK_TFLOPS, 4), "traffic": None, "launch_us": round(t * 1e6, 2),
             "flops_per_launch": flops}
@@ -289,7 +286,8 @@ def bench_vit(args):
                           "optimizer": cfg.optim, "parallelism": f"dp{world}"},
                "steps_per_sec": round(sps, 3), "tflops_per_gpu": round(flops * sps / 1e12, 3),
                "final_loss": round(loss, 4)}
-        out["roofline"] = vit_roofline_f32(state, shape) if cfg.vit_dtype == "float32" else vit_roofline(state, shape)
+        out["roofline"] = (vit_roofline_f32(state, shape, cfg.vit_dropout) if cfg.vit_dtype == "float32"
+                           else vit_roofline(state, shape))
         if world > 1:
             out["grad_allreduce"] = None   # filled below (collective: every rank takes part)
         if world == 1 and not args.no_cpu_baseline:

@@ -215,6 +215,20 @@ __device__ __forceinline__ void fa_row8(const float* X, int r, int g, float (&x)
   for (int j = 0; j < 4; ++j) { x[j] = a[j]; x[4 + j] = b[j]; }
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Products whose output rows are the head dimension (O^T, dQ^T, dK^T, dV^T) use two 16-row MFMA
+// tiles with the rows INTERLEAVED: tile dd holds d = 2i + dd, so a lane's A operand for both tiles
+// is one 8-B read X[row][2c .. 2c+1] and its outputs acc[dd][r] (d = 8g + 2r + dd) are 8
+// consecutive columns -- two 16-B stores.
+__device__ __forceinline__ f32x2 fa_pair(const float* X, int r, int c16) {
+  return *reinterpret_cast<const f32x2*>(X + fa_off(r, 2 * c16));
+}
+__device__ __forceinline__ void fa_store8(float* dst, const f32x4 (&acc)[2], float scale) {
+  *reinterpret_cast<f32x4*>(dst) = f32x4{acc[0][0], acc[1][0], acc[0][1], acc[1][1]} * scale;
+  *reinterpret_cast<f32x4*>(dst + 4) = f32x4{acc[0][2], acc[1][2], acc[0][3], acc[1][3]} * scale;
+}
+
 // the keep words of query rows [0, 16 * ceil(T/16)) (drop_word layout, shared by batch and heads)
 __host__ __device__ __forceinline__ int fa_mask_words(int T) { return ((T + 15) / 16) * 2 * ((T + 127) / 128) * 64; }
 __device__ __forceinline__ void fa_load_mask(uint16_t* dst, const uint16_t* src, int T) {
@@ -282,7 +296,7 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
       cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
       cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
       const float mnew = fmaxf(m, cmax);
-      const float alpha = expf(m - mnew);   // 0 on the first chunk (m = -inf)
+      const float alpha = __expf(m - mnew);   // 0 on the first chunk (m = -inf)
       m = mnew;
       l *= alpha;
       o[0] *= alpha;
@@ -294,13 +308,12 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
           if (DROP && qv) w = mk[f32_drop_word(q, (k0 + t) * 16 + 4 * g, a.n64)] >> ((q & 3) * 4);
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
-            float p = expf(st[t][s] - m);
+            float p = __expf(st[t][s] - m);
             l += p;
             if (DROP) p = ((w >> s) & 1u) ? p : 0.f;
-            const int key = (k0 + t) * 16 + 4 * g + s;
-#pragma unroll
-            for (int d = 0; d < 2; ++d)
-              o[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(Vs[fa_off(key, 16 * d + c16)], p, o[d], 0, 0, 0);
+            const f32x2 v2 = fa_pair(Vs, (k0 + t) * 16 + 4 * g + s, c16);
+            o[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v2[0], p, o[0], 0, 0, 0);
+            o[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v2[1], p, o[1], 0, 0, 0);
           }
         }
       }
@@ -310,9 +323,7 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
     const float inv = 1.f / l;
     const float os = DROP ? inv * a.dscale : inv;
     if (qv) {
-#pragma unroll
-      for (int d = 0; d < 2; ++d)   // o[d][r] = O^T[16d + 4g + r][q]
-        *reinterpret_cast<f32x4*>(a.out + (bT + q) * a.ldo + h * FA_DH + 16 * d + 4 * g) = o[d] * os;
+      fa_store8(a.out + (bT + q) * a.ldo + h * FA_DH + 8 * g, o, os);   // o[dd][r] = O^T[8g + 2r + dd][q]
       if (g == 0) {
         a.mrow[bh * T + q] = m;
         a.linv[bh * T + q] = inv;
@@ -374,23 +385,29 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
       fa_row8(Ks, key, g, kf);
       fa_row8(Vs, key, g, vf);
       f32x4 dv[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, dk[2] = {dv[0], dv[0]};
+      float qa[8], oa[8];
+      fa_row8(Qs, c16, g, qa);
+      fa_row8(Os, c16, g, oa);
       for (int qb = 0; qb < NB; ++qb) {
-        float qa[8], oa[8];
-        fa_row8(Qs, qb * 16 + c16, g, qa);
-        fa_row8(Os, qb * 16 + c16, g, oa);
         f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = sv;
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
           sv = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[s], kf[s], sv, 0, 0, 0);   // S[q 4g+r][key]
           dp = __builtin_amdgcn_mfma_f32_16x16x4f32(oa[s], vf[s], dp, 0, 0, 0);   // dPd[q][key]
         }
+        if (qb + 1 < NB) {   // next query block's fragments under this block's MFMAs
+          fa_row8(Qs, (qb + 1) * 16 + c16, g, qa);
+          fa_row8(Os, (qb + 1) * 16 + c16, g, oa);
+        }
+        const int q0 = qb * 16 + 4 * g;
+        const f32x4 m4 = *reinterpret_cast<const f32x4*>(Ms + q0), i4 = *reinterpret_cast<const f32x4*>(Is + q0);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(Dl + q0);
         uint32_t w = 0xFFFFu;
-        if (DROP && key < T) w = mk[f32_drop_word(qb * 16 + 4 * g, key, a.n64)] >> (key & 3);
+        if (DROP && key < T) w = mk[f32_drop_word(q0, key, a.n64)] >> (key & 3);
         float pd[4], ds[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int ql = qb * 16 + 4 * g + r;
-          const float p = expf(sv[r] * a.scale - Ms[ql]) * Is[ql];
+          const float p = __expf(sv[r] * a.scale - m4[r]) * i4[r];
           float pdv = p, dpv = dp[r];
           if (DROP) {
             const bool keep = (w >> (4 * r)) & 1u;
@@ -398,25 +415,21 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
             dpv = keep ? dpv * a.dscale : 0.f;
           }
           pd[r] = pdv;
-          ds[r] = p * (dpv - Dl[ql]);
+          ds[r] = p * (dpv - d4[r]);
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const int ql = qb * 16 + 4 * g + s;
-#pragma unroll
-          for (int d = 0; d < 2; ++d) {
-            dv[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(Os[fa_off(ql, 16 * d + c16)], pd[s], dv[d], 0, 0, 0);
-            dk[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(Qs[fa_off(ql, 16 * d + c16)], ds[s], dk[d], 0, 0, 0);
-          }
+          const f32x2 o2 = fa_pair(Os, q0 + s, c16), q2 = fa_pair(Qs, q0 + s, c16);
+          dv[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(o2[0], pd[s], dv[0], 0, 0, 0);
+          dv[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(o2[1], pd[s], dv[1], 0, 0, 0);
+          dk[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(q2[0], ds[s], dk[0], 0, 0, 0);
+          dk[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(q2[1], ds[s], dk[1], 0, 0, 0);
         }
       }
-      if (key < T) {
-        float* dst = a.dqkv + (bT + key) * a.lddqkv + h * FA_DH;
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {   // dv[d][r] = dV^T[16d + 4g + r][key]
-          *reinterpret_cast<f32x4*>(dst + 2 * a.D + 16 * d + 4 * g) = dv[d];
-          *reinterpret_cast<f32x4*>(dst + a.D + 16 * d + 4 * g) = dk[d] * a.scale;
-        }
+      if (key < T) {   // dv[dd][r] = dV^T[8g + 2r + dd][key]
+        float* dst = a.dqkv + (bT + key) * a.lddqkv + h * FA_DH + 8 * g;
+        fa_store8(dst + 2 * a.D, dv, 1.f);
+        fa_store8(dst + a.D, dk, a.scale);
       }
     }
   } else {
@@ -429,15 +442,19 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
       fa_row8(Os, q, g, of);
       const float mq = Ms[q], iq = Is[q], dq = Dl[q];
       f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      float ka[8], va[8];
+      fa_row8(Ks, c16, g, ka);
+      fa_row8(Vs, c16, g, va);
       for (int kb = 0; kb < NB; ++kb) {
-        float ka[8], va[8];
-        fa_row8(Ks, kb * 16 + c16, g, ka);
-        fa_row8(Vs, kb * 16 + c16, g, va);
         f32x4 st = {0.f, 0.f, 0.f, 0.f}, dpt = st;
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
           st = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[s], qf[s], st, 0, 0, 0);    // S^T[key 4g+r][q]
           dpt = __builtin_amdgcn_mfma_f32_16x16x4f32(va[s], of[s], dpt, 0, 0, 0);  // dPd^T
+        }
+        if (kb + 1 < NB) {
+          fa_row8(Ks, (kb + 1) * 16 + c16, g, ka);
+          fa_row8(Vs, (kb + 1) * 16 + c16, g, va);
         }
         uint32_t w = 0xFFFFu;
         if (DROP && q < T) w = mk[f32_drop_word(q, kb * 16 + 4 * g, a.n64)] >> ((q & 3) * 4);
@@ -445,24 +462,19 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = kb * 16 + 4 * g + r;
-          const float p = key < T ? expf(st[r] * a.scale - mq) * iq : 0.f;
+          const float p = key < T ? __expf(st[r] * a.scale - mq) * iq : 0.f;
           float dpv = dpt[r];
           if (DROP) dpv = ((w >> r) & 1u) ? dpv * a.dscale : 0.f;
           ds[r] = p * (dpv - dq);
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const int key = kb * 16 + 4 * g + s;
-#pragma unroll
-          for (int d = 0; d < 2; ++d)
-            acc[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ks[fa_off(key, 16 * d + c16)], ds[s], acc[d], 0, 0, 0);
+          const f32x2 k2 = fa_pair(Ks, kb * 16 + 4 * g + s, c16);
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(k2[0], ds[s], acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(k2[1], ds[s], acc[1], 0, 0, 0);
         }
       }
-      if (q < T) {
-#pragma unroll
-        for (int d = 0; d < 2; ++d)
-          *reinterpret_cast<f32x4*>(a.dqkv + (bT + q) * a.lddqkv + h * FA_DH + 16 * d + 4 * g) = acc[d] * a.scale;
-      }
+      if (q < T) fa_store8(a.dqkv + (bT + q) * a.lddqkv + h * FA_DH + 8 * g, acc, a.scale);
     }
   }
 }

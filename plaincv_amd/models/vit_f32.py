@@ -245,6 +245,14 @@ class ViTRunnerF32:
         self.g_wgrad_parts = [f(x) for x in (wg, wr) if x.jobs]
         self.g_wgrad = self.g_wgrad_parts[-1]
 
+    def attn_bwd(self, i, rate):
+        """Layer i's fused attention backward: dq | dk | dv of dqkv_l[i] from qkv, o, dO and the
+        forward's row statistics (one launch)."""
+        B, T, D = self.B, self.T, self.D
+        hip.call("pcv_attn_bwd_f32", ptr(self.qkv[i]), 3 * D, ptr(self.o[i]), D, ptr(self.dO), D,
+                 ptr(self.mrow[i]), ptr(self.linv[i]), ptr(self.dqkv_l[i]), 3 * D, B, T, self.H, D,
+                 ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
+
     def _mask(self, i):
         w = self.mask_words
         return self.attn_mask[i * w:(i + 1) * w]
@@ -333,9 +341,7 @@ class ViTRunnerF32:
             K.colsum(dx1, w["gbo"])
             g["out_d"].run()                                                           # self.dO = dx1 Wo^T
             if self.fused_attn:                                                        # dQ, dK, dV
-                hip.call("pcv_attn_bwd_f32", ptr(self.qkv[i]), 3 * D, ptr(self.o[i]), D, ptr(self.dO), D,
-                         ptr(self.mrow[i]), ptr(self.linv[i]), ptr(dqkv), 3 * D, B, T, self.H, D,
-                         ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
+                self.attn_bwd(i, rate)
             else:
                 g["dpv"].run()                                                         # dPd -> S, dV
                 hip.call("pcv_attn_softmax_bwd_f32", ptr(self.P[i]), ptr(self.S), self.S.shape[0], T,
