@@ -180,10 +180,11 @@ def vit_roofline_f32(state, image_shape, rate):
     t = timed_kernel(lambda: r.attn_bwd(0, rate))
     flops = 5 * 2 * r.B * r.H * r.T * r.T * r.Dh
     ach = flops / t / 1e12
+    traffic, tsrc = pmc_traffic("attn_bwd_f32_kernel<true>")
     return {"kernel": "attn_bwd_f32_kernel<dropout> (fused fp32 attention backward of one layer)", "bound": "mfma",
             "achieved": round(ach, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(ach / F32_PEAK_TFLOPS, 4), "traffic": None, "launch_us": round(t * 1e6, 2),
-            "flops_per_launch": flops}
+            "frac": round(ach / F32_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
+            "traffic_source": tsrc, "launch_us": round(t * 1e6, 2), "flops_per_launch": flops}
 
 
 def cpu_baseline_vit(cfg, seconds=12.0):
