@@ -239,7 +239,8 @@ int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls, float* dp
                           const uint32_t* seed, uint32_t site, void* stream);
 /* Exact-fp32 row-panel GEMM with the Dense epilogue fused (csrc/gemm_f32.hip): C[M][N] =
  * dropout(act(A[M][K] op(B) + bias)) + res_scale * res, op(B) = B [K][N] (tb = 0) or B^T with B
- * stored [N][K] (tb = 1); aux = the pre-activation when act = 1 (GELU tanh); dropout index row * N +
+ * stored [N][K] (tb = 1); aux = the pre-activation when act = 1 (GELU tanh); act = 2 is the backward of
+ * that MLP activation: C = dropout_vjp(A op(B)) * gelu'(aux) (aux read; no bias / res); dropout index row * N +
  * col (as pcv_f32_epilogue).  ok: N % 128 == 0, K % 64 == 0, 16-B aligned A / B, lda / ldb % 4 == 0. */
 int pcv_gemm_f32_rows_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb,
                          int tb);
@@ -248,8 +249,9 @@ int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, int64_t ldb, 
                       int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed, uint32_t site,
                       void* stream);
 /* Every fp32 weight gradient of a step in one launch (csrc/gemm_f32.hip): jobs_dev holds njobs
- * records (pcv_gemm_f32_wgrad_job_size() bytes) {A, B, C, lda, ldb, ldc, M, N, K, tiles_n, tiles,
- * ksplit, kchunk, first}: C[M][N] += A^T B with A [K][M], B [K][N] (K-major token rows), 64 x bn
+ * records (pcv_gemm_f32_wgrad_job_size() bytes) {A, B, C, colsum, lda, ldb, ldc, M, N, K, tiles_n,
+ * tiles, ksplit, kchunk, first} (colsum optional: += the column sums of B -- the Dense's bias
+ * gradient):  C[M][N] += A^T B with A [K][M], B [K][N] (K-major token rows), 64 x bn
  * panels x ksplit K slices added with fp32 atomics; first = prefix sum of tiles * ksplit.
  * Requires M % 64, N % bn, K % 64, kchunk % 64 == 0, 16-B aligned operands, ld % 4 == 0. */
 int pcv_gemm_f32_wgrad_job_size(void);

@@ -2,7 +2,8 @@
 // fp32 ViT's token-row products (flax Dense at models/vit_small.py:6-18 and the attention in/out
 // projections, fp32 as the reference computes them):
 //     C[M][N] = epi(A[M][K] op(B)),  op(B) = B [K][N] (TB = 0) or B^T with B stored [N][K] (TB = 1),
-//     epi(x) = dropout(act(x + bias)) + res_scale * res   (aux = x + bias when act = GELU),
+//     epi(x) = dropout(act(x + bias)) + res_scale * res   (aux = x + bias when act = 1, GELU),
+//     or, act = 2 (the GELU MLP's backward): epi(x) = dropout_vjp(x) * gelu'(aux),
 // the same element order and dropout index (row * N + col, hash3 of oracle/rng.py) as
 // pcv_f32_epilogue.  M = B*T token rows is large, K and N are the model widths (multiples of 64 /
 // 128), so one workgroup owns a 64 x 128 panel of C and walks K in 64-long chunks (LDS image +
@@ -39,6 +40,11 @@ __device__ __forceinline__ float gr_gelu(float x) {
   const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
   return x / (1.f + expf(-2.f * u));
 }
+__device__ __forceinline__ float gr_gelu_grad(float x) {   // as gelu_tanh_grad_f32 (vit_f32.hip)
+  const float k = 0.7978845608028654f;
+  const float t = tanhf(k * (x + 0.044715f * x * x * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
+}
 
 // Main loop shared by the row GEMM and the weight-gradient GEMM: acc += op(A)[m0.., kbeg:kend] .
 // op(B)[kbeg:kend, n0..] for one 64 x BN tile (waves 2 x 2, each 32 x BN/2).  Operand layouts:
@@ -51,7 +57,7 @@ __device__ __forceinline__ float gr_gelu(float x) {
 template <bool TA, bool TB, int BN>
 __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
                                             int64_t ldb, int M, int m0, int n0, int kbeg, int kend, float* As,
-                                            float* Bs, f32x4 (&acc)[2][BN / 32]) {
+                                            float* Bs, f32x4 (&acc)[2][BN / 32], float* colsum = nullptr) {
   constexpr int C4 = GR_BK / 4;                          // float4 per 64-long k row
   constexpr int NA = GR_BM * C4 / 256, NB = BN * C4 / 256;
   constexpr int WN = BN / 2, NJ = WN / 16;               // wave tile 32 x WN
@@ -113,10 +119,22 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
       fb[j] = *reinterpret_cast<const f32x4*>(&Bs[(wn * WN + j * 16 + c16) * GR_LDK + kk + 4 * g4]);
   };
   const int nk = (kend - kbeg) / GR_BK;
+  // column sums of the B chunks (colsum != nullptr): thread -> column n, a 64 / (256 / BN)-long
+  // k segment of each chunk's [n][k] image
+  constexpr int CS_SEG = GR_BK * BN / 256;
+  const int cs_n = tid % BN, cs_k = (tid / BN) * CS_SEG;
+  float cs = 0.f;
   gload(0);
   lstore();
   __syncthreads();
   for (int kc = 0; kc < nk; ++kc) {
+    if (colsum) {
+#pragma unroll
+      for (int e = 0; e < CS_SEG; e += 4) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(&Bs[cs_n * GR_LDK + cs_k + e]);
+        cs += (x[0] + x[1]) + (x[2] + x[3]);
+      }
+    }
     if (kc + 1 < nk) gload(kc + 1);
     f32x4 fa[2][2], fb[2][NJ];
     fload(0, fa[0], fb[0]);
@@ -138,6 +156,7 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
       __syncthreads();
     }
   }
+  if (colsum) atomicAdd(colsum + n0 + cs_n, cs);
 }
 
 template <bool TB, bool EPI, int BN>
@@ -179,12 +198,21 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
     f32x4 v = *reinterpret_cast<const f32x4*>(&smem[rl * LDC + cl]);
     if (EPI) {
       if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + col);
-      if (g.act) {
+      if (g.act == 2) {   // backward of dropout(gelu(pre)): keep bits, then gelu'(pre)
+        const f32x4 pre = *reinterpret_cast<const f32x4*>(g.aux + (int64_t)row * g.ldaux + col);
+        const uint32_t base = (uint32_t)((int64_t)row * g.N + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = v[e];
+          if (g.thresh) x = hash3(seed, (uint32_t)g.site, base + e) >= g.thresh ? x * g.dscale : 0.f;
+          v[e] = x * gr_gelu_grad(pre[e]);
+        }
+      } else if (g.act) {
         if (g.aux) *reinterpret_cast<f32x4*>(g.aux + (int64_t)row * g.ldaux + col) = v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = gr_gelu(v[e]);
       }
-      if (g.thresh) {
+      if (g.thresh && g.act != 2) {
         const uint32_t base = (uint32_t)((int64_t)row * g.N + col);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = hash3(seed, (uint32_t)g.site, base + e) >= g.thresh ? v[e] * g.dscale : 0.f;
@@ -198,12 +226,14 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
 // Weight gradients dW[M][N] += A^T B (A = activations [K][M], B = output gradients [K][N], K = B*T
 // rows) for every weight of the step in one launch: a table of jobs, each M/64 x N/BN tiles x
 // ksplit slices of K; slice partial sums are added with fp32 atomics (dW is zeroed per step).
+// colsum (optional): += the column sums of B (the bias gradient of the same Dense), accumulated by
+// the workgroups of the first 64-row panel from the B chunks they already hold in LDS.
 struct WgJob {
-  const float* A; const float* B; float* C;
+  const float* A; const float* B; float* C; float* colsum;
   int64_t lda, ldb, ldc;
   int32_t M, N, K, tiles_n, tiles, ksplit, kchunk, first;
 };
-static_assert(sizeof(WgJob) == 6 * 8 + 8 * 4, "WgJob layout");
+static_assert(sizeof(WgJob) == 7 * 8 + 8 * 4, "WgJob layout");
 
 template <int BN>
 __global__ __launch_bounds__(256) void gemm_f32_wgrad_kernel(const WgJob* __restrict__ jobs, int njobs) {
@@ -224,7 +254,8 @@ __global__ __launch_bounds__(256) void gemm_f32_wgrad_kernel(const WgJob* __rest
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int q = 0; q < NJ; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  gr_mainloop<true, false, BN>(jb.A, jb.lda, jb.B, jb.ldb, jb.M, m0, n0, kbeg, kend, As, Bs, acc);
+  gr_mainloop<true, false, BN>(jb.A, jb.lda, jb.B, jb.ldb, jb.M, m0, n0, kbeg, kend, As, Bs, acc,
+                               m0 == 0 ? jb.colsum : nullptr);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
   const int g4 = lane >> 4, c16 = lane & 15;
 #pragma unroll
@@ -254,7 +285,8 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
                                  int64_t ldc, int64_t M, int64_t N, int64_t K, const float* bias, float* aux,
                                  int64_t ldaux, const float* res, int64_t ldr, float res_scale, int act, float rate,
                                  const uint32_t* seed, uint32_t site, void* stream) {
-  if (!A || !B || !C || !pcv_gemm_f32_rows_ok(M, N, K, A, lda, B, ldb, tb) || ldc < N || (act && aux && ldaux < N) ||
+  if (!A || !B || !C || !pcv_gemm_f32_rows_ok(M, N, K, A, lda, B, ldb, tb) || act < 0 || act > 2 ||
+      (act == 2 && (!aux || bias || res)) || ldc < N || (act && aux && ldaux < N) ||
       (res && ldr < N) || rate < 0.f || rate >= 1.f || (rate > 0.f && !seed))
     return PCV_EINVAL;
   // the epilogue moves float4 rows: 16-B aligned C / aux / res / bias and row strides % 4

@@ -54,7 +54,8 @@ def _gemm(a, b, c, **kw):
 
 
 class _Dense:
-    """One token-row product c = epi(a op(b)) of the step: the fused row-panel GEMM of
+    """One token-row product c = epi(a op(b)) of the step (act = 2: the GELU-MLP backward,
+    c = dropout_vjp(a op(b)) * gelu'(aux)): the fused row-panel GEMM of
     csrc/gemm_f32.hip when the shape fits it (N % 128, K % 64), else a planned grouped-GEMM launch
     followed by the standalone epilogue kernel (same element order and dropout index)."""
 
@@ -80,7 +81,9 @@ class _Dense:
                      int(self.site), stream_ptr())
             return
         self.plan.run()
-        if self.epi:
+        if self.act == 2:   # backward of dropout(gelu(pre))
+            _epi_bwd(self.c, self.c, aux=self.aux, act=1, rate=rate, seed=seed, site=self.site)
+        elif self.epi:
             _epi(self.c, self.c, bias=self.bias, res=self.res, aux=self.aux, act=self.act, rate=rate, seed=seed,
                  site=self.site)
 
@@ -220,7 +223,8 @@ class ViTRunnerF32:
                            site=site_mlp_hidden(i), dropout=True),
                 fc2=_Dense(self.a[i], w["W1"], self.xs[i + 1], bias=w["b1"], res=self.x1s[i], site=site_mlp_out(i),
                            dropout=True)))
-            self.gb.append(dict(fc2_d=_Dense(self.dmo_l[i], w["W1"], self.da, tb=True),
+            self.gb.append(dict(fc2_d=_Dense(self.dmo_l[i], w["W1"], self.da_l[i], tb=True, aux=self.pre[i], act=2,
+                                             site=site_mlp_hidden(i), dropout=True),
                                 fc1_d=_Dense(self.da_l[i], w["W0"], self.dy1, tb=True),
                                 out_d=_Dense(self.dx1_l[i], w["Wo"], self.dO, tb=True), dpv=att.get("dpv"),
                                 dqk=att.get("dqk"),
@@ -232,18 +236,29 @@ class ViTRunnerF32:
         # the rest (head, patch conv, odd widths) to the grouped fp32 GEMM
         wg, wr = GemmF32(), WgradF32()
         ks = lambda t: max(1, t.shape[0] // 256)  # noqa: E731   (few tiles: a deep K split)
-        prods = [(self.yf, self.dlogits, self.gWh), (self.patches, self.dpatch, self.gWconv)]
+        # (+ the bias gradient = column sums of the same output gradient, folded into the row-panel
+        # launch where the product fits it; otherwise a colsum launch in the backward)
+        prods = [(self.yf, self.dlogits, self.gWh, self.gbh), (self.patches, self.dpatch, self.gWconv, self.gbconv)]
         for i in range(L):
             w = self.w[i]
-            prods += [(self.a[i], self.dmo_l[i], w["gW1"]), (self.y1[i], self.da_l[i], w["gW0"]),
-                      (self.o[i], self.dx1_l[i], w["gWo"]), (self.y0[i], self.dqkv_l[i], w["gWqkv"])]
-        for a, b, c in prods:
+            prods += [(self.a[i], self.dmo_l[i], w["gW1"], w["gb1"]), (self.y1[i], self.da_l[i], w["gW0"], w["gb0"]),
+                      (self.o[i], self.dx1_l[i], w["gWo"], w["gbo"]), (self.y0[i], self.dqkv_l[i], w["gWqkv"], w["gbqkv"])]
+        self.colsum_folded = set()
+        for a, b, c, gb in prods:
             if WgradF32.fits(a, b, c) and os.environ.get("PCV_F32_WGRAD_ROWS", "1") != "0":
-                wr.add(a, b, c)
+                fold = gb.is_contiguous() and gb.numel() == b.shape[1]
+                wr.add(a, b, c, colsum=gb if fold else None)
+                if fold:
+                    self.colsum_folded.add(gb.data_ptr())
             else:
                 wg.add(a, b, c, ta=True, beta=1.0, ksplit=ks(a))
         self.g_wgrad_parts = [f(x) for x in (wg, wr) if x.jobs]
         self.g_wgrad = self.g_wgrad_parts[-1]
+
+    def _colsum(self, x, gb):
+        """bias gradient += column sums of x, unless the weight-gradient launch folds it in"""
+        if gb.data_ptr() not in self.colsum_folded:
+            K.colsum(x, gb)
 
     def attn_bwd(self, i, rate):
         """Layer i's fused attention backward: dq | dk | dv of dqkv_l[i] from qkv, o, dO and the
@@ -316,7 +331,7 @@ class ViTRunnerF32:
         B, T, D = self.B, self.T, self.D
         rate = m.dropout_rate if train else 0.0
         seed = self.seed
-        K.colsum(self.dlogits, self.gbh)
+        self._colsum(self.dlogits, self.gbh)
         self.g_head_d.run()
         dxc = self.dx.view(B, T * D)[:, :D]
         xcls = self.xs[-1].view(B, T * D)[:, :D]
@@ -329,16 +344,15 @@ class ViTRunnerF32:
             w, g = self.w[i], self.gb[i]
             dmo, da, dx1, dqkv = self.dmo_l[i], self.da_l[i], self.dx1_l[i], self.dqkv_l[i]
             _epi_bwd(dx_in, dmo, rate=rate, seed=seed, site=site_mlp_out(i))            # MLP-out dropout VJP
-            K.colsum(dmo, w["gb1"])
-            g["fc2_d"].run()                                                           # self.da = dmo W1^T
-            _epi_bwd(self.da, da, aux=self.pre[i], act=1, rate=rate, seed=seed, site=site_mlp_hidden(i))
-            K.colsum(da, w["gb0"])
+            self._colsum(dmo, w["gb1"])
+            g["fc2_d"].run(rate, seed)                        # da = dropout_vjp(dmo W1^T) * gelu'(pre)
+            self._colsum(da, w["gb0"])
             g["fc1_d"].run()                                                           # self.dy1 = da W0^T
             if m.use_layernorm:
                 K.layernorm_bwd(self.dy1, self.x1s[i], w["s1"], *self.st1[i], dx_in, dx1, None, w["gs1"], w["gc1"])
             else:
                 _epi(self.dy1, dx1, res=dx_in)
-            K.colsum(dx1, w["gbo"])
+            self._colsum(dx1, w["gbo"])
             g["out_d"].run()                                                           # self.dO = dx1 Wo^T
             if self.fused_attn:                                                        # dQ, dK, dV
                 self.attn_bwd(i, rate)
@@ -347,7 +361,7 @@ class ViTRunnerF32:
                 hip.call("pcv_attn_softmax_bwd_f32", ptr(self.P[i]), ptr(self.S), self.S.shape[0], T,
                          ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
                 g["dqk"].run()                                                         # dQ, dK
-            K.colsum(dqkv, w["gbqkv"])
+            self._colsum(dqkv, w["gbqkv"])
             g["qkv_d"].run()                                                           # self.dy0 = dqkv Wqkv^T
             if m.use_layernorm:
                 K.layernorm_bwd(self.dy0, self.xs[i], w["s0"], *self.st0[i], dx1, self.dxo[i], None, w["gs0"],
@@ -357,7 +371,7 @@ class ViTRunnerF32:
             dx_in = self.dxo[i]
         hip.call("pcv_vit_embed_bwd_f32", ptr(dx_in), ptr(self.dpatch), ptr(self.gcls), ptr(self.gpos), B, T, D,
                  float(rate), ptr(seed), SITE_EMBED, stream_ptr())
-        K.colsum(self.dpatch, self.gbconv)
+        self._colsum(self.dpatch, self.gbconv)
         for part in self.g_wgrad_parts:
             part.run()
 

@@ -118,7 +118,7 @@ class WgradF32:
     split into slices accumulated with fp32 atomics (``target_blocks`` workgroups in total).
     ``fits(a, b, c)`` says whether a product can join (M, N % 64 / 128, K % 64, 16-B aligned)."""
 
-    FMT = "<3Q3q8i"
+    FMT = "<4Q3q8i"
     BN = 128
 
     def __init__(self, target_blocks=2048):
@@ -132,23 +132,27 @@ class WgradF32:
                 and all(t.dtype == torch.float32 and t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
                         for t in (a, b, c)))
 
-    def add(self, a, b, c):
+    def add(self, a, b, c, colsum=None):
+        """colsum (optional, fp32 [N]): += the column sums of b (the bias gradient of the same Dense)"""
         if not self.fits(a, b, c):
             raise ValueError(f"wgrad_f32 job does not fit: A {tuple(a.shape)} B {tuple(b.shape)} C {tuple(c.shape)}")
-        self.jobs.append((a, b, c))
+        if colsum is not None and (colsum.numel() < b.shape[1] or colsum.dtype != torch.float32
+                                   or not colsum.is_contiguous()):
+            raise ValueError("colsum must be a contiguous fp32 vector of N elements")
+        self.jobs.append((a, b, c, colsum))
         return self
 
     def finalize(self, device):
         lib = hip.load()
         assert lib.pcv_gemm_f32_wgrad_job_size() == struct.calcsize(self.FMT)
-        tiles = [(a.shape[1] // 64) * (b.shape[1] // self.BN) for a, b, _ in self.jobs]
-        chunks = max(1, -(-sum(tiles) * max(a.shape[0] // 64 for a, _, _ in self.jobs) // self.target))
+        tiles = [(a.shape[1] // 64) * (b.shape[1] // self.BN) for a, b, _, _ in self.jobs]
+        chunks = max(1, -(-sum(tiles) * max(a.shape[0] // 64 for a, _, _, _ in self.jobs) // self.target))
         recs, first = [], 0
-        for (a, b, c), t in zip(self.jobs, tiles):
+        for (a, b, c, cs), t in zip(self.jobs, tiles):
             K = a.shape[0]
             kchunk = 64 * min(chunks, K // 64)
             ksplit = -(-K // kchunk)
-            recs.append((a.data_ptr(), b.data_ptr(), c.data_ptr(), a.stride(0), b.stride(0), c.stride(0),
+            recs.append((a.data_ptr(), b.data_ptr(), c.data_ptr(), _addr(cs), a.stride(0), b.stride(0), c.stride(0),
                          a.shape[1], b.shape[1], K, b.shape[1] // self.BN, t, ksplit, kchunk, first))
             first += t * ksplit
         self.total = first

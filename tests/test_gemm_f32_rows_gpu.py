@@ -20,24 +20,28 @@ def _rows(a, b, tb, c, bias=None, aux=None, res=None, act=0, rate=0.0, seed=None
 
 @pytest.mark.parametrize("M,N,K,tb", [(16448, 128, 128, 0), (16448, 384, 128, 0), (1000, 256, 128, 0),
                                       (16448, 128, 256, 1), (77, 128, 384, 1), (64, 128, 64, 0)])
-@pytest.mark.parametrize("mode", ["plain", "bias_res", "gelu_drop", "bias_drop_res"])
+@pytest.mark.parametrize("mode", ["plain", "bias_res", "gelu_drop", "bias_drop_res", "gelubwd_drop"])
 def test_gemm_f32_rows(dev, M, N, K, tb, mode):
-    from plaincv_amd.models.vit_f32 import _epi
+    from plaincv_amd.models.vit_f32 import _epi, _epi_bwd
     g = torch.Generator().manual_seed(M + N + K + tb)
     a = torch.randn(M, K, generator=g).to(dev)
     b = (torch.randn(N, K, generator=g) if tb else torch.randn(K, N, generator=g)).to(dev) * K ** -0.5
-    bias = torch.randn(N, generator=g).to(dev) if mode != "plain" else None
+    bwd = "gelubwd" in mode
+    bias = torch.randn(N, generator=g).to(dev) if mode != "plain" and not bwd else None
     res = torch.randn(M, N, generator=g).to(dev) if "res" in mode else None
-    act = 1 if "gelu" in mode else 0
+    act = 2 if bwd else (1 if "gelu" in mode else 0)
     rate = 0.1 if "drop" in mode else 0.0
     seed = torch.tensor([12345], dtype=torch.int32, device=dev)
     c = torch.full((M, N), float("nan"), device=dev)
-    aux = torch.zeros(M, N, device=dev) if act else None
+    aux = (torch.randn(M, N, generator=g).to(dev) * 2 if bwd else torch.zeros(M, N, device=dev)) if act else None
     _rows(a, b, tb, c, bias, aux, res, act, rate, seed, site=7)
     x = (a.double() @ (b.double().t() if tb else b.double())).float()
     ref = torch.empty_like(c)
-    aux_ref = torch.zeros(M, N, device=dev) if act else None
-    _epi(x, ref, bias=bias, res=res, aux=aux_ref, act=act, rate=rate, seed=seed, site=7)
+    aux_ref = (aux.clone() if bwd else torch.zeros(M, N, device=dev)) if act else None
+    if bwd:
+        _epi_bwd(x, ref, aux=aux_ref, act=1, rate=rate, seed=seed, site=7)
+    else:
+        _epi(x, ref, bias=bias, res=res, aux=aux_ref, act=act, rate=rate, seed=seed, site=7)
     torch.cuda.synchronize()
     assert torch.isfinite(c).all()
     tol = 2e-5 * (1.0 + ref.abs())

@@ -108,8 +108,10 @@ def test_wgrad_f32_grouped(dev):
         a = torch.randn(K, M, generator=g).to(dev)
         b = torch.randn(K, N, generator=g).to(dev)
         c = torch.randn(M, N, generator=g).to(dev)
+        cs = torch.randn(N, generator=g).to(dev)
         refs.append((c, c.double() + a.double().t() @ b.double(), (a.abs().double().t() @ b.abs().double()).max().item()))
-        plan.add(a, b, c)
+        refs.append((cs, cs.double() + b.double().sum(0), b.abs().double().sum(0).max().item()))
+        plan.add(a, b, c, colsum=cs)
     assert not WgradF32.fits(torch.zeros(64, 48, device=dev), torch.zeros(64, 128, device=dev), torch.zeros(48, 128, device=dev))
     plan.finalize(dev).run()
     torch.cuda.synchronize()
