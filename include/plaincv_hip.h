@@ -256,6 +256,17 @@ int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, int64_t ldb, 
  * Requires M % 64, N % bn, K % 64, kchunk % 64 == 0, 16-B aligned operands, ld % 4 == 0. */
 int pcv_gemm_f32_wgrad_job_size(void);
 int pcv_gemm_f32_wgrad(const void* jobs_dev, int njobs, int64_t total_blocks, int bn, void* stream);
+/* Blocked Householder QR (csrc/qr_blocked.hip; jnp.linalg.qr of SOAP's refresh, soap.py:108-133):
+ * jobs {A, perm, Q, Wt, Qt, V, T, lda, ldq, n} (pcv_qrb_job_size() bytes; workspaces Wt, Qt, V
+ * n x n and T n x nb, fp32).  init: Wt = A[:, perm]^T, Qt = I; panel(j0, nb): factorise columns
+ * [j0, j0 + nb) of every matrix in LDS, write the reflector vectors into V and the block factor
+ * into T (the caller then applies the trailing update and, backwards, the Q accumulation as GEMMs);
+ * out: Q = Qt^T.  LAPACK sgeqrf / sorgqr conventions (same reflectors as pcv_householder_qr). */
+int pcv_qrb_job_size(void);
+size_t pcv_qrb_panel_lds(int max_n, int nb);
+int pcv_qrb_init(const void* jobs, int njobs, int max_n, void* stream);
+int pcv_qrb_panel(const void* jobs, int njobs, int max_n, int j0, int nb, void* stream);
+int pcv_qrb_out(const void* jobs, int njobs, int max_n, void* stream);
 /* Fused fp32 self-attention of one layer (flax MultiHeadDotProductAttention at
  * models/vit_small.py:41-45, fp32): qkv [B*T][ldqkv] holds q | k | v column blocks of width D = H * 32;
  * out [B*T][ldo] = softmax(q k^T / sqrt(32)) (weight dropout: packed keep words `mask`, rate) v;

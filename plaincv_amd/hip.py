@@ -72,6 +72,11 @@ SIGNATURES = {
     "pcv_gemm_f32_rows": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32, P],
     "pcv_gemm_f32_wgrad_job_size": [],
     "pcv_gemm_f32_wgrad": [P, I32, I64, I32, P],
+    "pcv_qrb_job_size": [],
+    "pcv_qrb_panel_lds": [I32, I32],
+    "pcv_qrb_init": [P, I32, I32, P],
+    "pcv_qrb_panel": [P, I32, I32, I32, I32, P],
+    "pcv_qrb_out": [P, I32, I32, P],
     "pcv_attn_fused_f32_ok": [I32, I32],
     "pcv_attn_fwd_f32": [P, I64, P, I64, P, P, I32, I32, I32, I32, P, F32, P],
     "pcv_attn_bwd_f32": [P, I64, P, I64, P, I64, P, P, P, I64, I32, I32, I32, I32, P, F32, P],
@@ -125,7 +130,7 @@ SIGNATURES = {
 }
 
 # non-status return types (everything else returns an int status)
-RESTYPES = {"pcv_attn_mask_words": I64, "pcv_batchnorm_workspace_size": SZ, "pcv_gemm_grouped_plan_size": I64, "pcv_eigh_log_floats": I64}
+RESTYPES = {"pcv_attn_mask_words": I64, "pcv_batchnorm_workspace_size": SZ, "pcv_qrb_panel_lds": SZ, "pcv_gemm_grouped_plan_size": I64, "pcv_eigh_log_floats": I64}
 
 _lib = None
 _err = None

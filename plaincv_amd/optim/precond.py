@@ -4,6 +4,7 @@ Each plan packs its job records once (plain 8-byte fields: pointers, int64, doub
 device tensor, so a step is a fixed sequence of stream-ordered launches with no host work
 beyond the launch itself.  Shapes are validated here, before anything reaches a kernel.
 """
+import os
 import struct
 
 import torch
@@ -341,13 +342,21 @@ class Eigh:
 
 
 class HouseholderQR:
-    """Q of A[:, perm] for a batch of square matrices (one workgroup each)."""
+    """Q of A[:, perm] for a batch of square matrices (LAPACK geqrf/orgqr conventions).
+
+    Small batches (every n <= 128) run the one-workgroup-per-matrix kernel; larger ones the blocked
+    form (csrc/qr_blocked.hip): an nb-column panel factorised in LDS per matrix, then the trailing
+    update and the backward Q accumulation as grouped fp32 MFMA GEMMs over all matrices.
+    ``blocked`` forces either path (PCV_QR_BLOCKED=0/1 likewise)."""
 
     FMT = "<5Q3q"
+    FMT_B = "<7Q3q"
 
-    def __init__(self, device):
+    def __init__(self, device, blocked=None):
         self.device = torch.device(device)
         self.items = []
+        env = os.environ.get("PCV_QR_BLOCKED")
+        self.blocked_req = blocked if blocked is not None else (None if env is None else env != "0")
 
     def add(self, a, q, perm=None):
         n = a.shape[0]
@@ -363,15 +372,71 @@ class HouseholderQR:
     def finalize(self):
         lib = hip.load()
         assert lib.pcv_qr_job_size() == struct.calcsize(self.FMT)
-        recs = [(_addr(it["a"]), _addr(it["perm"]), _addr(it["q"]), _addr(it["w"]), _addr(it["qt"]),
-                 it["a"].stride(0), it["q"].stride(0), it["n"]) for it in self.items]
         self.max_n = max([it["n"] for it in self.items], default=0)
-        self.dev = _pack(recs, self.FMT).to(self.device) if recs else None
+        self.blocked = self.blocked_req if self.blocked_req is not None else self.max_n > 128
+        if not self.items:
+            self.dev = None
+            return self
+        if not self.blocked:
+            recs = [(_addr(it["a"]), _addr(it["perm"]), _addr(it["q"]), _addr(it["w"]), _addr(it["qt"]),
+                     it["a"].stride(0), it["q"].stride(0), it["n"]) for it in self.items]
+            self.dev = _pack(recs, self.FMT).to(self.device)
+            return self
+        assert lib.pcv_qrb_job_size() == struct.calcsize(self.FMT_B)
+        nb = 32 if self.max_n <= 1024 else (16 if self.max_n <= 2048 else 8)
+        self.nb = nb
+        z = lambda *sh: torch.zeros(*sh, dtype=torch.float32, device=self.device)  # noqa: E731
+        recs = []
+        for it in self.items:
+            n = it["n"]
+            it.update(v=z(n, n), t=z(n, nb), y=z(n, nb), zz=z(n, nb))
+            recs.append((_addr(it["a"]), _addr(it["perm"]), _addr(it["q"]), _addr(it["w"]), _addr(it["qt"]),
+                         _addr(it["v"]), _addr(it["t"]), it["a"].stride(0), it["q"].stride(0), n))
+        self.dev = _pack(recs, self.FMT_B).to(self.device)
+        self.trail, self.qacc = [], []
+        for p in range(-(-self.max_n // nb)):
+            j0 = p * nb
+            g1, g2, g3, g4, g5, g6 = (GemmF32() for _ in range(6))
+            for it in self.items:
+                n = it["n"]
+                if j0 >= n:
+                    continue
+                nbp, m = min(nb, n - j0), n - j0
+                nt = m - nbp
+                wt, qt, v = it["w"].view(n, n), it["qt"].view(n, n), it["v"]
+                vd, tp = v[j0:, j0:j0 + nbp], it["t"][j0:j0 + nbp, :nbp]
+                y, zz = it["y"], it["zz"]
+                if nt > 0:   # A_tr <- (I - V T^T V^T) A_tr on the transposed image: Wt_tr -= (Wt_tr V T) V^T
+                    wtr = wt[j0 + nbp:, j0:]
+                    g1.add(wtr, vd, y[:nt, :nbp])
+                    g2.add(y[:nt, :nbp], tp, zz[:nt, :nbp])
+                    g3.add(zz[:nt, :nbp], vd, wtr, tb=True, alpha=-1.0, beta=1.0)
+                qs = qt[j0:, j0:]   # Q_sub <- (I - V T V^T) Q_sub on Qt: Qt_sub -= (Qt_sub V T^T) V^T
+                g4.add(qs, vd, y[:m, :nbp])
+                g5.add(y[:m, :nbp], tp, zz[:m, :nbp], tb=True)
+                g6.add(zz[:m, :nbp], vd, qs, tb=True, alpha=-1.0, beta=1.0)
+            fin = lambda gs: [g.finalize(self.device) for g in gs if g.jobs]  # noqa: E731
+            self.trail.append((j0, fin((g1, g2, g3))))
+            self.qacc.append(fin((g4, g5, g6)))
         return self
 
     def run(self):
-        if self.items:
-            hip.call("pcv_householder_qr", ptr(self.dev), len(self.items), self.max_n, stream_ptr())
+        if not self.items:
+            return
+        s = stream_ptr()
+        n_it = len(self.items)
+        if not self.blocked:
+            hip.call("pcv_householder_qr", ptr(self.dev), n_it, self.max_n, s)
+            return
+        hip.call("pcv_qrb_init", ptr(self.dev), n_it, self.max_n, s)
+        for j0, gs in self.trail:
+            hip.call("pcv_qrb_panel", ptr(self.dev), n_it, self.max_n, j0, self.nb, s)
+            for g in gs:
+                g.run()
+        for gs in reversed(self.qacc):
+            for g in gs:
+                g.run()
+        hip.call("pcv_qrb_out", ptr(self.dev), n_it, self.max_n, s)
 
 
 class EstSort:

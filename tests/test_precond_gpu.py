@@ -248,16 +248,18 @@ def test_eigh_warm_start_and_inverse_root(dev):
     assert int(w_it["nrounds"].item()) < int(c_it["nrounds"].item())
 
 
+@pytest.mark.parametrize("blocked", [False, True])
 @pytest.mark.parametrize("n,rank,use_perm", [(5, 5, False), (128, 128, True), (256, 256, True), (200, 60, True),
-                                             (1100, 1100, True), (1500, 400, True)])
-def test_householder_qr(dev, n, rank, use_perm):
+                                             (384, 384, True), (1100, 1100, True), (1500, 400, True)])
+def test_householder_qr(dev, n, rank, use_perm, blocked):
+    """one-workgroup and blocked (LDS panels + grouped-GEMM trailing / Q updates) forms"""
     from plaincv_amd.optim.precond import HouseholderQR
     g = torch.Generator().manual_seed(n)
     A = (torch.randn(n, rank, generator=g, dtype=torch.float64) @ torch.randn(rank, n, generator=g,
                                                                               dtype=torch.float64)).float().to(dev)
     perm = torch.randperm(n, generator=g).to(torch.int32).to(dev) if use_perm else None
     Q = torch.zeros(n, n, device=dev)
-    qr = HouseholderQR(dev)
+    qr = HouseholderQR(dev, blocked=blocked)
     qr.add(A, Q, perm)
     qr.finalize().run()
     torch.cuda.synchronize()
@@ -270,6 +272,27 @@ def test_householder_qr(dev, n, rank, use_perm):
     if rank == n:
         Q_ref, _ = torch.linalg.qr(Ap)
         assert (Qd - Q_ref).abs().max().item() < 1e-3
+
+
+def test_householder_qr_blocked_batch_matches_unblocked(dev):
+    """a mixed batch (n = 384, 200, 129, 64, 5) through the blocked plan == the one-workgroup kernel
+    (same reflectors, so the same LAPACK column signs)"""
+    from plaincv_amd.optim.precond import HouseholderQR
+    g = torch.Generator().manual_seed(42)
+    mats = [(torch.randn(n, n, generator=g).to(dev), torch.randperm(n, generator=g).to(torch.int32).to(dev))
+            for n in (384, 200, 129, 64, 5)]
+    outs = {}
+    for blocked in (False, True):
+        qr, qs = HouseholderQR(dev, blocked=blocked), []
+        for A, perm in mats:
+            Q = torch.zeros_like(A)
+            qr.add(A, Q, perm)
+            qs.append(Q)
+        qr.finalize().run()
+        torch.cuda.synchronize()
+        outs[blocked] = qs
+    for qu, qb in zip(outs[False], outs[True]):
+        assert (qu - qb).abs().max().item() < 2e-4
 
 
 # ----------------------------------------------------------------------------------- optimizers
