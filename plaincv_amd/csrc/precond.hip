@@ -47,14 +47,15 @@ struct F32Job {
 static_assert(sizeof(F32Job) == 32 * 8, "F32Job layout");
 
 constexpr int FG_T = 64, FG_K = 128;
-constexpr int LD_KX = FG_T + 16;    // k-major image [k][x]: fragment reads of 4 k-rows hit 4 bank groups
-constexpr int LD_XK = FG_K + 4;     // k-contiguous image [x][k]: 16 rows x 4 k of a read hit 64 banks
+constexpr int LD_XK = FG_K + 4;     // k-contiguous image [x][k]: 16 rows x 16 B of a read hit 64 banks
 constexpr int FG_NPER = FG_T * FG_K / 256;   // elements per thread per operand per k-chunk (32)
 
 // One operand's k-chunk staging.  ROWK: element (x, k) at base[x*ld + k] (A with ta=0, B with
-// tb=1), kept in LDS as [x][k]; otherwise element (x, k) at base[k*ld + x], kept as [k][x] -- so
-// every LDS store is row-contiguous (no transposed writes).  x is the tile's M (or N) index.
-// Offsets are int32 (the host checks every matrix has < 2^31 elements).
+// tb=1); otherwise at base[k*ld + x] (loaded along x, coalesced, and transposed by the LDS stores).
+// Both are kept k-contiguous, [x][k], so the MFMA loop reads one 16-B fragment per operand for
+// four k-steps (contraction index k = 4g + s inside each 16-long slice, lane group g, step s).
+// x is the tile's M (or N) index.  Offsets are int32 (the host checks every matrix has < 2^31
+// elements).
 template <bool ROWK, bool VEC>
 struct Stager {
   static constexpr int NL = VEC ? FG_NPER / 4 : FG_NPER;   // loads per thread
@@ -104,21 +105,19 @@ struct Stager {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int x = xs + dx * i, k = ks + dk * i;
-      if (VEC) {
-        float* d = ROWK ? S + x * LD_XK + k : S + k * LD_KX + x;
-        *(float4*)d = make_float4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+      if (VEC && ROWK) {
+        *(float4*)(S + x * LD_XK + k) = make_float4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
+      } else if (VEC) {   // float4 along x: four transposed scalar stores
+#pragma unroll
+        for (int q = 0; q < 4; ++q) S[(x + q) * LD_XK + k] = r[4 * i + q];
       } else {
-        S[ROWK ? x * LD_XK + k : k * LD_KX + x] = r[i];
+        S[x * LD_XK + k] = r[i];
       }
     }
   }
-  // MFMA 16x16x4 operand: element (x, k) of the staged chunk
-  __device__ __forceinline__ float frag(const float* S, int x, int k) const {
-    return ROWK ? S[x * LD_XK + k] : S[k * LD_KX + x];
-  }
 };
 
-constexpr int FG_LDS_FLOATS = (FG_T * LD_XK > FG_K * LD_KX ? FG_T * LD_XK : FG_K * LD_KX);
+constexpr int FG_LDS_FLOATS = FG_T * LD_XK;
 
 template <bool TA, bool TB, bool VEC>
 __device__ __forceinline__ void f32_tile(const F32Job& jb, int m0, int n0, int kbeg, int K, float* As, float* Bs,
@@ -146,18 +145,21 @@ __device__ __forceinline__ void f32_tile(const F32Job& jb, int m0, int n0, int k
       sa.load(A, k0 + FG_K, m0, M, K, amul, adiag, ksc, ra);
       sb.load(B, k0 + FG_K, n0, N, K, bmul, bdiag, nullptr, rb);
     }
-    const int kend = K - k0 < FG_K ? ((K - k0 + 3) & ~3) : FG_K;
-    for (int kk = 0; kk < kend; kk += 4) {
-      const int kr = kk + (lane >> 4);
-      float fa[2], fb[2];
+    // the chunk's images are zero past K, so the loop runs whole 16-long slices
+    const int kend = K - k0 < FG_K ? ((K - k0 + 15) & ~15) : FG_K;
+    const int g4 = 4 * (lane >> 4), c16 = lane & 15;
+    for (int kk = 0; kk < kend; kk += 16) {
+      f32x4 fa[2], fb[2];
 #pragma unroll
-      for (int a = 0; a < 2; ++a) fa[a] = sa.frag(As, wm * 32 + a * 16 + (lane & 15), kr);
+      for (int a = 0; a < 2; ++a) fa[a] = *(const f32x4*)(As + (wm * 32 + a * 16 + c16) * LD_XK + kk + g4);
 #pragma unroll
-      for (int b = 0; b < 2; ++b) fb[b] = sb.frag(Bs, wn * 32 + b * 16 + (lane & 15), kr);
+      for (int b = 0; b < 2; ++b) fb[b] = *(const f32x4*)(Bs + (wn * 32 + b * 16 + c16) * LD_XK + kk + g4);
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a], fb[b], acc[a][b], 0, 0, 0);
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[a][q], fb[b][q], acc[a][b], 0, 0, 0);
     }
     __syncthreads();
   }
