@@ -38,19 +38,24 @@ struct GrArgs {
 // also avoids the 1 + tanh(u) cancellation for very negative x)
 __device__ __forceinline__ float gr_gelu(float x) {
   const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-  return x / (1.f + expf(-2.f * u));
+  return x / (1.f + __expf(-2.f * u));
 }
-__device__ __forceinline__ float gr_gelu_grad(float x) {   // as gelu_tanh_grad_f32 (vit_f32.hip)
+// its derivative in the same form: with s = sigmoid(2u) = (1 + tanh u) / 2,
+// gelu'(x) = s (1 + 2 x u' (1 - s)), u' = sqrt(2/pi) (1 + 3 * 0.044715 x^2)  (= the tanh form of
+// gelu_tanh_grad_f32 in vit_f32.hip, one exp instead of tanhf)
+__device__ __forceinline__ float gr_gelu_grad(float x) {
   const float k = 0.7978845608028654f;
-  const float t = tanhf(k * (x + 0.044715f * x * x * x));
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * x * x);
+  const float u = k * (x + 0.044715f * x * x * x), du = k * (1.f + 3.f * 0.044715f * x * x);
+  const float sg = 1.f / (1.f + __expf(-2.f * u));
+  return sg * (1.f + 2.f * x * du * (1.f - sg));
 }
 
 // Main loop shared by the row GEMM and the weight-gradient GEMM: acc += op(A)[m0.., kbeg:kend] .
 // op(B)[kbeg:kend, n0..] for one 64 x BN tile (waves 2 x 2, each 32 x BN/2).  Operand layouts:
-//   A: !TA [M][K] (k-contiguous rows, float4 staged as is) / TA [K][M] (lanes along m for
-//      coalesced loads, transposed into the [m][k] image by scalar LDS stores);
-//   B:  TB [N][K] / !TB [K][N] (transposed likewise).
+//   A: !TA [M][K] (k-contiguous rows: image [m][k], one 16-B fragment read per four k-steps) /
+//      TA [K][M] (k-major: image [k][m] stored as loaded, float4; a fragment is four 4-B reads of
+//      consecutive k rows -- cheaper than transposing every element on the way into LDS);
+//   B:  TB [N][K] (image [n][k]) / !TB [K][N] (image [k][n], likewise).
 // (kend - kbeg) % 64 == 0; with TA, M % 64 == 0; B's n-range is always in bounds (N % BN == 0).
 // The next chunk's global loads are issued before this chunk's MFMAs; inside a chunk the next
 // 16-long slice's fragments are read from LDS while the current slice's MFMAs issue.
@@ -86,41 +91,46 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
     for (int i = 0; i < NB; ++i)
       rb[i] = *reinterpret_cast<const f32x4*>(bp[i] + (TB ? (int64_t)kc * GR_BK : (int64_t)kc * GR_BK * ldb));
   };
+  constexpr int LDA_K = GR_BM + 4, LDB_K = BN + 4;   // row strides of the k-major images
   auto lstore = [&]() {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int idx = tid + 256 * i;
-      if (TA) {
-        const int kr = idx / (GR_BM / 4), m = (idx % (GR_BM / 4)) * 4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) As[(m + j) * GR_LDK + kr] = ra[i][j];
-      } else {
-        *reinterpret_cast<f32x4*>(&As[(idx / C4) * GR_LDK + (idx % C4) * 4]) = ra[i];
-      }
+      if (TA) *reinterpret_cast<f32x4*>(&As[(idx / (GR_BM / 4)) * LDA_K + (idx % (GR_BM / 4)) * 4]) = ra[i];
+      else *reinterpret_cast<f32x4*>(&As[(idx / C4) * GR_LDK + (idx % C4) * 4]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int idx = tid + 256 * i;
-      if (TB) {
-        *reinterpret_cast<f32x4*>(&Bs[(idx / C4) * GR_LDK + (idx % C4) * 4]) = rb[i];
-      } else {
-        const int kr = idx / (BN / 4), n = (idx % (BN / 4)) * 4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) Bs[(n + j) * GR_LDK + kr] = rb[i][j];
-      }
+      if (TB) *reinterpret_cast<f32x4*>(&Bs[(idx / C4) * GR_LDK + (idx % C4) * 4]) = rb[i];
+      else *reinterpret_cast<f32x4*>(&Bs[(idx / (BN / 4)) * LDB_K + (idx % (BN / 4)) * 4]) = rb[i];
     }
   };
   auto fload = [&](int kk, f32x4 (&fa)[2], f32x4 (&fb)[NJ]) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      fa[i] = *reinterpret_cast<const f32x4*>(&As[(wm * 32 + i * 16 + c16) * GR_LDK + kk + 4 * g4]);
+    for (int i = 0; i < 2; ++i) {
+      const int x = wm * 32 + i * 16 + c16;
+      if (TA) {
+        const float* p = &As[(kk + 4 * g4) * LDA_K + x];
+        fa[i] = f32x4{p[0], p[LDA_K], p[2 * LDA_K], p[3 * LDA_K]};
+      } else {
+        fa[i] = *reinterpret_cast<const f32x4*>(&As[x * GR_LDK + kk + 4 * g4]);
+      }
+    }
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-      fb[j] = *reinterpret_cast<const f32x4*>(&Bs[(wn * WN + j * 16 + c16) * GR_LDK + kk + 4 * g4]);
+    for (int j = 0; j < NJ; ++j) {
+      const int x = wn * WN + j * 16 + c16;
+      if (TB) {
+        fb[j] = *reinterpret_cast<const f32x4*>(&Bs[x * GR_LDK + kk + 4 * g4]);
+      } else {
+        const float* p = &Bs[(kk + 4 * g4) * LDB_K + x];
+        fb[j] = f32x4{p[0], p[LDB_K], p[2 * LDB_K], p[3 * LDB_K]};
+      }
+    }
   };
   const int nk = (kend - kbeg) / GR_BK;
-  // column sums of the B chunks (colsum != nullptr): thread -> column n, a 64 / (256 / BN)-long
-  // k segment of each chunk's [n][k] image
+  // column sums of the B chunks (colsum != nullptr; the weight-gradient form, !TB): thread ->
+  // column n, a 64 / (256 / BN)-long k segment of each chunk's [k][n] image
   constexpr int CS_SEG = GR_BK * BN / 256;
   const int cs_n = tid % BN, cs_k = (tid / BN) * CS_SEG;
   float cs = 0.f;
@@ -130,10 +140,7 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
   for (int kc = 0; kc < nk; ++kc) {
     if (colsum) {
 #pragma unroll
-      for (int e = 0; e < CS_SEG; e += 4) {
-        const f32x4 x = *reinterpret_cast<const f32x4*>(&Bs[cs_n * GR_LDK + cs_k + e]);
-        cs += (x[0] + x[1]) + (x[2] + x[3]);
-      }
+      for (int e = 0; e < CS_SEG; ++e) cs += Bs[(cs_k + e) * LDB_K + cs_n];
     }
     if (kc + 1 < nk) gload(kc + 1);
     f32x4 fa[2][2], fb[2][NJ];
