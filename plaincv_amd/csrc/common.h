@@ -49,6 +49,32 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Job of a grouped launch: the last job whose first block index is <= blockIdx.x, given each job's
+// first block (a prefix sum, int64 field `first` of a device-side job table with record stride
+// `stride` bytes).  The firsts are gathered into LDS by the whole block in one round trip and
+// binary-searched there -- a per-block linear walk over the table costs one dependent L2 load per
+// skipped job.  `ft` holds >= njobs ints of LDS; falls back to the walk past `cap` jobs.
+template <typename FirstT>
+__device__ __forceinline__ int pcv_find_job(const void* jobs, int njobs, int stride, int first_off, int* ft, int cap) {
+  const int bid = (int)blockIdx.x;
+  const char* base = reinterpret_cast<const char*>(jobs);
+  if (njobs > cap) {
+    int j = 0;
+    while (j + 1 < njobs && (int)*reinterpret_cast<const FirstT*>(base + (size_t)(j + 1) * stride + first_off) <= bid) ++j;
+    return j;
+  }
+  for (int t = threadIdx.x; t < njobs; t += blockDim.x)
+    ft[t] = (int)*reinterpret_cast<const FirstT*>(base + (size_t)t * stride + first_off);
+  __syncthreads();
+  int lo = 0, hi = njobs - 1;   // ft[0] == 0 <= bid
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (ft[mid] <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
 // Block-wide sum for blockDim.x a multiple of 64 (<= 1024); `red` must hold
 // blockDim.x/64 floats of LDS.  Result is broadcast to every thread.
 __device__ __forceinline__ float block_sum(float v, float* red) {

@@ -247,9 +247,9 @@ __global__ __launch_bounds__(256) void gemm_f32_wgrad_kernel(const WgJob* __rest
   __shared__ __attribute__((aligned(16))) float As[GR_BM * GR_LDK];
   __shared__ __attribute__((aligned(16))) float Bs[BN * GR_LDK];
   constexpr int WN = BN / 2, NJ = WN / 16;
+  __shared__ int ft[256];
   const int bid = blockIdx.x;
-  int j = 0;
-  while (j + 1 < njobs && jobs[j + 1].first <= bid) ++j;
+  const int j = pcv_find_job<int32_t>(jobs, njobs, (int)sizeof(WgJob), (int)offsetof(WgJob, first), ft, 256);
   const WgJob jb = jobs[j];
   int t = bid - jb.first;
   const int sl = t / jb.tiles;   // slice-major: the blocks of one slice cover every tile of the job

@@ -47,6 +47,7 @@ struct F32Job {
 static_assert(sizeof(F32Job) == 32 * 8, "F32Job layout");
 
 constexpr int FG_T = 64, FG_K = 128;
+constexpr int FG_JOB_CAP = 1024;    // jobs whose first blocks are searched in LDS
 constexpr int LD_XK = FG_K + 4;     // k-contiguous image [x][k]: 16 rows x 16 B of a read hit 64 banks
 constexpr int FG_NPER = FG_T * FG_K / 256;   // elements per thread per operand per k-chunk (32)
 
@@ -169,9 +170,9 @@ template <bool VEC>
 __global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __restrict__ jobs, int njobs) {
   __shared__ __attribute__((aligned(16))) float As[FG_LDS_FLOATS];
   __shared__ __attribute__((aligned(16))) float Bs[FG_LDS_FLOATS];
+  __shared__ int ft[FG_JOB_CAP];
   const int bid = blockIdx.x;
-  int j = 0;
-  while (j + 1 < njobs && jobs[j + 1].first_tile <= bid) ++j;
+  const int j = pcv_find_job<int64_t>(jobs, njobs, (int)sizeof(F32Job), (int)offsetof(F32Job, first_tile), ft, FG_JOB_CAP);
   const F32Job jb = jobs[j];
   if (jb.conv_in && *jb.conv_in <= (float)jb.conv_tol) return;
   int t = bid - (int)jb.first_tile;
