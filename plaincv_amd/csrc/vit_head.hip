@@ -61,6 +61,29 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
   float* colred = red + 2 * VH_WAVES;    // [2][8][VH_DMAX]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 
+  // Both products' W fragments are issued first, so their global latency hides under the
+  // LayerNorm phase instead of stalling each MFMA k-step (wave w: classes 16w.. for the logits,
+  // columns 16w.. of D for dy).
+  bf16x8 wl[VH_DMAX / 32], wd[VH_KMAX / 32];
+  {
+    const int ncol = wave * 16 + (lane & 15), kg = lane >> 4;
+#pragma unroll
+    for (int ks = 0; ks < VH_DMAX / 32; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = ks * 32 + 8 * kg + j;
+        wl[ks][j] = (ks < D / 32 && ncol < K) ? a.W[(int64_t)k * a.ldw + ncol] : f2bf(0.f);
+      }
+    }
+    const int dcol = wave * 16 + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < VH_KMAX / 32; ++ks) {
+      const int k = ks * 32 + 8 * kg;
+      wd[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (ks < K32 / 32 && dcol < D && k < a.ldw) wd[ks] = *reinterpret_cast<const bf16x8*>(a.W + (int64_t)dcol * a.ldw + k);
+    }
+  }
+
   // ---- LayerNorm of the cls rows (one wave per row); pad rows of Y zero
   for (int b = wave; b < VH_BMAX; b += VH_WAVES) {
     if (b >= B) {
@@ -91,13 +114,10 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
   if (wave < (K + 15) / 16) {
     const int n0 = wave * 16, ncol = n0 + (lane & 15), kg = lane >> 4;
     f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    for (int ks = 0; ks < D / 32; ++ks) {
-      bf16x8 bfr;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = ks * 32 + 8 * kg + j;
-        bfr[j] = ncol < K ? a.W[(int64_t)k * a.ldw + ncol] : f2bf(0.f);
-      }
+    for (int ks = 0; ks < VH_DMAX / 32; ++ks) {
+      if (ks >= D / 32) break;
+      const bf16x8 bfr = wl[ks];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const bf16x8 afr = *reinterpret_cast<const bf16x8*>(Ys + (mt * 16 + (lane & 15)) * LY + ks * 32 + 8 * kg);
@@ -188,10 +208,11 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
   if (wave < D / 16) {
     const int d0 = wave * 16, dcol = d0 + (lane & 15), kg = lane >> 4;
     f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    for (int ks = 0; ks < K32 / 32; ++ks) {
+#pragma unroll
+    for (int ks = 0; ks < VH_KMAX / 32; ++ks) {
+      if (ks >= K32 / 32) break;
       const int k = ks * 32 + 8 * kg;
-      bf16x8 bfr = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (k < a.ldw) bfr = *reinterpret_cast<const bf16x8*>(a.W + (int64_t)dcol * a.ldw + k);   // dlogits is 0 past K
+      const bf16x8 bfr = wd[ks];   // dlogits is 0 past K
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const bf16x8 afr = *reinterpret_cast<const bf16x8*>(Ds + (mt * 16 + (lane & 15)) * LD + k);
