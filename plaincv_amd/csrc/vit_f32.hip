@@ -274,23 +274,41 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
     }
     float m = -__builtin_inff(), l = 0.f;
     f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    // Lane-constant LDS offsets: every row a lane reads sits at the same swizzle phase in each
+    // 16-row block ((row >> 1) & 7 depends only on the row within the block), so the addresses are
+    // row * 32 + a per-lane constant: K fragment rows (k0 + t) * 16 + c16 at slots 2g, 2g + 1; V
+    // pair rows (k0 + t) * 16 + 4g + s at column 2 c16.
+    const int kx = (c16 >> 1) & 7;
+    const float* kbase = Ks + c16 * FA_DH;
+    const int koff0 = ((2 * g) ^ kx) << 2, koff1 = ((2 * g + 1) ^ kx) << 2;
+    const float* vbase = Vs + 4 * g * FA_DH;
+    int voff[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) voff[s] = s * FA_DH + ((((2 * c16) >> 2) ^ ((2 * g + (s >> 1)) & 7)) << 2) + ((2 * c16) & 3);
+    // keep words: word(q, key block kb, lane group g) = base + (kb >> 2) * 64 + (kb & 3)
+    const int wbase = ((((q >> 4) * a.n64) * 4 + ((q & 15) >> 2)) * 16) + 4 * g;
+    const int wshift = (q & 3) * 4;
     for (int k0 = 0; k0 < NB; k0 += 4) {
+      const bool interior = k0 * 16 + 64 <= T;   // wave-uniform: every key of the chunk is < T
       f32x4 st[4];
       float cmax = -__builtin_inff();
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         if (k0 + t < NB) {
-          float kf[8];
-          fa_row8(Ks, (k0 + t) * 16 + c16, g, kf);
+          const float* kr = kbase + (k0 + t) * 16 * FA_DH;
+          const f32x4 ka = *reinterpret_cast<const f32x4*>(kr + koff0), kb4 = *reinterpret_cast<const f32x4*>(kr + koff1);
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s], qf[s], acc, 0, 0, 0);
+          for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[s], qf[s], acc, 0, 0, 0);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {   // (K Q^T)[key (k0+t)*16 + 4g + r][query q] * scale
-            const float v = ((k0 + t) * 16 + 4 * g + r < T) ? acc[r] * a.scale : -__builtin_inff();
-            st[t][r] = v;
-            cmax = fmaxf(cmax, v);
+          for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kb4[s], qf[4 + s], acc, 0, 0, 0);
+          acc *= a.scale;   // (K Q^T)[key (k0+t)*16 + 4g + r][query q] * scale
+          if (!interior) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = ((k0 + t) * 16 + 4 * g + r < T) ? acc[r] : -__builtin_inff();
           }
+          st[t] = acc;
+          cmax = fmaxf(cmax, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
         }
       }
       cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
@@ -304,14 +322,15 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         if (k0 + t < NB) {
-          uint32_t w = 0;
-          if (DROP && qv) w = mk[f32_drop_word(q, (k0 + t) * 16 + 4 * g, a.n64)] >> ((q & 3) * 4);
+          uint32_t w = 0xFFFFu;
+          if (DROP && qv) w = (uint32_t)mk[wbase + (k0 >> 2) * 64 + t] >> wshift;
+          const float* vr = vbase + (k0 + t) * 16 * FA_DH;
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
             float p = __expf(st[t][s] - m);
             l += p;
-            if (DROP) p = ((w >> s) & 1u) ? p : 0.f;
-            const f32x2 v2 = fa_pair(Vs, (k0 + t) * 16 + 4 * g + s, c16);
+            if (DROP) p = __uint_as_float(__float_as_uint(p) & (uint32_t)__builtin_amdgcn_sbfe((int)w, s, 1));
+            const f32x2 v2 = *reinterpret_cast<const f32x2*>(vr + voff[s]);
             o[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(v2[0], p, o[0], 0, 0, 0);
             o[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(v2[1], p, o[1], 0, 0, 0);
           }
