@@ -104,20 +104,25 @@ def timed_loop(step, min_steps=5, max_steps=50, seconds=12.0, warmup=2):
     return n, (time.perf_counter() - t0) / n
 
 
-def timed_kernel(fn, iters=50):
-    """Average duration of fn() (one kernel launch) with HIP events on a
-    dedicated stream (torch.cuda.Event only sees the stream it records on)."""
+def timed_kernel(fn, iters=50, rounds=3):
+    """Average duration of fn() (one kernel launch) with HIP events on a dedicated stream
+    (torch.cuda.Event only sees the stream it records on): the best of `rounds` averages over
+    `iters` back-to-back launches (one slow round -- clock ramp, a co-tenant -- does not set it)."""
     s = torch.cuda.Stream()
+    best = None
     with torch.cuda.stream(s):
         for _ in range(5):
             fn()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(iters):
-            fn()
-        e1.record(s)
-    e1.synchronize()
-    return e0.elapsed_time(e1) / iters * 1e-3
+        for _ in range(rounds):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(iters):
+                fn()
+            e1.record(s)
+            e1.synchronize()
+            t = e0.elapsed_time(e1) / iters * 1e-3
+            best = t if best is None else min(best, t)
+    return best
 
 
 def pmc_traffic(kernel):
