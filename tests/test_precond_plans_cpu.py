@@ -1,0 +1,75 @@
+"""Host-side plans of the fp32 GEMM / QR machinery (optim/precond.py), built on CPU tensors: job
+tables, split-K slicing, panel schedules and shape guards.  Nothing is launched."""
+import struct
+
+import pytest
+import torch
+
+
+def test_gemm_f32_split_k_plan():
+    from plaincv_amd.optim.precond import GemmF32
+    a, b, c = torch.zeros(16448, 128), torch.zeros(16448, 384), torch.zeros(128, 384)
+    g = GemmF32().add(a, b, c, ta=True, beta=1.0, ksplit=16)
+    j = g.jobs[0]
+    assert j["kchunk"] % 128 == 0 and j["ksplit"] * j["kchunk"] >= 16448 > (j["ksplit"] - 1) * j["kchunk"]
+    assert j["tiles"] == 2 * 6 * j["ksplit"]
+    g.finalize("cpu")
+    (dev, n, total, vec), = g.groups
+    assert n == 1 and total == j["tiles"] and dev.numel() == struct.calcsize(GemmF32.FMT)
+    with pytest.raises(ValueError):   # split-K accumulates: beta must be 1
+        GemmF32().add(a, b, c, ta=True, beta=0.0, ksplit=4)
+
+
+def test_wgrad_f32_plan_and_fits():
+    from plaincv_amd.optim.precond import WgradF32
+    R = 16448
+    mk = lambda *s: torch.zeros(*s)  # noqa: E731
+    ok = (mk(R, 128), mk(R, 384), mk(128, 384))
+    assert WgradF32.fits(*ok)
+    assert not WgradF32.fits(mk(R, 48), mk(R, 128), mk(48, 128))       # M % 64
+    assert not WgradF32.fits(mk(R, 128), mk(R, 200), mk(128, 200))     # N % 128
+    assert not WgradF32.fits(mk(R + 1, 128), mk(R + 1, 128), mk(128, 128))   # K % 64
+    plan = WgradF32(target_blocks=2048)
+    plan.add(*ok, colsum=mk(384))
+    plan.add(mk(R, 256), mk(R, 128), mk(256, 128))
+    with pytest.raises(ValueError):
+        plan.add(mk(R, 128), mk(R, 128), mk(128, 128), colsum=mk(64))
+    plan.finalize("cpu")
+    recs = [struct.unpack(WgradF32.FMT, bytes(plan.table[i * struct.calcsize(WgradF32.FMT):(i + 1) * struct.calcsize(WgradF32.FMT)].tolist()))
+            for i in range(2)]
+    first = 0
+    for rec in recs:
+        M, N, K, tiles_n, tiles, ksplit, kchunk, fst = rec[7:]
+        assert tiles == (M // 64) * (N // 128) and tiles_n == N // 128
+        assert kchunk % 64 == 0 and (ksplit - 1) * kchunk < K <= ksplit * kchunk
+        assert fst == first
+        first += tiles * ksplit
+    assert plan.total == first and 1024 <= first <= 4096
+    assert recs[0][3] != 0 and recs[1][3] == 0   # colsum pointer only where requested
+
+
+def test_blocked_qr_plan_schedule():
+    from plaincv_amd.optim.precond import HouseholderQR
+    qr = HouseholderQR("cpu", blocked=True)
+    sizes = (384, 200, 5)
+    for n in sizes:
+        qr.add(torch.zeros(n, n), torch.zeros(n, n))
+    qr.finalize()
+    assert qr.blocked and qr.nb == 32 and len(qr.trail) == 12 and len(qr.qacc) == 12
+    for p, (j0, gs) in enumerate(qr.trail):
+        assert j0 == 32 * p
+        live = [n for n in sizes if n > j0 + min(32, n - j0)]           # matrices with trailing columns
+        if live:
+            assert len(gs) == 3 and all(len(g.jobs) == len(live) for g in gs)
+            for n, job in zip(live, gs[0].jobs):                          # Y = Wt_tr V: (n-j0-nb) x nb, K = n-j0
+                assert (job["M"], job["N"], job["K"]) == (n - j0 - min(32, n - j0), min(32, n - j0), n - j0)
+        else:
+            assert gs == []
+    for p, gs in enumerate(qr.qacc):   # Q accumulation touches every matrix with n > j0
+        j0 = 32 * p
+        assert all(len(g.jobs) == sum(n > j0 for n in sizes) for g in gs)
+    small = HouseholderQR("cpu")
+    small.add(torch.zeros(100, 100), torch.zeros(100, 100))
+    assert not small.finalize().blocked   # <= 128: one workgroup per matrix
+    with pytest.raises(ValueError):
+        HouseholderQR("cpu").add(torch.zeros(4, 5), torch.zeros(4, 5))
