@@ -311,10 +311,15 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
     g.dscale = 1.f / (1.f - rate);
   }
   const bool epi = bias || act || res || g.thresh;
-  // 64 x 128 panels, or 64 x 64 when the 128-wide grid would leave fewer than two workgroups per
-  // CU (the N = 128 products: one workgroup per CU cannot hide its own load / epilogue latency)
+  // 64 x 128 panels, or 64 x 64 when the 128-wide grid would leave fewer than four workgroups per
+  // CU (the N = 128 / 256 products: with one or two per CU the load / epilogue latency is exposed;
+  // C4 step 2.185 -> 2.125 ms moving the N = 256 products to 64-wide panels)
   const int64_t mt = (M + GR_BM - 1) / GR_BM;
-  const bool narrow = mt * (N / 128) < 512;
+  static const int64_t narrow_below = [] {   // PCV_F32_NARROW_BELOW: A/B override (1024: swept 512-2048)
+    const char* e = getenv("PCV_F32_NARROW_BELOW");
+    return e ? (int64_t)atoll(e) : (int64_t)1024;
+  }();
+  const bool narrow = mt * (N / 128) < narrow_below;
   g.tiles_n = (int)(N / (narrow ? 64 : 128));
   const unsigned blocks = (unsigned)(mt * g.tiles_n);
   hipStream_t s = (hipStream_t)stream;
