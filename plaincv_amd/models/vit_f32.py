@@ -234,7 +234,7 @@ class ViTRunnerF32:
         # into ~1024-long slices accumulated with fp32 atomics -- ~2k workgroups instead of 138)
         # The layer weights go to the row-panel wgrad kernel (csrc/gemm_f32.hip) when their shapes fit,
         # the rest (head, patch conv, odd widths) to the grouped fp32 GEMM
-        wg, wr = GemmF32(), WgradF32()
+        wg, wr = GemmF32(), WgradF32(target_blocks=int(os.environ.get("PCV_F32_WGRAD_BLOCKS", "2048")))
         ks = lambda t: max(1, t.shape[0] // 256)  # noqa: E731   (few tiles: a deep K split)
         # (+ the bias gradient = column sums of the same output gradient, folded into the row-panel
         # launch where the product fits it; otherwise a colsum launch in the backward)
