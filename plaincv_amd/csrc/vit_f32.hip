@@ -152,7 +152,8 @@ __global__ __launch_bounds__(256) void attn_softmax_bwd_f32_kernel(const float* 
 }
 
 // embedding VJP with an fp32 patch gradient: g = dropout_bwd(dx); dpatch[b*hw+i] = g[b,1+i];
-// dpos[t] += sum_b g[b,t]; dcls += sum_b g[b,0]
+// dpos[t] += sum_b g[b,t]; dcls += sum_b g[b,0].  The batch is split over grid.y in 8-image slices
+// (partial sums added atomically): a thread walking all B images serialised B dependent loads.
 __global__ void vit_embed_bwd_f32_kernel(const float* dx, float* dpatch, float* dcls, float* dpos, int B, int T, int D,
                                          uint32_t thresh, float scale, const uint32_t* seedp, uint32_t site) {
   const uint32_t seed = thresh ? *seedp : 0u;
@@ -160,16 +161,18 @@ __global__ void vit_embed_bwd_f32_kernel(const float* dx, float* dpatch, float* 
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int d = (int)(i % D), t = (int)(i / D);
+  const int b0 = blockIdx.y * 8, b1 = min(B, b0 + 8);
   float s = 0.f;
-  for (int b = 0; b < B; ++b) {
+#pragma unroll 4
+  for (int b = b0; b < b1; ++b) {
     const int64_t idx = ((int64_t)b * T + t) * D + d;
     float g = dx[idx];
     if (thresh) g = keep_of(seed, site, (uint32_t)idx, thresh) ? g * scale : 0.f;
     s += g;
     if (t > 0) dpatch[((int64_t)b * (T - 1) + t - 1) * D + d] = g;
   }
-  dpos[i] += s;
-  if (t == 0) dcls[d] += s;
+  atomicAdd(dpos + i, s);
+  if (t == 0) atomicAdd(dcls + d, s);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -596,7 +599,8 @@ extern "C" int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls
   uint32_t th; float sc;
   f32_drop(rate, &th, &sc);
   const int64_t n = (int64_t)T * D;
-  hipLaunchKernelGGL(vit_embed_bwd_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(vit_embed_bwd_f32_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)((B + 7) / 8)), dim3(256), 0,
+                     (hipStream_t)stream,
                      dx, dpatch, dcls, dpos, B, T, D, th, sc, seed, site);
   return pcv_launch_status();
 }
