@@ -135,14 +135,17 @@ __global__ __launch_bounds__(256) void muon_prep_kernel(const MuonMat* mats, Muo
   const float gs = gscale ? *gscale : 1.f;
   const bool tr = M.rows > M.cols;
   float s = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int64_t r = i / M.cols, c = i % M.cols;
-    const int64_t off = r * M.ld + c;
+  // 32-bit element indices (the entry points reject max_elems >= 2^31): a 64-bit divide per element was
+  // the bulk of these streaming kernels' instructions
+  const int cols = (int)M.cols;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < (int)n; i += gridDim.x * 256) {
+    const int r = i / cols, c = i - r * cols;
+    const int64_t off = (int64_t)r * M.ld + c;
     const float gi = M.g[off] * gs;
     const float mi = h.beta * M.mu[off] + (1.f - h.beta) * gi;
     M.mu[off] = mi;
     const float xh = h.nesterov ? h.beta * mi / bcn + (1.f - h.beta) * gi / bc : mi / bc;
-    M.x32[tr ? c * M.ldx + r : r * M.ldx + c] = xh;
+    M.x32[tr ? (int64_t)c * M.ldx + r : (int64_t)r * M.ldx + c] = xh;
     s += xh * xh;
   }
   s = block_sum(s, red);
@@ -153,10 +156,10 @@ __global__ __launch_bounds__(256) void muon_norm_kernel(const MuonMat* mats, flo
   const MuonMat M = mats[blockIdx.y];
   const int64_t n = M.rows * M.cols;
   const float inv = 1.f / (sqrtf(*M.norm2) + eps);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-  {
-    const int64_t cx = M.rows > M.cols ? M.rows : M.cols;
-    const int64_t j = (i / cx) * M.ldx + i % cx;
+  const int cx = (int)(M.rows > M.cols ? M.rows : M.cols);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < (int)n; i += gridDim.x * 256) {
+    const int q = i / cx;
+    const int64_t j = (int64_t)q * M.ldx + (i - q * cx);
     const float x = M.x32[j] * inv;
     M.x32[j] = x;          // the fp32 X the NS chain carries across iterations
     M.xb[j] = f2bf(x);     // its bf16 MFMA operand
@@ -172,10 +175,11 @@ __global__ __launch_bounds__(256) void muon_apply_kernel(const MuonMat* mats, Mu
   const int64_t n = M.rows * M.cols;
   const bool tr = M.rows > M.cols;
   const float ss = h.shape_scale > 0.f ? sqrtf(fmaxf(1.f, (float)M.cols / (float)M.rows)) : 1.f;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int64_t r = i / M.cols, c = i % M.cols;
-    const int64_t off = r * M.ld + c;
-    const float o = bf2f(M.xo[tr ? c * M.ldx + r : r * M.ldx + c]);
+  const int cols = (int)M.cols;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < (int)n; i += gridDim.x * 256) {
+    const int r = i / cols, c = i - r * cols;
+    const int64_t off = (int64_t)r * M.ld + c;
+    const float o = bf2f(M.xo[tr ? (int64_t)c * M.ldx + r : (int64_t)r * M.ldx + c]);
     const float pi = M.p[off];
     const float u = -h.lr * (o * ss + h.wd * pi);
     if (M.upd) M.upd[off] = u;
@@ -243,7 +247,7 @@ extern "C" int pcv_step_bump(int* step, void* stream) {
 // normalised by pcv_muon_ns_fused while it loads x32)
 extern "C" int pcv_muon_prep(const void* mats, int nmats, int nnorm, int64_t max_elems, float beta, int nesterov,
                              float eps, const int* step, const float* gscale, void* stream) {
-  if (nmats <= 0 || nnorm < 0 || nnorm > nmats) return PCV_EINVAL;
+  if (nmats <= 0 || nnorm < 0 || nnorm > nmats || max_elems >= (1ll << 31)) return PCV_EINVAL;
   MuonHyper h{beta, 0.f, 0.f, eps, 0.f, nesterov, 0};
   int gx = (int)((max_elems + 256 * 8 - 1) / (256 * 8));
   gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
@@ -255,7 +259,7 @@ extern "C" int pcv_muon_prep(const void* mats, int nmats, int nnorm, int64_t max
 
 extern "C" int pcv_muon_apply(const void* mats, int nmats, int64_t max_elems, float lr, float wd, int shape_scale,
                               int apply, void* stream) {
-  if (nmats <= 0) return PCV_EINVAL;
+  if (nmats <= 0 || max_elems >= (1ll << 31)) return PCV_EINVAL;
   MuonHyper h{0.f, lr, wd, 0.f, shape_scale ? 1.f : 0.f, 0, apply};
   int gx = (int)((max_elems + 256 * 8 - 1) / (256 * 8));
   gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
