@@ -241,7 +241,7 @@ __device__ __forceinline__ void fa_load_mask(uint16_t* dst, const uint16_t* src,
 }
 
 __host__ __device__ constexpr size_t fa_fwd_lds(int NB) { return 2 * (size_t)NB * 16 * FA_DH * 4 + 17 * 6 * 64 * 2; }
-constexpr size_t FA_BWD_LDS = 4 * (size_t)FA_TMAX * FA_DH * 4 + 3 * FA_TMAX * 4 + 17 * 6 * 64 * 2;
+constexpr size_t FA_BWD_LDS = 4 * (size_t)FA_TMAX * FA_DH * 4 + 3 * FA_TMAX * 4 + 17 * 6 * 64 * 2 + 3 * 8 * FA_DH * 4;
 static_assert(FA_BWD_LDS <= 160 * 1024, "fp32 attention backward LDS");
 
 // Forward: 16-query groups dealt round-robin to the waves; per group an online softmax over
@@ -400,8 +400,17 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
   }
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  // T = 16 n + 1 (the ViT's 257): the last key block and the last query group each hold ONE row.
+  // Instead of a wave's whole block loop for that row (the 17th item made one SIMD carry 5 items
+  // where the others carry 4), its gradient is reduced across the waves that meet it anyway: the
+  // key waves see row T-1 as the last query of every loop (-> dQ[T-1]), the query waves see it as
+  // the last key (-> dK[T-1], dV[T-1]); per-wave partials meet in LDS.
+  const bool tail1 = (T & 15) == 1 && NB > 1;
+  const int NBF = tail1 ? NB - 1 : NB;
+  float* tailp = reinterpret_cast<float*>(mk + 17 * 6 * 64);   // [3][8][32]: dq, dk, dv of row T-1
   if (wave < 8) {
-    for (int kb = wave; kb < NB; kb += 8) {
+    if (tail1 && lane < FA_DH) tailp[wave * FA_DH + lane] = 0.f;
+    for (int kb = wave; kb < NBF; kb += 8) {
       const int key = kb * 16 + c16;
       float kf[8], vf[8];
       fa_row8(Ks, key, g, kf);
@@ -439,6 +448,16 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
           pd[r] = pdv;
           ds[r] = p * (dpv - d4[r]);
         }
+        if (tail1 && qb == NB - 1) {   // ds of (query T-1, this key) sits in lane (g = 0, c16)
+          const float dsb = __shfl(ds[0], c16, 64);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float t = dsb * kf[j];
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+            if (c16 == 0) tailp[wave * FA_DH + 8 * g + j] += t;   // wave-private slot
+          }
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const f32x2 o2 = fa_pair(Os, q0 + s, c16), q2 = fa_pair(Qs, q0 + s, c16);
@@ -455,9 +474,14 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
       }
     }
   } else {
-    // query group gq -> wave 8 + ((gq + 1) & 7): the 17th group (T = 257) lands on wave 9, whose
-    // SIMD holds no third key block
-    for (int gq = (wave - 9) & 7; gq < NB; gq += 8) {
+    // query groups: the 17th group (T = 16 n + 1) is handled by the tail reduction; without a tail
+    // row, group gq -> wave 8 + ((gq + 1) & 7) puts a 17th group on wave 9, whose SIMD holds no
+    // third key block
+    if (tail1 && lane < FA_DH) {
+      tailp[(wave) * FA_DH + lane] = 0.f;        // dk slots 8..15
+      tailp[(wave + 8) * FA_DH + lane] = 0.f;    // dv slots 16..23
+    }
+    for (int gq = tail1 ? wave - 8 : (wave - 9) & 7; gq < NBF; gq += 8) {
       const int q = gq * 16 + c16;
       float qf[8], of[8];
       fa_row8(Qs, q, g, qf);
@@ -480,7 +504,7 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
         }
         uint32_t w = 0xFFFFu;
         if (DROP && q < T) w = mk[f32_drop_word(q, kb * 16 + 4 * g, a.n64)] >> ((q & 3) * 4);
-        float ds[4];
+        float ds[4], pd0 = 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = kb * 16 + 4 * g + r;
@@ -488,6 +512,23 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
           float dpv = dpt[r];
           if (DROP) dpv = ((w >> r) & 1u) ? dpv * a.dscale : 0.f;
           ds[r] = p * (dpv - dq);
+          if (r == 0) pd0 = DROP ? (((w & 1u) != 0u) ? p * a.dscale : 0.f) : p;
+        }
+        if (tail1 && kb == NB - 1) {   // (key T-1, this query) sits in lane (g = 0, c16)
+          const float dsb = __shfl(ds[0], c16, 64), pdb = __shfl(pd0, c16, 64);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float tk = dsb * qf[j], tv = pdb * of[j];
+#pragma unroll
+            for (int o = 8; o > 0; o >>= 1) {
+              tk += __shfl_xor(tk, o, 64);
+              tv += __shfl_xor(tv, o, 64);
+            }
+            if (c16 == 0) {
+              tailp[wave * FA_DH + 8 * g + j] += tk;
+              tailp[(wave + 8) * FA_DH + 8 * g + j] += tv;
+            }
+          }
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -497,6 +538,32 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
         }
       }
       if (q < T) fa_store8(a.dqkv + (bT + q) * a.lddqkv + h * FA_DH + 8 * g, acc, a.scale);
+    }
+  }
+  if (tail1) {   // row T-1: dq | dk | dv = sums of the 8 wave partials
+    __syncthreads();
+    if (threadIdx.x < 3 * FA_DH) {
+      const int kind = threadIdx.x / FA_DH, d = threadIdx.x - kind * FA_DH, t = T - 1;
+      float sum = 0.f;
+#pragma unroll
+      for (int w8 = 0; w8 < 8; ++w8) sum += tailp[(kind * 8 + w8) * FA_DH + d];
+      // the corner (query T-1, key T-1) lies in neither wave family's blocks
+      float sv = 0.f, dpv = 0.f;
+#pragma unroll 8
+      for (int c = 0; c < FA_DH; ++c) {
+        sv += Qs[fa_off(t, c)] * Ks[fa_off(t, c)];
+        dpv += Os[fa_off(t, c)] * Vs[fa_off(t, c)];
+      }
+      const float p = __expf(sv * a.scale - Ms[t]) * Is[t];
+      float pd = p;
+      if (DROP) {
+        const bool keep = (mk[f32_drop_word(t, t, a.n64)] >> ((t & 3) * 4 + (t & 3))) & 1u;
+        pd = keep ? p * a.dscale : 0.f;
+        dpv = keep ? dpv * a.dscale : 0.f;
+      }
+      const float ds = p * (dpv - Dl[t]);
+      sum += kind == 0 ? ds * Ks[fa_off(t, d)] : kind == 1 ? ds * Qs[fa_off(t, d)] : pd * Os[fa_off(t, d)];
+      a.dqkv[(bT + T - 1) * a.lddqkv + kind * a.D + h * FA_DH + d] = kind == 2 ? sum : sum * a.scale;
     }
   }
 }
