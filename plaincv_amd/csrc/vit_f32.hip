@@ -240,7 +240,11 @@ __device__ __forceinline__ void fa_load_mask(uint16_t* dst, const uint16_t* src,
     reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
 }
 
-__host__ __device__ constexpr size_t fa_fwd_lds(int NB) { return 2 * (size_t)NB * 16 * FA_DH * 4 + 17 * 6 * 64 * 2; }
+// K, V images, keep words, then the tail-row scratch: q row, probabilities, wave partials, out partials
+constexpr int FA_TAIL_FLOATS = FA_DH + FA_TMAX + 32 + 32 * 33;
+__host__ __device__ constexpr size_t fa_fwd_lds(int NB) {
+  return 2 * (size_t)NB * 16 * FA_DH * 4 + 17 * 6 * 64 * 2 + FA_TAIL_FLOATS * 4;
+}
 constexpr size_t FA_BWD_LDS = 4 * (size_t)FA_TMAX * FA_DH * 4 + 3 * FA_TMAX * 4 + 17 * 6 * 64 * 2 + 3 * 8 * FA_DH * 4;
 static_assert(FA_BWD_LDS <= 160 * 1024, "fp32 attention backward LDS");
 
@@ -261,7 +265,11 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
   if (DROP) fa_load_mask(mk, a.mask, T);
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
-  for (int gq = wave; gq < NB; gq += FA_WAVES) {
+  // T = 16 n + 1 (the ViT's 257): the 17th query group holds ONE row; as a wave item it would run
+  // alone on its SIMD after the other 16 groups; it is computed by the whole block afterwards.
+  const bool tail1 = (T & 15) == 1 && NB > 1;
+  const int NBF = tail1 ? NB - 1 : NB;
+  for (int gq = wave; gq < NBF; gq += FA_WAVES) {
     const int q = gq * 16 + c16;
     const bool qv = q < T;
     float qf[8];
@@ -349,6 +357,60 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
       if (g == 0) {
         a.mrow[bh * T + q] = m;
         a.linv[bh * T + q] = inv;
+      }
+    }
+  }
+  if (tail1) {   // row t = T-1 on VALU: thread = key for the scores, (d, key slice) for P V
+    float* tq = reinterpret_cast<float*>(mk + 17 * 6 * 64);
+    float* tp = tq + FA_DH;
+    float* tr = tp + FA_TMAX;
+    float* to = tr + 32;
+    const int t = T - 1, key = threadIdx.x;
+    if (threadIdx.x < FA_DH) tq[threadIdx.x] = a.qkv[(bT + t) * a.ldqkv + h * FA_DH + threadIdx.x];
+    __syncthreads();
+    float sv = -__builtin_inff();
+    if (key < T) {
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < FA_DH; c += 4) {
+        const f32x4 k4 = *reinterpret_cast<const f32x4*>(Ks + fa_off(key, c));
+        acc += tq[c] * k4[0] + tq[c + 1] * k4[1] + tq[c + 2] * k4[2] + tq[c + 3] * k4[3];
+      }
+      sv = acc * a.scale;
+    }
+    float mx = sv;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0) tr[wave] = mx;
+    __syncthreads();
+    mx = tr[0];
+#pragma unroll
+    for (int w = 1; w < FA_WAVES; ++w) mx = fmaxf(mx, tr[w]);
+    const float p = key < T ? __expf(sv - mx) : 0.f;
+    float ls = p;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
+    if (lane == 0) tr[16 + wave] = ls;
+    if (key < TP) tp[key] = (DROP && key < T && !attn_keep(mk, t, key, a.n64)) ? 0.f : p;
+    __syncthreads();
+    {
+      const int d = threadIdx.x & 31, sl = threadIdx.x >> 5;
+      float acc = 0.f;
+      for (int k = sl; k < T; k += 32) acc += tp[k] * Vs[fa_off(k, d)];
+      to[d * 33 + sl] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x < FA_DH) {
+      float l = 0.f, acc = 0.f;
+#pragma unroll
+      for (int w = 0; w < FA_WAVES; ++w) l += tr[16 + w];
+#pragma unroll 8
+      for (int j = 0; j < 32; ++j) acc += to[threadIdx.x * 33 + j];
+      const float inv = 1.f / l;
+      a.out[(bT + t) * a.ldo + h * FA_DH + threadIdx.x] = acc * (DROP ? inv * a.dscale : inv);
+      if (threadIdx.x == 0) {
+        a.mrow[bh * T + t] = mx;
+        a.linv[bh * T + t] = inv;
       }
     }
   }
