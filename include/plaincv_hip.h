@@ -226,6 +226,21 @@ int pcv_embed_bwd(const int* ids, const void* dx, int64_t lddx, float* dtable, i
 int pcv_vit_patchify_f32(const uint8_t* img, float* out, int B, int H, int W, int C, int patch, void* stream);
 int pcv_layernorm_fwd_f32(const float* x, int64_t ldx, const float* scale, const float* bias, float* y, int64_t ldy,
                           float* mean, float* rstd, int64_t R, int D, float eps, void* stream);
+/* LayerNorm VJP with dscale/dbias (+=) computed in the same pass over dy and x (per-block partials
+ * in ws, pcv_layernorm_bwd_f32_ws(R, D) floats, then one small reduction launch); D in
+ * {64, 128, 256, 384, 512}, rows 16-B aligned (pcv_layernorm_bwd_f32_ok -> 0); dres may be NULL and
+ * may alias dx.  Replaces pcv_layernorm_bwd + its parameter-gradient launch for the fp32 ViT
+ * (models/vit_small.py:39-41 nn.LayerNorm under value_and_grad, flax_engine.py:95). */
+int pcv_layernorm_bwd_f32_ok(int D, int64_t lddy, int64_t ldx, int64_t ldres, int64_t lddx);
+int64_t pcv_layernorm_bwd_f32_ws(int64_t R, int D);
+int pcv_layernorm_bwd_f32(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* scale,
+                          const float* mean, const float* rstd, const float* dres, int64_t ldres, float* dx,
+                          int64_t lddx, float* dscale, float* dbias, float* ws, int64_t ws_floats, int64_t R, int D,
+                          void* stream);
+/* dscale == dbias == NULL: the partials stay in ws and a later pcv_layernorm_part_reduce adds the
+ * partials of several LayerNorms in one launch (device table of {part, dscale, dbias, nblk, D}). */
+int pcv_layernorm_part_job_size(void);
+int pcv_layernorm_part_reduce(const void* jobs, int njobs, int max_D, int64_t max_nblk, void* stream);
 int pcv_f32_epilogue(const float* x, int64_t ldx, const float* bias, const float* res, int64_t ldr, float res_scale,
                      float* aux, int64_t ldaux, float* out, int64_t ldo, int64_t R, int N, int act, float rate,
                      const uint32_t* seed, uint32_t site, void* stream);

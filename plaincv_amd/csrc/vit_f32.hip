@@ -58,6 +58,160 @@ __global__ __launch_bounds__(256) void ln_fwd_f32_kernel(const float* x, int64_t
   if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
 }
 
+// D = 64 NV: 16 lanes per row, lane l holds columns 4 (16 i + l) .. +3 (256-B coalesced per i), 4
+// rows per wave.  The D <= 512 ViT widths; ln_fwd_f32_kernel above covers the rest.
+template <int NV>
+__global__ __launch_bounds__(256) void ln16_fwd_f32_kernel(const float* x, int64_t ldx, const float* scale,
+                                                           const float* bias, float* y, int64_t ldy, float* mean,
+                                                           float* rstd, int64_t R, float eps) {
+  constexpr int D = 64 * NV;
+  const int l16 = threadIdx.x & 15;
+  const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (row >= R) return;   // whole 16-lane groups leave together; the xor shuffles stay inside one
+  f32x4 v[NV];
+  float s = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    v[i] = *reinterpret_cast<const f32x4*>(x + row * ldx + (16 * i + l16) * 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s += v[i][j];
+      s2 += v[i][j] * v[i][j];
+    }
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  const float mu = s / D, rs = rsqrtf(fmaxf(s2 / D - mu * mu, 0.f) + eps);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (16 * i + l16) * 4;
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c), bi = *reinterpret_cast<const f32x4*>(bias + c);
+    *reinterpret_cast<f32x4*>(y + row * ldy + c) = (v[i] - mu) * rs * sc + bi;
+  }
+  if (l16 == 0) { mean[row] = mu; rstd[row] = rs; }
+}
+
+// LayerNorm VJP with the parameter gradients from the same pass: dx = dres + rstd (g - mean(g) -
+// xhat mean(g xhat)), g = dy scale; per block (16 rows) the column sums of dy xhat and dy go to
+// part[block][0, D) / [D, 2 D) with plain stores, ln_part_reduce_kernel adds them up (device-scope
+// atomics from every block onto the same 2 D addresses serialised to ~8 us; 1024-thread blocks
+// over 64 rows gave 257 blocks for the ViT's 16448 rows, one more than there are CUs).
+template <int NV>
+__global__ __launch_bounds__(256) void ln16_bwd_f32_kernel(const float* dy, int64_t lddy, const float* x,
+                                                           int64_t ldx, const float* scale, const float* mean_in,
+                                                           const float* rstd_in, const float* dres, int64_t ldres,
+                                                           float* dx, int64_t lddx, float* part, int64_t R) {
+  constexpr int D = 64 * NV;
+  __shared__ float red[4][2][D];
+  const int l16 = threadIdx.x & 15, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  f32x4 pa[NV], pb[NV];
+  if (row < R) {   // whole 16-lane groups: the xor shuffles below stay inside one
+    const float mu = mean_in[row], rs = rstd_in[row];
+    f32x4 xh[NV], g[NV], r[NV];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (16 * i + l16) * 4;
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(x + row * ldx + c);
+      const f32x4 dv = *reinterpret_cast<const f32x4*>(dy + row * lddy + c);
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + c);
+      r[i] = dres ? *reinterpret_cast<const f32x4*>(dres + row * ldres + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      xh[i] = (xv - mu) * rs;
+      g[i] = dv * sc;
+      pa[i] = dv * xh[i];
+      pb[i] = dv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sg += g[i][j];
+        sgx += g[i][j] * xh[i][j];
+      }
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      sg += __shfl_xor(sg, o, 64);
+      sgx += __shfl_xor(sgx, o, 64);
+    }
+    sg /= D;
+    sgx /= D;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      *reinterpret_cast<f32x4*>(dx + row * lddx + (16 * i + l16) * 4) = r[i] + rs * (g[i] - sg - xh[i] * sgx);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) pa[i] = pb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float a = pa[i][j], b = pb[i][j];
+      a += __shfl_xor(a, 16, 64);
+      b += __shfl_xor(b, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      b += __shfl_xor(b, 32, 64);
+      if (lane < 16) {
+        red[wave][0][(16 * i + l16) * 4 + j] = a;
+        red[wave][1][(16 * i + l16) * 4 + j] = b;
+      }
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * D; t += 256) {
+    const int k = t / D, c = t - k * D;
+    part[(int64_t)blockIdx.x * 2 * D + t] = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+  }
+}
+
+// one LayerNorm's parameter-gradient partials: part [nblk][2 D] -> dscale [D], dbias [D] (+=)
+struct LnPartJob {
+  const float* part;
+  float* dscale;
+  float* dbias;
+  int64_t nblk, D;
+};
+static_assert(sizeof(LnPartJob) == 40, "LnPartJob layout");
+
+// dscale[c] += sum_b part[b][c], dbias[c] += sum_b part[b][D + c]: workgroup (x, y, z) sums 64
+// columns of job z (jobs == nullptr: the single job `one`) over block chunk y (4 slices), one atomic
+// per column and chunk
+__global__ __launch_bounds__(256) void ln_part_reduce_kernel(const LnPartJob* jobs, LnPartJob one) {
+  __shared__ float red[4][64];
+  const LnPartJob j = jobs ? jobs[blockIdx.z] : one;
+  const float* part = j.part;
+  const int nblk = (int)j.nblk, D = (int)j.D;
+  float *dscale = j.dscale, *dbias = j.dbias;
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63), sl = threadIdx.x >> 6;
+  const int chunk = (nblk + gridDim.y - 1) / gridDim.y, b0 = blockIdx.y * chunk;
+  const int b1 = b0 + chunk < nblk ? b0 + chunk : nblk;
+  float sum = 0.f;
+  if (col < 2 * D) {
+#pragma unroll 4
+    for (int b = b0 + sl; b < b1; b += 4) sum += part[(int64_t)b * 2 * D + col];
+  }
+  red[sl][threadIdx.x & 63] = sum;
+  __syncthreads();
+  if (sl == 0 && col < 2 * D) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(col < D ? dscale + col : dbias + (col - D), t);
+  }
+}
+
+#define PCV_LN16_DISPATCH(D, CALL)                            \
+  switch ((D) / 64) {                                         \
+    case 1: { constexpr int NV = 1; CALL; } break;            \
+    case 2: { constexpr int NV = 2; CALL; } break;            \
+    case 4: { constexpr int NV = 4; CALL; } break;            \
+    case 6: { constexpr int NV = 6; CALL; } break;            \
+    case 8: { constexpr int NV = 8; CALL; } break;            \
+    default: return PCV_EINVAL;                               \
+  }
+
+__host__ __device__ inline bool ln16_fits(int D) { return D % 64 == 0 && (D / 64 == 1 || D / 64 == 2 || D / 64 == 4 || D / 64 == 6 || D / 64 == 8); }
+
 __device__ __forceinline__ float gelu_tanh_f32(float x) {
   const float k = 0.7978845608028654f;   // sqrt(2/pi)
   return 0.5f * x * (1.f + tanhf(k * (x + 0.044715f * x * x * x)));
@@ -677,8 +831,59 @@ extern "C" int pcv_vit_patchify_f32(const uint8_t* img, float* out, int B, int H
 extern "C" int pcv_layernorm_fwd_f32(const float* x, int64_t ldx, const float* scale, const float* bias, float* y,
                                      int64_t ldy, float* mean, float* rstd, int64_t R, int D, float eps, void* stream) {
   if (R <= 0 || D <= 0 || !x || !y || !scale || !bias || !mean || !rstd) return PCV_EINVAL;
+  if (ln16_fits(D) && ((ldx | ldy) & 3) == 0 &&
+      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(scale) |
+        reinterpret_cast<uintptr_t>(bias)) & 15) == 0) {
+    PCV_LN16_DISPATCH(D, hipLaunchKernelGGL((ln16_fwd_f32_kernel<NV>), dim3((unsigned)((R + 15) / 16)), dim3(256), 0,
+                                            (hipStream_t)stream, x, ldx, scale, bias, y, ldy, mean, rstd, R, eps));
+    return pcv_launch_status();
+  }
   hipLaunchKernelGGL(ln_fwd_f32_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, ldx,
                      scale, bias, y, ldy, mean, rstd, R, D, eps);
+  return pcv_launch_status();
+}
+
+static int64_t ln16_bwd_blocks(int64_t R) { return R <= 0 ? 0 : (R + 15) / 16; }
+
+// floats of the per-block partial buffer pcv_layernorm_bwd_f32 needs for R rows of width D
+extern "C" int64_t pcv_layernorm_bwd_f32_ws(int64_t R, int D) { return ln16_bwd_blocks(R) * 2 * (int64_t)D; }
+
+// 0 when pcv_layernorm_bwd_f32 takes these shapes (D in {64, 128, 256, 384, 512}, 16-B rows)
+extern "C" int pcv_layernorm_bwd_f32_ok(int D, int64_t lddy, int64_t ldx, int64_t ldres, int64_t lddx) {
+  return ln16_fits(D) && ((lddy | ldx | ldres | lddx) & 3) == 0 ? 0 : PCV_EINVAL;
+}
+
+extern "C" int pcv_layernorm_bwd_f32(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* scale,
+                                     const float* mean, const float* rstd, const float* dres, int64_t ldres, float* dx,
+                                     int64_t lddx, float* dscale, float* dbias, float* ws, int64_t ws_floats, int64_t R,
+                                     int D, void* stream) {
+  if (R <= 0 || !dy || !x || !scale || !mean || !rstd || !dx || !ws || !dscale != !dbias) return PCV_EINVAL;
+  if (ws_floats < pcv_layernorm_bwd_f32_ws(R, D)) return PCV_EINVAL;
+  if (pcv_layernorm_bwd_f32_ok(D, lddy, ldx, dres ? ldres : 0, lddx)) return PCV_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dres) |
+       reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(scale)) & 15)
+    return PCV_EALIGN;
+  const int64_t blocks = ln16_bwd_blocks(R);
+  if (blocks >= (1ll << 31)) return PCV_EINVAL;
+  PCV_LN16_DISPATCH(D, hipLaunchKernelGGL((ln16_bwd_f32_kernel<NV>), dim3((unsigned)blocks), dim3(256), 0,
+                                          (hipStream_t)stream, dy, lddy, x, ldx, scale, mean, rstd, dres, ldres, dx,
+                                          lddx, ws, R));
+  if (!dscale) return pcv_launch_status();   // partials stay in ws for pcv_layernorm_part_reduce
+  const int chunks = (int)(blocks / 64 < 1 ? 1 : (blocks / 64 > 64 ? 64 : blocks / 64));   // ~64 partials each
+  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * D + 63) / 64), chunks), dim3(256), 0,
+                     (hipStream_t)stream, nullptr, LnPartJob{ws, dscale, dbias, blocks, D});
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_layernorm_part_job_size() { return (int)sizeof(LnPartJob); }
+
+// the deferred parameter-gradient reductions of njobs LayerNorm VJPs in one launch (jobs: device
+// table of LnPartJob; max_D / max_nblk bound the table's entries)
+extern "C" int pcv_layernorm_part_reduce(const void* jobs, int njobs, int max_D, int64_t max_nblk, void* stream) {
+  if (!jobs || njobs <= 0 || njobs > 65535 || max_D <= 0 || max_D > 512 || max_nblk <= 0) return PCV_EINVAL;
+  const int chunks = (int)(max_nblk / 64 < 1 ? 1 : (max_nblk / 64 > 64 ? 64 : max_nblk / 64));
+  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * max_D + 63) / 64), chunks, njobs), dim3(256), 0,
+                     (hipStream_t)stream, (const LnPartJob*)jobs, LnPartJob{});
   return pcv_launch_status();
 }
 

@@ -63,6 +63,11 @@ SIGNATURES = {
     "pcv_embed_bwd": [P, P, I64, P, I64, I64, I32, I32, P],
     "pcv_vit_patchify_f32": [P, P, I32, I32, I32, I32, I32, P],
     "pcv_layernorm_fwd_f32": [P, I64, P, P, P, I64, P, P, I64, I32, F32, P],
+    "pcv_layernorm_bwd_f32_ok": [I32, I64, I64, I64, I64],
+    "pcv_layernorm_bwd_f32_ws": [I64, I32],
+    "pcv_layernorm_part_job_size": [],
+    "pcv_layernorm_part_reduce": [P, I32, I32, I64, P],
+    "pcv_layernorm_bwd_f32": [P, I64, P, I64, P, P, P, P, I64, P, I64, P, P, P, I64, I64, I32, P],
     "pcv_f32_epilogue": [P, I64, P, P, I64, F32, P, I64, P, I64, I64, I32, I32, F32, P, U32, P],
     "pcv_f32_epilogue_bwd": [P, I64, P, I64, P, I64, I64, I32, I32, F32, P, U32, P],
     "pcv_attn_softmax_f32": [P, P, P, I64, I32, P, F32, P],
@@ -130,7 +135,8 @@ SIGNATURES = {
 }
 
 # non-status return types (everything else returns an int status)
-RESTYPES = {"pcv_attn_mask_words": I64, "pcv_batchnorm_workspace_size": SZ, "pcv_qrb_panel_lds": SZ, "pcv_gemm_grouped_plan_size": I64, "pcv_eigh_log_floats": I64}
+RESTYPES = {"pcv_attn_mask_words": I64, "pcv_batchnorm_workspace_size": SZ, "pcv_qrb_panel_lds": SZ, "pcv_gemm_grouped_plan_size": I64, "pcv_eigh_log_floats": I64,
+            "pcv_layernorm_bwd_f32_ws": I64}
 
 _lib = None
 _err = None

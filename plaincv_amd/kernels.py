@@ -317,6 +317,65 @@ def layernorm_bwd(dy, x, scale, mean, rstd, dres, dx, dx_bf16, dscale, dbias):
              _ld(dx_bf16) if dx_bf16 is not None else 0, ptr(dscale), ptr(dbias), R, D, stream_ptr())
 
 
+def layernorm_bwd_f32_ws(R, D):
+    """floats of the partial-sum workspace layernorm_bwd_f32 needs for [R, D]"""
+    return int(hip.load().pcv_layernorm_bwd_f32_ws(int(R), int(D)))
+
+
+def layernorm_bwd_f32_fits(D, *ts):
+    """whether pcv_layernorm_bwd_f32 takes width D with these (dy, x, dres or None, dx) row strides"""
+    lds = [_ld(t) if t is not None else 0 for t in ts]
+    return hip.load().pcv_layernorm_bwd_f32_ok(int(D), *lds) == 0
+
+
+def layernorm_bwd_f32(dy, x, scale, mean, rstd, dres, dx, dscale, dbias, ws):
+    """fp32 LayerNorm VJP with the parameter gradients from the same pass (pcv_layernorm_bwd_f32, ws:
+    fp32 workspace of layernorm_bwd_f32_ws(R, D) floats).  dscale = dbias = None leaves the per-block
+    partials in ws for a LayerNormParamReduce; shapes the fused kernel does not take go through
+    pcv_layernorm_bwd (same arithmetic, two launches, gradients added at once)."""
+    R, D = x.shape
+    ldr = _ld(dres) if dres is not None else 0
+    if not layernorm_bwd_f32_fits(D, dy, x, dres, dx):
+        _chk(dscale is not None, "deferred LayerNorm parameter gradients need the fused kernel's shapes")
+        return layernorm_bwd(dy, x, scale, mean, rstd, dres, dx, None, dscale, dbias)
+    _chk(dy.dtype == F32 and dx.dtype == F32 and tuple(dy.shape) == (R, D), "layernorm bwd f32")
+    _dev(dy, x, scale, mean, rstd, dres, dx, dscale, dbias, ws)
+    _chk(ws.dtype == F32 and ws.is_contiguous(), "layernorm bwd f32 workspace")
+    hip.call("pcv_layernorm_bwd_f32", ptr(dy), _ld(dy), ptr(x), _ld(x), ptr(scale), ptr(mean), ptr(rstd),
+             ptr(dres), ldr, ptr(dx), _ld(dx), ptr(dscale), ptr(dbias), ptr(ws), ws.numel(), R, D, stream_ptr())
+
+
+class LayerNormParamReduce:
+    """The deferred dscale/dbias reductions of several layernorm_bwd_f32 calls (each given its own
+    ws) as one pcv_layernorm_part_reduce launch."""
+
+    FMT = "<3Q2q"
+
+    def __init__(self):
+        self.jobs = []
+
+    def add(self, ws, R, D, dscale, dbias):
+        _chk(ws.numel() >= layernorm_bwd_f32_ws(R, D) and dscale.numel() == D and dbias.numel() == D
+             and dscale.is_contiguous() and dbias.is_contiguous(), "layernorm part job")
+        self.jobs.append((ws, dscale, dbias, -(-int(R) // 16), int(D)))
+        return self
+
+    def finalize(self, device):
+        import struct
+        lib = hip.load()
+        _chk(lib.pcv_layernorm_part_job_size() == struct.calcsize(self.FMT), "LnPartJob layout")
+        raw = b"".join(struct.pack(self.FMT, w.data_ptr(), s.data_ptr(), b.data_ptr(), n, d)
+                       for w, s, b, n, d in self.jobs)
+        self.table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+        self.max_D = max(j[4] for j in self.jobs)
+        self.max_nblk = max(j[3] for j in self.jobs)
+        return self
+
+    def run(self):
+        hip.call("pcv_layernorm_part_reduce", ptr(self.table), len(self.jobs), self.max_D, self.max_nblk,
+                 stream_ptr())
+
+
 def batchnorm_workspace_bytes(R, D):
     return int(hip.load().pcv_batchnorm_workspace_size(int(R), int(D)))
 

@@ -142,6 +142,9 @@ class ViTRunnerF32:
         self.dyf = z(B, D)
         self.dmo, self.da = z(R, D), z(R, M)
         self.dy1, self.dx1, self.dO = z(R, D), z(R, D), z(R, D)
+        # LayerNorm parameter-gradient partials: site 0 the final norm, 1 + 2i / 2 + 2i layer i's
+        # LayerNorm_1 / LayerNorm_0
+        self.ln_ws = z(2 * L + 1, max(K.layernorm_bwd_f32_ws(R, D), 1))
         self.dqkv, self.dy0 = z(R, 3 * D), z(R, D)
         self.dxo = [z(R, D) for _ in range(L)]
         self.dpatch = z(B * self.hw, D)
@@ -254,6 +257,24 @@ class ViTRunnerF32:
                 wg.add(a, b, c, ta=True, beta=1.0, ksplit=ks(a))
         self.g_wgrad_parts = [f(x) for x in (wg, wr) if x.jobs]
         self.g_wgrad = self.g_wgrad_parts[-1]
+        # LayerNorm dscale / dbias: every VJP leaves per-block column sums in its ws row, one launch
+        # at the end of backward adds them all (instead of a small reduction launch per LayerNorm)
+        self.ln_red = None
+        xcls, dxc = self.xs[-1].view(B, T * D)[:, :D], self.dx.view(B, T * D)[:, :D]
+        if self.m.use_layernorm and os.environ.get("PCV_F32_LN_DEFER", "1") != "0" and \
+                K.layernorm_bwd_f32_fits(D, self.dyf, xcls, None, dxc) and \
+                K.layernorm_bwd_f32_fits(D, self.dy1, self.x1s[0], self.dx, self.dx1):
+            red = K.LayerNormParamReduce().add(self.ln_ws[0], B, D, self.gsf, self.gcf)
+            for i in range(L):
+                w = self.w[i]
+                red.add(self.ln_ws[1 + 2 * i], B * T, D, w["gs1"], w["gc1"])
+                red.add(self.ln_ws[2 + 2 * i], B * T, D, w["gs0"], w["gc0"])
+            self.ln_red = red.finalize(dev)
+
+    def _ln_bwd(self, site, dy, x, scale, st, dres, dx, gs, gc):
+        """LayerNorm VJP; the parameter gradients deferred to self.ln_red when it is planned"""
+        d = self.ln_red is not None
+        K.layernorm_bwd_f32(dy, x, scale, *st, dres, dx, None if d else gs, None if d else gc, self.ln_ws[site])
 
     def _colsum(self, x, gb):
         """bias gradient += column sums of x, unless the weight-gradient launch folds it in"""
@@ -336,7 +357,7 @@ class ViTRunnerF32:
         dxc = self.dx.view(B, T * D)[:, :D]
         xcls = self.xs[-1].view(B, T * D)[:, :D]
         if m.use_layernorm:
-            K.layernorm_bwd(self.dyf, xcls, self.sf, *self.stf, None, dxc, None, self.gsf, self.gcf)
+            self._ln_bwd(0, self.dyf, xcls, self.sf, self.stf, None, dxc, self.gsf, self.gcf)
         else:
             _epi(self.dyf, dxc)
         dx_in = self.dx
@@ -349,7 +370,7 @@ class ViTRunnerF32:
             self._colsum(da, w["gb0"])
             g["fc1_d"].run()                                                           # self.dy1 = da W0^T
             if m.use_layernorm:
-                K.layernorm_bwd(self.dy1, self.x1s[i], w["s1"], *self.st1[i], dx_in, dx1, None, w["gs1"], w["gc1"])
+                self._ln_bwd(1 + 2 * i, self.dy1, self.x1s[i], w["s1"], self.st1[i], dx_in, dx1, w["gs1"], w["gc1"])
             else:
                 _epi(self.dy1, dx1, res=dx_in)
             self._colsum(dx1, w["gbo"])
@@ -364,8 +385,8 @@ class ViTRunnerF32:
             self._colsum(dqkv, w["gbqkv"])
             g["qkv_d"].run()                                                           # self.dy0 = dqkv Wqkv^T
             if m.use_layernorm:
-                K.layernorm_bwd(self.dy0, self.xs[i], w["s0"], *self.st0[i], dx1, self.dxo[i], None, w["gs0"],
-                                w["gc0"])
+                self._ln_bwd(2 + 2 * i, self.dy0, self.xs[i], w["s0"], self.st0[i], dx1, self.dxo[i], w["gs0"],
+                             w["gc0"])
             else:
                 _epi(self.dy0, self.dxo[i], res=dx1)
             dx_in = self.dxo[i]
@@ -374,6 +395,8 @@ class ViTRunnerF32:
         self._colsum(self.dpatch, self.gbconv)
         for part in self.g_wgrad_parts:
             part.run()
+        if self.ln_red is not None:
+            self.ln_red.run()
 
     def flops_per_step(self):
         B, T, D, M, Kc = self.B, self.T, self.D, self.M, self.Kc
