@@ -59,20 +59,27 @@ __device__ __forceinline__ float gr_gelu_grad(float x) {
 // (kend - kbeg) % 64 == 0; with TA, M % 64 == 0; B's n-range is always in bounds (N % BN == 0).
 // The next chunk's global loads are issued before this chunk's MFMAs; inside a chunk the next
 // 16-long slice's fragments are read from LDS while the current slice's MFMAs issue.
-template <bool TA, bool TB, int BN>
+// BM x BN tile (BM 64 or 32): the 4 waves as (BM / 32) x (4 / (BM / 32)), each a 32 x WN tile
+template <int BM, int BN>
+struct GrShape {
+  static constexpr int WNW = 4 / (BM / 32), WN = BN / WNW, NJ = WN / 16;
+};
+
+template <bool TA, bool TB, int BN, int BM = GR_BM>
 __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
                                             int64_t ldb, int M, int m0, int n0, int kbeg, int kend, float* As,
-                                            float* Bs, f32x4 (&acc)[2][BN / 32], float* colsum = nullptr) {
+                                            float* Bs, f32x4 (&acc)[2][GrShape<BM, BN>::NJ],
+                                            float* colsum = nullptr) {
   constexpr int C4 = GR_BK / 4;                          // float4 per 64-long k row
-  constexpr int NA = GR_BM * C4 / 256, NB = BN * C4 / 256;
-  constexpr int WN = BN / 2, NJ = WN / 16;               // wave tile 32 x WN
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  constexpr int NA = BM * C4 / 256, NB = BN * C4 / 256;
+  constexpr int WNW = GrShape<BM, BN>::WNW, WN = GrShape<BM, BN>::WN, NJ = GrShape<BM, BN>::NJ;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w / WNW, wn = w % WNW;
   const int g4 = lane >> 4, c16 = lane & 15;
   const float* ap[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
     const int idx = tid + 256 * i;
-    if (TA) ap[i] = A + (int64_t)(kbeg + idx / (GR_BM / 4)) * lda + m0 + (idx % (GR_BM / 4)) * 4;
+    if (TA) ap[i] = A + (int64_t)(kbeg + idx / (BM / 4)) * lda + m0 + (idx % (BM / 4)) * 4;
     else ap[i] = A + (int64_t)min(m0 + idx / C4, M - 1) * lda + kbeg + (idx % C4) * 4;
   }
   const float* bp[NB];
@@ -91,12 +98,12 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
     for (int i = 0; i < NB; ++i)
       rb[i] = *reinterpret_cast<const f32x4*>(bp[i] + (TB ? (int64_t)kc * GR_BK : (int64_t)kc * GR_BK * ldb));
   };
-  constexpr int LDA_K = GR_BM + 4, LDB_K = BN + 4;   // row strides of the k-major images
+  constexpr int LDA_K = BM + 4, LDB_K = BN + 4;   // row strides of the k-major images
   auto lstore = [&]() {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int idx = tid + 256 * i;
-      if (TA) *reinterpret_cast<f32x4*>(&As[(idx / (GR_BM / 4)) * LDA_K + (idx % (GR_BM / 4)) * 4]) = ra[i];
+      if (TA) *reinterpret_cast<f32x4*>(&As[(idx / (BM / 4)) * LDA_K + (idx % (BM / 4)) * 4]) = ra[i];
       else *reinterpret_cast<f32x4*>(&As[(idx / C4) * GR_LDK + (idx % C4) * 4]) = ra[i];
     }
 #pragma unroll
@@ -166,24 +173,24 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
   if (colsum) atomicAdd(colsum + n0 + cs_n, cs);
 }
 
-template <bool TB, bool EPI, int BN>
+template <bool TB, bool EPI, int BN, int BM>
 __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
-  // operand images during the main loop; the C tile [64][BN + 4] for the epilogue afterwards
-  __shared__ __attribute__((aligned(16))) float smem[(GR_BM + BN) * GR_LDK];
-  static_assert(GR_BM * (BN + 4) <= (GR_BM + BN) * GR_LDK, "C tile fits the operand images");
+  // operand images during the main loop; the C tile [BM][BN + 4] for the epilogue afterwards
+  __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * GR_LDK];
+  static_assert(BM * (BN + 4) <= (BM + BN) * GR_LDK, "C tile fits the operand images");
   float* As = smem;
-  float* Bs = smem + GR_BM * GR_LDK;
-  constexpr int WN = BN / 2, NJ = WN / 16;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
+  float* Bs = smem + BM * GR_LDK;
+  constexpr int WNW = GrShape<BM, BN>::WNW, WN = GrShape<BM, BN>::WN, NJ = GrShape<BM, BN>::NJ;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w / WNW, wn = w % WNW;
   const int g4 = lane >> 4, c16 = lane & 15;
   const int tn = blockIdx.x % g.tiles_n, tm = blockIdx.x / g.tiles_n;
-  const int m0 = tm * GR_BM, n0 = tn * BN;
+  const int m0 = tm * BM, n0 = tn * BN;
   f32x4 acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  gr_mainloop<false, TB, BN>(g.A, g.lda, g.B, g.ldb, g.M, m0, n0, 0, g.K, As, Bs, acc);
+  gr_mainloop<false, TB, BN, BM>(g.A, g.lda, g.B, g.ldb, g.M, m0, n0, 0, g.K, As, Bs, acc);
   // C tile through LDS, so the epilogue streams rows as float4: 16-B loads of bias / residual and
   // 16-B stores of C (and of the GELU pre-activation)
   constexpr int LDC = BN + 4;
@@ -198,7 +205,7 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
   const uint32_t seed = (EPI && g.thresh) ? *g.seed : 0u;
   constexpr int Q = BN / 4;
 #pragma unroll
-  for (int it = 0; it < GR_BM * Q / 256; ++it) {
+  for (int it = 0; it < BM * Q / 256; ++it) {
     const int idx = threadIdx.x + 256 * it, rl = idx / Q, cl = (idx % Q) * 4;
     const int row = m0 + rl, col = n0 + cl;
     if (row >= g.M) continue;
@@ -320,11 +327,22 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
     return e ? (int64_t)atoll(e) : (int64_t)1024;
   }();
   const bool narrow = mt * (N / 128) < narrow_below;
+  // 32 x 64 tiles when even the 64-wide grid is short of four workgroups per CU (the N = 128
+  // products: 514 -> 1028 workgroups, 2 -> 4 waves per SIMD)
+  static const int64_t short_below = [] {   // PCV_F32_SHORT_BELOW: A/B override
+    const char* e = getenv("PCV_F32_SHORT_BELOW");
+    return e ? (int64_t)atoll(e) : (int64_t)1024;
+  }();
+  const bool shrt = narrow && mt * (N / 64) < short_below;
   g.tiles_n = (int)(N / (narrow ? 64 : 128));
-  const unsigned blocks = (unsigned)(mt * g.tiles_n);
+  const unsigned blocks = (unsigned)((shrt ? (M + 31) / 32 : mt) * g.tiles_n);
   hipStream_t s = (hipStream_t)stream;
-#define GR_LAUNCH(TBv, EPv, BNv) hipLaunchKernelGGL((gemm_f32_rows_kernel<TBv, EPv, BNv>), dim3(blocks), dim3(256), 0, s, g)
-  if (narrow) {
+#define GR_LAUNCH(TBv, EPv, BNv) hipLaunchKernelGGL((gemm_f32_rows_kernel<TBv, EPv, BNv, 64>), dim3(blocks), dim3(256), 0, s, g)
+#define GR_LAUNCH32(TBv, EPv) hipLaunchKernelGGL((gemm_f32_rows_kernel<TBv, EPv, 64, 32>), dim3(blocks), dim3(256), 0, s, g)
+  if (shrt) {
+    if (tb) { if (epi) GR_LAUNCH32(true, true); else GR_LAUNCH32(true, false); }
+    else { if (epi) GR_LAUNCH32(false, true); else GR_LAUNCH32(false, false); }
+  } else if (narrow) {
     if (tb) { if (epi) GR_LAUNCH(true, true, 64); else GR_LAUNCH(true, false, 64); }
     else { if (epi) GR_LAUNCH(false, true, 64); else GR_LAUNCH(false, false, 64); }
   } else {
@@ -332,6 +350,7 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
     else { if (epi) GR_LAUNCH(false, true, 128); else GR_LAUNCH(false, false, 128); }
   }
 #undef GR_LAUNCH
+#undef GR_LAUNCH32
   return pcv_launch_status();
 }
 
