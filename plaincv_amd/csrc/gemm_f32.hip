@@ -327,11 +327,12 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
     return e ? (int64_t)atoll(e) : (int64_t)1024;
   }();
   const bool narrow = mt * (N / 128) < narrow_below;
-  // 32 x 64 tiles when even the 64-wide grid is short of four workgroups per CU (the N = 128
-  // products: 514 -> 1028 workgroups, 2 -> 4 waves per SIMD)
+  // 32 x 64 tiles when the 64-wide grid has fewer than 2048 workgroups (the ViT's N = 128 / 256 /
+  // 384 products: 2 -> 4+ waves per SIMD; C4 step 1.972 -> 1.934 (N = 128 only) -> 1.900 ms (all;
+  // thresholds 1024 / 1100 / 2048 / 4096 swept))
   static const int64_t short_below = [] {   // PCV_F32_SHORT_BELOW: A/B override
     const char* e = getenv("PCV_F32_SHORT_BELOW");
-    return e ? (int64_t)atoll(e) : (int64_t)1024;
+    return e ? (int64_t)atoll(e) : (int64_t)2048;
   }();
   const bool shrt = narrow && mt * (N / 64) < short_below;
   g.tiles_n = (int)(N / (narrow ? 64 : 128));
