@@ -229,14 +229,15 @@ int pcv_layernorm_fwd_f32(const float* x, int64_t ldx, const float* scale, const
 /* LayerNorm VJP with dscale/dbias (+=) computed in the same pass over dy and x (per-block partials
  * in ws, pcv_layernorm_bwd_f32_ws(R, D) floats, then one small reduction launch); D in
  * {64, 128, 256, 384, 512}, rows 16-B aligned (pcv_layernorm_bwd_f32_ok -> 0); dres may be NULL and
- * may alias dx.  Replaces pcv_layernorm_bwd + its parameter-gradient launch for the fp32 ViT
+ * may alias dx.  dxd (optional): also dxd = dropout_vjp(dx) with keep = hash3(*seed, site, row*D+col)
+ * (the next sublayer's dropout VJP, pcv_f32_epilogue_bwd's indexing).  Replaces pcv_layernorm_bwd + its parameter-gradient launch for the fp32 ViT
  * (models/vit_small.py:39-41 nn.LayerNorm under value_and_grad, flax_engine.py:95). */
 int pcv_layernorm_bwd_f32_ok(int D, int64_t lddy, int64_t ldx, int64_t ldres, int64_t lddx);
 int64_t pcv_layernorm_bwd_f32_ws(int64_t R, int D);
 int pcv_layernorm_bwd_f32(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* scale,
                           const float* mean, const float* rstd, const float* dres, int64_t ldres, float* dx,
                           int64_t lddx, float* dscale, float* dbias, float* ws, int64_t ws_floats, int64_t R, int D,
-                          void* stream);
+                          float* dxd, int64_t lddxd, float rate, const uint32_t* seed, uint32_t site, void* stream);
 /* dscale == dbias == NULL: the partials stay in ws and a later pcv_layernorm_part_reduce adds the
  * partials of several LayerNorms in one launch (device table of {part, dscale, dbias, nblk, D}). */
 int pcv_layernorm_part_job_size(void);

@@ -103,9 +103,12 @@ template <int NV>
 __global__ __launch_bounds__(256) void ln16_bwd_f32_kernel(const float* dy, int64_t lddy, const float* x,
                                                            int64_t ldx, const float* scale, const float* mean_in,
                                                            const float* rstd_in, const float* dres, int64_t ldres,
-                                                           float* dx, int64_t lddx, float* part, int64_t R) {
+                                                           float* dx, int64_t lddx, float* part, int64_t R,
+                                                           float* dxd, int64_t lddxd, uint32_t thresh, float dscale,
+                                                           const uint32_t* seedp, uint32_t site) {
   constexpr int D = 64 * NV;
   __shared__ float red[4][2][D];
+  const uint32_t seed = (dxd && thresh) ? *seedp : 0u;
   const int l16 = threadIdx.x & 15, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
   f32x4 pa[NV], pb[NV];
@@ -138,8 +141,20 @@ __global__ __launch_bounds__(256) void ln16_bwd_f32_kernel(const float* dy, int6
     sg /= D;
     sgx /= D;
 #pragma unroll
-    for (int i = 0; i < NV; ++i)
-      *reinterpret_cast<f32x4*>(dx + row * lddx + (16 * i + l16) * 4) = r[i] + rs * (g[i] - sg - xh[i] * sgx);
+    for (int i = 0; i < NV; ++i) {
+      const int c = (16 * i + l16) * 4;
+      const f32x4 o = r[i] + rs * (g[i] - sg - xh[i] * sgx);
+      *reinterpret_cast<f32x4*>(dx + row * lddx + c) = o;
+      if (dxd) {   // the next consumer's dropout VJP (flat index row * D + col, as f32_epilogue_bwd)
+        f32x4 od = o;
+        if (thresh) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            od[j] = keep_of(seed, site, (uint32_t)(row * D + c + j), thresh) ? o[j] * dscale : 0.f;
+        }
+        *reinterpret_cast<f32x4*>(dxd + row * lddxd + c) = od;
+      }
+    }
   } else {
 #pragma unroll
     for (int i = 0; i < NV; ++i) pa[i] = pb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -856,7 +871,13 @@ extern "C" int pcv_layernorm_bwd_f32_ok(int D, int64_t lddy, int64_t ldx, int64_
 extern "C" int pcv_layernorm_bwd_f32(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* scale,
                                      const float* mean, const float* rstd, const float* dres, int64_t ldres, float* dx,
                                      int64_t lddx, float* dscale, float* dbias, float* ws, int64_t ws_floats, int64_t R,
-                                     int D, void* stream) {
+                                     int D, float* dxd, int64_t lddxd, float rate, const uint32_t* seed, uint32_t site,
+                                     void* stream) {
+  if (dxd && (((reinterpret_cast<uintptr_t>(dxd)) & 15) || (lddxd & 3) || lddxd < D || (rate > 0.f && !seed)))
+    return PCV_EINVAL;
+  uint32_t th;
+  float sc;
+  f32_drop(dxd ? rate : 0.f, &th, &sc);
   if (R <= 0 || !dy || !x || !scale || !mean || !rstd || !dx || !ws || !dscale != !dbias) return PCV_EINVAL;
   if (ws_floats < pcv_layernorm_bwd_f32_ws(R, D)) return PCV_EINVAL;
   if (pcv_layernorm_bwd_f32_ok(D, lddy, ldx, dres ? ldres : 0, lddx)) return PCV_EINVAL;
@@ -867,7 +888,7 @@ extern "C" int pcv_layernorm_bwd_f32(const float* dy, int64_t lddy, const float*
   if (blocks >= (1ll << 31)) return PCV_EINVAL;
   PCV_LN16_DISPATCH(D, hipLaunchKernelGGL((ln16_bwd_f32_kernel<NV>), dim3((unsigned)blocks), dim3(256), 0,
                                           (hipStream_t)stream, dy, lddy, x, ldx, scale, mean, rstd, dres, ldres, dx,
-                                          lddx, ws, R));
+                                          lddx, ws, R, dxd, lddxd, th, sc, seed, site));
   if (!dscale) return pcv_launch_status();   // partials stay in ws for pcv_layernorm_part_reduce
   const int chunks = (int)(blocks / 64 < 1 ? 1 : (blocks / 64 > 64 ? 64 : blocks / 64));   // ~64 partials each
   hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * D + 63) / 64), chunks), dim3(256), 0,

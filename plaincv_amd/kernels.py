@@ -328,21 +328,24 @@ def layernorm_bwd_f32_fits(D, *ts):
     return hip.load().pcv_layernorm_bwd_f32_ok(int(D), *lds) == 0
 
 
-def layernorm_bwd_f32(dy, x, scale, mean, rstd, dres, dx, dscale, dbias, ws):
+def layernorm_bwd_f32(dy, x, scale, mean, rstd, dres, dx, dscale, dbias, ws, dxd=None, rate=0.0, seed=None, site=0):
     """fp32 LayerNorm VJP with the parameter gradients from the same pass (pcv_layernorm_bwd_f32, ws:
     fp32 workspace of layernorm_bwd_f32_ws(R, D) floats).  dscale = dbias = None leaves the per-block
     partials in ws for a LayerNormParamReduce; shapes the fused kernel does not take go through
-    pcv_layernorm_bwd (same arithmetic, two launches, gradients added at once)."""
+    pcv_layernorm_bwd (same arithmetic, two launches, gradients added at once).  dxd: also write
+    dropout_vjp(dx) (rate, seed, site) there -- the next sublayer's dropout VJP in the same pass."""
     R, D = x.shape
     ldr = _ld(dres) if dres is not None else 0
     if not layernorm_bwd_f32_fits(D, dy, x, dres, dx):
-        _chk(dscale is not None, "deferred LayerNorm parameter gradients need the fused kernel's shapes")
+        _chk(dscale is not None and dxd is None, "deferred LayerNorm parameter gradients / the fused dropout "
+             "VJP need the fused kernel's shapes")
         return layernorm_bwd(dy, x, scale, mean, rstd, dres, dx, None, dscale, dbias)
     _chk(dy.dtype == F32 and dx.dtype == F32 and tuple(dy.shape) == (R, D), "layernorm bwd f32")
     _dev(dy, x, scale, mean, rstd, dres, dx, dscale, dbias, ws)
     _chk(ws.dtype == F32 and ws.is_contiguous(), "layernorm bwd f32 workspace")
     hip.call("pcv_layernorm_bwd_f32", ptr(dy), _ld(dy), ptr(x), _ld(x), ptr(scale), ptr(mean), ptr(rstd),
-             ptr(dres), ldr, ptr(dx), _ld(dx), ptr(dscale), ptr(dbias), ptr(ws), ws.numel(), R, D, stream_ptr())
+             ptr(dres), ldr, ptr(dx), _ld(dx), ptr(dscale), ptr(dbias), ptr(ws), ws.numel(), R, D, ptr(dxd),
+             _ld(dxd) if dxd is not None else 0, float(rate), ptr(seed), int(site), stream_ptr())
 
 
 class LayerNormParamReduce:

@@ -271,10 +271,12 @@ class ViTRunnerF32:
                 red.add(self.ln_ws[2 + 2 * i], B * T, D, w["gs0"], w["gc0"])
             self.ln_red = red.finalize(dev)
 
-    def _ln_bwd(self, site, dy, x, scale, st, dres, dx, gs, gc):
-        """LayerNorm VJP; the parameter gradients deferred to self.ln_red when it is planned"""
+    def _ln_bwd(self, slot, dy, x, scale, st, dres, dx, gs, gc, **drop):
+        """LayerNorm VJP; the parameter gradients deferred to self.ln_red when it is planned (then the
+        fused kernel also takes the next sublayer's dropout VJP: drop = dxd, rate, seed, site)"""
         d = self.ln_red is not None
-        K.layernorm_bwd_f32(dy, x, scale, *st, dres, dx, None if d else gs, None if d else gc, self.ln_ws[site])
+        K.layernorm_bwd_f32(dy, x, scale, *st, dres, dx, None if d else gs, None if d else gc, self.ln_ws[slot],
+                            **(drop if d else {}))
 
     def _colsum(self, x, gb):
         """bias gradient += column sums of x, unless the weight-gradient launch folds it in"""
@@ -364,7 +366,8 @@ class ViTRunnerF32:
         for i in reversed(range(m.num_layers)):
             w, g = self.w[i], self.gb[i]
             dmo, da, dx1, dqkv = self.dmo_l[i], self.da_l[i], self.dx1_l[i], self.dqkv_l[i]
-            _epi_bwd(dx_in, dmo, rate=rate, seed=seed, site=site_mlp_out(i))            # MLP-out dropout VJP
+            if i == m.num_layers - 1 or self.ln_red is None:   # else written by layer i+1's LN_0 VJP
+                _epi_bwd(dx_in, dmo, rate=rate, seed=seed, site=site_mlp_out(i))        # MLP-out dropout VJP
             self._colsum(dmo, w["gb1"])
             g["fc2_d"].run(rate, seed)                        # da = dropout_vjp(dmo W1^T) * gelu'(pre)
             self._colsum(da, w["gb0"])
@@ -385,8 +388,9 @@ class ViTRunnerF32:
             self._colsum(dqkv, w["gbqkv"])
             g["qkv_d"].run()                                                           # self.dy0 = dqkv Wqkv^T
             if m.use_layernorm:
+                drop = dict(dxd=self.dmo_l[i - 1], rate=rate, seed=seed, site=site_mlp_out(i - 1)) if i > 0 else {}
                 self._ln_bwd(2 + 2 * i, self.dy0, self.xs[i], w["s0"], self.st0[i], dx1, self.dxo[i], w["gs0"],
-                             w["gc0"])
+                             w["gc0"], **drop)
             else:
                 _epi(self.dy0, self.dxo[i], res=dx1)
             dx_in = self.dxo[i]
