@@ -251,6 +251,10 @@ int pcv_attn_softmax_f32(const float* S, float* P, float* Pd, int64_t rows, int 
                          void* stream);
 int pcv_attn_softmax_bwd_f32(const float* P, float* dPd, int64_t rows, int T, const uint16_t* mask, float rate,
                              void* stream);
+/* x[b,t] = dropout((t == 0 ? cls : patch[b,t-1] + bias) + pos[t]) in fp32 (the patch-conv bias
+ * epilogue and flax's cls concat + pos add + Dropout, models/vit_small.py:95-109, in one pass; D % 4 == 0) */
+int pcv_vit_embed_fwd_f32(const float* patch, const float* bias, const float* cls, const float* pos, float* x, int B,
+                          int T, int D, float rate, const uint32_t* seed, uint32_t site, void* stream);
 int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls, float* dpos, int B, int T, int D, float rate,
                           const uint32_t* seed, uint32_t site, void* stream);
 /* Exact-fp32 row-panel GEMM with the Dense epilogue fused (csrc/gemm_f32.hip): C[M][N] =

@@ -227,6 +227,30 @@ __global__ __launch_bounds__(256) void ln_part_reduce_kernel(const LnPartJob* jo
 
 __host__ __device__ inline bool ln16_fits(int D) { return D % 64 == 0 && (D / 64 == 1 || D / 64 == 2 || D / 64 == 4 || D / 64 == 6 || D / 64 == 8); }
 
+// x[b, t] = (t == 0 ? cls : patch[b, t-1] + conv bias) + pos[t], dropout (flat index), 4 columns
+// per thread: the patch-conv bias epilogue and the embedding in one pass
+__global__ void vit_embed_fwd_f32_kernel(const float* patch, const float* bias, const float* cls, const float* pos,
+                                         float* x, int B, int T, int D, uint32_t thresh, float scale,
+                                         const uint32_t* seedp, uint32_t site) {
+  const uint32_t seed = thresh ? *seedp : 0u;
+  const int D4 = D / 4;
+  const int64_t n4 = (int64_t)B * T * D4;
+  for (int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i4 < n4; i4 += (int64_t)gridDim.x * blockDim.x) {
+    const int d = (int)(i4 % D4) * 4;
+    const int64_t bt = i4 / D4;
+    const int t = (int)(bt % T), b = (int)(bt / T);
+    f32x4 v = *reinterpret_cast<const f32x4*>(pos + (int64_t)t * D + d);
+    if (t == 0) v += *reinterpret_cast<const f32x4*>(cls + d);
+    else v += *reinterpret_cast<const f32x4*>(patch + ((int64_t)b * (T - 1) + t - 1) * D + d) +
+              *reinterpret_cast<const f32x4*>(bias + d);
+    if (thresh) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = hash3(seed, site, (uint32_t)(bt * D + d + j)) >= thresh ? v[j] * scale : 0.f;
+    }
+    *reinterpret_cast<f32x4*>(x + bt * D + d) = v;
+  }
+}
+
 __device__ __forceinline__ float gelu_tanh_f32(float x) {
   const float k = 0.7978845608028654f;   // sqrt(2/pi)
   return 0.5f * x * (1.f + tanhf(k * (x + 0.044715f * x * x * x)));
@@ -945,6 +969,21 @@ extern "C" int pcv_attn_softmax_bwd_f32(const float* P, float* dPd, int64_t rows
   const int n64 = 2 * ((T + 127) / 128);
   hipLaunchKernelGGL(attn_softmax_bwd_f32_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
                      P, dPd, rows, T, rate > 0.f ? mask : nullptr, n64, rate > 0.f ? 1.f / (1.f - rate) : 1.f);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_vit_embed_fwd_f32(const float* patch, const float* bias, const float* cls, const float* pos,
+                                     float* x, int B, int T, int D, float rate, const uint32_t* seed, uint32_t site,
+                                     void* stream) {
+  if (B <= 0 || T <= 1 || D <= 0 || (D & 3) || !patch || !bias || !cls || !pos || !x || (rate > 0.f && !seed))
+    return PCV_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(patch) | reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(cls) |
+       reinterpret_cast<uintptr_t>(pos) | reinterpret_cast<uintptr_t>(x)) & 15)
+    return PCV_EALIGN;
+  uint32_t th; float sc;
+  f32_drop(rate, &th, &sc);
+  hipLaunchKernelGGL(vit_embed_fwd_f32_kernel, dim3(f32_grid((int64_t)B * T * D / 4)), dim3(256), 0,
+                     (hipStream_t)stream, patch, bias, cls, pos, x, B, T, D, th, sc, seed, site);
   return pcv_launch_status();
 }
 

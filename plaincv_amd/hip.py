@@ -73,6 +73,7 @@ SIGNATURES = {
     "pcv_f32_epilogue_bwd": [P, I64, P, I64, P, I64, I64, I32, I32, F32, P, U32, P],
     "pcv_attn_softmax_f32": [P, P, P, I64, I32, P, F32, P],
     "pcv_attn_softmax_bwd_f32": [P, P, I64, I32, P, F32, P],
+    "pcv_vit_embed_fwd_f32": [P, P, P, P, P, I32, I32, I32, F32, P, U32, P],
     "pcv_vit_embed_bwd_f32": [P, P, P, P, I32, I32, I32, F32, P, U32, P],
     "pcv_gemm_f32_rows_ok": [I64, I64, I64, P, I64, P, I64, I32],
     "pcv_gemm_f32_rows": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32, P],

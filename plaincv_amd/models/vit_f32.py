@@ -306,8 +306,8 @@ class ViTRunnerF32:
         hip.call("pcv_vit_patchify_f32", ptr(images), ptr(self.patches), B, self.Hh, self.Ww, self.C, m.patch_size,
                  stream_ptr())
         self.g_patch.run()
-        _epi(self.patch_out, self.patch_out, bias=self.bconv)
-        K.vit_embed_fwd(self.patch_out, self.cls, self.pos, self.xs[0], None, B, T, D, rate, seed, SITE_EMBED)
+        hip.call("pcv_vit_embed_fwd_f32", ptr(self.patch_out), ptr(self.bconv), ptr(self.cls), ptr(self.pos),
+                 ptr(self.xs[0]), B, T, D, float(rate), ptr(seed), SITE_EMBED, stream_ptr())
         if rate > 0.0:
             K.attn_drop_mask(seed, site_attn(0), T, rate, self.attn_mask, layers=m.num_layers,
                              site_stride=site_attn(1) - site_attn(0))
