@@ -55,9 +55,35 @@ __global__ __launch_bounds__(QRB_THREADS) void qrb_panel_kernel(const QrbJob* __
   float* G = P + (int64_t)nb * m;   // G[k][i] = v_k . v_i (k < i)
   float* Ts = G + nb * nb;               // [nb][nb + 1]: row k owned by thread k, padded stride
   float* tau_s = Ts + nb * (nb + 1);
-  for (int e = tid; e < nbp * m; e += QRB_THREADS) {
-    const int c = e / m, r = e - c * m;
-    P[e] = jb.Wt[(int64_t)(j0 + c) * n + j0 + r];
+  if ((n & 3) == 0 && (j0 & 3) == 0) {
+    // float4 rows, 8 loads in flight per thread before their LDS stores (a one-float-per-iteration
+    // loop serialised ~24 global round trips per thread)
+    const int m4 = m >> 2, tot = nbp * m4;
+    constexpr int PF = 8;
+    for (int e0 = tid; e0 < tot; e0 += QRB_THREADS * PF) {
+      f32x4 v[PF];
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int e = e0 + u * QRB_THREADS;
+        if (e < tot) {
+          const int c = e / m4, r4 = e - c * m4;
+          v[u] = *reinterpret_cast<const f32x4*>(jb.Wt + (int64_t)(j0 + c) * n + j0 + 4 * r4);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int e = e0 + u * QRB_THREADS;
+        if (e < tot) {
+          const int c = e / m4, r4 = e - c * m4;
+          *reinterpret_cast<f32x4*>(P + c * m + 4 * r4) = v[u];
+        }
+      }
+    }
+  } else {
+    for (int e = tid; e < nbp * m; e += QRB_THREADS) {
+      const int c = e / m, r = e - c * m;
+      P[e] = jb.Wt[(int64_t)(j0 + c) * n + j0 + r];
+    }
   }
   __syncthreads();
   // Column c belongs to wave c % QRB_WAVES: the owner forms its reflector (norm by wave reduction),
