@@ -43,6 +43,22 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// The same total from DPP row operations (VALU, no LDS round trip; lane 63 gathers the rows, one
+// readlane broadcasts it): for serial chains of wave reductions, where each ds_bpermute of
+// wave_sum is a full LDS latency.  The whole wave must be active.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROW_MASK, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f32<0xB1, 0xF>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f32<0x4E, 0xF>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f32<0x141, 0xF>(v);   // row_half_mirror: 8-lane sums
+  v += dpp_f32<0x140, 0xF>(v);   // row_mirror: 16-lane row sums
+  v += dpp_f32<0x142, 0xA>(v);   // row_bcast:15 -> rows 1, 3 hold 32-lane sums
+  v += dpp_f32<0x143, 0xC>(v);   // row_bcast:31 -> row 3 holds the total
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

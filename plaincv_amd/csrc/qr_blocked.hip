@@ -95,7 +95,7 @@ __global__ __launch_bounds__(QRB_THREADS) void qrb_panel_kernel(const QrbJob* __
     if (wv == c % QRB_WAVES) {
       float s2 = 0.f;
       for (int r = c + 1 + lane; r < m; r += 64) s2 += x[r] * x[r];
-      s2 = wave_sum(s2);
+      s2 = wave_sum_dpp(s2);
       const float alpha = x[c];
       float tau = 0.f, scale = 0.f;
       if (s2 > 0.f) {
@@ -116,27 +116,46 @@ __global__ __launch_bounds__(QRB_THREADS) void qrb_panel_kernel(const QrbJob* __
       float d[QRB_MAXCOL];
 #pragma unroll
       for (int j = 0; j < QRB_MAXCOL; ++j) d[j] = 0.f;
+      // branch-free loads (columns clamped into the panel, masked): a per-j guard put every LDS
+      // read behind its own branch and wait
+      float* pc[QRB_MAXCOL];
+#pragma unroll
+      for (int j = 0; j < QRB_MAXCOL; ++j) pc[j] = P + min(c0 + j * QRB_WAVES, nbp - 1) * m;
       for (int r = c + lane; r < m; r += 64) {
         const float v = r == c ? 1.f : x[r];
 #pragma unroll
-        for (int j = 0; j < QRB_MAXCOL; ++j)
-          if (j < nc) d[j] += v * P[(c0 + j * QRB_WAVES) * m + r];
+        for (int j = 0; j < QRB_MAXCOL; ++j) d[j] += v * pc[j][r];
       }
 #pragma unroll
-      for (int j = 0; j < QRB_MAXCOL; ++j) d[j] = wave_sum(d[j]) * tau;
-      for (int r = c + lane; r < m; r += 64) {
+      for (int j = 0; j < QRB_MAXCOL; ++j) d[j] = j < nc ? d[j] : 0.f;   // (clamped columns: discarded)
+#pragma unroll
+      for (int j = 0; j < QRB_MAXCOL; ++j) d[j] = wave_sum_dpp(d[j]) * tau;
+      for (int r = c + lane; r < m; r += 64) {   // loads batched, stores guarded (d[j] = 0 past nc)
         const float v = r == c ? 1.f : x[r];
+        float nv[QRB_MAXCOL];
+#pragma unroll
+        for (int j = 0; j < QRB_MAXCOL; ++j) nv[j] = pc[j][r] - d[j] * v;
 #pragma unroll
         for (int j = 0; j < QRB_MAXCOL; ++j)
-          if (j < nc) P[(c0 + j * QRB_WAVES) * m + r] -= d[j] * v;
+          if (j < nc) pc[j][r] = nv[j];
       }
     }
   }
   __syncthreads();
   // V columns (unit diagonal, zeros above) into rows j0.. of V
-  for (int e = tid; e < m * nbp; e += QRB_THREADS) {
-    const int r = e / nbp, c = e - r * nbp;
-    jb.V[(int64_t)(j0 + r) * n + j0 + c] = r < c ? 0.f : (r == c ? 1.f : P[c * m + r]);
+  if ((nbp & 3) == 0 && (n & 3) == 0 && (j0 & 3) == 0) {   // float4 rows; lanes run along r (P reads conflict-free)
+    for (int e = tid; e < m * (nbp >> 2); e += QRB_THREADS) {
+      const int c4 = e / m, r = e - c4 * m, c = 4 * c4;
+      f32x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = r < c + j ? 0.f : (r == c + j ? 1.f : P[(c + j) * m + r]);
+      *reinterpret_cast<f32x4*>(jb.V + (int64_t)(j0 + r) * n + j0 + c) = v;
+    }
+  } else {
+    for (int e = tid; e < m * nbp; e += QRB_THREADS) {
+      const int r = e / nbp, c = e - r * nbp;
+      jb.V[(int64_t)(j0 + r) * n + j0 + c] = r < c ? 0.f : (r == c ? 1.f : P[c * m + r]);
+    }
   }
   // G[k][i] = v_k . v_i (k < i) over rows >= i (v_i is zero above i, v_i[i] = 1): wave w takes the
   // columns i = w, w + W, ...; one pass over v_i accumulates all k < i, reductions side by side
@@ -144,16 +163,15 @@ __global__ __launch_bounds__(QRB_THREADS) void qrb_panel_kernel(const QrbJob* __
     float d[QRB_MAXNB];
 #pragma unroll
     for (int k = 0; k < QRB_MAXNB; ++k) d[k] = 0.f;
-    for (int r = i + lane; r < m; r += 64) {
+    for (int r = i + lane; r < m; r += 64) {   // branch-free: columns clamped into the panel
       const float vi = r == i ? 1.f : P[i * m + r];
 #pragma unroll
-      for (int k = 0; k < QRB_MAXNB; ++k)
-        if (k < i) d[k] += P[k * m + r] * vi;
+      for (int k = 0; k < QRB_MAXNB; ++k) d[k] += P[min(k, nbp - 1) * m + r] * vi;
     }
 #pragma unroll
     for (int k = 0; k < QRB_MAXNB; ++k)
       if (k < i) {
-        const float t = wave_sum(d[k]);
+        const float t = wave_sum_dpp(d[k]);
         if (lane == 0) G[k * nb + i] = t;
       }
   }
@@ -168,10 +186,16 @@ __global__ __launch_bounds__(QRB_THREADS) void qrb_panel_kernel(const QrbJob* __
     for (int i = 0; i < QRB_MAXNB; ++i) {
       if (i < nbp) {
         const float ti = tau_s[i];
+        // G[0:i, i] in one LDS read (lane l holds G[l][i]), broadcast per l by readlane: the
+        // per-l LDS reads of the recurrence were a ~30 us latency chain
+        const float gcol = lane < i ? G[lane * nb + i] : 0.f;
         float acc = 0.f;
 #pragma unroll
         for (int l = 0; l < QRB_MAXNB; ++l)
-          if (l < i && l >= lane) acc += tr[l] * G[l * nb + i];
+          if (l < i) {
+            const float gl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gcol), l));
+            acc += l >= lane ? tr[l] * gl : 0.f;
+          }
         if (lane < i) tr[i] = ti == 0.f ? 0.f : -ti * acc;
         else if (lane == i) tr[i] = ti;
       }
