@@ -20,6 +20,8 @@ class AdamBranch:
 
     def __init__(self, store, names, b1, b2, eps, eps_root, wd, nesterov):
         self.chunks = store.chunks(names)
+        if 0 < self.chunks.shape[0] < 512:   # a small branch (the ViT's non-matrix leaves): 1024-element
+            self.chunks = store.chunks(names, chunk=1024)   # chunks, ~4x the workgroups (latency-bound)
         self.nchunks = int(self.chunks.shape[0])
         self.hp = (float(b1), float(b2), float(eps), float(eps_root), float(wd), int(nesterov))
         self.names = list(store.params) if names is None else list(names)
