@@ -18,10 +18,13 @@ from .base import GradientTransformation, OptState, ensure_grads
 class AdamBranch:
     """AdamW restricted to a set of leaves (all leaves when names is None)."""
 
-    def __init__(self, store, names, b1, b2, eps, eps_root, wd, nesterov):
+    def __init__(self, store, names, b1, b2, eps, eps_root, wd, nesterov, small_chunks=True):
+        """small_chunks: a small branch (< 512 chunks of 4096, the ViT's non-matrix leaves) runs
+        1024-element chunks, ~4x the workgroups of its latency-bound launch; Muon keeps 4096 (its
+        fused step launch runs the branch beside the NS workgroups, measured there)."""
         self.chunks = store.chunks(names)
-        if 0 < self.chunks.shape[0] < 512:   # a small branch (the ViT's non-matrix leaves): 1024-element
-            self.chunks = store.chunks(names, chunk=1024)   # chunks, ~4x the workgroups (latency-bound)
+        if small_chunks and 0 < self.chunks.shape[0] < 512:
+            self.chunks = store.chunks(names, chunk=1024)
         self.nchunks = int(self.chunks.shape[0])
         self.hp = (float(b1), float(b2), float(eps), float(eps_root), float(wd), int(nesterov))
         self.names = list(store.params) if names is None else list(names)

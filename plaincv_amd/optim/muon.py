@@ -83,7 +83,7 @@ class Muon(GradientTransformation):
         routed = [k for k, p in store.params.items() if should_use_matrix_preconditioner(k, p)]
         rest = [k for k in store.params if k not in routed]
         b1, b2, eps_root, awd = self.adam
-        st.branch = AdamBranch(store, rest, b1, b2, self.eps, eps_root, awd, self.nesterov)
+        st.branch = AdamBranch(store, rest, b1, b2, self.eps, eps_root, awd, self.nesterov, small_chunks=False)
         st.routed = routed
         # Group routed matrices by NS shape (min, max).  Groups whose operand fits one
         # workgroup's LDS (csrc/muon_fused.hip) run Newton-Schulz in a single launch; the
