@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void signum_kernel(float* p, const float* g, f
     const float mi = h.momentum * m[i] + (1.f - h.momentum) * gi;
     m[i] = mi;
     const float d = h.nesterov ? (1.f - h.momentum) * gi + h.momentum * mi : mi;
-    float u = (float)((d > 0.f) - (d < 0.f));   // jnp.sign (sign(0) = 0)
+    float u = d != d ? d : (float)((d > 0.f) - (d < 0.f));   // jnp.sign (sign(0) = 0, sign(NaN) = NaN)
     const float pi = p[i];
     if (h.wd > 0.f) u += h.wd * pi;
     u = -h.lr * u;
@@ -58,7 +58,8 @@ __global__ __launch_bounds__(256) void signum_kernel(float* p, const float* g, f
 // schedule-free scalars sf = [weight_sum, max_lr, ck]: max_lr = max(max_lr, lr), w = max_lr^power,
 // total = weight_sum + w, ck = w / total (nan -> 0, nan if w or total is nan), step_count += 1
 __global__ void sf_prep_kernel(float* sf, int* step_count, float lr, float power) {
-  const float max_lr = fmaxf(sf[1], lr);
+  const float prev = sf[1];
+  const float max_lr = (prev != prev || lr != lr) ? prev + lr : fmaxf(prev, lr);   // jnp.maximum propagates NaN
   const float w = powf(max_lr, power);
   const float total = sf[0] + w;
   float ck = w / total;

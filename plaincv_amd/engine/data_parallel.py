@@ -37,6 +37,25 @@ def rank():
     return dist.get_rank() if is_initialized() else 0
 
 
+def resolve_use_dp(cfg, world):
+    """train_lm.py:476-506: ``use_pmap`` (None = auto) and ``force_single_device`` decide whether the
+    visible devices train data-parallel.  Here the device count is the launcher's WORLD_SIZE (one
+    process per GPU), so a config that asks for single-device training while N > 1 ranks were
+    launched is rejected loudly instead of silently running N-way DP -- launch one process."""
+    requested = getattr(cfg, "use_pmap", None)
+    force_single = bool(getattr(cfg, "force_single_device", False))
+    if requested is None:
+        use_dp = world > 1 and not force_single
+    else:
+        use_dp = bool(requested) and world > 1 and not force_single
+    if world > 1 and not use_dp:
+        raise ValueError(
+            f"config requests single-device training (use_pmap={requested!r}, force_single_device="
+            f"{force_single}) but {world} ranks were launched; start one process (python train_lm.py ...) "
+            "or drop the key")
+    return use_dp
+
+
 def init_from_env(backend=None):
     """torchrun-style env (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR/PORT).  Returns
     (rank, local_rank, world_size, device)."""

@@ -198,6 +198,41 @@ def _device_storages(objs, depth=6):
     return list(found.values())
 
 
+def _host_scalars(obj, depth=6):
+    """(owner, key, value) for every host int/float/bool reachable from obj through plain objects,
+    dicts and lists -- e.g. Soap's ``host_step`` inside a ScheduleFree state's ``base``."""
+    found, seen = [], set()
+
+    def walk(o, d):
+        if d <= 0 or id(o) in seen or isinstance(o, (torch.Tensor, str, bytes, type(None))):
+            return
+        seen.add(id(o))
+        if isinstance(o, dict):
+            items = list(o.items())
+        elif isinstance(o, list):
+            items = list(enumerate(o))
+        elif hasattr(o, "__dict__") and not callable(o):
+            items = list(vars(o).items())
+        else:
+            return
+        for k, v in items:
+            if isinstance(v, (bool, int, float)):
+                found.append((o, k, v))
+            else:
+                walk(v, d - 1)
+
+    walk(obj, depth)
+    return found
+
+
+def _restore_host_scalars(found):
+    for o, k, v in found:
+        if isinstance(o, (dict, list)):
+            o[k] = v
+        else:
+            setattr(o, k, v)
+
+
 class GraphedTrainStep:
     """One hipGraph per step: seed advance, zero-grad, forward, backward,
     (all-reduce outside the graph when world_size > 1), optimizer.
@@ -225,7 +260,7 @@ class GraphedTrainStep:
         store = state.params
         saved = [(st, st.clone()) for st in _device_storages([store.flat, store.shadow, self.runner.seed,
                                                               state.opt_state, state.batch_stats])]
-        host = {k: v for k, v in vars(state.opt_state).items() if isinstance(v, (int, float, bool))}  # e.g. host_step
+        host = _host_scalars(state.opt_state)   # e.g. host_step, also inside wrapped (schedule-free) states
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self._fb()
@@ -237,8 +272,7 @@ class GraphedTrainStep:
             for st, copy in saved:
                 st.copy_(copy)
             torch.cuda.synchronize()
-            for k, v in host.items():
-                setattr(state.opt_state, k, v)
+            _restore_host_scalars(host)
             if self.distributed or not self.opt_graphed:
                 with torch.cuda.graph(self.g_fb, stream=s):
                     self._fb()

@@ -323,8 +323,8 @@ class Eigh:
     def _run_big(self, s):
         """Host-driven sweeps (one sync per sweep): SOAP's one-off initial basis and Shampoo's
         fallback; skipped jobs (Newton converged) are checked once up front."""
-        skips = [it["skip"] for it in self.big if it["skip"] is not None]
-        if len(skips) == len(self.big) and all(float(x.item()) <= 0.5 for x in skips):
+        skips = [it["skip"].reshape(-1)[:1] for it in self.big if it["skip"] is not None]
+        if len(skips) == len(self.big) and float(torch.cat(skips).max().item()) <= 0.5:   # one sync
             return
         nb, n_max = len(self.big), self.big_n
         hip.call("pcv_eigh_big_init", ptr(self.b_dev), nb, n_max, self.big_ldv, s)

@@ -25,7 +25,10 @@ class ScheduleFree(GradientTransformation):
             raise ValueError("The current implementation of schedule_free requires b1 > 0.")
         self.base = base
         self.lr, self.b1, self.power = float(learning_rate), float(b1), float(weight_lr_power)
-        self.graphable = bool(getattr(base, "graphable", True))
+
+    @property
+    def graphable(self):   # the base decides, after its init has seen the factor sizes
+        return bool(getattr(self.base, "graphable", True))
 
     def init(self, store):
         st = OptState(store.device)

@@ -30,7 +30,7 @@ from .. import kernels as K
 from .adamw import AdamBranch, _views
 from .base import GradientTransformation, OptState, ensure_grads
 from .matrix_routing import should_use_matrix_preconditioner
-from .precond import Eigh, GemmF32, NewtonRoot
+from .precond import EIGH_MAX_N, Eigh, GemmF32, NewtonRoot
 
 
 def _should_use_shampoo(name, p):
@@ -80,6 +80,9 @@ class Shampoo(GradientTransformation):
             s.TL, s.TR, s.AL, s.AR = z(r, r), z(c, c), z(r, r), z(c, c)
             s.PL, s.PR, s.T1 = z(r, r), z(c, c), z(r, c)
             st.mats.append(s)
+        # a factor above EIGH_MAX_N takes the host-driven big-matrix eigh as its Newton fallback
+        # (sweeps until converged, decided with host syncs), so such a step cannot be captured
+        self.graphable = self.root_method == "newton" and all(max(s.r, s.c) <= EIGH_MAX_N for s in st.mats)
         st.host_step = 0
         st.plans = {}
         return st

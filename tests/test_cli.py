@@ -160,3 +160,22 @@ def test_save_loss_curves(tmp_path):
         assert open(png, "rb").read(8) == b"\x89PNG\r\n\x1a\n"
     with pytest.raises(ValueError, match="same length"):
         save_loss_curves(cfg, "soap", [1.0], [1, 2], [2.0, 1.5], [2.1, 1.7], [0.1, 0.3], [0.1, 0.2])
+
+
+@pytest.mark.parametrize("keys,world,ok,use", [({}, 1, True, False), ({}, 4, True, True),
+                                               ({"use_pmap": True}, 1, True, False),
+                                               ({"use_pmap": True}, 2, True, True),
+                                               ({"use_pmap": False}, 1, True, False),
+                                               ({"use_pmap": False}, 2, False, None),
+                                               ({"force_single_device": True}, 8, False, None),
+                                               ({"force_single_device": True}, 1, True, False)])
+def test_use_pmap_force_single_device(keys, world, ok, use):
+    """train_lm.py:476-483: the keys decide DP; a single-device request under N > 1 ranks is refused."""
+    from plaincv_amd.engine.data_parallel import resolve_use_dp
+    from utils import Config
+    cfg = Config(model="transformer", **keys)
+    if ok:
+        assert resolve_use_dp(cfg, world) is use
+    else:
+        with pytest.raises(ValueError, match="single-device"):
+            resolve_use_dp(cfg, world)

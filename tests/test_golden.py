@@ -124,7 +124,8 @@ def test_hip_vit_golden_muon3(dev):
             continue
         r = _move_rel(got[k].numpy(), p[k].numpy(), z["muon3:" + k])
         print(f"GOLDEN_MUON3 {k} {r:.4f}")
-        assert r < 0.5, (k, r)
+        # measured <= 0.28 (r03; bf16 NS5 + bf16-placement gradients vs the fixture's oracle run)
+        assert r < 0.4, (k, r)
 
 
 @pytest.mark.gpu
@@ -156,4 +157,4 @@ def test_hip_lm_golden_adamw3(dev):
             idx = sample % g.size
             r = _move_rel(g[idx], p0[idx], z["adamw3_sample:" + k])
         print(f"GOLDEN_ADAMW3 {k} {r:.4f}")
-        assert r < 0.5, (k, r)
+        assert r < 0.08, (k, r)      # measured <= 0.040 (r03)

@@ -45,9 +45,17 @@ def test_lm_grads_match_oracle(dev, tie, b, T, mlp):
     (loss, acc), grads = value_and_grad(
         lambda p: lm_loss_and_acc(transformer_apply(p, ids[:, :-1], omc, torch.bfloat16), ids[:, 1:]), init)
     assert abs(met[0].item() - loss.item()) < 2e-2, (met[0].item(), loss.item())
+    init64 = {k: v.double() for k, v in init.items()}
+    _, g64 = value_and_grad(
+        lambda p: lm_loss_and_acc(transformer_apply(p, ids[:, :-1], omc, torch.float64), ids[:, 1:]), init64)
     for k in init:
         r = _rel(gg[k], grads[k])
+        # against exact fp64, relative to the bf16-placement oracle's own error (the 6e-2 bound
+        # against the bf16 oracle is the sum of the two sides' bf16 noise)
+        e_hip, e_bf = _rel(gg[k], g64[k]), _rel(grads[k], g64[k])
+        print(f"LMGRAD {k} hip_vs_bf16oracle {r:.4f} hip_vs_fp64 {e_hip:.4f} bf16oracle_vs_fp64 {e_bf:.4f}")
         assert r < 6e-2, (k, r)
+        assert e_hip < max(1e-2, 1.5 * e_bf), (k, e_hip, e_bf)
 
 
 @pytest.mark.parametrize("optim,clip", [("adamw", None), ("muon", 1.0), ("adamw", 0.05), ("muon", 0.05)])

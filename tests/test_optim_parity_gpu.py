@@ -48,7 +48,15 @@ def _lm_layout():
     return Transformer(mc).layout()
 
 
-LAYOUTS = {"vit_c2": _vit_layout, "lm768": _lm_layout}
+def _lm1024_layout():
+    """BASELINE configs[4] (tr_420M_x8gpu.yaml:9-35) block: d 1024, 16 heads, F = int(8/3 * 1024) = 2730
+    (ragged: w_qkv 1024x3072, fused gate|up 1024x2x2730 padded to 2736, fc2 2730x1024)."""
+    from plaincv_amd.models.LM.transformer import ModelConfig, Transformer
+    mc = ModelConfig(vocab_size=1000, dim=1024, expand=8 / 3, n_layers=1, n_heads=16, mlp="glu", seq_len=64)
+    return Transformer(mc).layout()
+
+
+LAYOUTS = {"vit_c2": _vit_layout, "lm768": _lm_layout, "lm1024": _lm1024_layout}
 
 
 def _grads(layout, gen, scale_by_leaf):
@@ -134,7 +142,7 @@ def test_adamw_update_parity(dev, which, mode, gscale):
     assert wa <= ADAM_TOL, wa
 
 
-@pytest.mark.parametrize("which", ["vit_c2", "lm768"])
+@pytest.mark.parametrize("which", ["vit_c2", "lm768", "lm1024"])
 @pytest.mark.parametrize("mode,gscale", [("update", 1.0), ("step_", 0.37)])
 def test_muon_update_parity(dev, which, mode, gscale):
     """Routed leaves through the fused one-workgroup NS kernel (ViT) and the batched-GEMM chain
@@ -144,7 +152,11 @@ def test_muon_update_parity(dev, which, mode, gscale):
     lr, wd = 1e-2, 0.1
     gpu = Muon(lr, weight_decay=wd, adam_b1=0.9, adam_b2=0.95, adam_weight_decay=wd)
     ora = oopt.muon(lr, weight_decay=wd, adam_b1=0.9, adam_b2=0.95, adam_weight_decay=wd)
-    steps = run_pair(dev, LAYOUTS[which](), gpu, ora, 3, mode, gscale)
+    lay = LAYOUTS[which]()
+    if which == "lm1024":   # the C5 routed shapes really are the ragged ones
+        shapes = {tuple(l.shape) for k, l in lay.leaves.items() if _routed(k, torch.empty(l.shape))}
+        assert {(1024, 3072), (1024, 2730), (2730, 1024), (1024, 1024)} <= shapes, shapes
+    steps = run_pair(dev, lay, gpu, ora, 3, mode, gscale)
     wr, wa = worst(steps, _routed)
     assert wr <= MUON_TOL, wr
     assert wa <= ADAM_TOL, wa

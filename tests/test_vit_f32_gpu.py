@@ -161,3 +161,54 @@ def test_vit_f32_unfused_attention_matches_fused(dev, monkeypatch):
         out.append((met[0].item(), st.params.grad_flat.clone()))
     assert abs(out[0][0] - out[1][0]) <= 1e-6 * abs(out[1][0])
     assert rel(out[0][1], out[1][1]) < 1e-5
+
+
+@pytest.mark.parametrize("optim,mlp", [("soap+schedule_free", 128), ("shampoo", 320)])
+def test_graphed_step_matches_eager_host_driven(dev, optim, mlp):
+    """GraphedTrainStep == eager steps where the optimizer keeps host state:
+    * schedule_free around SOAP: Soap's ``host_step`` lives in the wrapper's ``base`` state; the
+      warm-up must restore it (else the first real step skips SOAP's init eigh);
+    * Shampoo with a factor above 256 (mlp 320): its Newton fallback is the host-driven big eigh,
+      so the optimizer must stay out of the capture (``graphable`` False) and run eagerly."""
+    from plaincv_amd.engine import GraphedTrainStep, create_train_state, make_train_step
+    from utils import Config
+    name, _, wrap = optim.partition("+")
+    m = _model(0.1, M=mlp)
+    shape = (4, 16, 16, 3)
+    # no SOAP refresh inside the 4 steps: a refresh's QR power step amplifies the fp32 runner's
+    # run-to-run atomics noise (split-K weight gradients) to ~1 % in ANY two runs, graphed or not
+    cfg = Config(optim=name, lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9, precondition_frequency=10,
+                 schedule_free=bool(wrap), schedule_free_lr=0.01, eps=1e-8 if name == "soap" else 1e-4)
+    init = m.init(2, shape)
+    sa = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=init)
+    sb = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=init)
+    g = torch.Generator().manual_seed(1)
+    gs = GraphedTrainStep(sa, shape, warmup=2)
+    if name == "shampoo":
+        assert not sa.tx.graphable and not gs.opt_graphed
+    torch.cuda.synchronize()
+    assert torch.equal(sa.params.flat, sb.params.flat)
+    sb.runner_for(shape).seed.copy_(gs.runner.seed)
+    flat0 = sb.params.flat.clone()
+    step = make_train_step()
+    for _ in range(4):
+        images = torch.randint(0, 256, shape, generator=g, dtype=torch.uint8).to(dev)
+        labels = torch.randint(0, 10, (4,), generator=g, dtype=torch.int32).to(dev)
+        gs(images, labels)
+        step(sb, (images, labels))
+    torch.cuda.synchronize()
+    if name == "soap":
+        assert sa.opt_state.base.host_step == sb.opt_state.base.host_step == 3
+    # per-leaf movement (bias column sums use fp32 atomics, so bit equality is not expected; the
+    # attention key biases are excluded: their true gradient is exactly 0, so both runs feed the
+    # Adam branch pure rounding noise, which it normalises into full-size steps of random sign)
+    a, b = sa.params.to_dict(), sb.params.to_dict()
+    bad = {}
+    for k in b:
+        if k.endswith("key/bias"):
+            continue
+        p0 = sb.params._view(flat0, sb.params.leaf(k)).cpu()
+        e = rel(a[k] - p0, b[k] - p0)
+        if e > 1e-3:
+            bad[k] = e
+    assert not bad, bad

@@ -73,8 +73,10 @@ def test_vit_train_step_matches_oracle(dev, optim):
       (2) the applied update against the oracle optimizer fed the HIP step's own gradients
           (tests/parity_util.step_rel: AdamW leaves 1e-5, Muon routed leaves 2e-2), so an
           optimizer error cannot hide inside the bf16 gradient differences;
-    and after the 3 steps (3) the parameter movement against an independent oracle trajectory
-    (rel-L2 of the movement; key biases excluded: their true gradient is exactly 0).
+    and after the 3 steps (3) the parameter movement against an independent oracle trajectory in
+    the same bf16 placement (rel-L2 of the movement; key biases excluded: their true gradient is
+    exactly 0), bounded by the oracle's own bf16-placement-vs-fp32 spread of the same movement
+    (2x, floor 2 %) -- the precision noise any bf16 implementation carries, not a fixed 50 %.
     B = 16: the 10-class head gradient is then full rank (see test_optim_parity_gpu)."""
     from oracle import optim as oopt
     from oracle.engine import apply_updates, cross_entropy_loss, value_and_grad
@@ -91,8 +93,9 @@ def test_vit_train_step_matches_oracle(dev, optim):
     st = create_train_state(0, m, 1e-3, shape, m.num_classes, cfg=cfg, init_params=init)
     step = make_train_step()
     tx_h, tx_o = oopt.get_optimizer(cfg), oopt.get_optimizer(cfg)
-    s_h, s_o = tx_h.init(init), tx_o.init(init)
-    po = dict(init)
+    tx_32 = oopt.get_optimizer(cfg)
+    s_h, s_o, s_32 = tx_h.init(init), tx_o.init(init), tx_32.init(init)
+    po, p32 = dict(init), dict(init)
     oc = _oracle_cfg(m)
     gen = torch.Generator().manual_seed(5)
     for it in range(3):
@@ -120,10 +123,22 @@ def test_vit_train_step_matches_oracle(dev, optim):
                                                              labels), None), po)
         uo, s_o = tx_o.update(go, s_o, po)
         po = apply_updates(po, uo)
+        _, g32 = value_and_grad(lambda p: (cross_entropy_loss(vit_apply(p, images, oc, True, it), labels), None), p32)
+        u32, s_32 = tx_32.update(g32, s_32, p32)
+        p32 = apply_updates(p32, u32)
     got = st.params.to_dict()
+    flips, n = 0, 0
     for k in init:
         if k.endswith("key/bias"):
             continue
+        if name == "signum":   # -lr sign(d) per step: count elements whose movement differs by a sign flip
+            flips += int(((got[k] - po[k]).abs() > 0.5e-3).sum())
+            n += got[k].numel()
+            continue
         r = _rel(got[k] - init[k], po[k] - init[k])
-        print(f"VIT_MOVE {optim} {k} {r:.4f}")
-        assert r < 0.5, (k, r)
+        spread = _rel(p32[k] - init[k], po[k] - init[k])
+        print(f"VIT_MOVE {optim} {k} {r:.4f} spread {spread:.4f}")
+        assert r <= max(2.0 * spread, 2e-2), (k, r, spread)
+    if name == "signum":
+        print(f"VIT_MOVE signum flipped {flips}/{n}")
+        assert flips <= 1e-2 * n, (flips, n)

@@ -17,6 +17,7 @@ and the gradient mean is overlapped with the last micro-step's backward.  Out of
 (SURVEY §2): wandb, eigen tracking, curvature batches for PN-S/Sophia/HF.
 """
 import math
+import os
 import time
 
 import torch
@@ -31,7 +32,11 @@ from utils import load_config, log_scalar_dict, maybe_make_dir, parse_flags
 def run(cfg):
     if cfg.model != "transformer":
         raise ValueError(f"LM training expects model='transformer', got {cfg.model}.")
+    use_dp = dp.resolve_use_dp(cfg, int(os.environ.get("WORLD_SIZE", "1")))   # train_lm.py:476-483
     rank, _, world, dev = dp.init_from_env()
+    if rank == 0:
+        print(f"Using data parallelism over {world} GPUs (one process each)." if use_dp
+              else "Using single-device mode.")
     if world > 1:
         ok, err = dp.probe_collectives(dev)          # train_lm.py:442-462
         if not ok:
