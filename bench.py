@@ -1,7 +1,7 @@
 """Benchmark: plainCV training hot path on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload vit_c2|vit_c4_soap|vit_c4_shampoo|lm124m|lm420m]
-                    [--no-cpu-baseline] [--no-lm]
+                    [--no-cpu-baseline] [--no-lm] [--shard-opt]
 
 ``--gpus N`` (N > 1) without a torchrun environment: the parent process spawns N ranks of this
 script (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1/MASTER_PORT, one GPU each) BEFORE
@@ -246,9 +246,32 @@ def allreduce_busbw(buf, iters=10):
             "world": n, "backend": torch.distributed.get_backend()}
 
 
+def optimizer_ms(tx, store, opt_state, gscale=None, iters=5):
+    """Per-rank wall time of one optimizer step (incl. the sharded exchange), max over ranks;
+    run after the timed region (it moves the params)."""
+    dev = store.device
+    for _ in range(2):
+        tx.step_(store, opt_state, gscale) if gscale is not None else tx.step_(store, opt_state)
+    torch.cuda.synchronize()
+    if dp.world_size() > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        tx.step_(store, opt_state, gscale) if gscale is not None else tx.step_(store, opt_state)
+    torch.cuda.synchronize()
+    t = torch.tensor([(time.perf_counter() - t0) / iters * 1e3], device=dev)
+    if dp.world_size() > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    sh = getattr(opt_state, "shard", None)
+    return {"ms": round(float(t.item()), 4), "sharded": sh is not None,
+            "shard": sh.describe() if sh is not None else None}
+
+
 def bench_vit(args):
     rank, local_rank, world, dev = dp.init_from_env()
     cfg = Config(VIT_C2 if args.workload == "vit_c2" else VIT_C4[args.workload.split("_")[-1]])
+    if args.shard_opt:
+        cfg.shard_optimizer = True
     m = vit_model(cfg)
     B = cfg.batch_size
     shape = (B, cfg.image_size, cfg.image_size, cfg.num_channels)
@@ -301,8 +324,10 @@ def bench_vit(args):
         else:
             out["cpu_baseline"] = None
     ar = allreduce_busbw(state.params.grad_flat[: state.params.layout.size]) if world > 1 else None
+    om = optimizer_ms(state.tx, state.params, state.opt_state) if world > 1 else None
     if out is not None and world > 1:
         out["grad_allreduce"] = ar
+        out["optimizer_step_per_rank"] = om
     return out
 
 
@@ -363,6 +388,8 @@ def bench_lm(args):
     rank, local_rank, world, dev = dp.init_from_env()
     spec = LM_CFGS[args.workload]
     cfg = Config(spec["cfg"])
+    if args.shard_opt:
+        cfg.shard_optimizer = True
     if args.lm_micro_batch is None:
         args.lm_micro_batch = spec["mb"]
     if args.lm_accum is None:
@@ -401,6 +428,7 @@ def bench_lm(args):
     tokens = world * mb * accum * cfg.seq_len * args.steps
     fpt = model.flops_per_token(cfg.seq_len)
     ar = allreduce_busbw(st.params.grad_flat[: st.params.layout.size], iters=3) if world > 1 else None
+    om = optimizer_ms(st.tx, st.params, st.opt_state) if world > 1 else None
     if rank != 0:
         return None
     return {"metric": METRIC, "value": round(tokens / dt, 1), "unit": "tokens/s", "n_gpus": world,
@@ -413,7 +441,7 @@ def bench_lm(args):
             "steps_per_sec": round(args.steps / dt, 4),
             "tflops_per_gpu": round(tokens / world / dt * fpt / 1e12, 2),
             "roofline": lm_roofline(st),
-            "grad_allreduce": ar,
+            "grad_allreduce": ar, "optimizer_step_per_rank": om,
             "cpu_baseline": (cpu_baseline_lm(cfg, variables, spec["clip"], args.cpu_seconds)
                              if world == 1 and not args.no_cpu_baseline else None)}
 
@@ -520,6 +548,8 @@ def main():
     ap.add_argument("--no-lm", action="store_true", help="skip the attached 124M LM (configs[2]) line")
     ap.add_argument("--lm-steps", type=int, default=10)
     ap.add_argument("--lm-warmup", type=int, default=2)
+    ap.add_argument("--shard-opt", action="store_true",
+                    help="split muon/soap/shampoo per-matrix work across the DP ranks (optim/sharding.py)")
     args = ap.parse_args()
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:

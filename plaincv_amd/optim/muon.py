@@ -35,6 +35,7 @@ from ..hip import ptr, stream_ptr
 from .adamw import AdamBranch, _views
 from .base import GradientTransformation, OptState, ensure_grads
 from .matrix_routing import should_use_matrix_preconditioner
+from . import sharding
 
 
 def build_muon_dim_numbers(params):
@@ -59,7 +60,7 @@ class _Group:
 class Muon(GradientTransformation):
     def __init__(self, learning_rate, ns_coeffs=(3.4445, -4.7750, 2.0315), ns_steps=5, beta=0.95, eps=1e-8,
                  weight_decay=0.0, nesterov=True, adaptive=False, adam_b1=0.9, adam_b2=0.999, adam_eps_root=0.0,
-                 adam_weight_decay=0.0, shape_scale=True, fused=True):
+                 adam_weight_decay=0.0, shape_scale=True, fused=True, shard=None):
         if adaptive:
             raise NotImplementedError("muon_adaptive=True (dual-norm scaling) is not on the hot path")
         self.lr = float(learning_rate)
@@ -73,6 +74,7 @@ class Muon(GradientTransformation):
         # all-fused models run the whole step as one launch (PCV_MUON_ONE_LAUNCH=0: the 5-launch form)
         self.one_launch = os.environ.get("PCV_MUON_ONE_LAUNCH", "1") != "0"
         self.in_block = os.environ.get("PCV_MUON_IN_BLOCK", "0") == "1"
+        self.shard = shard           # optim/sharding.py: NS work split across DP ranks
 
     def init(self, store):
         dev = store.device
@@ -80,8 +82,9 @@ class Muon(GradientTransformation):
         st.tensors["mu"] = torch.zeros_like(store.flat)
         st.tensors["nu"] = torch.zeros_like(store.flat)
         st.upd = torch.zeros_like(store.flat)
-        routed = [k for k, p in store.params.items() if should_use_matrix_preconditioner(k, p)]
-        rest = [k for k in store.params if k not in routed]
+        routed_all = [k for k, p in store.params.items() if should_use_matrix_preconditioner(k, p)]
+        rest = [k for k in store.params if k not in routed_all]
+        routed, st.shard = sharding.setup(self, store, routed_all, sharding.muon_cost)
         b1, b2, eps_root, awd = self.adam
         st.branch = AdamBranch(store, rest, b1, b2, self.eps, eps_root, awd, self.nesterov, small_chunks=False)
         st.routed = routed
@@ -165,6 +168,7 @@ class Muon(GradientTransformation):
             if not self.in_block:
                 hip.call("pcv_muon_apply", ptr(mats), len(st.routed), st.max_elems, self.lr, self.wd,
                          int(self.shape_scale), int(apply), stream_ptr())
+            sharding.finish(st.shard, store, st, apply)
             return
         if st.routed:   # st.norm2 is zero here: created zeroed, reset by pcv_muon_apply after use
             hip.call("pcv_muon_prep", ptr(st.mats_apply), len(st.routed), st.n_general, st.max_elems, self.beta,
@@ -176,6 +180,7 @@ class Muon(GradientTransformation):
         st.branch.run(store, st.tensors["mu"], st.tensors["nu"], st.count, self.lr, gscale=gscale,
                       upd=None if apply else st.upd, apply=apply)
         K.step_bump(st.count)
+        sharding.finish(st.shard, store, st, apply)
 
     def update(self, grads, state, params=None):
         ensure_grads(params, grads)

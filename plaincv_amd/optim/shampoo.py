@@ -28,6 +28,7 @@ import torch
 
 from .. import kernels as K
 from .adamw import AdamBranch, _views
+from . import sharding
 from .base import GradientTransformation, OptState, ensure_grads
 from .matrix_routing import should_use_matrix_preconditioner
 from .precond import EIGH_MAX_N, Eigh, GemmF32, NewtonRoot
@@ -45,7 +46,8 @@ class _Mat:
 
 class Shampoo(GradientTransformation):
     def __init__(self, learning_rate, eps=1e-4, exponent=0.25, weight_decay=0.0, adam_b1=0.9, adam_b2=0.999,
-                 adam_eps=1e-8, restart_every=50, root_method="newton"):
+                 adam_eps=1e-8, restart_every=50, root_method="newton", shard=None):
+        self.shard = shard           # optim/sharding.py: per-matrix work split across DP ranks
         self.lr, self.eps, self.exponent, self.wd = float(learning_rate), float(eps), float(exponent), \
             float(weight_decay)
         self.adam = (float(adam_b1), float(adam_b2), float(adam_eps))
@@ -64,8 +66,9 @@ class Shampoo(GradientTransformation):
         st.tensors["mu"] = torch.zeros_like(store.flat)
         st.tensors["nu"] = torch.zeros_like(store.flat)
         st.upd = torch.zeros_like(store.flat)
-        routed = [k for k, p in store.params.items() if _should_use_shampoo(k, p)]
-        rest = [k for k in store.params if k not in routed]
+        routed_all = [k for k, p in store.params.items() if _should_use_shampoo(k, p)]
+        rest = [k for k in store.params if k not in routed_all]
+        routed, st.shard = sharding.setup(self, store, routed_all, sharding.shampoo_cost)
         b1, b2, eps = self.adam
         st.branch = AdamBranch(store, rest, b1, b2, eps, 0.0, self.wd, False)
         st.mats = []
@@ -82,7 +85,8 @@ class Shampoo(GradientTransformation):
             st.mats.append(s)
         # a factor above EIGH_MAX_N takes the host-driven big-matrix eigh as its Newton fallback
         # (sweeps until converged, decided with host syncs), so such a step cannot be captured
-        self.graphable = self.root_method == "newton" and all(max(s.r, s.c) <= EIGH_MAX_N for s in st.mats)
+        self.graphable = st.shard is None and self.root_method == "newton" and \
+            all(max(s.r, s.c) <= EIGH_MAX_N for s in st.mats)
         st.host_step = 0
         st.plans = {}
         return st
@@ -147,6 +151,7 @@ class Shampoo(GradientTransformation):
         st.branch.run(store, st.tensors["mu"], st.tensors["nu"], st.count, self.lr, gscale=gscale,
                       upd=None if apply else st.upd, apply=apply)
         K.step_bump(st.count)
+        sharding.finish(st.shard, store, st, apply)
         if apply:
             store.version += 1
 

@@ -19,6 +19,7 @@ import torch
 
 from .. import kernels as K
 from .adamw import AdamBranch, _views
+from . import sharding
 from .base import GradientTransformation, OptState, ensure_grads
 from .matrix_routing import should_use_matrix_preconditioner
 from .precond import Eigh, EstSort, GemmF32, HouseholderQR, PermuteRC, soap_adam
@@ -32,8 +33,9 @@ class Soap(GradientTransformation):
     graphable = False      # first step / refresh steps change the launch sequence (host-driven)
 
     def __init__(self, learning_rate, b1=0.95, b2=0.95, eps=1e-8, weight_decay=0.01, precondition_frequency=10,
-                 shampoo_beta2=None, correct_bias=True):
+                 shampoo_beta2=None, correct_bias=True, shard=None):
         self.lr = float(learning_rate)
+        self.shard = shard           # optim/sharding.py: per-matrix work split across DP ranks
         self.b1, self.b2, self.eps, self.wd = float(b1), float(b2), float(eps), float(weight_decay)
         self.f = int(precondition_frequency)
         self.sb2 = self.b2 if shampoo_beta2 is None else float(shampoo_beta2)
@@ -45,8 +47,9 @@ class Soap(GradientTransformation):
         st.tensors["mu"] = torch.zeros_like(store.flat)
         st.tensors["nu"] = torch.zeros_like(store.flat)
         st.upd = torch.zeros_like(store.flat)
-        routed = [k for k, p in store.params.items() if should_use_matrix_preconditioner(k, p)]
-        rest = [k for k in store.params if k not in routed]
+        routed_all = [k for k, p in store.params.items() if should_use_matrix_preconditioner(k, p)]
+        rest = [k for k in store.params if k not in routed_all]
+        routed, st.shard = sharding.setup(self, store, routed_all, sharding.soap_cost)
         st.branch = AdamBranch(store, rest, self.b1, self.b2, self.eps, 0.0, self.wd, False)
         st.routed = routed
         st.host_step = -1
@@ -151,6 +154,7 @@ class Soap(GradientTransformation):
         st.branch.run(store, st.tensors["mu"], st.tensors["nu"], st.count, self.lr, gscale=gscale,
                       upd=None if apply else st.upd, apply=apply)
         K.step_bump(st.count)
+        sharding.finish(st.shard, store, st, apply)
         if apply:
             store.version += 1
 

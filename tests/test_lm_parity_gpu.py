@@ -1,6 +1,7 @@
 """Causal LM on the HIP path vs the CPU oracle in the reference's bf16 placement.
 
-Tolerances (SURVEY §8c bf16 mode): loss abs <= 2e-2, gradient leaves rel-L2 <= 6e-2 (floor 1e-3),
+Tolerances (SURVEY §8c bf16 mode): loss abs <= 2e-2, gradient leaves rel-L2 <= 2e-2 against the bf16
+oracle and <= max(1e-2, 1.5x the bf16 oracle's own error) against fp64,
 grad norm rel 3e-2; the optimizer step given the HIP gradients within tests/parity_util's
 bounds (AdamW 1e-5, bf16-NS Muon 2e-2 relative to the update)."""
 import pytest
@@ -54,7 +55,7 @@ def test_lm_grads_match_oracle(dev, tie, b, T, mlp):
         # against the bf16 oracle is the sum of the two sides' bf16 noise)
         e_hip, e_bf = _rel(gg[k], g64[k]), _rel(grads[k], g64[k])
         print(f"LMGRAD {k} hip_vs_bf16oracle {r:.4f} hip_vs_fp64 {e_hip:.4f} bf16oracle_vs_fp64 {e_bf:.4f}")
-        assert r < 6e-2, (k, r)
+        assert r < 2e-2, (k, r)                # measured <= 0.009 (r03)
         assert e_hip < max(1e-2, 1.5 * e_bf), (k, e_hip, e_bf)
 
 
@@ -98,7 +99,8 @@ def test_lm_train_steps_match_oracle(dev, optim, clip):
         torch.cuda.synchronize()
         g_hip = st.params.grads_dict()
         for k in p0:
-            assert _rel(g_hip[k], g_or[k]) < 6e-2, (it, k, _rel(g_hip[k], g_or[k]))
+            print(f"LMACC {it} {k} {_rel(g_hip[k], g_or[k]):.4f}")
+            assert _rel(g_hip[k], g_or[k]) < 2e-2, (it, k, _rel(g_hip[k], g_or[k]))   # measured <= 0.0095 (r03)
         st, gnorm = apply_grads(st)
         torch.cuda.synchronize()
         p1 = st.params.to_dict()

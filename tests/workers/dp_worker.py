@@ -104,13 +104,56 @@ def lm(rep, dev):
     rep["checksum"] = float(sum(v.double().sum() * (i + 1) for i, v in enumerate(p1.values())))
 
 
+def shard(rep, dev, optim, layout_name):
+    """optim/sharding.py with the real kernels: the same gradients on both ranks, a sharded and an
+    unsharded optimizer side by side for 5 steps (SOAP: init step + a refresh at f = 2); the
+    sharded params must equal the unsharded ones and the replicas must end bit-identical."""
+    from collections import OrderedDict
+    from plaincv_amd.optim.factory import get_optimizer
+    from plaincv_amd.params import ParamStore
+    from tests.test_optim_parity_gpu import LAYOUTS, _grads
+    from utils import Config
+    lay = LAYOUTS[layout_name]()
+    gen = torch.Generator().manual_seed(0)
+    init = OrderedDict((k, 0.1 * torch.randn(l.shape, generator=gen)) for k, l in lay.leaves.items())
+    scale = {k: 0.1 for k in lay.leaves}
+    base = dict(optim=optim, lr=1e-2, weight_decay=0.05, beta1=0.9, beta2=0.95, precondition_frequency=2,
+                eps=1e-8 if optim == "soap" else 1e-4)
+    txs = get_optimizer(Config(shard_optimizer=True, **base))
+    txu = get_optimizer(Config(**base))
+    sa, su = ParamStore(lay, dev), ParamStore(lay, dev)
+    sa.load(init)
+    su.load(init)
+    ssa, ssu = txs.init(sa), txu.init(su)
+    rep["owned"] = len(ssa.shard.owned) if ssa.shard is not None else -1
+    rep["routed"] = len(ssu.routed) if hasattr(ssu, "routed") else len(ssu.mats)
+    for _ in range(5):
+        grads = _grads(lay, gen, scale)
+        for st_ in (sa, su):
+            st_.zero_grad()
+            for k, v in grads.items():
+                st_.grads[k].copy_(v.to(dev))
+        txs.step_(sa, ssa)
+        txu.step_(su, ssu)
+    torch.cuda.synchronize()
+    a, u = sa.flat.cpu(), su.flat.cpu()
+    rep["max_rel_vs_unsharded"] = float((a - u).abs().max() / u.abs().max())
+    rep["shadow_ok"] = bool(torch.equal(sa.shadow.cpu(), a.to(torch.bfloat16)))
+    rep["checksum"] = float(a.double().sum() + (a.double() ** 2).sum())
+    rep["step_excess"] = 0.0
+
+
 def main():
     which, out = sys.argv[1], sys.argv[2]
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
     rep = {"rank": dist.get_rank()}
-    (vit if which == "vit" else lm)(rep, dev)
+    if which.startswith("shard:"):
+        _, optim, layout_name = which.split(":")
+        shard(rep, dev, optim, layout_name)
+    else:
+        (vit if which == "vit" else lm)(rep, dev)
     dist.barrier()
     with open(out, "w") as f:
         json.dump(rep, f)
