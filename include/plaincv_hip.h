@@ -170,6 +170,10 @@ int pcv_batchnorm_stats(const float* x, int64_t ldx, int64_t R, int D, int train
                         void* stream);
 int pcv_batchnorm_apply(const float* x, int64_t ldx, int64_t R, int D, const float* mean, const float* rstd,
                         const float* scale, const float* bias, void* y, int64_t ldy, void* stream);
+/* the fp32 ViT runner's BatchNorm (models/vit_f32.py): the same normalisation, fp32 output
+   (the reference BatchNorm ViT computes in fp32, vit_small.py:95) */
+int pcv_batchnorm_apply_f32(const float* x, int64_t ldx, int64_t R, int D, const float* mean, const float* rstd,
+                            const float* scale, const float* bias, float* y, int64_t ldy, void* stream);
 int pcv_batchnorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, int64_t R, int D,
                       const float* mean, const float* rstd, const float* scale, const float* dres, int64_t ldres,
                       float* dx, int64_t lddx, void* dx_bf16, int64_t lddxb, float* dscale, float* dbias,

@@ -112,18 +112,23 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
   rstd[c] = rsqrtf(var + eps);
 }
 
-// y = (x - mean) rstd scale + bias (bf16 out), one float4 per thread
+// y = (x - mean) rstd scale + bias (bf16 out for the bf16-MFMA runner, fp32 out for the fp32 runner),
+// one float4 per thread
+template <typename OutT>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ x, int64_t ldx,
                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
                                                        const float* __restrict__ scale, const float* __restrict__ bias,
-                                                       bf16* __restrict__ y, int64_t ldy, int64_t R, int D) {
+                                                       OutT* __restrict__ y, int64_t ldy, int64_t R, int D) {
   const int CG = D >> 2;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= R * CG) return;
   const int64_t r = i / CG;
   const int c = (int)(i - r * CG) * 4;
   const f32x4 v = (ld4f(x + r * ldx + c) - ld4f(mean + c)) * ld4f(rstd + c) * ld4f(scale + c) + ld4f(bias + c);
-  *reinterpret_cast<bf16x4*>(y + r * ldy + c) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+  if constexpr (sizeof(OutT) == 4)
+    *reinterpret_cast<f32x4*>(y + r * ldy + c) = v;
+  else
+    *reinterpret_cast<bf16x4*>(y + r * ldy + c) = bf16x4{f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
 }
 
 // dx = dres + scale rstd (dy - coef0 - xhat coef1) (fp32, + optional bf16 copy); dres may alias dx
@@ -184,8 +189,19 @@ extern "C" int pcv_batchnorm_apply(const float* x, int64_t ldx, int64_t R, int D
   if (!bn_shape_ok(R, D) || !mean || !rstd || !scale || !bias || !y) return PCV_EINVAL;
   if ((ldx & 3) || (ldy & 3) || !pcv_aligned16(x) || ((uintptr_t)y & 7u)) return PCV_EALIGN;
   const int64_t n = R * (D >> 2);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, ldx,
-                     mean, rstd, scale, bias, (bf16*)y, ldy, R, D);
+  hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                     ldx, mean, rstd, scale, bias, (bf16*)y, ldy, R, D);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_batchnorm_apply_f32(const float* x, int64_t ldx, int64_t R, int D, const float* mean,
+                                       const float* rstd, const float* scale, const float* bias, float* y, int64_t ldy,
+                                       void* stream) {
+  if (!bn_shape_ok(R, D) || !mean || !rstd || !scale || !bias || !y) return PCV_EINVAL;
+  if ((ldx & 3) || (ldy & 3) || !pcv_aligned16(x) || !pcv_aligned16(y)) return PCV_EALIGN;
+  const int64_t n = R * (D >> 2);
+  hipLaunchKernelGGL(bn_apply_kernel<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                     ldx, mean, rstd, scale, bias, y, ldy, R, D);
   return pcv_launch_status();
 }
 

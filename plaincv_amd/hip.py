@@ -45,6 +45,7 @@ SIGNATURES = {
     "pcv_batchnorm_workspace_size": [I64, I32],
     "pcv_batchnorm_stats": [P, I64, I64, I32, I32, F32, F32, P, P, P, P, P, SZ, P],
     "pcv_batchnorm_apply": [P, I64, I64, I32, P, P, P, P, P, I64, P],
+    "pcv_batchnorm_apply_f32": [P, I64, I64, I32, P, P, P, P, P, I64, P],
     "pcv_batchnorm_bwd": [P, I64, P, I64, I64, I32, P, P, P, P, I64, P, I64, P, I64, P, P, P, SZ, P],
     "pcv_rope": [P, I64, I64, I32, I32, I32, P, P, I32, P],
     "pcv_swiglu_fwd": [P, I64, P, I64, I64, I32, I32, P],

@@ -396,11 +396,12 @@ def batchnorm_stats(x, ra_mean, ra_var, mean, rstd, ws, train, momentum=0.99, ep
 
 
 def batchnorm_apply(x, mean, rstd, scale, bias, y):
+    """y = (x - mean) rstd scale + bias; y bf16 (the bf16 runner's GEMM operand) or fp32."""
     R, D = x.shape
-    _chk(x.dtype == F32 and y.dtype == BF16 and tuple(y.shape) == (R, D), "batchnorm apply")
+    _chk(x.dtype == F32 and y.dtype in (BF16, F32) and tuple(y.shape) == (R, D), "batchnorm apply")
     _dev(x, mean, rstd, scale, bias, y)
-    hip.call("pcv_batchnorm_apply", ptr(x), _ld(x), R, D, ptr(mean), ptr(rstd), ptr(scale), ptr(bias), ptr(y),
-             _ld(y), stream_ptr())
+    hip.call("pcv_batchnorm_apply_f32" if y.dtype == F32 else "pcv_batchnorm_apply", ptr(x), _ld(x), R, D, ptr(mean),
+             ptr(rstd), ptr(scale), ptr(bias), ptr(y), _ld(y), stream_ptr())
 
 
 def batchnorm_bwd(dy, x, mean, rstd, scale, dres, dx, dx_bf16, dscale, dbias, ws):

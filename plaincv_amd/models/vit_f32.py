@@ -9,7 +9,8 @@ workgroup per (batch, head), scores never leave the CU; other shapes: per-head G
 softmax / weight-dropout kernel over materialised [B*H, T, T] scores) and the embedding VJP in
 csrc/vit_f32.hip.  Dropout bits and sites are those
 of the bf16 path (shared with oracle/rng.py), so the two runners draw identical masks.
-Supported: LayerNorm or no norm (use_batchnorm is bf16-path only).
+Supported: LayerNorm, BatchNorm (use_batchnorm: flax BatchNorm with the mutable batch_stats running
+averages, statistics over all B*T token rows, vit_small.py:35-36,49-50,121-122) or no norm.
 """
 import math
 import os
@@ -91,9 +92,11 @@ class _Dense:
 class ViTRunnerF32:
     """Fixed-shape fp32 forward/backward executor (graph-capturable, no allocation after init)."""
 
-    def __init__(self, model, store, image_shape, device):
-        if model.use_batchnorm:
-            raise NotImplementedError("the fp32 ViT path supports LayerNorm or no norm (use_batchnorm: bf16 path)")
+    def __init__(self, model, store, image_shape, device, batch_stats=None):
+        self.bn = bool(model.use_batchnorm)
+        if self.bn and batch_stats is None:
+            raise ValueError("the BatchNorm ViT needs its batch_stats (TrainState.batch_stats)")
+        self.bs = batch_stats
         self.m, self.s = model, store
         B, Hh, Ww, C = image_shape
         ps = model.patch_size
@@ -111,9 +114,9 @@ class ViTRunnerF32:
         self.patches, self.patch_out = z(B * self.hw, self.Kp), z(B * self.hw, D)
         self.xs = [z(R, D) for _ in range(L + 1)]
         self.x1s = [z(R, D) for _ in range(L)]
-        ln = model.use_layernorm
-        self.y0 = [z(R, D) for _ in range(L)] if ln else self.xs[:L]
-        self.y1 = [z(R, D) for _ in range(L)] if ln else self.x1s
+        nrm = model.use_layernorm or self.bn
+        self.y0 = [z(R, D) for _ in range(L)] if nrm else self.xs[:L]
+        self.y1 = [z(R, D) for _ in range(L)] if nrm else self.x1s
         self.st0 = [(z(R), z(R)) for _ in range(L)]
         self.st1 = [(z(R), z(R)) for _ in range(L)]
         self.qkv = [z(R, 3 * D) for _ in range(L)]
@@ -138,8 +141,16 @@ class ViTRunnerF32:
         self.mask_words = K.attn_mask_words(T)
         self.attn_mask = torch.zeros(L * self.mask_words, dtype=torch.int16, device=dev)
         # backward
-        self.dx = z(R, D)                                   # only the cls rows are written
-        self.dyf = z(B, D)
+        self.dx = z(R, D)                                   # LayerNorm: only the cls rows are written
+        if self.bn:   # BatchNorm: per-column [mean, rstd] per norm; the final norm's VJP spans every row
+            self.bn_ws = z((K.batchnorm_workspace_bytes(R, D) + 3) // 4)
+            self.bst0 = [(z(D), z(D)) for _ in range(L)]
+            self.bst1 = [(z(D), z(D)) for _ in range(L)]
+            self.bstf = (z(D), z(D))
+            self.dy_top = z(R, D)                           # zero except the cls rows (= dyf)
+            self.dyf = self.dy_top.view(B, T * D)[:, :D]
+        else:
+            self.dyf = z(B, D)
         self.dmo, self.da = z(R, D), z(R, M)
         self.dy1, self.dx1, self.dO = z(R, D), z(R, D), z(R, D)
         # LayerNorm parameter-gradient partials: site 0 the final norm, 1 + 2i / 2 + 2i layer i's
@@ -166,18 +177,25 @@ class ViTRunnerF32:
             for j, n in ((0, "Dense_0"), (1, "Dense_1")):
                 d[f"W{j}"], d[f"b{j}"] = P[f"{pre}/MlpBlock_0/{n}/kernel"], P[f"{pre}/MlpBlock_0/{n}/bias"]
                 d[f"gW{j}"], d[f"gb{j}"] = G[f"{pre}/MlpBlock_0/{n}/kernel"], G[f"{pre}/MlpBlock_0/{n}/bias"]
-            if m.use_layernorm:
+            norm = m._norm()
+            if norm:
                 for j in (0, 1):
-                    d[f"s{j}"], d[f"c{j}"] = P[f"{pre}/LayerNorm_{j}/scale"], P[f"{pre}/LayerNorm_{j}/bias"]
-                    d[f"gs{j}"], d[f"gc{j}"] = G[f"{pre}/LayerNorm_{j}/scale"], G[f"{pre}/LayerNorm_{j}/bias"]
+                    d[f"s{j}"], d[f"c{j}"] = P[f"{pre}/{norm}_{j}/scale"], P[f"{pre}/{norm}_{j}/bias"]
+                    d[f"gs{j}"], d[f"gc{j}"] = G[f"{pre}/{norm}_{j}/scale"], G[f"{pre}/{norm}_{j}/bias"]
+            if self.bn:
+                for j in (0, 1):
+                    d[f"ra{j}"] = (self.bs[f"{pre}/BatchNorm_{j}/mean"], self.bs[f"{pre}/BatchNorm_{j}/var"])
             self.w.append(d)
         self.Wconv, self.gWconv = P["Conv_0/kernel"].reshape(self.Kp, D), G["Conv_0/kernel"].reshape(self.Kp, D)
         self.bconv, self.gbconv = P["Conv_0/bias"], G["Conv_0/bias"]
         self.cls, self.gcls = P["cls_token"].reshape(D), G["cls_token"].reshape(D)
         self.pos, self.gpos = P["pos_embedding"].reshape(self.T, D), G["pos_embedding"].reshape(self.T, D)
-        if m.use_layernorm:
-            self.sf, self.cf = P["LayerNorm_0/scale"], P["LayerNorm_0/bias"]
-            self.gsf, self.gcf = G["LayerNorm_0/scale"], G["LayerNorm_0/bias"]
+        norm = m._norm()
+        if norm:
+            self.sf, self.cf = P[f"{norm}_0/scale"], P[f"{norm}_0/bias"]
+            self.gsf, self.gcf = G[f"{norm}_0/scale"], G[f"{norm}_0/bias"]
+        if self.bn:
+            self.raf = (self.bs["BatchNorm_0/mean"], self.bs["BatchNorm_0/var"])
         self.Wh, self.bh, self.gWh, self.gbh = P["Dense_0/kernel"], P["Dense_0/bias"], G["Dense_0/kernel"], G["Dense_0/bias"]
 
     def _heads(self, t, col0, i_b, i_h):
@@ -315,6 +333,8 @@ class ViTRunnerF32:
             w, x = self.w[i], self.xs[i]
             if m.use_layernorm:
                 self._ln(x, w["s0"], w["c0"], self.y0[i], self.st0[i])
+            elif self.bn:
+                self._bn(x, w["ra0"], self.bst0[i], w["s0"], w["c0"], self.y0[i], train)
             g = self.gf[i]
             g["qkv"].run()
             if self.fused_attn:
@@ -329,11 +349,16 @@ class ViTRunnerF32:
             g["out"].run()
             if m.use_layernorm:
                 self._ln(self.x1s[i], w["s1"], w["c1"], self.y1[i], self.st1[i])
+            elif self.bn:
+                self._bn(self.x1s[i], w["ra1"], self.bst1[i], w["s1"], w["c1"], self.y1[i], train)
             g["fc1"].run(rate, seed)
             g["fc2"].run(rate, seed)
         xcls = self.xs[-1].view(B, T * D)[:, :D]
         if m.use_layernorm:
             self._ln(xcls, self.sf, self.cf, self.yf, self.stf)
+        elif self.bn:   # statistics over every token row, normalise the cls rows only
+            K.batchnorm_stats(self.xs[-1], *self.raf, *self.bstf, self.bn_ws, train)
+            K.batchnorm_apply(xcls, *self.bstf, self.sf, self.cf, self.yf)
         else:
             _epi(xcls, self.yf)
         self.g_head.run()
@@ -342,6 +367,10 @@ class ViTRunnerF32:
                grad_scale=1.0 / B)
         K.mean2(self.row_loss, self.row_correct, B, 1.0 / B, self.metrics)
         return self.metrics
+
+    def _bn(self, x, ra, st, scale, bias, y, train):
+        K.batchnorm_stats(x, *ra, *st, self.bn_ws, train)
+        K.batchnorm_apply(x, *st, scale, bias, y)
 
     def _ln(self, x, s, c, y, st):
         R, D = x.shape
@@ -360,6 +389,9 @@ class ViTRunnerF32:
         xcls = self.xs[-1].view(B, T * D)[:, :D]
         if m.use_layernorm:
             self._ln_bwd(0, self.dyf, xcls, self.sf, self.stf, None, dxc, self.gsf, self.gcf)
+        elif self.bn:   # train-mode VJP through the all-row statistics: every row of dx is written
+            K.batchnorm_bwd(self.dy_top, self.xs[-1], *self.bstf, self.sf, None, self.dx, None, self.gsf, self.gcf,
+                            self.bn_ws)
         else:
             _epi(self.dyf, dxc)
         dx_in = self.dx
@@ -374,6 +406,9 @@ class ViTRunnerF32:
             g["fc1_d"].run()                                                           # self.dy1 = da W0^T
             if m.use_layernorm:
                 self._ln_bwd(1 + 2 * i, self.dy1, self.x1s[i], w["s1"], self.st1[i], dx_in, dx1, w["gs1"], w["gc1"])
+            elif self.bn:
+                K.batchnorm_bwd(self.dy1, self.x1s[i], *self.bst1[i], w["s1"], dx_in, dx1, None, w["gs1"], w["gc1"],
+                                self.bn_ws)
             else:
                 _epi(self.dy1, dx1, res=dx_in)
             self._colsum(dx1, w["gbo"])
@@ -391,6 +426,9 @@ class ViTRunnerF32:
                 drop = dict(dxd=self.dmo_l[i - 1], rate=rate, seed=seed, site=site_mlp_out(i - 1)) if i > 0 else {}
                 self._ln_bwd(2 + 2 * i, self.dy0, self.xs[i], w["s0"], self.st0[i], dx1, self.dxo[i], w["gs0"],
                              w["gc0"], **drop)
+            elif self.bn:
+                K.batchnorm_bwd(self.dy0, self.xs[i], *self.bst0[i], w["s0"], dx1, self.dxo[i], None, w["gs0"],
+                                w["gc0"], self.bn_ws)
             else:
                 _epi(self.dy0, self.dxo[i], res=dx1)
             dx_in = self.dxo[i]

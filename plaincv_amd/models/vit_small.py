@@ -157,7 +157,7 @@ class VisionTransformer:
     def bind(self, store, image_shape, device, side_stream=False, grouped_wgrad=True, batch_stats=None):
         if self.dtype == "float32":
             from .vit_f32 import ViTRunnerF32
-            return ViTRunnerF32(self, store, image_shape, device)
+            return ViTRunnerF32(self, store, image_shape, device, batch_stats=batch_stats)
         return ViTRunner(self, store, image_shape, device, side_stream=side_stream, grouped_wgrad=grouped_wgrad,
                          batch_stats=batch_stats)
 

@@ -221,3 +221,100 @@ def test_vit_batchnorm_train_steps_and_graph(dev):
     torch.cuda.synchronize()
     assert not torch.equal(st.batch_stats.flat, before_bs)
     assert torch.isfinite(st.params.flat).all() and torch.isfinite(st.batch_stats.flat).all()
+
+
+# ------------------------------------------------------------------ fp32 runner (the reference's precision)
+def _bn_model32(rate=0.1, classes=10, D=64, M=128, L=2, H=2):
+    from plaincv_amd.models.vit_small import VisionTransformer
+    return VisionTransformer(num_classes=classes, patch_size=4, hidden_size=D, mlp_dim=M, num_layers=L,
+                             num_heads=H, dropout_rate=rate, use_layernorm=False, use_batchnorm=True, dtype="float32")
+
+
+@pytest.mark.parametrize("rate,shape,classes,D,L,H", [(0.0, (8, 16, 16, 3), 10, 64, 2, 2),
+                                                      (0.1, (8, 16, 16, 3), 10, 64, 2, 2),
+                                                      (0.1, (4, 64, 64, 3), 200, 128, 4, 4)])
+def test_vit_batchnorm_f32_matches_oracle_fp32(dev, rate, shape, classes, D, L, H):
+    """fp32 BatchNorm ViT (models/vit_f32.py) vs the fp32 oracle at SURVEY §8c's fp32 bounds: loss
+    rel 1e-5, gradient leaves rel-L2 1e-4 (exactly-zero true gradients bounded by their kernel's),
+    running averages' movement rel 1e-5 (floored at 1 % of the running value); incl. the C2/C4 geometry (64x64x3, D 128, 4 layers)."""
+    from oracle.engine import cross_entropy_loss, value_and_grad
+    from oracle.vit import vit_apply
+    from plaincv_amd.engine import create_train_state
+    m = _bn_model32(rate, classes, D, 2 * D, L, H)
+    init = m.init(0, shape)
+    gen = torch.Generator().manual_seed(2)
+    stats0 = _rand_stats(m, gen)
+    images = torch.randint(0, 256, shape, generator=gen, dtype=torch.uint8)
+    labels = torch.randint(0, classes, (shape[0],), generator=gen, dtype=torch.int32)
+    st = create_train_state(0, m, 1e-3, shape, classes, init_params=init, init_batch_stats=stats0)
+    r = st.runner_for(shape)
+    r.seed.fill_(9)
+    st.params.zero_grad()
+    met = r.forward(images.to(dev), labels.to(dev), train=True)
+    r.backward(train=True)
+    torch.cuda.synchronize()
+    new_o = {}
+    (loss, _), grads = value_and_grad(
+        lambda p: (cross_entropy_loss(vit_apply(p, images, _ocfg(m), True, 9, batch_stats=stats0,
+                                                new_batch_stats=new_o), labels), None), init)
+    assert abs(met[0].item() - loss.item()) <= 1e-5 * abs(loss.item()), (met[0].item(), loss.item())
+    gg = st.params.grads_dict()
+    bad = []
+    for k in init:
+        if k.endswith(zero_grad_leaves(rate)):
+            sib = gg[k.rsplit("/", 1)[0] + "/kernel"].norm().item()
+            if gg[k].norm().item() >= 1e-4 * sib + 1e-9:
+                bad.append((k, gg[k].norm().item(), sib))
+        elif k.endswith("value/bias"):   # a cancellation (see the bf16 test): floor at 1e-3 of its kernel's
+            sib = grads[k.rsplit("/", 1)[0] + "/kernel"].norm().item()
+            if _rel_floor(gg[k], grads[k], 1e-3 * sib) >= 1e-4:
+                bad.append((k, _rel_floor(gg[k], grads[k], 1e-3 * sib)))
+        elif rel(gg[k], grads[k]) >= 1e-4:
+            bad.append((k, rel(gg[k], grads[k])))
+    assert not bad, bad
+    got = st.batch_stats.to_dict()
+    for k, v in new_o.items():
+        # floor: the movement is ~1 % of the running value, whose own fp32 rounding is ~6e-8
+        assert _rel_floor(got[k] - stats0[k], v.detach() - stats0[k], 1e-2 * stats0[k].norm().item()) < 1e-5, k
+
+
+def test_vit_batchnorm_f32_eval_and_steps(dev):
+    """eval logits from the running averages (rel 1e-5, stats untouched); 3 AdamW engine steps: the
+    update given the HIP gradients (1e-5) and the running averages against the oracle's (1e-5)."""
+    from oracle import optim as oopt
+    from oracle.engine import cross_entropy_loss, value_and_grad
+    from oracle.vit import vit_apply
+    from plaincv_amd.engine import create_train_state, make_eval_step, make_train_step
+    from utils import Config
+    m = _bn_model32()
+    shape = (16, 16, 16, 3)
+    gen = torch.Generator().manual_seed(4)
+    stats = _rand_stats(m, gen)
+    init = m.init(1, shape)
+    cfg = Config(optim="adamw", lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9)
+    st = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=init, init_batch_stats=stats)
+    images = torch.randint(0, 256, shape, generator=gen, dtype=torch.uint8)
+    labels = torch.randint(0, 10, (shape[0],), generator=gen, dtype=torch.int32)
+    make_eval_step()(st, (images.to(dev), labels.to(dev)))
+    ref = vit_apply(init, images, _ocfg(m), False, 0, batch_stats=stats)
+    assert rel(st.runner_for(shape).logits.cpu(), ref) < 1e-5
+    assert all(torch.equal(v, stats[k].float()) for k, v in st.batch_stats.to_dict().items())
+    tx = oopt.get_optimizer(cfg)
+    s_h = tx.init(init)
+    step = make_train_step()
+    for it in range(3):
+        images = torch.randint(0, 256, shape, generator=gen, dtype=torch.uint8)
+        labels = torch.randint(0, 10, (shape[0],), generator=gen, dtype=torch.int32)
+        p0, bs0 = st.params.to_dict(), st.batch_stats.to_dict()
+        st, met = step(st, (images.to(dev), labels.to(dev)), it)
+        torch.cuda.synchronize()
+        p1, g_hip, bs1 = st.params.to_dict(), st.params.grads_dict(), st.batch_stats.to_dict()
+        new_o = {}
+        (loss, _), _ = value_and_grad(lambda p: (cross_entropy_loss(vit_apply(
+            p, images, _ocfg(m), True, it, batch_stats=bs0, new_batch_stats=new_o), labels), None), p0)
+        assert abs(met["loss"].item() - loss.item()) <= 1e-5 * abs(loss.item()), (it, met["loss"].item(), loss.item())
+        for k, v in new_o.items():
+            assert _rel_floor(bs1[k] - bs0[k], v.detach() - bs0[k], 1e-2 * bs0[k].norm().item()) < 1e-5, (it, k)
+        u, s_h = tx.update(g_hip, s_h, p0)
+        for k in init:
+            assert step_rel(p0[k], p1[k], u[k]) <= step_bound("adamw", k, p0[k]), (it, k)

@@ -179,3 +179,14 @@ def test_use_pmap_force_single_device(keys, world, ok, use):
     else:
         with pytest.raises(ValueError, match="single-device"):
             resolve_use_dp(cfg, world)
+
+
+def test_batchnorm_vit_config_runs_fp32():
+    """vit_use_batchnorm configs build the fp32 runner (the reference BN ViT's precision) unless
+    vit_dtype asks for bf16; an unknown vit_dtype is refused."""
+    from utils import Config
+    base = dict(model="vit_small", dataset="fashion_mnist", vit_use_layernorm=False, vit_use_batchnorm=True)
+    assert train.construct_model(Config(**base)).dtype == "float32"
+    assert train.construct_model(Config(vit_dtype="bfloat16", **base)).dtype == "bfloat16"
+    with pytest.raises(ValueError, match="vit_dtype"):
+        train.construct_model(Config(vit_dtype="float16", **base))

@@ -42,10 +42,12 @@ def construct_model(cfg):
                          f"{sorted(VIT_NAMES)}; ResNet/MLP are out of scope)")
     g = lambda k, d: getattr(cfg, k, d)  # noqa: E731
     # vit_dtype: the reference ViT computes in fp32 (models/vit_small.py:95), so that is the CLI
-    # default; "bfloat16" selects the bf16-MFMA runner (BASELINE configs[1]).  BatchNorm runs on
-    # the bf16 runner only.
+    # default for every norm variant (LayerNorm, BatchNorm, none); "bfloat16" selects the bf16-MFMA
+    # runner (BASELINE configs[1]) only when the config asks for it.
     bn = g("vit_use_batchnorm", False)
-    dtype = g("vit_dtype", "bfloat16" if bn else "float32")
+    dtype = g("vit_dtype", "float32")
+    if dtype not in ("float32", "bfloat16"):
+        raise ValueError(f"vit_dtype must be float32 or bfloat16, got {dtype!r}")
     return VisionTransformer(num_classes=num_classes(cfg), patch_size=g("vit_patch_size", 4),
                              hidden_size=g("vit_hidden_size", 128), mlp_dim=g("vit_mlp_dim", 256),
                              num_layers=g("vit_layers", 4), num_heads=g("vit_heads", 4),
