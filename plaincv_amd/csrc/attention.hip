@@ -25,6 +25,7 @@
 namespace pcv {
 
 constexpr float LOG2E = 1.4426950408889634f;
+
 constexpr float NEG_BIG = -1.0e30f;
 constexpr f32x4 kZero4 = {0.f, 0.f, 0.f, 0.f};
 
@@ -120,6 +121,22 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* lds, int s, int cbase) {
   const int l = threadIdx.x & 63;
   const int g = l >> 4, w = l & 15, q = w >> 2, p = w & 3;
   const bf16* a0 = lds + toff<DH>(32 * s + 4 * g + q, (cbase >> 3) + (p >> 1)) + 4 * (p & 1);
+  const bf16* a1 = a0 + 16 * DH;   // row +16: same swizzle
+  bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
+  bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a1));
+  return bf16x8{t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+}
+// tr_frag split into a per-lane base (step 0) and a per-step constant offset: the swizzle of
+// rows 32 s + 4 g + q does not depend on s (one base per column block: the XOR does touch it)
+template <int DH>
+__device__ __forceinline__ const bf16* tr_base(const bf16* lds, int cbase) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, w = l & 15, q = w >> 2, p = w & 3;
+  return lds + toff<DH>(4 * g + q, (cbase >> 3) + (p >> 1)) + 4 * (p & 1);
+}
+template <int DH>
+__device__ __forceinline__ bf16x8 tr_at(const bf16* base, int s) {
+  const bf16* a0 = base + 32 * DH * s;
   const bf16* a1 = a0 + 16 * DH;   // row +16: same swizzle
   bf16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0));
   bf16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a1));
@@ -299,8 +316,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) bmax = fmaxf(bmax, s[gq][t][r]);
-        bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
-        bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+        bmax = xmax_rows(bmax);
         const float cand = bmax * c2;
         if (__ballot(cand > m2[gq] + 8.f) != 0) {   // some row's max moved: rescale (wave-uniform branch)
           const float mnew = fmaxf(m2[gq], cand);
@@ -335,8 +351,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
             if (DROP) p = __uint_as_float(__float_as_uint(p) & (uint32_t)__builtin_amdgcn_sbfe((int)wt[t], r, 1));
             s[gq][t][r] = p;
           }
-        rs += __shfl_xor(rs, 16, 64);
-        rs += __shfl_xor(rs, 32, 64);
+        rs = xsum_rows(rs);
         lsum[gq] += rs;
       };
 #pragma unroll
@@ -792,9 +807,77 @@ __device__ __forceinline__ void sh_load_mask(uint16_t* dst, const uint16_t* src,
 // Forward: 16-query groups dealt round-robin to the waves (17 at T = 257); per group an online
 // softmax over 64-key chunks (lazy rescale as attn_fwd_kernel), K and V fragments from LDS.
 // NT = TP / 16 key blocks (compile time: the chunk loop unrolls).
+// + the tail-query partials (T = 16 n + 1): per wave {m, l, o[32]}
+constexpr int SH_TAILQ_FLOATS = SH_WAVES * 36;
 template <int NT>
 __host__ __device__ constexpr size_t sh_fwd_lds(bool drop) {
-  return 3 * (size_t)NT * 16 * SH_DH * sizeof(bf16) + (drop ? SH_MASK_WORDS * sizeof(uint16_t) : 0);
+  return 3 * (size_t)NT * 16 * SH_DH * sizeof(bf16) + (drop ? SH_MASK_WORDS * sizeof(uint16_t) : 0) +
+         SH_TAILQ_FLOATS * sizeof(float);
+}
+
+// T = 16 n + 1 (the ViT's 257): the last query row, as a 17th query group, ran on one wave after its
+// first group -- twice that wave's time for the whole launch.  Instead every wave takes it against
+// its own 16-key blocks (lane = key c16 x head-dim group g; scores reduced over g, max / sum /
+// P V over the 16 keys by xor shuffles; fp32 P), wave 0 also against the tail key, and the waves'
+// (m, l, o) partials are merged flash-decoding style through LDS (one barrier).
+template <bool DROP>
+__device__ __forceinline__ void sh_fwd_tail_query(const AttnArgs& a, const bf16* Qs, const bf16* Ks, const bf16* Vs,
+                                                  const uint16_t* mk, float* red, int T, int b, int h, int64_t bT,
+                                                  float c2) {
+  constexpr int DH = SH_DH;
+  const int qt = T - 1, wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const int nkb = qt >> 4;                     // full key blocks (keys < T - 1)
+  const bf16x8 q8 = *reinterpret_cast<const bf16x8*>(Qs + toff<DH>(qt, g));
+  float m = NEG_BIG, l = 0.f, o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = 0.f;
+  auto merge = [&](int key, bool valid) {      // one key per lane-row (c16); g = head-dim group
+    const bf16x8 k8 = *reinterpret_cast<const bf16x8*>(Ks + toff<DH>(key, g));
+    float sv = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sv = fmaf(bf2f(q8[j]), bf2f(k8[j]), sv);
+    sv = xsum_rows(sv);
+    const float x = valid ? sv * c2 : NEG_BIG;
+    const float mb = dpp_row_max16(x);
+    const float mn = fmaxf(m, mb);
+    const float al = __builtin_amdgcn_exp2f(m - mn), p = valid ? __builtin_amdgcn_exp2f(x - mn) : 0.f;
+    l = l * al + dpp_row_sum16(p);
+    m = mn;
+    float pd = p;
+    if (DROP && valid) pd = ((mk[drop_word(qt, key, a.n64)] >> ((qt & 3) * 4 + (key & 3))) & 1u) ? p : 0.f;
+    const bf16x8 v8 = *reinterpret_cast<const bf16x8*>(Vs + toff<DH>(key, g));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = o[j] * al + dpp_row_sum16(pd * bf2f(v8[j]));
+    }
+  };
+  for (int kb = wave; kb < nkb; kb += SH_WAVES) merge(kb * 16 + c16, true);
+  if (wave == 0) merge(qt, c16 == 0);          // the tail key itself
+  float* rw = red + wave * 36;
+  if (lane == 0) { rw[0] = m; rw[1] = l; }
+  if (c16 == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rw[4 + 8 * g + j] = o[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < DH) {
+    const int d = threadIdx.x;
+    float M = NEG_BIG;
+#pragma unroll
+    for (int w = 0; w < SH_WAVES; ++w) M = fmaxf(M, red[w * 36]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < SH_WAVES; ++w) {
+      const float e = red[w * 36 + 1] > 0.f ? __builtin_amdgcn_exp2f(red[w * 36] - M) : 0.f;
+      L += red[w * 36 + 1] * e;
+      O += red[w * 36 + 4 + d] * e;
+    }
+    const float ov = O * (DROP ? a.drop_scale : 1.f) / L;
+    const bf16 oh = f2bf(ov);
+    a.out[(bT + qt) * a.ldout + h * DH + d] = oh;
+    if (a.out_lo) a.out_lo[(bT + qt) * a.ldout + h * DH + d] = f2bf(ov - bf2f(oh));
+    if (d == 0) a.lse2[((int64_t)b * a.H + h) * T + qt] = M + log2f(L);
+  }
 }
 template <int NT, bool DROP>
 __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs a) {
@@ -817,11 +900,20 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4;
   const float c2 = a.scale * LOG2E;
-  const int NG = (T + 15) / 16;
+  // T = 16 n + 1: the tail query row is merged from per-wave partials, the tail key joins every
+  // query group's softmax on VALU after its MFMA chunks (no 17th group, no chunk for one key)
+  const bool tail1 = (T & 15) == 1 && T > 16;
+  if (tail1)
+    sh_fwd_tail_query<DROP>(a, Qs, Ks, Vs, mk,
+                            reinterpret_cast<float*>(reinterpret_cast<char*>(shf_smem) + sh_fwd_lds<NT>(DROP) -
+                                                     SH_TAILQ_FLOATS * sizeof(float)),
+                            T, b, h, bT, c2);
+  const int NG = (T + 15) / 16 - (tail1 ? 1 : 0);
+  const int Tk = tail1 ? T - 1 : T;   // keys on the MFMA path
   for (int gq = wave; gq < NG; gq += SH_WAVES) {
     const int myq = gq * 16 + (lane & 15);
     const bool qv = myq < T;
-    int Tl = T;   // opaque: keeps the bounds tests of the tail chunk inside the loop
+    int Tl = Tk;   // opaque: keeps the bounds tests of the tail chunk inside the loop
     asm volatile("" : "+s"(Tl));
     const bf16x8 qf = row_frag<DH>(Qs, gq * 16, 0);
     float m2 = NEG_BIG, l = 0.f;
@@ -830,6 +922,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
     for (int d = 0; d < DT; ++d) acc[d] = kZero4;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
+      if (64 * c >= Tl) break;   // (tail1: the tail key's chunk holds no MFMA key)
       const int nt = (4 * c + 4 <= NT) ? 4 : NT - 4 * c;   // key blocks in this chunk (4 or 2)
       uint64_t mw = 0;
       if (DROP) mw = *reinterpret_cast<const uint64_t*>(mk + drop_word(myq, 64 * c + 4 * g, a.n64));
@@ -849,8 +942,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         if (t < nt) bmax = fmaxf(bmax, fmaxf(fmaxf(s[t][0], s[t][1]), fmaxf(s[t][2], s[t][3])));
-      bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
-      bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+      bmax = xmax_rows(bmax);
       const float cand = bmax * c2;
       if (__ballot(cand > m2 + 8.f) != 0) {   // a row's max moved by > 2^8: rescale (wave-uniform)
         const float mnew = fmaxf(m2, cand);
@@ -901,8 +993,28 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
         }
       }
     }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    l = xsum_rows(l);
+    if (tail1) {   // the tail key T-1 for this lane's query (fp32 p; l is now the full row sum)
+      const int kt = T - 1;
+      const bf16x8 k8 = *reinterpret_cast<const bf16x8*>(Ks + toff<DH>(kt, g));
+      float sv = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sv = fmaf(bf2f(qf[j]), bf2f(k8[j]), sv);
+      sv = xsum_rows(sv);
+      const float x = sv * c2, mn = fmaxf(m2, x);
+      const float al = __builtin_amdgcn_exp2f(m2 - mn), p = __builtin_amdgcn_exp2f(x - mn);
+      l = l * al + p;
+      m2 = mn;
+      float pd = p;
+      if (DROP) pd = ((mk[drop_word(myq, kt, a.n64)] >> ((myq & 3) * 4 + (kt & 3))) & 1u) ? p : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {   // acc[d][r] = O[query 4g + r][dim 16d + c16]
+        const float alr = __shfl(al, 4 * g + r, 64), pdr = __shfl(pd, 4 * g + r, 64);
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+          acc[d][r] = fmaf(pdr, bf2f(Vs[toff<DH>(kt, (16 * d + (lane & 15)) >> 3) + ((lane & 15) & 7)]), acc[d][r] * alr);
+      }
+    }
     const float inv = (DROP ? a.drop_scale : 1.f) / l;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -927,8 +1039,15 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
 // products need opposite MFMA orientations of the recomputed scores, and splitting the waves
 // keeps both in registers with no cross-wave sum and no barrier after the prologue.
 // delta = rowsum(dO o O) is formed in-kernel unless the dO producer already wrote it.
+// T = 16 n + 1 (the ViT's 257): the last key block and the last query group each hold ONE row.
+// As wave items they made one key wave and one query wave run a third item (T = 256: 22.6 us,
+// 257: 30 us).  Instead both rows leave the MFMA blocks: every key wave meets query T-1 once per
+// key block on VALU (its dK / dV terms stay lane-local, its dQ[T-1] terms are xor-reduced over the
+// 16 keys), every query wave meets key T-1 once per query group (dQ terms lane-local after a
+// broadcast, dK[T-1] / dV[T-1] terms reduced over the 16 queries); the per-wave partials and the
+// corner (T-1, T-1) meet in LDS at the end (as the fp32 kernel, vit_f32.hip).
 constexpr size_t SH_BWD_LDS = 4 * SH_TMAX * SH_DH * sizeof(bf16) + 2 * SH_TMAX * sizeof(float) +
-                              SH_MASK_WORDS * sizeof(uint16_t);
+                              SH_MASK_WORDS * sizeof(uint16_t) + (3 * 8 * SH_DH + 4) * sizeof(float);
 
 template <bool DROP>
 __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs a) {
@@ -993,9 +1112,19 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
     }
   }
   __syncthreads();
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
   const float c2 = a.scale * LOG2E;
-  const int NB = (T + 15) / 16;
+  const bool tail1 = (T & 15) == 1 && T > 16;
+  const int NB = (T + 15) / 16 - (tail1 ? 1 : 0);   // wave items: key blocks / query groups
+  const int Tm = tail1 ? T - 1 : T;                  // rows on the MFMA path (queries for the key
+  const int kt = T - 1;                              // waves, keys for the query waves)
+  float* tailp = reinterpret_cast<float*>(mk + SH_MASK_WORDS);   // [3][8][32]: dQ | dK | dV of row T-1
+  float tq[8];                                                     // this wave's partial of row T-1
+#pragma unroll
+  for (int j = 0; j < 8; ++j) tq[j] = 0.f;
+  float tv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) tv[j] = 0.f;
   if (wave < 8) {
     // ---- dK, dV of keys 16*kb .. +15 (lane & 15), over all queries
     for (int kb = wave; kb < NB; kb += 8) {
@@ -1005,21 +1134,36 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
       f32x4 dv[DT], dk[DT];
 #pragma unroll
       for (int d = 0; d < DT; ++d) { dv[d] = kZero4; dk[d] = kZero4; }
-      for (int st = 0; st < NT / 2; ++st) {
-        const bool interior = kb * 16 + 16 <= T && 32 * st + 32 <= T;   // wave-uniform: no bounds tests
+      // per-lane bases: every LDS operand of step st sits at base + a multiple of st (the image
+      // swizzle depends on row bits the step does not change), so the loop body adds constants
+      // instead of recomputing swizzled addresses; interior steps (no bounds tests) run in their
+      // own unrolled loop, the boundary steps after it
+      const bf16* qrow = Qs + toff<DH>(c16, g);
+      const bf16* orow = Os + toff<DH>(c16, g);
+      const bf16* otr[DT] = {tr_base<DH>(Os, 0), tr_base<DH>(Os, 16)};
+      const bf16* qtr[DT] = {tr_base<DH>(Qs, 0), tr_base<DH>(Qs, 16)};
+      const float* lrow = Ls + 4 * g;
+      const float* drow = Dl + 4 * g;
+      const uint16_t* mrow = mk + drop_word(4 * g, mykey, a.n64);
+      const int mstride = 64 * a.n64;   // mask words per 16 queries
+      auto kstep = [&](int st, auto interior_t) {
+        constexpr bool interior = decltype(interior_t)::value;
         f32x4 p[2], ds[2];
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
           const int t = 2 * st + tt;
-          const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Qs, 16 * t, 0), kf, kZero4, 0, 0, 0);
-          const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Os, 16 * t, 0), vf, kZero4, 0, 0, 0);
+          const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              *reinterpret_cast<const bf16x8*>(qrow + 16 * DH * t), kf, kZero4, 0, 0, 0);
+          const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              *reinterpret_cast<const bf16x8*>(orow + 16 * DH * t), vf, kZero4, 0, 0, 0);
           uint32_t wt = 0;
-          if (DROP) wt = (uint32_t)mk[drop_word(16 * t + 4 * g, mykey, a.n64)] >> (mykey & 3);
+          if (DROP) wt = (uint32_t)mrow[t * mstride] >> (mykey & 3);
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(lrow + 16 * t);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(drow + 16 * t);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int ql = 16 * t + 4 * g + r;
-            float pv = __builtin_amdgcn_exp2f(fmaf(sv[r], c2, -Ls[ql]));
-            if (!interior) pv = (mykey < T && ql < T) ? pv : 0.f;
+            float pv = __builtin_amdgcn_exp2f(fmaf(sv[r], c2, -l4[r]));
+            if constexpr (!interior) pv = (mykey < T && 16 * t + 4 * g + r < Tm) ? pv : 0.f;
             float dpv = dp[r];
             float pd = pv;
             if (DROP) {
@@ -1028,14 +1172,54 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
               dpv = __uint_as_float(__float_as_uint(dpv) & km) * a.drop_scale;
             }
             p[tt][r] = pd;
-            ds[tt][r] = pv * (dpv - Dl[ql]);
+            ds[tt][r] = pv * (dpv - d4[r]);
           }
         }
         const bf16x8 pb = pack8(p[0], p[1]), sb = pack8(ds[0], ds[1]);
 #pragma unroll
         for (int d = 0; d < DT; ++d) {
-          dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag<DH>(Os, st, 16 * d), pb, dv[d], 0, 0, 0);
-          dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag<DH>(Qs, st, 16 * d), sb, dk[d], 0, 0, 0);
+          dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_at<DH>(otr[d], st), pb, dv[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_at<DH>(qtr[d], st), sb, dk[d], 0, 0, 0);
+        }
+      };
+      const int nint = kb * 16 + 16 <= T ? Tm / 32 : 0;   // wave-uniform
+      int st = 0;
+#pragma unroll 2
+      for (; st < nint; ++st) kstep(st, std::true_type{});
+      for (; 32 * st < Tm; ++st) kstep(st, std::false_type{});
+      if (tail1) {   // query T-1 against this key block (lane = key c16 x head-dim group g)
+        const bf16x8 q8 = *reinterpret_cast<const bf16x8*>(Qs + toff<DH>(kt, g));
+        const bf16x8 o8 = *reinterpret_cast<const bf16x8*>(Os + toff<DH>(kt, g));
+        float sv = 0.f, dpp = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sv = fmaf(bf2f(q8[j]), bf2f(kf[j]), sv);
+          dpp = fmaf(bf2f(o8[j]), bf2f(vf[j]), dpp);
+        }
+        sv = xsum_rows(sv);
+        dpp = xsum_rows(dpp);
+        const float pv = __builtin_amdgcn_exp2f(fmaf(sv, c2, -Ls[kt]));
+        float pd = pv, dpv = dpp;
+        if (DROP) {
+          const bool keep = (mk[drop_word(kt, mykey, a.n64)] >> ((kt & 3) * 4 + (mykey & 3))) & 1u;
+          pd = keep ? pv : 0.f;
+          dpv = keep ? dpp * a.drop_scale : 0.f;
+        }
+        const float dsb = bf2f(f2bf(pv * (dpv - Dl[kt]))), pdb = bf2f(f2bf(pd));   // the MFMA path's bf16 P, dS
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {   // dv[d][r] / dk[d][r] = dV^T / dK^T[dim 16d + 4g + r][key c16]
+          const int dd = 16 * d + 4 * g;   // 4 consecutive dims: one 8-B read per image
+          const bf16x4 o4 = *reinterpret_cast<const bf16x4*>(Os + toff<DH>(kt, dd >> 3) + (dd & 7));
+          const bf16x4 q4 = *reinterpret_cast<const bf16x4*>(Qs + toff<DH>(kt, dd >> 3) + (dd & 7));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dv[d][r] = fmaf(pdb, bf2f(o4[r]), dv[d][r]);
+            dk[d][r] = fmaf(dsb, bf2f(q4[r]), dk[d][r]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {   // dQ[T-1][8g + j] += sum over the 16 keys of dS K
+          tq[j] += dpp_row_sum16(dsb * bf2f(kf[j]));
         }
       }
       if (mykey < T) {
@@ -1053,7 +1237,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
     // ---- dQ of queries 16*gq .. +15 (lane & 15), over all keys.  Query group gq goes to wave
     // 8 + ((gq + 1) & 7): with NB = 17 the third item lands on wave 9 (SIMD of wave 1), not on
     // wave 8, which shares a SIMD with wave 0 that already holds the third key block
-    for (int gq = (wave - 9) & 7; gq < NB; gq += 8) {
+    for (int gq = tail1 ? wave - 8 : (wave - 9) & 7; gq < NB; gq += 8) {
       const int q0 = gq * 16;
       const int myq = q0 + (lane & 15);
       const bf16x8 qf = row_frag<DH>(Qs, q0, 0);
@@ -1062,21 +1246,28 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
       f32x4 acc[DT];
 #pragma unroll
       for (int d = 0; d < DT; ++d) acc[d] = kZero4;
-      for (int st = 0; st < NT / 2; ++st) {
-        const bool interior = q0 + 16 <= T && 32 * st + 32 <= T;
+      const bf16* krow = Ks + toff<DH>(c16, g);
+      const bf16* vrow = Vs + toff<DH>(c16, g);
+      const bf16* ktr[DT] = {tr_base<DH>(Ks, 0), tr_base<DH>(Ks, 16)};
+      // this query's keep words: keys 64u + 16v + 4g + r sit at word mq + 64u + v (drop_word)
+      const uint16_t* mq = mk + drop_word(myq, 4 * g, a.n64);
+      auto qstep = [&](int st, auto interior_t) {
+        constexpr bool interior = decltype(interior_t)::value;
         f32x4 ds[2];
+        uint32_t w2 = 0;   // the words of t = 2 st, 2 st + 1 (adjacent: v = 2 (st & 1) + tt)
+        if (DROP) w2 = *reinterpret_cast<const uint32_t*>(mq + 64 * (st >> 1) + 2 * (st & 1));
 #pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
           const int t = 2 * st + tt;
-          const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Ks, 16 * t, 0), qf, kZero4, 0, 0, 0);
-          const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Vs, 16 * t, 0), of, kZero4, 0, 0, 0);
-          uint32_t wt = 0;
-          if (DROP) wt = (uint32_t)mk[drop_word(myq, 16 * t + 4 * g, a.n64)] >> (4 * (myq & 3));
+          const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              *reinterpret_cast<const bf16x8*>(krow + 16 * DH * t), qf, kZero4, 0, 0, 0);
+          const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              *reinterpret_cast<const bf16x8*>(vrow + 16 * DH * t), of, kZero4, 0, 0, 0);
+          const uint32_t wt = DROP ? (w2 >> (16 * tt + 4 * (myq & 3))) : 0u;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int key = 16 * t + 4 * g + r;
             float pv = __builtin_amdgcn_exp2f(fmaf(sv[r], c2, -myl));
-            if (!interior) pv = (myq < T && key < T) ? pv : 0.f;
+            if constexpr (!interior) pv = (myq < T && 16 * t + 4 * g + r < Tm) ? pv : 0.f;
             float dpv = dp[r];
             if (DROP)
               dpv = __uint_as_float(__float_as_uint(dpv) & (uint32_t)__builtin_amdgcn_sbfe((int)wt, r, 1)) *
@@ -1087,7 +1278,44 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
         const bf16x8 sa = pack8(ds[0], ds[1]);
 #pragma unroll
         for (int d = 0; d < DT; ++d)
-          acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, tr_frag<DH>(Ks, st, 16 * d), acc[d], 0, 0, 0);
+          acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, tr_at<DH>(ktr[d], st), acc[d], 0, 0, 0);
+      };
+      const int nint = q0 + 16 <= T ? Tm / 32 : 0;   // wave-uniform
+      int st = 0;
+#pragma unroll 2
+      for (; st < nint; ++st) qstep(st, std::true_type{});
+      for (; 32 * st < Tm; ++st) qstep(st, std::false_type{});
+      if (tail1) {   // key T-1 against this query group (lane = query c16 x head-dim group g)
+        const bf16x8 k8 = *reinterpret_cast<const bf16x8*>(Ks + toff<DH>(kt, g));
+        const bf16x8 v8 = *reinterpret_cast<const bf16x8*>(Vs + toff<DH>(kt, g));
+        float sv = 0.f, dpp = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sv = fmaf(bf2f(qf[j]), bf2f(k8[j]), sv);
+          dpp = fmaf(bf2f(of[j]), bf2f(v8[j]), dpp);
+        }
+        sv = xsum_rows(sv);
+        dpp = xsum_rows(dpp);
+        const float pv = myq < T ? __builtin_amdgcn_exp2f(fmaf(sv, c2, -myl)) : 0.f;
+        float pd = pv, dpv = dpp;
+        if (DROP) {
+          const bool keep = (mk[drop_word(myq, kt, a.n64)] >> ((myq & 3) * 4 + (kt & 3))) & 1u;
+          pd = keep ? pv : 0.f;
+          dpv = keep ? dpp * a.drop_scale : 0.f;
+        }
+        const float dsb = bf2f(f2bf(pv * (dpv - myd))), pdb = bf2f(f2bf(pd));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {   // acc[d][r] = dQ[query q0 + 4g + r][dim 16d + c16]
+          const float dr = __shfl(dsb, 4 * g + r, 64);
+#pragma unroll
+          for (int d = 0; d < DT; ++d)
+            acc[d][r] = fmaf(dr, bf2f(Ks[toff<DH>(kt, (16 * d + c16) >> 3) + (c16 & 7)]), acc[d][r]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {   // dK / dV[T-1][8g + j] += sum over the 16 queries
+          tq[j] += dpp_row_sum16(dsb * bf2f(qf[j]));
+          tv[j] += dpp_row_sum16(pdb * bf2f(of[j]));
+        }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1097,6 +1325,56 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
           for (int d = 0; d < DT; ++d)
             a.dq[(bT + qq) * a.lddq + h * DH + 16 * d + (lane & 15)] = f2bf(acc[d][r] * a.scale);
         }
+      }
+    }
+  }
+  if (tail1) {   // row T-1: the 8 wave partials of each kind + the corner (T-1, T-1)
+    float* corner = tailp + 3 * 8 * DH;   // {dS, Pd} of (T-1, T-1), bf16-rounded
+    if (wave == 0) {   // one 32-lane dot product each for the corner's score and dPd
+      const int d = lane & 31;
+      const int co = toff<DH>(kt, d >> 3) + (d & 7);
+      float sv = bf2f(Qs[co]) * bf2f(Ks[co]), dpv = bf2f(Os[co]) * bf2f(Vs[co]);
+      sv = xsum16(dpp_row_sum16(sv));     // lanes 0-31 hold the same 32 terms as 32-63
+      dpv = xsum16(dpp_row_sum16(dpv));
+      const float pv = __builtin_amdgcn_exp2f(fmaf(sv, c2, -Ls[kt]));
+      float pd = pv;
+      if (DROP) {
+        const bool keep = (mk[drop_word(kt, kt, a.n64)] >> ((kt & 3) * 4 + (kt & 3))) & 1u;
+        pd = keep ? pv : 0.f;
+        dpv = keep ? dpv * a.drop_scale : 0.f;
+      }
+      if (lane == 0) {
+        corner[0] = bf2f(f2bf(pv * (dpv - Dl[kt])));
+        corner[1] = bf2f(f2bf(pd));
+      }
+    }
+    if (c16 == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (wave < 8) tailp[wave * DH + 8 * g + j] = tq[j];                       // dQ
+        else {
+          tailp[(wave) * DH + 8 * g + j] = tq[j];                                 // dK: slots 8..15
+          tailp[(wave + 8) * DH + 8 * g + j] = tv[j];                             // dV: slots 16..23
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 * DH) {
+      const int kind = threadIdx.x / DH, d = threadIdx.x - kind * DH;
+      float sum = 0.f;
+#pragma unroll
+      for (int w8 = 0; w8 < 8; ++w8) sum += tailp[(kind * 8 + w8) * DH + d];
+      const float dsb = corner[0], pdb = corner[1];
+      const int col = d >> 3, el = d & 7;
+      if (kind == 0) {
+        sum = fmaf(dsb, bf2f(Ks[toff<DH>(kt, col) + el]), sum);
+        a.dq[(bT + kt) * a.lddq + h * DH + d] = f2bf(sum * a.scale);
+      } else if (kind == 1) {
+        sum = fmaf(dsb, bf2f(Qs[toff<DH>(kt, col) + el]), sum);
+        a.dk[(bT + kt) * a.lddq + h * DH + d] = f2bf(sum * a.scale);
+      } else {
+        sum = fmaf(pdb, bf2f(Os[toff<DH>(kt, col) + el]), sum);
+        a.dv[(bT + kt) * a.lddq + h * DH + d] = f2bf(DROP ? sum * a.drop_scale : sum);
       }
     }
   }

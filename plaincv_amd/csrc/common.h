@@ -120,6 +120,48 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   return fmaf(x * s * (1.f - s), fmaf(3.f * GELU_A * GELU_K, x2, GELU_K), s);
 }
 
+// ---- cross-lane reductions on VALU (no ds_bpermute round trips through the LDS crossbar)
+// sum / max over the 16 lanes of a DPP row (all 16 receive it): quad butterflies, then the half-row
+// and row mirrors pair the remaining partials
+#define PCV_DPP(v, ctrl) __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), ctrl, 0xF, 0xF, false))
+__device__ __forceinline__ float dpp_row_sum16(float v) {
+  v += PCV_DPP(v, 0xB1);    // quad_perm [1,0,3,2]
+  v += PCV_DPP(v, 0x4E);    // quad_perm [2,3,0,1]
+  v += PCV_DPP(v, 0x141);   // row_half_mirror
+  v += PCV_DPP(v, 0x140);   // row_mirror
+  return v;
+}
+__device__ __forceinline__ float dpp_row_max16(float v) {
+  v = fmaxf(v, PCV_DPP(v, 0xB1));
+  v = fmaxf(v, PCV_DPP(v, 0x4E));
+  v = fmaxf(v, PCV_DPP(v, 0x141));
+  v = fmaxf(v, PCV_DPP(v, 0x140));
+  return v;
+}
+#undef PCV_DPP
+// v (op) v[lane ^ 16] and v (op) v[lane ^ 32]: gfx950 v_permlane16_swap / v_permlane32_swap exchange
+// the two rows of a pair (halves of the wave) between two registers; with both operands = v the
+// two results are {v, partner} in some order
+__device__ __forceinline__ float xsum16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xmax16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xmax32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+// over the 4 rows of the wave (lanes l, l^16, l^32, l^48 all receive it)
+__device__ __forceinline__ float xsum_rows(float v) { return xsum32(xsum16(v)); }
+__device__ __forceinline__ float xmax_rows(float v) { return xmax32(xmax16(v)); }
+
 }  // namespace pcv
 
 static inline int pcv_launch_status() {

@@ -380,15 +380,6 @@ __device__ __forceinline__ void ln_prefetch(const GemmArgs& g, int64_t m0, LnPre
   p.seed = g.drop_thresh ? *g.seedp : 0u;
 }
 
-// sum over the 16 lanes of a DPP row (all 16 receive it): quad butterflies, then the half-row
-// and row mirrors pair the remaining partial sums -- VALU only, no LDS round trips
-__device__ __forceinline__ float dpp_row_sum16(float v) {
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));  // row_half_mirror
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));  // row_mirror
-  return v;
-}
 
 template <int BM>
 __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, const LnPre<BM>& pre) {

@@ -79,11 +79,8 @@ __global__ __launch_bounds__(256) void ln16_fwd_f32_kernel(const float* x, int64
       s2 += v[i][j] * v[i][j];
     }
   }
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) {
-    s += __shfl_xor(s, o, 64);
-    s2 += __shfl_xor(s2, o, 64);
-  }
+  s = dpp_row_sum16(s);   // 16 lanes per row: one DPP row
+  s2 = dpp_row_sum16(s2);
   const float mu = s / D, rs = rsqrtf(fmaxf(s2 / D - mu * mu, 0.f) + eps);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -133,11 +130,8 @@ __global__ __launch_bounds__(256) void ln16_bwd_f32_kernel(const float* dy, int6
         sgx += g[i][j] * xh[i][j];
       }
     }
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) {
-      sg += __shfl_xor(sg, o, 64);
-      sgx += __shfl_xor(sgx, o, 64);
-    }
+    sg = dpp_row_sum16(sg);
+    sgx = dpp_row_sum16(sgx);
     sg /= D;
     sgx /= D;
 #pragma unroll
@@ -164,10 +158,8 @@ __global__ __launch_bounds__(256) void ln16_bwd_f32_kernel(const float* dy, int6
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float a = pa[i][j], b = pb[i][j];
-      a += __shfl_xor(a, 16, 64);
-      b += __shfl_xor(b, 16, 64);
-      a += __shfl_xor(a, 32, 64);
-      b += __shfl_xor(b, 32, 64);
+      a = xsum_rows(a);
+      b = xsum_rows(b);
       if (lane < 16) {
         red[wave][0][(16 * i + l16) * 4 + j] = a;
         red[wave][1][(16 * i + l16) * 4 + j] = b;
@@ -438,7 +430,7 @@ constexpr int FA_TAIL_FLOATS = FA_DH + FA_TMAX + 32 + 32 * 33;
 __host__ __device__ constexpr size_t fa_fwd_lds(int NB) {
   return 2 * (size_t)NB * 16 * FA_DH * 4 + 17 * 6 * 64 * 2 + FA_TAIL_FLOATS * 4;
 }
-constexpr size_t FA_BWD_LDS = 4 * (size_t)FA_TMAX * FA_DH * 4 + 3 * FA_TMAX * 4 + 17 * 6 * 64 * 2 + 3 * 8 * FA_DH * 4;
+constexpr size_t FA_BWD_LDS = 4 * (size_t)FA_TMAX * FA_DH * 4 + 3 * FA_TMAX * 4 + 17 * 6 * 64 * 2 + (3 * 8 * FA_DH + 4) * 4;
 static_assert(FA_BWD_LDS <= 160 * 1024, "fp32 attention backward LDS");
 
 // Forward: 16-query groups dealt round-robin to the waves; per group an online softmax over
@@ -515,8 +507,7 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
           cmax = fmaxf(cmax, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
         }
       }
-      cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+      cmax = xmax_rows(cmax);
       const float mnew = fmaxf(m, cmax);
       const float alpha = __expf(m - mnew);   // 0 on the first chunk (m = -inf)
       m = mnew;
@@ -541,8 +532,7 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
         }
       }
     }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
+    l = xsum_rows(l);
     const float inv = 1.f / l;
     const float os = DROP ? inv * a.dscale : inv;
     if (qv) {
@@ -572,8 +562,7 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
       sv = acc * a.scale;
     }
     float mx = sv;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    mx = xmax_rows(dpp_row_max16(mx));
     if (lane == 0) tr[wave] = mx;
     __syncthreads();
     mx = tr[0];
@@ -581,8 +570,7 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
     for (int w = 1; w < FA_WAVES; ++w) mx = fmaxf(mx, tr[w]);
     const float p = key < T ? __expf(sv - mx) : 0.f;
     float ls = p;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ls += __shfl_xor(ls, o, 64);
+    ls = xsum_rows(dpp_row_sum16(ls));
     if (lane == 0) tr[16 + wave] = ls;
     if (key < TP) tp[key] = (DROP && key < T && !attn_keep(mk, t, key, a.n64)) ? 0.f : p;
     __syncthreads();
@@ -708,8 +696,7 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             float t = dsb * kf[j];
-#pragma unroll
-            for (int o = 8; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+            t = dpp_row_sum16(t);
             if (c16 == 0) tailp[wave * FA_DH + 8 * g + j] += t;   // wave-private slot
           }
         }
@@ -774,11 +761,8 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             float tk = dsb * qf[j], tv = pdb * of[j];
-#pragma unroll
-            for (int o = 8; o > 0; o >>= 1) {
-              tk += __shfl_xor(tk, o, 64);
-              tv += __shfl_xor(tv, o, 64);
-            }
+            tk = dpp_row_sum16(tk);
+            tv = dpp_row_sum16(tv);
             if (c16 == 0) {
               tailp[wave * FA_DH + 8 * g + j] += tk;
               tailp[(wave + 8) * FA_DH + 8 * g + j] += tv;
@@ -796,19 +780,15 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
     }
   }
   if (tail1) {   // row T-1: dq | dk | dv = sums of the 8 wave partials
-    __syncthreads();
-    if (threadIdx.x < 3 * FA_DH) {
-      const int kind = threadIdx.x / FA_DH, d = threadIdx.x - kind * FA_DH, t = T - 1;
-      float sum = 0.f;
-#pragma unroll
-      for (int w8 = 0; w8 < 8; ++w8) sum += tailp[(kind * 8 + w8) * FA_DH + d];
-      // the corner (query T-1, key T-1) lies in neither wave family's blocks
-      float sv = 0.f, dpv = 0.f;
-#pragma unroll 8
-      for (int c = 0; c < FA_DH; ++c) {
-        sv += Qs[fa_off(t, c)] * Ks[fa_off(t, c)];
-        dpv += Os[fa_off(t, c)] * Vs[fa_off(t, c)];
-      }
+    // the corner (query T-1, key T-1) lies in neither wave family's blocks: its score and dPd as
+    // one 32-lane dot product each on wave 0 (96 threads each walking both rows through LDS took
+    // a serial chain of 128 LDS reads)
+    float* corner = tailp + 3 * 8 * FA_DH;
+    if (wave == 0) {
+      const int t = T - 1, c = lane & 31;
+      float sv = Qs[fa_off(t, c)] * Ks[fa_off(t, c)], dpv = Os[fa_off(t, c)] * Vs[fa_off(t, c)];
+      sv = xsum16(dpp_row_sum16(sv));
+      dpv = xsum16(dpp_row_sum16(dpv));
       const float p = __expf(sv * a.scale - Ms[t]) * Is[t];
       float pd = p;
       if (DROP) {
@@ -816,7 +796,18 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
         pd = keep ? p * a.dscale : 0.f;
         dpv = keep ? dpv * a.dscale : 0.f;
       }
-      const float ds = p * (dpv - Dl[t]);
+      if (lane == 0) {
+        corner[0] = p * (dpv - Dl[t]);
+        corner[1] = pd;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 * FA_DH) {
+      const int kind = threadIdx.x / FA_DH, d = threadIdx.x - kind * FA_DH, t = T - 1;
+      float sum = 0.f;
+#pragma unroll
+      for (int w8 = 0; w8 < 8; ++w8) sum += tailp[(kind * 8 + w8) * FA_DH + d];
+      const float ds = corner[0], pd = corner[1];
       sum += kind == 0 ? ds * Ks[fa_off(t, d)] : kind == 1 ? ds * Qs[fa_off(t, d)] : pd * Os[fa_off(t, d)];
       a.dqkv[(bT + T - 1) * a.lddqkv + kind * a.D + h * FA_DH + d] = kind == 2 ? sum : sum * a.scale;
     }

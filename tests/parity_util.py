@@ -11,14 +11,15 @@ def rel(a, b, floor=1e-30):
     return (a - b).norm().item() / max(b.norm().item(), floor)
 
 
-def step_rel(p0, p1, u):
+def step_rel(p0, p1, u, ulps=0.5):
     """Relative error of the applied step p1 - p0 against the expected update u, net of the
-    fp32 rounding of p0 + u (half an ulp of p1 per element)."""
+    fp32 rounding of p0 + u (`ulps` ulps of p1 per element: half an ulp for p + u; a few for
+    schedule-free, whose y' = b1 x + (1 - b1) z' re-forms p from several rounded terms)."""
     p0, p1, u = p0.double(), p1.double(), u.double()
     err = (p1 - p0 - u).norm().item()
     p1f = p1.float()
     ulp = (torch.nextafter(p1f.abs(), torch.full_like(p1f, float("inf"))) - p1f.abs()).double()
-    floor = 0.5 * ulp.norm().item()
+    floor = ulps * ulp.norm().item()
     un = max(u.norm().item(), 1e-30)
     return max(0.0, err - floor) / un
 

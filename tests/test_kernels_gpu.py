@@ -86,10 +86,13 @@ def test_attention_fwd_bwd(dev, B, T, H, Dh, causal, rate):
 
 @pytest.mark.parametrize("B,T,H,rate,delta_ready", [(2, 257, 4, 0.1, False), (3, 17, 2, 0.0, False),
                                                      (1, 320, 3, 0.2, True), (2, 1, 2, 0.0, False),
-                                                     (2, 64, 4, 0.1, True), (4, 257, 4, 0.0, True)])
+                                                     (2, 64, 4, 0.1, True), (4, 257, 4, 0.0, True),
+                                                     (3, 50, 4, 0.1, False), (2, 256, 4, 0.1, False),
+                                                     (2, 33, 2, 0.1, False), (2, 241, 4, 0.0, False)])
 def test_attention_short_path(dev, B, T, H, rate, delta_ready, monkeypatch):
     """One-workgroup-per-(batch, head) kernels for Dh = 32, T <= 320, non-causal (the ViT):
-    against the fp32 reference, and against the tiled kernels (PCV_ATTN_NO_SHORT) on the same inputs."""
+    against the fp32 reference, and against the tiled kernels (PCV_ATTN_NO_SHORT) on the same inputs.
+    T = 16 n + 1 (257, 33, 17): the single tail key / query row is handled outside the MFMA blocks."""
     from oracle import rng
     from plaincv_amd import kernels as K
     Dh = 32

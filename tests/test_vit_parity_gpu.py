@@ -117,7 +117,7 @@ def test_vit_train_step_matches_oracle(dev, optim):
                 d = (p1[k].double() - p0[k].double() - u[k].double()).abs()
                 assert (d > 0.5e-3).double().mean().item() <= 1e-3, (it, k)
                 continue
-            e = step_rel(p0[k], p1[k], u[k])
+            e = step_rel(p0[k], p1[k], u[k], ulps=4.0 if wrap else 0.5)
             assert e <= step_bound(name, k, p0[k]), (it, k, e)
         _, go = value_and_grad(lambda p: (cross_entropy_loss(vit_apply(p, images, oc, True, it, bf16=True),
                                                              labels), None), po)
