@@ -310,14 +310,17 @@ int pcv_attn_bwd_f32(const float* qkv, int64_t ldqkv, const float* o, int64_t ld
  * (optional) += the column sums of dlogits, and dym
  * (cls rows) = bf16 dropout VJP of dx (index (b * row_stride) * D + c, the top block's MLP-out site).
  * x / dx / dym rows: stride ldx / lddx / lddym (T * D for the cls rows).  pcv_vit_head_ok(B, D, K):
- * B <= 64, D <= 128 multiple of 32, K <= 256. */
+ * B <= 64, D <= 128 multiple of 32, K <= 256.  work (optional, 16-B aligned, zero-filled once before
+ * first use, pcv_vit_head_work_floats(B, D, K) floats): one workgroup per 16 rows with a
+ * deterministic last-workgroup reduction of the cross-row sums; NULL: one workgroup. */
 int pcv_vit_head_ok(int B, int D, int K);
+int64_t pcv_vit_head_work_floats(int B, int D, int K);
 int pcv_vit_head(const float* x, int64_t ldx, const float* ln_scale, const float* ln_bias, float eps, const void* W,
                  int64_t ldw, const float* bias, const int* labels, int B, int D, int K, void* yf, int64_t ldy,
                  float* logits, int64_t ldl, float* metrics, float grad_scale, float* dlogits, void* dlogits_b,
                  int64_t ldd, float* dx, int64_t lddx, float* dscale, float* dbias, float* dhead_bias, void* dym,
                  int64_t lddym, float drop_rate, const uint32_t* seed, uint32_t site, int64_t row_stride,
-                 void* stream);
+                 float* work, void* stream);
 /* ---------------------------------------------------------------- loss ----
  * Softmax cross-entropy + argmax accuracy per row, gradient (softmax-onehot)*grad_scale
  * (engine/flax_engine.py:13-22; train_lm.py:181-186).  pcv_mean2: deterministic means. */
@@ -397,8 +400,11 @@ int pcv_chunk_size(void);
  *   conv_in: the job is skipped when *conv_in <= conv_tol; conv_out: atomic max of |C - I|.
  *   record {A, B, C, kscale, R, Cb, alpha_dev, conv_in, conv_out, M, N, K, lda, ldb, ldc, ldr, ldcb,
  *           ta, tb, apow, tiles_n, first_tile, ksplit, kchunk, alpha, beta, rscale, a_diag, a_mul, b_diag, b_mul,
- *           conv_tol} (64x64 tiles, first_tile = prefix sum; apow bit 4 marks a float4-aligned job).
- * vec = 1: every job is float4-aligned (16-B bases, ld % 4, M, N, K % 4) -> vector staging. */
+ *           conv_tol} (64x64 tiles, first_tile = prefix sum; apow bit 4 marks a float4-aligned job,
+ *           bit 5 a symmetric result: upper-triangle tiles only, mirrored).
+ * vec = 1: every job is float4-aligned (16-B bases, ld % 4, M, N, K % 4) -> vector staging.
+ * vec = 2: small jobs (M, N, K <= 512, ta = 0, tb = 1, float4-aligned, no kscale / split-K) on
+ *          32x32 tiles with K split over the workgroup's waves (tiles_n / first_tile in 32-tiles). */
 int pcv_f32_job_size(void);
 int pcv_gemm_f32_grouped(const void* jobs, int njobs, int64_t total_tiles, int vec, void* stream);
 /* Shampoo inverse p-th root (shampoo.py:195-215) by the coupled Newton iteration on the grouped

@@ -71,8 +71,9 @@ __device__ __forceinline__ float wave_max(float v) {
 // binary-searched there -- a per-block linear walk over the table costs one dependent L2 load per
 // skipped job.  `ft` holds >= njobs ints of LDS; falls back to the walk past `cap` jobs.
 template <typename FirstT>
-__device__ __forceinline__ int pcv_find_job(const void* jobs, int njobs, int stride, int first_off, int* ft, int cap) {
-  const int bid = (int)blockIdx.x;
+__device__ __forceinline__ int pcv_find_job(const void* jobs, int njobs, int stride, int first_off, int* ft, int cap,
+                                            int bid = -1) {
+  if (bid < 0) bid = (int)blockIdx.x;
   const char* base = reinterpret_cast<const char*>(jobs);
   if (njobs > cap) {
     int j = 0;
@@ -90,6 +91,17 @@ __device__ __forceinline__ int pcv_find_job(const void* jobs, int njobs, int str
   }
   return lo;
 }
+
+// XCD-aware block order for grouped launches: workgroup b runs on XCD b % 8, so logical tile
+// (b % 8) * (grid / 8) + b / 8 gives each XCD one contiguous run of the job table's tiles -- a
+// job's operands then fill one XCD's L2 instead of being fetched from the MALL by all eight.
+// The grid is a multiple of 8; logical tiles past `total` exit.
+constexpr int PCV_NXCD = 8;
+__device__ __forceinline__ int pcv_xcd_tile() {
+  const int b = (int)blockIdx.x, per = (int)gridDim.x / PCV_NXCD;
+  return (b % PCV_NXCD) * per + b / PCV_NXCD;
+}
+__host__ __device__ inline int64_t pcv_xcd_grid(int64_t total) { return (total + PCV_NXCD - 1) / PCV_NXCD * PCV_NXCD; }
 
 // Block-wide sum for blockDim.x a multiple of 64 (<= 1024); `red` must hold
 // blockDim.x/64 floats of LDS.  Result is broadcast to every thread.

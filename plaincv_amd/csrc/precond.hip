@@ -33,6 +33,9 @@ namespace pcv {
 //   op(A)[m][k] = a_mul * A[m][k] + a_diag * (m == k), op(B) likewise with b_mul / b_diag.
 // conv_in: skip the whole job when *conv_in <= conv_tol (matrix already converged);
 // conv_out: atomic max over the tile of |C - I| (the next iteration's conv_in).
+// sym (apow bit 32; M == N, the product known to be symmetric -- e.g. two commuting polynomials
+// of one symmetric matrix in the Newton chain, or G G^T): only the upper-triangle tiles run
+// (T(T+1)/2 of T^2) and each writes its entries and their mirror, so C comes out exactly symmetric.
 // ksplit > 1 (split-K, for long-K jobs such as weight gradients with K = B*T): the job's tiles are
 // ksplit x (M/64 x N/64), each summing a kchunk-long slice of K and adding alpha * partial to C
 // with fp32 atomics -- only for C += alpha op(A) op(B) (beta = 1, no R / Cb / conv_out).
@@ -75,37 +78,52 @@ struct Stager {
     }
     off0 = ROWK ? (x0 + xs) * ld + ks : ks * ld + x0 + xs;
   }
-  __device__ __forceinline__ float xform(float v, int gx, int gk, int X, int K, float mul, float diag,
-                                         const float* __restrict__ ksc) const {
-    if (gx >= X || gk >= K) return 0.f;
-    float y = mul * v;
-    if (gx == gk) y += diag;
-    if (ksc) y *= ksc[gk];
-    return y;
-  }
-  __device__ void load(const float* __restrict__ base, int k0, int x0, int X, int K, float mul, float diag,
-                       const float* __restrict__ ksc, float (&r)[FG_NPER]) const {
+  // Raw loads only: nothing here consumes the loaded values, so the next chunk's loads stay in
+  // flight under the current chunk's MFMAs (the affine / kscale transform is applied in store()).
+  // kscale values ride along in kv when the job has one (a uniform branch).
+  __device__ void load(const float* __restrict__ base, int k0, int x0, int X, int K,
+                       const float* __restrict__ ksc, float (&r)[FG_NPER], float (&kv)[FG_NPER]) const {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int x = xs + dx * i, k = ks + dk * i, gx = x0 + x, gk = k0 + k;
       const int o = off0 + (ROWK ? dx * i * ld + k0 : (dk * i + k0) * ld);
+      const bool in = gx < X && gk < K;
       if (VEC) {
         // VEC jobs: K % 4 == 0 and X % 4 == 0, so each float4 is all in range or all out
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (gx < X && gk < K) v = *(const float4*)(base + o);
-        const float e[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          r[4 * i + q] = xform(e[q], gx + (ROWK ? 0 : q), gk + (ROWK ? q : 0), X, K, mul, diag, ksc);
+        if (in) v = *(const float4*)(base + o);
+        r[4 * i] = v.x; r[4 * i + 1] = v.y; r[4 * i + 2] = v.z; r[4 * i + 3] = v.w;
       } else {
-        r[i] = (gx < X && gk < K) ? xform(base[o], gx, gk, X, K, mul, diag, ksc) : 0.f;
+        r[i] = in ? base[o] : 0.f;
+      }
+    }
+    if (ksc) {
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        const int k = ks + dk * i, gk = k0 + k;
+#pragma unroll
+        for (int q = 0; q < (VEC ? 4 : 1); ++q) {
+          const int gq = gk + ((VEC && ROWK) ? q : 0);
+          kv[(VEC ? 4 : 1) * i + q] = gq < K ? ksc[gq] : 0.f;
+        }
       }
     }
   }
-  __device__ void store(float* S, const float (&r)[FG_NPER]) const {
+  // transform (mul * v + diag * [gx == gk], times kscale) and write the [x][k] image
+  __device__ void store(float* S, float (&r)[FG_NPER], const float (&kv)[FG_NPER], int k0, int x0, int X, int K,
+                        float mul, float diag, bool has_ks) const {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int x = xs + dx * i, k = ks + dk * i;
+#pragma unroll
+      for (int q = 0; q < (VEC ? 4 : 1); ++q) {
+        const int e = (VEC ? 4 : 1) * i + q;
+        const int gx = x0 + x + ((VEC && !ROWK) ? q : 0), gk = k0 + k + ((VEC && ROWK) ? q : 0);
+        float y = mul * r[e];
+        if (gx == gk && gx < X && gk < K) y += diag;
+        if (has_ks) y *= kv[e];
+        r[e] = y;
+      }
       if (VEC && ROWK) {
         *(float4*)(S + x * LD_XK + k) = make_float4(r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]);
       } else if (VEC) {   // float4 along x: four transposed scalar stores
@@ -135,16 +153,17 @@ __device__ __forceinline__ void f32_tile(const F32Job& jb, int m0, int n0, int k
   const float* __restrict__ A = jb.A;
   const float* __restrict__ B = jb.B;
   const float* __restrict__ ksc = jb.kscale;
-  float ra[FG_NPER], rb[FG_NPER];
-  sa.load(A, kbeg, m0, M, K, amul, adiag, ksc, ra);
-  sb.load(B, kbeg, n0, N, K, bmul, bdiag, nullptr, rb);
+  float ra[FG_NPER], rb[FG_NPER], kv[FG_NPER];
+  const bool has_ks = ksc != nullptr;
+  sa.load(A, kbeg, m0, M, K, ksc, ra, kv);
+  sb.load(B, kbeg, n0, N, K, nullptr, rb, kv);
   for (int k0 = kbeg; k0 < K; k0 += FG_K) {
-    sa.store(As, ra);
-    sb.store(Bs, rb);
+    sa.store(As, ra, kv, k0, m0, M, K, amul, adiag, has_ks);
+    sb.store(Bs, rb, kv, k0, n0, N, K, bmul, bdiag, false);
     __syncthreads();
     if (k0 + FG_K < K) {     // next chunk's loads in flight under this chunk's MFMAs
-      sa.load(A, k0 + FG_K, m0, M, K, amul, adiag, ksc, ra);
-      sb.load(B, k0 + FG_K, n0, N, K, bmul, bdiag, nullptr, rb);
+      sa.load(A, k0 + FG_K, m0, M, K, ksc, ra, kv);
+      sb.load(B, k0 + FG_K, n0, N, K, nullptr, rb, kv);
     }
     // the chunk's images are zero past K, so the loop runs whole 16-long slices
     const int kend = K - k0 < FG_K ? ((K - k0 + 15) & ~15) : FG_K;
@@ -167,12 +186,14 @@ __device__ __forceinline__ void f32_tile(const F32Job& jb, int m0, int n0, int k
 }
 
 template <bool VEC>
-__global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __restrict__ jobs, int njobs) {
+__global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __restrict__ jobs, int njobs, int total) {
   __shared__ __attribute__((aligned(16))) float As[FG_LDS_FLOATS];
   __shared__ __attribute__((aligned(16))) float Bs[FG_LDS_FLOATS];
   __shared__ int ft[FG_JOB_CAP];
-  const int bid = blockIdx.x;
-  const int j = pcv_find_job<int64_t>(jobs, njobs, (int)sizeof(F32Job), (int)offsetof(F32Job, first_tile), ft, FG_JOB_CAP);
+  const int bid = pcv_xcd_tile();
+  if (bid >= total) return;
+  const int j = pcv_find_job<int64_t>(jobs, njobs, (int)sizeof(F32Job), (int)offsetof(F32Job, first_tile), ft,
+                                      FG_JOB_CAP, bid);
   const F32Job jb = jobs[j];
   if (jb.conv_in && *jb.conv_in <= (float)jb.conv_tol) return;
   int t = bid - (int)jb.first_tile;
@@ -184,7 +205,14 @@ __global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __r
     kbeg = sl * (int)jb.kchunk;
     kend = min(kend, kbeg + (int)jb.kchunk);
   }
-  const int m0 = (t / (int)jb.tiles_n) * FG_T, n0 = (t % (int)jb.tiles_n) * FG_T;
+  const bool sym = (jb.apow & 32) != 0;
+  int tm = t / (int)jb.tiles_n, tn = t % (int)jb.tiles_n;
+  if (sym) {   // upper-triangle tile t, row-major: row i holds tiles_n - i tiles
+    tm = 0;
+    for (int len = (int)jb.tiles_n; t >= len; --len) { t -= len; ++tm; }
+    tn = tm + t;
+  }
+  const int m0 = tm * FG_T, n0 = tn * FG_T;
   f32x4 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -218,6 +246,22 @@ __global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __r
         }
     return;
   }
+  // beta * C and rscale * R terms: all 16 reads issued before any is consumed
+  float cr[2][2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + a * 16 + (lane >> 4) * 4 + r;
+        const int col = n0 + wn * 32 + b * 16 + (lane & 15);
+        const bool in = row < M && col < N;
+        float cv = 0.f, rv = 0.f;
+        if (beta != 0.f && in) cv = jb.C[(int64_t)row * jb.ldc + col];
+        if (jb.R && in) rv = jb.R[(int64_t)row * jb.ldr + col];
+        cr[a][b][r] = beta * cv + rscale * rv;
+      }
   float dev_max = 0.f;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -227,13 +271,15 @@ __global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __r
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm * 32 + a * 16 + (lane >> 4) * 4 + r;
         const int col = n0 + wn * 32 + b * 16 + (lane & 15);
-        if (row < M && col < N) {
-          float v = alpha * acc[a][b][r];
+        if (row < M && col < N && (!sym || row <= col)) {
+          const float v = alpha * acc[a][b][r] + cr[a][b][r];
           float* c = jb.C + (int64_t)row * jb.ldc + col;
-          if (beta != 0.f) v += beta * *c;
-          if (jb.R) v += rscale * jb.R[(int64_t)row * jb.ldr + col];
           *c = v;
           if (jb.Cb) jb.Cb[(int64_t)row * jb.ldcb + col] = f2bf(v);
+          if (sym && row != col) {
+            jb.C[(int64_t)col * jb.ldc + row] = v;
+            if (jb.Cb) jb.Cb[(int64_t)col * jb.ldcb + row] = f2bf(v);
+          }
           const float d = fabsf(v - (row == col ? 1.f : 0.f));
           dev_max = (d == d) ? fmaxf(dev_max, d) : __builtin_inff();   // NaN -> never converged
         }
@@ -241,6 +287,141 @@ __global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __r
   if (jb.conv_out) {
     dev_max = wave_max(dev_max);
     if ((threadIdx.x & 63) == 0) atomicMax((unsigned int*)jb.conv_out, __float_as_uint(dev_max));
+  }
+}
+
+// Small-matrix variant (n, K <= 512: the Kronecker factors of the ViT, and every Newton iterate):
+// a 64 x 64 tile's K-long MFMA chain is the launch's critical path there (32 K cycles per wave for
+// a few hundred tiles on 256 CUs), so the tile shrinks to 32 x 32 and the workgroup's four waves
+// split K: wave w sums its quarter of K for the whole tile straight from registers -- both
+// operands stored along k (A [M][K], B [N][K]: ta = 0, tb = 1, which a symmetric B satisfies as
+// stored), one float4 per lane per 16-long k slab (contraction index 4 g + s inside a slab, the
+// same permutation for both operands), all of a batch's loads issued before its first MFMA -- and
+// the four partial tiles are summed in LDS in wave order (deterministic).  Same epilogue as above
+// (affine operands, alpha_dev, beta C, R, Cb, sym, conv_in / conv_out); no kscale, no split-K.
+constexpr int FS_T = 32, FS_SLABS = 4;   // tile edge; 16-long k slabs per load batch
+constexpr int FS_LD = FS_T + 1;
+
+__global__ __launch_bounds__(256) void gemm_f32_small_kernel(const F32Job* __restrict__ jobs, int njobs, int total) {
+  __shared__ float part[4][FS_T][FS_LD];
+  __shared__ int ft[FG_JOB_CAP];
+  const int bid = pcv_xcd_tile();
+  if (bid >= total) return;
+  const int j = pcv_find_job<int64_t>(jobs, njobs, (int)sizeof(F32Job), (int)offsetof(F32Job, first_tile), ft,
+                                      FG_JOB_CAP, bid);
+  const F32Job& jb = jobs[j];
+  if (jb.conv_in && *jb.conv_in <= (float)jb.conv_tol) return;
+  const int tiles_n = (int)jb.tiles_n;
+  int t = bid - (int)jb.first_tile;
+  const bool sym = (jb.apow & 32) != 0;
+  int tm = t / tiles_n, tn = t % tiles_n;
+  if (sym) {
+    tm = 0;
+    for (int len = tiles_n; t >= len; --len) { t -= len; ++tm; }
+    tn = tm + t;
+  }
+  const int m0 = tm * FS_T, n0 = tn * FS_T;
+  const int M = (int)jb.M, N = (int)jb.N, K = (int)jb.K;
+  const int lda = (int)jb.lda, ldb = (int)jb.ldb;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r16 = lane & 15, g = lane >> 4;
+  const float amul = (float)jb.a_mul, adiag = (float)jb.a_diag, bmul = (float)jb.b_mul, bdiag = (float)jb.b_diag;
+  const bool aff = amul != 1.f || adiag != 0.f || bmul != 1.f || bdiag != 0.f;
+  const float* __restrict__ A = jb.A;
+  const float* __restrict__ B = jb.B;
+  // this wave's K range: whole 16-long slabs
+  const int kq = (((K + 3) / 4) + 15) & ~15;
+  const int kb = w * kq, ke = min(K, kb + kq);
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = kb; k0 < ke; k0 += 16 * FS_SLABS) {
+    float4 fa[FS_SLABS][2], fb[FS_SLABS][2];
+#pragma unroll
+    for (int sl = 0; sl < FS_SLABS; ++sl) {
+      const int k = k0 + 16 * sl + 4 * g;      // K % 4 == 0: the float4 is all in range or all out
+      const bool kin = k < ke;
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int row = m0 + 16 * a + r16;
+        fa[sl][a] = (kin && row < M) ? *(const float4*)(A + row * lda + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int col = n0 + 16 * a + r16;
+        fb[sl][a] = (kin && col < N) ? *(const float4*)(B + col * ldb + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    if (aff) {   // op(X) = mul X + diag I on the in-range entries
+#pragma unroll
+      for (int sl = 0; sl < FS_SLABS; ++sl) {
+        const int k = k0 + 16 * sl + 4 * g;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const int row = m0 + 16 * a + r16, col = n0 + 16 * a + r16;
+          float* pa = &fa[sl][a].x;
+          float* pb = &fb[sl][a].x;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            pa[q] = amul * pa[q] + ((row == k + q && k < ke && row < M) ? adiag : 0.f);
+            pb[q] = bmul * pb[q] + ((col == k + q && k < ke && col < N) ? bdiag : 0.f);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < FS_SLABS; ++sl) {
+      if (k0 + 16 * sl >= ke) break;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32((&fa[sl][a].x)[q], (&fb[sl][b].x)[q], acc[a][b], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part[w][16 * a + 4 * g + i][16 * b + r16] = acc[a][b][i];
+  __syncthreads();
+  float alpha = (float)jb.alpha;
+  if (jb.alpha_dev) {
+    const float sc = *jb.alpha_dev;
+    alpha *= (jb.apow & 15) == 2 ? sc * sc : sc;
+  }
+  const float beta = (float)jb.beta, rscale = (float)jb.rscale;
+  const int lr = tid >> 3, lc = (tid & 7) * 4, row = m0 + lr;
+  float cr[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int col = n0 + lc + q;
+    const bool in = row < M && col < N;
+    float cv = 0.f, rv = 0.f;
+    if (beta != 0.f && in) cv = jb.C[(int64_t)row * jb.ldc + col];
+    if (jb.R && in) rv = jb.R[(int64_t)row * jb.ldr + col];
+    cr[q] = beta * cv + rscale * rv;
+  }
+  float dev_max = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int col = n0 + lc + q;
+    if (row < M && col < N && (!sym || row <= col)) {
+      const float v = alpha * (((part[0][lr][lc + q] + part[1][lr][lc + q]) + part[2][lr][lc + q]) + part[3][lr][lc + q]) + cr[q];
+      jb.C[(int64_t)row * jb.ldc + col] = v;
+      if (jb.Cb) jb.Cb[(int64_t)row * jb.ldcb + col] = f2bf(v);
+      if (sym && row != col) {
+        jb.C[(int64_t)col * jb.ldc + row] = v;
+        if (jb.Cb) jb.Cb[(int64_t)col * jb.ldcb + row] = f2bf(v);
+      }
+      const float d = fabsf(v - (row == col ? 1.f : 0.f));
+      dev_max = (d == d) ? fmaxf(dev_max, d) : __builtin_inff();
+    }
+  }
+  if (jb.conv_out) {
+    dev_max = wave_max(dev_max);
+    if (lane == 0) atomicMax((unsigned int*)jb.conv_out, __float_as_uint(dev_max));
   }
 }
 
@@ -263,22 +444,32 @@ __global__ __launch_bounds__(1024) void newton_init_kernel(const NewtonJob* __re
                                                            float kappa_max) {
   __shared__ float red[16];
   const NewtonJob jb = jobs[blockIdx.x];
-  const int n = (int)jb.n;
+  const int n = (int)jb.n, ldl = (int)jb.ldl;
   const float sh = (float)jb.shift;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // a row per wave, coalesced along the row; independent loads in flight per lane
   float s = 0.f;
-  for (int e = threadIdx.x; e < n * n; e += 1024) {
-    const int r = e / n, c = e - r * n;
-    const float x = jb.L[(int64_t)r * jb.ldl + c] + (r == c ? sh : 0.f);
-    s += x * x;
+  for (int r = w; r < n; r += 16) {
+    const float* row = jb.L + (int64_t)r * ldl;
+#pragma unroll 4
+    for (int c = lane; c < n; c += 64) {
+      const float x = row[c] + (r == c ? sh : 0.f);
+      s += x * x;
+    }
   }
   s = block_sum(s, red);
   const float fro = sqrtf(s);
   const float z = (1.f + p) / (2.f * fro);
   const float xz = powf(z, 1.f / p);
-  for (int e = threadIdx.x; e < n * n; e += 1024) {
-    const int r = e / n, c = e - r * n;
-    jb.M0[e] = z * (jb.L[(int64_t)r * jb.ldl + c] + (r == c ? sh : 0.f));
-    jb.X0[e] = r == c ? xz : 0.f;
+  for (int r = w; r < n; r += 16) {
+    const float* row = jb.L + (int64_t)r * ldl;
+    float* m0 = jb.M0 + (int64_t)r * n;
+    float* x0 = jb.X0 + (int64_t)r * n;
+#pragma unroll 4
+    for (int c = lane; c < n; c += 64) {
+      m0[c] = z * (row[c] + (r == c ? sh : 0.f));
+      x0[c] = r == c ? xz : 0.f;
+    }
   }
   for (int i = threadIdx.x; i <= iters; i += 1024)
     jb.conv[i] = i > 0 ? 0.f : ((fro <= kappa_max * sh && fro == fro) ? 1.f : 0.f);
@@ -679,12 +870,17 @@ extern "C" int pcv_perm_job_size(void) { return (int)sizeof(PermJob); }
 
 extern "C" int pcv_gemm_f32_grouped(const void* jobs_dev, int njobs, int64_t total_tiles, int vec, void* stream) {
   if (!jobs_dev || njobs <= 0 || total_tiles <= 0 || total_tiles >= (1ll << 31)) return PCV_EINVAL;
-  if (vec)
-    hipLaunchKernelGGL(gemm_f32_grouped_kernel<true>, dim3((unsigned)total_tiles), dim3(256), 0, (hipStream_t)stream,
-                       (const F32Job*)jobs_dev, njobs);
+  const dim3 grid((unsigned)pcv_xcd_grid(total_tiles));
+  const int total = (int)total_tiles;
+  if (vec == 2)
+    hipLaunchKernelGGL(gemm_f32_small_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const F32Job*)jobs_dev, njobs,
+                       total);
+  else if (vec)
+    hipLaunchKernelGGL(gemm_f32_grouped_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const F32Job*)jobs_dev, njobs, total);
   else
-    hipLaunchKernelGGL(gemm_f32_grouped_kernel<false>, dim3((unsigned)total_tiles), dim3(256), 0,
-                       (hipStream_t)stream, (const F32Job*)jobs_dev, njobs);
+    hipLaunchKernelGGL(gemm_f32_grouped_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const F32Job*)jobs_dev, njobs, total);
   return pcv_launch_status();
 }
 

@@ -15,6 +15,12 @@
 // (v_mfma_f32_16x16x32_bf16) with fp32 accumulation, as the unfused GEMM kernels did; LayerNorm
 // and CE statistics in fp32 (fast variance, eps 1e-6; log-sum-exp with exact first-index argmax).
 // Limits: B <= 64, D <= 128 (multiple of 32), K <= 256 (ldw >= K, multiple of 8).
+//
+// Split form (a workspace given): one workgroup per 16 rows (B = 64: four CUs instead of one --
+// the single workgroup walked its rows' LayerNorm / CE / VJP four deep, and this chain sits on the
+// step's critical path).  Cross-row sums (CE / accuracy means, head-bias, LayerNorm scale / bias
+// gradients) are per-workgroup partials in the workspace; the last workgroup to finish (a ticket
+// counter, reset by that workgroup) adds them in workgroup order -- deterministic.
 #include "common.h"
 
 namespace pcv {
@@ -22,6 +28,7 @@ namespace pcv {
 constexpr int VH_THREADS = 1024, VH_WAVES = 16, VH_BMAX = 64, VH_DMAX = 128, VH_KMAX = 256;
 
 struct VitHeadArgs {
+  float* work;                  // split form: [4] ticket (int) + [nblk][2 + K + 2D] partials; null: one workgroup
   const float* x; int64_t ldx;
   const float* ln_s; const float* ln_b; float eps;
   const bf16* W; int64_t ldw; const float* bias;
@@ -41,24 +48,32 @@ struct VitHeadArgs {
 
 // LDS: X fp32 [64][D], Y bf16 [64][D+8], L fp32 [64][max(K32, D)+4] (logits, later dy), Dl bf16 [64][K32+8],
 // row stats, reductions
-__host__ __device__ constexpr size_t vh_lds(int D, int K) {
+__host__ __device__ constexpr size_t vh_lds(int D, int K, int R) {   // R rows per workgroup
   const int K32 = (K + 31) / 32 * 32, LW = K32 > D ? K32 : D;   // L holds logits [K32] and later dy [D]
-  return (size_t)VH_BMAX * D * 4 + (size_t)VH_BMAX * (D + 8) * 2 + (size_t)VH_BMAX * (LW + 4) * 4 +
-         (size_t)VH_BMAX * (K32 + 8) * 2 + 4 * VH_BMAX * 4 + 2 * VH_WAVES * 4 + 2 * 8 * VH_DMAX * 4;
+  return (size_t)R * D * 4 + (size_t)R * (D + 8) * 2 + (size_t)R * (LW + 4) * 4 +
+         (size_t)R * (K32 + 8) * 2 + 4 * R * 4 + 2 * VH_WAVES * 4 + 2 * 8 * VH_DMAX * 4 + 16;
 }
+__host__ __device__ constexpr int vh_part_floats(int D, int K) { return 2 + K + 2 * D; }
 
+// MT 16-row M tiles per workgroup: 4 (one workgroup, all B <= 64 rows) or 1 (split form)
+template <int MT>
 __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
+  constexpr int R = 16 * MT;
   extern __shared__ __attribute__((aligned(16))) char vh_smem[];
   const int B = a.B, D = a.D, K = a.K, K32 = (K + 31) / 32 * 32;
   const int LY = D + 8, LL = (K32 > D ? K32 : D) + 4, LD = K32 + 8;
+  const int r0 = blockIdx.x * R, Bl = min(R, B - r0);    // this workgroup's rows [r0, r0 + Bl)
+  const bool split = a.work != nullptr;
+  float* part = split ? a.work + 4 + (size_t)blockIdx.x * vh_part_floats(D, K) : nullptr;
   float* Xs = reinterpret_cast<float*>(vh_smem);
-  bf16* Ys = reinterpret_cast<bf16*>(Xs + VH_BMAX * D);
-  float* Ls = reinterpret_cast<float*>(Ys + VH_BMAX * LY);
-  bf16* Ds = reinterpret_cast<bf16*>(Ls + VH_BMAX * LL);
-  float* mean = reinterpret_cast<float*>(Ds + VH_BMAX * LD);
-  float* rstd = mean + VH_BMAX;
-  float* red = rstd + 2 * VH_BMAX;       // [16 waves][2]
+  bf16* Ys = reinterpret_cast<bf16*>(Xs + R * D);
+  float* Ls = reinterpret_cast<float*>(Ys + R * LY);
+  bf16* Ds = reinterpret_cast<bf16*>(Ls + R * LL);
+  float* mean = reinterpret_cast<float*>(Ds + R * LD);
+  float* rstd = mean + R;
+  float* red = rstd + 2 * R;             // [16 waves][2]
   float* colred = red + 2 * VH_WAVES;    // [2][8][VH_DMAX]
+  int* flag = reinterpret_cast<int*>(colred + 2 * 8 * VH_DMAX);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 
   // Both products' W fragments are issued first, so their global latency hides under the
@@ -84,15 +99,15 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
     }
   }
 
-  // ---- LayerNorm of the cls rows (one wave per row); pad rows of Y zero
-  for (int b = wave; b < VH_BMAX; b += VH_WAVES) {
-    if (b >= B) {
+  // ---- LayerNorm of the cls rows (one wave per row); pad rows of Y zero.  b: local row
+  for (int b = wave; b < R; b += VH_WAVES) {
+    if (b >= Bl) {
       for (int c = lane; c < LY; c += 64) Ys[b * LY + c] = f2bf(0.f);
       continue;
     }
     float s = 0.f, s2 = 0.f;
     for (int c = lane; c < D; c += 64) {
-      const float v = a.x[(int64_t)b * a.ldx + c];
+      const float v = a.x[(int64_t)(r0 + b) * a.ldx + c];
       Xs[b * D + c] = v;
       s += v;
       s2 += v * v;
@@ -103,7 +118,7 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
     for (int c = lane; c < D; c += 64) {
       const bf16 y = f2bf((Xs[b * D + c] - mu) * rs * a.ln_s[c] + a.ln_b[c]);
       Ys[b * LY + c] = y;
-      a.yf[(int64_t)b * a.ldy + c] = y;
+      a.yf[(int64_t)(r0 + b) * a.ldy + c] = y;
     }
     if (lane == 0) { mean[b] = mu; rstd[b] = rs; }
   }
@@ -113,26 +128,28 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
   const int nkt = K32 / 16;
   if (wave < (K + 15) / 16) {
     const int n0 = wave * 16, ncol = n0 + (lane & 15), kg = lane >> 4;
-    f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < VH_DMAX / 32; ++ks) {
       if (ks >= D / 32) break;
       const bf16x8 bfr = wl[ks];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         const bf16x8 afr = *reinterpret_cast<const bf16x8*>(Ys + (mt * 16 + (lane & 15)) * LY + ks * 32 + 8 * kg);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr, acc[mt], 0, 0, 0);
       }
     }
     const float bv = ncol < K ? a.bias[ncol] : 0.f;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = mt * 16 + 4 * kg + r;
         const float z = acc[mt][r] + bv;
         Ls[b * LL + ncol] = z;
-        if (b < B && ncol < K) a.logits[(int64_t)b * a.ldl + ncol] = z;
+        if (b < Bl && ncol < K) a.logits[(int64_t)(r0 + b) * a.ldl + ncol] = z;
       }
   }
   (void)nkt;
@@ -140,8 +157,8 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
 
   // ---- softmax cross-entropy + accuracy per row; dlogits
   float lsum = 0.f, csum = 0.f;
-  for (int b = wave; b < VH_BMAX; b += VH_WAVES) {
-    if (b >= B) {
+  for (int b = wave; b < R; b += VH_WAVES) {
+    if (b >= Bl) {
       if (a.need_grad)
         for (int c = lane; c < LD; c += 64) Ds[b * LD + c] = f2bf(0.f);
       continue;
@@ -162,7 +179,7 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
     for (int c = lane; c < K; c += 64) s += __expf(Ls[b * LL + c] - m);
     s = wave_sum(s);
     const float lse = m + __logf(s);
-    const int y = a.labels[b];
+    const int y = a.labels[r0 + b];
     const bool yok = y >= 0 && y < K;
     if (lane == 0) {
       lsum += yok ? lse - Ls[b * LL + y] : 0.f;
@@ -175,9 +192,9 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
           d = __expf(Ls[b * LL + c] - lse);
           if (c == y) d -= 1.f;
           d *= a.grad_scale;
-          a.dlogits[(int64_t)b * a.ldd + c] = d;
+          a.dlogits[(int64_t)(r0 + b) * a.ldd + c] = d;
           const bf16 db = f2bf(d);
-          a.dlogits_b[(int64_t)b * a.ldd + c] = db;
+          a.dlogits_b[(int64_t)(r0 + b) * a.ldd + c] = db;
           Ds[b * LD + c] = db;
           Ls[b * LL + c] = d;   // this lane's logit is no longer needed: keep d for the bias column sums
         } else {
@@ -191,36 +208,38 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
   if (tid == 0) {
     float l = 0.f, c = 0.f;
     for (int w = 0; w < VH_WAVES; ++w) { l += red[w]; c += red[VH_WAVES + w]; }
-    a.metrics[0] = l / B;
-    a.metrics[1] = c / B;
+    if (split) { part[0] = l; part[1] = c; }
+    else { a.metrics[0] = l / B; a.metrics[1] = c / B; }
   }
-  if (!a.need_grad) return;
-
+  if (a.need_grad) {
   // ---- head bias gradient: column sums of dlogits over the rows (fixed order)
   if (a.gbias && tid < K) {
     float sb = 0.f;
-    for (int b = 0; b < B; ++b) sb += Ls[b * LL + tid];
-    a.gbias[tid] += sb;
+    for (int b = 0; b < Bl; ++b) sb += Ls[b * LL + tid];
+    if (split) part[2 + tid] = sb;
+    else a.gbias[tid] += sb;
   }
   __syncthreads();
   // ---- dy = dlogits W^T (bf16 operands as the unfused dgrad GEMM): wave w owns columns 16w..+15
   float* Dy = Ls;
   if (wave < D / 16) {
     const int d0 = wave * 16, dcol = d0 + (lane & 15), kg = lane >> 4;
-    f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < VH_KMAX / 32; ++ks) {
       if (ks >= K32 / 32) break;
       const int k = ks * 32 + 8 * kg;
       const bf16x8 bfr = wd[ks];   // dlogits is 0 past K
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
+      for (int mt = 0; mt < MT; ++mt) {
         const bf16x8 afr = *reinterpret_cast<const bf16x8*>(Ds + (mt * 16 + (lane & 15)) * LD + k);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr, bfr, acc[mt], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) Dy[(mt * 16 + 4 * kg + r) * LL + dcol] = acc[mt][r];
   }
@@ -228,7 +247,7 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
 
   // ---- LayerNorm VJP per row -> dx (cls rows) and the top block's dropout-VJP bf16 rows
   const uint32_t seed = a.thresh ? *a.seed : 0u;
-  for (int b = wave; b < B; b += VH_WAVES) {
+  for (int b = wave; b < Bl; b += VH_WAVES) {
     const float mu = mean[b], rs = rstd[b];
     float sg = 0.f, sgx = 0.f;
     for (int c = lane; c < D; c += 64) {
@@ -243,11 +262,12 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
       const float g = Dy[b * LL + c] * a.ln_s[c];
       const float xh = (Xs[b * D + c] - mu) * rs;
       const float dxv = rs * (g - sg - xh * sgx);
-      a.dx[(int64_t)b * a.lddx + c] = dxv;
+      a.dx[(int64_t)(r0 + b) * a.lddx + c] = dxv;
       float yv = dxv;
       if (a.thresh)
-        yv = hash3(seed, a.site, (uint32_t)((int64_t)b * a.row_stride * D + c)) >= a.thresh ? dxv * a.drop_scale : 0.f;
-      a.dym[(int64_t)b * a.lddym + c] = f2bf(yv);
+        yv = hash3(seed, a.site, (uint32_t)((int64_t)(r0 + b) * a.row_stride * D + c)) >= a.thresh ? dxv * a.drop_scale
+                                                                                                 : 0.f;
+      a.dym[(int64_t)(r0 + b) * a.lddym + c] = f2bf(yv);
     }
   }
   // ---- scale / bias gradients: column sums over the rows (8 row groups x D columns, fixed order)
@@ -255,7 +275,7 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
     const int col = tid % VH_DMAX, rg = tid / VH_DMAX;   // 8 row groups
     float s1 = 0.f, s0 = 0.f;
     if (col < D)
-      for (int b = rg; b < B; b += 8) {
+      for (int b = rg; b < Bl; b += 8) {
         const float dy = Dy[b * LL + col];
         s1 += dy * (Xs[b * D + col] - mean[b]) * rstd[b];
         s0 += dy;
@@ -267,8 +287,42 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
   if (tid < D) {
     float s1 = 0.f, s0 = 0.f;
     for (int rg = 0; rg < 8; ++rg) { s1 += colred[rg * VH_DMAX + tid]; s0 += colred[8 * VH_DMAX + rg * VH_DMAX + tid]; }
-    a.gs[tid] += s1;
-    a.gc[tid] += s0;
+    if (split) { part[2 + K + tid] = s1; part[2 + K + D + tid] = s0; }
+    else { a.gs[tid] += s1; a.gc[tid] += s0; }
+  }
+  }   // need_grad
+  if (!split) return;
+  // ---- split form: the last workgroup adds every workgroup's partials, in workgroup order
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    const int t = atomicAdd(reinterpret_cast<int*>(a.work), 1);
+    *flag = t == (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  __threadfence();
+  const int nb = (int)gridDim.x, PF = vh_part_floats(D, K);
+  const float* P = a.work + 4;
+  if (tid == 0) {
+    float l = 0.f, c = 0.f;
+    for (int j = 0; j < nb; ++j) { l += P[j * PF]; c += P[j * PF + 1]; }
+    a.metrics[0] = l / B;
+    a.metrics[1] = c / B;
+    *reinterpret_cast<int*>(a.work) = 0;     // ticket reset for the next launch
+  }
+  if (a.need_grad) {
+    if (a.gbias && tid < K) {
+      float sb = 0.f;
+      for (int j = 0; j < nb; ++j) sb += P[j * PF + 2 + tid];
+      a.gbias[tid] += sb;
+    }
+    if (tid < D) {
+      float s1 = 0.f, s0 = 0.f;
+      for (int j = 0; j < nb; ++j) { s1 += P[j * PF + 2 + K + tid]; s0 += P[j * PF + 2 + K + D + tid]; }
+      a.gs[tid] += s1;
+      a.gc[tid] += s0;
+    }
   }
 }
 
@@ -285,7 +339,7 @@ extern "C" int pcv_vit_head(const float* x, int64_t ldx, const float* ln_scale, 
                             void* yf, int64_t ldy, float* logits, int64_t ldl, float* metrics, float grad_scale,
                             float* dlogits, void* dlogits_b, int64_t ldd, float* dx, int64_t lddx, float* dscale,
                             float* dbias, float* dhead_bias, void* dym, int64_t lddym, float drop_rate,
-                            const uint32_t* seed, uint32_t site, int64_t row_stride, void* stream) {
+                            const uint32_t* seed, uint32_t site, int64_t row_stride, float* work, void* stream) {
   if (!pcv_vit_head_ok(B, D, K) || !x || !ln_scale || !ln_bias || !W || !bias || !labels || !yf || !logits ||
       !metrics || ldw < K || (ldw & 7))
     return PCV_EINVAL;
@@ -306,9 +360,20 @@ extern "C" int pcv_vit_head(const float* x, int64_t ldx, const float* ln_scale, 
     a.drop_scale = 1.f / (1.f - drop_rate);
   }
   a.seed = seed; a.site = site; a.row_stride = row_stride;
-  const size_t lds = vh_lds(D, K);
+  a.work = work;
+  if (work && !pcv_aligned16(work)) return PCV_EALIGN;
+  if (work && B > 16) {
+    hipLaunchKernelGGL(vit_head_kernel<1>, dim3((B + 15) / 16), dim3(VH_THREADS), vh_lds(D, K, 16),
+                       (hipStream_t)stream, a);
+    return pcv_launch_status();
+  }
+  a.work = nullptr;
   static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
-  if (const int e = optin.ensure((const void*)vit_head_kernel, (int)vh_lds(VH_DMAX, VH_KMAX))) return e;
-  hipLaunchKernelGGL(vit_head_kernel, dim3(1), dim3(VH_THREADS), lds, (hipStream_t)stream, a);
+  if (const int e = optin.ensure((const void*)vit_head_kernel<4>, (int)vh_lds(VH_DMAX, VH_KMAX, VH_BMAX))) return e;
+  hipLaunchKernelGGL(vit_head_kernel<4>, dim3(1), dim3(VH_THREADS), vh_lds(D, K, VH_BMAX), (hipStream_t)stream, a);
   return pcv_launch_status();
+}
+
+extern "C" int64_t pcv_vit_head_work_floats(int B, int D, int K) {
+  return 4 + (int64_t)((B + 15) / 16) * vh_part_floats(D, K);
 }

@@ -579,9 +579,10 @@ def vit_head_ok(B, D, K):
 
 def vit_head(x, ln_scale, ln_bias, W, bias, labels, yf, logits, metrics, grad_scale=1.0, dlogits=None,
              dlogits_b=None, dx=None, dscale=None, dbias=None, dym=None, drop_rate=0.0, seed=None, site=0,
-             row_stride=1, eps=1e-6, dhead_bias=None):
+             row_stride=1, eps=1e-6, dhead_bias=None, work=None):
     """Fused ViT head (pcv_vit_head): final LayerNorm of the cls rows x [B, D] (strided), logits, CE
-    metrics and, with dlogits given, the whole head backward down to the top block's dropout VJP."""
+    metrics and, with dlogits given, the whole head backward down to the top block's dropout VJP.
+    work (vit_head_work(B, D, K)): one workgroup per 16 rows instead of one for all."""
     B, D = x.shape
     Kc = bias.numel()
     _chk(vit_head_ok(B, D, Kc), "vit_head shape")
@@ -593,13 +594,20 @@ def vit_head(x, ln_scale, ln_bias, W, bias, labels, yf, logits, metrics, grad_sc
         _chk(tuple(dlogits.shape) == (B, Kc) and tuple(dlogits_b.shape) == (B, Kc) and _ld(dlogits) == _ld(dlogits_b) and
              tuple(dx.shape) == (B, D) and tuple(dym.shape) == (B, D) and dx.dtype == F32 and dym.dtype == BF16,
              "vit_head grads")
+    if work is not None:
+        _chk(work.dtype == F32 and work.numel() >= hip.load().pcv_vit_head_work_floats(B, D, Kc), "vit_head work")
     _dev(x, ln_scale, ln_bias, W, bias, labels, yf, logits, metrics, dlogits, dlogits_b, dx, dscale, dbias, dym, seed,
-         dhead_bias)
+         dhead_bias, work)
     hip.call("pcv_vit_head", ptr(x), _ld(x), ptr(ln_scale), ptr(ln_bias), float(eps), ptr(W), _ld(W), ptr(bias),
              ptr(labels), B, D, Kc, ptr(yf), _ld(yf), ptr(logits), _ld(logits), ptr(metrics), float(grad_scale),
              ptr(dlogits), ptr(dlogits_b), _ld(dlogits) if grad else 0, ptr(dx), _ld(dx) if grad else 0,
              ptr(dscale), ptr(dbias), ptr(dhead_bias), ptr(dym), _ld(dym) if grad else 0, float(drop_rate), ptr(seed),
-             int(site) & 0xFFFFFFFF, int(row_stride), stream_ptr())
+             int(site) & 0xFFFFFFFF, int(row_stride), ptr(work), stream_ptr())
+
+
+def vit_head_work(B, D, K, device):
+    """Zero-filled workspace of the split head (its ticket must start at 0; the kernel resets it)."""
+    return torch.zeros(int(hip.load().pcv_vit_head_work_floats(int(B), int(D), int(K))), dtype=F32, device=device)
 
 
 def mean2(x, y, n, scale, out):

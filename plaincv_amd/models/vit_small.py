@@ -261,6 +261,9 @@ class ViTRunner:
                            os.environ.get("PCV_VIT_FUSED_HEAD", "1") != "0")
         if self.fused_head:   # only the cls rows of the top block's dropout-VJP operand are ever written
             self.dym[Lc - 1] = torch.zeros(R, D, dtype=bf, device=dev)
+            # one workgroup per 16 rows (PCV_VIT_HEAD_SPLIT=0: the single-workgroup form)
+            self.head_work = (K.vit_head_work(B, D, self.Kc, dev)
+                              if os.environ.get("PCV_VIT_HEAD_SPLIT", "1") != "0" else None)
         self.dh = [e(R, M, dt=bf) for _ in range(Lc)]
         # LayerNorm fused into the residual-stream GEMM epilogues (pcv_gemm_ln) when rows fit one tile
         self.fuse_ln = bool(model.use_layernorm) and D <= 128 and D % 8 == 0
@@ -444,7 +447,7 @@ class ViTRunner:
                        dx=self.dx.view(B, T * D)[:, :D] if g else None, dscale=self.gsf if g else None,
                        dbias=self.gcf if g else None, dym=self.dym[L - 1].view(B, T * D)[:, :D] if g else None,
                        drop_rate=rate, seed=seed, site=site_mlp_out(L - 1), row_stride=T,
-                       dhead_bias=self.gbh if g else None)
+                       dhead_bias=self.gbh if g else None, work=self.head_work)
             return self.metrics
         if self.bn:   # statistics over every row, normalise the cls rows only (vit_small.py:121-125)
             K.batchnorm_stats(self.xs[-1], *self.raf, *self.bstf, self.bn_ws, train)

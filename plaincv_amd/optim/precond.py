@@ -13,6 +13,7 @@ from .. import hip
 from ..hip import ptr, stream_ptr
 
 TILE = 64
+SMALL_TILE, SMALL_MAX = 32, 512     # K-split small-matrix kernel: tile edge, largest M / N / K
 EIGH_MAX_N = 256          # two-sided LDS Jacobi (one CU per matrix)
 EIGH_BIG_MAX_N = 4096     # one-sided Jacobi in HBM (csrc/eigh_big.hip)
 QR_MAX_N = 4096
@@ -41,17 +42,21 @@ class GemmF32:
 
     FMT = "<9Q15q8d"
 
-    def __init__(self):
+    def __init__(self, small=True):
+        """small: route eligible jobs to the K-split 32x32 kernel (False: always 64x64 tiles)"""
         self.jobs = []
         self.dev = None
+        self.small = bool(small)
 
     def add(self, a, b, c, ta=False, tb=False, alpha=1.0, beta=0.0, kscale=None, r=None, rscale=0.0, cb=None,
             alpha_dev=None, apow=1, a_affine=(1.0, 0.0), b_affine=(1.0, 0.0), conv_in=None, conv_out=None,
-            conv_tol=0.0, ksplit=1):
+            conv_tol=0.0, ksplit=1, sym=False):
         """a_affine = (mul, diag): op(A) -> mul * op(A) + diag * I (b_affine likewise);
         conv_in: skip this job when *conv_in <= conv_tol; conv_out: atomic max of |C - I|;
         ksplit > 1: split K over that many tiles per C tile, accumulated with fp32 atomics (only
-        C += alpha op(A) op(B): beta 1, no r / cb / conv_out)."""
+        C += alpha op(A) op(B): beta 1, no r / cb / conv_out).
+        sym: the caller knows the result is symmetric (and C / R too when read): only the
+        upper-triangle tiles are computed, and mirrored."""
         M, K = (a.shape[1], a.shape[0]) if ta else (a.shape[0], a.shape[1])
         K2, N = (b.shape[1], b.shape[0]) if tb else (b.shape[0], b.shape[1])
         if K != K2 or tuple(c.shape) != (M, N):
@@ -64,6 +69,8 @@ class GemmF32:
             raise ValueError("bf16 copy shape")
         tiles_n = (N + TILE - 1) // TILE
         ksplit = max(1, int(ksplit))
+        if sym and (M != N or ksplit > 1):
+            raise ValueError("sym jobs: square C, no split-K")
         kchunk = K
         if ksplit > 1:
             if beta != 1.0 or r is not None or cb is not None or conv_out is not None:
@@ -77,10 +84,18 @@ class GemmF32:
         # float4 staging: 16-B aligned bases, row strides % 4, K and the operand x-extents % 4
         vec = (K % 4 == 0 and M % 4 == 0 and N % 4 == 0 and all(
             t.data_ptr() % 16 == 0 and t.stride(0) % 4 == 0 for t in (a, b)))
+        # small jobs: both operands stored along k, K-split 32x32 tiles (csrc/precond.hip)
+        small = (self.small and vec and not ta and tb and kscale is None and ksplit == 1
+                 and max(M, N, K) <= SMALL_MAX and a.stride(1) == 1 and b.stride(1) == 1)
+        if small:
+            tiles_n = (N + SMALL_TILE - 1) // SMALL_TILE
         self.jobs.append(dict(A=a, B=b, C=c, ks=kscale, R=r, Cb=cb, ad=alpha_dev, M=M, N=N, K=K, lda=_ld(a),
                               ldb=_ld(b), ldc=_ld(c), ldr=_ld(r) if r is not None else 0,
-                              ldcb=cb.stride(0) if cb is not None else 0, ta=int(ta), tb=int(tb), apow=int(apow) | (16 if vec else 0),
-                              tiles=((M + TILE - 1) // TILE) * tiles_n * ksplit, tiles_n=tiles_n, ksplit=ksplit,
+                              ldcb=cb.stride(0) if cb is not None else 0, ta=int(ta), tb=int(tb),
+                              apow=int(apow) | (16 if vec else 0) | (32 if sym else 0), kind=2 if small else int(vec),
+                              tiles=(tiles_n * (tiles_n + 1) // 2 if sym else
+                                     ((M + (SMALL_TILE if small else TILE) - 1) // (SMALL_TILE if small else TILE))
+                                     * tiles_n * ksplit), tiles_n=tiles_n, ksplit=ksplit,
                               kchunk=kchunk, alpha=float(alpha),
                               beta=float(beta), rscale=float(rscale), aff=(float(a_affine[1]), float(a_affine[0]),
                                                                            float(b_affine[1]), float(b_affine[0])),
@@ -92,10 +107,10 @@ class GemmF32:
         lib = hip.load()
         assert lib.pcv_f32_job_size() == struct.calcsize(self.FMT)
         self.groups = []
-        for vec in (True, False):
+        for vec in (2, 1, 0):
             recs, first = [], 0
             for j in self.jobs:
-                if bool(j["apow"] & 16) != vec:
+                if j["kind"] != vec:
                     continue
                 recs.append((_addr(j["A"]), _addr(j["B"]), _addr(j["C"]), _addr(j["ks"]), _addr(j["R"]),
                              _addr(j["Cb"]), _addr(j["ad"]), _addr(j["ci"]), _addr(j["co"]), j["M"], j["N"], j["K"],
@@ -210,7 +225,9 @@ class NewtonRoot:
             for it in self.items:
                 cin, cout = it["conv"][i:i + 1], it["conv"][i + 1:i + 2]
                 M, X = it["M"], it["X"]
-                kw = dict(conv_in=cin, conv_tol=self.tol)
+                # every iterate is a polynomial in A, stored exactly symmetric (sym jobs mirror their
+                # upper triangle), so each right operand is read along k as its own transpose (tb)
+                kw = dict(conv_in=cin, conv_tol=self.tol, sym=True, tb=True)
                 l1.add(X[cur], M[cur], X[nxt], b_affine=T, **kw)                              # X' = X T
                 if self.p == 1:
                     l1.add(M[cur], M[cur], M[nxt], a_affine=T, conv_out=cout, **kw)           # M' = T M

@@ -102,8 +102,8 @@ class Shampoo(GradientTransformation):
         pmat, left, final = GemmF32(), GemmF32(), GemmF32()
         for s in st.mats:
             g, p = store.grads[s.name], store.params[s.name]
-            gram.add(g, g, s.L, tb=True, beta=1.0, alpha_dev=gscale, apow=2)
-            gram.add(g, g, s.R, ta=True, beta=1.0, alpha_dev=gscale, apow=2)
+            gram.add(g, g, s.L, tb=True, beta=1.0, alpha_dev=gscale, apow=2, sym=True)
+            gram.add(g, g, s.R, ta=True, beta=1.0, alpha_dev=gscale, apow=2, sym=True)
             if newton is not None:
                 # fast path + exact fallback: a matrix whose Newton chain does not converge (fp32
                 # rounding can leave L + eps I indefinite once kappa >~ 1e7) takes a cold Jacobi eigh
@@ -111,7 +111,7 @@ class Shampoo(GradientTransformation):
                 for M, Pm, U in ((s.L, s.PL, s.UL), (s.R, s.PR, s.UR)):
                     nt = newton.add(M, Pm, self.eps)
                     e = eig.add(M, U, shift=self.eps, want_pow=True, skip=nt["status"])
-                    pmat.add(U, U, Pm, tb=True, kscale=e["wpow"], conv_in=nt["status"], conv_tol=0.5)
+                    pmat.add(U, U, Pm, tb=True, kscale=e["wpow"], conv_in=nt["status"], conv_tol=0.5, sym=True)
             else:
                 w1.add(s.L, s.UL, s.TL)
                 w1.add(s.R, s.UR, s.TR)

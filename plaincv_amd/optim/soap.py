@@ -92,8 +92,8 @@ class Soap(GradientTransformation):
         rep1, rep2 = GemmF32(), GemmF32()
         for s in st.mats:
             g, p = store.grads[s.name], store.params[s.name]
-            gram.add(g, g, s.L, tb=True, alpha=1.0 - self.sb2, beta=self.sb2, alpha_dev=gscale, apow=2)
-            gram.add(g, g, s.R, ta=True, alpha=1.0 - self.sb2, beta=self.sb2, alpha_dev=gscale, apow=2)
+            gram.add(g, g, s.L, tb=True, alpha=1.0 - self.sb2, beta=self.sb2, alpha_dev=gscale, apow=2, sym=True)
+            gram.add(g, g, s.R, ta=True, alpha=1.0 - self.sb2, beta=self.sb2, alpha_dev=gscale, apow=2, sym=True)
             init.add(s.L, s.QL)
             init.add(s.R, s.QR)
             rot1.add(s.QL, g, s.T1, ta=True, alpha_dev=gscale, apow=1)

@@ -486,11 +486,14 @@ def test_transpose_batch(dev):
         assert torch.equal(dst, src.t())
 
 
+@pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("B,D,Kc,rate", [(64, 128, 200, 0.1), (4, 64, 10, 0.0), (33, 96, 256, 0.3), (1, 32, 1, 0.0)])
-def test_vit_head_fused(dev, B, D, Kc, rate):
+def test_vit_head_fused(dev, B, D, Kc, rate, split):
     """csrc/vit_head.hip vs torch fp32 on the same bf16-rounded GEMM operands: LayerNorm of strided cls
     rows, logits, CE metrics, dlogits, the head bias / LN parameter gradients, dx and the dropout-VJP
-    bf16 rows (dropout bits from oracle.rng at the flat index (b * T) * D + c)."""
+    bf16 rows (dropout bits from oracle.rng at the flat index (b * T) * D + c).  split: one
+    workgroup per 16 rows with the last-workgroup reduction; a second launch on the same workspace
+    (ticket reset by the kernel) reproduces the first bit for bit."""
     from oracle import rng
     from plaincv_amd import kernels as K
     T = 5
@@ -513,9 +516,19 @@ def test_vit_head_fused(dev, B, D, Kc, rate):
     DYM = torch.zeros(B * T, D, dtype=torch.bfloat16, device=dev)
     gs, gc, gb = torch.full((D,), 0.5, device=dev), torch.full((D,), -0.25, device=dev), torch.full((Kc,), 1.0, device=dev)
     seed = torch.tensor([99], dtype=torch.int32, device=dev)
-    K.vit_head(x, s, c, W, bias, labels, yf, logits, met, grad_scale=1.0 / B, dlogits=dl, dlogits_b=dlb,
-               dx=DX.view(B, T * D)[:, :D], dscale=gs, dbias=gc, dym=DYM.view(B, T * D)[:, :D], drop_rate=rate,
-               seed=seed, site=13, row_stride=T, dhead_bias=gb)
+    work = K.vit_head_work(B, D, Kc, dev) if split else None
+
+    def run():
+        K.vit_head(x, s, c, W, bias, labels, yf, logits, met, grad_scale=1.0 / B, dlogits=dl, dlogits_b=dlb,
+                   dx=DX.view(B, T * D)[:, :D], dscale=gs, dbias=gc, dym=DYM.view(B, T * D)[:, :D], drop_rate=rate,
+                   seed=seed, site=13, row_stride=T, dhead_bias=gb, work=work)
+    run()
+    if split:
+        first = [t.clone() for t in (met, gs, gc, gb, DX, DYM, dl)]
+        gs.fill_(0.5), gc.fill_(-0.25), gb.fill_(1.0)
+        run()
+        for a, b in zip(first, (met, gs, gc, gb, DX, DYM, dl)):
+            assert torch.equal(a, b)
     torch.cuda.synchronize()
     # torch reference with the same bf16 operand rounding
     xr = x.clone().requires_grad_(True)

@@ -98,6 +98,84 @@ def test_gemm_f32_split_k(dev, M, N, K, ks, ta, tb):
         GemmF32().add(a, b, c, ta=bool(ta), tb=bool(tb), beta=0.0, ksplit=ks)
 
 
+@pytest.mark.parametrize("n,K", [(64, 64), (200, 77), (384, 384), (37, 300)])
+def test_gemm_f32_symmetric_jobs(dev, n, K):
+    """sym jobs (upper-triangle tiles + mirror): G G^T with beta / bf16 copy, a product of two
+    commuting polynomials of one symmetric matrix with affine operands, and an unsplit
+    non-symmetric job in the same launch; results exactly symmetric"""
+    from plaincv_amd.optim.precond import GemmF32
+    g = torch.Generator().manual_seed(n + K)
+    a = torch.randn(n, K, generator=g).to(dev)
+    s0 = torch.randn(n, n, generator=g)
+    s0 = (s0 + s0.t()).to(dev)
+    c1 = s0.clone()
+    c1b = torch.zeros(n, n, dtype=torch.bfloat16, device=dev)
+    m = (a @ a.t() / K).contiguous()
+    c2 = torch.full((n, n), 7.0, device=dev)
+    x, y = torch.randn(n, 33, generator=g).to(dev), torch.randn(33, 20, generator=g).to(dev)
+    c3 = torch.zeros(n, 20, device=dev)
+    plan = GemmF32().add(a, a, c1, tb=True, alpha=0.3, beta=0.9, cb=c1b, sym=True)
+    plan.add(m, m, c2, a_affine=(-0.25, 1.25), b_affine=(-0.25, 1.25), sym=True)     # T^2, T = 1.25 I - m/4
+    plan.add(x, y, c3)
+    tl = (n + 31) // 32 if plan.jobs[0]["kind"] == 2 else (n + 63) // 64
+    assert plan.jobs[0]["tiles"] == tl * (tl + 1) // 2
+    plan.finalize(dev).run()
+    torch.cuda.synchronize()
+    A, S0 = a.double(), s0.double()
+    ref1 = 0.3 * A @ A.t() + 0.9 * S0
+    T = 1.25 * torch.eye(n, dtype=torch.float64, device=dev) - 0.25 * m.double()
+    ref2 = T @ T
+    for c, ref, scale in ((c1, ref1, (A.abs() @ A.abs().t()).max().item() + S0.abs().max().item()),
+                          (c2, ref2, (T.abs() @ T.abs()).max().item())):
+        assert torch.equal(c, c.t())
+        assert (c.double() - ref).abs().max().item() <= 2e-5 * scale
+    assert torch.equal(c1b, c1.to(torch.bfloat16))
+    assert (c3.double() - x.double() @ y.double()).abs().max().item() < 1e-4
+    with pytest.raises(ValueError):
+        GemmF32().add(x, y, c3, sym=True)
+
+
+@pytest.mark.parametrize("small", [True, False])
+def test_gemm_f32_small_jobs(dev, small):
+    """The K-split 32x32 kernel (ta 0, tb 1, n, K <= 512) vs the 64x64 kernel, both vs fp64: ragged
+    edges (n 100, K 36), affine operands on both sides, alpha_dev^2, beta C + rscale R, bf16 copy,
+    sym, conv_in skip and conv_out = max|C - I|"""
+    from plaincv_amd.optim.precond import GemmF32
+    g = torch.Generator().manual_seed(17)
+    plan, refs = GemmF32(small=small), []
+    adev = torch.tensor([0.8], device=dev)
+    for (M, N, K) in [(100, 36, 36), (256, 256, 256), (128, 200, 512), (4, 8, 4)]:
+        a = torch.randn(M, K, generator=g).to(dev)
+        b = torch.randn(N, K, generator=g).to(dev)
+        c = torch.randn(M, N, generator=g).to(dev)
+        r = torch.randn(M, N, generator=g).to(dev)
+        cb = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+        ref = 0.5 * 0.64 * a.double() @ b.double().t() + 0.25 * c.double() - 0.75 * r.double()
+        plan.add(a, b, c, tb=True, alpha=0.5, alpha_dev=adev, apow=2, beta=0.25, r=r, rscale=-0.75, cb=cb)
+        refs.append((c, ref, cb, (a.double().abs() @ b.double().abs().t()).max().item() + 1.0))
+    n = 136
+    s = torch.randn(n, n, generator=g)
+    s = ((s + s.t()) / 40).to(dev)
+    t2, conv = torch.zeros(n, n, device=dev), torch.zeros(1, device=dev)
+    plan.add(s, s, t2, tb=True, a_affine=(-0.25, 1.25), b_affine=(-0.25, 1.25), sym=True, conv_out=conv)
+    T = 1.25 * torch.eye(n, dtype=torch.float64, device=dev) - 0.25 * s.double()
+    refs.append((t2, T @ T, None, (T.abs() @ T.abs()).max().item()))
+    skipped = torch.full((8, 8), 3.0, device=dev)
+    plan.add(s[:8, :8].contiguous(), s[:8, :8].contiguous(), skipped, tb=True, conv_in=torch.zeros(1, device=dev),
+             conv_tol=1e-6)
+    assert all(j["kind"] == (2 if small else 1) for j in plan.jobs)
+    plan.finalize(dev).run()
+    torch.cuda.synchronize()
+    for c, ref, cb, scale in refs:
+        assert (c.double() - ref).abs().max().item() <= 2e-5 * scale, (c.shape, small)
+        if cb is not None:
+            assert torch.equal(cb, c.to(torch.bfloat16))
+    assert torch.equal(t2, t2.t())
+    want = (t2.double() - torch.eye(n, dtype=torch.float64, device=dev)).abs().max().item()
+    assert abs(conv.item() - want) <= 1e-6 * max(1.0, want)
+    assert (skipped == 3.0).all()
+
+
 def test_wgrad_f32_grouped(dev):
     """row-panel weight-gradient launch (csrc/gemm_f32.hip): several C += A^T B jobs with K = 16448
     token rows, split-K slices added with atomics, vs fp64"""
