@@ -406,7 +406,8 @@ int pcv_chunk_size(void);
  * vec = 2: small jobs (M, N, K <= 512, ta = 0, tb = 1, float4-aligned, no kscale / split-K) on
  *          32x32 tiles with K split over the workgroup's waves (tiles_n / first_tile in 32-tiles). */
 int pcv_f32_job_size(void);
-int pcv_gemm_f32_grouped(const void* jobs, int njobs, int64_t total_tiles, int vec, void* stream);
+int pcv_gemm_f32_grouped(const void* jobs, int njobs, int64_t total_tiles, int vec, const int64_t* firsts_host,
+                         void* stream);   /* firsts_host (optional): the jobs' first_tile values, host copy */
 /* Shampoo inverse p-th root (shampoo.py:195-215) by the coupled Newton iteration on the grouped
  * GEMM above: pcv_newton_init (record {L, M0, X0, conv[iters], X1, P, ldl, n, shift}; M0 = zA,
  * X0 = z^(1/p) I with A = L + shift I, z = (1+p)/(2||A||_F)), the per-iteration GEMM jobs, and

@@ -50,6 +50,24 @@ struct F32Job {
 static_assert(sizeof(F32Job) == 32 * 8, "F32Job layout");
 
 constexpr int FG_T = 64, FG_K = 128;
+
+// First tile of each job, passed by value in the kernel arguments when the launch has at most
+// FG_KA_JOBS jobs: the job search is then scalar loads of the (already fetched) argument block
+// instead of a dependent global round trip + LDS gather + barrier (n = 0: search the table).
+constexpr int FG_KA_JOBS = 62;
+struct F32Firsts {
+  int n, pad;
+  int first[FG_KA_JOBS];
+};
+__device__ __forceinline__ int f32_job_of(const F32Firsts& f, int bid) {
+  int lo = 0, hi = f.n - 1;   // first[0] == 0 <= bid
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (f.first[mid] <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
 constexpr int FG_JOB_CAP = 1024;    // jobs whose first blocks are searched in LDS
 constexpr int LD_XK = FG_K + 4;     // k-contiguous image [x][k]: 16 rows x 16 B of a read hit 64 banks
 constexpr int FG_NPER = FG_T * FG_K / 256;   // elements per thread per operand per k-chunk (32)
@@ -186,14 +204,16 @@ __device__ __forceinline__ void f32_tile(const F32Job& jb, int m0, int n0, int k
 }
 
 template <bool VEC>
-__global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __restrict__ jobs, int njobs, int total) {
+__global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __restrict__ jobs, int njobs, int total,
+                                                                const F32Firsts firsts) {
   __shared__ __attribute__((aligned(16))) float As[FG_LDS_FLOATS];
   __shared__ __attribute__((aligned(16))) float Bs[FG_LDS_FLOATS];
   __shared__ int ft[FG_JOB_CAP];
   const int bid = pcv_xcd_tile();
   if (bid >= total) return;
-  const int j = pcv_find_job<int64_t>(jobs, njobs, (int)sizeof(F32Job), (int)offsetof(F32Job, first_tile), ft,
-                                      FG_JOB_CAP, bid);
+  const int j = firsts.n ? f32_job_of(firsts, bid)
+                         : pcv_find_job<int64_t>(jobs, njobs, (int)sizeof(F32Job), (int)offsetof(F32Job, first_tile),
+                                                 ft, FG_JOB_CAP, bid);
   const F32Job jb = jobs[j];
   if (jb.conv_in && *jb.conv_in <= (float)jb.conv_tol) return;
   int t = bid - (int)jb.first_tile;
@@ -292,23 +312,27 @@ __global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __r
 
 // Small-matrix variant (n, K <= 512: the Kronecker factors of the ViT, and every Newton iterate):
 // a 64 x 64 tile's K-long MFMA chain is the launch's critical path there (32 K cycles per wave for
-// a few hundred tiles on 256 CUs), so the tile shrinks to 32 x 32 and the workgroup's four waves
-// split K: wave w sums its quarter of K for the whole tile straight from registers -- both
+// a few hundred tiles on 256 CUs), so the tile shrinks to 32 x 32 and the workgroup's eight waves
+// split K: wave w sums its eighth of K for the whole tile straight from registers -- both
 // operands stored along k (A [M][K], B [N][K]: ta = 0, tb = 1, which a symmetric B satisfies as
 // stored), one float4 per lane per 16-long k slab (contraction index 4 g + s inside a slab, the
 // same permutation for both operands), all of a batch's loads issued before its first MFMA -- and
-// the four partial tiles are summed in LDS in wave order (deterministic).  Same epilogue as above
+// the eight partial tiles are summed in LDS in wave order (deterministic).  Same epilogue as above
 // (affine operands, alpha_dev, beta C, R, Cb, sym, conv_in / conv_out); no kscale, no split-K.
 constexpr int FS_T = 32, FS_SLABS = 4;   // tile edge; 16-long k slabs per load batch
 constexpr int FS_LD = FS_T + 1;
+constexpr int FS_WAVES = 8;              // K split over the workgroup's waves
+constexpr int FS_THREADS = 64 * FS_WAVES;
 
-__global__ __launch_bounds__(256) void gemm_f32_small_kernel(const F32Job* __restrict__ jobs, int njobs, int total) {
-  __shared__ float part[4][FS_T][FS_LD];
+__global__ __launch_bounds__(FS_THREADS) void gemm_f32_small_kernel(const F32Job* __restrict__ jobs, int njobs,
+                                                                    int total, const F32Firsts firsts) {
+  __shared__ float part[FS_WAVES][FS_T][FS_LD];
   __shared__ int ft[FG_JOB_CAP];
   const int bid = pcv_xcd_tile();
   if (bid >= total) return;
-  const int j = pcv_find_job<int64_t>(jobs, njobs, (int)sizeof(F32Job), (int)offsetof(F32Job, first_tile), ft,
-                                      FG_JOB_CAP, bid);
+  const int j = firsts.n ? f32_job_of(firsts, bid)
+                         : pcv_find_job<int64_t>(jobs, njobs, (int)sizeof(F32Job), (int)offsetof(F32Job, first_tile),
+                                                 ft, FG_JOB_CAP, bid);
   const F32Job& jb = jobs[j];
   if (jb.conv_in && *jb.conv_in <= (float)jb.conv_tol) return;
   const int tiles_n = (int)jb.tiles_n;
@@ -329,7 +353,7 @@ __global__ __launch_bounds__(256) void gemm_f32_small_kernel(const F32Job* __res
   const float* __restrict__ A = jb.A;
   const float* __restrict__ B = jb.B;
   // this wave's K range: whole 16-long slabs
-  const int kq = (((K + 3) / 4) + 15) & ~15;
+  const int kq = (((K + FS_WAVES - 1) / FS_WAVES) + 15) & ~15;
   const int kb = w * kq, ke = min(K, kb + kq);
   f32x4 acc[2][2];
 #pragma unroll
@@ -350,9 +374,11 @@ __global__ __launch_bounds__(256) void gemm_f32_small_kernel(const F32Job* __res
         fb[sl][a] = (kin && col < N) ? *(const float4*)(B + col * ldb + k) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
-    if (aff) {   // op(X) = mul X + diag I on the in-range entries
+    // slab by slab (the loads retire in issue order, so slab 0's MFMAs start under the later loads)
 #pragma unroll
-      for (int sl = 0; sl < FS_SLABS; ++sl) {
+    for (int sl = 0; sl < FS_SLABS; ++sl) {
+      if (k0 + 16 * sl >= ke) break;
+      if (aff) {   // op(X) = mul X + diag I on the in-range entries
         const int k = k0 + 16 * sl + 4 * g;
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
@@ -366,10 +392,6 @@ __global__ __launch_bounds__(256) void gemm_f32_small_kernel(const F32Job* __res
           }
         }
       }
-    }
-#pragma unroll
-    for (int sl = 0; sl < FS_SLABS; ++sl) {
-      if (k0 + 16 * sl >= ke) break;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -392,10 +414,11 @@ __global__ __launch_bounds__(256) void gemm_f32_small_kernel(const F32Job* __res
     alpha *= (jb.apow & 15) == 2 ? sc * sc : sc;
   }
   const float beta = (float)jb.beta, rscale = (float)jb.rscale;
-  const int lr = tid >> 3, lc = (tid & 7) * 4, row = m0 + lr;
-  float cr[4];
+  constexpr int PER = FS_T * FS_T / FS_THREADS;          // outputs per thread (2), consecutive columns
+  const int lr = tid / (FS_T / PER), lc = (tid % (FS_T / PER)) * PER, row = m0 + lr;
+  float cr[PER];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < PER; ++q) {
     const int col = n0 + lc + q;
     const bool in = row < M && col < N;
     float cv = 0.f, rv = 0.f;
@@ -405,10 +428,13 @@ __global__ __launch_bounds__(256) void gemm_f32_small_kernel(const F32Job* __res
   }
   float dev_max = 0.f;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < PER; ++q) {
     const int col = n0 + lc + q;
     if (row < M && col < N && (!sym || row <= col)) {
-      const float v = alpha * (((part[0][lr][lc + q] + part[1][lr][lc + q]) + part[2][lr][lc + q]) + part[3][lr][lc + q]) + cr[q];
+      float sum = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < FS_WAVES; ++ww) sum += part[ww][lr][lc + q];   // wave order: deterministic
+      const float v = alpha * sum + cr[q];
       jb.C[(int64_t)row * jb.ldc + col] = v;
       if (jb.Cb) jb.Cb[(int64_t)row * jb.ldcb + col] = f2bf(v);
       if (sym && row != col) {
@@ -440,10 +466,13 @@ struct NewtonJob {
 };
 static_assert(sizeof(NewtonJob) == 10 * 8, "NewtonJob layout");
 
+// grid (NI_SPLIT, jobs): every workgroup of a matrix forms ||A||_F itself (the matrix is a few
+// hundred KB, L2-resident after the first reader) and writes its 1/NI_SPLIT of the rows of M0, X0.
+constexpr int NI_SPLIT = 16;
 __global__ __launch_bounds__(1024) void newton_init_kernel(const NewtonJob* __restrict__ jobs, float p, int iters,
                                                            float kappa_max) {
   __shared__ float red[16];
-  const NewtonJob jb = jobs[blockIdx.x];
+  const NewtonJob jb = jobs[blockIdx.y];
   const int n = (int)jb.n, ldl = (int)jb.ldl;
   const float sh = (float)jb.shift;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -461,7 +490,8 @@ __global__ __launch_bounds__(1024) void newton_init_kernel(const NewtonJob* __re
   const float fro = sqrtf(s);
   const float z = (1.f + p) / (2.f * fro);
   const float xz = powf(z, 1.f / p);
-  for (int r = w; r < n; r += 16) {
+  const int rows = (n + NI_SPLIT - 1) / NI_SPLIT, rb = blockIdx.x * rows, re = min(n, rb + rows);
+  for (int r = rb + w; r < re; r += 16) {
     const float* row = jb.L + (int64_t)r * ldl;
     float* m0 = jb.M0 + (int64_t)r * n;
     float* x0 = jb.X0 + (int64_t)r * n;
@@ -471,8 +501,9 @@ __global__ __launch_bounds__(1024) void newton_init_kernel(const NewtonJob* __re
       x0[c] = r == c ? xz : 0.f;
     }
   }
-  for (int i = threadIdx.x; i <= iters; i += 1024)
-    jb.conv[i] = i > 0 ? 0.f : ((fro <= kappa_max * sh && fro == fro) ? 1.f : 0.f);
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i <= iters; i += 1024)
+      jb.conv[i] = i > 0 ? 0.f : ((fro <= kappa_max * sh && fro == fro) ? 1.f : 0.f);
 }
 
 // P = the X of the first converged iteration (X buffers ping-pong: iteration i writes X[(i+1)&1]);
@@ -848,7 +879,7 @@ extern "C" int pcv_newton_job_size(void) { return (int)sizeof(NewtonJob); }
 extern "C" int pcv_newton_init(const void* jobs_dev, int njobs, float p, int iters, float kappa_max,
                                void* stream) {
   if (!jobs_dev || njobs <= 0 || p <= 0.f || iters <= 0) return PCV_EINVAL;
-  hipLaunchKernelGGL(newton_init_kernel, dim3(njobs), dim3(1024), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(newton_init_kernel, dim3(NI_SPLIT, njobs), dim3(1024), 0, (hipStream_t)stream,
                      (const NewtonJob*)jobs_dev, p, iters, kappa_max);
   return pcv_launch_status();
 }
@@ -868,19 +899,26 @@ extern "C" int pcv_qr_job_size(void) { return (int)sizeof(QrJob); }
 extern "C" int pcv_sort_job_size(void) { return (int)sizeof(SortJob); }
 extern "C" int pcv_perm_job_size(void) { return (int)sizeof(PermJob); }
 
-extern "C" int pcv_gemm_f32_grouped(const void* jobs_dev, int njobs, int64_t total_tiles, int vec, void* stream) {
+extern "C" int pcv_gemm_f32_grouped(const void* jobs_dev, int njobs, int64_t total_tiles, int vec,
+                                    const int64_t* firsts_host, void* stream) {
   if (!jobs_dev || njobs <= 0 || total_tiles <= 0 || total_tiles >= (1ll << 31)) return PCV_EINVAL;
   const dim3 grid((unsigned)pcv_xcd_grid(total_tiles));
   const int total = (int)total_tiles;
+  F32Firsts f{};
+  if (firsts_host && njobs <= FG_KA_JOBS) {
+    if (firsts_host[0] != 0) return PCV_EINVAL;
+    f.n = njobs;
+    for (int i = 0; i < njobs; ++i) f.first[i] = (int)firsts_host[i];
+  }
   if (vec == 2)
-    hipLaunchKernelGGL(gemm_f32_small_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const F32Job*)jobs_dev, njobs,
-                       total);
+    hipLaunchKernelGGL(gemm_f32_small_kernel, grid, dim3(FS_THREADS), 0, (hipStream_t)stream, (const F32Job*)jobs_dev,
+                       njobs, total, f);
   else if (vec)
     hipLaunchKernelGGL(gemm_f32_grouped_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream,
-                       (const F32Job*)jobs_dev, njobs, total);
+                       (const F32Job*)jobs_dev, njobs, total, f);
   else
     hipLaunchKernelGGL(gemm_f32_grouped_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream,
-                       (const F32Job*)jobs_dev, njobs, total);
+                       (const F32Job*)jobs_dev, njobs, total, f);
   return pcv_launch_status();
 }
 

@@ -123,7 +123,7 @@ SIGNATURES = {
     "pcv_qr_job_size": [],
     "pcv_sort_job_size": [],
     "pcv_perm_job_size": [],
-    "pcv_gemm_f32_grouped": [P, I32, I64, I32, P],
+    "pcv_gemm_f32_grouped": [P, I32, I64, I32, P, P],
     "pcv_eigh_log_floats": [I64, I32],
     "pcv_eigh_jacobi": [P, I32, I32, I32, F32, F32, I32, F32, F32, P],
     "pcv_eigh_vectors": [P, I32, I32, P],

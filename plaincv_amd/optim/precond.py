@@ -4,6 +4,7 @@ Each plan packs its job records once (plain 8-byte fields: pointers, int64, doub
 device tensor, so a step is a fixed sequence of stream-ordered launches with no host work
 beyond the launch itself.  Shapes are validated here, before anything reaches a kernel.
 """
+import ctypes
 import os
 import struct
 
@@ -109,9 +110,11 @@ class GemmF32:
         self.groups = []
         for vec in (2, 1, 0):
             recs, first = [], 0
+            firsts = []
             for j in self.jobs:
                 if j["kind"] != vec:
                     continue
+                firsts.append(first)
                 recs.append((_addr(j["A"]), _addr(j["B"]), _addr(j["C"]), _addr(j["ks"]), _addr(j["R"]),
                              _addr(j["Cb"]), _addr(j["ad"]), _addr(j["ci"]), _addr(j["co"]), j["M"], j["N"], j["K"],
                              j["lda"], j["ldb"], j["ldc"], j["ldr"], j["ldcb"], j["ta"], j["tb"], j["apow"],
@@ -119,13 +122,16 @@ class GemmF32:
                             + (j["tol"],))
                 first += j["tiles"]
             if recs:
-                self.groups.append((_pack(recs, self.FMT).to(device), len(recs), first, int(vec)))
+                fh = (ctypes.c_int64 * len(firsts))(*firsts)       # job search from the kernel arguments
+                self._keep = getattr(self, "_keep", []) + [fh]
+                self.groups.append((_pack(recs, self.FMT).to(device), len(recs), first, int(vec),
+                                    ctypes.cast(fh, ctypes.c_void_p)))
         return self
 
     def run(self):
         s = stream_ptr()
-        for dev, n, total, vec in self.groups:
-            hip.call("pcv_gemm_f32_grouped", ptr(dev), n, total, vec, s)
+        for dev, n, total, vec, fh in self.groups:
+            hip.call("pcv_gemm_f32_grouped", ptr(dev), n, total, vec, fh, s)
 
 
 class WgradF32:
