@@ -356,7 +356,8 @@ int pcv_grad_scale(const float* g, const void* chunks, int nchunks, float* parti
 int pcv_step_bump(int* step, void* stream);
 /* Muon (optax.contrib.muon scale_by_muon): momentum + nesterov + Frobenius normalisation
  * into NS workspaces, and the shape-scaled weight-decayed update; descriptors are
- * pcv_muon_mat_size()-byte records (see optim.hip MuonMat). */
+ * pcv_muon_mat_size()-byte records (see optim_types.h MuonMat; norm2 is a zeroed double: the
+ * per-block partial sums add exactly in fp64, so the result does not depend on atomic order). */
 int pcv_muon_prep(const void* mats, int nmats, int nnorm, int64_t max_elems, float beta, int nesterov, float eps,
                   const int* step, const float* gscale, void* stream);
 int pcv_muon_apply(const void* mats, int nmats, int64_t max_elems, float lr, float wd, int shape_scale,

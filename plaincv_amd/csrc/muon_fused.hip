@@ -306,7 +306,7 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
                                                              float ns_c, int ns_steps) {
   extern __shared__ __attribute__((aligned(16))) char smem_m[];
   const MuonMat M = mats[blockIdx.x];
-  ns_core(M, 1.f / (sqrtf(*M.norm2) + eps), ns_a, ns_b, ns_c, ns_steps, smem_m);
+  ns_core(M, 1.f / ((float)sqrt(*M.norm2) + eps), ns_a, ns_b, ns_c, ns_steps, smem_m);
   // X_ns -> xo [rx][ldx] (real rows/columns only)
   const bf16* X = reinterpret_cast<const bf16*>(smem_m);
   const int rx = (int)(M.rows < M.cols ? M.rows : M.cols), cx = (int)(M.rows < M.cols ? M.cols : M.rows);
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(MF_THREADS) void muon_step_kernel(MuonStepArgs a) {
     // muon_apply_kernel (both wide launches: one CU moves only ~10 B/cycle, so the per-matrix
     // streaming of prep / apply belongs on many CUs, not on the NS workgroup)
     const MuonMat M = a.mats[blockIdx.x];
-    ns_core(M, 1.f / (sqrtf(*M.norm2) + a.mh.eps), a.ns_a, a.ns_b, a.ns_c, a.ns_steps, smem_m);
+    ns_core(M, 1.f / ((float)sqrt(*M.norm2) + a.mh.eps), a.ns_a, a.ns_b, a.ns_c, a.ns_steps, smem_m);
     const bf16* X = reinterpret_cast<const bf16*>(smem_m);
     const int rx = (int)(M.rows < M.cols ? M.rows : M.cols), cx = (int)(M.rows < M.cols ? M.cols : M.rows);
     const int ldx = (int)M.ldx;

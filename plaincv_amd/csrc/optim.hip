@@ -150,13 +150,13 @@ __global__ __launch_bounds__(256) void muon_prep_kernel(const MuonMat* mats, Muo
     s += xh * xh;
   }
   s = block_sum(s, red);
-  if (threadIdx.x == 0) atomicAdd(M.norm2, s);
+  if (threadIdx.x == 0) atomicAdd(M.norm2, (double)s);
 }
 
 __global__ __launch_bounds__(256) void muon_norm_kernel(const MuonMat* mats, float eps) {
   const MuonMat M = mats[blockIdx.y];
   const int64_t n = M.rows * M.cols;
-  const float inv = 1.f / (sqrtf(*M.norm2) + eps);
+  const float inv = 1.f / ((float)sqrt(*M.norm2) + eps);
   const int cx = (int)(M.rows > M.cols ? M.rows : M.cols);
   for (int i = blockIdx.x * 256 + threadIdx.x; i < (int)n; i += gridDim.x * 256) {
     const int q = i / cx;
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void muon_apply_kernel(const MuonMat* mats, Mu
   const MuonMat M = mats[blockIdx.y];
   // the matrix's sum of squares was last read by the NS normalisation: reset it for the next step
   // here instead of a separate fill launch (muon_prep accumulates into it with atomics)
-  if (blockIdx.x == 0 && threadIdx.x == 0) *M.norm2 = 0.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *M.norm2 = 0.0;
   const int64_t n = M.rows * M.cols;
   const bool tr = M.rows > M.cols;
   const float ss = h.shape_scale > 0.f ? sqrtf(fmaxf(1.f, (float)M.cols / (float)M.rows)) : 1.f;

@@ -12,7 +12,8 @@ struct MuonMat {
   float* x32;                  // workspace [r', c'] (transposed if rows > cols)
   bf16* xb;                    // bf16 copy of the normalised X (NS input)
   const bf16* xo;              // NS output [r', c'] (bf16)
-  float* norm2;                // sum of squares of x32
+  double* norm2;               // sum of squares of x32 (fp64: the per-block float partials add exactly,
+                               // so the atomic order cannot change the result -- replicas stay bit-identical)
 };
 
 struct MuonHyper {

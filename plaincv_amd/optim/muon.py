@@ -103,7 +103,7 @@ class Muon(GradientTransformation):
         st.groups = [g for g in gl if not g.fused] + [g for g in gl if g.fused]
         st.n_general = sum(len(g.names) for g in st.groups if not g.fused)
         st.n_fused = len(routed) - st.n_general
-        st.norm2 = torch.zeros(max(1, len(routed)), dtype=torch.float32, device=dev)
+        st.norm2 = torch.zeros(max(1, len(routed)), dtype=torch.float64, device=dev)   # fp64: order-free sums
         st.ticket = torch.zeros(1, dtype=torch.int32, device=dev)   # last-block counter of the one-launch step
         # the one-launch step moves 4 consecutive columns per lane (16-B accesses of p, g, mu)
         st.vec4 = all(store.params[k].shape[1] % 4 == 0 and store.leaf(k).offset % 4 == 0 and
@@ -123,7 +123,7 @@ class Muon(GradientTransformation):
                 base = [store.flat.data_ptr() + off * 4, store.grad_flat.data_ptr() + off * 4,
                         mu.data_ptr() + off * 4, store.shadow.data_ptr() + off * 2]
                 tail = [rows, cols, leaf.strides[0], g.ldx, g.x32[j].data_ptr(), g.xb[j].data_ptr(),
-                        xo.data_ptr(), st.norm2.data_ptr() + idx * 4]
+                        xo.data_ptr(), st.norm2.data_ptr() + idx * 8]
                 recs_apply.append(base + [0] + tail)
                 recs_upd.append(base + [st.upd.data_ptr() + off * 4] + tail)
                 idx += 1
