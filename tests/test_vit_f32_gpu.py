@@ -201,7 +201,12 @@ def test_graphed_step_matches_eager_host_driven(dev, optim, mlp):
         assert sa.opt_state.base.host_step == sb.opt_state.base.host_step == 3
     # per-leaf movement (bias column sums use fp32 atomics, so bit equality is not expected; the
     # attention key biases are excluded: their true gradient is exactly 0, so both runs feed the
-    # Adam branch pure rounding noise, which it normalises into full-size steps of random sign)
+    # Adam branch pure rounding noise, which it normalises into full-size steps of random sign).
+    # Bound: SOAP's init eigh of these rank-deficient 4-image Gram matrices turns the two runs'
+    # atomics noise into up to ~4e-3 of a leaf's movement (measured); the failures this test is
+    # for -- a warm-up that leaves host_step advanced (SOAP's first step is then not the zero
+    # update) or a captured host-driven eigh -- move leaves by O(1) of their movement
+    tol = 2e-2 if name == "soap" else 1e-3
     a, b = sa.params.to_dict(), sb.params.to_dict()
     bad = {}
     for k in b:
@@ -209,6 +214,6 @@ def test_graphed_step_matches_eager_host_driven(dev, optim, mlp):
             continue
         p0 = sb.params._view(flat0, sb.params.leaf(k)).cpu()
         e = rel(a[k] - p0, b[k] - p0)
-        if e > 1e-3:
+        if e > tol:
             bad[k] = e
     assert not bad, bad
