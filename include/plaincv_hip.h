@@ -91,11 +91,17 @@ int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, int64_t N, in
  * resets A after reading it (the fold of col_reps replica rows, below).
  * plan: host descriptors -> device plan buffer (pcv_gemm_grouped_plan_size(n) bytes, caller
  * owned, synchronous copy); run: stream-ordered, graph-capturable.  No two descriptors of a
- * plan may share a C. */
+ * plan may share a C.  sk_ws (optional, pcv_gemm_grouped_ws_floats(...) floats, 16-B aligned):
+ * split-K slices write their partial tiles there with plain stores instead of fp32 atomics into C,
+ * and pcv_gemm_grouped_fold (after run, fold_blocks from the plan) adds them to C in slice order --
+ * deterministic and free of contended atomics. */
 int64_t pcv_gemm_grouped_plan_size(int n);
 int pcv_gemm_desc_size(void);
-int pcv_gemm_grouped_plan(const void* descs, int n, int tile /* 64 | 128 */, void* plan_dev, int64_t* total_blocks);
+int64_t pcv_gemm_grouped_ws_floats(const void* descs, int n, int tile);
+int pcv_gemm_grouped_plan(const void* descs, int n, int tile /* 64 | 128 */, void* plan_dev, int64_t* total_blocks,
+                          float* sk_ws, int64_t ws_floats, int64_t* fold_blocks);
 int pcv_gemm_grouped_run(const void* plan_dev, int n, int tile /* as planned */, int64_t total_blocks, void* stream);
+int pcv_gemm_grouped_fold(const void* plan_dev, int n, int tile, int64_t fold_blocks, void* stream);
 
 /* ----------------------------------------------------------- attention ----
  * Flash attention on the packed QKV activation (q/k/v = column blocks, head h

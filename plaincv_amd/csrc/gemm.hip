@@ -71,6 +71,10 @@ struct GemmArgs {
   // produces dO): delta[(b H + h) T + t] = <bf16(C[row, h dh : (h+1) dh]), dl_o[row, same]>,
   // row = b T + t -- replaces attn_bwd_delta_kernel
   const bf16* dl_o; int64_t ld_dlo; float* dl_delta; int dl_T, dl_H, dl_dh;
+  // split-K partial tiles (grouped launch with a workspace): slice kz of C tile t writes alpha * its
+  // partial to sk_ws[(t * split_k + kz) * BM * BN ...] with plain stores, and a fold launch adds the
+  // slices to C in slice order -- deterministic, and no contended float atomics
+  float* sk_ws;
 };
 
 __device__ __forceinline__ int64_t col_rep_off(const GemmArgs& g) {
@@ -802,6 +806,17 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
           ct[(rt - rc + (lane >> 4) * 4 + r) * CLD + wc * (BN / 2) + j * 16 + (lane & 15)] = acc[i][j][r];
     }
     __syncthreads();
+    if (g.split_k > 1 && g.sk_ws) {
+      // partial tile -> workspace (16-B plain stores), summed by pcv_gemm_grouped_fold
+      float* part = g.sk_ws + ((int64_t)(tm * g.tiles_n + tn) * g.split_k + kz) * (BM * BN) + (int64_t)rc * BN;
+      for (int idx = threadIdx.x; idx < CH * BN / 4; idx += 256) {
+        const int rr = (idx * 4) / BN, c = (idx * 4) % BN;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ct + rr * CLD + c);
+        *reinterpret_cast<f32x4*>(part + rr * BN + c) = g.alpha * v;
+      }
+      PCV_TREC(4);
+      continue;
+    }
     if (g.split_k > 1) {
       // split-K partial: fp32 atomics shaped as 64 consecutive floats (256 B) per
       // wave-instruction -- the full-rate atomic shape (MI355X_MICROARCH "Global float atomics")
@@ -811,6 +826,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
         const int64_t row = m0 + rc + rr, cl = n0 + c;
         if (row < g.M && cl < g.N) atomicAdd(C + row * g.ldc + cl, g.alpha * ct[rr * CLD + c]);
       }
+      PCV_TREC(4);
       continue;
     }
     if constexpr (LN_TILE) {
@@ -1056,6 +1072,47 @@ __global__ __launch_bounds__(256, (WM * WN >= 64) ? 1 : 2) void gemm_grouped_ker
   gemm_tile<A_KC, B_KC, WM, WN, GroupedStages<WM>::S>(g, local % tiles, 0, local / tiles, false);
 }
 
+// Fold of the split-K workspace: block b -> (GEMM i, C tile t, row group) by fold_prefix (FOLD_BPT
+// blocks per tile); each thread owns 4 consecutive columns of one row and sums that float4 over
+// the slices kz = 0.. in order (8 loads in flight), then C[r][c..c+3] += sum.
+template <int TILE>
+struct FoldCfg {
+  static constexpr int RPB = 256 / (TILE / 4);      // rows per block
+  static constexpr int BPT = TILE / RPB;            // blocks per tile
+};
+template <int TILE>
+__global__ __launch_bounds__(256) void grouped_fold_kernel(const GemmArgs* __restrict__ gs, const int* __restrict__ fprefix,
+                                                           int n) {
+  constexpr int CPR = TILE / 4, RPB = FoldCfg<TILE>::RPB, BPT = FoldCfg<TILE>::BPT;
+  const int b = blockIdx.x / BPT, rg = blockIdx.x % BPT;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (fprefix[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const GemmArgs& g = gs[lo];
+  const int t = b - fprefix[lo];
+  const int tm = t / g.tiles_n, tn = t % g.tiles_n;
+  const int rr = rg * RPB + threadIdx.x / CPR, c = (threadIdx.x % CPR) * 4;
+  const int64_t row = (int64_t)tm * TILE + rr, col = (int64_t)tn * TILE + c;
+  if (row >= g.M || col >= g.N) return;
+  const float* p = g.sk_ws + (int64_t)t * g.split_k * (TILE * TILE) + rr * TILE + c;
+  const int S = g.split_k;
+  f32x4 acc{0.f, 0.f, 0.f, 0.f};
+  int q = 0;
+  for (; q + 8 <= S; q += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(p + (int64_t)(q + u) * TILE * TILE);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; q < S; ++q) acc += *reinterpret_cast<const f32x4*>(p + (int64_t)q * TILE * TILE);
+  float* cp = (float*)g.C + row * g.ldc + col;
+  for (int e = 0; e < 4; ++e)
+    if (col + e < g.N) cp[e] += acc[e];
+}
+
 template <int WM, int WN, int S = GemmStages<WM, WN>::S>
 static constexpr size_t gemm_lds() {   // dynamic LDS of one workgroup (k-tile ring vs epilogue staging)
   constexpr int BM = 32 * WM, BN = 32 * WN;
@@ -1248,17 +1305,41 @@ struct PcvGemmDesc {
   int pad_;
 };
 
-extern "C" int64_t pcv_gemm_grouped_plan_size(int n) {
-  return n <= 0 ? 0 : (int64_t)((n * sizeof(GemmArgs) + 255) / 256 * 256 + (n + 1) * sizeof(int));
+extern "C" int64_t pcv_gemm_grouped_plan_size(int n) {   // GemmArgs[n] | block prefix[n+1] | fold prefix[n+1]
+  return n <= 0 ? 0 : (int64_t)((n * sizeof(GemmArgs) + 255) / 256 * 256 + 2 * (n + 1) * sizeof(int));
 }
 extern "C" int pcv_gemm_desc_size(void) { return (int)sizeof(PcvGemmDesc); }
 
-extern "C" int pcv_gemm_grouped_plan(const void* descs, int n, int tile, void* plan_dev, int64_t* total_blocks) {
+// split-K slices per GEMM descriptor, as the plan computes them
+static int grouped_split(const PcvGemmDesc& e, int64_t* kps_out) {
+  const int split = e.split_k < 1 ? 1 : e.split_k;
+  const int64_t kps = ((e.K + split - 1) / split + 63) / 64 * 64;
+  if (kps_out) *kps_out = kps;
+  return (int)((e.K + kps - 1) / kps);
+}
+
+extern "C" int64_t pcv_gemm_grouped_ws_floats(const void* descs, int n, int tile) {
+  if (n <= 0 || !descs || (tile != 64 && tile != 128)) return -1;
+  const PcvGemmDesc* d = (const PcvGemmDesc*)descs;
+  int64_t need = 0;
+  for (int i = 0; i < n; ++i) {
+    const PcvGemmDesc& e = d[i];
+    if (e.kind != 0 || e.M <= 0 || e.N <= 0 || e.K <= 0) continue;
+    const int sk = grouped_split(e, nullptr);
+    if (sk > 1) need += ((e.M + tile - 1) / tile) * ((e.N + tile - 1) / tile) * (int64_t)sk * tile * tile;
+  }
+  return need;
+}
+
+extern "C" int pcv_gemm_grouped_plan(const void* descs, int n, int tile, void* plan_dev, int64_t* total_blocks,
+                                     float* sk_ws, int64_t ws_floats, int64_t* fold_blocks) {
   if (n <= 0 || !descs || !plan_dev || !total_blocks || (tile != 64 && tile != 128)) return PCV_EINVAL;
+  if (sk_ws && (!fold_blocks || !pcv_aligned16(sk_ws) || ws_floats < pcv_gemm_grouped_ws_floats(descs, n, tile)))
+    return PCV_EINVAL;
   const PcvGemmDesc* d = (const PcvGemmDesc*)descs;
   std::vector<GemmArgs> gs(n);
-  std::vector<int> prefix(n + 1);
-  int64_t tot = 0;
+  std::vector<int> prefix(n + 1), fprefix(n + 1);
+  int64_t tot = 0, ftot = 0, ws_off = 0;
   for (int i = 0; i < n; ++i) {
     const PcvGemmDesc& e = d[i];
     if (e.kind == GROUPED_JOB_COLSUM) {   // rows split into split_k slices of whole 32-row steps
@@ -1273,6 +1354,7 @@ extern "C" int pcv_gemm_grouped_plan(const void* descs, int n, int tile, void* p
       g.split_k = (int)((e.M + g.k_per_split - 1) / g.k_per_split);
       g.tiles_m = 1;
       g.tiles_n = (int)((e.N + 63) / 64);
+      fprefix[i] = (int)ftot;
       prefix[i] = (int)tot;
       tot += (int64_t)g.tiles_n * g.split_k;
       gs[i] = g;
@@ -1287,22 +1369,47 @@ extern "C" int pcv_gemm_grouped_plan(const void* descs, int n, int tile, void* p
     g.alpha = e.alpha; g.beta = 1.f; g.out_f32 = 1; g.res_scale = 1.f;
     g.drop_scale = 1.f; g.glds_ok = 1;
     g.vec_ok = pcv_aligned16(e.C) && (e.ldc % 4 == 0);
-    int split = e.split_k < 1 ? 1 : e.split_k;
-    const int64_t kps = ((e.K + split - 1) / split + 63) / 64 * 64;
-    g.split_k = (int)((e.K + kps - 1) / kps);
+    int64_t kps = 0;
+    g.split_k = grouped_split(e, &kps);
     g.k_per_split = kps;
     g.tiles_m = (int)((e.M + tile - 1) / tile);
     g.tiles_n = (int)((e.N + tile - 1) / tile);
+    fprefix[i] = (int)ftot;
+    if (sk_ws && g.split_k > 1) {   // partials to the workspace, summed by the fold launch
+      g.sk_ws = sk_ws + ws_off;
+      ws_off += (int64_t)g.tiles_m * g.tiles_n * g.split_k * tile * tile;
+      ftot += (int64_t)g.tiles_m * g.tiles_n;
+    }
     prefix[i] = (int)tot;
     tot += (int64_t)g.tiles_m * g.tiles_n * g.split_k;
     gs[i] = g;
   }
   prefix[n] = (int)tot;
+  fprefix[n] = (int)ftot;
   const size_t off = (n * sizeof(GemmArgs) + 255) / 256 * 256;
   hipError_t e = hipMemcpy(plan_dev, gs.data(), n * sizeof(GemmArgs), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy((char*)plan_dev + off, prefix.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy((char*)plan_dev + off + (n + 1) * sizeof(int), fprefix.data(), (n + 1) * sizeof(int),
+                  hipMemcpyHostToDevice);
   *total_blocks = tot;
+  if (fold_blocks) *fold_blocks = ftot;
   return e == hipSuccess ? 0 : (int)e;
+}
+
+extern "C" int pcv_gemm_grouped_fold(const void* plan_dev, int n, int tile, int64_t fold_blocks, void* stream) {
+  if (n <= 0 || !plan_dev || (tile != 64 && tile != 128) || fold_blocks < 0) return PCV_EINVAL;
+  if (fold_blocks == 0) return 0;
+  const size_t off = (n * sizeof(GemmArgs) + 255) / 256 * 256;
+  const GemmArgs* gs = (const GemmArgs*)plan_dev;
+  const int* fp = (const int*)((const char*)plan_dev + off + (n + 1) * sizeof(int));
+  if (tile == 64)
+    hipLaunchKernelGGL(grouped_fold_kernel<64>, dim3((unsigned)(fold_blocks * FoldCfg<64>::BPT)), dim3(256), 0,
+                       (hipStream_t)stream, gs, fp, n);
+  else
+    hipLaunchKernelGGL(grouped_fold_kernel<128>, dim3((unsigned)(fold_blocks * FoldCfg<128>::BPT)), dim3(256), 0,
+                       (hipStream_t)stream, gs, fp, n);
+  return pcv_launch_status();
 }
 
 template <int W>

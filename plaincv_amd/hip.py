@@ -28,8 +28,10 @@ SIGNATURES = {
                     P, I64, P, P, P, I64, P, P, P, I32, P],
     "pcv_gemm_grouped_plan_size": [I32],
     "pcv_gemm_desc_size": [],
-    "pcv_gemm_grouped_plan": [P, I32, I32, P, P],
+    "pcv_gemm_grouped_ws_floats": [P, I32, I32],
+    "pcv_gemm_grouped_plan": [P, I32, I32, P, P, P, I64, P],
     "pcv_gemm_grouped_run": [P, I32, I32, I64, P],
+    "pcv_gemm_grouped_fold": [P, I32, I32, I64, P],
     "pcv_attn_fwd": [P, P, P, I64, P, I64, P, I32, I32, I32, I32, I32, F32, P, P, P, P, P],
     "pcv_attn_bwd": [P, P, P, I64, P, I64, P, I64, P, P, P, P, P, I64, I32, I32, I32, I32, I32,
                      F32, P, I32, P, P, P, P],
@@ -139,7 +141,7 @@ SIGNATURES = {
 }
 
 # non-status return types (everything else returns an int status)
-RESTYPES = {"pcv_attn_mask_words": I64, "pcv_batchnorm_workspace_size": SZ, "pcv_qrb_panel_lds": SZ, "pcv_gemm_grouped_plan_size": I64, "pcv_eigh_log_floats": I64,
+RESTYPES = {"pcv_attn_mask_words": I64, "pcv_batchnorm_workspace_size": SZ, "pcv_qrb_panel_lds": SZ, "pcv_gemm_grouped_plan_size": I64, "pcv_gemm_grouped_ws_floats": I64, "pcv_eigh_log_floats": I64,
             "pcv_layernorm_bwd_f32_ws": I64}
 
 _lib = None

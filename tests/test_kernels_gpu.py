@@ -413,9 +413,10 @@ def test_gemm_colsum_epilogue(dev, M, N, K):
     assert torch.allclose(cs - 1.0, ref.sum(0), atol=5e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("tile", [64, 128])
-def test_grouped_wgrad(dev, tile):
-    """One grouped launch of weight-gradient GEMMs == separate fp32 A^T B accumulations."""
+@pytest.mark.parametrize("tile,det", [(64, True), (128, True), (64, False)])
+def test_grouped_wgrad(dev, tile, det):
+    """One grouped launch of weight-gradient GEMMs == separate fp32 A^T B accumulations; det: split-K
+    partials through the workspace + fold launch (bit-identical on a repeat), else fp32 atomics."""
     from plaincv_amd import kernels as K_
     torch.manual_seed(9)
     shapes = [(16640, 128, 384), (16640, 128, 128), (16640, 128, 512), (16640, 512, 128), (300, 72, 40),
@@ -432,9 +433,21 @@ def test_grouped_wgrad(dev, tile):
           torch.randn(7, 8, device=dev).to(torch.bfloat16)]
     outs = [torch.randn(x.shape[1], device=dev) for x in xs]
     cref = [o + x.float().sum(0) for x, o in zip(xs, outs)]
-    g = K_.GroupedWGrad(items + [("colsum", x, o) for x, o in zip(xs, outs)], dev, tile=tile)
+    g = K_.GroupedWGrad(items + [("colsum", x, o) for x, o in zip(xs, outs)], dev, tile=tile, deterministic=det)
+    assert (g.fold_blocks > 0) == det and (g.ws is not None) == det
+    c0 = [c.clone() for _, _, c, _ in items]
     g()
     torch.cuda.synchronize()
+    if det:   # the GEMM outputs are a fixed-order sum: a repeat from the same C is bit-identical
+        first = [c.clone() for _, _, c, _ in items]
+        for (_, _, c, _), c_ in zip(items, c0):
+            c.copy_(c_)
+        for o, r, x in zip(outs, cref, xs):
+            o.sub_(x.float().sum(0))      # (column sums use atomics: not compared bitwise)
+        g()
+        torch.cuda.synchronize()
+        for (_, _, c, _), f in zip(items, first):
+            assert torch.equal(c, f)
     for o, r in zip(outs, cref):
         assert torch.allclose(o, r, atol=2e-2, rtol=1e-4), (o - r).abs().max().item()
     for (a, b, c, _), ref in zip(items, refs):
