@@ -279,13 +279,17 @@ int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, int64_t ldb, 
                       int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed, uint32_t site,
                       void* stream);
 /* Every fp32 weight gradient of a step in one launch (csrc/gemm_f32.hip): jobs_dev holds njobs
- * records (pcv_gemm_f32_wgrad_job_size() bytes) {A, B, C, colsum, lda, ldb, ldc, M, N, K, tiles_n,
- * tiles, ksplit, kchunk, first} (colsum optional: += the column sums of B -- the Dense's bias
- * gradient):  C[M][N] += A^T B with A [K][M], B [K][N] (K-major token rows), 64 x bn
- * panels x ksplit K slices added with fp32 atomics; first = prefix sum of tiles * ksplit.
+ * records (pcv_gemm_f32_wgrad_job_size() bytes) {A, B, C, colsum, ws, lda, ldb, ldc, M, N, K, tiles_n,
+ * tiles, ksplit, kchunk, first, ffirst, pad} (colsum optional: += the column sums of B -- the Dense's
+ * bias gradient):  C[M][N] += A^T B with A [K][M], B [K][N] (K-major token rows), 64 x bn
+ * panels x ksplit K slices; first = prefix sum of tiles * ksplit.  ws == NULL: the slices are added
+ * with fp32 atomics; ws (tiles * ksplit * 64 * bn floats): each slice stores its partial tile there and
+ * pcv_gemm_f32_wgrad_fold (fold_tiles = sum of tiles over the ws jobs; ffirst = their prefix) adds
+ * the slices to C in order -- deterministic.
  * Requires M % 64, N % bn, K % 64, kchunk % 64 == 0, 16-B aligned operands, ld % 4 == 0. */
 int pcv_gemm_f32_wgrad_job_size(void);
 int pcv_gemm_f32_wgrad(const void* jobs_dev, int njobs, int64_t total_blocks, int bn, void* stream);
+int pcv_gemm_f32_wgrad_fold(const void* jobs_dev, int njobs, int64_t fold_tiles, int bn, void* stream);
 /* Blocked Householder QR (csrc/qr_blocked.hip; jnp.linalg.qr of SOAP's refresh, soap.py:108-133):
  * jobs {A, perm, Q, Wt, Qt, V, T, lda, ldq, n} (pcv_qrb_job_size() bytes; workspaces Wt, Qt, V
  * n x n and T n x nb, fp32).  init: Wt = A[:, perm]^T, Qt = I; panel(j0, nb): factorise columns

@@ -242,12 +242,15 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
 // ksplit slices of K; slice partial sums are added with fp32 atomics (dW is zeroed per step).
 // colsum (optional): += the column sums of B (the bias gradient of the same Dense), accumulated by
 // the workgroups of the first 64-row panel from the B chunks they already hold in LDS.
+// ws (optional, jobs with ksplit > 1): slice sl of tile t stores its partial to
+// ws[(t * ksplit + sl) * 64 * BN ...] with plain stores and pcv_gemm_f32_wgrad_fold adds the slices
+// to C in slice order (ffirst = the job's first fold tile) -- deterministic, no contended atomics.
 struct WgJob {
-  const float* A; const float* B; float* C; float* colsum;
+  const float* A; const float* B; float* C; float* colsum; float* ws;
   int64_t lda, ldb, ldc;
-  int32_t M, N, K, tiles_n, tiles, ksplit, kchunk, first;
+  int32_t M, N, K, tiles_n, tiles, ksplit, kchunk, first, ffirst, pad;
 };
-static_assert(sizeof(WgJob) == 7 * 8 + 8 * 4, "WgJob layout");
+static_assert(sizeof(WgJob) == 8 * 8 + 10 * 4, "WgJob layout");
 
 template <int BN>
 __global__ __launch_bounds__(256) void gemm_f32_wgrad_kernel(const WgJob* __restrict__ jobs, int njobs) {
@@ -272,6 +275,18 @@ __global__ __launch_bounds__(256) void gemm_f32_wgrad_kernel(const WgJob* __rest
                                m0 == 0 ? jb.colsum : nullptr);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
   const int g4 = lane >> 4, c16 = lane & 15;
+  if (jb.ws && jb.ksplit > 1) {
+    float* part = jb.ws + ((int64_t)t * jb.ksplit + sl) * (GR_BM * BN);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 32 + i * 16 + 4 * g4 + r;
+#pragma unroll
+        for (int q = 0; q < NJ; ++q) part[row * BN + wn * WN + q * 16 + c16] = acc[i][q][r];
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -281,6 +296,37 @@ __global__ __launch_bounds__(256) void gemm_f32_wgrad_kernel(const WgJob* __rest
       for (int q = 0; q < NJ; ++q)
         atomicAdd(jb.C + (int64_t)row * jb.ldc + n0 + wn * WN + q * 16 + c16, acc[i][q][r]);
     }
+}
+
+// Fold of the slices: block -> (job, tile, 256 / (BN / 4) rows); one float4 of a row per thread,
+// summed over the slices in order (8 loads in flight), added to C.
+template <int BN>
+__global__ __launch_bounds__(256) void wgrad_fold_kernel(const WgJob* __restrict__ jobs, int njobs) {
+  constexpr int CPR = BN / 4, RPB = 256 / CPR, BPT = GR_BM / RPB;
+  const int b = blockIdx.x / BPT, rg = blockIdx.x % BPT;
+  int lo = 0, hi = njobs - 1;   // last job whose first fold tile <= b (jobs without a fold hold 0 tiles)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].ffirst <= b) lo = mid; else hi = mid - 1;
+  }
+  const WgJob& jb = jobs[lo];
+  const int t = b - jb.ffirst;
+  const int m0 = (t / jb.tiles_n) * GR_BM, n0 = (t % jb.tiles_n) * BN;
+  const int rr = rg * RPB + threadIdx.x / CPR, c = (threadIdx.x % CPR) * 4;
+  const float* p = jb.ws + (int64_t)t * jb.ksplit * (GR_BM * BN) + rr * BN + c;
+  const int S = jb.ksplit;
+  f32x4 acc{0.f, 0.f, 0.f, 0.f};
+  int q = 0;
+  for (; q + 8 <= S; q += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(p + (int64_t)(q + u) * GR_BM * BN);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; q < S; ++q) acc += *reinterpret_cast<const f32x4*>(p + (int64_t)q * GR_BM * BN);
+  float* cp = jb.C + (int64_t)(m0 + rr) * jb.ldc + n0 + c;   // M % 64 == 0, N % BN == 0: in range
+  *reinterpret_cast<f32x4*>(cp) = *reinterpret_cast<const f32x4*>(cp) + acc;
 }
 
 static bool gr_al(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -360,6 +406,19 @@ extern "C" int pcv_gemm_f32_wgrad_job_size(void) { return (int)sizeof(WgJob); }
 // jobs_dev: njobs WgJob records (host-packed; first = prefix sum of tiles * ksplit, every job with
 // M % 64 == 0, N % 64 == 0, K % 64 == 0, kchunk % 64 == 0, 16-B aligned operands, ld % 4 == 0),
 // all of one panel width bn (64 or 128; N % bn == 0)
+extern "C" int pcv_gemm_f32_wgrad_fold(const void* jobs_dev, int njobs, int64_t fold_tiles, int bn, void* stream) {
+  if (!jobs_dev || njobs <= 0 || fold_tiles < 0 || (bn != 64 && bn != 128)) return PCV_EINVAL;
+  if (fold_tiles == 0) return 0;
+  const int64_t bpt = GR_BM / (256 / (bn / 4));
+  if (bn == 64)
+    hipLaunchKernelGGL((wgrad_fold_kernel<64>), dim3((unsigned)(fold_tiles * bpt)), dim3(256), 0, (hipStream_t)stream,
+                       (const WgJob*)jobs_dev, njobs);
+  else
+    hipLaunchKernelGGL((wgrad_fold_kernel<128>), dim3((unsigned)(fold_tiles * bpt)), dim3(256), 0, (hipStream_t)stream,
+                       (const WgJob*)jobs_dev, njobs);
+  return pcv_launch_status();
+}
+
 extern "C" int pcv_gemm_f32_wgrad(const void* jobs_dev, int njobs, int64_t total_blocks, int bn, void* stream) {
   if (!jobs_dev || njobs <= 0 || total_blocks <= 0 || total_blocks >= (1ll << 31) || (bn != 64 && bn != 128))
     return PCV_EINVAL;

@@ -82,6 +82,7 @@ SIGNATURES = {
     "pcv_gemm_f32_rows": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32, P],
     "pcv_gemm_f32_wgrad_job_size": [],
     "pcv_gemm_f32_wgrad": [P, I32, I64, I32, P],
+    "pcv_gemm_f32_wgrad_fold": [P, I32, I64, I32, P],
     "pcv_qrb_job_size": [],
     "pcv_qrb_panel_lds": [I32, I32],
     "pcv_qrb_init": [P, I32, I32, P],

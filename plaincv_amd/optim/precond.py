@@ -140,11 +140,18 @@ class WgradF32:
     split into slices accumulated with fp32 atomics (``target_blocks`` workgroups in total).
     ``fits(a, b, c)`` says whether a product can join (M, N % 64 / 128, K % 64, 16-B aligned)."""
 
-    FMT = "<4Q3q8i"
+    FMT = "<5Q3q10i"
     BN = 128
 
-    def __init__(self, target_blocks=2048):
+    def __init__(self, target_blocks=2048, deterministic=None):
+        """deterministic (PCV_F32_WGRAD_DET=1): split-K slices store their partial tiles to a workspace
+        and a fold launch adds them to C in slice order (no float atomics, run-to-run identical).  Off
+        by default: unlike the bf16 grouped launch, this MFMA-bound launch does not wait on its atomics,
+        and the workspace round trip measured +0.8 % on the C4 step (1.7455 -> 1.760 ms)."""
         self.jobs, self.target = [], int(target_blocks)
+        if deterministic is None:
+            deterministic = os.environ.get("PCV_F32_WGRAD_DET", "0") == "1"
+        self.deterministic = bool(deterministic)
 
     @classmethod
     def fits(cls, a, b, c):
@@ -169,20 +176,33 @@ class WgradF32:
         assert lib.pcv_gemm_f32_wgrad_job_size() == struct.calcsize(self.FMT)
         tiles = [(a.shape[1] // 64) * (b.shape[1] // self.BN) for a, b, _, _ in self.jobs]
         chunks = max(1, -(-sum(tiles) * max(a.shape[0] // 64 for a, _, _, _ in self.jobs) // self.target))
-        recs, first = [], 0
+        plans = []
         for (a, b, c, cs), t in zip(self.jobs, tiles):
             K = a.shape[0]
             kchunk = 64 * min(chunks, K // 64)
-            ksplit = -(-K // kchunk)
-            recs.append((a.data_ptr(), b.data_ptr(), c.data_ptr(), _addr(cs), a.stride(0), b.stride(0), c.stride(0),
-                         a.shape[1], b.shape[1], K, b.shape[1] // self.BN, t, ksplit, kchunk, first))
+            plans.append((kchunk, -(-K // kchunk)))
+        nws = sum(t * ks * 64 * self.BN for t, (_, ks) in zip(tiles, plans) if ks > 1) if self.deterministic else 0
+        self.ws = torch.empty(nws, dtype=torch.float32, device=device) if nws else None
+        recs, first, ffirst, woff = [], 0, 0, 0
+        for (a, b, c, cs), t, (kchunk, ksplit) in zip(self.jobs, tiles, plans):
+            K = a.shape[0]
+            wsp = 0
+            if self.ws is not None and ksplit > 1:
+                wsp = self.ws.data_ptr() + 4 * woff
+                woff += t * ksplit * 64 * self.BN
+            recs.append((a.data_ptr(), b.data_ptr(), c.data_ptr(), _addr(cs), wsp, a.stride(0), b.stride(0),
+                         c.stride(0), a.shape[1], b.shape[1], K, b.shape[1] // self.BN, t, ksplit, kchunk, first,
+                         ffirst, 0))
             first += t * ksplit
-        self.total = first
+            ffirst += t if wsp else 0
+        self.total, self.fold_tiles = first, ffirst
         self.table = _pack(recs, self.FMT).to(device)
         return self
 
     def run(self):
         hip.call("pcv_gemm_f32_wgrad", ptr(self.table), len(self.jobs), self.total, self.BN, stream_ptr())
+        if self.fold_tiles:
+            hip.call("pcv_gemm_f32_wgrad_fold", ptr(self.table), len(self.jobs), self.fold_tiles, self.BN, stream_ptr())
 
 
 class NewtonRoot:

@@ -176,12 +176,14 @@ def test_gemm_f32_small_jobs(dev, small):
     assert (skipped == 3.0).all()
 
 
-def test_wgrad_f32_grouped(dev):
+@pytest.mark.parametrize("det", [True, False])
+def test_wgrad_f32_grouped(dev, det):
     """row-panel weight-gradient launch (csrc/gemm_f32.hip): several C += A^T B jobs with K = 16448
-    token rows, split-K slices added with atomics, vs fp64"""
+    token rows, split-K slices through the workspace + fold launch (det; bit-identical on a repeat)
+    or added with atomics, vs fp64"""
     from plaincv_amd.optim.precond import WgradF32
     g = torch.Generator().manual_seed(11)
-    plan, refs = WgradF32(target_blocks=700), []
+    plan, refs = WgradF32(target_blocks=700, deterministic=det), []
     for (M, N, K) in [(128, 384, 16448), (256, 128, 16448), (64, 128, 640), (128, 256, 1024)]:
         a = torch.randn(K, M, generator=g).to(dev)
         b = torch.randn(K, N, generator=g).to(dev)
@@ -191,10 +193,21 @@ def test_wgrad_f32_grouped(dev):
         refs.append((cs, cs.double() + b.double().sum(0), b.abs().double().sum(0).max().item()))
         plan.add(a, b, c, colsum=cs)
     assert not WgradF32.fits(torch.zeros(64, 48, device=dev), torch.zeros(64, 128, device=dev), torch.zeros(48, 128, device=dev))
-    plan.finalize(dev).run()
+    plan.finalize(dev)
+    assert (plan.fold_tiles > 0) == det
+    cs0 = [t.clone() for t, _, _ in refs[::2]]
+    plan.run()
     torch.cuda.synchronize()
     for c, ref, scale in refs:
         assert (c.double() - ref).abs().max().item() <= 2e-6 * scale
+    if det:
+        first = [t.clone() for t, _, _ in refs[::2]]
+        for (t, _, _), t0 in zip(refs[::2], cs0):
+            t.copy_(t0)
+        plan.run()
+        torch.cuda.synchronize()
+        for (t, _, _), f in zip(refs[::2], first):
+            assert torch.equal(t, f)
 
 
 def _spd(n, rank, g, dev, scale=1.0):
