@@ -283,7 +283,10 @@ def bench_vit(args):
     nb = 4
     pool_x = torch.randint(0, 256, (nb,) + shape, generator=gen, dtype=torch.uint8).to(dev)
     pool_y = torch.randint(0, cfg.num_classes, (nb, B), generator=gen, dtype=torch.int32).to(dev)
-    step = GraphedTrainStep(state, shape, warmup=2)
+    # the batch pool is the step's input ring: each slot has its own captured graph that reads the
+    # batch in place (a loader fills the slots; no per-step copy into a static buffer)
+    ring = None if os.environ.get("PCV_BENCH_COPY_INPUTS") == "1" else (pool_x, pool_y)   # A/B switch
+    step = GraphedTrainStep(state, shape, warmup=2, inputs=ring)
     for i in range(args.warmup):
         step(pool_x[i % nb], pool_y[i % nb])
     torch.cuda.synchronize()

@@ -65,7 +65,9 @@ struct GemmArgs {
   // column accumulators (colsum, ln_dscale, ln_dbias) replicated over col_reps rows of N:
   // workgroup b adds into row b % col_reps, so no single row takes every workgroup's atomics
   // (one contended row runs ~14x below the chip's float-atomic rate); the caller folds the
-  // replicas (pcv_gemm_grouped column-sum jobs with zero_after)
+  // replicas (pcv_gemm_grouped column-sum jobs with zero_after).  col_reps = -1: one row per
+  // output row-tile (m0 / BM), written with plain stores (no atomics; deterministic), summed by a
+  // plain column-sum job
   int col_reps;
   // attention-backward row constant fused into a bf16 epilogue (the out-projection dgrad
   // produces dO): delta[(b H + h) T + t] = <bf16(C[row, h dh : (h+1) dh]), dl_o[row, same]>,
@@ -77,8 +79,13 @@ struct GemmArgs {
   float* sk_ws;
 };
 
-__device__ __forceinline__ int64_t col_rep_off(const GemmArgs& g) {
+__device__ __forceinline__ int64_t col_rep_off(const GemmArgs& g, int64_t m0 = 0, int bm = 1) {
+  if (g.col_reps < 0) return (m0 / bm) * g.N;
   return g.col_reps > 1 ? (int64_t)(blockIdx.x % g.col_reps) * g.N : 0;
+}
+__device__ __forceinline__ void col_put(const GemmArgs& g, float* p, float v) {
+  if (g.col_reps < 0) *p = v;
+  else atomicAdd(p, v);
 }
 
 #ifdef PCV_GEMM_TIMING
@@ -519,10 +526,10 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
         return v;
       };
       if (tid < 128) {
-        if (g.ln_dscale) atomicAdd(g.ln_dscale + col_rep_off(g) + c, colsum16(0));
-        if (g.colsum) atomicAdd(g.colsum + col_rep_off(g) + c, colsum16(2));
+        if (g.ln_dscale) col_put(g, g.ln_dscale + col_rep_off(g, m0, BM) + c, colsum16(0));
+        if (g.colsum) col_put(g, g.colsum + col_rep_off(g, m0, BM) + c, colsum16(2));
       } else if (g.ln_dbias) {
-        atomicAdd(g.ln_dbias + col_rep_off(g) + c, colsum16(1));
+        col_put(g, g.ln_dbias + col_rep_off(g, m0, BM) + c, colsum16(1));
       }
     }
   }
@@ -956,7 +963,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
     if (threadIdx.x < BN && n0 + threadIdx.x < g.N) {
       float t = 0.f;
       for (int q = 0; q < RPP; ++q) t += red[q * BN + threadIdx.x];
-      atomicAdd(g.colsum + col_rep_off(g) + n0 + threadIdx.x, t);
+      col_put(g, g.colsum + col_rep_off(g, m0, BM) + n0 + threadIdx.x, t);
     }
   }
 }

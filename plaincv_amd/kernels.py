@@ -83,8 +83,8 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
             raise ValueError("gelu epilogue needs bf16 aux [M,N]")
         ldaux = _ld(aux)
     if colsum is not None:
-        _chk(not batched and colsum.dtype == F32 and colsum.numel() >= N * max(1, col_reps) and colsum.is_cuda and
-             colsum.is_contiguous(), "gemm colsum")
+        _chk(not batched and colsum.dtype == F32 and colsum.numel() >= N * col_rows(M, col_reps) and colsum.is_cuda
+             and colsum.is_contiguous(), "gemm colsum")
         split_k = 1
     dl_o, dl_ld, dl, dl_T, dl_H = None, 0, None, 0, 0
     if attn_delta is not None:
@@ -110,6 +110,16 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
     return out
 
 
+def col_rows(M, col_reps):
+    """Rows of a column-accumulator buffer: col_reps replicas (atomics), or with col_reps = -1 one row
+    per output row tile of M rows (plain stores): 64-row tiles (the GEMM and LayerNorm-epilogue
+    tiles), 32 under PCV_LN_TILE=32."""
+    import os
+    if col_reps >= 0:
+        return max(1, int(col_reps))
+    return -(-int(M) // (32 if os.environ.get("PCV_LN_TILE", "64") == "32" else 64))
+
+
 def gemm_ln(a, b, out, *, ln_mode, res, ln_scale, ln_y, ln_mean, ln_rstd, ta=False, tb=False, alpha=1.0, bias=None,
             drop_rate=0.0, seed=None, site=0, ln_bias=None, ln_eps=1e-6, ln_x=None, ln_dscale=None, ln_dbias=None,
             colsum=None, col_reps=1):
@@ -117,7 +127,8 @@ def gemm_ln(a, b, out, *, ln_mode, res, ln_scale, ln_y, ln_mean, ln_rstd, ta=Fal
 
     ln_mode 1: out = x1 = op(a)@op(b)*alpha + bias (+dropout) + res;  ln_y = LN(x1) (bf16), stats out.
     ln_mode 2: dy = op(a)@op(b)*alpha;  out = dx = res + LN_bwd(dy; ln_x, stats, ln_scale); ln_y = bf16(dx);
-               ln_dscale / ln_dbias / colsum accumulate ([col_reps, N] replica rows when col_reps > 1)."""
+               ln_dscale / ln_dbias / colsum accumulate ([col_reps, N] replica rows when col_reps > 1;
+               col_reps = -1: one row per 64-row (or 32-row) output tile, written with plain stores)."""
     M, K = (a.shape[1], a.shape[0]) if ta else tuple(a.shape)
     N, K2 = tuple(b.shape) if tb else (b.shape[1], b.shape[0])
     _chk(K == K2 and tuple(out.shape) == (M, N) and tuple(res.shape) == (M, N), "gemm_ln shapes")
@@ -128,6 +139,9 @@ def gemm_ln(a, b, out, *, ln_mode, res, ln_scale, ln_y, ln_mean, ln_rstd, ta=Fal
     _chk(ln_mode in (1, 2) and N <= 128 and N % 8 == 0, "gemm_ln mode / N")
     if ln_mode == 2:
         _chk(ln_x is not None and tuple(ln_x.shape) == (M, N) and ln_x.dtype == F32, "gemm_ln ln_x")
+    for acc in (ln_dscale, ln_dbias, colsum):
+        _chk(acc is None or (acc.dtype == F32 and acc.is_contiguous() and acc.numel() >= N * col_rows(M, col_reps)),
+             "gemm_ln column accumulators")
     _dev(a, b, out, res, ln_scale, ln_y, ln_mean, ln_rstd, bias, ln_bias, ln_x, ln_dscale, ln_dbias, colsum)
     hip.call("pcv_gemm_ln", ptr(a), ptr(b), ptr(out), M, N, K, _ld(a), _ld(b), _ld(out), int(ta), int(tb),
              float(alpha), ptr(bias), ptr(res), _ld(res), float(drop_rate), ptr(seed), int(site) & 0xFFFFFFFF,

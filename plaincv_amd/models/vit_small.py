@@ -313,13 +313,17 @@ class ViTRunner:
             if self.head_bias_grouped:
                 items.append(("colsum", self.dlogits, self.gbh))
             # Column accumulators written by every row tile of a GEMM epilogue (bias and LayerNorm
-            # parameter gradients) go to 32 replica rows, folded into the gradients by the same launch
-            self.reps = int(os.environ.get("PCV_COL_REPS", "32"))
+            # parameter gradients): each row tile stores its partial to its own row (col_reps = -1,
+            # plain stores: no contended atomics, deterministic) and a column-sum job of the same
+            # grouped launch adds the rows into the gradient.  PCV_COL_REPS=n > 0: the previous form
+            # (atomics into n replica rows, folded and zeroed by the launch).
+            self.reps = int(os.environ.get("PCV_COL_REPS", "-1"))
+            rows = K.col_rows(R, self.reps)
 
             def replicate(key, target):
-                ws = torch.zeros(self.reps, target.numel(), dtype=f32, device=dev)
+                ws = torch.zeros(rows, target.numel(), dtype=f32, device=dev)
                 self.rep_ws[key] = ws
-                items.append(("fold", ws, target.view(-1)))
+                items.append(("colsum" if self.reps < 0 else "fold", ws, target.view(-1)))
 
             for i, w in enumerate(self.w):
                 replicate(("gb0", i), w["gb0"])

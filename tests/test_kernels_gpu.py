@@ -348,7 +348,7 @@ def test_gemm_ln_forward(dev, M, N, K, rate):
 
 
 @pytest.mark.parametrize("M,N,K,rate,reps", [(1000, 128, 256, 0.0, 1), (513, 64, 128, 0.0, 1), (700, 128, 384, 0.1, 1),
-                                             (1000, 128, 256, 0.1, 32)])
+                                             (1000, 128, 256, 0.1, 32), (1000, 128, 256, 0.1, -1), (16448, 128, 256, 0.1, -1)])
 def test_gemm_ln_backward(dev, M, N, K, rate, reps):
     """pcv_gemm_ln mode 2 (dgrad GEMM, LayerNorm backward, residual add, parameter grads, and the
     dropout-backward bf16 copy + column sum consumed by the sublayer below)."""
@@ -366,7 +366,18 @@ def test_gemm_ln_backward(dev, M, N, K, rate, reps):
     dxb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     ds, db, cs = (torch.full((N,), 0.5, device=dev) for _ in range(3))
     seed = torch.tensor([5], dtype=torch.int32, device=dev)
-    if reps > 1:   # replica rows [reps, N], folded afterwards
+    if reps < 0:   # one plain-stored row per output row tile, summed by a column-sum job
+        wss = [torch.full((K_.col_rows(M, reps), N), 9.0, device=dev) for _ in range(3)]
+        assert wss[0].shape[0] == -(-M // 64)
+        K_.gemm_ln(dh, w, dx, tb=True, ln_mode=2, res=dres, ln_scale=sc, ln_y=dxb, ln_mean=mean, ln_rstd=rstd,
+                   ln_x=x, ln_dscale=wss[0], ln_dbias=wss[1], colsum=wss[2], col_reps=reps, drop_rate=rate,
+                   seed=seed, site=11)
+        snap = [ws_.clone() for ws_ in wss]
+        K_.GroupedWGrad([("colsum", ws_, t) for ws_, t in zip(wss, (ds, db, cs))], dev)()
+        torch.cuda.synchronize()
+        assert all(torch.equal(a_, b_) for a_, b_ in zip(snap, wss))   # plain column sums leave the rows
+        assert all((ws_[: -(-M // 64)] != 9.0).all() for ws_ in wss)      # every row tile stored its partial
+    elif reps > 1:   # replica rows [reps, N], folded afterwards
         wss = [torch.zeros(reps, N, device=dev) for _ in range(3)]
         K_.gemm_ln(dh, w, dx, tb=True, ln_mode=2, res=dres, ln_scale=sc, ln_y=dxb, ln_mean=mean, ln_rstd=rstd,
                    ln_x=x, ln_dscale=wss[0], ln_dbias=wss[1], colsum=wss[2], col_reps=reps, drop_rate=rate,

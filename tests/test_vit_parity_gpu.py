@@ -142,3 +142,45 @@ def test_vit_train_step_matches_oracle(dev, optim):
     if name == "signum":
         print(f"VIT_MOVE signum flipped {flips}/{n}")
         assert flips <= 1e-2 * n, (flips, n)
+
+
+@pytest.mark.parametrize("dtype,optim", [("bfloat16", "muon"), ("float32", "soap")])
+def test_graphed_step_input_slots(dev, dtype, optim):
+    """GraphedTrainStep(inputs=ring): each slot's graph reads its batch in place.  Stepping through
+    the ring (slot replays) and through copies into the static buffer (the copy-in graph) from the
+    same state on the same batches give the same loss every step and the same params (rel 1e-5:
+    the bias column-sum jobs still add their row slices with fp32 atomics); labels follow the slot;
+    a tensor that is not a slot still goes through the copy-in graph.  SOAP (its optimizer runs
+    eagerly after the captured forward/backward) refreshes every 2 steps, and its QR power step
+    amplifies the fp32 weight-gradient atomics' run-to-run noise: loss 3e-3, params 1e-2 there
+    (a wrong batch or label slot moves the loss by O(1))."""
+    from plaincv_amd.engine import GraphedTrainStep, create_train_state
+    from plaincv_amd.models.vit_small import VisionTransformer
+    from tests.parity_util import rel
+    from utils import Config
+    m = VisionTransformer(num_classes=10, patch_size=4, hidden_size=64, mlp_dim=128, num_layers=2, num_heads=2,
+                          dropout_rate=0.1, dtype=dtype)
+    shape = (8, 16, 16, 3)
+    cfg = Config(optim=optim, lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9, precondition_frequency=2)
+    init = m.init(4, shape)
+    g = torch.Generator().manual_seed(3)
+    ring_x = torch.randint(0, 256, (3,) + shape, generator=g, dtype=torch.uint8).to(dev)
+    ring_y = torch.randint(0, 10, (3, shape[0]), generator=g, dtype=torch.int32).to(dev)
+    sa = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=init)
+    sb = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=init)
+    ga = GraphedTrainStep(sa, shape, warmup=2, inputs=(ring_x, ring_y))
+    gb = GraphedTrainStep(sb, shape, warmup=2)
+    assert len(ga.g_slots) == 3 and ga._slot_of(ring_x[1], ring_y[1]) == 1
+    assert ga._slot_of(ring_x[1].clone(), ring_y[1]) is None
+    gb.runner.seed.copy_(ga.runner.seed)
+    torch.cuda.synchronize()
+    assert torch.equal(sa.params.flat, sb.params.flat)
+    for it in range(5):
+        k = it % 3
+        ma = ga(ring_x[k], ring_y[k]).clone()
+        mb = gb(ring_x[k].clone(), ring_y[k].clone()).clone()
+        torch.cuda.synchronize()
+        tol = 3e-3 if optim == "soap" else 1e-5
+        assert abs(ma[0].item() - mb[0].item()) <= tol * abs(mb[0].item()), (it, ma, mb)
+        assert ma[1].item() == mb[1].item()
+    assert rel(sa.params.flat, sb.params.flat) < (1e-2 if optim == "soap" else 1e-5)
