@@ -14,8 +14,9 @@ def test_gemm_f32_split_k_plan():
     assert j["kchunk"] % 128 == 0 and j["ksplit"] * j["kchunk"] >= 16448 > (j["ksplit"] - 1) * j["kchunk"]
     assert j["tiles"] == 2 * 6 * j["ksplit"]
     g.finalize("cpu")
-    (dev, n, total, vec), = g.groups
+    (dev, n, total, vec, firsts), = g.groups
     assert n == 1 and total == j["tiles"] and dev.numel() == struct.calcsize(GemmF32.FMT)
+    assert vec == 1 and firsts.value is not None      # 64x64 float4 kernel; host first-tile table
     with pytest.raises(ValueError):   # split-K accumulates: beta must be 1
         GemmF32().add(a, b, c, ta=True, beta=0.0, ksplit=4)
 
@@ -39,7 +40,8 @@ def test_wgrad_f32_plan_and_fits():
             for i in range(2)]
     first = 0
     for rec in recs:
-        M, N, K, tiles_n, tiles, ksplit, kchunk, fst = rec[7:]
+        M, N, K, tiles_n, tiles, ksplit, kchunk, fst, ffirst, _ = rec[8:]
+        assert rec[4] == 0 and ffirst == 0      # atomic split-K by default (no workspace, no fold)
         assert tiles == (M // 64) * (N // 128) and tiles_n == N // 128
         assert kchunk % 64 == 0 and (ksplit - 1) * kchunk < K <= ksplit * kchunk
         assert fst == first
@@ -73,3 +75,26 @@ def test_blocked_qr_plan_schedule():
     assert not small.finalize().blocked   # <= 128: one workgroup per matrix
     with pytest.raises(ValueError):
         HouseholderQR("cpu").add(torch.zeros(4, 5), torch.zeros(4, 5))
+
+
+def test_gemm_f32_small_and_sym_routing():
+    """Host routing of the grouped fp32 GEMM: ta = 0 / tb = 1 jobs with n, K <= 512 and float4
+    alignment go to the K-split 32x32 kernel (kind 2), sym jobs count only upper-triangle tiles,
+    and the rest keep the 64x64 kernels (kind 1 aligned, 0 otherwise)."""
+    from plaincv_amd.optim.precond import GemmF32
+    z = torch.zeros
+    g = GemmF32()
+    g.add(z(256, 256), z(256, 256), z(256, 256), tb=True, sym=True)          # small, sym: 8x8 -> 36 tiles
+    g.add(z(200, 128), z(200, 128), z(200, 200), tb=True)                     # small, full: 7x7 tiles
+    g.add(z(600, 600), z(600, 600), z(600, 600), tb=True, sym=True)           # > 512: 64-tile kernel, 10x10 -> 55
+    g.add(z(128, 256), z(128, 256), z(256, 256), ta=True)                     # ta: 64-tile kernel
+    g.add(z(37, 50), z(50, 29), z(37, 29))                                    # unaligned: kind 0
+    kinds = [j["kind"] for j in g.jobs]
+    tiles = [j["tiles"] for j in g.jobs]
+    assert kinds == [2, 2, 1, 1, 0] and tiles == [36, 49, 55, 16, 1]
+    assert [bool(j["apow"] & 32) for j in g.jobs] == [True, False, True, False, False]
+    assert GemmF32(small=False).add(z(256, 256), z(256, 256), z(256, 256), tb=True).jobs[0]["kind"] == 1
+    with pytest.raises(ValueError):
+        GemmF32().add(z(64, 32), z(48, 32), z(64, 48), tb=True, sym=True)     # sym needs a square C
+    g.finalize("cpu")
+    assert [(n, total, vec) for _, n, total, vec, _ in g.groups] == [(2, 85, 2), (2, 71, 1), (1, 1, 0)]
