@@ -415,69 +415,93 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
   // the previous rows' stores (vmcnt counts stores too on gfx9).
   __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
   PCV_TREC(6);
+  // The BM/16 rows of this thread are processed in phases over all rows at once (element math,
+  // then every row's DPP row sums, then the outputs), so the rows' dependent chains -- four
+  // DPP steps with their hazard nops per sum -- interleave instead of running back to back on
+  // the wave's single SIMD slot (one 256-thread workgroup per CU on the ViT grid).  Rows past M
+  // (their C tile rows hold clamped-load garbage) contribute nothing and store nothing.
+  constexpr int NQ = BM / 16;
+  bool rok[NQ];
+  float v[NQ][8], s1[NQ], s2[NQ];
 #pragma unroll
-  for (int q = 0; q < BM / 16; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     const int rr = (tid >> 4) + 16 * q;
     const int64_t row = m0 + rr;
-    if (row >= g.M) break;                // uniform over the row's 16 lanes
-    float v[8];
+    rok[q] = row < g.M;
+    const bool ok = rok[q] && colok;
     const f32x4 c0 = *reinterpret_cast<const f32x4*>(ct + rr * CLD + col);
     const f32x4 c1 = *reinterpret_cast<const f32x4*>(ct + rr * CLD + col + 4);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { v[e] = g.alpha * c0[e] + bv[e]; v[e + 4] = g.alpha * c1[e] + bv[e + 4]; }
+    for (int e = 0; e < 4; ++e) {
+      v[q][e] = ok ? g.alpha * c0[e] + bv[e] : 0.f;
+      v[q][e + 4] = ok ? g.alpha * c1[e] + bv[e + 4] : 0.f;
+    }
     if (g.drop_thresh && g.ln_mode == 1) {
       const uint32_t base = (uint32_t)(row * g.N + col);
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        v[e] = (hash3(seed, g.site, base + e) >= g.drop_thresh) ? v[e] * g.drop_scale : 0.f;
+        v[q][e] = (hash3(seed, g.site, base + e) >= g.drop_thresh) ? v[q][e] * g.drop_scale : 0.f;
     }
-    float rv[8];
+  }
+  if (g.ln_mode == 1) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { rv[e] = pre.r[q][0][e]; rv[e + 4] = pre.r[q][1][e]; }
-    if (!colok) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = 0.f;
-    }
-    float* cp = (float*)g.C + row * g.ldc + col;
-    bf16* yp = g.ln_y ? g.ln_y + row * g.ld_lny + col : nullptr;
-    if (g.ln_mode == 1) {
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { v[e] += rv[e]; s1 += v[e]; s2 += v[e] * v[e]; }
-      s1 = dpp_row_sum16(s1);
-      s2 = dpp_row_sum16(s2);
-      const float mean = s1 * invN;
-      const float rs = rsqrtf(fmaxf(s2 * invN - mean * mean, 0.f) + g.ln_eps);
-      if (colok && PCV_DBG_STORE) {
-        *reinterpret_cast<f32x4*>(cp) = f32x4{v[0], v[1], v[2], v[3]};
-        *reinterpret_cast<f32x4*>(cp + 4) = f32x4{v[4], v[5], v[6], v[7]};
-        bf16x8 y;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) y[e] = f2bf((v[e] - mean) * rs * sc[e] + sh[e]);
-        *reinterpret_cast<bf16x8*>(yp) = y;
-      }
-      if (cc == 0) { g.ln_mean[row] = mean; g.ln_rstd[row] = rs; }
-    } else {
-      const float mean = pre.mean[q], rs = pre.rstd[q];
-      float xh[8], gx[8], s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {     // zero-filled for columns >= N (prefetch)
-        xh[e] = colok ? (pre.x[q][0][e] - mean) * rs : 0.f;
-        xh[e + 4] = colok ? (pre.x[q][1][e] - mean) * rs : 0.f;
-      }
+    for (int q = 0; q < NQ; ++q) {
+      s1[q] = 0.f; s2[q] = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        gx[e] = v[e] * sc[e];
-        s1 += gx[e];
-        s2 += gx[e] * xh[e];
-        dsc[e] += v[e] * xh[e];
-        dbi[e] += v[e];
+        v[q][e] += e < 4 ? pre.r[q][0][e] : pre.r[q][1][e - 4];   // zero-filled past M / N
+        s1[q] += v[q][e];
+        s2[q] += v[q][e] * v[q][e];
       }
-      s1 = dpp_row_sum16(s1) * invN;
-      s2 = dpp_row_sum16(s2) * invN;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) { s1[q] = dpp_row_sum16(s1[q]); s2[q] = dpp_row_sum16(s2[q]); }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int64_t row = m0 + (tid >> 4) + 16 * q;
+      const float mean = s1[q] * invN;
+      const float rs = rsqrtf(fmaxf(s2[q] * invN - mean * mean, 0.f) + g.ln_eps);
+      if (rok[q] && colok && PCV_DBG_STORE) {
+        float* cp = (float*)g.C + row * g.ldc + col;
+        *reinterpret_cast<f32x4*>(cp) = f32x4{v[q][0], v[q][1], v[q][2], v[q][3]};
+        *reinterpret_cast<f32x4*>(cp + 4) = f32x4{v[q][4], v[q][5], v[q][6], v[q][7]};
+        bf16x8 y;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) y[e] = f2bf((v[q][e] - mean) * rs * sc[e] + sh[e]);
+        *reinterpret_cast<bf16x8*>(g.ln_y + row * g.ld_lny + col) = y;
+      }
+      if (rok[q] && cc == 0) { g.ln_mean[row] = mean; g.ln_rstd[row] = rs; }
+    }
+  } else {
+    float xh[NQ][8];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const float mean = pre.mean[q], rs = pre.rstd[q];
+      s1[q] = 0.f; s2[q] = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {     // x zero-filled for rows >= M / columns >= N (prefetch)
+        const float xv = e < 4 ? pre.x[q][0][e] : pre.x[q][1][e - 4];
+        xh[q][e] = (rok[q] && colok) ? (xv - mean) * rs : 0.f;
+        const float gx = v[q][e] * sc[e];
+        s1[q] += gx;
+        s2[q] += gx * xh[q][e];
+        dsc[e] += v[q][e] * xh[q][e];
+        dbi[e] += v[q][e];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) { s1[q] = dpp_row_sum16(s1[q]) * invN; s2[q] = dpp_row_sum16(s2[q]) * invN; }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int64_t row = m0 + (tid >> 4) + 16 * q;
+      const float rs = pre.rstd[q];
       float dx[8], yv[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { dx[e] = rv[e] + rs * (gx[e] - s1 - xh[e] * s2); yv[e] = dx[e]; }
+      for (int e = 0; e < 8; ++e) {
+        const float rv = e < 4 ? pre.r[q][0][e] : pre.r[q][1][e - 4];
+        dx[e] = rv + rs * (v[q][e] * sc[e] - s1[q] - xh[q][e] * s2[q]);
+        yv[e] = dx[e];
+      }
       if (g.drop_thresh) {   // ln_y / colsum carry the dropout backward of dx (the producer's dropout)
         const uint32_t base = (uint32_t)(row * g.N + col);
 #pragma unroll
@@ -485,15 +509,16 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
           yv[e] = (hash3(seed, g.site, base + e) >= g.drop_thresh) ? yv[e] * g.drop_scale : 0.f;
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) cs[e] += colok ? yv[e] : 0.f;
-      if (colok && PCV_DBG_STORE) {
+      for (int e = 0; e < 8; ++e) cs[e] += (rok[q] && colok) ? yv[e] : 0.f;
+      if (rok[q] && colok && PCV_DBG_STORE) {
+        float* cp = (float*)g.C + row * g.ldc + col;
         *reinterpret_cast<f32x4*>(cp) = f32x4{dx[0], dx[1], dx[2], dx[3]};
         *reinterpret_cast<f32x4*>(cp + 4) = f32x4{dx[4], dx[5], dx[6], dx[7]};
         if (g.ln_y) {
           bf16x8 y;
 #pragma unroll
           for (int e = 0; e < 8; ++e) y[e] = f2bf(yv[e]);
-          *reinterpret_cast<bf16x8*>(yp) = y;
+          *reinterpret_cast<bf16x8*>(g.ln_y + row * g.ld_lny + col) = y;
         }
       }
     }
