@@ -72,7 +72,10 @@ int pcv_gemm_big_wgrad(const void* A, const void* B, float* C, int64_t M, int64_
  *            ln_mean / ln_rstd written (flax LayerNorm fwd, models/vit_small.py:38,52).
  * ln_mode 2: dy = alpha*op(A)op(B); C = dx = res + LN_bwd(dy; ln_x, ln_mean, ln_rstd, ln_scale);
  *            y = dropout_bwd(dx) (site/seed/rate of the sublayer below; rate 0: y = dx):
- *            ln_y = bf16(y) (optional), colsum += sum y; ln_dscale += sum dy*xhat, ln_dbias += sum dy. */
+ *            ln_y = bf16(y) (optional), colsum += sum y; ln_dscale += sum dy*xhat, ln_dbias += sum dy;
+ *            requires trans_b (B stored [N][K]: the dgrad against the weight rows).
+ * col_reps = -1: ln_dscale / ln_dbias / colsum are [ceil(M/64)][N] blocks, each 64-row output tile
+ * storing its partial to its own row (plain stores, deterministic; a column-sum job adds them). */
 int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, int trans_a, int trans_b, float alpha, const float* bias, const float* res, int64_t ldr,
                 float dropout_rate, const uint32_t* seed, uint32_t site, int ln_mode, const float* ln_scale,

@@ -353,15 +353,19 @@ __device__ __forceinline__ void mc_piece_ptrs(const bf16** out, const bf16* base
 
 // Row operands of the LN epilogue (residual, LN input, row statistics) for this thread's
 // BM/16 rows, loaded before the GEMM main loop so their latency hides behind it.
-template <int BM>
+// M2: the tile can run the backward (mode 2) epilogue -- only the B-K-contiguous instantiation
+// (the dgrad against the weight rows; pcv_gemm_ln rejects mode 2 otherwise), so the forward
+// tile does not hold the LN-input rows and statistics across its main loop (36 VGPRs).
+template <int BM, bool M2 = true>
 struct LnPre {
-  f32x4 r[BM / 16][2], x[BM / 16][2];
-  float mean[BM / 16], rstd[BM / 16];
+  static constexpr int QX = M2 ? BM / 16 : 1;
+  f32x4 r[BM / 16][2], x[QX][2];
+  float mean[QX], rstd[QX];
   f32x4 bias[2], scale[2], shift[2];   // this lane's 8 columns
   uint32_t seed;
 };
-template <int BM>
-__device__ __forceinline__ void ln_prefetch(const GemmArgs& g, int64_t m0, LnPre<BM>& p) {
+template <int BM, bool M2>
+__device__ __forceinline__ void ln_prefetch(const GemmArgs& g, int64_t m0, LnPre<BM, M2>& p) {
   const int tid = threadIdx.x, col = (tid & 15) * 8;
   const bool colok = col < g.N;
 #pragma unroll
@@ -372,7 +376,7 @@ __device__ __forceinline__ void ln_prefetch(const GemmArgs& g, int64_t m0, LnPre
     const float* rp = (const float*)g.res + row * g.ldr + col;
     p.r[q][0] = ok ? *reinterpret_cast<const f32x4*>(rp) : z;
     p.r[q][1] = ok ? *reinterpret_cast<const f32x4*>(rp + 4) : z;
-    if (g.ln_mode == 2) {
+    if (M2 && g.ln_mode == 2) {
       const float* xp = g.ln_x + row * g.ld_lnx + col;
       p.x[q][0] = ok ? *reinterpret_cast<const f32x4*>(xp) : z;
       p.x[q][1] = ok ? *reinterpret_cast<const f32x4*>(xp + 4) : z;
@@ -392,8 +396,8 @@ __device__ __forceinline__ void ln_prefetch(const GemmArgs& g, int64_t m0, LnPre
 }
 
 
-template <int BM>
-__device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, const LnPre<BM>& pre) {
+template <int BM, bool M2>
+__device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, const LnPre<BM, M2>& pre) {
   constexpr int CLD = 128 + 4;
   const int tid = threadIdx.x, cc = tid & 15, wave = tid >> 6, lane = tid & 63;
   const int col = cc * 8;
@@ -472,7 +476,7 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
       }
       if (rok[q] && cc == 0) { g.ln_mean[row] = mean; g.ln_rstd[row] = rs; }
     }
-  } else {
+  } else if constexpr (M2) {
     float xh[NQ][8];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -524,7 +528,7 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
     }
   }
   PCV_TREC(3);
-  if (g.ln_mode != 2) return;
+  if (!M2 || g.ln_mode != 2) return;
   // column reductions: every lane's 8-column partials (16 row-groups: 4 per wave) through LDS,
   // summed per column by one thread, one atomic per column and array
   __syncthreads();                        // ct is no longer read; reuse its LDS
@@ -640,9 +644,9 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
   PCV_TREC(7);
   // the 64 x 128 tile (pcv_gemm_ln) prefetches its LN row operands before the main loop
   constexpr bool LN_TILE = BM <= 64 && BN == 128;   // 64x128 / 32x128: pcv_gemm_ln tiles (whole rows)
-  LnPre<LN_TILE ? BM : 16> lnpre;
+  LnPre<LN_TILE ? BM : 16, B_KC> lnpre;
   if constexpr (LN_TILE) {
-    if (g.ln_mode) ln_prefetch<BM>(g, m0, lnpre);
+    if (g.ln_mode) ln_prefetch<BM, B_KC>(g, m0, lnpre);
   }
 
   u32x4 stA[BM * 8 / 256], stB[BN * 8 / 256];
@@ -862,7 +866,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
       continue;
     }
     if constexpr (LN_TILE) {
-      if (g.ln_mode) { PCV_TREC(2); ln_epilogue<BM>(g, ct, m0, lnpre); PCV_TREC(5); return; }
+      if (g.ln_mode) { PCV_TREC(2); ln_epilogue<BM, B_KC>(g, ct, m0, lnpre); PCV_TREC(5); return; }
     }
     if (col >= g.N) continue;
     for (int rr = threadIdx.x / CPR; rr < CH; rr += RPP) {
@@ -1287,7 +1291,7 @@ extern "C" int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, in
   if (M < 0 || N <= 0 || K < 0 || N > 128 || (N & 7) || (ln_mode != 1 && ln_mode != 2)) return PCV_EINVAL;
   if (!res || !ln_scale || !ln_mean || !ln_rstd) return PCV_EINVAL;
   if (ln_mode == 1 && (!ln_bias || !ln_y)) return PCV_EINVAL;
-  if (ln_mode == 2 && (!ln_x || bias)) return PCV_EINVAL;
+  if (ln_mode == 2 && (!ln_x || bias || !trans_b)) return PCV_EINVAL;   // mode 2: B stored [N][K]
   if (dropout_rate > 0.f && !seed) return PCV_EINVAL;
   if (M == 0) return 0;
   if ((lda & 7) || (ldb & 7) || !pcv_aligned16(A) || !pcv_aligned16(B)) return PCV_EALIGN;

@@ -139,6 +139,7 @@ def gemm_ln(a, b, out, *, ln_mode, res, ln_scale, ln_y, ln_mean, ln_rstd, ta=Fal
     _chk(ln_mode in (1, 2) and N <= 128 and N % 8 == 0, "gemm_ln mode / N")
     if ln_mode == 2:
         _chk(ln_x is not None and tuple(ln_x.shape) == (M, N) and ln_x.dtype == F32, "gemm_ln ln_x")
+        _chk(tb, "gemm_ln mode 2 takes B stored [N][K] (tb=True: the dgrad against the weight rows)")
     for acc in (ln_dscale, ln_dbias, colsum):
         _chk(acc is None or (acc.dtype == F32 and acc.is_contiguous() and acc.numel() >= N * col_rows(M, col_reps)),
              "gemm_ln column accumulators")
