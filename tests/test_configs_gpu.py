@@ -82,9 +82,10 @@ def test_c1_fashion_mnist_adamw_10_steps(dev):
     assert hip64 <= max(1e-5, 2.0 * o64), (hip64, o64)
 
 
-def _c4_pair(dev, optim, steps, extra, soap_f=0, batch=8):
-    """Per step: (p0, p1, oracle update given the HIP gradients).  SOAP: basis checks and the
-    basis-dependent state hand-over after step 0 and each refresh (test_engine_parity_gpu.py)."""
+def _c4_pair(dev, optim, steps, extra, soap_f=0, batch=8, fp64=False):
+    """Per step: (p0, p1, oracle update given the HIP gradients[, the fp64 oracle's update]).  SOAP:
+    basis checks and the basis-dependent state hand-over after step 0 and each refresh
+    (test_engine_parity_gpu.py), to the fp64 oracle as well."""
     from oracle import optim as oopt
     from plaincv_amd.engine import create_train_state, make_train_step
     from utils import Config
@@ -97,6 +98,8 @@ def _c4_pair(dev, optim, steps, extra, soap_f=0, batch=8):
     step = make_train_step()
     tx = oopt.get_optimizer(cfg)
     ost = tx.init(init)
+    tx64 = oopt.get_optimizer(cfg) if fp64 else None
+    ost64 = tx64.init({k: v.double() for k, v in init.items()}) if fp64 else None
     gen = torch.Generator().manual_seed(4)
     out = []
     for it in range(steps):
@@ -108,6 +111,8 @@ def _c4_pair(dev, optim, steps, extra, soap_f=0, batch=8):
         torch.cuda.synchronize()
         p1, g = st.params.to_dict(), st.params.grads_dict()
         u, ost = tx.update(g, ost, p0)
+        if fp64:
+            u64, ost64 = tx64.update({k: v.double() for k, v in g.items()}, ost64, {k: v.double() for k, v in p0.items()})
         if soap_f:
             for s_ in st.opt_state.mats:
                 o = ost[s_.name]
@@ -117,25 +122,33 @@ def _c4_pair(dev, optim, steps, extra, soap_f=0, batch=8):
                     _check_basis(it, s_, o, prev[s_.name])
                     for nm in ("QL", "QR", "m", "v"):
                         setattr(o, nm, getattr(s_, nm).cpu().clone().reshape(getattr(o, nm).shape))
-        out.append((p0, p1, u))
+                        if fp64:
+                            setattr(ost64[s_.name], nm, getattr(o, nm).double())
+        out.append((p0, p1, u, u64) if fp64 else (p0, p1, u))
     return out, st
 
 
 def test_c4_fp32_soap_13_steps_two_refreshes(dev):
-    out, st = _c4_pair(dev, "soap", 13, dict(precondition_frequency=5, eps=1e-8), soap_f=5)
+    """Each step's update against the fp64 oracle fed the same gradients and handed the same bases,
+    bounded per leaf by max(5e-4, 2x the fp32 oracle's own distance from it): the Adam step in the
+    rotated basis (eps 1e-8) divides rotated-gradient coordinates by their own running RMS, so a
+    coordinate that is ~0 in the rotated basis carries its fp32 rounding noise at O(1) into the
+    update -- any fp32 implementation, the CPU oracle's included, moves by up to ~1e-3 there."""
+    out, st = _c4_pair(dev, "soap", 13, dict(precondition_frequency=5, eps=1e-8), soap_f=5, fp64=True)
     assert st.opt_state.host_step == 12
     sizes = {max(s.r, s.c) for s in st.opt_state.mats}
     assert 256 in sizes and 200 in sizes, sizes          # n = 256 factors (blocked QR) and the head
     worst = {}
-    for it, (p0, p1, u) in enumerate(out):
+    for it, (p0, p1, u, u64) in enumerate(out):
         for k in p0:
             d = p1[k].double() - p0[k].double()
             if it == 0 and routed(k, p0[k]):
                 assert d.abs().max().item() == 0.0, k        # SOAP's first step: update exactly 0
                 continue
-            worst[k] = max(worst.get(k, 0.0), rel(d, u[k]))
-    print("C4_SOAP", sorted(worst.items(), key=lambda kv: -kv[1])[:6])
-    bad = {k: v for k, v in worst.items() if v > 5e-4}      # measured <= 1.1e-4 (r03)
+            now = (rel(d, u64[k]), rel(u[k], u64[k]), rel(d, u[k]))
+            worst[k] = tuple(max(a, b) for a, b in zip(worst.get(k, now), now))
+    print("C4_SOAP (hip-fp64, oracle32-fp64, hip-oracle32)", sorted(worst.items(), key=lambda kv: -kv[1][0])[:6])
+    bad = {k: v for k, v in worst.items() if v[0] > max(5e-4, 2.0 * v[1])}
     assert not bad, bad
 
 
