@@ -11,6 +11,9 @@
 //   patch gradient.  Dropout bits: hash3(seed, site, flat index) as every other kernel (oracle/rng.py).
 #include "common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace pcv {
 
 __device__ __forceinline__ bool keep_of(uint32_t seed, uint32_t site, uint32_t idx, uint32_t thresh) {
@@ -814,6 +817,276 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
   }
 }
 
+// Backward, score-sharing form (at most 16 MFMA key blocks: T <= 256, or 257 with its one-row
+// tail): wave w owns key block w and meets every query block once, so each 16 x 16 score tile is
+// computed ONCE -- S, dPd, P and dS feed dV and dK in registers and dQ through per-query-block
+// accumulators in LDS (5 T x T x 32 products; the two-family form above recomputes S and dPd in the
+// query orientation, 7).  dQ^T[d][q] = K^T dS^T needs dS with the key along the MFMA k index, the
+// transpose of the tile's output layout: each wave passes its tile through a private LDS scratch.
+// Iteration i gives wave w query block (w + i) mod NQ -- a Latin square, so no two waves touch one
+// accumulator in an iteration and a barrier between iterations suffices; every dQ tile is summed
+// over the key blocks in one fixed order (deterministic).  The one-row tails of T = 16 n + 1 run on
+// VALU: key T-1's column with each wave's first query block, query T-1's row after the loop; their
+// per-wave partials meet in LDS.
+constexpr int FK_DS_LD = 20;   // scratch row stride (floats): b128 row writes, conflict-free column reads
+constexpr int FK_QMAX = 16 * FA_WAVES;
+constexpr size_t FK_BWD_LDS = 2 * (size_t)FA_TMAX * FA_DH * 4 + 3 * FA_TMAX * 4 + 17 * 6 * 64 * 2 +
+                              (size_t)FK_QMAX * FA_DH * 4 + FA_WAVES * 16 * FK_DS_LD * 4 + (3 * FA_WAVES * FA_DH + 4) * 4;
+static_assert(FK_BWD_LDS <= 160 * 1024, "fp32 attention backward (score-sharing) LDS");
+
+__device__ __forceinline__ void fk_put8(float* X, int r, int g, const f32x4 (&acc)[2]) {   // acc layout of fa_store8
+  *reinterpret_cast<f32x4*>(X + fa_off(r, 8 * g)) = f32x4{acc[0][0], acc[1][0], acc[0][1], acc[1][1]};
+  *reinterpret_cast<f32x4*>(X + fa_off(r, 8 * g + 4)) = f32x4{acc[0][2], acc[1][2], acc[0][3], acc[1][3]};
+}
+__device__ __forceinline__ void fk_get8(const float* X, int r, int g, f32x4 (&acc)[2]) {
+  const f32x4 x0 = *reinterpret_cast<const f32x4*>(X + fa_off(r, 8 * g));
+  const f32x4 x1 = *reinterpret_cast<const f32x4*>(X + fa_off(r, 8 * g + 4));
+  acc[0] = f32x4{x0[0], x0[2], x1[0], x1[2]};
+  acc[1] = f32x4{x0[1], x0[3], x1[1], x1[3]};
+}
+
+template <bool DROP>
+__global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kshare_kernel(FaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char fk_smem[];
+  const int h = blockIdx.x, b = blockIdx.y, T = a.T;
+  const int NB = (T + 15) / 16, TP = NB * 16;
+  const bool tail1 = (T & 15) == 1 && NB > 1;
+  const int NQ = tail1 ? NB - 1 : NB;   // MFMA query blocks = key blocks = working waves (<= 16)
+  float* Qs = reinterpret_cast<float*>(fk_smem);
+  float* Os = Qs + TP * FA_DH;   // dO
+  float* Ms = Os + TP * FA_DH;
+  float* Is = Ms + TP;
+  float* Dl = Is + TP;
+  uint16_t* mk = reinterpret_cast<uint16_t*>(Dl + TP);
+  float* dQa = reinterpret_cast<float*>(mk + 17 * 6 * 64);   // [16 NQ][32] dQ accumulators (fa_off)
+  float* dsx = dQa + FK_QMAX * FA_DH;                         // [wave][16 keys][FK_DS_LD] dS^T
+  float* tailp = dsx + FA_WAVES * 16 * FK_DS_LD;              // [dq | dk | dv][wave][32] of row T-1
+  float* corner = tailp + 3 * FA_WAVES * FA_DH;
+  const int64_t bT = (int64_t)b * T, bh = (int64_t)b * a.H + h;
+  const int64_t ld = a.ldqkv;
+  const float* base = a.qkv + bT * ld + h * FA_DH;
+  const float* kg = base + a.D;
+  const float* vg = base + 2 * a.D;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  const bool own = wave < NQ;
+  const int key = wave * 16 + c16;
+  const bool kv = key < T;
+  // the wave's key block in registers: kf / vf = K / V[key][8g .. 8g+7] (S and dPd operands),
+  // kp[s] = K[16 w + 4g + s][2 c16 .. 2 c16 + 1] (the dQ product's A operand)
+  float kf[8], vf[8];
+  f32x2 kp[4];
+  {
+    f32x4 k0 = {0.f, 0.f, 0.f, 0.f}, k1 = k0, v0 = k0, v1 = k0;
+    if (own && kv) {
+      k0 = *reinterpret_cast<const f32x4*>(kg + key * ld + 8 * g);
+      k1 = *reinterpret_cast<const f32x4*>(kg + key * ld + 8 * g + 4);
+      v0 = *reinterpret_cast<const f32x4*>(vg + key * ld + 8 * g);
+      v1 = *reinterpret_cast<const f32x4*>(vg + key * ld + 8 * g + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { kf[j] = k0[j]; kf[4 + j] = k1[j]; vf[j] = v0[j]; vf[4 + j] = v1[j]; }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int row = wave * 16 + 4 * g + s;
+      kp[s] = f32x2{0.f, 0.f};
+      if (own && row < T) kp[s] = *reinterpret_cast<const f32x2*>(kg + row * ld + 2 * c16);
+    }
+  }
+  fa_load(Qs, base, ld, T, TP);
+  fa_load(Os, a.dout + bT * a.lddo + h * FA_DH, a.lddo, T, TP);
+  if (DROP) fa_load_mask(mk, a.mask, T);
+  for (int r = threadIdx.x; r < TP; r += FA_THREADS) {
+    Ms[r] = r < T ? a.mrow[bh * T + r] : 0.f;
+    Is[r] = r < T ? a.linv[bh * T + r] : 0.f;   // 0: padded queries get P = 0
+  }
+  for (int i = threadIdx.x; i < TP * 4; i += FA_THREADS) {   // delta = rowsum(dO o O)
+    const int r = i >> 2, c = (i & 3) * 8;
+    float sum = 0.f;
+    if (r < T) {
+      const float* op = a.o + (bT + r) * a.ldo + h * FA_DH + c;
+      const float* dp = a.dout + (bT + r) * a.lddo + h * FA_DH + c;
+      const f32x4 o0 = *reinterpret_cast<const f32x4*>(op), o1 = *reinterpret_cast<const f32x4*>(op + 4);
+      const f32x4 d0 = *reinterpret_cast<const f32x4*>(dp), d1 = *reinterpret_cast<const f32x4*>(dp + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sum += o0[j] * d0[j] + o1[j] * d1[j];
+    }
+    sum += __shfl_xor(sum, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    if ((i & 3) == 0) Dl[r] = sum;
+  }
+  __syncthreads();
+  f32x4 dv[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, dk[2] = {dv[0], dv[0]};
+  float* dsw = dsx + wave * 16 * FK_DS_LD;
+  for (int i = 0; i < NQ; ++i) {
+    if (own) {
+      int qb = wave + i;
+      if (qb >= NQ) qb -= NQ;
+      const int qrow = qb * 16 + c16;
+      float qa[8], oa[8];
+      fa_row8(Qs, qrow, g, qa);
+      fa_row8(Os, qrow, g, oa);
+      f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // dQ^T[8g + 2r + dd][qrow]
+      if (i > 0) fk_get8(dQa, qrow, g, acc);
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = sv;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        sv = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[s], kf[s], sv, 0, 0, 0);   // S[q 4g+r][key]
+        dp = __builtin_amdgcn_mfma_f32_16x16x4f32(oa[s], vf[s], dp, 0, 0, 0);   // dPd[q][key]
+      }
+      const int q0 = qb * 16 + 4 * g;
+      const f32x4 m4 = *reinterpret_cast<const f32x4*>(Ms + q0), i4 = *reinterpret_cast<const f32x4*>(Is + q0);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(Dl + q0);
+      uint32_t w = 0xFFFFu;
+      if (DROP && kv) w = mk[f32_drop_word(q0, key, a.n64)] >> (key & 3);
+      float pd[4], ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = kv ? __expf(sv[r] * a.scale - m4[r]) * i4[r] : 0.f;   // padded keys must not reach dQ
+        float pdv = p, dpv = dp[r];
+        if (DROP) {
+          const bool keep = (w >> (4 * r)) & 1u;
+          pdv = keep ? p * a.dscale : 0.f;
+          dpv = keep ? dpv * a.dscale : 0.f;
+        }
+        pd[r] = pdv;
+        ds[r] = p * (dpv - d4[r]);
+      }
+      // dS^T through the wave's scratch: row = key c16, columns q 4g .. 4g+3
+      *reinterpret_cast<f32x4*>(dsw + c16 * FK_DS_LD + 4 * g) = f32x4{ds[0], ds[1], ds[2], ds[3]};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const f32x2 o2 = fa_pair(Os, q0 + s, c16), q2 = fa_pair(Qs, q0 + s, c16);
+        dv[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(o2[0], pd[s], dv[0], 0, 0, 0);
+        dv[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(o2[1], pd[s], dv[1], 0, 0, 0);
+        dk[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(q2[0], ds[s], dk[0], 0, 0, 0);
+        dk[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(q2[1], ds[s], dk[1], 0, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();
+      float dt[4];   // dS[q = 16 qb + c16][key = 16 w + 4g + s]
+#pragma unroll
+      for (int s = 0; s < 4; ++s) dt[s] = dsw[(4 * g + s) * FK_DS_LD + c16];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(kp[s][0], dt[s], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(kp[s][1], dt[s], acc[1], 0, 0, 0);
+      }
+      if (tail1 && i == 0) {   // key T-1 against this query block (lane: query qrow, d slice 8g ..)
+        const float* kt = kg + (int64_t)(T - 1) * ld + 8 * g;
+        const float* vt = vg + (int64_t)(T - 1) * ld + 8 * g;
+        const f32x4 ka = *reinterpret_cast<const f32x4*>(kt), kb4 = *reinterpret_cast<const f32x4*>(kt + 4);
+        const f32x4 va = *reinterpret_cast<const f32x4*>(vt), vb4 = *reinterpret_cast<const f32x4*>(vt + 4);
+        float st = 0.f, dpt = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          st += qa[j] * ka[j] + qa[4 + j] * kb4[j];
+          dpt += oa[j] * va[j] + oa[4 + j] * vb4[j];
+        }
+        st = xsum_rows(st);
+        dpt = xsum_rows(dpt);
+        const float p = __expf(st * a.scale - Ms[qrow]) * Is[qrow];
+        float pdv = p;
+        if (DROP) {
+          const bool keep = attn_keep(mk, qrow, T - 1, a.n64);
+          pdv = keep ? p * a.dscale : 0.f;
+          dpt = keep ? dpt * a.dscale : 0.f;
+        }
+        const float dst = p * (dpt - Dl[qrow]);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {   // d = 8g + 2r + dd
+          acc[0][r] += dst * ka[2 * r];
+          acc[1][r] += dst * ka[2 * r + 1];
+          acc[0][2 + r] += dst * kb4[2 * r];
+          acc[1][2 + r] += dst * kb4[2 * r + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float tk = dpp_row_sum16(dst * qa[j]), tv = dpp_row_sum16(pdv * oa[j]);
+          if (c16 == 0) {
+            tailp[(FA_WAVES + wave) * FA_DH + 8 * g + j] = tk;
+            tailp[(2 * FA_WAVES + wave) * FA_DH + 8 * g + j] = tv;
+          }
+        }
+      }
+      if (i == NQ - 1) {
+        if (qrow < T) fa_store8(a.dqkv + (bT + qrow) * a.lddqkv + h * FA_DH + 8 * g, acc, a.scale);
+      } else {
+        fk_put8(dQa, qrow, g, acc);
+      }
+    }
+    __syncthreads();
+  }
+  if (own) {
+    if (tail1) {   // query T-1 against the wave's key block
+      const int t = T - 1;
+      float qt[8], ot[8];
+      fa_row8(Qs, t, g, qt);
+      fa_row8(Os, t, g, ot);
+      float st = 0.f, dpt = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        st += qt[j] * kf[j];
+        dpt += ot[j] * vf[j];
+      }
+      st = xsum_rows(st);
+      dpt = xsum_rows(dpt);
+      const float p = __expf(st * a.scale - Ms[t]) * Is[t];
+      float pdv = p;
+      if (DROP) {
+        const bool keep = attn_keep(mk, t, key, a.n64);
+        pdv = keep ? p * a.dscale : 0.f;
+        dpt = keep ? dpt * a.dscale : 0.f;
+      }
+      const float dst = p * (dpt - Dl[t]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {   // d = 8g + 2r + dd
+        dk[0][r] += dst * qt[2 * r];
+        dk[1][r] += dst * qt[2 * r + 1];
+        dv[0][r] += pdv * ot[2 * r];
+        dv[1][r] += pdv * ot[2 * r + 1];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float tq = dpp_row_sum16(dst * kf[j]);
+        if (c16 == 0) tailp[wave * FA_DH + 8 * g + j] = tq;
+      }
+    }
+    if (kv) {   // dv[dd][r] = dV^T[8g + 2r + dd][key]
+      float* dst = a.dqkv + (bT + key) * a.lddqkv + h * FA_DH + 8 * g;
+      fa_store8(dst + 2 * a.D, dv, 1.f);
+      fa_store8(dst + a.D, dk, a.scale);
+    }
+  }
+  if (tail1) {   // row T-1: dq | dk | dv = fixed-order sums of the per-wave partials + the corner
+    const int t = T - 1;
+    if (wave == 0) {
+      const int c = lane & 31;
+      float sv = Qs[fa_off(t, c)] * kg[(int64_t)t * ld + c], dpv = Os[fa_off(t, c)] * vg[(int64_t)t * ld + c];
+      sv = xsum16(dpp_row_sum16(sv));
+      dpv = xsum16(dpp_row_sum16(dpv));
+      const float p = __expf(sv * a.scale - Ms[t]) * Is[t];
+      float pd = p;
+      if (DROP) {
+        const bool keep = attn_keep(mk, t, t, a.n64);
+        pd = keep ? p * a.dscale : 0.f;
+        dpv = keep ? dpv * a.dscale : 0.f;
+      }
+      if (lane == 0) {
+        corner[0] = p * (dpv - Dl[t]);
+        corner[1] = pd;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 * FA_DH) {
+      const int kind = threadIdx.x / FA_DH, d = threadIdx.x - kind * FA_DH;
+      float sum = 0.f;
+      for (int w = 0; w < NQ; ++w) sum += tailp[(kind * FA_WAVES + w) * FA_DH + d];
+      const float ds = corner[0], pd = corner[1];
+      sum += kind == 0 ? ds * kg[(int64_t)t * ld + d] : kind == 1 ? ds * Qs[fa_off(t, d)] : pd * Os[fa_off(t, d)];
+      a.dqkv[(bT + t) * a.lddqkv + kind * a.D + h * FA_DH + d] = kind == 2 ? sum : sum * a.scale;
+    }
+  }
+}
+
 template <bool D>
 static int fa_fwd_launch(const FaArgs& a, int B, hipStream_t s) {
   static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
@@ -823,6 +1096,16 @@ static int fa_fwd_launch(const FaArgs& a, int B, hipStream_t s) {
 }
 template <bool D>
 static int fa_bwd_launch(const FaArgs& a, int B, hipStream_t s) {
+  // the score-sharing form whenever its 16 waves cover the key blocks (PCV_F32_ATTN_BWD=two keeps
+  // the two-family form for A/B measurements)
+  static const bool two = [] { const char* e = getenv("PCV_F32_ATTN_BWD"); return e && !strcmp(e, "two"); }();
+  const int NB = (a.T + 15) / 16, NQ = ((a.T & 15) == 1 && NB > 1) ? NB - 1 : NB;
+  if (!two && NQ <= FA_WAVES) {
+    static PcvLdsOptIn optk;
+    if (const int e = optk.ensure((const void*)attn_bwd_f32_kshare_kernel<D>, (int)FK_BWD_LDS)) return e;
+    hipLaunchKernelGGL((attn_bwd_f32_kshare_kernel<D>), dim3(a.H, B), dim3(FA_THREADS), FK_BWD_LDS, s, a);
+    return 0;
+  }
   static PcvLdsOptIn optin;
   if (const int e = optin.ensure((const void*)attn_bwd_f32_kernel<D>, (int)FA_BWD_LDS)) return e;
   hipLaunchKernelGGL((attn_bwd_f32_kernel<D>), dim3(a.H, B), dim3(FA_THREADS), FA_BWD_LDS, s, a);
