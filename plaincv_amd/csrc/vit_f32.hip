@@ -823,28 +823,54 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
 // accumulators in LDS (5 T x T x 32 products; the two-family form above recomputes S and dPd in the
 // query orientation, 7).  dQ^T[d][q] = K^T dS^T needs dS with the key along the MFMA k index, the
 // transpose of the tile's output layout: each wave passes its tile through a private LDS scratch.
-// Iteration i gives wave w query block (w + i) mod NQ -- a Latin square, so no two waves touch one
-// accumulator in an iteration and a barrier between iterations suffices; every dQ tile is summed
-// over the key blocks in one fixed order (deterministic).  The one-row tails of T = 16 n + 1 run on
+// Iteration i gives wave w query block (w + i) mod NQ -- a Latin square: tile qb receives its
+// contributions from waves qb, qb - 1, ... in iteration order, so every dQ tile is summed over the
+// key blocks in one fixed order (deterministic).  Instead of a block barrier per iteration (which
+// re-aligned all waves of a SIMD to the same phase), each tile carries a counter in LDS: the wave
+// at iteration i waits, just before its dQ product, until the tile holds i contributions (the
+// previous one was made by wave w + 1 at iteration i - 1, a full iteration earlier); the waits form
+// chains that end at iteration 0, so they cannot cycle.  The one-row tails of T = 16 n + 1 run on
 // VALU: key T-1's column with each wave's first query block, query T-1's row after the loop; their
 // per-wave partials meet in LDS.
+#ifdef PCV_FK_TIMING
+// debug builds only: per-wave phase stamps (s_memrealtime, 100 MHz) of the score-sharing backward:
+// [wg][wave][start, prologue done, loop done, end, spin count, s_memtime at start, at loop end, -,
+//             16 iteration-start stamps]
+__device__ uint64_t* pcv_fk_timing_buf;
+#define PCV_FKREC(slot, v)                                                                              \
+  do {                                                                                                   \
+    if (lane == 0 && pcv_fk_timing_buf)                                                                  \
+      pcv_fk_timing_buf[((size_t)(blockIdx.x + gridDim.x * blockIdx.y) * FA_WAVES + wave) * 24 + (slot)] = (v); \
+  } while (0)
+extern "C" int pcv_debug_fk_timing(void* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(pcv_fk_timing_buf), &buf, sizeof(buf));
+}
+#else
+#define PCV_FKREC(slot, v) do {} while (0)
+#endif
+constexpr float kLog2e = 1.4426950408889634f;
 constexpr int FK_DS_LD = 20;   // scratch row stride (floats): b128 row writes, conflict-free column reads
 constexpr int FK_QMAX = 16 * FA_WAVES;
-constexpr size_t FK_BWD_LDS = 2 * (size_t)FA_TMAX * FA_DH * 4 + 3 * FA_TMAX * 4 + 17 * 6 * 64 * 2 +
-                              (size_t)FK_QMAX * FA_DH * 4 + FA_WAVES * 16 * FK_DS_LD * 4 + (3 * FA_WAVES * FA_DH + 4) * 4;
+constexpr size_t FK_BWD_LDS = 2 * (size_t)FA_TMAX * FA_DH * 4 + 2 * FA_TMAX * 4 + 17 * 6 * 64 * 2 +
+                              (size_t)FK_QMAX * FA_DH * 4 + FA_WAVES * 16 * FK_DS_LD * 4 + (3 * FA_WAVES * FA_DH + 4 + FA_WAVES) * 4;
 static_assert(FK_BWD_LDS <= 160 * 1024, "fp32 attention backward (score-sharing) LDS");
 
-__device__ __forceinline__ void fk_put8(float* X, int r, int g, const f32x4 (&acc)[2]) {   // acc layout of fa_store8
-  *reinterpret_cast<f32x4*>(X + fa_off(r, 8 * g)) = f32x4{acc[0][0], acc[1][0], acc[0][1], acc[1][1]};
-  *reinterpret_cast<f32x4*>(X + fa_off(r, 8 * g + 4)) = f32x4{acc[0][2], acc[1][2], acc[0][3], acc[1][3]};
-}
-__device__ __forceinline__ void fk_get8(const float* X, int r, int g, f32x4 (&acc)[2]) {
-  const f32x4 x0 = *reinterpret_cast<const f32x4*>(X + fa_off(r, 8 * g));
-  const f32x4 x1 = *reinterpret_cast<const f32x4*>(X + fa_off(r, 8 * g + 4));
-  acc[0] = f32x4{x0[0], x0[2], x1[0], x1[2]};
-  acc[1] = f32x4{x0[1], x0[3], x1[1], x1[3]};
+// the 16-B loads of rows [qb * 16 + c16][8g .. 8g+7] of a swizzled [TP][32] image: the swizzle phase
+// of a row depends only on its place in the 16-row block, so the address is qb * 512 + a lane constant
+__device__ __forceinline__ void fk_row8(const float* X, int qb, int o0, int o1, float (&x)[8]) {
+  const f32x4 a0 = *reinterpret_cast<const f32x4*>(X + qb * 512 + o0);
+  const f32x4 a1 = *reinterpret_cast<const f32x4*>(X + qb * 512 + o1);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { x[j] = a0[j]; x[4 + j] = a1[j]; }
 }
 
+// dropout keep bit -> all-ones / zero lane mask applied to an fp32 value's bits
+__device__ __forceinline__ float fk_keep(float v, int m) { return __uint_as_float(__float_as_uint(v) & (uint32_t)m); }
+
+// Per-row softmax statistic: Ml[q] = m_q log2 e + log2 l_q (so P = exp2(S scale log2 e - Ml), one
+// fused multiply-add and one exp2 per score); +inf for padded rows (P = 0).  With dropout the dO
+// image in LDS is pre-scaled by 1 / (1 - rate): dPd' = dO' V^T = dscale dPd and Pd^T dO' with
+// Pd = keep * P carries dV's dscale, so the keep bit is the only per-score dropout work.
 template <bool DROP>
 __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kshare_kernel(FaArgs a) {
   extern __shared__ __attribute__((aligned(16))) char fk_smem[];
@@ -853,24 +879,30 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kshare_kernel(FaAr
   const bool tail1 = (T & 15) == 1 && NB > 1;
   const int NQ = tail1 ? NB - 1 : NB;   // MFMA query blocks = key blocks = working waves (<= 16)
   float* Qs = reinterpret_cast<float*>(fk_smem);
-  float* Os = Qs + TP * FA_DH;   // dO
-  float* Ms = Os + TP * FA_DH;
-  float* Is = Ms + TP;
-  float* Dl = Is + TP;
+  float* Os = Qs + TP * FA_DH;   // dO (x dscale with dropout)
+  float* Ml = Os + TP * FA_DH;
+  float* Dl = Ml + TP;
   uint16_t* mk = reinterpret_cast<uint16_t*>(Dl + TP);
-  float* dQa = reinterpret_cast<float*>(mk + 17 * 6 * 64);   // [16 NQ][32] dQ accumulators (fa_off)
+  float* dQa = reinterpret_cast<float*>(mk + 17 * 6 * 64);   // [qb][2][64 lanes][4] dQ accumulators
   float* dsx = dQa + FK_QMAX * FA_DH;                         // [wave][16 keys][FK_DS_LD] dS^T
   float* tailp = dsx + FA_WAVES * 16 * FK_DS_LD;              // [dq | dk | dv][wave][32] of row T-1
   float* corner = tailp + 3 * FA_WAVES * FA_DH;
+  int* ready = reinterpret_cast<int*>(corner + 4);   // [qb] contributions in dQa's tile
   const int64_t bT = (int64_t)b * T, bh = (int64_t)b * a.H + h;
   const int64_t ld = a.ldqkv;
   const float* base = a.qkv + bT * ld + h * FA_DH;
   const float* kg = base + a.D;
   const float* vg = base + 2 * a.D;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
+  // wave-uniform in an SGPR: block offsets (qb * 512) become scalar adds
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
   const bool own = wave < NQ;
   const int key = wave * 16 + c16;
   const bool kv = key < T;
+  const float kb = kv ? 0.f : __builtin_inff();   // padded keys: P = exp2(-inf) = 0, never reaching dQ
+  const float sl2 = a.scale * kLog2e;
+  PCV_FKREC(0, __builtin_amdgcn_s_memrealtime());
+  PCV_FKREC(5, __builtin_amdgcn_s_memtime());
+  int spins = 0;
   // the wave's key block in registers: kf / vf = K / V[key][8g .. 8g+7] (S and dPd operands),
   // kp[s] = K[16 w + 4g + s][2 c16 .. 2 c16 + 1] (the dQ product's A operand)
   float kf[8], vf[8];
@@ -893,13 +925,21 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kshare_kernel(FaAr
     }
   }
   fa_load(Qs, base, ld, T, TP);
-  fa_load(Os, a.dout + bT * a.lddo + h * FA_DH, a.lddo, T, TP);
-  if (DROP) fa_load_mask(mk, a.mask, T);
-  for (int r = threadIdx.x; r < TP; r += FA_THREADS) {
-    Ms[r] = r < T ? a.mrow[bh * T + r] : 0.f;
-    Is[r] = r < T ? a.linv[bh * T + r] : 0.f;   // 0: padded queries get P = 0
+  {   // dO image, x dscale with dropout
+    const float* src = a.dout + bT * a.lddo + h * FA_DH;
+    const float sc = DROP ? a.dscale : 1.f;
+    for (int i = threadIdx.x; i < TP * (FA_DH / 4); i += FA_THREADS) {
+      const int r = i >> 3, c = (i & 7) * 4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (r < T) v = *reinterpret_cast<const f32x4*>(src + (int64_t)r * a.lddo + c);
+      if (DROP) v *= sc;
+      *reinterpret_cast<f32x4*>(Os + fa_off(r, c)) = v;
+    }
   }
-  for (int i = threadIdx.x; i < TP * 4; i += FA_THREADS) {   // delta = rowsum(dO o O)
+  if (DROP) fa_load_mask(mk, a.mask, T);
+  for (int r = threadIdx.x; r < TP; r += FA_THREADS)
+    Ml[r] = r < T ? a.mrow[bh * T + r] * kLog2e - log2f(a.linv[bh * T + r]) : __builtin_inff();
+  for (int i = threadIdx.x; i < TP * 4; i += FA_THREADS) {   // delta = rowsum(dO o O), unscaled dO
     const int r = i >> 2, c = (i & 3) * 8;
     float sum = 0.f;
     if (r < T) {
@@ -914,62 +954,32 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kshare_kernel(FaAr
     sum += __shfl_xor(sum, 2, 64);
     if ((i & 3) == 0) Dl[r] = sum;
   }
+  if (threadIdx.x < FA_WAVES) ready[threadIdx.x] = 0;
   __syncthreads();
+  PCV_FKREC(1, __builtin_amdgcn_s_memrealtime());
+  // lane-constant LDS offsets (floats, + qb * 512 per query block)
+  const int sw = (c16 >> 1) & 7;
+  const int ro0 = c16 * FA_DH + (((2 * g) ^ sw) << 2), ro1 = c16 * FA_DH + (((2 * g + 1) ^ sw) << 2);
+  int po[4];   // fa_pair(X, 16 qb + 4g + s, c16)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) po[s] = (4 * g + s) * FA_DH + (((c16 >> 1) ^ ((2 * g + (s >> 1)) & 7)) << 2) + ((2 * c16) & 3);
+  // f32_drop_word(16 qb + 4g, key) = (16 qb n64 * 4 + 16 g) + ko
+  const int ko = (key >> 6) * 64 + ((key & 15) >> 2) * 4 + ((key & 63) >> 4);
   f32x4 dv[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, dk[2] = {dv[0], dv[0]};
   float* dsw = dsx + wave * 16 * FK_DS_LD;
+  float qa[8], oa[8];   // Q / dO'[16 qb + c16][8g .. 8g+7] of the iteration's query block, prefetched
+  if (own) {
+    fk_row8(Qs, wave, ro0, ro1, qa);
+    fk_row8(Os, wave, ro0, ro1, oa);
+  }
   for (int i = 0; i < NQ; ++i) {
+    PCV_FKREC(8 + (i & 15), __builtin_amdgcn_s_memrealtime());
     if (own) {
-      int qb = wave + i;
-      if (qb >= NQ) qb -= NQ;
+      int qb = wave - i;
+      if (qb < 0) qb += NQ;
       const int qrow = qb * 16 + c16;
-      float qa[8], oa[8];
-      fa_row8(Qs, qrow, g, qa);
-      fa_row8(Os, qrow, g, oa);
+      float* dqt = dQa + qb * 512 + lane * 4;
       f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // dQ^T[8g + 2r + dd][qrow]
-      if (i > 0) fk_get8(dQa, qrow, g, acc);
-      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = sv;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        sv = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[s], kf[s], sv, 0, 0, 0);   // S[q 4g+r][key]
-        dp = __builtin_amdgcn_mfma_f32_16x16x4f32(oa[s], vf[s], dp, 0, 0, 0);   // dPd[q][key]
-      }
-      const int q0 = qb * 16 + 4 * g;
-      const f32x4 m4 = *reinterpret_cast<const f32x4*>(Ms + q0), i4 = *reinterpret_cast<const f32x4*>(Is + q0);
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(Dl + q0);
-      uint32_t w = 0xFFFFu;
-      if (DROP && kv) w = mk[f32_drop_word(q0, key, a.n64)] >> (key & 3);
-      float pd[4], ds[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = kv ? __expf(sv[r] * a.scale - m4[r]) * i4[r] : 0.f;   // padded keys must not reach dQ
-        float pdv = p, dpv = dp[r];
-        if (DROP) {
-          const bool keep = (w >> (4 * r)) & 1u;
-          pdv = keep ? p * a.dscale : 0.f;
-          dpv = keep ? dpv * a.dscale : 0.f;
-        }
-        pd[r] = pdv;
-        ds[r] = p * (dpv - d4[r]);
-      }
-      // dS^T through the wave's scratch: row = key c16, columns q 4g .. 4g+3
-      *reinterpret_cast<f32x4*>(dsw + c16 * FK_DS_LD + 4 * g) = f32x4{ds[0], ds[1], ds[2], ds[3]};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const f32x2 o2 = fa_pair(Os, q0 + s, c16), q2 = fa_pair(Qs, q0 + s, c16);
-        dv[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(o2[0], pd[s], dv[0], 0, 0, 0);
-        dv[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(o2[1], pd[s], dv[1], 0, 0, 0);
-        dk[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(q2[0], ds[s], dk[0], 0, 0, 0);
-        dk[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(q2[1], ds[s], dk[1], 0, 0, 0);
-      }
-      __builtin_amdgcn_wave_barrier();
-      float dt[4];   // dS[q = 16 qb + c16][key = 16 w + 4g + s]
-#pragma unroll
-      for (int s = 0; s < 4; ++s) dt[s] = dsw[(4 * g + s) * FK_DS_LD + c16];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(kp[s][0], dt[s], acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(kp[s][1], dt[s], acc[1], 0, 0, 0);
-      }
       if (tail1 && i == 0) {   // key T-1 against this query block (lane: query qrow, d slice 8g ..)
         const float* kt = kg + (int64_t)(T - 1) * ld + 8 * g;
         const float* vt = vg + (int64_t)(T - 1) * ld + 8 * g;
@@ -983,20 +993,16 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kshare_kernel(FaAr
         }
         st = xsum_rows(st);
         dpt = xsum_rows(dpt);
-        const float p = __expf(st * a.scale - Ms[qrow]) * Is[qrow];
+        const float p = __builtin_amdgcn_exp2f(fmaf(st, sl2, -Ml[qrow]));
         float pdv = p;
-        if (DROP) {
-          const bool keep = attn_keep(mk, qrow, T - 1, a.n64);
-          pdv = keep ? p * a.dscale : 0.f;
-          dpt = keep ? dpt * a.dscale : 0.f;
-        }
+        if (DROP && !attn_keep(mk, qrow, T - 1, a.n64)) pdv = dpt = 0.f;
         const float dst = p * (dpt - Dl[qrow]);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {   // d = 8g + 2r + dd
-          acc[0][r] += dst * ka[2 * r];
-          acc[1][r] += dst * ka[2 * r + 1];
-          acc[0][2 + r] += dst * kb4[2 * r];
-          acc[1][2 + r] += dst * kb4[2 * r + 1];
+        for (int r = 0; r < 2; ++r) {   // the tile's first contribution (d = 8g + 2r + dd)
+          acc[0][r] = dst * ka[2 * r];
+          acc[1][r] = dst * ka[2 * r + 1];
+          acc[0][2 + r] = dst * kb4[2 * r];
+          acc[1][2 + r] = dst * kb4[2 * r + 1];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -1007,14 +1013,73 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kshare_kernel(FaAr
           }
         }
       }
+      const int q0 = qb * 16 + 4 * g;
+      const f32x4 m4 = *reinterpret_cast<const f32x4*>(Ml + q0), d4 = *reinterpret_cast<const f32x4*>(Dl + q0);
+      int w = 0xFFFF;
+      if (DROP) w = (int)mk[(qb * a.n64 * 4 + g) * 16 + ko] >> (key & 3);   // bit 4r: query q0 + r
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = sv;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        sv = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[s], kf[s], sv, 0, 0, 0);   // S[q 4g+r][key]
+        dp = __builtin_amdgcn_mfma_f32_16x16x4f32(oa[s], vf[s], dp, 0, 0, 0);   // dPd'[q][key]
+      }
+      if (i + 1 < NQ) {   // the next query block's fragments under this block's MFMAs
+        const int qn = qb == 0 ? NQ - 1 : qb - 1;
+        fk_row8(Qs, qn, ro0, ro1, qa);
+        fk_row8(Os, qn, ro0, ro1, oa);
+      }
+      float pd[4], ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(sv[r], sl2, -(m4[r] + kb)));
+        float dpv = dp[r];
+        pd[r] = p;
+        if (DROP) {
+          const int m = __builtin_amdgcn_sbfe(w, 4 * r, 1);
+          pd[r] = fk_keep(p, m);
+          dpv = fk_keep(dpv, m);
+        }
+        ds[r] = p * (dpv - d4[r]);
+      }
+      // dS^T through the wave's scratch: row = key c16, columns q 4g .. 4g+3
+      *reinterpret_cast<f32x4*>(dsw + c16 * FK_DS_LD + 4 * g) = f32x4{ds[0], ds[1], ds[2], ds[3]};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const f32x2 o2 = *reinterpret_cast<const f32x2*>(Os + qb * 512 + po[s]);
+        const f32x2 q2 = *reinterpret_cast<const f32x2*>(Qs + qb * 512 + po[s]);
+        dv[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(o2[0], pd[s], dv[0], 0, 0, 0);
+        dv[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(o2[1], pd[s], dv[1], 0, 0, 0);
+        dk[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(q2[0], ds[s], dk[0], 0, 0, 0);
+        dk[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(q2[1], ds[s], dk[1], 0, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();
+      float dt[4];   // dS[q = 16 qb + c16][key = 16 w + 4g + s]
+#pragma unroll
+      for (int s = 0; s < 4; ++s) dt[s] = dsw[(4 * g + s) * FK_DS_LD + c16];
+      if (i > 0) {   // bounded spin: a broken chain gives wrong numbers (caught by the tests), never a hang
+        for (int spin = 0; __hip_atomic_load(ready + qb, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < i &&
+                           spin < (1 << 22); ++spin, ++spins)
+          __builtin_amdgcn_s_sleep(1);
+        acc[0] = *reinterpret_cast<const f32x4*>(dqt);
+        acc[1] = *reinterpret_cast<const f32x4*>(dqt + 256);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(kp[s][0], dt[s], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(kp[s][1], dt[s], acc[1], 0, 0, 0);
+      }
       if (i == NQ - 1) {
         if (qrow < T) fa_store8(a.dqkv + (bT + qrow) * a.lddqkv + h * FA_DH + 8 * g, acc, a.scale);
       } else {
-        fk_put8(dQa, qrow, g, acc);
+        *reinterpret_cast<f32x4*>(dqt) = acc[0];
+        *reinterpret_cast<f32x4*>(dqt + 256) = acc[1];
+        __hip_atomic_store(ready + qb, i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
-    __syncthreads();
   }
+  PCV_FKREC(2, __builtin_amdgcn_s_memrealtime());
+  PCV_FKREC(6, __builtin_amdgcn_s_memtime());
+  PCV_FKREC(4, (uint64_t)spins);
   if (own) {
     if (tail1) {   // query T-1 against the wave's key block
       const int t = T - 1;
@@ -1029,13 +1094,9 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kshare_kernel(FaAr
       }
       st = xsum_rows(st);
       dpt = xsum_rows(dpt);
-      const float p = __expf(st * a.scale - Ms[t]) * Is[t];
+      const float p = __builtin_amdgcn_exp2f(fmaf(st, sl2, -Ml[t]));
       float pdv = p;
-      if (DROP) {
-        const bool keep = attn_keep(mk, t, key, a.n64);
-        pdv = keep ? p * a.dscale : 0.f;
-        dpt = keep ? dpt * a.dscale : 0.f;
-      }
+      if (DROP && !attn_keep(mk, t, key, a.n64)) pdv = dpt = 0.f;
       const float dst = p * (dpt - Dl[t]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {   // d = 8g + 2r + dd
@@ -1063,13 +1124,9 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kshare_kernel(FaAr
       float sv = Qs[fa_off(t, c)] * kg[(int64_t)t * ld + c], dpv = Os[fa_off(t, c)] * vg[(int64_t)t * ld + c];
       sv = xsum16(dpp_row_sum16(sv));
       dpv = xsum16(dpp_row_sum16(dpv));
-      const float p = __expf(sv * a.scale - Ms[t]) * Is[t];
+      const float p = __builtin_amdgcn_exp2f(fmaf(sv, sl2, -Ml[t]));
       float pd = p;
-      if (DROP) {
-        const bool keep = attn_keep(mk, t, t, a.n64);
-        pd = keep ? p * a.dscale : 0.f;
-        dpv = keep ? dpv * a.dscale : 0.f;
-      }
+      if (DROP && !attn_keep(mk, t, t, a.n64)) pd = dpv = 0.f;
       if (lane == 0) {
         corner[0] = p * (dpv - Dl[t]);
         corner[1] = pd;
@@ -1085,6 +1142,7 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kshare_kernel(FaAr
       a.dqkv[(bT + t) * a.lddqkv + kind * a.D + h * FA_DH + d] = kind == 2 ? sum : sum * a.scale;
     }
   }
+  PCV_FKREC(3, __builtin_amdgcn_s_memrealtime());
 }
 
 template <bool D>
