@@ -823,13 +823,18 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kernel(FaArgs a) {
 // accumulators in LDS (5 T x T x 32 products; the two-family form above recomputes S and dPd in the
 // query orientation, 7).  dQ^T[d][q] = K^T dS^T needs dS with the key along the MFMA k index, the
 // transpose of the tile's output layout: each wave passes its tile through a private LDS scratch.
-// Iteration i gives wave w query block (w + i) mod NQ -- a Latin square: tile qb receives its
-// contributions from waves qb, qb - 1, ... in iteration order, so every dQ tile is summed over the
+// Iteration i gives wave w query block (w - i) mod NQ -- a Latin square: tile qb receives its
+// contributions from waves qb, qb + 1, ... in iteration order, so every dQ tile is summed over the
 // key blocks in one fixed order (deterministic).  Instead of a block barrier per iteration (which
 // re-aligned all waves of a SIMD to the same phase), each tile carries a counter in LDS: the wave
 // at iteration i waits, just before its dQ product, until the tile holds i contributions (the
-// previous one was made by wave w + 1 at iteration i - 1, a full iteration earlier); the waits form
-// chains that end at iteration 0, so they cannot cycle.  The one-row tails of T = 16 n + 1 run on
+// previous one was made by wave w - 1 at iteration i - 1, a full iteration earlier); the waits form
+// chains that end at iteration 0, so they cannot cycle.  The chain runs from the youngest waves
+// (which the SIMD's oldest-first issue leaves behind) to the oldest, so the old waves are the ones
+// held back and the four waves of a SIMD finish closer together.  Issue budget: an f32 MFMA and
+// VALU issue serialise on a SIMD, so each VALU instruction in the loop costs ~1/8 of an MFMA --
+// the per-score work is one fma + exp2 (+ a keep-bit mask with dropout), addresses are lane
+// constants plus scalar block offsets.  The one-row tails of T = 16 n + 1 run on
 // VALU: key T-1's column with each wave's first query block, query T-1's row after the loop; their
 // per-wave partials meet in LDS.
 #ifdef PCV_FK_TIMING
@@ -924,35 +929,48 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_bwd_f32_kshare_kernel(FaAr
       if (own && row < T) kp[s] = *reinterpret_cast<const f32x2*>(kg + row * ld + 2 * c16);
     }
   }
-  fa_load(Qs, base, ld, T, TP);
-  {   // dO image, x dscale with dropout
-    const float* src = a.dout + bT * a.lddo + h * FA_DH;
-    const float sc = DROP ? a.dscale : 1.f;
-    for (int i = threadIdx.x; i < TP * (FA_DH / 4); i += FA_THREADS) {
-      const int r = i >> 3, c = (i & 7) * 4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (r < T) v = *reinterpret_cast<const f32x4*>(src + (int64_t)r * a.lddo + c);
-      if (DROP) v *= sc;
-      *reinterpret_cast<f32x4*>(Os + fa_off(r, c)) = v;
-    }
-  }
-  if (DROP) fa_load_mask(mk, a.mask, T);
-  for (int r = threadIdx.x; r < TP; r += FA_THREADS)
-    Ml[r] = r < T ? a.mrow[bh * T + r] * kLog2e - log2f(a.linv[bh * T + r]) : __builtin_inff();
-  for (int i = threadIdx.x; i < TP * 4; i += FA_THREADS) {   // delta = rowsum(dO o O), unscaled dO
-    const int r = i >> 2, c = (i & 3) * 8;
-    float sum = 0.f;
-    if (r < T) {
-      const float* op = a.o + (bT + r) * a.ldo + h * FA_DH + c;
-      const float* dp = a.dout + (bT + r) * a.lddo + h * FA_DH + c;
-      const f32x4 o0 = *reinterpret_cast<const f32x4*>(op), o1 = *reinterpret_cast<const f32x4*>(op + 4);
-      const f32x4 d0 = *reinterpret_cast<const f32x4*>(dp), d1 = *reinterpret_cast<const f32x4*>(dp + 4);
+  {   // every global load of the prologue issued before any LDS store (the burst is bound by each
+      // CU's load throughput, not by the latency of one dependent chain): Q, dO, O rows as 16-B
+      // pieces (8 per row), the softmax statistics, the keep words; delta = rowsum(dO o O) of the
+      // unscaled dO from the same pieces (8 lanes x 4 columns per row, within one wave)
+    constexpr int NP = (FA_TMAX * (FA_DH / 4) + FA_THREADS - 1) / FA_THREADS;
+    const float* dsrc = a.dout + bT * a.lddo + h * FA_DH;
+    const float* osrc = a.o + bT * a.ldo + h * FA_DH;
+    f32x4 qv[NP], dv4[NP], ov[NP];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) sum += o0[j] * d0[j] + o1[j] * d1[j];
+    for (int k = 0; k < NP; ++k) {
+      const int idx = threadIdx.x + k * FA_THREADS, r = idx >> 3, c = (idx & 7) * 4;
+      qv[k] = dv4[k] = ov[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (r < T) {
+        qv[k] = *reinterpret_cast<const f32x4*>(base + (int64_t)r * ld + c);
+        dv4[k] = *reinterpret_cast<const f32x4*>(dsrc + (int64_t)r * a.lddo + c);
+        ov[k] = *reinterpret_cast<const f32x4*>(osrc + (int64_t)r * a.ldo + c);
+      }
     }
-    sum += __shfl_xor(sum, 1, 64);
-    sum += __shfl_xor(sum, 2, 64);
-    if ((i & 3) == 0) Dl[r] = sum;
+    float mr = 0.f, li = 1.f;
+    const int rr = threadIdx.x;
+    if (rr < T) {
+      mr = a.mrow[bh * T + rr];
+      li = a.linv[bh * T + rr];
+    }
+    uint4 mw = {0u, 0u, 0u, 0u};
+    const int nmw = fa_mask_words(T) / 8;
+    if (DROP && (int)threadIdx.x < nmw) mw = reinterpret_cast<const uint4*>(a.mask)[threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int idx = threadIdx.x + k * FA_THREADS, r = idx >> 3, c = (idx & 7) * 4;
+      float sum = dv4[k][0] * ov[k][0] + dv4[k][1] * ov[k][1] + dv4[k][2] * ov[k][2] + dv4[k][3] * ov[k][3];
+      sum += __shfl_xor(sum, 1, 64);
+      sum += __shfl_xor(sum, 2, 64);
+      sum += __shfl_xor(sum, 4, 64);
+      if (r < TP) {
+        if ((idx & 7) == 0) Dl[r] = sum;
+        *reinterpret_cast<f32x4*>(Qs + fa_off(r, c)) = qv[k];
+        *reinterpret_cast<f32x4*>(Os + fa_off(r, c)) = DROP ? dv4[k] * a.dscale : dv4[k];
+      }
+    }
+    if (rr < TP) Ml[rr] = rr < T ? mr * kLog2e - log2f(li) : __builtin_inff();
+    if (DROP && (int)threadIdx.x < nmw) reinterpret_cast<uint4*>(mk)[threadIdx.x] = mw;
   }
   if (threadIdx.x < FA_WAVES) ready[threadIdx.x] = 0;
   __syncthreads();
