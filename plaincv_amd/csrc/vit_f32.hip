@@ -420,6 +420,14 @@ __device__ __forceinline__ void fa_store8(float* dst, const f32x4 (&acc)[2], flo
   *reinterpret_cast<f32x4*>(dst + 4) = f32x4{acc[0][2], acc[1][2], acc[0][3], acc[1][3]} * scale;
 }
 
+// max of three scores without the NaN-canonicalising v_max x, x that fmaxf adds per operand (MFMA
+// results are not known canonical): scores are finite or -inf here
+__device__ __forceinline__ float fa_max3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // the keep words of query rows [0, 16 * ceil(T/16)) (drop_word layout, shared by batch and heads)
 __host__ __device__ __forceinline__ int fa_mask_words(int T) { return ((T + 15) / 16) * 2 * ((T + 127) / 128) * 64; }
 __device__ __forceinline__ void fa_load_mask(uint16_t* dst, const uint16_t* src, int T) {
@@ -471,6 +479,8 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) { qf[j] = x0[j]; qf[4 + j] = x1[j]; }
     }
+    // raw scores (scale > 0 commutes with the max): P = exp2(s c2 - m c2), c2 = scale log2 e
+    const float c2 = a.scale * 1.4426950408889634f;
     float m = -__builtin_inff(), l = 0.f;
     f32x4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     // Lane-constant LDS offsets: every row a lane reads sits at the same swizzle phase in each
@@ -501,19 +511,20 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
           for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[s], qf[s], acc, 0, 0, 0);
 #pragma unroll
           for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kb4[s], qf[4 + s], acc, 0, 0, 0);
-          acc *= a.scale;   // (K Q^T)[key (k0+t)*16 + 4g + r][query q] * scale
+          // acc = (K Q^T)[key (k0+t)*16 + 4g + r][query q], unscaled
           if (!interior) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) acc[r] = ((k0 + t) * 16 + 4 * g + r < T) ? acc[r] : -__builtin_inff();
           }
           st[t] = acc;
-          cmax = fmaxf(cmax, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
+          cmax = fa_max3(fa_max3(cmax, acc[0], acc[1]), acc[2], acc[3]);
         }
       }
       cmax = xmax_rows(cmax);
       const float mnew = fmaxf(m, cmax);
-      const float alpha = __expf(m - mnew);   // 0 on the first chunk (m = -inf)
+      const float alpha = __builtin_amdgcn_exp2f((m - mnew) * c2);   // 0 on the first chunk (m = -inf)
       m = mnew;
+      const float mc = mnew * c2;
       l *= alpha;
       o[0] *= alpha;
       o[1] *= alpha;
@@ -525,7 +536,7 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
           const float* vr = vbase + (k0 + t) * 16 * FA_DH;
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
-            float p = __expf(st[t][s] - m);
+            float p = __builtin_amdgcn_exp2f(fmaf(st[t][s], c2, -mc));
             l += p;
             if (DROP) p = __uint_as_float(__float_as_uint(p) & (uint32_t)__builtin_amdgcn_sbfe((int)w, s, 1));
             const f32x2 v2 = *reinterpret_cast<const f32x2*>(vr + voff[s]);
@@ -541,7 +552,7 @@ __global__ __launch_bounds__(FA_THREADS, 1) void attn_fwd_f32_kernel(FaArgs a) {
     if (qv) {
       fa_store8(a.out + (bT + q) * a.ldo + h * FA_DH + 8 * g, o, os);   // o[dd][r] = O^T[8g + 2r + dd][q]
       if (g == 0) {
-        a.mrow[bh * T + q] = m;
+        a.mrow[bh * T + q] = m * a.scale;   // the row max of the scaled scores
         a.linv[bh * T + q] = inv;
       }
     }
