@@ -175,18 +175,21 @@ def vit_roofline(state, image_shape):
 
 
 def vit_roofline_f32(state, image_shape, rate):
-    """fp32 ViT path: the dominant kernel of the step is the fused fp32 attention backward
-    (attn_bwd_f32_kernel, one launch per layer): its algorithmic FLOPs are the five T x T x Dh
-    products of a (batch, head) -- the score recompute, dPd = dO V^T, dV, dK, dQ -- 5 * 2 * T^2 * Dh
-    per (batch, head), timed live on layer 0 against the fp32 MFMA peak (157.3 TF/s)."""
+    """fp32 ViT path: the dominant kernel of the step is the fused fp32 attention backward, one
+    launch per layer (attn_bwd_f32_kshare_kernel, the score-sharing form, for T <= 257 -- the ViT's
+    257 -- else attn_bwd_f32_kernel): its algorithmic FLOPs are the five T x T x Dh products of a
+    (batch, head) -- S, dPd = dO V^T, dV, dK, dQ -- 5 * 2 * T^2 * Dh per (batch, head), timed live on
+    layer 0 against the fp32 MFMA peak (157.3 TF/s)."""
     r = state.runner_for(image_shape)
     if not getattr(r, "fused_attn", False):
         return None
     t = timed_kernel(lambda: r.attn_bwd(0, rate))
     flops = 5 * 2 * r.B * r.H * r.T * r.T * r.Dh
     ach = flops / t / 1e12
-    traffic, tsrc = pmc_traffic("attn_bwd_f32_kernel<true>")
-    return {"kernel": "attn_bwd_f32_kernel<dropout> (fused fp32 attention backward of one layer)", "bound": "mfma",
+    nq = (r.T + 15) // 16 - (1 if (r.T % 16 == 1 and r.T > 16) else 0)
+    name = "attn_bwd_f32_kshare_kernel" if nq <= 16 else "attn_bwd_f32_kernel"
+    traffic, tsrc = pmc_traffic(f"{name}<true>" if rate > 0 else f"{name}<false>")
+    return {"kernel": f"{name}<dropout> (fused fp32 attention backward of one layer)", "bound": "mfma",
             "achieved": round(ach, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / F32_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
             "traffic_source": tsrc, "launch_us": round(t * 1e6, 2), "flops_per_launch": flops}

@@ -36,6 +36,6 @@ timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_f32_write -o p -- pytho
 J=$O/${TAG}_pmc_traffic.json
 rm -f $J
 (cd $R/profiles && python3 pmc_traffic.py "$(db $O/pmc_fetch)" "$(db $O/pmc_write)" "gemm_bf16_kernel<true, true, 2, 4>" $J \
-   && python3 pmc_traffic.py "$(db $O/pmc_f32_fetch)" "$(db $O/pmc_f32_write)" "attn_bwd_f32_kernel<true>" $J) > $O/${TAG}_pmc_traffic.txt 2>&1 || exit 1
+   && python3 pmc_traffic.py "$(db $O/pmc_f32_fetch)" "$(db $O/pmc_f32_write)" "attn_bwd_f32_kshare_kernel<true>" $J) > $O/${TAG}_pmc_traffic.txt 2>&1 || exit 1
 rm -rf $O/pmc_fetch $O/pmc_write $O/pmc_f32_fetch $O/pmc_f32_write
 echo done
