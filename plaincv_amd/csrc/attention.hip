@@ -305,12 +305,17 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : PCV_ATTN_FWD_OCC) void attn_fw
         uint32_t okbits = 0xFFFFu;
         if constexpr (MASK) {
           okbits = 0u;
+          // bounds relative to this lane's first key, through readfirstlane (convergent: the
+          // compiler cannot hoist these compares out of the boundary path into every tile, as it
+          // did with the 16 key < T compares -- ~35 VALU and SGPR spills per interior tile)
+          const int kl = __builtin_amdgcn_readfirstlane(kb * 64) + 4 * g;
+          const int tl = __builtin_amdgcn_readfirstlane(T) - kl;
 #pragma unroll
           for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const int key = kb * 64 + 16 * t + 4 * g + r;
-              bool ok = key < T;
+              const int key = kl + 16 * t + r;
+              bool ok = 16 * t + r < tl;
               if (CAUSAL) ok = ok && key <= myq;
               if (doc) ok = ok && key >= myds[gq];
               s[gq][t][r] = ok ? s[gq][t][r] : NEG_BIG;

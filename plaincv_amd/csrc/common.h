@@ -162,13 +162,21 @@ __device__ __forceinline__ float xsum32(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// max of two scores as one v_max_f32: fmaxf adds a NaN-canonicalising v_max x, x per operand
+// whose producer is not known canonical (a permlane swap, an MFMA); the row maxima here are over
+// finite scores or the -inf / NEG_BIG of masked ones
+__device__ __forceinline__ float vmax_nc(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ float xmax16(float v) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  return vmax_nc(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 __device__ __forceinline__ float xmax32(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  return vmax_nc(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 // over the 4 rows of the wave (lanes l, l^16, l^32, l^48 all receive it)
 __device__ __forceinline__ float xsum_rows(float v) { return xsum32(xsum16(v)); }
