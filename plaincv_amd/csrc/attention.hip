@@ -456,7 +456,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
   constexpr int KS = DH / 32, DT = DH / 16, KG = 2, CPR = DH / 8;
   constexpr int TILE = 64 * DH;
   __shared__ __attribute__((aligned(16))) bf16 qo_smem[2 * 2 * TILE];   // [buffer][Q|dO][TILE]
-  __shared__ float ld_smem[2 * 128];                                    // [buffer][lse|delta][64]
+  __shared__ __attribute__((aligned(16))) float ld_smem[2 * 128];       // [buffer][lse|delta][64]
   int kb, h, b;
   light_last<CAUSAL>(kb, h, b);
   const int T = a.T;
@@ -561,33 +561,41 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
             dp[gk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[gk][ks], ks ? dp[gk] : kZero4, 0, 0, 0);
           }
         }
+        // the 4 queries' lse / delta as one 16-B read each (a per-element read waited on its own
+        // LDS round trip inside a per-element branch); the boundary test in a path of its own
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(Ls + 16 * t + 4 * g);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(Dl + 16 * t + 4 * g);
+        auto probs = [&](auto interior_t) {
+          constexpr bool INTERIOR = decltype(interior_t)::value;
 #pragma unroll
-        for (int gk = 0; gk < KG; ++gk) {
-          const int mykey = kw + gk * 16 + (lane & 15);
-          uint32_t wt = 0;
-          if (DROP) wt = (uint32_t)a.mask[drop_word(qb * 64 + 16 * t + 4 * g, mykey, a.n64)] >> (mykey & 3);
+          for (int gk = 0; gk < KG; ++gk) {
+            const int mykey = kw + gk * 16 + (lane & 15);
+            uint32_t wt = 0;
+            if (DROP) wt = (uint32_t)a.mask[drop_word(qb * 64 + 16 * t + 4 * g, mykey, a.n64)] >> (mykey & 3);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int ql = 16 * t + 4 * g + r;
-            float pv = __builtin_amdgcn_exp2f(fmaf(sv[gk][r], c2, -Ls[ql]));
-            if (!interior) {
-              const int qq = qb * 64 + ql;
-              bool ok = mykey < T && qq < T;
-              if (CAUSAL) ok = ok && mykey <= qq;
-              if (doc) ok = ok && qq < myde[gk];
-              pv = ok ? pv : 0.f;
+            for (int r = 0; r < 4; ++r) {
+              float pv = __builtin_amdgcn_exp2f(fmaf(sv[gk][r], c2, -l4[r]));
+              if constexpr (!INTERIOR) {
+                const int qq = qb * 64 + 16 * t + 4 * g + r;
+                bool ok = mykey < T && qq < T;
+                if (CAUSAL) ok = ok && mykey <= qq;
+                if (doc) ok = ok && qq < myde[gk];
+                pv = ok ? pv : 0.f;
+              }
+              float dpv = dp[gk][r];
+              float pd = pv;
+              if (DROP) {   // keep bit as an all-ones/zero mask; dV's 1/keep scale is applied at the store
+                const uint32_t km = (uint32_t)__builtin_amdgcn_sbfe((int)wt, 4 * r, 1);
+                pd = __uint_as_float(__float_as_uint(pv) & km);
+                dpv = __uint_as_float(__float_as_uint(dpv) & km) * a.drop_scale;
+              }
+              p[gk][t][r] = pd;
+              ds[gk][t][r] = pv * (dpv - d4[r]);
             }
-            float dpv = dp[gk][r];
-            float pd = pv;
-            if (DROP) {   // keep bit as an all-ones/zero mask; dV's 1/keep scale is applied at the store
-              const uint32_t km = (uint32_t)__builtin_amdgcn_sbfe((int)wt, 4 * r, 1);
-              pd = __uint_as_float(__float_as_uint(pv) & km);
-              dpv = __uint_as_float(__float_as_uint(dpv) & km) * a.drop_scale;
-            }
-            p[gk][t][r] = pd;
-            ds[gk][t][r] = pv * (dpv - Dl[ql]);
           }
-        }
+        };
+        if (interior) probs(std::true_type{});
+        else probs(std::false_type{});
       }
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
@@ -707,28 +715,33 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : PCV_ATTN_DQ_OCC) void attn_bwd
             dp[gq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, of[gq][ks], ks ? dp[gq] : kZero4, 0, 0, 0);
           }
         }
+        auto probs = [&](auto interior_t) {   // the boundary test in a path of its own
+          constexpr bool INTERIOR = decltype(interior_t)::value;
 #pragma unroll
-        for (int gq = 0; gq < QG; ++gq) {
-          const int myq = qw + gq * 16 + (lane & 15);
-          uint32_t wt = 0;
-          if (DROP) wt = (uint32_t)a.mask[drop_word(myq, kb * 64 + 16 * t + 4 * g, a.n64)] >> (4 * (myq & 3));
+          for (int gq = 0; gq < QG; ++gq) {
+            const int myq = qw + gq * 16 + (lane & 15);
+            uint32_t wt = 0;
+            if (DROP) wt = (uint32_t)a.mask[drop_word(myq, kb * 64 + 16 * t + 4 * g, a.n64)] >> (4 * (myq & 3));
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float pv = __builtin_amdgcn_exp2f(fmaf(sv[gq][r], c2, -myl[gq]));
-            if (!interior) {
-              const int key = kb * 64 + 16 * t + 4 * g + r;
-              bool ok = myq < T && key < T;
-              if (CAUSAL) ok = ok && key <= myq;
-              if (doc) ok = ok && key >= myds[gq];
-              pv = ok ? pv : 0.f;
+            for (int r = 0; r < 4; ++r) {
+              float pv = __builtin_amdgcn_exp2f(fmaf(sv[gq][r], c2, -myl[gq]));
+              if constexpr (!INTERIOR) {
+                const int key = kb * 64 + 16 * t + 4 * g + r;
+                bool ok = myq < T && key < T;
+                if (CAUSAL) ok = ok && key <= myq;
+                if (doc) ok = ok && key >= myds[gq];
+                pv = ok ? pv : 0.f;
+              }
+              float dpv = dp[gq][r];
+              if (DROP)
+                dpv = __uint_as_float(__float_as_uint(dpv) & (uint32_t)__builtin_amdgcn_sbfe((int)wt, r, 1)) *
+                      a.drop_scale;
+              ds[gq][t][r] = pv * (dpv - myd[gq]);
             }
-            float dpv = dp[gq][r];
-            if (DROP)
-              dpv = __uint_as_float(__float_as_uint(dpv) & (uint32_t)__builtin_amdgcn_sbfe((int)wt, r, 1)) *
-                    a.drop_scale;
-            ds[gq][t][r] = pv * (dpv - myd[gq]);
           }
-        }
+        };
+        if (interior) probs(std::true_type{});
+        else probs(std::false_type{});
       }
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
