@@ -325,7 +325,12 @@ int pcv_attn_bwd_f32(const float* qkv, int64_t ldqkv, const float* o, int64_t ld
  * x / dx / dym rows: stride ldx / lddx / lddym (T * D for the cls rows).  pcv_vit_head_ok(B, D, K):
  * B <= 64, D <= 128 multiple of 32, K <= 256.  work (optional, 16-B aligned, zero-filled once before
  * first use, pcv_vit_head_work_floats(B, D, K) floats): one workgroup per 16 rows with a
- * deterministic last-workgroup reduction of the cross-row sums; NULL: one workgroup. */
+ * deterministic last-workgroup reduction of the cross-row sums; NULL: one workgroup.
+ * defer != 0 (split form with dlogits, B > 16, K and D multiples of 8): no last-workgroup reduction;
+ * each workgroup leaves its partial row at work + 4 + j * (8 + K + 2D) -- [loss/B, accuracy/B, 0 x 6 |
+ * dhead_bias K | dscale D | dbias D] -- metrics[0..8) are zeroed (metrics must hold 8 floats), and a
+ * later launch adds the rows into metrics / dhead_bias / dscale / dbias (the grouped weight-gradient
+ * launch's fold jobs, pcv_gemm_grouped_run). */
 int pcv_vit_head_ok(int B, int D, int K);
 int64_t pcv_vit_head_work_floats(int B, int D, int K);
 int pcv_vit_head(const float* x, int64_t ldx, const float* ln_scale, const float* ln_bias, float eps, const void* W,
@@ -333,7 +338,7 @@ int pcv_vit_head(const float* x, int64_t ldx, const float* ln_scale, const float
                  float* logits, int64_t ldl, float* metrics, float grad_scale, float* dlogits, void* dlogits_b,
                  int64_t ldd, float* dx, int64_t lddx, float* dscale, float* dbias, float* dhead_bias, void* dym,
                  int64_t lddym, float drop_rate, const uint32_t* seed, uint32_t site, int64_t row_stride,
-                 float* work, void* stream);
+                 float* work, int defer, void* stream);
 /* ---------------------------------------------------------------- loss ----
  * Softmax cross-entropy + argmax accuracy per row, gradient (softmax-onehot)*grad_scale
  * (engine/flax_engine.py:13-22; train_lm.py:181-186).  pcv_mean2: deterministic means. */

@@ -28,7 +28,8 @@ namespace pcv {
 constexpr int VH_THREADS = 1024, VH_WAVES = 16, VH_BMAX = 64, VH_DMAX = 128, VH_KMAX = 256;
 
 struct VitHeadArgs {
-  float* work;                  // split form: [4] ticket (int) + [nblk][2 + K + 2D] partials; null: one workgroup
+  float* work;                  // split form: [4] ticket (int) + [nblk][8 + K + 2D] partials; null: one workgroup
+  int defer;                    // split form: the partial rows are summed by a later launch (no last-workgroup sum)
   const float* x; int64_t ldx;
   const float* ln_s; const float* ln_b; float eps;
   const bf16* W; int64_t ldw; const float* bias;
@@ -53,7 +54,10 @@ __host__ __device__ constexpr size_t vh_lds(int D, int K, int R) {   // R rows p
   return (size_t)R * D * 4 + (size_t)R * (D + 8) * 2 + (size_t)R * (LW + 4) * 4 +
          (size_t)R * (K32 + 8) * 2 + 4 * R * 4 + 2 * VH_WAVES * 4 + 2 * 8 * VH_DMAX * 4 + 16;
 }
-__host__ __device__ constexpr int vh_part_floats(int D, int K) { return 2 + K + 2 * D; }
+// partial row of one workgroup: [loss / B, accuracy / B, 0 x 6 | bias grad K | scale grad D | bias grad D]
+// (8-float metrics slot: with K, D multiples of 8 every segment starts 32-B aligned for the fold)
+constexpr int VH_PM = 8;
+__host__ __device__ constexpr int vh_part_floats(int D, int K) { return VH_PM + K + 2 * D; }
 
 // MT 16-row M tiles per workgroup: 4 (one workgroup, all B <= 64 rows) or 1 (split form)
 template <int MT>
@@ -208,7 +212,16 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
   if (tid == 0) {
     float l = 0.f, c = 0.f;
     for (int w = 0; w < VH_WAVES; ++w) { l += red[w]; c += red[VH_WAVES + w]; }
-    if (split) { part[0] = l; part[1] = c; }
+    if (split) {
+      part[0] = a.defer ? l / B : l;
+      part[1] = a.defer ? c / B : c;
+#pragma unroll
+      for (int e = 2; e < VH_PM; ++e) part[e] = 0.f;
+      // deferred sum: the fold launch adds every row into metrics, which start from zero
+      if (a.defer && blockIdx.x == 0)
+#pragma unroll
+        for (int e = 0; e < VH_PM; ++e) a.metrics[e] = 0.f;
+    }
     else { a.metrics[0] = l / B; a.metrics[1] = c / B; }
   }
   if (a.need_grad) {
@@ -216,7 +229,7 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
   if (a.gbias && tid < K) {
     float sb = 0.f;
     for (int b = 0; b < Bl; ++b) sb += Ls[b * LL + tid];
-    if (split) part[2 + tid] = sb;
+    if (split) part[VH_PM + tid] = sb;
     else a.gbias[tid] += sb;
   }
   __syncthreads();
@@ -287,11 +300,11 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
   if (tid < D) {
     float s1 = 0.f, s0 = 0.f;
     for (int rg = 0; rg < 8; ++rg) { s1 += colred[rg * VH_DMAX + tid]; s0 += colred[8 * VH_DMAX + rg * VH_DMAX + tid]; }
-    if (split) { part[2 + K + tid] = s1; part[2 + K + D + tid] = s0; }
+    if (split) { part[VH_PM + K + tid] = s1; part[VH_PM + K + D + tid] = s0; }
     else { a.gs[tid] += s1; a.gc[tid] += s0; }
   }
   }   // need_grad
-  if (!split) return;
+  if (!split || a.defer) return;
   // ---- split form: the last workgroup adds every workgroup's partials, in workgroup order
   __syncthreads();
   if (tid == 0) {
@@ -314,12 +327,12 @@ __global__ __launch_bounds__(VH_THREADS) void vit_head_kernel(VitHeadArgs a) {
   if (a.need_grad) {
     if (a.gbias && tid < K) {
       float sb = 0.f;
-      for (int j = 0; j < nb; ++j) sb += P[j * PF + 2 + tid];
+      for (int j = 0; j < nb; ++j) sb += P[j * PF + VH_PM + tid];
       a.gbias[tid] += sb;
     }
     if (tid < D) {
       float s1 = 0.f, s0 = 0.f;
-      for (int j = 0; j < nb; ++j) { s1 += P[j * PF + 2 + K + tid]; s0 += P[j * PF + 2 + K + D + tid]; }
+      for (int j = 0; j < nb; ++j) { s1 += P[j * PF + VH_PM + K + tid]; s0 += P[j * PF + VH_PM + K + D + tid]; }
       a.gs[tid] += s1;
       a.gc[tid] += s0;
     }
@@ -339,7 +352,8 @@ extern "C" int pcv_vit_head(const float* x, int64_t ldx, const float* ln_scale, 
                             void* yf, int64_t ldy, float* logits, int64_t ldl, float* metrics, float grad_scale,
                             float* dlogits, void* dlogits_b, int64_t ldd, float* dx, int64_t lddx, float* dscale,
                             float* dbias, float* dhead_bias, void* dym, int64_t lddym, float drop_rate,
-                            const uint32_t* seed, uint32_t site, int64_t row_stride, float* work, void* stream) {
+                            const uint32_t* seed, uint32_t site, int64_t row_stride, float* work, int defer,
+                            void* stream) {
   if (!pcv_vit_head_ok(B, D, K) || !x || !ln_scale || !ln_bias || !W || !bias || !labels || !yf || !logits ||
       !metrics || ldw < K || (ldw & 7))
     return PCV_EINVAL;
@@ -361,7 +375,11 @@ extern "C" int pcv_vit_head(const float* x, int64_t ldx, const float* ln_scale, 
   }
   a.seed = seed; a.site = site; a.row_stride = row_stride;
   a.work = work;
+  a.defer = defer ? 1 : 0;
   if (work && !pcv_aligned16(work)) return PCV_EALIGN;
+  // deferred partial sums (a later launch folds the rows): split form with gradients only, and
+  // 8-float-aligned segments
+  if (defer && (!work || B <= 16 || !need_grad || (K & 7) || (D & 7))) return PCV_EINVAL;
   if (work && B > 16) {
     hipLaunchKernelGGL(vit_head_kernel<1>, dim3((B + 15) / 16), dim3(VH_THREADS), vh_lds(D, K, 16),
                        (hipStream_t)stream, a);

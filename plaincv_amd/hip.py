@@ -94,7 +94,7 @@ SIGNATURES = {
     "pcv_vit_head_ok": [I32, I32, I32],
     "pcv_vit_head_work_floats": [I32, I32, I32],
     "pcv_vit_head": [P, I64, P, P, F32, P, I64, P, P, I32, I32, I32, P, I64, P, I64, P, F32, P, P, I64, P, I64, P, P,
-                     P, P, I64, F32, P, U32, I64, P, P],
+                     P, P, I64, F32, P, U32, I64, P, I32, P],
     "pcv_xent_fwd_bwd": [P, I64, I32, P, I64, I32, P, P, P, I64, F32, P],
     "pcv_mean2": [P, P, I64, F32, P, P],
     "pcv_adamw_step": [P, P, P, P, P, P, P, I32, F32, F32, F32, F32, F32, F32, I32, I32, P, P, P],

@@ -607,10 +607,12 @@ def vit_head_ok(B, D, K):
 
 def vit_head(x, ln_scale, ln_bias, W, bias, labels, yf, logits, metrics, grad_scale=1.0, dlogits=None,
              dlogits_b=None, dx=None, dscale=None, dbias=None, dym=None, drop_rate=0.0, seed=None, site=0,
-             row_stride=1, eps=1e-6, dhead_bias=None, work=None):
+             row_stride=1, eps=1e-6, dhead_bias=None, work=None, defer=False):
     """Fused ViT head (pcv_vit_head): final LayerNorm of the cls rows x [B, D] (strided), logits, CE
     metrics and, with dlogits given, the whole head backward down to the top block's dropout VJP.
-    work (vit_head_work(B, D, K)): one workgroup per 16 rows instead of one for all."""
+    work (vit_head_work(B, D, K)): one workgroup per 16 rows instead of one for all.  defer: the
+    workgroups leave their cross-row partial sums in work for a later fold (vit_head_fold_views);
+    metrics must then hold 8 floats."""
     B, D = x.shape
     Kc = bias.numel()
     _chk(vit_head_ok(B, D, Kc), "vit_head shape")
@@ -624,13 +626,25 @@ def vit_head(x, ln_scale, ln_bias, W, bias, labels, yf, logits, metrics, grad_sc
              "vit_head grads")
     if work is not None:
         _chk(work.dtype == F32 and work.numel() >= hip.load().pcv_vit_head_work_floats(B, D, Kc), "vit_head work")
+    if defer:
+        _chk(work is not None and grad and B > 16 and Kc % 8 == 0 and D % 8 == 0 and metrics.numel() >= 8,
+             "vit_head defer")
     _dev(x, ln_scale, ln_bias, W, bias, labels, yf, logits, metrics, dlogits, dlogits_b, dx, dscale, dbias, dym, seed,
          dhead_bias, work)
     hip.call("pcv_vit_head", ptr(x), _ld(x), ptr(ln_scale), ptr(ln_bias), float(eps), ptr(W), _ld(W), ptr(bias),
              ptr(labels), B, D, Kc, ptr(yf), _ld(yf), ptr(logits), _ld(logits), ptr(metrics), float(grad_scale),
              ptr(dlogits), ptr(dlogits_b), _ld(dlogits) if grad else 0, ptr(dx), _ld(dx) if grad else 0,
              ptr(dscale), ptr(dbias), ptr(dhead_bias), ptr(dym), _ld(dym) if grad else 0, float(drop_rate), ptr(seed),
-             int(site) & 0xFFFFFFFF, int(row_stride), ptr(work), stream_ptr())
+             int(site) & 0xFFFFFFFF, int(row_stride), ptr(work), int(bool(defer)), stream_ptr())
+
+
+def vit_head_fold_views(work, B, D, K):
+    """The deferred head's partial rows as fold operands [(rows, target-kind)]: metrics [nblk, 8],
+    head-bias gradient [nblk, K], LayerNorm scale / bias gradients [nblk, D] (row stride 8 + K + 2 D)."""
+    nblk, pf = (B + 15) // 16, 8 + K + 2 * D
+    rows = work[4:4 + nblk * pf].view(nblk, pf)
+    return {"metrics": rows[:, :8], "dhead_bias": rows[:, 8:8 + K], "dscale": rows[:, 8 + K:8 + K + D],
+            "dbias": rows[:, 8 + K + D:]}
 
 
 def vit_head_work(B, D, K, device):

@@ -244,7 +244,7 @@ class ViTRunner:
         self.dlogits_b = torch.zeros(B, self.Kcp, dtype=bf, device=dev)[:, : self.Kc]
         self.row_loss = e(B)
         self.row_correct = e(B)
-        self.metrics = torch.zeros(2, dtype=f32, device=dev)  # [loss, accuracy]
+        self.metrics = torch.zeros(8, dtype=f32, device=dev)  # [loss, accuracy] (+6: the deferred head's fold row)
         # backward workspaces.  Weight/bias/norm-parameter gradients may run on a side stream
         # beside the data-gradient chain (side_stream=True), so every activation gradient they
         # read has its own per-layer buffer (nothing is overwritten while the side stream may
@@ -332,6 +332,15 @@ class ViTRunner:
                         replicate((k, i), w[k])
                     if i + 1 < len(self.w):
                         replicate(("gb1", i), w["gb1"])   # produced by the LayerNorm_0 backward of block i+1
+            # the split head's cross-row sums (loss, accuracy, head-bias and final-LayerNorm parameter
+            # gradients) fold in this launch instead of a last-workgroup reduction inside the head
+            # (its agent-scope fence and cross-XCD reads cost ~7.5 us at the end of the head)
+            self.head_defer = (self.fused_head and self.head_work is not None and B > 16 and self.Kc % 8 == 0
+                               and D % 8 == 0 and os.environ.get("PCV_VIT_HEAD_DEFER", "1") != "0")
+            if self.head_defer:
+                v = K.vit_head_fold_views(self.head_work, B, D, self.Kc)
+                items += [("fold", v["metrics"], self.metrics), ("fold", v["dhead_bias"], self.gbh),
+                          ("fold", v["dscale"], self.gsf), ("fold", v["dbias"], self.gcf)]
             self.wgrad = K.GroupedWGrad(items, dev)
 
     # ------------------------------------------------------------ views
@@ -451,7 +460,8 @@ class ViTRunner:
                        dx=self.dx.view(B, T * D)[:, :D] if g else None, dscale=self.gsf if g else None,
                        dbias=self.gcf if g else None, dym=self.dym[L - 1].view(B, T * D)[:, :D] if g else None,
                        drop_rate=rate, seed=seed, site=site_mlp_out(L - 1), row_stride=T,
-                       dhead_bias=self.gbh if g else None, work=self.head_work)
+                       dhead_bias=self.gbh if g else None, work=self.head_work,
+                       defer=bool(g and getattr(self, "head_defer", False)))
             return self.metrics
         if self.bn:   # statistics over every row, normalise the cls rows only (vit_small.py:121-125)
             K.batchnorm_stats(self.xs[-1], *self.raf, *self.bstf, self.bn_ws, train)

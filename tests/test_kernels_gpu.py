@@ -510,14 +510,15 @@ def test_transpose_batch(dev):
         assert torch.equal(dst, src.t())
 
 
-@pytest.mark.parametrize("split", [True, False])
+@pytest.mark.parametrize("split", [True, False, "defer"])
 @pytest.mark.parametrize("B,D,Kc,rate", [(64, 128, 200, 0.1), (4, 64, 10, 0.0), (33, 96, 256, 0.3), (1, 32, 1, 0.0)])
 def test_vit_head_fused(dev, B, D, Kc, rate, split):
     """csrc/vit_head.hip vs torch fp32 on the same bf16-rounded GEMM operands: LayerNorm of strided cls
     rows, logits, CE metrics, dlogits, the head bias / LN parameter gradients, dx and the dropout-VJP
     bf16 rows (dropout bits from oracle.rng at the flat index (b * T) * D + c).  split: one
     workgroup per 16 rows with the last-workgroup reduction; a second launch on the same workspace
-    (ticket reset by the kernel) reproduces the first bit for bit."""
+    (ticket reset by the kernel) reproduces the first bit for bit.  defer: the workgroups leave their
+    partial rows for a later fold (done here row by row, as the grouped launch's fold jobs)."""
     from oracle import rng
     from plaincv_amd import kernels as K
     T = 5
@@ -533,7 +534,9 @@ def test_vit_head_fused(dev, B, D, Kc, rate, split):
     labels = torch.randint(0, Kc, (B,), generator=g, dtype=torch.int32).to(dev)
     yf = torch.empty(B, D, dtype=torch.bfloat16, device=dev)
     logits = torch.empty(B, Kp, device=dev)[:, :Kc]
-    met = torch.empty(2, device=dev)
+    if split == "defer" and not (B > 16 and Kc % 8 == 0 and D % 8 == 0):
+        pytest.skip("deferred head sums need B > 16 and K, D multiples of 8")
+    met = torch.empty(8 if split == "defer" else 2, device=dev)
     dl = torch.empty(B, Kp, device=dev)[:, :Kc]
     dlb = torch.zeros(B, Kp, dtype=torch.bfloat16, device=dev)[:, :Kc]
     DX = torch.zeros(B * T, D, device=dev)
@@ -545,7 +548,13 @@ def test_vit_head_fused(dev, B, D, Kc, rate, split):
     def run():
         K.vit_head(x, s, c, W, bias, labels, yf, logits, met, grad_scale=1.0 / B, dlogits=dl, dlogits_b=dlb,
                    dx=DX.view(B, T * D)[:, :D], dscale=gs, dbias=gc, dym=DYM.view(B, T * D)[:, :D], drop_rate=rate,
-                   seed=seed, site=13, row_stride=T, dhead_bias=gb, work=work)
+                   seed=seed, site=13, row_stride=T, dhead_bias=gb, work=work, defer=split == "defer")
+        if split == "defer":
+            v = K.vit_head_fold_views(work, B, D, Kc)
+            assert float(met.abs().sum()) == 0.0            # zeroed by the head, for the fold to add into
+            for key, out in (("metrics", met), ("dhead_bias", gb), ("dscale", gs), ("dbias", gc)):
+                for j in range(v[key].shape[0]):
+                    out += v[key][j]
     run()
     if split:
         first = [t.clone() for t in (met, gs, gc, gb, DX, DYM, dl)]
