@@ -954,6 +954,15 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         if (t < nt) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(row_frag<DH>(Ks, 64 * c + 16 * t, 0), qf, kZero4, 0, 0, 0);
+      // the chunk's V fragments read under the score MFMAs and the softmax (left to the scheduler
+      // they were read right before the P.V MFMAs, each pair behind a full LDS wait)
+      bf16x8 vts[2][DT];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int d = 0; d < DT; ++d)
+          if (2 * u < nt) vts[u][d] = tr_frag<DH>(Vs, 2 * c + u, 16 * d);
+      __builtin_amdgcn_sched_barrier(0);
       if (64 * c + 16 * nt > Tl) {   // chunk reaches past T: padded keys -> NEG_BIG
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -965,7 +974,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
       float bmax = NEG_BIG;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
-        if (t < nt) bmax = fmaxf(bmax, fmaxf(fmaxf(s[t][0], s[t][1]), fmaxf(s[t][2], s[t][3])));
+        if (t < nt) bmax = vmax3_nc(vmax3_nc(bmax, s[t][0], s[t][1]), s[t][2], s[t][3]);
       bmax = xmax_rows(bmax);
       const float cand = bmax * c2;
       if (__ballot(cand > m2 + 8.f) != 0) {   // a row's max moved by > 2^8: rescale (wave-uniform)
@@ -1010,7 +1019,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
           const bf16x8 pl = pack8(r0, r1);
 #pragma unroll
           for (int d = 0; d < DT; ++d) {
-            const bf16x8 vt = tr_frag<DH>(Vs, 2 * c + u, 16 * d);
+            const bf16x8 vt = vts[u][d];
             acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vt, acc[d], 0, 0, 0);
             acc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pl, vt, acc[d], 0, 0, 0);
           }
