@@ -51,6 +51,13 @@ def case(M, Kd, mode, N=128):
                              tb=True, ln_x=x, ln_dscale=ds, ln_dbias=db, col_reps=-1)
 
 
+# cold operands: cycle through 8 operand sets (8 x ~40 MB > the 256 MB MALL), so no launch finds its
+# inputs in an XCD's L2 -- as in the step, where each launch reads what the previous kernel wrote
+cold = [case(16448, 256, 2) for _ in range(8)]
+cold1 = [case(16448, 256, 1) for _ in range(8)]
+print(f"cold operands, M=16448 K=256: mode 2 {tm(lambda: [f() for f in cold], iters=10) / 8:6.2f} us  "
+      f"mode 1 {tm(lambda: [f() for f in cold1], iters=10) / 8:6.2f} us", flush=True)
+del cold, cold1
 for mode in (1, 2):
     for Kd in (128, 256):
         t = {M: tm(case(M, Kd, mode)) for M in (16448, 16384, 16320)}
