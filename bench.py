@@ -60,7 +60,12 @@ VIT_C2 = dict(dataset="tiny_imagenet_synthetic", batch_size=64, image_size=64, n
 VIT_C4 = {"soap": dict(VIT_C2, optim="soap", eps=1e-8, precondition_frequency=10, vit_dtype="float32"),
           "shampoo": dict(VIT_C2, optim="shampoo", eps=1e-4, shampoo_exponent=0.25, adam_eps=1e-8,
                           vit_dtype="float32")}
+# configs[1] in the reference ViT's own precision (models/vit_small.py:95 computes in fp32): the same
+# workload on the exact-fp32 runner, reported beside the bf16 headline (a sub-line of the default run)
+VIT_C2_F32 = dict(VIT_C2, vit_dtype="float32")
 WORKLOAD_NAMES = {"vit_c2": "vit_small_tinyimagenet_muon (BASELINE configs[1])",
+                  "vit_c2_f32": "vit_small_tinyimagenet_muon_fp32 (BASELINE configs[1] workload, reference fp32 "
+                                "precision)",
                   "vit_c4_soap": "vit_small_tinyimagenet_soap (BASELINE configs[3] optimizer)",
                   "vit_c4_shampoo": "vit_small_tinyimagenet_shampoo (BASELINE configs[3] optimizer)"}
 
@@ -272,7 +277,8 @@ def optimizer_ms(tx, store, opt_state, gscale=None, iters=5):
 
 def bench_vit(args):
     rank, local_rank, world, dev = dp.init_from_env()
-    cfg = Config(VIT_C2 if args.workload == "vit_c2" else VIT_C4[args.workload.split("_")[-1]])
+    cfg = Config({"vit_c2": VIT_C2, "vit_c2_f32": VIT_C2_F32}.get(args.workload)
+                 or VIT_C4[args.workload.split("_")[-1]])
     if args.shard_opt:
         cfg.shard_optimizer = True
     m = vit_model(cfg)
@@ -318,7 +324,9 @@ def bench_vit(args):
                "data": "synthetic (uint8 images U[0,255], labels U[0,200), seeded, resident in HBM)",
                "config": {"workload": WORKLOAD_NAMES[args.workload], "global_batch": world * B,
                           "per_gpu_batch": B, "image": [64, 64, 3], "classes": 200, "tokens": 257,
-                          "optimizer": cfg.optim, "parallelism": f"dp{world}"},
+                          "optimizer": cfg.optim, "parallelism": f"dp{world}",
+                          "inputs": "copy-in (one static batch buffer per step)" if ring is None else
+                                    "input ring (one captured graph per resident batch slot, read in place)"},
                "steps_per_sec": round(sps, 3), "tflops_per_gpu": round(flops * sps / 1e12, 3),
                "final_loss": round(loss, 4)}
         out["roofline"] = (vit_roofline_f32(state, shape, cfg.vit_dropout) if cfg.vit_dtype == "float32"
@@ -546,12 +554,15 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="vit_c2",
-                    choices=["vit_c2", "vit_c4_soap", "vit_c4_shampoo", "lm124m", "lm420m", "dp_stub"])
+                    choices=["vit_c2", "vit_c2_f32", "vit_c4_soap", "vit_c4_shampoo", "lm124m", "lm420m",
+                             "dp_stub"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--lm-micro-batch", type=int, default=None, help="default: the workload's config")
     ap.add_argument("--lm-accum", type=int, default=None, help="default: the workload's config")
     ap.add_argument("--no-lm", action="store_true", help="skip the attached 124M LM (configs[2]) line")
+    ap.add_argument("--no-f32", action="store_true",
+                    help="skip the attached vit_c2_f32 line (configs[1] in the reference's fp32 precision)")
     ap.add_argument("--lm-steps", type=int, default=10)
     ap.add_argument("--lm-warmup", type=int, default=2)
     ap.add_argument("--shard-opt", action="store_true",
@@ -568,6 +579,14 @@ def main():
         out = bench_lm(args)
     else:
         out = bench_vit(args)
+        if args.workload == "vit_c2" and not args.no_f32:
+            a2 = argparse.Namespace(**vars(args))
+            a2.workload, a2.no_cpu_baseline = "vit_c2_f32", True
+            f32 = bench_vit(a2)
+            if out is not None:
+                f32["cpu_baseline"] = dict(out["cpu_baseline"], shared_with="headline vit_c2 line (the same fp32 "
+                                           "oracle workload)") if out.get("cpu_baseline") else None
+                out["vit_c2_f32"] = f32
         if not args.no_lm:   # every rank: the LM line is a DDP run over the same ranks
             a2 = argparse.Namespace(**vars(args))
             a2.steps, a2.warmup, a2.workload = args.lm_steps, args.lm_warmup, "lm124m"

@@ -380,6 +380,13 @@ int pcv_muon_prep(const void* mats, int nmats, int nnorm, int64_t max_elems, flo
                   const int* step, const float* gscale, void* stream);
 int pcv_muon_apply(const void* mats, int nmats, int64_t max_elems, float lr, float wd, int shape_scale,
                    int apply, void* stream);
+/* muon_adaptive (factory.py:457,475 -> optax.contrib.muon adaptive=True): dual[m] += <mu_hat, O>_F per
+ * record (dual: nmats zeroed doubles; mu_hat re-formed from mu, g, *step, *gscale as pcv_muon_prep did),
+ * then pcv_muon_apply_dual scales each record's orthogonalised update by dual[m] before the shape scale. */
+int pcv_muon_dual_dot(const void* mats, int nmats, int64_t max_elems, float beta, int nesterov, const int* step,
+                      const float* gscale, double* dual, void* stream);
+int pcv_muon_apply_dual(const void* mats, int nmats, int64_t max_elems, float lr, float wd, int shape_scale,
+                        int apply, const double* dual, void* stream);
 int pcv_muon_mat_size(void);
 /* Batched bf16 transpose (64x64 tiles, many matrices per launch): records
  * {src, dst, rows, cols, ld_src, ld_dst, first_tile} (pcv_transpose_rec_size() bytes),

@@ -18,10 +18,45 @@ def rnd(x, bf16: bool):
     return x
 
 
+class _RoundGrad(torch.autograd.Function):
+    """Identity forward; the backward rounds the incoming gradient to bf16 (a gradient that the
+    device backward stores in bf16 -- as the dY operand of the bf16 dgrad / wgrad GEMMs)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+_GRAD_STORAGE = {"bf16": False}
+
+
+class bf16_grad_storage:
+    """Context manager: inside it, every bf16-placement ``mm`` also rounds the gradient of its output
+    to bf16, modelling a backward that keeps each Dense output's gradient as a bf16 GEMM operand
+    (the HIP ViT's dgrad / wgrad chains).  Used to measure the rounding-noise spread that such a
+    backward carries (tests/test_golden.py); the reference's own placement model is the default."""
+
+    def __enter__(self):
+        self.prev = _GRAD_STORAGE["bf16"]
+        _GRAD_STORAGE["bf16"] = True
+        return self
+
+    def __exit__(self, *exc):
+        _GRAD_STORAGE["bf16"] = self.prev
+        return False
+
+
 def mm(x, w, bf16: bool = False):
     """Dense contraction x @ w; in bf16 placement both operands are rounded to
     bf16 and accumulated in fp32 (the MFMA bf16 contract)."""
-    return rnd(x, bf16) @ rnd(w, bf16)
+    out = rnd(x, bf16) @ rnd(w, bf16)
+    if bf16 and _GRAD_STORAGE["bf16"] and out.requires_grad and out.dtype != torch.float64:
+        out = _RoundGrad.apply(out)
+    return out
 
 
 def layernorm(x, scale, bias, eps=1e-6):

@@ -97,13 +97,16 @@ def newton_schulz(x, coeffs=(3.4445, -4.7750, 2.0315), steps=5, eps=1e-8):
 
 def muon(learning_rate, ns_coeffs=(3.4445, -4.7750, 2.0315), ns_steps=5, beta=0.95, eps=1e-8,
          weight_decay=0.0, nesterov=True, adam_b1=0.9, adam_b2=0.999, adam_eps_root=0.0,
-         adam_weight_decay=0.0, adam_nesterov=True, shape_scale=True, routed=None):
+         adam_weight_decay=0.0, adam_nesterov=True, shape_scale=True, routed=None, adaptive=False):
     """partition{'muon': chain(scale_by_muon, add_decayed_weights(wd), scale_by_lr),
     'adam': adamw(b1, b2, eps, eps_root, wd, nesterov)}; labels from
     optim/muon.py:120-129 (should_use_matrix_preconditioner).
 
     scale_by_muon: mu = beta*mu + (1-beta)*g; nesterov mu_hat = beta*mu/(1-beta^(t+1))
-    + (1-beta)*g/(1-beta^t); NS5 orthogonalisation; x sqrt(max(1, fan_out/fan_in)).
+    + (1-beta)*g/(1-beta^t); NS5 orthogonalisation; adaptive (factory.py:457,475 muon_adaptive):
+    O <- <mu_hat, O>_F * O, optax.contrib.muon's dual-norm scaling (einsum('ij,ij,ab->ab', mu_hat, O,
+    O), arXiv 2409.20325; recalled from the optax source -- optax is absent here, so unpinned);
+    x sqrt(max(1, fan_out/fan_in)).
     ``adam_nesterov``/``shape_scale`` are switches for the two recalled optax details
     (SURVEY.md §7 hard part (i))."""
     routed = routed or should_use_matrix_preconditioner
@@ -124,6 +127,8 @@ def muon(learning_rate, ns_coeffs=(3.4445, -4.7750, 2.0315), ns_steps=5, beta=0.
                 else:
                     mh = mu[k] / (1.0 - beta ** count)
                 o = newton_schulz(mh, ns_coeffs, ns_steps, eps)
+                if adaptive:
+                    o = (mh * o).sum() * o
                 if shape_scale:
                     o = o * max(1.0, p.shape[1] / p.shape[0]) ** 0.5
                 if weight_decay != 0.0:
@@ -371,7 +376,8 @@ def get_optimizer(cfg):
                   ns_steps=g("muon_ns_steps", 5), beta=g("muon_beta", 0.95), eps=g("eps", 1e-8),
                   weight_decay=wd, nesterov=g("muon_nesterov", True), adam_b1=g("beta1", 0.9),
                   adam_b2=g("beta2", 0.999), adam_eps_root=g("adam_eps_root", 0.0),
-                  adam_weight_decay=wd, adam_nesterov=g("muon_nesterov", True))
+                  adam_weight_decay=wd, adam_nesterov=g("muon_nesterov", True),
+                  adaptive=bool(g("muon_adaptive", False)))
     elif name == "soap":
         tx = soap(lr, b1=g("beta1", 0.95), b2=g("beta2", 0.95), eps=g("eps", 1e-8),
                   weight_decay=g("weight_decay", 0.01), precondition_frequency=g("precondition_frequency", 10),

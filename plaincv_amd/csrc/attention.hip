@@ -790,6 +790,24 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : PCV_ATTN_DQ_OCC) void attn_bwd
 // (measured: 8 waves spent 58 % of wave-cycles parked in s_waitcnt).
 constexpr int SH_TMAX = 320, SH_DH = 32, SH_THREADS = 1024, SH_WAVES = SH_THREADS / 64;
 
+#ifdef PCV_SH_TIMING
+// debug builds only: per-wave phase stamps (s_memrealtime, 100 MHz) of the short kernels:
+// [workgroup][wave][4] = start, prologue done, main work done, end
+__device__ uint64_t* pcv_sh_timing_buf;
+#define PCV_SHREC(slot)                                                                           \
+  do {                                                                                            \
+    if ((threadIdx.x & 63) == 0 && pcv_sh_timing_buf)                                             \
+      pcv_sh_timing_buf[((size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * \
+                             (blockDim.x >> 6) + (threadIdx.x >> 6)) * 4 + (slot)] =              \
+          __builtin_amdgcn_s_memrealtime();                                                       \
+  } while (0)
+extern "C" int pcv_debug_sh_timing(void* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(pcv_sh_timing_buf), &buf, sizeof(buf));
+}
+#else
+#define PCV_SHREC(slot) do {} while (0)
+#endif
+
 // Cooperative load of rows [0, TP) of N column blocks into swizzled LDS images: all of a thread's
 // 16-B loads are issued before the first LDS store (one HBM latency for the whole prologue).
 template <int N>
@@ -911,6 +929,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
   bf16* Ks = Qs + TP * DH;
   bf16* Vs = Ks + TP * DH;
   uint16_t* mk = reinterpret_cast<uint16_t*>(Vs + TP * DH);
+  PCV_SHREC(0);
   const int h = blockIdx.x, b = blockIdx.y;
   const int T = a.T;
   const int64_t bT = (int64_t)b * T;
@@ -922,6 +941,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
   }
   if (DROP) sh_load_mask(mk, a.mask, T);
   __syncthreads();
+  PCV_SHREC(1);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4;
   const float c2 = a.scale * LOG2E;
   // T = 16 n + 1: the tail query row is merged from per-wave partials, the tail key joins every
@@ -932,6 +952,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
                             reinterpret_cast<float*>(reinterpret_cast<char*>(shf_smem) + sh_fwd_lds<NT>(DROP) -
                                                      SH_TAILQ_FLOATS * sizeof(float)),
                             T, b, h, bT, c2);
+  PCV_SHREC(2);
   const int NG = (T + 15) / 16 - (tail1 ? 1 : 0);
   const int Tk = tail1 ? T - 1 : T;   // keys on the MFMA path
   for (int gq = wave; gq < NG; gq += SH_WAVES) {
@@ -1065,6 +1086,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
     }
     if (g == 0 && qv) a.lse2[((int64_t)b * a.H + h) * T + myq] = m2 + log2f(l);
   }
+  PCV_SHREC(3);
 }
 
 // Backward: waves 0-7 own key blocks (dK, dV of 16 keys over all queries, k = queries in the
@@ -1093,6 +1115,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
   float* Ls = reinterpret_cast<float*>(Os + SH_TMAX * DH);
   float* Dl = Ls + SH_TMAX;
   uint16_t* mk = reinterpret_cast<uint16_t*>(Dl + SH_TMAX);
+  PCV_SHREC(0);
   const int h = blockIdx.x, b = blockIdx.y;
   const int T = a.T, TP = (T + 31) & ~31, NT = TP / 16;
   const int64_t bT = (int64_t)b * T, bh = (int64_t)b * a.H + h;
@@ -1145,6 +1168,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
     }
   }
   __syncthreads();
+  PCV_SHREC(1);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
   const float c2 = a.scale * LOG2E;
   const bool tail1 = (T & 15) == 1 && T > 16;
@@ -1361,6 +1385,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
       }
     }
   }
+  PCV_SHREC(2);
   if (tail1) {   // row T-1: the 8 wave partials of each kind + the corner (T-1, T-1)
     float* corner = tailp + 3 * 8 * DH;   // {dS, Pd} of (T-1, T-1), bf16-rounded
     if (wave == 0) {   // one 32-lane dot product each for the corner's score and dPd
@@ -1411,6 +1436,7 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
       }
     }
   }
+  PCV_SHREC(3);
 }
 
 static bool short_ok(const AttnArgs& a, int dh, int causal, bool) {

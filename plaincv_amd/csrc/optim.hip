@@ -125,29 +125,72 @@ __global__ __launch_bounds__(1024) void gscale_kernel(const float* partial, int 
 __global__ void bump_kernel(int* step) { *step += 1; }
 
 // ------------------------------------------------------------------- Muon
-// mu = beta*mu + (1-beta)*g*gs; X = nesterov-corrected mu_hat, stored transposed when rows > cols
+// mu = beta*mu + (1-beta)*g*gs; X = nesterov-corrected mu_hat, stored transposed when rows > cols.
+// Four consecutive elements per thread with every load of a pass issued before its stores: the
+// element loop it replaces re-entered the memory pipeline once per element (the compiler cannot
+// move the next element's g / mu loads above this element's mu store), eight dependent round trips
+// per thread -- ~10 us for the ViT's nine matrices.  v4: 16-B accesses when the row length, the row
+// stride and the pointers allow it (every ViT kernel; the LM's 2730-wide rows take the scalar form).
+__device__ __forceinline__ bool muon_v4(const MuonMat& M) {
+  return (M.cols & 3) == 0 && (M.ld & 3) == 0 && (M.ldx & 3) == 0 &&
+         ((reinterpret_cast<uintptr_t>(M.g) | reinterpret_cast<uintptr_t>(M.mu) |
+           reinterpret_cast<uintptr_t>(M.p) | reinterpret_cast<uintptr_t>(M.x32)) & 15) == 0 &&
+         (M.upd == nullptr || (reinterpret_cast<uintptr_t>(M.upd) & 15) == 0) &&
+         (M.pb == nullptr || (reinterpret_cast<uintptr_t>(M.pb) & 7) == 0);
+}
+
 __global__ __launch_bounds__(256) void muon_prep_kernel(const MuonMat* mats, MuonHyper h, const int* step,
                                                         const float* gscale) {
   __shared__ float red[4];
   const MuonMat M = mats[blockIdx.y];
-  const int64_t n = M.rows * M.cols;
+  const int n = (int)(M.rows * M.cols);
   const float t = (float)(*step + 1);
   const float bc = 1.f - powf(h.beta, t), bcn = 1.f - powf(h.beta, t + 1.f);
   const float gs = gscale ? *gscale : 1.f;
-  const bool tr = M.rows > M.cols;
-  float s = 0.f;
-  // 32-bit element indices (the entry points reject max_elems >= 2^31): a 64-bit divide per element was
-  // the bulk of these streaming kernels' instructions
+  const bool tr = M.rows > M.cols, v4 = muon_v4(M);
   const int cols = (int)M.cols;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < (int)n; i += gridDim.x * 256) {
-    const int r = i / cols, c = i - r * cols;
-    const int64_t off = (int64_t)r * M.ld + c;
-    const float gi = M.g[off] * gs;
-    const float mi = h.beta * M.mu[off] + (1.f - h.beta) * gi;
-    M.mu[off] = mi;
-    const float xh = h.nesterov ? h.beta * mi / bcn + (1.f - h.beta) * gi / bc : mi / bc;
-    M.x32[tr ? (int64_t)c * M.ldx + r : (int64_t)r * M.ldx + c] = xh;
-    s += xh * xh;
+  float s = 0.f;
+  // 32-bit element indices (the entry points reject max_elems >= 2^31)
+  for (int i0 = (blockIdx.x * 256 + threadIdx.x) * 4; i0 < n; i0 += gridDim.x * 1024) {
+    float gv[4], mv[4];
+    int64_t off[4];
+    int rr[4], cc[4];
+    if (v4) {   // 4 | cols: the 4 elements share a row
+      const int r = i0 / cols, c = i0 - r * cols;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { rr[e] = r; cc[e] = c + e; off[e] = (int64_t)r * M.ld + c + e; }
+      const float4 g4 = *reinterpret_cast<const float4*>(M.g + off[0]);
+      const float4 m4 = *reinterpret_cast<const float4*>(M.mu + off[0]);
+      gv[0] = g4.x; gv[1] = g4.y; gv[2] = g4.z; gv[3] = g4.w;
+      mv[0] = m4.x; mv[1] = m4.y; mv[2] = m4.z; mv[3] = m4.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = i0 + e < n ? i0 + e : n - 1;
+        rr[e] = i / cols; cc[e] = i - rr[e] * cols;
+        off[e] = (int64_t)rr[e] * M.ld + cc[e];
+        gv[e] = M.g[off[e]];
+        mv[e] = M.mu[off[e]];
+      }
+    }
+    float mi[4], xh[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gi = gv[e] * gs;
+      mi[e] = h.beta * mv[e] + (1.f - h.beta) * gi;
+      xh[e] = h.nesterov ? h.beta * mi[e] / bcn + (1.f - h.beta) * gi / bc : mi[e] / bc;
+    }
+    if (v4) {
+      *reinterpret_cast<float4*>(M.mu + off[0]) = float4{mi[0], mi[1], mi[2], mi[3]};
+      if (!tr) *reinterpret_cast<float4*>(M.x32 + (int64_t)rr[0] * M.ldx + cc[0]) = float4{xh[0], xh[1], xh[2], xh[3]};
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (i0 + e >= n) break;
+      if (!v4) M.mu[off[e]] = mi[e];
+      if (tr || !v4) M.x32[tr ? (int64_t)cc[e] * M.ldx + rr[e] : (int64_t)rr[e] * M.ldx + cc[e]] = xh[e];
+      s += xh[e] * xh[e];
+    }
   }
   s = block_sum(s, red);
   if (threadIdx.x == 0) atomicAdd(M.norm2, (double)s);
@@ -167,27 +210,93 @@ __global__ __launch_bounds__(256) void muon_norm_kernel(const MuonMat* mats, flo
   }
 }
 
-// u = -lr*(O*shape_scale + wd*p); p += u
+// muon_adaptive (optax.contrib.muon adaptive=True): dual[m] += <mu_hat, O>_F, the dual norm that
+// scales the orthogonalised update (arXiv 2409.20325).  mu_hat is re-formed from the updated mu and
+// g exactly as muon_prep formed it (the step counter is bumped only after the apply launch).
+__global__ __launch_bounds__(256) void muon_dual_dot_kernel(const MuonMat* mats, MuonHyper h, const int* step,
+                                                            const float* gscale, double* dual) {
+  __shared__ float red[4];
+  const MuonMat M = mats[blockIdx.y];
+  const int64_t n = M.rows * M.cols;
+  const float t = (float)(*step + 1);
+  const float bc = 1.f - powf(h.beta, t), bcn = 1.f - powf(h.beta, t + 1.f);
+  const float gs = gscale ? *gscale : 1.f;
+  const bool tr = M.rows > M.cols;
+  const int cols = (int)M.cols;
+  float s = 0.f;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < (int)n; i += gridDim.x * 256) {
+    const int r = i / cols, c = i - r * cols;
+    const int64_t off = (int64_t)r * M.ld + c;
+    const float gi = M.g[off] * gs;
+    const float mi = M.mu[off];
+    const float xh = h.nesterov ? h.beta * mi / bcn + (1.f - h.beta) * gi / bc : mi / bc;
+    s += xh * bf2f(M.xo[tr ? (int64_t)c * M.ldx + r : (int64_t)r * M.ldx + c]);
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) atomicAdd(dual + blockIdx.y, (double)s);
+}
+
+// u = -lr*(O*[dual]*shape_scale + wd*p); p += u   (4 elements per thread, loads first, as muon_prep)
 __global__ __launch_bounds__(256) void muon_apply_kernel(const MuonMat* mats, MuonHyper h) {
   const MuonMat M = mats[blockIdx.y];
   // the matrix's sum of squares was last read by the NS normalisation: reset it for the next step
   // here instead of a separate fill launch (muon_prep accumulates into it with atomics)
   if (blockIdx.x == 0 && threadIdx.x == 0) *M.norm2 = 0.0;
-  const int64_t n = M.rows * M.cols;
-  const bool tr = M.rows > M.cols;
-  const float ss = h.shape_scale > 0.f ? sqrtf(fmaxf(1.f, (float)M.cols / (float)M.rows)) : 1.f;
+  const int n = (int)(M.rows * M.cols);
+  const bool tr = M.rows > M.cols, v4 = muon_v4(M);
+  const float ss = (h.shape_scale > 0.f ? sqrtf(fmaxf(1.f, (float)M.cols / (float)M.rows)) : 1.f) *
+                   (h.dual ? (float)h.dual[blockIdx.y] : 1.f);
   const int cols = (int)M.cols;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < (int)n; i += gridDim.x * 256) {
-    const int r = i / cols, c = i - r * cols;
-    const int64_t off = (int64_t)r * M.ld + c;
-    const float o = bf2f(M.xo[tr ? (int64_t)c * M.ldx + r : (int64_t)r * M.ldx + c]);
-    const float pi = M.p[off];
-    const float u = -h.lr * (o * ss + h.wd * pi);
-    if (M.upd) M.upd[off] = u;
-    if (h.apply) {
-      const float pn = pi + u;
-      M.p[off] = pn;
-      if (M.pb) M.pb[off] = f2bf(pn);
+  for (int i0 = (blockIdx.x * 256 + threadIdx.x) * 4; i0 < n; i0 += gridDim.x * 1024) {
+    float pv[4], o[4];
+    int64_t off[4];
+    int rr[4], cc[4];
+    if (v4) {
+      const int r = i0 / cols, c = i0 - r * cols;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { rr[e] = r; cc[e] = c + e; off[e] = (int64_t)r * M.ld + c + e; }
+      const float4 p4 = *reinterpret_cast<const float4*>(M.p + off[0]);
+      pv[0] = p4.x; pv[1] = p4.y; pv[2] = p4.z; pv[3] = p4.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = i0 + e < n ? i0 + e : n - 1;
+        rr[e] = i / cols; cc[e] = i - rr[e] * cols;
+        off[e] = (int64_t)rr[e] * M.ld + cc[e];
+        pv[e] = M.p[off[e]];
+      }
+    }
+    if (v4 && !tr) {
+      const bf16x4 x4 = *reinterpret_cast<const bf16x4*>(M.xo + (int64_t)rr[0] * M.ldx + cc[0]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = bf2f(x4[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = bf2f(M.xo[tr ? (int64_t)cc[e] * M.ldx + rr[e] : (int64_t)rr[e] * M.ldx + cc[e]]);
+    }
+    float u[4], pn[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      u[e] = -h.lr * (o[e] * ss + h.wd * pv[e]);
+      pn[e] = pv[e] + u[e];
+    }
+    if (v4) {
+      if (M.upd) *reinterpret_cast<float4*>(M.upd + off[0]) = float4{u[0], u[1], u[2], u[3]};
+      if (h.apply) {
+        *reinterpret_cast<float4*>(M.p + off[0]) = float4{pn[0], pn[1], pn[2], pn[3]};
+        if (M.pb) *reinterpret_cast<bf16x4*>(M.pb + off[0]) = bf16x4{f2bf(pn[0]), f2bf(pn[1]), f2bf(pn[2]), f2bf(pn[3])};
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (i0 + e >= n) break;
+        if (M.upd) M.upd[off[e]] = u[e];
+        if (h.apply) {
+          M.p[off[e]] = pn[e];
+          if (M.pb) M.pb[off[e]] = f2bf(pn[e]);
+        }
+      }
     }
   }
 }
@@ -249,21 +358,42 @@ extern "C" int pcv_step_bump(int* step, void* stream) {
 extern "C" int pcv_muon_prep(const void* mats, int nmats, int nnorm, int64_t max_elems, float beta, int nesterov,
                              float eps, const int* step, const float* gscale, void* stream) {
   if (nmats <= 0 || nnorm < 0 || nnorm > nmats || max_elems >= (1ll << 31)) return PCV_EINVAL;
-  MuonHyper h{beta, 0.f, 0.f, eps, 0.f, nesterov, 0};
-  int gx = (int)((max_elems + 256 * 8 - 1) / (256 * 8));
-  gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
+  MuonHyper h{beta, 0.f, 0.f, eps, 0.f, nesterov, 0, nullptr};
   hipStream_t s = (hipStream_t)stream;
+  // one 4-element group per thread; at most 256 blocks per matrix (each adds one fp64 atomic to norm2)
+  int gx = (int)((max_elems + 256 * 4 - 1) / (256 * 4));
+  gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
   hipLaunchKernelGGL(muon_prep_kernel, dim3(gx, nmats), dim3(256), 0, s, (const MuonMat*)mats, h, step, gscale);
+  gx = (int)((max_elems + 256 * 8 - 1) / (256 * 8));
+  gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
   if (nnorm > 0) hipLaunchKernelGGL(muon_norm_kernel, dim3(gx, nnorm), dim3(256), 0, s, (const MuonMat*)mats, eps);
   return pcv_launch_status();
 }
 
-extern "C" int pcv_muon_apply(const void* mats, int nmats, int64_t max_elems, float lr, float wd, int shape_scale,
-                              int apply, void* stream) {
-  if (nmats <= 0 || max_elems >= (1ll << 31)) return PCV_EINVAL;
-  MuonHyper h{0.f, lr, wd, 0.f, shape_scale ? 1.f : 0.f, 0, apply};
+extern "C" int pcv_muon_dual_dot(const void* mats, int nmats, int64_t max_elems, float beta, int nesterov,
+                                 const int* step, const float* gscale, double* dual, void* stream) {
+  if (nmats <= 0 || max_elems >= (1ll << 31) || !step || !dual) return PCV_EINVAL;
+  MuonHyper h{beta, 0.f, 0.f, 0.f, 0.f, nesterov, 0, nullptr};
   int gx = (int)((max_elems + 256 * 8 - 1) / (256 * 8));
   gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
+  hipLaunchKernelGGL(muon_dual_dot_kernel, dim3(gx, nmats), dim3(256), 0, (hipStream_t)stream, (const MuonMat*)mats,
+                     h, step, gscale, dual);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_muon_apply_dual(const void* mats, int nmats, int64_t max_elems, float lr, float wd,
+                                   int shape_scale, int apply, const double* dual, void* stream);
+extern "C" int pcv_muon_apply(const void* mats, int nmats, int64_t max_elems, float lr, float wd, int shape_scale,
+                              int apply, void* stream) {
+  return pcv_muon_apply_dual(mats, nmats, max_elems, lr, wd, shape_scale, apply, nullptr, stream);
+}
+
+extern "C" int pcv_muon_apply_dual(const void* mats, int nmats, int64_t max_elems, float lr, float wd,
+                                   int shape_scale, int apply, const double* dual, void* stream) {
+  if (nmats <= 0 || max_elems >= (1ll << 31)) return PCV_EINVAL;
+  MuonHyper h{0.f, lr, wd, 0.f, shape_scale ? 1.f : 0.f, 0, apply, dual};
+  int gx = (int)((max_elems + 256 * 4 - 1) / (256 * 4));   // one 4-element group per thread
+  gx = gx < 1 ? 1 : (gx > 1024 ? 1024 : gx);
   hipLaunchKernelGGL(muon_apply_kernel, dim3(gx, nmats), dim3(256), 0, (hipStream_t)stream, (const MuonMat*)mats, h);
   return pcv_launch_status();
 }

@@ -12,13 +12,16 @@ struct MuonMat {
   float* x32;                  // workspace [r', c'] (transposed if rows > cols)
   bf16* xb;                    // bf16 copy of the normalised X (NS input)
   const bf16* xo;              // NS output [r', c'] (bf16)
-  double* norm2;               // sum of squares of x32 (fp64: the per-block float partials add exactly,
-                               // so the atomic order cannot change the result -- replicas stay bit-identical)
+  double* norm2;               // sum of squares of x32 in fp64: n float partials (24-bit mantissas) add
+                               // exactly while their exponents span <= 29 - log2(n) binades, so the
+                               // atomic order does not change the result for any realistic spread of
+                               // per-block partials (not a guarantee for arbitrary data)
 };
 
 struct MuonHyper {
   float beta, lr, wd, eps, shape_scale;
   int nesterov, apply;
+  const double* dual;          // muon_adaptive: per-record <mu_hat, O>_F scale (nullptr: off)
 };
 
 struct Chunk { int64_t start; int64_t len; };

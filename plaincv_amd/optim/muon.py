@@ -61,8 +61,9 @@ class Muon(GradientTransformation):
     def __init__(self, learning_rate, ns_coeffs=(3.4445, -4.7750, 2.0315), ns_steps=5, beta=0.95, eps=1e-8,
                  weight_decay=0.0, nesterov=True, adaptive=False, adam_b1=0.9, adam_b2=0.999, adam_eps_root=0.0,
                  adam_weight_decay=0.0, shape_scale=True, fused=True, shard=None):
-        if adaptive:
-            raise NotImplementedError("muon_adaptive=True (dual-norm scaling) is not on the hot path")
+        # muon_adaptive (factory.py:457,475): O <- <mu_hat, O>_F O before the shape scale, one
+        # pcv_muon_dual_dot launch between NS and the apply launch (the one-launch step is skipped)
+        self.adaptive = bool(adaptive)
         self.lr = float(learning_rate)
         self.a, self.b, self.c = (float(x) for x in ns_coeffs)
         self.ns_steps = int(ns_steps)
@@ -104,6 +105,7 @@ class Muon(GradientTransformation):
         st.n_general = sum(len(g.names) for g in st.groups if not g.fused)
         st.n_fused = len(routed) - st.n_general
         st.norm2 = torch.zeros(max(1, len(routed)), dtype=torch.float64, device=dev)   # fp64: order-free sums
+        st.dual = torch.zeros(max(1, len(routed)), dtype=torch.float64, device=dev) if self.adaptive else None
         st.ticket = torch.zeros(1, dtype=torch.int32, device=dev)   # last-block counter of the one-launch step
         # the one-launch step moves 4 consecutive columns per lane (16-B accesses of p, g, mu)
         st.vec4 = all(store.params[k].shape[1] % 4 == 0 and store.leaf(k).offset % 4 == 0 and
@@ -150,7 +152,7 @@ class Muon(GradientTransformation):
                      stream_ptr())
 
     def _run(self, store, st, gscale, apply):
-        if st.routed and st.n_general == 0 and self.one_launch and st.vec4:
+        if st.routed and st.n_general == 0 and self.one_launch and st.vec4 and not self.adaptive:
             # every routed matrix fits the one-workgroup NS: the NS workgroups, the Adam branch and the
             # step bump share one launch (csrc/muon_fused.hip muon_step_kernel); prep and apply stay
             # wide launches around it (PCV_MUON_IN_BLOCK=1 moves them into the NS workgroups)
@@ -175,8 +177,12 @@ class Muon(GradientTransformation):
                      int(self.nesterov), self.eps, ptr(st.count), ptr(gscale), stream_ptr())
             self._newton_schulz(st)
             mats = st.mats_apply if apply else st.mats_upd
-            hip.call("pcv_muon_apply", ptr(mats), len(st.routed), st.max_elems, self.lr, self.wd,
-                     int(self.shape_scale), int(apply), stream_ptr())
+            if self.adaptive:
+                st.dual.zero_()
+                hip.call("pcv_muon_dual_dot", ptr(st.mats_apply), len(st.routed), st.max_elems, self.beta,
+                         int(self.nesterov), ptr(st.count), ptr(gscale), ptr(st.dual), stream_ptr())
+            hip.call("pcv_muon_apply_dual", ptr(mats), len(st.routed), st.max_elems, self.lr, self.wd,
+                     int(self.shape_scale), int(apply), ptr(st.dual) if self.adaptive else None, stream_ptr())
         st.branch.run(store, st.tensors["mu"], st.tensors["nu"], st.count, self.lr, gscale=gscale,
                       upd=None if apply else st.upd, apply=apply)
         K.step_bump(st.count)

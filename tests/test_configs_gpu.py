@@ -153,12 +153,18 @@ def test_c4_fp32_soap_13_steps_two_refreshes(dev):
 
 
 def test_c4_fp32_shampoo_6_steps(dev):
-    out, _ = _c4_pair(dev, "shampoo", 6, dict(eps=1e-4))
+    """Each step's update against the fp64 oracle (fp64 eigh) fed the same gradients, bounded per leaf
+    by max(5e-4, 2x the fp32 oracle's own distance from it), as SOAP above.  L + eps I has every
+    eigenvalue >= eps, so the reference's clamp max(lambda, eps) (optim/shampoo.py:199-214) never
+    binds and the coupled-Newton inverse root computes the same P as eigh."""
+    out, _ = _c4_pair(dev, "shampoo", 6, dict(eps=1e-4), fp64=True)
     worst = {}
-    for it, (p0, p1, u) in enumerate(out):
+    for it, (p0, p1, u, u64) in enumerate(out):
         for k in p0:
-            worst[k] = max(worst.get(k, 0.0), rel(p1[k].double() - p0[k].double(), u[k]))
-    print("C4_SHAMPOO", sorted(worst.items(), key=lambda kv: -kv[1])[:6])
-    # the coupled-Newton inverse 4th root vs the oracle's fp32 eigh
-    bad = {k: v for k, v in worst.items() if v > 5e-3}
+            d = p1[k].double() - p0[k].double()
+            now = (rel(d, u64[k]), rel(u[k], u64[k]), rel(d, u[k]))
+            worst[k] = tuple(max(a, b) for a, b in zip(worst.get(k, now), now))
+    print("C4_SHAMPOO (hip-fp64, oracle32-fp64, hip-oracle32)",
+          sorted(worst.items(), key=lambda kv: -kv[1][0])[:8])
+    bad = {k: v for k, v in worst.items() if v[0] > max(5e-4, 2.0 * v[1])}
     assert not bad, bad

@@ -101,14 +101,44 @@ def _move_rel(got, p0, ref):
 
 @pytest.mark.gpu
 def test_hip_vit_golden_muon3(dev):
-    """3 Muon steps (lr 1e-3, wd 0.01, Adam b1/b2 0.9) on the golden batch without dropout vs the
-    committed oracle trajectory ``muon3:*``: rel-L2 of each leaf's movement (key biases excluded:
-    their true gradient is exactly 0, the bf16 one is noise that Adam normalises)."""
+    """3 Muon steps (lr 1e-3, wd 0.01, Adam b1/b2 0.9) on the golden batch without dropout.  Each leaf's
+    movement is compared with the exact (fp64) oracle trajectory computed here, bounded by
+    max(5e-2, 2x the rounding-noise spread of the leaf's class), the spread being the distance from
+    the fp64 trajectory of a bf16 trajectory that rounds what the HIP backward rounds: the GEMM
+    operands AND each Dense output's gradient (stored in bf16 as the dgrad / wgrad operand;
+    oracle.nn.bf16_grad_storage), taken as the largest over the class (LayerNorm scales /
+    LayerNorm biases / other 1-D / Muon-routed kernels / other >= 2-D).  Why the gradient storage
+    matters: a LayerNorm_0 scale gradient collects the key-gradient terms, which cancel in exact
+    arithmetic (softmax shift invariance), so it is mostly rounding noise that Adam's sign-like first
+    steps turn into O(0.1) relative movement -- r04 measured 0.13 / 0.15 (HIP) for the two LN_0
+    scales, the committed operand-only fixture ``muon3:*`` 0.008, and the gradient-storage model
+    0.014 / 0.148.  The movement against the committed fixture is printed beside.  Key biases are
+    excluded (their true gradient is exactly 0)."""
+    from oracle import optim as oopt
+    from oracle.engine import apply_updates, cross_entropy_loss, value_and_grad
+    from oracle.vit import vit_apply
     from plaincv_amd.engine import create_train_state, make_train_step
     from plaincv_amd.models.vit_small import VisionTransformer
     from utils import Config
     z = _load("vit_tiny.npz")
-    _, p = vit_params()
+    ocfg, p = vit_params()
+    imgs_c, labels_c = torch.from_numpy(z["images"]), torch.from_numpy(z["labels"])
+    from oracle.nn import bf16_grad_storage
+
+    def traj(dt, bf16):
+        tx = oopt.muon(1e-3, weight_decay=0.01, adam_b1=0.9, adam_b2=0.9, adam_weight_decay=0.01)
+        q = {k: v.to(dt) for k, v in p.items()}
+        s_ = tx.init(q)
+        for _ in range(3):
+            _, gr = value_and_grad(lambda r: (cross_entropy_loss(
+                vit_apply(r, imgs_c, ocfg, False, 0, bf16=bf16, dtype=dt), labels_c), None), q)
+            u, s_ = tx.update(gr, s_, q)
+            q = apply_updates(q, u)
+        return q
+
+    q64 = traj(torch.float64, False)
+    with bf16_grad_storage():
+        qgs = traj(torch.float32, True)
     m = VisionTransformer(**dict(VIT_CFG, dropout_rate=0.0))
     shape = tuple(z["images"].shape)
     cfg = Config(optim="muon", lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9)
@@ -119,13 +149,26 @@ def test_hip_vit_golden_muon3(dev):
         st, _ = step(st, (imgs, labels), it)
     torch.cuda.synchronize()
     got = st.params.to_dict()
-    for k in p:
-        if k.endswith("key/bias"):
-            continue
-        r = _move_rel(got[k].numpy(), p[k].numpy(), z["muon3:" + k])
-        print(f"GOLDEN_MUON3 {k} {r:.4f}")
-        # measured <= 0.28 (r03; bf16 NS5 + bf16-placement gradients vs the fixture's oracle run)
-        assert r < 0.4, (k, r)
+    from tests.parity_util import routed
+
+    def cls(k):
+        if p[k].dim() == 1:
+            return ("ln_" + k.split("/")[-1]) if "LayerNorm" in k else "vec"
+        return "routed" if routed(k, p[k]) else "mat"
+
+    keys = [k for k in p if not k.endswith("key/bias")]
+    e = {}
+    spread = {}
+    for k in keys:
+        p0, ref64 = p[k].numpy(), q64[k].numpy()
+        e[k] = (_move_rel(got[k].numpy(), p0, ref64), _move_rel(z["muon3:" + k], p0, ref64),
+                _move_rel(qgs[k].numpy(), p0, ref64), _move_rel(got[k].numpy(), p0, z["muon3:" + k]))
+        spread[cls(k)] = max(spread.get(cls(k), 0.0), e[k][2])
+        print(f"GOLDEN_MUON3 {k} hip_vs_fp64 {e[k][0]:.4f} fixture_vs_fp64 {e[k][1]:.4f} "
+              f"gradstore_model_vs_fp64 {e[k][2]:.4f} hip_vs_fixture {e[k][3]:.4f}")
+    print("GOLDEN_MUON3 class spreads", spread)
+    bad = {k: (v[0], spread[cls(k)]) for k, v in e.items() if v[0] > max(5e-2, 2.0 * spread[cls(k)])}
+    assert not bad, bad
 
 
 @pytest.mark.gpu

@@ -162,6 +162,27 @@ def test_muon_update_parity(dev, which, mode, gscale):
     assert wa <= ADAM_TOL, wa
 
 
+@pytest.mark.parametrize("which", ["vit_c2", "lm768"])
+@pytest.mark.parametrize("mode,gscale", [("update", 1.0), ("step_", 0.37)])
+def test_muon_adaptive_update_parity(dev, which, mode, gscale):
+    """muon_adaptive (factory.py:457,475 -> optax.contrib.muon adaptive=True): the orthogonalised update
+    scaled by <mu_hat, O>_F (pcv_muon_dual_dot) on the fused-NS (ViT) and GEMM-chain (LM) groups.  The
+    dual scale changes the update's size by orders of magnitude, so a dropped or misplaced scale fails
+    the bound by far; a scaled-but-not-adaptive run must fail it (teeth)."""
+    from oracle import optim as oopt
+    from plaincv_amd.optim.muon import Muon
+    lr, wd = 1e-2, 0.1
+    kw = dict(weight_decay=wd, adam_b1=0.9, adam_b2=0.95, adam_weight_decay=wd)
+    steps = run_pair(dev, LAYOUTS[which](), Muon(lr, adaptive=True, **kw), oopt.muon(lr, adaptive=True, **kw), 3,
+                     mode, gscale)
+    wr, wa = worst(steps, _routed)
+    print(f"MUON_ADAPTIVE {which} {mode} routed {wr:.3e} adam {wa:.3e}")
+    assert wr <= MUON_TOL, wr
+    assert wa <= ADAM_TOL, wa
+    plain = run_pair(dev, LAYOUTS[which](), Muon(lr, **kw), oopt.muon(lr, adaptive=True, **kw), 2, mode, gscale)
+    assert worst(plain, _routed)[0] > 10 * MUON_TOL
+
+
 def test_muon_ragged_fused_shapes(dev):
     """Fused NS kernel on ragged routed shapes (7x33, 48x100, 200x64) vs fp32 NS5."""
     from oracle import optim as oopt
