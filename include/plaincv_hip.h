@@ -46,8 +46,8 @@ int pcv_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, i
                   const float* bias, const void* res, int64_t ldr, int64_t stride_r, int res_f32, float res_scale,
                   void* aux, int64_t ldaux, int act,
                   float dropout_rate, const uint32_t* seed, uint32_t site, float* colsum, int col_reps,
-                  const void* attn_o, int64_t ld_attn_o, float* attn_delta, int attn_T, int attn_H, int split_k,
-                  void* stream);
+                  const void* attn_o, int64_t ld_attn_o, const void* attn_o_lo, float* attn_delta, int attn_T,
+                  int attn_H, int split_k, void* stream);
 
 /* 256x256 8-wave ping-pong GEMM (csrc/gemm_big.hip) for large products with BOTH operands
  * K-contiguous: C[M,N] (bf16) = alpha * A[M,K] . B[N,K]^T (+ res_scale * res (bf16)).  pcv_gemm_bf16
@@ -55,6 +55,10 @@ int pcv_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, i
  * pcv_gemm_big_enable(on) toggles that dispatch (on < 0: query) and returns the previous state.
  * Replaces the same flax Dense contractions as pcv_gemm_bf16 (the LM forward and dgrad GEMMs). */
 int pcv_gemm_big_enable(int on);
+/* Row-panel dispatch of pcv_gemm_bf16 / pcv_gemm_ln (csrc/rowgemm.inc: the skinny token-row products,
+ * A K-contiguous, N % 128 == 0 <= 384, K % 64 == 0): on (1) / off (0), on < 0 queries; returns the
+ * previous state (off unless PCV_ROWGEMM=1). */
+int pcv_rowgemm_enable(int on);
 int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb);
 int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                  int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale, void* stream);

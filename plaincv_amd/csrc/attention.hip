@@ -836,6 +836,63 @@ __device__ __forceinline__ void sh_load_images(bf16* const (&img)[N], const bf16
   }
 }
 
+// The whole prologue of a short-path workgroup in one memory round trip: the N head images, the
+// layer's dropout keep words and (ROWF) the row constants lse2 / delta are all loaded into registers
+// before the first LDS store (the separate mask-copy and row-constant loops each waited a full cold
+// trip of their own).
+constexpr int SH_MASK_CHUNKS = 8 * ((SH_TMAX + 127) / 128) * (2 * ((SH_TMAX + 127) / 128)) * 64 / 8;
+template <int N, bool DROP, bool ROWF>
+__device__ __forceinline__ void sh_prologue(bf16* const (&img)[N], const bf16* const (&src)[N],
+                                            const int64_t (&ld)[N], int T, int TP, int64_t bT, uint16_t* mk,
+                                            const uint16_t* msrc, int nmask_chunks, float* Ls, float* Dl,
+                                            const float* lse, const float* dlt) {
+  constexpr int CPR = SH_DH / 8, ITER = (SH_TMAX * CPR + SH_THREADS - 1) / SH_THREADS;
+  constexpr int MITER = (SH_MASK_CHUNKS + SH_THREADS - 1) / SH_THREADS;
+  const int tid = threadIdx.x;
+  u32x4 v[ITER][N];
+#pragma unroll
+  for (int i = 0; i < ITER; ++i) {
+    const int idx = tid + SH_THREADS * i;
+    const int r = idx / CPR, c = idx % CPR;
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      v[i][n] = u32x4{0u, 0u, 0u, 0u};
+      if (r < T) v[i][n] = *reinterpret_cast<const u32x4*>(src[n] + (bT + r) * ld[n] + c * 8);
+    }
+  }
+  u32x4 mv[DROP ? MITER : 1];
+  if constexpr (DROP) {
+#pragma unroll
+    for (int i = 0; i < MITER; ++i) {
+      const int idx = tid + SH_THREADS * i;
+      if (idx < nmask_chunks) mv[i] = reinterpret_cast<const u32x4*>(msrc)[idx];
+    }
+  }
+  float lv = 0.f, dv = 0.f;
+  if constexpr (ROWF) {
+    if (tid < T) { lv = lse[tid]; dv = dlt[tid]; }
+  }
+#pragma unroll
+  for (int i = 0; i < ITER; ++i) {
+    const int idx = tid + SH_THREADS * i;
+    const int r = idx / CPR, c = idx % CPR;
+    if (r < TP) {
+#pragma unroll
+      for (int n = 0; n < N; ++n) *reinterpret_cast<u32x4*>(img[n] + toff<SH_DH>(r, c)) = v[i][n];
+    }
+  }
+  if constexpr (DROP) {
+#pragma unroll
+    for (int i = 0; i < MITER; ++i) {
+      const int idx = tid + SH_THREADS * i;
+      if (idx < nmask_chunks) reinterpret_cast<u32x4*>(mk)[idx] = mv[i];
+    }
+  }
+  if constexpr (ROWF) {
+    if (tid < TP) { Ls[tid] = lv; Dl[tid] = dv; }
+  }
+}
+
 // The layer's packed [T,T] dropout keep words (drop_word layout, shared by every batch and head)
 // staged into LDS once per workgroup: read per score element, a global 2-byte load each time
 // serialised a few microseconds of latency into every score chain.
@@ -937,9 +994,9 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
     bf16* const img[3] = {Qs, Ks, Vs};
     const bf16* const src[3] = {a.q + h * DH, a.k + h * DH, a.v + h * DH};
     const int64_t ld[3] = {a.ldq, a.ldq, a.ldq};
-    sh_load_images<3>(img, src, ld, T, TP, bT);
+    sh_prologue<3, DROP, false>(img, src, ld, T, TP, bT, mk, a.mask, (int)(drop_words(T) / 8), nullptr, nullptr,
+                                nullptr, nullptr);
   }
-  if (DROP) sh_load_mask(mk, a.mask, T);
   __syncthreads();
   PCV_SHREC(1);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4;
@@ -1119,19 +1176,15 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
   const int h = blockIdx.x, b = blockIdx.y;
   const int T = a.T, TP = (T + 31) & ~31, NT = TP / 16;
   const int64_t bT = (int64_t)b * T, bh = (int64_t)b * a.H + h;
-  {
-    bf16* const img[4] = {Qs, Ks, Vs, Os};
-    const bf16* const src[4] = {a.q + h * DH, a.k + h * DH, a.v + h * DH, a.dout + h * DH};
-    const int64_t ld[4] = {a.ldq, a.ldq, a.ldq, a.lddo};
-    sh_load_images<4>(img, src, ld, T, TP, bT);
-  }
-  if (DROP) sh_load_mask(mk, a.mask, T);
-  if (a.delta_ready) {
-    for (int r = threadIdx.x; r < TP; r += blockDim.x) {
-      Ls[r] = r < T ? a.lse2[bh * T + r] : 0.f;
-      Dl[r] = r < T ? a.delta[bh * T + r] : 0.f;
-    }
+  bf16* const img[4] = {Qs, Ks, Vs, Os};
+  const bf16* const src[4] = {a.q + h * DH, a.k + h * DH, a.v + h * DH, a.dout + h * DH};
+  const int64_t ld[4] = {a.ldq, a.ldq, a.ldq, a.lddo};
+  if (a.delta_ready) {   // images, mask words and row constants in one round trip
+    sh_prologue<4, DROP, true>(img, src, ld, T, TP, bT, mk, a.mask, (int)(drop_words(T) / 8), Ls, Dl,
+                               a.lse2 + bh * T, a.delta + bh * T);
   } else {
+    sh_load_images<4>(img, src, ld, T, TP, bT);
+    if (DROP) sh_load_mask(mk, a.mask, T);
     // delta = rowsum(dO o O): 4 lanes x 8 columns per row, all loads issued first
     constexpr int ITER = (SH_TMAX * 4 + SH_THREADS - 1) / SH_THREADS;
     bf16x8 xo[ITER], xl[ITER], xd[ITER];

@@ -73,6 +73,7 @@ struct GemmArgs {
   // produces dO): delta[(b H + h) T + t] = <bf16(C[row, h dh : (h+1) dh]), dl_o[row, same]>,
   // row = b T + t -- replaces attn_bwd_delta_kernel
   const bf16* dl_o; int64_t ld_dlo; float* dl_delta; int dl_T, dl_H, dl_dh;
+  const bf16* dl_olo;            // optional O - bf16(O) residual (same row stride): delta = <dO, O_hi + O_lo>
   // split-K partial tiles (grouped launch with a workspace): slice kz of C tile t writes alpha * its
   // partial to sk_ws[(t * split_k + kz) * BM * BN ...] with plain stores, and a fold launch adds the
   // slices to C in slice order -- deterministic, and no contended float atomics
@@ -963,8 +964,14 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
           if (g.dl_delta) {   // lanes of one head are dh/8 consecutive lanes (a quad or an octet)
             const bf16x8 ov = *reinterpret_cast<const bf16x8*>(g.dl_o + row * g.ld_dlo + col);
             float d = 0.f;
+            if (g.dl_olo) {
+              const bf16x8 ol = *reinterpret_cast<const bf16x8*>(g.dl_olo + row * g.ld_dlo + col);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) d += bf2f(o[e]) * bf2f(ov[e]);
+              for (int e = 0; e < 8; ++e) d += (bf2f(ov[e]) + bf2f(ol[e])) * bf2f(o[e]);
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) d += bf2f(o[e]) * bf2f(ov[e]);
+            }
             d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0xB1, 0xF, 0xF, false));
             d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x4E, 0xF, 0xF, false));
             if (g.dl_dh == 64)
@@ -1182,9 +1189,17 @@ static hipError_t launch_sz(const GemmArgs& a, int ta, int tb, int batch, hipStr
   return launch_t<false, true, WM, WN>(a, batch, s);
 }
 
+#include "rowgemm.inc"
+
 }  // namespace pcv
 
 using namespace pcv;
+
+extern "C" int pcv_rowgemm_enable(int on) {
+  const int old = rp_on() ? 1 : 0;
+  if (on >= 0) g_rp_enabled = on ? 1 : 0;
+  return old;
+}
 
 extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
                              int64_t M, int64_t N, int64_t K,
@@ -1196,7 +1211,8 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
                              void* aux, int64_t ldaux, int act,
                              float drop_rate, const uint32_t* seed, uint32_t site,
                              float* colsum, int col_reps, const void* attn_o, int64_t ld_attn_o,
-                             float* attn_delta, int attn_T, int attn_H, int split_k, void* stream) {
+                             const void* attn_o_lo, float* attn_delta, int attn_T, int attn_H, int split_k,
+                             void* stream) {
   if (M < 0 || N < 0 || K < 0 || batch < 1) return PCV_EINVAL;
   if (colsum && (batch > 1 || split_k > 1)) return PCV_EINVAL;
   if (M == 0 || N == 0) return 0;
@@ -1219,7 +1235,9 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
     if (!attn_o || out_f32 || split_k > 1 || batch > 1 || attn_T <= 0 || attn_H <= 0 || N % attn_H) return PCV_EINVAL;
     const int64_t dh = N / attn_H;
     if ((dh != 32 && dh != 64) || (ld_attn_o & 7) || !pcv_aligned16(attn_o) || M % attn_T) return PCV_EINVAL;
+    if (attn_o_lo && !pcv_aligned16(attn_o_lo)) return PCV_EALIGN;
     g.dl_o = (const bf16*)attn_o; g.ld_dlo = ld_attn_o; g.dl_delta = attn_delta;
+    g.dl_olo = (const bf16*)attn_o_lo;
     g.dl_T = attn_T; g.dl_H = attn_H; g.dl_dh = (int)dh;
   }
   g.drop_thresh = 0; g.drop_scale = 1.f; g.seedp = seed; g.site = site;
@@ -1259,6 +1277,11 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
   if (trans_a && !trans_b && out_f32 && beta == 1.f && batch == 1 && !bias && !res && !aux && act == EPI_NONE &&
       g.drop_thresh == 0 && !colsum && !attn_delta && pcv_aligned16(C) && pcv_gemm_big_wgrad_ok(M, N, K, A, lda, B, ldb))
     return pcv_gemm_big_wgrad(A, B, (float*)C, M, N, K, lda, ldb, ldc, alpha, stream);
+  // skinny token-row products (the ViT's): one row panel per CU across the whole width (rowgemm.inc)
+  if (rp_eligible(g, trans_a, (int)batch, 0)) {
+    const hipError_t e = rp_launch(g, trans_b, s);
+    return e == hipSuccess ? 0 : (int)e;
+  }
   // tile: 128x128 when that grid covers the chip and K is deep, else 64x64.  (A 256x256 tile with
   // one 128x128 block per wave was measured 15-45 % slower at the LM shapes: it needs
   // all 512 registers, spills, and runs one wave per SIMD.)
@@ -1320,6 +1343,10 @@ extern "C" int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, in
   // ViT C2 step 0.858 -> 0.852 ms, but each launch alone 16.9 -> 21.7 us back to back (the per-column
   // LN-parameter atomics double), so the 64x128 tile stays the default.
   static const int ln32 = getenv("PCV_LN_TILE") ? atoi(getenv("PCV_LN_TILE")) == 32 : 0;
+  if (!ln32 && rp_eligible(g, trans_a, 1, ln_mode)) {
+    const hipError_t e = rp_launch(g, trans_b, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : (int)e;
+  }
   hipError_t e = ln32 ? launch_sz<1, 4>(g, trans_a, trans_b, 1, (hipStream_t)stream)
                       : launch_sz<2, 4>(g, trans_a, trans_b, 1, (hipStream_t)stream);
   return e == hipSuccess ? 0 : (int)e;

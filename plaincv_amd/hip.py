@@ -22,8 +22,8 @@ SZ = ctypes.c_size_t
 # name -> argtypes (return type is always int status)
 SIGNATURES = {
     "pcv_gemm_bf16": [P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, I64, I64, I64, I64,
-                      F32, F32, I32, P, P, I64, I64, I32, F32, P, I64, I32, F32, P, U32, P, I32, P, I64, P, I32, I32,
-                      I32, P],
+                      F32, F32, I32, P, P, I64, I64, I32, F32, P, I64, I32, F32, P, U32, P, I32, P, I64, P, P, I32,
+                      I32, I32, P],
     "pcv_gemm_ln": [P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, F32, P, P, I64, F32, P, U32, I32, P, P, F32,
                     P, I64, P, P, P, I64, P, P, P, I32, P],
     "pcv_gemm_grouped_plan_size": [I32],
@@ -115,6 +115,7 @@ SIGNATURES = {
     "pcv_muon_mat_size": [],
     "pcv_chunk_size": [],
     "pcv_gemm_big_enable": [I32],
+    "pcv_rowgemm_enable": [I32],
     "pcv_gemm_big_ok": [I64, I64, I64, P, I64, P, I64],
     "pcv_gemm_big": [P, P, P, I64, I64, I64, I64, I64, I64, F32, P, I64, F32, P],
     "pcv_gemm_big_wgrad_ok": [I64, I64, I64, P, I64, P, I64],

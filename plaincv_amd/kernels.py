@@ -33,8 +33,9 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
     bf16 or fp32 output (fp32: out = v + beta*out).  Epilogue order:
     +bias -> [gelu (aux<-preact) | *gelu'(aux)] -> dropout -> +res.  colsum (fp32 [N]) += column sums
     of the stored values (not with split-K or batches); col_reps > 1: colsum is [col_reps, N] and
-    workgroup b adds into row b % col_reps (the caller folds the rows).  attn_delta=(o, delta, T, H):
-    with bf16 out = dO, also delta[(b H + h) T + t] = <out[b T + t, head h], o[b T + t, head h]>."""
+    workgroup b adds into row b % col_reps (the caller folds the rows).  attn_delta=(o, delta, T, H[, o_lo]):
+    with bf16 out = dO, also delta[(b H + h) T + t] = <out[b T + t, head h], o[b T + t, head h]> (o + o_lo
+    when the short attention's O residual is given)."""
     batched = a.dim() == 3
     if batched:
         nb = a.shape[0]
@@ -86,11 +87,14 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
         _chk(not batched and colsum.dtype == F32 and colsum.numel() >= N * col_rows(M, col_reps) and colsum.is_cuda
              and colsum.is_contiguous(), "gemm colsum")
         split_k = 1
-    dl_o, dl_ld, dl, dl_T, dl_H = None, 0, None, 0, 0
+    dl_o, dl_ld, dl, dl_T, dl_H, dl_lo = None, 0, None, 0, 0, None
     if attn_delta is not None:
-        dl_o, dl, dl_T, dl_H = attn_delta
+        dl_o, dl, dl_T, dl_H = attn_delta[:4]
+        dl_lo = attn_delta[4] if len(attn_delta) > 4 else None
         _chk(not batched and out.dtype == BF16 and dl_o.dtype == BF16 and tuple(dl_o.shape) == (M, N) and
              dl.dtype == F32 and dl.numel() >= M * dl_H, "gemm attn_delta")
+        _chk(dl_lo is None or (dl_lo.dtype == BF16 and dl_lo.shape == dl_o.shape and dl_lo.stride() == dl_o.stride()),
+             "gemm attn_delta o_lo")
         dl_ld = _ld(dl_o)
         split_k = 1
     if split_k is None:
@@ -106,7 +110,7 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
              int(ta), int(tb), nb, sa, sb, sc, float(alpha), float(beta), out_f32,
              ptr(bias), ptr(res), ldr, sr, res_f32, float(res_scale), ptr(aux), ldaux, int(act),
              float(drop_rate), ptr(seed), int(site) & 0xFFFFFFFF, ptr(colsum), int(col_reps), ptr(dl_o), dl_ld,
-             ptr(dl), int(dl_T), int(dl_H), int(split_k), stream_ptr())
+             ptr(dl_lo), ptr(dl), int(dl_T), int(dl_H), int(split_k), stream_ptr())
     return out
 
 

@@ -267,6 +267,9 @@ class ViTRunner:
         self.dh = [e(R, M, dt=bf) for _ in range(Lc)]
         # LayerNorm fused into the residual-stream GEMM epilogues (pcv_gemm_ln) when rows fit one tile
         self.fuse_ln = bool(model.use_layernorm) and D <= 128 and D % 8 == 0
+        # the short attention's delta formed by the dO GEMM's epilogue (PCV_VIT_DELTA_GEMM=0: in the
+        # attention backward's prologue)
+        self.delta_in_gemm = os.environ.get("PCV_VIT_DELTA_GEMM", "1") != "0"
         self.dy_m = [e(R, D) for _ in range(Lc)] if not self.fuse_ln else None
         self.dx_mid = [e(R, D) for _ in range(Lc)]
         self.dxb_mid = [e(R, D, dt=bf) for _ in range(Lc)]
@@ -590,11 +593,17 @@ class ViTRunner:
                 K.gemm(self.o[i], dxb_mid, w["gWo"], ta=True, beta=1.0)
             if not self.fuse_ln:
                 K.colsum(dx_mid, w["gbo"])
-        if self.short_attn:
+        if self.short_attn and not self.delta_in_gemm:
             # dO = dy Wo^T; the short backward forms delta = <dO, O_hi + O_lo> in its prologue
             K.gemm(dxb_mid, w["Wo"], self.do, tb=True)
             K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
                        causal=False, drop_rate=rate, mask=self._mask(i), o_lo=self.o_lo[i])
+        elif self.short_attn:
+            # dO = dy Wo^T; its epilogue forms delta = <dO, O_hi + O_lo> (the short backward's prologue
+            # then loads only Q, K, V, dO, the row constants and the mask words)
+            K.gemm(dxb_mid, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H, self.o_lo[i]))
+            K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, dqkv, B, T, H, Dh,
+                       causal=False, drop_rate=rate, mask=self._mask(i), delta_ready=True)
         else:
             # dO = dy Wo^T; its epilogue also forms the attention-backward row constant delta
             K.gemm(dxb_mid, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H))

@@ -53,7 +53,7 @@ def _gemm(lib, A=A16, lda=64, M=64, N=64, K=64, batch=1, act=0, split_k=1, out_f
           colsum=None, drop=0.0, delta=None, T=0, H=0, attn_o=None):
     return lib.pcv_gemm_bf16(P(A), P(A16), P(A16), M, N, K, lda, 64, 64, 0, 0, batch, 0, 0, 0, 1.0, beta, out_f32,
                              None, None, 0, 0, 0, 1.0, None, 64, act, drop, None, 0,
-                             P(colsum) if colsum else None, 1, P(attn_o) if attn_o else None, 64,
+                             P(colsum) if colsum else None, 1, P(attn_o) if attn_o else None, 64, None,
                              P(delta) if delta else None, T, H, split_k, None)
 
 

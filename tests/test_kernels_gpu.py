@@ -376,7 +376,7 @@ def test_gemm_ln_backward(dev, M, N, K, rate, reps):
         K_.GroupedWGrad([("colsum", ws_, t) for ws_, t in zip(wss, (ds, db, cs))], dev)()
         torch.cuda.synchronize()
         assert all(torch.equal(a_, b_) for a_, b_ in zip(snap, wss))   # plain column sums leave the rows
-        assert all((ws_[: -(-M // 64)] != 9.0).all() for ws_ in wss)      # every row tile stored its partial
+        assert all((ws_[: -(-M // 64)] != 9.0).all() for ws_ in wss)      # every row of the buffer was stored
     elif reps > 1:   # replica rows [reps, N], folded afterwards
         wss = [torch.zeros(reps, N, device=dev) for _ in range(3)]
         K_.gemm_ln(dh, w, dx, tb=True, ln_mode=2, res=dres, ln_scale=sc, ln_y=dxb, ln_mean=mean, ln_rstd=rstd,

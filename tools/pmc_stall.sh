@@ -5,7 +5,7 @@ TAG=${1:-r03_stall}
 WL=${2:-"--steps 10 --warmup 2"}
 PROG=${3:-bench.py}
 EXTRA=""
-if [ "$PROG" = "bench.py" ]; then EXTRA="--no-cpu-baseline --no-lm"; fi
+if [ "$PROG" = "bench.py" ]; then EXTRA="--no-cpu-baseline --no-lm --no-f32"; fi
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$TAG
 mkdir -p $O

@@ -40,6 +40,10 @@ def bwd():
     K.attn_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, Dh, False, p, mask, o_lo=out_lo)
 
 
+def bwd_ready():
+    K.attn_bwd(qkv, out, dout, lse, delta, dqkv, B, T, H, Dh, False, p, mask, delta_ready=True)
+
+
 def report(name, fn, cold):
     rows = []
     for it in range(6):
@@ -70,5 +74,6 @@ def report(name, fn, cold):
 for cold in (False, True):
     report("fwd", fwd, cold)
     report("bwd", bwd, cold)
+    report("bwdR", bwd_ready, cold)   # delta from the dO GEMM (the ViT runner's form)
 if "--graph" in sys.argv:
     pass
