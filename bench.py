@@ -295,15 +295,21 @@ def bench_vit(args):
     # the batch pool is the step's input ring: each slot has its own captured graph that reads the
     # batch in place (a loader fills the slots; no per-step copy into a static buffer)
     ring = None if os.environ.get("PCV_BENCH_COPY_INPUTS") == "1" else (pool_x, pool_y)   # A/B switch
-    step = GraphedTrainStep(state, shape, warmup=2, inputs=ring)
+    # Muon: the Newton-Schulz workgroups of step t run beside step t+1's forward head (engine.py
+    # GraphedTrainStep overlap_opt; PCV_BENCH_OPT_OVERLAP=0 runs them inside the step); the last step's
+    # are drained by flush() inside the timed region
+    overlap = os.environ.get("PCV_BENCH_OPT_OVERLAP", "1") != "0"
+    step = GraphedTrainStep(state, shape, warmup=2, inputs=ring, overlap_opt=overlap)
     for i in range(args.warmup):
         step(pool_x[i % nb], pool_y[i % nb])
+    step.flush()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(pool_x[i % nb], pool_y[i % nb])
+    step.flush()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -326,7 +332,8 @@ def bench_vit(args):
                           "per_gpu_batch": B, "image": [64, 64, 3], "classes": 200, "tokens": 257,
                           "optimizer": cfg.optim, "parallelism": f"dp{world}",
                           "inputs": "copy-in (one static batch buffer per step)" if ring is None else
-                                    "input ring (one captured graph per resident batch slot, read in place)"},
+                                    "input ring (one captured graph per resident batch slot, read in place)",
+                          "optimizer_overlap": bool(step.overlap)},
                "steps_per_sec": round(sps, 3), "tflops_per_gpu": round(flops * sps / 1e12, 3),
                "final_loss": round(loss, 4)}
         out["roofline"] = (vit_roofline_f32(state, shape, cfg.vit_dropout) if cfg.vit_dtype == "float32"

@@ -264,7 +264,11 @@ class GraphedTrainStep:
     seed they touch are snapshotted and restored, so construction does not train the model,
     and under data parallelism the warm-up gradients are all-reduced like a real step."""
 
-    def __init__(self, state: TrainState, image_shape, warmup=2, inputs=None):
+    # each ring slot is one more captured forward/backward graph (construction time and graph memory
+    # grow with the ring); the slot graphs share the copy-in graph's memory pool
+    MAX_SLOTS = 8
+
+    def __init__(self, state: TrainState, image_shape, warmup=2, inputs=None, overlap_opt=False):
         self.state = state
         self.runner = state.runner_for(image_shape)
         dev = state.params.device
@@ -278,11 +282,22 @@ class GraphedTrainStep:
                     tuple(ys.shape) != (xs.shape[0], B) or not xs.is_cuda or not ys.is_cuda or
                     not xs.is_contiguous() or not ys.is_contiguous()):
                 raise ValueError("inputs: (uint8 [N, *image_shape], int32 [N, B]) contiguous device tensors")
+            if xs.shape[0] > self.MAX_SLOTS:
+                raise ValueError(f"inputs: at most {self.MAX_SLOTS} ring slots (one captured graph each)")
             self.slots = [(xs[k], ys[k]) for k in range(xs.shape[0])]
         self.distributed = dp.world_size() > 1
         # SOAP/Shampoo steps are host-driven (first step, refreshes, basis restarts): they run
         # eagerly after the captured forward/backward.
         self.opt_graphed = bool(getattr(state.tx, "graphable", True))
+        # overlap_opt: an optimizer whose step splits into a gradient phase and a matrix phase (Muon:
+        # momentum + Adam branch | Newton-Schulz + routed update) runs the matrix phase of step t on a
+        # side stream at the start of step t+1, beside that step's forward up to the first read of a
+        # routed weight (runner.forward(join=...)).  The phase order per step is step_()'s; the last
+        # step's matrix phase runs in flush() (called by whoever reads the params next: bench, eval).
+        self.overlap = bool(overlap_opt and self.opt_graphed and not self.distributed and
+                            getattr(self.runner, "supports_join", False) and
+                            hasattr(state.tx, "split_capable") and state.tx.split_capable(state.opt_state))
+        self.pending = False
         self.stream = torch.cuda.Stream(device=dev)
         self.g_fb = torch.cuda.CUDAGraph()
         self.g_opt = torch.cuda.CUDAGraph() if (self.distributed and self.opt_graphed) else None
@@ -310,30 +325,67 @@ class GraphedTrainStep:
             for images, labels in [(None, None)] + self.slots:   # the copy-in graph, then one per slot
                 g = self.g_fb if images is None else torch.cuda.CUDAGraph()
                 with _labels_bound(self.runner, labels):
-                    with torch.cuda.graph(g, stream=s):
+                    # slot graphs replay one at a time on this stream, after the copy-in graph's capture:
+                    # they can share its memory pool
+                    with torch.cuda.graph(g, stream=s, pool=None if images is None else self.g_fb.pool()):
                         self._fb(images)
-                        if not split:
+                        if self.overlap:
+                            state.tx.step_grad_phase_(store, state.opt_state)
+                        elif not split:
                             self._opt()
                 if images is None:
                     after_first = _host_scalars(state.opt_state)   # host state as after one capture
                 else:
                     self.g_slots.append(g)
                     _restore_host_scalars(after_first)
+            if self.overlap:
+                # steady-state graphs: the previous step's matrix phase on a side stream beside this
+                # step's forward head, joined before the first routed-weight read
+                self.side = torch.cuda.Stream(device=dev)
+                self.g_steady = []
+                for images, labels in [(None, None)] + self.slots:
+                    g = torch.cuda.CUDAGraph()
+                    with _labels_bound(self.runner, labels):
+                        with torch.cuda.graph(g, stream=s, pool=self.g_fb.pool()):
+                            self.side.wait_stream(s)
+                            with torch.cuda.stream(self.side):
+                                state.tx.step_ns_phase_(store, state.opt_state)
+                            self._fb(images, join=lambda: s.wait_stream(self.side))
+                            state.tx.step_grad_phase_(store, state.opt_state)
+                    self.g_steady.append(g)
+                self.g_flush = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.g_flush, stream=s, pool=self.g_fb.pool()):
+                    state.tx.step_ns_phase_(store, state.opt_state)
             if self.g_opt is not None:
                 with torch.cuda.graph(self.g_opt, stream=s):
                     self._opt()
         torch.cuda.current_stream().wait_stream(s)
         self.metrics = self.runner.metrics
 
-    def _fb(self, images=None):
+    def _fb(self, images=None, join=None):
         K.zero_seed(self.state.params.grad_flat, self.runner.seed)   # zero grads + advance seed
-        self.runner.forward(self.images if images is None else images, None, train=True, need_grad=True)
+        kw = {"join": join} if join is not None else {}
+        self.runner.forward(self.images if images is None else images, None, train=True, need_grad=True, **kw)
         self.runner.backward(train=True)
 
+    def flush(self):
+        """Finish the last step's deferred matrix phase (overlap_opt): the params and optimizer state
+        are then exactly those after the steps taken.  A no-op otherwise."""
+        if self.pending:
+            self.g_flush.replay()
+            self.pending = False
+
     def _slot_of(self, images, labels):
+        """The input slot holding exactly this batch: both the images AND the labels must be that slot's
+        tensors (or views of the same storage and shape); anything else goes through the copy-in graph."""
+        if images is None or labels is None:
+            return None
+
+        def same(a, b):
+            return a is b or (a.data_ptr() == b.data_ptr() and a.shape == b.shape and a.dtype == b.dtype)
+
         for k, (x, y) in enumerate(self.slots):
-            if images is x or (images is not None and labels is not None and images.data_ptr() == x.data_ptr()
-                               and labels.data_ptr() == y.data_ptr() and images.shape == x.shape):
+            if same(images, x) and same(labels, y):
                 return k
         return None
 
@@ -342,14 +394,18 @@ class GraphedTrainStep:
 
     def __call__(self, images=None, labels=None):
         k = self._slot_of(images, labels) if self.slots else None
+        steady = self.overlap and self.pending
         if k is not None:
-            self.g_slots[k].replay()        # the batch is read in place from its input slot
+            # the batch is read in place from its input slot
+            (self.g_steady[k + 1] if steady else self.g_slots[k]).replay()
         else:
             if images is not None:
                 self.images.copy_(images, non_blocking=True)
             if labels is not None:
                 self.labels.copy_(labels, non_blocking=True)
-            self.g_fb.replay()
+            (self.g_steady[0] if steady else self.g_fb).replay()
+        if self.overlap:
+            self.pending = True
         if self.distributed:
             dp.all_reduce_grads(self.state.params)
             _reduce_batch_stats(self.state)

@@ -88,6 +88,8 @@ class Muon(GradientTransformation):
         routed, st.shard = sharding.setup(self, store, routed_all, sharding.muon_cost)
         b1, b2, eps_root, awd = self.adam
         st.branch = AdamBranch(store, rest, b1, b2, self.eps, eps_root, awd, self.nesterov, small_chunks=False)
+        # the split step's Adam branch runs as its own launch: 1024-element chunks (more workgroups)
+        st.branch_small = AdamBranch(store, rest, b1, b2, self.eps, eps_root, awd, self.nesterov)
         st.routed = routed
         # Group routed matrices by NS shape (min, max).  Groups whose operand fits one
         # workgroup's LDS (csrc/muon_fused.hip) run Newton-Schulz in a single launch; the
@@ -187,6 +189,29 @@ class Muon(GradientTransformation):
                       upd=None if apply else st.upd, apply=apply)
         K.step_bump(st.count)
         sharding.finish(st.shard, store, st, apply)
+
+    # ---- the step split in two phases, for overlapping the Newton-Schulz workgroups with the next
+    # step's forward (engine.GraphedTrainStep(overlap_opt=True)).  grad phase: momentum / Nesterov blend
+    # into the NS operands (muon_prep) and the Adam branch -- everything that reads the gradients; NS
+    # phase: the one-workgroup Newton-Schulz of every routed matrix (+ the step-counter bump) and the
+    # routed matrices' update.  grad phase of step t, then NS phase of step t, is exactly step_().
+    def split_capable(self, st):
+        return bool(st.routed) and st.n_general == 0 and st.vec4 and not self.adaptive and st.shard is None
+
+    def step_grad_phase_(self, store, st, gscale=None):
+        hip.call("pcv_muon_prep", ptr(st.mats_apply), len(st.routed), 0, st.max_elems, self.beta,
+                 int(self.nesterov), self.eps, ptr(st.count), ptr(gscale), stream_ptr())
+        st.branch_small.run(store, st.tensors["mu"], st.tensors["nu"], st.count, self.lr, gscale=gscale, apply=True)
+
+    def step_ns_phase_(self, store, st):
+        b1, b2, eps_root, awd = self.adam
+        hip.call("pcv_muon_step_fused", ptr(st.mats_apply), len(st.routed), None, 0, ptr(store.flat),
+                 ptr(store.grad_flat), ptr(st.tensors["mu"]), ptr(st.tensors["nu"]), ptr(store.shadow), None,
+                 self.lr, self.wd, self.beta, int(self.nesterov), self.eps, int(self.shape_scale), self.a, self.b,
+                 self.c, self.ns_steps, b1, b2, eps_root, awd, 1, ptr(st.count), None, ptr(st.ticket), 0,
+                 stream_ptr())
+        hip.call("pcv_muon_apply", ptr(st.mats_apply), len(st.routed), st.max_elems, self.lr, self.wd,
+                 int(self.shape_scale), 1, stream_ptr())
 
     def update(self, grads, state, params=None):
         ensure_grads(params, grads)

@@ -72,12 +72,12 @@ def test_sharded_optimizer_two_ranks(dev, tmp_path, optim, layout):
     reps = _two_ranks(tmp_path, f"shard:{optim}:{layout}")
     assert sum(r["owned"] for r in reps) == reps[0]["routed"], reps
     assert all(r["owned"] > 0 for r in reps), reps
-    # SOAP / Shampoo: measured exact.  Muon's Frobenius normaliser is an fp32 atomic sum of squares
-    # (not bitwise reproducible run to run, sharded or not) that bf16 Newton-Schulz turns into
-    # ~1e-4 relative parameter differences (~0.5 % of one update, inside MUON_TOL)
-    tol = 1e-3 if optim == "muon" else 1e-6
+    # every optimizer runs the same per-matrix kernels on the owner: Muon's Frobenius normaliser is an
+    # fp64 sum of fp32 block partials (no order dependence at these magnitudes), so the sharded step
+    # is expected to equal the unsharded one; 1e-6 leaves room only for a reordered fp32 reduction
     for r in reps:
-        assert r["max_rel_vs_unsharded"] <= tol, r
+        print(f"SHARD {optim} {layout} max_rel_vs_unsharded {r['max_rel_vs_unsharded']:.3e}")
+        assert r["max_rel_vs_unsharded"] <= 1e-6, r
         assert r["shadow_ok"], r
     assert reps[0]["checksum"] == reps[1]["checksum"], reps
 
@@ -112,3 +112,18 @@ def test_lm_on_ready_offsets_mark_final_gradients(dev):
         assert torch.equal(snap, store.grad_flat[off:n]), off
     # and the regions are not trivially empty: the last report covers every layer's gradient
     assert snaps[-1][1].abs().sum().item() > 0
+
+
+@pytest.mark.parametrize("kind,optim", [("vit", "muon"), ("vit", "soap"), ("lm", "muon"), ("lm", "shampoo")])
+def test_sharded_optimizer_inside_engines(dev, tmp_path, kind, optim):
+    """shard_optimizer=True through GraphedTrainStep (ViT) and compute_grads / apply_grads with the
+    OverlappedReducer and clip 1.0 (LM): 3 data-parallel steps, a sharded and an unsharded state
+    side by side -- params equal (the owner runs the same kernels on the same reduced gradients)
+    and the two replicas bit-identical."""
+    reps = _two_ranks(tmp_path, f"engine_shard:{kind}:{optim}")
+    assert all(r["owned"] > 0 for r in reps), reps
+    for r in reps:
+        print(f"ENGINE_SHARD {kind} {optim} max_rel_vs_unsharded {r['max_rel_vs_unsharded']:.3e}")
+        assert r["max_rel_vs_unsharded"] <= 1e-6, r
+        assert r["shadow_ok"], r
+    assert reps[0]["checksum"] == reps[1]["checksum"], reps

@@ -172,6 +172,9 @@ def test_graphed_step_input_slots(dev, dtype, optim):
     gb = GraphedTrainStep(sb, shape, warmup=2)
     assert len(ga.g_slots) == 3 and ga._slot_of(ring_x[1], ring_y[1]) == 1
     assert ga._slot_of(ring_x[1].clone(), ring_y[1]) is None
+    assert ga._slot_of(ring_x[1], ring_y[2]) is None        # a slot's images with other labels: copy-in
+    assert ga._slot_of(ring_x[1], ring_y[1].clone()) is None
+    assert ga._slot_of(ring_x[1], None) is None
     gb.runner.seed.copy_(ga.runner.seed)
     torch.cuda.synchronize()
     assert torch.equal(sa.params.flat, sb.params.flat)
@@ -184,3 +187,47 @@ def test_graphed_step_input_slots(dev, dtype, optim):
         assert abs(ma[0].item() - mb[0].item()) <= tol * abs(mb[0].item()), (it, ma, mb)
         assert ma[1].item() == mb[1].item()
     assert rel(sa.params.flat, sb.params.flat) < (1e-2 if optim == "soap" else 1e-5)
+
+
+@pytest.mark.parametrize("ring", [False, True])
+def test_graphed_step_optimizer_overlap(dev, ring):
+    """GraphedTrainStep(overlap_opt=True): Muon's Newton-Schulz phase of step t runs on a side stream
+    beside step t+1's forward head (joined before the first routed-weight read), the last step's in
+    flush().  Against the in-step optimizer on the same batches: the same loss every step and the
+    same params, optimizer moments and step counter after flush() -- bit for bit (the same kernels
+    on the same data, only reordered against independent work)."""
+    from plaincv_amd.engine import GraphedTrainStep, create_train_state
+    from plaincv_amd.models.vit_small import VisionTransformer
+    from utils import Config
+    m = VisionTransformer(num_classes=10, patch_size=4, hidden_size=64, mlp_dim=128, num_layers=2, num_heads=2,
+                          dropout_rate=0.1)
+    shape = (8, 16, 16, 3)
+    cfg = Config(optim="muon", lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9)
+    init = m.init(5, shape)
+    g = torch.Generator().manual_seed(7)
+    xs = torch.randint(0, 256, (3,) + shape, generator=g, dtype=torch.uint8).to(dev)
+    ys = torch.randint(0, 10, (3, shape[0]), generator=g, dtype=torch.int32).to(dev)
+    sa = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=init)
+    sb = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=init)
+    inputs = (xs, ys) if ring else None
+    ga = GraphedTrainStep(sa, shape, warmup=2, inputs=inputs, overlap_opt=True)
+    gb = GraphedTrainStep(sb, shape, warmup=2, inputs=inputs)
+    assert ga.overlap and not gb.overlap
+    gb.runner.seed.copy_(ga.runner.seed)
+    for it in range(6):
+        k = it % 3
+        ma = ga(xs[k], ys[k]).clone()
+        mb = gb(xs[k], ys[k]).clone()
+        torch.cuda.synchronize()
+        assert torch.equal(ma, mb), (it, ma, mb)
+        if it == 3:   # a flush mid-run, then the first (non-steady) graph again
+            ga.flush()
+            torch.cuda.synchronize()
+            assert torch.equal(sa.params.flat, sb.params.flat)
+    ga.flush()
+    torch.cuda.synchronize()
+    assert torch.equal(sa.params.flat, sb.params.flat)
+    assert torch.equal(sa.params.shadow, sb.params.shadow)
+    for name in ("mu", "nu"):
+        assert torch.equal(sa.opt_state.tensors[name], sb.opt_state.tensors[name]), name
+    assert torch.equal(sa.opt_state.count, sb.opt_state.count)

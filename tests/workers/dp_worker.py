@@ -143,6 +143,62 @@ def shard(rep, dev, optim, layout_name):
     rep["step_excess"] = 0.0
 
 
+def engine_shard(rep, dev, kind, optim):
+    """shard_optimizer inside the real engines: GraphedTrainStep (ViT: warm-up snapshot / restore, the
+    eager sharded optimizer after the captured forward / backward and the DP reduce) and LM
+    compute_grads / apply_grads (the OverlappedReducer finishing before the sharded step and its
+    broadcasts), a sharded and an unsharded state side by side on the same per-rank data for 3 steps:
+    the params must be equal and the replicas bit-identical."""
+    from utils import Config
+    rank = dist.get_rank()
+    base = dict(optim=optim, lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.95, precondition_frequency=2,
+                eps=1e-8 if optim == "soap" else (1e-4 if optim == "shampoo" else 1e-8))
+    g = torch.Generator().manual_seed(300 + rank)
+    if kind == "vit":
+        from plaincv_amd.engine import GraphedTrainStep, create_train_state
+        from plaincv_amd.models.vit_small import VisionTransformer
+        m = VisionTransformer(num_classes=10, patch_size=4, hidden_size=64, mlp_dim=128, num_layers=2, num_heads=2,
+                              dropout_rate=0.1)
+        shape = (8, 16, 16, 3)
+        init = m.init(3, shape)
+        states = [create_train_state(0, m, 1e-3, shape, 10, cfg=Config(shard_optimizer=sh, **base), init_params=init)
+                  for sh in (True, False)]
+        steps = [GraphedTrainStep(st, shape, warmup=2) for st in states]
+        for _ in range(3):
+            imgs = torch.randint(0, 256, shape, generator=g, dtype=torch.uint8).to(dev)
+            labels = torch.randint(0, 10, (shape[0],), generator=g, dtype=torch.int32).to(dev)
+            for step in steps:
+                step(imgs, labels)
+        stores = [st.params for st in states]
+        rep["owned"] = len(states[0].opt_state.shard.owned) if states[0].opt_state.shard is not None else -1
+    else:
+        from plaincv_amd.engine.lm import create_lm_state, make_apply_grads_fn, make_train_fns
+        from plaincv_amd.models.LM.constructor import construct_model
+        cfgs = [Config(model="transformer", vocab_size=512, d_model=128, expand="8/3", n_layers=2, n_heads=2,
+                       mlp_class="glu", seq_len=64, tie_embeddings=False, rope_theta=500000.0, dtype="bfloat16",
+                       seed=0, shard_optimizer=sh, **base) for sh in (True, False)]
+        model, _, variables = construct_model(cfgs[0])
+        states = [create_lm_state(c, model, variables, 2, dev, accum=2) for c in cfgs]
+        for st in states:
+            st.reducer.bucket = 4096   # several buckets launched during the last micro-step's backward
+        compute_grads, _ = make_train_fns()
+        apply_grads = make_apply_grads_fn(1.0)
+        for _ in range(3):
+            batches = [torch.randint(0, 512, (2, 65), generator=g, dtype=torch.int32).to(dev) for _ in range(2)]
+            for i, st in enumerate(states):
+                for x in batches:
+                    compute_grads(st, x)
+                states[i], _ = apply_grads(st)
+        stores = [st.params for st in states]
+        rep["owned"] = len(states[0].opt_state.shard.owned) if states[0].opt_state.shard is not None else -1
+    torch.cuda.synchronize()
+    a, u = stores[0].flat.cpu(), stores[1].flat.cpu()
+    rep["max_rel_vs_unsharded"] = float((a - u).abs().max() / u.abs().max())
+    rep["shadow_ok"] = bool(torch.equal(stores[0].shadow.cpu(), a.to(torch.bfloat16)))
+    rep["checksum"] = float(a.double().sum() + (a.double() ** 2).sum())
+    rep["step_excess"] = 0.0
+
+
 def main():
     which, out = sys.argv[1], sys.argv[2]
     dev = torch.device("cuda:0")
@@ -152,6 +208,9 @@ def main():
     if which.startswith("shard:"):
         _, optim, layout_name = which.split(":")
         shard(rep, dev, optim, layout_name)
+    elif which.startswith("engine_shard:"):
+        _, kind, optim = which.split(":")
+        engine_shard(rep, dev, kind, optim)
     else:
         (vit if which == "vit" else lm)(rep, dev)
     dist.barrier()
