@@ -225,6 +225,12 @@ int pcv_colsum(const void* x, int64_t ld, int64_t R, int N, int x_f32, float* ou
 int pcv_vit_patchify(const uint8_t* img, void* out, int B, int H, int W, int C, int patch, void* stream);
 int pcv_vit_embed_fwd(const float* patch, const float* cls, const float* pos, float* x, void* x_bf16,
                       int B, int T, int D, float rate, const uint32_t* seed, uint32_t site, void* stream);
+/* pcv_vit_embed_fwd followed by the first block's LayerNorm_0 in one launch (D <= 256, D % 4 == 0,
+ * 16-B aligned x / patch / cls / pos / LN parameters): x as pcv_vit_embed_fwd, y = bf16(LN(x)) with row
+ * stride ldy, mean / rstd per row -- bit-identical to the two-launch form (vit_small.py:110-116, 38). */
+int pcv_vit_embed_ln_fwd(const float* patch, const float* cls, const float* pos, float* x, int B, int T, int D,
+                         float rate, const uint32_t* seed, uint32_t site, const float* ln_scale, const float* ln_bias,
+                         void* y, int64_t ldy, float* mean, float* rstd, float eps, void* stream);
 int pcv_vit_embed_bwd(const float* dx, void* dpatch, float* dcls, float* dpos, float* dbias,
                       int B, int T, int D, float rate, const uint32_t* seed, uint32_t site, void* stream);
 /* nn.Embed gather / scatter-add (models/LM/transformer.py:361-369). */

@@ -59,6 +59,7 @@ SIGNATURES = {
     "pcv_colsum": [P, I64, I64, I32, I32, P, P],
     "pcv_vit_patchify": [P, P, I32, I32, I32, I32, I32, P],
     "pcv_vit_embed_fwd": [P, P, P, P, P, I32, I32, I32, F32, P, U32, P],
+    "pcv_vit_embed_ln_fwd": [P, P, P, P, I32, I32, I32, F32, P, U32, P, P, P, I64, P, P, F32, P],
     "pcv_vit_embed_bwd": [P, P, P, P, P, I32, I32, I32, F32, P, U32, P],
     "pcv_seed_next": [P, P],
     "pcv_zero_seed": [P, I64, P, P],

@@ -571,6 +571,16 @@ def vit_embed_fwd(patch_out, cls, pos, x, x_bf16, B, T, D, rate=0.0, seed=None, 
              ptr(seed), int(site), stream_ptr())
 
 
+def vit_embed_ln_fwd(patch_out, cls, pos, x, B, T, D, ln_scale, ln_bias, y, mean, rstd, rate=0.0, seed=None, site=0,
+                     eps=1e-6):
+    """vit_embed_fwd + LayerNorm_0 of the first block in one launch (bit-identical to the two launches)."""
+    _chk(patch_out.numel() == B * (T - 1) * D and x.numel() == B * T * D and pos.numel() == T * D and
+         x.dtype == F32 and y.dtype == BF16 and tuple(y.shape) == (B * T, D) and y.stride(1) == 1, "embed+ln fwd")
+    _dev(patch_out, cls, pos, x, ln_scale, ln_bias, y, mean, rstd)
+    hip.call("pcv_vit_embed_ln_fwd", ptr(patch_out), ptr(cls), ptr(pos), ptr(x), B, T, D, float(rate), ptr(seed),
+             int(site), ptr(ln_scale), ptr(ln_bias), ptr(y), y.stride(0), ptr(mean), ptr(rstd), float(eps), stream_ptr())
+
+
 def vit_embed_bwd(dx, dpatch, dcls, dpos, dbias, B, T, D, rate=0.0, seed=None, site=0):
     _chk(dx.numel() == B * T * D and dpatch.numel() == B * (T - 1) * D, "embed bwd")
     _dev(dx, dpatch, dcls, dpos, dbias)

@@ -270,6 +270,8 @@ class ViTRunner:
         # the short attention's delta formed by the dO GEMM's epilogue (PCV_VIT_DELTA_GEMM=0: in the
         # attention backward's prologue)
         self.delta_in_gemm = os.environ.get("PCV_VIT_DELTA_GEMM", "1") != "0"
+        # the patch embedding and the first LayerNorm_0 in one launch (PCV_VIT_EMBED_LN=0: two)
+        self.embed_ln = os.environ.get("PCV_VIT_EMBED_LN", "1") != "0"
         self.dy_m = [e(R, D) for _ in range(Lc)] if not self.fuse_ln else None
         self.dx_mid = [e(R, D) for _ in range(Lc)]
         self.dxb_mid = [e(R, D, dt=bf) for _ in range(Lc)]
@@ -419,7 +421,14 @@ class ViTRunner:
             self.labels.copy_(labels, non_blocking=True)
         K.vit_patchify(images, self.patches, m.patch_size)
         K.gemm(self.patches, self.Wconv, self.patch_out, bias=self.bconv)
-        K.vit_embed_fwd(self.patch_out, self.cls, self.pos, self.xs[0], None, B, T, D, rate, seed, SITE_EMBED)
+        # the first block's LayerNorm_0 rides along with the embedding (fused-LN runners)
+        embed_ln = self.fuse_ln and not self.bn and D <= 256 and self.embed_ln
+        if embed_ln:
+            w0 = self.w[0]
+            K.vit_embed_ln_fwd(self.patch_out, self.cls, self.pos, self.xs[0], B, T, D, w0["s0"], w0["c0"], self.y0[0],
+                               *self.st0[0], rate=rate, seed=seed, site=SITE_EMBED)
+        else:
+            K.vit_embed_fwd(self.patch_out, self.cls, self.pos, self.xs[0], None, B, T, D, rate, seed, SITE_EMBED)
         if rate > 0.0:
             K.attn_drop_mask(seed, site_attn(0), T, rate, self.attn_mask, layers=m.num_layers,
                              site_stride=site_attn(1) - site_attn(0))
@@ -434,7 +443,7 @@ class ViTRunner:
                     K.layernorm_fwd(x, w["s0"], w["c0"], self.y0[i], *self.st0[i])
                 else:
                     K.dropout_bwd_cast(x, self.y0[i])
-            elif i == 0:
+            elif i == 0 and not embed_ln:
                 K.layernorm_fwd(x, w["s0"], w["c0"], self.y0[0], *self.st0[0])
             K.gemm(self.y0[i], w["Wqkv"], self.qkv[i], bias=w["bqkv"])
             K.attn_fwd(self.qkv[i], self.o[i], self.lse[i], B, T, H, Dh, causal=False, drop_rate=rate,

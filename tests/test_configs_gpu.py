@@ -18,9 +18,13 @@
   the HIP step's own gradients, SOAP's factor EMAs at every step, and the SOAP basis checks of
   test_engine_parity_gpu.py after step 0 and after each refresh.
 * C2 (configs[1]) is test_engine_parity_gpu.py::test_vit_c2_exact_shapes_match_oracle (bf16 runner,
-  every gradient leaf) plus test_optim_parity_gpu.py's ``vit_c2`` Muon layout; C3 (configs[2]) is
-  test_lm_parity_gpu.py at d 768 plus the ``lm768`` AdamW layout; C5 (configs[4]) is the ``lm1024``
-  Muon layout (w_qkv 1024x3072, fc_gate|fc_up 1024x2730, fc2 2730x1024) of test_optim_parity_gpu.py.
+  every gradient leaf) plus test_optim_parity_gpu.py's ``vit_c2`` Muon layout; C3 (configs[2]) and C5
+  (configs[4]) are test_lm_geometry_gpu.py: the LM at d 768 / 12 heads / T 1024 / V 50257 (AdamW) and
+  d 1024 / 16 heads / F 2730 / T 2048 / V 50280 (Muon, clip 1.0) through compute_grads / apply_grads
+  against the bf16-placement and fp64 oracles (loss, every gradient leaf, global norm, the update, the
+  params after 3 steps), plus the ``lm768`` / ``lm1024`` optimizer layouts of test_optim_parity_gpu.py.
+  (test_lm_parity_gpu.py covers the other LM variants -- tied embeddings, MLP / MLPReluSquared, clip
+  0.05, SOAP / Shampoo past the LDS eigh -- at d 128 / 320.)
 """
 import pytest
 import torch

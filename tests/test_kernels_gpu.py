@@ -596,3 +596,29 @@ def test_vit_head_fused(dev, B, D, Kc, rate, split):
     assert rel(DYM.view(B, T * D)[:, :D].float(), want) < 4e-3
     others = DYM.view(B, T, D)[:, 1:]
     assert (others == 0).all()
+
+
+@pytest.mark.parametrize("rate", [0.0, 0.1])
+def test_vit_embed_ln_fused(dev, rate):
+    """pcv_vit_embed_ln_fwd == pcv_vit_embed_fwd + pcv_layernorm_fwd, bit for bit (x, y, mean, rstd)."""
+    from plaincv_amd import kernels as K_
+    B, T, D = 64, 257, 128
+    g = torch.Generator(device=dev).manual_seed(1)
+    patch = torch.randn(B * (T - 1), D, device=dev, generator=g)
+    cls, pos = torch.randn(D, device=dev, generator=g), torch.randn(T, D, device=dev, generator=g)
+    sc, bi = torch.randn(D, device=dev, generator=g), torch.randn(D, device=dev, generator=g)
+    seed = torch.tensor([11], dtype=torch.int32, device=dev)
+    outs = []
+    for fused in (True, False):
+        x = torch.empty(B * T, D, device=dev)
+        y = torch.empty(B * T, D, device=dev, dtype=torch.bfloat16)
+        mean, rstd = torch.empty(B * T, device=dev), torch.empty(B * T, device=dev)
+        if fused:
+            K_.vit_embed_ln_fwd(patch, cls, pos, x, B, T, D, sc, bi, y, mean, rstd, rate=rate, seed=seed, site=1)
+        else:
+            K_.vit_embed_fwd(patch, cls, pos, x, None, B, T, D, rate, seed, 1)
+            K_.layernorm_fwd(x, sc, bi, y, mean, rstd)
+        torch.cuda.synchronize()
+        outs.append((x, y, mean, rstd))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
