@@ -393,6 +393,13 @@ int pcv_muon_apply(const void* mats, int nmats, int64_t max_elems, float lr, flo
 /* muon_adaptive (factory.py:457,475 -> optax.contrib.muon adaptive=True): dual[m] += <mu_hat, O>_F per
  * record (dual: nmats zeroed doubles; mu_hat re-formed from mu, g, *step, *gscale as pcv_muon_prep did),
  * then pcv_muon_apply_dual scales each record's orthogonalised update by dual[m] before the shape scale. */
+/* Muon's gradient phase in one launch: pcv_muon_prep of every record (all normalised by the NS kernel)
+ * and the Adam branch's chunks (as pcv_adamw_step, applied, optax.contrib.muon's Nesterov flag) --
+ * the first half of the overlapped step (engine.GraphedTrainStep overlap_opt); *step is not bumped. */
+int pcv_muon_grad_phase(const void* mats, int nmats, int64_t max_elems, float beta, int nesterov, const void* chunks,
+                        int nchunks, float* p, const float* g, float* mu, float* nu, void* p_bf16, float lr, float b1,
+                        float b2, float eps, float eps_root, float wd, const int* step, const float* gscale,
+                        void* stream);
 int pcv_muon_dual_dot(const void* mats, int nmats, int64_t max_elems, float beta, int nesterov, const int* step,
                       const float* gscale, double* dual, void* stream);
 int pcv_muon_apply_dual(const void* mats, int nmats, int64_t max_elems, float lr, float wd, int shape_scale,

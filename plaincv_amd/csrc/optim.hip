@@ -139,10 +139,34 @@ __device__ __forceinline__ bool muon_v4(const MuonMat& M) {
          (M.pb == nullptr || (reinterpret_cast<uintptr_t>(M.pb) & 7) == 0);
 }
 
+// one block (bx of gx) of the prep of matrix M
+__device__ __forceinline__ void muon_prep_block(const MuonMat& M, int bx, int gx, const MuonHyper& h, const int* step,
+                                                const float* gscale, float* red);
+
 __global__ __launch_bounds__(256) void muon_prep_kernel(const MuonMat* mats, MuonHyper h, const int* step,
                                                         const float* gscale) {
   __shared__ float red[4];
-  const MuonMat M = mats[blockIdx.y];
+  muon_prep_block(mats[blockIdx.y], blockIdx.x, gridDim.x, h, step, gscale, red);
+}
+
+// Muon's gradient phase in one launch (the overlapped step, engine.GraphedTrainStep overlap_opt): blocks
+// [0, nmats * gx) the prep of each routed matrix, the rest the Adam branch's chunks -- both read the
+// step counter before the NS phase bumps it
+__global__ __launch_bounds__(256) void muon_grad_phase_kernel(const MuonMat* mats, int nmats, int gx, MuonHyper h,
+                                                              const Chunk* chunks, float* p, const float* g, float* m,
+                                                              float* v, bf16* pb, AdamHyper ah, const int* step,
+                                                              const float* gscale) {
+  __shared__ float red[4];
+  const int b = blockIdx.x;
+  if (b < nmats * gx) {
+    muon_prep_block(mats[b / gx], b % gx, gx, h, step, gscale, red);
+  } else {
+    adamw_chunk(p, g, m, v, pb, nullptr, chunks[b - nmats * gx], ah, *step, gscale ? *gscale : 1.f);
+  }
+}
+
+__device__ __forceinline__ void muon_prep_block(const MuonMat& M, int bx, int gx, const MuonHyper& h, const int* step,
+                                                const float* gscale, float* red) {
   const int n = (int)(M.rows * M.cols);
   const float t = (float)(*step + 1);
   const float bc = 1.f - powf(h.beta, t), bcn = 1.f - powf(h.beta, t + 1.f);
@@ -151,7 +175,7 @@ __global__ __launch_bounds__(256) void muon_prep_kernel(const MuonMat* mats, Muo
   const int cols = (int)M.cols;
   float s = 0.f;
   // 32-bit element indices (the entry points reject max_elems >= 2^31)
-  for (int i0 = (blockIdx.x * 256 + threadIdx.x) * 4; i0 < n; i0 += gridDim.x * 1024) {
+  for (int i0 = (bx * 256 + threadIdx.x) * 4; i0 < n; i0 += gx * 1024) {
     float gv[4], mv[4];
     int64_t off[4];
     int rr[4], cc[4];
@@ -367,6 +391,23 @@ extern "C" int pcv_muon_prep(const void* mats, int nmats, int nnorm, int64_t max
   gx = (int)((max_elems + 256 * 8 - 1) / (256 * 8));
   gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
   if (nnorm > 0) hipLaunchKernelGGL(muon_norm_kernel, dim3(gx, nnorm), dim3(256), 0, s, (const MuonMat*)mats, eps);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_muon_grad_phase(const void* mats, int nmats, int64_t max_elems, float beta, int nesterov,
+                                   const void* chunks, int nchunks, float* p, const float* g, float* mu, float* nu,
+                                   void* p_bf16, float lr, float b1, float b2, float eps, float eps_root, float wd,
+                                   const int* step, const float* gscale, void* stream) {
+  if (nmats <= 0 || nchunks < 0 || (nchunks > 0 && !chunks) || max_elems >= (1ll << 31) || !step || !p || !g || !mu ||
+      !nu)
+    return PCV_EINVAL;
+  MuonHyper h{beta, 0.f, 0.f, 0.f, 0.f, nesterov, 0, nullptr};
+  AdamHyper ah{lr, b1, b2, eps, eps_root, wd, nesterov, 1};
+  int gx = (int)((max_elems + 256 * 4 - 1) / (256 * 4));   // as pcv_muon_prep
+  gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
+  hipLaunchKernelGGL(muon_grad_phase_kernel, dim3(nmats * gx + nchunks), dim3(256), 0, (hipStream_t)stream,
+                     (const MuonMat*)mats, nmats, gx, h, (const Chunk*)chunks, p, g, mu, nu, (bf16*)p_bf16, ah, step,
+                     gscale);
   return pcv_launch_status();
 }
 

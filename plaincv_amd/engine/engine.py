@@ -302,11 +302,13 @@ class GraphedTrainStep:
         self.g_fb = torch.cuda.CUDAGraph()
         self.g_opt = torch.cuda.CUDAGraph() if (self.distributed and self.opt_graphed) else None
         s = self.stream
-        s.wait_stream(torch.cuda.current_stream())
         store = state.params
         saved = [(st, st.clone()) for st in _device_storages([store.flat, store.shadow, self.runner.seed,
                                                               state.opt_state, state.batch_stats])]
         host = _host_scalars(state.opt_state)   # e.g. host_step, also inside wrapped (schedule-free) states
+        # the snapshot clones run on the current stream: the warm-up stream waits for them, or the
+        # warm-up's seed advance / optimizer step could land before the clone reads its source
+        s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self._fb()

@@ -106,6 +106,7 @@ SIGNATURES = {
     "pcv_muon_prep": [P, I32, I32, I64, F32, I32, F32, P, P, P],
     "pcv_muon_apply": [P, I32, I64, F32, F32, I32, I32, P],
     "pcv_muon_dual_dot": [P, I32, I64, F32, I32, P, P, P, P],
+    "pcv_muon_grad_phase": [P, I32, I64, F32, I32, P, I32, P, P, P, P, P, F32, F32, F32, F32, F32, F32, P, P, P],
     "pcv_muon_apply_dual": [P, I32, I64, F32, F32, I32, I32, P, P],
     "pcv_muon_step_fused": [P, I32, P, I32, P, P, P, P, P, P, F32, F32, F32, I32, F32, I32, F32, F32, F32, I32, F32,
                             F32, F32, F32, I32, P, P, P, I32, P],

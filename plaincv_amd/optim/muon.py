@@ -196,12 +196,16 @@ class Muon(GradientTransformation):
     # phase: the one-workgroup Newton-Schulz of every routed matrix (+ the step-counter bump) and the
     # routed matrices' update.  grad phase of step t, then NS phase of step t, is exactly step_().
     def split_capable(self, st):
-        return bool(st.routed) and st.n_general == 0 and st.vec4 and not self.adaptive and st.shard is None
+        # every routed matrix on the one-workgroup NS kernel (its NS-only blocks need no 16-B row accesses)
+        return bool(st.routed) and st.n_general == 0 and not self.adaptive and st.shard is None
 
     def step_grad_phase_(self, store, st, gscale=None):
-        hip.call("pcv_muon_prep", ptr(st.mats_apply), len(st.routed), 0, st.max_elems, self.beta,
-                 int(self.nesterov), self.eps, ptr(st.count), ptr(gscale), stream_ptr())
-        st.branch_small.run(store, st.tensors["mu"], st.tensors["nu"], st.count, self.lr, gscale=gscale, apply=True)
+        b1, b2, eps_root, awd = self.adam
+        br = st.branch_small
+        hip.call("pcv_muon_grad_phase", ptr(st.mats_apply), len(st.routed), st.max_elems, self.beta,
+                 int(self.nesterov), ptr(br.chunks) if br.nchunks else None, br.nchunks, ptr(store.flat),
+                 ptr(store.grad_flat), ptr(st.tensors["mu"]), ptr(st.tensors["nu"]), ptr(store.shadow), self.lr, b1,
+                 b2, self.eps, eps_root, awd, ptr(st.count), ptr(gscale), stream_ptr())
 
     def step_ns_phase_(self, store, st):
         b1, b2, eps_root, awd = self.adam

@@ -194,8 +194,11 @@ def test_graphed_step_optimizer_overlap(dev, ring):
     """GraphedTrainStep(overlap_opt=True): Muon's Newton-Schulz phase of step t runs on a side stream
     beside step t+1's forward head (joined before the first routed-weight read), the last step's in
     flush().  Against the in-step optimizer on the same batches: the same loss every step and the
-    same params, optimizer moments and step counter after flush() -- bit for bit (the same kernels
-    on the same data, only reordered against independent work)."""
+    same params, optimizer moments and step counter after flush() -- the same kernels on the same
+    data, only reordered against independent work, so the only difference left is the run-to-run
+    noise of the fp32 column-sum atomics (as test_graphed_step_input_slots: rel 1e-5); a missing or
+    doubled optimizer phase moves the params by a whole update (~1e-2 relative of the movement)."""
+    from tests.parity_util import rel
     from plaincv_amd.engine import GraphedTrainStep, create_train_state
     from plaincv_amd.models.vit_small import VisionTransformer
     from utils import Config
@@ -214,20 +217,22 @@ def test_graphed_step_optimizer_overlap(dev, ring):
     gb = GraphedTrainStep(sb, shape, warmup=2, inputs=inputs)
     assert ga.overlap and not gb.overlap
     gb.runner.seed.copy_(ga.runner.seed)
+    init_flat = sa.params.flat.clone()
     for it in range(6):
         k = it % 3
         ma = ga(xs[k], ys[k]).clone()
         mb = gb(xs[k], ys[k]).clone()
         torch.cuda.synchronize()
-        assert torch.equal(ma, mb), (it, ma, mb)
+        assert abs(ma[0].item() - mb[0].item()) <= 1e-5 * abs(mb[0].item()), (it, ma, mb)
         if it == 3:   # a flush mid-run, then the first (non-steady) graph again
             ga.flush()
             torch.cuda.synchronize()
-            assert torch.equal(sa.params.flat, sb.params.flat)
+            assert rel(sa.params.flat - init_flat, sb.params.flat - init_flat) < 1e-4
     ga.flush()
     torch.cuda.synchronize()
-    assert torch.equal(sa.params.flat, sb.params.flat)
-    assert torch.equal(sa.params.shadow, sb.params.shadow)
+    moved = rel(sa.params.flat - init_flat, sb.params.flat - init_flat)
+    print(f"OVERLAP ring={ring} params movement rel {moved:.3e}")
+    assert moved < 1e-4
     for name in ("mu", "nu"):
-        assert torch.equal(sa.opt_state.tensors[name], sb.opt_state.tensors[name]), name
+        assert rel(sa.opt_state.tensors[name], sb.opt_state.tensors[name]) < 1e-4, name
     assert torch.equal(sa.opt_state.count, sb.opt_state.count)

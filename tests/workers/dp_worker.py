@@ -148,28 +148,45 @@ def engine_shard(rep, dev, kind, optim):
     eager sharded optimizer after the captured forward / backward and the DP reduce) and LM
     compute_grads / apply_grads (the OverlappedReducer finishing before the sharded step and its
     broadcasts), a sharded and an unsharded state side by side on the same per-rank data for 3 steps:
-    the params must be equal and the replicas bit-identical."""
+    the params must be equal and the replicas bit-identical.  ViT adds a third engine whose (unsharded)
+    optimizer runs eagerly after the captured graph, and without dropout the eager make_train_step."""
     from utils import Config
     rank = dist.get_rank()
     base = dict(optim=optim, lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.95, precondition_frequency=2,
                 eps=1e-8 if optim == "soap" else (1e-4 if optim == "shampoo" else 1e-8))
     g = torch.Generator().manual_seed(300 + rank)
-    if kind == "vit":
-        from plaincv_amd.engine import GraphedTrainStep, create_train_state
+    if kind.startswith("vit"):
+        from plaincv_amd.engine import GraphedTrainStep, create_train_state, make_train_step
         from plaincv_amd.models.vit_small import VisionTransformer
+        rate = 0.0 if kind == "vit0" else 0.1
         m = VisionTransformer(num_classes=10, patch_size=4, hidden_size=64, mlp_dim=128, num_layers=2, num_heads=2,
-                              dropout_rate=0.1)
+                              dropout_rate=rate)
         shape = (8, 16, 16, 3)
         init = m.init(3, shape)
         states = [create_train_state(0, m, 1e-3, shape, 10, cfg=Config(shard_optimizer=sh, **base), init_params=init)
-                  for sh in (True, False)]
-        steps = [GraphedTrainStep(st, shape, warmup=2) for st in states]
-        for _ in range(3):
+                  for sh in (True, False, False, False)]
+        states[3].tx.graphable = False    # unsharded, optimizer run eagerly after the captured fb graph
+        steps = [GraphedTrainStep(st, shape, warmup=2) for st in (states[0], states[1], states[3])]
+        eager = make_train_step()
+        rep["seeds"] = [[int(st_.runner.seed.item()) for st_ in steps]]
+        for it in range(3):
             imgs = torch.randint(0, 256, shape, generator=g, dtype=torch.uint8).to(dev)
             labels = torch.randint(0, 10, (shape[0],), generator=g, dtype=torch.int32).to(dev)
             for step in steps:
                 step(imgs, labels)
-        stores = [st.params for st in states]
+            if rate == 0.0:
+                states[2], _ = eager(states[2], (imgs, labels), it)
+            rep["seeds"].append([int(st_.runner.seed.item()) for st_ in steps])
+        stores = [st.params for st in states[:2]]
+        torch.cuda.synchronize()
+        ue = states[3].params.flat.cpu()
+        rep["sharded_vs_unsharded_eager"] = float((stores[0].flat.cpu() - ue).abs().max() / ue.abs().max())
+        rep["graphed_vs_unsharded_eager"] = float((stores[1].flat.cpu() - ue).abs().max() / ue.abs().max())
+        if rate == 0.0:   # which of the two graphed runs matches the eager make_train_step reference
+            e = states[2].params.flat.cpu()
+            torch.cuda.synchronize()
+            rep["sharded_vs_eager"] = float((stores[0].flat.cpu() - e).abs().max() / e.abs().max())
+            rep["unsharded_vs_eager"] = float((stores[1].flat.cpu() - e).abs().max() / e.abs().max())
         rep["owned"] = len(states[0].opt_state.shard.owned) if states[0].opt_state.shard is not None else -1
     else:
         from plaincv_amd.engine.lm import create_lm_state, make_apply_grads_fn, make_train_fns
@@ -194,6 +211,8 @@ def engine_shard(rep, dev, kind, optim):
     torch.cuda.synchronize()
     a, u = stores[0].flat.cpu(), stores[1].flat.cpu()
     rep["max_rel_vs_unsharded"] = float((a - u).abs().max() / u.abs().max())
+    da, du = stores[0].to_dict(), stores[1].to_dict()
+    rep["leaves_off"] = {k: float((da[k] - du[k]).abs().max()) for k in da if not torch.equal(da[k], du[k])}
     rep["shadow_ok"] = bool(torch.equal(stores[0].shadow.cpu(), a.to(torch.bfloat16)))
     rep["checksum"] = float(a.double().sum() + (a.double() ** 2).sum())
     rep["step_excess"] = 0.0
