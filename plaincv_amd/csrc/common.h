@@ -29,6 +29,15 @@ namespace pcv {
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 
+// host: dropout keep threshold on hash3's 32-bit output (drop iff hash < thresh) and the keep scale
+inline void drop_params(float rate, uint32_t* thresh, float* scale) {
+  *thresh = 0; *scale = 1.f;
+  if (rate > 0.f) {
+    double t = (double)rate * 4294967296.0;
+    *thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+    *scale = 1.f / (1.f - rate);
+  }
+}
 // 32-bit lowbias hash of (seed, site, idx); restated in oracle/rng.py.
 __device__ __forceinline__ uint32_t hash3(uint32_t seed, uint32_t site, uint32_t idx) {
   uint32_t x = idx * 0x9E3779B1u + site * 0x85EBCA77u + seed * 0xC2B2AE3Du;

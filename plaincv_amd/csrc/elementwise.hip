@@ -190,56 +190,6 @@ __global__ void vit_embed_fwd_kernel(const float* patch, const float* cls, const
   }
 }
 
-// vit_embed_fwd + the first encoder block's LayerNorm_0 (models/vit_small.py:110-116 + 38) in one pass:
-// one wave per token row (D <= 256, 4 columns per lane), x = dropout(cls | patch + pos) written in fp32,
-// then y = LN(x) (bf16), mean / rstd -- the same element hash index as vit_embed_fwd_kernel and the
-// same reduction order as ln_fwd_kernel<1>, so x, y and the statistics equal the two-launch form bit
-// for bit.  (Saves one launch and the LN's re-read of x.)
-__global__ __launch_bounds__(256) void vit_embed_ln_fwd_kernel(const float* patch, const float* cls, const float* pos,
-                                                               float* x, int B, int T, int D, uint32_t thresh,
-                                                               float dscale, const uint32_t* seedp, uint32_t site,
-                                                               const float* lscale, const float* lbias, bf16* y,
-                                                               int64_t ldy, float* mean_out, float* rstd_out,
-                                                               float eps) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= (int64_t)B * T) return;
-  const uint32_t seed = thresh ? *seedp : 0u;
-  const int t = (int)(row % T), b = (int)(row / T);
-  const int c = lane * 4;
-  float v[4] = {0.f, 0.f, 0.f, 0.f};
-  float s = 0.f, s2 = 0.f;
-  if (c < D) {
-    const float* src = t == 0 ? cls + c : patch + ((int64_t)b * (T - 1) + t - 1) * D + c;
-    const float4 a = *reinterpret_cast<const float4*>(src);
-    const float4 p = *reinterpret_cast<const float4*>(pos + (int64_t)t * D + c);
-    v[0] = a.x + p.x; v[1] = a.y + p.y; v[2] = a.z + p.z; v[3] = a.w + p.w;
-    const int64_t i0 = row * D + c;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (thresh) v[j] = hash3(seed, site, (uint32_t)(i0 + j)) >= thresh ? v[j] * dscale : 0.f;
-      s += v[j];
-      s2 += v[j] * v[j];
-    }
-    *reinterpret_cast<float4*>(x + i0) = float4{v[0], v[1], v[2], v[3]};
-  }
-  s = wave_sum(s);
-  s2 = wave_sum(s2);
-  const float mean = s / D;
-  const float var = fmaxf(s2 / D - mean * mean, 0.f);
-  const float rs = rsqrtf(var + eps);
-  if (c < D) {
-    const float4 sc = *reinterpret_cast<const float4*>(lscale + c), bi = *reinterpret_cast<const float4*>(lbias + c);
-    bf16x4 o;
-    o[0] = f2bf((v[0] - mean) * rs * sc.x + bi.x);
-    o[1] = f2bf((v[1] - mean) * rs * sc.y + bi.y);
-    o[2] = f2bf((v[2] - mean) * rs * sc.z + bi.z);
-    o[3] = f2bf((v[3] - mean) * rs * sc.w + bi.w);
-    *reinterpret_cast<bf16x4*>(y + row * ldy + c) = o;
-  }
-  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rs; }
-}
-
 // g = dx*mask; dpatch[b*hw+i] = bf16(g[b,1+i]); dpos[t] += sum_b g[b,t]; dcls += sum_b g[b,0];
 // dbias += sum_{b,t>=1} g[b,t]
 __global__ void vit_embed_bwd_kernel(const float* dx, bf16* dpatch, float* dcls, float* dpos, float* dbias, int B,
@@ -307,15 +257,6 @@ static int grid_for(int64_t n, int block = 256) {
   if (g > 4096) g = 4096;
   return (int)(g < 1 ? 1 : g);
 }
-static void drop_params(float rate, uint32_t* thresh, float* scale) {
-  *thresh = 0; *scale = 1.f;
-  if (rate > 0.f) {
-    double t = (double)rate * 4294967296.0;
-    *thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
-    *scale = 1.f / (1.f - rate);
-  }
-}
-
 }  // namespace pcv
 
 using namespace pcv;
@@ -415,24 +356,6 @@ extern "C" int pcv_vit_embed_fwd(const float* patch, const float* cls, const flo
   const int64_t n = (int64_t)B * T * D;
   hipLaunchKernelGGL(vit_embed_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, patch, cls, pos, x,
                      (bf16*)x_bf16, B, T, D, th, sc, seed, site);
-  return pcv_launch_status();
-}
-
-extern "C" int pcv_vit_embed_ln_fwd(const float* patch, const float* cls, const float* pos, float* x, int B, int T,
-                                    int D, float rate, const uint32_t* seed, uint32_t site, const float* ln_scale,
-                                    const float* ln_bias, void* y, int64_t ldy, float* mean, float* rstd, float eps,
-                                    void* stream) {
-  if (B <= 0 || T <= 1 || D <= 0 || D > 256 || (D & 3) || (ldy & 3) || !ln_scale || !ln_bias || !y || !mean || !rstd)
-    return PCV_EINVAL;
-  if (rate > 0.f && !seed) return PCV_EINVAL;
-  if (((uintptr_t)patch | (uintptr_t)cls | (uintptr_t)pos | (uintptr_t)x | (uintptr_t)ln_scale | (uintptr_t)ln_bias) & 15)
-    return PCV_EALIGN;
-  if ((uintptr_t)y & 7) return PCV_EALIGN;
-  uint32_t th; float sc;
-  drop_params(rate, &th, &sc);
-  const int64_t R = (int64_t)B * T;
-  hipLaunchKernelGGL(vit_embed_ln_fwd_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, (hipStream_t)stream, patch,
-                     cls, pos, x, B, T, D, th, sc, seed, site, ln_scale, ln_bias, (bf16*)y, ldy, mean, rstd, eps);
   return pcv_launch_status();
 }
 

@@ -33,22 +33,18 @@ __device__ __forceinline__ void st4(bf16* p, const F4& f) {
 }
 
 // ----------------------------------------------------------------- LayerNorm
+// One row's statistics and normalised output from its values already in registers (lane holds
+// columns [(i * 64 + lane) * 4, +4)): shared by ln_fwd_kernel and vit_embed_ln_fwd_kernel, so the
+// fused embed + LN equals the two-launch form bit for bit (one instruction sequence, one TU).
 template <int NV>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* x, int64_t ldx, const float* scale,
-                                                     const float* bias, bf16* y, int64_t ldy, float* mean_out,
-                                                     float* rstd_out, int64_t R, int D, float eps) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= R) return;
-  F4 v[NV];
+__device__ __forceinline__ void ln_row_fwd(const F4 (&v)[NV], int lane, int D, const float* scale, const float* bias,
+                                           bf16* yrow, float* mean_out, float* rstd_out, int64_t row, float eps) {
   float s = 0.f, s2 = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int c = (i * 64 + lane) * 4;
-    if (c < D) {
-      v[i] = ld4(x + row * ldx + c);
+    if ((i * 64 + lane) * 4 < D) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { s += v[i].v[j]; s2 += v[i].v[j] * v[i].v[j]; }
+      for (int j = 0; j < 4; ++j) { s += v[i].v[j]; s2 = fmaf(v[i].v[j], v[i].v[j], s2); }
     }
   }
   s = wave_sum(s);
@@ -62,11 +58,61 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* x, int64_t ldx
     if (c < D) {
       F4 sc = ld4(scale + c), bi = ld4(bias + c), o;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o.v[j] = (v[i].v[j] - mean) * rs * sc.v[j] + bi.v[j];
-      st4(y + row * ldy + c, o);
+      // explicit roundings: no contraction left to the compiler, whose choice differed between the
+      // two kernels (1-ulp bf16 differences in a few elements)
+      for (int j = 0; j < 4; ++j) o.v[j] = fmaf(__fmul_rn(__fsub_rn(v[i].v[j], mean), rs), sc.v[j], bi.v[j]);
+      st4(yrow + c, o);
     }
   }
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rs; }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* x, int64_t ldx, const float* scale,
+                                                     const float* bias, bf16* y, int64_t ldy, float* mean_out,
+                                                     float* rstd_out, int64_t R, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  F4 v[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D) v[i] = ld4(x + row * ldx + c);
+  }
+  ln_row_fwd<NV>(v, lane, D, scale, bias, y + row * ldy, mean_out, rstd_out, row, eps);
+}
+
+// vit_embed_fwd + the first encoder block's LayerNorm_0 (models/vit_small.py:110-116 + 38) in one pass:
+// one wave per token row (D <= 256, 4 columns per lane), x = dropout(cls | patch + pos) written in fp32
+// with vit_embed_fwd_kernel's element hash index (elementwise.hip), then LN through ln_row_fwd -- x, y
+// and the statistics equal the two-launch form bit for bit.  (Saves one launch and the LN's re-read of x.)
+__global__ __launch_bounds__(256) void vit_embed_ln_fwd_kernel(const float* patch, const float* cls, const float* pos,
+                                                               float* x, int B, int T, int D, uint32_t thresh,
+                                                               float dscale, const uint32_t* seedp, uint32_t site,
+                                                               const float* lscale, const float* lbias, bf16* y,
+                                                               int64_t ldy, float* mean_out, float* rstd_out,
+                                                               float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (int64_t)B * T) return;
+  const uint32_t seed = thresh ? *seedp : 0u;
+  const int t = (int)(row % T), b = (int)(row / T);
+  const int c = lane * 4;
+  F4 v[1];
+  if (c < D) {
+    const F4 a = ld4(t == 0 ? cls + c : patch + ((int64_t)b * (T - 1) + t - 1) * D + c);
+    const F4 p = ld4(pos + (int64_t)t * D + c);
+    const int64_t i0 = row * D + c;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float e = a.v[j] + p.v[j];
+      if (thresh) e = hash3(seed, site, (uint32_t)(i0 + j)) >= thresh ? e * dscale : 0.f;
+      v[0].v[j] = e;
+    }
+    st4(x + i0, v[0]);
+  }
+  ln_row_fwd<1>(v, lane, D, lscale, lbias, y + row * ldy, mean_out, rstd_out, row, eps);
 }
 
 // dx = dres + rstd*(g - mean(g) - xhat*mean(g*xhat)),  g = dy*scale
@@ -240,6 +286,24 @@ extern "C" int pcv_layernorm_fwd(const float* x, int64_t ldx, const float* scale
   hipStream_t s = (hipStream_t)stream;
   PCV_NV_DISPATCH(D, hipLaunchKernelGGL(ln_fwd_kernel<NV>, grid_rows(R), dim3(256), 0, s, x, ldx, scale, bias,
                                         (bf16*)y, ldy, mean, rstd, R, D, eps));
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_vit_embed_ln_fwd(const float* patch, const float* cls, const float* pos, float* x, int B, int T,
+                                    int D, float rate, const uint32_t* seed, uint32_t site, const float* ln_scale,
+                                    const float* ln_bias, void* y, int64_t ldy, float* mean, float* rstd, float eps,
+                                    void* stream) {
+  if (B <= 0 || T <= 1 || D <= 0 || D > 256 || (D & 3) || (ldy & 3) || !ln_scale || !ln_bias || !y || !mean || !rstd)
+    return PCV_EINVAL;
+  if (rate > 0.f && !seed) return PCV_EINVAL;
+  if (((uintptr_t)patch | (uintptr_t)cls | (uintptr_t)pos | (uintptr_t)x | (uintptr_t)ln_scale | (uintptr_t)ln_bias) & 15)
+    return PCV_EALIGN;
+  if ((uintptr_t)y & 7) return PCV_EALIGN;
+  uint32_t th; float sc;
+  drop_params(rate, &th, &sc);
+  const int64_t R = (int64_t)B * T;
+  hipLaunchKernelGGL(vit_embed_ln_fwd_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, (hipStream_t)stream, patch,
+                     cls, pos, x, B, T, D, th, sc, seed, site, ln_scale, ln_bias, (bf16*)y, ldy, mean, rstd, eps);
   return pcv_launch_status();
 }
 
