@@ -348,22 +348,37 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : PCV_ATTN_FWD_OCC) void attn_fw
 #pragma unroll
           for (int t = 0; t < 4; ++t) wt[t] = (uint32_t)(mw >> (16 * t)) >> (4 * (myq & 3));
         }
-        const float mneg = -m2[gq];
-        float rs = 0.f;
+        // packed fp32 pairs for the scaling and the row sum (VALU issue is what the softmax costs;
+        // see the short kernels)
+        const f2v mn2 = {-m2[gq], -m2[gq]}, c2v = {c2, c2};
+        f2v rs2 = {0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float p = __builtin_amdgcn_exp2f(fmaf(s[gq][t][r], c2, mneg));
-            // masked keys contribute exactly 0 (under a document mask a row can see no valid key in
-            // a tile while its running max is still the initial value)
-            if (MASK) p = ((okbits >> (4 * t + r)) & 1u) ? p : 0.f;
-            rs += p;
-            // dropped weights -> 0 (bit select); the 1/keep scale is applied at the end
-            if (DROP) p = __uint_as_float(__float_as_uint(p) & (uint32_t)__builtin_amdgcn_sbfe((int)wt[t], r, 1));
-            s[gq][t][r] = p;
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const f2v x = __builtin_elementwise_fma((f2v){s[gq][t][2 * h2], s[gq][t][2 * h2 + 1]}, c2v, mn2);
+            float p[2] = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const int r = 2 * h2 + e;
+              // masked keys contribute exactly 0 (under a document mask a row can see no valid key in
+              // a tile while its running max is still the initial value)
+              if (MASK) p[e] = ((okbits >> (4 * t + r)) & 1u) ? p[e] : 0.f;
+            }
+            rs2 += (f2v){p[0], p[1]};
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const int r = 2 * h2 + e;
+              // dropped weights -> 0 (bit select); the 1/keep scale is applied at the end
+              if (DROP) {
+                int km = __builtin_amdgcn_sbfe((int)wt[t], r, 1);
+                asm volatile("" : "+v"(km));
+                p[e] = __uint_as_float(__float_as_uint(p[e]) & (uint32_t)km);
+              }
+              s[gq][t][r] = p[e];
+            }
           }
-        rs = xsum_rows(rs);
+        const float rs = xsum_rows(rs2.x + rs2.y);
         lsum[gq] += rs;
       };
 #pragma unroll
@@ -672,6 +687,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : PCV_ATTN_DQ_OCC) void attn_bwd
     }
   }
   const float c2 = a.scale * LOG2E;
+  const f2v c2v = {c2, c2}, dsc = {DROP ? a.drop_scale : 1.f, DROP ? a.drop_scale : 1.f};
   f32x4 acc[QG][DT];
 #pragma unroll
   for (int gq = 0; gq < QG; ++gq)
@@ -723,21 +739,37 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : PCV_ATTN_DQ_OCC) void attn_bwd
             const int myq = qw + gq * 16 + (lane & 15);
             uint32_t wt = 0;
             if (DROP) wt = (uint32_t)a.mask[drop_word(myq, kb * 64 + 16 * t + 4 * g, a.n64)] >> (4 * (myq & 3));
+            float pv[4], dm[4];
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) {
+              const f2v x = __builtin_elementwise_fma((f2v){sv[gq][2 * h2], sv[gq][2 * h2 + 1]}, c2v,
+                                                      (f2v){-myl[gq], -myl[gq]});
+              pv[2 * h2] = __builtin_amdgcn_exp2f(x.x);
+              pv[2 * h2 + 1] = __builtin_amdgcn_exp2f(x.y);
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              float pv = __builtin_amdgcn_exp2f(fmaf(sv[gq][r], c2, -myl[gq]));
               if constexpr (!INTERIOR) {
                 const int key = kb * 64 + 16 * t + 4 * g + r;
                 bool ok = myq < T && key < T;
                 if (CAUSAL) ok = ok && key <= myq;
                 if (doc) ok = ok && key >= myds[gq];
-                pv = ok ? pv : 0.f;
+                pv[r] = ok ? pv[r] : 0.f;
               }
-              float dpv = dp[gq][r];
-              if (DROP)
-                dpv = __uint_as_float(__float_as_uint(dpv) & (uint32_t)__builtin_amdgcn_sbfe((int)wt, r, 1)) *
-                      a.drop_scale;
-              ds[gq][t][r] = pv * (dpv - myd[gq]);
+              dm[r] = dp[gq][r];
+              if (DROP) {
+                int km = __builtin_amdgcn_sbfe((int)wt, r, 1);
+                asm volatile("" : "+v"(km));
+                dm[r] = __uint_as_float(__float_as_uint(dm[r]) & (uint32_t)km);
+              }
+            }
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) {
+              const f2v u = __builtin_elementwise_fma((f2v){dm[2 * h2], dm[2 * h2 + 1]}, dsc,
+                                                      (f2v){-myd[gq], -myd[gq]});
+              const f2v v2 = (f2v){pv[2 * h2], pv[2 * h2 + 1]} * u;
+              ds[gq][t][2 * h2] = v2.x;
+              ds[gq][t][2 * h2 + 1] = v2.y;
             }
           }
         };
