@@ -43,6 +43,7 @@ struct AttnArgs {
   const uint16_t* mask;                   // packed keep bits, see drop_word()
   int n64;                                // key-tile count of the mask (2*ceil(T/128))
   int delta_ready;                        // bwd: delta already computed (fused into the dO producer)
+  int xcd_map;                            // short path: place batch b's heads on the XCD of its rows
   // short (ViT) path: O's bf16 rounding residual O - bf16(O) (fwd writes it, bwd reads it; row
   // strides ldout / ldo).  The backward's softmax row constant delta = <dO, O> must be formed
   // from the O the backward's own P reproduces (fp32 P, not the bf16-rounded P of the P.V
@@ -841,6 +842,17 @@ extern "C" int pcv_debug_sh_timing(void* buf) {
 #define PCV_SHREC(slot) do {} while (0)
 #endif
 
+// (b, h) of a short-path workgroup.  Default: grid (H, B).  xcd_map: workgroup ids are dealt to the
+// 8 XCDs round-robin (id & 7), and the row-tiled GEMMs give XCD x the x-th eighth of the token rows
+// (gemm_tile's contiguous remap), so batch b's rows were written from XCD 8b / B: with xcd_map the
+// heads of batch b run on that XCD (B % 8 == 0; checked on the host).
+__device__ __forceinline__ void sh_head_of(const AttnArgs& a, int& h, int& b) {
+  if (!a.xcd_map) { h = blockIdx.x; b = blockIdx.y; return; }
+  const int w = blockIdx.x + gridDim.x * blockIdx.y, x = w & 7, j = w >> 3;
+  b = x * (a.B >> 3) + j / a.H;
+  h = j % a.H;
+}
+
 // Cooperative load of rows [0, TP) of N column blocks into swizzled LDS images: all of a thread's
 // 16-B loads are issued before the first LDS store (one HBM latency for the whole prologue).
 template <int N>
@@ -1020,7 +1032,8 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
   bf16* Vs = Ks + TP * DH;
   uint16_t* mk = reinterpret_cast<uint16_t*>(Vs + TP * DH);
   PCV_SHREC(0);
-  const int h = blockIdx.x, b = blockIdx.y;
+  int h, b;
+  sh_head_of(a, h, b);
   const int T = a.T;
   const int64_t bT = (int64_t)b * T;
   {
@@ -1220,7 +1233,8 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
   float* Dl = Ls + SH_TMAX;
   uint16_t* mk = reinterpret_cast<uint16_t*>(Dl + SH_TMAX);
   PCV_SHREC(0);
-  const int h = blockIdx.x, b = blockIdx.y;
+  int h, b;
+  sh_head_of(a, h, b);
   const int T = a.T, TP = (T + 31) & ~31, NT = TP / 16;
   const int64_t bT = (int64_t)b * T, bh = (int64_t)b * a.H + h;
   bf16* const img[4] = {Qs, Ks, Vs, Os};
@@ -1605,7 +1619,8 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd2_kernel(AttnArgs
   bf16* ring = reinterpret_cast<bf16*>(mk + SH_MASK_WORDS);               // [4][256 keys][32 queries]
   float* tailp = reinterpret_cast<float*>(ring + SH2_RING);                // [3][16][32] + corner
   PCV_SHREC(0);
-  const int h = blockIdx.x, b = blockIdx.y;
+  int h, b;
+  sh_head_of(a, h, b);
   const int T = a.T, TP = min((T + 31) & ~31, SH2_ROWS);   // image rows (padding past the MFMA rows unread)
   const int64_t bT = (int64_t)b * T, bh = (int64_t)b * a.H + h;
   const bool tail1 = (T & 15) == 1 && T > 16;
@@ -1996,10 +2011,11 @@ static void launch_bwd(const AttnArgs& a, hipStream_t s) {
 }
 
 template <bool FWD>
-static int dispatch(const AttnArgs& a, int dh, int causal, int drop, hipStream_t s) {
+static int dispatch(AttnArgs a, int dh, int causal, int drop, hipStream_t s) {
   if ((a.out_lo || a.o_lo) && !short_ok(a, dh, causal, FWD)) return PCV_EINVAL;   // short path only
   if (a.o_lo && a.delta_ready) return PCV_EINVAL;                                 // delta is formed here
   if (short_ok(a, dh, causal, FWD)) {
+    a.xcd_map = (a.B % 8 == 0 && getenv("PCV_ATTN_XCD") != nullptr) ? 1 : 0;   // A/B experiment
     const int e = FWD ? (drop ? launch_short_fwd<true>(a, s) : launch_short_fwd<false>(a, s))
                       : (drop ? launch_short_bwd<true>(a, s) : launch_short_bwd<false>(a, s));
     return e ? e : pcv_launch_status();
