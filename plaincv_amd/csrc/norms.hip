@@ -94,8 +94,13 @@ __global__ __launch_bounds__(256) void vit_embed_ln_fwd_kernel(const float* patc
                                                                int64_t ldy, float* mean_out, float* rstd_out,
                                                                float eps) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= (int64_t)B * T) return;
+  // XCD-ordered rows: workgroup ids go to the 8 XCDs round-robin (id & 7); XCD x takes the x-th
+  // eighth of the rows, as the row-tiled GEMM that reads y next does (gemm_tile's contiguous remap),
+  // so its A tiles are still in that XCD's L2
+  const int64_t nblk = ((int64_t)B * T + 3) / 4, per = (nblk + 7) / 8;
+  const int64_t lb = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  const int64_t row = lb * 4 + (threadIdx.x >> 6);
+  if (lb >= nblk || row >= (int64_t)B * T) return;
   const uint32_t seed = thresh ? *seedp : 0u;
   const int t = (int)(row % T), b = (int)(row / T);
   const int c = lane * 4;
@@ -302,7 +307,8 @@ extern "C" int pcv_vit_embed_ln_fwd(const float* patch, const float* cls, const 
   uint32_t th; float sc;
   drop_params(rate, &th, &sc);
   const int64_t R = (int64_t)B * T;
-  hipLaunchKernelGGL(vit_embed_ln_fwd_kernel, dim3((unsigned)((R + 3) / 4)), dim3(256), 0, (hipStream_t)stream, patch,
+  hipLaunchKernelGGL(vit_embed_ln_fwd_kernel, dim3((unsigned)(8 * (((R + 3) / 4 + 7) / 8))), dim3(256), 0,
+                     (hipStream_t)stream, patch,
                      cls, pos, x, B, T, D, th, sc, seed, site, ln_scale, ln_bias, (bf16*)y, ldy, mean, rstd, eps);
   return pcv_launch_status();
 }
