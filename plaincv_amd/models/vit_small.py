@@ -301,6 +301,7 @@ class ViTRunner:
         # alone is a few dozen 64x64 output tiles over K = B*T rows, a latency-bound partial
         # wave; all of them together fill the chip (csrc/gemm.hip gemm_grouped_kernel).
         self.wgrad = None
+        self.wgrad_early = None
         self.rep_ws, self.reps = {}, 1
         if grouped_wgrad and self.side is None and dev.type == "cuda":
             items = [(self.yf, self.dlogits_b, self.gWh, 1.0), (self.patches, self.dpatch, self.gWconv, 1.0)]
@@ -346,6 +347,20 @@ class ViTRunner:
                 v = K.vit_head_fold_views(self.head_work, B, D, self.Kc)
                 items += [("fold", v["metrics"], self.metrics), ("fold", v["dhead_bias"], self.gbh),
                           ("fold", v["dscale"], self.gsf), ("fold", v["dbias"], self.gcf)]
+            # PCV_WGRAD_SPLIT=1: the head's and the upper half of the blocks' weight gradients run as a
+            # grouped launch of their own on a side stream, forked once their dY exist (after block
+            # L/2's backward) and joined after the final grouped launch, beside the lower blocks'
+            # data-gradient chain
+            self.wgrad_early, self.wside = None, None
+            if os.environ.get("PCV_WGRAD_SPLIT", "0") == "1" and model.num_layers >= 2:
+                half = model.num_layers // 2
+                early_keys = {id(self.gWh)} | {id(w[k]) for i, w in enumerate(self.w) if i >= half
+                                               for k in ("gW1", "gW0", "gWo", "gWqkv")}
+                early = [it for it in items if not isinstance(it[0], str) and id(it[2]) in early_keys]
+                items = [it for it in items if isinstance(it[0], str) or id(it[2]) not in early_keys]
+                self.wgrad_early = K.GroupedWGrad(early, dev)
+                self.wside = torch.cuda.Stream(device=dev)
+                self.wsplit_at = half
             self.wgrad = K.GroupedWGrad(items, dev)
 
     # ------------------------------------------------------------ views
@@ -536,6 +551,10 @@ class ViTRunner:
                     K.colsum(dym, w["gb1"])
             self._block_backward(i, dx_in, rate, seed)
             dx_in = self.dx_out[i]
+            if self.wgrad_early is not None and i == self.wsplit_at:
+                self.wside.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self.wside):
+                    self.wgrad_early()
         K.vit_embed_bwd(dx_in, self.dpatch, self.gcls, self.gpos, None, B, T, D, rate, seed, SITE_EMBED)
         with self._fork():
             if self.wgrad is None:
@@ -544,6 +563,8 @@ class ViTRunner:
                 K.gemm(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
         if self.wgrad is not None:
             self.wgrad()
+        if self.wgrad_early is not None:
+            torch.cuda.current_stream().wait_stream(self.wside)
         if self.side is not None:
             torch.cuda.current_stream().wait_stream(self.side)
 
