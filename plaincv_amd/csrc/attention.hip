@@ -1297,7 +1297,10 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
 #pragma unroll
   for (int j = 0; j < 8; ++j) { tq[j] = 0.f; tk[j] = 0.f; tv[j] = 0.f; }
   // (Tried: every wave one key block AND one query group instead of the 8 / 8 role split, so that
-  // no role finishes early -- main phase 19.7 vs 18.6 us, C2 0.777 vs 0.771 ms.)
+  // no role finishes early -- main phase 19.7 vs 18.6 us, C2 0.777 vs 0.771 ms; with the two halves
+  // of each SIMD's waves taking the roles in opposite orders, 21.4 vs 18.8 us.  The oldest-first
+  // issue arbitration starves the youngest waves either way: the kernel is bound by the VALU issue
+  // of the whole workgroup, so only fewer VALU instructions shorten it.)
   if (wave < 8) {
     // ---- dK, dV of keys 16*kb .. +15 (lane & 15), over all queries
     for (int kb = wave; kb < NB; kb += 8) {
