@@ -34,7 +34,11 @@ extern "C" int pcv_gemm_big_wgrad(const void* A, const void* B, float* C, int64_
 
 namespace pcv {
 
-enum { EPI_NONE = 0, EPI_GELU = 1, EPI_GELU_BWD = 2 };
+// EPI_GELU: aux <- pre-activation h, out = gelu(h); EPI_GELU_BWD: out *= gelu'(aux = h).
+// EPI_GELU_D: aux <- bf16(gelu'(h)) instead (a few VALU in the forward, sharing its sigmoid), and
+// EPI_MUL_AUX: out *= aux -- the backward then skips gelu' (an exp, a rcp and ~9 more VALU per
+// element in a latency-bound epilogue) and evaluates it at the fp32 h rather than at bf16(h)
+enum { EPI_NONE = 0, EPI_GELU = 1, EPI_GELU_BWD = 2, EPI_GELU_D = 3, EPI_MUL_AUX = 4 };
 
 struct GemmArgs {
   const bf16* A; const bf16* B; void* C;
@@ -891,6 +895,27 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
           }
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+        } else if (g.act == EPI_GELU_D) {
+          bf16x8 dv;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = v[e], x2 = x * x, sg = gelu_sig(x, x2), gx = x * sg;
+            dv[e] = f2bf(fmaf(gx * (1.f - sg), fmaf(3.f * GELU_A * GELU_K, x2, GELU_K), sg));   // gelu'(x)
+            v[e] = gx;
+          }
+          if (vec) {
+            *reinterpret_cast<bf16x8*>(ap) = dv;
+          } else {
+            for (int e = 0; e < 8; ++e) if (col + e < g.N) ap[e] = dv[e];
+          }
+        } else if (g.act == EPI_MUL_AUX) {
+          if (vec) {
+            const bf16x8 d8 = *reinterpret_cast<const bf16x8*>(ap);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= bf2f(d8[e]);
+          } else {
+            for (int e = 0; e < 8; ++e) v[e] *= (col + e < g.N) ? bf2f(ap[e]) : 0.f;
+          }
         } else {
           float hv[8];
           if (vec) {
@@ -1219,6 +1244,7 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
   if ((lda & 7) || (ldb & 7) || !pcv_aligned16(A) || !pcv_aligned16(B)) return PCV_EALIGN;
   if ((stride_a & 7) || (stride_b & 7)) return PCV_EALIGN;
   if (act != EPI_NONE && !aux) return PCV_EINVAL;
+  if (act < EPI_NONE || act > EPI_MUL_AUX) return PCV_EINVAL;
   if (split_k > 1 && (!out_f32 || beta != 1.f || bias || res || act || drop_rate > 0.f)) return PCV_EINVAL;
   GemmArgs g{};
   g.A = (const bf16*)A; g.B = (const bf16*)B; g.C = C;

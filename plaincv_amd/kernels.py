@@ -13,7 +13,8 @@ from .hip import ptr, stream_ptr
 BF16 = torch.bfloat16
 F32 = torch.float32
 
-EPI_NONE, EPI_GELU, EPI_GELU_BWD = 0, 1, 2
+# EPI_GELU_D / EPI_MUL_AUX: the forward saves gelu'(h) (bf16) in aux, the backward multiplies by it
+EPI_NONE, EPI_GELU, EPI_GELU_BWD, EPI_GELU_D, EPI_MUL_AUX = 0, 1, 2, 3, 4
 
 
 def _ld(t):

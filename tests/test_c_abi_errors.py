@@ -64,6 +64,7 @@ def test_gemm_entry_point(lib):
     assert _gemm(lib, A=A2) == EALIGN
     assert _gemm(lib, lda=63) == EALIGN
     assert _gemm(lib, act=1) == EINVAL                               # GELU epilogue needs the aux buffer
+    assert _gemm(lib, act=3) == EINVAL                               # saved-derivative GELU: aux too
     assert _gemm(lib, split_k=4, beta=0.0) == EINVAL                 # split-K accumulates: beta must be 1
     assert _gemm(lib, colsum=A16, batch=2) == EINVAL
     assert _gemm(lib, drop=0.1) == EINVAL                            # dropout without a seed

@@ -636,3 +636,33 @@ def test_vit_embed_ln_fused(dev, rate):
         bad = (a != b).nonzero()
         assert bad.numel() == 0, (name, bad.shape[0], bad[:4].tolist(), (a.float() - b.float()).abs().max().item(),
                                   a.flatten()[:4].tolist(), b.flatten()[:4].tolist())
+
+
+def test_gemm_gelu_saved_derivative(dev):
+    """EPI_GELU_D (forward: out = gelu(h), aux = bf16(gelu'(h))) + EPI_MUL_AUX (backward: out *= aux)
+    against EPI_GELU / EPI_GELU_BWD on the same operands: the forward outputs are bit-identical (the
+    same sigmoid form); aux is gelu' at the fp32 pre-activation within bf16 rounding of the exact
+    torch derivative; the backward product within bf16 rounding of dY * gelu'(h)."""
+    from plaincv_amd import kernels as K_
+    M, N, Kd = 16448, 256, 128
+    g = torch.Generator(device=dev).manual_seed(4)
+    x = torch.randn(M, Kd, device=dev, generator=g).to(torch.bfloat16)
+    w = (0.2 * torch.randn(Kd, N, device=dev, generator=g)).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev, generator=g)
+    o1, o2 = (torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(2))
+    h, d = (torch.empty(M, N, device=dev, dtype=torch.bfloat16) for _ in range(2))
+    K_.gemm(x, w, o1, bias=bias, aux=h, act=K_.EPI_GELU)
+    K_.gemm(x, w, o2, bias=bias, aux=d, act=K_.EPI_GELU_D)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    pre = (x.float() @ w.float() + bias).requires_grad_(True)
+    torch.nn.functional.gelu(pre, approximate="tanh").sum().backward()
+    exact = pre.grad
+    assert ((d.float() - exact).abs() <= 2 ** -8 * exact.abs() + 1e-3).all()
+    dy = torch.randn(M, Kd, device=dev, generator=g).to(torch.bfloat16)
+    wt = (0.2 * torch.randn(N, Kd, device=dev, generator=g)).to(torch.bfloat16)
+    b1 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K_.gemm(dy, wt, b1, tb=True, aux=d, act=K_.EPI_MUL_AUX)
+    torch.cuda.synchronize()
+    ref = (dy.float() @ wt.float().t()) * d.float()
+    assert ((b1.float() - ref).abs() <= 2 ** -7 * ref.abs() + 1e-2).all()
