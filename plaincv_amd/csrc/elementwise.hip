@@ -163,7 +163,10 @@ __global__ void colsum_kernel(const T* x, int64_t ld, int64_t R, int N, float* o
 __global__ void patchify_kernel(const uint8_t* img, bf16* out, int B, int Hh, int Ww, int C, int ps, int gh, int gw) {
   const int K = ps * ps * C;
   const int64_t n = (int64_t)B * gh * gw * K;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  // XCD-ordered blocks: ids go to the 8 XCDs round-robin, and XCD x takes the x-th eighth of the
+  // patch rows -- the rows its L2 serves to the patch GEMM (gemm_tile's contiguous remap)
+  const int64_t lb = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  for (int64_t i = lb * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int k = (int)(i % K);
     const int64_t p = i / K;
     const int pw = (int)(p % gw), ph = (int)((p / gw) % gh), b = (int)(p / ((int64_t)gw * gh));
@@ -197,10 +200,18 @@ __global__ void vit_embed_bwd_kernel(const float* dx, bf16* dpatch, float* dcls,
                                      uint32_t site) {
   const uint32_t seed = thresh ? *seedp : 0u;
   const int64_t n = (int64_t)T * D;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // 8 batch groups (B = 64): group y on XCD y, whose L2 holds those rows of dx (written by the last
+  // row-tiled GEMM, XCD x = x-th eighth of the rows); otherwise the plain 2-D order
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (gridDim.y == 8) {
+    const int L = blockIdx.x + gridDim.x * blockIdx.y;
+    by = L & 7;
+    bx = L >> 3;
+  }
+  const int64_t i = (int64_t)bx * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int d = (int)(i % D), t = (int)(i / D);
-  const int b0 = blockIdx.y * 8, b1 = min(B, b0 + 8);
+  const int b0 = by * 8, b1 = min(B, b0 + 8);
   float s = 0.f;
 #pragma unroll 4
   for (int b = b0; b < b1; ++b) {
