@@ -14,6 +14,7 @@ whole step (forward, backward, optimizer) can be captured into one hipGraph
 (``GraphedTrainStep``) because every kernel runs on the current stream with
 device-resident seeds/counters.
 """
+import os
 from dataclasses import dataclass, field
 from typing import Any, Dict, Optional
 
@@ -344,6 +345,13 @@ class GraphedTrainStep:
                 # steady-state graphs: the previous step's matrix phase on a side stream beside this
                 # step's forward head, joined before the first routed-weight read
                 self.side = torch.cuda.Stream(device=dev)
+                # split apply (PCV_MUON_SPLIT_APPLY=1, opt-in): block 0's routed matrices are updated
+                # first and joined before block 0's MLP; the rest update beside block 0's MLP and block
+                # 1's head and are joined before block 1's MLP
+                self.split_first = 0
+                if os.environ.get("PCV_MUON_SPLIT_APPLY", "0") == "1" and hasattr(state.tx, "split_first"):
+                    self.split_first = state.tx.split_first(
+                        state.opt_state, [t.data_ptr() for t in self.runner.join_weights(0)])
                 self.g_steady = []
                 for images, labels in [(None, None)] + self.slots:
                     g = torch.cuda.CUDAGraph()
@@ -351,8 +359,20 @@ class GraphedTrainStep:
                         with torch.cuda.graph(g, stream=s, pool=self.g_fb.pool()):
                             self.side.wait_stream(s)
                             with torch.cuda.stream(self.side):
-                                state.tx.step_ns_phase_(store, state.opt_state)
-                            self._fb(images, join=lambda: s.wait_stream(self.side))
+                                if self.split_first:
+                                    state.tx.step_ns_phase_(store, state.opt_state, part="a")
+                                    first = torch.cuda.Event()
+                                    first.record(self.side)
+                                    state.tx.step_ns_phase_(store, state.opt_state, part="b")
+                                else:
+                                    state.tx.step_ns_phase_(store, state.opt_state)
+                            if self.split_first:
+                                join = lambda i, e=first: (s.wait_event(e) if i == 0 else  # noqa: E731
+                                                           s.wait_stream(self.side) if i == 1 else None)
+                            else:
+                                join = lambda i: s.wait_stream(self.side) if i == 0 else None  # noqa: E731
+                            self._fb(images, join=join)
+                            s.wait_stream(self.side)   # (a one-block model never joins at block 1)
                             state.tx.step_grad_phase_(store, state.opt_state)
                     self.g_steady.append(g)
                 self.g_flush = torch.cuda.CUDAGraph()

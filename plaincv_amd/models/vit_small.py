@@ -427,10 +427,15 @@ class ViTRunner:
         return self.attn_mask[i * w:(i + 1) * w]
 
     # ---------------------------------------------------------- forward
-    # forward(join=fn) calls fn() right before the first launch that reads a Muon-routed weight (the
-    # first block's MlpBlock Dense_0): everything before it -- patch embedding, LayerNorm, attention,
-    # out projection of block 0 -- only reads AdamW-branch leaves (engine.GraphedTrainStep overlap_opt)
+    # forward(join=fn) calls fn(i) right before block i's MlpBlock Dense_0 launch, the first read of
+    # block i's Muon-routed weights (join_weights(i)): everything before block 0's -- patch embedding,
+    # LayerNorm, attention, out projection of block 0 -- only reads AdamW-branch leaves
+    # (engine.GraphedTrainStep overlap_opt)
     supports_join = True
+
+    def join_weights(self, i):
+        w = self.w[i]
+        return [w["W0"], w["W1"]]
 
     def forward(self, images, labels=None, train=True, need_grad=True, join=None):
         """images: uint8 (B,H,W,C) on the GPU; labels int32 (B,).  Leaves
@@ -481,8 +486,8 @@ class ViTRunner:
                     K.layernorm_fwd(self.x1s[i], w["s1"], w["c1"], self.y1[i], *self.st1[i])
                 else:
                     K.dropout_bwd_cast(self.x1s[i], self.y1[i])
-            if i == 0 and join is not None:
-                join()
+            if join is not None:
+                join(i)
             K.gemm(self.y1[i], w["W0"], self.a[i], bias=w["b0"], aux=self.h[i],
                    act=K.EPI_GELU_D if self.gelu_d else K.EPI_GELU,
                    drop_rate=rate, seed=seed, site=site_mlp_hidden(i))

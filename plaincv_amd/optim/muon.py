@@ -207,15 +207,42 @@ class Muon(GradientTransformation):
                  ptr(store.grad_flat), ptr(st.tensors["mu"]), ptr(st.tensors["nu"]), ptr(store.shadow), self.lr, b1,
                  b2, self.eps, eps_root, awd, ptr(st.count), ptr(gscale), stream_ptr())
 
-    def step_ns_phase_(self, store, st):
+    def split_first(self, st, ptrs):
+        """Order the NS-phase records so the routed matrices whose weights (fp32 or bf16-shadow data
+        pointers in ptrs) the next forward reads first come first; returns how many (0: no split).
+        step_ns_phase_(part="a") then updates only those, part="b" the rest -- the same per-matrix
+        kernels on the same records, so the result is step_ns_phase_()'s."""
+        n = len(st.routed)
+        recs = st.mats_apply.view(n, -1).cpu().numpy().view(np.uint64)
+        want = {int(p) for p in ptrs}
+        front = [i for i in range(n) if int(recs[i, 0]) in want or int(recs[i, 3]) in want]
+        if not front or len(front) == n:
+            st.n_first = 0
+            return 0
+        order = front + [i for i in range(n) if i not in set(front)]
+        st.mats_split = st.mats_apply.view(n, -1)[order].reshape(-1).contiguous()
+        st.rec_len = st.mats_apply.numel() // n
+        st.n_first = len(front)
+        return st.n_first
+
+    def step_ns_phase_(self, store, st, part=None):
+        """part None: NS + update of every routed matrix; "a": NS of all + update of the first
+        split_first() matrices; "b": update of the rest (after "a", on the same stream)."""
         b1, b2, eps_root, awd = self.adam
-        hip.call("pcv_muon_step_fused", ptr(st.mats_apply), len(st.routed), None, 0, ptr(store.flat),
-                 ptr(store.grad_flat), ptr(st.tensors["mu"]), ptr(st.tensors["nu"]), ptr(store.shadow), None,
-                 self.lr, self.wd, self.beta, int(self.nesterov), self.eps, int(self.shape_scale), self.a, self.b,
-                 self.c, self.ns_steps, b1, b2, eps_root, awd, 1, ptr(st.count), None, ptr(st.ticket), 0,
-                 stream_ptr())
-        hip.call("pcv_muon_apply", ptr(st.mats_apply), len(st.routed), st.max_elems, self.lr, self.wd,
-                 int(self.shape_scale), 1, stream_ptr())
+        n = len(st.routed)
+        mats = st.mats_apply if part is None else st.mats_split
+        if part != "b":
+            hip.call("pcv_muon_step_fused", ptr(mats), n, None, 0, ptr(store.flat),
+                     ptr(store.grad_flat), ptr(st.tensors["mu"]), ptr(st.tensors["nu"]), ptr(store.shadow), None,
+                     self.lr, self.wd, self.beta, int(self.nesterov), self.eps, int(self.shape_scale), self.a, self.b,
+                     self.c, self.ns_steps, b1, b2, eps_root, awd, 1, ptr(st.count), None, ptr(st.ticket), 0,
+                     stream_ptr())
+        if part is None:
+            lo, hi = 0, n
+        else:
+            lo, hi = (0, st.n_first) if part == "a" else (st.n_first, n)
+        hip.call("pcv_muon_apply", ptr(mats[lo * st.rec_len:] if lo else mats), hi - lo, st.max_elems, self.lr,
+                 self.wd, int(self.shape_scale), 1, stream_ptr())
 
     def update(self, grads, state, params=None):
         ensure_grads(params, grads)
