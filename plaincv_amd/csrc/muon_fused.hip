@@ -327,6 +327,42 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
 // chunks run under the NS workgroups' latency, and the step counter is bumped by whichever block
 // finishes last (a ticket counter: every block reads the counter before taking its ticket), so
 // prep + NS + apply + AdamW + bump are one launch instead of five.
+// the routed matrix's shape-scaled, weight-decayed update applied straight from the NS result in LDS
+// (muon_apply_kernel's math): each thread owns 4 consecutive columns of a row, MF_UB rows in flight
+__device__ void muon_apply_lds(const MuonMat& M, const MuonHyper& h, const bf16* X) {
+  const bool tr = M.rows > M.cols;
+  const int rows = (int)M.rows, cols = (int)M.cols, ldp = (int)M.ld;
+  const int tpr = cols >> 2, rpp = MF_THREADS / tpr;
+  const int myr = (int)threadIdx.x / tpr, myc = ((int)threadIdx.x - myr * tpr) * 4;
+  const bool act = myr < rpp;
+  constexpr int MF_UB = 4;
+  const float sc = h.shape_scale > 0.f ? sqrtf(fmaxf(1.f, (float)M.cols / (float)M.rows)) : 1.f;
+  for (int rb = 0; rb < rows; rb += rpp * MF_UB) {
+    f32x4v pv[MF_UB];
+#pragma unroll
+    for (int u = 0; u < MF_UB; ++u) {
+      const int r = rb + u * rpp + myr;
+      if (act && r < rows) pv[u] = *reinterpret_cast<const f32x4v*>(M.p + r * ldp + myc);
+    }
+#pragma unroll
+    for (int u = 0; u < MF_UB; ++u) {
+      const int r = rb + u * rpp + myr;
+      if (!(act && r < rows)) continue;
+      f32x4v o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = bf2f(X[tr ? mf_off(myc + e, r, MF_LDX) : mf_off(r, myc + e, MF_LDX)]);
+      const f32x4v uu = -h.lr * (o * sc + h.wd * pv[u]);
+      if (M.upd) *reinterpret_cast<f32x4v*>(M.upd + r * ldp + myc) = uu;
+      if (h.apply) {
+        const f32x4v pn = pv[u] + uu;
+        *reinterpret_cast<f32x4v*>(M.p + r * ldp + myc) = pn;
+        if (M.pb) *reinterpret_cast<bf16x4*>(M.pb + r * ldp + myc) = bf16x4{f2bf(pn[0]), f2bf(pn[1]), f2bf(pn[2]), f2bf(pn[3])};
+      }
+    }
+  }
+}
+
 struct MuonStepArgs {
   const MuonMat* mats; int nmats;
   const Chunk* chunks;
@@ -335,14 +371,24 @@ struct MuonStepArgs {
   MuonHyper mh;
   float ns_a, ns_b, ns_c; int ns_steps;
   int* step; const float* gscale; int* ticket;
-  int in_block;   // 1: prep and apply inside the NS workgroup; 0: NS only (prep / apply launched around it)
+  int in_block;   // 1: prep and apply inside the NS workgroup; 0: NS only (prep / apply launched around
+                  // it); 2: NS + apply inside the workgroup (prep launched before it)
 };
 
 __global__ __launch_bounds__(MF_THREADS) void muon_step_kernel(MuonStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_m[];
   const int step = *a.step;
   const float gs = a.gscale ? *a.gscale : 1.f;
-  if ((int)blockIdx.x < a.nmats && !a.in_block) {
+  if ((int)blockIdx.x < a.nmats && a.in_block == 2) {
+    // NS from muon_prep's x32 and squared norm, then the update from the LDS image: the overlapped
+    // matrix phase (engine.GraphedTrainStep) has no wide apply launch left to wait for CUs behind the
+    // forward's kernels
+    const MuonMat M = a.mats[blockIdx.x];
+    ns_core(M, 1.f / ((float)sqrt(*M.norm2) + a.mh.eps), a.ns_a, a.ns_b, a.ns_c, a.ns_steps, smem_m);
+    // every thread read norm2 before ns_core's first barrier: reset it for the next prep (as muon_apply)
+    if (threadIdx.x == 0) *M.norm2 = 0.0;
+    muon_apply_lds(M, a.mh, reinterpret_cast<const bf16*>(smem_m));
+  } else if ((int)blockIdx.x < a.nmats && !a.in_block) {
     // NS only: x32 and its squared norm come from muon_prep_kernel, X_ns goes to xo for
     // muon_apply_kernel (both wide launches: one CU moves only ~10 B/cycle, so the per-matrix
     // streaming of prep / apply belongs on many CUs, not on the NS workgroup)
@@ -404,32 +450,7 @@ __global__ __launch_bounds__(MF_THREADS) void muon_step_kernel(MuonStepArgs a) {
     ss = block_sum(ss, red);
     __syncthreads();
     ns_core(M, 1.f / (sqrtf(ss) + h.eps), a.ns_a, a.ns_b, a.ns_c, a.ns_steps, smem_m);
-    const bf16* X = reinterpret_cast<const bf16*>(smem_m);
-    const float sc = h.shape_scale > 0.f ? sqrtf(fmaxf(1.f, (float)M.cols / (float)M.rows)) : 1.f;
-    for (int rb = 0; rb < rows; rb += rpp * MF_UB) {
-      f32x4v pv[MF_UB];
-#pragma unroll
-      for (int u = 0; u < MF_UB; ++u) {
-        const int r = rb + u * rpp + myr;
-        if (act && r < rows) pv[u] = *reinterpret_cast<const f32x4v*>(M.p + r * ldp + myc);
-      }
-#pragma unroll
-      for (int u = 0; u < MF_UB; ++u) {
-        const int r = rb + u * rpp + myr;
-        if (!(act && r < rows)) continue;
-        f32x4v o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          o[e] = bf2f(X[tr ? mf_off(myc + e, r, MF_LDX) : mf_off(r, myc + e, MF_LDX)]);
-        const f32x4v uu = -h.lr * (o * sc + h.wd * pv[u]);
-        if (M.upd) *reinterpret_cast<f32x4v*>(M.upd + r * ldp + myc) = uu;
-        if (h.apply) {
-          const f32x4v pn = pv[u] + uu;
-          *reinterpret_cast<f32x4v*>(M.p + r * ldp + myc) = pn;
-          if (M.pb) *reinterpret_cast<bf16x4*>(M.pb + r * ldp + myc) = bf16x4{f2bf(pn[0]), f2bf(pn[1]), f2bf(pn[2]), f2bf(pn[3])};
-        }
-      }
-    }
+    muon_apply_lds(M, h, reinterpret_cast<const bf16*>(smem_m));
   } else {
     adamw_chunk(a.p, a.g, a.m, a.v, a.pb, a.upd, a.chunks[blockIdx.x - a.nmats], a.ah, step, gs);
   }
@@ -461,6 +482,7 @@ extern "C" int pcv_muon_step_fused(const void* mats, int nmats, const void* chun
                                    float adam_wd, int apply, int* step, const float* gscale, int* ticket,
                                    int in_block, void* stream) {
   if (nmats <= 0 || nchunks < 0 || (nchunks > 0 && !chunks) || ns_steps < 0 || ns_b == 0.f || !step || !ticket ||
+      in_block < 0 || in_block > 2 ||
       !p || !g || !mu || !nu || (!apply && !upd))
     return PCV_EINVAL;
   MuonStepArgs a{};

@@ -75,6 +75,9 @@ class Muon(GradientTransformation):
         # all-fused models run the whole step as one launch (PCV_MUON_ONE_LAUNCH=0: the 5-launch form)
         self.one_launch = os.environ.get("PCV_MUON_ONE_LAUNCH", "1") != "0"
         self.in_block = os.environ.get("PCV_MUON_IN_BLOCK", "0") == "1"
+        # PCV_MUON_OVERLAP_IN_BLOCK=1: the overlapped matrix phase applies each update from the NS
+        # workgroup's LDS instead of a wide muon_apply launch -- exact, but slower
+        self.overlap_in_block = os.environ.get("PCV_MUON_OVERLAP_IN_BLOCK", "0") == "1"
         self.shard = shard           # optim/sharding.py: NS work split across DP ranks
 
     def init(self, store):
@@ -231,12 +234,15 @@ class Muon(GradientTransformation):
         b1, b2, eps_root, awd = self.adam
         n = len(st.routed)
         mats = st.mats_apply if part is None else st.mats_split
+        in_block = part is None and self.overlap_in_block and st.vec4
         if part != "b":
             hip.call("pcv_muon_step_fused", ptr(mats), n, None, 0, ptr(store.flat),
                      ptr(store.grad_flat), ptr(st.tensors["mu"]), ptr(st.tensors["nu"]), ptr(store.shadow), None,
                      self.lr, self.wd, self.beta, int(self.nesterov), self.eps, int(self.shape_scale), self.a, self.b,
-                     self.c, self.ns_steps, b1, b2, eps_root, awd, 1, ptr(st.count), None, ptr(st.ticket), 0,
-                     stream_ptr())
+                     self.c, self.ns_steps, b1, b2, eps_root, awd, 1, ptr(st.count), None, ptr(st.ticket),
+                     2 if in_block else 0, stream_ptr())
+        if in_block:
+            return
         if part is None:
             lo, hi = 0, n
         else:

@@ -189,12 +189,13 @@ def test_graphed_step_input_slots(dev, dtype, optim):
     assert rel(sa.params.flat, sb.params.flat) < (1e-2 if optim == "soap" else 1e-5)
 
 
-@pytest.mark.parametrize("ring,split", [(False, True), (True, True), (False, False)])
-def test_graphed_step_optimizer_overlap(dev, ring, split, monkeypatch):
+@pytest.mark.parametrize("ring,mode", [(False, "split"), (True, "split"), (False, "plain"), (True, "in_block")])
+def test_graphed_step_optimizer_overlap(dev, ring, mode, monkeypatch):
     """GraphedTrainStep(overlap_opt=True): Muon's Newton-Schulz phase of step t runs on a side stream
     beside step t+1's forward head (joined before the first routed-weight read), the last step's in
     flush().  split: block 0's routed matrices updated (and joined) first, the rest joined before
-    block 1's MLP (PCV_MUON_SPLIT_APPLY).  Against the in-step optimizer on the same batches: the same loss every step and the
+    block 1's MLP (PCV_MUON_SPLIT_APPLY); in_block: the updates applied inside the NS workgroups
+    (PCV_MUON_OVERLAP_IN_BLOCK).  Against the in-step optimizer on the same batches: the same loss every step and the
     same params, optimizer moments and step counter after flush() -- the same kernels on the same
     data, only reordered against independent work, so the only difference left is the run-to-run
     noise of the fp32 column-sum atomics (as test_graphed_step_input_slots: rel 1e-5); a missing or
@@ -214,11 +215,13 @@ def test_graphed_step_optimizer_overlap(dev, ring, split, monkeypatch):
     sa = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=init)
     sb = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=init)
     inputs = (xs, ys) if ring else None
-    monkeypatch.setenv("PCV_MUON_SPLIT_APPLY", "1" if split else "0")
+    monkeypatch.setenv("PCV_MUON_SPLIT_APPLY", "1" if mode == "split" else "0")
+    sa.tx.overlap_in_block = mode == "in_block"
     ga = GraphedTrainStep(sa, shape, warmup=2, inputs=inputs, overlap_opt=True)
     gb = GraphedTrainStep(sb, shape, warmup=2, inputs=inputs)
     assert ga.overlap and not gb.overlap
-    assert ga.split_first == (2 if split else 0)
+    assert ga.split_first == (2 if mode == "split" else 0)
+    assert sa.opt_state.vec4 or mode != "in_block"
     gb.runner.seed.copy_(ga.runner.seed)
     init_flat = sa.params.flat.clone()
     for it in range(6):
