@@ -366,6 +366,8 @@ class GraphedTrainStep:
                                     state.tx.step_ns_phase_(store, state.opt_state, part="b")
                                 else:
                                     state.tx.step_ns_phase_(store, state.opt_state)
+                            if os.environ.get("PCV_OVERLAP_SERIAL") == "1":   # diagnostic: no concurrency
+                                s.wait_stream(self.side)
                             if self.split_first:
                                 join = lambda i, e=first: (s.wait_event(e) if i == 0 else  # noqa: E731
                                                            s.wait_stream(self.side) if i == 1 else None)

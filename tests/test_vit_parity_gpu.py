@@ -198,7 +198,8 @@ _OPEN16 = pytest.mark.xfail(reason="aligned-head overlap vs in-step discrepancy 
 @pytest.mark.parametrize("ring,mode", [(False, "split"), (True, "split"), (False, "plain"),
                                        pytest.param(True, "plain16", marks=_OPEN16),
                                        pytest.param(False, "plain16_5l", marks=_OPEN16),
-                                       pytest.param(True, "in_block", marks=_OPEN16)])
+                                       pytest.param(True, "in_block", marks=_OPEN16),
+                                       pytest.param(False, "serial16", marks=_OPEN16)])
 def test_graphed_step_optimizer_overlap(dev, ring, mode, monkeypatch):
     """GraphedTrainStep(overlap_opt=True): Muon's Newton-Schulz phase of step t runs on a side stream
     beside step t+1's forward head (joined before the first routed-weight read), the last step's in
@@ -214,7 +215,7 @@ def test_graphed_step_optimizer_overlap(dev, ring, mode, monkeypatch):
     from plaincv_amd.models.vit_small import VisionTransformer
     from utils import Config
     # in_block needs every routed matrix's columns in 16-B groups: a 16-class head (10: the plain path)
-    m = VisionTransformer(num_classes=16 if mode in ("in_block", "plain16", "plain16_5l") else 10, patch_size=4, hidden_size=64, mlp_dim=128,
+    m = VisionTransformer(num_classes=16 if mode in ("in_block", "plain16", "plain16_5l", "serial16") else 10, patch_size=4, hidden_size=64, mlp_dim=128,
                           num_layers=2, num_heads=2, dropout_rate=0.1)
     shape = (8, 16, 16, 3)
     cfg = Config(optim="muon", lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9)
@@ -229,11 +230,12 @@ def test_graphed_step_optimizer_overlap(dev, ring, mode, monkeypatch):
     sa.tx.overlap_in_block = mode == "in_block"
     if mode == "plain16_5l":
         sb.tx.one_launch = False
+    monkeypatch.setenv("PCV_OVERLAP_SERIAL", "1" if mode == "serial16" else "0")
     ga = GraphedTrainStep(sa, shape, warmup=2, inputs=inputs, overlap_opt=True)
     gb = GraphedTrainStep(sb, shape, warmup=2, inputs=inputs)
     assert ga.overlap and not gb.overlap
     assert ga.split_first == (2 if mode == "split" else 0)
-    assert sa.opt_state.vec4 == (mode in ("in_block", "plain16", "plain16_5l"))
+    assert sa.opt_state.vec4 == (mode in ("in_block", "plain16", "plain16_5l", "serial16"))
     gb.runner.seed.copy_(ga.runner.seed)
     init_flat = sa.params.flat.clone()
     for it in range(6):
