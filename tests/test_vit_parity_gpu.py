@@ -189,15 +189,8 @@ def test_graphed_step_input_slots(dev, dtype, optim):
     assert rel(sa.params.flat, sb.params.flat) < (1e-2 if optim == "soap" else 1e-5)
 
 
-# the aligned-model cases' bounds are new: non-strict until a GPU pass confirms them
-_NEW = pytest.mark.xfail(reason="key-bias-excluding bounds not yet confirmed on the GPU", strict=False)
-
-
-@pytest.mark.parametrize("ring,mode", [(False, "split"), (True, "split"), (False, "plain"),
-                                       pytest.param(True, "plain16", marks=_NEW),
-                                       pytest.param(False, "plain16_5l", marks=_NEW),
-                                       pytest.param(True, "in_block", marks=_NEW),
-                                       pytest.param(False, "serial16", marks=_NEW)])
+@pytest.mark.parametrize("ring,mode", [(False, "split"), (True, "split"), (False, "plain"), (True, "plain16"),
+                                       (False, "plain16_5l"), (True, "in_block"), (False, "serial16")])
 def test_graphed_step_optimizer_overlap(dev, ring, mode, monkeypatch):
     """GraphedTrainStep(overlap_opt=True): Muon's Newton-Schulz phase of step t runs on a side stream
     beside step t+1's forward head (joined before the first routed-weight read), the last step's in
@@ -212,9 +205,11 @@ def test_graphed_step_optimizer_overlap(dev, ring, mode, monkeypatch):
     -- whose gradient is analytically zero (softmax is invariant to a per-query shift) -- turns such
     ulps into lr-sized Adam steps of arbitrary sign (m / sqrt(v) of rounding residue), after which
     the loss may move by ~1e-4 relative (tools/overlap_diag16b.py: key-bias gradients 0.5 apart at
-    the fourth step, every other leaf ~1e-8).  So: the loss at 1e-5 for the first three steps and
-    1e-3 after, params / moments at 1e-3 of the movement without the key biases, the step counter
-    exact; a missing or doubled optimizer phase moves the params by a whole update (~1e-2)."""
+    the fourth step, every other leaf ~1e-8) and the rest of the model follows slowly.  The 10-class
+    model's ulps do not reach the key biases: loss 1e-5 every step, params / moments 1e-4.  The
+    aligned model: loss 1e-5 for the first three steps and 1e-3 after, params 5e-3 of the movement
+    (1.4e-3 measured after six steps) and moments 1e-2, key biases left out.  A missing or doubled
+    optimizer phase moves the params by a whole update: ~1/6 of six steps' movement."""
     from tests.parity_util import rel
     from plaincv_amd.engine import GraphedTrainStep, create_train_state
     from plaincv_amd.models.vit_small import VisionTransformer
@@ -245,6 +240,7 @@ def test_graphed_step_optimizer_overlap(dev, ring, mode, monkeypatch):
     gb.runner.seed.copy_(ga.runner.seed)
     init = {k: v.clone() for k, v in sa.params.to_dict().items()}
     keep = [k for k in init if not k.endswith("key/bias")]
+    ptol = 5e-3 if aligned else 1e-4
 
     def without_key_bias(store, buf=None):
         d = store.to_dict() if buf is None else {k: store._view(buf, lf) for k, lf in store.layout.leaves.items()}
@@ -255,21 +251,21 @@ def test_graphed_step_optimizer_overlap(dev, ring, mode, monkeypatch):
         ma = ga(xs[k], ys[k]).clone()
         mb = gb(xs[k], ys[k]).clone()
         torch.cuda.synchronize()
-        tol = 1e-5 if it < 3 else 1e-3
+        tol = 1e-3 if aligned and it >= 3 else 1e-5
         assert abs(ma[0].item() - mb[0].item()) <= tol * abs(mb[0].item()), (it, ma, mb)
         if it == 3:   # a flush mid-run, then the first (non-steady) graph again
             ga.flush()
             torch.cuda.synchronize()
-            assert rel(without_key_bias(sa.params), without_key_bias(sb.params)) < 1e-3
+            assert rel(without_key_bias(sa.params), without_key_bias(sb.params)) < ptol
     ga.flush()
     torch.cuda.synchronize()
     moved = rel(without_key_bias(sa.params), without_key_bias(sb.params))
     print(f"OVERLAP ring={ring} mode={mode} params movement rel {moved:.3e}")
-    assert moved < 1e-3
+    assert moved < ptol
     for name in ("mu", "nu"):
         ta = without_key_bias(sa.params, sa.opt_state.tensors[name])
         tb = without_key_bias(sb.params, sb.opt_state.tensors[name])
-        assert rel(ta, tb) < 1e-3, name
+        assert rel(ta, tb) < (1e-2 if aligned else 1e-4), name
     assert torch.equal(sa.opt_state.count, sb.opt_state.count)
 
 
