@@ -421,7 +421,9 @@ int pcv_muon_fused_ok(int64_t rows, int64_t cols);
  * bumps *step (ticket: a zeroed device int the call leaves zeroed).  apply = 0: updates to the
  * records' upd and to the flat upd (functional update()).  in_block = 0: the matrix workgroups run
  * NS only (x32 / norm2 from pcv_muon_prep before, xo for pcv_muon_apply after: the streaming
- * parts stay wide), the Adam branch and the bump still ride in this launch. */
+ * parts stay wide), the Adam branch and the bump still ride in this launch.  in_block = 2: NS from
+ * pcv_muon_prep's x32 / norm2 (norm2 reset here), then the update applied from the workgroup's LDS
+ * (no pcv_muon_apply after it).  Any other in_block: PCV_EINVAL. */
 int pcv_muon_step_fused(const void* mats, int nmats, const void* chunks, int nchunks, float* p, const float* g,
                         float* mu, float* nu, void* p_bf16, float* upd, float lr, float wd, float beta, int nesterov,
                         float eps, int shape_scale, float ns_a, float ns_b, float ns_c, int ns_steps, float adam_b1,
