@@ -1,27 +1,32 @@
 """Benchmark: plainCV training hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload vit_c2|vit_c4_soap|vit_c4_shampoo|lm124m|lm420m]
-                    [--no-cpu-baseline] [--no-lm] [--shard-opt]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+                    [--workload vit_c2_f32|vit_c2|vit_c4_soap|vit_c4_shampoo|lm124m|lm420m]
+                    [--no-cpu-baseline] [--no-sub] [--no-lm] [--shard-opt]
 
 ``--gpus N`` (N > 1) without a torchrun environment: the parent process spawns N ranks of this
 script (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1/MASTER_PORT, one GPU each) BEFORE
 anything touches the GPU, relays rank 0's JSON line and exits with the worst rank's status.
 Under torchrun (WORLD_SIZE set) it runs as the given rank, and --gpus must equal WORLD_SIZE.
 
-Default workload (N=1): BASELINE.json configs[1] -- ViT-small on Tiny-ImageNet-
-shaped synthetic data (uint8 64x64x3, 200 classes, per-GPU batch 64, dropout 0.1,
-LayerNorm), Muon optimizer, bf16 MFMA compute with fp32 master params.  One
-"step" = one full optimizer step (forward + backward + Muon/AdamW update) on
-one batch per GPU, replayed from a hipGraph; inputs are resident in HBM.
-With N>1 each rank runs the same per-GPU batch (weak scaling) and gradients
-are averaged over RCCL once per step.  ``value`` = images/s over all ranks.
-The line also carries ``lm124m``: BASELINE configs[2] at its exact shape (124M LM, AdamW,
-seq 1024, micro-batch 16, grad accumulation 8, DDP over the same ranks) with its own
-roofline and CPU baseline (``--no-lm`` skips it).
+Default workload (N=1): BASELINE.json configs[1] -- ViT-small on Tiny-ImageNet-shaped synthetic
+data (uint8 64x64x3, 200 classes, per-GPU batch 64, dropout 0.1, LayerNorm), Muon optimizer -- in
+the reference ViT's own precision: every contraction on the exact-fp32 MFMA (models/vit_small.py:95
+computes in fp32; the reference has no dtype knob).  One "step" = one full optimizer step (forward
++ backward + Muon/AdamW update) on one batch per GPU, replayed from a hipGraph; inputs are resident
+in HBM.  With N>1 each rank runs the same per-GPU batch (weak scaling) and gradients are averaged
+over RCCL once per step.  ``value`` = images/s over all ranks.
 
-Also reported: the roofline of the dominant kernel (timed live with HIP
-events on its own stream, algorithmic bytes or FLOPs per launch) and the CPU
-baseline (the oracle/ restatement timed on this host's cores on a bounded sample).
+Sub-lines of the default run (``--no-sub`` skips them, ``--no-lm`` only the LM ones), each with its
+own roofline and (N=1) CPU baseline: ``vit_c2_bf16`` (the same workload with bf16 MFMA operands,
+configs[1]'s wording), ``vit_c4_soap`` / ``vit_c4_shampoo`` (configs[3]'s optimizers, fp32),
+``lm124m`` (configs[2]: 124M LM, AdamW, seq 1024, micro-batch 16, accumulation 8) and ``lm420m``
+(configs[4]: tr_420M_x8gpu.yaml shape, Muon, seq 2048, micro-batch 8, accumulation 4, clip 1.0); the
+LM lines are DDP runs over the same ranks.
+
+Also reported: the roofline of the dominant kernel (the kernel family with the largest measured
+share of the step, timed live with HIP events on its own stream; algorithmic bytes or FLOPs per
+launch) and the CPU baseline (the oracle/ restatement timed on this host's cores on a bounded sample).
 """
 import argparse
 import json
@@ -63,11 +68,29 @@ VIT_C4 = {"soap": dict(VIT_C2, optim="soap", eps=1e-8, precondition_frequency=10
 # configs[1] in the reference ViT's own precision (models/vit_small.py:95 computes in fp32): the same
 # workload on the exact-fp32 runner, reported beside the bf16 headline (a sub-line of the default run)
 VIT_C2_F32 = dict(VIT_C2, vit_dtype="float32")
-WORKLOAD_NAMES = {"vit_c2": "vit_small_tinyimagenet_muon (BASELINE configs[1])",
-                  "vit_c2_f32": "vit_small_tinyimagenet_muon_fp32 (BASELINE configs[1] workload, reference fp32 "
+WORKLOAD_NAMES = {"vit_c2": "vit_small_tinyimagenet_muon_bf16 (BASELINE configs[1] workload, bf16 MFMA operands, "
+                            "fp32 master params)",
+                  "vit_c2_f32": "vit_small_tinyimagenet_muon (BASELINE configs[1], in the reference ViT's fp32 "
                                 "precision)",
                   "vit_c4_soap": "vit_small_tinyimagenet_soap (BASELINE configs[3] optimizer)",
                   "vit_c4_shampoo": "vit_small_tinyimagenet_shampoo (BASELINE configs[3] optimizer)"}
+
+
+# bounded CPU-baseline samples per workload (ViT ~0.6 s, LM 124M ~2.7 s, LM 420M ~22 s per oracle step on
+# the box's 16 threads), so the default run (headline + 5 sub-lines) stays well under three minutes;
+# --cpu-seconds overrides `seconds`
+CPU_SAMPLE = {"vit_c2_f32": dict(seconds=6.0, min_steps=5), "vit_c2": dict(seconds=6.0, min_steps=5),
+              "vit_c4_soap": dict(seconds=3.0, min_steps=3), "vit_c4_shampoo": dict(seconds=3.0, min_steps=3),
+              "lm124m": dict(seconds=5.0, min_steps=2, warmup=1),
+              # one un-warmed step: at ~22 s per step the first call's allocations are < 1 % of it
+              "lm420m": dict(seconds=0.0, min_steps=1, warmup=0)}
+
+
+def cpu_sample(args):
+    kw = dict(CPU_SAMPLE[args.workload])
+    if args.cpu_seconds is not None:
+        kw["seconds"] = args.cpu_seconds
+    return kw
 
 
 def vit_model(cfg):
@@ -180,27 +203,52 @@ def vit_roofline(state, image_shape):
 
 
 def vit_roofline_f32(state, image_shape, rate):
-    """fp32 ViT path: the dominant kernel of the step is the fused fp32 attention backward, one
-    launch per layer (attn_bwd_f32_kshare_kernel, the score-sharing form, for T <= 257 -- the ViT's
-    257 -- else attn_bwd_f32_kernel): its algorithmic FLOPs are the five T x T x Dh products of a
-    (batch, head) -- S, dPd = dO V^T, dV, dK, dQ -- 5 * 2 * T^2 * Dh per (batch, head), timed live on
-    layer 0 against the fp32 MFMA peak (157.3 TF/s)."""
+    """fp32 ViT path.  Two kernel families carry most of the step; both are timed live (HIP events on
+    their own stream, layer 1's launches) and the one with the larger share of the step is reported
+    as ``roofline`` (the other as ``roofline_other``):
+    * the fused fp32 attention backward (attn_bwd_f32_kshare_kernel for T <= 257 -- the ViT's 257 --
+      else attn_bwd_f32_kernel), one launch per layer.  Algorithmic FLOPs = SURVEY §8(d)'s 3 x fwd
+      accounting: the backward of the two T x T x Dh forward products is 4 products (dPd = dO V^T,
+      dV, dK, dQ), 4 * 2 * T^2 * Dh per (batch, head) -- the recomputed S (issued, not algorithmic)
+      is reported as ``issued_flops_per_launch``;
+    * the fp32 token-row GEMMs with the fused Dense epilogue (gemm_f32_rows_kernel): the forward's
+      qkv / out / fc1 / fc2 products, 2 M N K each per launch.
+    Both are MFMA-bound against the 157.3 TF/s fp32 MFMA peak."""
     r = state.runner_for(image_shape)
     if not getattr(r, "fused_attn", False):
         return None
-    t = timed_kernel(lambda: r.attn_bwd(0, rate))
-    flops = 5 * 2 * r.B * r.H * r.T * r.T * r.Dh
-    ach = flops / t / 1e12
-    nq = (r.T + 15) // 16 - (1 if (r.T % 16 == 1 and r.T > 16) else 0)
+    B, H, T, Dh = r.B, r.H, r.T, r.Dh
+    t = timed_kernel(lambda: r.attn_bwd(1, rate))
+    flops = 4 * 2 * B * H * T * T * Dh
+    nq = (T + 15) // 16 - (1 if (T % 16 == 1 and T > 16) else 0)
     name = "attn_bwd_f32_kshare_kernel" if nq <= 16 else "attn_bwd_f32_kernel"
     traffic, tsrc = pmc_traffic(f"{name}<true>" if rate > 0 else f"{name}<false>")
-    return {"kernel": f"{name}<dropout> (fused fp32 attention backward of one layer)", "bound": "mfma",
-            "achieved": round(ach, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+    attn = {"kernel": f"{name}<dropout> (fused fp32 attention backward of one layer; B={B} H={H} T={T} Dh={Dh})",
+            "bound": "mfma", "achieved": round(flops / t / 1e12, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(flops / t / 1e12 / F32_PEAK_TFLOPS, 4), "traffic": traffic,
+            "traffic_unit": "bytes per launch", "traffic_source": tsrc, "launch_us": round(t * 1e6, 2),
+            "flops_per_launch": flops, "issued_flops_per_launch": 5 * 2 * B * H * T * T * Dh,
+            "launches_per_step": r.m.num_layers, "step_share_us": round(r.m.num_layers * t * 1e6, 1)}
+    dense = [r.gf[1][k] for k in ("qkv", "out", "fc1", "fc2")]
+    ts = [timed_kernel(lambda d=d: d.run(rate, r.seed)) for d in dense]
+    fl = [2 * d.M * d.N * d.K for d in dense]
+    ach = sum(fl) / sum(ts) / 1e12
+    traffic, tsrc = pmc_traffic("gemm_f32_rows_kernel<false, true, 64, 32>")
+    rows = {"kernel": "gemm_f32_rows_kernel<false,true,*> (fp32 token-row GEMM + fused Dense epilogue: the "
+                      "forward qkv / out / fc1 / fc2 products of one layer, "
+                      + ", ".join(f"M={d.M} N={d.N} K={d.K}" for d in dense) + ")",
+            "bound": "mfma", "achieved": round(ach, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / F32_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
-            "traffic_source": tsrc, "launch_us": round(t * 1e6, 2), "flops_per_launch": flops}
+            "traffic_source": tsrc, "launch_us": round(sum(ts) / len(ts) * 1e6, 2),
+            "launch_us_by_shape": [round(x * 1e6, 2) for x in ts], "flops_per_launch": fl,
+            "launches_per_step": 4 * r.m.num_layers, "step_share_us": round(r.m.num_layers * sum(ts) * 1e6, 1)}
+    dom, other = (rows, attn) if rows["step_share_us"] >= attn["step_share_us"] else (attn, rows)
+    dom = dict(dom)
+    dom["roofline_other"] = other
+    return dom
 
 
-def cpu_baseline_vit(cfg, seconds=12.0):
+def cpu_baseline_vit(cfg, seconds=6.0, min_steps=5):
     """oracle/ (PyTorch CPU fp32 restatement) timed on this host: the same
     workload (B=64 TI-shaped, Muon), bounded to ~`seconds` of CPU work."""
     from oracle import optim as oopt
@@ -227,11 +275,11 @@ def cpu_baseline_vit(cfg, seconds=12.0):
         upd, st = tx.update(grads, st, params)
         params = apply_updates(params, upd)
 
-    n, dt = timed_loop(step, seconds=seconds)
+    n, dt = timed_loop(step, seconds=seconds, min_steps=min_steps)
     return {"value": round(cfg.batch_size / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
             "steps_per_sec": round(1.0 / dt, 4),
             "sample": f"{n} timed oracle ViT-small {cfg.optim} train steps (fp32, B={cfg.batch_size}, 64x64x3, "
-                      f"200 classes) after 2 warm-up steps, {threads} threads (affinity set "
+                      f"200 classes, dropout {cfg.vit_dropout}) after 2 warm-up steps, {threads} threads (affinity set "
                       f"{len(os.sched_getaffinity(0))}, cgroup-capped); CPU {cpu_model()}"}
 
 
@@ -336,12 +384,13 @@ def bench_vit(args):
                           "optimizer_overlap": bool(step.overlap)},
                "steps_per_sec": round(sps, 3), "tflops_per_gpu": round(flops * sps / 1e12, 3),
                "final_loss": round(loss, 4)}
-        out["roofline"] = (vit_roofline_f32(state, shape, cfg.vit_dropout) if cfg.vit_dtype == "float32"
+        out["roofline"] = (None if args.no_roofline else
+                           vit_roofline_f32(state, shape, cfg.vit_dropout) if cfg.vit_dtype == "float32"
                            else vit_roofline(state, shape))
         if world > 1:
             out["grad_allreduce"] = None   # filled below (collective: every rank takes part)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline_vit(cfg, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline_vit(cfg, **cpu_sample(args))
         else:
             out["cpu_baseline"] = None
     ar = allreduce_busbw(state.params.grad_flat[: state.params.layout.size]) if world > 1 else None
@@ -352,7 +401,7 @@ def bench_vit(args):
     return out
 
 
-def cpu_baseline_lm(cfg, variables, clip, seconds=12.0):
+def cpu_baseline_lm(cfg, variables, clip, seconds=6.0, min_steps=2, warmup=1):
     """oracle/ (PyTorch CPU fp32 restatement) timed on this host: the same LM and optimizer at
     micro-batch 1 x seq_len tokens, bounded to ~`seconds` of CPU work."""
     from oracle import optim as oopt
@@ -376,10 +425,10 @@ def cpu_baseline_lm(cfg, variables, clip, seconds=12.0):
         upd, st = tx.update(grads, st, params)
         params = apply_updates(params, upd)
 
-    n, dt = timed_loop(step, seconds=seconds, max_steps=20)
+    n, dt = timed_loop(step, seconds=seconds, min_steps=min_steps, max_steps=20, warmup=warmup)
     return {"value": round(cfg.seq_len / dt, 2), "unit": "tokens/s", "cores": threads, "kind": "port",
             "steps_per_sec": round(1.0 / dt, 4),
-            "sample": f"{n} timed oracle {cfg.optim} train steps of 1 x {cfg.seq_len} tokens (fp32) after 2 warm-up "
+            "sample": f"{n} timed oracle {cfg.optim} train steps of 1 x {cfg.seq_len} tokens (fp32) after {warmup} warm-up "
                       f"steps, {threads} threads (affinity set {len(os.sched_getaffinity(0))}, cgroup-capped); "
                       f"CPU {cpu_model()}"}
 
@@ -461,9 +510,9 @@ def bench_lm(args):
                        "parallelism": f"dp{world}"},
             "steps_per_sec": round(args.steps / dt, 4),
             "tflops_per_gpu": round(tokens / world / dt * fpt / 1e12, 2),
-            "roofline": lm_roofline(st),
+            "roofline": None if args.no_roofline else lm_roofline(st),
             "grad_allreduce": ar, "optimizer_step_per_rank": om,
-            "cpu_baseline": (cpu_baseline_lm(cfg, variables, spec["clip"], args.cpu_seconds)
+            "cpu_baseline": (cpu_baseline_lm(cfg, variables, spec["clip"], **cpu_sample(args))
                              if world == 1 and not args.no_cpu_baseline else None)}
 
 
@@ -555,21 +604,25 @@ def launch_ranks(n, argv):
     return 0 if failed is None else (failed if failed > 0 else 1)
 
 
+SUB_LINES = [("vit_c2_bf16", "vit_c2"), ("vit_c4_soap", "vit_c4_soap"), ("vit_c4_shampoo", "vit_c4_shampoo"),
+             ("lm124m", "lm124m"), ("lm420m", "lm420m")]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="vit_c2",
-                    choices=["vit_c2", "vit_c2_f32", "vit_c4_soap", "vit_c4_shampoo", "lm124m", "lm420m",
-                             "dp_stub"])
+    ap.add_argument("--workload", default="vit_c2_f32",
+                    choices=["vit_c2_f32", "vit_c2", "vit_c4_soap", "vit_c4_shampoo", "lm124m", "lm420m", "dp_stub"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-roofline", action="store_true",
+                    help="skip the live roofline launches (profiling runs: keeps timing launches out of the trace)")
+    ap.add_argument("--cpu-seconds", type=float, default=None, help="override the CPU-baseline time budget")
     ap.add_argument("--lm-micro-batch", type=int, default=None, help="default: the workload's config")
     ap.add_argument("--lm-accum", type=int, default=None, help="default: the workload's config")
-    ap.add_argument("--no-lm", action="store_true", help="skip the attached 124M LM (configs[2]) line")
-    ap.add_argument("--no-f32", action="store_true",
-                    help="skip the attached vit_c2_f32 line (configs[1] in the reference's fp32 precision)")
+    ap.add_argument("--no-sub", action="store_true", help="only the selected workload's line (no sub-lines)")
+    ap.add_argument("--no-lm", action="store_true", help="skip the LM sub-lines (configs[2] / configs[4])")
     ap.add_argument("--lm-steps", type=int, default=10)
     ap.add_argument("--lm-warmup", type=int, default=2)
     ap.add_argument("--shard-opt", action="store_true",
@@ -586,20 +639,25 @@ def main():
         out = bench_lm(args)
     else:
         out = bench_vit(args)
-        if args.workload == "vit_c2" and not args.no_f32:
-            a2 = argparse.Namespace(**vars(args))
-            a2.workload, a2.no_cpu_baseline = "vit_c2_f32", True
-            f32 = bench_vit(a2)
-            if out is not None:
-                f32["cpu_baseline"] = dict(out["cpu_baseline"], shared_with="headline vit_c2 line (the same fp32 "
-                                           "oracle workload)") if out.get("cpu_baseline") else None
-                out["vit_c2_f32"] = f32
-        if not args.no_lm:   # every rank: the LM line is a DDP run over the same ranks
-            a2 = argparse.Namespace(**vars(args))
-            a2.steps, a2.warmup, a2.workload = args.lm_steps, args.lm_warmup, "lm124m"
-            lm = bench_lm(a2)
-            if out is not None:
-                out["lm124m"] = lm
+        if args.workload == "vit_c2_f32" and not args.no_sub:
+            # every rank runs every sub-line (the DDP ones are collective)
+            for key, wl in SUB_LINES:
+                if args.no_lm and wl.startswith("lm"):
+                    continue
+                a2 = argparse.Namespace(**vars(args))
+                a2.workload = wl
+                if wl.startswith("lm"):
+                    a2.steps, a2.warmup, a2.lm_micro_batch, a2.lm_accum = args.lm_steps, args.lm_warmup, None, None
+                    sub = bench_lm(a2)
+                else:
+                    a2.no_cpu_baseline = args.no_cpu_baseline or wl == "vit_c2"   # bf16: the same oracle workload
+                    sub = bench_vit(a2)
+                if out is None:
+                    continue
+                if wl == "vit_c2" and out.get("cpu_baseline"):
+                    sub["cpu_baseline"] = dict(out["cpu_baseline"], shared_with="the headline line (the same fp32 "
+                                                                                 "oracle workload)")
+                out[key] = sub
     if out is not None:
         print(json.dumps(out), flush=True)
     if dp.is_initialized():

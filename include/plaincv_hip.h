@@ -219,7 +219,10 @@ int pcv_seed_next(uint32_t* seed, void* stream);
  * gradients and per-step dropout rng). */
 int pcv_zero_seed(float* x, int64_t n, uint32_t* seed, void* stream);
 /* out[c] += sum_r x[r,c]  (Dense bias gradients). */
-int pcv_colsum(const void* x, int64_t ld, int64_t R, int N, int x_f32, float* out, void* stream);
+/* out[c] += sum_r x[r][c]; ws (optional, pcv_colsum_ws_floats(R, N) floats): the row groups' partials
+ * are stored there and added in order by a second launch (deterministic); ws null: fp32 atomics. */
+int64_t pcv_colsum_ws_floats(int64_t R, int N);
+int pcv_colsum(const void* x, int64_t ld, int64_t R, int N, int x_f32, float* out, float* ws, void* stream);
 /* ViT patch embedding input (models/vit_small.py:78-88, (kh,kw,c) flatten, /255) and token
  * assembly cls|patches + pos_embedding + dropout (models/vit_small.py:95-109). */
 int pcv_vit_patchify(const uint8_t* img, void* out, int B, int H, int W, int C, int patch, void* stream);
@@ -231,8 +234,10 @@ int pcv_vit_embed_fwd(const float* patch, const float* cls, const float* pos, fl
 int pcv_vit_embed_ln_fwd(const float* patch, const float* cls, const float* pos, float* x, int B, int T, int D,
                          float rate, const uint32_t* seed, uint32_t site, const float* ln_scale, const float* ln_bias,
                          void* y, int64_t ldy, float* mean, float* rstd, float eps, void* stream);
-int pcv_vit_embed_bwd(const float* dx, void* dpatch, float* dcls, float* dpos, float* dbias,
-                      int B, int T, int D, float rate, const uint32_t* seed, uint32_t site, void* stream);
+/* The embedding VJP: g = dropout_vjp(dx); dpatch rows = bf16(g[b, 1:]); dpos += sum_b g; dcls += sum_b g[b, 0]
+ * (fixed-order sums: run-to-run identical). */
+int pcv_vit_embed_bwd(const float* dx, void* dpatch, float* dcls, float* dpos, int B, int T, int D, float rate,
+                      const uint32_t* seed, uint32_t site, void* stream);
 /* nn.Embed gather / scatter-add (models/LM/transformer.py:361-369). */
 int pcv_embed_fwd(const int* ids, const void* table, int64_t ldt, void* out, int64_t ldo, int64_t R,
                   int D, int V, int* oob_flag, void* stream);
@@ -298,7 +303,9 @@ int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, int64_t ldb, 
  * panels x ksplit K slices; first = prefix sum of tiles * ksplit.  ws == NULL: the slices are added
  * with fp32 atomics; ws (tiles * ksplit * 64 * bn floats): each slice stores its partial tile there and
  * pcv_gemm_f32_wgrad_fold (fold_tiles = sum of tiles over the ws jobs; ffirst = their prefix) adds
- * the slices to C in order -- deterministic.
+ * the slices to C in order -- deterministic.  With colsum and ws, the first 64-row panel's column
+ * partials go to ws + tiles * ksplit * 64 * bn ([N / bn][ksplit][bn] floats) and the fold adds them
+ * to colsum in slice order too.
  * Requires M % 64, N % bn, K % 64, kchunk % 64 == 0, 16-B aligned operands, ld % 4 == 0. */
 int pcv_gemm_f32_wgrad_job_size(void);
 int pcv_gemm_f32_wgrad(const void* jobs_dev, int njobs, int64_t total_blocks, int bn, void* stream);
@@ -384,8 +391,10 @@ int pcv_grad_scale(const float* g, const void* chunks, int nchunks, float* parti
 int pcv_step_bump(int* step, void* stream);
 /* Muon (optax.contrib.muon scale_by_muon): momentum + nesterov + Frobenius normalisation
  * into NS workspaces, and the shape-scaled weight-decayed update; descriptors are
- * pcv_muon_mat_size()-byte records (see optim_types.h MuonMat; norm2 is a zeroed double: the
- * per-block partial sums add exactly in fp64, so the result does not depend on atomic order). */
+ * pcv_muon_mat_size()-byte records (see optim_types.h MuonMat; norm2 points to MUON_NSLOT = 256
+ * zeroed doubles: prep block b stores its partial sum of squares in slot b, the NS / norm kernels add
+ * the slots in slot order, so the norm does not depend on block order -- by construction). */
+int pcv_muon_norm_slots(void);
 int pcv_muon_prep(const void* mats, int nmats, int nnorm, int64_t max_elems, float beta, int nesterov, float eps,
                   const int* step, const float* gscale, void* stream);
 int pcv_muon_apply(const void* mats, int nmats, int64_t max_elems, float lr, float wd, int shape_scale,
@@ -414,21 +423,18 @@ int pcv_transpose_rec_size(void);
  * workgroup's LDS (csrc/muon_fused.hip): reads each record's x32 (un-normalised, from
  * pcv_muon_prep) and norm2, writes xo.  pcv_muon_fused_ok(rows, cols) says which shapes qualify. */
 int pcv_muon_fused_ok(int64_t rows, int64_t cols);
-/* The whole Muon step in ONE launch when every routed matrix fits pcv_muon_ns_fused (ViT-small):
- * nmats workgroups run momentum/Nesterov prep, the in-block Frobenius norm, NS and the update of one
- * matrix each (records as pcv_muon_prep / pcv_muon_apply: p/pb or upd per record), nchunks more run
+/* The Muon step's middle launch when every routed matrix fits pcv_muon_ns_fused (ViT-small), between
+ * pcv_muon_prep and pcv_muon_apply: nmats workgroups run the NS of one matrix each (x32 / norm slots
+ * from pcv_muon_prep, xo for pcv_muon_apply: the streaming parts stay wide launches), nchunks more run
  * the Adam branch (chunk table as pcv_adamw_step) over the flat p, g, mu, nu; the last block to finish
- * bumps *step (ticket: a zeroed device int the call leaves zeroed).  apply = 0: updates to the
- * records' upd and to the flat upd (functional update()).  in_block = 0: the matrix workgroups run
- * NS only (x32 / norm2 from pcv_muon_prep before, xo for pcv_muon_apply after: the streaming
- * parts stay wide), the Adam branch and the bump still ride in this launch.  in_block = 2: NS from
- * pcv_muon_prep's x32 / norm2 (norm2 reset here), then the update applied from the workgroup's LDS
- * (no pcv_muon_apply after it).  Any other in_block: PCV_EINVAL. */
+ * bumps *step (ticket: a zeroed device int the call leaves zeroed).  apply = 0: updates to the flat upd
+ * (functional update()).  nchunks = 0: the NS phase of the overlapped step (pcv_muon_grad_phase ran
+ * the prep and the Adam branch). */
 int pcv_muon_step_fused(const void* mats, int nmats, const void* chunks, int nchunks, float* p, const float* g,
                         float* mu, float* nu, void* p_bf16, float* upd, float lr, float wd, float beta, int nesterov,
                         float eps, int shape_scale, float ns_a, float ns_b, float ns_c, int ns_steps, float adam_b1,
                         float adam_b2, float adam_eps_root, float adam_wd, int apply, int* step, const float* gscale,
-                        int* ticket, int in_block, void* stream);
+                        int* ticket, void* stream);
 int pcv_muon_ns_fused(const void* mats, int nmats, float eps, float ns_a, float ns_b, float ns_c, int ns_steps,
                       void* stream);
 int pcv_chunk_size(void);
@@ -449,10 +455,17 @@ int pcv_chunk_size(void);
  *           bit 5 a symmetric result: upper-triangle tiles only, mirrored).
  * vec = 1: every job is float4-aligned (16-B bases, ld % 4, M, N, K % 4) -> vector staging.
  * vec = 2: small jobs (M, N, K <= 512, ta = 0, tb = 1, float4-aligned, no kscale / split-K) on
- *          32x32 tiles with K split over the workgroup's waves (tiles_n / first_tile in 32-tiles). */
+ *          32x32 tiles with K split over the workgroup's waves (tiles_n / first_tile in 32-tiles).
+ * Split-K jobs (ksplit > 1; C += alpha op(A) op(B) only): R null -> the slices are added to C with fp32
+ * atomics; R = a workspace of ksplit * ntile * 4096 floats (ntile = the job's 64x64 C tiles) -> each
+ * slice stores its partial tile there and pcv_gemm_f32_split_fold adds them to C in slice order
+ * (deterministic): fold records {ws, C, M, N, ldc, tiles_n, ntile, ksplit, first} (pcv_f32_fold_size()
+ * bytes; first = prefix sum of ntile), one block per C tile. */
 int pcv_f32_job_size(void);
 int pcv_gemm_f32_grouped(const void* jobs, int njobs, int64_t total_tiles, int vec, const int64_t* firsts_host,
                          void* stream);   /* firsts_host (optional): the jobs' first_tile values, host copy */
+int pcv_f32_fold_size(void);
+int pcv_gemm_f32_split_fold(const void* folds_dev, int nfolds, int64_t total_tiles, void* stream);
 /* Shampoo inverse p-th root (shampoo.py:195-215) by the coupled Newton iteration on the grouped
  * GEMM above: pcv_newton_init (record {L, M0, X0, conv[iters], X1, P, ldl, n, shift}; M0 = zA,
  * X0 = z^(1/p) I with A = L + shift I, z = (1+p)/(2||A||_F)), the per-iteration GEMM jobs, and

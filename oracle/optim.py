@@ -80,24 +80,40 @@ def adamw(learning_rate, b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0, weight_decay=
 # ----------------------------------------------------------------------------
 # Muon (optim/factory.py:441-484 -> optax.contrib.muon)
 # ----------------------------------------------------------------------------
-def newton_schulz(x, coeffs=(3.4445, -4.7750, 2.0315), steps=5, eps=1e-8):
+def _bf(x):
+    return x.to(torch.bfloat16).to(x.dtype)
+
+
+def newton_schulz(x, coeffs=(3.4445, -4.7750, 2.0315), steps=5, eps=1e-8, bf16=False):
     """optax.contrib orthogonalize_via_newton_schulz for dimension numbers (0,1):
-    transpose if rows > cols, X /= ||X||_F + eps, 5x {A=XX^T; B=bA+cA^2; X=aX+BX}."""
+    transpose if rows > cols, X /= ||X||_F + eps, 5x {A=XX^T; B=bA+cA^2; X=aX+BX}.
+
+    ``bf16=True`` is a NOISE MODEL of the device's one-workgroup NS (csrc/muon_fused.hip), not a
+    reference semantic: the MFMA operands bf16(X) and A' = bf16(b X X^T) with fp32 accumulation,
+    B = (c/b^2) A'A' + A' kept in fp32 (the kernel's hi + lo images), X carried in fp32 across
+    iterations (X' = B bf16(X) + a X) -- the parity tests use it to size the rounding spread of a
+    bf16-NS trajectory."""
     a, b, c = coeffs
     transposed = x.shape[0] > x.shape[1]
     if transposed:
         x = x.t()
     x = x / (torch.linalg.norm(x) + eps)
     for _ in range(steps):
-        A = x @ x.t()
-        B = b * A + c * (A @ A)
-        x = a * x + B @ x
+        if bf16:
+            xb = _bf(x)
+            A1 = _bf(b * (xb @ xb.t()))
+            B = (c / (b * b)) * (A1 @ A1) + A1
+            x = a * x + B @ xb
+        else:
+            A = x @ x.t()
+            B = b * A + c * (A @ A)
+            x = a * x + B @ x
     return x.t() if transposed else x
 
 
 def muon(learning_rate, ns_coeffs=(3.4445, -4.7750, 2.0315), ns_steps=5, beta=0.95, eps=1e-8,
          weight_decay=0.0, nesterov=True, adam_b1=0.9, adam_b2=0.999, adam_eps_root=0.0,
-         adam_weight_decay=0.0, adam_nesterov=True, shape_scale=True, routed=None, adaptive=False):
+         adam_weight_decay=0.0, adam_nesterov=True, shape_scale=True, routed=None, adaptive=False, ns_bf16=False):
     """partition{'muon': chain(scale_by_muon, add_decayed_weights(wd), scale_by_lr),
     'adam': adamw(b1, b2, eps, eps_root, wd, nesterov)}; labels from
     optim/muon.py:120-129 (should_use_matrix_preconditioner).
@@ -108,7 +124,7 @@ def muon(learning_rate, ns_coeffs=(3.4445, -4.7750, 2.0315), ns_steps=5, beta=0.
     O), arXiv 2409.20325; recalled from the optax source -- optax is absent here, so unpinned);
     x sqrt(max(1, fan_out/fan_in)).
     ``adam_nesterov``/``shape_scale`` are switches for the two recalled optax details
-    (SURVEY.md §7 hard part (i))."""
+    (SURVEY.md §7 hard part (i)); ``ns_bf16``: newton_schulz's device noise model (tests only)."""
     routed = routed or should_use_matrix_preconditioner
 
     def init(params):
@@ -126,7 +142,7 @@ def muon(learning_rate, ns_coeffs=(3.4445, -4.7750, 2.0315), ns_steps=5, beta=0.
                     mh = beta * mu[k] / (1.0 - beta ** (count + 1)) + (1.0 - beta) * g / (1.0 - beta ** count)
                 else:
                     mh = mu[k] / (1.0 - beta ** count)
-                o = newton_schulz(mh, ns_coeffs, ns_steps, eps)
+                o = newton_schulz(mh, ns_coeffs, ns_steps, eps, bf16=ns_bf16)
                 if adaptive:
                     o = (mh * o).sum() * o
                 if shape_scale:
@@ -362,8 +378,9 @@ def schedule_free(base, learning_rate, b1=0.9, weight_lr_power=2.0):
     return SimpleNamespace(init=init, update=update)
 
 
-def get_optimizer(cfg):
-    """optim/factory.py:180-802 restricted to the hot-path branches (+ the schedule-free wrapper)."""
+def get_optimizer(cfg, ns_bf16=False):
+    """optim/factory.py:180-802 restricted to the hot-path branches (+ the schedule-free wrapper).
+    ``ns_bf16``: Muon's Newton-Schulz through the device noise model (newton_schulz)."""
     name = str(getattr(cfg, "optim", "adamw")).lower()
     lr = float(cfg.lr)
     g = lambda k, d: getattr(cfg, k, d)  # noqa: E731
@@ -377,7 +394,7 @@ def get_optimizer(cfg):
                   weight_decay=wd, nesterov=g("muon_nesterov", True), adam_b1=g("beta1", 0.9),
                   adam_b2=g("beta2", 0.999), adam_eps_root=g("adam_eps_root", 0.0),
                   adam_weight_decay=wd, adam_nesterov=g("muon_nesterov", True),
-                  adaptive=bool(g("muon_adaptive", False)))
+                  adaptive=bool(g("muon_adaptive", False)), ns_bf16=ns_bf16)
     elif name == "soap":
         tx = soap(lr, b1=g("beta1", 0.95), b2=g("beta2", 0.95), eps=g("eps", 1e-8),
                   weight_decay=g("weight_decay", 0.01), precondition_frequency=g("precondition_frequency", 10),

@@ -222,3 +222,24 @@ struct PcvLdsOptIn {
     return err[dev];
   }
 };
+
+// Compute units of the current device (hipDeviceAttributeMultiprocessorCount), cached per device:
+// persistent grids size themselves to it.
+struct PcvCuCount {
+  static constexpr int kMaxDev = 64;
+  std::once_flag once[kMaxDev];
+  int n[kMaxDev] = {};
+  int get() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 256;
+    std::call_once(once[dev], [&] {
+      int v = 0;
+      n[dev] = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+    });
+    return n[dev];
+  }
+};
+static inline int pcv_cu_count() {
+  static PcvCuCount c;
+  return c.get();
+}

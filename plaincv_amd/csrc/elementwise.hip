@@ -142,9 +142,11 @@ __global__ void cast_kernel(const float* x, bf16* y, int64_t n) {
 }
 
 // ------------------------------------------------------------- column sums
-// out[c] += sum_r x[r,c]; block = 256 threads over 64 columns x 4 row lanes
+// out[c] += sum_r x[r,c]; block = 256 threads over 64 columns x 4 row lanes, gridDim.y row groups.
+// ws == nullptr: each row group adds its partial with an fp32 atomic; ws: it stores the partial to
+// ws[blockIdx.y][c] and colsum_fold_kernel adds the row groups in order (deterministic).
 template <typename T>
-__global__ void colsum_kernel(const T* x, int64_t ld, int64_t R, int N, float* out) {
+__global__ void colsum_kernel(const T* x, int64_t ld, int64_t R, int N, float* out, float* ws) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -155,7 +157,26 @@ __global__ void colsum_kernel(const T* x, int64_t ld, int64_t R, int N, float* o
   }
   red[rl][cl] = s;
   __syncthreads();
-  if (rl == 0 && c < N) atomicAdd(out + c, red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
+  if (rl == 0 && c < N) {
+    const float v = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    if (ws) ws[(int64_t)blockIdx.y * N + c] = v;
+    else atomicAdd(out + c, v);
+  }
+}
+__global__ void colsum_fold_kernel(const float* ws, int gy, int N, float* out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float v = 0.f;
+  int q = 0;
+  for (; q + 8 <= gy; q += 8) {   // 8 loads in flight, added in row-group order
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = ws[(int64_t)(q + u) * N + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += x[u];
+  }
+  for (; q < gy; ++q) v += ws[(int64_t)q * N + c];
+  out[c] += v;
 }
 
 // -------------------------------------------------------------------- ViT
@@ -193,37 +214,39 @@ __global__ void vit_embed_fwd_kernel(const float* patch, const float* cls, const
   }
 }
 
-// g = dx*mask; dpatch[b*hw+i] = bf16(g[b,1+i]); dpos[t] += sum_b g[b,t]; dcls += sum_b g[b,0];
-// dbias += sum_{b,t>=1} g[b,t]
-__global__ void vit_embed_bwd_kernel(const float* dx, bf16* dpatch, float* dcls, float* dpos, float* dbias, int B,
-                                     int T, int D, uint32_t thresh, float scale, const uint32_t* seedp,
-                                     uint32_t site) {
+// g = dx*mask; dpatch[b*hw+i] = bf16(g[b,1+i]); dpos[t] += sum_b g[b,t]; dcls += sum_b g[b,0].
+// One block per (token t, 32 columns): its 8 row lanes take interleaved eighths of the batch and
+// the 8 partials are added in lane order through LDS -- one add per output element, no float
+// atomics, so the embedding gradients are run-to-run identical (the batch-group atomics it replaces
+// made pos_embedding / cls_token gradients depend on block order).
+__global__ __launch_bounds__(256) void vit_embed_bwd_kernel(const float* dx, bf16* dpatch, float* dcls, float* dpos,
+                                                            int B, int T, int D, uint32_t thresh, float scale,
+                                                            const uint32_t* seedp, uint32_t site) {
+  __shared__ float red[8][33];
   const uint32_t seed = thresh ? *seedp : 0u;
-  const int64_t n = (int64_t)T * D;
-  // 8 batch groups (B = 64): group y on XCD y, whose L2 holds those rows of dx (written by the last
-  // row-tiled GEMM, XCD x = x-th eighth of the rows); otherwise the plain 2-D order
-  int bx = blockIdx.x, by = blockIdx.y;
-  if (gridDim.y == 8) {
-    const int L = blockIdx.x + gridDim.x * blockIdx.y;
-    by = L & 7;
-    bx = L >> 3;
-  }
-  const int64_t i = (int64_t)bx * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int d = (int)(i % D), t = (int)(i / D);
-  const int b0 = by * 8, b1 = min(B, b0 + 8);
+  const int nseg = (D + 31) / 32;
+  const int t = (int)blockIdx.x / nseg, d = ((int)blockIdx.x % nseg) * 32 + (threadIdx.x & 31);
+  const int ln = threadIdx.x >> 5;
   float s = 0.f;
+  if (d < D) {
 #pragma unroll 4
-  for (int b = b0; b < b1; ++b) {
-    const int64_t idx = ((int64_t)b * T + t) * D + d;
-    float g = dx[idx];
-    if (thresh) g = hash3(seed, site, (uint32_t)idx) >= thresh ? g * scale : 0.f;
-    s += g;
-    if (t > 0) dpatch[((int64_t)b * (T - 1) + t - 1) * D + d] = f2bf(g);
+    for (int b = ln; b < B; b += 8) {
+      const int64_t idx = ((int64_t)b * T + t) * D + d;
+      float g = dx[idx];
+      if (thresh) g = hash3(seed, site, (uint32_t)idx) >= thresh ? g * scale : 0.f;
+      s += g;
+      if (t > 0) dpatch[((int64_t)b * (T - 1) + t - 1) * D + d] = f2bf(g);
+    }
   }
-  atomicAdd(dpos + i, s);
-  if (t == 0) atomicAdd(dcls + d, s);
-  else if (dbias) atomicAdd(dbias + d, s);  // high contention: callers prefer colsum(dpatch)
+  red[ln][threadIdx.x & 31] = s;
+  __syncthreads();
+  if (threadIdx.x < 32 && d < D) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v += red[q][threadIdx.x];
+    dpos[(int64_t)t * D + d] += v;
+    if (t == 0) dcls[d] += v;
+  }
 }
 
 // --------------------------------------------------------------- embedding
@@ -337,15 +360,25 @@ extern "C" int pcv_cast_f32_bf16(const float* x, void* y, int64_t n, void* strea
   return pcv_launch_status();
 }
 
-extern "C" int pcv_colsum(const void* x, int64_t ld, int64_t R, int N, int x_f32, float* out, void* stream) {
-  if (R <= 0 || N <= 0) return PCV_EINVAL;
-  int gy = (int)((R + 31) / 32);
-  if (gy > 128) gy = 128;
+static int colsum_groups(int64_t R) {
+  int64_t gy = (R + 31) / 32;
+  return (int)(gy > 128 ? 128 : gy);
+}
+extern "C" int64_t pcv_colsum_ws_floats(int64_t R, int N) { return R > 0 && N > 0 ? colsum_groups(R) * (int64_t)N : 0; }
+
+// ws (optional, pcv_colsum_ws_floats(R, N) floats): the deterministic two-launch form
+extern "C" int pcv_colsum(const void* x, int64_t ld, int64_t R, int N, int x_f32, float* out, float* ws, void* stream) {
+  if (R <= 0 || N <= 0 || !x || !out) return PCV_EINVAL;
+  const int gy = colsum_groups(R);
+  if (gy <= 1) ws = nullptr;   // one row group: a single add per column
   dim3 grid((N + 63) / 64, gy);
   if (x_f32)
-    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)x, ld, R, N, out);
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)x, ld, R, N, out,
+                       ws);
   else
-    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, ld, R, N, out);
+    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, ld, R, N, out, ws);
+  if (ws)
+    hipLaunchKernelGGL(colsum_fold_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, ws, gy, N, out);
   return pcv_launch_status();
 }
 
@@ -370,16 +403,14 @@ extern "C" int pcv_vit_embed_fwd(const float* patch, const float* cls, const flo
   return pcv_launch_status();
 }
 
-extern "C" int pcv_vit_embed_bwd(const float* dx, void* dpatch, float* dcls, float* dpos, float* dbias, int B, int T,
-                                 int D, float rate, const uint32_t* seed, uint32_t site, void* stream) {
-  if (B <= 0 || T <= 1 || D <= 0) return PCV_EINVAL;
+extern "C" int pcv_vit_embed_bwd(const float* dx, void* dpatch, float* dcls, float* dpos, int B, int T, int D,
+                                 float rate, const uint32_t* seed, uint32_t site, void* stream) {
+  if (B <= 0 || T <= 1 || D <= 0 || !dx || !dpatch || !dcls || !dpos) return PCV_EINVAL;
   if (rate > 0.f && !seed) return PCV_EINVAL;
   uint32_t th; float sc;
   drop_params(rate, &th, &sc);
-  const int64_t n = (int64_t)T * D;
-  dim3 grid((unsigned)((n + 255) / 256), (unsigned)((B + 7) / 8));
-  hipLaunchKernelGGL(vit_embed_bwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, dx, (bf16*)dpatch,
-                     dcls, dpos, dbias, B, T, D, th, sc, seed, site);
+  hipLaunchKernelGGL(vit_embed_bwd_kernel, dim3((unsigned)((int64_t)T * ((D + 31) / 32))), dim3(256), 0,
+                     (hipStream_t)stream, dx, (bf16*)dpatch, dcls, dpos, B, T, D, th, sc, seed, site);
   return pcv_launch_status();
 }
 

@@ -1113,7 +1113,10 @@ __device__ __forceinline__ void colsum_job(const GemmArgs& g, int local) {
     float v = 0.f;
 #pragma unroll 8
     for (int q = 0; q < 32; ++q) v += red[q * 64 + tid];
-    atomicAdd((float*)g.C + cb * 64 + tid, v);
+    // several row slices: the slice's partial row goes to the workspace, the fold launch adds the
+    // slices in order (deterministic); one slice: the single add per column
+    if (g.sk_ws) g.sk_ws[(int64_t)slice * g.N + cb * 64 + tid] = v;
+    else atomicAdd((float*)g.C + cb * 64 + tid, v);
   }
 }
 
@@ -1160,6 +1163,24 @@ __global__ __launch_bounds__(256) void grouped_fold_kernel(const GemmArgs* __res
   }
   const GemmArgs& g = gs[lo];
   const int t = b - fprefix[lo];
+  if (g.act == GROUPED_JOB_COLSUM) {   // column-sum slices: partial rows [split_k][N], TILE columns per tile
+    if (rg != 0 || (int)threadIdx.x >= CPR) return;
+    const int64_t col = (int64_t)t * TILE + (threadIdx.x % CPR) * 4;
+    if (col >= g.N) return;
+    f32x4 acc{0.f, 0.f, 0.f, 0.f};
+    int q = 0;
+    for (; q + 8 <= g.split_k; q += 8) {   // 8 loads in flight, added in slice order
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(g.sk_ws + (int64_t)(q + u) * g.N + col);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; q < g.split_k; ++q) acc += *reinterpret_cast<const f32x4*>(g.sk_ws + (int64_t)q * g.N + col);
+    float* cp = (float*)g.C + col;
+    for (int e = 0; e < 4; ++e) cp[e] += acc[e];
+    return;
+  }
   const int tm = t / g.tiles_n, tn = t % g.tiles_n;
   const int rr = rg * RPB + threadIdx.x / CPR, c = (threadIdx.x % CPR) * 4;
   const int64_t row = (int64_t)tm * TILE + rr, col = (int64_t)tn * TILE + c;
@@ -1413,6 +1434,13 @@ extern "C" int64_t pcv_gemm_grouped_ws_floats(const void* descs, int n, int tile
   int64_t need = 0;
   for (int i = 0; i < n; ++i) {
     const PcvGemmDesc& e = d[i];
+    if (e.kind == GROUPED_JOB_COLSUM && e.M > 0 && e.N > 0) {   // partial rows of a sliced column sum
+      const int split = e.split_k < 1 ? 1 : e.split_k;
+      const int64_t kps = ((e.M + split - 1) / split + 31) / 32 * 32;
+      const int64_t sl = (e.M + kps - 1) / kps;
+      if (sl > 1) need += (sl * e.N + 3) / 4 * 4;
+      continue;
+    }
     if (e.kind != 0 || e.M <= 0 || e.N <= 0 || e.K <= 0) continue;
     const int sk = grouped_split(e, nullptr);
     if (sk > 1) need += ((e.M + tile - 1) / tile) * ((e.N + tile - 1) / tile) * (int64_t)sk * tile * tile;
@@ -1444,6 +1472,12 @@ extern "C" int pcv_gemm_grouped_plan(const void* descs, int n, int tile, void* p
       g.tiles_m = 1;
       g.tiles_n = (int)((e.N + 63) / 64);
       fprefix[i] = (int)ftot;
+      if (sk_ws && g.split_k > 1) {   // slice partials to the workspace, summed in order by the fold
+        g.sk_ws = sk_ws + ws_off;
+        ws_off += (int64_t)g.split_k * e.N;
+        ws_off = (ws_off + 3) / 4 * 4;   // keep every workspace region 16-B aligned
+        ftot += (e.N + tile - 1) / tile;
+      }
       prefix[i] = (int)tot;
       tot += (int64_t)g.tiles_n * g.split_k;
       gs[i] = g;

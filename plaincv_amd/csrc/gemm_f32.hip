@@ -69,7 +69,7 @@ template <bool TA, bool TB, int BN, int BM = GR_BM>
 __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
                                             int64_t ldb, int M, int m0, int n0, int kbeg, int kend, float* As,
                                             float* Bs, f32x4 (&acc)[2][GrShape<BM, BN>::NJ],
-                                            float* colsum = nullptr) {
+                                            bool colsum = false, float* cs_out = nullptr) {
   constexpr int C4 = GR_BK / 4;                          // float4 per 64-long k row
   constexpr int NA = BM * C4 / 256, NB = BN * C4 / 256;
   constexpr int WNW = GrShape<BM, BN>::WNW, WN = GrShape<BM, BN>::WN, NJ = GrShape<BM, BN>::NJ;
@@ -170,7 +170,44 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
       __syncthreads();
     }
   }
-  if (colsum) atomicAdd(colsum + n0 + cs_n, cs);
+  if (colsum) *cs_out = cs;   // this thread's partial column sum (column n0 + tid % BN)
+}
+
+// The Dense epilogue on 4 consecutive columns [col, col + 4) of one row, in the element order of
+// pcv_f32_epilogue: x + bias, then GELU (aux <- pre-activation) or, act = 2, dropout_vjp * gelu'(aux),
+// dropout (index row * N + col), + res_scale * res.  The operands it reads (bias, aux of act = 2,
+// res) come in `in`, loaded by gr_epi_load ahead of the MFMAs that produce v.
+struct GrEpiIn { f32x4 bias, aux, res; };
+__device__ __forceinline__ GrEpiIn gr_epi_load(const GrArgs& g, int row, int col) {
+  GrEpiIn in;
+  in.bias = g.bias ? *reinterpret_cast<const f32x4*>(g.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+  in.aux = g.act == 2 ? *reinterpret_cast<const f32x4*>(g.aux + (int64_t)row * g.ldaux + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+  in.res = g.res ? *reinterpret_cast<const f32x4*>(g.res + (int64_t)row * g.ldr + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+  return in;
+}
+__device__ __forceinline__ f32x4 gr_epi_apply(const GrArgs& g, f32x4 v, const GrEpiIn& in, int row, int col,
+                                              uint32_t seed) {
+  if (g.bias) v += in.bias;
+  if (g.act == 2) {   // backward of dropout(gelu(pre)): keep bits, then gelu'(pre)
+    const uint32_t base = (uint32_t)((int64_t)row * g.N + col);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = v[e];
+      if (g.thresh) x = hash3(seed, (uint32_t)g.site, base + e) >= g.thresh ? x * g.dscale : 0.f;
+      v[e] = x * gr_gelu_grad(in.aux[e]);
+    }
+  } else if (g.act) {
+    if (g.aux) *reinterpret_cast<f32x4*>(g.aux + (int64_t)row * g.ldaux + col) = v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = gr_gelu(v[e]);
+  }
+  if (g.thresh && g.act != 2) {
+    const uint32_t base = (uint32_t)((int64_t)row * g.N + col);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = hash3(seed, (uint32_t)g.site, base + e) >= g.thresh ? v[e] * g.dscale : 0.f;
+  }
+  if (g.res) v += g.res_scale * in.res;
+  return v;
 }
 
 template <bool TB, bool EPI, int BN, int BM>
@@ -190,6 +227,19 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int Q = BN / 4, IT = BM * Q / 256;
+  // the epilogue's operands (bias, residual, act = 2's pre-activation) are loaded before the main
+  // loop (<= 4 float4 rows per thread), so their round trip overlaps the MFMAs instead of following them
+  constexpr bool PRE = EPI && IT <= 4;
+  GrEpiIn pin[PRE ? IT : 1];
+  if (PRE) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = threadIdx.x + 256 * it;
+      pin[it] = gr_epi_load(g, min(m0 + idx / Q, g.M - 1), n0 + (idx % Q) * 4);
+    }
+  }
+  const uint32_t seed = (EPI && g.thresh) ? *g.seed : 0u;
   gr_mainloop<false, TB, BN, BM>(g.A, g.lda, g.B, g.ldb, g.M, m0, n0, 0, g.K, As, Bs, acc);
   // C tile through LDS, so the epilogue streams rows as float4: 16-B loads of bias / residual and
   // 16-B stores of C (and of the GELU pre-activation)
@@ -202,37 +252,13 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) smem[(wm * 32 + i * 16 + 4 * g4 + r) * LDC + wn * WN + j * 16 + c16] = acc[i][j][r];
   __syncthreads();
-  const uint32_t seed = (EPI && g.thresh) ? *g.seed : 0u;
-  constexpr int Q = BN / 4;
 #pragma unroll
-  for (int it = 0; it < BM * Q / 256; ++it) {
+  for (int it = 0; it < IT; ++it) {
     const int idx = threadIdx.x + 256 * it, rl = idx / Q, cl = (idx % Q) * 4;
     const int row = m0 + rl, col = n0 + cl;
     if (row >= g.M) continue;
     f32x4 v = *reinterpret_cast<const f32x4*>(&smem[rl * LDC + cl]);
-    if (EPI) {
-      if (g.bias) v += *reinterpret_cast<const f32x4*>(g.bias + col);
-      if (g.act == 2) {   // backward of dropout(gelu(pre)): keep bits, then gelu'(pre)
-        const f32x4 pre = *reinterpret_cast<const f32x4*>(g.aux + (int64_t)row * g.ldaux + col);
-        const uint32_t base = (uint32_t)((int64_t)row * g.N + col);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x = v[e];
-          if (g.thresh) x = hash3(seed, (uint32_t)g.site, base + e) >= g.thresh ? x * g.dscale : 0.f;
-          v[e] = x * gr_gelu_grad(pre[e]);
-        }
-      } else if (g.act) {
-        if (g.aux) *reinterpret_cast<f32x4*>(g.aux + (int64_t)row * g.ldaux + col) = v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = gr_gelu(v[e]);
-      }
-      if (g.thresh && g.act != 2) {
-        const uint32_t base = (uint32_t)((int64_t)row * g.N + col);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = hash3(seed, (uint32_t)g.site, base + e) >= g.thresh ? v[e] * g.dscale : 0.f;
-      }
-      if (g.res) v += g.res_scale * *reinterpret_cast<const f32x4*>(g.res + (int64_t)row * g.ldr + col);
-    }
+    if (EPI) v = gr_epi_apply(g, v, PRE ? pin[PRE ? it : 0] : gr_epi_load(g, row, col), row, col, seed);
     *reinterpret_cast<f32x4*>(g.C + (int64_t)row * g.ldc + col) = v;
   }
 }
@@ -241,10 +267,14 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
 // rows) for every weight of the step in one launch: a table of jobs, each M/64 x N/BN tiles x
 // ksplit slices of K; slice partial sums are added with fp32 atomics (dW is zeroed per step).
 // colsum (optional): += the column sums of B (the bias gradient of the same Dense), accumulated by
-// the workgroups of the first 64-row panel from the B chunks they already hold in LDS.
-// ws (optional, jobs with ksplit > 1): slice sl of tile t stores its partial to
-// ws[(t * ksplit + sl) * 64 * BN ...] with plain stores and pcv_gemm_f32_wgrad_fold adds the slices
-// to C in slice order (ffirst = the job's first fold tile) -- deterministic, no contended atomics.
+// the workgroups of the first 64-row panel from the B chunks they already hold in LDS (the 256 / BN
+// per-thread partials of a column summed in thread order through LDS).
+// ws (jobs with ksplit > 1): slice sl of tile t stores its partial to ws[(t * ksplit + sl) * 64 * BN
+// ...] with plain stores, the first panel's column partials to ws[tiles * ksplit * 64 * BN +
+// (tn * ksplit + sl) * BN ...], and pcv_gemm_f32_wgrad_fold adds the slices to C and colsum in slice
+// order (ffirst = the job's first fold tile) -- deterministic: no float atomics whose order varies.
+// A job with ksplit == 1 adds its single partial per element (C and colsum start zeroed per step, and
+// two adds onto zero commute), so the launch is run-to-run identical either way.
 struct WgJob {
   const float* A; const float* B; float* C; float* colsum; float* ws;
   int64_t lda, ldb, ldc;
@@ -271,10 +301,25 @@ __global__ __launch_bounds__(256) void gemm_f32_wgrad_kernel(const WgJob* __rest
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int q = 0; q < NJ; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  gr_mainloop<true, false, BN>(jb.A, jb.lda, jb.B, jb.ldb, jb.M, m0, n0, kbeg, kend, As, Bs, acc,
-                               m0 == 0 ? jb.colsum : nullptr);
+  const bool cs_on = m0 == 0 && jb.colsum;
+  float cs = 0.f;
+  gr_mainloop<true, false, BN>(jb.A, jb.lda, jb.B, jb.ldb, jb.M, m0, n0, kbeg, kend, As, Bs, acc, cs_on, &cs);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
   const int g4 = lane >> 4, c16 = lane & 15;
+  if (cs_on) {   // (block-uniform) the column's 256 / BN thread partials in thread order
+    __syncthreads();   // the main loop's last LDS reads are done: As is free
+    As[threadIdx.x] = cs;
+    __syncthreads();
+    if (threadIdx.x < BN) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < 256 / BN; ++q) v += As[q * BN + threadIdx.x];
+      if (jb.ws && jb.ksplit > 1)
+        jb.ws[(int64_t)jb.tiles * jb.ksplit * (GR_BM * BN) + ((int64_t)(n0 / BN) * jb.ksplit + sl) * BN + threadIdx.x] = v;
+      else
+        atomicAdd(jb.colsum + n0 + threadIdx.x, v);
+    }
+  }
   if (jb.ws && jb.ksplit > 1) {
     float* part = jb.ws + ((int64_t)t * jb.ksplit + sl) * (GR_BM * BN);
 #pragma unroll
@@ -327,6 +372,20 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(const WgJob* __restrict
   for (; q < S; ++q) acc += *reinterpret_cast<const f32x4*>(p + (int64_t)q * GR_BM * BN);
   float* cp = jb.C + (int64_t)(m0 + rr) * jb.ldc + n0 + c;   // M % 64 == 0, N % BN == 0: in range
   *reinterpret_cast<f32x4*>(cp) = *reinterpret_cast<const f32x4*>(cp) + acc;
+  if (jb.colsum && m0 == 0 && rg == 0 && threadIdx.x < BN) {   // the first panel's column partials
+    const float* qp = jb.ws + (int64_t)jb.tiles * S * (GR_BM * BN) + (int64_t)(n0 / BN) * S * BN + threadIdx.x;
+    float v = 0.f;
+    int u = 0;
+    for (; u + 8 <= S; u += 8) {   // 8 loads in flight, added in slice order
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = qp[(int64_t)(u + e) * BN];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v += x[e];
+    }
+    for (; u < S; ++u) v += qp[(int64_t)u * BN];
+    jb.colsum[n0 + threadIdx.x] += v;
+  }
 }
 
 static bool gr_al(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -364,6 +423,7 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
     g.dscale = 1.f / (1.f - rate);
   }
   const bool epi = bias || act || res || g.thresh;
+  hipStream_t s = (hipStream_t)stream;
   // 64 x 128 panels, or 64 x 64 when the 128-wide grid would leave fewer than four workgroups per
   // CU (the N = 128 / 256 products: with one or two per CU the load / epilogue latency is exposed;
   // C4 step 2.185 -> 2.125 ms moving the N = 256 products to 64-wide panels)
@@ -383,7 +443,6 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
   const bool shrt = narrow && mt * (N / 64) < short_below;
   g.tiles_n = (int)(N / (narrow ? 64 : 128));
   const unsigned blocks = (unsigned)((shrt ? (M + 31) / 32 : mt) * g.tiles_n);
-  hipStream_t s = (hipStream_t)stream;
 #define GR_LAUNCH(TBv, EPv, BNv) hipLaunchKernelGGL((gemm_f32_rows_kernel<TBv, EPv, BNv, 64>), dim3(blocks), dim3(256), 0, s, g)
 #define GR_LAUNCH32(TBv, EPv) hipLaunchKernelGGL((gemm_f32_rows_kernel<TBv, EPv, 64, 32>), dim3(blocks), dim3(256), 0, s, g)
   if (shrt) {

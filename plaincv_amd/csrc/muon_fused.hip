@@ -306,7 +306,8 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
                                                              float ns_c, int ns_steps) {
   extern __shared__ __attribute__((aligned(16))) char smem_m[];
   const MuonMat M = mats[blockIdx.x];
-  ns_core(M, 1.f / ((float)sqrt(*M.norm2) + eps), ns_a, ns_b, ns_c, ns_steps, smem_m);
+  const float inv = muon_inv_norm(M, eps, reinterpret_cast<double*>(smem_m));   // before ns_core claims the LDS
+  ns_core(M, inv, ns_a, ns_b, ns_c, ns_steps, smem_m);
   // X_ns -> xo [rx][ldx] (real rows/columns only)
   const bf16* X = reinterpret_cast<const bf16*>(smem_m);
   const int rx = (int)(M.rows < M.cols ? M.rows : M.cols), cx = (int)(M.rows < M.cols ? M.cols : M.rows);
@@ -319,50 +320,14 @@ __global__ __launch_bounds__(MF_THREADS) void muon_ns_kernel(const MuonMat* mats
   }
 }
 
-// ---- the whole Muon step of a model whose routed matrices all fit the one-workgroup NS (ViT-small):
-// blocks [0, nmats): one routed matrix each -- momentum + Nesterov blend (muon_prep_kernel's math)
-// into x32, its Frobenius norm reduced in-block, the NS iterations, and the shape-scaled,
-// weight-decayed update applied straight from the LDS image (muon_apply_kernel's math); blocks
-// [nmats, nmats + nchunks): the Adam branch over the non-routed leaves (adamw_chunk).  The Adam
-// chunks run under the NS workgroups' latency, and the step counter is bumped by whichever block
-// finishes last (a ticket counter: every block reads the counter before taking its ticket), so
-// prep + NS + apply + AdamW + bump are one launch instead of five.
-// the routed matrix's shape-scaled, weight-decayed update applied straight from the NS result in LDS
-// (muon_apply_kernel's math): each thread owns 4 consecutive columns of a row, MF_UB rows in flight
-__device__ void muon_apply_lds(const MuonMat& M, const MuonHyper& h, const bf16* X) {
-  const bool tr = M.rows > M.cols;
-  const int rows = (int)M.rows, cols = (int)M.cols, ldp = (int)M.ld;
-  const int tpr = cols >> 2, rpp = MF_THREADS / tpr;
-  const int myr = (int)threadIdx.x / tpr, myc = ((int)threadIdx.x - myr * tpr) * 4;
-  const bool act = myr < rpp;
-  constexpr int MF_UB = 4;
-  const float sc = h.shape_scale > 0.f ? sqrtf(fmaxf(1.f, (float)M.cols / (float)M.rows)) : 1.f;
-  for (int rb = 0; rb < rows; rb += rpp * MF_UB) {
-    f32x4v pv[MF_UB];
-#pragma unroll
-    for (int u = 0; u < MF_UB; ++u) {
-      const int r = rb + u * rpp + myr;
-      if (act && r < rows) pv[u] = *reinterpret_cast<const f32x4v*>(M.p + r * ldp + myc);
-    }
-#pragma unroll
-    for (int u = 0; u < MF_UB; ++u) {
-      const int r = rb + u * rpp + myr;
-      if (!(act && r < rows)) continue;
-      f32x4v o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        o[e] = bf2f(X[tr ? mf_off(myc + e, r, MF_LDX) : mf_off(r, myc + e, MF_LDX)]);
-      const f32x4v uu = -h.lr * (o * sc + h.wd * pv[u]);
-      if (M.upd) *reinterpret_cast<f32x4v*>(M.upd + r * ldp + myc) = uu;
-      if (h.apply) {
-        const f32x4v pn = pv[u] + uu;
-        *reinterpret_cast<f32x4v*>(M.p + r * ldp + myc) = pn;
-        if (M.pb) *reinterpret_cast<bf16x4*>(M.pb + r * ldp + myc) = bf16x4{f2bf(pn[0]), f2bf(pn[1]), f2bf(pn[2]), f2bf(pn[3])};
-      }
-    }
-  }
-}
-
+// ---- the Muon step of a model whose routed matrices all fit the one-workgroup NS (ViT-small), one
+// launch between muon_prep and muon_apply: blocks [0, nmats) run the NS of one routed matrix each
+// (x32 and its norm slots from muon_prep, X_ns to xo for muon_apply: the per-matrix streaming of
+// prep / apply belongs on many CUs, not on the NS workgroup -- one CU moves only ~10 B/cycle); blocks
+// [nmats, nmats + nchunks) run the Adam branch over the non-routed leaves (adamw_chunk) under the NS
+// workgroups' latency; the step counter is bumped by whichever block finishes last (a ticket counter:
+// every block reads the counter before taking its ticket).  nchunks = 0: the NS phase of the
+// overlapped step (engine.GraphedTrainStep overlap_opt), whose Adam branch ran in pcv_muon_grad_phase.
 struct MuonStepArgs {
   const MuonMat* mats; int nmats;
   const Chunk* chunks;
@@ -371,29 +336,16 @@ struct MuonStepArgs {
   MuonHyper mh;
   float ns_a, ns_b, ns_c; int ns_steps;
   int* step; const float* gscale; int* ticket;
-  int in_block;   // 1: prep and apply inside the NS workgroup; 0: NS only (prep / apply launched around
-                  // it); 2: NS + apply inside the workgroup (prep launched before it)
 };
 
 __global__ __launch_bounds__(MF_THREADS) void muon_step_kernel(MuonStepArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_m[];
   const int step = *a.step;
   const float gs = a.gscale ? *a.gscale : 1.f;
-  if ((int)blockIdx.x < a.nmats && a.in_block == 2) {
-    // NS from muon_prep's x32 and squared norm, then the update from the LDS image: the overlapped
-    // matrix phase (engine.GraphedTrainStep) has no wide apply launch left to wait for CUs behind the
-    // forward's kernels
+  if ((int)blockIdx.x < a.nmats) {
     const MuonMat M = a.mats[blockIdx.x];
-    ns_core(M, 1.f / ((float)sqrt(*M.norm2) + a.mh.eps), a.ns_a, a.ns_b, a.ns_c, a.ns_steps, smem_m);
-    // every thread read norm2 before ns_core's first barrier: reset it for the next prep (as muon_apply)
-    if (threadIdx.x == 0) *M.norm2 = 0.0;
-    muon_apply_lds(M, a.mh, reinterpret_cast<const bf16*>(smem_m));
-  } else if ((int)blockIdx.x < a.nmats && !a.in_block) {
-    // NS only: x32 and its squared norm come from muon_prep_kernel, X_ns goes to xo for
-    // muon_apply_kernel (both wide launches: one CU moves only ~10 B/cycle, so the per-matrix
-    // streaming of prep / apply belongs on many CUs, not on the NS workgroup)
-    const MuonMat M = a.mats[blockIdx.x];
-    ns_core(M, 1.f / ((float)sqrt(*M.norm2) + a.mh.eps), a.ns_a, a.ns_b, a.ns_c, a.ns_steps, smem_m);
+    const float inv = muon_inv_norm(M, a.mh.eps, reinterpret_cast<double*>(smem_m));
+    ns_core(M, inv, a.ns_a, a.ns_b, a.ns_c, a.ns_steps, smem_m);
     const bf16* X = reinterpret_cast<const bf16*>(smem_m);
     const int rx = (int)(M.rows < M.cols ? M.rows : M.cols), cx = (int)(M.rows < M.cols ? M.cols : M.rows);
     const int ldx = (int)M.ldx;
@@ -403,54 +355,6 @@ __global__ __launch_bounds__(MF_THREADS) void muon_step_kernel(MuonStepArgs a) {
       if (c4 < cx)
         *reinterpret_cast<bf16x4*>(xo + (int64_t)r * ldx + c4) = *reinterpret_cast<const bf16x4*>(X + mf_off(r, c4, MF_LDX));
     }
-  } else if ((int)blockIdx.x < a.nmats) {
-    const MuonMat M = a.mats[blockIdx.x];
-    const MuonHyper& h = a.mh;
-    const int64_t n = M.rows * M.cols;
-    const float t = (float)(step + 1);
-    const float bc = 1.f - powf(h.beta, t), bcn = 1.f - powf(h.beta, t + 1.f);
-    const bool tr = M.rows > M.cols;
-    // rows are contiguous (row stride ld): each thread owns 4 consecutive columns of a row, and
-    // MF_UB passes are loaded before any is used, so the loads of a thread overlap (a plain
-    // element loop serialised 64 dependent global round trips per thread)
-    const int rows = (int)M.rows, cols = (int)M.cols, ldp = (int)M.ld, ldx = (int)M.ldx;
-    const int tpr = cols >> 2, rpp = MF_THREADS / tpr;           // threads per row, rows per pass
-    const int myr = (int)threadIdx.x / tpr, myc = ((int)threadIdx.x - myr * tpr) * 4;
-    const bool act = myr < rpp;
-    constexpr int MF_UB = 4;
-    float ss = 0.f;
-    for (int rb = 0; rb < rows; rb += rpp * MF_UB) {
-      f32x4v gv[MF_UB], mv[MF_UB];
-#pragma unroll
-      for (int u = 0; u < MF_UB; ++u) {
-        const int r = rb + u * rpp + myr;
-        if (act && r < rows) {
-          gv[u] = *reinterpret_cast<const f32x4v*>(M.g + r * ldp + myc);
-          mv[u] = *reinterpret_cast<const f32x4v*>(M.mu + r * ldp + myc);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < MF_UB; ++u) {
-        const int r = rb + u * rpp + myr;
-        if (!(act && r < rows)) continue;
-        const f32x4v gi = gv[u] * gs;
-        const f32x4v mi = h.beta * mv[u] + (1.f - h.beta) * gi;
-        *reinterpret_cast<f32x4v*>(M.mu + r * ldp + myc) = mi;
-        const f32x4v xh = h.nesterov ? h.beta * mi / bcn + (1.f - h.beta) * gi / bc : mi / bc;
-        if (tr) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) M.x32[(myc + e) * ldx + r] = xh[e];
-        } else {
-          *reinterpret_cast<f32x4v*>(M.x32 + r * ldx + myc) = xh;
-        }
-        ss += xh[0] * xh[0] + xh[1] * xh[1] + xh[2] * xh[2] + xh[3] * xh[3];
-      }
-    }
-    float* red = reinterpret_cast<float*>(smem_m);   // scratch before ns_core claims the LDS
-    ss = block_sum(ss, red);
-    __syncthreads();
-    ns_core(M, 1.f / (sqrtf(ss) + h.eps), a.ns_a, a.ns_b, a.ns_c, a.ns_steps, smem_m);
-    muon_apply_lds(M, h, reinterpret_cast<const bf16*>(smem_m));
   } else {
     adamw_chunk(a.p, a.g, a.m, a.v, a.pb, a.upd, a.chunks[blockIdx.x - a.nmats], a.ah, step, gs);
   }
@@ -480,9 +384,8 @@ extern "C" int pcv_muon_step_fused(const void* mats, int nmats, const void* chun
                                    float beta, int nesterov, float eps, int shape_scale, float ns_a, float ns_b,
                                    float ns_c, int ns_steps, float adam_b1, float adam_b2, float adam_eps_root,
                                    float adam_wd, int apply, int* step, const float* gscale, int* ticket,
-                                   int in_block, void* stream) {
+                                   void* stream) {
   if (nmats <= 0 || nchunks < 0 || (nchunks > 0 && !chunks) || ns_steps < 0 || ns_b == 0.f || !step || !ticket ||
-      in_block < 0 || in_block > 2 ||
       !p || !g || !mu || !nu || (!apply && !upd))
     return PCV_EINVAL;
   MuonStepArgs a{};
@@ -492,7 +395,7 @@ extern "C" int pcv_muon_step_fused(const void* mats, int nmats, const void* chun
   a.ah = AdamHyper{lr, adam_b1, adam_b2, eps, adam_eps_root, adam_wd, nesterov, apply};
   a.mh = MuonHyper{beta, lr, wd, eps, shape_scale ? 1.f : 0.f, nesterov, apply};
   a.ns_a = ns_a; a.ns_b = ns_b; a.ns_c = ns_c; a.ns_steps = ns_steps;
-  a.step = step; a.gscale = gscale; a.ticket = ticket; a.in_block = in_block;
+  a.step = step; a.gscale = gscale; a.ticket = ticket;
   static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
   if (const int e = optin.ensure((const void*)muon_step_kernel, (int)((int)MF_LDS))) return e;
   hipLaunchKernelGGL(muon_step_kernel, dim3(nmats + nchunks), dim3(MF_THREADS), MF_LDS, (hipStream_t)stream, a);

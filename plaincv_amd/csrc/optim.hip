@@ -136,7 +136,8 @@ __device__ __forceinline__ bool muon_v4(const MuonMat& M) {
          ((reinterpret_cast<uintptr_t>(M.g) | reinterpret_cast<uintptr_t>(M.mu) |
            reinterpret_cast<uintptr_t>(M.p) | reinterpret_cast<uintptr_t>(M.x32)) & 15) == 0 &&
          (M.upd == nullptr || (reinterpret_cast<uintptr_t>(M.upd) & 15) == 0) &&
-         (M.pb == nullptr || (reinterpret_cast<uintptr_t>(M.pb) & 7) == 0);
+         (M.pb == nullptr || (reinterpret_cast<uintptr_t>(M.pb) & 7) == 0) &&
+         (M.xo == nullptr || (reinterpret_cast<uintptr_t>(M.xo) & 7) == 0);   // xo is read as bf16x4
 }
 
 // one block (bx of gx) of the prep of matrix M
@@ -167,9 +168,11 @@ __global__ __launch_bounds__(256) void muon_grad_phase_kernel(const MuonMat* mat
 
 __device__ __forceinline__ void muon_prep_block(const MuonMat& M, int bx, int gx, const MuonHyper& h, const int* step,
                                                 const float* gscale, float* red) {
+#pragma clang fp contract(off)   // inlined into two kernels: the same roundings in both (optim_types.h)
   const int n = (int)(M.rows * M.cols);
   const float t = (float)(*step + 1);
   const float bc = 1.f - powf(h.beta, t), bcn = 1.f - powf(h.beta, t + 1.f);
+  const float omb = 1.f - h.beta;
   const float gs = gscale ? *gscale : 1.f;
   const bool tr = M.rows > M.cols, v4 = muon_v4(M);
   const int cols = (int)M.cols;
@@ -201,8 +204,8 @@ __device__ __forceinline__ void muon_prep_block(const MuonMat& M, int bx, int gx
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float gi = gv[e] * gs;
-      mi[e] = h.beta * mv[e] + (1.f - h.beta) * gi;
-      xh[e] = h.nesterov ? h.beta * mi[e] / bcn + (1.f - h.beta) * gi / bc : mi[e] / bc;
+      mi[e] = h.beta * mv[e] + omb * gi;
+      xh[e] = h.nesterov ? h.beta * mi[e] / bcn + omb * gi / bc : mi[e] / bc;
     }
     if (v4) {
       *reinterpret_cast<float4*>(M.mu + off[0]) = float4{mi[0], mi[1], mi[2], mi[3]};
@@ -217,13 +220,14 @@ __device__ __forceinline__ void muon_prep_block(const MuonMat& M, int bx, int gx
     }
   }
   s = block_sum(s, red);
-  if (threadIdx.x == 0) atomicAdd(M.norm2, (double)s);
+  if (threadIdx.x == 0) M.norm2[bx] = (double)s;   // slot bx (bx < gx <= MUON_NSLOT)
 }
 
 __global__ __launch_bounds__(256) void muon_norm_kernel(const MuonMat* mats, float eps) {
+  __shared__ double sh;
   const MuonMat M = mats[blockIdx.y];
   const int64_t n = M.rows * M.cols;
-  const float inv = 1.f / ((float)sqrt(*M.norm2) + eps);
+  const float inv = muon_inv_norm(M, eps, &sh);
   const int cx = (int)(M.rows > M.cols ? M.rows : M.cols);
   for (int i = blockIdx.x * 256 + threadIdx.x; i < (int)n; i += gridDim.x * 256) {
     const int q = i / cx;
@@ -263,9 +267,6 @@ __global__ __launch_bounds__(256) void muon_dual_dot_kernel(const MuonMat* mats,
 // u = -lr*(O*[dual]*shape_scale + wd*p); p += u   (4 elements per thread, loads first, as muon_prep)
 __global__ __launch_bounds__(256) void muon_apply_kernel(const MuonMat* mats, MuonHyper h) {
   const MuonMat M = mats[blockIdx.y];
-  // the matrix's sum of squares was last read by the NS normalisation: reset it for the next step
-  // here instead of a separate fill launch (muon_prep accumulates into it with atomics)
-  if (blockIdx.x == 0 && threadIdx.x == 0) *M.norm2 = 0.0;
   const int n = (int)(M.rows * M.cols);
   const bool tr = M.rows > M.cols, v4 = muon_v4(M);
   const float ss = (h.shape_scale > 0.f ? sqrtf(fmaxf(1.f, (float)M.cols / (float)M.rows)) : 1.f) *
@@ -377,6 +378,8 @@ extern "C" int pcv_step_bump(int* step, void* stream) {
   return pcv_launch_status();
 }
 
+extern "C" int pcv_muon_norm_slots(void) { return MUON_NSLOT; }
+
 // nnorm: the leading records whose bf16 NS input the norm kernel writes (the others are
 // normalised by pcv_muon_ns_fused while it loads x32)
 extern "C" int pcv_muon_prep(const void* mats, int nmats, int nnorm, int64_t max_elems, float beta, int nesterov,
@@ -384,9 +387,9 @@ extern "C" int pcv_muon_prep(const void* mats, int nmats, int nnorm, int64_t max
   if (nmats <= 0 || nnorm < 0 || nnorm > nmats || max_elems >= (1ll << 31)) return PCV_EINVAL;
   MuonHyper h{beta, 0.f, 0.f, eps, 0.f, nesterov, 0, nullptr};
   hipStream_t s = (hipStream_t)stream;
-  // one 4-element group per thread; at most 256 blocks per matrix (each adds one fp64 atomic to norm2)
+  // one 4-element group per thread; at most MUON_NSLOT blocks per matrix (each stores one norm slot)
   int gx = (int)((max_elems + 256 * 4 - 1) / (256 * 4));
-  gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
+  gx = gx < 1 ? 1 : (gx > MUON_NSLOT ? MUON_NSLOT : gx);
   hipLaunchKernelGGL(muon_prep_kernel, dim3(gx, nmats), dim3(256), 0, s, (const MuonMat*)mats, h, step, gscale);
   gx = (int)((max_elems + 256 * 8 - 1) / (256 * 8));
   gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
@@ -404,7 +407,7 @@ extern "C" int pcv_muon_grad_phase(const void* mats, int nmats, int64_t max_elem
   MuonHyper h{beta, 0.f, 0.f, 0.f, 0.f, nesterov, 0, nullptr};
   AdamHyper ah{lr, b1, b2, eps, eps_root, wd, nesterov, 1};
   int gx = (int)((max_elems + 256 * 4 - 1) / (256 * 4));   // as pcv_muon_prep
-  gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
+  gx = gx < 1 ? 1 : (gx > MUON_NSLOT ? MUON_NSLOT : gx);
   hipLaunchKernelGGL(muon_grad_phase_kernel, dim3(nmats * gx + nchunks), dim3(256), 0, (hipStream_t)stream,
                      (const MuonMat*)mats, nmats, gx, h, (const Chunk*)chunks, p, g, mu, nu, (bf16*)p_bf16, ah, step,
                      gscale);

@@ -37,8 +37,11 @@ namespace pcv {
 // of one symmetric matrix in the Newton chain, or G G^T): only the upper-triangle tiles run
 // (T(T+1)/2 of T^2) and each writes its entries and their mirror, so C comes out exactly symmetric.
 // ksplit > 1 (split-K, for long-K jobs such as weight gradients with K = B*T): the job's tiles are
-// ksplit x (M/64 x N/64), each summing a kchunk-long slice of K and adding alpha * partial to C
-// with fp32 atomics -- only for C += alpha op(A) op(B) (beta = 1, no R / Cb / conv_out).
+// ksplit x (M/64 x N/64), each summing a kchunk-long slice of K -- only for C += alpha op(A) op(B)
+// (beta = 1, no R / Cb / conv_out).  The R field then holds a workspace: slice sl of C tile t stores
+// alpha * partial (the whole 64 x 64 tile, plain stores) at R + (sl * ntile + t) * 4096 and
+// pcv_gemm_f32_split_fold adds the slices to C in slice order (deterministic: no float atomics);
+// with R null the partials are added to C with fp32 atomics.
 struct F32Job {
   const float* A; const float* B; float* C;
   const float* kscale; const float* R; bf16* Cb; const float* alpha_dev;
@@ -254,15 +257,22 @@ __global__ __launch_bounds__(256) void gemm_f32_grouped_kernel(const F32Job* __r
   }
   const float beta = (float)jb.beta, rscale = (float)jb.rscale;
   if (jb.ksplit > 1) {
+    float* part = nullptr;
+    if (jb.R) {
+      const int ntile = (int)(((jb.M + FG_T - 1) / FG_T) * jb.tiles_n);
+      const int sl = (bid - (int)jb.first_tile) / ntile;
+      part = const_cast<float*>(jb.R) + ((int64_t)sl * ntile + t) * (FG_T * FG_T);
+    }
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm * 32 + a * 16 + (lane >> 4) * 4 + r;
-          const int col = n0 + wn * 32 + b * 16 + (lane & 15);
-          if (row < M && col < N) atomicAdd(jb.C + (int64_t)row * jb.ldc + col, alpha * acc[a][b][r]);
+          const int rl = wm * 32 + a * 16 + (lane >> 4) * 4 + r, cl = wn * 32 + b * 16 + (lane & 15);
+          const int row = m0 + rl, col = n0 + cl;
+          if (part) part[rl * FG_T + cl] = alpha * acc[a][b][r];
+          else if (row < M && col < N) atomicAdd(jb.C + (int64_t)row * jb.ldc + col, alpha * acc[a][b][r]);
         }
     return;
   }
@@ -869,6 +879,46 @@ __global__ __launch_bounds__(256) void permute_rc_kernel(const PermJob* __restri
   jb.dst[e] = jb.src[(int64_t)jb.pl[r] * jb.cols + jb.pr[c]];
 }
 
+// Fold of the split-K workspaces (see F32Job): FOLD_BPT blocks per C tile of the split jobs, one float4
+// of the tile per thread, the slices summed in slice order with FOLD_U loads in flight (the fold is a
+// chain of dependent-latency rounds: 64 slices one at a time cost ~200 us at C2's patch-conv gradient)
+constexpr int FOLD_BPT = 4, FOLD_U = 16;
+struct F32Fold {
+  const float* ws; float* C;
+  int64_t M, N, ldc, tiles_n, ntile, ksplit, first;
+};
+__global__ __launch_bounds__(256) void f32_split_fold_kernel(const F32Fold* __restrict__ folds, int nfolds) {
+  const int b = (int)blockIdx.x / FOLD_BPT, part = (int)blockIdx.x % FOLD_BPT;
+  int lo = 0, hi = nfolds - 1;
+  while (lo < hi) {   // last fold record whose first tile <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (folds[mid].first <= b) lo = mid; else hi = mid - 1;
+  }
+  const F32Fold f = folds[lo];
+  const int t = b - (int)f.first;
+  const int m0 = (t / (int)f.tiles_n) * FG_T, n0 = (t % (int)f.tiles_n) * FG_T;
+  const int idx = (part * 256 + (int)threadIdx.x) * 4, rl = idx / FG_T, cl = idx % FG_T;   // 4 columns
+  const int row = m0 + rl, col = n0 + cl;
+  if (row >= f.M || col >= f.N) return;
+  const float* p = f.ws + (int64_t)t * (FG_T * FG_T) + idx;
+  const int64_t stride = f.ntile * (FG_T * FG_T);
+  const int S = (int)f.ksplit;
+  f32x4 acc{0.f, 0.f, 0.f, 0.f};
+  int q = 0;
+  for (; q + FOLD_U <= S; q += FOLD_U) {
+    f32x4 v[FOLD_U];
+#pragma unroll
+    for (int u = 0; u < FOLD_U; ++u) v[u] = *reinterpret_cast<const f32x4*>(p + (int64_t)(q + u) * stride);
+#pragma unroll
+    for (int u = 0; u < FOLD_U; ++u) acc += v[u];
+  }
+  for (; q < S; ++q) acc += *reinterpret_cast<const f32x4*>(p + (int64_t)q * stride);
+  float* cp = f.C + (int64_t)row * f.ldc + col;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (col + e < f.N) cp[e] += acc[e];
+}
+
 }  // namespace pcv
 
 using namespace pcv;
@@ -919,6 +969,14 @@ extern "C" int pcv_gemm_f32_grouped(const void* jobs_dev, int njobs, int64_t tot
   else
     hipLaunchKernelGGL(gemm_f32_grouped_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream,
                        (const F32Job*)jobs_dev, njobs, total, f);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_f32_fold_size(void) { return (int)sizeof(F32Fold); }
+extern "C" int pcv_gemm_f32_split_fold(const void* folds_dev, int nfolds, int64_t total_tiles, void* stream) {
+  if (!folds_dev || nfolds <= 0 || total_tiles <= 0 || total_tiles >= (1ll << 31)) return PCV_EINVAL;
+  hipLaunchKernelGGL(f32_split_fold_kernel, dim3((unsigned)(total_tiles * FOLD_BPT)), dim3(256), 0, (hipStream_t)stream,
+                     (const F32Fold*)folds_dev, nfolds);
   return pcv_launch_status();
 }
 

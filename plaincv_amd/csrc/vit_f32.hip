@@ -185,28 +185,31 @@ struct LnPartJob {
 };
 static_assert(sizeof(LnPartJob) == 40, "LnPartJob layout");
 
-// dscale[c] += sum_b part[b][c], dbias[c] += sum_b part[b][D + c]: workgroup (x, y, z) sums 64
-// columns of job z (jobs == nullptr: the single job `one`) over block chunk y (4 slices), one atomic
-// per column and chunk
-__global__ __launch_bounds__(256) void ln_part_reduce_kernel(const LnPartJob* jobs, LnPartJob one) {
-  __shared__ float red[4][64];
+// dscale[c] += sum_b part[b][c], dbias[c] += sum_b part[b][D + c]: workgroup (x, z) sums 64 columns
+// of job z (jobs == nullptr: the single job `one`) over all of its nblk partial rows -- 16 row lanes
+// of 64 columns, the lanes' sums added in lane order through LDS and ONE add per column: the result is
+// run-to-run identical (no float atomics whose order varies)
+constexpr int LNR_THREADS = 1024, LNR_LANES = LNR_THREADS / 64;
+__global__ __launch_bounds__(LNR_THREADS) void ln_part_reduce_kernel(const LnPartJob* jobs, LnPartJob one) {
+  __shared__ float red[LNR_LANES][64];
   const LnPartJob j = jobs ? jobs[blockIdx.z] : one;
   const float* part = j.part;
   const int nblk = (int)j.nblk, D = (int)j.D;
   float *dscale = j.dscale, *dbias = j.dbias;
   const int col = blockIdx.x * 64 + (threadIdx.x & 63), sl = threadIdx.x >> 6;
-  const int chunk = (nblk + gridDim.y - 1) / gridDim.y, b0 = blockIdx.y * chunk;
-  const int b1 = b0 + chunk < nblk ? b0 + chunk : nblk;
   float sum = 0.f;
   if (col < 2 * D) {
-#pragma unroll 4
-    for (int b = b0 + sl; b < b1; b += 4) sum += part[(int64_t)b * 2 * D + col];
+#pragma unroll 16
+    for (int b = sl; b < nblk; b += LNR_LANES) sum += part[(int64_t)b * 2 * D + col];
   }
   red[sl][threadIdx.x & 63] = sum;
   __syncthreads();
   if (sl == 0 && col < 2 * D) {
-    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(col < D ? dscale + col : dbias + (col - D), t);
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < LNR_LANES; ++q) t += red[q][threadIdx.x];
+    float* o = col < D ? dscale + col : dbias + (col - D);
+    *o += t;
   }
 }
 
@@ -340,27 +343,37 @@ __global__ __launch_bounds__(256) void attn_softmax_bwd_f32_kernel(const float* 
 }
 
 // embedding VJP with an fp32 patch gradient: g = dropout_bwd(dx); dpatch[b*hw+i] = g[b,1+i];
-// dpos[t] += sum_b g[b,t]; dcls += sum_b g[b,0].  The batch is split over grid.y in 8-image slices
-// (partial sums added atomically): a thread walking all B images serialised B dependent loads.
-__global__ void vit_embed_bwd_f32_kernel(const float* dx, float* dpatch, float* dcls, float* dpos, int B, int T, int D,
-                                         uint32_t thresh, float scale, const uint32_t* seedp, uint32_t site) {
+// dpos[t] += sum_b g[b,t]; dcls += sum_b g[b,0].  One block per (token t, 32 columns): its 8 row
+// lanes take interleaved eighths of the batch and the 8 partials are added in lane order through
+// LDS, so the sums are run-to-run identical (one add per output element, no float atomics).
+__global__ __launch_bounds__(256) void vit_embed_bwd_f32_kernel(const float* dx, float* dpatch, float* dcls,
+                                                                float* dpos, int B, int T, int D, uint32_t thresh,
+                                                                float scale, const uint32_t* seedp, uint32_t site) {
+  __shared__ float red[8][33];
   const uint32_t seed = thresh ? *seedp : 0u;
-  const int64_t n = (int64_t)T * D;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int d = (int)(i % D), t = (int)(i / D);
-  const int b0 = blockIdx.y * 8, b1 = min(B, b0 + 8);
+  const int nseg = (D + 31) / 32;
+  const int t = (int)blockIdx.x / nseg, d = ((int)blockIdx.x % nseg) * 32 + (threadIdx.x & 31);
+  const int ln = threadIdx.x >> 5;
   float s = 0.f;
+  if (d < D) {
 #pragma unroll 4
-  for (int b = b0; b < b1; ++b) {
-    const int64_t idx = ((int64_t)b * T + t) * D + d;
-    float g = dx[idx];
-    if (thresh) g = keep_of(seed, site, (uint32_t)idx, thresh) ? g * scale : 0.f;
-    s += g;
-    if (t > 0) dpatch[((int64_t)b * (T - 1) + t - 1) * D + d] = g;
+    for (int b = ln; b < B; b += 8) {
+      const int64_t idx = ((int64_t)b * T + t) * D + d;
+      float g = dx[idx];
+      if (thresh) g = keep_of(seed, site, (uint32_t)idx, thresh) ? g * scale : 0.f;
+      s += g;
+      if (t > 0) dpatch[((int64_t)b * (T - 1) + t - 1) * D + d] = g;
+    }
   }
-  atomicAdd(dpos + i, s);
-  if (t == 0) atomicAdd(dcls + d, s);
+  red[ln][threadIdx.x & 31] = s;
+  __syncthreads();
+  if (threadIdx.x < 32 && d < D) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v += red[q][threadIdx.x];
+    dpos[(int64_t)t * D + d] += v;
+    if (t == 0) dcls[d] += v;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1275,8 +1288,7 @@ extern "C" int pcv_layernorm_bwd_f32(const float* dy, int64_t lddy, const float*
                                           (hipStream_t)stream, dy, lddy, x, ldx, scale, mean, rstd, dres, ldres, dx,
                                           lddx, ws, R, dxd, lddxd, th, sc, seed, site));
   if (!dscale) return pcv_launch_status();   // partials stay in ws for pcv_layernorm_part_reduce
-  const int chunks = (int)(blocks / 64 < 1 ? 1 : (blocks / 64 > 64 ? 64 : blocks / 64));   // ~64 partials each
-  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * D + 63) / 64), chunks), dim3(256), 0,
+  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * D + 63) / 64)), dim3(LNR_THREADS), 0,
                      (hipStream_t)stream, nullptr, LnPartJob{ws, dscale, dbias, blocks, D});
   return pcv_launch_status();
 }
@@ -1287,8 +1299,7 @@ extern "C" int pcv_layernorm_part_job_size() { return (int)sizeof(LnPartJob); }
 // table of LnPartJob; max_D / max_nblk bound the table's entries)
 extern "C" int pcv_layernorm_part_reduce(const void* jobs, int njobs, int max_D, int64_t max_nblk, void* stream) {
   if (!jobs || njobs <= 0 || njobs > 65535 || max_D <= 0 || max_D > 512 || max_nblk <= 0) return PCV_EINVAL;
-  const int chunks = (int)(max_nblk / 64 < 1 ? 1 : (max_nblk / 64 > 64 ? 64 : max_nblk / 64));
-  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * max_D + 63) / 64), chunks, njobs), dim3(256), 0,
+  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * max_D + 63) / 64), 1, njobs), dim3(LNR_THREADS), 0,
                      (hipStream_t)stream, (const LnPartJob*)jobs, LnPartJob{});
   return pcv_launch_status();
 }
@@ -1353,10 +1364,8 @@ extern "C" int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls
   if (B <= 0 || T <= 1 || D <= 0 || !dx || !dpatch || !dcls || !dpos || (rate > 0.f && !seed)) return PCV_EINVAL;
   uint32_t th; float sc;
   f32_drop(rate, &th, &sc);
-  const int64_t n = (int64_t)T * D;
-  hipLaunchKernelGGL(vit_embed_bwd_f32_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)((B + 7) / 8)), dim3(256), 0,
-                     (hipStream_t)stream,
-                     dx, dpatch, dcls, dpos, B, T, D, th, sc, seed, site);
+  hipLaunchKernelGGL(vit_embed_bwd_f32_kernel, dim3((unsigned)((int64_t)T * ((D + 31) / 32))), dim3(256), 0,
+                     (hipStream_t)stream, dx, dpatch, dcls, dpos, B, T, D, th, sc, seed, site);
   return pcv_launch_status();
 }
 

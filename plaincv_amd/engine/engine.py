@@ -14,7 +14,6 @@ whole step (forward, backward, optimizer) can be captured into one hipGraph
 (``GraphedTrainStep``) because every kernel runs on the current stream with
 device-resident seeds/counters.
 """
-import os
 from dataclasses import dataclass, field
 from typing import Any, Dict, Optional
 
@@ -138,6 +137,7 @@ def make_train_step(return_updates: bool = False):
         else:
             runner.seed.fill_(seed)
         store = state.params
+        store.settle()   # a GraphedTrainStep's deferred matrix phase, if any, first
         store.zero_grad()
         metrics = runner.forward(images, labels, train=True, need_grad=True)
         runner.backward(train=True)
@@ -164,6 +164,7 @@ def make_eval_step():
         images, labels = batch
         runner = state.runner_for(images.shape)
         images, labels = _prepare(runner, images, labels)
+        state.params.settle()
         m = runner.forward(images, labels, train=False, need_grad=False)
         return {"loss": m[0].clone(), "accuracy": m[1].clone()}
 
@@ -345,13 +346,6 @@ class GraphedTrainStep:
                 # steady-state graphs: the previous step's matrix phase on a side stream beside this
                 # step's forward head, joined before the first routed-weight read
                 self.side = torch.cuda.Stream(device=dev)
-                # split apply (PCV_MUON_SPLIT_APPLY=1, opt-in): block 0's routed matrices are updated
-                # first and joined before block 0's MLP; the rest update beside block 0's MLP and block
-                # 1's head and are joined before block 1's MLP
-                self.split_first = 0
-                if os.environ.get("PCV_MUON_SPLIT_APPLY", "0") == "1" and hasattr(state.tx, "split_first"):
-                    self.split_first = state.tx.split_first(
-                        state.opt_state, [t.data_ptr() for t in self.runner.join_weights(0)])
                 self.g_steady = []
                 for images, labels in [(None, None)] + self.slots:
                     g = torch.cuda.CUDAGraph()
@@ -359,20 +353,8 @@ class GraphedTrainStep:
                         with torch.cuda.graph(g, stream=s, pool=self.g_fb.pool()):
                             self.side.wait_stream(s)
                             with torch.cuda.stream(self.side):
-                                if self.split_first:
-                                    state.tx.step_ns_phase_(store, state.opt_state, part="a")
-                                    first = torch.cuda.Event()
-                                    first.record(self.side)
-                                    state.tx.step_ns_phase_(store, state.opt_state, part="b")
-                                else:
-                                    state.tx.step_ns_phase_(store, state.opt_state)
-                            if os.environ.get("PCV_OVERLAP_SERIAL") == "1":   # diagnostic: no concurrency
-                                s.wait_stream(self.side)
-                            if self.split_first:
-                                join = lambda i, e=first: (s.wait_event(e) if i == 0 else  # noqa: E731
-                                                           s.wait_stream(self.side) if i == 1 else None)
-                            else:
-                                join = lambda i: s.wait_stream(self.side) if i == 0 else None  # noqa: E731
+                                state.tx.step_ns_phase_(store, state.opt_state)
+                            join = lambda i: s.wait_stream(self.side) if i == 0 else None  # noqa: E731
                             self._fb(images, join=join)
                             s.wait_stream(self.side)   # (a one-block model never joins at block 1)
                             state.tx.step_grad_phase_(store, state.opt_state)
@@ -394,10 +376,14 @@ class GraphedTrainStep:
 
     def flush(self):
         """Finish the last step's deferred matrix phase (overlap_opt): the params and optimizer state
-        are then exactly those after the steps taken.  A no-op otherwise."""
+        are then exactly those after the steps taken.  A no-op otherwise.  Also run by
+        ParamStore.settle() (to_dict, load, the eager train / eval steps), so nothing reads the
+        params with a phase still owed."""
         if self.pending:
             self.g_flush.replay()
             self.pending = False
+        if self.state.params.pending == self.flush:
+            self.state.params.pending = None
 
     def _slot_of(self, images, labels):
         """The input slot holding exactly this batch: both the images AND the labels must be that slot's
@@ -430,6 +416,7 @@ class GraphedTrainStep:
             (self.g_steady[0] if steady else self.g_fb).replay()
         if self.overlap:
             self.pending = True
+            self.state.params.pending = self.flush
         if self.distributed:
             dp.all_reduce_grads(self.state.params)
             _reduce_batch_stats(self.state)

@@ -56,11 +56,12 @@ SIGNATURES = {
     "pcv_mlp_act_bwd": [P, I64, P, I64, P, I64, I64, I32, I32, I32, P],
     "pcv_dropout_bwd_cast": [P, I64, P, I64, I64, I32, F32, P, U32, P],
     "pcv_cast_f32_bf16": [P, P, I64, P],
-    "pcv_colsum": [P, I64, I64, I32, I32, P, P],
+    "pcv_colsum_ws_floats": [I64, I32],
+    "pcv_colsum": [P, I64, I64, I32, I32, P, P, P],
     "pcv_vit_patchify": [P, P, I32, I32, I32, I32, I32, P],
     "pcv_vit_embed_fwd": [P, P, P, P, P, I32, I32, I32, F32, P, U32, P],
     "pcv_vit_embed_ln_fwd": [P, P, P, P, I32, I32, I32, F32, P, U32, P, P, P, I64, P, P, F32, P],
-    "pcv_vit_embed_bwd": [P, P, P, P, P, I32, I32, I32, F32, P, U32, P],
+    "pcv_vit_embed_bwd": [P, P, P, P, I32, I32, I32, F32, P, U32, P],
     "pcv_seed_next": [P, P],
     "pcv_zero_seed": [P, I64, P, P],
     "pcv_embed_fwd": [P, P, I64, P, I64, I64, I32, I32, P, P],
@@ -109,8 +110,9 @@ SIGNATURES = {
     "pcv_muon_grad_phase": [P, I32, I64, F32, I32, P, I32, P, P, P, P, P, F32, F32, F32, F32, F32, F32, P, P, P],
     "pcv_muon_apply_dual": [P, I32, I64, F32, F32, I32, I32, P, P],
     "pcv_muon_step_fused": [P, I32, P, I32, P, P, P, P, P, P, F32, F32, F32, I32, F32, I32, F32, F32, F32, I32, F32,
-                            F32, F32, F32, I32, P, P, P, I32, P],
+                            F32, F32, F32, I32, P, P, P, P],
     "pcv_muon_ns_fused": [P, I32, F32, F32, F32, F32, I32, P],
+    "pcv_muon_norm_slots": [],
     "pcv_muon_fused_ok": [I64, I64],
     "pcv_transpose_bf16_batch": [P, I32, I64, P],
     "pcv_transpose_rec_size": [],
@@ -132,6 +134,8 @@ SIGNATURES = {
     "pcv_sort_job_size": [],
     "pcv_perm_job_size": [],
     "pcv_gemm_f32_grouped": [P, I32, I64, I32, P, P],
+    "pcv_f32_fold_size": [],
+    "pcv_gemm_f32_split_fold": [P, I32, I64, P],
     "pcv_eigh_log_floats": [I64, I32],
     "pcv_eigh_jacobi": [P, I32, I32, I32, F32, F32, I32, F32, F32, P],
     "pcv_eigh_vectors": [P, I32, I32, P],
@@ -148,7 +152,7 @@ SIGNATURES = {
 
 # non-status return types (everything else returns an int status)
 RESTYPES = {"pcv_attn_mask_words": I64, "pcv_batchnorm_workspace_size": SZ, "pcv_qrb_panel_lds": SZ, "pcv_gemm_grouped_plan_size": I64, "pcv_gemm_grouped_ws_floats": I64, "pcv_eigh_log_floats": I64,
-            "pcv_layernorm_bwd_f32_ws": I64}
+            "pcv_layernorm_bwd_f32_ws": I64, "pcv_colsum_ws_floats": I64}
 
 _lib = None
 _err = None

@@ -549,11 +549,17 @@ def cast_f32_bf16(x, y):
     hip.call("pcv_cast_f32_bf16", ptr(x), ptr(y), x.numel(), stream_ptr())
 
 
-def colsum(x, out):
+def colsum_ws_floats(R, N):
+    return int(hip.load().pcv_colsum_ws_floats(R, N))
+
+
+def colsum(x, out, ws=None):
+    """out += column sums of x; ws (fp32, >= colsum_ws_floats(R, N) elements): deterministic form."""
     R, N = x.shape
     _chk(out.dtype == F32 and out.numel() == N and out.is_contiguous(), "colsum out")
+    _chk(ws is None or (ws.dtype == F32 and ws.is_contiguous() and ws.numel() >= colsum_ws_floats(R, N)), "colsum ws")
     _dev(x, out)
-    hip.call("pcv_colsum", ptr(x), _ld(x), R, N, int(x.dtype == F32), ptr(out), stream_ptr())
+    hip.call("pcv_colsum", ptr(x), _ld(x), R, N, int(x.dtype == F32), ptr(out), ptr(ws), stream_ptr())
 
 
 def vit_patchify(images, out, patch):
@@ -582,10 +588,10 @@ def vit_embed_ln_fwd(patch_out, cls, pos, x, B, T, D, ln_scale, ln_bias, y, mean
              int(site), ptr(ln_scale), ptr(ln_bias), ptr(y), y.stride(0), ptr(mean), ptr(rstd), float(eps), stream_ptr())
 
 
-def vit_embed_bwd(dx, dpatch, dcls, dpos, dbias, B, T, D, rate=0.0, seed=None, site=0):
+def vit_embed_bwd(dx, dpatch, dcls, dpos, B, T, D, rate=0.0, seed=None, site=0):
     _chk(dx.numel() == B * T * D and dpatch.numel() == B * (T - 1) * D, "embed bwd")
-    _dev(dx, dpatch, dcls, dpos, dbias)
-    hip.call("pcv_vit_embed_bwd", ptr(dx), ptr(dpatch), ptr(dcls), ptr(dpos), ptr(dbias), B, T, D, float(rate),
+    _dev(dx, dpatch, dcls, dpos)
+    hip.call("pcv_vit_embed_bwd", ptr(dx), ptr(dpatch), ptr(dcls), ptr(dpos), B, T, D, float(rate),
              ptr(seed), int(site), stream_ptr())
 
 

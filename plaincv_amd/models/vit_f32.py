@@ -255,7 +255,7 @@ class ViTRunnerF32:
         # into ~1024-long slices accumulated with fp32 atomics -- ~2k workgroups instead of 138)
         # The layer weights go to the row-panel wgrad kernel (csrc/gemm_f32.hip) when their shapes fit,
         # the rest (head, patch conv, odd widths) to the grouped fp32 GEMM
-        wg, wr = GemmF32(), WgradF32(target_blocks=int(os.environ.get("PCV_F32_WGRAD_BLOCKS", "2048")))
+        wg, wr = GemmF32(), WgradF32(target_blocks=2048)
         ks = lambda t: max(1, t.shape[0] // 256)  # noqa: E731   (few tiles: a deep K split)
         # (+ the bias gradient = column sums of the same output gradient, folded into the row-panel
         # launch where the product fits it; otherwise a colsum launch in the backward)
@@ -265,6 +265,9 @@ class ViTRunnerF32:
             prods += [(self.a[i], self.dmo_l[i], w["gW1"], w["gb1"]), (self.y1[i], self.da_l[i], w["gW0"], w["gb0"]),
                       (self.o[i], self.dx1_l[i], w["gWo"], w["gbo"]), (self.y0[i], self.dqkv_l[i], w["gWqkv"], w["gbqkv"])]
         self.colsum_folded = set()
+        # one workspace for every stand-alone bias column sum (they run one after another)
+        self.colsum_ws = torch.zeros(max(K.colsum_ws_floats(B * T, max(3 * D, self.M, self.Kc)),
+                                         K.colsum_ws_floats(B * self.hw, D), 1), dtype=torch.float32, device=dev)
         for a, b, c, gb in prods:
             if WgradF32.fits(a, b, c) and os.environ.get("PCV_F32_WGRAD_ROWS", "1") != "0":
                 fold = gb.is_contiguous() and gb.numel() == b.shape[1]
@@ -297,9 +300,10 @@ class ViTRunnerF32:
                             **(drop if d else {}))
 
     def _colsum(self, x, gb):
-        """bias gradient += column sums of x, unless the weight-gradient launch folds it in"""
+        """bias gradient += column sums of x (deterministic two-launch form), unless the weight-gradient
+        launch folds it in"""
         if gb.data_ptr() not in self.colsum_folded:
-            K.colsum(x, gb)
+            K.colsum(x, gb, self.colsum_ws)
 
     def attn_bwd(self, i, rate):
         """Layer i's fused attention backward: dq | dk | dv of dqkv_l[i] from qkv, o, dO and the
@@ -314,7 +318,16 @@ class ViTRunnerF32:
         return self.attn_mask[i * w:(i + 1) * w]
 
     # ---------------------------------------------------------- forward
-    def forward(self, images, labels=None, train=True, need_grad=True):
+    # forward(join=fn) calls fn(i) right before block i's MlpBlock Dense_0, the first read of block i's
+    # Muon-routed weights (join_weights(i)); everything before block 0's reads only AdamW-branch leaves
+    # (engine.GraphedTrainStep overlap_opt: the previous step's Newton-Schulz phase runs beside it)
+    supports_join = True
+
+    def join_weights(self, i):
+        w = self.w[i]
+        return [w["W0"], w["W1"]]
+
+    def forward(self, images, labels=None, train=True, need_grad=True, join=None):
         m = self.m
         B, T, D = self.B, self.T, self.D
         rate = m.dropout_rate if train else 0.0
@@ -351,6 +364,8 @@ class ViTRunnerF32:
                 self._ln(self.x1s[i], w["s1"], w["c1"], self.y1[i], self.st1[i])
             elif self.bn:
                 self._bn(self.x1s[i], w["ra1"], self.bst1[i], w["s1"], w["c1"], self.y1[i], train)
+            if join is not None:
+                join(i)
             g["fc1"].run(rate, seed)
             g["fc2"].run(rate, seed)
         xcls = self.xs[-1].view(B, T * D)[:, :D]

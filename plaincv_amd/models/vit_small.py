@@ -568,7 +568,7 @@ class ViTRunner:
                 self.wside.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(self.wside):
                     self.wgrad_early()
-        K.vit_embed_bwd(dx_in, self.dpatch, self.gcls, self.gpos, None, B, T, D, rate, seed, SITE_EMBED)
+        K.vit_embed_bwd(dx_in, self.dpatch, self.gcls, self.gpos, B, T, D, rate, seed, SITE_EMBED)
         with self._fork():
             if self.wgrad is None:
                 K.colsum(self.dpatch, self.gbconv)

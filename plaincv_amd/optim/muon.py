@@ -24,7 +24,6 @@ workgroup with X, A, B resident in LDS -- one launch for all such matrices.
 """
 from collections import OrderedDict
 
-import os
 
 import numpy as np
 import torch
@@ -72,12 +71,6 @@ class Muon(GradientTransformation):
         self.adam = (float(adam_b1), float(adam_b2), float(adam_eps_root), float(adam_weight_decay))
         self.shape_scale = bool(shape_scale)
         self.fused = bool(fused)     # False: every routed matrix takes the batched-GEMM chain
-        # all-fused models run the whole step as one launch (PCV_MUON_ONE_LAUNCH=0: the 5-launch form)
-        self.one_launch = os.environ.get("PCV_MUON_ONE_LAUNCH", "1") != "0"
-        self.in_block = os.environ.get("PCV_MUON_IN_BLOCK", "0") == "1"
-        # PCV_MUON_OVERLAP_IN_BLOCK=1: the overlapped matrix phase applies each update from the NS
-        # workgroup's LDS instead of a wide muon_apply launch -- exact, but slower
-        self.overlap_in_block = os.environ.get("PCV_MUON_OVERLAP_IN_BLOCK", "0") == "1"
         self.shard = shard           # optim/sharding.py: NS work split across DP ranks
 
     def init(self, store):
@@ -109,7 +102,9 @@ class Muon(GradientTransformation):
         st.groups = [g for g in gl if not g.fused] + [g for g in gl if g.fused]
         st.n_general = sum(len(g.names) for g in st.groups if not g.fused)
         st.n_fused = len(routed) - st.n_general
-        st.norm2 = torch.zeros(max(1, len(routed)), dtype=torch.float64, device=dev)   # fp64: order-free sums
+        # per matrix MUON_NSLOT fp64 slots, one per prep block, added in slot order by the consumers
+        st.nslot = int(lib.pcv_muon_norm_slots())
+        st.norm2 = torch.zeros(max(1, len(routed)) * st.nslot, dtype=torch.float64, device=dev)
         st.dual = torch.zeros(max(1, len(routed)), dtype=torch.float64, device=dev) if self.adaptive else None
         st.ticket = torch.zeros(1, dtype=torch.int32, device=dev)   # last-block counter of the one-launch step
         # the one-launch step moves 4 consecutive columns per lane (16-B accesses of p, g, mu)
@@ -130,7 +125,7 @@ class Muon(GradientTransformation):
                 base = [store.flat.data_ptr() + off * 4, store.grad_flat.data_ptr() + off * 4,
                         mu.data_ptr() + off * 4, store.shadow.data_ptr() + off * 2]
                 tail = [rows, cols, leaf.strides[0], g.ldx, g.x32[j].data_ptr(), g.xb[j].data_ptr(),
-                        xo.data_ptr(), st.norm2.data_ptr() + idx * 8]
+                        xo.data_ptr(), st.norm2.data_ptr() + idx * st.nslot * 8]
                 recs_apply.append(base + [0] + tail)
                 recs_upd.append(base + [st.upd.data_ptr() + off * 4] + tail)
                 idx += 1
@@ -157,27 +152,25 @@ class Muon(GradientTransformation):
                      stream_ptr())
 
     def _run(self, store, st, gscale, apply):
-        if st.routed and st.n_general == 0 and self.one_launch and st.vec4 and not self.adaptive:
+        if st.routed and st.n_general == 0 and st.vec4 and not self.adaptive:
             # every routed matrix fits the one-workgroup NS: the NS workgroups, the Adam branch and the
-            # step bump share one launch (csrc/muon_fused.hip muon_step_kernel); prep and apply stay
-            # wide launches around it (PCV_MUON_IN_BLOCK=1 moves them into the NS workgroups)
+            # step bump share one launch (csrc/muon_fused.hip muon_step_kernel), between the wide prep
+            # and apply launches
             b1, b2, eps_root, awd = self.adam
             br = st.branch
             mats = st.mats_apply if apply else st.mats_upd
-            if not self.in_block:
-                hip.call("pcv_muon_prep", ptr(st.mats_apply), len(st.routed), 0, st.max_elems, self.beta,
-                         int(self.nesterov), self.eps, ptr(st.count), ptr(gscale), stream_ptr())
+            hip.call("pcv_muon_prep", ptr(st.mats_apply), len(st.routed), 0, st.max_elems, self.beta,
+                     int(self.nesterov), self.eps, ptr(st.count), ptr(gscale), stream_ptr())
             hip.call("pcv_muon_step_fused", ptr(mats), len(st.routed), ptr(br.chunks) if br.nchunks else None,
                      br.nchunks, ptr(store.flat), ptr(store.grad_flat), ptr(st.tensors["mu"]), ptr(st.tensors["nu"]),
                      ptr(store.shadow), ptr(st.upd), self.lr, self.wd, self.beta, int(self.nesterov), self.eps,
                      int(self.shape_scale), self.a, self.b, self.c, self.ns_steps, b1, b2, eps_root, awd, int(apply),
-                     ptr(st.count), ptr(gscale), ptr(st.ticket), int(self.in_block), stream_ptr())
-            if not self.in_block:
-                hip.call("pcv_muon_apply", ptr(mats), len(st.routed), st.max_elems, self.lr, self.wd,
-                         int(self.shape_scale), int(apply), stream_ptr())
+                     ptr(st.count), ptr(gscale), ptr(st.ticket), stream_ptr())
+            hip.call("pcv_muon_apply", ptr(mats), len(st.routed), st.max_elems, self.lr, self.wd,
+                     int(self.shape_scale), int(apply), stream_ptr())
             sharding.finish(st.shard, store, st, apply)
             return
-        if st.routed:   # st.norm2 is zero here: created zeroed, reset by pcv_muon_apply after use
+        if st.routed:
             hip.call("pcv_muon_prep", ptr(st.mats_apply), len(st.routed), st.n_general, st.max_elems, self.beta,
                      int(self.nesterov), self.eps, ptr(st.count), ptr(gscale), stream_ptr())
             self._newton_schulz(st)
@@ -197,7 +190,9 @@ class Muon(GradientTransformation):
     # step's forward (engine.GraphedTrainStep(overlap_opt=True)).  grad phase: momentum / Nesterov blend
     # into the NS operands (muon_prep) and the Adam branch -- everything that reads the gradients; NS
     # phase: the one-workgroup Newton-Schulz of every routed matrix (+ the step-counter bump) and the
-    # routed matrices' update.  grad phase of step t, then NS phase of step t, is exactly step_().
+    # routed matrices' update.  grad phase of step t, then NS phase of step t, computes step_()'s bits:
+    # the same device functions with every rounding explicit (csrc/optim_types.h), the same NS and
+    # apply kernels, order-free norm slots (tests/test_vit_parity_gpu.py asserts torch.equal).
     def split_capable(self, st):
         # every routed matrix on the one-workgroup NS kernel (its NS-only blocks need no 16-B row accesses)
         return bool(st.routed) and st.n_general == 0 and not self.adaptive and st.shard is None
@@ -210,45 +205,16 @@ class Muon(GradientTransformation):
                  ptr(store.grad_flat), ptr(st.tensors["mu"]), ptr(st.tensors["nu"]), ptr(store.shadow), self.lr, b1,
                  b2, self.eps, eps_root, awd, ptr(st.count), ptr(gscale), stream_ptr())
 
-    def split_first(self, st, ptrs):
-        """Order the NS-phase records so the routed matrices whose weights (fp32 or bf16-shadow data
-        pointers in ptrs) the next forward reads first come first; returns how many (0: no split).
-        step_ns_phase_(part="a") then updates only those, part="b" the rest -- the same per-matrix
-        kernels on the same records, so the result is step_ns_phase_()'s."""
-        n = len(st.routed)
-        recs = st.mats_apply.view(n, -1).cpu().numpy().view(np.uint64)
-        want = {int(p) for p in ptrs}
-        front = [i for i in range(n) if int(recs[i, 0]) in want or int(recs[i, 3]) in want]
-        if not front or len(front) == n:
-            st.n_first = 0
-            return 0
-        order = front + [i for i in range(n) if i not in set(front)]
-        st.mats_split = st.mats_apply.view(n, -1)[order].reshape(-1).contiguous()
-        st.rec_len = st.mats_apply.numel() // n
-        st.n_first = len(front)
-        return st.n_first
-
-    def step_ns_phase_(self, store, st, part=None):
-        """part None: NS + update of every routed matrix; "a": NS of all + update of the first
-        split_first() matrices; "b": update of the rest (after "a", on the same stream)."""
+    def step_ns_phase_(self, store, st):
+        """NS + update of every routed matrix (and the step-counter bump)."""
         b1, b2, eps_root, awd = self.adam
         n = len(st.routed)
-        mats = st.mats_apply if part is None else st.mats_split
-        in_block = part is None and self.overlap_in_block and st.vec4
-        if part != "b":
-            hip.call("pcv_muon_step_fused", ptr(mats), n, None, 0, ptr(store.flat),
-                     ptr(store.grad_flat), ptr(st.tensors["mu"]), ptr(st.tensors["nu"]), ptr(store.shadow), None,
-                     self.lr, self.wd, self.beta, int(self.nesterov), self.eps, int(self.shape_scale), self.a, self.b,
-                     self.c, self.ns_steps, b1, b2, eps_root, awd, 1, ptr(st.count), None, ptr(st.ticket),
-                     2 if in_block else 0, stream_ptr())
-        if in_block:
-            return
-        if part is None:
-            lo, hi = 0, n
-        else:
-            lo, hi = (0, st.n_first) if part == "a" else (st.n_first, n)
-        hip.call("pcv_muon_apply", ptr(mats[lo * st.rec_len:] if lo else mats), hi - lo, st.max_elems, self.lr,
-                 self.wd, int(self.shape_scale), 1, stream_ptr())
+        hip.call("pcv_muon_step_fused", ptr(st.mats_apply), n, None, 0, ptr(store.flat),
+                 ptr(store.grad_flat), ptr(st.tensors["mu"]), ptr(st.tensors["nu"]), ptr(store.shadow), None,
+                 self.lr, self.wd, self.beta, int(self.nesterov), self.eps, int(self.shape_scale), self.a, self.b,
+                 self.c, self.ns_steps, b1, b2, eps_root, awd, 1, ptr(st.count), None, ptr(st.ticket), stream_ptr())
+        hip.call("pcv_muon_apply", ptr(st.mats_apply), n, st.max_elems, self.lr, self.wd, int(self.shape_scale), 1,
+                 stream_ptr())
 
     def update(self, grads, state, params=None):
         ensure_grads(params, grads)

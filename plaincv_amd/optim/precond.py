@@ -54,8 +54,9 @@ class GemmF32:
             conv_tol=0.0, ksplit=1, sym=False):
         """a_affine = (mul, diag): op(A) -> mul * op(A) + diag * I (b_affine likewise);
         conv_in: skip this job when *conv_in <= conv_tol; conv_out: atomic max of |C - I|;
-        ksplit > 1: split K over that many tiles per C tile, accumulated with fp32 atomics (only
-        C += alpha op(A) op(B): beta 1, no r / cb / conv_out).
+        ksplit > 1: split K over that many tiles per C tile, the slices' partial tiles kept in a
+        workspace and added to C in slice order by a fold launch (deterministic; only C += alpha
+        op(A) op(B): beta 1, no r / cb / conv_out).
         sym: the caller knows the result is symmetric (and C / R too when read): only the
         upper-triangle tiles are computed, and mirrored."""
         M, K = (a.shape[1], a.shape[0]) if ta else (a.shape[0], a.shape[1])
@@ -103,10 +104,28 @@ class GemmF32:
                               ci=conv_in, co=conv_out, tol=float(conv_tol)))
         return self
 
+    FOLD_FMT = "<2Q7q"
+
     def finalize(self, device):
-        """Two device tables: float4-aligned jobs (vector staging kernel) and the rest."""
+        """Two device tables: float4-aligned jobs (vector staging kernel) and the rest; the split-K
+        jobs' workspace (passed in their R field) and fold table."""
         lib = hip.load()
         assert lib.pcv_f32_job_size() == struct.calcsize(self.FMT)
+        assert lib.pcv_f32_fold_size() == struct.calcsize(self.FOLD_FMT)
+        split = [j for j in self.jobs if j["ksplit"] > 1]
+        self.fold = None
+        if split:
+            ntile = lambda j: -(-j["M"] // TILE) * j["tiles_n"]  # noqa: E731
+            self.split_ws = torch.empty(sum(j["ksplit"] * ntile(j) * TILE * TILE for j in split),
+                                        dtype=torch.float32, device=device)
+            folds, off, first = [], 0, 0
+            for j in split:
+                j["R"] = self.split_ws[off:]
+                folds.append((self.split_ws.data_ptr() + 4 * off, _addr(j["C"]), j["M"], j["N"], j["ldc"],
+                              j["tiles_n"], ntile(j), j["ksplit"], first))
+                off += j["ksplit"] * ntile(j) * TILE * TILE
+                first += ntile(j)
+            self.fold = (_pack(folds, self.FOLD_FMT).to(device), len(folds), first)
         self.groups = []
         for vec in (2, 1, 0):
             recs, first = [], 0
@@ -132,6 +151,8 @@ class GemmF32:
         s = stream_ptr()
         for dev, n, total, vec, fh in self.groups:
             hip.call("pcv_gemm_f32_grouped", ptr(dev), n, total, vec, fh, s)
+        if self.fold is not None:
+            hip.call("pcv_gemm_f32_split_fold", ptr(self.fold[0]), self.fold[1], self.fold[2], s)
 
 
 class WgradF32:
@@ -143,15 +164,12 @@ class WgradF32:
     FMT = "<5Q3q10i"
     BN = 128
 
-    def __init__(self, target_blocks=2048, deterministic=None):
-        """deterministic (PCV_F32_WGRAD_DET=1): split-K slices store their partial tiles to a workspace
-        and a fold launch adds them to C in slice order (no float atomics, run-to-run identical).  Off
-        by default: unlike the bf16 grouped launch, this MFMA-bound launch does not wait on its atomics,
-        and the workspace round trip measured +0.8 % on the C4 step (1.7455 -> 1.760 ms)."""
+    def __init__(self, target_blocks=2048):
+        """Deterministic: split-K slices store their partial tiles (and the first panel's bias column
+        sums) to a workspace and a fold launch adds them to C in slice order -- no float atomics, so
+        the weight gradients are run-to-run identical (the workspace round trip measured +0.8 % on
+        the C4 step in round 3, when it was opt-in)."""
         self.jobs, self.target = [], int(target_blocks)
-        if deterministic is None:
-            deterministic = os.environ.get("PCV_F32_WGRAD_DET", "0") == "1"
-        self.deterministic = bool(deterministic)
 
     @classmethod
     def fits(cls, a, b, c):
@@ -181,7 +199,9 @@ class WgradF32:
             K = a.shape[0]
             kchunk = 64 * min(chunks, K // 64)
             plans.append((kchunk, -(-K // kchunk)))
-        nws = sum(t * ks * 64 * self.BN for t, (_, ks) in zip(tiles, plans) if ks > 1) if self.deterministic else 0
+        def nws_of(job, t, ks):   # tile partials + the first panel's column partials
+            return t * ks * 64 * self.BN + (job[3] is not None) * (job[1].shape[1] // self.BN) * ks * self.BN
+        nws = sum(nws_of(j, t, ks) for j, t, (_, ks) in zip(self.jobs, tiles, plans) if ks > 1)
         self.ws = torch.empty(nws, dtype=torch.float32, device=device) if nws else None
         recs, first, ffirst, woff = [], 0, 0, 0
         for (a, b, c, cs), t, (kchunk, ksplit) in zip(self.jobs, tiles, plans):
@@ -189,7 +209,7 @@ class WgradF32:
             wsp = 0
             if self.ws is not None and ksplit > 1:
                 wsp = self.ws.data_ptr() + 4 * woff
-                woff += t * ksplit * 64 * self.BN
+                woff += nws_of((a, b, c, cs), t, ksplit)
             recs.append((a.data_ptr(), b.data_ptr(), c.data_ptr(), _addr(cs), wsp, a.stride(0), b.stride(0),
                          c.stride(0), a.shape[1], b.shape[1], K, b.shape[1] // self.BN, t, ksplit, kchunk, first,
                          ffirst, 0))

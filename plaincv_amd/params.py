@@ -126,6 +126,10 @@ class ParamStore:
         # bumped whenever the bf16 shadow changes (load, optimizer step), so derived
         # copies (e.g. the LM runner's transposed forward weights) know to refresh
         self.version = 0
+        # a deferred optimizer phase still owed to these params (engine.GraphedTrainStep overlap_opt:
+        # the last step's Newton-Schulz phase): settle() runs it; every reader that must see the
+        # params as after the steps taken -- to_dict, load, the eager train / eval steps -- settles first
+        self.pending = None
 
     @staticmethod
     def _view(buf, leaf):
@@ -140,8 +144,15 @@ class ParamStore:
     def leaf(self, name):
         return self.layout.leaves[name]
 
+    def settle(self):
+        """Run the deferred optimizer phase, if one is pending (a no-op otherwise)."""
+        fn, self.pending = self.pending, None
+        if fn is not None:
+            fn()
+
     def load(self, values):
         """Copy a {name: tensor(Flax shape)} dict into the master buffer (pads stay 0)."""
+        self.settle()
         for k, v in values.items():
             self.params[k].copy_(torch.as_tensor(v, dtype=torch.float32))
         self.sync_shadow()
@@ -152,6 +163,7 @@ class ParamStore:
         self.version += 1
 
     def to_dict(self):
+        self.settle()
         return OrderedDict((k, v.detach().clone().cpu()) for k, v in self.params.items())
 
     def grads_dict(self):

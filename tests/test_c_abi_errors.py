@@ -78,10 +78,12 @@ def test_optimizer_entry_points(lib):
     assert lib.pcv_muon_ns_fused(P(A16), 1, 1e-8, 3.4445, 0.0, 2.0315, 5, None) == EINVAL   # b = 0
     assert lib.pcv_muon_prep(P(A16), 2, 3, 100, 0.95, 1, 1e-8, P(A16), None, None) == EINVAL  # nnorm > nmats
     assert lib.pcv_muon_apply(P(A16), 0, 100, 1e-3, 0.0, 1, 1, None) == EINVAL
-    step = lambda in_block: lib.pcv_muon_step_fused(  # noqa: E731
-        P(A16), 1, None, 0, P(A16), P(A16), P(A16), P(A16), P(A16), None, 1e-3, 0.0, 0.95, 1, 1e-8, 1, 3.4445,
-        -4.775, 2.0315, 5, 0.9, 0.95, 0.0, 0.0, 1, P(A16), None, P(A16), in_block, None)
-    assert step(3) == EINVAL and step(-1) == EINVAL                  # in_block: 0, 1 or 2
+    step = lambda nmats, ticket: lib.pcv_muon_step_fused(  # noqa: E731
+        P(A16), nmats, None, 0, P(A16), P(A16), P(A16), P(A16), P(A16), None, 1e-3, 0.0, 0.95, 1, 1e-8, 1, 3.4445,
+        -4.775, 2.0315, 5, 0.9, 0.95, 0.0, 0.0, 1, P(A16), None, ticket, None)
+    assert step(0, P(A16)) == EINVAL and step(1, None) == EINVAL       # no matrices / no ticket
+    assert lib.pcv_muon_norm_slots() == 256
+    assert lib.pcv_colsum(P(A16), 4, 0, 4, 1, P(A16), None, None) == EINVAL   # R = 0
     assert lib.pcv_grad_scale(P(A16), P(A16), 0, P(A16), 1.0, 1.0, P(A16), P(A16), None) == EINVAL
     assert lib.pcv_cast_f32_bf16(P(A16), P(A16), -1, None) == EINVAL
     assert lib.pcv_cast_f32_bf16(P(A16), P(A16), 0, None) == 0

@@ -86,10 +86,11 @@ def test_c1_fashion_mnist_adamw_10_steps(dev):
     assert hip64 <= max(1e-5, 2.0 * o64), (hip64, o64)
 
 
-def _c4_pair(dev, optim, steps, extra, soap_f=0, batch=8, fp64=False):
-    """Per step: (p0, p1, oracle update given the HIP gradients[, the fp64 oracle's update]).  SOAP:
-    basis checks and the basis-dependent state hand-over after step 0 and each refresh
-    (test_engine_parity_gpu.py), to the fp64 oracle as well."""
+def _c4_pair(dev, optim, steps, extra, soap_f=0, batch=64, fp64=False, noise_samples=3):
+    """Per step: (p0, p1, oracle update given the HIP gradients[, the fp64 oracle's update, the fp32
+    oracle's updates on `noise_samples` 1-ulp perturbations of the gradients]).  SOAP: basis checks and
+    the basis-dependent state hand-over after step 0 and each refresh (test_engine_parity_gpu.py), to the
+    fp64 oracle as well.  Batch 64: the benchmarked per-GPU batch."""
     from oracle import optim as oopt
     from plaincv_amd.engine import create_train_state, make_train_step
     from utils import Config
@@ -114,6 +115,12 @@ def _c4_pair(dev, optim, steps, extra, soap_f=0, batch=8, fp64=False):
         st, _ = step(st, (imgs.to(dev), labels.to(dev)), it)
         torch.cuda.synchronize()
         p1, g = st.params.to_dict(), st.params.grads_dict()
+        if fp64:   # fp32 rounding-noise samples: the fp32 oracle on the gradient perturbed by ~1 ulp
+            pert = []
+            for j in range(noise_samples):
+                gj = torch.Generator().manual_seed(100 * it + j)
+                pert.append(tx.update({k: v * (1.0 + (torch.rand(v.shape, generator=gj) * 2 - 1) * 2.0 ** -23)
+                                       for k, v in g.items()}, ost, p0)[0])
         u, ost = tx.update(g, ost, p0)
         if fp64:
             u64, ost64 = tx64.update({k: v.double() for k, v in g.items()}, ost64, {k: v.double() for k, v in p0.items()})
@@ -128,50 +135,61 @@ def _c4_pair(dev, optim, steps, extra, soap_f=0, batch=8, fp64=False):
                         setattr(o, nm, getattr(s_, nm).cpu().clone().reshape(getattr(o, nm).shape))
                         if fp64:
                             setattr(ost64[s_.name], nm, getattr(o, nm).double())
-        out.append((p0, p1, u, u64) if fp64 else (p0, p1, u))
+        out.append((p0, p1, u, u64, pert) if fp64 else (p0, p1, u))
     return out, st
+
+
+def _noise_bound(out, floor, soap=False):
+    """Per leaf: (HIP distance from the fp64 update, the fp32 noise spread, bound, worst step).  The
+    spread is the largest distance from the fp64 update over the fp32 oracle's own update and its
+    updates on 1-ulp perturbations of the same gradients -- several samples of fp32 rounding noise,
+    because the noise is heavy-tailed: Adam's m / (sqrt(v) + eps) (eps 1e-8) turns a coordinate that is
+    ~0 (in SOAP's rotated basis, or a raw gradient coordinate) into an O(1) step of either sign, so ONE
+    fp32 sample under-estimates the spread whenever such a coordinate exists.  bound = max(floor, 2 x
+    spread), per leaf and over the steps."""
+    worst = {}
+    for it, (p0, p1, u, u64, pert) in enumerate(out):
+        for k in p0:
+            d = p1[k].double() - p0[k].double()
+            if soap and it == 0 and routed(k, p0[k]):
+                assert d.abs().max().item() == 0.0, k        # SOAP's first step: update exactly 0
+                continue
+            hip = rel(d, u64[k])
+            spread = max([rel(u[k], u64[k])] + [rel(q[k], u64[k]) for q in pert])
+            w = worst.get(k)
+            if w is None or hip > w[0]:
+                worst[k] = (hip, spread, it)
+            worst[k] = (max(worst[k][0], hip), max(worst[k][1], spread), worst[k][2])
+    return {k: (h, sp, max(floor, 2.0 * sp), it) for k, (h, sp, it) in worst.items()}
 
 
 def test_c4_fp32_soap_13_steps_two_refreshes(dev):
     """Each step's update against the fp64 oracle fed the same gradients and handed the same bases,
-    bounded per leaf by max(5e-4, 2x the fp32 oracle's own distance from it): the Adam step in the
-    rotated basis (eps 1e-8) divides rotated-gradient coordinates by their own running RMS, so a
-    coordinate that is ~0 in the rotated basis carries its fp32 rounding noise at O(1) into the
-    update -- any fp32 implementation, the CPU oracle's included, moves by up to ~1e-3 there.  Bound:
-    max(1e-3, 4x) -- one GPU sample against one oracle sample: in one of six r04 runs an MLP leaf sat
-    at 2.6e-3 against the oracle's 7.6e-4 (the other runs' worst leaf ~1.1e-4); a wrong step (bias
-    correction, basis, eps) is off by 1e-1 or more."""
+    bounded per leaf by max(5e-4, 2x the fp32 noise spread) (_noise_bound).  Round 4 saw one run in
+    six with an MLP leaf at 2.6e-3 against a 5e-4 / 2x-one-sample bound: the fp32 weight-gradient
+    reductions used atomics (gradients differed run to run, and with them which rotated coordinates sit
+    near 0), and a single fp32 oracle sample set the spread.  Both are fixed: the fp32 step is bitwise
+    deterministic (test_vit_f32_gpu.py::test_vit_f32_step_is_bitwise_deterministic) and the spread is
+    the maximum over four noise samples.  The worst step of every leaf is printed (refresh steps are 5
+    and 10)."""
     out, st = _c4_pair(dev, "soap", 13, dict(precondition_frequency=5, eps=1e-8), soap_f=5, fp64=True)
     assert st.opt_state.host_step == 12
     sizes = {max(s.r, s.c) for s in st.opt_state.mats}
     assert 256 in sizes and 200 in sizes, sizes          # n = 256 factors (blocked QR) and the head
-    worst = {}
-    for it, (p0, p1, u, u64) in enumerate(out):
-        for k in p0:
-            d = p1[k].double() - p0[k].double()
-            if it == 0 and routed(k, p0[k]):
-                assert d.abs().max().item() == 0.0, k        # SOAP's first step: update exactly 0
-                continue
-            now = (rel(d, u64[k]), rel(u[k], u64[k]), rel(d, u[k]))
-            worst[k] = tuple(max(a, b) for a, b in zip(worst.get(k, now), now))
-    print("C4_SOAP (hip-fp64, oracle32-fp64, hip-oracle32)", sorted(worst.items(), key=lambda kv: -kv[1][0])[:6])
-    bad = {k: v for k, v in worst.items() if v[0] > max(1e-3, 4.0 * v[1])}
+    res = _noise_bound(out, 5e-4, soap=True)
+    print("C4_SOAP (hip-fp64, spread, bound, worst step)", sorted(res.items(), key=lambda kv: -kv[1][0] / kv[1][2])[:8])
+    bad = {k: v for k, v in res.items() if v[0] > v[2]}
     assert not bad, bad
 
 
 def test_c4_fp32_shampoo_6_steps(dev):
     """Each step's update against the fp64 oracle (fp64 eigh) fed the same gradients, bounded per leaf
-    by max(5e-4, 2x the fp32 oracle's own distance from it), as SOAP above.  L + eps I has every
-    eigenvalue >= eps, so the reference's clamp max(lambda, eps) (optim/shampoo.py:199-214) never
-    binds and the coupled-Newton inverse root computes the same P as eigh."""
+    by max(5e-4, 2x the fp32 noise spread), as SOAP above.  L + eps I has every eigenvalue >= eps, so the
+    reference's clamp max(lambda, eps) (optim/shampoo.py:199-214) never binds and the coupled-Newton
+    inverse root computes the same P as eigh."""
     out, _ = _c4_pair(dev, "shampoo", 6, dict(eps=1e-4), fp64=True)
-    worst = {}
-    for it, (p0, p1, u, u64) in enumerate(out):
-        for k in p0:
-            d = p1[k].double() - p0[k].double()
-            now = (rel(d, u64[k]), rel(u[k], u64[k]), rel(d, u[k]))
-            worst[k] = tuple(max(a, b) for a, b in zip(worst.get(k, now), now))
-    print("C4_SHAMPOO (hip-fp64, oracle32-fp64, hip-oracle32)",
-          sorted(worst.items(), key=lambda kv: -kv[1][0])[:8])
-    bad = {k: v for k, v in worst.items() if v[0] > max(5e-4, 2.0 * v[1])}
+    res = _noise_bound(out, 5e-4)
+    print("C4_SHAMPOO (hip-fp64, spread, bound, worst step)",
+          sorted(res.items(), key=lambda kv: -kv[1][0] / kv[1][2])[:8])
+    bad = {k: v for k, v in res.items() if v[0] > v[2]}
     assert not bad, bad

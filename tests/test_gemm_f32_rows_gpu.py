@@ -18,8 +18,12 @@ def _rows(a, b, tb, c, bias=None, aux=None, res=None, act=0, rate=0.0, seed=None
              res.stride(0) if res is not None else 0, 1.0, int(act), float(rate), ptr(seed), int(site), stream_ptr())
 
 
+# K in {128, 256, 384} take the weight-stationary kernel (every ViT-small product: fwd qkv / out / fc1 /
+# fc2 and the dgrads, C2's M = 64 * 257 and C1's M = 32 * 50), other K the tiled one
 @pytest.mark.parametrize("M,N,K,tb", [(16448, 128, 128, 0), (16448, 384, 128, 0), (1000, 256, 128, 0),
-                                      (16448, 128, 256, 1), (77, 128, 384, 1), (64, 128, 64, 0)])
+                                      (16448, 128, 256, 1), (77, 128, 384, 1), (64, 128, 64, 0),
+                                      (16448, 256, 128, 1), (16448, 128, 384, 1), (16448, 128, 256, 0),
+                                      (1600, 384, 128, 0), (16, 128, 128, 1), (3000, 128, 192, 0)])
 @pytest.mark.parametrize("mode", ["plain", "bias_res", "gelu_drop", "bias_drop_res", "gelubwd_drop"])
 def test_gemm_f32_rows(dev, M, N, K, tb, mode):
     from plaincv_amd.models.vit_f32 import _epi, _epi_bwd

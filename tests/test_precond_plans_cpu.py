@@ -38,15 +38,22 @@ def test_wgrad_f32_plan_and_fits():
     plan.finalize("cpu")
     recs = [struct.unpack(WgradF32.FMT, bytes(plan.table[i * struct.calcsize(WgradF32.FMT):(i + 1) * struct.calcsize(WgradF32.FMT)].tolist()))
             for i in range(2)]
-    first = 0
-    for rec in recs:
+    first = ffirst_exp = 0
+    ws0 = plan.ws.data_ptr()
+    woff = 0
+    for i, rec in enumerate(recs):
         M, N, K, tiles_n, tiles, ksplit, kchunk, fst, ffirst, _ = rec[8:]
-        assert rec[4] == 0 and ffirst == 0      # atomic split-K by default (no workspace, no fold)
+        # deterministic split-K: every split job has its workspace (tile partials, then -- with a bias
+        # column sum -- the first panel's column partials) and fold tiles in job order
+        assert ksplit > 1 and rec[4] == ws0 + 4 * woff and ffirst == ffirst_exp
+        woff += tiles * ksplit * 64 * 128 + (N // 128 * ksplit * 128 if i == 0 else 0)
+        ffirst_exp += tiles
         assert tiles == (M // 64) * (N // 128) and tiles_n == N // 128
         assert kchunk % 64 == 0 and (ksplit - 1) * kchunk < K <= ksplit * kchunk
         assert fst == first
         first += tiles * ksplit
     assert plan.total == first and 1024 <= first <= 4096
+    assert plan.ws.numel() == woff and plan.fold_tiles == ffirst_exp
     assert recs[0][3] != 0 and recs[1][3] == 0   # colsum pointer only where requested
 
 

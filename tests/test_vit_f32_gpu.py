@@ -217,3 +217,35 @@ def test_graphed_step_matches_eager_host_driven(dev, optim, mlp):
         if e > tol:
             bad[k] = e
     assert not bad, bad
+
+
+@pytest.mark.parametrize("optim", ["muon", "soap"])
+def test_vit_f32_step_is_bitwise_deterministic(dev, optim):
+    """The fp32 step has no order-dependent float reduction (round 5): the weight-gradient split-K
+    slices and bias column sums are folded in slice order, the grouped launch's split-K (patch-conv
+    weight gradient) likewise, the stand-alone bias column sums run the two-launch form, the
+    embedding VJP and the LayerNorm parameter reductions sum in a fixed order.  Two identical steps from
+    the same state -- C2/C4 geometry at B 64 -- give bitwise equal gradients and parameters."""
+    from plaincv_amd.engine import create_train_state, make_train_step
+    from utils import Config
+    m = _model(0.1, 200, 128, 256, 4, 4)
+    shape = (64, 64, 64, 3)
+    init = m.init(0, shape)
+    g = torch.Generator().manual_seed(5)
+    images = torch.randint(0, 256, shape, generator=g, dtype=torch.uint8).to(dev)
+    labels = torch.randint(0, 200, (shape[0],), generator=g, dtype=torch.int32).to(dev)
+    extra = dict(precondition_frequency=10, eps=1e-8) if optim == "soap" else {}
+    outs = []
+    for _ in range(2):
+        cfg = Config(optim=optim, lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9, **extra)
+        st = create_train_state(0, m, 1e-3, shape, 200, cfg=cfg, init_params=init)
+        step = make_train_step()
+        for it in range(2):
+            st, _ = step(st, (images, labels), 7 + it)
+        torch.cuda.synchronize()
+        outs.append((st.params.grads_dict(), st.params.to_dict()))
+    (g0, p0), (g1, p1) = outs
+    diff = [k for k in g0 if not torch.equal(g0[k], g1[k])]
+    assert not diff, diff
+    diff = [k for k in p0 if not torch.equal(p0[k], p1[k])]
+    assert not diff, diff
