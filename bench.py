@@ -191,8 +191,7 @@ def vit_roofline(state, image_shape):
     b1 = R * M * 2 + D * M * 2 + rows
     b2 = R * 3 * D * 2 + D * 3 * D * 2 + rows
     achieved = (b1 + b2) / (t1 + t2) / 1e9
-    wm = 1 if os.environ.get("PCV_LN_TILE") == "32" else 2   # pcv_gemm_ln tile: 64x128 (default) or 32x128
-    kname = f"gemm_bf16_kernel<true,true,{wm},4>"
+    kname = "gemm_bf16_kernel<true,true,2,4>"   # pcv_gemm_ln's 64x128 tile
     traffic, tsrc = pmc_traffic(kname)   # mean HBM bytes per launch (PMC)
     return {"kernel": f"{kname} = pcv_gemm_ln mode 2 (dgrad GEMM + LayerNorm backward "
                       f"epilogue; MLP M={R} N={D} K={M} and QKV M={R} N={D} K={3 * D})", "bound": "hbm",

@@ -55,10 +55,6 @@ int pcv_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, i
  * pcv_gemm_big_enable(on) toggles that dispatch (on < 0: query) and returns the previous state.
  * Replaces the same flax Dense contractions as pcv_gemm_bf16 (the LM forward and dgrad GEMMs). */
 int pcv_gemm_big_enable(int on);
-/* Row-panel dispatch of pcv_gemm_bf16 / pcv_gemm_ln (csrc/rowgemm.inc: the skinny token-row products,
- * A K-contiguous, N % 128 == 0 <= 384, K % 64 == 0): on (1) / off (0), on < 0 queries; returns the
- * previous state (off unless PCV_ROWGEMM=1). */
-int pcv_rowgemm_enable(int on);
 int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb);
 int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                  int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale, void* stream);

@@ -1589,361 +1589,9 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
   PCV_SHREC(3);
 }
 
-// Backward, key-owned form (T - tail <= 256, i.e. at most 16 key blocks on the MFMA path; the ViT's
-// T = 257 and every smaller T).  The kernel above recomputes the scores twice -- once per MFMA
-// orientation, in the key waves (dK, dV) and again in the query waves (dQ) -- and the short
-// kernels are VALU-issue bound (16 waves, 4 per SIMD: ~2.2k VALU instructions a wave against
-// 18 us; tools/icache_probe.hip rules out instruction fetch), so that second exp / dropout / dS
-// pass was ~40 % of the main phase.  Here every wave owns one key block and computes P and dS
-// once; dS (bf16, exactly the dK MFMA's operand) goes to a two-slot LDS ring [keys][32 queries]
-// per 32-query step, and after the step's barrier the owner of each 16-query tile (wave j owns
-// tile j, two per step) forms dQ = dS K from the ring with transposing reads: the MFMA keeps
-// the whole key sum in one wave, so dQ is deterministic (no atomics).  Row T - 1 is handled as
-// in the kernel above: the tail query by the key waves (VALU), the tail key by the tile owners.
-constexpr int SH2_KB = 16;   // key blocks / query tiles on the MFMA path
-constexpr int SH2_ROWS = SH2_KB * 16 + 16;   // image rows: the MFMA rows + the tail row (T <= 257)
-constexpr int SH2_SLOTS = 4;                  // ring slots: a barrier every 2 steps, slots reused after 4
-constexpr size_t SH2_SLOT = (size_t)SH2_KB * 16 * SH_DH;              // bf16 elements per slot
-constexpr size_t SH2_RING = SH2_SLOTS * SH2_SLOT;
-constexpr size_t SH_BWD2_LDS = 4 * SH2_ROWS * SH_DH * sizeof(bf16) + 2 * SH2_ROWS * sizeof(float) +
-                               SH_MASK_WORDS * sizeof(uint16_t) + SH2_RING * sizeof(bf16) +
-                               (3 * SH_WAVES * SH_DH + 4) * sizeof(float);
-
-static_assert(SH_BWD2_LDS <= 160 * 1024, "key-owned backward: LDS over the 160 KiB of a CU");
-template <int NS, bool DROP>   // NS = 32-row steps on the MFMA path (compile time: the loops unroll)
-__global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd2_kernel(AttnArgs a) {
-  constexpr int DH = SH_DH, DT = DH / 16;
-  extern __shared__ __attribute__((aligned(16))) char sh2_smem[];
-  bf16* Qs = reinterpret_cast<bf16*>(sh2_smem);
-  bf16* Ks = Qs + SH2_ROWS * DH;
-  bf16* Vs = Ks + SH2_ROWS * DH;
-  bf16* Os = Vs + SH2_ROWS * DH;   // dO
-  float* Ls = reinterpret_cast<float*>(Os + SH2_ROWS * DH);
-  float* Dl = Ls + SH2_ROWS;
-  uint16_t* mk = reinterpret_cast<uint16_t*>(Dl + SH2_ROWS);
-  bf16* ring = reinterpret_cast<bf16*>(mk + SH_MASK_WORDS);               // [4][256 keys][32 queries]
-  float* tailp = reinterpret_cast<float*>(ring + SH2_RING);                // [3][16][32] + corner
-  PCV_SHREC(0);
-  int h, b;
-  sh_head_of(a, h, b);
-  const int T = a.T, TP = min((T + 31) & ~31, SH2_ROWS);   // image rows (padding past the MFMA rows unread)
-  const int64_t bT = (int64_t)b * T, bh = (int64_t)b * a.H + h;
-  const bool tail1 = (T & 15) == 1 && T > 16;
-  const int Tm = tail1 ? T - 1 : T;          // rows on the MFMA path
-  const int NB = (Tm + 15) / 16;             // key blocks = query tiles (<= 16)
-  {
-    bf16* const img[4] = {Qs, Ks, Vs, Os};
-    const bf16* const src[4] = {a.q + h * DH, a.k + h * DH, a.v + h * DH, a.dout + h * DH};
-    const int64_t ld[4] = {a.ldq, a.ldq, a.ldq, a.lddo};
-    if (a.delta_ready) {
-      sh_prologue<4, DROP, true>(img, src, ld, T, TP, bT, mk, a.mask, (int)(drop_words(T) / 8), Ls, Dl,
-                                 a.lse2 + bh * T, a.delta + bh * T);
-    } else {
-      sh_load_images<4>(img, src, ld, T, TP, bT);
-      if (DROP) sh_load_mask(mk, a.mask, T);
-      constexpr int ITER = (SH_TMAX * 4 + SH_THREADS - 1) / SH_THREADS;
-      bf16x8 xo[ITER], xl[ITER], xd[ITER];
-      float lv[ITER];
-#pragma unroll
-      for (int i = 0; i < ITER; ++i) {
-        const int idx = threadIdx.x + SH_THREADS * i;
-        const int r = idx >> 2, c = (idx & 3) * 8;
-        xo[i] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        xl[i] = xo[i];
-        xd[i] = xo[i];
-        lv[i] = 0.f;
-        if (r < T) {
-          xo[i] = *reinterpret_cast<const bf16x8*>(a.o + (bT + r) * a.ldo + h * DH + c);
-          if (a.o_lo) xl[i] = *reinterpret_cast<const bf16x8*>(a.o_lo + (bT + r) * a.ldo + h * DH + c);
-          xd[i] = *reinterpret_cast<const bf16x8*>(a.dout + (bT + r) * a.lddo + h * DH + c);
-          lv[i] = a.lse2[bh * T + r];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < ITER; ++i) {
-        const int idx = threadIdx.x + SH_THREADS * i;
-        const int r = idx >> 2;
-        float sum = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sum += (bf2f(xo[i][j]) + bf2f(xl[i][j])) * bf2f(xd[i][j]);
-        sum += __shfl_xor(sum, 1, 64);
-        sum += __shfl_xor(sum, 2, 64);
-        if ((idx & 3) == 0 && r < TP) {
-          Dl[r] = -sum;
-          Ls[r] = -lv[i];
-          if (r < T) a.delta[bh * T + r] = sum;
-        }
-      }
-    }
-    // ring rows of keys [16 NB, 32 NS) are read by the dQ MFMAs but owned by no key wave: zero
-    for (int i = threadIdx.x; i < SH2_SLOTS * (32 * NS - 16 * NB) * (DH / 8); i += SH_THREADS) {
-      const int slot = i / ((32 * NS - 16 * NB) * (DH / 8)), rem = i % ((32 * NS - 16 * NB) * (DH / 8));
-      *reinterpret_cast<u32x4*>(ring + slot * SH2_SLOT + (16 * NB + rem / (DH / 8)) * DH + (rem % (DH / 8)) * 8) =
-          u32x4{0u, 0u, 0u, 0u};
-    }
-  }
-  __syncthreads();
-  PCV_SHREC(1);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c16 = lane & 15;
-  const float c2 = a.scale * LOG2E;
-  const int kt = T - 1;
-  float tq[8], tk[8], tv[8];   // this wave's partials of dQ / dK / dV[T-1]
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { tq[j] = 0.f; tk[j] = 0.f; tv[j] = 0.f; }
-  const bool haskey = wave < NB;
-  const int kb = wave, mykey = kb * 16 + c16;
-  bf16x8 kf = bf16x8{0, 0, 0, 0, 0, 0, 0, 0}, vf = kf;
-  if (haskey) { kf = row_frag<DH>(Ks, kb * 16, 0); vf = row_frag<DH>(Vs, kb * 16, 0); }
-  f32x4 dv[DT], dk[DT];
-#pragma unroll
-  for (int d = 0; d < DT; ++d) { dv[d] = kZero4; dk[d] = kZero4; }
-  const bf16* qrow = Qs + toff<DH>(c16, g);
-  const bf16* orow = Os + toff<DH>(c16, g);
-  const bf16* otr[DT] = {tr_base<DH>(Os, 0), tr_base<DH>(Os, 16)};
-  const bf16* qtr[DT] = {tr_base<DH>(Qs, 0), tr_base<DH>(Qs, 16)};
-  const float* lrow = Ls + 4 * g;
-  const float* drow = Dl + 4 * g;
-  const uint16_t* mrow = mk + drop_word(4 * g, haskey ? mykey : 0, a.n64);
-  const int mstride = 64 * a.n64;   // mask words per 16 queries
-  const f2v c2v = {c2, c2}, dsc = {DROP ? a.drop_scale : 1.f, DROP ? a.drop_scale : 1.f};
-  // this lane's two 8-B ring slots (queries 16 tt + 4 g .. +3 of key mykey), slot 0
-  bf16* rw0 = ring + toff<DH>(mykey & (SH2_KB * 16 - 1), g >> 1) + 4 * (g & 1);
-  bf16* rw1 = ring + toff<DH>(mykey & (SH2_KB * 16 - 1), 2 + (g >> 1)) + 4 * (g & 1);
-  auto kstep = [&](int st, auto interior_t) {
-    constexpr bool interior = decltype(interior_t)::value;
-    f32x4 p[2], ds[2];
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const int t = 2 * st + tt;
-      const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-          *reinterpret_cast<const bf16x8*>(qrow + 16 * DH * t), kf, kZero4, 0, 0, 0);
-      const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-          *reinterpret_cast<const bf16x8*>(orow + 16 * DH * t), vf, kZero4, 0, 0, 0);
-      uint32_t wt = 0;
-      if (DROP) wt = (uint32_t)mrow[t * mstride] >> (mykey & 3);
-      const f32x4 l4 = *reinterpret_cast<const f32x4*>(lrow + 16 * t);
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(drow + 16 * t);
-      // packed fp32 pairs and a v_bfe_i32 / v_and keep mask (see attn_short_fwd_kernel)
-      float pv[4], dm[4];
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {
-        const f2v x = __builtin_elementwise_fma((f2v){sv[2 * h2], sv[2 * h2 + 1]}, c2v,
-                                                (f2v){l4[2 * h2], l4[2 * h2 + 1]});
-        pv[2 * h2] = __builtin_amdgcn_exp2f(x.x);
-        pv[2 * h2 + 1] = __builtin_amdgcn_exp2f(x.y);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if constexpr (!interior) pv[r] = (mykey < Tm && 16 * t + 4 * g + r < Tm) ? pv[r] : 0.f;
-        p[tt][r] = pv[r];
-        dm[r] = dp[r];
-        if (DROP) {
-          int km = __builtin_amdgcn_sbfe((int)wt, 4 * r, 1);
-          asm volatile("" : "+v"(km));
-          p[tt][r] = __uint_as_float(__float_as_uint(pv[r]) & (uint32_t)km);
-          dm[r] = __uint_as_float(__float_as_uint(dp[r]) & (uint32_t)km);
-        }
-      }
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2) {   // dS = P (dP_dropped * scale - delta)
-        const f2v u = __builtin_elementwise_fma((f2v){dm[2 * h2], dm[2 * h2 + 1]}, dsc,
-                                                (f2v){d4[2 * h2], d4[2 * h2 + 1]});
-        const f2v v2 = (f2v){pv[2 * h2], pv[2 * h2 + 1]} * u;
-        ds[tt][2 * h2] = v2.x;
-        ds[tt][2 * h2 + 1] = v2.y;
-      }
-    }
-    const bf16x8 pb = pack8(p[0], p[1]), sb = pack8(ds[0], ds[1]);
-    const int so = (st & (SH2_SLOTS - 1)) * SH2_SLOT;
-    *reinterpret_cast<bf16x4*>(rw0 + so) = bf16x4{sb[0], sb[1], sb[2], sb[3]};
-    *reinterpret_cast<bf16x4*>(rw1 + so) = bf16x4{sb[4], sb[5], sb[6], sb[7]};
-#pragma unroll
-    for (int d = 0; d < DT; ++d) {
-      dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_at<DH>(otr[d], st), pb, dv[d], 0, 0, 0);
-      dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_at<DH>(qtr[d], st), sb, dk[d], 0, 0, 0);
-    }
-  };
-  // dQ of query tile j = wave (queries 16 j .. +15, lane & 15), over the MFMA keys from ring slot
-  // (j / 2) & 1 right after its step's barrier; key T - 1 (VALU, with its dK / dV[T-1] terms reduced
-  // over the 16 queries into tk / tv) and the store after the step loop, outside the lock-step
-  // region (in it, this serial tail work stalled every other wave at the next barrier)
-  f32x4 qacc[DT];
-#pragma unroll
-  for (int d = 0; d < DT; ++d) qacc[d] = kZero4;
-  auto dq_mfma = [&](int j) {
-    const bf16* rb = tr_base<DH>(ring + ((j >> 1) & (SH2_SLOTS - 1)) * SH2_SLOT, 16 * (j & 1));
-    const bf16* ktr[DT] = {tr_base<DH>(Ks, 0), tr_base<DH>(Ks, 16)};
-#pragma unroll
-    for (int st = 0; st < NS; ++st) {
-      const bf16x8 sa = tr_at<DH>(rb, st);
-#pragma unroll
-      for (int d = 0; d < DT; ++d)
-        qacc[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sa, tr_at<DH>(ktr[d], st), qacc[d], 0, 0, 0);
-    }
-  };
-  auto dq_finish = [&](int j) {
-    const int q0 = j * 16, myq = q0 + c16;
-    if (tail1) {   // key T-1 against this query tile (lane = query c16 x head-dim group g)
-      const bf16x8 qf = row_frag<DH>(Qs, q0, 0);
-      const bf16x8 of = row_frag<DH>(Os, q0, 0);
-      const float myl = Ls[myq], myd = Dl[myq];   // -lse2, -delta (staged negated)
-      const bf16x8 k8 = *reinterpret_cast<const bf16x8*>(Ks + toff<DH>(kt, g));
-      const bf16x8 v8 = *reinterpret_cast<const bf16x8*>(Vs + toff<DH>(kt, g));
-      float sv = 0.f, dpp = 0.f;
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        sv = fmaf(bf2f(qf[jj]), bf2f(k8[jj]), sv);
-        dpp = fmaf(bf2f(of[jj]), bf2f(v8[jj]), dpp);
-      }
-      sv = xsum_rows(sv);
-      dpp = xsum_rows(dpp);
-      const float pv = myq < Tm ? __builtin_amdgcn_exp2f(fmaf(sv, c2, myl)) : 0.f;
-      float pd = pv, dpv = dpp;
-      if (DROP) {
-        const bool keep = (mk[drop_word(myq, kt, a.n64)] >> ((myq & 3) * 4 + (kt & 3))) & 1u;
-        pd = keep ? pv : 0.f;
-        dpv = keep ? dpp * a.drop_scale : 0.f;
-      }
-      const float dsb = bf2f(f2bf(pv * (dpv + myd))), pdb = bf2f(f2bf(pd));
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {   // qacc[d][r] = dQ[query q0 + 4g + r][dim 16d + c16]
-        const float dr = __shfl(dsb, 4 * g + r, 64);
-#pragma unroll
-        for (int d = 0; d < DT; ++d)
-          qacc[d][r] = fmaf(dr, bf2f(Ks[toff<DH>(kt, (16 * d + c16) >> 3) + (c16 & 7)]), qacc[d][r]);
-      }
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {   // dK / dV[T-1][8g + jj] += sum over the 16 queries
-        tk[jj] += dpp_row_sum16(dsb * bf2f(qf[jj]));
-        tv[jj] += dpp_row_sum16(pdb * bf2f(of[jj]));
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int qq = q0 + 4 * g + r;
-      if (qq < Tm) {
-#pragma unroll
-        for (int d = 0; d < DT; ++d)
-          a.dq[(bT + qq) * a.lddq + h * DH + 16 * d + (lane & 15)] = f2bf(qacc[d][r] * a.scale);
-      }
-    }
-  };
-  const int nint = haskey && kb * 16 + 16 <= Tm ? Tm / 32 : 0;   // wave-uniform
-  // steps in pairs between barriers (the pair's MFMA and VALU chains interleave in one wave); the
-  // four query tiles of a pair go to waves 4p .. 4p + 3, one per SIMD
-#pragma unroll
-  for (int sp = 0; sp < NS; sp += 2) {
-    if (haskey) {
-#pragma unroll
-      for (int st = sp; st < sp + 2 && st < NS; ++st) {
-        if (st < nint) kstep(st, std::true_type{});
-        else kstep(st, std::false_type{});
-      }
-    }
-    __syncthreads();   // the pair's dS rows are in ring slots sp & 3, (sp + 1) & 3
-    if ((wave >> 2) == (sp >> 1) && wave < NB) dq_mfma(wave);
-  }
-  if (wave < NB) dq_finish(wave);
-  if (haskey) {
-    if (tail1) {   // query T-1 against this key block (lane = key c16 x head-dim group g)
-      const bf16x8 q8 = *reinterpret_cast<const bf16x8*>(Qs + toff<DH>(kt, g));
-      const bf16x8 o8 = *reinterpret_cast<const bf16x8*>(Os + toff<DH>(kt, g));
-      float sv = 0.f, dpp = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sv = fmaf(bf2f(q8[j]), bf2f(kf[j]), sv);
-        dpp = fmaf(bf2f(o8[j]), bf2f(vf[j]), dpp);
-      }
-      sv = xsum_rows(sv);
-      dpp = xsum_rows(dpp);
-      const float pv = __builtin_amdgcn_exp2f(fmaf(sv, c2, Ls[kt]));
-      float pd = pv, dpv = dpp;
-      if (DROP) {
-        const bool keep = (mk[drop_word(kt, mykey, a.n64)] >> ((kt & 3) * 4 + (mykey & 3))) & 1u;
-        pd = keep ? pv : 0.f;
-        dpv = keep ? dpp * a.drop_scale : 0.f;
-      }
-      const float dsb = bf2f(f2bf(pv * (dpv + Dl[kt]))), pdb = bf2f(f2bf(pd));   // the MFMA path's bf16 P, dS
-#pragma unroll
-      for (int d = 0; d < DT; ++d) {   // dv[d][r] / dk[d][r] = dV^T / dK^T[dim 16d + 4g + r][key c16]
-        const int dd = 16 * d + 4 * g;
-        const bf16x4 o4 = *reinterpret_cast<const bf16x4*>(Os + toff<DH>(kt, dd >> 3) + (dd & 7));
-        const bf16x4 q4 = *reinterpret_cast<const bf16x4*>(Qs + toff<DH>(kt, dd >> 3) + (dd & 7));
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          dv[d][r] = fmaf(pdb, bf2f(o4[r]), dv[d][r]);
-          dk[d][r] = fmaf(dsb, bf2f(q4[r]), dk[d][r]);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) tq[j] += dpp_row_sum16(dsb * bf2f(kf[j]));   // dQ[T-1] over the 16 keys
-    }
-    if (mykey < Tm) {
-#pragma unroll
-      for (int d = 0; d < DT; ++d)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int dd = 16 * d + 4 * g + r;
-          a.dv[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(DROP ? dv[d][r] * a.drop_scale : dv[d][r]);
-          a.dk[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(dk[d][r] * a.scale);
-        }
-    }
-  }
-  PCV_SHREC(2);
-  if (tail1) {   // row T-1: the 16 wave partials of each kind + the corner (T-1, T-1)
-    float* corner = tailp + 3 * SH_WAVES * DH;   // {dS, Pd} of (T-1, T-1), bf16-rounded
-    if (wave == 0) {
-      const int d = lane & 31;
-      const int co = toff<DH>(kt, d >> 3) + (d & 7);
-      float sv = bf2f(Qs[co]) * bf2f(Ks[co]), dpv = bf2f(Os[co]) * bf2f(Vs[co]);
-      sv = xsum16(dpp_row_sum16(sv));     // lanes 0-31 hold the same 32 terms as 32-63
-      dpv = xsum16(dpp_row_sum16(dpv));
-      const float pv = __builtin_amdgcn_exp2f(fmaf(sv, c2, Ls[kt]));
-      float pd = pv;
-      if (DROP) {
-        const bool keep = (mk[drop_word(kt, kt, a.n64)] >> ((kt & 3) * 4 + (kt & 3))) & 1u;
-        pd = keep ? pv : 0.f;
-        dpv = keep ? dpv * a.drop_scale : 0.f;
-      }
-      if (lane == 0) {
-        corner[0] = bf2f(f2bf(pv * (dpv + Dl[kt])));
-        corner[1] = bf2f(f2bf(pd));
-      }
-    }
-    if (c16 == 0) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        tailp[(0 * SH_WAVES + wave) * DH + 8 * g + j] = tq[j];
-        tailp[(1 * SH_WAVES + wave) * DH + 8 * g + j] = tk[j];
-        tailp[(2 * SH_WAVES + wave) * DH + 8 * g + j] = tv[j];
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x < 3 * DH) {
-      const int kind = threadIdx.x / DH, d = threadIdx.x - kind * DH;
-      float sum = 0.f;
-#pragma unroll
-      for (int w = 0; w < SH_WAVES; ++w) sum += tailp[(kind * SH_WAVES + w) * DH + d];
-      const float dsb = corner[0], pdb = corner[1];
-      const int col = d >> 3, el = d & 7;
-      if (kind == 0) {
-        sum = fmaf(dsb, bf2f(Ks[toff<DH>(kt, col) + el]), sum);
-        a.dq[(bT + kt) * a.lddq + h * DH + d] = f2bf(sum * a.scale);
-      } else if (kind == 1) {
-        sum = fmaf(dsb, bf2f(Qs[toff<DH>(kt, col) + el]), sum);
-        a.dk[(bT + kt) * a.lddq + h * DH + d] = f2bf(sum * a.scale);
-      } else {
-        sum = fmaf(pdb, bf2f(Os[toff<DH>(kt, col) + el]), sum);
-        a.dv[(bT + kt) * a.lddq + h * DH + d] = f2bf(DROP ? sum * a.drop_scale : sum);
-      }
-    }
-  }
-  PCV_SHREC(3);
-}
 
 static bool short_ok(const AttnArgs& a, int dh, int causal, bool) {
-  return dh == SH_DH && !causal && a.T >= 1 && a.T <= SH_TMAX && a.dstart == nullptr &&
-         getenv("PCV_ATTN_NO_SHORT") == nullptr;
+  return dh == SH_DH && !causal && a.T >= 1 && a.T <= SH_TMAX && a.dstart == nullptr;
 }
 template <int NT, bool D>
 static int launch_short_fwd_nt(const AttnArgs& a, hipStream_t s) {
@@ -1967,32 +1615,11 @@ static int launch_short_fwd(const AttnArgs& a, hipStream_t s) {
     default: return launch_short_fwd_nt<20, D>(a, s);
   }
 }
-template <int NS, bool D>
-static int launch_short_bwd2(const AttnArgs& a, hipStream_t s) {
-  static PcvLdsOptIn optin;
-  if (const int e = optin.ensure((const void*)attn_short_bwd2_kernel<NS, D>, (int)SH_BWD2_LDS)) return e;
-  hipLaunchKernelGGL((attn_short_bwd2_kernel<NS, D>), dim3(a.H, a.B), dim3(SH_THREADS), SH_BWD2_LDS, s, a);
-  return 0;
-}
 template <bool D>
 static int launch_short_bwd(const AttnArgs& a, hipStream_t s) {
-  // the key-owned form is opt-in: measured slower at T = 257 (main phase 20 vs 18 us; the per-pair
-  // barriers leave the waves in lock step, so the MFMA and VALU phases of different waves stop
-  // overlapping -- wait cycles +18 % -- which outweighs its 27 % fewer VALU instructions)
-  const bool key_owned = getenv("PCV_ATTN_BWD_KEY_OWNED") != nullptr;
-  const int tm = ((a.T & 15) == 1 && a.T > 16) ? a.T - 1 : a.T;
-  if (tm <= SH2_KB * 16 && key_owned) {
-    switch ((tm + 31) / 32) {
-      case 1: return launch_short_bwd2<1, D>(a, s);
-      case 2: return launch_short_bwd2<2, D>(a, s);
-      case 3: return launch_short_bwd2<3, D>(a, s);
-      case 4: return launch_short_bwd2<4, D>(a, s);
-      case 5: return launch_short_bwd2<5, D>(a, s);
-      case 6: return launch_short_bwd2<6, D>(a, s);
-      case 7: return launch_short_bwd2<7, D>(a, s);
-      default: return launch_short_bwd2<8, D>(a, s);
-    }
-  }
+  // (a key-owned form -- every wave one key block, P and dS computed once and handed to the dQ owners
+  // through an LDS ring -- measured slower at T = 257: its barriers keep the 16 waves in lock step,
+  // DESIGN.md; removed in round 5)
   static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
   if (const int e = optin.ensure((const void*)attn_short_bwd_kernel<D>, (int)((int)SH_BWD_LDS))) return e;
   hipLaunchKernelGGL((attn_short_bwd_kernel<D>), dim3(a.H, a.B), dim3(SH_THREADS), SH_BWD_LDS, s, a);
@@ -2020,9 +1647,8 @@ static int dispatch(AttnArgs a, int dh, int causal, int drop, hipStream_t s) {
   if ((a.out_lo || a.o_lo) && !short_ok(a, dh, causal, FWD)) return PCV_EINVAL;   // short path only
   if (a.o_lo && a.delta_ready) return PCV_EINVAL;                                 // delta is formed here
   if (short_ok(a, dh, causal, FWD)) {
-    // batch b's heads on the XCD that wrote its rows (C2: step 0.778 -> 0.768 ms); PCV_ATTN_XCD=0: off
-    const char* xe = getenv("PCV_ATTN_XCD");
-    a.xcd_map = (a.B % 8 == 0 && !(xe && xe[0] == '0')) ? 1 : 0;
+    // batch b's heads on the XCD that wrote its rows (C2: step 0.778 -> 0.768 ms)
+    a.xcd_map = a.B % 8 == 0 ? 1 : 0;
     const int e = FWD ? (drop ? launch_short_fwd<true>(a, s) : launch_short_fwd<false>(a, s))
                       : (drop ? launch_short_bwd<true>(a, s) : launch_short_bwd<false>(a, s));
     return e ? e : pcv_launch_status();

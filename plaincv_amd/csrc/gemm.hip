@@ -1235,17 +1235,9 @@ static hipError_t launch_sz(const GemmArgs& a, int ta, int tb, int batch, hipStr
   return launch_t<false, true, WM, WN>(a, batch, s);
 }
 
-#include "rowgemm.inc"
-
 }  // namespace pcv
 
 using namespace pcv;
-
-extern "C" int pcv_rowgemm_enable(int on) {
-  const int old = rp_on() ? 1 : 0;
-  if (on >= 0) g_rp_enabled = on ? 1 : 0;
-  return old;
-}
 
 extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
                              int64_t M, int64_t N, int64_t K,
@@ -1324,20 +1316,14 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
   if (trans_a && !trans_b && out_f32 && beta == 1.f && batch == 1 && !bias && !res && !aux && act == EPI_NONE &&
       g.drop_thresh == 0 && !colsum && !attn_delta && pcv_aligned16(C) && pcv_gemm_big_wgrad_ok(M, N, K, A, lda, B, ldb))
     return pcv_gemm_big_wgrad(A, B, (float*)C, M, N, K, lda, ldb, ldc, alpha, stream);
-  // skinny token-row products (the ViT's): one row panel per CU across the whole width (rowgemm.inc)
-  if (rp_eligible(g, trans_a, (int)batch, 0)) {
-    const hipError_t e = rp_launch(g, trans_b, s);
-    return e == hipSuccess ? 0 : (int)e;
-  }
   // tile: 128x128 when that grid covers the chip and K is deep, else 64x64.  (A 256x256 tile with
   // one 128x128 block per wave was measured 15-45 % slower at the LM shapes: it needs
   // all 512 registers, spills, and runs one wave per SIMD.)
   const int64_t t128 = ((M + 127) / 128) * ((N + 127) / 128) * batch * g.split_k;
-  static const int tile_env = getenv("PCV_GEMM_TILE") ? atoi(getenv("PCV_GEMM_TILE")) : 0;   // 64 / 128: A/B runs
   // 128x128 only for deep products: at K <= 384 (every ViT GEMM) a 128x128 tile is 2-6 k-tiles of
   // prologue/epilogue-bound work at 2 workgroups per CU; the 64x64 tile runs 4 per CU (ViT C2 step
   // 0.899 -> 0.863 ms with every GEMM on 64x64)
-  const bool big_tile = tile_env ? tile_env == 128 : (t128 >= 240 && K >= 512);
+  const bool big_tile = t128 >= 240 && K >= 512;
   hipError_t e = big_tile ? launch_sz<4, 4>(g, trans_a, trans_b, (int)batch, s)
                           : launch_sz<2, 2>(g, trans_a, trans_b, (int)batch, s);
   return e == hipSuccess ? 0 : (int)e;
@@ -1385,17 +1371,9 @@ extern "C" int pcv_gemm_ln(const void* A, const void* B, float* C, int64_t M, in
   g.ln_y = (bf16*)ln_y; g.ld_lny = ld_lny; g.ln_mean = ln_mean; g.ln_rstd = ln_rstd;
   g.ln_x = ln_x; g.ld_lnx = ld_lnx; g.ln_dscale = ln_dscale; g.ln_dbias = ln_dbias; g.colsum = colsum;
   g.col_reps = col_reps;
-  // 64 x 128 tiles (a 32-row tile doubles every workgroup's weight traffic: measured slower)
-  // PCV_LN_TILE=32: 32x128 tiles (514 workgroups at the ViT's 16448 rows instead of 257).  Measured:
-  // ViT C2 step 0.858 -> 0.852 ms, but each launch alone 16.9 -> 21.7 us back to back (the per-column
-  // LN-parameter atomics double), so the 64x128 tile stays the default.
-  static const int ln32 = getenv("PCV_LN_TILE") ? atoi(getenv("PCV_LN_TILE")) == 32 : 0;
-  if (!ln32 && rp_eligible(g, trans_a, 1, ln_mode)) {
-    const hipError_t e = rp_launch(g, trans_b, (hipStream_t)stream);
-    return e == hipSuccess ? 0 : (int)e;
-  }
-  hipError_t e = ln32 ? launch_sz<1, 4>(g, trans_a, trans_b, 1, (hipStream_t)stream)
-                      : launch_sz<2, 4>(g, trans_a, trans_b, 1, (hipStream_t)stream);
+  // 64 x 128 tiles (32-row tiles, 514 workgroups at the ViT's 16448 rows: each launch alone 16.9 ->
+  // 21.7 us; a one-panel-per-CU row form: C2 0.858 vs 0.806 ms -- both measured and dropped)
+  const hipError_t e = launch_sz<2, 4>(g, trans_a, trans_b, 1, (hipStream_t)stream);
   return e == hipSuccess ? 0 : (int)e;
 }
 

@@ -534,8 +534,7 @@ extern "C" int pcv_gemm_big_wgrad(const void* A, const void* B, float* C, int64_
   g.M = (int)M; g.N = (int)N; g.K = (int)K; g.alpha = alpha;
   g.tiles_m = (int)((M + GB_T - 1) / GB_T);
   g.tiles_n = (int)((N + GB_T - 1) / GB_T);
-  static const int forced = getenv("PCV_WGRAD_SPLITS") ? atoi(getenv("PCV_WGRAD_SPLITS")) : 0;
-  const int s = forced > 0 ? forced : wgrad_splits((int64_t)g.tiles_m * g.tiles_n, K);
+  const int s = wgrad_splits((int64_t)g.tiles_m * g.tiles_n, K);
   g.kps = (int)(((K + s - 1) / s + 31) / 32 * 32);
   const int nsplit = (int)((K + g.kps - 1) / g.kps);
   static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device

@@ -428,18 +428,12 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
   // CU (the N = 128 / 256 products: with one or two per CU the load / epilogue latency is exposed;
   // C4 step 2.185 -> 2.125 ms moving the N = 256 products to 64-wide panels)
   const int64_t mt = (M + GR_BM - 1) / GR_BM;
-  static const int64_t narrow_below = [] {   // PCV_F32_NARROW_BELOW: A/B override (1024: swept 512-2048)
-    const char* e = getenv("PCV_F32_NARROW_BELOW");
-    return e ? (int64_t)atoll(e) : (int64_t)1024;
-  }();
+  constexpr int64_t narrow_below = 1024;   // (swept 512-2048)
   const bool narrow = mt * (N / 128) < narrow_below;
   // 32 x 64 tiles when the 64-wide grid has fewer than 2048 workgroups (the ViT's N = 128 / 256 /
   // 384 products: 2 -> 4+ waves per SIMD; C4 step 1.972 -> 1.934 (N = 128 only) -> 1.900 ms (all;
   // thresholds 1024 / 1100 / 2048 / 4096 swept))
-  static const int64_t short_below = [] {   // PCV_F32_SHORT_BELOW: A/B override
-    const char* e = getenv("PCV_F32_SHORT_BELOW");
-    return e ? (int64_t)atoll(e) : (int64_t)2048;
-  }();
+  constexpr int64_t short_below = 2048;
   const bool shrt = narrow && mt * (N / 64) < short_below;
   g.tiles_n = (int)(N / (narrow ? 64 : 128));
   const unsigned blocks = (unsigned)((shrt ? (M + 31) / 32 : mt) * g.tiles_n);

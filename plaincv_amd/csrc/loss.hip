@@ -353,7 +353,7 @@ extern "C" int pcv_xent_fwd_bwd(const void* logits, int64_t ld, int logits_f32, 
   const size_t es = logits_f32 ? 4 : 2;
   const bool aligned = pcv_aligned16(logits) && ((ld * es) % 16 == 0) &&
                        (!dlogits || (pcv_aligned16(dlogits) && (ldd * es) % 16 == 0));
-  if (V >= 4096 && V <= 8 * 1024 * XR_CH && aligned && !logits_f32 && getenv("PCV_XENT_STREAM") == nullptr) {
+  if (V >= 4096 && V <= 8 * 1024 * XR_CH && aligned && !logits_f32) {
     hipLaunchKernelGGL(xent_reg_kernel, dim3((unsigned)R), dim3(1024), 0, s, (const bf16*)logits, ld, labels, (int)V,
                        row_loss, row_correct, (bf16*)dlogits, ldd, grad_scale);
     return pcv_launch_status();

@@ -1196,11 +1196,9 @@ static int fa_fwd_launch(const FaArgs& a, int B, hipStream_t s) {
 }
 template <bool D>
 static int fa_bwd_launch(const FaArgs& a, int B, hipStream_t s) {
-  // the score-sharing form whenever its 16 waves cover the key blocks (PCV_F32_ATTN_BWD=two keeps
-  // the two-family form for A/B measurements)
-  static const bool two = [] { const char* e = getenv("PCV_F32_ATTN_BWD"); return e && !strcmp(e, "two"); }();
+  // the score-sharing form whenever its 16 waves cover the key blocks, the two-family form past that
   const int NB = (a.T + 15) / 16, NQ = ((a.T & 15) == 1 && NB > 1) ? NB - 1 : NB;
-  if (!two && NQ <= FA_WAVES) {
+  if (NQ <= FA_WAVES) {
     static PcvLdsOptIn optk;
     if (const int e = optk.ensure((const void*)attn_bwd_f32_kshare_kernel<D>, (int)FK_BWD_LDS)) return e;
     hipLaunchKernelGGL((attn_bwd_f32_kshare_kernel<D>), dim3(a.H, B), dim3(FA_THREADS), FK_BWD_LDS, s, a);

@@ -119,7 +119,6 @@ SIGNATURES = {
     "pcv_muon_mat_size": [],
     "pcv_chunk_size": [],
     "pcv_gemm_big_enable": [I32],
-    "pcv_rowgemm_enable": [I32],
     "pcv_gemm_big_ok": [I64, I64, I64, P, I64, P, I64],
     "pcv_gemm_big": [P, P, P, I64, I64, I64, I64, I64, I64, F32, P, I64, F32, P],
     "pcv_gemm_big_wgrad_ok": [I64, I64, I64, P, I64, P, I64],

@@ -117,12 +117,10 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
 
 def col_rows(M, col_reps):
     """Rows of a column-accumulator buffer: col_reps replicas (atomics), or with col_reps = -1 one row
-    per output row tile of M rows (plain stores): 64-row tiles (the GEMM and LayerNorm-epilogue
-    tiles), 32 under PCV_LN_TILE=32."""
-    import os
+    per 64-row output tile of M rows (plain stores; the GEMM and LayerNorm-epilogue tiles)."""
     if col_reps >= 0:
         return max(1, int(col_reps))
-    return -(-int(M) // (32 if os.environ.get("PCV_LN_TILE", "64") == "32" else 64))
+    return -(-int(M) // 64)
 
 
 def gemm_ln(a, b, out, *, ln_mode, res, ln_scale, ln_y, ln_mean, ln_rstd, ta=False, tb=False, alpha=1.0, bias=None,
@@ -164,23 +162,21 @@ class GroupedWGrad:
     column-sum items ("colsum", X [R,N] bf16|fp32, out fp32 [N]): out += X.sum(0);
     ("fold", X fp32 [reps,N], out): the same, then X = 0 (replicated column accumulators).
     split_k None picks a GEMM split so the GEMM jobs hold ~target_blocks workgroups; column sums
-    take ~colsum_rows rows per workgroup.  tile: 64 or 128 (env PCV_WGRAD_TILE overrides).
-    deterministic (default; PCV_WGRAD_ATOMIC=1 turns it off): split-K partial tiles go to a
-    workspace with plain stores and a second launch (pcv_gemm_grouped_fold) adds them to C in
-    slice order -- run-to-run identical gradients, and no contended float atomics (which cost as
-    much as the GEMM's main loop per workgroup at ViT C2: 12.5 vs 13.8 us, PCV_GEMM_TIMING)."""
+    take ~colsum_rows rows per workgroup.  tile: 64 or 128.
+    Deterministic: split-K partial tiles -- and the row slices of a column sum -- go to a workspace
+    with plain stores and a second launch (pcv_gemm_grouped_fold) adds them in slice order: run-to-run
+    identical gradients, and no contended float atomics (which cost as much as the GEMM's main loop
+    per workgroup at ViT C2: 12.5 vs 13.8 us, phase stamps)."""
 
-    def __init__(self, items, device, split_k=None, target_blocks=None, tile=None, colsum_rows=512,
-                 deterministic=None):
-        import os
+    def __init__(self, items, device, split_k=None, target_blocks=None, tile=None, colsum_rows=512):
         import ctypes
         import numpy as np
         lib = hip.load()
         _chk(lib.pcv_gemm_desc_size() == 96, "gemm desc size")
-        tile = int(os.environ.get("PCV_WGRAD_TILE", tile or 64))
+        tile = int(tile or 64)
         if target_blocks is None:
             # 2048 64x64 blocks: ViT C2 step 0.860 -> 0.855 ms vs 1024 (1024-6144 swept; 128x128 tiles slower)
-            target_blocks = int(os.environ.get("PCV_WGRAD_BLOCKS", 2048 if tile == 64 else 512))
+            target_blocks = 2048 if tile == 64 else 512
         self.tile = tile
         gemms = [it for it in items if not isinstance(it[0], str)]
         tiles = sum(math.ceil(a.shape[1] / tile) * math.ceil(b.shape[1] / tile) for a, b, _, _ in gemms)
@@ -218,9 +214,7 @@ class GroupedWGrad:
         self.n = len(items)
         self.plan = torch.empty(lib.pcv_gemm_grouped_plan_size(self.n), dtype=torch.uint8, device=device)
         buf = ctypes.create_string_buffer(bytes(raw), len(raw))
-        if deterministic is None:
-            deterministic = os.environ.get("PCV_WGRAD_ATOMIC", "0") != "1"
-        nws = lib.pcv_gemm_grouped_ws_floats(ctypes.addressof(buf), self.n, self.tile) if deterministic else 0
+        nws = lib.pcv_gemm_grouped_ws_floats(ctypes.addressof(buf), self.n, self.tile)
         _chk(nws >= 0, "grouped wgrad descriptors")
         self.ws = torch.empty(max(1, nws), dtype=F32, device=device) if nws > 0 else None
         total, fold = ctypes.c_int64(0), ctypes.c_int64(0)

@@ -13,7 +13,6 @@ Supported: LayerNorm, BatchNorm (use_batchnorm: flax BatchNorm with the mutable 
 averages, statistics over all B*T token rows, vit_small.py:35-36,49-50,121-122) or no norm.
 """
 import math
-import os
 
 import torch
 
@@ -92,7 +91,9 @@ class _Dense:
 class ViTRunnerF32:
     """Fixed-shape fp32 forward/backward executor (graph-capturable, no allocation after init)."""
 
-    def __init__(self, model, store, image_shape, device, batch_stats=None):
+    def __init__(self, model, store, image_shape, device, batch_stats=None, fused_attn=True):
+        """fused_attn False: the per-(batch, head) GEMM path around a materialised softmax (also taken
+        for shapes the fused kernels do not cover) -- the tests compare the two."""
         self.bn = bool(model.use_batchnorm)
         if self.bn and batch_stats is None:
             raise ValueError("the BatchNorm ViT needs its batch_stats (TrainState.batch_stats)")
@@ -120,8 +121,7 @@ class ViTRunnerF32:
         self.st0 = [(z(R), z(R)) for _ in range(L)]
         self.st1 = [(z(R), z(R)) for _ in range(L)]
         self.qkv = [z(R, 3 * D) for _ in range(L)]
-        self.fused_attn = (bool(hip.load().pcv_attn_fused_f32_ok(T, self.Dh))
-                           and os.environ.get("PCV_F32_FUSED_ATTN", "1") != "0")
+        self.fused_attn = bool(hip.load().pcv_attn_fused_f32_ok(T, self.Dh)) and fused_attn
         if self.fused_attn:   # per-query softmax row max and 1/sum, read back by the backward
             self.mrow = [z(BH * T) for _ in range(L)]
             self.linv = [z(BH * T) for _ in range(L)]
@@ -269,7 +269,7 @@ class ViTRunnerF32:
         self.colsum_ws = torch.zeros(max(K.colsum_ws_floats(B * T, max(3 * D, self.M, self.Kc)),
                                          K.colsum_ws_floats(B * self.hw, D), 1), dtype=torch.float32, device=dev)
         for a, b, c, gb in prods:
-            if WgradF32.fits(a, b, c) and os.environ.get("PCV_F32_WGRAD_ROWS", "1") != "0":
+            if WgradF32.fits(a, b, c):
                 fold = gb.is_contiguous() and gb.numel() == b.shape[1]
                 wr.add(a, b, c, colsum=gb if fold else None)
                 if fold:
@@ -282,7 +282,7 @@ class ViTRunnerF32:
         # at the end of backward adds them all (instead of a small reduction launch per LayerNorm)
         self.ln_red = None
         xcls, dxc = self.xs[-1].view(B, T * D)[:, :D], self.dx.view(B, T * D)[:, :D]
-        if self.m.use_layernorm and os.environ.get("PCV_F32_LN_DEFER", "1") != "0" and \
+        if self.m.use_layernorm and \
                 K.layernorm_bwd_f32_fits(D, self.dyf, xcls, None, dxc) and \
                 K.layernorm_bwd_f32_fits(D, self.dy1, self.x1s[0], self.dx, self.dx1):
             red = K.LayerNormParamReduce().add(self.ln_ws[0], B, D, self.gsf, self.gcf)

@@ -13,7 +13,6 @@ LayerNorm / BatchNorm statistics, softmax and every gradient reduction stay fp32
 """
 import contextlib
 import math
-import os
 
 import torch
 
@@ -257,28 +256,18 @@ class ViTRunner:
         self.dx = torch.zeros(R, D, dtype=f32, device=dev)
         self.dym = [e(R, D, dt=bf) for _ in range(Lc)]
         # the final LayerNorm, head, CE and the head's whole backward in one workgroup (csrc/vit_head.hip)
-        self.fused_head = (bool(model.use_layernorm) and not self.bn and K.vit_head_ok(B, D, self.Kc) and
-                           os.environ.get("PCV_VIT_FUSED_HEAD", "1") != "0")
+        self.fused_head = bool(model.use_layernorm) and not self.bn and K.vit_head_ok(B, D, self.Kc)
         if self.fused_head:   # only the cls rows of the top block's dropout-VJP operand are ever written
             self.dym[Lc - 1] = torch.zeros(R, D, dtype=bf, device=dev)
-            # one workgroup per 16 rows (PCV_VIT_HEAD_SPLIT=0: the single-workgroup form)
-            self.head_work = (K.vit_head_work(B, D, self.Kc, dev)
-                              if os.environ.get("PCV_VIT_HEAD_SPLIT", "1") != "0" else None)
+            # one workgroup per 16 rows (the single-workgroup form: 28.8 -> 19.4 us)
+            self.head_work = K.vit_head_work(B, D, self.Kc, dev)
         self.dh = [e(R, M, dt=bf) for _ in range(Lc)]
         # LayerNorm fused into the residual-stream GEMM epilogues (pcv_gemm_ln) when rows fit one tile
         self.fuse_ln = bool(model.use_layernorm) and D <= 128 and D % 8 == 0
-        # the short attention's delta formed by the dO GEMM's epilogue (PCV_VIT_DELTA_GEMM=0: in the
-        # attention backward's prologue)
-        self.delta_in_gemm = os.environ.get("PCV_VIT_DELTA_GEMM", "1") != "0"
-        # the patch embedding and the first LayerNorm_0 in one launch (PCV_VIT_EMBED_LN=0: two)
-        self.embed_ln = os.environ.get("PCV_VIT_EMBED_LN", "1") != "0"
-        # PCV_VIT_GELU_D=1: self.h holds bf16(gelu'(pre-activation)) instead of bf16(pre-activation), so
-        # the fc2 dgrad epilogue multiplies instead of evaluating gelu' (C2 -4 us, 0.768 vs 0.772 ms).
-        # Off by default: it moves a rounding point (gelu' at the fp32 pre-activation, then rounded)
-        # that the golden trajectory's rounding model does not include, and the block-0 LayerNorm_0
-        # bias -- a near-zero-gradient leaf whose first Adam steps amplify rounding -- then leaves
-        # that model's spread (0.132 vs 0.008, test_golden.py::test_hip_vit_golden_muon3)
-        self.gelu_d = os.environ.get("PCV_VIT_GELU_D", "0") == "1"
+        # the short attention's delta is formed by the dO GEMM's epilogue; the patch embedding and the
+        # first LayerNorm_0 run as one launch
+        self.delta_in_gemm = True
+        self.embed_ln = True
         self.dy_m = [e(R, D) for _ in range(Lc)] if not self.fuse_ln else None
         self.dx_mid = [e(R, D) for _ in range(Lc)]
         self.dxb_mid = [e(R, D, dt=bf) for _ in range(Lc)]
@@ -308,7 +297,6 @@ class ViTRunner:
         # alone is a few dozen 64x64 output tiles over K = B*T rows, a latency-bound partial
         # wave; all of them together fill the chip (csrc/gemm.hip gemm_grouped_kernel).
         self.wgrad = None
-        self.wgrad_early = None
         self.rep_ws, self.reps = {}, 1
         if grouped_wgrad and self.side is None and dev.type == "cuda":
             items = [(self.yf, self.dlogits_b, self.gWh, 1.0), (self.patches, self.dpatch, self.gWconv, 1.0)]
@@ -328,15 +316,14 @@ class ViTRunner:
             # Column accumulators written by every row tile of a GEMM epilogue (bias and LayerNorm
             # parameter gradients): each row tile stores its partial to its own row (col_reps = -1,
             # plain stores: no contended atomics, deterministic) and a column-sum job of the same
-            # grouped launch adds the rows into the gradient.  PCV_COL_REPS=n > 0: the previous form
-            # (atomics into n replica rows, folded and zeroed by the launch).
-            self.reps = int(os.environ.get("PCV_COL_REPS", "-1"))
+            # grouped launch adds the rows into the gradient.
+            self.reps = -1
             rows = K.col_rows(R, self.reps)
 
             def replicate(key, target):
                 ws = torch.zeros(rows, target.numel(), dtype=f32, device=dev)
                 self.rep_ws[key] = ws
-                items.append(("colsum" if self.reps < 0 else "fold", ws, target.view(-1)))
+                items.append(("colsum", ws, target.view(-1)))
 
             for i, w in enumerate(self.w):
                 replicate(("gb0", i), w["gb0"])
@@ -349,25 +336,11 @@ class ViTRunner:
             # gradients) fold in this launch instead of a last-workgroup reduction inside the head
             # (its agent-scope fence and cross-XCD reads cost ~7.5 us at the end of the head)
             self.head_defer = (self.fused_head and self.head_work is not None and B > 16 and self.Kc % 8 == 0
-                               and D % 8 == 0 and os.environ.get("PCV_VIT_HEAD_DEFER", "1") != "0")
+                               and D % 8 == 0)
             if self.head_defer:
                 v = K.vit_head_fold_views(self.head_work, B, D, self.Kc)
                 items += [("fold", v["metrics"], self.metrics), ("fold", v["dhead_bias"], self.gbh),
                           ("fold", v["dscale"], self.gsf), ("fold", v["dbias"], self.gcf)]
-            # PCV_WGRAD_SPLIT=1: the head's and the upper half of the blocks' weight gradients run as a
-            # grouped launch of their own on a side stream, forked once their dY exist (after block
-            # L/2's backward) and joined after the final grouped launch, beside the lower blocks'
-            # data-gradient chain
-            self.wgrad_early, self.wside = None, None
-            if os.environ.get("PCV_WGRAD_SPLIT", "0") == "1" and model.num_layers >= 2:
-                half = model.num_layers // 2
-                early_keys = {id(self.gWh)} | {id(w[k]) for i, w in enumerate(self.w) if i >= half
-                                               for k in ("gW1", "gW0", "gWo", "gWqkv")}
-                early = [it for it in items if not isinstance(it[0], str) and id(it[2]) in early_keys]
-                items = [it for it in items if isinstance(it[0], str) or id(it[2]) not in early_keys]
-                self.wgrad_early = K.GroupedWGrad(early, dev)
-                self.wside = torch.cuda.Stream(device=dev)
-                self.wsplit_at = half
             self.wgrad = K.GroupedWGrad(items, dev)
 
     # ------------------------------------------------------------ views
@@ -489,7 +462,7 @@ class ViTRunner:
             if join is not None:
                 join(i)
             K.gemm(self.y1[i], w["W0"], self.a[i], bias=w["b0"], aux=self.h[i],
-                   act=K.EPI_GELU_D if self.gelu_d else K.EPI_GELU,
+                   act=K.EPI_GELU,
                    drop_rate=rate, seed=seed, site=site_mlp_hidden(i))
             if self.fuse_ln and i + 1 < L:   # MLP out + dropout + residual + next block's LayerNorm_0
                 wn = self.w[i + 1]
@@ -564,10 +537,6 @@ class ViTRunner:
                     K.colsum(dym, w["gb1"])
             self._block_backward(i, dx_in, rate, seed)
             dx_in = self.dx_out[i]
-            if self.wgrad_early is not None and i == self.wsplit_at:
-                self.wside.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(self.wside):
-                    self.wgrad_early()
         K.vit_embed_bwd(dx_in, self.dpatch, self.gcls, self.gpos, B, T, D, rate, seed, SITE_EMBED)
         with self._fork():
             if self.wgrad is None:
@@ -576,8 +545,6 @@ class ViTRunner:
                 K.gemm(self.patches, self.dpatch, self.gWconv, ta=True, beta=1.0)
         if self.wgrad is not None:
             self.wgrad()
-        if self.wgrad_early is not None:
-            torch.cuda.current_stream().wait_stream(self.wside)
         if self.side is not None:
             torch.cuda.current_stream().wait_stream(self.side)
 
@@ -612,7 +579,7 @@ class ViTRunner:
             if self.wgrad is None:
                 K.gemm(self.a[i], dym, w["gW1"], ta=True, beta=1.0)
         gb0, reps = self._acc(("gb0", i), w["gb0"])
-        K.gemm(dym, w["W1"], dh, tb=True, aux=self.h[i], act=K.EPI_MUL_AUX if self.gelu_d else K.EPI_GELU_BWD,
+        K.gemm(dym, w["W1"], dh, tb=True, aux=self.h[i], act=K.EPI_GELU_BWD,
                drop_rate=rate,
                seed=seed, site=site_mlp_hidden(i), colsum=gb0 if self.side is None else None, col_reps=reps)
         with self._fork():

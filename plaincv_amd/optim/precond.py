@@ -5,7 +5,6 @@ device tensor, so a step is a fixed sequence of stream-ordered launches with no 
 beyond the launch itself.  Shapes are validated here, before anything reaches a kernel.
 """
 import ctypes
-import os
 import struct
 
 import torch
@@ -410,7 +409,7 @@ class HouseholderQR:
     Small batches (every n <= 128) run the one-workgroup-per-matrix kernel; larger ones the blocked
     form (csrc/qr_blocked.hip): an nb-column panel factorised in LDS per matrix, then the trailing
     update and the backward Q accumulation as grouped fp32 MFMA GEMMs over all matrices.
-    ``blocked`` forces either path (PCV_QR_BLOCKED=0/1 likewise)."""
+    ``blocked`` forces either path."""
 
     FMT = "<5Q3q"
     FMT_B = "<7Q3q"
@@ -418,8 +417,7 @@ class HouseholderQR:
     def __init__(self, device, blocked=None):
         self.device = torch.device(device)
         self.items = []
-        env = os.environ.get("PCV_QR_BLOCKED")
-        self.blocked_req = blocked if blocked is not None else (None if env is None else env != "0")
+        self.blocked_req = blocked
 
     def add(self, a, q, perm=None):
         n = a.shape[0]

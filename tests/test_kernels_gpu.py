@@ -89,12 +89,23 @@ def test_attention_fwd_bwd(dev, B, T, H, Dh, causal, rate):
                                                      (2, 64, 4, 0.1, True), (4, 257, 4, 0.0, True),
                                                      (3, 50, 4, 0.1, False), (2, 256, 4, 0.1, False),
                                                      (2, 33, 2, 0.1, False), (2, 241, 4, 0.0, False)])
-def test_attention_short_path(dev, B, T, H, rate, delta_ready, monkeypatch):
-    """One-workgroup-per-(batch, head) kernels for Dh = 32, T <= 320, non-causal (the ViT):
-    against the fp32 reference, and against the tiled kernels (PCV_ATTN_NO_SHORT) on the same inputs;
-    the opt-in key-owned backward (PCV_ATTN_BWD_KEY_OWNED, T - tail <= 256) against the default
-    two-pass one, and the default against itself (bit-identical reruns).
-    T = 16 n + 1 (257, 33, 17): the single tail key / query row is handled outside the MFMA blocks."""
+def test_attention_short_path(dev, B, T, H, rate, delta_ready):
+    """One-workgroup-per-(batch, head) kernels for Dh = 32, T <= 320, non-causal (the ViT): against
+    the fp32 reference, and against themselves (bit-identical reruns: dQ is summed in a fixed order).
+    T = 16 n + 1 (257, 33, 17): the single tail key / query row is handled outside the MFMA blocks.
+    B = 64 (the benchmarked batch, XCD placement of the (b, h) workgroups on) is
+    test_attention_short_path_c2_batch."""
+    _short_path_case(dev, B, T, H, rate, delta_ready)
+
+
+@pytest.mark.parametrize("rate", [0.0, 0.1])
+def test_attention_short_path_c2_batch(dev, rate):
+    """The benchmarked shape: B 64, T 257, 4 heads of 32 -- B % 8 == 0, so the (batch, head) workgroups
+    are placed on the XCD whose L2 holds batch b's rows."""
+    _short_path_case(dev, 64, 257, 4, rate, False)
+
+
+def _short_path_case(dev, B, T, H, rate, delta_ready):
     from oracle import rng
     from plaincv_amd import kernels as K
     Dh = 32
@@ -107,15 +118,8 @@ def test_attention_short_path(dev, B, T, H, rate, delta_ready, monkeypatch):
     if rate > 0:
         mask = torch.zeros(K.attn_mask_words(T), dtype=torch.int16, device=dev)
         K.attn_drop_mask(seed, 5, T, rate, mask)
-    res = {}
-    for short in (True, False, "key_owned", "again"):
-        monkeypatch.delenv("PCV_ATTN_BWD_KEY_OWNED", raising=False)
-        if short is False:
-            monkeypatch.setenv("PCV_ATTN_NO_SHORT", "1")
-        else:
-            monkeypatch.delenv("PCV_ATTN_NO_SHORT", raising=False)
-            if short == "key_owned":
-                monkeypatch.setenv("PCV_ATTN_BWD_KEY_OWNED", "1")
+    res = []
+    for _ in range(2):
         out = torch.empty(B * T, D, device=dev, dtype=torch.bfloat16)
         lse = torch.empty(B * H * T, device=dev)
         K.attn_fwd(qkv, out, lse, B, T, H, Dh, False, drop_rate=rate, mask=mask)
@@ -127,29 +131,17 @@ def test_attention_short_path(dev, B, T, H, rate, delta_ready, monkeypatch):
         K.attn_bwd(qkv, out, do, lse, delta, dqkv, B, T, H, Dh, False, drop_rate=rate, mask=mask,
                    delta_ready=delta_ready)
         torch.cuda.synchronize()
-        res[short] = (out.float(), lse.clone(), dqkv.float(), delta.clone())
-    monkeypatch.delenv("PCV_ATTN_NO_SHORT", raising=False)
-    monkeypatch.delenv("PCV_ATTN_BWD_KEY_OWNED", raising=False)
-    # both short backward forms sum dQ in a fixed order (no atomics): run to run bit-identical
-    assert torch.equal(res[True][2], res["again"][2])
+        res.append((out.float(), lse.clone(), dqkv.float(), delta.clone()))
+    for x, y in zip(res[0], res[1]):
+        assert torch.equal(x, y)
     keep = torch.from_numpy(rng.keep_mask(99, 5, (T, T), rate)).to(dev) if rate > 0 else None
     qf = qkv.float().requires_grad_(True)
     ref = _attn_ref(qf, B, T, H, Dh, False, keep, rate)
     ref.backward(do.float())
-    for short in (True, False, "key_owned"):
-        out, lse, dqkv, delta = res[short]
-        assert (out - ref).abs().max().item() < 2e-2
-        err, scale = (dqkv - qf.grad).abs().max().item(), qf.grad.abs().max().item()
-        assert err < 3e-2 * max(1.0, scale), (short, err, scale)
-    a, b = res[True], res[False]
-    assert (a[0] - b[0]).abs().max().item() <= 1e-2
-    assert (a[1] - b[1]).abs().max().item() <= 1e-4
-    assert (a[2] - b[2]).abs().max().item() <= 2e-2 * max(1.0, b[2].abs().max().item())
-    assert (a[3] - b[3]).abs().max().item() <= 1e-2 * max(1.0, b[3].abs().max().item())   # from each path's bf16 O
-    # key-owned (opt-in, T - tail <= 256) vs two-pass short backward: the same P / dS up to the MFMA
-    # orientation of the scores
-    c = res["key_owned"]
-    assert (a[2] - c[2]).abs().max().item() <= 2e-2 * max(1.0, c[2].abs().max().item())
+    out, lse, dqkv, delta = res[0]
+    assert (out - ref).abs().max().item() < 2e-2
+    err, scale = (dqkv - qf.grad).abs().max().item(), qf.grad.abs().max().item()
+    assert err < 3e-2 * max(1.0, scale), (err, scale)
 
 
 def test_layernorm_rmsnorm(dev):
@@ -436,10 +428,11 @@ def test_gemm_colsum_epilogue(dev, M, N, K):
     assert torch.allclose(cs - 1.0, ref.sum(0), atol=5e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("tile,det", [(64, True), (128, True), (64, False)])
-def test_grouped_wgrad(dev, tile, det):
-    """One grouped launch of weight-gradient GEMMs == separate fp32 A^T B accumulations; det: split-K
-    partials through the workspace + fold launch (bit-identical on a repeat), else fp32 atomics."""
+@pytest.mark.parametrize("tile", [64, 128])
+def test_grouped_wgrad(dev, tile):
+    """One grouped launch of weight-gradient GEMMs == separate fp32 A^T B accumulations, split-K partials
+    and the row slices of the column sums through the workspace + fold launch: a repeat from the same
+    C / column accumulators is bit-identical."""
     from plaincv_amd import kernels as K_
     torch.manual_seed(9)
     shapes = [(16640, 128, 384), (16640, 128, 128), (16640, 128, 512), (16640, 512, 128), (300, 72, 40),
@@ -456,21 +449,21 @@ def test_grouped_wgrad(dev, tile, det):
           torch.randn(7, 8, device=dev).to(torch.bfloat16)]
     outs = [torch.randn(x.shape[1], device=dev) for x in xs]
     cref = [o + x.float().sum(0) for x, o in zip(xs, outs)]
-    g = K_.GroupedWGrad(items + [("colsum", x, o) for x, o in zip(xs, outs)], dev, tile=tile, deterministic=det)
-    assert (g.fold_blocks > 0) == det and (g.ws is not None) == det
+    g = K_.GroupedWGrad(items + [("colsum", x, o) for x, o in zip(xs, outs)], dev, tile=tile)
+    assert g.fold_blocks > 0 and g.ws is not None
     c0 = [c.clone() for _, _, c, _ in items]
+    o0 = [o.clone() for o in outs]
     g()
     torch.cuda.synchronize()
-    if det:   # the GEMM outputs are a fixed-order sum: a repeat from the same C is bit-identical
-        first = [c.clone() for _, _, c, _ in items]
-        for (_, _, c, _), c_ in zip(items, c0):
-            c.copy_(c_)
-        for o, r, x in zip(outs, cref, xs):
-            o.sub_(x.float().sum(0))      # (column sums use atomics: not compared bitwise)
-        g()
-        torch.cuda.synchronize()
-        for (_, _, c, _), f in zip(items, first):
-            assert torch.equal(c, f)
+    first = [c.clone() for _, _, c, _ in items] + [o.clone() for o in outs]
+    for (_, _, c, _), c_ in zip(items, c0):
+        c.copy_(c_)
+    for o, o_ in zip(outs, o0):
+        o.copy_(o_)
+    g()
+    torch.cuda.synchronize()
+    for t, f in zip([c for _, _, c, _ in items] + outs, first):
+        assert torch.equal(t, f)
     for o, r in zip(outs, cref):
         assert torch.allclose(o, r, atol=2e-2, rtol=1e-4), (o - r).abs().max().item()
     for (a, b, c, _), ref in zip(items, refs):

@@ -137,7 +137,7 @@ def test_vit_f32_graphed_step(dev):
     assert torch.isfinite(sc.params.flat).all()
 
 
-def test_vit_f32_unfused_attention_matches_fused(dev, monkeypatch):
+def test_vit_f32_unfused_attention_matches_fused(dev):
     """The general attention path (per-head GEMM jobs around the materialised-score softmax, used
     past T = 272 or head_dim != 32) and the fused kernels give the same step (rel 1e-5)."""
     from plaincv_amd.engine import create_train_state
@@ -148,11 +148,12 @@ def test_vit_f32_unfused_attention_matches_fused(dev, monkeypatch):
     images = torch.randint(0, 256, shape, generator=g, dtype=torch.uint8).to(dev)
     labels = torch.randint(0, 10, (4,), generator=g, dtype=torch.int32).to(dev)
     out = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("PCV_F32_FUSED_ATTN", flag)
+    from plaincv_amd.models.vit_f32 import ViTRunnerF32
+    for fused in (True, False):
         st = create_train_state(0, m, 1e-3, shape, 10, init_params=init)
-        r = st.runner_for(shape)
-        assert r.fused_attn == (flag == "1")
+        r = ViTRunnerF32(m, st.params, shape, dev, fused_attn=fused)
+        st.runners[tuple(shape)] = r
+        assert r.fused_attn == fused
         r.seed.fill_(9)
         st.params.zero_grad()
         met = r.forward(images, labels, train=True)
