@@ -59,6 +59,16 @@ def mm(x, w, bf16: bool = False):
     return out
 
 
+def dense(x, w, b, bf16: bool = False):
+    """flax Dense: x @ w + b, in bf16 placement with bf16 operands.  Inside ``bf16_grad_storage`` the
+    gradient of the whole output (bias included) is rounded to bf16: the device keeps dY in bf16, and
+    the bias gradient is the column sum of that stored dY (the weight gradient's dY operand too)."""
+    out = rnd(x, bf16) @ rnd(w, bf16) + b
+    if bf16 and _GRAD_STORAGE["bf16"] and out.requires_grad and out.dtype != torch.float64:
+        out = _RoundGrad.apply(out)
+    return out
+
+
 def layernorm(x, scale, bias, eps=1e-6):
     """flax.linen.LayerNorm: fast variance E[x^2]-E[x]^2 (clipped at 0), eps 1e-6
     (used at models/vit_small.py:38,52,124)."""

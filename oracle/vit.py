@@ -8,7 +8,7 @@ from dataclasses import dataclass
 
 import torch
 
-from .nn import batchnorm, dropout, gelu_tanh, layernorm, mm, rnd
+from .nn import dense, batchnorm, dropout, gelu_tanh, layernorm, mm, rnd
 
 # dropout site ids shared with plaincv_amd.models.vit_small (the kernel side)
 SITE_EMBED = 1
@@ -48,9 +48,9 @@ def self_attention(params, pre, y, cfg: ViTConfig, train, seed, layer, bf16):
     B, T, D = y.shape
     H = cfg.num_heads
     Dh = D // H
-    q = mm(y, params[f"{pre}/query/kernel"].reshape(D, H * Dh), bf16) + params[f"{pre}/query/bias"].reshape(-1)
-    k = mm(y, params[f"{pre}/key/kernel"].reshape(D, H * Dh), bf16) + params[f"{pre}/key/bias"].reshape(-1)
-    v = mm(y, params[f"{pre}/value/kernel"].reshape(D, H * Dh), bf16) + params[f"{pre}/value/bias"].reshape(-1)
+    q = dense(y, params[f"{pre}/query/kernel"].reshape(D, H * Dh), params[f"{pre}/query/bias"].reshape(-1), bf16)
+    k = dense(y, params[f"{pre}/key/kernel"].reshape(D, H * Dh), params[f"{pre}/key/bias"].reshape(-1), bf16)
+    v = dense(y, params[f"{pre}/value/kernel"].reshape(D, H * Dh), params[f"{pre}/value/bias"].reshape(-1), bf16)
     q = q.reshape(B, T, H, Dh)
     k = k.reshape(B, T, H, Dh)
     v = v.reshape(B, T, H, Dh)
@@ -60,16 +60,16 @@ def self_attention(params, pre, y, cfg: ViTConfig, train, seed, layer, bf16):
     if train and cfg.dropout_rate > 0.0:
         w = dropout(w, cfg.dropout_rate, seed, site_attn(layer), train, mask_shape=(T, T))
     o = torch.einsum("bhqk,bkhd->bqhd", rnd(w, bf16), rnd(v, bf16)).reshape(B, T, H * Dh)
-    out = mm(o, params[f"{pre}/out/kernel"].reshape(H * Dh, D), bf16) + params[f"{pre}/out/bias"]
+    out = dense(o, params[f"{pre}/out/kernel"].reshape(H * Dh, D), params[f"{pre}/out/bias"], bf16)
     return out
 
 
 def mlp_block(params, pre, y, cfg: ViTConfig, train, seed, layer, bf16):
     """MlpBlock (models/vit_small.py:6-18): Dense -> gelu(tanh) -> Dropout -> Dense -> Dropout."""
-    h = mm(y, params[f"{pre}/Dense_0/kernel"], bf16) + params[f"{pre}/Dense_0/bias"]
+    h = dense(y, params[f"{pre}/Dense_0/kernel"], params[f"{pre}/Dense_0/bias"], bf16)
     h = gelu_tanh(h)
     h = dropout(h, cfg.dropout_rate, seed, site_mlp_hidden(layer), train)
-    o = mm(h, params[f"{pre}/Dense_1/kernel"], bf16) + params[f"{pre}/Dense_1/bias"]
+    o = dense(h, params[f"{pre}/Dense_1/kernel"], params[f"{pre}/Dense_1/bias"], bf16)
     return dropout(o, cfg.dropout_rate, seed, site_mlp_out(layer), train)
 
 
@@ -104,7 +104,7 @@ def vit_apply(params, images, cfg: ViTConfig, train: bool = True, seed: int = 0,
     # VALID conv with kernel=stride=patch == GEMM over (kh,kw,c)-flattened patches
     patches = x.reshape(B, gh, ps, gw, ps, C).permute(0, 1, 3, 2, 4, 5).reshape(B, gh * gw, ps * ps * C)
     D = cfg.hidden_size
-    x = mm(patches, params["Conv_0/kernel"].reshape(ps * ps * C, D), bf16) + params["Conv_0/bias"]
+    x = dense(patches, params["Conv_0/kernel"].reshape(ps * ps * C, D), params["Conv_0/bias"], bf16)
     cls = params["cls_token"].expand(B, 1, D)
     x = torch.cat([cls, x], dim=1) + params["pos_embedding"]
     x = dropout(x, cfg.dropout_rate, seed, SITE_EMBED, train)
@@ -116,7 +116,7 @@ def vit_apply(params, images, cfg: ViTConfig, train: bool = True, seed: int = 0,
         x = x + mlp_block(params, f"{pre}/MlpBlock_0", y, cfg, train, seed, i, bf16)
     x = _prenorm(params, f"{norm}_0", x, cfg, train, batch_stats, new_batch_stats)
     cls_repr = x[:, 0]
-    return mm(cls_repr, params["Dense_0/kernel"], bf16) + params["Dense_0/bias"]
+    return dense(cls_repr, params["Dense_0/kernel"], params["Dense_0/bias"], bf16)
 
 
 def vit_param_shapes(cfg: ViTConfig, image_size: int, channels: int):
