@@ -380,7 +380,10 @@ def bench_vit(args):
                           "optimizer": cfg.optim, "parallelism": f"dp{world}",
                           "inputs": "copy-in (one static batch buffer per step)" if ring is None else
                                     "input ring (one captured graph per resident batch slot, read in place)",
-                          "optimizer_overlap": bool(step.overlap)},
+                          "optimizer_overlap": bool(step.overlap),
+                          "grad_reduce": None if world == 1 else
+                                         ("RCCL all-reduce captured in the step graph" if step.capture_reduce
+                                          else "eager all-reduce between the step's two graph replays")},
                "steps_per_sec": round(sps, 3), "tflops_per_gpu": round(flops * sps / 1e12, 3),
                "final_loss": round(loss, 4)}
         out["roofline"] = (None if args.no_roofline else

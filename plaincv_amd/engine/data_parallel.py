@@ -94,10 +94,12 @@ def _avg_supported(t):
     return t.is_cuda and dist.get_backend() == "nccl"
 
 
-def all_reduce_mean_(t, bucket_bytes=DEFAULT_BUCKET_BYTES):
-    """In-place mean of a flat tensor across ranks, bucketed back to front."""
+def all_reduce_mean_(t, bucket_bytes=DEFAULT_BUCKET_BYTES, always=False):
+    """In-place mean of a flat tensor across ranks, bucketed back to front.  A one-rank group skips the
+    collective unless ``always`` (a one-rank RCCL group still launches it: how the captured-reduce step
+    graph is exercised on one GPU)."""
     n = world_size()
-    if n <= 1:
+    if n <= 1 and not (always and is_initialized()):
         return t
     per = max(1, bucket_bytes // t.element_size())
     total = t.numel()
@@ -115,9 +117,39 @@ def all_reduce_mean_(t, bucket_bytes=DEFAULT_BUCKET_BYTES):
     return t
 
 
-def all_reduce_grads(store, bucket_bytes=DEFAULT_BUCKET_BYTES):
-    if world_size() > 1:
-        all_reduce_mean_(store.grad_flat[: store.layout.size], bucket_bytes)
+def all_reduce_grads(store, bucket_bytes=DEFAULT_BUCKET_BYTES, always=False):
+    if world_size() > 1 or always:
+        all_reduce_mean_(store.grad_flat[: store.layout.size], bucket_bytes, always=always)
+
+
+def captured_reduce_works(device, stream):
+    """Whether an all-reduce captured into a hipGraph runs correctly on this process group.  Every rank
+    captures one on ``stream``; the ranks agree (eagerly) that every capture succeeded before any rank
+    replays, then replay once and agree the mean is right -- so all ranks take the same decision.  Only
+    RCCL ("nccl") collectives are graph-capturable; gloo runs on the host."""
+    if not is_initialized() or device.type != "cuda" or dist.get_backend() != "nccl":
+        return False
+    n = dist.get_world_size()
+    t = torch.full((256,), float(rank() + 1), device=device)
+    g = torch.cuda.CUDAGraph()
+    ok = 1
+    stream.wait_stream(torch.cuda.current_stream(device))
+    try:
+        with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
+            all_reduce_mean_(t, always=True)
+    except Exception:   # pragma: no cover - depends on the RCCL / HIP build
+        ok = 0
+
+    def agree(v):
+        f = torch.tensor([v], dtype=torch.int32, device=device)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        return bool(f.item())
+
+    if not agree(ok):
+        return False
+    g.replay()
+    torch.cuda.synchronize(device)
+    return agree(int(bool(torch.all(t == (n + 1) / 2.0).item())))
 
 
 def all_reduce_metrics(m):

@@ -254,8 +254,8 @@ class _labels_bound:
 
 
 class GraphedTrainStep:
-    """One hipGraph per step: seed advance, zero-grad, forward, backward,
-    (all-reduce outside the graph when world_size > 1), optimizer.
+    """One hipGraph per step: seed advance, zero-grad, forward, backward, the data-parallel gradient
+    mean (world_size > 1), optimizer.
 
     Inputs are copied into static buffers before each replay -- unless they are one of the
     ``inputs`` slots: ``inputs=(images [N, B, H, W, C] uint8, labels [N, B] int32)`` on the device is a
@@ -264,13 +264,21 @@ class GraphedTrainStep:
     graph boundary plus two copy kernels, ~18 us, at ViT C2).  The warm-up launches that
     precede capture (lazy library setup) run on zero images; the params, optimizer state and
     seed they touch are snapshotted and restored, so construction does not train the model,
-    and under data parallelism the warm-up gradients are all-reduced like a real step."""
+    and under data parallelism the warm-up gradients are all-reduced like a real step.
+
+    Data parallelism (``reduce``, default world_size > 1): the gradient mean over ranks (and the
+    BatchNorm running averages) sits between the backward and the optimizer.  On RCCL it is captured
+    inside the step graph (``capture_reduce``, default: when dp.captured_reduce_works), so a step stays
+    one replay, Muon's matrix-phase overlap included.  Otherwise (gloo, or a build whose collectives do
+    not capture) each step replays the forward/backward graph, reduces eagerly and replays a second
+    graph holding the optimizer's part of the step -- the overlap holds there too."""
 
     # each ring slot is one more captured forward/backward graph (construction time and graph memory
     # grow with the ring); the slot graphs share the copy-in graph's memory pool
     MAX_SLOTS = 8
 
-    def __init__(self, state: TrainState, image_shape, warmup=2, inputs=None, overlap_opt=False):
+    def __init__(self, state: TrainState, image_shape, warmup=2, inputs=None, overlap_opt=False,
+                 reduce=None, capture_reduce=None):
         self.state = state
         self.runner = state.runner_for(image_shape)
         dev = state.params.device
@@ -287,7 +295,9 @@ class GraphedTrainStep:
             if xs.shape[0] > self.MAX_SLOTS:
                 raise ValueError(f"inputs: at most {self.MAX_SLOTS} ring slots (one captured graph each)")
             self.slots = [(xs[k], ys[k]) for k in range(xs.shape[0])]
-        self.distributed = dp.world_size() > 1
+        # reduce=True on a one-rank process group still launches the collective (tests of the
+        # captured-reduce graph on one GPU); without a process group there is nothing to reduce over
+        self.distributed = (dp.world_size() > 1) if reduce is None else bool(reduce and dp.is_initialized())
         # SOAP/Shampoo steps are host-driven (first step, refreshes, basis restarts): they run
         # eagerly after the captured forward/backward.
         self.opt_graphed = bool(getattr(state.tx, "graphable", True))
@@ -296,13 +306,13 @@ class GraphedTrainStep:
         # side stream at the start of step t+1, beside that step's forward up to the first read of a
         # routed weight (runner.forward(join=...)).  The phase order per step is step_()'s; the last
         # step's matrix phase runs in flush() (called by whoever reads the params next: bench, eval).
-        self.overlap = bool(overlap_opt and self.opt_graphed and not self.distributed and
+        self.overlap = bool(overlap_opt and self.opt_graphed and
                             getattr(self.runner, "supports_join", False) and
                             hasattr(state.tx, "split_capable") and state.tx.split_capable(state.opt_state))
         self.pending = False
         self.stream = torch.cuda.Stream(device=dev)
         self.g_fb = torch.cuda.CUDAGraph()
-        self.g_opt = torch.cuda.CUDAGraph() if (self.distributed and self.opt_graphed) else None
+        self.g_post = None
         s = self.stream
         store = state.params
         saved = [(st, st.clone()) for st in _device_storages([store.flat, store.shadow, self.runner.seed,
@@ -315,15 +325,20 @@ class GraphedTrainStep:
             for _ in range(warmup):
                 self._fb()
                 if self.distributed:
-                    dp.all_reduce_grads(store)
-                    _reduce_batch_stats(state)
+                    self._reduce()
                 self._opt()
             torch.cuda.synchronize()
             for st, copy in saved:
                 st.copy_(copy)
             torch.cuda.synchronize()
             _restore_host_scalars(host)
-            split = self.distributed or not self.opt_graphed
+            if self.distributed and capture_reduce is None:
+                capture_reduce = self.opt_graphed and dp.captured_reduce_works(dev, s)
+            self.capture_reduce = bool(self.distributed and capture_reduce)
+            # split: the step graph ends after the backward; the reduce and the optimizer's part run
+            # after its replay (eager reduce, then g_post, or the eager optimizer)
+            self.split = (self.distributed and not self.capture_reduce) or not self.opt_graphed
+            mode = "thread_local" if self.capture_reduce else "global"
             self.g_slots = []
             after_first = None
             for images, labels in [(None, None)] + self.slots:   # the copy-in graph, then one per slot
@@ -331,12 +346,9 @@ class GraphedTrainStep:
                 with _labels_bound(self.runner, labels):
                     # slot graphs replay one at a time on this stream, after the copy-in graph's capture:
                     # they can share its memory pool
-                    with torch.cuda.graph(g, stream=s, pool=None if images is None else self.g_fb.pool()):
-                        self._fb(images)
-                        if self.overlap:
-                            state.tx.step_grad_phase_(store, state.opt_state)
-                        elif not split:
-                            self._opt()
+                    with torch.cuda.graph(g, stream=s, pool=None if images is None else self.g_fb.pool(),
+                                          capture_error_mode=mode):
+                        self._body(images, steady=False)
                 if images is None:
                     after_first = _host_scalars(state.opt_state)   # host state as after one capture
                 else:
@@ -350,23 +362,50 @@ class GraphedTrainStep:
                 for images, labels in [(None, None)] + self.slots:
                     g = torch.cuda.CUDAGraph()
                     with _labels_bound(self.runner, labels):
-                        with torch.cuda.graph(g, stream=s, pool=self.g_fb.pool()):
-                            self.side.wait_stream(s)
-                            with torch.cuda.stream(self.side):
-                                state.tx.step_ns_phase_(store, state.opt_state)
-                            join = lambda i: s.wait_stream(self.side) if i == 0 else None  # noqa: E731
-                            self._fb(images, join=join)
-                            s.wait_stream(self.side)   # (a one-block model never joins at block 1)
-                            state.tx.step_grad_phase_(store, state.opt_state)
+                        with torch.cuda.graph(g, stream=s, pool=self.g_fb.pool(), capture_error_mode=mode):
+                            self._body(images, steady=True)
                     self.g_steady.append(g)
                 self.g_flush = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.g_flush, stream=s, pool=self.g_fb.pool()):
                     state.tx.step_ns_phase_(store, state.opt_state)
-            if self.g_opt is not None:
-                with torch.cuda.graph(self.g_opt, stream=s):
-                    self._opt()
+            if self.split and self.opt_graphed:
+                self.g_post = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.g_post, stream=s, pool=self.g_fb.pool()):
+                    self._post()
         torch.cuda.current_stream().wait_stream(s)
         self.metrics = self.runner.metrics
+
+    def _body(self, images, steady):
+        """What one step graph holds: [the previous step's matrix phase on the side stream, joined before
+        the first routed-weight read] forward, backward, then -- unless split -- the reduce and the
+        optimizer's part."""
+        s, state = self.stream, self.state
+        if steady:
+            self.side.wait_stream(s)
+            with torch.cuda.stream(self.side):
+                state.tx.step_ns_phase_(state.params, state.opt_state)
+            join = lambda i: s.wait_stream(self.side) if i == 0 else None  # noqa: E731
+            self._fb(images, join=join)
+            s.wait_stream(self.side)   # (a one-block model never joins at block 1)
+        else:
+            self._fb(images)
+        if self.split:
+            return
+        if self.distributed:
+            self._reduce()
+        self._post()
+
+    def _post(self):
+        """The optimizer's part of a step: the gradient phase when the matrix phase is deferred."""
+        if self.overlap:
+            self.state.tx.step_grad_phase_(self.state.params, self.state.opt_state)
+        else:
+            self._opt()
+
+    def _reduce(self):
+        dp.all_reduce_grads(self.state.params, always=True)
+        if self.state.batch_stats is not None:
+            dp.all_reduce_mean_(self.state.batch_stats.flat, always=True)
 
     def _fb(self, images=None, join=None):
         K.zero_seed(self.state.params.grad_flat, self.runner.seed)   # zero grads + advance seed
@@ -417,12 +456,12 @@ class GraphedTrainStep:
         if self.overlap:
             self.pending = True
             self.state.params.pending = self.flush
-        if self.distributed:
-            dp.all_reduce_grads(self.state.params)
-            _reduce_batch_stats(self.state)
-        if self.g_opt is not None:
-            self.g_opt.replay()
-        elif self.distributed or not self.opt_graphed:
-            self._opt()
+        if self.split:
+            if self.distributed:
+                self._reduce()
+            if self.g_post is not None:
+                self.g_post.replay()
+            else:
+                self._opt()
         self.state.step += 1
         return self.metrics

@@ -47,19 +47,43 @@ def test_dp_two_ranks(dev, tmp_path, which):
     assert reps[0]["checksum"] == reps[1]["checksum"], reps
 
 
-def _two_ranks(tmp_path, which):
+def _two_ranks(tmp_path, which, n=2):
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), PYTHONPATH=ROOT)
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "workers", "dp_worker.py"), which,
                                        str(tmp_path / f"r{r}.json")], env=env, cwd=ROOT))
     codes = [p.wait(timeout=150) for p in procs]
-    assert codes == [0, 0], codes
-    return [json.load(open(tmp_path / f"r{r}.json")) for r in range(2)]
+    assert codes == [0] * n, codes
+    return [json.load(open(tmp_path / f"r{r}.json")) for r in range(n)]
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_dp_step_keeps_optimizer_overlap(dev, tmp_path, dtype):
+    """Two ranks (gloo) through GraphedTrainStep(overlap_opt=True): the overlap stays on under DP, a
+    replica fed the same batches as its peer equals the single-rank in-step run bit for bit, and
+    replicas fed their own batches end bit-identical (params, bf16 shadow, Muon / Adam moments)."""
+    reps = _two_ranks(tmp_path, f"dp_overlap:{dtype}")
+    for r in reps:
+        assert r["overlap_under_dp"], r
+        assert r["dp_equals_single_in_step"], r
+    assert reps[0]["checksum"] == reps[1]["checksum"], reps
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_captured_reduce_step_graph(dev, tmp_path, dtype):
+    """The RCCL path's all-reduce captured inside the step graph, on a one-rank RCCL group (two ranks
+    cannot share one GPU under RCCL): the capture probe passes, the step is one replay with the overlap
+    on, and the state equals the split (eager-reduce) variant, the plain overlapped step and the
+    in-step run bit for bit."""
+    rep, = _two_ranks(tmp_path, f"captured:{dtype}", n=1)
+    print(f"CAPTURED_REDUCE {dtype} {rep}")
+    assert rep["probe"] and rep["captured"] and rep["split"], rep
+    assert len(set(rep["digests"])) == 1, rep["digests"]
 
 
 @pytest.mark.parametrize("optim,layout", [("muon", "vit_c2"), ("muon", "lm768"), ("soap", "vit_c2"),

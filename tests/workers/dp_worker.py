@@ -218,11 +218,81 @@ def engine_shard(rep, dev, kind, optim):
     rep["step_excess"] = 0.0
 
 
+def _digest(st):
+    import hashlib
+    h = hashlib.sha256()
+    for t in (st.params.flat, st.params.shadow, st.opt_state.tensors["mu"], st.opt_state.tensors["nu"]):
+        h.update(t.detach().cpu().contiguous().view(torch.uint8).numpy().tobytes())
+    return h.hexdigest()
+
+
+def _overlap_steps(dev, dtype, per_rank, engines):
+    """Three steps of a small ViT (dropout 0.1, Muon) through each GraphedTrainStep configuration in
+    ``engines`` (kwargs) from one initial state, + flush; returns [(state digest, step object)]."""
+    from plaincv_amd.engine import GraphedTrainStep, create_train_state
+    from plaincv_amd.models.vit_small import VisionTransformer
+    from utils import Config
+    m = VisionTransformer(num_classes=10, patch_size=4, hidden_size=64, mlp_dim=128, num_layers=2, num_heads=2,
+                          dropout_rate=0.1, dtype=dtype)
+    shape = (8, 16, 16, 3)
+    cfg = Config(optim="muon", lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9)
+    init = m.init(3, shape)
+    g = torch.Generator().manual_seed(400 + (dist.get_rank() if per_rank else 0))
+    xs = torch.randint(0, 256, (3,) + shape, generator=g, dtype=torch.uint8).to(dev)
+    ys = torch.randint(0, 10, (3, shape[0]), generator=g, dtype=torch.int32).to(dev)
+    out = []
+    for kw in engines:
+        st = create_train_state(0, m, 1e-3, shape, 10, cfg=cfg, init_params=init)
+        step = GraphedTrainStep(st, shape, warmup=2, **kw)
+        for i in range(3):
+            step(xs[i], ys[i])
+        step.flush()
+        torch.cuda.synchronize()
+        out.append((_digest(st), step))
+    return out
+
+
+def dp_overlap(rep, dev, dtype):
+    """Two ranks (gloo): the data-parallel step keeps Muon's matrix-phase overlap (gloo cannot be
+    captured: forward/backward graph, eager gradient mean, gradient-phase graph).  (1) Both ranks on the
+    same batches: the mean of two equal gradients is that gradient exactly, so every replica must equal
+    the single-rank in-step run (overlap off, no reduce) bit for bit.  (2) Per-rank batches: the
+    replicas must end bit-identical (digest compared by the parent)."""
+    same = _overlap_steps(dev, dtype, False, [dict(overlap_opt=True), dict(overlap_opt=False, reduce=False)])
+    (d_dp, s_dp), (d_single, _) = same
+    rep["overlap_under_dp"] = bool(s_dp.overlap and s_dp.distributed and s_dp.split and not s_dp.capture_reduce)
+    rep["dp_equals_single_in_step"] = d_dp == d_single
+    (d_pr, _), = _overlap_steps(dev, dtype, True, [dict(overlap_opt=True)])
+    rep["checksum"] = d_pr
+    rep["step_excess"] = 0.0
+
+
+def captured_reduce(rep, dev, dtype):
+    """A one-rank RCCL group (reduce=True still launches the collective): the all-reduce captured inside
+    the step graph (and the split eager variant) must leave exactly the state of the plain single-rank
+    step -- overlapped and in-step."""
+    from plaincv_amd.engine import data_parallel as dp
+    rep["probe"] = dp.captured_reduce_works(dev, torch.cuda.Stream(device=dev))
+    runs = _overlap_steps(dev, dtype, False, [dict(overlap_opt=True, reduce=True),
+                                              dict(overlap_opt=True, reduce=True, capture_reduce=False),
+                                              dict(overlap_opt=True, reduce=False),
+                                              dict(overlap_opt=False, reduce=False)])
+    s = runs[0][1]
+    rep["captured"] = bool(s.distributed and s.capture_reduce and not s.split and s.overlap)
+    rep["split"] = bool(runs[1][1].split and runs[1][1].overlap)
+    rep["digests"] = [d for d, _ in runs]
+    rep["checksum"] = runs[0][0]
+    rep["step_excess"] = 0.0
+
+
 def main():
     which, out = sys.argv[1], sys.argv[2]
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    dist.init_process_group("gloo")
+    if which.startswith("captured:"):
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
     rep = {"rank": dist.get_rank()}
     if which.startswith("shard:"):
         _, optim, layout_name = which.split(":")
@@ -230,6 +300,10 @@ def main():
     elif which.startswith("engine_shard:"):
         _, kind, optim = which.split(":")
         engine_shard(rep, dev, kind, optim)
+    elif which.startswith("dp_overlap:"):
+        dp_overlap(rep, dev, which.split(":")[1])
+    elif which.startswith("captured:"):
+        captured_reduce(rep, dev, which.split(":")[1])
     else:
         (vit if which == "vit" else lm)(rep, dev)
     dist.barrier()
