@@ -292,6 +292,16 @@ int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, int64_t ldb, 
                       int64_t M, int64_t N, int64_t K, const float* bias, float* aux, int64_t ldaux, const float* res,
                       int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed, uint32_t site,
                       void* stream);
+/* The same product in the tiled form only (32 x 64 / 64 x 64 / 64 x 128 tiles; what pcv_gemm_f32_rows
+ * runs for shapes outside the panel form).  pcv_gemm_f32_rows takes the panel form -- a persistent grid of
+ * one workgroup per CU owning 64-row panels, the A strip in registers, op(B) streamed through LDS in
+ * column blocks -- when pcv_gemm_f32_rows_form(M, N, K) is 1: K in {128, 256, 384}, M >= 64 and the rows
+ * past the persistent panels fit one tail unit per workgroup. */
+int pcv_gemm_f32_rows_tiled(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C, int64_t ldc,
+                            int64_t M, int64_t N, int64_t K, const float* bias, float* aux, int64_t ldaux,
+                            const float* res, int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed,
+                            uint32_t site, void* stream);
+int pcv_gemm_f32_rows_form(int64_t M, int64_t N, int64_t K);
 /* Every fp32 weight gradient of a step in one launch (csrc/gemm_f32.hip): jobs_dev holds njobs
  * records (pcv_gemm_f32_wgrad_job_size() bytes) {A, B, C, colsum, ws, lda, ldb, ldc, M, N, K, tiles_n,
  * tiles, ksplit, kchunk, first, ffirst, pad} (colsum optional: += the column sums of B -- the Dense's

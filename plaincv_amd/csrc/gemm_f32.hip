@@ -19,6 +19,8 @@
 // (8 MFMAs per k-step).
 #include "common.h"
 
+#include <algorithm>
+
 namespace pcv {
 
 constexpr int GR_BM = 64, GR_BN = 128, GR_BK = 64, GR_LDK = GR_BK + 4;   // GR_BN: the widest panel
@@ -388,7 +390,335 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(const WgJob* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+constexpr int PN_RM = 64;         // rows per panel: 4 strips of 16
+constexpr int PN_THREADS = 512;   // 8 waves, two per SIMD: wave w -> strip w & 3, column half w >> 2
+
+// epilogue flags (template, so the epilogue operand loads are branch-free: a load under a runtime
+// branch costs an s_waitcnt vmcnt(0) at the merge, which also waits for the next block's prefetch)
+enum : int { PN_BIAS = 1, PN_RES = 2, PN_GELU = 4, PN_GELUBWD = 8, PN_DROP = 16 };
+
+template <bool TB, int K, int CB>
+struct PnShape {
+  static constexpr int NSB = CB / 16;                             // 16-column sub-blocks per block
+  static constexpr int HSB = NSB / 2;                             // ... per wave (its column half)
+  // stage image: TB [n][K + 8] (k-contiguous rows; the pad of 8, not 4, makes the ds_read_b128 lane
+  // groups conflict-free); !TB [k / 4][n][4] (each n's four consecutive k together, unpadded): either
+  // way a fragment is one conflict-free ds_read_b128
+  static constexpr int LDW = K + 8;
+  static constexpr int WIMG = TB ? CB * LDW : K * CB;             // floats per ring stage
+  static constexpr int F4 = CB / 4;                               // !TB: float4s per k row of a block
+  static constexpr int NLD = CB * K / 4 / PN_THREADS;             // float4 loads per thread per block
+  // the ring + the tail unit's K-part partials (8 waves x 64 lanes x 16 B); > 80 KiB, so the dispatcher
+  // cannot put two workgroups on one CU (the grid is one per CU)
+  static constexpr int LDS_USED = 2 * WIMG * 4 + 8 * 64 * 16;
+  static constexpr int LDS_BYTES = LDS_USED > 81920 ? LDS_USED : 81920 + 16;
+  static_assert(CB * K % (4 * PN_THREADS) == 0 && NSB % 2 == 0 && NSB <= 4, "block shape");
+};
+
+// float4 piece idx of a block: TB -> (n, k4) of a [n][k] row; !TB -> (k, n4) of a [k][n] row, mapped
+// so that a 32-lane group covers the 16 (n4 mod 4, k mod 4) pairs: the four 4-B stores of each float4
+// into the [k / 4][n][4] image are then at most 2-way bank-conflicted, which costs nothing on
+// ds_write_b32 (global reads stay 64-B row segments of the L2-resident weight)
+template <int K, int CB>
+__device__ __forceinline__ void pn_piece(int idx, int& k, int& n4) {
+  constexpr int HB = CB / 16;   // high n4 values (F4 / 4)
+  n4 = (idx & 3) | (((idx >> 4) % HB) << 2);
+  k = ((idx >> 2) & 3) | ((idx / (16 * HB)) << 2);
+}
+template <bool TB, int K, int CB>
+__device__ __forceinline__ f32x4 pn_gload1(const float* __restrict__ B, int64_t ldb, int n0, int i) {
+  const int idx = threadIdx.x + PN_THREADS * i;
+  if (TB) return *reinterpret_cast<const f32x4*>(B + (int64_t)(n0 + idx / (K / 4)) * ldb + (idx % (K / 4)) * 4);
+  int k, n4;
+  pn_piece<K, CB>(idx, k, n4);
+  return *reinterpret_cast<const f32x4*>(B + (int64_t)k * ldb + n0 + 4 * n4);
+}
+template <bool TB, int K, int CB>
+__device__ __forceinline__ void pn_gload(const float* __restrict__ B, int64_t ldb, int n0,
+                                         f32x4 (&rw)[PnShape<TB, K, CB>::NLD]) {
+#pragma unroll
+  for (int i = 0; i < PnShape<TB, K, CB>::NLD; ++i) rw[i] = pn_gload1<TB, K, CB>(B, ldb, n0, i);
+}
+template <bool TB, int K, int CB>
+__device__ __forceinline__ void pn_lstore(float* Ws, const f32x4 (&rw)[PnShape<TB, K, CB>::NLD]) {
+  constexpr int LDW = PnShape<TB, K, CB>::LDW;
+#pragma unroll
+  for (int i = 0; i < PnShape<TB, K, CB>::NLD; ++i) {
+    const int idx = threadIdx.x + PN_THREADS * i;
+    if (TB) {
+      *reinterpret_cast<f32x4*>(&Ws[(idx / (K / 4)) * LDW + (idx % (K / 4)) * 4]) = rw[i];
+    } else {
+      int k, n4;
+      pn_piece<K, CB>(idx, k, n4);
+      float* p = &Ws[((k >> 2) * CB + 4 * n4) * 4 + (k & 3)];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) p[4 * e] = rw[i][e];
+    }
+  }
+}
+// op(B) fragment of slice s, sub-block sb: lane (g4, c16) -> column n = 16 sb + c16, k = 16 s + 4 g4 + e
+template <bool TB, int K, int CB>
+__device__ __forceinline__ f32x4 pn_wfrag(const float* Ws, int s, int sb, int g4, int c16) {
+  if (TB) return *reinterpret_cast<const f32x4*>(&Ws[(16 * sb + c16) * PnShape<TB, K, CB>::LDW + 16 * s + 4 * g4]);
+  return *reinterpret_cast<const f32x4*>(&Ws[((4 * s + g4) * CB + 16 * sb + c16) * 4]);
+}
+
+// the Dense epilogue of gr_epi_apply with the operand set fixed at compile time (same element order)
+template <int EF>
+__device__ __forceinline__ GrEpiIn pn_epi_load(const GrArgs& g, int row, int col) {
+  GrEpiIn in;
+  if (EF & PN_BIAS) in.bias = *reinterpret_cast<const f32x4*>(g.bias + col);
+  if (EF & PN_GELUBWD) in.aux = *reinterpret_cast<const f32x4*>(g.aux + (int64_t)row * g.ldaux + col);
+  if (EF & PN_RES) in.res = *reinterpret_cast<const f32x4*>(g.res + (int64_t)row * g.ldr + col);
+  return in;
+}
+template <int EF>
+__device__ __forceinline__ f32x4 pn_epi_apply(const GrArgs& g, f32x4 v, const GrEpiIn& in, int row, int col,
+                                              uint32_t seed) {
+  if (EF & PN_BIAS) v += in.bias;
+  const uint32_t base = (uint32_t)((int64_t)row * g.N + col);
+  if (EF & PN_GELUBWD) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = v[e];
+      if (EF & PN_DROP) x = hash3(seed, (uint32_t)g.site, base + e) >= g.thresh ? x * g.dscale : 0.f;
+      v[e] = x * gr_gelu_grad(in.aux[e]);
+    }
+    return v;
+  }
+  if (EF & PN_GELU) {
+    if (g.aux) *reinterpret_cast<f32x4*>(g.aux + (int64_t)row * g.ldaux + col) = v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = gr_gelu(v[e]);
+  }
+  if (EF & PN_DROP) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = hash3(seed, (uint32_t)g.site, base + e) >= g.thresh ? v[e] * g.dscale : 0.f;
+  }
+  if (EF & PN_RES) v += g.res_scale * in.res;
+  return v;
+}
+
+#ifdef PCV_PANEL_STAMPS
+// diagnostic build only (tools/panel_stamps.py): per-phase shader-clock stamps of waves 0 and 4 of
+// every workgroup, vector-stored by lane 0 into a buffer the host registers; no output depends on them
+__device__ unsigned long long* pn_stamp_buf;
+#define PN_STAMP(idx)                                                                               \
+  do {                                                                                              \
+    if ((threadIdx.x & 255) == 0 && pn_stamp_buf)                                                   \
+      pn_stamp_buf[((int64_t)blockIdx.x * 2 + (threadIdx.x >> 8)) * 32 + (idx)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define PN_STAMP(idx) do { } while (0)
+#endif
+
+// Panel form of the row GEMM, for the ViT widths K in {128, 256, 384}.  The tiled kernel above runs
+// ~4 co-resident 32 x 64 tiles per CU through the same phases at the same time (first-chunk load,
+// MFMAs, epilogue), so nothing overlaps the load burst with compute and the rows kernels sat at
+// 0.30-0.43 of the fp32 MFMA peak.  Here a persistent grid of one 512-thread workgroup per CU
+// (G = min(CUs, M / 64)) owns 64-row panels b, b + G, ...; wave w computes 16-row strip w & 3 of the
+// panel for the column half w >> 2 of every block (two waves per SIMD).  Each wave keeps its strip of
+// A in registers for the whole of N, and op(B) streams through a two-stage LDS ring in CB-column
+// blocks: the next block's global loads are spread over the first slices of this block's MFMA loop
+// and stored to the other stage near its end, so one barrier per block remains.  MFMA orientation
+// C^T = op(B)^T A^T: the op(B) fragment is the A operand (i = column n), the A strip the B operand
+// (j = row m), so lane (g4, c16) holds C[m0 + c16][n .. n + 3], n = 16 sb + 4 g4, and the Dense
+// epilogue works on float4 rows straight from the accumulators.  Contraction index of MFMA step e in
+// lane group g4 within slice s: k = 16 s + 4 g4 + e -- one conflict-free 16-B read feeds four MFMAs
+// (a [k][n] operand, TB = 0, is stored [k / 4][n][4] for that: four 4-B LDS stores per float4).
+// Rows past the G * q panels (M = 64 * 257 at B 64: one 64-row tail for 256 CUs) are tail units
+// (16-row tail strip t, block j): workgroup u = t * NB + j computes unit u in its block-j iteration
+// from the block already in LDS, split over its 8 waves as (16-column sub-block) x (K part); the K
+// parts are summed in a fixed order through LDS after the loop.  (A 257th panel would double the
+// launch; computing the units from global memory before the loop cost those workgroups 4-18k cycles.)
+template <bool TB, int EF, int K, int CB>
+__global__ __launch_bounds__(PN_THREADS, 1) void gemm_f32_panel_kernel(GrArgs g, int q, int tail0) {
+  using S = PnShape<TB, K, CB>;
+  constexpr int NSB = S::NSB, HSB = S::HSB, NS = K / 16, NLD = S::NLD;
+  constexpr int KP = 8 / NSB, TNS = NS / KP;   // tail unit: K parts, slices per part
+  constexpr int LST = NS - 2;                  // slice at which the next block goes to LDS
+  static_assert(NLD < LST && NS % KP == 0, "block pipeline shape");
+  extern __shared__ __attribute__((aligned(16))) float pn_lds[];
+  float* const Wst0 = pn_lds;
+  float* const Wst1 = pn_lds + S::WIMG;
+  f32x4* const red = reinterpret_cast<f32x4*>(pn_lds + 2 * S::WIMG);   // tail partials [8 waves][64 lanes]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g4 = lane >> 4, c16 = lane & 15;
+  const int sb0 = (w >> 2) * HSB;   // this wave's first sub-block of each block
+  const int G = (int)gridDim.x, NB = g.N / CB, iters = q * NB;
+  const uint32_t seed = (EF & PN_DROP) ? *g.seed : 0u;
+  PN_STAMP(0);
+
+  // this workgroup's tail unit (block-uniform), and this wave's (sub-block, K part) of it
+  const int ts = (g.M - tail0 + 15) / 16;
+  const bool tail = (int)blockIdx.x < ts * NB;
+  const int tt = tail ? (int)blockIdx.x / NB : 0, tj = tail ? (int)blockIdx.x % NB : 0;
+  const int tsb = w % NSB, tkp = w / NSB;
+  const int trow = tail0 + 16 * tt + c16;
+
+  // prologue: op(B) block 0, the tail's A fragments, this wave's strip
+  f32x4 rw[NLD];
+  pn_gload<TB, K, CB>(g.B, g.ldb, 0, rw);
+  f32x4 ta[TNS];
+  if (tail) {
+    const float* ap = g.A + (int64_t)min(trow, g.M - 1) * g.lda + 4 * g4 + 16 * TNS * tkp;
+#pragma unroll
+    for (int s = 0; s < TNS; ++s) ta[s] = *reinterpret_cast<const f32x4*>(ap + 16 * s);
+  }
+  int row = (int)blockIdx.x * PN_RM + (w & 3) * 16 + c16;
+  f32x4 fa[NS];
+  {
+    const float* ap = g.A + (int64_t)row * g.lda + 4 * g4;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) fa[s] = *reinterpret_cast<const f32x4*>(ap + 16 * s);
+  }
+  PN_STAMP(1);
+  pn_lstore<TB, K, CB>(Wst0, rw);
+  // every prologue load complete before the loop: a strip slice still in flight at the loop head
+  // would put counted vmcnt waits into every iteration's MFMAs, where (in-order counting) they also
+  // wait for the previous block's output stores
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+  __syncthreads();
+  PN_STAMP(2);
+  for (int it = 0; it < iters; ++it) {
+    const int j = it % NB;
+    const float* Ws = (it & 1) ? Wst1 : Wst0;
+    const bool more = it + 1 < iters;
+    const int n1 = ((it + 1) % NB) * CB;
+    GrEpiIn pin[HSB];
+    f32x4 acc[HSB];
+#pragma unroll
+    for (int h = 0; h < HSB; ++h) acc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 wf[2][HSB];
+#pragma unroll
+    for (int h = 0; h < HSB; ++h) wf[0][h] = pn_wfrag<TB, K, CB>(Ws, 0, sb0 + h, g4, c16);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int cur = s & 1;
+      // the next block's loads, one float4 per slice; then this block's epilogue operands
+      if (s < NLD) {
+        if (more) rw[s] = pn_gload1<TB, K, CB>(g.B, g.ldb, n1, s);
+      } else if (s == NLD) {
+#pragma unroll
+        for (int h = 0; h < HSB; ++h) pin[h] = pn_epi_load<EF>(g, row, CB * j + 16 * (sb0 + h) + 4 * g4);
+      }
+      if (s == LST && more) pn_lstore<TB, K, CB>((it & 1) ? Wst0 : Wst1, rw);
+      if (s + 1 < NS) {
+#pragma unroll
+        for (int h = 0; h < HSB; ++h) wf[cur ^ 1][h] = pn_wfrag<TB, K, CB>(Ws, s + 1, sb0 + h, g4, c16);
+      }
+      // keep the next slice's LDS reads ahead of this slice's MFMAs (the scheduler would sink them)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int h = 0; h < HSB; ++h)
+          acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[cur][h][e], fa[s][e], acc[h], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (it < 14) PN_STAMP(3 + 2 * it);
+#pragma unroll
+    for (int h = 0; h < HSB; ++h) {
+      const int col = CB * j + 16 * (sb0 + h) + 4 * g4;
+      const f32x4 v = pn_epi_apply<EF>(g, acc[h], pin[h], row, col, seed);
+      *reinterpret_cast<f32x4*>(g.C + (int64_t)row * g.ldc + col) = v;
+    }
+    if (tail && it == tj) {   // block-uniform: this wave's part of the tail unit, from the same block
+      f32x4 tw[TNS];
+#pragma unroll
+      for (int s = 0; s < TNS; ++s) tw[s] = pn_wfrag<TB, K, CB>(Ws, TNS * tkp + s, tsb, g4, c16);
+      f32x4 tacc{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < TNS; ++s)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tacc = __builtin_amdgcn_mfma_f32_16x16x4f32(tw[s][e], ta[s][e], tacc, 0, 0, 0);
+      red[w * 64 + lane] = tacc;
+    }
+    if (more) {
+      if (j == NB - 1) {   // next panel: this wave's strip of it (q > 1 only)
+        row += G * PN_RM;
+        const float* ap = g.A + (int64_t)row * g.lda + 4 * g4;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) fa[s] = *reinterpret_cast<const f32x4*>(ap + 16 * s);
+        // complete them here: the MFMA loop must not wait on the vector-memory counter (in-order: a
+        // wait for these would also wait for the next block's loads)
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+      }
+      __syncthreads();
+    }
+    if (it < 14) PN_STAMP(4 + 2 * it);
+  }
+  if (tail) {   // block-uniform: K parts summed in order, epilogue, store
+    __syncthreads();
+    if (w < NSB) {
+      f32x4 v = red[w * 64 + lane];
+#pragma unroll
+      for (int p = 1; p < KP; ++p) v += red[(w + NSB * p) * 64 + lane];
+      const int col = CB * tj + 16 * w + 4 * g4;
+      const int lrow = min(trow, g.M - 1);
+      v = pn_epi_apply<EF>(g, v, pn_epi_load<EF>(g, lrow, col), lrow, col, seed);
+      if (trow < g.M) *reinterpret_cast<f32x4*>(g.C + (int64_t)trow * g.ldc + col) = v;
+    }
+  }
+  PN_STAMP(31);
+}
+
 static bool gr_al(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// the panel form's shape rule (K, the column block, the persistent grid and its tail units), or 0
+struct PnPlan { int cb, grid, q, tail0; };
+// Measured per launch at C2's M = 64 * 257 (tools/panel_probe.py, profiles/r05_panel_vs_tiled.txt), the
+// panel form wins where the block loop is long and the prologue short -- K = 128 with N >= 256 (qkv,
+// fc1, the GELU backward: 24.5 / 22.0 / 21.2 vs 25.1 / 22.3 / 23.3 us) -- and loses at N = 128 (two
+// blocks: the 64-row strip prologue is not amortised) and K >= 256 (a 1-1.5 KiB strip per row to
+// land before the first MFMA): out 11.9 vs 11.4, fc2 20.9 vs 19.6, qkv_d 26.0 vs 24.2 us.
+static PnPlan pn_plan(int64_t M, int64_t N, int64_t K) {
+  PnPlan p = {0, 0, 0, 0};
+  if (K != 128 || N < 256) return p;
+  const int cb = 64;
+  if (N % cb || M < PN_RM) return p;
+  const int64_t G = std::min<int64_t>(pcv_cu_count(), M / PN_RM);
+  const int64_t q = M / (PN_RM * G), tail0 = PN_RM * G * q;
+  const int64_t units = (M - tail0 + 15) / 16 * (N / cb);
+  if (units > G || M >= (1ll << 31)) return p;
+  p.cb = cb; p.grid = (int)G; p.q = (int)q; p.tail0 = (int)tail0;
+  return p;
+}
+
+template <bool TB, int EF, int K, int CB>
+static int pn_launch(const GrArgs& g, const PnPlan& p, hipStream_t s) {
+  static PcvLdsOptIn optin;
+  const int bytes = PnShape<TB, K, CB>::LDS_BYTES;
+  const int err = optin.ensure(reinterpret_cast<const void*>(&gemm_f32_panel_kernel<TB, EF, K, CB>), bytes);
+  if (err) return err;
+  hipLaunchKernelGGL((gemm_f32_panel_kernel<TB, EF, K, CB>), dim3(p.grid), dim3(PN_THREADS), bytes, s, g, p.q,
+                     p.tail0);
+  return pcv_launch_status();
+}
+
+// (the kernel is written for K in {128, 256, 384} with CB = 64 / 64 / 32; pn_plan admits K = 128 only)
+template <bool TB, int EF>
+static int pn_dispatch_k(const GrArgs& g, const PnPlan& p, hipStream_t s) {
+  return pn_launch<TB, EF, 128, 64>(g, p, s);
+}
+
+// the epilogue operand sets instantiated for the panel form (the fp32 ViT's Dense calls, train and
+// eval, and the test modes); other sets take the tiled kernel (PN_NOT_LAUNCHED).
+constexpr int PN_NOT_LAUNCHED = -1000;
+template <bool TB>
+static int pn_dispatch(const GrArgs& g, int ef, const PnPlan& p, hipStream_t s) {
+  switch (ef) {
+    case 0: return pn_dispatch_k<TB, 0>(g, p, s);
+    case PN_BIAS: return pn_dispatch_k<TB, PN_BIAS>(g, p, s);
+    case PN_BIAS | PN_RES: return pn_dispatch_k<TB, PN_BIAS | PN_RES>(g, p, s);
+    case PN_BIAS | PN_GELU: return pn_dispatch_k<TB, PN_BIAS | PN_GELU>(g, p, s);
+    case PN_BIAS | PN_GELU | PN_DROP: return pn_dispatch_k<TB, PN_BIAS | PN_GELU | PN_DROP>(g, p, s);
+    case PN_BIAS | PN_RES | PN_DROP: return pn_dispatch_k<TB, PN_BIAS | PN_RES | PN_DROP>(g, p, s);
+    case PN_GELUBWD: return pn_dispatch_k<TB, PN_GELUBWD>(g, p, s);
+    case PN_GELUBWD | PN_DROP: return pn_dispatch_k<TB, PN_GELUBWD | PN_DROP>(g, p, s);
+    default: return PN_NOT_LAUNCHED;
+  }
+}
 
 }  // namespace pcv
 
@@ -400,10 +730,10 @@ extern "C" int pcv_gemm_f32_rows_ok(int64_t M, int64_t N, int64_t K, const void*
          ldb >= (tb ? K : N) && lda % 4 == 0 && ldb % 4 == 0 && gr_al(A) && gr_al(B);
 }
 
-extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C,
-                                 int64_t ldc, int64_t M, int64_t N, int64_t K, const float* bias, float* aux,
-                                 int64_t ldaux, const float* res, int64_t ldr, float res_scale, int act, float rate,
-                                 const uint32_t* seed, uint32_t site, void* stream) {
+static int gr_rows(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C, int64_t ldc,
+                   int64_t M, int64_t N, int64_t K, const float* bias, float* aux, int64_t ldaux, const float* res,
+                   int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed, uint32_t site,
+                   void* stream, bool panel) {
   if (!A || !B || !C || !pcv_gemm_f32_rows_ok(M, N, K, A, lda, B, ldb, tb) || act < 0 || act > 2 ||
       (act == 2 && (!aux || bias || res)) || ldc < N || (act && aux && ldaux < N) ||
       (res && ldr < N) || rate < 0.f || rate >= 1.f || (rate > 0.f && !seed))
@@ -424,6 +754,13 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
   }
   const bool epi = bias || act || res || g.thresh;
   hipStream_t s = (hipStream_t)stream;
+  const PnPlan pp = panel ? pn_plan(M, N, K) : PnPlan{0, 0, 0, 0};
+  if (pp.cb) {
+    const int ef = (bias ? PN_BIAS : 0) | (res ? PN_RES : 0) | (act == 1 ? PN_GELU : 0) |
+                   (act == 2 ? PN_GELUBWD : 0) | (g.thresh ? PN_DROP : 0);
+    const int r = tb ? pn_dispatch<true>(g, ef, pp, s) : pn_dispatch<false>(g, ef, pp, s);
+    if (r != PN_NOT_LAUNCHED) return r;
+  }
   // 64 x 128 panels, or 64 x 64 when the 128-wide grid would leave fewer than four workgroups per
   // CU (the N = 128 / 256 products: with one or two per CU the load / epilogue latency is exposed;
   // C4 step 2.185 -> 2.125 ms moving the N = 256 products to 64-wide panels)
@@ -453,6 +790,30 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
 #undef GR_LAUNCH32
   return pcv_launch_status();
 }
+
+extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C,
+                                 int64_t ldc, int64_t M, int64_t N, int64_t K, const float* bias, float* aux,
+                                 int64_t ldaux, const float* res, int64_t ldr, float res_scale, int act, float rate,
+                                 const uint32_t* seed, uint32_t site, void* stream) {
+  return gr_rows(A, lda, B, ldb, tb, C, ldc, M, N, K, bias, aux, ldaux, res, ldr, res_scale, act, rate, seed, site,
+                 stream, true);
+}
+
+extern "C" int pcv_gemm_f32_rows_tiled(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C,
+                                       int64_t ldc, int64_t M, int64_t N, int64_t K, const float* bias, float* aux,
+                                       int64_t ldaux, const float* res, int64_t ldr, float res_scale, int act,
+                                       float rate, const uint32_t* seed, uint32_t site, void* stream) {
+  return gr_rows(A, lda, B, ldb, tb, C, ldc, M, N, K, bias, aux, ldaux, res, ldr, res_scale, act, rate, seed, site,
+                 stream, false);
+}
+
+extern "C" int pcv_gemm_f32_rows_form(int64_t M, int64_t N, int64_t K) { return pn_plan(M, N, K).cb ? 1 : 0; }
+
+#ifdef PCV_PANEL_STAMPS
+extern "C" int pcv_panel_stamp_buffer(unsigned long long* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(pn_stamp_buf), &buf, sizeof(buf));
+}
+#endif
 
 extern "C" int pcv_gemm_f32_wgrad_job_size(void) { return (int)sizeof(WgJob); }
 

@@ -82,6 +82,9 @@ SIGNATURES = {
     "pcv_vit_embed_bwd_f32": [P, P, P, P, I32, I32, I32, F32, P, U32, P],
     "pcv_gemm_f32_rows_ok": [I64, I64, I64, P, I64, P, I64, I32],
     "pcv_gemm_f32_rows": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32, P],
+    "pcv_gemm_f32_rows_tiled": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32,
+                                P],
+    "pcv_gemm_f32_rows_form": [I64, I64, I64],
     "pcv_gemm_f32_wgrad_job_size": [],
     "pcv_gemm_f32_wgrad": [P, I32, I64, I32, P],
     "pcv_gemm_f32_wgrad_fold": [P, I32, I64, I32, P],

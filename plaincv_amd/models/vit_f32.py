@@ -55,9 +55,12 @@ def _gemm(a, b, c, **kw):
 
 class _Dense:
     """One token-row product c = epi(a op(b)) of the step (act = 2: the GELU-MLP backward,
-    c = dropout_vjp(a op(b)) * gelu'(aux)): the fused row-panel GEMM of
-    csrc/gemm_f32.hip when the shape fits it (N % 128, K % 64), else a planned grouped-GEMM launch
-    followed by the standalone epilogue kernel (same element order and dropout index)."""
+    c = dropout_vjp(a op(b)) * gelu'(aux)): the fused row GEMM of csrc/gemm_f32.hip when the shape
+    fits it (N % 128, K % 64; its panel form for K in 128 / 256 / 384), else a planned grouped-GEMM
+    launch followed by the standalone epilogue kernel (same element order and dropout index).
+    ``entry`` names the C entry point (tools time the tiled form through it)."""
+
+    entry = "pcv_gemm_f32_rows"
 
     def __init__(self, a, b, c, tb=False, bias=None, res=None, aux=None, act=0, site=0, dropout=False):
         self.a, self.b, self.c, self.tb = a, b, c, bool(tb)
@@ -74,7 +77,7 @@ class _Dense:
     def run(self, rate=0.0, seed=None):
         rate = rate if self.dropout else 0.0
         if self.fused:
-            hip.call("pcv_gemm_f32_rows", ptr(self.a), self.a.stride(0), ptr(self.b), self.b.stride(0), int(self.tb),
+            hip.call(self.entry, ptr(self.a), self.a.stride(0), ptr(self.b), self.b.stride(0), int(self.tb),
                      ptr(self.c), self.c.stride(0), self.M, self.N, self.K, ptr(self.bias), ptr(self.aux),
                      self.aux.stride(0) if self.aux is not None else 0, ptr(self.res),
                      self.res.stride(0) if self.res is not None else 0, 1.0, int(self.act), float(rate), ptr(seed),

@@ -7,26 +7,31 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _rows(a, b, tb, c, bias=None, aux=None, res=None, act=0, rate=0.0, seed=None, site=0):
+def _rows(a, b, tb, c, bias=None, aux=None, res=None, act=0, rate=0.0, seed=None, site=0, form="auto"):
     from plaincv_amd import hip
     from plaincv_amd.hip import ptr, stream_ptr
     M, K = a.shape
     N = c.shape[1]
     assert hip.load().pcv_gemm_f32_rows_ok(M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0), int(tb))
-    hip.call("pcv_gemm_f32_rows", ptr(a), a.stride(0), ptr(b), b.stride(0), int(tb), ptr(c), c.stride(0), M, N, K,
+    hip.call("pcv_gemm_f32_rows" if form == "auto" else "pcv_gemm_f32_rows_tiled", ptr(a), a.stride(0), ptr(b), b.stride(0), int(tb), ptr(c), c.stride(0), M, N, K,
              ptr(bias), ptr(aux), aux.stride(0) if aux is not None else 0, ptr(res),
              res.stride(0) if res is not None else 0, 1.0, int(act), float(rate), ptr(seed), int(site), stream_ptr())
 
 
-# K in {128, 256, 384} take the weight-stationary kernel (every ViT-small product: fwd qkv / out / fc1 /
-# fc2 and the dgrads, C2's M = 64 * 257 and C1's M = 32 * 50), other K the tiled one
+# K = 128 with N >= 256 take the panel form (C2's M = 64 * 257 = 256 panels + a 64-row tail, 32896 = two
+# panels per CU + a 128-row tail, 16453 / 1000 a partial tail strip, 1600 no tail), every other shape the
+# tiled one; "tiled" forces the tiled kernel on the same shapes
 @pytest.mark.parametrize("M,N,K,tb", [(16448, 128, 128, 0), (16448, 384, 128, 0), (1000, 256, 128, 0),
                                       (16448, 128, 256, 1), (77, 128, 384, 1), (64, 128, 64, 0),
                                       (16448, 256, 128, 1), (16448, 128, 384, 1), (16448, 128, 256, 0),
-                                      (1600, 384, 128, 0), (16, 128, 128, 1), (3000, 128, 192, 0)])
+                                      (1600, 384, 128, 0), (16, 128, 128, 1), (3000, 128, 192, 0),
+                                      (32896, 256, 128, 1), (16453, 256, 128, 1), (16453, 384, 128, 0)])
+@pytest.mark.parametrize("form", ["auto", "tiled"])
 @pytest.mark.parametrize("mode", ["plain", "bias_res", "gelu_drop", "bias_drop_res", "gelubwd_drop"])
-def test_gemm_f32_rows(dev, M, N, K, tb, mode):
+def test_gemm_f32_rows(dev, M, N, K, tb, mode, form):
     from plaincv_amd.models.vit_f32 import _epi, _epi_bwd
+    if form == "tiled" and mode not in ("plain", "gelu_drop", "gelubwd_drop"):
+        pytest.skip("the tiled form's epilogue modes are covered by the shapes it runs under auto")
     g = torch.Generator().manual_seed(M + N + K + tb)
     a = torch.randn(M, K, generator=g).to(dev)
     b = (torch.randn(N, K, generator=g) if tb else torch.randn(K, N, generator=g)).to(dev) * K ** -0.5
@@ -38,7 +43,7 @@ def test_gemm_f32_rows(dev, M, N, K, tb, mode):
     seed = torch.tensor([12345], dtype=torch.int32, device=dev)
     c = torch.full((M, N), float("nan"), device=dev)
     aux = (torch.randn(M, N, generator=g).to(dev) * 2 if bwd else torch.zeros(M, N, device=dev)) if act else None
-    _rows(a, b, tb, c, bias, aux, res, act, rate, seed, site=7)
+    _rows(a, b, tb, c, bias, aux, res, act, rate, seed, site=7, form=form)
     x = (a.double() @ (b.double().t() if tb else b.double())).float()
     ref = torch.empty_like(c)
     aux_ref = (aux.clone() if bwd else torch.zeros(M, N, device=dev)) if act else None
@@ -67,3 +72,17 @@ def test_gemm_f32_rows_rejects_bad_shapes(dev):
     assert not hip.load().pcv_gemm_f32_rows_ok(100, 128, 48, ptr(a), 48, ptr(b), 128, 0)   # K % 32
     b2 = torch.zeros(32, 200, device=dev)
     assert not hip.load().pcv_gemm_f32_rows_ok(100, 200, 32, ptr(a), 48, ptr(b2), 200, 0)  # N % 128
+
+
+def test_gemm_f32_rows_panel_form_covers_the_vit(dev):
+    """The fp32 ViT-small products the panel form measured faster on (K = 128, N >= 256: qkv, fc1 and
+    the GELU backward) take it at C2 / C4's B 64 (M = 64 * 257) and C1's B 32 x T 50; the others stay
+    on the tiled form."""
+    from plaincv_amd import hip
+    lib = hip.load()
+    for M in (64 * 257, 32 * 50):
+        for N, K in ((384, 128), (256, 128)):
+            assert lib.pcv_gemm_f32_rows_form(M, N, K) == 1, (M, N, K)
+        for N, K in ((128, 128), (128, 256), (128, 384)):
+            assert lib.pcv_gemm_f32_rows_form(M, N, K) == 0, (M, N, K)
+    assert lib.pcv_gemm_f32_rows_form(16, 384, 128) == 0 and lib.pcv_gemm_f32_rows_form(16448, 384, 192) == 0

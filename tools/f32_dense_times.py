@@ -29,18 +29,23 @@ def main():
     seed = r.seed
     tot = 0.0
     rows = []
+    tot_t = 0.0
     for name, d in list(r.gf[1].items()) + list(r.gb[1].items()):
         if d is None or not hasattr(d, "M"):
             continue
         t = bench.timed_kernel(lambda: d.run(0.1, seed), iters=30)
-        fl = 2 * d.M * d.N * d.K
-        rows.append((name, d.M, d.N, d.K, d.fused, t))
+        d.entry = "pcv_gemm_f32_rows_tiled"
+        tt = bench.timed_kernel(lambda: d.run(0.1, seed), iters=30)
+        del d.entry
+        rows.append((name, d.M, d.N, d.K, d.fused, t, tt))
         tot += t
-    for name, M, N, K, fused, t in rows:
+        tot_t += tt
+    for name, M, N, K, fused, t, tt in rows:
         fl = 2 * M * N * K
         print(f"{name:6s} M={M} N={N:4d} K={K:4d} fused={int(fused)} {t * 1e6:8.2f} us {fl / t / 1e12:7.1f} TF "
-              f"{fl / t / 1e12 / bench.F32_PEAK_TFLOPS:.3f}", flush=True)
-    print(f"row GEMMs of one layer: {tot * 1e6:.1f} us; x{m.num_layers} layers = {tot * 1e6 * m.num_layers:.1f} us")
+              f"{fl / t / 1e12 / bench.F32_PEAK_TFLOPS:.3f}   tiled form {tt * 1e6:8.2f} us", flush=True)
+    print(f"row GEMMs of one layer: {tot * 1e6:.1f} us (tiled form {tot_t * 1e6:.1f}); x{m.num_layers} layers = "
+          f"{tot * 1e6 * m.num_layers:.1f} us")
     ta = bench.timed_kernel(lambda: r.attn_bwd(1, 0.1), iters=30)
     print(f"attn_bwd {ta * 1e6:.2f} us {4 * 2 * B * r.H * r.T ** 2 * r.Dh / ta / 1e12:.1f} TF (4 products)")
     tw = sum(bench.timed_kernel(p.run, iters=20) for p in r.g_wgrad_parts)
