@@ -281,6 +281,21 @@ int pcv_vit_embed_fwd_f32(const float* patch, const float* bias, const float* cl
                           int T, int D, float rate, const uint32_t* seed, uint32_t site, void* stream);
 int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls, float* dpos, int B, int T, int D, float rate,
                           const uint32_t* seed, uint32_t site, void* stream);
+/* Fused fp32 patch embedding (models/vit_small.py:78-109): x[b, t] = dropout(t == 0 ? cls + pos[0] :
+ * pos[t] + (patch(b, t - 1) . w + bias)) straight from the uint8 images (patch = the (kh, kw, c) flatten
+ * / 255, w = Conv_0/kernel as [patch*patch*C][D]) -- pcv_vit_patchify_f32 + the patch GEMM +
+ * pcv_vit_embed_fwd_f32 in one launch, same element order and dropout index.  Its VJP: dpos += sum_b g,
+ * dcls += sum_b g[b, 0], gw += patches^T g[:, 1:], gbias += column sums of g[:, 1:] (g =
+ * dropout_vjp(dx)), through ws (pcv_vit_patch_embed_bwd_f32_ws floats) in a fixed order.  ok: patch *
+ * patch * C <= 48, D % 4 == 0, the LDS images fit (B <= ~200 at C = 3). */
+int pcv_vit_patch_embed_f32_ok(int B, int H, int W, int C, int patch, int D);
+int64_t pcv_vit_patch_embed_bwd_f32_ws(int B, int H, int W, int C, int patch, int D);
+int pcv_vit_patch_embed_fwd_f32(const uint8_t* img, const float* w, const float* bias, const float* cls,
+                                const float* pos, float* x, int B, int H, int W, int C, int patch, int D, float rate,
+                                const uint32_t* seed, uint32_t site, void* stream);
+int pcv_vit_patch_embed_bwd_f32(const float* dx, const uint8_t* img, float* dcls, float* dpos, float* ws, float* gw,
+                                float* gbias, int B, int H, int W, int C, int patch, int D, float rate,
+                                const uint32_t* seed, uint32_t site, void* stream);
 /* Exact-fp32 row-panel GEMM with the Dense epilogue fused (csrc/gemm_f32.hip): C[M][N] =
  * dropout(act(A[M][K] op(B) + bias)) + res_scale * res, op(B) = B [K][N] (tb = 0) or B^T with B
  * stored [N][K] (tb = 1); aux = the pre-activation when act = 1 (GELU tanh); act = 2 is the backward of

@@ -377,6 +377,187 @@ __global__ __launch_bounds__(256) void vit_embed_bwd_f32_kernel(const float* dx,
 }
 
 // ---------------------------------------------------------------------------------------------
+// Fused patch embedding (models/vit_small.py:78-109 in fp32): patchify (the (kh, kw, c) flatten of a
+// ps x ps patch, / 255), the patch conv as a K = ps*ps*C product (VALU fp32 FMAs in k order: K is 16-48,
+// too short for an MFMA tile to pay), + bias, the cls / pos assembly and the embedding dropout --
+// one launch instead of patchify + a grouped GEMM + the assembly kernel.  Block: PE_TT tokens of one
+// image; the conv weight and the block's patches staged in LDS; shapes are template parameters (the
+// runtime-divisor index math of a generic version cost more than the product: 24 us).  The element
+// order of the assembly is vit_embed_fwd_f32's: pos + (conv + bias), dropout index (b T + t) D + d.
+constexpr int PE_TT = 32;   // tokens per forward block
+
+// Stage patches [n][KP] (floats, the (kh, kw, c) order / 255) of tokens t0 + r (patch t0 + r - 1 of
+// image b; zero rows outside 1 .. T-1) from the uint8 image: a patch row is PS*C contiguous bytes, read
+// as 4-byte words (the host checks the alignment), so there is one image load per 4 pixels.
+template <int PS, int C>
+__device__ __forceinline__ void pe_stage(const uint8_t* __restrict__ img, float* Ps, int n, int b_of_row0, bool per_row_b,
+                                         int t0, int T, int Hh, int Ww, int tid, int nthr) {
+  constexpr int KP = PS * PS * C, RW = PS * C / 4, NW = PS * RW;
+  const int gw = Ww / PS;
+  for (int i = tid; i < n * NW; i += nthr) {
+    const int r = i / NW, wd = i % NW, kh = wd / RW, q = wd % RW;
+    const int b = per_row_b ? r : b_of_row0, t = per_row_b ? t0 : t0 + r;
+    uint32_t v = 0;
+    if (t >= 1 && t < T) {
+      const int p = t - 1, ph = p / gw, pw = p - ph * gw;
+      v = *reinterpret_cast<const uint32_t*>(img + (((int64_t)b * Hh + ph * PS + kh) * Ww + pw * PS) * C + 4 * q);
+    }
+    float* o = Ps + r * KP + kh * PS * C + 4 * q;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (float)((v >> (8 * e)) & 255u) / 255.f;
+  }
+}
+
+template <int PS, int C, int D>
+__global__ __launch_bounds__(256) void patch_embed_fwd_f32_kernel(const uint8_t* __restrict__ img,
+                                                                  const float* __restrict__ W,
+                                                                  const float* __restrict__ bias,
+                                                                  const float* __restrict__ cls,
+                                                                  const float* __restrict__ pos, float* __restrict__ x,
+                                                                  int Hh, int Ww, int T, uint32_t thresh, float scale,
+                                                                  const uint32_t* seedp, uint32_t site) {
+  constexpr int KP = PS * PS * C, D4 = D / 4, RS = 256 / D4, RT = PE_TT / RS;
+  static_assert(256 % D4 == 0 && PE_TT % RS == 0, "thread -> (column group, RT tokens)");
+  __shared__ __attribute__((aligned(16))) float Ws[KP * D];
+  __shared__ float Ps[PE_TT * KP];
+  const int ngrp = (T + PE_TT - 1) / PE_TT;
+  const int b = (int)blockIdx.x / ngrp, t0 = ((int)blockIdx.x % ngrp) * PE_TT;
+  for (int i = threadIdx.x; i < KP * D4; i += 256)
+    reinterpret_cast<f32x4*>(Ws)[i] = reinterpret_cast<const f32x4*>(W)[i];
+  pe_stage<PS, C>(img, Ps, PE_TT, b, false, t0, T, Hh, Ww, threadIdx.x, 256);
+  __syncthreads();
+  const uint32_t seed = thresh ? *seedp : 0u;
+  // thread -> one float4 column group d and the tokens r0, r0 + RS, ...: each weight float4 read from
+  // LDS feeds all of the thread's tokens
+  const int d = (threadIdx.x % D4) * 4, r0 = threadIdx.x / D4;
+  f32x4 acc[RT];
+#pragma unroll
+  for (int j = 0; j < RT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+  for (int k = 0; k < KP; ++k) {
+    const f32x4 w4 = *reinterpret_cast<const f32x4*>(Ws + k * D + d);
+#pragma unroll
+    for (int j = 0; j < RT; ++j) acc[j] += Ps[(r0 + j * RS) * KP + k] * w4;
+  }
+#pragma unroll
+  for (int j = 0; j < RT; ++j) {
+    const int t = t0 + r0 + j * RS;
+    if (t >= T) continue;
+    f32x4 v = *reinterpret_cast<const f32x4*>(pos + (int64_t)t * D + d);
+    if (t == 0) v += *reinterpret_cast<const f32x4*>(cls + d);
+    else v += acc[j] + *reinterpret_cast<const f32x4*>(bias + d);
+    const int64_t bt = (int64_t)b * T + t;
+    if (thresh) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = keep_of(seed, site, (uint32_t)(bt * D + d + e), thresh) ? v[e] * scale : 0.f;
+    }
+    *reinterpret_cast<f32x4*>(x + bt * D + d) = v;
+  }
+}
+
+// Its VJP.  Block = token t (every image, every column), 512 threads: g = dropout_vjp(dx[b, t]) staged
+// in LDS with the token's patches; dpos[t] += sum_b g (and dcls for t = 0), and for t >= 1 the token's
+// partials of the conv weight and bias gradients, ws[t - 1][k][d] = sum_b patch(b, t - 1)[k] g[b][d]
+// (k < KP) and ws[t - 1][KP][d] = sum_b g[b][d] -- fixed summation orders (the batch sums as 512 / D
+// contiguous runs added in run order); patch_embed_fold_kernel adds the token partials in token order
+// (no atomics: run-to-run identical).
+constexpr int PB_THREADS = 512;
+template <int PS, int C, int D>
+__global__ __launch_bounds__(PB_THREADS) void patch_embed_bwd_f32_kernel(const float* __restrict__ dx,
+                                                                         const uint8_t* __restrict__ img, float* dcls,
+                                                                         float* dpos, float* __restrict__ ws, int B,
+                                                                         int Hh, int Ww, int T, uint32_t thresh,
+                                                                         float scale, const uint32_t* seedp,
+                                                                         uint32_t site) {
+  constexpr int KP = PS * PS * C, D4 = D / 4, NG = PB_THREADS / D, IT = (KP * D4 + PB_THREADS - 1) / PB_THREADS;
+  static_assert(PB_THREADS % D == 0, "column-sum groups");
+  extern __shared__ __attribute__((aligned(16))) float pb_lds[];   // g [B][D], patches [B][KP], red [NG][D]
+  const int t = (int)blockIdx.x;
+  float* G = pb_lds;
+  float* Ps = pb_lds + B * D;
+  float* red = Ps + B * KP;
+  const uint32_t seed = thresh ? *seedp : 0u;
+  for (int i = threadIdx.x; i < B * D4; i += PB_THREADS) {
+    const int bb = i / D4, d = (i % D4) * 4;
+    const int64_t idx = ((int64_t)bb * T + t) * D + d;
+    f32x4 g = *reinterpret_cast<const f32x4*>(dx + idx);
+    if (thresh) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) g[e] = keep_of(seed, site, (uint32_t)(idx + e), thresh) ? g[e] * scale : 0.f;
+    }
+    *reinterpret_cast<f32x4*>(G + bb * D + d) = g;
+  }
+  if (t > 0) pe_stage<PS, C>(img, Ps, B, 0, true, t, T, Hh, Ww, threadIdx.x, PB_THREADS);
+  __syncthreads();
+  {   // column sums over the batch: NG contiguous runs of b, then the runs in order
+    const int d = threadIdx.x % D, q = threadIdx.x / D, bc = (B + NG - 1) / NG;
+    float v = 0.f;
+    for (int bb = q * bc; bb < min(B, (q + 1) * bc); ++bb) v += G[bb * D + d];
+    red[q * D + d] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < D) {
+    const int d = threadIdx.x;
+    float v = red[d];
+#pragma unroll
+    for (int q = 1; q < NG; ++q) v += red[q * D + d];
+    dpos[(int64_t)t * D + d] += v;
+    if (t == 0) dcls[d] += v;
+    else ws[((int64_t)(t - 1) * (KP + 1) + KP) * D + d] = v;
+  }
+  if (t == 0) return;
+  f32x4 acc[IT];
+#pragma unroll
+  for (int j = 0; j < IT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int bb = 0; bb < B; ++bb) {
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+      const int i = threadIdx.x + PB_THREADS * j;
+      if (i < KP * D4) acc[j] += Ps[bb * KP + i / D4] * *reinterpret_cast<const f32x4*>(G + bb * D + (i % D4) * 4);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < IT; ++j) {
+    const int i = threadIdx.x + PB_THREADS * j;
+    if (i < KP * D4) *reinterpret_cast<f32x4*>(ws + ((int64_t)(t - 1) * (KP + 1) + i / D4) * D + (i % D4) * 4) = acc[j];
+  }
+}
+
+// gW[k][d] += sum_t ws[t][k][d] (k < Kp), gbias[d] += sum_t ws[t][Kp][d], t = 0 .. NT-1 in order of 32
+// interleaved partial sums (thread group q sums t = q, q + 32, ...) combined in q order through LDS.
+__global__ __launch_bounds__(256) void patch_embed_fold_kernel(const float* __restrict__ ws, float* gW, float* gbias,
+                                                               int NT, int Kp, int D) {
+  __shared__ f32x4 part[32][8];
+  const int D4 = D / 4, nout = (Kp + 1) * D4;
+  const int o = (int)blockIdx.x * 8 + (threadIdx.x & 7), q = threadIdx.x >> 3;
+  f32x4 acc{0.f, 0.f, 0.f, 0.f};
+  if (o < nout) {
+    const int k = o / D4, d = (o % D4) * 4;
+    const float* p = ws + (int64_t)k * D + d;
+    const int64_t st = (int64_t)(Kp + 1) * D;
+    int t = q;
+    for (; t + 32 * 3 < NT; t += 32 * 4) {
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(p + t * st);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(p + (t + 32) * st);
+      const f32x4 a2 = *reinterpret_cast<const f32x4*>(p + (t + 64) * st);
+      const f32x4 a3 = *reinterpret_cast<const f32x4*>(p + (t + 96) * st);
+      acc += a0; acc += a1; acc += a2; acc += a3;
+    }
+    for (; t < NT; t += 32) acc += *reinterpret_cast<const f32x4*>(p + t * st);
+  }
+  part[q][threadIdx.x & 7] = acc;
+  __syncthreads();
+  if (threadIdx.x < 8 && o < nout) {
+    f32x4 v = part[0][threadIdx.x];
+#pragma unroll
+    for (int i = 1; i < 32; ++i) v += part[i][threadIdx.x];
+    const int k = o / D4, d = (o % D4) * 4;
+    float* dst = k < Kp ? gW + (int64_t)k * D + d : gbias + d;
+    *reinterpret_cast<f32x4*>(dst) = *reinterpret_cast<const f32x4*>(dst) + v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Fused fp32 attention for the ViT shapes (head_dim 32, T <= 272): one workgroup of 16 waves per
 // (batch, head), Q/K/V (and dO) of the head staged once in swizzled LDS images, every product on
 // v_mfma_f32_16x16x4_f32.  No [B*H, T, T] score tensor: the forward keeps the row max m and
@@ -1366,6 +1547,83 @@ extern "C" int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls
                      (hipStream_t)stream, dx, dpatch, dcls, dpos, B, T, D, th, sc, seed, site);
   return pcv_launch_status();
 }
+
+// ---- fused patch embedding ----
+// instantiated shapes: (patch, C, D) = (4, 3, 128) the ViT-small on Tiny-ImageNet, (4, 1, 128) on
+// Fashion-MNIST, (4, 3, 64) a small test model
+static int pe_shape(int patch, int C, int D) {
+  if (patch == 4 && C == 3 && D == 128) return 1;
+  if (patch == 4 && C == 1 && D == 128) return 2;
+  if (patch == 4 && C == 3 && D == 64) return 3;
+  return 0;
+}
+static int pe_lds_bwd(int B, int Kp, int D) { return (B * (D + Kp) + PB_THREADS) * 4; }
+
+extern "C" int pcv_vit_patch_embed_f32_ok(int B, int H, int W, int C, int patch, int D) {
+  if (B <= 0 || C <= 0 || patch <= 0 || H % patch || W % patch || !pe_shape(patch, C, D) || (W * C) % 4) return 0;
+  return pe_lds_bwd(B, patch * patch * C, D) <= 65536 ? 1 : 0;
+}
+
+extern "C" int64_t pcv_vit_patch_embed_bwd_f32_ws(int B, int H, int W, int C, int patch, int D) {
+  if (!pcv_vit_patch_embed_f32_ok(B, H, W, C, patch, D)) return 0;
+  return (int64_t)(H / patch) * (W / patch) * (patch * patch * C + 1) * D;
+}
+
+#define PE_DISPATCH(sh, FN)                   \
+  switch (sh) {                               \
+    case 1: FN(4, 3, 128); break;             \
+    case 2: FN(4, 1, 128); break;             \
+    default: FN(4, 3, 64); break;             \
+  }
+
+extern "C" int pcv_vit_patch_embed_fwd_f32(const uint8_t* img, const float* w, const float* bias, const float* cls,
+                                           const float* pos, float* x, int B, int H, int W, int C, int patch, int D,
+                                           float rate, const uint32_t* seed, uint32_t site, void* stream) {
+  if (!pcv_vit_patch_embed_f32_ok(B, H, W, C, patch, D) || !img || !w || !bias || !cls || !pos || !x ||
+      rate < 0.f || rate >= 1.f || (rate > 0.f && !seed))
+    return PCV_EINVAL;
+  if (((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(cls) |
+        reinterpret_cast<uintptr_t>(pos) | reinterpret_cast<uintptr_t>(x)) & 15) ||
+      (reinterpret_cast<uintptr_t>(img) & 3))
+    return PCV_EALIGN;
+  const int T = (H / patch) * (W / patch) + 1;
+  uint32_t th; float sc;
+  f32_drop(rate, &th, &sc);
+  const dim3 grid((unsigned)(B * ((T + PE_TT - 1) / PE_TT)));
+#define PE_FWD(P, CC, DD)                                                                                    \
+  hipLaunchKernelGGL((patch_embed_fwd_f32_kernel<P, CC, DD>), grid, dim3(256), 0, (hipStream_t)stream, img, w, \
+                     bias, cls, pos, x, H, W, T, th, sc, seed, site)
+  PE_DISPATCH(pe_shape(patch, C, D), PE_FWD)
+#undef PE_FWD
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_vit_patch_embed_bwd_f32(const float* dx, const uint8_t* img, float* dcls, float* dpos, float* ws,
+                                           float* gw, float* gbias, int B, int H, int W, int C, int patch, int D,
+                                           float rate, const uint32_t* seed, uint32_t site, void* stream) {
+  if (!pcv_vit_patch_embed_f32_ok(B, H, W, C, patch, D) || !dx || !img || !dcls || !dpos || !ws || !gw || !gbias ||
+      rate < 0.f || rate >= 1.f || (rate > 0.f && !seed))
+    return PCV_EINVAL;
+  if (((reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(ws) | reinterpret_cast<uintptr_t>(gw) |
+        reinterpret_cast<uintptr_t>(gbias)) & 15) ||
+      (reinterpret_cast<uintptr_t>(img) & 3))
+    return PCV_EALIGN;
+  const int T = (H / patch) * (W / patch) + 1, Kp = patch * patch * C;
+  uint32_t th; float sc;
+  f32_drop(rate, &th, &sc);
+  hipStream_t s = (hipStream_t)stream;
+  const int lds = pe_lds_bwd(B, Kp, D);
+#define PE_BWD(P, CC, DD)                                                                                     \
+  hipLaunchKernelGGL((patch_embed_bwd_f32_kernel<P, CC, DD>), dim3((unsigned)T), dim3(PB_THREADS), lds, s, dx, \
+                     img, dcls, dpos, ws, B, H, W, T, th, sc, seed, site)
+  PE_DISPATCH(pe_shape(patch, C, D), PE_BWD)
+#undef PE_BWD
+  const int nout = (Kp + 1) * (D / 4);
+  hipLaunchKernelGGL(patch_embed_fold_kernel, dim3((unsigned)((nout + 7) / 8)), dim3(256), 0, s, ws, gw, gbias, T - 1,
+                     Kp, D);
+  return pcv_launch_status();
+}
+#undef PE_DISPATCH
 
 // ---- fused fp32 attention (head_dim 32, T <= 272) ----
 extern "C" int pcv_attn_fused_f32_ok(int T, int head_dim) { return T >= 1 && T <= FA_TMAX && head_dim == FA_DH; }

@@ -115,7 +115,14 @@ class ViTRunnerF32:
         dev = torch.device(device)
         z = lambda *sh: torch.zeros(*sh, dtype=torch.float32, device=dev)  # noqa: E731
         BH = B * H
-        self.patches, self.patch_out = z(B * self.hw, self.Kp), z(B * self.hw, D)
+        # the fused patch embedding reads the uint8 images itself (no patches / conv-output buffers)
+        lib = hip.load()
+        self.pe_fused = bool(lib.pcv_vit_patch_embed_f32_ok(B, Hh, Ww, C, ps, D))
+        if self.pe_fused:
+            self.pe_ws = z(max(int(lib.pcv_vit_patch_embed_bwd_f32_ws(B, Hh, Ww, C, ps, D)), 4))
+            self.images = None   # the batch the forward read (its backward reads the same pixels)
+        else:
+            self.patches, self.patch_out = z(B * self.hw, self.Kp), z(B * self.hw, D)
         self.xs = [z(R, D) for _ in range(L + 1)]
         self.x1s = [z(R, D) for _ in range(L)]
         nrm = model.use_layernorm or self.bn
@@ -161,7 +168,8 @@ class ViTRunnerF32:
         self.ln_ws = z(2 * L + 1, max(K.layernorm_bwd_f32_ws(R, D), 1))
         self.dqkv, self.dy0 = z(R, 3 * D), z(R, D)
         self.dxo = [z(R, D) for _ in range(L)]
-        self.dpatch = z(B * self.hw, D)
+        if not self.pe_fused:
+            self.dpatch = z(B * self.hw, D)
         self._views()
         self._plan()
 
@@ -212,7 +220,7 @@ class ViTRunnerF32:
         B, H, T, D = self.B, self.H, self.T, self.D
         sc = 1.0 / math.sqrt(self.Dh)
         f = lambda g: g.finalize(dev)  # noqa: E731
-        self.g_patch = f(_gemm(self.patches, self.Wconv, self.patch_out))
+        self.g_patch = None if self.pe_fused else f(_gemm(self.patches, self.Wconv, self.patch_out))
         self.g_head = f(_gemm(self.yf, self.Wh, self.logits))
         self.g_head_d = f(_gemm(self.dlogits, self.Wh, self.dyf, tb=True))
         L = self.m.num_layers
@@ -253,6 +261,11 @@ class ViTRunnerF32:
                                 out_d=_Dense(self.dx1_l[i], w["Wo"], self.dO, tb=True), dpv=att.get("dpv"),
                                 dqk=att.get("dqk"),
                                 qkv_d=_Dense(dqkv, w["Wqkv"], self.dy0, tb=True)))
+        # block 0's qkv product runs beside the previous step's Newton-Schulz phase when the optimizer
+        # overlaps it (GraphedTrainStep overlap_opt, joined before block 0's fc1): the panel form's
+        # persistent grid (one workgroup per CU) then waits for CUs the side stream holds (37.6 vs 24.5 us
+        # in profiles/r05o_vit_c2_f32_step_timeline.txt), so that launch takes the tiled form
+        self.gf[0]["qkv"].entry = "pcv_gemm_f32_rows_tiled"
         # every weight gradient (K = B*T rows) in one grouped launch at the end of backward
         # (split-K: a [D, N] gradient is only a few 64x64 tiles, so each tile's K = B*T sum is cut
         # into ~1024-long slices accumulated with fp32 atomics -- ~2k workgroups instead of 138)
@@ -262,7 +275,9 @@ class ViTRunnerF32:
         ks = lambda t: max(1, t.shape[0] // 256)  # noqa: E731   (few tiles: a deep K split)
         # (+ the bias gradient = column sums of the same output gradient, folded into the row-panel
         # launch where the product fits it; otherwise a colsum launch in the backward)
-        prods = [(self.yf, self.dlogits, self.gWh, self.gbh), (self.patches, self.dpatch, self.gWconv, self.gbconv)]
+        prods = [(self.yf, self.dlogits, self.gWh, self.gbh)]
+        if not self.pe_fused:   # (else the fused embedding VJP forms the conv gradients)
+            prods.append((self.patches, self.dpatch, self.gWconv, self.gbconv))
         for i in range(L):
             w = self.w[i]
             prods += [(self.a[i], self.dmo_l[i], w["gW1"], w["gb1"]), (self.y1[i], self.da_l[i], w["gW0"], w["gb0"]),
@@ -270,7 +285,8 @@ class ViTRunnerF32:
         self.colsum_folded = set()
         # one workspace for every stand-alone bias column sum (they run one after another)
         self.colsum_ws = torch.zeros(max(K.colsum_ws_floats(B * T, max(3 * D, self.M, self.Kc)),
-                                         K.colsum_ws_floats(B * self.hw, D), 1), dtype=torch.float32, device=dev)
+                                         0 if self.pe_fused else K.colsum_ws_floats(B * self.hw, D), 1),
+                                     dtype=torch.float32, device=dev)
         for a, b, c, gb in prods:
             if WgradF32.fits(a, b, c):
                 fold = gb.is_contiguous() and gb.numel() == b.shape[1]
@@ -337,11 +353,17 @@ class ViTRunnerF32:
         seed = self.seed
         if labels is not None:
             self.labels.copy_(labels, non_blocking=True)
-        hip.call("pcv_vit_patchify_f32", ptr(images), ptr(self.patches), B, self.Hh, self.Ww, self.C, m.patch_size,
-                 stream_ptr())
-        self.g_patch.run()
-        hip.call("pcv_vit_embed_fwd_f32", ptr(self.patch_out), ptr(self.bconv), ptr(self.cls), ptr(self.pos),
-                 ptr(self.xs[0]), B, T, D, float(rate), ptr(seed), SITE_EMBED, stream_ptr())
+        if self.pe_fused:   # patchify + conv + bias + cls / pos + dropout in one launch
+            self.images = images
+            hip.call("pcv_vit_patch_embed_fwd_f32", ptr(images), ptr(self.Wconv), ptr(self.bconv), ptr(self.cls),
+                     ptr(self.pos), ptr(self.xs[0]), B, self.Hh, self.Ww, self.C, m.patch_size, D, float(rate),
+                     ptr(seed), SITE_EMBED, stream_ptr())
+        else:
+            hip.call("pcv_vit_patchify_f32", ptr(images), ptr(self.patches), B, self.Hh, self.Ww, self.C, m.patch_size,
+                     stream_ptr())
+            self.g_patch.run()
+            hip.call("pcv_vit_embed_fwd_f32", ptr(self.patch_out), ptr(self.bconv), ptr(self.cls), ptr(self.pos),
+                     ptr(self.xs[0]), B, T, D, float(rate), ptr(seed), SITE_EMBED, stream_ptr())
         if rate > 0.0:
             K.attn_drop_mask(seed, site_attn(0), T, rate, self.attn_mask, layers=m.num_layers,
                              site_stride=site_attn(1) - site_attn(0))
@@ -450,9 +472,14 @@ class ViTRunnerF32:
             else:
                 _epi(self.dy0, self.dxo[i], res=dx1)
             dx_in = self.dxo[i]
-        hip.call("pcv_vit_embed_bwd_f32", ptr(dx_in), ptr(self.dpatch), ptr(self.gcls), ptr(self.gpos), B, T, D,
-                 float(rate), ptr(seed), SITE_EMBED, stream_ptr())
-        self._colsum(self.dpatch, self.gbconv)
+        if self.pe_fused:   # dpos, dcls and the conv weight / bias gradients from the same images
+            hip.call("pcv_vit_patch_embed_bwd_f32", ptr(dx_in), ptr(self.images), ptr(self.gcls), ptr(self.gpos),
+                     ptr(self.pe_ws), ptr(self.gWconv), ptr(self.gbconv), B, self.Hh, self.Ww, self.C, m.patch_size, D,
+                     float(rate), ptr(seed), SITE_EMBED, stream_ptr())
+        else:
+            hip.call("pcv_vit_embed_bwd_f32", ptr(dx_in), ptr(self.dpatch), ptr(self.gcls), ptr(self.gpos), B, T, D,
+                     float(rate), ptr(seed), SITE_EMBED, stream_ptr())
+            self._colsum(self.dpatch, self.gbconv)
         for part in self.g_wgrad_parts:
             part.run()
         if self.ln_red is not None:
