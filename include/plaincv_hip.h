@@ -281,6 +281,23 @@ int pcv_vit_embed_fwd_f32(const float* patch, const float* bias, const float* cl
                           int T, int D, float rate, const uint32_t* seed, uint32_t site, void* stream);
 int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls, float* dpos, int B, int T, int D, float rate,
                           const uint32_t* seed, uint32_t site, void* stream);
+/* Fused fp32 classifier head (models/vit_small.py:111-127 + the softmax cross-entropy of
+ * flax_engine.py:38-44): per cls row b (x + b ldx), yf = LayerNorm(x; scale, bias, eps) (+ mean / rstd),
+ * logits = yf wh + bh (wh [D][Kc]), row_loss = lse - logits[label], row_correct = argmax == label (lowest
+ * index on ties), dlogits = (softmax - onehot) grad_scale (NULL: none).  Its VJP: dyf = dlogits wh^T, the
+ * LayerNorm VJP into dx's cls rows (dx + b lddx), the LayerNorm parameter partials part [B][2 D] =
+ * [dyf xhat | dyf] (for pcv_layernorm_part_reduce with B partial rows), gwh += yf^T dlogits, gbh +=
+ * column sums of dlogits -- fixed summation orders.  wh / gwh rows ldw / ldgw apart (the ParamStore pads
+ * rows to 8).  ok: D <= 256, D % 16 == 0, Kc <= 1024 (and B <= 1024 for the VJP). */
+int pcv_vit_head_f32_ok(int D, int Kc);
+int pcv_vit_head_fwd_f32(const float* x, int64_t ldx, const float* scale, const float* bias, const float* wh,
+                         int64_t ldw, const float* bh, const int* labels, float* yf, float* mean, float* rstd,
+                         float* logits, float* row_loss, float* row_correct, float* dlogits, int B, int D, int Kc,
+                         float eps, float grad_scale, void* stream);
+int pcv_vit_head_bwd_f32(const float* dlogits, const float* wh, int64_t ldw, const float* x, int64_t ldx,
+                         const float* scale, const float* mean, const float* rstd, const float* yf, float* dx,
+                         int64_t lddx, float* part, float* gwh, int64_t ldgw, float* gbh, int B, int D, int Kc,
+                         void* stream);
 /* Fused fp32 patch embedding (models/vit_small.py:78-109): x[b, t] = dropout(t == 0 ? cls + pos[0] :
  * pos[t] + (patch(b, t - 1) . w + bias)) straight from the uint8 images (patch = the (kh, kw, c) flatten
  * / 255, w = Conv_0/kernel as [patch*patch*C][D]) -- pcv_vit_patchify_f32 + the patch GEMM +

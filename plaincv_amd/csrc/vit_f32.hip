@@ -558,6 +558,202 @@ __global__ __launch_bounds__(256) void patch_embed_fold_kernel(const float* __re
 }
 
 // ---------------------------------------------------------------------------------------------
+// Fused classifier head of the fp32 ViT (models/vit_small.py:111-127 + flax_engine's loss): per cls
+// row b, the final LayerNorm (ln16_fwd_f32's math: fast variance clipped at 0, eps), logits = y Wh + bh
+// (fp32 FMAs in k order), the softmax cross-entropy with the row loss, the argmax hit (lowest index on
+// ties, as xent_kernel) and dlogits = (softmax - onehot) grad_scale -- one launch for the LayerNorm,
+// head GEMM, bias epilogue and loss kernels.  Block = row, 256 threads; D <= 256, Kc <= 1024.
+constexpr int HD_THREADS = 256;
+__device__ __forceinline__ float hd_block_sum(float v, float* red) {   // fixed order: waves in index order
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < HD_THREADS / 64; ++i) s += red[i];
+  return s;
+}
+
+__global__ __launch_bounds__(HD_THREADS) void vit_head_fwd_f32_kernel(
+    const float* __restrict__ x, int64_t ldx, const float* __restrict__ scale, const float* __restrict__ bias,
+    const float* __restrict__ Wh, int64_t ldw, const float* __restrict__ bh, const int* __restrict__ labels,
+    float* yf, float* mean, float* rstd, float* logits, float* row_loss, float* row_correct, float* dlogits, int D,
+    int Kc, float eps, float grad_scale) {
+  __shared__ __attribute__((aligned(16))) float ys[256];
+  __shared__ float zs[1024];
+  __shared__ float red[HD_THREADS / 64];
+  __shared__ float sm[HD_THREADS / 64];
+  __shared__ int si[HD_THREADS / 64];
+  const int b = blockIdx.x, D4 = D / 4, lane = threadIdx.x & 63;
+  // the LayerNorm on wave 0 (one float4 of the row per lane)
+  if (threadIdx.x < 64) {
+    f32x4 v{0.f, 0.f, 0.f, 0.f};
+    if (lane < D4) v = *reinterpret_cast<const f32x4*>(x + (int64_t)b * ldx + 4 * lane);
+    float s1 = v[0] + v[1] + v[2] + v[3];
+    float s2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    const float mu = s1 / D, rs = rsqrtf(fmaxf(s2 / D - mu * mu, 0.f) + eps);
+    if (lane < D4) {
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(scale + 4 * lane), bi = *reinterpret_cast<const f32x4*>(bias + 4 * lane);
+      const f32x4 y = (v - mu) * rs * sc + bi;
+      *reinterpret_cast<f32x4*>(ys + 4 * lane) = y;
+      *reinterpret_cast<f32x4*>(yf + (int64_t)b * D + 4 * lane) = y;
+    }
+    if (lane == 0) { mean[b] = mu; rstd[b] = rs; }
+  }
+  __syncthreads();
+  float m = -3.0e38f;
+  int am = 0x7fffffff;
+  for (int c = threadIdx.x; c < Kc; c += HD_THREADS) {
+    float acc = 0.f;
+    for (int k0 = 0; k0 < D; k0 += 16) {   // 16 weight loads in flight, summed in k order
+      float wv[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) wv[j] = Wh[(int64_t)(k0 + j) * ldw + c];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc += ys[k0 + j] * wv[j];
+    }
+    const float z = acc + bh[c];
+    zs[c] = z;
+    logits[(int64_t)b * Kc + c] = z;
+    if (z > m) { m = z; am = c; }
+  }
+  // row max / argmax (lowest index on ties), then the log-sum-exp
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64);
+    const int a2 = __shfl_xor(am, o, 64);
+    if (m2 > m || (m2 == m && a2 < am)) { m = m2; am = a2; }
+  }
+  if (lane == 0) { sm[threadIdx.x >> 6] = m; si[threadIdx.x >> 6] = am; }
+  __syncthreads();
+  m = sm[0]; am = si[0];
+#pragma unroll
+  for (int i = 1; i < HD_THREADS / 64; ++i)
+    if (sm[i] > m || (sm[i] == m && si[i] < am)) { m = sm[i]; am = si[i]; }
+  float se = 0.f;
+  for (int c = threadIdx.x; c < Kc; c += HD_THREADS) se += __expf(zs[c] - m);
+  se = hd_block_sum(se, red);
+  const float lse = m + __logf(se);
+  const int y = labels[b];
+  const bool yok = y >= 0 && y < Kc;
+  if (threadIdx.x == 0) {
+    row_loss[b] = yok ? lse - zs[y] : 0.f;
+    row_correct[b] = (yok && am == y) ? 1.f : 0.f;
+  }
+  if (dlogits) {
+    for (int c = threadIdx.x; c < Kc; c += HD_THREADS) {
+      float p = __expf(zs[c] - lse);
+      if (c == y) p -= 1.f;
+      dlogits[(int64_t)b * Kc + c] = p * grad_scale;
+    }
+  }
+}
+
+// Its VJP per cls row: dyf = dlogits Wh^T (thread = weight row k, its row read as float4s, 8 in flight,
+// summed in c order), then the final LayerNorm's VJP (ln16_bwd_f32's math, no residual) into the cls row
+// of dx, and the row's LayerNorm parameter partials part[b] = [dyf xhat | dyf] for ln_part_reduce_kernel
+// (B partial rows).
+__global__ __launch_bounds__(HD_THREADS) void vit_head_bwd_f32_kernel(
+    const float* __restrict__ dlogits, const float* __restrict__ Wh, int64_t ldw, const float* __restrict__ x,
+    int64_t ldx, const float* __restrict__ scale, const float* __restrict__ mean, const float* __restrict__ rstd,
+    float* dx, int64_t lddx, float* part, int D, int Kc) {
+  __shared__ float ds[1024];
+  __shared__ __attribute__((aligned(16))) float dys[256];
+  const int b = blockIdx.x, lane = threadIdx.x & 63;
+  for (int c = threadIdx.x; c < Kc; c += HD_THREADS) ds[c] = dlogits[(int64_t)b * Kc + c];
+  __syncthreads();
+  if ((int)threadIdx.x < D) {
+    const int k = threadIdx.x;
+    const float* wr = Wh + (int64_t)k * ldw;
+    const int K4 = Kc / 4;
+    float a = 0.f;
+    int c4 = 0;
+    for (; c4 + 8 <= K4; c4 += 8) {
+      f32x4 w[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = *reinterpret_cast<const f32x4*>(wr + 4 * (c4 + j));
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a += ds[4 * (c4 + j) + e] * w[j][e];
+    }
+    for (int c = 4 * c4; c < Kc; ++c) a += ds[c] * wr[c];
+    dys[k] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int D4 = D / 4;
+    const float mu = mean[b], rs = rstd[b];
+    f32x4 xh{0.f, 0.f, 0.f, 0.f}, dv{0.f, 0.f, 0.f, 0.f}, g{0.f, 0.f, 0.f, 0.f};
+    if (lane < D4) {
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(x + (int64_t)b * ldx + 4 * lane);
+      dv = *reinterpret_cast<const f32x4*>(dys + 4 * lane);
+      xh = (xv - mu) * rs;
+      g = dv * *reinterpret_cast<const f32x4*>(scale + 4 * lane);
+    }
+    float sg = g[0] + g[1] + g[2] + g[3];
+    float sgx = g[0] * xh[0] + g[1] * xh[1] + g[2] * xh[2] + g[3] * xh[3];
+    sg = wave_sum(sg) / D;
+    sgx = wave_sum(sgx) / D;
+    if (lane < D4) {
+      *reinterpret_cast<f32x4*>(dx + (int64_t)b * lddx + 4 * lane) = rs * (g - sg - xh * sgx);
+      *reinterpret_cast<f32x4*>(part + (int64_t)b * 2 * D + 4 * lane) = dv * xh;
+      *reinterpret_cast<f32x4*>(part + (int64_t)b * 2 * D + D + 4 * lane) = dv;
+    }
+  }
+}
+
+// Head parameter gradients: gWh[k][c] += sum_b yf[b][k] dlogits[b][c], gbh[c] += sum_b dlogits[b][c]
+// (b in order, 8 loads in flight).  Block = 4 weight rows (the last block: the bias), thread = column;
+// the block's 4 columns of yf staged in LDS.
+__global__ __launch_bounds__(HD_THREADS) void vit_head_wgrad_f32_kernel(const float* __restrict__ yf,
+                                                                        const float* __restrict__ dlogits, float* gWh,
+                                                                        int64_t ldgw, float* gbh, int B, int D,
+                                                                        int Kc) {
+  __shared__ float ycol[1024][4];
+  const int k0 = blockIdx.x * 4;
+  const bool bias_blk = k0 >= D;
+  if (!bias_blk)
+    for (int i = threadIdx.x; i < B * 4; i += HD_THREADS) ycol[i / 4][i % 4] = k0 + i % 4 < D ? yf[(int64_t)(i / 4) * D + k0 + i % 4] : 0.f;
+  __syncthreads();
+  for (int c = threadIdx.x; c < Kc; c += HD_THREADS) {
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int b = 0;
+    for (; b + 8 <= B; b += 8) {
+      float g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = dlogits[(int64_t)(b + j) * Kc + c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (bias_blk) a[0] += g[j];
+        else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) a[q] += ycol[b + j][q] * g[j];
+        }
+      }
+    }
+    for (; b < B; ++b) {
+      const float g = dlogits[(int64_t)b * Kc + c];
+      if (bias_blk) a[0] += g;
+      else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] += ycol[b][q] * g;
+      }
+    }
+    if (bias_blk) {
+      gbh[c] += a[0];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (k0 + q < D) gWh[(int64_t)(k0 + q) * ldgw + c] += a[q];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Fused fp32 attention for the ViT shapes (head_dim 32, T <= 272): one workgroup of 16 waves per
 // (batch, head), Q/K/V (and dO) of the head staged once in swizzled LDS images, every product on
 // v_mfma_f32_16x16x4_f32.  No [B*H, T, T] score tensor: the forward keeps the row max m and
@@ -1545,6 +1741,44 @@ extern "C" int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls
   f32_drop(rate, &th, &sc);
   hipLaunchKernelGGL(vit_embed_bwd_f32_kernel, dim3((unsigned)((int64_t)T * ((D + 31) / 32))), dim3(256), 0,
                      (hipStream_t)stream, dx, dpatch, dcls, dpos, B, T, D, th, sc, seed, site);
+  return pcv_launch_status();
+}
+
+// ---- fused classifier head ----
+extern "C" int pcv_vit_head_f32_ok(int D, int Kc) { return D > 0 && D <= 256 && D % 16 == 0 && Kc > 0 && Kc <= 1024; }
+
+extern "C" int pcv_vit_head_fwd_f32(const float* x, int64_t ldx, const float* scale, const float* bias, const float* wh,
+                                    int64_t ldw, const float* bh, const int* labels, float* yf, float* mean,
+                                    float* rstd, float* logits, float* row_loss, float* row_correct, float* dlogits,
+                                    int B, int D, int Kc, float eps, float grad_scale, void* stream) {
+  if (B <= 0 || !pcv_vit_head_f32_ok(D, Kc) || !x || !scale || !bias || !wh || !bh || !labels || !yf || !mean ||
+      !rstd || !logits || !row_loss || !row_correct || ldx < D || (ldx & 3) || ldw < Kc)
+    return PCV_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(scale) | reinterpret_cast<uintptr_t>(bias) |
+       reinterpret_cast<uintptr_t>(yf)) & 15)
+    return PCV_EALIGN;
+  hipLaunchKernelGGL(vit_head_fwd_f32_kernel, dim3((unsigned)B), dim3(HD_THREADS), 0, (hipStream_t)stream, x, ldx, scale,
+                     bias, wh, ldw, bh, labels, yf, mean, rstd, logits, row_loss, row_correct, dlogits, D, Kc, eps,
+                     grad_scale);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_vit_head_bwd_f32(const float* dlogits, const float* wh, int64_t ldw, const float* x, int64_t ldx,
+                                    const float* scale, const float* mean, const float* rstd, const float* yf, float* dx,
+                                    int64_t lddx, float* part, float* gwh, int64_t ldgw, float* gbh, int B, int D,
+                                    int Kc, void* stream) {
+  if (B <= 0 || B > 1024 || !pcv_vit_head_f32_ok(D, Kc) || !dlogits || !wh || !x || !scale || !mean || !rstd ||
+      !yf || !dx || !part || !gwh || !gbh || ldx < D || lddx < D || ((ldx | lddx | ldw) & 3) || ldw < Kc ||
+      ldgw < Kc)
+    return PCV_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(scale) | reinterpret_cast<uintptr_t>(dx) |
+       reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(wh)) & 15)
+    return PCV_EALIGN;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(vit_head_bwd_f32_kernel, dim3((unsigned)B), dim3(HD_THREADS), 0, s, dlogits, wh, ldw, x, ldx,
+                     scale, mean, rstd, dx, lddx, part, D, Kc);
+  hipLaunchKernelGGL(vit_head_wgrad_f32_kernel, dim3((unsigned)((D + 3) / 4 + 1)), dim3(HD_THREADS), 0, s, yf, dlogits,
+                     gwh, ldgw, gbh, B, D, Kc);
   return pcv_launch_status();
 }
 

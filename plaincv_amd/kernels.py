@@ -384,10 +384,13 @@ class LayerNormParamReduce:
     def __init__(self):
         self.jobs = []
 
-    def add(self, ws, R, D, dscale, dbias):
-        _chk(ws.numel() >= layernorm_bwd_f32_ws(R, D) and dscale.numel() == D and dbias.numel() == D
-             and dscale.is_contiguous() and dbias.is_contiguous(), "layernorm part job")
-        self.jobs.append((ws, dscale, dbias, -(-int(R) // 16), int(D)))
+    def add(self, ws, R, D, dscale, dbias, nblk=None):
+        """nblk: the number of [2 D] partial rows in ws, when a kernel other than layernorm_bwd_f32 wrote
+        them (pcv_vit_head_bwd_f32: one per row); default the VJP's 16-row blocks of R rows."""
+        nblk = -(-int(R) // 16) if nblk is None else int(nblk)
+        _chk(ws.numel() >= max(layernorm_bwd_f32_ws(R, D), nblk * 2 * D) and dscale.numel() == D and
+             dbias.numel() == D and dscale.is_contiguous() and dbias.is_contiguous(), "layernorm part job")
+        self.jobs.append((ws, dscale, dbias, nblk, int(D)))
         return self
 
     def finalize(self, device):

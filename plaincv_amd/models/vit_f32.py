@@ -275,7 +275,16 @@ class ViTRunnerF32:
         ks = lambda t: max(1, t.shape[0] // 256)  # noqa: E731   (few tiles: a deep K split)
         # (+ the bias gradient = column sums of the same output gradient, folded into the row-panel
         # launch where the product fits it; otherwise a colsum launch in the backward)
-        prods = [(self.yf, self.dlogits, self.gWh, self.gbh)]
+        # the LayerNorm ViT's classifier head runs as two fused kernels (pcv_vit_head_{fwd,bwd}_f32: final
+        # LayerNorm + head GEMM + bias + cross-entropy, and the VJP with the head's parameter gradients)
+        # when the LayerNorm parameter partials are deferred to ln_red (planned below)
+        head_ok = self.m.use_layernorm and bool(hip.load().pcv_vit_head_f32_ok(D, self.Kc)) and B <= 1024 and \
+            self.Wh.stride(1) == 1 and self.gWh.stride(1) == 1 and self.Wh.stride(0) % 4 == 0
+        xcls = self.xs[-1].view(B, T * D)[:, :D]
+        dxc = self.dx.view(B, T * D)[:, :D]
+        self.head_fused = head_ok and K.layernorm_bwd_f32_fits(D, self.dyf, xcls, None, dxc) and \
+            K.layernorm_bwd_f32_fits(D, self.dy1, self.x1s[0], self.dx, self.dx1)
+        prods = [] if self.head_fused else [(self.yf, self.dlogits, self.gWh, self.gbh)]
         if not self.pe_fused:   # (else the fused embedding VJP forms the conv gradients)
             prods.append((self.patches, self.dpatch, self.gWconv, self.gbconv))
         for i in range(L):
@@ -304,7 +313,8 @@ class ViTRunnerF32:
         if self.m.use_layernorm and \
                 K.layernorm_bwd_f32_fits(D, self.dyf, xcls, None, dxc) and \
                 K.layernorm_bwd_f32_fits(D, self.dy1, self.x1s[0], self.dx, self.dx1):
-            red = K.LayerNormParamReduce().add(self.ln_ws[0], B, D, self.gsf, self.gcf)
+            red = K.LayerNormParamReduce().add(self.ln_ws[0], B, D, self.gsf, self.gcf,
+                                               nblk=B if self.head_fused else None)
             for i in range(L):
                 w = self.w[i]
                 red.add(self.ln_ws[1 + 2 * i], B * T, D, w["gs1"], w["gc1"])
@@ -394,6 +404,14 @@ class ViTRunnerF32:
             g["fc1"].run(rate, seed)
             g["fc2"].run(rate, seed)
         xcls = self.xs[-1].view(B, T * D)[:, :D]
+        if self.head_fused:   # final LayerNorm + head + bias + cross-entropy in one launch
+            hip.call("pcv_vit_head_fwd_f32", ptr(xcls), T * D, ptr(self.sf), ptr(self.cf), ptr(self.Wh),
+                     self.Wh.stride(0), ptr(self.bh),
+                     ptr(self.labels), ptr(self.yf), ptr(self.stf[0]), ptr(self.stf[1]), ptr(self.logits),
+                     ptr(self.row_loss), ptr(self.row_correct), ptr(self.dlogits) if need_grad else None, B, D, self.Kc,
+                     1e-6, 1.0 / B, stream_ptr())
+            K.mean2(self.row_loss, self.row_correct, B, 1.0 / B, self.metrics)
+            return self.metrics
         if m.use_layernorm:
             self._ln(xcls, self.sf, self.cf, self.yf, self.stf)
         elif self.bn:   # statistics over every token row, normalise the cls rows only
@@ -423,17 +441,22 @@ class ViTRunnerF32:
         B, T, D = self.B, self.T, self.D
         rate = m.dropout_rate if train else 0.0
         seed = self.seed
-        self._colsum(self.dlogits, self.gbh)
-        self.g_head_d.run()
         dxc = self.dx.view(B, T * D)[:, :D]
         xcls = self.xs[-1].view(B, T * D)[:, :D]
-        if m.use_layernorm:
-            self._ln_bwd(0, self.dyf, xcls, self.sf, self.stf, None, dxc, self.gsf, self.gcf)
-        elif self.bn:   # train-mode VJP through the all-row statistics: every row of dx is written
-            K.batchnorm_bwd(self.dy_top, self.xs[-1], *self.bstf, self.sf, None, self.dx, None, self.gsf, self.gcf,
-                            self.bn_ws)
+        if self.head_fused:   # dyf, the final LayerNorm VJP into dx's cls rows, gWh / gbh, the LN partials
+            hip.call("pcv_vit_head_bwd_f32", ptr(self.dlogits), ptr(self.Wh), self.Wh.stride(0), ptr(xcls), T * D,
+                     ptr(self.sf), ptr(self.stf[0]), ptr(self.stf[1]), ptr(self.yf), ptr(dxc), T * D,
+                     ptr(self.ln_ws[0]), ptr(self.gWh), self.gWh.stride(0), ptr(self.gbh), B, D, self.Kc, stream_ptr())
         else:
-            _epi(self.dyf, dxc)
+            self._colsum(self.dlogits, self.gbh)
+            self.g_head_d.run()
+            if m.use_layernorm:
+                self._ln_bwd(0, self.dyf, xcls, self.sf, self.stf, None, dxc, self.gsf, self.gcf)
+            elif self.bn:   # train-mode VJP through the all-row statistics: every row of dx is written
+                K.batchnorm_bwd(self.dy_top, self.xs[-1], *self.bstf, self.sf, None, self.dx, None, self.gsf,
+                                self.gcf, self.bn_ws)
+            else:
+                _epi(self.dyf, dxc)
         dx_in = self.dx
         for i in reversed(range(m.num_layers)):
             w, g = self.w[i], self.gb[i]
