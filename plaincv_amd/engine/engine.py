@@ -338,7 +338,11 @@ class GraphedTrainStep:
             # split: the step graph ends after the backward; the reduce and the optimizer's part run
             # after its replay (eager reduce, then g_post, or the eager optimizer)
             self.split = (self.distributed and not self.capture_reduce) or not self.opt_graphed
-            mode = "thread_local" if self.capture_reduce else "global"
+            # with a process group up, its watchdog thread polls events while we capture: under the
+            # "global" mode a poll during capture invalidates the capture (seen once in a one-rank RCCL run,
+            # "operation failed due to a previous error during capture"), so only this thread's calls
+            # are checked then
+            mode = "thread_local" if dp.is_initialized() else "global"
             self.g_slots = []
             after_first = None
             for images, labels in [(None, None)] + self.slots:   # the copy-in graph, then one per slot
@@ -366,11 +370,11 @@ class GraphedTrainStep:
                             self._body(images, steady=True)
                     self.g_steady.append(g)
                 self.g_flush = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.g_flush, stream=s, pool=self.g_fb.pool()):
+                with torch.cuda.graph(self.g_flush, stream=s, pool=self.g_fb.pool(), capture_error_mode=mode):
                     state.tx.step_ns_phase_(store, state.opt_state)
             if self.split and self.opt_graphed:
                 self.g_post = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.g_post, stream=s, pool=self.g_fb.pool()):
+                with torch.cuda.graph(self.g_post, stream=s, pool=self.g_fb.pool(), capture_error_mode=mode):
                     self._post()
         torch.cuda.current_stream().wait_stream(s)
         self.metrics = self.runner.metrics
