@@ -288,7 +288,9 @@ int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls, float* dp
  * LayerNorm VJP into dx's cls rows (dx + b lddx), the LayerNorm parameter partials part [B][2 D] =
  * [dyf xhat | dyf] (for pcv_layernorm_part_reduce with B partial rows), gwh += yf^T dlogits, gbh +=
  * column sums of dlogits -- fixed summation orders.  wh / gwh rows ldw / ldgw apart (the ParamStore pads
- * rows to 8).  ok: D <= 256, D % 16 == 0, Kc <= 1024 (and B <= 1024 for the VJP). */
+ * rows to 8).  dxd (optional): also the next consumer's dropout VJP of the dx cls rows, dxd[b] =
+ * dropout_vjp(dx[b]) with index (b drow) D + d (the MLP-out dropout of the last block).  ok: D <= 256,
+ * D % 16 == 0, Kc <= 1024 (and B <= 1024 for the VJP). */
 int pcv_vit_head_f32_ok(int D, int Kc);
 int pcv_vit_head_fwd_f32(const float* x, int64_t ldx, const float* scale, const float* bias, const float* wh,
                          int64_t ldw, const float* bh, const int* labels, float* yf, float* mean, float* rstd,
@@ -297,6 +299,7 @@ int pcv_vit_head_fwd_f32(const float* x, int64_t ldx, const float* scale, const 
 int pcv_vit_head_bwd_f32(const float* dlogits, const float* wh, int64_t ldw, const float* x, int64_t ldx,
                          const float* scale, const float* mean, const float* rstd, const float* yf, float* dx,
                          int64_t lddx, float* part, float* gwh, int64_t ldgw, float* gbh, int B, int D, int Kc,
+                         float* dxd, int64_t lddxd, int64_t drow, float rate, const uint32_t* seed, uint32_t site,
                          void* stream);
 /* Fused fp32 patch embedding (models/vit_small.py:78-109): x[b, t] = dropout(t == 0 ? cls + pos[0] :
  * pos[t] + (patch(b, t - 1) . w + bias)) straight from the uint8 images (patch = the (kh, kw, c) flatten
@@ -334,6 +337,23 @@ int pcv_gemm_f32_rows_tiled(const float* A, int64_t lda, const float* B, int64_t
                             const float* res, int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed,
                             uint32_t site, void* stream);
 int pcv_gemm_f32_rows_form(int64_t M, int64_t N, int64_t K);
+/* pcv_gemm_f32_rows whose dropout index of output row r is r * drop_row_step * N + col: the product of a
+ * strided subset of the token rows (every drop_row_step-th, e.g. the cls rows b * T) with the dropout bits
+ * those rows have in the full [rows][N] product. */
+int pcv_gemm_f32_rows_rs(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C, int64_t ldc,
+                         int64_t M, int64_t N, int64_t K, const float* bias, float* aux, int64_t ldaux,
+                         const float* res, int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed,
+                         uint32_t site, int64_t drop_row_step, void* stream);
+/* Attention of the cls query only (query 0 of each (b, h); head_dim 32, T <= 512): O row 0 and its row
+ * statistics (mrow = max of the scaled scores, linv = 1 / sum at slot b H T + h T), the same numerics and
+ * dropout keep bits as pcv_attn_fwd_f32's row 0; the VJP with dO nonzero only at query 0: dK / dV of
+ * every key and dQ of query 0 (the other dQ rows are not written). */
+int pcv_attn_cls_f32_ok(int T, int head_dim);
+int pcv_attn_cls_fwd_f32(const float* qkv, int64_t ldqkv, float* out, int64_t ldo, float* mrow, float* linv, int B,
+                         int T, int H, int D, const uint16_t* mask, float rate, void* stream);
+int pcv_attn_cls_bwd_f32(const float* qkv, int64_t ldqkv, const float* dout, int64_t lddo, const float* mrow,
+                         const float* linv, float* dqkv, int64_t lddqkv, int B, int T, int H, int D,
+                         const uint16_t* mask, float rate, void* stream);
 /* Every fp32 weight gradient of a step in one launch (csrc/gemm_f32.hip): jobs_dev holds njobs
  * records (pcv_gemm_f32_wgrad_job_size() bytes) {A, B, C, colsum, ws, lda, ldb, ldc, M, N, K, tiles_n,
  * tiles, ksplit, kchunk, first, ffirst, pad} (colsum optional: += the column sums of B -- the Dense's

@@ -33,6 +33,7 @@ struct GrArgs {
   int M, N, K, act, site, tiles_n;
   uint32_t thresh;
   float dscale, res_scale;
+  int rstep;   // dropout index of output row r: r * rstep * N + col (rstep > 1: C is a strided row subset)
 };
 
 // GELU (tanh form): 0.5 x (1 + tanh(u)) = x / (1 + exp(-2u)), u = sqrt(2/pi) (x + 0.044715 x^3) --
@@ -191,7 +192,7 @@ __device__ __forceinline__ f32x4 gr_epi_apply(const GrArgs& g, f32x4 v, const Gr
                                               uint32_t seed) {
   if (g.bias) v += in.bias;
   if (g.act == 2) {   // backward of dropout(gelu(pre)): keep bits, then gelu'(pre)
-    const uint32_t base = (uint32_t)((int64_t)row * g.N + col);
+    const uint32_t base = (uint32_t)((int64_t)row * g.rstep * g.N + col);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float x = v[e];
@@ -204,7 +205,7 @@ __device__ __forceinline__ f32x4 gr_epi_apply(const GrArgs& g, f32x4 v, const Gr
     for (int e = 0; e < 4; ++e) v[e] = gr_gelu(v[e]);
   }
   if (g.thresh && g.act != 2) {
-    const uint32_t base = (uint32_t)((int64_t)row * g.N + col);
+    const uint32_t base = (uint32_t)((int64_t)row * g.rstep * g.N + col);
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = hash3(seed, (uint32_t)g.site, base + e) >= g.thresh ? v[e] * g.dscale : 0.f;
   }
@@ -477,7 +478,7 @@ template <int EF>
 __device__ __forceinline__ f32x4 pn_epi_apply(const GrArgs& g, f32x4 v, const GrEpiIn& in, int row, int col,
                                               uint32_t seed) {
   if (EF & PN_BIAS) v += in.bias;
-  const uint32_t base = (uint32_t)((int64_t)row * g.N + col);
+  const uint32_t base = (uint32_t)((int64_t)row * g.rstep * g.N + col);
   if (EF & PN_GELUBWD) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -674,7 +675,7 @@ struct PnPlan { int cb, grid, q, tail0; };
 // land before the first MFMA): out 11.9 vs 11.4, fc2 20.9 vs 19.6, qkv_d 26.0 vs 24.2 us.
 static PnPlan pn_plan(int64_t M, int64_t N, int64_t K) {
   PnPlan p = {0, 0, 0, 0};
-  if (K != 128 || N < 256) return p;
+  if (K != 128 || N < 256 || M < 64 * 64) return p;   // (a persistent grid of a few workgroups loses)
   const int cb = 64;
   if (N % cb || M < PN_RM) return p;
   const int64_t G = std::min<int64_t>(pcv_cu_count(), M / PN_RM);
@@ -733,7 +734,7 @@ extern "C" int pcv_gemm_f32_rows_ok(int64_t M, int64_t N, int64_t K, const void*
 static int gr_rows(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C, int64_t ldc,
                    int64_t M, int64_t N, int64_t K, const float* bias, float* aux, int64_t ldaux, const float* res,
                    int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed, uint32_t site,
-                   void* stream, bool panel) {
+                   void* stream, bool panel, int64_t rstep = 1) {
   if (!A || !B || !C || !pcv_gemm_f32_rows_ok(M, N, K, A, lda, B, ldb, tb) || act < 0 || act > 2 ||
       (act == 2 && (!aux || bias || res)) || ldc < N || (act && aux && ldaux < N) ||
       (res && ldr < N) || rate < 0.f || rate >= 1.f || (rate > 0.f && !seed))
@@ -747,6 +748,8 @@ static int gr_rows(const float* A, int64_t lda, const float* B, int64_t ldb, int
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldr = ldr; g.ldaux = ldaux;
   g.M = (int)M; g.N = (int)N; g.K = (int)K; g.act = act; g.site = (int)site;
   g.thresh = 0; g.dscale = 1.f; g.res_scale = res_scale;
+  if (rstep < 1 || rstep * M >= (1ll << 31)) return PCV_EINVAL;
+  g.rstep = (int)rstep;
   if (rate > 0.f) {   // as drop_params (elementwise.hip)
     const double t = (double)rate * 4294967296.0;
     g.thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
@@ -808,6 +811,14 @@ extern "C" int pcv_gemm_f32_rows_tiled(const float* A, int64_t lda, const float*
 }
 
 extern "C" int pcv_gemm_f32_rows_form(int64_t M, int64_t N, int64_t K) { return pn_plan(M, N, K).cb ? 1 : 0; }
+
+extern "C" int pcv_gemm_f32_rows_rs(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C,
+                                    int64_t ldc, int64_t M, int64_t N, int64_t K, const float* bias, float* aux,
+                                    int64_t ldaux, const float* res, int64_t ldr, float res_scale, int act, float rate,
+                                    const uint32_t* seed, uint32_t site, int64_t drop_row_step, void* stream) {
+  return gr_rows(A, lda, B, ldb, tb, C, ldc, M, N, K, bias, aux, ldaux, res, ldr, res_scale, act, rate, seed, site,
+                 stream, true, drop_row_step);
+}
 
 #ifdef PCV_PANEL_STAMPS
 extern "C" int pcv_panel_stamp_buffer(unsigned long long* buf) {

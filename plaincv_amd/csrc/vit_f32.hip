@@ -20,6 +20,8 @@ __device__ __forceinline__ bool keep_of(uint32_t seed, uint32_t site, uint32_t i
   return hash3(seed, site, idx) >= thresh;
 }
 
+constexpr int FA_DH_CLS = 32, FA_TMAX_CLS = 512;   // cls-query attention: head dim, max tokens
+
 // same packed [T,T] keep words as attention.hip (drop_word layout)
 __device__ __forceinline__ int64_t f32_drop_word(int q, int k, int n64) {
   return (((int64_t)(q >> 4) * n64 + (k >> 6)) * 4 + ((q & 15) >> 2)) * 16 + ((k & 15) >> 2) * 4 + ((k & 63) >> 4);
@@ -558,6 +560,165 @@ __global__ __launch_bounds__(256) void patch_embed_fold_kernel(const float* __re
 }
 
 // ---------------------------------------------------------------------------------------------
+// Attention of the cls query only (the last encoder block of a cls-token ViT: only x[:, 0] reaches
+// the loss, so only the cls row of that block's attention output is ever used).  Block = (b, h),
+// thread = key: the same numerics as the fused forward's VALU tail row (scaled scores, max, exp,
+// sum; dropout keep bits of query 0 from the packed mask; O = sum_k Pd V / l * dscale) and the same
+// row statistics (mrow = max of the scaled scores, linv = 1 / sum) at query slot 0.
+constexpr int AC_THREADS = 256;
+__global__ __launch_bounds__(AC_THREADS) void attn_cls_fwd_f32_kernel(const float* __restrict__ qkv, int64_t ldqkv,
+                                                                      float* out, int64_t ldo, float* mrow,
+                                                                      float* linv, const uint16_t* __restrict__ mask,
+                                                                      int T, int H, int D, int n64, float scale,
+                                                                      float dscale) {
+  __shared__ float q0[FA_DH_CLS];
+  __shared__ float pk[FA_TMAX_CLS];
+  __shared__ float red[2 * (AC_THREADS / 64)];
+  __shared__ float part[FA_DH_CLS][9];
+  const int h = blockIdx.x, b = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t bT = (int64_t)b * T, bh = (int64_t)b * H + h;
+  if (threadIdx.x < FA_DH_CLS) q0[threadIdx.x] = qkv[bT * ldqkv + h * FA_DH_CLS + threadIdx.x];
+  __syncthreads();
+  float sv[2] = {-__builtin_inff(), -__builtin_inff()};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = threadIdx.x + AC_THREADS * j;
+    if (key < T) {
+      const float* kr = qkv + (bT + key) * ldqkv + D + h * FA_DH_CLS;
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < FA_DH_CLS; c += 4) {
+        const f32x4 k4 = *reinterpret_cast<const f32x4*>(kr + c);
+        acc += q0[c] * k4[0] + q0[c + 1] * k4[1] + q0[c + 2] * k4[2] + q0[c + 3] * k4[3];
+      }
+      sv[j] = acc * scale;
+    }
+  }
+  float mx = wave_max(fmaxf(sv[0], sv[1]));
+  if (lane == 0) red[wv] = mx;
+  __syncthreads();
+  mx = red[0];
+#pragma unroll
+  for (int w = 1; w < AC_THREADS / 64; ++w) mx = fmaxf(mx, red[w]);
+  float ls = 0.f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = threadIdx.x + AC_THREADS * j;
+    if (key < T) {
+      const float p = __expf(sv[j] - mx);
+      ls += p;
+      pk[key] = (mask && !attn_keep(mask, 0, key, n64)) ? 0.f : p;
+    }
+  }
+  ls = wave_sum(ls);
+  if (lane == 0) red[AC_THREADS / 64 + wv] = ls;
+  __syncthreads();
+  {   // O = sum_k Pd V: thread (d, key slice of 8)
+    const int d = threadIdx.x & 31, sl = threadIdx.x >> 5;
+    float acc = 0.f;
+    for (int k = sl; k < T; k += 8) acc += pk[k] * qkv[(bT + k) * ldqkv + 2 * D + h * FA_DH_CLS + d];
+    part[d][sl] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < FA_DH_CLS) {
+    float l = 0.f, acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < AC_THREADS / 64; ++w) l += red[AC_THREADS / 64 + w];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += part[threadIdx.x][j];
+    const float inv = 1.f / l;
+    out[bT * ldo + h * FA_DH_CLS + threadIdx.x] = acc * (mask ? inv * dscale : inv);
+    if (threadIdx.x == 0) {
+      mrow[bh * T] = mx;
+      linv[bh * T] = inv;
+    }
+  }
+}
+
+// Its VJP with dO nonzero only at the cls query: P of query 0 recomputed from mrow / linv; dPd_k =
+// dO0 . V_k, dP = dropout_vjp(dPd), delta = sum_k dP_k P_k, dS_k = P_k (dP_k - delta); dV_k = Pd_k dO0,
+// dK_k = scale dS_k q0 for every key, dQ_0 = scale sum_k dS_k K_k.  The other query rows of dQ are
+// zero and are not written (the caller's dqkv holds zeros there).
+__global__ __launch_bounds__(AC_THREADS) void attn_cls_bwd_f32_kernel(const float* __restrict__ qkv, int64_t ldqkv,
+                                                                      const float* __restrict__ dout, int64_t lddo,
+                                                                      const float* __restrict__ mrow,
+                                                                      const float* __restrict__ linv, float* dqkv,
+                                                                      int64_t lddqkv, const uint16_t* __restrict__ mask,
+                                                                      int T, int H, int D, int n64, float scale,
+                                                                      float dscale) {
+  __shared__ float q0[FA_DH_CLS], do0[FA_DH_CLS];
+  __shared__ float dsk[FA_TMAX_CLS];
+  __shared__ float red[AC_THREADS / 64];
+  __shared__ float part[FA_DH_CLS][9];
+  const int h = blockIdx.x, b = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t bT = (int64_t)b * T, bh = (int64_t)b * H + h;
+  if (threadIdx.x < FA_DH_CLS) q0[threadIdx.x] = qkv[bT * ldqkv + h * FA_DH_CLS + threadIdx.x];
+  else if (threadIdx.x < 2 * FA_DH_CLS) do0[threadIdx.x - FA_DH_CLS] = dout[bT * lddo + h * FA_DH_CLS + threadIdx.x - FA_DH_CLS];
+  __syncthreads();
+  const float m0 = mrow[bh * T], l0 = linv[bh * T];
+  float pv[2] = {0.f, 0.f}, dpv[2] = {0.f, 0.f};
+  bool kp[2] = {true, true};
+  float dot = 0.f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = threadIdx.x + AC_THREADS * j;
+    if (key < T) {
+      const float* kr = qkv + (bT + key) * ldqkv + D + h * FA_DH_CLS;
+      const float* vr = kr + D;
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int c = 0; c < FA_DH_CLS; c += 4) {
+        const f32x4 k4 = *reinterpret_cast<const f32x4*>(kr + c), v4 = *reinterpret_cast<const f32x4*>(vr + c);
+        s += q0[c] * k4[0] + q0[c + 1] * k4[1] + q0[c + 2] * k4[2] + q0[c + 3] * k4[3];
+        dp += do0[c] * v4[0] + do0[c + 1] * v4[1] + do0[c + 2] * v4[2] + do0[c + 3] * v4[3];
+      }
+      const float p = __expf(s * scale - m0) * l0;
+      kp[j] = !mask || attn_keep(mask, 0, key, n64);
+      const float dpk = kp[j] ? dp * (mask ? dscale : 1.f) : 0.f;
+      pv[j] = p;
+      dpv[j] = dpk;
+      dot += dpk * p;
+    }
+  }
+  dot = wave_sum(dot);
+  if (lane == 0) red[wv] = dot;
+  __syncthreads();
+  float delta = red[0];
+#pragma unroll
+  for (int w = 1; w < AC_THREADS / 64; ++w) delta += red[w];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = threadIdx.x + AC_THREADS * j;
+    if (key < T) {
+      const float ds = pv[j] * (dpv[j] - delta);
+      dsk[key] = ds;
+      const float pd = kp[j] ? pv[j] * (mask ? dscale : 1.f) : 0.f;
+      float* dk = dqkv + (bT + key) * lddqkv + D + h * FA_DH_CLS;
+      float* dvv = dk + D;
+#pragma unroll
+      for (int c = 0; c < FA_DH_CLS; c += 4) {
+        *reinterpret_cast<f32x4*>(dk + c) = f32x4{q0[c], q0[c + 1], q0[c + 2], q0[c + 3]} * (scale * ds);
+        *reinterpret_cast<f32x4*>(dvv + c) = f32x4{do0[c], do0[c + 1], do0[c + 2], do0[c + 3]} * pd;
+      }
+    }
+  }
+  __syncthreads();
+  {   // dQ_0 = scale sum_k dS_k K_k: thread (d, key slice of 8)
+    const int d = threadIdx.x & 31, sl = threadIdx.x >> 5;
+    float acc = 0.f;
+    for (int k = sl; k < T; k += 8) acc += dsk[k] * qkv[(bT + k) * ldqkv + D + h * FA_DH_CLS + d];
+    part[d][sl] = acc;
+  }
+  __syncthreads();
+  if (threadIdx.x < FA_DH_CLS) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += part[threadIdx.x][j];
+    dqkv[bT * lddqkv + h * FA_DH_CLS + threadIdx.x] = acc * scale;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Fused classifier head of the fp32 ViT (models/vit_small.py:111-127 + flax_engine's loss): per cls
 // row b, the final LayerNorm (ln16_fwd_f32's math: fast variance clipped at 0, eps), logits = y Wh + bh
 // (fp32 FMAs in k order), the softmax cross-entropy with the row loss, the argmax hit (lowest index on
@@ -659,7 +820,8 @@ __global__ __launch_bounds__(HD_THREADS) void vit_head_fwd_f32_kernel(
 __global__ __launch_bounds__(HD_THREADS) void vit_head_bwd_f32_kernel(
     const float* __restrict__ dlogits, const float* __restrict__ Wh, int64_t ldw, const float* __restrict__ x,
     int64_t ldx, const float* __restrict__ scale, const float* __restrict__ mean, const float* __restrict__ rstd,
-    float* dx, int64_t lddx, float* part, int D, int Kc) {
+    float* dx, int64_t lddx, float* part, int D, int Kc, float* dxd, int64_t lddxd, int64_t drow, uint32_t thresh,
+    float dscale, const uint32_t* seedp, uint32_t site) {
   __shared__ float ds[1024];
   __shared__ __attribute__((aligned(16))) float dys[256];
   const int b = blockIdx.x, lane = threadIdx.x & 63;
@@ -699,7 +861,18 @@ __global__ __launch_bounds__(HD_THREADS) void vit_head_bwd_f32_kernel(
     sg = wave_sum(sg) / D;
     sgx = wave_sum(sgx) / D;
     if (lane < D4) {
-      *reinterpret_cast<f32x4*>(dx + (int64_t)b * lddx + 4 * lane) = rs * (g - sg - xh * sgx);
+      const f32x4 o = rs * (g - sg - xh * sgx);
+      *reinterpret_cast<f32x4*>(dx + (int64_t)b * lddx + 4 * lane) = o;
+      if (dxd) {   // the next consumer's dropout VJP at the row's token index (b drow) D + d
+        f32x4 od = o;
+        if (thresh) {
+          const uint32_t seed = *seedp;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            od[e] = keep_of(seed, site, (uint32_t)((int64_t)b * drow * D + 4 * lane + e), thresh) ? o[e] * dscale : 0.f;
+        }
+        *reinterpret_cast<f32x4*>(dxd + (int64_t)b * lddxd + 4 * lane) = od;
+      }
       *reinterpret_cast<f32x4*>(part + (int64_t)b * 2 * D + 4 * lane) = dv * xh;
       *reinterpret_cast<f32x4*>(part + (int64_t)b * 2 * D + D + 4 * lane) = dv;
     }
@@ -1744,6 +1917,36 @@ extern "C" int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls
   return pcv_launch_status();
 }
 
+// ---- cls-query attention ----
+extern "C" int pcv_attn_cls_f32_ok(int T, int head_dim) { return T >= 1 && T <= FA_TMAX_CLS && T <= 2 * AC_THREADS && head_dim == FA_DH_CLS; }
+
+extern "C" int pcv_attn_cls_fwd_f32(const float* qkv, int64_t ldqkv, float* out, int64_t ldo, float* mrow, float* linv,
+                                    int B, int T, int H, int D, const uint16_t* mask, float rate, void* stream) {
+  if (!qkv || !out || !mrow || !linv || B <= 0 || H <= 0 || !pcv_attn_cls_f32_ok(T, D / H) || D != H * FA_DH_CLS ||
+      ldqkv < 3 * D || ldo < D || ((ldqkv | ldo) & 3) || (rate > 0.f && !mask) || rate < 0.f || rate >= 1.f)
+    return PCV_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(out)) & 15) return PCV_EALIGN;
+  hipLaunchKernelGGL(attn_cls_fwd_f32_kernel, dim3(H, B), dim3(AC_THREADS), 0, (hipStream_t)stream, qkv, ldqkv, out, ldo,
+                     mrow, linv, rate > 0.f ? mask : nullptr, T, H, D, 2 * ((T + 127) / 128), 1.f / sqrtf((float)FA_DH_CLS),
+                     rate > 0.f ? 1.f / (1.f - rate) : 1.f);
+  return pcv_launch_status();
+}
+
+extern "C" int pcv_attn_cls_bwd_f32(const float* qkv, int64_t ldqkv, const float* dout, int64_t lddo,
+                                    const float* mrow, const float* linv, float* dqkv, int64_t lddqkv, int B, int T,
+                                    int H, int D, const uint16_t* mask, float rate, void* stream) {
+  if (!qkv || !dout || !mrow || !linv || !dqkv || B <= 0 || H <= 0 || !pcv_attn_cls_f32_ok(T, D / H) ||
+      D != H * FA_DH_CLS || ldqkv < 3 * D || lddqkv < 3 * D || lddo < D || ((ldqkv | lddqkv | lddo) & 3) ||
+      (rate > 0.f && !mask) || rate < 0.f || rate >= 1.f)
+    return PCV_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(dqkv) | reinterpret_cast<uintptr_t>(dout)) & 15)
+    return PCV_EALIGN;
+  hipLaunchKernelGGL(attn_cls_bwd_f32_kernel, dim3(H, B), dim3(AC_THREADS), 0, (hipStream_t)stream, qkv, ldqkv, dout,
+                     lddo, mrow, linv, dqkv, lddqkv, rate > 0.f ? mask : nullptr, T, H, D, 2 * ((T + 127) / 128),
+                     1.f / sqrtf((float)FA_DH_CLS), rate > 0.f ? 1.f / (1.f - rate) : 1.f);
+  return pcv_launch_status();
+}
+
 // ---- fused classifier head ----
 extern "C" int pcv_vit_head_f32_ok(int D, int Kc) { return D > 0 && D <= 256 && D % 16 == 0 && Kc > 0 && Kc <= 1024; }
 
@@ -1766,7 +1969,13 @@ extern "C" int pcv_vit_head_fwd_f32(const float* x, int64_t ldx, const float* sc
 extern "C" int pcv_vit_head_bwd_f32(const float* dlogits, const float* wh, int64_t ldw, const float* x, int64_t ldx,
                                     const float* scale, const float* mean, const float* rstd, const float* yf, float* dx,
                                     int64_t lddx, float* part, float* gwh, int64_t ldgw, float* gbh, int B, int D,
-                                    int Kc, void* stream) {
+                                    int Kc, float* dxd, int64_t lddxd, int64_t drow, float rate, const uint32_t* seed,
+                                    uint32_t site, void* stream) {
+  if (dxd && (lddxd < D || (lddxd & 3) || (reinterpret_cast<uintptr_t>(dxd) & 15) || drow < 1 ||
+              (rate > 0.f && !seed) || rate < 0.f || rate >= 1.f))
+    return PCV_EINVAL;
+  uint32_t th; float sc;
+  f32_drop(dxd ? rate : 0.f, &th, &sc);
   if (B <= 0 || B > 1024 || !pcv_vit_head_f32_ok(D, Kc) || !dlogits || !wh || !x || !scale || !mean || !rstd ||
       !yf || !dx || !part || !gwh || !gbh || ldx < D || lddx < D || ((ldx | lddx | ldw) & 3) || ldw < Kc ||
       ldgw < Kc)
@@ -1776,7 +1985,7 @@ extern "C" int pcv_vit_head_bwd_f32(const float* dlogits, const float* wh, int64
     return PCV_EALIGN;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(vit_head_bwd_f32_kernel, dim3((unsigned)B), dim3(HD_THREADS), 0, s, dlogits, wh, ldw, x, ldx,
-                     scale, mean, rstd, dx, lddx, part, D, Kc);
+                     scale, mean, rstd, dx, lddx, part, D, Kc, dxd, lddxd, drow, th, sc, seed, site);
   hipLaunchKernelGGL(vit_head_wgrad_f32_kernel, dim3((unsigned)((D + 3) / 4 + 1)), dim3(HD_THREADS), 0, s, yf, dlogits,
                      gwh, ldgw, gbh, B, D, Kc);
   return pcv_launch_status();

@@ -82,7 +82,8 @@ SIGNATURES = {
     "pcv_vit_embed_bwd_f32": [P, P, P, P, I32, I32, I32, F32, P, U32, P],
     "pcv_vit_head_f32_ok": [I32, I32],
     "pcv_vit_head_fwd_f32": [P, I64, P, P, P, I64, P, P, P, P, P, P, P, P, P, I32, I32, I32, F32, F32, P],
-    "pcv_vit_head_bwd_f32": [P, P, I64, P, I64, P, P, P, P, P, I64, P, P, I64, P, I32, I32, I32, P],
+    "pcv_vit_head_bwd_f32": [P, P, I64, P, I64, P, P, P, P, P, I64, P, P, I64, P, I32, I32, I32, P, I64, I64, F32, P, U32,
+                             P],
     "pcv_vit_patch_embed_f32_ok": [I32, I32, I32, I32, I32, I32],
     "pcv_vit_patch_embed_bwd_f32_ws": [I32, I32, I32, I32, I32, I32],
     "pcv_vit_patch_embed_fwd_f32": [P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, F32, P, U32, P],
@@ -92,6 +93,11 @@ SIGNATURES = {
     "pcv_gemm_f32_rows_tiled": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32,
                                 P],
     "pcv_gemm_f32_rows_form": [I64, I64, I64],
+    "pcv_gemm_f32_rows_rs": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32, I64,
+                             P],
+    "pcv_attn_cls_f32_ok": [I32, I32],
+    "pcv_attn_cls_fwd_f32": [P, I64, P, I64, P, P, I32, I32, I32, I32, P, F32, P],
+    "pcv_attn_cls_bwd_f32": [P, I64, P, I64, P, P, P, I64, I32, I32, I32, I32, P, F32, P],
     "pcv_gemm_f32_wgrad_job_size": [],
     "pcv_gemm_f32_wgrad": [P, I32, I64, I32, P],
     "pcv_gemm_f32_wgrad_fold": [P, I32, I64, I32, P],

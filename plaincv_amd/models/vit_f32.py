@@ -62,26 +62,35 @@ class _Dense:
 
     entry = "pcv_gemm_f32_rows"
 
-    def __init__(self, a, b, c, tb=False, bias=None, res=None, aux=None, act=0, site=0, dropout=False):
+    def __init__(self, a, b, c, tb=False, bias=None, res=None, aux=None, act=0, site=0, dropout=False, rstep=1):
+        """rstep > 1: a, c (aux, res) are every rstep-th token row (the cls rows b * T); the dropout bits
+        are those of the full-height product (pcv_gemm_f32_rows_rs)"""
         self.a, self.b, self.c, self.tb = a, b, c, bool(tb)
         self.bias, self.res, self.aux, self.act, self.site, self.dropout = bias, res, aux, act, site, dropout
+        self.rstep = int(rstep)
         M, K = a.shape
         self.M, self.N, self.K = M, c.shape[1], K
         al = all(t is None or (t.data_ptr() % 16 == 0 and (t.dim() == 1 or t.stride(0) % 4 == 0))
                  for t in (c, aux, res, bias))
         self.fused = al and bool(hip.load().pcv_gemm_f32_rows_ok(M, self.N, K, ptr(a), a.stride(0), ptr(b),
                                                                  b.stride(0), int(tb)))
+        if self.rstep != 1 and not self.fused:
+            raise ValueError("a strided-row Dense needs the fused row GEMM's shapes")
         self.plan = None if self.fused else GemmF32().add(a, b, c, tb=tb).finalize(c.device)
         self.epi = bias is not None or res is not None or act or dropout
 
     def run(self, rate=0.0, seed=None):
         rate = rate if self.dropout else 0.0
         if self.fused:
-            hip.call(self.entry, ptr(self.a), self.a.stride(0), ptr(self.b), self.b.stride(0), int(self.tb),
-                     ptr(self.c), self.c.stride(0), self.M, self.N, self.K, ptr(self.bias), ptr(self.aux),
-                     self.aux.stride(0) if self.aux is not None else 0, ptr(self.res),
-                     self.res.stride(0) if self.res is not None else 0, 1.0, int(self.act), float(rate), ptr(seed),
-                     int(self.site), stream_ptr())
+            args = (ptr(self.a), self.a.stride(0), ptr(self.b), self.b.stride(0), int(self.tb), ptr(self.c),
+                    self.c.stride(0), self.M, self.N, self.K, ptr(self.bias), ptr(self.aux),
+                    self.aux.stride(0) if self.aux is not None else 0, ptr(self.res),
+                    self.res.stride(0) if self.res is not None else 0, 1.0, int(self.act), float(rate), ptr(seed),
+                    int(self.site))
+            if self.rstep != 1:
+                hip.call("pcv_gemm_f32_rows_rs", *args, self.rstep, stream_ptr())
+            else:
+                hip.call(self.entry, *args, stream_ptr())
             return
         self.plan.run()
         if self.act == 2:   # backward of dropout(gelu(pre))
@@ -261,6 +270,46 @@ class ViTRunnerF32:
                                 out_d=_Dense(self.dx1_l[i], w["Wo"], self.dO, tb=True), dpv=att.get("dpv"),
                                 dqk=att.get("dqk"),
                                 qkv_d=_Dense(dqkv, w["Wqkv"], self.dy0, tb=True)))
+        # the LayerNorm ViT's classifier head runs as two fused kernels (pcv_vit_head_{fwd,bwd}_f32: final
+        # LayerNorm + head GEMM + bias + cross-entropy, and the VJP with the head's parameter gradients)
+        # when the LayerNorm parameter partials are deferred to ln_red (planned below)
+        head_ok = self.m.use_layernorm and bool(hip.load().pcv_vit_head_f32_ok(D, self.Kc)) and B <= 1024 and \
+            self.Wh.stride(1) == 1 and self.gWh.stride(1) == 1 and self.Wh.stride(0) % 4 == 0
+        xcls = self.xs[-1].view(B, T * D)[:, :D]
+        dxc = self.dx.view(B, T * D)[:, :D]
+        self.head_fused = head_ok and K.layernorm_bwd_f32_fits(D, self.dyf, xcls, None, dxc) and \
+            K.layernorm_bwd_f32_fits(D, self.dy1, self.x1s[0], self.dx, self.dx1)
+        # cls-sparse last block: only x[:, 0] of the last encoder block reaches the classifier head
+        # (models/vit_small.py:111-127), so past its qkv product that block is computed for the cls rows
+        # only -- the cls query's attention (pcv_attn_cls_fwd_f32), out projection, LayerNorm_1 and MLP on
+        # the B cls rows -- and its VJP likewise (the head VJP's dropout output, the MLP / LayerNorm /
+        # out-projection VJPs on the cls rows, pcv_attn_cls_bwd_f32: dK / dV of every key, dQ of the cls
+        # query).  Exact: every skipped value is multiplied by zero downstream.  The LayerNorm ViT with the
+        # fused head and attention only (the BatchNorm ViT's final norm reads every row).
+        self.cls_last = bool(self.head_fused and self.fused_attn and not self.bn and
+                             hip.load().pcv_attn_cls_f32_ok(T, self.Dh))
+        if self.cls_last:
+            i = L - 1
+            w = self.w[i]
+            c = lambda t: t.view(B, T, t.shape[1])[:, 0]  # noqa: E731   (the cls rows, stride T rows)
+            try:   # (the dropout-carrying products need the fused row GEMM: N % 128, K % 64)
+                gf = dict(
+                    out=_Dense(c(self.o[i]), w["Wo"], c(self.x1s[i]), bias=w["bo"], res=c(self.xs[i])),
+                    fc1=_Dense(c(self.y1[i]), w["W0"], c(self.a[i]), bias=w["b0"], aux=c(self.pre[i]), act=1,
+                               site=site_mlp_hidden(i), dropout=True, rstep=T),
+                    fc2=_Dense(c(self.a[i]), w["W1"], c(self.xs[i + 1]), bias=w["b1"], res=c(self.x1s[i]),
+                               site=site_mlp_out(i), dropout=True, rstep=T))
+                gb = dict(
+                    fc2_d=_Dense(c(self.dmo_l[i]), w["W1"], c(self.da_l[i]), tb=True, aux=c(self.pre[i]), act=2,
+                                 site=site_mlp_hidden(i), dropout=True, rstep=T),
+                    fc1_d=_Dense(c(self.da_l[i]), w["W0"], c(self.dy1), tb=True),
+                    out_d=_Dense(c(self.dx1_l[i]), w["Wo"], c(self.dO), tb=True))
+            except ValueError:
+                self.cls_last = False
+            else:
+                self.gf[i].update(gf)
+                self.gb[i].update(gb)
+                self.cls_rows = c
         # block 0's qkv product runs beside the previous step's Newton-Schulz phase when the optimizer
         # overlaps it (GraphedTrainStep overlap_opt, joined before block 0's fc1): the panel form's
         # persistent grid (one workgroup per CU) then waits for CUs the side stream holds (37.6 vs 24.5 us
@@ -275,22 +324,16 @@ class ViTRunnerF32:
         ks = lambda t: max(1, t.shape[0] // 256)  # noqa: E731   (few tiles: a deep K split)
         # (+ the bias gradient = column sums of the same output gradient, folded into the row-panel
         # launch where the product fits it; otherwise a colsum launch in the backward)
-        # the LayerNorm ViT's classifier head runs as two fused kernels (pcv_vit_head_{fwd,bwd}_f32: final
-        # LayerNorm + head GEMM + bias + cross-entropy, and the VJP with the head's parameter gradients)
-        # when the LayerNorm parameter partials are deferred to ln_red (planned below)
-        head_ok = self.m.use_layernorm and bool(hip.load().pcv_vit_head_f32_ok(D, self.Kc)) and B <= 1024 and \
-            self.Wh.stride(1) == 1 and self.gWh.stride(1) == 1 and self.Wh.stride(0) % 4 == 0
-        xcls = self.xs[-1].view(B, T * D)[:, :D]
-        dxc = self.dx.view(B, T * D)[:, :D]
-        self.head_fused = head_ok and K.layernorm_bwd_f32_fits(D, self.dyf, xcls, None, dxc) and \
-            K.layernorm_bwd_f32_fits(D, self.dy1, self.x1s[0], self.dx, self.dx1)
         prods = [] if self.head_fused else [(self.yf, self.dlogits, self.gWh, self.gbh)]
         if not self.pe_fused:   # (else the fused embedding VJP forms the conv gradients)
             prods.append((self.patches, self.dpatch, self.gWconv, self.gbconv))
         for i in range(L):
             w = self.w[i]
-            prods += [(self.a[i], self.dmo_l[i], w["gW1"], w["gb1"]), (self.y1[i], self.da_l[i], w["gW0"], w["gb0"]),
-                      (self.o[i], self.dx1_l[i], w["gWo"], w["gbo"]), (self.y0[i], self.dqkv_l[i], w["gWqkv"], w["gbqkv"])]
+            c = self.cls_rows if (self.cls_last and i == L - 1) else (lambda t: t)   # (K = B cls rows there)
+            prods += [(c(self.a[i]), c(self.dmo_l[i]), w["gW1"], w["gb1"]),
+                      (c(self.y1[i]), c(self.da_l[i]), w["gW0"], w["gb0"]),
+                      (c(self.o[i]), c(self.dx1_l[i]), w["gWo"], w["gbo"]),
+                      (self.y0[i], self.dqkv_l[i], w["gWqkv"], w["gbqkv"])]
         self.colsum_folded = set()
         # one workspace for every stand-alone bias column sum (they run one after another)
         self.colsum_ws = torch.zeros(max(K.colsum_ws_floats(B * T, max(3 * D, self.M, self.Kc)),
@@ -317,7 +360,7 @@ class ViTRunnerF32:
                                                nblk=B if self.head_fused else None)
             for i in range(L):
                 w = self.w[i]
-                red.add(self.ln_ws[1 + 2 * i], B * T, D, w["gs1"], w["gc1"])
+                red.add(self.ln_ws[1 + 2 * i], B if (self.cls_last and i == L - 1) else B * T, D, w["gs1"], w["gc1"])
                 red.add(self.ln_ws[2 + 2 * i], B * T, D, w["gs0"], w["gc0"])
             self.ln_red = red.finalize(dev)
 
@@ -385,7 +428,12 @@ class ViTRunnerF32:
                 self._bn(x, w["ra0"], self.bst0[i], w["s0"], w["c0"], self.y0[i], train)
             g = self.gf[i]
             g["qkv"].run()
-            if self.fused_attn:
+            last_cls = self.cls_last and i == m.num_layers - 1
+            if last_cls:   # the cls query's attention only (the rest of the block follows on the cls rows)
+                hip.call("pcv_attn_cls_fwd_f32", ptr(self.qkv[i]), 3 * D, ptr(self.o[i]), D, ptr(self.mrow[i]),
+                         ptr(self.linv[i]), B, T, self.H, D, ptr(self._mask(i)) if rate > 0 else None, float(rate),
+                         stream_ptr())
+            elif self.fused_attn:
                 hip.call("pcv_attn_fwd_f32", ptr(self.qkv[i]), 3 * D, ptr(self.o[i]), D, ptr(self.mrow[i]),
                          ptr(self.linv[i]), B, T, self.H, D, ptr(self._mask(i)) if rate > 0 else None, float(rate),
                          stream_ptr())
@@ -395,7 +443,9 @@ class ViTRunnerF32:
                          self.S.shape[0], T, ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
                 g["pv"].run()
             g["out"].run()
-            if m.use_layernorm:
+            if last_cls:
+                self._ln(self.cls_rows(self.x1s[i]), w["s1"], w["c1"], self.cls_rows(self.y1[i]), self.st1[i])
+            elif m.use_layernorm:
                 self._ln(self.x1s[i], w["s1"], w["c1"], self.y1[i], self.st1[i])
             elif self.bn:
                 self._bn(self.x1s[i], w["ra1"], self.bst1[i], w["s1"], w["c1"], self.y1[i], train)
@@ -444,9 +494,12 @@ class ViTRunnerF32:
         dxc = self.dx.view(B, T * D)[:, :D]
         xcls = self.xs[-1].view(B, T * D)[:, :D]
         if self.head_fused:   # dyf, the final LayerNorm VJP into dx's cls rows, gWh / gbh, the LN partials
+            # (cls-sparse last block: also its MLP-out dropout VJP of those rows, into dmo's cls rows)
+            dmo = self.dmo_l[m.num_layers - 1] if self.cls_last else None
             hip.call("pcv_vit_head_bwd_f32", ptr(self.dlogits), ptr(self.Wh), self.Wh.stride(0), ptr(xcls), T * D,
                      ptr(self.sf), ptr(self.stf[0]), ptr(self.stf[1]), ptr(self.yf), ptr(dxc), T * D,
-                     ptr(self.ln_ws[0]), ptr(self.gWh), self.gWh.stride(0), ptr(self.gbh), B, D, self.Kc, stream_ptr())
+                     ptr(self.ln_ws[0]), ptr(self.gWh), self.gWh.stride(0), ptr(self.gbh), B, D, self.Kc, ptr(dmo),
+                     T * D, T, float(rate), ptr(seed), site_mlp_out(m.num_layers - 1), stream_ptr())
         else:
             self._colsum(self.dlogits, self.gbh)
             self.g_head_d.run()
@@ -461,6 +514,22 @@ class ViTRunnerF32:
         for i in reversed(range(m.num_layers)):
             w, g = self.w[i], self.gb[i]
             dmo, da, dx1, dqkv = self.dmo_l[i], self.da_l[i], self.dx1_l[i], self.dqkv_l[i]
+            if self.cls_last and i == m.num_layers - 1:   # the cls rows only (dmo's were written by the head VJP)
+                c = self.cls_rows
+                self._colsum(c(dmo), w["gb1"])
+                g["fc2_d"].run(rate, seed)
+                self._colsum(c(da), w["gb0"])
+                g["fc1_d"].run()
+                self._ln_bwd(1 + 2 * i, c(self.dy1), c(self.x1s[i]), w["s1"], self.st1[i], c(dx_in), c(dx1), w["gs1"],
+                             w["gc1"])
+                self._colsum(c(dx1), w["gbo"])
+                g["out_d"].run()
+                hip.call("pcv_attn_cls_bwd_f32", ptr(self.qkv[i]), 3 * D, ptr(self.dO), D, ptr(self.mrow[i]),
+                         ptr(self.linv[i]), ptr(dqkv), 3 * D, B, T, self.H, D,
+                         ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
+                self._qkv_bwd(i, rate, seed, dx1)
+                dx_in = self.dxo[i]
+                continue
             if i == m.num_layers - 1 or self.ln_red is None:   # else written by layer i+1's LN_0 VJP
                 _epi_bwd(dx_in, dmo, rate=rate, seed=seed, site=site_mlp_out(i))        # MLP-out dropout VJP
             self._colsum(dmo, w["gb1"])
@@ -483,17 +552,7 @@ class ViTRunnerF32:
                 hip.call("pcv_attn_softmax_bwd_f32", ptr(self.P[i]), ptr(self.S), self.S.shape[0], T,
                          ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
                 g["dqk"].run()                                                         # dQ, dK
-            self._colsum(dqkv, w["gbqkv"])
-            g["qkv_d"].run()                                                           # self.dy0 = dqkv Wqkv^T
-            if m.use_layernorm:
-                drop = dict(dxd=self.dmo_l[i - 1], rate=rate, seed=seed, site=site_mlp_out(i - 1)) if i > 0 else {}
-                self._ln_bwd(2 + 2 * i, self.dy0, self.xs[i], w["s0"], self.st0[i], dx1, self.dxo[i], w["gs0"],
-                             w["gc0"], **drop)
-            elif self.bn:
-                K.batchnorm_bwd(self.dy0, self.xs[i], *self.bst0[i], w["s0"], dx1, self.dxo[i], None, w["gs0"],
-                                w["gc0"], self.bn_ws)
-            else:
-                _epi(self.dy0, self.dxo[i], res=dx1)
+            self._qkv_bwd(i, rate, seed, dx1)
             dx_in = self.dxo[i]
         if self.pe_fused:   # dpos, dcls and the conv weight / bias gradients from the same images
             hip.call("pcv_vit_patch_embed_bwd_f32", ptr(dx_in), ptr(self.images), ptr(self.gcls), ptr(self.gpos),
@@ -507,6 +566,21 @@ class ViTRunnerF32:
             part.run()
         if self.ln_red is not None:
             self.ln_red.run()
+
+    def _qkv_bwd(self, i, rate, seed, dx1):
+        """Block i's qkv-product VJP and LayerNorm_0 VJP (with the residual gradient dx1) into dxo[i]."""
+        m, w = self.m, self.w[i]
+        self._colsum(self.dqkv_l[i], w["gbqkv"])
+        self.gb[i]["qkv_d"].run()                                                      # self.dy0 = dqkv Wqkv^T
+        if m.use_layernorm:
+            drop = dict(dxd=self.dmo_l[i - 1], rate=rate, seed=seed, site=site_mlp_out(i - 1)) if i > 0 else {}
+            self._ln_bwd(2 + 2 * i, self.dy0, self.xs[i], w["s0"], self.st0[i], dx1, self.dxo[i], w["gs0"], w["gc0"],
+                         **drop)
+        elif self.bn:
+            K.batchnorm_bwd(self.dy0, self.xs[i], *self.bst0[i], w["s0"], dx1, self.dxo[i], None, w["gs0"], w["gc0"],
+                            self.bn_ws)
+        else:
+            _epi(self.dy0, self.dxo[i], res=dx1)
 
     def flops_per_step(self):
         B, T, D, M, Kc = self.B, self.T, self.D, self.M, self.Kc
