@@ -565,26 +565,42 @@ __global__ __launch_bounds__(256) void patch_embed_fold_kernel(const float* __re
 // thread = key: the same numerics as the fused forward's VALU tail row (scaled scores, max, exp,
 // sum; dropout keep bits of query 0 from the packed mask; O = sum_k Pd V / l * dscale) and the same
 // row statistics (mrow = max of the scaled scores, linv = 1 / sum) at query slot 0.
-constexpr int AC_THREADS = 256;
+constexpr int AC_THREADS = 256, AC_LD = FA_DH_CLS + 4;   // K / V images [T][36] (conflict-free float4 rows)
+
+// the head's K and V rows of batch b into LDS (each row = one 128-B line; all loads issued at once)
+__device__ __forceinline__ void ac_stage(const float* __restrict__ qkv, int64_t ldqkv, int64_t bT, int h, int D, int T,
+                                         float* Ks, float* Vs) {
+  for (int i = threadIdx.x; i < T * (FA_DH_CLS / 4); i += AC_THREADS) {
+    const int k = i / (FA_DH_CLS / 4), c = (i % (FA_DH_CLS / 4)) * 4;
+    const float* r = qkv + (bT + k) * ldqkv + h * FA_DH_CLS + c;
+    *reinterpret_cast<f32x4*>(Ks + k * AC_LD + c) = *reinterpret_cast<const f32x4*>(r + D);
+    *reinterpret_cast<f32x4*>(Vs + k * AC_LD + c) = *reinterpret_cast<const f32x4*>(r + 2 * D);
+  }
+}
+
 __global__ __launch_bounds__(AC_THREADS) void attn_cls_fwd_f32_kernel(const float* __restrict__ qkv, int64_t ldqkv,
                                                                       float* out, int64_t ldo, float* mrow,
                                                                       float* linv, const uint16_t* __restrict__ mask,
                                                                       int T, int H, int D, int n64, float scale,
                                                                       float dscale) {
+  extern __shared__ __attribute__((aligned(16))) float ac_lds[];   // K [T][36], V [T][36]
   __shared__ float q0[FA_DH_CLS];
   __shared__ float pk[FA_TMAX_CLS];
   __shared__ float red[2 * (AC_THREADS / 64)];
   __shared__ float part[FA_DH_CLS][9];
+  float* Ks = ac_lds;
+  float* Vs = ac_lds + T * AC_LD;
   const int h = blockIdx.x, b = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t bT = (int64_t)b * T, bh = (int64_t)b * H + h;
   if (threadIdx.x < FA_DH_CLS) q0[threadIdx.x] = qkv[bT * ldqkv + h * FA_DH_CLS + threadIdx.x];
+  ac_stage(qkv, ldqkv, bT, h, D, T, Ks, Vs);
   __syncthreads();
   float sv[2] = {-__builtin_inff(), -__builtin_inff()};
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int key = threadIdx.x + AC_THREADS * j;
     if (key < T) {
-      const float* kr = qkv + (bT + key) * ldqkv + D + h * FA_DH_CLS;
+      const float* kr = Ks + key * AC_LD;
       float acc = 0.f;
 #pragma unroll
       for (int c = 0; c < FA_DH_CLS; c += 4) {
@@ -616,7 +632,7 @@ __global__ __launch_bounds__(AC_THREADS) void attn_cls_fwd_f32_kernel(const floa
   {   // O = sum_k Pd V: thread (d, key slice of 8)
     const int d = threadIdx.x & 31, sl = threadIdx.x >> 5;
     float acc = 0.f;
-    for (int k = sl; k < T; k += 8) acc += pk[k] * qkv[(bT + k) * ldqkv + 2 * D + h * FA_DH_CLS + d];
+    for (int k = sl; k < T; k += 8) acc += pk[k] * Vs[k * AC_LD + d];
     part[d][sl] = acc;
   }
   __syncthreads();
@@ -646,14 +662,18 @@ __global__ __launch_bounds__(AC_THREADS) void attn_cls_bwd_f32_kernel(const floa
                                                                       int64_t lddqkv, const uint16_t* __restrict__ mask,
                                                                       int T, int H, int D, int n64, float scale,
                                                                       float dscale) {
+  extern __shared__ __attribute__((aligned(16))) float ac_lds[];   // K [T][36], V [T][36]
   __shared__ float q0[FA_DH_CLS], do0[FA_DH_CLS];
-  __shared__ float dsk[FA_TMAX_CLS];
+  __shared__ float dsk[FA_TMAX_CLS], pdk[FA_TMAX_CLS];
   __shared__ float red[AC_THREADS / 64];
   __shared__ float part[FA_DH_CLS][9];
+  float* Ks = ac_lds;
+  float* Vs = ac_lds + T * AC_LD;
   const int h = blockIdx.x, b = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t bT = (int64_t)b * T, bh = (int64_t)b * H + h;
   if (threadIdx.x < FA_DH_CLS) q0[threadIdx.x] = qkv[bT * ldqkv + h * FA_DH_CLS + threadIdx.x];
   else if (threadIdx.x < 2 * FA_DH_CLS) do0[threadIdx.x - FA_DH_CLS] = dout[bT * lddo + h * FA_DH_CLS + threadIdx.x - FA_DH_CLS];
+  ac_stage(qkv, ldqkv, bT, h, D, T, Ks, Vs);
   __syncthreads();
   const float m0 = mrow[bh * T], l0 = linv[bh * T];
   float pv[2] = {0.f, 0.f}, dpv[2] = {0.f, 0.f};
@@ -663,8 +683,8 @@ __global__ __launch_bounds__(AC_THREADS) void attn_cls_bwd_f32_kernel(const floa
   for (int j = 0; j < 2; ++j) {
     const int key = threadIdx.x + AC_THREADS * j;
     if (key < T) {
-      const float* kr = qkv + (bT + key) * ldqkv + D + h * FA_DH_CLS;
-      const float* vr = kr + D;
+      const float* kr = Ks + key * AC_LD;
+      const float* vr = Vs + key * AC_LD;
       float s = 0.f, dp = 0.f;
 #pragma unroll
       for (int c = 0; c < FA_DH_CLS; c += 4) {
@@ -690,23 +710,23 @@ __global__ __launch_bounds__(AC_THREADS) void attn_cls_bwd_f32_kernel(const floa
   for (int j = 0; j < 2; ++j) {
     const int key = threadIdx.x + AC_THREADS * j;
     if (key < T) {
-      const float ds = pv[j] * (dpv[j] - delta);
-      dsk[key] = ds;
-      const float pd = kp[j] ? pv[j] * (mask ? dscale : 1.f) : 0.f;
-      float* dk = dqkv + (bT + key) * lddqkv + D + h * FA_DH_CLS;
-      float* dvv = dk + D;
-#pragma unroll
-      for (int c = 0; c < FA_DH_CLS; c += 4) {
-        *reinterpret_cast<f32x4*>(dk + c) = f32x4{q0[c], q0[c + 1], q0[c + 2], q0[c + 3]} * (scale * ds);
-        *reinterpret_cast<f32x4*>(dvv + c) = f32x4{do0[c], do0[c + 1], do0[c + 2], do0[c + 3]} * pd;
-      }
+      dsk[key] = pv[j] * (dpv[j] - delta);
+      pdk[key] = kp[j] ? pv[j] * (mask ? dscale : 1.f) : 0.f;
     }
   }
   __syncthreads();
+  // dK / dV rows: thread -> (key, float4 column) so a wave writes whole 128-B rows
+  for (int i = threadIdx.x; i < T * (FA_DH_CLS / 4); i += AC_THREADS) {
+    const int key = i / (FA_DH_CLS / 4), c = (i % (FA_DH_CLS / 4)) * 4;
+    float* dk = dqkv + (bT + key) * lddqkv + D + h * FA_DH_CLS + c;
+    const float ds = dsk[key] * scale, pd = pdk[key];
+    *reinterpret_cast<f32x4*>(dk) = f32x4{q0[c], q0[c + 1], q0[c + 2], q0[c + 3]} * ds;
+    *reinterpret_cast<f32x4*>(dk + D) = f32x4{do0[c], do0[c + 1], do0[c + 2], do0[c + 3]} * pd;
+  }
   {   // dQ_0 = scale sum_k dS_k K_k: thread (d, key slice of 8)
     const int d = threadIdx.x & 31, sl = threadIdx.x >> 5;
     float acc = 0.f;
-    for (int k = sl; k < T; k += 8) acc += dsk[k] * qkv[(bT + k) * ldqkv + D + h * FA_DH_CLS + d];
+    for (int k = sl; k < T; k += 8) acc += dsk[k] * Ks[k * AC_LD + d];
     part[d][sl] = acc;
   }
   __syncthreads();
@@ -1918,7 +1938,14 @@ extern "C" int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls
 }
 
 // ---- cls-query attention ----
-extern "C" int pcv_attn_cls_f32_ok(int T, int head_dim) { return T >= 1 && T <= FA_TMAX_CLS && T <= 2 * AC_THREADS && head_dim == FA_DH_CLS; }
+// (K / V images of 2 T 36 floats: 74 KiB at T = 257, 110 KiB at the T <= 384 cap, dynamic LDS past 64 KiB
+// opted in per kernel)
+extern "C" int pcv_attn_cls_f32_ok(int T, int head_dim) { return T >= 1 && T <= 384 && head_dim == FA_DH_CLS; }
+static int ac_optin(const void* fn) {
+  static PcvLdsOptIn f, b;
+  return fn == reinterpret_cast<const void*>(&attn_cls_fwd_f32_kernel) ? f.ensure(fn, 2 * 384 * AC_LD * 4)
+                                                                       : b.ensure(fn, 2 * 384 * AC_LD * 4);
+}
 
 extern "C" int pcv_attn_cls_fwd_f32(const float* qkv, int64_t ldqkv, float* out, int64_t ldo, float* mrow, float* linv,
                                     int B, int T, int H, int D, const uint16_t* mask, float rate, void* stream) {
@@ -1926,7 +1953,9 @@ extern "C" int pcv_attn_cls_fwd_f32(const float* qkv, int64_t ldqkv, float* out,
       ldqkv < 3 * D || ldo < D || ((ldqkv | ldo) & 3) || (rate > 0.f && !mask) || rate < 0.f || rate >= 1.f)
     return PCV_EINVAL;
   if ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(out)) & 15) return PCV_EALIGN;
-  hipLaunchKernelGGL(attn_cls_fwd_f32_kernel, dim3(H, B), dim3(AC_THREADS), 0, (hipStream_t)stream, qkv, ldqkv, out, ldo,
+  if (const int e = ac_optin(reinterpret_cast<const void*>(&attn_cls_fwd_f32_kernel))) return e;
+  hipLaunchKernelGGL(attn_cls_fwd_f32_kernel, dim3(H, B), dim3(AC_THREADS), 2 * T * AC_LD * 4, (hipStream_t)stream, qkv,
+                     ldqkv, out, ldo,
                      mrow, linv, rate > 0.f ? mask : nullptr, T, H, D, 2 * ((T + 127) / 128), 1.f / sqrtf((float)FA_DH_CLS),
                      rate > 0.f ? 1.f / (1.f - rate) : 1.f);
   return pcv_launch_status();
@@ -1941,7 +1970,9 @@ extern "C" int pcv_attn_cls_bwd_f32(const float* qkv, int64_t ldqkv, const float
     return PCV_EINVAL;
   if ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(dqkv) | reinterpret_cast<uintptr_t>(dout)) & 15)
     return PCV_EALIGN;
-  hipLaunchKernelGGL(attn_cls_bwd_f32_kernel, dim3(H, B), dim3(AC_THREADS), 0, (hipStream_t)stream, qkv, ldqkv, dout,
+  if (const int e = ac_optin(reinterpret_cast<const void*>(&attn_cls_bwd_f32_kernel))) return e;
+  hipLaunchKernelGGL(attn_cls_bwd_f32_kernel, dim3(H, B), dim3(AC_THREADS), 2 * T * AC_LD * 4, (hipStream_t)stream, qkv,
+                     ldqkv, dout,
                      lddo, mrow, linv, dqkv, lddqkv, rate > 0.f ? mask : nullptr, T, H, D, 2 * ((T + 127) / 128),
                      1.f / sqrtf((float)FA_DH_CLS), rate > 0.f ? 1.f / (1.f - rate) : 1.f);
   return pcv_launch_status();
