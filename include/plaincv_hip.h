@@ -281,6 +281,26 @@ int pcv_vit_embed_fwd_f32(const float* patch, const float* bias, const float* cl
                           int T, int D, float rate, const uint32_t* seed, uint32_t site, void* stream);
 int pcv_vit_embed_bwd_f32(const float* dx, float* dpatch, float* dcls, float* dpos, int B, int T, int D, float rate,
                           const uint32_t* seed, uint32_t site, void* stream);
+/* The cls-row chain of a cls-token ViT's last encoder block (after its cls-query attention), one launch
+ * per direction, block = cls row b (rows b ldrow of the D-wide and b ldrowm of the M-wide tensors; the
+ * dropout index uses the token row b T): forward x1 = o wo + bo + x, y1 = LayerNorm(x1; s1, c1, eps) (+
+ * mean / rstd at b), pre = y1 w0 + b0, a = dropout(gelu(pre)) (site_h), xo = x1 + dropout(a w1 + b1)
+ * (site_o); VJP da = dropout_vjp(dmo w1^T) gelu'(pre), dy1 = da w0^T, dx1 = dres + LayerNorm VJP(dy1),
+ * dO = dx1 wo^T and the LayerNorm parameter partials part[b] = [dy1 xhat | dy1] (B partial rows for
+ * pcv_layernorm_part_reduce).  The row GEMM epilogue's GELU / dropout conventions.  ok: D <= 256,
+ * M <= 1024, D % 32 == 0, M % 32 == 0. */
+int pcv_vit_cls_chain_f32_ok(int D, int M);
+int pcv_vit_cls_chain_fwd_f32(const float* o, const float* x, const float* wo, int64_t ldwo, const float* bo,
+                              const float* s1, const float* c1, const float* w0, int64_t ldw0, const float* b0,
+                              const float* w1, int64_t ldw1, const float* b1, float* x1, float* y1, float* mean,
+                              float* rstd, float* pre, float* a, float* xo, int64_t ldrow, int64_t ldrowm, int B, int T,
+                              int D, int M, float eps, float rate, const uint32_t* seed, uint32_t site_h,
+                              uint32_t site_o, void* stream);
+int pcv_vit_cls_chain_bwd_f32(const float* dmo, const float* w1, int64_t ldw1, const float* pre, const float* w0,
+                              int64_t ldw0, const float* x1, const float* s1, const float* mean, const float* rstd,
+                              const float* dres, const float* wo, int64_t ldwo, float* da, float* dx1, float* dO,
+                              float* part, int64_t ldrow, int64_t ldrowm, int B, int T, int D, int M, float rate,
+                              const uint32_t* seed, uint32_t site_h, void* stream);
 /* Fused fp32 classifier head (models/vit_small.py:111-127 + the softmax cross-entropy of
  * flax_engine.py:38-44): per cls row b (x + b ldx), yf = LayerNorm(x; scale, bias, eps) (+ mean / rstd),
  * logits = yf wh + bh (wh [D][Kc]), row_loss = lse - logits[label], row_correct = argmax == label (lowest

@@ -738,12 +738,6 @@ __global__ __launch_bounds__(AC_THREADS) void attn_cls_bwd_f32_kernel(const floa
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Fused classifier head of the fp32 ViT (models/vit_small.py:111-127 + flax_engine's loss): per cls
-// row b, the final LayerNorm (ln16_fwd_f32's math: fast variance clipped at 0, eps), logits = y Wh + bh
-// (fp32 FMAs in k order), the softmax cross-entropy with the row loss, the argmax hit (lowest index on
-// ties, as xent_kernel) and dlogits = (softmax - onehot) grad_scale -- one launch for the LayerNorm,
-// head GEMM, bias epilogue and loss kernels.  Block = row, 256 threads; D <= 256, Kc <= 1024.
 constexpr int HD_THREADS = 256;
 __device__ __forceinline__ float hd_block_sum(float v, float* red) {   // fixed order: waves in index order
   v = wave_sum(v);
@@ -755,6 +749,189 @@ __device__ __forceinline__ float hd_block_sum(float v, float* red) {   // fixed 
   for (int i = 0; i < HD_THREADS / 64; ++i) s += red[i];
   return s;
 }
+
+// ---------------------------------------------------------------------------------------------
+// The cls-row chain of the last encoder block (after its cls-query attention) as one launch per
+// direction, block = cls row b (token row b T), 256 threads, weights read from L2 as matvecs (16 loads in
+// flight, summed in k order):
+//   forward  x1 = o Wo + bo + x;  y1 = LayerNorm_1(x1);  pre = y1 W0 + b0;  a = dropout(gelu(pre));
+//            xo = x1 + dropout(a W1 + b1)
+//   VJP      da = dropout_vjp(dmo W1^T) gelu'(pre);  dy1 = da W0^T;  dx1 = dres + LN_1 VJP(dy1);
+//            dO = dx1 Wo^T;  + the LayerNorm_1 parameter partials of the row
+// with the row GEMM epilogue's element order, GELU (sigmoid form) and dropout indices (token row T b).
+__device__ __forceinline__ float cc_gelu(float x) {   // = gr_gelu (gemm_f32.hip)
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return x / (1.f + __expf(-2.f * u));
+}
+__device__ __forceinline__ float cc_gelu_grad(float x) {   // = gr_gelu_grad
+  const float k = 0.7978845608028654f;
+  const float u = k * (x + 0.044715f * x * x * x), du = k * (1.f + 3.f * 0.044715f * x * x);
+  const float sg = 1.f / (1.f + __expf(-2.f * u));
+  return sg * (1.f + 2.f * x * du * (1.f - sg));
+}
+// out[n] = sum_k v[k] W[k][n] for n < N (W row-major, rows ld apart), v in LDS: thread -> (float4 column
+// group, k slice of K / NS consecutive rows), every load of the slice in flight at once; the slices'
+// partials summed in slice order through LDS (part: NS x N floats).  Ends with out written (LDS).
+__device__ __forceinline__ void cc_mv(const float* v, const float* __restrict__ W, int64_t ld, int K, int N,
+                                      float* part, float* out) {
+  const int G = N / 4, NS = HD_THREADS / G, KS = K / NS;
+  const int t = threadIdx.x, gcol = (t % G) * 4, sl = t / G;
+  f32x4 acc{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = sl * KS; k0 < (sl + 1) * KS; k0 += 16) {
+    f32x4 w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = *reinterpret_cast<const f32x4*>(W + (int64_t)(k0 + j) * ld + gcol);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc += v[k0 + j] * w[j];
+  }
+  *reinterpret_cast<f32x4*>(part + sl * N + gcol) = acc;
+  __syncthreads();
+  for (int n = t; n < N; n += HD_THREADS) {
+    float r = 0.f;
+    for (int q = 0; q < NS; ++q) r += part[q * N + n];
+    out[n] = r;
+  }
+  __syncthreads();
+}
+// out[r] = sum_j v[j] W[r][j] for r < N (rows of length K, contiguous): thread -> (row, slice of K / NS),
+// the slice's float4s all in flight; slice partials summed in order through LDS.
+__device__ __forceinline__ void cc_mvt(const float* v, const float* __restrict__ W, int64_t ld, int K, int N,
+                                       float* part, float* out) {
+  const int NS = HD_THREADS / N, KS = K / NS;
+  const int t = threadIdx.x, r = t % N, sl = t / N;
+  const float* wr = W + (int64_t)r * ld + sl * KS;
+  const float* vs = v + sl * KS;
+  float a = 0.f;
+  for (int c0 = 0; c0 < KS; c0 += 64) {
+    f32x4 w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = *reinterpret_cast<const f32x4*>(wr + c0 + 4 * j);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a += vs[c0 + 4 * j + e] * w[j][e];
+  }
+  part[sl * N + r] = a;
+  __syncthreads();
+  for (int n = t; n < N; n += HD_THREADS) {
+    float q = 0.f;
+    for (int i = 0; i < NS; ++i) q += part[i * N + n];
+    out[n] = q;
+  }
+  __syncthreads();
+}
+
+struct ClsArgs {
+  const float *o, *x, *Wo, *bo, *s1, *c1, *W0, *b0, *W1, *b1;
+  float *x1, *y1, *mean, *rstd, *pre, *a, *xo;
+  const float *dmo;
+  float *da, *dx1, *dO, *part;
+  const float* dres;
+  const uint32_t* seed;
+  int64_t ldrow, ldrowm, ldWo, ldW0, ldW1;   // token-row strides (D / M wide tensors), weight row strides
+  int D, M, T;
+  uint32_t thresh, site_h, site_o;
+  float dscale, eps;
+};
+
+__global__ __launch_bounds__(HD_THREADS) void cls_chain_fwd_f32_kernel(ClsArgs g) {
+  __shared__ __attribute__((aligned(16))) float part[HD_THREADS * 4];
+  __shared__ float ov[256], x1v[256], yv[256], hv[1024], red[8];
+  const int b = blockIdx.x, t = threadIdx.x, D = g.D, M = g.M;
+  const int64_t rD = (int64_t)b * g.ldrow, rM = (int64_t)b * g.ldrowm;
+  const int64_t tok = (int64_t)b * g.T;   // token row of the dropout index
+  const uint32_t seed = g.thresh ? *g.seed : 0u;
+  for (int k = t; k < D; k += HD_THREADS) ov[k] = g.o[rD + k];
+  __syncthreads();
+  cc_mv(ov, g.Wo, g.ldWo, D, D, part, x1v);   // out projection
+  for (int n = t; n < D; n += HD_THREADS) {   // + bias + residual
+    const float v = (x1v[n] + g.bo[n]) + g.x[rD + n];
+    x1v[n] = v;
+    g.x1[rD + n] = v;
+  }
+  __syncthreads();
+  {   // LayerNorm_1 (fast variance, clipped at 0)
+    float s1 = 0.f, s2 = 0.f;
+    for (int n = t; n < D; n += HD_THREADS) { s1 += x1v[n]; s2 += x1v[n] * x1v[n]; }
+    s1 = hd_block_sum(s1, red);
+    s2 = hd_block_sum(s2, red + 4);
+    const float mu = s1 / D, rs = rsqrtf(fmaxf(s2 / D - mu * mu, 0.f) + g.eps);
+    for (int n = t; n < D; n += HD_THREADS) {
+      const float y = (x1v[n] - mu) * rs * g.s1[n] + g.c1[n];
+      yv[n] = y;
+      g.y1[rD + n] = y;
+    }
+    if (t == 0) { g.mean[b] = mu; g.rstd[b] = rs; }
+  }
+  __syncthreads();
+  cc_mv(yv, g.W0, g.ldW0, D, M, part, hv);   // fc1
+  for (int j = t; j < M; j += HD_THREADS) {   // + bias, GELU (pre stored), dropout
+    float v = hv[j] + g.b0[j];
+    g.pre[rM + j] = v;
+    v = cc_gelu(v);
+    if (g.thresh) v = hash3(seed, g.site_h, (uint32_t)(tok * M + j)) >= g.thresh ? v * g.dscale : 0.f;
+    hv[j] = v;
+    g.a[rM + j] = v;
+  }
+  __syncthreads();
+  cc_mv(hv, g.W1, g.ldW1, M, D, part, ov);   // fc2
+  for (int n = t; n < D; n += HD_THREADS) {   // + bias, dropout, + residual
+    float v = ov[n] + g.b1[n];
+    if (g.thresh) v = hash3(seed, g.site_o, (uint32_t)(tok * D + n)) >= g.thresh ? v * g.dscale : 0.f;
+    g.xo[rD + n] = v + x1v[n];
+  }
+}
+
+__global__ __launch_bounds__(HD_THREADS) void cls_chain_bwd_f32_kernel(ClsArgs g) {
+  __shared__ __attribute__((aligned(16))) float part[HD_THREADS * 4];
+  __shared__ __attribute__((aligned(16))) float dmv[256], dav[1024], dyv[256], dxv[256];
+  __shared__ float red[8];
+  const int b = blockIdx.x, t = threadIdx.x, D = g.D, M = g.M;
+  const int64_t rD = (int64_t)b * g.ldrow, rM = (int64_t)b * g.ldrowm;
+  const int64_t tok = (int64_t)b * g.T;
+  const uint32_t seed = g.thresh ? *g.seed : 0u;
+  for (int n = t; n < D; n += HD_THREADS) dmv[n] = g.dmo[rD + n];
+  __syncthreads();
+  cc_mvt(dmv, g.W1, g.ldW1, D, M, part, dav);   // fc2 VJP: rows j of W1 (length D)
+  for (int j = t; j < M; j += HD_THREADS) {   // the GELU-backward epilogue
+    float x = dav[j];
+    if (g.thresh) x = hash3(seed, g.site_h, (uint32_t)(tok * M + j)) >= g.thresh ? x * g.dscale : 0.f;
+    const float v = x * cc_gelu_grad(g.pre[rM + j]);
+    dav[j] = v;
+    g.da[rM + j] = v;
+  }
+  __syncthreads();
+  cc_mvt(dav, g.W0, g.ldW0, M, D, part, dyv);   // fc1 VJP: rows k of W0 (length M)
+  {   // LayerNorm_1 VJP (+ the residual gradient) and the row's parameter partials
+    const float mu = g.mean[b], rs = g.rstd[b];
+    float sg = 0.f, sgx = 0.f;
+    for (int n = t; n < D; n += HD_THREADS) {
+      const float xh = (g.x1[rD + n] - mu) * rs, gg = dyv[n] * g.s1[n];
+      sg += gg;
+      sgx += gg * xh;
+    }
+    sg = hd_block_sum(sg, red) / D;
+    sgx = hd_block_sum(sgx, red + 4) / D;
+    for (int n = t; n < D; n += HD_THREADS) {
+      const float xh = (g.x1[rD + n] - mu) * rs, gg = dyv[n] * g.s1[n];
+      const float v = g.dres[rD + n] + rs * (gg - sg - xh * sgx);
+      dxv[n] = v;
+      g.dx1[rD + n] = v;
+      g.part[(int64_t)b * 2 * D + n] = dyv[n] * xh;
+      g.part[(int64_t)b * 2 * D + D + n] = dyv[n];
+    }
+  }
+  __syncthreads();
+  cc_mvt(dxv, g.Wo, g.ldWo, D, D, dmv, dyv);   // out-projection VJP (dmv reused as the partial buffer)
+  for (int k = t; k < D; k += HD_THREADS) g.dO[rD + k] = dyv[k];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused classifier head of the fp32 ViT (models/vit_small.py:111-127 + flax_engine's loss): per cls
+// row b, the final LayerNorm (ln16_fwd_f32's math: fast variance clipped at 0, eps), logits = y Wh + bh
+// (fp32 FMAs in k order), the softmax cross-entropy with the row loss, the argmax hit (lowest index on
+// ties, as xent_kernel) and dlogits = (softmax - onehot) grad_scale -- one launch for the LayerNorm,
+// head GEMM, bias epilogue and loss kernels.  Block = row, 256 threads; D <= 256, Kc <= 1024.
 
 __global__ __launch_bounds__(HD_THREADS) void vit_head_fwd_f32_kernel(
     const float* __restrict__ x, int64_t ldx, const float* __restrict__ scale, const float* __restrict__ bias,
@@ -1975,6 +2152,57 @@ extern "C" int pcv_attn_cls_bwd_f32(const float* qkv, int64_t ldqkv, const float
                      ldqkv, dout,
                      lddo, mrow, linv, dqkv, lddqkv, rate > 0.f ? mask : nullptr, T, H, D, 2 * ((T + 127) / 128),
                      1.f / sqrtf((float)FA_DH_CLS), rate > 0.f ? 1.f / (1.f - rate) : 1.f);
+  return pcv_launch_status();
+}
+
+// ---- the last block's cls-row chain ----
+// widths: the matvecs' (float4 column group, k slice) maps need 256 % (N / 4) == 0 and 16-row slices
+// (cc_mv), 256 % rows == 0 and 64-long row slices (cc_mvt)
+extern "C" int pcv_vit_cls_chain_f32_ok(int D, int M) {
+  auto mv = [](int K, int N) { return N % 4 == 0 && N <= 1024 && 256 % (N / 4) == 0 && K % (16 * (256 / (N / 4))) == 0; };
+  auto mvt = [](int K, int N) { return N <= 256 && 256 % N == 0 && K % (64 * (256 / N)) == 0; };
+  return D > 0 && M > 0 && D <= 256 && M <= 1024 && mv(D, D) && mv(D, M) && mv(M, D) && mvt(D, M) && mvt(M, D) &&
+         mvt(D, D);
+}
+extern "C" int pcv_vit_cls_chain_fwd_f32(const float* o, const float* x, const float* wo, int64_t ldwo, const float* bo,
+                                         const float* s1, const float* c1, const float* w0, int64_t ldw0, const float* b0,
+                                         const float* w1, int64_t ldw1, const float* b1, float* x1, float* y1,
+                                         float* mean, float* rstd, float* pre, float* a, float* xo, int64_t ldrow,
+                                         int64_t ldrowm, int B, int T, int D, int M, float eps, float rate,
+                                         const uint32_t* seed, uint32_t site_h, uint32_t site_o, void* stream) {
+  if (B <= 0 || T <= 0 || !pcv_vit_cls_chain_f32_ok(D, M) || !o || !x || !wo || !bo || !s1 || !c1 || !w0 || !b0 ||
+      !w1 || !b1 || !x1 || !y1 || !mean || !rstd || !pre || !a || !xo || ldrow < D || ldrowm < M ||
+      (rate > 0.f && !seed) || rate < 0.f || rate >= 1.f)
+    return PCV_EINVAL;
+  ClsArgs g = {};
+  g.o = o; g.x = x; g.Wo = wo; g.bo = bo; g.s1 = s1; g.c1 = c1; g.W0 = w0; g.b0 = b0; g.W1 = w1; g.b1 = b1;
+  g.x1 = x1; g.y1 = y1; g.mean = mean; g.rstd = rstd; g.pre = pre; g.a = a; g.xo = xo; g.seed = seed;
+  g.ldrow = ldrow; g.ldrowm = ldrowm; g.ldWo = ldwo; g.ldW0 = ldw0; g.ldW1 = ldw1;
+  g.D = D; g.M = M; g.T = T; g.site_h = site_h; g.site_o = site_o; g.eps = eps;
+  f32_drop(rate, &g.thresh, &g.dscale);
+  hipLaunchKernelGGL(cls_chain_fwd_f32_kernel, dim3((unsigned)B), dim3(HD_THREADS), 0, (hipStream_t)stream, g);
+  return pcv_launch_status();
+}
+extern "C" int pcv_vit_cls_chain_bwd_f32(const float* dmo, const float* w1, int64_t ldw1, const float* pre,
+                                         const float* w0, int64_t ldw0, const float* x1, const float* s1,
+                                         const float* mean, const float* rstd, const float* dres, const float* wo,
+                                         int64_t ldwo, float* da, float* dx1, float* dO, float* part, int64_t ldrow,
+                                         int64_t ldrowm, int B, int T, int D, int M, float rate, const uint32_t* seed,
+                                         uint32_t site_h, void* stream) {
+  if (B <= 0 || T <= 0 || !pcv_vit_cls_chain_f32_ok(D, M) || !dmo || !w1 || !pre || !w0 || !x1 || !s1 || !mean ||
+      !rstd || !dres || !wo || !da || !dx1 || !dO || !part || ldrow < D || ldrowm < M ||
+      ((ldw1 | ldw0 | ldwo) & 3) || (rate > 0.f && !seed) || rate < 0.f || rate >= 1.f)
+    return PCV_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(w1) | reinterpret_cast<uintptr_t>(w0) | reinterpret_cast<uintptr_t>(wo)) & 15)
+    return PCV_EALIGN;
+  ClsArgs g = {};
+  g.dmo = dmo; g.W1 = w1; g.pre = const_cast<float*>(pre); g.W0 = w0; g.x1 = const_cast<float*>(x1); g.s1 = s1;
+  g.mean = const_cast<float*>(mean); g.rstd = const_cast<float*>(rstd); g.dres = dres; g.Wo = wo;
+  g.da = da; g.dx1 = dx1; g.dO = dO; g.part = part; g.seed = seed;
+  g.ldrow = ldrow; g.ldrowm = ldrowm; g.ldWo = ldwo; g.ldW0 = ldw0; g.ldW1 = ldw1;
+  g.D = D; g.M = M; g.T = T; g.site_h = site_h;
+  f32_drop(rate, &g.thresh, &g.dscale);
+  hipLaunchKernelGGL(cls_chain_bwd_f32_kernel, dim3((unsigned)B), dim3(HD_THREADS), 0, (hipStream_t)stream, g);
   return pcv_launch_status();
 }
 

@@ -80,6 +80,11 @@ SIGNATURES = {
     "pcv_attn_softmax_bwd_f32": [P, P, I64, I32, P, F32, P],
     "pcv_vit_embed_fwd_f32": [P, P, P, P, P, I32, I32, I32, F32, P, U32, P],
     "pcv_vit_embed_bwd_f32": [P, P, P, P, I32, I32, I32, F32, P, U32, P],
+    "pcv_vit_cls_chain_f32_ok": [I32, I32],
+    "pcv_vit_cls_chain_fwd_f32": [P, P, P, I64, P, P, P, P, I64, P, P, I64, P, P, P, P, P, P, P, P, I64, I64, I32, I32,
+                                  I32, I32, F32, F32, P, U32, U32, P],
+    "pcv_vit_cls_chain_bwd_f32": [P, P, I64, P, P, I64, P, P, P, P, P, P, I64, P, P, P, P, I64, I64, I32, I32, I32,
+                                  I32, F32, P, U32, P],
     "pcv_vit_head_f32_ok": [I32, I32],
     "pcv_vit_head_fwd_f32": [P, I64, P, P, P, I64, P, P, P, P, P, P, P, P, P, I32, I32, I32, F32, F32, P],
     "pcv_vit_head_bwd_f32": [P, P, I64, P, I64, P, P, P, P, P, I64, P, P, I64, P, I32, I32, I32, P, I64, I64, F32, P, U32,

@@ -310,6 +310,11 @@ class ViTRunnerF32:
                 self.gf[i].update(gf)
                 self.gb[i].update(gb)
                 self.cls_rows = c
+        # ... and that block's out projection / LayerNorm_1 / MLP (and their VJPs) on the cls rows as one
+        # launch per direction (pcv_vit_cls_chain_{fwd,bwd}_f32) where its widths fit
+        self.cls_chain = bool(self.cls_last and hip.load().pcv_vit_cls_chain_f32_ok(D, self.M) and
+                              all(self.w[L - 1][k].stride(0) % 4 == 0 and self.w[L - 1][k].stride(1) == 1
+                                  for k in ("Wo", "W0", "W1")))
         # block 0's qkv product runs beside the previous step's Newton-Schulz phase when the optimizer
         # overlaps it (GraphedTrainStep overlap_opt, joined before block 0's fc1): the panel form's
         # persistent grid (one workgroup per CU) then waits for CUs the side stream holds (37.6 vs 24.5 us
@@ -360,7 +365,9 @@ class ViTRunnerF32:
                                                nblk=B if self.head_fused else None)
             for i in range(L):
                 w = self.w[i]
-                red.add(self.ln_ws[1 + 2 * i], B if (self.cls_last and i == L - 1) else B * T, D, w["gs1"], w["gc1"])
+                last = self.cls_last and i == L - 1   # (cls rows: B; the fused chain leaves one partial per row)
+                red.add(self.ln_ws[1 + 2 * i], B if last else B * T, D, w["gs1"], w["gc1"],
+                        nblk=B if (last and self.cls_chain) else None)
                 red.add(self.ln_ws[2 + 2 * i], B * T, D, w["gs0"], w["gc0"])
             self.ln_red = red.finalize(dev)
 
@@ -442,6 +449,17 @@ class ViTRunnerF32:
                 hip.call("pcv_attn_softmax_f32", ptr(self.S), ptr(self.P[i]), ptr(self.Pd[i]),
                          self.S.shape[0], T, ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
                 g["pv"].run()
+            if last_cls and self.cls_chain:   # out projection, LayerNorm_1 and the MLP on the cls rows: one launch
+                if join is not None:
+                    join(i)
+                M = self.M
+                hip.call("pcv_vit_cls_chain_fwd_f32", ptr(self.o[i]), ptr(x), ptr(w["Wo"]), w["Wo"].stride(0),
+                         ptr(w["bo"]), ptr(w["s1"]), ptr(w["c1"]), ptr(w["W0"]), w["W0"].stride(0), ptr(w["b0"]),
+                         ptr(w["W1"]), w["W1"].stride(0), ptr(w["b1"]), ptr(self.x1s[i]), ptr(self.y1[i]),
+                         ptr(self.st1[i][0]), ptr(self.st1[i][1]), ptr(self.pre[i]), ptr(self.a[i]), ptr(self.xs[i + 1]),
+                         T * D, T * M, B, T, D, M, 1e-6, float(rate), ptr(seed), site_mlp_hidden(i), site_mlp_out(i),
+                         stream_ptr())
+                continue
             g["out"].run()
             if last_cls:
                 self._ln(self.cls_rows(self.x1s[i]), w["s1"], w["c1"], self.cls_rows(self.y1[i]), self.st1[i])
@@ -516,14 +534,24 @@ class ViTRunnerF32:
             dmo, da, dx1, dqkv = self.dmo_l[i], self.da_l[i], self.dx1_l[i], self.dqkv_l[i]
             if self.cls_last and i == m.num_layers - 1:   # the cls rows only (dmo's were written by the head VJP)
                 c = self.cls_rows
-                self._colsum(c(dmo), w["gb1"])
-                g["fc2_d"].run(rate, seed)
-                self._colsum(c(da), w["gb0"])
-                g["fc1_d"].run()
-                self._ln_bwd(1 + 2 * i, c(self.dy1), c(self.x1s[i]), w["s1"], self.st1[i], c(dx_in), c(dx1), w["gs1"],
-                             w["gc1"])
-                self._colsum(c(dx1), w["gbo"])
-                g["out_d"].run()
+                if self.cls_chain:   # MLP / LayerNorm_1 / out-projection VJPs of the cls rows: one launch
+                    M = self.M
+                    hip.call("pcv_vit_cls_chain_bwd_f32", ptr(dmo), ptr(w["W1"]), w["W1"].stride(0), ptr(self.pre[i]),
+                             ptr(w["W0"]), w["W0"].stride(0), ptr(self.x1s[i]), ptr(w["s1"]), ptr(self.st1[i][0]),
+                             ptr(self.st1[i][1]), ptr(dx_in), ptr(w["Wo"]), w["Wo"].stride(0), ptr(da), ptr(dx1),
+                             ptr(self.dO), ptr(self.ln_ws[1 + 2 * i]), T * D, T * M, B, T, D, M, float(rate),
+                             ptr(seed), site_mlp_hidden(i), stream_ptr())
+                    for t, gbias in ((dmo, "gb1"), (da, "gb0"), (dx1, "gbo")):
+                        self._colsum(c(t), w[gbias])
+                else:
+                    self._colsum(c(dmo), w["gb1"])
+                    g["fc2_d"].run(rate, seed)
+                    self._colsum(c(da), w["gb0"])
+                    g["fc1_d"].run()
+                    self._ln_bwd(1 + 2 * i, c(self.dy1), c(self.x1s[i]), w["s1"], self.st1[i], c(dx_in), c(dx1),
+                                 w["gs1"], w["gc1"])
+                    self._colsum(c(dx1), w["gbo"])
+                    g["out_d"].run()
                 hip.call("pcv_attn_cls_bwd_f32", ptr(self.qkv[i]), 3 * D, ptr(self.dO), D, ptr(self.mrow[i]),
                          ptr(self.linv[i]), ptr(dqkv), 3 * D, B, T, self.H, D,
                          ptr(self._mask(i)) if rate > 0 else None, float(rate), stream_ptr())
