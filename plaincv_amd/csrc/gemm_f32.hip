@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
 
 // Weight gradients dW[M][N] += A^T B (A = activations [K][M], B = output gradients [K][N], K = B*T
 // rows) for every weight of the step in one launch: a table of jobs, each M/64 x N/BN tiles x
-// ksplit slices of K; slice partial sums are added with fp32 atomics (dW is zeroed per step).
+// ksplit near-equal slices of K (dW is zeroed per step).
 // colsum (optional): += the column sums of B (the bias gradient of the same Dense), accumulated by
 // the workgroups of the first 64-row panel from the B chunks they already hold in LDS (the 256 / BN
 // per-thread partials of a column summed in thread order through LDS).
@@ -286,19 +286,25 @@ struct WgJob {
 static_assert(sizeof(WgJob) == 8 * 8 + 10 * 4, "WgJob layout");
 
 template <int BN>
-__global__ __launch_bounds__(256) void gemm_f32_wgrad_kernel(const WgJob* __restrict__ jobs, int njobs) {
+__global__ __launch_bounds__(256) void gemm_f32_wgrad_kernel(const WgJob* __restrict__ jobs, int njobs, int total) {
   __shared__ __attribute__((aligned(16))) float As[GR_BM * GR_LDK];
   __shared__ __attribute__((aligned(16))) float Bs[BN * GR_LDK];
   constexpr int WN = BN / 2, NJ = WN / 16;
   __shared__ int ft[256];
-  const int bid = blockIdx.x;
-  const int j = pcv_find_job<int32_t>(jobs, njobs, (int)sizeof(WgJob), (int)offsetof(WgJob, first), ft, 256);
+  // XCD-aware order: the tiles of one K slice (which share its A and B rows) and the job's next
+  // slices run on one XCD, so the operand rows are fetched into one L2 once instead of by all eight
+  const int bid = pcv_xcd_tile();
+  if (bid >= total) return;
+  const int j = pcv_find_job<int32_t>(jobs, njobs, (int)sizeof(WgJob), (int)offsetof(WgJob, first), ft, 256, bid);
   const WgJob jb = jobs[j];
   int t = bid - jb.first;
   const int sl = t / jb.tiles;   // slice-major: the blocks of one slice cover every tile of the job
   t -= sl * jb.tiles;
   const int m0 = (t / jb.tiles_n) * GR_BM, n0 = (t % jb.tiles_n) * BN;
-  const int kbeg = sl * jb.kchunk, kend = min(jb.K, kbeg + jb.kchunk);
+  // slice sl: chunks [sl nch / ksplit, (sl + 1) nch / ksplit) of the nch = K / 64 -- lengths differ by
+  // at most one chunk, so a launch planned as one resident round finishes together
+  const int nch = jb.K / GR_BK;
+  const int kbeg = GR_BK * (int)((int64_t)sl * nch / jb.ksplit), kend = GR_BK * (int)((int64_t)(sl + 1) * nch / jb.ksplit);
   f32x4 acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -364,15 +370,17 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(const WgJob* __restrict
   const float* p = jb.ws + (int64_t)t * jb.ksplit * (GR_BM * BN) + rr * BN + c;
   const int S = jb.ksplit;
   f32x4 acc{0.f, 0.f, 0.f, 0.f};
-  int q = 0;
-  for (; q + 8 <= S; q += 8) {
-    f32x4 v[8];
+  // batches of 16 slices with every load in flight (a ragged last batch masked, not a serial loop),
+  // added in slice order
+  for (int q = 0; q < S; q += 16) {
+    f32x4 v[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(p + (int64_t)(q + u) * GR_BM * BN);
+    for (int u = 0; u < 16; ++u)
+      v[u] = q + u < S ? *reinterpret_cast<const f32x4*>(p + (int64_t)(q + u) * GR_BM * BN) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc += v[u];
+    for (int u = 0; u < 16; ++u)
+      if (q + u < S) acc += v[u];
   }
-  for (; q < S; ++q) acc += *reinterpret_cast<const f32x4*>(p + (int64_t)q * GR_BM * BN);
   float* cp = jb.C + (int64_t)(m0 + rr) * jb.ldc + n0 + c;   // M % 64 == 0, N % BN == 0: in range
   *reinterpret_cast<f32x4*>(cp) = *reinterpret_cast<const f32x4*>(cp) + acc;
   if (jb.colsum && m0 == 0 && rg == 0 && threadIdx.x < BN) {   // the first panel's column partials
@@ -847,11 +855,12 @@ extern "C" int pcv_gemm_f32_wgrad_fold(const void* jobs_dev, int njobs, int64_t 
 extern "C" int pcv_gemm_f32_wgrad(const void* jobs_dev, int njobs, int64_t total_blocks, int bn, void* stream) {
   if (!jobs_dev || njobs <= 0 || total_blocks <= 0 || total_blocks >= (1ll << 31) || (bn != 64 && bn != 128))
     return PCV_EINVAL;
+  const unsigned grid = (unsigned)pcv_xcd_grid(total_blocks);
   if (bn == 64)
-    hipLaunchKernelGGL((gemm_f32_wgrad_kernel<64>), dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream,
-                       (const WgJob*)jobs_dev, njobs);
+    hipLaunchKernelGGL((gemm_f32_wgrad_kernel<64>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const WgJob*)jobs_dev, njobs, (int)total_blocks);
   else
-    hipLaunchKernelGGL((gemm_f32_wgrad_kernel<128>), dim3((unsigned)total_blocks), dim3(256), 0, (hipStream_t)stream,
-                       (const WgJob*)jobs_dev, njobs);
+    hipLaunchKernelGGL((gemm_f32_wgrad_kernel<128>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const WgJob*)jobs_dev, njobs, (int)total_blocks);
   return pcv_launch_status();
 }

@@ -325,7 +325,10 @@ class ViTRunnerF32:
         # into ~1024-long slices accumulated with fp32 atomics -- ~2k workgroups instead of 138)
         # The layer weights go to the row-panel wgrad kernel (csrc/gemm_f32.hip) when their shapes fit,
         # the rest (head, patch conv, odd widths) to the grouped fp32 GEMM
-        wg, wr = GemmF32(), WgradF32(target_blocks=2048)
+        # (the row-panel wgrad launch as one resident round: 3 of its workgroups fit a CU -- 53 KB of LDS,
+        # 158 registers -- and its slices are planned near-equal, profiles/r05_wgrad_sweep.txt)
+        wg = GemmF32()
+        wr = WgradF32(target_blocks=3 * torch.cuda.get_device_properties(dev).multi_processor_count)
         ks = lambda t: max(1, t.shape[0] // 256)  # noqa: E731   (few tiles: a deep K split)
         # (+ the bias gradient = column sums of the same output gradient, folded into the row-panel
         # launch where the product fits it; otherwise a colsum launch in the backward)

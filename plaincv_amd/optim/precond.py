@@ -156,8 +156,10 @@ class GemmF32:
 
 class WgradF32:
     """One launch of every fp32 weight gradient C += A^T B (A [K][M] activations, B [K][N] output
-    gradients, K = token rows) on the row-panel kernel of csrc/gemm_f32.hip: 64 x 128 panels, K
-    split into slices accumulated with fp32 atomics (``target_blocks`` workgroups in total).
+    gradients, K = token rows) on the row-panel kernel of csrc/gemm_f32.hip: 64 x 128 panels, each
+    job's K split into ksplit slices of near-equal length (at most ``target_blocks`` workgroups in
+    total, the longest slice as short as that allows -- with target_blocks = the workgroups the chip
+    holds at once the launch is one balanced resident round).
     ``fits(a, b, c)`` says whether a product can join (M, N % 64 / 128, K % 64, 16-B aligned)."""
 
     FMT = "<5Q3q10i"
@@ -192,12 +194,20 @@ class WgradF32:
         lib = hip.load()
         assert lib.pcv_gemm_f32_wgrad_job_size() == struct.calcsize(self.FMT)
         tiles = [(a.shape[1] // 64) * (b.shape[1] // self.BN) for a, b, _, _ in self.jobs]
-        chunks = max(1, -(-sum(tiles) * max(a.shape[0] // 64 for a, _, _, _ in self.jobs) // self.target))
+        nch = [a.shape[0] // 64 for a, _, _, _ in self.jobs]
+        # the smallest per-slice chunk cap whose slices (ksplit = ceil(nch / cap) per job) fit the target
+        blocks = lambda cap: sum(t * -(-n // cap) for t, n in zip(tiles, nch))  # noqa: E731
+        lo, hi = 1, max(nch)
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if blocks(mid) <= self.target:
+                hi = mid
+            else:
+                lo = mid + 1
         plans = []
-        for (a, b, c, cs), t in zip(self.jobs, tiles):
-            K = a.shape[0]
-            kchunk = 64 * min(chunks, K // 64)
-            plans.append((kchunk, -(-K // kchunk)))
+        for n in nch:   # (kchunk: the longest slice; the kernel cuts K at sl * nch / ksplit)
+            ks = -(-n // lo)
+            plans.append((64 * -(-n // ks), ks))
         def nws_of(job, t, ks):   # tile partials + the first panel's column partials
             return t * ks * 64 * self.BN + (job[3] is not None) * (job[1].shape[1] // self.BN) * ks * self.BN
         nws = sum(nws_of(j, t, ks) for j, t, (_, ks) in zip(self.jobs, tiles, plans) if ks > 1)

@@ -49,10 +49,14 @@ def test_wgrad_f32_plan_and_fits():
         woff += tiles * ksplit * 64 * 128 + (N // 128 * ksplit * 128 if i == 0 else 0)
         ffirst_exp += tiles
         assert tiles == (M // 64) * (N // 128) and tiles_n == N // 128
-        assert kchunk % 64 == 0 and (ksplit - 1) * kchunk < K <= ksplit * kchunk
+        # near-equal slices: the longest is ceil(chunks / ksplit) 64-row chunks
+        assert kchunk == 64 * -(-(K // 64) // ksplit)
         assert fst == first
         first += tiles * ksplit
-    assert plan.total == first and 1024 <= first <= 4096
+    # the smallest longest-slice whose launch fits the target workgroups
+    assert plan.total == first and first <= 2048
+    cap = max(-(-(R // 64) // r[13]) for r in recs)
+    assert sum(r[12] * -(-(R // 64) // (cap - 1)) for r in recs) > 2048
     assert plan.ws.numel() == woff and plan.fold_tiles == ffirst_exp
     assert recs[0][3] != 0 and recs[1][3] == 0   # colsum pointer only where requested
 
