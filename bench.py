@@ -161,7 +161,7 @@ def pmc_traffic(kernel):
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    k = d.get("kernels", {}).get(kernel)
+    k = d.get("kernels", {}).get(kernel.replace(" ", ""))   # (keys are stored without spaces)
     if not k:
         return None, None
     return k.get("mean_hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)

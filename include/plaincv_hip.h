@@ -357,6 +357,14 @@ int pcv_gemm_f32_rows_tiled(const float* A, int64_t lda, const float* B, int64_t
                             const float* res, int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed,
                             uint32_t site, void* stream);
 int pcv_gemm_f32_rows_form(int64_t M, int64_t N, int64_t K);
+/* C = A B + bias, dropout, + res_scale res (pcv_gemm_f32_rows with tb = 0, act = 0) for N = 128, then the
+ * LayerNorm of every C row -> ln_y (row stride ldy), ln_mean / ln_rstd [M] (flax LayerNorm, fast variance
+ * clipped at 0, ln_eps): the ViT's attention residual -> LayerNorm_1 (models/vit_small.py:46, :52) and
+ * MLP residual -> the next block's LayerNorm_0 (:56, :38) in one launch.  PCV_EINVAL for N != 128, K % 64. */
+int pcv_gemm_f32_rows_lnout(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
+                            int64_t N, int64_t K, const float* bias, const float* res, int64_t ldr, float res_scale,
+                            float rate, const uint32_t* seed, uint32_t site, const float* ln_s, const float* ln_c,
+                            float* ln_y, int64_t ldy, float* ln_mean, float* ln_rstd, float ln_eps, void* stream);
 /* pcv_gemm_f32_rows whose dropout index of output row r is r * drop_row_step * N + col: the product of a
  * strided subset of the token rows (every drop_row_step-th, e.g. the cls rows b * T) with the dropout bits
  * those rows have in the full [rows][N] product. */

@@ -34,6 +34,11 @@ struct GrArgs {
   uint32_t thresh;
   float dscale, res_scale;
   int rstep;   // dropout index of output row r: r * rstep * N + col (rstep > 1: C is a strided row subset)
+  // LNO (pcv_gemm_f32_rows_lnout): the LayerNorm of each finished C row -> ln_y (row stride ldy), ln_mean,
+  // ln_rstd
+  const float* ln_s; const float* ln_c; float* ln_y; float* ln_mean; float* ln_rstd;
+  int64_t ldy;
+  float ln_eps;
 };
 
 // GELU (tanh form): 0.5 x (1 + tanh(u)) = x / (1 + exp(-2u)), u = sqrt(2/pi) (x + 0.044715 x^3) --
@@ -63,32 +68,33 @@ __device__ __forceinline__ float gr_gelu_grad(float x) {
 // The next chunk's global loads are issued before this chunk's MFMAs; inside a chunk the next
 // 16-long slice's fragments are read from LDS while the current slice's MFMAs issue.
 // BM x BN tile (BM 64 or 32): the 4 waves as (BM / 32) x (4 / (BM / 32)), each a 32 x WN tile
-template <int BM, int BN>
+template <int BM, int BN, int NT = 256>
 struct GrShape {
-  static constexpr int WNW = 4 / (BM / 32), WN = BN / WNW, NJ = WN / 16;
+  static constexpr int WNW = (NT / 64) / (BM / 32), WN = BN / WNW, NJ = WN / 16;
 };
 
-template <bool TA, bool TB, int BN, int BM = GR_BM>
+template <bool TA, bool TB, int BN, int BM = GR_BM, int NT = 256>
 __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
                                             int64_t ldb, int M, int m0, int n0, int kbeg, int kend, float* As,
-                                            float* Bs, f32x4 (&acc)[2][GrShape<BM, BN>::NJ],
+                                            float* Bs, f32x4 (&acc)[2][GrShape<BM, BN, NT>::NJ],
                                             bool colsum = false, float* cs_out = nullptr) {
   constexpr int C4 = GR_BK / 4;                          // float4 per 64-long k row
-  constexpr int NA = BM * C4 / 256, NB = BN * C4 / 256;
-  constexpr int WNW = GrShape<BM, BN>::WNW, WN = GrShape<BM, BN>::WN, NJ = GrShape<BM, BN>::NJ;
+  constexpr int NA = BM * C4 / NT, NB = BN * C4 / NT;
+  static_assert(NA * NT == BM * C4 && NB * NT == BN * C4, "whole float4 loads per thread");
+  constexpr int WNW = GrShape<BM, BN, NT>::WNW, WN = GrShape<BM, BN, NT>::WN, NJ = GrShape<BM, BN, NT>::NJ;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w / WNW, wn = w % WNW;
   const int g4 = lane >> 4, c16 = lane & 15;
   const float* ap[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
-    const int idx = tid + 256 * i;
+    const int idx = tid + NT * i;
     if (TA) ap[i] = A + (int64_t)(kbeg + idx / (BM / 4)) * lda + m0 + (idx % (BM / 4)) * 4;
     else ap[i] = A + (int64_t)min(m0 + idx / C4, M - 1) * lda + kbeg + (idx % C4) * 4;
   }
   const float* bp[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    const int idx = tid + 256 * i;
+    const int idx = tid + NT * i;
     if (TB) bp[i] = B + (int64_t)(n0 + idx / C4) * ldb + kbeg + (idx % C4) * 4;
     else bp[i] = B + (int64_t)(kbeg + idx / (BN / 4)) * ldb + n0 + (idx % (BN / 4)) * 4;
   }
@@ -105,13 +111,13 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
   auto lstore = [&]() {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NT * i;
       if (TA) *reinterpret_cast<f32x4*>(&As[(idx / (BM / 4)) * LDA_K + (idx % (BM / 4)) * 4]) = ra[i];
       else *reinterpret_cast<f32x4*>(&As[(idx / C4) * GR_LDK + (idx % C4) * 4]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NT * i;
       if (TB) *reinterpret_cast<f32x4*>(&Bs[(idx / C4) * GR_LDK + (idx % C4) * 4]) = rb[i];
       else *reinterpret_cast<f32x4*>(&Bs[(idx / (BN / 4)) * LDB_K + (idx % (BN / 4)) * 4]) = rb[i];
     }
@@ -141,7 +147,7 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
   const int nk = (kend - kbeg) / GR_BK;
   // column sums of the B chunks (colsum != nullptr; the weight-gradient form, !TB): thread ->
   // column n, a 64 / (256 / BN)-long k segment of each chunk's [k][n] image
-  constexpr int CS_SEG = GR_BK * BN / 256;
+  constexpr int CS_SEG = GR_BK * BN / NT;
   const int cs_n = tid % BN, cs_k = (tid / BN) * CS_SEG;
   float cs = 0.f;
   gload(0);
@@ -213,14 +219,14 @@ __device__ __forceinline__ f32x4 gr_epi_apply(const GrArgs& g, f32x4 v, const Gr
   return v;
 }
 
-template <bool TB, bool EPI, int BN, int BM>
-__global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
+template <bool TB, bool EPI, int BN, int BM, bool LNO = false, int NT = 256>
+__global__ __launch_bounds__(NT) void gemm_f32_rows_kernel(GrArgs g) {
   // operand images during the main loop; the C tile [BM][BN + 4] for the epilogue afterwards
   __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * GR_LDK];
   static_assert(BM * (BN + 4) <= (BM + BN) * GR_LDK, "C tile fits the operand images");
   float* As = smem;
   float* Bs = smem + BM * GR_LDK;
-  constexpr int WNW = GrShape<BM, BN>::WNW, WN = GrShape<BM, BN>::WN, NJ = GrShape<BM, BN>::NJ;
+  constexpr int WNW = GrShape<BM, BN, NT>::WNW, WN = GrShape<BM, BN, NT>::WN, NJ = GrShape<BM, BN, NT>::NJ;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w / WNW, wn = w % WNW;
   const int g4 = lane >> 4, c16 = lane & 15;
   const int tn = blockIdx.x % g.tiles_n, tm = blockIdx.x / g.tiles_n;
@@ -230,7 +236,7 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int Q = BN / 4, IT = BM * Q / 256;
+  constexpr int Q = BN / 4, IT = BM * Q / NT;
   // the epilogue's operands (bias, residual, act = 2's pre-activation) are loaded before the main
   // loop (<= 4 float4 rows per thread), so their round trip overlaps the MFMAs instead of following them
   constexpr bool PRE = EPI && IT <= 4;
@@ -238,12 +244,12 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
   if (PRE) {
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
-      const int idx = threadIdx.x + 256 * it;
+      const int idx = threadIdx.x + NT * it;
       pin[it] = gr_epi_load(g, min(m0 + idx / Q, g.M - 1), n0 + (idx % Q) * 4);
     }
   }
   const uint32_t seed = (EPI && g.thresh) ? *g.seed : 0u;
-  gr_mainloop<false, TB, BN, BM>(g.A, g.lda, g.B, g.ldb, g.M, m0, n0, 0, g.K, As, Bs, acc);
+  gr_mainloop<false, TB, BN, BM, NT>(g.A, g.lda, g.B, g.ldb, g.M, m0, n0, 0, g.K, As, Bs, acc);
   // C tile through LDS, so the epilogue streams rows as float4: 16-B loads of bias / residual and
   // 16-B stores of C (and of the GELU pre-activation)
   constexpr int LDC = BN + 4;
@@ -257,12 +263,25 @@ __global__ __launch_bounds__(256) void gemm_f32_rows_kernel(GrArgs g) {
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    const int idx = threadIdx.x + 256 * it, rl = idx / Q, cl = (idx % Q) * 4;
+    const int idx = threadIdx.x + NT * it, rl = idx / Q, cl = (idx % Q) * 4;
     const int row = m0 + rl, col = n0 + cl;
     if (row >= g.M) continue;
     f32x4 v = *reinterpret_cast<const f32x4*>(&smem[rl * LDC + cl]);
     if (EPI) v = gr_epi_apply(g, v, PRE ? pin[PRE ? it : 0] : gr_epi_load(g, row, col), row, col, seed);
     *reinterpret_cast<f32x4*>(g.C + (int64_t)row * g.ldc + col) = v;
+    if constexpr (LNO) {   // the row's LayerNorm: its Q = 32 float4 sit in 32 consecutive lanes (BN = N = 128)
+      static_assert(BN == 128, "a whole row per tile");
+      float s1 = v[0] + v[1] + v[2] + v[3], s2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+#pragma unroll
+      for (int o = 1; o < Q; o <<= 1) {   // (butterfly: every lane of the row ends with the same sums)
+        s1 += __shfl_xor(s1, o, Q);
+        s2 += __shfl_xor(s2, o, Q);
+      }
+      const float mu = s1 / BN, rs = rsqrtf(fmaxf(s2 / BN - mu * mu, 0.f) + g.ln_eps);
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(g.ln_s + cl), bi = *reinterpret_cast<const f32x4*>(g.ln_c + cl);
+      *reinterpret_cast<f32x4*>(g.ln_y + (int64_t)row * g.ldy + cl) = (v - mu) * rs * sc + bi;
+      if (cl == 0) { g.ln_mean[row] = mu; g.ln_rstd[row] = rs; }
+    }
   }
 }
 
@@ -819,6 +838,39 @@ extern "C" int pcv_gemm_f32_rows_tiled(const float* A, int64_t lda, const float*
 }
 
 extern "C" int pcv_gemm_f32_rows_form(int64_t M, int64_t N, int64_t K) { return pn_plan(M, N, K).cb ? 1 : 0; }
+
+// C = A B + bias, dropout, + res_scale res (as pcv_gemm_f32_rows, tb = 0, act = 0) for N = 128, then the
+// LayerNorm of every C row -> ln_y (row stride ldy), ln_mean / ln_rstd [M] (flax LayerNorm: fast variance
+// clipped at 0, ln_eps), from the C tile still in LDS: 32 x 128 tiles, one whole row per tile
+extern "C" int pcv_gemm_f32_rows_lnout(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                                       int64_t M, int64_t N, int64_t K, const float* bias, const float* res,
+                                       int64_t ldr, float res_scale, float rate, const uint32_t* seed, uint32_t site,
+                                       const float* ln_s, const float* ln_c, float* ln_y, int64_t ldy, float* ln_mean,
+                                       float* ln_rstd, float ln_eps, void* stream) {
+  if (N != 128 || M <= 0 || K <= 0 || K % GR_BK || !A || !B || !C || !ln_s || !ln_c || !ln_y || !ln_mean || !ln_rstd ||
+      (rate > 0.f && !seed) || ldy < N || (ldy & 3) || (lda & 3) || (ldb & 3) || (ldc & 3) || (res && (ldr & 3)) ||
+      lda < K || ldb < N || ldc < N || (res && ldr < N) || (M + 31) / 32 >= (1ll << 31))
+    return PCV_EINVAL;
+  if (!gr_al(A) || !gr_al(B) || !gr_al(C) || !gr_al(ln_s) || !gr_al(ln_c) || !gr_al(ln_y) || (bias && !gr_al(bias)) ||
+      (res && !gr_al(res)))
+    return PCV_EALIGN;
+  GrArgs g = {};
+  g.A = A; g.B = B; g.C = C; g.bias = bias; g.res = res; g.seed = seed;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldr = ldr;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K; g.site = (int)site; g.res_scale = res_scale; g.rstep = 1;
+  g.tiles_n = 1;
+  if (rate > 0.f) {   // as drop_params (elementwise.hip)
+    const double t = (double)rate * 4294967296.0;
+    g.thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+    g.dscale = 1.f / (1.f - rate);
+  }
+  g.ln_s = ln_s; g.ln_c = ln_c; g.ln_y = ln_y; g.ln_mean = ln_mean; g.ln_rstd = ln_rstd; g.ldy = ldy; g.ln_eps = ln_eps;
+  // (8 waves of 32 x 16: the per-wave shape and waves per CU of the 32 x 64 tiled form, whose 256-thread
+  // 32 x 128 variant ran 18.1 / 26.9 us against 11.2 + 5.8 / 18.4 + 5.8 us for the product + LayerNorm)
+  hipLaunchKernelGGL((gemm_f32_rows_kernel<false, true, 128, 32, true, 512>), dim3((unsigned)((M + 31) / 32)), dim3(512), 0,
+                     (hipStream_t)stream, g);
+  return pcv_launch_status();
+}
 
 extern "C" int pcv_gemm_f32_rows_rs(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C,
                                     int64_t ldc, int64_t M, int64_t N, int64_t K, const float* bias, float* aux,

@@ -78,9 +78,27 @@ class _Dense:
             raise ValueError("a strided-row Dense needs the fused row GEMM's shapes")
         self.plan = None if self.fused else GemmF32().add(a, b, c, tb=tb).finalize(c.device)
         self.epi = bias is not None or res is not None or act or dropout
+        self.ln = None
+
+    def fuse_layernorm_out(self, scale, bias, y, st):
+        """Take the LayerNorm of this product's output (y = LN(c), statistics st) into the launch
+        (pcv_gemm_f32_rows_lnout: N = 128, the whole row in one tile); False: keep the LayerNorm launch."""
+        ok = self.fused and self.entry == "pcv_gemm_f32_rows" and self.rstep == 1 and not self.tb and \
+            self.act == 0 and self.N == 128 and self.K % 64 == 0 and y.stride(1) == 1 and \
+            y.stride(0) % 4 == 0 and y.data_ptr() % 16 == 0 and tuple(y.shape) == (self.M, self.N)
+        if ok:
+            self.ln = (scale, bias, y, st)
+        return ok
 
     def run(self, rate=0.0, seed=None):
         rate = rate if self.dropout else 0.0
+        if self.ln is not None:
+            sc, bi, y, st = self.ln
+            hip.call("pcv_gemm_f32_rows_lnout", ptr(self.a), self.a.stride(0), ptr(self.b), self.b.stride(0),
+                     ptr(self.c), self.c.stride(0), self.M, self.N, self.K, ptr(self.bias), ptr(self.res),
+                     self.res.stride(0) if self.res is not None else 0, 1.0, float(rate), ptr(seed), int(self.site),
+                     ptr(sc), ptr(bi), ptr(y), y.stride(0), ptr(st[0]), ptr(st[1]), 1e-6, stream_ptr())
+            return
         if self.fused:
             args = (ptr(self.a), self.a.stride(0), ptr(self.b), self.b.stride(0), int(self.tb), ptr(self.c),
                     self.c.stride(0), self.M, self.N, self.K, ptr(self.bias), ptr(self.aux),
@@ -320,6 +338,18 @@ class ViTRunnerF32:
         # persistent grid (one workgroup per CU) then waits for CUs the side stream holds (37.6 vs 24.5 us
         # in profiles/r05o_vit_c2_f32_step_timeline.txt), so that launch takes the tiled form
         self.gf[0]["qkv"].entry = "pcv_gemm_f32_rows_tiled"
+        # the residual products whose output feeds a LayerNorm (out projection -> LayerNorm_1, MLP Dense_1
+        # -> the next block's LayerNorm_0) take it into their epilogue (pcv_gemm_f32_rows_lnout)
+        self.ln_fused = set()   # (block, 0 | 1): that block's LayerNorm_0 / _1 forward runs in a product
+        if self.m.use_layernorm:
+            for i in range(L):
+                w = self.w[i]
+                if not (self.cls_last and i == L - 1) and \
+                        self.gf[i]["out"].fuse_layernorm_out(w["s1"], w["c1"], self.y1[i], self.st1[i]):
+                    self.ln_fused.add((i, 1))
+                if i + 1 < L and self.gf[i]["fc2"].fuse_layernorm_out(self.w[i + 1]["s0"], self.w[i + 1]["c0"],
+                                                                      self.y0[i + 1], self.st0[i + 1]):
+                    self.ln_fused.add((i + 1, 0))
         # every weight gradient (K = B*T rows) in one grouped launch at the end of backward
         # (split-K: a [D, N] gradient is only a few 64x64 tiles, so each tile's K = B*T sum is cut
         # into ~1024-long slices accumulated with fp32 atomics -- ~2k workgroups instead of 138)
@@ -433,7 +463,8 @@ class ViTRunnerF32:
         for i in range(m.num_layers):
             w, x = self.w[i], self.xs[i]
             if m.use_layernorm:
-                self._ln(x, w["s0"], w["c0"], self.y0[i], self.st0[i])
+                if (i, 0) not in self.ln_fused:
+                    self._ln(x, w["s0"], w["c0"], self.y0[i], self.st0[i])
             elif self.bn:
                 self._bn(x, w["ra0"], self.bst0[i], w["s0"], w["c0"], self.y0[i], train)
             g = self.gf[i]
@@ -467,7 +498,8 @@ class ViTRunnerF32:
             if last_cls:
                 self._ln(self.cls_rows(self.x1s[i]), w["s1"], w["c1"], self.cls_rows(self.y1[i]), self.st1[i])
             elif m.use_layernorm:
-                self._ln(self.x1s[i], w["s1"], w["c1"], self.y1[i], self.st1[i])
+                if (i, 1) not in self.ln_fused:
+                    self._ln(self.x1s[i], w["s1"], w["c1"], self.y1[i], self.st1[i])
             elif self.bn:
                 self._bn(self.x1s[i], w["ra1"], self.bst1[i], w["s1"], w["c1"], self.y1[i], train)
             if join is not None:

@@ -88,3 +88,54 @@ def test_gemm_f32_rows_panel_form_covers_the_vit(dev):
     for m_small in (16, 64, 32 * 50):
         assert lib.pcv_gemm_f32_rows_form(m_small, 384, 128) == 0
     assert lib.pcv_gemm_f32_rows_form(16448, 384, 192) == 0
+
+
+# the LayerNorm of the output row (pcv_gemm_f32_rows_lnout): out projection -> LayerNorm_1 (K = 128, residual)
+# and MLP Dense_1 -> the next block's LayerNorm_0 (K = 256, dropout + residual); ragged M included
+@pytest.mark.parametrize("M,K,rate", [(16448, 128, 0.0), (16448, 256, 0.1), (1000, 256, 0.1), (77, 128, 0.0),
+                                      (64, 384, 0.3)])
+def test_gemm_f32_rows_layernorm_of_output(dev, M, K, rate):
+    from plaincv_amd import hip
+    from plaincv_amd.hip import ptr, stream_ptr
+    from plaincv_amd.models.vit_f32 import _epi
+    N = 128
+    g = torch.Generator().manual_seed(M + K)
+    a = torch.randn(M, K, generator=g).to(dev)
+    b = (torch.randn(K, N, generator=g) * K ** -0.5).to(dev)
+    bias = torch.randn(N, generator=g).to(dev)
+    res = (torch.randn(M, N, generator=g) * 2 + 0.5).to(dev)
+    sc = (1 + 0.3 * torch.randn(N, generator=g)).to(dev)
+    bi = (0.2 * torch.randn(N, generator=g)).to(dev)
+    seed = torch.tensor([4242], dtype=torch.int32, device=dev)
+    c = torch.full((M, N), float("nan"), device=dev)
+    y = torch.full((M, N + 4), float("nan"), device=dev)[:, :N]   # (a strided y)
+    mean = torch.full((M,), float("nan"), device=dev)
+    rstd = torch.full((M,), float("nan"), device=dev)
+    eps = 1e-6
+    hip.call("pcv_gemm_f32_rows_lnout", ptr(a), K, ptr(b), N, ptr(c), N, M, N, K, ptr(bias), ptr(res), N, 1.0,
+             float(rate), ptr(seed), 9, ptr(sc), ptr(bi), ptr(y), y.stride(0), ptr(mean), ptr(rstd), eps, stream_ptr())
+    ref = torch.empty_like(c)
+    _epi((a.double() @ b.double()).float(), ref, bias=bias, res=res, rate=rate, seed=seed, site=9)
+    torch.cuda.synchronize()
+    bad = (c - ref).abs() > 2e-5 * (1.0 + ref.abs())
+    assert not bad.any(), (int(bad.sum()), (c - ref).abs().max().item())
+    # the LayerNorm of the kernel's own output rows (the check is the statistics and the affine map)
+    cd = c.double()
+    mu = cd.mean(1, keepdim=True)
+    rs = 1.0 / torch.sqrt(((cd * cd).mean(1, keepdim=True) - mu * mu).clamp_min(0) + eps)
+    yr = (cd - mu) * rs * sc.double() + bi.double()
+    assert ((mean.double() - mu[:, 0]).abs() <= 1e-5 * (1 + mu[:, 0].abs())).all()
+    assert ((rstd.double() - rs[:, 0]).abs() <= 1e-5 * rs[:, 0]).all()
+    assert ((y.double() - yr).abs() <= 2e-5 * (1 + yr.abs())).all(), (y.double() - yr).abs().max().item()
+
+
+def test_gemm_f32_rows_layernorm_of_output_rejects_other_widths(dev):
+    from plaincv_amd import hip
+    from plaincv_amd.hip import ptr
+    t = torch.zeros(256, 256, device=dev)
+    v = torch.zeros(256, device=dev)
+    lib = hip.load()
+    for N, K in ((256, 128), (128, 96)):
+        assert lib.pcv_gemm_f32_rows_lnout(ptr(t), 256, ptr(t), 256, ptr(t), 256, 64, N, K, None, None, 0, 1.0, 0.0,
+                                           None, 0, ptr(v), ptr(v), ptr(t), 256, ptr(v), ptr(v), 1e-6, None) != 0
+
