@@ -219,6 +219,9 @@ def vit_roofline_f32(state, image_shape, rate):
     B, H, T, Dh = r.B, r.H, r.T, r.Dh
     t = timed_kernel(lambda: r.attn_bwd(1, rate))
     flops = 4 * 2 * B * H * T * T * Dh
+    # full-height launches per step: the cls-sparse last block (runner.cls_last) runs its attention for
+    # the cls query and its out / MLP products on the cls rows only (other kernels)
+    full = r.m.num_layers - (1 if getattr(r, "cls_last", False) else 0)
     nq = (T + 15) // 16 - (1 if (T % 16 == 1 and T > 16) else 0)
     name = "attn_bwd_f32_kshare_kernel" if nq <= 16 else "attn_bwd_f32_kernel"
     traffic, tsrc = pmc_traffic(f"{name}<true>" if rate > 0 else f"{name}<false>")
@@ -227,20 +230,28 @@ def vit_roofline_f32(state, image_shape, rate):
             "frac": round(flops / t / 1e12 / F32_PEAK_TFLOPS, 4), "traffic": traffic,
             "traffic_unit": "bytes per launch", "traffic_source": tsrc, "launch_us": round(t * 1e6, 2),
             "flops_per_launch": flops, "issued_flops_per_launch": 5 * 2 * B * H * T * T * Dh,
-            "launches_per_step": r.m.num_layers, "step_share_us": round(r.m.num_layers * t * 1e6, 1)}
+            "launches_per_step": full, "step_share_us": round(full * t * 1e6, 1)}
     dense = [r.gf[1][k] for k in ("qkv", "out", "fc1", "fc2")]
     ts = [timed_kernel(lambda d=d: d.run(rate, r.seed)) for d in dense]
     fl = [2 * d.M * d.N * d.K for d in dense]
     ach = sum(fl) / sum(ts) / 1e12
-    traffic, tsrc = pmc_traffic("gemm_f32_rows_kernel<false, true, 64, 32>")
-    rows = {"kernel": "gemm_f32_rows_kernel<false,true,*> (fp32 token-row GEMM + fused Dense epilogue: the "
-                      "forward qkv / out / fc1 / fc2 products of one layer, "
-                      + ", ".join(f"M={d.M} N={d.N} K={d.K}" for d in dense) + ")",
+    # PMC bytes of the four launches: qkv / fc1 on the row-panel form, out / fc2 on the full-row tile with
+    # the LayerNorm of the output (one launch shape: the PMC summary's mean over its grid is their mean)
+    kn = {"qkv": "gemm_f32_panel_kernel<false, 1, 128, 64>", "fc1": "gemm_f32_panel_kernel<false, 21, 128, 64>",
+          "out": "gemm_f32_rows_kernel<false, true, 128, 32, true, 512>",
+          "fc2": "gemm_f32_rows_kernel<false, true, 128, 32, true, 512>"}
+    pm = [pmc_traffic(kn[k]) for k in ("qkv", "out", "fc1", "fc2")]
+    traffic = round(sum(b for b, _ in pm) / 4) if all(b for b, _ in pm) else None
+    tsrc = pm[0][1] if traffic else None
+    rows = {"kernel": "fp32 token-row GEMM + fused Dense epilogue (gemm_f32_panel_kernel for qkv / fc1, "
+                      "gemm_f32_rows_kernel<..., 128, 32, LayerNorm-of-output> for out / fc2): the forward "
+                      "products of one layer, " + ", ".join(f"M={d.M} N={d.N} K={d.K}" for d in dense) + ")",
             "bound": "mfma", "achieved": round(ach, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / F32_PEAK_TFLOPS, 4), "traffic": traffic, "traffic_unit": "bytes per launch",
             "traffic_source": tsrc, "launch_us": round(sum(ts) / len(ts) * 1e6, 2),
             "launch_us_by_shape": [round(x * 1e6, 2) for x in ts], "flops_per_launch": fl,
-            "launches_per_step": 4 * r.m.num_layers, "step_share_us": round(r.m.num_layers * sum(ts) * 1e6, 1)}
+            "launches_per_step": 4 * full + (r.m.num_layers - full),
+            "step_share_us": round((full * sum(ts) + (r.m.num_layers - full) * ts[0]) * 1e6, 1)}
     dom, other = (rows, attn) if rows["step_share_us"] >= attn["step_share_us"] else (attn, rows)
     dom = dict(dom)
     dom["roofline_other"] = other

@@ -220,13 +220,7 @@ __device__ __forceinline__ void light_last(int& kb, int& h, int& b) {
 // Workgroup = 4 waves x 32 queries (two 16-query groups per wave share every K/V
 // fragment read from LDS); K/V tiles of 64 keys double-buffered in LDS.
 template <int DH, bool CAUSAL, bool DROP>
-#ifndef PCV_ATTN_FWD_OCC
-#define PCV_ATTN_FWD_OCC 2
-#endif
-#ifndef PCV_ATTN_DQ_OCC
-#define PCV_ATTN_DQ_OCC 2
-#endif
-__global__ __launch_bounds__(256, DH >= 128 ? 1 : PCV_ATTN_FWD_OCC) void attn_fwd_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnArgs a) {
   constexpr int KS = DH / 32, DT = DH / 16, QG = 2;
   constexpr int TILE = 64 * DH;
   __shared__ __attribute__((aligned(16))) bf16 kv_smem[2 * 2 * TILE];   // [buffer][K|V][TILE]
@@ -656,7 +650,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
 // --------------------------------------------------------------- bwd: dQ
 // Workgroup = 4 waves x 32 queries; loops over prefetched, double-buffered K/V tiles.
 template <int DH, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256, DH >= 128 ? 1 : PCV_ATTN_DQ_OCC) void attn_bwd_dq_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int TILE = 64 * DH;
   constexpr int KS = DH / 32, DT = DH / 16, QG = 2;
   __shared__ __attribute__((aligned(16))) bf16 kv_smem[2 * 2 * TILE];   // [buffer][K|V][TILE]

@@ -569,24 +569,11 @@ __device__ void ln_epilogue(const GemmArgs& g, const float* ct, int64_t m0, cons
   }
 }
 
-// k-tiles in flight: the 64x64 tile has little MFMA work per k-tile, so more of them
-// must be in flight to cover load latency (4 x 16 KiB ring); 128x128 keeps 2 x 32 KiB.
-#ifndef PCV_GEMM_STAGES_SMALL
-#define PCV_GEMM_STAGES_SMALL 2
-#endif
-#ifndef PCV_GEMM_STAGES_LN
-#define PCV_GEMM_STAGES_LN 2
-#endif
-#ifndef PCV_GEMM_STAGES_BIG
-#define PCV_GEMM_STAGES_BIG 2
-#endif
-#ifndef PCV_GEMM_RAW_BARRIER
-#define PCV_GEMM_RAW_BARRIER 0
-#endif
+// k-tiles in flight: a 2-stage ring for every tile family (3- and 4-deep rings measured slower:
+// they cost the second workgroup per CU)
 template <int WM, int WN>
 struct GemmStages {
-  static constexpr int S =
-      (WM == 2 && WN == 4) ? PCV_GEMM_STAGES_LN : (WM * WN <= 4 ? PCV_GEMM_STAGES_SMALL : PCV_GEMM_STAGES_BIG);
+  static constexpr int S = 2;
 };
 
 // s_waitcnt until at most P * min(n, N) vector-memory ops of this wave are outstanding
@@ -766,17 +753,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, int bid, int64_t bz
     for (int i = 0; i < S - 1; ++i) issue(i);
     for (int kt = 0; kt < nfull; ++kt) {
       wait_tiles<PIECES, S - 2>(nfull - 1 - kt);   // tile kt landed: later tiles may stay in flight
-#if PCV_GEMM_RAW_BARRIER
-      // raw s_barrier: __syncthreads() would add a vmcnt(0) and drain the deeper ring's later
-      // tiles at every k-step.  RAW: each wave's counted vmcnt above + this barrier order the
-      // LDS-DMA data for every reader; WAR: a stage is re-issued only after all waves passed this
-      // barrier, i.e. finished the MFMAs (and so the ds_reads) of the tile it held.
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-#else
       __syncthreads();
-#endif
       issue(kt + S - 1);
       compute(smem + (kt % S) * STAGE);
     }
@@ -1038,16 +1015,10 @@ __global__ __launch_bounds__(256, (WM * WN >= 64) ? 1 : 2) void gemm_bf16_kernel
 // (ViT weight gradients: every layer's dW = X^T dY shares K = rows of the batch, and one
 // launch of all of them fills the chip where each alone ran one latency-bound wave of
 // workgroups).  prefix[i] = first block of GEMM i (tiles_m * tiles_n * split_k blocks each).
-// k-tiles in flight for the grouped (weight-gradient) launch: long K slices, so deeper rings
-#ifndef PCV_GROUPED_STAGES_64
-#define PCV_GROUPED_STAGES_64 2
-#endif
-#ifndef PCV_GROUPED_STAGES_128
-#define PCV_GROUPED_STAGES_128 2
-#endif
+// k-tiles in flight for the grouped launch (as GemmStages)
 template <int W>
 struct GroupedStages {
-  static constexpr int S = W == 2 ? PCV_GROUPED_STAGES_64 : PCV_GROUPED_STAGES_128;
+  static constexpr int S = 2;
 };
 
 // Column-sum job of the grouped launch (bias gradients): out[c] += sum_r x[r, c] over one
