@@ -220,7 +220,7 @@ __device__ __forceinline__ f32x4 gr_epi_apply(const GrArgs& g, f32x4 v, const Gr
 }
 
 template <bool TB, bool EPI, int BN, int BM, bool LNO = false, int NT = 256>
-__global__ __launch_bounds__(NT) void gemm_f32_rows_kernel(GrArgs g) {
+__global__ __launch_bounds__(NT, LNO ? 6 : 1) void gemm_f32_rows_kernel(GrArgs g) {
   // operand images during the main loop; the C tile [BM][BN + 4] for the epilogue afterwards
   __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * GR_LDK];
   static_assert(BM * (BN + 4) <= (BM + BN) * GR_LDK, "C tile fits the operand images");
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(NT) void gemm_f32_rows_kernel(GrArgs g) {
   constexpr int Q = BN / 4, IT = BM * Q / NT;
   // the epilogue's operands (bias, residual, act = 2's pre-activation) are loaded before the main
   // loop (<= 4 float4 rows per thread), so their round trip overlaps the MFMAs instead of following them
-  constexpr bool PRE = EPI && IT <= 4;
+  constexpr bool PRE = EPI && IT <= 4 && !LNO;   // (LNO: registers for a third workgroup per CU instead)
   GrEpiIn pin[PRE ? IT : 1];
   if (PRE) {
 #pragma unroll
@@ -865,8 +865,11 @@ extern "C" int pcv_gemm_f32_rows_lnout(const float* A, int64_t lda, const float*
     g.dscale = 1.f / (1.f - rate);
   }
   g.ln_s = ln_s; g.ln_c = ln_c; g.ln_y = ln_y; g.ln_mean = ln_mean; g.ln_rstd = ln_rstd; g.ldy = ldy; g.ln_eps = ln_eps;
-  // (8 waves of 32 x 16: the per-wave shape and waves per CU of the 32 x 64 tiled form, whose 256-thread
-  // 32 x 128 variant ran 18.1 / 26.9 us against 11.2 + 5.8 / 18.4 + 5.8 us for the product + LayerNorm)
+  // (8 waves of 32 x 16: the per-wave shape of the 32 x 64 tiled form, whose 256-thread 32 x 128 variant
+  // ran 18.1 / 26.9 us against 11.2 + 5.8 / 18.4 + 5.8 us for the product + LayerNorm.  <= 85 VGPRs (six
+  // waves per SIMD, the epilogue operands loaded after the main loop): three workgroups per CU, so the
+  // 514 of C2 start together -- at two per CU the two tail tiles ran as a second round, 16.3 / 25.8 vs
+  // 14.7 / 23.5 us, tools/lnout_probe.py)
   hipLaunchKernelGGL((gemm_f32_rows_kernel<false, true, 128, 32, true, 512>), dim3((unsigned)((M + 31) / 32)), dim3(512), 0,
                      (hipStream_t)stream, g);
   return pcv_launch_status();
