@@ -73,12 +73,12 @@ struct GrShape {
   static constexpr int WNW = (NT / 64) / (BM / 32), WN = BN / WNW, NJ = WN / 16;
 };
 
-template <bool TA, bool TB, int BN, int BM = GR_BM, int NT = 256>
+template <bool TA, bool TB, int BN, int BM = GR_BM, int NT = 256, int BK = GR_BK>
 __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
                                             int64_t ldb, int M, int m0, int n0, int kbeg, int kend, float* As,
                                             float* Bs, f32x4 (&acc)[2][GrShape<BM, BN, NT>::NJ],
                                             bool colsum = false, float* cs_out = nullptr) {
-  constexpr int C4 = GR_BK / 4;                          // float4 per 64-long k row
+  constexpr int C4 = BK / 4, LDK = BK + 4;               // float4 per k row; k-contiguous image stride
   constexpr int NA = BM * C4 / NT, NB = BN * C4 / NT;
   static_assert(NA * NT == BM * C4 && NB * NT == BN * C4, "whole float4 loads per thread");
   constexpr int WNW = GrShape<BM, BN, NT>::WNW, WN = GrShape<BM, BN, NT>::WN, NJ = GrShape<BM, BN, NT>::NJ;
@@ -102,10 +102,10 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
   auto gload = [&](int kc) {   // chunk kc (relative to kbeg)
 #pragma unroll
     for (int i = 0; i < NA; ++i)
-      ra[i] = *reinterpret_cast<const f32x4*>(ap[i] + (TA ? (int64_t)kc * GR_BK * lda : (int64_t)kc * GR_BK));
+      ra[i] = *reinterpret_cast<const f32x4*>(ap[i] + (TA ? (int64_t)kc * BK * lda : (int64_t)kc * BK));
 #pragma unroll
     for (int i = 0; i < NB; ++i)
-      rb[i] = *reinterpret_cast<const f32x4*>(bp[i] + (TB ? (int64_t)kc * GR_BK : (int64_t)kc * GR_BK * ldb));
+      rb[i] = *reinterpret_cast<const f32x4*>(bp[i] + (TB ? (int64_t)kc * BK : (int64_t)kc * BK * ldb));
   };
   constexpr int LDA_K = BM + 4, LDB_K = BN + 4;   // row strides of the k-major images
   auto lstore = [&]() {
@@ -113,12 +113,12 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
     for (int i = 0; i < NA; ++i) {
       const int idx = tid + NT * i;
       if (TA) *reinterpret_cast<f32x4*>(&As[(idx / (BM / 4)) * LDA_K + (idx % (BM / 4)) * 4]) = ra[i];
-      else *reinterpret_cast<f32x4*>(&As[(idx / C4) * GR_LDK + (idx % C4) * 4]) = ra[i];
+      else *reinterpret_cast<f32x4*>(&As[(idx / C4) * LDK + (idx % C4) * 4]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int idx = tid + NT * i;
-      if (TB) *reinterpret_cast<f32x4*>(&Bs[(idx / C4) * GR_LDK + (idx % C4) * 4]) = rb[i];
+      if (TB) *reinterpret_cast<f32x4*>(&Bs[(idx / C4) * LDK + (idx % C4) * 4]) = rb[i];
       else *reinterpret_cast<f32x4*>(&Bs[(idx / (BN / 4)) * LDB_K + (idx % (BN / 4)) * 4]) = rb[i];
     }
   };
@@ -130,24 +130,24 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
         const float* p = &As[(kk + 4 * g4) * LDA_K + x];
         fa[i] = f32x4{p[0], p[LDA_K], p[2 * LDA_K], p[3 * LDA_K]};
       } else {
-        fa[i] = *reinterpret_cast<const f32x4*>(&As[x * GR_LDK + kk + 4 * g4]);
+        fa[i] = *reinterpret_cast<const f32x4*>(&As[x * LDK + kk + 4 * g4]);
       }
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int x = wn * WN + j * 16 + c16;
       if (TB) {
-        fb[j] = *reinterpret_cast<const f32x4*>(&Bs[x * GR_LDK + kk + 4 * g4]);
+        fb[j] = *reinterpret_cast<const f32x4*>(&Bs[x * LDK + kk + 4 * g4]);
       } else {
         const float* p = &Bs[(kk + 4 * g4) * LDB_K + x];
         fb[j] = f32x4{p[0], p[LDB_K], p[2 * LDB_K], p[3 * LDB_K]};
       }
     }
   };
-  const int nk = (kend - kbeg) / GR_BK;
+  const int nk = (kend - kbeg) / BK;
   // column sums of the B chunks (colsum != nullptr; the weight-gradient form, !TB): thread ->
   // column n, a 64 / (256 / BN)-long k segment of each chunk's [k][n] image
-  constexpr int CS_SEG = GR_BK * BN / NT;
+  constexpr int CS_SEG = BK * BN / NT;
   const int cs_n = tid % BN, cs_k = (tid / BN) * CS_SEG;
   float cs = 0.f;
   gload(0);
@@ -162,9 +162,9 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
     f32x4 fa[2][2], fb[2][NJ];
     fload(0, fa[0], fb[0]);
 #pragma unroll
-    for (int sl = 0; sl < GR_BK / 16; ++sl) {
+    for (int sl = 0; sl < BK / 16; ++sl) {
       const int cur = sl & 1;
-      if (sl + 1 < GR_BK / 16) fload((sl + 1) * 16, fa[cur ^ 1], fb[cur ^ 1]);
+      if (sl + 1 < BK / 16) fload((sl + 1) * 16, fa[cur ^ 1], fb[cur ^ 1]);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -304,10 +304,11 @@ struct WgJob {
 };
 static_assert(sizeof(WgJob) == 8 * 8 + 10 * 4, "WgJob layout");
 
+constexpr int WG_BK = 32;   // (k chunk of the weight-gradient main loop)
 template <int BN>
-__global__ __launch_bounds__(256) void gemm_f32_wgrad_kernel(const WgJob* __restrict__ jobs, int njobs, int total) {
-  __shared__ __attribute__((aligned(16))) float As[GR_BM * GR_LDK];
-  __shared__ __attribute__((aligned(16))) float Bs[BN * GR_LDK];
+__global__ __launch_bounds__(256, 4) void gemm_f32_wgrad_kernel(const WgJob* __restrict__ jobs, int njobs, int total) {
+  __shared__ __attribute__((aligned(16))) float As[WG_BK * (GR_BM + 4)];   // [k][m] images
+  __shared__ __attribute__((aligned(16))) float Bs[WG_BK * (BN + 4)];      // [k][n]
   constexpr int WN = BN / 2, NJ = WN / 16;
   __shared__ int ft[256];
   // XCD-aware order: the tiles of one K slice (which share its A and B rows) and the job's next
@@ -331,7 +332,8 @@ __global__ __launch_bounds__(256) void gemm_f32_wgrad_kernel(const WgJob* __rest
     for (int q = 0; q < NJ; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bool cs_on = m0 == 0 && jb.colsum;
   float cs = 0.f;
-  gr_mainloop<true, false, BN>(jb.A, jb.lda, jb.B, jb.ldb, jb.M, m0, n0, kbeg, kend, As, Bs, acc, cs_on, &cs);
+  gr_mainloop<true, false, BN, GR_BM, 256, WG_BK>(jb.A, jb.lda, jb.B, jb.ldb, jb.M, m0, n0, kbeg, kend, As, Bs, acc, cs_on,
+                                                 &cs);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
   const int g4 = lane >> 4, c16 = lane & 15;
   if (cs_on) {   // (block-uniform) the column's 256 / BN thread partials in thread order

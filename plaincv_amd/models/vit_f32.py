@@ -355,8 +355,8 @@ class ViTRunnerF32:
         # into ~1024-long slices accumulated with fp32 atomics -- ~2k workgroups instead of 138)
         # The layer weights go to the row-panel wgrad kernel (csrc/gemm_f32.hip) when their shapes fit,
         # the rest (head, patch conv, odd widths) to the grouped fp32 GEMM
-        # (the row-panel wgrad launch as one resident round: 3 of its workgroups fit a CU -- 53 KB of LDS,
-        # 158 registers -- and its slices are planned near-equal, profiles/r05_wgrad_sweep.txt)
+        # (the row-panel wgrad launch planned as 3 workgroups per CU with near-equal slices: one round
+        # that finishes together -- the best of the targets swept, profiles/r05_wgrad_sweep.txt)
         wg = GemmF32()
         wr = WgradF32(target_blocks=3 * torch.cuda.get_device_properties(dev).multi_processor_count)
         ks = lambda t: max(1, t.shape[0] // 256)  # noqa: E731   (few tiles: a deep K split)
