@@ -537,12 +537,14 @@ def lm_roofline(st):
     r = st.runner
     M, Kd = r.yf.shape
     N = r.logits.shape[1]
-    dt = timed_kernel(lambda: K.gemm(r.yf, r.WhT, r.logits, tb=True), iters=10)
+    # the launch the step makes: hipBLASLt for the vocabulary products (csrc/blaslt.hip), when it initialised
+    dt = timed_kernel(lambda: K.gemm(r.yf, r.WhT, r.logits, tb=True, library=r.vocab_lib), iters=10)
     flops = 2.0 * M * N * Kd
     achieved = flops / dt / 1e12
     lib = hip.load()
     big = lib.pcv_gemm_big_ok(M, N, Kd, hip.ptr(r.yf), r.yf.stride(0), hip.ptr(r.WhT), r.WhT.stride(0))
-    name = "gemm_big_kernel<256>" if big else "gemm_bf16_kernel<true,true,4,4>"
+    name = ("hipBLASLt via pcv_blaslt_gemm_bf16" if r.vocab_lib else
+            "gemm_big_kernel<256>" if big else "gemm_bf16_kernel<true,true,4,4>")
     return {"kernel": f"{name} (lm_head fwd on the K-contiguous weight copy, "
                       f"M={M} N={N} K={Kd})", "bound": "mfma",
             "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -365,6 +365,15 @@ int pcv_gemm_f32_rows_lnout(const float* A, int64_t lda, const float* B, int64_t
                             int64_t N, int64_t K, const float* bias, const float* res, int64_t ldr, float res_scale,
                             float rate, const uint32_t* seed, uint32_t site, const float* ln_s, const float* ln_c,
                             float* ln_y, int64_t ldy, float* ln_mean, float* ln_rstd, float ln_eps, void* stream);
+/* The LM's plain vocabulary GEMMs (lm_head / tied embedding, models/LM/transformer.py:393-405, and the
+ * data-gradient of the same product) through hipBLASLt: C[M][N] = alpha op(a) op(b) + beta C with pcv_gemm_bf16's
+ * row-major conventions (a [M][K] or, ta, [K][M]; b [K][N] or, tb, [N][K]), bf16 operands, C bf16 or (out_f32)
+ * fp32; ws: device workspace of ws_bytes.  One plan (descriptors + the heuristic's algorithm) per shape, built
+ * on first use.  0 ok, <0 invalid argument, 1000 + hipblasStatus_t on a library error. */
+int pcv_blaslt_available(void);
+int pcv_blaslt_gemm_bf16(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* a, int64_t lda, const void* b,
+                         int64_t ldb, void* c, int64_t ldc, int out_f32, float alpha, float beta, void* ws,
+                         int64_t ws_bytes, void* stream);
 /* pcv_gemm_f32_rows whose dropout index of output row r is r * drop_row_step * N + col: the product of a
  * strided subset of the token rows (every drop_row_step-th, e.g. the cls rows b * T) with the dropout bits
  * those rows have in the full [rows][N] product. */

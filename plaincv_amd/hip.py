@@ -100,6 +100,8 @@ SIGNATURES = {
     "pcv_gemm_f32_rows_form": [I64, I64, I64],
     "pcv_gemm_f32_rows_lnout": [P, I64, P, I64, P, I64, I64, I64, I64, P, P, I64, F32, F32, P, U32, P, P, P, I64, P, P,
                                 F32, P],
+    "pcv_blaslt_available": [],
+    "pcv_blaslt_gemm_bf16": [I32, I32, I64, I64, I64, P, I64, P, I64, P, I64, I32, F32, F32, P, I64, P],
     "pcv_gemm_f32_rows_rs": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32, I64,
                              P],
     "pcv_attn_cls_f32_ok": [I32, I32],
