@@ -374,6 +374,15 @@ int pcv_blaslt_available(void);
 int pcv_blaslt_gemm_bf16(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* a, int64_t lda, const void* b,
                          int64_t ldb, void* c, int64_t ldc, int out_f32, float alpha, float beta, void* ws,
                          int64_t ws_bytes, void* stream);
+/* pcv_gemm_f32_rows with a workspace for the split tail of its tiled form (data-gradient products, no
+ * epilogue: the few tiles past a whole number of 4-per-CU rounds run as K slices beside the first round, the
+ * tile's last slice adding the slabs in order); pcv_gemm_f32_rows_ws_floats gives the floats needed (0: no
+ * split at this shape).  The workspace starts zeroed and is used by one launch at a time (stream order). */
+int64_t pcv_gemm_f32_rows_ws_floats(int64_t M, int64_t N, int64_t K, int tb, int epi);
+int pcv_gemm_f32_rows_ws(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C, int64_t ldc,
+                         int64_t M, int64_t N, int64_t K, const float* bias, float* aux, int64_t ldaux, const float* res,
+                         int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed, uint32_t site,
+                         float* ws, int64_t ws_floats, void* stream);
 /* pcv_gemm_f32_rows whose dropout index of output row r is r * drop_row_step * N + col: the product of a
  * strided subset of the token rows (every drop_row_step-th, e.g. the cls rows b * T) with the dropout bits
  * those rows have in the full [rows][N] product. */

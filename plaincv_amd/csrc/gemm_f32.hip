@@ -39,6 +39,11 @@ struct GrArgs {
   const float* ln_s; const float* ln_c; float* ln_y; float* ln_mean; float* ln_rstd;
   int64_t ldy;
   float ln_eps;
+  // split tail (gr_split_plan): the first tail_blocks workgroups are tail_tiles tiles of rows [tail_m0, M)
+  // x tail_split K slices; slice partials -> tail_ws slabs, the last arriver of a tile (tail_cnt) adds them
+  // in slice order and runs the epilogue; the other workgroups are the row tiles of [0, tail_m0)
+  float* tail_ws; unsigned* tail_cnt;
+  int tail_blocks, tail_split, tail_m0;
 };
 
 // GELU (tanh form): 0.5 x (1 + tanh(u)) = x / (1 + exp(-2u)), u = sqrt(2/pi) (x + 0.044715 x^3) --
@@ -229,8 +234,21 @@ __global__ __launch_bounds__(NT, LNO ? 6 : 1) void gemm_f32_rows_kernel(GrArgs g
   constexpr int WNW = GrShape<BM, BN, NT>::WNW, WN = GrShape<BM, BN, NT>::WN, NJ = GrShape<BM, BN, NT>::NJ;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w / WNW, wn = w % WNW;
   const int g4 = lane >> 4, c16 = lane & 15;
-  const int tn = blockIdx.x % g.tiles_n, tm = blockIdx.x / g.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  int m0, n0, kb = 0, ke = g.K, tt = 0, tsl = 0;
+  const bool tail = (int)blockIdx.x < g.tail_blocks;   // (block-uniform)
+  if (tail) {   // tile tt, K slice tsl of the split tail
+    tt = (int)blockIdx.x / g.tail_split;
+    tsl = (int)blockIdx.x % g.tail_split;
+    m0 = g.tail_m0 + (tt / g.tiles_n) * BM;
+    n0 = (tt % g.tiles_n) * BN;
+    const int nch = g.K / GR_BK;
+    kb = GR_BK * (tsl * nch / g.tail_split);
+    ke = GR_BK * ((tsl + 1) * nch / g.tail_split);
+  } else {
+    const int b = (int)blockIdx.x - g.tail_blocks;
+    m0 = (b / g.tiles_n) * BM;
+    n0 = (b % g.tiles_n) * BN;
+  }
   f32x4 acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -249,7 +267,43 @@ __global__ __launch_bounds__(NT, LNO ? 6 : 1) void gemm_f32_rows_kernel(GrArgs g
     }
   }
   const uint32_t seed = (EPI && g.thresh) ? *g.seed : 0u;
-  gr_mainloop<false, TB, BN, BM, NT>(g.A, g.lda, g.B, g.ldb, g.M, m0, n0, 0, g.K, As, Bs, acc);
+  gr_mainloop<false, TB, BN, BM, NT>(g.A, g.lda, g.B, g.ldb, g.M, m0, n0, kb, ke, As, Bs, acc);
+  if (!LNO && tail) {
+    // the slice's partial tile -> its slab (thread-major register order), published with one agent-scope
+    // release; the tile's last arriver (ticket S - 1) acquires and adds the slabs in slice order
+    // (MI355X in-launch split-K recipe: plain stores, every wave's vmcnt(0), barrier, lane 0 release
+    // fence + vmcnt(0), relaxed agent fetch_add; the reducer: lane 0 acquire fence + vmcnt(0), barrier)
+    f32x4* slab = reinterpret_cast<f32x4*>(g.tail_ws) + ((int64_t)tt * g.tail_split) * (NT * 2 * NJ);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) slab[(int64_t)tsl * (NT * 2 * NJ) + (i * NJ + j) * NT + threadIdx.x] = acc[i][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // (also: every wave is done with the operand images)
+    int* flag = reinterpret_cast<int*>(smem);
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned old = __hip_atomic_fetch_add(g.tail_cnt + tt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == (unsigned)(g.tail_split - 1);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(g.tail_cnt + tt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // (next launch)
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;   // (block-uniform)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        f32x4 v = slab[(i * NJ + j) * NT + threadIdx.x];
+        for (int q = 1; q < g.tail_split; ++q) v += slab[(int64_t)q * (NT * 2 * NJ) + (i * NJ + j) * NT + threadIdx.x];
+        acc[i][j] = v;
+      }
+  }
   // C tile through LDS, so the epilogue streams rows as float4: 16-B loads of bias / residual and
   // 16-B stores of C (and of the GELU pre-activation)
   constexpr int LDC = BN + 4;
@@ -760,10 +814,32 @@ extern "C" int pcv_gemm_f32_rows_ok(int64_t M, int64_t N, int64_t K, const void*
          ldb >= (tb ? K : N) && lda % 4 == 0 && ldb % 4 == 0 && gr_al(A) && gr_al(B);
 }
 
+// Split tail of the tiled form (32 x 64 tiles of a product without epilogue -- the data-gradient
+// products, whose kernel holds 5 workgroups per CU): when the tile count is a few tiles past a whole
+// number of 4-per-CU rounds (C2's M = 64 * 257: 1024 + 4 tiles), those last tiles' K is cut into 64-deep
+// slices run as extra workgroups beside the first round (the 5th slot), the slices meeting in a
+// workspace: the launch then takes about one round instead of one round plus a CU with a fifth tile.
+struct GrSplit { int tiles, split, m0; };
+static GrSplit gr_split_plan(int64_t M, int64_t N, int64_t K, bool tb, bool epi, bool panel) {
+  GrSplit p = {0, 0, 0};
+  if (epi || (panel && pn_plan(M, N, K).cb) || N % 64 || K % GR_BK) return p;
+  const int64_t mt = (M + GR_BM - 1) / GR_BM;
+  if (!(mt * (N / 128) < 1024 && mt * (N / 64) < 2048)) return p;   // (the 32 x 64 form: gr_rows below)
+  const int64_t tn = N / 64, rt = (M + 31) / 32, total = rt * tn, round = 4 * (int64_t)pcv_cu_count();
+  const int64_t r = total % round, S = std::min<int64_t>(K / GR_BK, 8);
+  if (total < round || r == 0 || r % tn || r > round / 16 || S < 2) return p;
+  p.tiles = (int)r;
+  p.split = (int)S;
+  p.m0 = (int)((rt - r / tn) * 32);
+  (void)tb;
+  return p;
+}
+static int64_t gr_split_ws_floats(const GrSplit& p) { return p.tiles ? (int64_t)p.tiles * p.split * 32 * 64 + p.tiles : 0; }
+
 static int gr_rows(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C, int64_t ldc,
                    int64_t M, int64_t N, int64_t K, const float* bias, float* aux, int64_t ldaux, const float* res,
                    int64_t ldr, float res_scale, int act, float rate, const uint32_t* seed, uint32_t site,
-                   void* stream, bool panel, int64_t rstep = 1) {
+                   void* stream, bool panel, int64_t rstep = 1, float* ws = nullptr, int64_t ws_floats = 0) {
   if (!A || !B || !C || !pcv_gemm_f32_rows_ok(M, N, K, A, lda, B, ldb, tb) || act < 0 || act > 2 ||
       (act == 2 && (!aux || bias || res)) || ldc < N || (act && aux && ldaux < N) ||
       (res && ldr < N) || rate < 0.f || rate >= 1.f || (rate > 0.f && !seed))
@@ -805,7 +881,18 @@ static int gr_rows(const float* A, int64_t lda, const float* B, int64_t ldb, int
   constexpr int64_t short_below = 2048;
   const bool shrt = narrow && mt * (N / 64) < short_below;
   g.tiles_n = (int)(N / (narrow ? 64 : 128));
-  const unsigned blocks = (unsigned)((shrt ? (M + 31) / 32 : mt) * g.tiles_n);
+  unsigned blocks = (unsigned)((shrt ? (M + 31) / 32 : mt) * g.tiles_n);
+  if (ws && shrt && rstep == 1) {
+    const GrSplit sp = gr_split_plan(M, N, K, tb, epi, panel);
+    if (sp.tiles && ws_floats >= gr_split_ws_floats(sp) && gr_al(ws)) {
+      g.tail_ws = ws;
+      g.tail_cnt = reinterpret_cast<unsigned*>(ws + (int64_t)sp.tiles * sp.split * 32 * 64);
+      g.tail_blocks = sp.tiles * sp.split;
+      g.tail_split = sp.split;
+      g.tail_m0 = sp.m0;
+      blocks = blocks - sp.tiles + g.tail_blocks;
+    }
+  }
 #define GR_LAUNCH(TBv, EPv, BNv) hipLaunchKernelGGL((gemm_f32_rows_kernel<TBv, EPv, BNv, 64>), dim3(blocks), dim3(256), 0, s, g)
 #define GR_LAUNCH32(TBv, EPv) hipLaunchKernelGGL((gemm_f32_rows_kernel<TBv, EPv, 64, 32>), dim3(blocks), dim3(256), 0, s, g)
   if (shrt) {
@@ -829,6 +916,22 @@ extern "C" int pcv_gemm_f32_rows(const float* A, int64_t lda, const float* B, in
                                  const uint32_t* seed, uint32_t site, void* stream) {
   return gr_rows(A, lda, B, ldb, tb, C, ldc, M, N, K, bias, aux, ldaux, res, ldr, res_scale, act, rate, seed, site,
                  stream, true);
+}
+
+// floats of the workspace pcv_gemm_f32_rows_ws uses for its split tail at this shape (0: none); the
+// workspace must start zeroed (its tile counters return to 0 at the end of every launch)
+extern "C" int64_t pcv_gemm_f32_rows_ws_floats(int64_t M, int64_t N, int64_t K, int tb, int epi) {
+  return gr_split_ws_floats(gr_split_plan(M, N, K, tb != 0, epi != 0, true));
+}
+
+// pcv_gemm_f32_rows with a workspace for the split tail (pcv_gemm_f32_rows_ws_floats; ws = nullptr or
+// too small: as pcv_gemm_f32_rows).  Stream-ordered use only: one launch per workspace at a time.
+extern "C" int pcv_gemm_f32_rows_ws(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C,
+                                    int64_t ldc, int64_t M, int64_t N, int64_t K, const float* bias, float* aux,
+                                    int64_t ldaux, const float* res, int64_t ldr, float res_scale, int act, float rate,
+                                    const uint32_t* seed, uint32_t site, float* ws, int64_t ws_floats, void* stream) {
+  return gr_rows(A, lda, B, ldb, tb, C, ldc, M, N, K, bias, aux, ldaux, res, ldr, res_scale, act, rate, seed, site,
+                 stream, true, 1, ws, ws_floats);
 }
 
 extern "C" int pcv_gemm_f32_rows_tiled(const float* A, int64_t lda, const float* B, int64_t ldb, int tb, float* C,

@@ -79,6 +79,10 @@ class _Dense:
         self.plan = None if self.fused else GemmF32().add(a, b, c, tb=tb).finalize(c.device)
         self.epi = bias is not None or res is not None or act or dropout
         self.ln = None
+        # the split tail of the tiled form (pcv_gemm_f32_rows_ws: the data-gradient products at C2's rows)
+        nws = int(hip.load().pcv_gemm_f32_rows_ws_floats(M, self.N, K, int(tb), int(bool(self.epi)))) \
+            if self.fused and self.rstep == 1 else 0
+        self.ws = torch.zeros(nws, dtype=torch.float32, device=c.device) if nws else None
 
     def fuse_layernorm_out(self, scale, bias, y, st):
         """Take the LayerNorm of this product's output (y = LN(c), statistics st) into the launch
@@ -107,6 +111,8 @@ class _Dense:
                     int(self.site))
             if self.rstep != 1:
                 hip.call("pcv_gemm_f32_rows_rs", *args, self.rstep, stream_ptr())
+            elif self.ws is not None and self.entry == "pcv_gemm_f32_rows":
+                hip.call("pcv_gemm_f32_rows_ws", *args, ptr(self.ws), self.ws.numel(), stream_ptr())
             else:
                 hip.call(self.entry, *args, stream_ptr())
             return

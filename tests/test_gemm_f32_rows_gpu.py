@@ -139,3 +139,34 @@ def test_gemm_f32_rows_layernorm_of_output_rejects_other_widths(dev):
         assert lib.pcv_gemm_f32_rows_lnout(ptr(t), 256, ptr(t), 256, ptr(t), 256, 64, N, K, None, None, 0, 1.0, 0.0,
                                            None, 0, ptr(v), ptr(v), ptr(t), 256, ptr(v), ptr(v), 1e-6, None) != 0
 
+
+
+# the split tail (pcv_gemm_f32_rows_ws): C2's data-gradient products, whose last 4 tiles run as K slices beside
+# the first round and meet in the workspace; checked against fp64, repeated launches bit-identical, the tile
+# counters back at zero after every launch
+@pytest.mark.parametrize("K", [128, 256, 384])
+def test_gemm_f32_rows_split_tail(dev, K):
+    from plaincv_amd import hip
+    from plaincv_amd.hip import ptr, stream_ptr
+    M, N = 16448, 128
+    lib = hip.load()
+    nws = lib.pcv_gemm_f32_rows_ws_floats(M, N, K, 1, 0)
+    assert nws > 0 and lib.pcv_gemm_f32_rows_ws_floats(M, N, K, 1, 1) == 0   # (no split with an epilogue)
+    g = torch.Generator().manual_seed(K)
+    a = torch.randn(M, K, generator=g).to(dev)
+    b = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev)
+    ws = torch.zeros(nws, device=dev)
+    ref = (a.double() @ b.double().t()).float()
+    outs = []
+    for _ in range(3):
+        c = torch.full((M, N), float("nan"), device=dev)
+        hip.call("pcv_gemm_f32_rows_ws", ptr(a), K, ptr(b), K, 1, ptr(c), N, M, N, K, None, None, 0, None, 0, 1.0, 0,
+                 0.0, None, 0, ptr(ws), nws, stream_ptr())
+        torch.cuda.synchronize()
+        outs.append(c)
+    bad = (outs[0] - ref).abs() > 2e-5 * (1.0 + ref.abs())
+    assert not bad.any(), (int(bad.sum()), bad.nonzero()[:4].tolist())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    ntail = 4   # C2: 1028 tiles = 1024 + 4
+    cnt = ws[nws - ntail:].view(torch.int32)
+    assert (cnt == 0).all()
