@@ -360,11 +360,15 @@ int pcv_gemm_f32_rows_form(int64_t M, int64_t N, int64_t K);
 /* C = A B + bias, dropout, + res_scale res (pcv_gemm_f32_rows with tb = 0, act = 0) for N = 128, then the
  * LayerNorm of every C row -> ln_y (row stride ldy), ln_mean / ln_rstd [M] (flax LayerNorm, fast variance
  * clipped at 0, ln_eps): the ViT's attention residual -> LayerNorm_1 (models/vit_small.py:46, :52) and
- * MLP residual -> the next block's LayerNorm_0 (:56, :38) in one launch.  PCV_EINVAL for N != 128, K % 64. */
+ * MLP residual -> the next block's LayerNorm_0 (:56, :38) in one launch.  PCV_EINVAL for N != 128, K % 64.
+ * ws (optional, pcv_gemm_f32_rows_lnout_ws_floats): the split tail, as pcv_gemm_f32_rows_ws. */
 int pcv_gemm_f32_rows_lnout(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc, int64_t M,
                             int64_t N, int64_t K, const float* bias, const float* res, int64_t ldr, float res_scale,
                             float rate, const uint32_t* seed, uint32_t site, const float* ln_s, const float* ln_c,
-                            float* ln_y, int64_t ldy, float* ln_mean, float* ln_rstd, float ln_eps, void* stream);
+                            float* ln_y, int64_t ldy, float* ln_mean, float* ln_rstd, float ln_eps, float* ws,
+                            int64_t ws_floats, void* stream);
+/* floats of pcv_gemm_f32_rows_lnout's split-tail workspace at (M, K) (0: none; zeroed, one launch at a time) */
+int64_t pcv_gemm_f32_rows_lnout_ws_floats(int64_t M, int64_t K);
 /* The LM's plain vocabulary GEMMs (lm_head / tied embedding, models/LM/transformer.py:393-405, and the
  * data-gradient of the same product) through hipBLASLt: C[M][N] = alpha op(a) op(b) + beta C with pcv_gemm_bf16's
  * row-major conventions (a [M][K] or, ta, [K][M]; b [K][N] or, tb, [N][K]), bf16 operands, C bf16 or (out_f32)

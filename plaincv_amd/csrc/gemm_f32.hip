@@ -268,7 +268,7 @@ __global__ __launch_bounds__(NT, LNO ? 6 : 1) void gemm_f32_rows_kernel(GrArgs g
   }
   const uint32_t seed = (EPI && g.thresh) ? *g.seed : 0u;
   gr_mainloop<false, TB, BN, BM, NT>(g.A, g.lda, g.B, g.ldb, g.M, m0, n0, kb, ke, As, Bs, acc);
-  if (!LNO && tail) {
+  if (tail) {
     // the slice's partial tile -> its slab (thread-major register order), published with one agent-scope
     // release; the tile's last arriver (ticket S - 1) acquires and adds the slabs in slice order
     // (MI355X in-launch split-K recipe: plain stores, every wave's vmcnt(0), barrier, lane 0 release
@@ -947,11 +947,29 @@ extern "C" int pcv_gemm_f32_rows_form(int64_t M, int64_t N, int64_t K) { return 
 // C = A B + bias, dropout, + res_scale res (as pcv_gemm_f32_rows, tb = 0, act = 0) for N = 128, then the
 // LayerNorm of every C row -> ln_y (row stride ldy), ln_mean / ln_rstd [M] (flax LayerNorm: fast variance
 // clipped at 0, ln_eps), from the C tile still in LDS: 32 x 128 tiles, one whole row per tile
+// split tail of the LayerNorm-of-output form (32-row full-width tiles, 2 per CU per round; the tail tiles'
+// K slices beside the first round, the last slice's workgroup adding the slabs and running the epilogue and
+// the LayerNorm): C2's 514 = 512 + 2 tiles
+static GrSplit ln_split_plan(int64_t M, int64_t K) {
+  GrSplit p = {0, 0, 0};
+  const int64_t rt = (M + 31) / 32, round = 2 * (int64_t)pcv_cu_count(), r = rt % round;
+  const int64_t S = std::min<int64_t>(K / GR_BK, 8);
+  if (rt < round || r == 0 || r > round / 16 || S < 2) return p;
+  p.tiles = (int)r;
+  p.split = (int)S;
+  p.m0 = (int)((rt - r) * 32);
+  return p;
+}
+extern "C" int64_t pcv_gemm_f32_rows_lnout_ws_floats(int64_t M, int64_t K) {
+  const GrSplit p = ln_split_plan(M, K);
+  return p.tiles ? (int64_t)p.tiles * p.split * 32 * 128 + p.tiles : 0;
+}
+
 extern "C" int pcv_gemm_f32_rows_lnout(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                                        int64_t M, int64_t N, int64_t K, const float* bias, const float* res,
                                        int64_t ldr, float res_scale, float rate, const uint32_t* seed, uint32_t site,
                                        const float* ln_s, const float* ln_c, float* ln_y, int64_t ldy, float* ln_mean,
-                                       float* ln_rstd, float ln_eps, void* stream) {
+                                       float* ln_rstd, float ln_eps, float* ws, int64_t ws_floats, void* stream) {
   if (N != 128 || M <= 0 || K <= 0 || K % GR_BK || !A || !B || !C || !ln_s || !ln_c || !ln_y || !ln_mean || !ln_rstd ||
       (rate > 0.f && !seed) || ldy < N || (ldy & 3) || (lda & 3) || (ldb & 3) || (ldc & 3) || (res && (ldr & 3)) ||
       lda < K || ldb < N || ldc < N || (res && ldr < N) || (M + 31) / 32 >= (1ll << 31))
@@ -970,12 +988,22 @@ extern "C" int pcv_gemm_f32_rows_lnout(const float* A, int64_t lda, const float*
     g.dscale = 1.f / (1.f - rate);
   }
   g.ln_s = ln_s; g.ln_c = ln_c; g.ln_y = ln_y; g.ln_mean = ln_mean; g.ln_rstd = ln_rstd; g.ldy = ldy; g.ln_eps = ln_eps;
+  unsigned blocks = (unsigned)((M + 31) / 32);
+  const GrSplit sp = ln_split_plan(M, K);
+  if (ws && sp.tiles && ws_floats >= pcv_gemm_f32_rows_lnout_ws_floats(M, K) && gr_al(ws)) {
+    g.tail_ws = ws;
+    g.tail_cnt = reinterpret_cast<unsigned*>(ws + (int64_t)sp.tiles * sp.split * 32 * 128);
+    g.tail_blocks = sp.tiles * sp.split;
+    g.tail_split = sp.split;
+    g.tail_m0 = sp.m0;
+    blocks = blocks - sp.tiles + g.tail_blocks;
+  }
   // (8 waves of 32 x 16: the per-wave shape of the 32 x 64 tiled form, whose 256-thread 32 x 128 variant
   // ran 18.1 / 26.9 us against 11.2 + 5.8 / 18.4 + 5.8 us for the product + LayerNorm.  <= 85 VGPRs (six
   // waves per SIMD, the epilogue operands loaded after the main loop): three workgroups per CU, so the
   // 514 of C2 start together -- at two per CU the two tail tiles ran as a second round, 16.3 / 25.8 vs
   // 14.7 / 23.5 us, tools/lnout_probe.py)
-  hipLaunchKernelGGL((gemm_f32_rows_kernel<false, true, 128, 32, true, 512>), dim3((unsigned)((M + 31) / 32)), dim3(512), 0,
+  hipLaunchKernelGGL((gemm_f32_rows_kernel<false, true, 128, 32, true, 512>), dim3(blocks), dim3(512), 0,
                      (hipStream_t)stream, g);
   return pcv_launch_status();
 }

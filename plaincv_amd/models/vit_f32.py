@@ -92,6 +92,8 @@ class _Dense:
             y.stride(0) % 4 == 0 and y.data_ptr() % 16 == 0 and tuple(y.shape) == (self.M, self.N)
         if ok:
             self.ln = (scale, bias, y, st)
+            nws = int(hip.load().pcv_gemm_f32_rows_lnout_ws_floats(self.M, self.K))
+            self.ws = torch.zeros(nws, dtype=torch.float32, device=y.device) if nws else None
         return ok
 
     def run(self, rate=0.0, seed=None):
@@ -101,7 +103,8 @@ class _Dense:
             hip.call("pcv_gemm_f32_rows_lnout", ptr(self.a), self.a.stride(0), ptr(self.b), self.b.stride(0),
                      ptr(self.c), self.c.stride(0), self.M, self.N, self.K, ptr(self.bias), ptr(self.res),
                      self.res.stride(0) if self.res is not None else 0, 1.0, float(rate), ptr(seed), int(self.site),
-                     ptr(sc), ptr(bi), ptr(y), y.stride(0), ptr(st[0]), ptr(st[1]), 1e-6, stream_ptr())
+                     ptr(sc), ptr(bi), ptr(y), y.stride(0), ptr(st[0]), ptr(st[1]), 1e-6, ptr(self.ws),
+                     self.ws.numel() if self.ws is not None else 0, stream_ptr())
             return
         if self.fused:
             args = (ptr(self.a), self.a.stride(0), ptr(self.b), self.b.stride(0), int(self.tb), ptr(self.c),

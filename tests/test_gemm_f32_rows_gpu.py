@@ -112,8 +112,12 @@ def test_gemm_f32_rows_layernorm_of_output(dev, M, K, rate):
     mean = torch.full((M,), float("nan"), device=dev)
     rstd = torch.full((M,), float("nan"), device=dev)
     eps = 1e-6
+    nws = hip.load().pcv_gemm_f32_rows_lnout_ws_floats(M, K)   # (the split tail at C2's 16448 rows)
+    assert (nws > 0) == (M == 16448)
+    ws = torch.zeros(max(nws, 1), device=dev)
     hip.call("pcv_gemm_f32_rows_lnout", ptr(a), K, ptr(b), N, ptr(c), N, M, N, K, ptr(bias), ptr(res), N, 1.0,
-             float(rate), ptr(seed), 9, ptr(sc), ptr(bi), ptr(y), y.stride(0), ptr(mean), ptr(rstd), eps, stream_ptr())
+             float(rate), ptr(seed), 9, ptr(sc), ptr(bi), ptr(y), y.stride(0), ptr(mean), ptr(rstd), eps, ptr(ws), nws,
+             stream_ptr())
     ref = torch.empty_like(c)
     _epi((a.double() @ b.double()).float(), ref, bias=bias, res=res, rate=rate, seed=seed, site=9)
     torch.cuda.synchronize()
@@ -127,6 +131,14 @@ def test_gemm_f32_rows_layernorm_of_output(dev, M, K, rate):
     assert ((mean.double() - mu[:, 0]).abs() <= 1e-5 * (1 + mu[:, 0].abs())).all()
     assert ((rstd.double() - rs[:, 0]).abs() <= 1e-5 * rs[:, 0]).all()
     assert ((y.double() - yr).abs() <= 2e-5 * (1 + yr.abs())).all(), (y.double() - yr).abs().max().item()
+    if nws:   # the tile counters are back at zero; a repeat is bit-identical
+        assert (ws[-(nws - (nws // 4096) * 4096):].view(torch.int32) == 0).all()
+        c2 = torch.empty_like(c)
+        hip.call("pcv_gemm_f32_rows_lnout", ptr(a), K, ptr(b), N, ptr(c2), N, M, N, K, ptr(bias), ptr(res), N, 1.0,
+                 float(rate), ptr(seed), 9, ptr(sc), ptr(bi), ptr(y), y.stride(0), ptr(mean), ptr(rstd), eps, ptr(ws),
+                 nws, stream_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(c, c2)
 
 
 def test_gemm_f32_rows_layernorm_of_output_rejects_other_widths(dev):
@@ -137,7 +149,8 @@ def test_gemm_f32_rows_layernorm_of_output_rejects_other_widths(dev):
     lib = hip.load()
     for N, K in ((256, 128), (128, 96)):
         assert lib.pcv_gemm_f32_rows_lnout(ptr(t), 256, ptr(t), 256, ptr(t), 256, 64, N, K, None, None, 0, 1.0, 0.0,
-                                           None, 0, ptr(v), ptr(v), ptr(t), 256, ptr(v), ptr(v), 1e-6, None) != 0
+                                           None, 0, ptr(v), ptr(v), ptr(t), 256, ptr(v), ptr(v), 1e-6, None, 0,
+                                           None) != 0
 
 
 

@@ -27,12 +27,14 @@ def main():
         c, y = torch.empty(M0, N, device=dev), torch.empty(M0, N, device=dev)
         st = torch.empty(2, M0, device=dev)
         seed = torch.tensor([3], dtype=torch.int32, device=dev)
+        ws = torch.zeros(1 << 16, device=dev)   # (the split tail's workspace, as the runner's)
         out = []
         for M in (64 * 257, 64 * 256):
             def ln():
+                nws = hip.load().pcv_gemm_f32_rows_lnout_ws_floats(M, K)
                 hip.call("pcv_gemm_f32_rows_lnout", ptr(a), K, ptr(b), N, ptr(c), N, M, N, K, ptr(bias), ptr(res), N,
-                         1.0, rate, ptr(seed), 1, ptr(sc), ptr(bi), ptr(y), N, ptr(st[0]), ptr(st[1]), 1e-6,
-                         stream_ptr())
+                         1.0, rate, ptr(seed), 1, ptr(sc), ptr(bi), ptr(y), N, ptr(st[0]), ptr(st[1]), 1e-6, ptr(ws),
+                         nws, stream_ptr())
 
             def tiled():
                 hip.call("pcv_gemm_f32_rows_tiled", ptr(a), K, ptr(b), N, 0, ptr(c), N, M, N, K, ptr(bias), None, 0,
