@@ -933,6 +933,19 @@ __global__ __launch_bounds__(HD_THREADS) void cls_chain_bwd_f32_kernel(ClsArgs g
 // ties, as xent_kernel) and dlogits = (softmax - onehot) grad_scale -- one launch for the LayerNorm,
 // head GEMM, bias epilogue and loss kernels.  Block = row, 256 threads; D <= 256, Kc <= 1024.
 
+template <int CH>
+__device__ __forceinline__ float hd_col_dot(const float* ys, const float* __restrict__ Wh, int64_t ldw, int c, int D) {
+  float acc = 0.f;
+  for (int k0 = 0; k0 < D; k0 += CH) {
+    float wv[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) wv[j] = Wh[(int64_t)(k0 + j) * ldw + c];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) acc += ys[k0 + j] * wv[j];
+  }
+  return acc;
+}
+
 __global__ __launch_bounds__(HD_THREADS) void vit_head_fwd_f32_kernel(
     const float* __restrict__ x, int64_t ldx, const float* __restrict__ scale, const float* __restrict__ bias,
     const float* __restrict__ Wh, int64_t ldw, const float* __restrict__ bh, const int* __restrict__ labels,
@@ -965,14 +978,8 @@ __global__ __launch_bounds__(HD_THREADS) void vit_head_fwd_f32_kernel(
   float m = -3.0e38f;
   int am = 0x7fffffff;
   for (int c = threadIdx.x; c < Kc; c += HD_THREADS) {
-    float acc = 0.f;
-    for (int k0 = 0; k0 < D; k0 += 16) {   // 16 weight loads in flight, summed in k order
-      float wv[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) wv[j] = Wh[(int64_t)(k0 + j) * ldw + c];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) acc += ys[k0 + j] * wv[j];
-    }
+    // the column's weights with 64 (D % 64 == 0) or 16 loads in flight, summed in k order
+    const float acc = D % 64 == 0 ? hd_col_dot<64>(ys, Wh, ldw, c, D) : hd_col_dot<16>(ys, Wh, ldw, c, D);
     const float z = acc + bh[c];
     zs[c] = z;
     logits[(int64_t)b * Kc + c] = z;
