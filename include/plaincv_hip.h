@@ -333,6 +333,12 @@ int64_t pcv_vit_patch_embed_bwd_f32_ws(int B, int H, int W, int C, int patch, in
 int pcv_vit_patch_embed_fwd_f32(const uint8_t* img, const float* w, const float* bias, const float* cls,
                                 const float* pos, float* x, int B, int H, int W, int C, int patch, int D, float rate,
                                 const uint32_t* seed, uint32_t site, void* stream);
+/* pcv_vit_patch_embed_fwd_f32 + the first encoder block's LayerNorm_0 of every row (vit_small.py:38) in the same
+ * pass: y [B*T][D] (flax LayerNorm, fast variance clipped at 0, ln_eps), mean / rstd [B*T] */
+int pcv_vit_patch_embed_ln_fwd_f32(const uint8_t* img, const float* w, const float* bias, const float* cls,
+                                   const float* pos, float* x, int B, int H, int W, int C, int patch, int D, float rate,
+                                   const uint32_t* seed, uint32_t site, const float* ln_s, const float* ln_c, float* y,
+                                   float* ln_mean, float* ln_rstd, float ln_eps, void* stream);
 int pcv_vit_patch_embed_bwd_f32(const float* dx, const uint8_t* img, float* dcls, float* dpos, float* ws, float* gw,
                                 float* gbias, int B, int H, int W, int C, int patch, int D, float rate,
                                 const uint32_t* seed, uint32_t site, void* stream);

@@ -417,7 +417,10 @@ __global__ __launch_bounds__(256) void patch_embed_fwd_f32_kernel(const uint8_t*
                                                                   const float* __restrict__ cls,
                                                                   const float* __restrict__ pos, float* __restrict__ x,
                                                                   int Hh, int Ww, int T, uint32_t thresh, float scale,
-                                                                  const uint32_t* seedp, uint32_t site) {
+                                                                  const uint32_t* seedp, uint32_t site,
+                                                                  const float* __restrict__ ln_s,
+                                                                  const float* __restrict__ ln_c, float* y,
+                                                                  float* ln_mean, float* ln_rstd, float ln_eps) {
   constexpr int KP = PS * PS * C, D4 = D / 4, RS = 256 / D4, RT = PE_TT / RS;
   static_assert(256 % D4 == 0 && PE_TT % RS == 0, "thread -> (column group, RT tokens)");
   __shared__ __attribute__((aligned(16))) float Ws[KP * D];
@@ -454,6 +457,18 @@ __global__ __launch_bounds__(256) void patch_embed_fwd_f32_kernel(const uint8_t*
       for (int e = 0; e < 4; ++e) v[e] = keep_of(seed, site, (uint32_t)(bt * D + d + e), thresh) ? v[e] * scale : 0.f;
     }
     *reinterpret_cast<f32x4*>(x + bt * D + d) = v;
+    if (ln_s) {   // the first block's LayerNorm_0 of the row: its D4 float4 in D4 consecutive lanes
+      float s1 = v[0] + v[1] + v[2] + v[3], s2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+#pragma unroll
+      for (int o = 1; o < D4; o <<= 1) {   // (butterfly: every lane of the row ends with the same sums)
+        s1 += __shfl_xor(s1, o, D4);
+        s2 += __shfl_xor(s2, o, D4);
+      }
+      const float mu = s1 / D, rs = rsqrtf(fmaxf(s2 / D - mu * mu, 0.f) + ln_eps);
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(ln_s + d), bi = *reinterpret_cast<const f32x4*>(ln_c + d);
+      *reinterpret_cast<f32x4*>(y + bt * D + d) = (v - mu) * rs * sc + bi;
+      if (d == 0) { ln_mean[bt] = mu; ln_rstd[bt] = rs; }
+    }
   }
 }
 
@@ -2285,12 +2300,15 @@ extern "C" int64_t pcv_vit_patch_embed_bwd_f32_ws(int B, int H, int W, int C, in
     default: FN(4, 3, 64); break;             \
   }
 
-extern "C" int pcv_vit_patch_embed_fwd_f32(const uint8_t* img, const float* w, const float* bias, const float* cls,
-                                           const float* pos, float* x, int B, int H, int W, int C, int patch, int D,
-                                           float rate, const uint32_t* seed, uint32_t site, void* stream) {
+static int pe_fwd(const uint8_t* img, const float* w, const float* bias, const float* cls, const float* pos, float* x,
+                  int B, int H, int W, int C, int patch, int D, float rate, const uint32_t* seed, uint32_t site,
+                  const float* ln_s, const float* ln_c, float* y, float* ln_mean, float* ln_rstd, float ln_eps,
+                  void* stream) {
   if (!pcv_vit_patch_embed_f32_ok(B, H, W, C, patch, D) || !img || !w || !bias || !cls || !pos || !x ||
-      rate < 0.f || rate >= 1.f || (rate > 0.f && !seed))
+      rate < 0.f || rate >= 1.f || (rate > 0.f && !seed) || (ln_s && (!ln_c || !y || !ln_mean || !ln_rstd)))
     return PCV_EINVAL;
+  if (ln_s && ((reinterpret_cast<uintptr_t>(ln_s) | reinterpret_cast<uintptr_t>(ln_c) | reinterpret_cast<uintptr_t>(y)) & 15))
+    return PCV_EALIGN;
   if (((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(cls) |
         reinterpret_cast<uintptr_t>(pos) | reinterpret_cast<uintptr_t>(x)) & 15) ||
       (reinterpret_cast<uintptr_t>(img) & 3))
@@ -2301,10 +2319,28 @@ extern "C" int pcv_vit_patch_embed_fwd_f32(const uint8_t* img, const float* w, c
   const dim3 grid((unsigned)(B * ((T + PE_TT - 1) / PE_TT)));
 #define PE_FWD(P, CC, DD)                                                                                    \
   hipLaunchKernelGGL((patch_embed_fwd_f32_kernel<P, CC, DD>), grid, dim3(256), 0, (hipStream_t)stream, img, w, \
-                     bias, cls, pos, x, H, W, T, th, sc, seed, site)
+                     bias, cls, pos, x, H, W, T, th, sc, seed, site, ln_s, ln_c, y, ln_mean, ln_rstd, ln_eps)
   PE_DISPATCH(pe_shape(patch, C, D), PE_FWD)
 #undef PE_FWD
   return pcv_launch_status();
+}
+
+extern "C" int pcv_vit_patch_embed_fwd_f32(const uint8_t* img, const float* w, const float* bias, const float* cls,
+                                           const float* pos, float* x, int B, int H, int W, int C, int patch, int D,
+                                           float rate, const uint32_t* seed, uint32_t site, void* stream) {
+  return pe_fwd(img, w, bias, cls, pos, x, B, H, W, C, patch, D, rate, seed, site, nullptr, nullptr, nullptr, nullptr,
+                nullptr, 0.f, stream);
+}
+
+// + the first encoder block's LayerNorm_0 of every row (vit_small.py:38): y [B*T][D], mean / rstd [B*T]
+extern "C" int pcv_vit_patch_embed_ln_fwd_f32(const uint8_t* img, const float* w, const float* bias, const float* cls,
+                                              const float* pos, float* x, int B, int H, int W, int C, int patch, int D,
+                                              float rate, const uint32_t* seed, uint32_t site, const float* ln_s,
+                                              const float* ln_c, float* y, float* ln_mean, float* ln_rstd,
+                                              float ln_eps, void* stream) {
+  if (!ln_s) return PCV_EINVAL;
+  return pe_fwd(img, w, bias, cls, pos, x, B, H, W, C, patch, D, rate, seed, site, ln_s, ln_c, y, ln_mean, ln_rstd,
+                ln_eps, stream);
 }
 
 extern "C" int pcv_vit_patch_embed_bwd_f32(const float* dx, const uint8_t* img, float* dcls, float* dpos, float* ws,

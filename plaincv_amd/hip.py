@@ -92,6 +92,8 @@ SIGNATURES = {
     "pcv_vit_patch_embed_f32_ok": [I32, I32, I32, I32, I32, I32],
     "pcv_vit_patch_embed_bwd_f32_ws": [I32, I32, I32, I32, I32, I32],
     "pcv_vit_patch_embed_fwd_f32": [P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, F32, P, U32, P],
+    "pcv_vit_patch_embed_ln_fwd_f32": [P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, F32, P, U32, P, P, P, P, P, F32,
+                                       P],
     "pcv_vit_patch_embed_bwd_f32": [P, P, P, P, P, P, P, I32, I32, I32, I32, I32, I32, F32, P, U32, P],
     "pcv_gemm_f32_rows_ok": [I64, I64, I64, P, I64, P, I64, I32],
     "pcv_gemm_f32_rows": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32, P],

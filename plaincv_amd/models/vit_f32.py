@@ -350,6 +350,9 @@ class ViTRunnerF32:
         # the residual products whose output feeds a LayerNorm (out projection -> LayerNorm_1, MLP Dense_1
         # -> the next block's LayerNorm_0) take it into their epilogue (pcv_gemm_f32_rows_lnout)
         self.ln_fused = set()   # (block, 0 | 1): that block's LayerNorm_0 / _1 forward runs in a product
+        # (and block 0's LayerNorm_0 in the fused patch embedding, pcv_vit_patch_embed_ln_fwd_f32)
+        if self.m.use_layernorm and self.pe_fused and self.y0[0].is_contiguous():
+            self.ln_fused.add((0, 0))
         if self.m.use_layernorm:
             for i in range(L):
                 w = self.w[i]
@@ -457,9 +460,16 @@ class ViTRunnerF32:
             self.labels.copy_(labels, non_blocking=True)
         if self.pe_fused:   # patchify + conv + bias + cls / pos + dropout in one launch
             self.images = images
-            hip.call("pcv_vit_patch_embed_fwd_f32", ptr(images), ptr(self.Wconv), ptr(self.bconv), ptr(self.cls),
-                     ptr(self.pos), ptr(self.xs[0]), B, self.Hh, self.Ww, self.C, m.patch_size, D, float(rate),
-                     ptr(seed), SITE_EMBED, stream_ptr())
+            if (0, 0) in self.ln_fused:   # + block 0's LayerNorm_0
+                w0 = self.w[0]
+                hip.call("pcv_vit_patch_embed_ln_fwd_f32", ptr(images), ptr(self.Wconv), ptr(self.bconv),
+                         ptr(self.cls), ptr(self.pos), ptr(self.xs[0]), B, self.Hh, self.Ww, self.C, m.patch_size, D,
+                         float(rate), ptr(seed), SITE_EMBED, ptr(w0["s0"]), ptr(w0["c0"]), ptr(self.y0[0]),
+                         ptr(self.st0[0][0]), ptr(self.st0[0][1]), 1e-6, stream_ptr())
+            else:
+                hip.call("pcv_vit_patch_embed_fwd_f32", ptr(images), ptr(self.Wconv), ptr(self.bconv), ptr(self.cls),
+                         ptr(self.pos), ptr(self.xs[0]), B, self.Hh, self.Ww, self.C, m.patch_size, D, float(rate),
+                         ptr(seed), SITE_EMBED, stream_ptr())
         else:
             hip.call("pcv_vit_patchify_f32", ptr(images), ptr(self.patches), B, self.Hh, self.Ww, self.C, m.patch_size,
                      stream_ptr())

@@ -77,3 +77,35 @@ def test_patch_embed_f32_rejects_unsupported(dev):
     assert not lib.pcv_vit_patch_embed_f32_ok(8, 64, 64, 3, 8, 128)    # 8 x 8 x 3 = 192 > 48
     assert not lib.pcv_vit_patch_embed_f32_ok(8, 62, 62, 3, 4, 128)    # 62 % 4
     assert not lib.pcv_vit_patch_embed_f32_ok(8, 64, 64, 3, 4, 130)    # D % 4
+
+
+@pytest.mark.parametrize("B,H,C,ps,D,rate", [(64, 64, 3, 4, 128, 0.1), (5, 16, 3, 4, 64, 0.1), (8, 64, 3, 4, 128, 0.0)])
+def test_patch_embed_with_layernorm(dev, B, H, C, ps, D, rate):
+    """pcv_vit_patch_embed_ln_fwd_f32: x bit-identical to the embedding alone; y / mean / rstd the flax
+    LayerNorm of x's rows (fast variance clipped at 0)."""
+    from plaincv_amd.hip import ptr, stream_ptr
+    g = torch.Generator().manual_seed(B + D)
+    hw = (H // ps) ** 2
+    T, Kp = hw + 1, ps * ps * C
+    img = torch.randint(0, 256, (B, H, H, C), generator=g, dtype=torch.uint8).to(dev)
+    w = (torch.randn(Kp, D, generator=g) * Kp ** -0.5).to(dev)
+    bias, cls = torch.randn(D, generator=g).to(dev), torch.randn(D, generator=g).to(dev)
+    pos = torch.randn(T, D, generator=g).to(dev)
+    sc, bi = (1 + 0.3 * torch.randn(D, generator=g)).to(dev), (0.2 * torch.randn(D, generator=g)).to(dev)
+    seed = torch.tensor([77], dtype=torch.int32, device=dev)
+    x0 = torch.full((B * T, D), float("nan"), device=dev)
+    x1, y = torch.full_like(x0, float("nan")), torch.full_like(x0, float("nan"))
+    mean, rstd = torch.full((B * T,), float("nan"), device=dev), torch.full((B * T,), float("nan"), device=dev)
+    _call("pcv_vit_patch_embed_fwd_f32", ptr(img), ptr(w), ptr(bias), ptr(cls), ptr(pos), ptr(x0), B, H, H, C, ps, D,
+          float(rate), ptr(seed), 5, stream_ptr())
+    _call("pcv_vit_patch_embed_ln_fwd_f32", ptr(img), ptr(w), ptr(bias), ptr(cls), ptr(pos), ptr(x1), B, H, H, C, ps, D,
+          float(rate), ptr(seed), 5, ptr(sc), ptr(bi), ptr(y), ptr(mean), ptr(rstd), 1e-6, stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(x0, x1)
+    xd = x1.double()
+    mu = xd.mean(1, keepdim=True)
+    rs = 1.0 / torch.sqrt(((xd * xd).mean(1, keepdim=True) - mu * mu).clamp_min(0) + 1e-6)
+    yr = (xd - mu) * rs * sc.double() + bi.double()
+    assert ((mean.double() - mu[:, 0]).abs() <= 1e-5 * (1 + mu[:, 0].abs())).all()
+    assert ((rstd.double() - rs[:, 0]).abs() <= 1e-5 * rs[:, 0]).all()
+    assert ((y.double() - yr).abs() <= 2e-5 * (1 + yr.abs())).all(), (y.double() - yr).abs().max().item()
