@@ -200,9 +200,16 @@ __global__ __launch_bounds__(LNR_THREADS) void ln_part_reduce_kernel(const LnPar
   float *dscale = j.dscale, *dbias = j.dbias;
   const int col = blockIdx.x * 64 + (threadIdx.x & 63), sl = threadIdx.x >> 6;
   float sum = 0.f;
-  if (col < 2 * D) {
-#pragma unroll 16
-    for (int b = sl; b < nblk; b += LNR_LANES) sum += part[(int64_t)b * 2 * D + col];
+  if (col < 2 * D) {   // rows sl, sl + LNR_LANES, ... added in order, 64 loads in flight per batch
+    int b = sl;
+    for (; b + 63 * LNR_LANES < nblk; b += 64 * LNR_LANES) {
+      float v[64];
+#pragma unroll
+      for (int j = 0; j < 64; ++j) v[j] = part[(int64_t)(b + j * LNR_LANES) * 2 * D + col];
+#pragma unroll
+      for (int j = 0; j < 64; ++j) sum += v[j];
+    }
+    for (; b < nblk; b += LNR_LANES) sum += part[(int64_t)b * 2 * D + col];
   }
   red[sl][threadIdx.x & 63] = sum;
   __syncthreads();
