@@ -266,6 +266,10 @@ int pcv_layernorm_bwd_f32(const float* dy, int64_t lddy, const float* x, int64_t
  * partials of several LayerNorms in one launch (device table of {part, dscale, dbias, nblk, D}). */
 int pcv_layernorm_part_job_size(void);
 int pcv_layernorm_part_reduce(const void* jobs, int njobs, int max_D, int64_t max_nblk, void* stream);
+/* pcv_layernorm_part_reduce + the step's metrics (pcv_mean2 of loss / correct: metrics = [mean loss, mean
+ * accuracy] * n * scale) in the same launch -- the training step's metrics taken off a launch of their own */
+int pcv_layernorm_part_reduce_metrics(const void* jobs, int njobs, int max_D, int64_t max_nblk, const float* loss,
+                                      const float* correct, int64_t n, float scale, float* metrics, void* stream);
 int pcv_f32_epilogue(const float* x, int64_t ldx, const float* bias, const float* res, int64_t ldr, float res_scale,
                      float* aux, int64_t ldaux, float* out, int64_t ldo, int64_t R, int N, int act, float rate,
                      const uint32_t* seed, uint32_t site, void* stream);

@@ -192,8 +192,22 @@ static_assert(sizeof(LnPartJob) == 40, "LnPartJob layout");
 // of 64 columns, the lanes' sums added in lane order through LDS and ONE add per column: the result is
 // run-to-run identical (no float atomics whose order varies)
 constexpr int LNR_THREADS = 1024, LNR_LANES = LNR_THREADS / 64;
-__global__ __launch_bounds__(LNR_THREADS) void ln_part_reduce_kernel(const LnPartJob* jobs, LnPartJob one) {
+// (metrics != nullptr: the z-slice past the jobs is mean2_kernel's work -- the step's mean loss / accuracy,
+// moved off its own launch; the same block_sum, so the same values)
+__global__ __launch_bounds__(LNR_THREADS) void ln_part_reduce_kernel(const LnPartJob* jobs, LnPartJob one,
+                                                                     const float* m_loss, const float* m_correct,
+                                                                     int64_t m_n, float m_scale, float* metrics) {
   __shared__ float red[LNR_LANES][64];
+  if (metrics && (int)blockIdx.z == (int)gridDim.z - 1) {
+    if (blockIdx.x != 0) return;
+    float* r16 = &red[0][0];
+    float a = 0.f, b = 0.f;
+    for (int64_t i = threadIdx.x; i < m_n; i += LNR_THREADS) { a += m_loss[i]; b += m_correct[i]; }
+    a = block_sum(a, r16);
+    b = block_sum(b, r16);
+    if (threadIdx.x == 0) { metrics[0] = a * m_scale; metrics[1] = b * m_scale; }
+    return;
+  }
   const LnPartJob j = jobs ? jobs[blockIdx.z] : one;
   const float* part = j.part;
   const int nblk = (int)j.nblk, D = (int)j.D;
@@ -2063,7 +2077,8 @@ extern "C" int pcv_layernorm_bwd_f32(const float* dy, int64_t lddy, const float*
                                           lddx, ws, R, dxd, lddxd, th, sc, seed, site));
   if (!dscale) return pcv_launch_status();   // partials stay in ws for pcv_layernorm_part_reduce
   hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * D + 63) / 64)), dim3(LNR_THREADS), 0,
-                     (hipStream_t)stream, nullptr, LnPartJob{ws, dscale, dbias, blocks, D});
+                     (hipStream_t)stream, nullptr, LnPartJob{ws, dscale, dbias, blocks, D}, nullptr, nullptr, 0, 0.f,
+                     nullptr);
   return pcv_launch_status();
 }
 
@@ -2074,7 +2089,19 @@ extern "C" int pcv_layernorm_part_job_size() { return (int)sizeof(LnPartJob); }
 extern "C" int pcv_layernorm_part_reduce(const void* jobs, int njobs, int max_D, int64_t max_nblk, void* stream) {
   if (!jobs || njobs <= 0 || njobs > 65535 || max_D <= 0 || max_D > 512 || max_nblk <= 0) return PCV_EINVAL;
   hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * max_D + 63) / 64), 1, njobs), dim3(LNR_THREADS), 0,
-                     (hipStream_t)stream, (const LnPartJob*)jobs, LnPartJob{});
+                     (hipStream_t)stream, (const LnPartJob*)jobs, LnPartJob{}, nullptr, nullptr, 0, 0.f, nullptr);
+  return pcv_launch_status();
+}
+
+// pcv_layernorm_part_reduce + pcv_mean2(loss, correct, n, scale, metrics) in the same launch
+extern "C" int pcv_layernorm_part_reduce_metrics(const void* jobs, int njobs, int max_D, int64_t max_nblk,
+                                                 const float* loss, const float* correct, int64_t n, float scale,
+                                                 float* metrics, void* stream) {
+  if (!jobs || njobs <= 0 || njobs >= 65535 || max_D <= 0 || max_D > 512 || max_nblk <= 0 || !loss || !correct ||
+      !metrics || n <= 0)
+    return PCV_EINVAL;
+  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * max_D + 63) / 64), 1, njobs + 1), dim3(LNR_THREADS),
+                     0, (hipStream_t)stream, (const LnPartJob*)jobs, LnPartJob{}, loss, correct, n, scale, metrics);
   return pcv_launch_status();
 }
 

@@ -310,6 +310,8 @@ class GraphedTrainStep:
                             getattr(self.runner, "supports_join", False) and
                             hasattr(state.tx, "split_capable") and state.tx.split_capable(state.opt_state))
         self.pending = False
+        if hasattr(self.runner, "metrics_in_backward"):   # (this step always runs the backward)
+            self.runner.metrics_in_backward = True
         self.stream = torch.cuda.Stream(device=dev)
         self.g_fb = torch.cuda.CUDAGraph()
         self.g_post = None

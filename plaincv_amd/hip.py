@@ -71,6 +71,7 @@ SIGNATURES = {
     "pcv_layernorm_bwd_f32_ok": [I32, I64, I64, I64, I64],
     "pcv_layernorm_bwd_f32_ws": [I64, I32],
     "pcv_layernorm_part_job_size": [],
+    "pcv_layernorm_part_reduce_metrics": [P, I32, I32, I64, P, P, I64, F32, P, P],
     "pcv_layernorm_part_reduce": [P, I32, I32, I64, P],
     "pcv_layernorm_bwd_f32": [P, I64, P, I64, P, P, P, P, I64, P, I64, P, P, P, I64, I64, I32, P, I64, F32, P, U32,
                               P],

@@ -424,9 +424,15 @@ class LayerNormParamReduce:
         self.max_nblk = max(j[3] for j in self.jobs)
         return self
 
-    def run(self):
-        hip.call("pcv_layernorm_part_reduce", ptr(self.table), len(self.jobs), self.max_D, self.max_nblk,
-                 stream_ptr())
+    def run(self, metrics=None):
+        """metrics = (loss, correct, n, scale, out): also out = [sum loss, sum correct] * scale (mean2)"""
+        if metrics is not None:
+            loss, correct, n, scale, out = metrics
+            hip.call("pcv_layernorm_part_reduce_metrics", ptr(self.table), len(self.jobs), self.max_D, self.max_nblk,
+                     ptr(loss), ptr(correct), int(n), float(scale), ptr(out), stream_ptr())
+        else:
+            hip.call("pcv_layernorm_part_reduce", ptr(self.table), len(self.jobs), self.max_D, self.max_nblk,
+                     stream_ptr())
 
 
 def batchnorm_workspace_bytes(R, D):

@@ -130,6 +130,11 @@ class _Dense:
 class ViTRunnerF32:
     """Fixed-shape fp32 forward/backward executor (graph-capturable, no allocation after init)."""
 
+    # True (set by the graphed training step, which always runs forward + backward): a training
+    # forward leaves the loss / accuracy metrics to backward(), which computes them in the launch of
+    # the LayerNorm parameter reduction instead of a launch of their own
+    metrics_in_backward = False
+
     def __init__(self, model, store, image_shape, device, batch_stats=None, fused_attn=True):
         """fused_attn False: the per-(batch, head) GEMM path around a materialised softmax (also taken
         for shapes the fused kernels do not cover) -- the tests compare the two."""
@@ -532,7 +537,9 @@ class ViTRunnerF32:
                      ptr(self.labels), ptr(self.yf), ptr(self.stf[0]), ptr(self.stf[1]), ptr(self.logits),
                      ptr(self.row_loss), ptr(self.row_correct), ptr(self.dlogits) if need_grad else None, B, D, self.Kc,
                      1e-6, 1.0 / B, stream_ptr())
-            K.mean2(self.row_loss, self.row_correct, B, 1.0 / B, self.metrics)
+            if not (need_grad and self.metrics_in_backward and self.ln_red is not None):
+                K.mean2(self.row_loss, self.row_correct, B, 1.0 / B, self.metrics)
+            # (else backward() computes them inside the LayerNorm parameter reduction's launch)
             return self.metrics
         if m.use_layernorm:
             self._ln(xcls, self.sf, self.cf, self.yf, self.stf)
@@ -647,7 +654,8 @@ class ViTRunnerF32:
         for part in self.g_wgrad_parts:
             part.run()
         if self.ln_red is not None:
-            self.ln_red.run()
+            self.ln_red.run(metrics=(self.row_loss, self.row_correct, self.B, 1.0 / self.B, self.metrics)
+                            if (self.head_fused and self.metrics_in_backward) else None)
 
     def _qkv_bwd(self, i, rate, seed, dx1):
         """Block i's qkv-product VJP and LayerNorm_0 VJP (with the residual gradient dx1) into dxo[i]."""
