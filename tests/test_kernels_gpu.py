@@ -659,3 +659,33 @@ def test_gemm_gelu_saved_derivative(dev):
     torch.cuda.synchronize()
     ref = (dy.float() @ wt.float().t()) * d.float()
     assert ((b1.float() - ref).abs() <= 2 ** -7 * ref.abs() + 1e-2).all()
+
+
+@pytest.mark.parametrize("B,T,H", [(2, 1024, 12), (1, 2048, 16)])   # 124M (C3) / 420M (C5) head geometry
+def test_attention_lm_geometry(dev, B, T, H):
+    """The LM's causal flash attention at the benchmarked head counts (12 heads at T 1024, 16 at T 2048,
+    Dh 64) against the fp32 reference, with bounds relative to the reference's own magnitude: the output
+    to 1e-2 of max |O| (bf16 output rounding is 2^-9), dq | dk | dv to 1e-2 of max |grad| (bf16 P and dS
+    operands); measured values printed (LMATTN)."""
+    from plaincv_amd import kernels as K
+    torch.manual_seed(1)
+    Dh = 64
+    D = H * Dh
+    qkv = torch.randn(B * T, 3 * D, device=dev).to(torch.bfloat16)
+    out = torch.empty(B * T, D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * T, device=dev)
+    K.attn_fwd(qkv, out, lse, B, T, H, Dh, True)
+    qf = qkv.float().requires_grad_(True)
+    ref = _attn_ref(qf, B, T, H, Dh, True, None, 0.0)
+    fwd_rel = ((out.float() - ref).abs().max() / ref.abs().max()).item()
+    do = torch.randn(B * T, D, device=dev).to(torch.bfloat16)
+    ref.backward(do.float())
+    dqkv = torch.zeros(B * T, 3 * D, device=dev, dtype=torch.bfloat16)
+    delta = torch.empty(B * H * T, device=dev)
+    K.attn_bwd(qkv, out, do, lse, delta, dqkv, B, T, H, Dh, True)
+    g = qf.grad
+    rel = [((dqkv.float()[:, k * D:(k + 1) * D] - g[:, k * D:(k + 1) * D]).abs().max() /
+            g[:, k * D:(k + 1) * D].abs().max()).item() for k in range(3)]
+    print(f"LMATTN B={B} T={T} H={H}: fwd rel {fwd_rel:.2e}  dq / dk / dv rel {rel[0]:.2e} {rel[1]:.2e} {rel[2]:.2e}")
+    assert fwd_rel <= 1e-2, fwd_rel
+    assert max(rel) <= 1e-2, rel
