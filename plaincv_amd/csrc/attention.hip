@@ -295,11 +295,23 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
       // more than 2^8 (log2 domain), so steady-state tiles skip the rescale of the output
       // accumulators; exp2 arguments stay <= 8, which bf16 P and the fp32 sums absorb.
       // The first key tile always holds a valid key for every row, so m2 is finite after it.
-      auto softmax = [&](auto maskc, int gq) {
-        constexpr bool MASK = decltype(maskc)::value;
+      auto softmax = [&](auto maskc, auto docc, int gq) {
+        constexpr bool MASK = decltype(maskc)::value, DOC = decltype(docc)::value;
         const int myq = qw + gq * 16 + (lane & 15);
         uint32_t okbits = 0xFFFFu;
-        if constexpr (MASK) {
+        if constexpr (MASK && !DOC) {
+          // ragged tail / causal diagonal: one bound per lane, 2 VALU per score.  Every row sees
+          // key kb * 64 (<= qw for an active wave), so its running max is finite after this tile
+          // and the NEG_BIG scores underflow exp2 to exactly 0 -- no select on P.
+          const int kl = __builtin_amdgcn_readfirstlane(kb * 64) + 4 * g;
+          int lim = __builtin_amdgcn_readfirstlane(T) - kl - 1;
+          if (CAUSAL) lim = min(lim, myq - kl);
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[gq][t][r] = 16 * t + r <= lim ? s[gq][t][r] : NEG_BIG;
+        }
+        if constexpr (MASK && DOC) {
           okbits = 0u;
           // bounds relative to this lane's first key, through readfirstlane (convergent: the
           // compiler cannot hoist these compares out of the boundary path into every tile, as it
@@ -358,7 +370,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
               const int r = 2 * h2 + e;
               // masked keys contribute exactly 0 (under a document mask a row can see no valid key in
               // a tile while its running max is still the initial value)
-              if (MASK) p[e] = ((okbits >> (4 * t + r)) & 1u) ? p[e] : 0.f;
+              if (MASK && DOC) p[e] = ((okbits >> (4 * t + r)) & 1u) ? p[e] : 0.f;
             }
             rs2 += (f2v){p[0], p[1]};
 #pragma unroll
@@ -380,8 +392,9 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
       for (int gq = 0; gq < QG; ++gq) {
         const bool interior = kb * 64 + 63 < T && (!CAUSAL || kb * 64 + 63 <= qw + gq * 16) &&
                               (!doc || kb * 64 >= gds[gq]);
-        if (interior) softmax(std::false_type{}, gq);
-        else softmax(std::true_type{}, gq);
+        if (interior) softmax(std::false_type{}, std::false_type{}, gq);
+        else if (!doc) softmax(std::true_type{}, std::false_type{}, gq);
+        else softmax(std::true_type{}, std::true_type{}, gq);
       }
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
@@ -576,21 +589,28 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
         // LDS round trip inside a per-element branch); the boundary test in a path of its own
         const f32x4 l4 = *reinterpret_cast<const f32x4*>(Ls + 16 * t + 4 * g);
         const f32x4 d4 = *reinterpret_cast<const f32x4*>(Dl + 16 * t + 4 * g);
-        auto probs = [&](auto interior_t) {
-          constexpr bool INTERIOR = decltype(interior_t)::value;
+        // MODE 0: every pair valid; 1: ragged tail / causal diagonal as one window [lo, hi) of this
+        // lane's 4 queries (3 VALU a score); 2: the document mask, per pair
+        auto probs = [&](auto mode_t) {
+          constexpr int MODE = decltype(mode_t)::value;
 #pragma unroll
           for (int gk = 0; gk < KG; ++gk) {
             const int mykey = kw + gk * 16 + (lane & 15);
             uint32_t wt = 0;
             if (DROP) wt = (uint32_t)a.mask[drop_word(qb * 64 + 16 * t + 4 * g, mykey, a.n64)] >> (mykey & 3);
+            int lo = 0, span = 0;
+            if constexpr (MODE == 1) {
+              const int ql = __builtin_amdgcn_readfirstlane(qb * 64 + 16 * t) + 4 * g;
+              lo = mykey >= T ? 4 : (CAUSAL ? mykey - ql : 0);
+              span = (__builtin_amdgcn_readfirstlane(T) - ql) - lo;
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               float pv = __builtin_amdgcn_exp2f(fmaf(sv[gk][r], c2, -l4[r]));
-              if constexpr (!INTERIOR) {
+              if constexpr (MODE == 1) pv = (uint32_t)(r - lo) < (uint32_t)span ? pv : 0.f;
+              if constexpr (MODE == 2) {
                 const int qq = qb * 64 + 16 * t + 4 * g + r;
-                bool ok = mykey < T && qq < T;
-                if (CAUSAL) ok = ok && mykey <= qq;
-                if (doc) ok = ok && qq < myde[gk];
+                const bool ok = mykey < T && qq < T && mykey <= qq && qq < myde[gk];
                 pv = ok ? pv : 0.f;
               }
               float dpv = dp[gk][r];
@@ -605,8 +625,9 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
             }
           }
         };
-        if (interior) probs(std::true_type{});
-        else probs(std::false_type{});
+        if (interior) probs(std::integral_constant<int, 0>{});
+        else if (!doc) probs(std::integral_constant<int, 1>{});
+        else probs(std::integral_constant<int, 2>{});
       }
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
@@ -727,11 +748,20 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
             dp[gq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, of[gq][ks], ks ? dp[gq] : kZero4, 0, 0, 0);
           }
         }
-        auto probs = [&](auto interior_t) {   // the boundary test in a path of its own
-          constexpr bool INTERIOR = decltype(interior_t)::value;
+        // the boundary test in a path of its own.  MODE 0: every pair valid; 1: ragged tail / causal
+        // diagonal as one bound on this lane's 4 keys (2 VALU a score); 2: the document mask, per pair
+        auto probs = [&](auto mode_t) {
+          constexpr int MODE = decltype(mode_t)::value;
 #pragma unroll
           for (int gq = 0; gq < QG; ++gq) {
             const int myq = qw + gq * 16 + (lane & 15);
+            int lim = 3;
+            if constexpr (MODE == 1) {
+              const int kl = __builtin_amdgcn_readfirstlane(kb * 64 + 16 * t) + 4 * g;
+              lim = __builtin_amdgcn_readfirstlane(T) - 1 - kl;
+              if (CAUSAL) lim = min(lim, myq - kl);
+              if (myq >= T) lim = -1;
+            }
             uint32_t wt = 0;
             if (DROP) wt = (uint32_t)a.mask[drop_word(myq, kb * 64 + 16 * t + 4 * g, a.n64)] >> (4 * (myq & 3));
             float pv[4], dm[4];
@@ -744,11 +774,10 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              if constexpr (!INTERIOR) {
+              if constexpr (MODE == 1) pv[r] = r <= lim ? pv[r] : 0.f;
+              if constexpr (MODE == 2) {
                 const int key = kb * 64 + 16 * t + 4 * g + r;
-                bool ok = myq < T && key < T;
-                if (CAUSAL) ok = ok && key <= myq;
-                if (doc) ok = ok && key >= myds[gq];
+                const bool ok = myq < T && key < T && key <= myq && key >= myds[gq];
                 pv[r] = ok ? pv[r] : 0.f;
               }
               dm[r] = dp[gq][r];
@@ -768,8 +797,9 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
             }
           }
         };
-        if (interior) probs(std::true_type{});
-        else probs(std::false_type{});
+        if (interior) probs(std::integral_constant<int, 0>{});
+        else if (!doc) probs(std::integral_constant<int, 1>{});
+        else probs(std::integral_constant<int, 2>{});
       }
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
