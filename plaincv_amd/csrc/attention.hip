@@ -219,7 +219,7 @@ __device__ __forceinline__ void light_last(int& kb, int& h, int& b) {
 
 // Workgroup = 4 waves x 32 queries (two 16-query groups per wave share every K/V
 // fragment read from LDS); K/V tiles of 64 keys double-buffered in LDS.
-template <int DH, bool CAUSAL, bool DROP>
+template <int DH, bool CAUSAL, bool DROP, bool DOC>
 __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnArgs a) {
   constexpr int KS = DH / 32, DT = DH / 16, QG = 2;
   constexpr int TILE = 64 * DH;
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
   int nkb = (T + 63) / 64;
   if (CAUSAL) nkb = min(nkb, (qb * 128 + 127) / 64 + 1);
   // document mask: keys below the block's first document start are never visible
-  const bool doc = CAUSAL && a.dstart != nullptr;
+  constexpr bool doc = CAUSAL && DOC;   // a.dstart != nullptr, fixed at launch
   int kb0 = 0, wds = 0, gds[QG], myds[QG];
   if (doc) {
     kb0 = a.dstart[bT + min(qb * 128, T - 1)] / 64;
@@ -296,10 +296,10 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
       // accumulators; exp2 arguments stay <= 8, which bf16 P and the fp32 sums absorb.
       // The first key tile always holds a valid key for every row, so m2 is finite after it.
       auto softmax = [&](auto maskc, auto docc, int gq) {
-        constexpr bool MASK = decltype(maskc)::value, DOC = decltype(docc)::value;
+        constexpr bool MASK = decltype(maskc)::value, MDOC = decltype(docc)::value;
         const int myq = qw + gq * 16 + (lane & 15);
         uint32_t okbits = 0xFFFFu;
-        if constexpr (MASK && !DOC) {
+        if constexpr (MASK && !MDOC) {
           // ragged tail / causal diagonal: one bound per lane, 2 VALU per score.  Every row sees
           // key kb * 64 (<= qw for an active wave), so its running max is finite after this tile
           // and the NEG_BIG scores underflow exp2 to exactly 0 -- no select on P.
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
 #pragma unroll
             for (int r = 0; r < 4; ++r) s[gq][t][r] = 16 * t + r <= lim ? s[gq][t][r] : NEG_BIG;
         }
-        if constexpr (MASK && DOC) {
+        if constexpr (MASK && MDOC) {
           okbits = 0u;
           // bounds relative to this lane's first key, through readfirstlane (convergent: the
           // compiler cannot hoist these compares out of the boundary path into every tile, as it
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
               const int r = 2 * h2 + e;
               // masked keys contribute exactly 0 (under a document mask a row can see no valid key in
               // a tile while its running max is still the initial value)
-              if (MASK && DOC) p[e] = ((okbits >> (4 * t + r)) & 1u) ? p[e] : 0.f;
+              if (MASK && MDOC) p[e] = ((okbits >> (4 * t + r)) & 1u) ? p[e] : 0.f;
             }
             rs2 += (f2v){p[0], p[1]};
 #pragma unroll
@@ -475,7 +475,7 @@ struct QTileRegs {
   float l, d;
 };
 
-template <int DH, bool CAUSAL, bool DROP>
+template <int DH, bool CAUSAL, bool DROP, bool DOC>
 __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(AttnArgs a) {
   constexpr int KS = DH / 32, DT = DH / 16, KG = 2, CPR = DH / 8;
   constexpr int TILE = 64 * DH;
@@ -535,7 +535,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
   int nqb = (T + 63) / 64;
   const int qb0 = CAUSAL ? (kb * 128) / 64 : 0;
   // document mask: queries at or past the end of the block's last document never see its keys
-  const bool doc = CAUSAL && a.dstart != nullptr;
+  constexpr bool doc = CAUSAL && DOC;   // a.dstart != nullptr, fixed at launch
   int wde_lo = 0, wde_hi = 0, myde[KG];
   if (doc) {
     nqb = min(nqb, (a.dend[bT + min(kb * 128 + 127, T - 1)] + 63) / 64);
@@ -670,7 +670,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
 
 // --------------------------------------------------------------- bwd: dQ
 // Workgroup = 4 waves x 32 queries; loops over prefetched, double-buffered K/V tiles.
-template <int DH, bool CAUSAL, bool DROP>
+template <int DH, bool CAUSAL, bool DROP, bool DOC>
 __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int TILE = 64 * DH;
   constexpr int KS = DH / 32, DT = DH / 16, QG = 2;
@@ -712,7 +712,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
 
   int nkb = (T + 63) / 64;
   if (CAUSAL) nkb = min(nkb, (qb * 128 + 127) / 64 + 1);
-  const bool doc = CAUSAL && a.dstart != nullptr;
+  constexpr bool doc = CAUSAL && DOC;   // a.dstart != nullptr, fixed at launch
   int kb0 = 0, wds_lo = 0, wds_hi = 0, myds[QG];
   if (doc) {
     kb0 = a.dstart[bT + min(qb * 128, T - 1)] / 64;
@@ -1650,10 +1650,15 @@ static int launch_short_bwd(const AttnArgs& a, hipStream_t s) {
   return 0;
 }
 
+// The document mask is its own instantiation (causal only): as a runtime flag the compiler merged
+// its per-pair boundary path with the plain causal one through selects.
 template <int DH, bool C, bool D>
 static void launch_fwd(const AttnArgs& a, hipStream_t s) {
   dim3 grid((a.T + 127) / 128, a.H, a.B);
-  hipLaunchKernelGGL((attn_fwd_kernel<DH, C, D>), grid, dim3(256), 0, s, a);
+  if constexpr (C) {
+    if (a.dstart) { hipLaunchKernelGGL((attn_fwd_kernel<DH, C, D, true>), grid, dim3(256), 0, s, a); return; }
+  }
+  hipLaunchKernelGGL((attn_fwd_kernel<DH, C, D, false>), grid, dim3(256), 0, s, a);
 }
 template <int DH, bool C, bool D>
 static void launch_bwd(const AttnArgs& a, hipStream_t s) {
@@ -1662,8 +1667,15 @@ static void launch_bwd(const AttnArgs& a, hipStream_t s) {
   if (!a.delta_ready)
     hipLaunchKernelGGL((attn_bwd_delta_kernel<DH>), dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a);
   dim3 grid((a.T + 127) / 128, a.H, a.B);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH, C, D>), grid, dim3(256), 0, s, a);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, C, D>), grid, dim3(256), 0, s, a);
+  if constexpr (C) {
+    if (a.dstart) {
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH, C, D, true>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, C, D, true>), grid, dim3(256), 0, s, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH, C, D, false>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, C, D, false>), grid, dim3(256), 0, s, a);
 }
 
 template <bool FWD>
