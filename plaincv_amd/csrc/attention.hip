@@ -385,8 +385,9 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
               s[gq][t][r] = p[e];
             }
           }
-        const float rs = xsum_rows(rs2.x + rs2.y);
-        lsum[gq] += rs;
+        // per-lane partial row sum: every lane of a query row holds the same m2 / alpha, so the
+        // cross-lane sum is deferred to the end (one reduction instead of one per tile)
+        lsum[gq] += rs2.x + rs2.y;
       };
 #pragma unroll
       for (int gq = 0; gq < QG; ++gq) {
@@ -420,6 +421,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
 #pragma unroll
   for (int gq = 0; gq < QG; ++gq) {
     const int q0 = qw + gq * 16;
+    lsum[gq] = xsum_rows(lsum[gq]);
     const float inv = (DROP ? a.drop_scale : 1.f) / lsum[gq];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
