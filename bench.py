@@ -333,6 +333,16 @@ def optimizer_ms(tx, store, opt_state, gscale=None, iters=5):
             "shard": sh.describe() if sh is not None else None}
 
 
+def vit_dtype_label(cfg, state):
+    """The arithmetic the step computes in.  The fp32 runner's Muon Newton-Schulz chain runs on bf16
+    MFMA operands unless the optimizer reports an fp32 chain (optim/muon.py ns_dtype)."""
+    if cfg.vit_dtype != "float32":
+        return "bf16"
+    if cfg.optim == "muon" and getattr(state.tx, "ns_dtype", "bf16") != "f32":
+        return "f32 (Muon NS bf16)"
+    return "f32"
+
+
 def bench_vit(args):
     rank, local_rank, world, dev = dp.init_from_env()
     cfg = Config({"vit_c2": VIT_C2, "vit_c2_f32": VIT_C2_F32}.get(args.workload)
@@ -377,14 +387,17 @@ def bench_vit(args):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     dt = float(t.item())
     loss = float(step.metrics[0].item())
-    flops = state.runner_for(shape).flops_per_step()
+    runner = state.runner_for(shape)
+    flops = runner.flops_per_step()
+    executed = getattr(runner, "executed_flops_per_step", runner.flops_per_step)()
+    peak = F32_PEAK_TFLOPS if cfg.vit_dtype == "float32" else BF16_PEAK_TFLOPS
     out = None
     if rank == 0:
         sps = args.steps / dt
         out = {"metric": METRIC, "value": round(world * B * sps, 2), "unit": "images/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-               "dtype": "f32" if cfg.vit_dtype == "float32" else "bf16",
+               "dtype": vit_dtype_label(cfg, state),
                "data": "synthetic (uint8 images U[0,255], labels U[0,200), seeded, resident in HBM)",
                "config": {"workload": WORKLOAD_NAMES[args.workload], "global_batch": world * B,
                           "per_gpu_batch": B, "image": [64, 64, 3], "classes": 200, "tokens": 257,
@@ -396,6 +409,12 @@ def bench_vit(args):
                                          ("RCCL all-reduce captured in the step graph" if step.capture_reduce
                                           else "eager all-reduce between the step's two graph replays")},
                "steps_per_sec": round(sps, 3), "tflops_per_gpu": round(flops * sps / 1e12, 3),
+               # tflops_per_gpu counts SURVEY §8d's algorithmic work (3x the full forward's matmuls); the
+               # fp32 runner's cls-sparse last block skips part of it, so the executed FLOPs are stated too
+               "algorithmic_gflop_per_step": round(flops / 1e9, 3),
+               "executed_gflop_per_step": round(executed / 1e9, 3),
+               "e2e_frac_algorithmic": round(flops * sps / 1e12 / peak, 4),
+               "e2e_frac_executed": round(executed * sps / 1e12 / peak, 4),
                "final_loss": round(loss, 4)}
         out["roofline"] = (None if args.no_roofline else
                            vit_roofline_f32(state, shape, cfg.vit_dropout) if cfg.vit_dtype == "float32"

@@ -604,7 +604,9 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
             if constexpr (MODE == 1) {
               const int ql = __builtin_amdgcn_readfirstlane(qb * 64 + 16 * t) + 4 * g;
               lo = mykey >= T ? 4 : (CAUSAL ? mykey - ql : 0);
-              span = (__builtin_amdgcn_readfirstlane(T) - ql) - lo;
+              // clamped: an empty window (padding queries past T, keys past T near the tail) keeps nothing,
+              // instead of relying on the zero-filled Q / dO / lse / delta rows of the padding
+              span = max((__builtin_amdgcn_readfirstlane(T) - ql) - lo, 0);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {

@@ -280,6 +280,9 @@ class GraphedTrainStep:
     def __init__(self, state: TrainState, image_shape, warmup=2, inputs=None, overlap_opt=False,
                  reduce=None, capture_reduce=None):
         self.state = state
+        # another step object's deferred matrix phase must land before this one snapshots the state
+        # and replays its own gradient phase over the same moments / fp32 copies
+        state.params.settle()
         self.runner = state.runner_for(image_shape)
         dev = state.params.device
         self.images = torch.zeros(tuple(image_shape), dtype=torch.uint8, device=dev)
@@ -310,8 +313,20 @@ class GraphedTrainStep:
                             getattr(self.runner, "supports_join", False) and
                             hasattr(state.tx, "split_capable") and state.tx.split_capable(state.opt_state))
         self.pending = False
-        if hasattr(self.runner, "metrics_in_backward"):   # (this step always runs the backward)
+        # the captured step always runs the backward, so its metrics come from there; the flag is set
+        # only while this constructor warms up and captures (the runner's eager behaviour is unchanged)
+        had_flag = hasattr(self.runner, "metrics_in_backward")
+        old_flag = getattr(self.runner, "metrics_in_backward", None)
+        if had_flag:
             self.runner.metrics_in_backward = True
+        try:
+            self._build(state, warmup, capture_reduce, dev)
+        finally:
+            if had_flag:
+                self.runner.metrics_in_backward = old_flag
+        self.metrics = self.runner.metrics
+
+    def _build(self, state, warmup, capture_reduce, dev):
         self.stream = torch.cuda.Stream(device=dev)
         self.g_fb = torch.cuda.CUDAGraph()
         self.g_post = None
@@ -379,7 +394,6 @@ class GraphedTrainStep:
                 with torch.cuda.graph(self.g_post, stream=s, pool=self.g_fb.pool(), capture_error_mode=mode):
                     self._post()
         torch.cuda.current_stream().wait_stream(s)
-        self.metrics = self.runner.metrics
 
     def _body(self, images, steady):
         """What one step graph holds: [the previous step's matrix phase on the side stream, joined before
@@ -448,6 +462,11 @@ class GraphedTrainStep:
         self.state.tx.step_(self.state.params, self.state.opt_state)
 
     def __call__(self, images=None, labels=None):
+        owed = self.state.params.pending
+        if owed is not None and owed != self.flush:
+            # another step object (e.g. the runner of a different batch shape) still owes its matrix
+            # phase: run it before this step's gradient phase rewrites the moments it reads
+            self.state.params.settle()
         k = self._slot_of(images, labels) if self.slots else None
         steady = self.overlap and self.pending
         if k is not None:

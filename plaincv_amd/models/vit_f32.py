@@ -677,3 +677,16 @@ class ViTRunnerF32:
         per_layer = 2 * B * T * D * 3 * D + 2 * B * T * D * D + 2 * 2 * B * T * T * D + 2 * 2 * B * T * D * M
         fwd = self.m.num_layers * per_layer + 2 * B * self.hw * self.Kp * D + 2 * B * D * Kc
         return 3 * fwd
+
+    def executed_flops_per_step(self):
+        """The matmul FLOPs the step actually issues (forward + both VJPs): flops_per_step() minus what
+        the cls-sparse last block skips.  That block keeps its full-height qkv product (and its two VJPs);
+        its attention runs for the cls query only (scores and P.V over T keys, their VJPs), and the out
+        projection and the MLP run on the B cls rows."""
+        full = self.flops_per_step()
+        if not self.cls_last:
+            return full
+        B, T, D, M = self.B, self.T, self.D, self.M
+        skipped_fwd = (2 * B * T * D * D + 2 * 2 * B * T * T * D + 2 * 2 * B * T * D * M) \
+            - (2 * B * D * D + 2 * 2 * B * T * D + 2 * 2 * B * D * M)
+        return full - 3 * skipped_fwd

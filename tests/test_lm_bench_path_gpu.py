@@ -1,0 +1,119 @@
+"""The LM exactly as bench.py builds it (bench.py LM_CFGS / bench_lm), at the benchmarked micro-batch,
+against the CPU oracle: the M dimension of every launch is the bench's own 16 384 token rows.
+
+* lm124m (BASELINE configs[2]): d 768, 12 heads, F 2048, V 50257, AdamW; micro-batch 16 x T 1024;
+  2 layers (the bench runs 12; every per-layer launch is the same shape).
+* lm420m (BASELINE configs[4]): d 1024, 16 heads, F 2730 (2736 in HBM), V 50280, Muon, clip 1.0;
+  micro-batch 8 x T 2048; 1 layer (the bench runs 24).
+
+So the vocabulary products (16 384 x 50 257 x 768 and its data / weight gradients), the 256 x 256 /
+256 x 192 forward and data-gradient dispatch, the split-K weight gradients and the B = 16 / B = 8
+attention grids all run at the sizes the bench times (models/LM/transformer.py:171-407,
+train_lm.py:189-353).  One optimizer step of two accumulated micro-steps; checked (values printed as
+LMBENCH lines):
+  (1) each micro-step's loss vs the bf16-placement oracle at the same params, abs <= 2e-2;
+  (2) every accumulated gradient leaf vs the bf16-placement oracle, rel-L2 <= 2e-2, and vs the fp64
+      oracle, <= max(1e-2, 1.5x the bf16 oracle's own error against fp64);
+  (3) the global norm vs the oracle's (rel 3e-2), and (lm420m) the clip factor from the HIP norm;
+  (4) the applied update vs the oracle optimizer fed the HIP gradients (AdamW 1e-5, bf16-NS Muon 2e-2);
+  (5) a second state built from the same init and fed the same micro-batches ends with bitwise-equal
+      gradients and params: every launch of the step (split-K folds, attention, cross-entropy) is
+      run-to-run deterministic at this size.
+"""
+import pytest
+import torch
+
+from tests.parity_util import global_norm, rel, step_bound, step_rel
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
+
+CASES = {"lm124m": dict(n_layers=2), "lm420m": dict(n_layers=1)}
+ACCUM = 2
+
+
+@pytest.mark.parametrize("workload", ["lm124m", "lm420m"])
+def test_lm_bench_path_matches_oracle(dev, workload):
+    import bench
+    from oracle import optim as oopt
+    from oracle.engine import clip_grads, lm_loss_and_acc, value_and_grad
+    from oracle.lm import model_config_from_cfg, transformer_apply
+    from plaincv_amd.engine.lm import create_lm_state, make_apply_grads_fn, make_train_fns
+    from plaincv_amd.models.LM.constructor import construct_model
+    from utils import Config
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    spec = bench.LM_CFGS[workload]
+    cfg = Config(dict(spec["cfg"], **CASES[workload]))
+    mb, clip = spec["mb"], spec["clip"]
+    model, _, variables = construct_model(cfg)
+    init = {k: v.clone() for k, v in variables["params"].items()}
+    # two states from the same init (bitwise determinism, check 5)
+    sts = [create_lm_state(cfg, model, variables, mb, dev, accum=ACCUM) for _ in range(2)]
+    compute_grads, _ = make_train_fns()
+    apply_grads = make_apply_grads_fn(clip)
+    omc = model_config_from_cfg(cfg)
+    T = cfg.seq_len
+    gen = torch.Generator().manual_seed(7)
+    batches = [torch.randint(0, cfg.vocab_size, (mb, T + 1), generator=gen, dtype=torch.int32) for _ in range(ACCUM)]
+    assert batches[0].shape[0] * T == 16384   # the bench's token rows per micro-step
+
+    def grads(p, ids, dt):
+        (loss, _), gr = value_and_grad(
+            lambda q: lm_loss_and_acc(transformer_apply(q, ids[:, :-1], omc, dt), ids[:, 1:]), p)
+        return loss.item(), gr
+
+    losses = [[], []]
+    for ids in batches:
+        for k, st in enumerate(sts):
+            met = compute_grads(st, ids.to(dev))
+            torch.cuda.synchronize()
+            losses[k].append(met[0].item())
+    g_hip = sts[0].params.grads_dict()
+    g_hip2 = sts[1].params.grads_dict()
+    for k in g_hip:
+        assert torch.equal(g_hip[k], g_hip2[k]), ("gradients not run-to-run identical", k)
+    assert losses[0] == losses[1], losses
+
+    p64 = {k: v.double() for k, v in init.items()}
+    g_b, g_64 = None, None
+    for a, ids in enumerate(batches):
+        loss_b, gb = grads(init, ids, torch.bfloat16)
+        print(f"LMBENCH {workload} micro {a} loss hip {losses[0][a]:.5f} oracle {loss_b:.5f}")
+        assert abs(losses[0][a] - loss_b) <= 2e-2, (a, losses[0][a], loss_b)
+        _, g6 = grads(p64, ids, torch.float64)
+        g_b = gb if g_b is None else {k: g_b[k] + gb[k] for k in gb}
+        g_64 = g6 if g_64 is None else {k: g_64[k] + g6[k] for k in g6}
+    g_b = {k: v / ACCUM for k, v in g_b.items()}
+    g_64 = {k: v / ACCUM for k, v in g_64.items()}
+    worst = 0.0
+    for k in init:
+        r = rel(g_hip[k], g_b[k], 1e-3)
+        e_hip, e_bf = rel(g_hip[k], g_64[k], 1e-3), rel(g_b[k], g_64[k], 1e-3)
+        worst = max(worst, r)
+        print(f"LMBENCH {workload} grad {k} hip_vs_bf16 {r:.4f} hip_vs_fp64 {e_hip:.4f} bf16_vs_fp64 {e_bf:.4f}")
+        assert r < 2e-2, (workload, k, r)
+        assert e_hip < max(1e-2, 1.5 * e_bf), (workload, k, e_hip, e_bf)
+    print(f"LMBENCH {workload} worst grad rel vs bf16 oracle {worst:.4f}")
+
+    p0 = sts[0].params.to_dict()
+    outs = [apply_grads(st) for st in sts]
+    torch.cuda.synchronize()
+    gnorm = outs[0][1].item()
+    p1 = outs[0][0].params.to_dict()
+    p1b = outs[1][0].params.to_dict()
+    for k in p1:
+        assert torch.equal(p1[k], p1b[k]), ("params not run-to-run identical", k)
+    n_hip, n_or = global_norm(g_hip), global_norm(g_b)
+    print(f"LMBENCH {workload} gnorm hip {n_hip:.5f} oracle {n_or:.5f}")
+    assert abs(n_hip - n_or) <= 3e-2 * n_or, (n_hip, n_or)
+    if clip is not None:
+        assert abs(gnorm - n_hip) <= 1e-4 * n_hip, (gnorm, n_hip)
+        want = min(1.0, clip / (n_hip + 1e-6))
+        assert abs(outs[0][0].gscale.item() - want) <= 1e-5 * want, (outs[0][0].gscale.item(), want)
+    tx = oopt.get_optimizer(cfg)
+    u, _ = tx.update(clip_grads(g_hip, clip), tx.init(dict(init)), p0)
+    worst_u = 0.0
+    for k in p0:
+        e = step_rel(p0[k], p1[k], u[k])
+        worst_u = max(worst_u, e / step_bound(cfg.optim, k, p0[k]))
+        assert e <= step_bound(cfg.optim, k, p0[k]), (workload, k, e)
+    print(f"LMBENCH {workload} worst update error / bound {worst_u:.3f}")

@@ -240,3 +240,45 @@ def test_graphed_step_optimizer_overlap(dev, ring, aligned):
     for name in ("mu", "nu"):
         assert torch.equal(sa.opt_state.tensors[name], sb.opt_state.tensors[name]), name
     assert torch.equal(sa.opt_state.count, sb.opt_state.count)
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_two_overlapped_steps_share_one_state(dev, dtype):
+    """Two GraphedTrainStep(overlap_opt=True) objects on ONE state (two batch shapes, as a smaller
+    final batch gives: each shape has its own runner and graphs), called alternately, against the
+    in-step optimizer on the same two shapes -- bitwise, every step and after the last.  Each step
+    object parks its owed Muon matrix phase in ParamStore.pending; the other object must settle it
+    before replaying its own gradient phase over the same moments (engine.py GraphedTrainStep), and
+    the second object's construction must settle the first's before it snapshots the state."""
+    from plaincv_amd.engine import GraphedTrainStep, create_train_state
+    from plaincv_amd.models.vit_small import VisionTransformer
+    from utils import Config
+    m = VisionTransformer(num_classes=16, patch_size=4, hidden_size=64, mlp_dim=128, num_layers=2, num_heads=2,
+                          dropout_rate=0.1, dtype=dtype)
+    shapes = [(8, 16, 16, 3), (4, 16, 16, 3)]
+    cfg = Config(optim="muon", lr=1e-3, weight_decay=0.01, beta1=0.9, beta2=0.9)
+    init = m.init(6, shapes[0])
+    g = torch.Generator().manual_seed(11)
+    batches = [(torch.randint(0, 256, s, generator=g, dtype=torch.uint8).to(dev),
+                torch.randint(0, 16, (s[0],), generator=g, dtype=torch.int32).to(dev)) for s in shapes]
+    sa = create_train_state(0, m, 1e-3, shapes[0], 16, cfg=cfg, init_params=init)
+    sb = create_train_state(0, m, 1e-3, shapes[0], 16, cfg=cfg, init_params=init)
+    ga = [GraphedTrainStep(sa, s, warmup=1, overlap_opt=True) for s in shapes]
+    gb = [GraphedTrainStep(sb, s, warmup=1) for s in shapes]
+    assert all(x.overlap for x in ga) and not any(x.overlap for x in gb)
+    for x, y in zip(ga, gb):
+        y.runner.seed.copy_(x.runner.seed)
+    torch.cuda.synchronize()
+    assert torch.equal(sa.params.flat, sb.params.flat)
+    for it, k in enumerate([0, 1, 1, 0, 1, 0, 0]):
+        ma = ga[k](*batches[k]).clone()
+        mb = gb[k](*batches[k]).clone()
+        torch.cuda.synchronize()
+        assert torch.equal(ma, mb), (it, k, ma, mb)
+    pa, pb = sa.params.to_dict(), sb.params.to_dict()
+    assert sa.params.pending is None and not any(x.pending for x in ga)
+    diff = [k for k in pa if not torch.equal(pa[k], pb[k])]
+    assert not diff, diff
+    for name in ("mu", "nu"):
+        assert torch.equal(sa.opt_state.tensors[name], sb.opt_state.tensors[name]), name
+    assert torch.equal(sa.opt_state.count, sb.opt_state.count)
