@@ -58,6 +58,17 @@ int pcv_gemm_big_enable(int on);
 int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb);
 int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                  int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale, void* stream);
+/* Persistent form (csrc/gemm_stream.hip): one workgroup per CU, the 32-deep K steps of all its
+ * 256x256 / 256x192 output tiles in one continuous LDS-DMA ring, epilogue stored straight from the
+ * accumulators (operand-swapped MFMAs, 16-B column chunks).  Same product and operand rules as
+ * pcv_gemm_big (K % 32 != 0 allowed: the tail goes through registers).  pcv_gemm_bf16 prefers it when
+ * pcv_gemm_stream_ok(); pcv_gemm_stream_enable(on) toggles that (on < 0: query).  Replaces the LM's
+ * forward / data-gradient Dense products incl. the vocabulary-wide lm_head (transformer.py:393-405). */
+int pcv_gemm_stream_enable(int on);
+int pcv_gemm_stream_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb);
+int pcv_gemm_stream(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                    int64_t ldb, int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale,
+                    void* stream);
 /* Weight-gradient form of the same kernel: C[M,N] (fp32) += alpha * A[K,M]^T . B[K,N] with A and B
  * K-major (M-/N-contiguous rows), K split over the grid and added with fp32 atomics (K % 32 == 0).
  * pcv_gemm_bf16 dispatches trans_a, !trans_b, fp32-out, beta == 1 products without epilogue here.

@@ -25,6 +25,11 @@ extern "C" int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, i
 extern "C" int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                             int64_t ldb, int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale,
                             void* stream);
+extern "C" int pcv_gemm_stream_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
+                                  int64_t ldb);
+extern "C" int pcv_gemm_stream(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                               int64_t ldb, int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale,
+                               void* stream);
 extern "C" int pcv_gemm_big_wgrad_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
                                      int64_t ldb);
 extern "C" int pcv_gemm_big_wgrad(const void* A, const void* B, float* C, int64_t M, int64_t N, int64_t K,
@@ -1278,10 +1283,14 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
   hipStream_t s = (hipStream_t)stream;
   // large products with both operands K-contiguous and a plain (or residual) bf16 epilogue:
   // the 256x256 8-wave ping-pong kernel (gemm_big.hip)
+  // (the persistent continuous-ring form, gemm_stream.hip, first; gemm_big when it is switched off)
   if (!trans_a && trans_b && !out_f32 && batch == 1 && g.split_k == 1 && !bias && !aux && act == EPI_NONE &&
-      g.drop_thresh == 0 && !colsum && !attn_delta && (!res || !res_f32) &&
-      pcv_gemm_big_ok(M, N, K, A, lda, B, ldb))
-    return pcv_gemm_big(A, B, C, M, N, K, lda, ldb, ldc, alpha, res, ldr, res_scale, stream);
+      g.drop_thresh == 0 && !colsum && !attn_delta && (!res || !res_f32)) {
+    if (pcv_gemm_stream_ok(M, N, K, A, lda, B, ldb))
+      return pcv_gemm_stream(A, B, C, M, N, K, lda, ldb, ldc, alpha, res, ldr, res_scale, stream);
+    if (pcv_gemm_big_ok(M, N, K, A, lda, B, ldb))
+      return pcv_gemm_big(A, B, C, M, N, K, lda, ldb, ldc, alpha, res, ldr, res_scale, stream);
+  }
   // weight gradients accumulated into fp32 (C += alpha A^T B, both operands K-major): the 256x256
   // split-K / atomic form of the same kernel; it picks its own split count
   if (trans_a && !trans_b && out_f32 && beta == 1.f && batch == 1 && !bias && !res && !aux && act == EPI_NONE &&

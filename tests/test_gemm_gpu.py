@@ -128,15 +128,19 @@ def test_gemm_big_kernel(dev, M, N, K, res):
     r = _padded(M, N, dev, g) if res else None
     assert lib.pcv_gemm_big_ok(M, N, K, hip.ptr(a), a.stride(0), hip.ptr(b), b.stride(0)) == 1
     outs = []
-    for on in (1, 0):
-        prev = lib.pcv_gemm_big_enable(on)
-        try:
-            out = torch.empty(M, (N + 7) // 8 * 8, device=dev, dtype=torch.bfloat16)[:, :N]
-            k.gemm(a, b, out, tb=True, alpha=0.5, res=r)
-            torch.cuda.synchronize()
-        finally:
-            lib.pcv_gemm_big_enable(prev)
-        outs.append(out.float())
+    prev_stream = lib.pcv_gemm_stream_enable(0)   # (pcv_gemm_bf16 prefers the persistent kernel)
+    try:
+        for on in (1, 0):
+            prev = lib.pcv_gemm_big_enable(on)
+            try:
+                out = torch.empty(M, (N + 7) // 8 * 8, device=dev, dtype=torch.bfloat16)[:, :N]
+                k.gemm(a, b, out, tb=True, alpha=0.5, res=r)
+                torch.cuda.synchronize()
+            finally:
+                lib.pcv_gemm_big_enable(prev)
+            outs.append(out.float())
+    finally:
+        lib.pcv_gemm_stream_enable(prev_stream)
     ref = 0.5 * (a.float() @ b.float().t())
     if res:
         ref = ref + r.float()
@@ -144,3 +148,51 @@ def test_gemm_big_kernel(dev, M, N, K, res):
     for out in outs:
         assert (out - ref).abs().max().item() <= tol
     assert (outs[0] - outs[1]).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize("M,N,K,res", [(16384, 50257, 768, False), (16384, 768, 50257, False), (8192, 4096, 1000, True),
+                                       (16384, 2304, 128, False), (6000, 5472, 2736, True), (4100, 8200, 200, False),
+                                       (16384, 768, 2304, True), (16384, 768, 4100, False), (16384, 1024, 1024, True),
+                                       (16384, 2048, 768, False), (8000, 1000, 136, True), (16384, 5472, 1024, False)])
+def test_gemm_stream_kernel(dev, M, N, K, res):
+    """Persistent continuous-ring kernel (gemm_stream.hip) through pcv_gemm_bf16's dispatch: many tiles per
+    workgroup (the lm_head: 49-50 per CU), one tile per workgroup (N = 768, 256 x 192), ragged M / N (masked
+    tiles), ragged K (the masked last ring step: K % 32 = 17, 8, 4, 16), the residual epilogue and padded row
+    strides.  Against an fp32 product of the same bf16 operands, against gemm_big and the 128x128 family on
+    the same call, and bitwise run-to-run."""
+    from plaincv_amd import hip
+    from plaincv_amd import kernels as k
+    lib = hip.load()
+    g = torch.Generator(device=dev).manual_seed(M + 3 * N + K)
+    a = _padded(M, K, dev, g)
+    b = _padded(N, K, dev, g)
+    r = _padded(M, N, dev, g) if res else None
+    assert lib.pcv_gemm_stream_ok(M, N, K, hip.ptr(a), a.stride(0), hip.ptr(b), b.stride(0)) == 1
+
+    def run(stream_on, big_on):
+        ps, pb = lib.pcv_gemm_stream_enable(stream_on), lib.pcv_gemm_big_enable(big_on)
+        try:
+            out = torch.full((M, (N + 7) // 8 * 8), 7.0, device=dev, dtype=torch.bfloat16)
+            k.gemm(a, b, out[:, :N], tb=True, alpha=0.5, res=r)
+            torch.cuda.synchronize()
+        finally:
+            lib.pcv_gemm_stream_enable(ps)
+            lib.pcv_gemm_big_enable(pb)
+        return out
+
+    o1, o2 = run(1, 1), run(1, 1)
+    assert torch.equal(o1, o2), "persistent GEMM not run-to-run identical"
+    assert bool((o1[:, N:] == 7.0).all()), "wrote into the row padding past N"
+    ref = 0.5 * (a.float() @ b.float().t())
+    if res:
+        ref = ref + r.float()
+    tol = 1e-3 * (K ** 0.5) * 4 + 1e-2 * ref.abs().max().item()   # bf16 output rounding
+    err = (o1[:, :N].float() - ref).abs().max().item()
+    print(f"GEMMSTREAM M={M} N={N} K={K} res={res} max|err| {err:.3g} tol {tol:.3g}")
+    assert err <= tol
+    del ref
+    for other in ((0, 1), (0, 0)):
+        if other == (0, 1) and not lib.pcv_gemm_big_ok(M, N, K, hip.ptr(a), a.stride(0), hip.ptr(b), b.stride(0)):
+            continue
+        o = run(*other)
+        assert (o[:, :N].float() - o1[:, :N].float()).abs().max().item() <= tol, other

@@ -15,7 +15,8 @@ mkdir -p "$O"
 cd "$R" || exit 1
 export PYTHONPATH=$R
 if [ -n "$TESTS" ]; then
-  timeout -k 10 1100 python -u -m pytest $TESTS -v -s --tb=short --timeout 600 --timeout-method thread \
+  eval "targs=($TESTS)"   # quoted pieces (e.g. -k "a or b") stay one argument
+  timeout -k 10 1100 python -u -m pytest "${targs[@]}" -v -s --tb=short --timeout 600 --timeout-method thread \
     > "$O/tests.log" 2>&1
   rc=$?
   grep -E "FAILED|ERROR" "$O/tests.log" | head -20
