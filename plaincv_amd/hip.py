@@ -153,6 +153,9 @@ SIGNATURES = {
     "pcv_gemm_big_enable": [I32],
     "pcv_gemm_big_ok": [I64, I64, I64, P, I64, P, I64],
     "pcv_gemm_big": [P, P, P, I64, I64, I64, I64, I64, I64, F32, P, I64, F32, P],
+    "pcv_gemm_stream_enable": [I32],
+    "pcv_gemm_stream_ok": [I64, I64, I64, P, I64, P, I64],
+    "pcv_gemm_stream": [P, P, P, I64, I64, I64, I64, I64, I64, F32, P, I64, F32, P],
     "pcv_gemm_big_wgrad_ok": [I64, I64, I64, P, I64, P, I64],
     "pcv_gemm_big_wgrad": [P, P, P, I64, I64, I64, I64, I64, I64, F32, P],
     "pcv_f32_job_size": [],
