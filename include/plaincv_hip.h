@@ -69,6 +69,19 @@ int pcv_gemm_stream_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t l
 int pcv_gemm_stream(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                     int64_t ldb, int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale,
                     void* stream);
+/* Grouped deterministic split-K weight gradients (csrc/gemm_wgrad.hip): for j < njobs (<= 8),
+ * C_j[M,N] (fp32) = beta * C_j + alpha * A_j[K,M]^T . B_j[K,N], A_j [K][lda >= M] and B_j [K][ldb >= N]
+ * bf16 (K-major: the Dense layer's inputs and output gradients), dims[6 j ..] = {M, N, K, lda, ldb,
+ * ldc}, K % 32 == 0.  256 x 256 tiles, K split `splits` ways (0: automatic); the splits' fp32
+ * partials go to workspace slabs and the last split of each tile sums them in split order, so the
+ * result is run-to-run identical.  ws: pcv_gemm_wgrad_ws_bytes() bytes (0 when the plan has one
+ * split), zero-filled once before first use (tile tickets the kernel leaves at zero).  Replaces the
+ * kernel cotangents X^T dY of the LM's Dense layers and lm_head (transformer.py:194-201, 246-253,
+ * 110-134, 393-405 VJPs; accumulated over micro-steps with beta = 1, train_lm.py:189-241). */
+int64_t pcv_gemm_wgrad_ws_bytes(int njobs, const int64_t* dims, int splits);
+int pcv_gemm_wgrad_grouped(int njobs, const void* const* A, const void* const* B, float* const* C,
+                           const int64_t* dims, float alpha, float beta, int splits, void* ws, int64_t ws_bytes,
+                           void* stream);
 /* Weight-gradient form of the same kernel: C[M,N] (fp32) += alpha * A[K,M]^T . B[K,N] with A and B
  * K-major (M-/N-contiguous rows), K split over the grid and added with fp32 atomics (K % 32 == 0).
  * pcv_gemm_bf16 dispatches trans_a, !trans_b, fp32-out, beta == 1 products without epilogue here.

@@ -135,6 +135,56 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
     return out
 
 
+_WGRAD_WS = {}
+
+
+def wgrad_workspace(dev, nbytes):
+    """The device's shared workspace of the grouped weight-gradient launches (tile tickets first, zero-
+    filled on allocation and left at zero by every launch; split partial slabs after).  Grown outside
+    graph capture only: WGradGroup sizes it when it is built."""
+    w = _WGRAD_WS.get(dev)
+    if w is None or w.numel() < nbytes:
+        w = _WGRAD_WS[dev] = torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+    return w
+
+
+class WGradGroup:
+    """A fixed set of weight-gradient products C_j = beta C_j + alpha A_j^T B_j (A_j [K,M], B_j [K,N] bf16,
+    C_j [M,N] fp32) run as ONE grouped deterministic split-K launch (pcv_gemm_wgrad_grouped,
+    csrc/gemm_wgrad.hip).  Built once outside graph capture on persistent buffers: shapes are validated
+    here, the ctypes argument arrays kept, the shared workspace sized."""
+
+    def __init__(self, jobs, device, splits=0):
+        import ctypes
+        n = len(jobs)
+        _chk(1 <= n <= 8, "WGradGroup: 1..8 jobs")
+        dims = []
+        for a, b, c in jobs:
+            _chk(a.dtype == BF16 and b.dtype == BF16 and c.dtype == F32 and a.dim() == 2 and b.dim() == 2 and
+                 c.dim() == 2 and a.is_cuda and b.is_cuda and c.is_cuda, "WGradGroup operands")
+            K, M = a.shape
+            K2, N = b.shape
+            _chk(K == K2 and tuple(c.shape) == (M, N) and K % 32 == 0, f"WGradGroup shapes {a.shape} {b.shape} {c.shape}")
+            dims += [M, N, K, _ld(a), _ld(b), _ld(c)]
+        self.jobs = jobs
+        self.n = n
+        self.splits = int(splits)
+        self._keep = [(a, b, c) for a, b, c in jobs]
+        self._A = (ctypes.c_void_p * n)(*[a.data_ptr() for a, _, _ in jobs])
+        self._B = (ctypes.c_void_p * n)(*[b.data_ptr() for _, b, _ in jobs])
+        self._C = (ctypes.c_void_p * n)(*[c.data_ptr() for _, _, c in jobs])
+        self._dims = (ctypes.c_int64 * len(dims))(*dims)
+        self.ws_bytes = int(hip.load().pcv_gemm_wgrad_ws_bytes(n, self._dims, self.splits))
+        _chk(self.ws_bytes >= 0, "WGradGroup: unsupported job description")
+        self.device = torch.device(device)
+        self.ws = wgrad_workspace(self.device, self.ws_bytes)
+
+    def __call__(self, alpha=1.0, beta=1.0):
+        ws = self.ws if self.ws_bytes > 0 else None
+        hip.call("pcv_gemm_wgrad_grouped", self.n, self._A, self._B, self._C, self._dims, float(alpha), float(beta),
+                 self.splits, ptr(ws), int(ws.numel()) if ws is not None else 0, stream_ptr())
+
+
 def col_rows(M, col_reps):
     """Rows of a column-accumulator buffer: col_reps replicas (atomics), or with col_reps = -1 one row
     per 64-row output tile of M rows (plain stores; the GEMM and LayerNorm-epilogue tiles)."""

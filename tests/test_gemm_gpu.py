@@ -196,3 +196,45 @@ def test_gemm_stream_kernel(dev, M, N, K, res):
             continue
         o = run(*other)
         assert (o[:, :N].float() - o1[:, :N].float()).abs().max().item() <= tol, other
+
+
+@pytest.mark.parametrize("case", ["layer124", "layer420", "lm_head124", "ragged", "beta0"])
+def test_gemm_wgrad_grouped(dev, case):
+    """Grouped deterministic split-K weight gradients (gemm_wgrad.hip): C_j = beta C_j + alpha A_j^T B_j for
+    the four matrices of an LM layer in one launch (124M / 420M widths at the bench's 16 384 token rows),
+    the vocabulary-wide lm_head alone, ragged M / N (not multiples of 256), beta 0 and explicit splits.
+    Against an fp32 product of the same bf16 operands, and bitwise run-to-run (the splits' partial slabs
+    are summed in split order by whichever split finishes last)."""
+    from plaincv_amd import kernels as k
+    g = torch.Generator(device=dev).manual_seed(hash(case) % 1000)
+    R = 16384
+    shapes = {"layer124": [(2048, 768), (768, 4096), (768, 768), (768, 2304)],
+              "layer420": [(2730, 1024), (1024, 5472), (1024, 1024), (1024, 3072)],
+              "lm_head124": [(768, 50257)],
+              "ragged": [(300, 1000), (777, 130)],
+              "beta0": [(768, 2304)]}[case]
+    Kr = 4096 if case == "ragged" else R
+    jobs = []
+    for M, N in shapes:
+        a = _padded(Kr, M, dev, g)
+        b = _padded(Kr, N, dev, g) * 0.1
+        c = torch.randn(M, N, device=dev, generator=g)
+        jobs.append((a, b, c))
+    beta = 0.0 if case == "beta0" else 1.0
+    splits = {"ragged": 3, "beta0": 2}.get(case, 0)
+    c0 = [c.clone() for _, _, c in jobs]
+    grp = k.WGradGroup(jobs, dev, splits=splits)
+    grp(alpha=0.5, beta=beta)
+    torch.cuda.synchronize()
+    first = [c.clone() for _, _, c in jobs]
+    for (_, _, c), init in zip(jobs, c0):
+        c.copy_(init)
+    grp(alpha=0.5, beta=beta)
+    torch.cuda.synchronize()
+    for (a, b, c), init, f in zip(jobs, c0, first):
+        assert torch.equal(c, f), "grouped weight gradient not run-to-run identical"
+        ref = beta * init + 0.5 * (a.float().t() @ b.float())
+        err = (c - ref).abs().max().item()
+        tol = 2e-5 * (a.float().abs().t() @ b.float().abs()).max().item() + 1e-5
+        print(f"WGRAD {case} M={a.shape[1]} N={b.shape[1]} K={a.shape[0]} splits={splits} max|err| {err:.3g} tol {tol:.3g}")
+        assert err <= tol
