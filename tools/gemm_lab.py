@@ -85,6 +85,26 @@ def nt(quick):
         torch.cuda.empty_cache()
 
 
+LAYERS = {"124M": [(2048, 768), (768, 4096), (768, 768), (768, 2304)],
+          "420M": [(2730, 1024), (1024, 5472), (1024, 1024), (1024, 3072)]}
+
+
+def grouped():
+    """The grouped deterministic launch (gemm_wgrad.hip) on the four matrices of a layer / the lm_head,
+    against the per-matrix dispatched hand path (128x128 split-K atomics / gemm_big_wgrad)."""
+    R = 16384
+    for name, shapes in list(LAYERS.items()) + [("124M lm_head", [(768, 50257)]), ("420M lm_head", [(1024, 50280)])]:
+        jobs = [(padded(R, M), padded(R, N), torch.zeros(M, N, device=dev)) for M, N in shapes]
+        fl = sum(2.0 * M * N * R for M, N in shapes)
+        grp = K.WGradGroup(jobs, dev)
+        t_g = tm(lambda: grp(beta=1.0))
+        t_h = tm(lambda: [K.gemm(a, b, c, ta=True, beta=1.0) for a, b, c in jobs])
+        print(f"{name:14s} grouped wgrad ({len(jobs)} jobs, {fl / 1e9:.0f} GFLOP): grouped {t_g:8.1f} us "
+              f"{fl / t_g / 1e6:6.0f} TF/s | per-matrix hand {t_h:8.1f} us {fl / t_h / 1e6:6.0f} TF/s", flush=True)
+        del jobs, grp
+        torch.cuda.empty_cache()
+
+
 def wgrad(quick):
     for name, M, N, Kd in (WG[:3] if quick else WG):
         a, b = padded(Kd, M), padded(Kd, N)
@@ -106,3 +126,5 @@ if __name__ == "__main__":
         nt(quick)
     if what in ("wgrad", "all"):
         wgrad(quick)
+    if what in ("grouped", "all"):
+        grouped()
