@@ -38,6 +38,7 @@
 // round_up(K, 8) re-read an in-bounds chunk and every fragment element with k >= K is zeroed on
 // both operands before the MFMAs (rows must be padded to round_up(K, 8) elements: host-checked).
 #include "common.h"
+#include <type_traits>
 
 namespace pcv {
 
@@ -99,7 +100,7 @@ __device__ __forceinline__ int st_brow(int wc, int j, int rho) {
   return wc * WN + (WN / 32) * 32 + rho;
 }
 
-template <int BN, bool RES>
+template <int BN, bool RES, bool RK>
 __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
   using C = StCfg<BN>;
   constexpr int NJ = C::NJ, NP = C::NP, WN = C::WN;
@@ -116,7 +117,8 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
   const int nt = (tcount - li + P8 - 1) / P8;
   const int S = (g.K + 31) >> 5;   // 32-deep steps per tile (>= 4); a ragged last step when K % 32 != 0
   const int Kp8 = (g.K + 7) & ~7;  // row reads stay below round_up(K, 8) <= ld (host-checked)
-  const bool ragged_k = (g.K & 31) != 0;
+  // RK (K % 32 != 0) is a template parameter: as a runtime flag, the compiler turned the last step's
+  // fragment masking into unconditional v_and's on every step (48 VALU per step, -30 % measured)
   const int G = nt * S;
   const int per_group = 8 * g.tiles_n;
   auto coords = [&](int k, int& m0, int& n0) {
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
     // ragged last step: a 16-B chunk that starts at or past round_up(K, 8) re-reads the chunk 32
     // columns back (in bounds; its elements are zeroed in the fragments like every k >= K)
     int dA[2] = {ko, ko}, dB[2] = {ko, ko};
-    if (ragged_k && iss_s == S - 1) {
+    if (RK && iss_s == S - 1) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         dA[i] -= (ko + kcA[i] >= Kp8) ? 32 : 0;
@@ -293,7 +295,11 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
   st_barrier();
   if (wr == 1) st_barrier();    // stagger: group 1 runs one barrier behind
   int ck = 0, cs = 0;           // compute tile / step within it
-  for (int gi = 0; gi < G; ++gi) {
+  int gi = 0;
+  // one step of the stream; MASKED: the ragged last step of a tile (k >= K zeroed on both operands).
+  // The two forms are separate copies of the whole step so the mask cannot leak into the others.
+  auto step = [&](auto masked_t) {
+    constexpr bool MASKED = decltype(masked_t)::value;
     if (gi + 3 < G) issue_next();
     const char* slot = smem + (gi & 3) * C::SLOT;
     bf16x8 a[8], b[NJ];
@@ -303,7 +309,7 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
     for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(slot + offA0 + i * 1024);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (ragged_k && cs == S - 1) {   // zero k >= K on both operands (uniform branch, once per tile)
+    if constexpr (MASKED) {
       const int kb = cs * 32 + lq * 8;
       u32x4 mk;
 #pragma unroll
@@ -326,6 +332,14 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
     __builtin_amdgcn_sched_barrier(0);
     if (wr == 0 && gi + 1 < G) st_wait(n);
     st_barrier();
+  };
+  for (; gi < G; ++gi) {
+    if constexpr (RK) {
+      if (cs == S - 1) step(std::true_type{});
+      else step(std::false_type{});
+    } else {
+      step(std::false_type{});
+    }
     if (++cs == S) {
       epilogue(ck);
       cs = 0;
@@ -372,16 +386,23 @@ extern "C" int pcv_gemm_stream_ok(int64_t M, int64_t N, int64_t K, const void* A
   if (!g_stream_enabled || !stream_shape_ok(M, N, K, A, lda, B, ldb)) return 0;
   const int ncu = pcv_cu_count();
   const int bn = stream_bn(M, N, ncu);
+  if ((K & 31) && bn != 192) return 0;   // ragged K only in the 256 x 192 form
   const int64_t tiles = ((M + ST_T - 1) / ST_T) * ((N + bn - 1) / bn);
   return tiles * 2 >= ncu ? 1 : 0;
 }
 
+template <int BN, bool RES, bool RK>
+static int launch_stream3(const StArgs& g, int grid, hipStream_t s) {
+  static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
+  if (const int e = optin.ensure((const void*)gemm_stream_kernel<BN, RES, RK>, (int)(StCfg<BN>::LDS))) return e;
+  hipLaunchKernelGGL((gemm_stream_kernel<BN, RES, RK>), dim3(grid), dim3(512), StCfg<BN>::LDS, s, g);
+  return 0;
+}
 template <int BN, bool RES>
 static int launch_stream(const StArgs& g, int grid, hipStream_t s) {
-  static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
-  if (const int e = optin.ensure((const void*)gemm_stream_kernel<BN, RES>, (int)(StCfg<BN>::LDS))) return e;
-  hipLaunchKernelGGL((gemm_stream_kernel<BN, RES>), dim3(grid), dim3(512), StCfg<BN>::LDS, s, g);
-  return 0;
+  if constexpr (BN == 192)   // (the 256-wide ragged-K form spills ~120 VGPRs: not built, not dispatched)
+    if (g.K & 31) return launch_stream3<BN, RES, true>(g, grid, s);
+  return launch_stream3<BN, RES, false>(g, grid, s);
 }
 
 extern "C" int pcv_gemm_stream(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
@@ -389,6 +410,7 @@ extern "C" int pcv_gemm_stream(const void* A, const void* B, void* C, int64_t M,
                                void* stream) {
   if (!stream_shape_ok(M, N, K, A, lda, B, ldb) || !C || ldc < N || (res && ldr < N)) return PCV_EINVAL;
   const int ncu = pcv_cu_count();
+  if ((K & 31) && stream_bn(M, N, ncu) != 192) return PCV_EINVAL;
   StArgs g{};
   g.A = (const bf16*)A; g.B = (const bf16*)B; g.C = (bf16*)C; g.res = (const bf16*)res;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldr = ldr;
