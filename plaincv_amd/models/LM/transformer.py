@@ -184,6 +184,7 @@ class LMRunner:
         self.doc = None
         self._views()
         self._transposed_weights(dev)
+        self._wgrad_groups(dev)
         # flat-gradient offsets above which the backward has finished (overlapped DP reduction)
         lv = store.layout.leaves
         first = lambda pre: min(l.offset for k, l in lv.items() if k.startswith(pre))  # noqa: E731
@@ -210,6 +211,33 @@ class LMRunner:
         self.sf, self.gsf = P["out_norm/RMSNorm_0/scale"], G["out_norm/RMSNorm_0/scale"]
         if not c.tie_embeddings:
             self.Wh, self.gWh = W["lm_head/kernel"], G["lm_head/kernel"]
+
+    def _wgrad_groups(self, dev):
+        """The weight gradients as grouped deterministic split-K launches (csrc/gemm_wgrad.hip): the four
+        matrices of a layer (fc2, gate|up or fc1, out, qkv) in ONE launch at the end of the layer's
+        backward, and the vocabulary-wide lm_head (or tied embedding) product on its own.  The layer's
+        incoming, middle and outgoing gradients rotate through three buffers so the deferred products
+        still see their inputs (layer at backward position p: in 2p % 3, middle 2p+1 % 3, out 2p+2 % 3).
+        Token rows not a multiple of 32: the per-matrix 128x128 products instead."""
+        c, R, d = self.c, self.R, self.d
+        self.dxb = [self.dx] + [torch.empty(R, d, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+        self.wg_layers = None
+        self.wg_head = None
+        if R % 32:
+            return
+        L = c.n_layers
+        self.wg_layers = []
+        for i in range(L):
+            p = L - 1 - i
+            w = self.w[i]
+            dx_in, dx_mid = self.dxb[(2 * p) % 3], self.dxb[(2 * p + 1) % 3]
+            dgu = self.dgu if self.glu else self.dgu[:, : self.F]
+            self.wg_layers.append(K.WGradGroup([(self.hm[i], dx_in, w["gW2"]), (self.y1[i], dgu, w["gWgu"]),
+                                                (self.o[i], dx_mid, w["gWo"]), (self.y0[i], self.dqkv, w["gWqkv"])],
+                                               dev))
+        dl = self.logits
+        self.wg_head = (K.WGradGroup([(dl, self.yf, self.gWemb)], dev) if c.tie_embeddings else
+                        K.WGradGroup([(self.yf, dl, self.gWh)], dev))
 
     def _transposed_weights(self, dev):
         """K-contiguous ([out][in]) bf16 copies of the forward-GEMM weights, so every forward
@@ -299,39 +327,56 @@ class LMRunner:
         c = self.c
         b, T, d, H, Dh = self.b, self.T, self.d, self.H, self.Dh
         dl = self.logits  # dlogits (in place)
-        if c.tie_embeddings:
+        grouped = self.wg_layers is not None
+        if grouped:
+            self.wg_head(beta=1.0)
+        elif c.tie_embeddings:
             K.gemm(dl, self.yf, self.gWemb, ta=True, beta=1.0)
-            K.gemm(dl, self.Wemb, self.dy, tb=False, library=self.vocab_lib)
         else:
             K.gemm(self.yf, dl, self.gWh, ta=True, beta=1.0)
+        if c.tie_embeddings:
+            K.gemm(dl, self.Wemb, self.dy, tb=False, library=self.vocab_lib)
+        else:
             K.gemm(dl, self.Wh, self.dy, tb=True, library=self.vocab_lib)
-        K.rmsnorm_bwd(self.dy, self.x[-1], self.sf, self.rf, None, self.dx, self.gsf)
+        K.rmsnorm_bwd(self.dy, self.x[-1], self.sf, self.rf, None, self.dxb[0], self.gsf)
         if on_ready is not None:
             on_ready(self._ready_off["head"])
-        for i in reversed(range(c.n_layers)):
+        L = c.n_layers
+        for i in reversed(range(L)):
             w = self.w[i]
-            K.gemm(self.hm[i], self.dx, w["gW2"], ta=True, beta=1.0)
-            K.gemm(self.dx, w["W2"], self.dh, tb=True)
+            p = L - 1 - i
+            if grouped:
+                dx_in, dx_mid, dx_out = self.dxb[(2 * p) % 3], self.dxb[(2 * p + 1) % 3], self.dxb[(2 * p + 2) % 3]
+            else:
+                dx_in = dx_mid = dx_out = self.dxb[0]
+                K.gemm(self.hm[i], dx_in, w["gW2"], ta=True, beta=1.0)
+            K.gemm(dx_in, w["W2"], self.dh, tb=True)
             if self.glu:
                 K.swiglu_bwd(self.dh, self.gu[i], self.dgu, F=self.F)
                 dgu = self.dgu
             else:
                 K.mlp_act_bwd(self.dh, self.gu[i], self.dgu, self.F, c.mlp)
                 dgu = self.dgu[:, : self.F]
-            K.gemm(self.y1[i], dgu, w["gWgu"], ta=True, beta=1.0)
+            if not grouped:
+                K.gemm(self.y1[i], dgu, w["gWgu"], ta=True, beta=1.0)
             K.gemm(dgu, w["Wgu"], self.dy, tb=True)
-            K.rmsnorm_bwd(self.dy, self.x1[i], w["s1"], self.r1[i], self.dx, self.dx, w["gs1"])
-            K.gemm(self.o[i], self.dx, w["gWo"], ta=True, beta=1.0)
-            K.gemm(self.dx, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H))   # + delta
+            K.rmsnorm_bwd(self.dy, self.x1[i], w["s1"], self.r1[i], dx_in, dx_mid, w["gs1"])
+            if not grouped:
+                K.gemm(self.o[i], dx_mid, w["gWo"], ta=True, beta=1.0)
+            K.gemm(dx_mid, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H))   # + delta
             K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, self.dqkv, b, T, H, Dh, causal=True,
                        doc=self.doc,
                        delta_ready=True)
             K.rope(self.dqkv, T, Dh, self.cos, self.sin, backward=True, ncols=2 * d)
-            K.gemm(self.y0[i], self.dqkv, w["gWqkv"], ta=True, beta=1.0)
+            if grouped:
+                self.wg_layers[i](beta=1.0)   # fc2, gate|up, out, qkv weight gradients: one launch
+            else:
+                K.gemm(self.y0[i], self.dqkv, w["gWqkv"], ta=True, beta=1.0)
             K.gemm(self.dqkv, w["Wqkv"], self.dy, tb=True)
-            K.rmsnorm_bwd(self.dy, self.x[i], w["s0"], self.r0[i], self.dx, self.dx, w["gs0"])
+            K.rmsnorm_bwd(self.dy, self.x[i], w["s0"], self.r0[i], dx_mid, dx_out, w["gs0"])
             if on_ready is not None and i > 0:
                 on_ready(self._ready_off[i])
-        K.embed_bwd(self.inputs, self.dx, self.gWemb)
+        dx_fin = self.dxb[(2 * L) % 3] if grouped else self.dxb[0]
+        K.embed_bwd(self.inputs, dx_fin, self.gWemb)
         if on_ready is not None:
             on_ready(0)
