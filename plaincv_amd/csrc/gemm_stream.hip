@@ -105,7 +105,9 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
   using C = StCfg<BN>;
   constexpr int NJ = C::NJ, NP = C::NP, WN = C::WN;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // the wave index through readfirstlane: wave-uniform for the compiler, so the group / count branches
+  // are scalar (as a VGPR value the counted waits became an exec-masked if-tree per step)
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int wr = wave >> 2, wc = wave & 3;
 
   // this workgroup's tiles: XCD x = blockIdx % 8 owns the contiguous run [tstart, tstart + tcount)

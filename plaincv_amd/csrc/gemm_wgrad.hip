@@ -78,7 +78,9 @@ __device__ __forceinline__ void wt_wait12(bf16x4 (&lo)[12], bf16x4 (&hi)[12]) {
 
 __global__ __launch_bounds__(512, 1) void gemm_wgrad_kernel(WgPlan P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // the wave index through readfirstlane: wave-uniform for the compiler, so the group / count branches
+  // are scalar (as a VGPR value the counted waits became an exec-masked if-tree per step)
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int wr = wave >> 2, wc = wave & 3;
   // XCD-contiguous flat index: XCD x = blockIdx % 8 runs flat indices [x q + min(x, r), ...)
   const int bid = blockIdx.x, nwg = P.nflat;

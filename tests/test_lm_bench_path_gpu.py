@@ -17,8 +17,11 @@ LMBENCH lines):
   (3) the global norm vs the oracle's (rel 3e-2), and (lm420m) the clip factor from the HIP norm;
   (4) the applied update vs the oracle optimizer fed the HIP gradients (AdamW 1e-5, bf16-NS Muon 2e-2);
   (5) a second state built from the same init and fed the same micro-batches ends with bitwise-equal
-      gradients and params: every launch of the step (split-K folds, attention, cross-entropy) is
-      run-to-run deterministic at this size.
+      gradients and params on every matrix leaf (the GEMM-produced weight gradients: the grouped split-K
+      launches fold their partials in split order, the persistent forward / data-gradient kernel has no
+      split; attention and cross-entropy are atomic-free).  Two leaf classes still sum with fp32
+      atomics: the embedding table (a scatter-add over token ids, embed_bwd_kernel) and the RMSNorm
+      scales (column sums over 16 384 rows, norm_param_grad_kernel); they are held to 1e-6 relative.
 """
 import pytest
 import torch
@@ -69,8 +72,12 @@ def test_lm_bench_path_matches_oracle(dev, workload):
             losses[k].append(met[0].item())
     g_hip = sts[0].params.grads_dict()
     g_hip2 = sts[1].params.grads_dict()
+    atomic = lambda k: k.endswith("/scale") or k.startswith("embed_tokens/")  # noqa: E731
     for k in g_hip:
-        assert torch.equal(g_hip[k], g_hip2[k]), ("gradients not run-to-run identical", k)
+        if atomic(k):
+            assert rel(g_hip2[k], g_hip[k], 1e-30) <= 1e-6, k
+        else:
+            assert torch.equal(g_hip[k], g_hip2[k]), ("gradients not run-to-run identical", k)
     assert losses[0] == losses[1], losses
 
     p64 = {k: v.double() for k, v in init.items()}
@@ -100,8 +107,14 @@ def test_lm_bench_path_matches_oracle(dev, workload):
     gnorm = outs[0][1].item()
     p1 = outs[0][0].params.to_dict()
     p1b = outs[1][0].params.to_dict()
+    # a matrix leaf's update depends on its own gradient and, under clipping, on the global norm, which
+    # sums the atomic leaves too: bitwise when the two clip factors agree, else within 1e-6
+    same_scale = clip is None or outs[0][0].gscale.item() == outs[1][0].gscale.item()
     for k in p1:
-        assert torch.equal(p1[k], p1b[k]), ("params not run-to-run identical", k)
+        if same_scale and not atomic(k):
+            assert torch.equal(p1[k], p1b[k]), ("params not run-to-run identical", k)
+        else:
+            assert rel(p1b[k] - p0[k], p1[k] - p0[k], 1e-30) <= 1e-5, k
     n_hip, n_or = global_norm(g_hip), global_norm(g_b)
     print(f"LMBENCH {workload} gnorm hip {n_hip:.5f} oracle {n_or:.5f}")
     assert abs(n_hip - n_or) <= 3e-2 * n_or, (n_hip, n_or)
