@@ -542,33 +542,67 @@ def bench_lm(args):
                        "parallelism": f"dp{world}"},
             "steps_per_sec": round(args.steps / dt, 4),
             "tflops_per_gpu": round(tokens / world / dt * fpt / 1e12, 2),
-            "roofline": None if args.no_roofline else lm_roofline(st),
+            "roofline": None if args.no_roofline else lm_roofline(st, dt / args.steps / accum * 1e3),
             "grad_allreduce": ar, "optimizer_step_per_rank": om,
             "cpu_baseline": (cpu_baseline_lm(cfg, variables, spec["clip"], **cpu_sample(args))
                              if world == 1 and not args.no_cpu_baseline else None)}
 
 
-def lm_roofline(st):
-    """Largest MFMA-bound kernel of the LM step: the lm_head GEMM (logits = y . W_head,
-    M = micro_batch*T, N = vocab, K = d_model), timed live with HIP events."""
-    from plaincv_amd import hip
+def lm_roofline(st, ms_per_micro):
+    """The LM step's kernel families, each launch timed live with HIP events on its stream (layer 0's
+    launches; the step repeats them per layer), with its share of a micro-step = launch time x launches
+    per micro-step / measured micro-step time.  `roofline` is the family with the LARGEST share (by
+    these live times: the grouped layer weight gradient at 124M / 420M), the others are listed in
+    `families`.  Work per launch is algorithmic: 2 M N K per GEMM; causal attention counts the
+    T (T + 1) / 2 visible (query, key) pairs, forward 2 products (S, P.V), backward 4 (dP, dV, dK, dQ)."""
     from plaincv_amd import kernels as K
     r = st.runner
-    M, Kd = r.yf.shape
-    N = r.logits.shape[1]
-    # the launch the step makes: hipBLASLt for the vocabulary products (csrc/blaslt.hip), when it initialised
-    dt = timed_kernel(lambda: K.gemm(r.yf, r.WhT, r.logits, tb=True, library=r.vocab_lib), iters=10)
-    flops = 2.0 * M * N * Kd
-    achieved = flops / dt / 1e12
-    lib = hip.load()
-    big = lib.pcv_gemm_big_ok(M, N, Kd, hip.ptr(r.yf), r.yf.stride(0), hip.ptr(r.WhT), r.WhT.stride(0))
-    name = ("hipBLASLt via pcv_blaslt_gemm_bf16" if r.vocab_lib else
-            "gemm_big_kernel<256>" if big else "gemm_bf16_kernel<true,true,4,4>")
-    return {"kernel": f"{name} (lm_head fwd on the K-contiguous weight copy, "
-                      f"M={M} N={N} K={Kd})", "bound": "mfma",
-            "achieved": round(achieved, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / BF16_PEAK_TFLOPS, 4), "traffic": None, "launch_us": round(dt * 1e6, 2),
-            "flops_per_launch": flops}
+    R, d, H, Dh, T, b = r.R, r.d, r.H, r.Dh, r.T, r.b
+    L = r.c.n_layers
+    w = r.w[0]
+    fams = []
+
+    def add(name, kernel, fn, flops, per_micro):
+        t = timed_kernel(fn, iters=10)
+        fams.append({"family": name, "kernel": kernel, "launch_us": round(t * 1e6, 2), "launches_per_micro_step":
+                     per_micro, "flops_per_launch": flops, "tflops": round(flops / t / 1e12, 1),
+                     "share_of_micro_step": round(t * per_micro / (ms_per_micro * 1e-3), 4)})
+
+    gu_n = r.gu[0].shape[1]
+    if r.wg_layers is not None:
+        fl = sum(2.0 * R * c.shape[0] * c.shape[1] for _, _, c in r.wg_layers[0].jobs)
+        add("layer weight gradients (fc2, gate|up, out, qkv: one grouped split-K launch)",
+            "gemm_wgrad_kernel (csrc/gemm_wgrad.hip)", lambda: r.wg_layers[0](beta=1.0), fl, L)
+        fl = sum(2.0 * R * c.shape[0] * c.shape[1] for _, _, c in r.wg_head.jobs)
+        add("lm_head weight gradient", "gemm_wgrad_kernel (csrc/gemm_wgrad.hip)", lambda: r.wg_head(beta=1.0), fl, 1)
+    nt = "gemm_stream_kernel / gemm_big_kernel (pcv_gemm_bf16 dispatch)"
+    if not r.c.tie_embeddings:
+        add("lm_head forward (logits)", nt, lambda: K.gemm(r.yf, r.WhT, r.logits, tb=True),
+            2.0 * R * r.V * d, 1)
+        add("lm_head data gradient", nt, lambda: K.gemm(r.logits, r.Wh, r.dy, tb=True), 2.0 * R * r.V * d, 1)
+    fl_fwd = 2.0 * R * d * (3 * d + d + gu_n + r.F)
+    add("layer forward products (qkv, out + residual, gate|up, fc2 + residual)", nt,
+        lambda: (K.gemm(r.y0[0], w["WqkvT"], r.qkv[0], tb=True), K.gemm(r.o[0], w["WoT"], r.x1[0], tb=True, res=r.x[0]),
+                 K.gemm(r.y1[0], w["WguT"], r.gu[0], tb=True),
+                 K.gemm(r.hm[0], w["W2T"], r.x[1], tb=True, res=r.x1[0])), fl_fwd, L)
+    dgu = r.dgu if r.glu else r.dgu[:, : r.F]
+    add("layer data-gradient products (fc2, gate|up, qkv; out with the attention delta)", nt,
+        lambda: (K.gemm(r.dx, w["W2"], r.dh, tb=True), K.gemm(dgu, w["Wgu"], r.dy, tb=True),
+                 K.gemm(r.dx, w["Wo"], r.do, tb=True, attn_delta=(r.o[0], r.delta, T, H)),
+                 K.gemm(r.dqkv, w["Wqkv"], r.dy, tb=True)), fl_fwd, L)
+    pairs = b * H * T * (T + 1) / 2.0
+    add("causal attention forward", "attn_fwd_kernel (csrc/attention.hip)",
+        lambda: K.attn_fwd(r.qkv[0], r.o[0], r.lse[0], b, T, H, Dh, causal=True), 2 * 2.0 * pairs * Dh, L)
+    add("causal attention backward (dK/dV + dQ kernels)", "attn_bwd_dkdv_kernel + attn_bwd_dq_kernel",
+        lambda: K.attn_bwd(r.qkv[0], r.o[0], r.do, r.lse[0], r.delta, r.dqkv, b, T, H, Dh, causal=True,
+                           delta_ready=True), 4 * 2.0 * pairs * Dh, L)
+    fams.sort(key=lambda f: -f["share_of_micro_step"])
+    top = fams[0]
+    achieved = top["tflops"]
+    return {"kernel": f"{top['kernel']}: {top['family']}", "bound": "mfma", "achieved": achieved,
+            "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
+            "traffic": None, "launch_us": top["launch_us"], "flops_per_launch": top["flops_per_launch"],
+            "share_of_micro_step": top["share_of_micro_step"], "families": fams}
 
 
 def bench_dp_stub(args):

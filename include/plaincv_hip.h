@@ -403,15 +403,6 @@ int pcv_gemm_f32_rows_lnout(const float* A, int64_t lda, const float* B, int64_t
                             int64_t ws_floats, void* stream);
 /* floats of pcv_gemm_f32_rows_lnout's split-tail workspace at (M, K) (0: none; zeroed, one launch at a time) */
 int64_t pcv_gemm_f32_rows_lnout_ws_floats(int64_t M, int64_t K);
-/* The LM's plain vocabulary GEMMs (lm_head / tied embedding, models/LM/transformer.py:393-405, and the
- * data-gradient of the same product) through hipBLASLt: C[M][N] = alpha op(a) op(b) + beta C with pcv_gemm_bf16's
- * row-major conventions (a [M][K] or, ta, [K][M]; b [K][N] or, tb, [N][K]), bf16 operands, C bf16 or (out_f32)
- * fp32; ws: device workspace of ws_bytes.  One plan (descriptors + the heuristic's algorithm) per shape, built
- * on first use.  0 ok, <0 invalid argument, 1000 + hipblasStatus_t on a library error. */
-int pcv_blaslt_available(void);
-int pcv_blaslt_gemm_bf16(int ta, int tb, int64_t M, int64_t N, int64_t K, const void* a, int64_t lda, const void* b,
-                         int64_t ldb, void* c, int64_t ldc, int out_f32, float alpha, float beta, void* ws,
-                         int64_t ws_bytes, void* stream);
 /* pcv_gemm_f32_rows with a workspace for the split tail of its tiled form (data-gradient products, no
  * epilogue: the few tiles past a whole number of 4-per-CU rounds run as K slices beside the first round, the
  * tile's last slice adding the slabs in order); pcv_gemm_f32_rows_ws_floats gives the floats needed (0: no

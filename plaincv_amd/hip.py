@@ -104,8 +104,6 @@ SIGNATURES = {
     "pcv_gemm_f32_rows_lnout": [P, I64, P, I64, P, I64, I64, I64, I64, P, P, I64, F32, F32, P, U32, P, P, P, I64, P, P,
                                 F32, P, I64, P],
     "pcv_gemm_f32_rows_lnout_ws_floats": [I64, I64],
-    "pcv_blaslt_available": [],
-    "pcv_blaslt_gemm_bf16": [I32, I32, I64, I64, I64, P, I64, P, I64, P, I64, I32, F32, F32, P, I64, P],
     "pcv_gemm_f32_rows_ws_floats": [I64, I64, I64, I32, I32],
     "pcv_gemm_f32_rows_ws": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32, P, I64,
                              P],

@@ -25,20 +25,8 @@ def _ld(t):
     return t.stride(-2)
 
 
-_BLASLT_WS = {}
-
-
-def _blaslt_ws(dev, nbytes=64 << 20):
-    """the hipBLASLt workspace of a device (allocated on first use, outside any capture)"""
-    w = _BLASLT_WS.get(dev)
-    if w is None:
-        w = _BLASLT_WS[dev] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    return w
-
-
 def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=None, res_scale=1.0, aux=None,
-         act=EPI_NONE, drop_rate=0.0, seed=None, site=0, split_k=None, colsum=None, col_reps=1, attn_delta=None,
-         library=False):
+         act=EPI_NONE, drop_rate=0.0, seed=None, site=0, split_k=None, colsum=None, col_reps=1, attn_delta=None):
     """out[M,N] = epi(alpha * op(a) @ op(b)).
 
     a: [M,K] (ta=False) or [K,M] (ta=True); b: [K,N] (tb=False) or [N,K] (tb=True).
@@ -48,8 +36,7 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
     of the stored values (not with split-K or batches); col_reps > 1: colsum is [col_reps, N] and
     workgroup b adds into row b % col_reps (the caller folds the rows).  attn_delta=(o, delta, T, H[, o_lo]):
     with bf16 out = dO, also delta[(b H + h) T + t] = <out[b T + t, head h], o[b T + t, head h]> (o + o_lo
-    when the short attention's O residual is given).  library=True: a plain product (no epilogue, no batch)
-    through hipBLASLt (pcv_blaslt_gemm_bf16) -- the LM's vocabulary GEMMs."""
+    when the short attention's O residual is given)."""
     batched = a.dim() == 3
     if batched:
         nb = a.shape[0]
@@ -111,13 +98,6 @@ def gemm(a, b, out, *, ta=False, tb=False, alpha=1.0, beta=0.0, bias=None, res=N
              "gemm attn_delta o_lo")
         dl_ld = _ld(dl_o)
         split_k = 1
-    if library:
-        _chk(not batched and bias is None and res is None and act == EPI_NONE and drop_rate == 0.0 and
-             colsum is None and attn_delta is None, "library gemm: plain products only")
-        ws = _blaslt_ws(out.device)
-        hip.call("pcv_blaslt_gemm_bf16", int(ta), int(tb), M, N, K, ptr(a2), _ld(a2), ptr(b2), _ld(b2), ptr(o2),
-                 _ld(o2), out_f32, float(alpha), float(beta), ptr(ws), ws.numel(), stream_ptr())
-        return out
     if split_k is None:
         split_k = 1
         plain = out_f32 and beta == 1.0 and bias is None and res is None and act == EPI_NONE and drop_rate == 0.0

@@ -162,10 +162,6 @@ class LMRunner:
         self.yf = e(R, d)
         self.rf = e(R, dt=f32)
         self.logits = e(R, self.Vp)[:, : self.V]
-        # the vocabulary products (logits and their data gradient: plain GEMMs, no epilogue) through
-        # hipBLASLt (csrc/blaslt.hip: 1138 vs 1584 us for the 124M logits, profiles/r04_lmhead_vs_hipblaslt.txt);
-        # the weight gradient stays on the hand-written kernel (on par with the library, fp32 accumulate)
-        self.vocab_lib = bool(hip.load().pcv_blaslt_available())
         self.row_loss = e(R, dt=f32)
         self.row_correct = e(R, dt=f32)
         self.metrics = torch.zeros(2, dtype=f32, device=dev)
@@ -312,9 +308,9 @@ class LMRunner:
             K.gemm(self.hm[i], w["W2T"], self.x[i + 1], tb=True, res=self.x1[i])
         K.rmsnorm_fwd(self.x[-1], self.sf, self.yf, self.rf, eps)
         if c.tie_embeddings:
-            K.gemm(self.yf, self.Wemb, self.logits, tb=True, library=self.vocab_lib)
+            K.gemm(self.yf, self.Wemb, self.logits, tb=True)
         else:
-            K.gemm(self.yf, self.WhT, self.logits, tb=True, library=self.vocab_lib)
+            K.gemm(self.yf, self.WhT, self.logits, tb=True)
         K.xent(self.logits, self.labels, self.row_loss, self.row_correct,
                self.logits if need_grad else None, grad_scale=self.grad_scale)
         K.mean2(self.row_loss, self.row_correct, self.R, 1.0 / self.R, self.metrics)
@@ -335,9 +331,9 @@ class LMRunner:
         else:
             K.gemm(self.yf, dl, self.gWh, ta=True, beta=1.0)
         if c.tie_embeddings:
-            K.gemm(dl, self.Wemb, self.dy, tb=False, library=self.vocab_lib)
+            K.gemm(dl, self.Wemb, self.dy, tb=False)
         else:
-            K.gemm(dl, self.Wh, self.dy, tb=True, library=self.vocab_lib)
+            K.gemm(dl, self.Wh, self.dy, tb=True)
         K.rmsnorm_bwd(self.dy, self.x[-1], self.sf, self.rf, None, self.dxb[0], self.gsf)
         if on_ready is not None:
             on_ready(self._ready_off["head"])
