@@ -389,8 +389,11 @@ extern "C" int pcv_gemm_stream_ok(int64_t M, int64_t N, int64_t K, const void* A
   const int ncu = pcv_cu_count();
   const int bn = stream_bn(M, N, ncu);
   if ((K & 31) && bn != 192) return 0;   // ragged K only in the 256 x 192 form
+  // only where each CU runs many tiles (the vocabulary-wide lm_head: ~49 per CU): there the ring that
+  // spans tiles pays (124M logits 1470 vs 1607 us for gemm_big); at one to six tiles per CU gemm_big's
+  // loop measured 0-15 % faster (tools/gemm_lab.py)
   const int64_t tiles = ((M + ST_T - 1) / ST_T) * ((N + bn - 1) / bn);
-  return tiles * 2 >= ncu ? 1 : 0;
+  return tiles >= 8 * (int64_t)ncu ? 1 : 0;
 }
 
 template <int BN, bool RES, bool RK>

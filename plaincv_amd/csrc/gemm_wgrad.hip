@@ -24,6 +24,7 @@
 namespace pcv {
 
 constexpr int WG_MAXJ = 8;
+constexpr int64_t WG_TICKET_BYTES = 64 * 1024;   // tile tickets at the workspace front (<= 16384 tiles)
 struct WgJob {
   const bf16* A; const bf16* B; float* C;
   int64_t lda, ldb, ldc;
@@ -315,9 +316,11 @@ static bool wgrad_plan(int njobs, const void* const* A, const void* const* B, fl
     f0 += p.job[i].tiles_m * p.job[i].tiles_n * S;
   }
   p.njobs = njobs; p.S = S; p.nflat = f0;
-  // [tile tickets, padded to 256 B][slabs]: the tickets sit at the front so that workspaces shared by
-  // different groups never put one group's slabs over another's (zero) tickets
-  ws_bytes = S > 1 ? (tiles * 4 + 255) / 256 * 256 + (int64_t)tiles * S * WT * WT * 4 : 0;
+  // [tile tickets: a FIXED WG_TICKET_BYTES region][slabs]: every group puts its slabs past the same
+  // ticket region, so groups sharing one workspace never write slabs over another group's (zero)
+  // tickets (a per-group region sized by its own tile count did exactly that)
+  if (tiles > WG_TICKET_BYTES / 4) return false;
+  ws_bytes = S > 1 ? WG_TICKET_BYTES + (int64_t)tiles * S * WT * WT * 4 : 0;
   return true;
 }
 
@@ -345,7 +348,7 @@ extern "C" int pcv_gemm_wgrad_grouped(int njobs, const void* const* A, const voi
   int64_t tiles = 0;
   for (int i = 0; i < njobs; ++i) tiles += (int64_t)p.job[i].tiles_m * p.job[i].tiles_n;
   p.tickets = need > 0 ? (int*)ws : nullptr;
-  p.slabs = need > 0 ? (float*)((char*)ws + (tiles * 4 + 255) / 256 * 256) : nullptr;
+  p.slabs = need > 0 ? (float*)((char*)ws + WG_TICKET_BYTES) : nullptr;
   static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
   if (const int e = optin.ensure((const void*)gemm_wgrad_kernel, WT_LDS)) return e;
   hipLaunchKernelGGL(gemm_wgrad_kernel, dim3(p.nflat), dim3(512), WT_LDS, (hipStream_t)stream, p);

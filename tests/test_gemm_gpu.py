@@ -153,13 +153,14 @@ def test_gemm_big_kernel(dev, M, N, K, res):
 @pytest.mark.parametrize("M,N,K,res", [(16384, 50257, 768, False), (16384, 768, 50257, False), (8192, 4096, 1024, True),
                                        (16384, 2304, 128, False), (6000, 5472, 2736, True), (4100, 8200, 200, False),
                                        (16384, 768, 2304, True), (16384, 768, 4100, False), (16384, 1024, 1024, True),
-                                       (16384, 2048, 768, False), (8000, 1000, 136, True), (16384, 5472, 1024, False)])
+                                       (16384, 2048, 768, False), (8000, 1000, 136, True), (16384, 5472, 1024, False),
+                                       (16384, 50280, 1024, False), (20000, 30000, 256, True)])
 def test_gemm_stream_kernel(dev, M, N, K, res):
-    """Persistent continuous-ring kernel (gemm_stream.hip) through pcv_gemm_bf16's dispatch: many tiles per
-    workgroup (the lm_head: 49-50 per CU), one tile per workgroup (N = 768, 256 x 192), ragged M / N (masked
-    tiles), ragged K (the masked last ring step: K % 32 = 17, 8, 4, 16), the residual epilogue and padded row
-    strides.  Against an fp32 product of the same bf16 operands, against gemm_big and the 128x128 family on
-    the same call, and bitwise run-to-run."""
+    """Persistent continuous-ring kernel (gemm_stream.hip), called through its own entry point: many tiles
+    per workgroup (the lm_head: 49-50 per CU, the shapes pcv_gemm_bf16 dispatches to it), one tile per
+    workgroup (N = 768, 256 x 192), ragged M / N (masked tiles), ragged K (the masked last ring step: K % 32 =
+    17, 8, 4, 16), the residual epilogue and padded row strides.  Against an fp32 product of the same bf16
+    operands, against gemm_big and the 128x128 family on the same product, and bitwise run-to-run."""
     from plaincv_amd import hip
     from plaincv_amd import kernels as k
     lib = hip.load()
@@ -167,13 +168,18 @@ def test_gemm_stream_kernel(dev, M, N, K, res):
     a = _padded(M, K, dev, g)
     b = _padded(N, K, dev, g)
     r = _padded(M, N, dev, g) if res else None
-    assert lib.pcv_gemm_stream_ok(M, N, K, hip.ptr(a), a.stride(0), hip.ptr(b), b.stride(0)) == 1
+    dispatched = lib.pcv_gemm_stream_ok(M, N, K, hip.ptr(a), a.stride(0), hip.ptr(b), b.stride(0)) == 1
+    print(f"GEMMSTREAM M={M} N={N} K={K}: pcv_gemm_bf16 dispatches it: {dispatched}")
 
     def run(stream_on, big_on):
         ps, pb = lib.pcv_gemm_stream_enable(stream_on), lib.pcv_gemm_big_enable(big_on)
         try:
             out = torch.full((M, (N + 7) // 8 * 8), 7.0, device=dev, dtype=torch.bfloat16)
-            k.gemm(a, b, out[:, :N], tb=True, alpha=0.5, res=r)
+            if stream_on:   # the kernel itself, whatever pcv_gemm_bf16's dispatch rule picks
+                hip.call("pcv_gemm_stream", hip.ptr(a), hip.ptr(b), hip.ptr(out), M, N, K, a.stride(0), b.stride(0),
+                         out.stride(0), 0.5, hip.ptr(r), r.stride(0) if r is not None else 0, 1.0, hip.stream_ptr())
+            else:
+                k.gemm(a, b, out[:, :N], tb=True, alpha=0.5, res=r)
             torch.cuda.synchronize()
         finally:
             lib.pcv_gemm_stream_enable(ps)
@@ -191,7 +197,7 @@ def test_gemm_stream_kernel(dev, M, N, K, res):
     print(f"GEMMSTREAM M={M} N={N} K={K} res={res} max|err| {err:.3g} tol {tol:.3g}")
     assert err <= tol
     del ref
-    for other in ((0, 1), (0, 0)):
+    for other in ((0, 1), (0, 0)):   # pcv_gemm_bf16 with the stream path off: gemm_big, then the 128 x 128 family
         if other == (0, 1) and not lib.pcv_gemm_big_ok(M, N, K, hip.ptr(a), a.stride(0), hip.ptr(b), b.stride(0)):
             continue
         o = run(*other)
@@ -239,3 +245,26 @@ def test_gemm_wgrad_grouped(dev, case):
         tol = 2e-5 * (a.float().abs().t() @ b.float().abs()).max().item() + 1e-5
         print(f"WGRAD {case} M={a.shape[1]} N={b.shape[1]} K={a.shape[0]} splits={splits} max|err| {err:.3g} tol {tol:.3g}")
         assert err <= tol
+
+
+def test_gemm_wgrad_groups_share_workspace(dev):
+    """Groups of different tile counts built on ONE shared workspace (the LM builds the 4-matrix layer groups
+    and the lm_head group on the device's workspace) and launched interleaved: each group's slabs must
+    never overwrite another group's tile tickets (a per-group ticket region sized by its own tile count
+    did, and the lm_head weight gradient came out 0.6 off)."""
+    from plaincv_amd import kernels as k
+    g = torch.Generator(device=dev).manual_seed(5)
+    Kr = 2048
+    big = [(_padded(Kr, 768, dev, g), _padded(Kr, 20000, dev, g), torch.zeros(768, 20000, device=dev))]
+    small = [(_padded(Kr, 512, dev, g), _padded(Kr, 512, dev, g), torch.zeros(512, 512, device=dev)),
+             (_padded(Kr, 256, dev, g), _padded(Kr, 768, dev, g), torch.zeros(256, 768, device=dev))]
+    gb, gs = k.WGradGroup(big, dev), k.WGradGroup(small, dev, splits=4)
+    assert gb.ws.data_ptr() == gs.ws.data_ptr() and gb.ws_bytes > 0 and gs.ws_bytes > 0
+    for _ in range(3):
+        gs(beta=1.0)
+        gb(beta=1.0)
+    torch.cuda.synchronize()
+    for a, b, c in big + small:
+        ref = 3.0 * (a.float().t() @ b.float())
+        err = (c - ref).abs().max().item()
+        assert err <= 1e-4 * ref.abs().max().item(), err
