@@ -14,5 +14,5 @@ case "$WL" in lm*) LMARGS="--lm-steps $STEPS --lm-warmup $WARM";; esac
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$O/prof_$WL" -o p -- python3 "$R/bench.py" --workload "$WL" \
   --steps "$STEPS" --warmup "$WARM" --no-sub --no-roofline --no-cpu-baseline > "$O/prof_$WL.log" 2>&1 || { tail -20 "$O/prof_$WL.log"; exit 1; }
 DB=$(find "$O/prof_$WL" -name "*.db" | head -1)
-python3 "$R/profiles/summarize_rocpd.py" "$DB" "$STEPS" > "$O/${WL}_kernel_stats.txt"
+python3 "$R/profiles/summarize_rocpd.py" "$DB" "$((STEPS + WARM))" > "$O/${WL}_kernel_stats.txt"
 head -25 "$O/${WL}_kernel_stats.txt"
