@@ -5,9 +5,12 @@ gradients C[M,N] += A[K,M]^T B[K,N] (fp32): the dispatched hand path and hipBLAS
 
     python tools/gemm_lab.py [nt|wgrad|all] [--quick]
 """
+import os
 import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from plaincv_amd import hip
 from plaincv_amd import kernels as K

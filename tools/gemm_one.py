@@ -2,9 +2,12 @@
     python tools/gemm_one.py KIND M N K [reps]
 KIND: stream | big | 128 (forward / data-gradient product C = A B^T, both K-contiguous), or
 wgrad (the grouped split-K weight gradient C += A^T B, A [K, M], B [K, N])."""
+import os
 import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from plaincv_amd import hip
 from plaincv_amd import kernels as K
