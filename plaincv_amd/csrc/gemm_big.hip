@@ -29,6 +29,7 @@
 //   * the bf16 tile is staged through LDS and stored as 16-byte rows (+ residual).
 #include "common.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace pcv {
 
@@ -77,7 +78,9 @@ template <int BN>
 __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
   using C = GbCfg<BN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // the wave index through readfirstlane: wave-uniform for the compiler, so the per-group loop below
+  // is chosen by one scalar branch (as a VGPR value every group test was an exec-masked branch)
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int wr = wave >> 2, wc = wave & 3;
 
   // XCD-aware bijective remap, then 8-row groups along M (as gemm.hip)
@@ -92,48 +95,55 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
 
   // DMA sources: A pieces (16 per step) two per wave; B pieces (BN/16 per step) two per wave, or for
   // BN = 192 two for waves 0-3 and one for waves 4-7.  Piece p = image rows 16p .. 16p+15;
-  // lane -> row (lane >> 2), stored chunk (lane & 3) <- source k-chunk (lane & 3) ^ 2*((row >> 3) & 1)
+  // lane -> row (lane >> 2), stored chunk (lane & 3) <- source k-chunk (lane & 3) ^ 2*((row >> 3) & 1).
+  // Sources = a wave-uniform panel base advancing 64 B per step (SGPRs) + a per-lane 32-bit byte
+  // offset (the saddr form of global_load_lds: no 64-bit VALU address arithmetic per step)
   constexpr bool B3 = C::BPIECES == 12;
   const int nbp = (!B3 || wave < 4) ? 2 : 1;
-  const bool three = nbp == 1;   // this wave's loads per step: 2 A + nbp B
   int bpiece[2];
   if (!B3) { bpiece[0] = wave * 2; bpiece[1] = wave * 2 + 1; }
   else { bpiece[0] = wave < 4 ? wave * 2 : 8 + (wave - 4); bpiece[1] = wave < 4 ? wave * 2 + 1 : bpiece[0]; }
-  const bf16* srcA[2];
-  const bf16* srcB[2];
+  uint32_t offSA[2], offSB[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = (wave * 2 + i) * 16 + (lane >> 2);
     const int kc = (lane & 3) ^ (((row >> 3) & 1) << 1);
-    const int ra = min(m0 + row, g.M - 1);   // clamped rows feed only masked outputs
-    srcA[i] = g.A + (int64_t)ra * g.lda + kc * 8;
+    const int ra = min(m0 + row, g.M - 1) - m0;   // clamped rows feed only masked outputs
+    offSA[i] = (uint32_t)(((int64_t)ra * g.lda + kc * 8) * 2);
     const int rowb = bpiece[i] * 16 + (lane >> 2);
     const int kcb = (lane & 3) ^ (((rowb >> 3) & 1) << 1);
-    const int rb = min(n0 + rowb, g.N - 1);
-    srcB[i] = g.B + (int64_t)rb * g.ldb + kcb * 8;
+    const int rb = min(n0 + rowb, g.N - 1) - n0;
+    offSB[i] = (uint32_t)(((int64_t)rb * g.ldb + kcb * 8) * 2);
   }
+  const char* panelA = reinterpret_cast<const char*>(g.A + (int64_t)m0 * g.lda);
+  const char* panelB = reinterpret_cast<const char*>(g.B + (int64_t)n0 * g.ldb);
   const int nsteps = g.K / 32;
   auto issue = [&](int s) {
     char* slot = smem + (s & 3) * C::SLOT;
+    const char* pa = panelA + s * 64;
+    const char* pb = panelB + s * 64;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(srcA[i] + s * 32), (gb_lds_void*)(slot + (wave * 2 + i) * 1024),
+      __builtin_amdgcn_global_load_lds((const void*)(pa + offSA[i]), (gb_lds_void*)(slot + (wave * 2 + i) * 1024),
                                        16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(srcB[0] + s * 32),
-                                     (gb_lds_void*)(slot + GB_IMG + bpiece[0] * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(pb + offSB[0]), (gb_lds_void*)(slot + GB_IMG + bpiece[0] * 1024),
+                                     16, 0, 0);
     if (nbp == 2)
-      __builtin_amdgcn_global_load_lds((const void*)(srcB[1] + s * 32),
+      __builtin_amdgcn_global_load_lds((const void*)(pb + offSB[1]),
                                        (gb_lds_void*)(slot + GB_IMG + bpiece[1] * 1024), 16, 0, 0);
   };
 
-  // fragment offsets within an image (the swizzle depends only on lane & 15)
+  // fragment offsets: one per-lane base per operand, rows i*16 / j*16 as immediate ds_read offsets
+  // (the swizzle depends only on lane & 15)
   const int fsw = (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) << 4);
   constexpr int NJ = C::NJ;
+  const int offA0 = (wr * 128 + (lane & 15)) * 64 + fsw;
+  const int offB0 = GB_IMG + (wc * C::WN + (lane & 15)) * 64 + fsw;
   int offA[8], offB[NJ];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) offA[i] = (wr * 128 + i * 16 + (lane & 15)) * 64 + fsw;
+  for (int i = 0; i < 8; ++i) offA[i] = offA0 + i * 1024;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) offB[j] = GB_IMG + (wc * C::WN + j * 16 + (lane & 15)) * 64 + fsw;
+  for (int j = 0; j < NJ; ++j) offB[j] = offB0 + j * 1024;
 
   f32x4 acc[8][NJ];
 #pragma unroll
@@ -148,13 +158,18 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
       for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
   };
 
-  if (nsteps > 0) {
-    for (int s = 0; s < 3 && s < nsteps; ++s) issue(s);
-    gb_wait_next(min(2, nsteps - 1), three);   // step 0 retired (loads of steps 1, 2 may fly)
-    gb_barrier();
-    if (wr == 1) gb_barrier();          // stagger: group 1 runs one barrier behind
-    for (int s = 0; s < nsteps; ++s) {
-      if (s + 3 < nsteps) issue(s + 3);
+  // The main loop, specialised per wave group (GRP = wr) with compile-time wait counts: steps
+  // s < nsteps - 3 issue step s+3 and retire step s+1 with vmcnt(2L) (L = the group's loads per step:
+  // 4, or 3 for BN = 192's waves 4-7); the last three steps issue nothing and wait vmcnt(L), vmcnt(0),
+  // nothing.  (As runtime values the counts, the issue test and the group tests cost ~40 SALU and
+  // exec-mask branches per step: 39 SALU / 44 VALU per 24 MFMAs measured by PMC, profiles/r06j_*.)
+  auto main_loop = [&](auto grp_t) {
+    constexpr int GRP = decltype(grp_t)::value;
+    constexpr int L = (B3 && GRP == 1) ? 3 : 4;
+    auto step = [&](int s, auto issue_t, auto wait_t) {
+      constexpr bool ISS = decltype(issue_t)::value;
+      constexpr int WN = decltype(wait_t)::value;   // vmcnt count retiring step s+1, or -1: none
+      if constexpr (ISS) issue(s + 3);
       const char* slot = smem + (s & 3) * C::SLOT;
       bf16x8 a[8], b[NJ];
 #pragma unroll
@@ -163,18 +178,30 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
       for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(slot + offA[i]);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      const int after = min(nsteps - 1, s + 3) - (s + 1);   // steps issued after step s+1
-      if (wr == 1 && s + 1 < nsteps) gb_wait_next(after, three);
+      if constexpr (GRP == 1 && WN >= 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WN) : "memory");
       gb_barrier();
       __builtin_amdgcn_s_setprio(1);
       mfmas(a, b);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
-      if (wr == 0 && s + 1 < nsteps) gb_wait_next(after, three);
+      if constexpr (GRP == 0 && WN >= 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WN) : "memory");
       gb_barrier();
-    }
-    if (wr == 0) gb_barrier();          // equal barrier counts for both groups
-  }
+    };
+    using yes = std::true_type;
+    using no = std::false_type;
+    for (int s = 0; s < 3; ++s) issue(s);   // nsteps >= 4 (big_shape_ok: K >= 128)
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * L) : "memory");   // step 0 retired (1, 2 may fly)
+    gb_barrier();
+    if constexpr (GRP == 1) gb_barrier();   // stagger: group 1 runs one barrier behind
+    int s = 0;
+    for (; s + 3 < nsteps; ++s) step(s, yes{}, std::integral_constant<int, 2 * L>{});
+    step(s, no{}, std::integral_constant<int, L>{});
+    step(s + 1, no{}, std::integral_constant<int, 0>{});
+    step(s + 2, no{}, std::integral_constant<int, -1>{});
+    if constexpr (GRP == 0) gb_barrier();   // equal barrier counts for both groups
+  };
+  if (wr == 0) main_loop(std::integral_constant<int, 0>{});
+  else main_loop(std::integral_constant<int, 1>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 

@@ -20,6 +20,7 @@
 // the ticket for the next launch.  The result does not depend on arrival order or placement.  With
 // S = 1 the workgroup owns its tile and writes C directly.
 #include "common.h"
+#include <type_traits>
 
 namespace pcv {
 
@@ -150,12 +151,9 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_kernel(WgPlan P) {
     // (kr1 = kr0 + 4 has the same swizzle block: (k & 3) and (k >> 3) & 1 agree, so +2048 B)
     const uint32_t lds0 = (uint32_t)(uintptr_t)(wt_lds_char*)smem;
 
-    for (int st = 0; st < 3 && st < nsteps; ++st) issue(st);
-    wt_wait_n<4>(min(2, nsteps - 1));
-    wt_barrier();
-    if (wr == 1) wt_barrier();
-    for (int st = 0; st < nsteps; ++st) {
-      if (st + 3 < nsteps) issue(st + 3);
+    auto step = [&](int st, bool iss, int grp, auto wait_t, bool runtime_wait, int after) {
+      constexpr int WN = decltype(wait_t)::value;   // vmcnt count retiring step st+1, or -1: none
+      if (iss) issue(st + 3);
       const uint32_t sb = lds0 + (uint32_t)((st & 3) * WT_SLOT);
       bf16x4 lo[12], hi[12];
 #pragma unroll
@@ -169,8 +167,10 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_kernel(WgPlan P) {
       for (int i = 0; i < 8; ++i) a[i] = __builtin_shufflevector(lo[i], hi[i], 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) b[jj] = __builtin_shufflevector(lo[8 + jj], hi[8 + jj], 0, 1, 2, 3, 4, 5, 6, 7);
-      const int after = min(nsteps - 1, st + 3) - (st + 1);
-      if (wr == 1 && st + 1 < nsteps) wt_wait_n<4>(after);
+      if (grp == 1) {
+        if (runtime_wait) wt_wait_n<4>(after);
+        else if constexpr (WN >= 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WN) : "memory");
+      }
       wt_barrier();
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -180,8 +180,34 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_kernel(WgPlan P) {
           acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[jj], acc[i][jj], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
-      if (wr == 0 && st + 1 < nsteps) wt_wait_n<4>(after);
+      if (grp == 0) {
+        if (runtime_wait) wt_wait_n<4>(after);
+        else if constexpr (WN >= 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WN) : "memory");
+      }
       wt_barrier();
+    };
+    using none_t = std::integral_constant<int, -1>;
+    for (int st = 0; st < 3 && st < nsteps; ++st) issue(st);
+    wt_wait_n<4>(min(2, nsteps - 1));
+    wt_barrier();
+    if (wr == 1) wt_barrier();
+    if (nsteps >= 4) {
+      // steady state with compile-time counts (steps st < nsteps - 3 issue st + 3 and retire st + 1 with
+      // vmcnt(8); then vmcnt(4), vmcnt(0), none), one copy per wave group (wr is wave-uniform): the
+      // runtime form cost ~38 SALU and exec-mask branches per step (PMC, profiles/r06j_*)
+      auto run = [&](auto grp_t) {
+        constexpr int GRP = decltype(grp_t)::value;
+        int st = 0;
+        for (; st + 3 < nsteps; ++st) step(st, true, GRP, std::integral_constant<int, 8>{}, false, 0);
+        step(st, false, GRP, std::integral_constant<int, 4>{}, false, 0);
+        step(st + 1, false, GRP, std::integral_constant<int, 0>{}, false, 0);
+        step(st + 2, false, GRP, none_t{}, false, 0);
+      };
+      if (wr == 0) run(std::integral_constant<int, 0>{});
+      else run(std::integral_constant<int, 1>{});
+    } else {
+      for (int st = 0; st < nsteps; ++st)
+        step(st, st + 3 < nsteps, wr, none_t{}, st + 1 < nsteps, min(nsteps - 1, st + 3) - (st + 1));
     }
     if (wr == 0) wt_barrier();   // equal barrier counts for both groups
   }
