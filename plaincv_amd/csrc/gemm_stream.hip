@@ -335,6 +335,62 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
     if (wr == 0 && gi + 1 < G) st_wait(n);
     st_barrier();
   };
+  if constexpr (!RK) {
+    if (S >= 6) {
+      // Steady form: per wave group (wr is wave-uniform) and with compile-time vmcnt counts -- per tile:
+      // steps 0, 1 of every tile after the first retire step gi+1 past the previous epilogue's 16 stores
+      // (2L + 16), the others 2L; the last tile's last three steps issue nothing (L, 0, none).  S >= 6
+      // keeps those two cases apart.  (The runtime form cost ~70 SALU + ~66 VALU per 32 MFMAs, PMC r06j.)
+      auto run = [&](auto grp_t) {
+        constexpr int GRP = decltype(grp_t)::value;
+        constexpr int LL = (B3 && GRP == 1) ? 3 : 4;
+        auto stp = [&](auto iss_t, auto wait_t) {
+          constexpr bool ISS = decltype(iss_t)::value;
+          constexpr int WN = decltype(wait_t)::value;
+          if constexpr (ISS) issue_next();
+          const char* slot = smem + (gi & 3) * C::SLOT;
+          bf16x8 a[8], b[NJ];
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(slot + offB(j));
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(slot + offA0 + i * 1024);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (GRP == 1 && WN >= 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WN) : "memory");
+          st_barrier();
+          __builtin_amdgcn_s_setprio(1);
+          mfmas(a, b);
+          __builtin_amdgcn_s_setprio(0);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (GRP == 0 && WN >= 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(WN) : "memory");
+          st_barrier();
+          ++gi;
+        };
+        using yes = std::true_type;
+        using no = std::false_type;
+        for (int k = 0; k < nt; ++k) {
+          const int cs_end = k == nt - 1 ? S - 3 : S;
+          int c = 0;
+          if (k > 0) {
+            stp(yes{}, std::integral_constant<int, 2 * LL + 16>{});
+            stp(yes{}, std::integral_constant<int, 2 * LL + 16>{});
+            c = 2;
+          }
+          for (; c < cs_end; ++c) stp(yes{}, std::integral_constant<int, 2 * LL>{});
+          if (k == nt - 1) {
+            stp(no{}, std::integral_constant<int, LL>{});
+            stp(no{}, std::integral_constant<int, 0>{});
+            stp(no{}, std::integral_constant<int, -1>{});
+          }
+          epilogue(k);
+        }
+        if constexpr (GRP == 0) st_barrier();   // equal barrier counts for both groups
+      };
+      if (wr == 0) run(std::integral_constant<int, 0>{});
+      else run(std::integral_constant<int, 1>{});
+      return;
+    }
+  }
   for (; gi < G; ++gi) {
     if constexpr (RK) {
       if (cs == S - 1) step(std::true_type{});
