@@ -118,7 +118,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
   const char* panelA = reinterpret_cast<const char*>(g.A + (int64_t)m0 * g.lda);
   const char* panelB = reinterpret_cast<const char*>(g.B + (int64_t)n0 * g.ldb);
   const int nsteps = g.K / 32;
-  auto issue = [&](int s) {
+  auto issue = [&](int s) __attribute__((always_inline)) {
     char* slot = smem + (s & 3) * C::SLOT;
     const char* pa = panelA + s * 64;
     const char* pb = panelB + s * 64;
@@ -163,10 +163,10 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
   // 4, or 3 for BN = 192's waves 4-7); the last three steps issue nothing and wait vmcnt(L), vmcnt(0),
   // nothing.  (As runtime values the counts, the issue test and the group tests cost ~40 SALU and
   // exec-mask branches per step: 39 SALU / 44 VALU per 24 MFMAs measured by PMC, profiles/r06j_*.)
-  auto main_loop = [&](auto grp_t) {
+  auto main_loop = [&](auto grp_t) __attribute__((always_inline)) {
     constexpr int GRP = decltype(grp_t)::value;
     constexpr int L = (B3 && GRP == 1) ? 3 : 4;
-    auto step = [&](int s, auto issue_t, auto wait_t) {
+    auto step = [&](int s, auto issue_t, auto wait_t) __attribute__((always_inline)) {
       constexpr bool ISS = decltype(issue_t)::value;
       constexpr int WN = decltype(wait_t)::value;   // vmcnt count retiring step s+1, or -1: none
       if constexpr (ISS) issue(s + 3);
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_wgrad_kernel(WgArgs g) {
     srcB[i] = g.B + (int64_t)(kbeg + kr) * g.ldb + cbb;
   }
   const int64_t stepA = 32 * g.lda, stepB = 32 * g.ldb;
-  auto issue = [&](int s) {
+  auto issue = [&](int s) __attribute__((always_inline)) {
     char* slot = smem + (s & 3) * GW_SLOT;
 #pragma unroll
     for (int i = 0; i < 2; ++i)

@@ -123,7 +123,7 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
   // fragment masking into unconditional v_and's on every step (48 VALU per step, -30 % measured)
   const int G = nt * S;
   const int per_group = 8 * g.tiles_n;
-  auto coords = [&](int k, int& m0, int& n0) {
+  auto coords = [&](int k, int& m0, int& n0) __attribute__((always_inline)) {
     const int t = tstart + li + k * P8;
     const int first_m = (t / per_group) * 8;
     const int gsz = min(g.tiles_m - first_m, 8);
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
   const bf16* baseA = g.A;
   const bf16* baseB = g.B;
   int iss_k = 0, iss_s = 0;   // next (tile, step) to issue
-  auto issue_next = [&]() {
+  auto issue_next = [&]() __attribute__((always_inline)) {
     if (iss_s == 0) {
       int m0, n0;
       coords(iss_k, m0, n0);
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
   const int offA0 = (wr * 128 + ml) * 64 + fsw;
   const int offP0 = ST_IMG + (wc * WN + 8 * (ml >> 2) + (ml & 3)) * 64 + fsw;
   const int offU0 = ST_IMG + (wc * WN + 32 * NP + ml) * 64 + fsw;
-  auto offB = [&](int j) { return j < 2 * NP ? offP0 + (32 * (j >> 1) + 4 * (j & 1)) * 64 : offU0; };
+  auto offB = [&](int j) __attribute__((always_inline)) { return j < 2 * NP ? offP0 + (32 * (j >> 1) + 4 * (j & 1)) * 64 : offU0; };
 
   f32x4 acc[8][NJ];
 #pragma unroll
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
   };
 
   // epilogue of compute tile ck: 16 vector-memory ops per lane on interior tiles (see the header)
-  auto epilogue = [&](int ck) {
+  auto epilogue = [&](int ck) __attribute__((always_inline)) {
     int m0, n0;
     coords(ck, m0, n0);
     const int rbase = m0 + wr * 128 + ml;
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
   int gi = 0;
   // one step of the stream; MASKED: the ragged last step of a tile (k >= K zeroed on both operands).
   // The two forms are separate copies of the whole step so the mask cannot leak into the others.
-  auto step = [&](auto masked_t) {
+  auto step = [&](auto masked_t) __attribute__((always_inline)) {
     constexpr bool MASKED = decltype(masked_t)::value;
     if (gi + 3 < G) issue_next();
     const char* slot = smem + (gi & 3) * C::SLOT;
@@ -336,15 +336,15 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
     st_barrier();
   };
   if constexpr (!RK) {
-    if (S >= 6) {
+    {   // (the host requires S >= 6 for K % 32 == 0: stream_shape_ok)
       // Steady form: per wave group (wr is wave-uniform) and with compile-time vmcnt counts -- per tile:
       // steps 0, 1 of every tile after the first retire step gi+1 past the previous epilogue's 16 stores
       // (2L + 16), the others 2L; the last tile's last three steps issue nothing (L, 0, none).  S >= 6
       // keeps those two cases apart.  (The runtime form cost ~70 SALU + ~66 VALU per 32 MFMAs, PMC r06j.)
-      auto run = [&](auto grp_t) {
+      auto run = [&](auto grp_t) __attribute__((always_inline)) {
         constexpr int GRP = decltype(grp_t)::value;
         constexpr int LL = (B3 && GRP == 1) ? 3 : 4;
-        auto stp = [&](auto iss_t, auto wait_t) {
+        auto stp = [&](auto iss_t, auto wait_t) __attribute__((always_inline)) {
           constexpr bool ISS = decltype(iss_t)::value;
           constexpr int WN = decltype(wait_t)::value;
           if constexpr (ISS) issue_next();
@@ -391,6 +391,7 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
       return;
     }
   }
+  if constexpr (RK) {
   for (; gi < G; ++gi) {
     if constexpr (RK) {
       if (cs == S - 1) step(std::true_type{});
@@ -405,6 +406,7 @@ __global__ __launch_bounds__(512, 1) void gemm_stream_kernel(StArgs g) {
     }
   }
   if (wr == 0) st_barrier();    // equal barrier counts for both groups
+  }
 }
 
 }  // namespace pcv
@@ -420,8 +422,8 @@ extern "C" int pcv_gemm_stream_enable(int on) {
 }
 
 static bool stream_shape_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb) {
-  if (M <= 0 || N <= 0 || K < 32 * 4 || M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return false;
-  // rows padded to round_up(K, 8): the ragged last step reads whole 16-B chunks; per-tile panel
+  if (M <= 0 || N <= 0 || K < 32 * 6 || M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return false;
+  // (K >= 192: the steady loop needs six steps per tile) rows padded to round_up(K, 8): the ragged last step reads whole 16-B chunks; per-tile panel
   // offsets (256 rows x ld) fit 32 bits
   const int64_t kp8 = (K + 7) / 8 * 8;
   if (lda < kp8 || ldb < kp8 || 256 * (lda > ldb ? lda : ldb) >= (1ll << 31)) return false;

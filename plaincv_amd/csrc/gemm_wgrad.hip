@@ -128,7 +128,7 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_kernel(WgPlan P) {
       srcB[i] = g.B + (int64_t)(kbeg + kr) * g.ldb + cbb;
     }
     const int64_t stepA = 32 * g.lda, stepB = 32 * g.ldb;
-    auto issue = [&](int st) {
+    auto issue = [&](int st) __attribute__((always_inline)) {
       char* slot = smem + (st & 3) * WT_SLOT;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_kernel(WgPlan P) {
     // (kr1 = kr0 + 4 has the same swizzle block: (k & 3) and (k >> 3) & 1 agree, so +2048 B)
     const uint32_t lds0 = (uint32_t)(uintptr_t)(wt_lds_char*)smem;
 
-    auto step = [&](int st, bool iss, int grp, auto wait_t, bool runtime_wait, int after) {
+    auto step = [&](int st, bool iss, int grp, auto wait_t, bool runtime_wait, int after) __attribute__((always_inline)) {
       constexpr int WN = decltype(wait_t)::value;   // vmcnt count retiring step st+1, or -1: none
       if (iss) issue(st + 3);
       const uint32_t sb = lds0 + (uint32_t)((st & 3) * WT_SLOT);
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_kernel(WgPlan P) {
       // steady state with compile-time counts (steps st < nsteps - 3 issue st + 3 and retire st + 1 with
       // vmcnt(8); then vmcnt(4), vmcnt(0), none), one copy per wave group (wr is wave-uniform): the
       // runtime form cost ~38 SALU and exec-mask branches per step (PMC, profiles/r06j_*)
-      auto run = [&](auto grp_t) {
+      auto run = [&](auto grp_t) __attribute__((always_inline)) {
         constexpr int GRP = decltype(grp_t)::value;
         int st = 0;
         for (; st + 3 < nsteps; ++st) step(st, true, GRP, std::integral_constant<int, 8>{}, false, 0);
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(512, 1) void gemm_wgrad_kernel(WgPlan P) {
   const int gtile = g.tile0 + rt;
   float* myslab = S > 1 ? P.slabs + ((int64_t)gtile * S + s) * (WT * WT) : nullptr;
   const bool vecC = ((g.ldc & 3) == 0) && (((uintptr_t)g.C & 15) == 0);
-  auto store_c = [&](int row, int col, f32x4 v) {   // C = beta C + alpha v on the valid part
+  auto store_c = [&](int row, int col, f32x4 v) __attribute__((always_inline)) {   // C = beta C + alpha v on the valid part
     const int gr = m0 + row, gc = n0 + col;
     if (gr >= g.M || gc >= g.N) return;
     float* dst = g.C + (int64_t)gr * g.ldc + gc;

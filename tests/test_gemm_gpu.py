@@ -151,9 +151,9 @@ def test_gemm_big_kernel(dev, M, N, K, res):
 
 
 @pytest.mark.parametrize("M,N,K,res", [(16384, 50257, 768, False), (16384, 768, 50257, False), (8192, 4096, 1024, True),
-                                       (16384, 2304, 128, False), (6000, 5472, 2736, True), (4100, 8200, 200, False),
+                                       (16384, 2304, 192, False), (6000, 5472, 2736, True), (4100, 8200, 200, False),
                                        (16384, 768, 2304, True), (16384, 768, 4100, False), (16384, 1024, 1024, True),
-                                       (16384, 2048, 768, False), (8000, 1000, 136, True), (16384, 5472, 1024, False),
+                                       (16384, 2048, 768, False), (8000, 1000, 200, True), (16384, 5472, 1024, False),
                                        (16384, 50280, 1024, False), (20000, 30000, 256, True)])
 def test_gemm_stream_kernel(dev, M, N, K, res):
     """Persistent continuous-ring kernel (gemm_stream.hip), called through its own entry point: many tiles
