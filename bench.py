@@ -154,17 +154,15 @@ def timed_kernel(fn, iters=50, rounds=3):
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/r*_pmc_traffic.json, FETCH_SIZE/WRITE_SIZE passes made by tools/gpu_full.sh)."""
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary that lists it
+    (profiles/r*_pmc_traffic.json: FETCH_SIZE / WRITE_SIZE passes of tools/gpu_profile.sh)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    k = d.get("kernels", {}).get(kernel.replace(" ", ""))   # (keys are stored without spaces)
-    if not k:
-        return None, None
-    return k.get("mean_hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+    key = kernel.replace(" ", "")   # (keys are stored without spaces)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")), reverse=True):
+        k = json.load(open(f)).get("kernels", {}).get(key)
+        if k:
+            return k.get("mean_hbm_bytes_per_launch"), os.path.relpath(f, ROOT)
+    return None, None
 
 
 def vit_roofline(state, image_shape):
