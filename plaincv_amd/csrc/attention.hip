@@ -574,6 +574,10 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
                           (!doc || qb * 64 + 63 < wde_lo);
     if (active) {
       f32x4 p[KG][4], ds[KG][4];
+      // the boundary mode picks one straight-line copy of the whole 4-substep score loop, so the
+      // scheduler can start substep t+1's MFMAs under substep t's softmax VALU (a mode branch inside
+      // each substep kept them apart: the waves sat in dependency waits, SQ counters r05)
+      auto scores = [&](auto mode_outer) __attribute__((always_inline)) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         f32x4 sv[KG], dp[KG];
@@ -629,10 +633,12 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
             }
           }
         };
-        if (interior) probs(std::integral_constant<int, 0>{});
-        else if (!doc) probs(std::integral_constant<int, 1>{});
-        else probs(std::integral_constant<int, 2>{});
+        probs(mode_outer);
       }
+      };
+      if (interior) scores(std::integral_constant<int, 0>{});
+      else if (!doc) scores(std::integral_constant<int, 1>{});
+      else scores(std::integral_constant<int, 2>{});
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         bf16x8 pb[KG], sb[KG];
@@ -739,6 +745,7 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
                           (!doc || kb * 64 >= wds_hi);
     if (active) {
       f32x4 ds[QG][4];
+      auto scores = [&](auto mode_outer) __attribute__((always_inline)) {   // (as the dK/dV kernel)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         f32x4 sv[QG], dp[QG];
@@ -801,10 +808,12 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
             }
           }
         };
-        if (interior) probs(std::integral_constant<int, 0>{});
-        else if (!doc) probs(std::integral_constant<int, 1>{});
-        else probs(std::integral_constant<int, 2>{});
+        probs(mode_outer);
       }
+      };
+      if (interior) scores(std::integral_constant<int, 0>{});
+      else if (!doc) scores(std::integral_constant<int, 1>{});
+      else scores(std::integral_constant<int, 2>{});
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         bf16x8 sa[QG];
