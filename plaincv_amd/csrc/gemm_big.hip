@@ -472,17 +472,17 @@ static bool big_shape_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t
 }
 
 static int big_bn(int64_t M, int64_t N) {
-  // N width per tile (one 128-KiB workgroup per CU, 256 CUs): 256 when that grid has >= 512 tiles
-  // or whole rounds of 256; else 192 when N % 192 == 0 gives whole rounds (N = 768: the LM's
-  // d-wide products, 256 tiles instead of 192); 0 = leave it to the 128x128 family
+  // N width per tile (one 128-KiB workgroup per CU, 256 CUs): the width with fewer tile rounds, a
+  // 256-wide round weighted 1 and a 192-wide one 0.78 (its 24 MFMAs per step against 32 read 11 of
+  // 12 fragments): N = 768 (the LM's d-wide products) -> 256 x 192 tiles, one round; the 124M qkv
+  // product (N = 2304) -> 3 rounds of 256 x 192 instead of 2.25 of 256 x 256 (a quarter of the chip
+  // idle in the third).  At least one round of tiles, or the 128x128 family takes it.
   const int64_t tm = (M + GB_T - 1) / GB_T;
-  const int64_t t256 = tm * ((N + 255) / 256);
-  if (t256 >= 512) return 256;
-  if (N % 192 == 0) {
-    const int64_t t192 = tm * (N / 192);
-    if (t192 >= 256 && t192 % 256 == 0) return 192;
-  }
-  if (t256 >= 256 && t256 % 256 == 0) return 256;
+  const int64_t t256 = tm * ((N + 255) / 256), t192 = tm * ((N + 191) / 192);
+  const int64_t r256 = (t256 + 255) / 256, r192 = (t192 + 255) / 256;
+  const bool w192 = N % 192 == 0 && (double)r192 * 0.78 < (double)r256;
+  const int64_t t = w192 ? t192 : t256;
+  if (t >= 512 || (t >= 256 && t % 256 == 0)) return w192 ? 192 : 256;
   return 0;
 }
 

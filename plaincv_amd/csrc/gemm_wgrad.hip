@@ -371,8 +371,6 @@ extern "C" int pcv_gemm_wgrad_grouped(int njobs, const void* const* A, const voi
   if (!wgrad_plan(njobs, A, B, C, dims, splits, pcv_cu_count(), p, need)) return PCV_EINVAL;
   if (need > 0 && (!ws || ws_bytes < need || !pcv_aligned16(ws))) return PCV_EINVAL;
   p.alpha = alpha; p.beta = beta;
-  int64_t tiles = 0;
-  for (int i = 0; i < njobs; ++i) tiles += (int64_t)p.job[i].tiles_m * p.job[i].tiles_n;
   p.tickets = need > 0 ? (int*)ws : nullptr;
   p.slabs = need > 0 ? (float*)((char*)ws + WG_TICKET_BYTES) : nullptr;
   static PcvLdsOptIn optin;  // > 64 KiB of dynamic LDS: opt in once per device
