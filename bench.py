@@ -577,7 +577,7 @@ def lm_roofline(st, ms_per_micro):
     if not r.c.tie_embeddings:
         add("lm_head forward (logits)", nt, lambda: K.gemm(r.yf, r.WhT, r.logits, tb=True),
             2.0 * R * r.V * d, 1)
-        add("lm_head data gradient", nt, lambda: K.gemm(r.logits, r.Wh, r.dy, tb=True), 2.0 * R * r.V * d, 1)
+        add("lm_head data gradient", nt, lambda: K.gemm(r.logits, r.WhK, r.dy, tb=True), 2.0 * R * r.V * d, 1)
     fl_fwd = 2.0 * R * d * (3 * d + d + gu_n + r.F)
     add("layer forward products (qkv, out + residual, gate|up, fc2 + residual)", nt,
         lambda: (K.gemm(r.y0[0], w["WqkvT"], r.qkv[0], tb=True), K.gemm(r.o[0], w["WoT"], r.x1[0], tb=True, res=r.x[0]),

@@ -135,7 +135,6 @@ class LMRunner:
         self.F = c.hidden_dim
         self.Fp = _pad8(self.F)
         self.V = c.vocab_size
-        self.Vp = _pad8(self.V)
         if self.Dh not in (32, 64, 128) or self.d % 8:
             raise ValueError("head_dim must be 32/64/128 and d_model a multiple of 8")
         dev = torch.device(device)
@@ -158,17 +157,24 @@ class LMRunner:
         self.glu = c.mlp == "glu"
         nmlp = 2 * self.Fp if self.glu else self.Fp
         self.gu = [e(R, nmlp) for _ in range(L)]
-        self.hm = [e(R, self.Fp)[:, : self.F] for _ in range(L)]
+        # rows of the K = F operands (hm, and W2T below) start on 128-B lines (420M fc2 forward
+        # 88.3 -> 81.6 us, profiles/r06q_gemm_lab_nt_pad64.txt)
+        Fl = (self.F + 63) // 64 * 64
+        self.hm = [e(R, Fl)[:, : self.F] for _ in range(L)]
         self.yf = e(R, d)
         self.rf = e(R, dt=f32)
-        self.logits = e(R, self.Vp)[:, : self.V]
+        # vocab-axis row stride a multiple of 64 elements: every row starts on a 128-B line, so the
+        # 64-B k-step loads of the vocabulary-wide products never straddle two lines (dgrad 1684 ->
+        # 1124 us at 124M, profiles/r06p_gemm_lab_vocab.txt)
+        self.Vl = (self.V + 63) // 64 * 64
+        self.logits = e(R, self.Vl)[:, : self.V]
         self.row_loss = e(R, dt=f32)
         self.row_correct = e(R, dt=f32)
         self.metrics = torch.zeros(2, dtype=f32, device=dev)
         # backward workspaces
         self.dx = e(R, d)
         self.dy = e(R, d)
-        self.dh = e(R, self.Fp)[:, : self.F]
+        self.dh = e(R, Fl)[:, : self.F]
         self.dgu = e(R, nmlp)
         self.do = e(R, d)
         self.dqkv = e(R, 3 * d)
@@ -241,7 +247,7 @@ class LMRunner:
         transposing LDS path, measured ~25 % slower at these shapes).  Refreshed from the
         bf16 shadow by one batched transpose launch whenever the store's version changes."""
         def t(rows, cols):
-            ld = (cols + 7) // 8 * 8
+            ld = (cols + 63) // 64 * 64   # 128-B aligned rows (see self.hm)
             return torch.zeros(rows, ld, dtype=torch.bfloat16, device=dev)[:, :cols]
         pairs = []
         for w in self.w:
@@ -250,16 +256,21 @@ class LMRunner:
                 dst = t(src.shape[1], src.shape[0])
                 w[k + "T"] = dst
                 pairs.append((src, dst))
-        self.WhT = None
+        self.WhT = self.WhK = None
         if not self.c.tie_embeddings:
             self.WhT = t(self.Wh.shape[1], self.Wh.shape[0])
             pairs.append((self.Wh, self.WhT))
+            # the data-gradient operand W [d][V] (K = V contiguous) with a 128-B aligned row stride
+            d, V = self.Wh.shape
+            self.WhK = torch.zeros(d, (V + 63) // 64 * 64, dtype=torch.bfloat16, device=dev)[:, :V]
         self._tr = K.TransposeBatch(pairs, dev)
         self._wt_version = -1
 
     def _refresh_weights(self):
         if self._wt_version != self.s.version:
             self._tr()
+            if self.WhK is not None:
+                self.WhK.copy_(self.Wh)
             self._wt_version = self.s.version
 
     def set_batch(self, input_ids, doc=None):
@@ -333,7 +344,7 @@ class LMRunner:
         if c.tie_embeddings:
             K.gemm(dl, self.Wemb, self.dy, tb=False)
         else:
-            K.gemm(dl, self.Wh, self.dy, tb=True)
+            K.gemm(dl, self.WhK, self.dy, tb=True)
         K.rmsnorm_bwd(self.dy, self.x[-1], self.sf, self.rf, None, self.dxb[0], self.gsf)
         if on_ready is not None:
             on_ready(self._ready_off["head"])

@@ -3,7 +3,7 @@ HIP events, random operands.  Forward / data-gradient products C[M,N] = A[M,K] .
 K-contiguous): persistent continuous-ring kernel (gemm_stream.hip), gemm_big.hip, hipBLASLt; weight
 gradients C[M,N] += A[K,M]^T B[K,N] (fp32): the dispatched hand path and hipBLASLt (bf16 out).
 
-    python tools/gemm_lab.py [nt|wgrad|all] [--quick]
+    python tools/gemm_lab.py [nt|wgrad|grouped|vocab|all] [--quick]
 """
 import os
 import sys
@@ -40,8 +40,8 @@ def tm(fn, iters=10, reps=3):
     return best
 
 
-def padded(r, c):
-    ld = (c + 7) // 8 * 8
+def padded(r, c, to=8):
+    ld = (c + to - 1) // to * to
     return (torch.rand(r, ld, device=dev) * 2 - 1).to(torch.bfloat16)[:, :c]
 
 
@@ -62,9 +62,9 @@ WG = [("124M lm_head wgrad", 768, 50257, 16384), ("124M qkv wgrad", 768, 2304, 1
       ("420M fc2 wgrad", 2736, 1024, 16384)]
 
 
-def nt(quick):
+def nt(quick, pad=8):
     for name, M, N, Kd, res in (NT[:4] if quick else NT):
-        a, b = padded(M, Kd), padded(N, Kd)
+        a, b = padded(M, Kd, pad), padded(N, Kd, pad)
         r = padded(M, N) if res else None
         out = torch.empty(M, (N + 7) // 8 * 8, device=dev, dtype=torch.bfloat16)[:, :N]
         fl = 2.0 * M * N * Kd
@@ -122,11 +122,36 @@ def wgrad(quick):
         torch.cuda.empty_cache()
 
 
+def vocab():
+    """The vocabulary products with the vocab-axis row stride padded to 8 elements (16 B) against 64
+    (128 B, every row starting on a cache line)."""
+    R = 16384
+    for tag, d, V in (("124M", 768, 50257), ("420M", 1024, 50280)):
+        for to in (8, 64):
+            y, wt = padded(R, d), padded(V, d)
+            lg = torch.empty(R, (V + to - 1) // to * to, device=dev, dtype=torch.bfloat16)[:, :V]
+            w = padded(d, V, to)
+            dy = torch.empty(R, d, device=dev, dtype=torch.bfloat16)
+            gw = torch.zeros(d, V, device=dev)
+            t_f = tm(lambda: K.gemm(y, wt, lg, tb=True))
+            lg.copy_(padded(R, V))
+            t_d = tm(lambda: K.gemm(lg, w, dy, tb=True))
+            grp = K.WGradGroup([(y, lg, gw)], dev)
+            t_w = tm(lambda: grp(beta=1.0))
+            fl = 2.0 * R * d * V
+            print(f"{tag} vocab ld pad {to:2d}: logits {t_f:8.1f} us {fl / t_f / 1e6:5.0f} TF/s | dgrad {t_d:8.1f} us "
+                  f"{fl / t_d / 1e6:5.0f} TF/s | wgrad {t_w:8.1f} us {fl / t_w / 1e6:5.0f} TF/s", flush=True)
+            del y, wt, lg, w, dy, gw, grp
+            torch.cuda.empty_cache()
+
+
 if __name__ == "__main__":
+    if sys.argv[1:2] == ["vocab"]:
+        vocab()
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     quick = "--quick" in sys.argv
     if what in ("nt", "all"):
-        nt(quick)
+        nt(quick, int(sys.argv[sys.argv.index("--pad") + 1]) if "--pad" in sys.argv else 8)
     if what in ("wgrad", "all"):
         wgrad(quick)
     if what in ("grouped", "all"):
