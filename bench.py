@@ -579,21 +579,24 @@ def lm_roofline(st, ms_per_micro):
             2.0 * R * r.V * d, 1)
         add("lm_head data gradient", nt, lambda: K.gemm(r.logits, r.WhK, r.dy, tb=True), 2.0 * R * r.V * d, 1)
     fl_fwd = 2.0 * R * d * (3 * d + d + gu_n + r.F)
-    add("layer forward products (qkv, out + residual, gate|up, fc2 + residual)", nt,
-        lambda: (K.gemm(r.y0[0], w["WqkvT"], r.qkv[0], tb=True), K.gemm(r.o[0], w["WoT"], r.x1[0], tb=True, res=r.x[0]),
+    add("layer forward products (qkv + RoPE, out + residual, gate|up, fc2 + residual)", nt,
+        lambda: (K.gemm_rope(r.y0[0], w["WqkvT"], r.qkv[0], T, Dh, r.cos, r.sin, 2 * d),
+                 K.gemm(r.o[0], w["WoT"], r.x1[0], tb=True, res=r.x[0]),
                  K.gemm(r.y1[0], w["WguT"], r.gu[0], tb=True),
                  K.gemm(r.hm[0], w["W2T"], r.x[1], tb=True, res=r.x1[0])), fl_fwd, L)
     dgu = r.dgu if r.glu else r.dgu[:, : r.F]
-    add("layer data-gradient products (fc2, gate|up, qkv; out with the attention delta)", nt,
-        lambda: (K.gemm(r.dx, w["W2"], r.dh, tb=True), K.gemm(dgu, w["Wgu"], r.dy, tb=True),
+    add("layer data-gradient products (fc2 + GLU backward, gate|up, qkv; out with the attention delta)", nt,
+        lambda: ((K.gemm_swiglu_bwd(r.dx, w["W2"], r.gu[0], r.dgu, r.dh, r.F) if r.glu else
+                  K.gemm(r.dx, w["W2"], r.dh, tb=True)), K.gemm(dgu, w["Wgu"], r.dy, tb=True),
                  K.gemm(r.dx, w["Wo"], r.do, tb=True, attn_delta=(r.o[0], r.delta, T, H)),
                  K.gemm(r.dqkv, w["Wqkv"], r.dy, tb=True)), fl_fwd, L)
     pairs = b * H * T * (T + 1) / 2.0
     add("causal attention forward", "attn_fwd_kernel (csrc/attention.hip)",
         lambda: K.attn_fwd(r.qkv[0], r.o[0], r.lse[0], b, T, H, Dh, causal=True), 2 * 2.0 * pairs * Dh, L)
-    add("causal attention backward (dK/dV + dQ kernels)", "attn_bwd_dkdv_kernel + attn_bwd_dq_kernel",
+    add("causal attention backward (dK/dV + dQ kernels, inverse RoPE in the stores)",
+        "attn_bwd_dkdv_kernel + attn_bwd_dq_kernel",
         lambda: K.attn_bwd(r.qkv[0], r.o[0], r.do, r.lse[0], r.delta, r.dqkv, b, T, H, Dh, causal=True,
-                           delta_ready=True), 4 * 2.0 * pairs * Dh, L)
+                           delta_ready=True, rope=(r.cos, r.sin)), 4 * 2.0 * pairs * Dh, L)
     fams.sort(key=lambda f: -f["share_of_micro_step"])
     top = fams[0]
     achieved = top["tflops"]

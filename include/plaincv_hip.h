@@ -58,6 +58,20 @@ int pcv_gemm_big_enable(int on);
 int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb);
 int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                  int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale, void* stream);
+/* C[M,N] (bf16) = A[M,K] . B[N,K]^T with the forward RoPE on columns [0, rope_cols) (heads of head_dim,
+ * row r at position r % T, cos/sin fp32 [T][head_dim/2]): the LM's qkv Dense product and the rotation
+ * of its q | k heads (models/LM/transformer.py:194-201, embedding.py:29-66) -- pcv_gemm_bf16 + pcv_rope in
+ * one pass (the rotation on the bf16-rounded product in the 256-wide kernel's epilogue; otherwise the
+ * two launches). */
+int pcv_gemm_rope(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                  int64_t ldc, int rope_cols, int T, int head_dim, const float* cos_tab, const float* sin_tab,
+                  void* stream);
+/* dgu = SwiGLU VJP of dh = A[M,K] . B[F,K]^T against gu = [gate | up] (halves Fp = F rounded to 8
+ * apart; pad columns of dgu written 0): the LM's fc2 data gradient and the GLU backward
+ * (models/LM/transformer.py:110-134) in one pass, dh never stored; products the 256-wide kernel does
+ * not take run as pcv_gemm_bf16 into the caller's dh [M][lddh >= Fp] + pcv_swiglu_bwd. */
+int pcv_gemm_swiglu_bwd(const void* A, const void* B, int64_t M, int64_t F, int64_t K, int64_t lda, int64_t ldb,
+                        const void* gu, int64_t ldgu, void* dgu, int64_t lddgu, void* dh, int64_t lddh, void* stream);
 /* Persistent form (csrc/gemm_stream.hip): one workgroup per CU, the 32-deep K steps of all its
  * 256x256 / 256x192 output tiles in one continuous LDS-DMA ring, epilogue stored straight from the
  * accumulators (operand-swapped MFMAs, 16-B column chunks).  Same product and operand rules as
@@ -147,6 +161,16 @@ int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t ldq,
                  int B, int T, int H, int head_dim, int causal,
                  float dropout_rate, const uint16_t* drop_mask, int delta_ready, const int* doc_start,
                  const int* doc_end, const void* o_lo, void* stream);
+/* pcv_attn_bwd followed by the inverse RoPE of the q and k heads of dq / dk (pcv_rope backward on both):
+ * the attention VJP through apply_rotary_emb (models/LM/transformer.py:228-240, embedding.py:29-66).
+ * cos/sin fp32 [T][head_dim/2]; no o_lo.  The tiled kernels rotate the bf16-rounded values in their
+ * stores; the short-sequence path runs the two rope launches after it. */
+int pcv_attn_bwd_rope(const void* q, const void* k, const void* v, int64_t ldq,
+                      const void* o, int64_t ldo, const void* dout, int64_t lddo,
+                      const float* lse2, float* delta_ws, void* dq, void* dk, void* dv, int64_t lddq,
+                      int B, int T, int H, int head_dim, int causal, float dropout_rate,
+                      const uint16_t* drop_mask, int delta_ready, const int* doc_start, const int* doc_end,
+                      const float* cos_tab, const float* sin_tab, void* stream);
 /* out_lo / o_lo (optional, short-sequence path only -- pcv_attn_short_ok): the forward also
  * writes O's bf16 rounding residual O - bf16(O) (row stride ldo, P.V accumulated with P split
  * into bf16 hi + lo), and the backward forms delta = <dO, O_hi + O_lo> from it, so delta

@@ -56,7 +56,37 @@ struct AttnArgs {
   // dend[t] = end (exclusive) of t's document.  Documents are contiguous, so dstart/dend are
   // non-decreasing in t and a tile's extreme values are those of its first/last row.
   const int* dstart; const int* dend;
+  // bwd, tiled path: inverse RoPE on the stored dq / dk (pcv_attn_bwd_rope); cos/sin [T][DH/2]
+  const float* rcos; const float* rsin;
 };
+
+// The backward kernels' outputs leave through an LDS image of the workgroup's 128 rows x DH
+// (row stride DH + 8 elements), stored as 16-B row chunks (per-lane 2-B stores at a row stride
+// touched a 64-B segment per 16 lanes) -- and with the inverse RoPE of rope_kernel (sign -1) applied
+// to a chunk's 4 interleaved pairs on the bf16-rounded values when rcos is set.
+template <int DH>
+__device__ __forceinline__ void store_rows_lds(const bf16* img, bf16* out, int64_t ld, int64_t bT, int row0, int T,
+                                               const float* rcos, const float* rsin) {
+  constexpr int CPR = DH / 8, LDR = DH + 8;
+  for (int idx = threadIdx.x; idx < 128 * CPR; idx += 256) {
+    const int r = idx / CPR, c8 = (idx % CPR) * 8;
+    const int t = row0 + r;
+    if (t >= T) continue;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(img + r * LDR + c8);
+    if (rcos) {
+      const f32x4 c4 = *reinterpret_cast<const f32x4*>(rcos + (int64_t)t * (DH / 2) + c8 / 2);
+      const f32x4 s4 = *reinterpret_cast<const f32x4*>(rsin + (int64_t)t * (DH / 2) + c8 / 2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float c = c4[j], s = -1.f * s4[j];
+        const float x0 = bf2f(v[2 * j]), x1 = bf2f(v[2 * j + 1]);
+        v[2 * j] = f2bf(x0 * c - x1 * s);
+        v[2 * j + 1] = f2bf(x1 * c + x0 * s);
+      }
+    }
+    *reinterpret_cast<bf16x8*>(out + (bT + t) * ld + c8) = v;
+  }
+}
 
 // Dropout keep-mask layout.  flax SelfAttention broadcasts one [T,T] mask over batch
 // and heads (models/vit_small.py:41-45, broadcast_dropout=True), so the bits are drawn
@@ -417,7 +447,10 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
     }
     __syncthreads();
   }
-  // normalise + store
+  // normalise; O through an LDS image of the 128 rows (the K/V buffers are free: the loop ended on a
+  // barrier), stored as 16-B row chunks
+  constexpr int LDR = DH + 8;
+  bf16* oimg = kv_smem;
 #pragma unroll
   for (int gq = 0; gq < QG; ++gq) {
     const int q0 = qw + gq * 16;
@@ -426,16 +459,15 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_fwd_kernel(AttnAr
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float iv = __shfl(inv, 4 * g + r, 64);
-      const int qq = q0 + 4 * g + r;
-      if (qq < T) {
+      const int lr = wave * 32 + gq * 16 + 4 * g + r;
 #pragma unroll
-        for (int d = 0; d < DT; ++d)
-          a.out[(bT + qq) * a.ldout + h * DH + 16 * d + (lane & 15)] = f2bf(acc[gq][d][r] * iv);
-      }
+      for (int d = 0; d < DT; ++d) oimg[lr * LDR + 16 * d + (lane & 15)] = f2bf(acc[gq][d][r] * iv);
     }
     const int myq = q0 + (lane & 15);
     if (g == 0 && myq < T) a.lse2[((int64_t)b * a.H + h) * T + myq] = m2[gq] + log2f(lsum[gq]);
   }
+  __syncthreads();
+  store_rows_lds<DH>(oimg, a.out + h * DH, a.ldout, bT, qb * 128, T, nullptr, nullptr);
 }
 
 // ------------------------------------------------------------- bwd: delta
@@ -466,28 +498,53 @@ __global__ void attn_bwd_delta_kernel(AttnArgs a) {
   }
 }
 
-// --------------------------------------------------------- bwd: dK, dV
-// Workgroup = 4 waves x 32 keys (two 16-key groups per wave share every Q/dO
-// fragment); loops over 64-query tiles (Q, dO, lse2, delta) prefetched into
-// registers one tile ahead and double-buffered in LDS.
-template <int DH>
-struct QTileRegs {
-  static constexpr int N = 64 * DH / 8 / 256;
-  u32x4 q[N], o[N];
-  float l, d;
-};
+// dK/dV: the Q / dO tiles stream through a 3-slot LDS ring filled by LDS-DMA
+// (global_load_lds) two tiles ahead, one barrier per tile, counted vmcnt waits:
+//   per tile j: wait until tile j's pieces landed (tile j+1's may fly) -> barrier (tile j visible to
+//   every wave; every wave finished reading tile j-1) -> issue tile j+2 into tile j-1's slot ->
+//   compute tile j.
+// Against the one-tile register-staged prefetch it replaced: dK/dV 120.4 -> 116.6 us at the 124M
+// shape; the same ring made the forward 27 % slower and the dQ kernel no faster (r06 A/B), so those
+// keep register staging.  The DMA writes a 1-KiB piece lane-linearly; the image swizzle tswz is
+// applied on the SOURCE (lane -> row, stored chunk pc <- source chunk pc ^ tswz(row)), so the LDS
+// images are those of the register-staged form.  Rows past T are fetched clamped to row T-1 (finite
+// data): every score they take part in is masked by the boundary path, so they contribute nothing.
+typedef __attribute__((address_space(3))) void attn_lds_void;
 
+__device__ __forceinline__ void attn_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+
+// --------------------------------------------------------- bwd: dK, dV
+// Workgroup = 4 waves x 32 keys (two 16-key groups per wave share every Q/dO fragment); loops over
+// 64-query tiles (Q, dO rows and the lse / delta of the 64 queries) through the ring.
+template <int DH>
+struct QoRing {
+  static constexpr int TILE = 64 * DH;                    // bf16 elements of one 64-row image
+  static constexpr int NS = 3;                            // slots (tiles in flight: 2 ahead)
+  static constexpr int SLOT = 2 * TILE * 2 + 2 * 64 * 4;  // bytes: Q | dO images, lse | delta
+  static constexpr int BYTES = NS * SLOT;
+  static constexpr int PIECES = TILE * 2 / 1024;          // 1-KiB pieces per image
+  static constexpr int PPW = 2 * PIECES / 4;              // pieces per wave per tile
+  static constexpr int OPS = PPW + 2;                     // DMA ops per wave per tile (+ lse, delta)
+  static constexpr int RPP = 1024 / (DH * 2);             // rows per piece
+};
 template <int DH, bool CAUSAL, bool DROP, bool DOC>
 __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(AttnArgs a) {
+  using RG = QoRing<DH>;
   constexpr int KS = DH / 32, DT = DH / 16, KG = 2, CPR = DH / 8;
-  constexpr int TILE = 64 * DH;
-  __shared__ __attribute__((aligned(16))) bf16 qo_smem[2 * 2 * TILE];   // [buffer][Q|dO][TILE]
-  __shared__ __attribute__((aligned(16))) float ld_smem[2 * 128];       // [buffer][lse|delta][64]
+  constexpr int TILE = RG::TILE;
+  extern __shared__ __attribute__((aligned(16))) char ring[];
   int kb, h, b;
   light_last<CAUSAL>(kb, h, b);
   const int T = a.T;
   const int64_t bT = (int64_t)b * T;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave index through readfirstlane: the per-wave key range, and with it the active / interior
+  // tests, are scalar (as VGPR values they were exec-mask branches around the score loop)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int g = lane >> 4;
   const int kw = kb * 128 + wave * 32;
   const bf16* Qp = a.q + h * DH;
@@ -514,26 +571,6 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
 #pragma unroll
     for (int d = 0; d < DT; ++d) { dv[gk][d] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[gk][d] = f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-  auto qload = [&](QTileRegs<DH>& t, int q0) {
-#pragma unroll
-    for (int i = 0; i < QTileRegs<DH>::N; ++i) {
-      const int idx = threadIdx.x + 256 * i;
-      const int r = idx / CPR, c = idx % CPR;
-      const int gr = q0 + r;
-      if (gr < T) {
-        t.q[i] = *reinterpret_cast<const u32x4*>(Qp + (bT + gr) * a.ldq + c * 8);
-        t.o[i] = *reinterpret_cast<const u32x4*>(dOp + (bT + gr) * a.lddo + c * 8);
-      } else {
-        t.q[i] = u32x4{0u, 0u, 0u, 0u};
-        t.o[i] = u32x4{0u, 0u, 0u, 0u};
-      }
-    }
-    if (threadIdx.x < 64) {
-      const int qq = q0 + threadIdx.x;
-      t.l = qq < T ? lse[qq] : 0.f;
-      t.d = qq < T ? del[qq] : 0.f;
-    }
-  };
   int nqb = (T + 63) / 64;
   const int qb0 = CAUSAL ? (kb * 128) / 64 : 0;
   // document mask: queries at or past the end of the block's last document never see its keys
@@ -546,28 +583,54 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
 #pragma unroll
     for (int gk = 0; gk < KG; ++gk) myde[gk] = a.dend[bT + min(kw + gk * 16 + (lane & 15), T - 1)];
   }
-  auto qstore = [&](const QTileRegs<DH>& t, int buf) {
+  const int nt = max(nqb - qb0, 0);
+
+  // this wave's DMA pieces: piece p = wave * PPW + i, image p / PIECES (0 Q, 1 dO), rows
+  // (p % PIECES) * RPP + lane / CPR; per-lane row and byte offset of the stored chunk's source
+  int prow[RG::PPW];
+  uint32_t poff[RG::PPW];
 #pragma unroll
-    for (int i = 0; i < QTileRegs<DH>::N; ++i) {
-      const int idx = threadIdx.x + 256 * i;
-      const int r = idx / CPR, c = idx % CPR;
-      *reinterpret_cast<u32x4*>(qo_smem + 2 * buf * TILE + toff<DH>(r, c)) = t.q[i];
-      *reinterpret_cast<u32x4*>(qo_smem + (2 * buf + 1) * TILE + toff<DH>(r, c)) = t.o[i];
+  for (int i = 0; i < RG::PPW; ++i) {
+    const int p = wave * RG::PPW + i;
+    const int row = (p % RG::PIECES) * RG::RPP + lane / CPR;
+    const int c = (lane % CPR) ^ tswz<DH>(row);
+    prow[i] = row;
+    poff[i] = (uint32_t)(c * 16);
+  }
+  auto issue = [&](int j) __attribute__((always_inline)) {
+    const int q0 = (qb0 + j) * 64;
+    char* slot = ring + (j % RG::NS) * RG::SLOT;
+    const bool full = q0 + 63 < T;
+#pragma unroll
+    for (int i = 0; i < RG::PPW; ++i) {
+      const int p = wave * RG::PPW + i;
+      const bool isq = p < RG::PIECES;   // wave-uniform
+      const bf16* base = isq ? Qp : dOp;
+      const int64_t ld = isq ? a.ldq : a.lddo;
+      const int r = full ? prow[i] : min(prow[i], T - 1 - q0);
+      const char* src = reinterpret_cast<const char*>(base + (bT + q0) * ld) + ((int64_t)r * ld * 2 + poff[i]);
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (attn_lds_void*)(slot + (isq ? 0 : TILE * 2) + (p % RG::PIECES) * 1024),
+                                       16, 0, 0);
     }
-    if (threadIdx.x < 64) { ld_smem[buf * 128 + threadIdx.x] = t.l; ld_smem[buf * 128 + 64 + threadIdx.x] = t.d; }
+    const int qq = min(q0 + lane, T - 1);
+    __builtin_amdgcn_global_load_lds((const void*)(lse + qq), (attn_lds_void*)(slot + 4 * TILE), 4, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(del + qq), (attn_lds_void*)(slot + 4 * TILE + 256), 4, 0, 0);
   };
 
-  QTileRegs<DH> pre;
-  if (qb0 < nqb) { qload(pre, qb0 * 64); qstore(pre, 0); }
-  __syncthreads();
-  for (int qb = qb0; qb < nqb; ++qb) {
-    const int buf = (qb - qb0) & 1;
-    const bf16* Qs = qo_smem + 2 * buf * TILE;
+  if (nt > 0) issue(0);
+  if (nt > 1) issue(1);
+  for (int j = 0; j < nt; ++j) {
+    const int qb = qb0 + j;
+    if (j + 1 < nt) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(RG::OPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    attn_barrier();
+    if (j + 2 < nt) issue(j + 2);
+    const char* slot = ring + (j % RG::NS) * RG::SLOT;
+    const bf16* Qs = reinterpret_cast<const bf16*>(slot);
     const bf16* Ds = Qs + TILE;
-    const float* Ls = ld_smem + buf * 128;
+    const float* Ls = reinterpret_cast<const float*>(slot + 4 * TILE);
     const float* Dl = Ls + 64;
-    const bool more = qb + 1 < nqb;
-    if (more) qload(pre, (qb + 1) * 64);
     const bool active = kw < T && (!CAUSAL || qb * 64 + 63 >= kw) && (!doc || qb * 64 < wde_hi);
     // every (query, key) pair of this wave's 64x32 block valid: skip per-element masks
     const bool interior = qb * 64 + 63 < T && kw + 31 < T && (!CAUSAL || kw + 31 <= qb * 64) &&
@@ -581,6 +644,10 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         f32x4 sv[KG], dp[KG];
+        // the 4 queries' lse / delta as one 16-B read each; -delta is dP's initial accumulator
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(Ls + 16 * t + 4 * g);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(Dl + 16 * t + 4 * g);
+        const f32x4 nd4 = f32x4{-d4[0], -d4[1], -d4[2], -d4[3]};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const bf16x8 qa = row_frag<DH>(Qs, 16 * t, ks);
@@ -588,16 +655,13 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
 #pragma unroll
           for (int gk = 0; gk < KG; ++gk) {
             sv[gk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[gk][ks], ks ? sv[gk] : kZero4, 0, 0, 0);
-            dp[gk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[gk][ks], ks ? dp[gk] : kZero4, 0, 0, 0);
+            dp[gk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[gk][ks], ks ? dp[gk] : (DROP ? kZero4 : nd4),
+                                                             0, 0, 0);
           }
         }
-        // the 4 queries' lse / delta as one 16-B read each (a per-element read waited on its own
-        // LDS round trip inside a per-element branch); the boundary test in a path of its own
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(Ls + 16 * t + 4 * g);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(Dl + 16 * t + 4 * g);
         // MODE 0: every pair valid; 1: ragged tail / causal diagonal as one window [lo, hi) of this
         // lane's 4 queries (3 VALU a score); 2: the document mask, per pair
-        auto probs = [&](auto mode_t) {
+        auto probs = [&](auto mode_t) __attribute__((always_inline)) {
           constexpr int MODE = decltype(mode_t)::value;
 #pragma unroll
           for (int gk = 0; gk < KG; ++gk) {
@@ -606,11 +670,10 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
             if (DROP) wt = (uint32_t)a.mask[drop_word(qb * 64 + 16 * t + 4 * g, mykey, a.n64)] >> (mykey & 3);
             int lo = 0, span = 0;
             if constexpr (MODE == 1) {
-              const int ql = __builtin_amdgcn_readfirstlane(qb * 64 + 16 * t) + 4 * g;
+              const int ql = qb * 64 + 16 * t + 4 * g;
               lo = mykey >= T ? 4 : (CAUSAL ? mykey - ql : 0);
-              // clamped: an empty window (padding queries past T, keys past T near the tail) keeps nothing,
-              // instead of relying on the zero-filled Q / dO / lse / delta rows of the padding
-              span = max((__builtin_amdgcn_readfirstlane(T) - ql) - lo, 0);
+              // clamped: an empty window (padding queries past T, keys past T near the tail) keeps nothing
+              span = max((T - ql) - lo, 0);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -621,15 +684,17 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
                 const bool ok = mykey < T && qq < T && mykey <= qq && qq < myde[gk];
                 pv = ok ? pv : 0.f;
               }
-              float dpv = dp[gk][r];
-              float pd = pv;
+              float pd = pv, dsv;
               if (DROP) {   // keep bit as an all-ones/zero mask; dV's 1/keep scale is applied at the store
                 const uint32_t km = (uint32_t)__builtin_amdgcn_sbfe((int)wt, 4 * r, 1);
                 pd = __uint_as_float(__float_as_uint(pv) & km);
-                dpv = __uint_as_float(__float_as_uint(dpv) & km) * a.drop_scale;
+                const float dpv = __uint_as_float(__float_as_uint(dp[gk][r]) & km) * a.drop_scale;
+                dsv = pv * (dpv - d4[r]);
+              } else {
+                dsv = pv * dp[gk][r];   // dp already holds dP - delta
               }
               p[gk][t][r] = pd;
-              ds[gk][t][r] = pv * (dpv - d4[r]);
+              ds[gk][t][r] = dsv;
             }
           }
         };
@@ -659,23 +724,30 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dkdv_kernel(A
         }
       }
     }
-    if (more) qstore(pre, buf ^ 1);
-    __syncthreads();
   }
+  // dK, dV through LDS (the ring is free once every wave passed this barrier)
+  constexpr int LDR = DH + 8;
+  __syncthreads();
+  bf16* kimg = reinterpret_cast<bf16*>(ring);
+  bf16* vimg = kimg + 128 * LDR;
 #pragma unroll
   for (int gk = 0; gk < KG; ++gk) {
-    const int mykey = kw + gk * 16 + (lane & 15);
-    if (mykey < T) {
+    const int lk = wave * 32 + gk * 16 + (lane & 15);
 #pragma unroll
-      for (int d = 0; d < DT; ++d)
+    for (int d = 0; d < DT; ++d) {
+      bf16x4 kq, vq;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int dd = 16 * d + 4 * g + r;
-          a.dv[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(DROP ? dv[gk][d][r] * a.drop_scale : dv[gk][d][r]);
-          a.dk[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(dk[gk][d][r] * a.scale);
-        }
+      for (int r = 0; r < 4; ++r) {
+        kq[r] = f2bf(dk[gk][d][r] * a.scale);
+        vq[r] = f2bf(DROP ? dv[gk][d][r] * a.drop_scale : dv[gk][d][r]);
+      }
+      *reinterpret_cast<bf16x4*>(kimg + lk * LDR + 16 * d + 4 * g) = kq;
+      *reinterpret_cast<bf16x4*>(vimg + lk * LDR + 16 * d + 4 * g) = vq;
     }
   }
+  __syncthreads();
+  store_rows_lds<DH>(kimg, a.dk + h * DH, a.lddq, bT, kb * 128, T, a.rcos, a.rsin);
+  store_rows_lds<DH>(vimg, a.dv + h * DH, a.lddq, bT, kb * 128, T, nullptr, nullptr);
 }
 
 // --------------------------------------------------------------- bwd: dQ
@@ -834,19 +906,19 @@ __global__ __launch_bounds__(256, DH >= 128 ? 1 : 2) void attn_bwd_dq_kernel(Att
     }
     __syncthreads();
   }
+  // dQ through LDS (the K/V buffers are free: the loop ended on a barrier)
+  constexpr int LDR = DH + 8;
+  bf16* qimg = kv_smem;
 #pragma unroll
-  for (int gq = 0; gq < QG; ++gq) {
-    const int q0 = qw + gq * 16;
+  for (int gq = 0; gq < QG; ++gq)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int qq = q0 + 4 * g + r;
-      if (qq < T) {
+      const int lr = wave * 32 + gq * 16 + 4 * g + r;
 #pragma unroll
-        for (int d = 0; d < DT; ++d)
-          a.dq[(bT + qq) * a.lddq + h * DH + 16 * d + (lane & 15)] = f2bf(acc[gq][d][r] * a.scale);
-      }
+      for (int d = 0; d < DT; ++d) qimg[lr * LDR + 16 * d + (lane & 15)] = f2bf(acc[gq][d][r] * a.scale);
     }
-  }
+  __syncthreads();
+  store_rows_lds<DH>(qimg, a.dq + h * DH, a.lddq, bT, qb * 128, T, a.rcos, a.rsin);
 }
 
 // ------------------------------------------------------- short sequences (ViT)
@@ -1673,22 +1745,28 @@ static void launch_fwd(const AttnArgs& a, hipStream_t s) {
   }
   hipLaunchKernelGGL((attn_fwd_kernel<DH, C, D, false>), grid, dim3(256), 0, s, a);
 }
+template <int DH, bool C, bool D, bool DOC>
+static void launch_bwd_main(const AttnArgs& a, hipStream_t s) {
+  dim3 grid((a.T + 127) / 128, a.H, a.B);
+  auto kdkdv = attn_bwd_dkdv_kernel<DH, C, D, DOC>;
+  constexpr int LDS = QoRing<DH>::BYTES;
+  if constexpr (LDS > 65536) {   // DH = 128: opt in once per instantiation and device
+    static PcvLdsOptIn optin;
+    if (optin.ensure((const void*)kdkdv, LDS)) return;
+  }
+  hipLaunchKernelGGL(kdkdv, grid, dim3(256), LDS, s, a);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, C, D, DOC>), grid, dim3(256), 0, s, a);
+}
 template <int DH, bool C, bool D>
 static void launch_bwd(const AttnArgs& a, hipStream_t s) {
   const int64_t n = (int64_t)a.B * a.T * a.H;
   const int64_t nd = n * (DH / 8);
   if (!a.delta_ready)
     hipLaunchKernelGGL((attn_bwd_delta_kernel<DH>), dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a);
-  dim3 grid((a.T + 127) / 128, a.H, a.B);
   if constexpr (C) {
-    if (a.dstart) {
-      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH, C, D, true>), grid, dim3(256), 0, s, a);
-      hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, C, D, true>), grid, dim3(256), 0, s, a);
-      return;
-    }
+    if (a.dstart) { launch_bwd_main<DH, C, D, true>(a, s); return; }
   }
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<DH, C, D, false>), grid, dim3(256), 0, s, a);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<DH, C, D, false>), grid, dim3(256), 0, s, a);
+  launch_bwd_main<DH, C, D, false>(a, s);
 }
 
 template <bool FWD>
@@ -1702,6 +1780,10 @@ static int dispatch(AttnArgs a, int dh, int causal, int drop, hipStream_t s) {
                       : (drop ? launch_short_bwd<true>(a, s) : launch_short_bwd<false>(a, s));
     return e ? e : pcv_launch_status();
   }
+  // the tiled kernels store 16-B row chunks of their outputs
+  if (FWD ? (!pcv_aligned16(a.out) || (a.ldout & 7))
+          : (!pcv_aligned16(a.dq) || !pcv_aligned16(a.dk) || !pcv_aligned16(a.dv) || (a.lddq & 7)))
+    return PCV_EALIGN;
 #define PCV_ATT(DHV, CV, DV) \
   if (dh == DHV && causal == CV && drop == DV) { FWD ? launch_fwd<DHV, CV, DV>(a, s) : launch_bwd<DHV, CV, DV>(a, s); return pcv_launch_status(); }
   PCV_ATT(32, 0, 0) PCV_ATT(32, 0, 1) PCV_ATT(32, 1, 0) PCV_ATT(32, 1, 1)
@@ -1785,6 +1867,48 @@ extern "C" int pcv_attn_bwd(const void* q, const void* k, const void* v, int64_t
   a.lse2 = (float*)lse2; a.delta = delta_ws; a.delta_ready = delta_ready;
   a.B = B; a.T = T; a.H = H; a.scale = 1.f / sqrtf((float)head_dim);
   a.dstart = doc_start; a.dend = doc_end;
+  set_drop(a, dropout_rate, drop_mask);
+  return dispatch<false>(a, head_dim, causal ? 1 : 0, a.drop, (hipStream_t)stream);
+}
+
+// pcv_attn_bwd followed by the inverse RoPE of the q and k heads (pcv_rope backward on dq, dk): the LM's
+// attention VJP through apply_rotary_emb (models/LM/transformer.py:228-240, embedding.py:29-66).  The
+// tiled kernels rotate the bf16-rounded dq / dk in their stores (same values as the two launches);
+// the short-sequence path runs the rope launches after it.
+extern "C" int pcv_rope(void* qk, int64_t ld, int64_t R, int ncols, int T, int head_dim, const float* cos_tab,
+                        const float* sin_tab, int backward, void* stream);
+extern "C" int pcv_attn_bwd_rope(const void* q, const void* k, const void* v, int64_t ldq,
+                                 const void* o, int64_t ldo, const void* dout, int64_t lddo,
+                                 const float* lse2, float* delta_ws,
+                                 void* dq, void* dk, void* dv, int64_t lddq,
+                                 int B, int T, int H, int head_dim, int causal,
+                                 float dropout_rate, const uint16_t* drop_mask, int delta_ready,
+                                 const int* doc_start, const int* doc_end, const float* cos_tab, const float* sin_tab,
+                                 void* stream) {
+  if (!cos_tab || !sin_tab || (lddq & 7) || !pcv_aligned16(dq) || !pcv_aligned16(dk)) return PCV_EINVAL;
+  AttnArgs t{};
+  t.T = T;
+  if (short_ok(t, head_dim, causal, false)) {
+    int e = pcv_attn_bwd(q, k, v, ldq, o, ldo, dout, lddo, lse2, delta_ws, dq, dk, dv, lddq, B, T, H, head_dim, causal,
+                         dropout_rate, drop_mask, delta_ready, doc_start, doc_end, nullptr, stream);
+    if (!e) e = pcv_rope(dq, lddq, (int64_t)B * T, H * head_dim, T, head_dim, cos_tab, sin_tab, 1, stream);
+    if (!e) e = pcv_rope(dk, lddq, (int64_t)B * T, H * head_dim, T, head_dim, cos_tab, sin_tab, 1, stream);
+    return e;
+  }
+  if (B <= 0 || T <= 0 || H <= 0) return PCV_EINVAL;
+  if ((doc_start != nullptr) != (doc_end != nullptr) || (doc_start && !causal)) return PCV_EINVAL;
+  if (dropout_rate > 0.f && (!drop_mask || ((uintptr_t)drop_mask & 7))) return PCV_EINVAL;
+  if ((ldq & 7) || (ldo & 7) || (lddo & 7) || !pcv_aligned16(q) || !pcv_aligned16(k) || !pcv_aligned16(v) ||
+      !pcv_aligned16(o) || !pcv_aligned16(dout))
+    return PCV_EALIGN;
+  AttnArgs a{};
+  a.q = (const bf16*)q; a.k = (const bf16*)k; a.v = (const bf16*)v; a.ldq = ldq;
+  a.o = (const bf16*)o; a.ldo = ldo; a.dout = (const bf16*)dout; a.lddo = lddo;
+  a.dq = (bf16*)dq; a.dk = (bf16*)dk; a.dv = (bf16*)dv; a.lddq = lddq;
+  a.lse2 = (float*)lse2; a.delta = delta_ws; a.delta_ready = delta_ready;
+  a.B = B; a.T = T; a.H = H; a.scale = 1.f / sqrtf((float)head_dim);
+  a.dstart = doc_start; a.dend = doc_end;
+  a.rcos = cos_tab; a.rsin = sin_tab;
   set_drop(a, dropout_rate, drop_mask);
   return dispatch<false>(a, head_dim, causal ? 1 : 0, a.drop, (hipStream_t)stream);
 }

@@ -38,6 +38,16 @@ struct BigArgs {
   int64_t lda, ldb, ldc, ldr;
   int M, N, K, tiles_m, tiles_n;
   float alpha, res_scale;
+  // RoPE on the stored bf16 values of columns [0, rope_cols) (pcv_gemm_rope): row r at position
+  // r % rope_T, interleaved pairs of heads rope_half * 2 wide, as rope_kernel (elementwise.hip)
+  const float* rcos; const float* rsin;
+  int rope_cols, rope_T, rope_half;
+  // SwiGLU VJP in place of the store (pcv_gemm_swiglu_bwd): the product is dh [M, F = N]; from it and
+  // gu = [gate | up] (halves Fp = N rounded to 8 apart) the epilogue writes dgu = [dgate | dup] (pad
+  // columns 0), as swiglu_bwd_kernel (elementwise.hip) on the stored dh; C is not written
+  const bf16* sw_gu; bf16* sw_dgu;
+  int64_t sw_ldgu, sw_lddgu;
+  int sw_Fp;
 };
 
 constexpr int GB_T = 256;                 // tile rows (M); the N width BN is a template parameter
@@ -256,9 +266,39 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
   for (int e = tid; e < GB_T * CPR; e += 512) {
     const int row = e / CPR, cc = (e % CPR) * 8;
     const int gr = m0 + row, gc = n0 + cc;
-    if (gr >= g.M || gc >= g.N) continue;
+    if (gr >= g.M || gc >= (g.sw_gu ? g.sw_Fp : g.N)) continue;
     bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + row * C::CLD + cc * 2);
+    if (g.sw_gu) {   // SwiGLU VJP (columns past N of the staged tile are masked, not read as data)
+      const bf16* gp = g.sw_gu + (int64_t)gr * g.sw_ldgu + gc;
+      const bf16x8 gg = *reinterpret_cast<const bf16x8*>(gp);
+      const bf16x8 uu = *reinterpret_cast<const bf16x8*>(gp + g.sw_Fp);
+      bf16x8 dg, du;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool ok = gc + j < g.N;
+        const float gv = bf2f(gg[j]), uv = bf2f(uu[j]), dv = ok ? bf2f(v[j]) : 0.f;
+        const float sg = 1.f / (1.f + __expf(-gv));
+        du[j] = f2bf(ok ? dv * gv * sg : 0.f);
+        dg[j] = f2bf(ok ? dv * uv * sg * (1.f + gv * (1.f - sg)) : 0.f);
+      }
+      bf16* dp = g.sw_dgu + (int64_t)gr * g.sw_lddgu + gc;
+      *reinterpret_cast<bf16x8*>(dp) = dg;
+      *reinterpret_cast<bf16x8*>(dp + g.sw_Fp) = du;
+      continue;
+    }
     bf16* dst = g.C + (int64_t)gr * g.ldc + gc;
+    if (g.rcos && gc < g.rope_cols) {   // (no residual with RoPE: pcv_gemm_rope)
+      const int t = gr % g.rope_T, p0 = (gc % (2 * g.rope_half)) / 2;
+      const float* ct = g.rcos + (int64_t)t * g.rope_half + p0;
+      const float* st = g.rsin + (int64_t)t * g.rope_half + p0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float c = ct[j], sn = st[j];
+        const float x0 = bf2f(v[2 * j]), x1 = bf2f(v[2 * j + 1]);
+        v[2 * j] = f2bf(x0 * c - x1 * sn);
+        v[2 * j + 1] = f2bf(x1 * c + x0 * sn);
+      }
+    }
     if (vec && gc + 8 <= g.N) {
       if (g.res) {
         const bf16x8 rv = *reinterpret_cast<const bf16x8*>(g.res + (int64_t)gr * g.ldr + gc);
@@ -514,6 +554,82 @@ extern "C" int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, in
   const int bn = big_bn(M, N) == 192 ? 192 : 256;
   g.tiles_m = (int)((M + GB_T - 1) / GB_T);
   g.tiles_n = (int)((N + bn - 1) / bn);
+  const int e = bn == 192 ? launch_big<192>(g, (hipStream_t)stream) : launch_big<256>(g, (hipStream_t)stream);
+  return e ? e : pcv_launch_status();
+}
+
+// C = A . B^T (bf16) with the forward RoPE applied to columns [0, rope_cols) of every stored row --
+// the LM's qkv product and the rotation of its q | k heads (models/LM/transformer.py:194-201,
+// embedding.py:29-66) in one pass: the rotation runs on the bf16-rounded product in fp32 and rounds
+// again, exactly as rope_kernel on the stored qkv, so the result is bitwise that of the two launches.
+// Products the 256-wide kernel does not take run as pcv_gemm_bf16 + pcv_rope.
+extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                             int64_t ldb, int64_t ldc, int trans_a, int trans_b, int64_t batch, int64_t stride_a,
+                             int64_t stride_b, int64_t stride_c, float alpha, float beta, int out_f32,
+                             const float* bias, const void* res, int64_t ldr, int64_t stride_r, int res_f32,
+                             float res_scale, void* aux, int64_t ldaux, int act, float drop_rate,
+                             const uint32_t* seed, uint32_t site, float* colsum, int col_reps, const void* attn_o,
+                             int64_t ld_attn_o, const void* attn_o_lo, float* attn_delta, int attn_T, int attn_H,
+                             int split_k, void* stream);
+extern "C" int pcv_rope(void* qk, int64_t ld, int64_t R, int ncols, int T, int head_dim, const float* cos_tab,
+                        const float* sin_tab, int backward, void* stream);
+extern "C" int pcv_gemm_rope(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                             int64_t ldb, int64_t ldc, int rope_cols, int T, int head_dim, const float* cos_tab,
+                             const float* sin_tab, void* stream) {
+  if (!C || !cos_tab || !sin_tab || T <= 0 || head_dim <= 0 || (head_dim & 7) || rope_cols < 0 || rope_cols > N ||
+      (rope_cols % head_dim) || M % T)
+    return PCV_EINVAL;
+  if ((ldc & 7) || !pcv_aligned16(C)) return PCV_EALIGN;
+  if (!pcv_gemm_big_ok(M, N, K, A, lda, B, ldb)) {
+    const int e = pcv_gemm_bf16(A, B, C, M, N, K, lda, ldb, ldc, 0, 1, 1, 0, 0, 0, 1.f, 0.f, 0, nullptr, nullptr, 0, 0,
+                                0, 1.f, nullptr, 0, 0, 0.f, nullptr, 0, nullptr, 0, nullptr, 0, nullptr, nullptr, 0, 0,
+                                1, stream);
+    if (e || rope_cols == 0) return e;
+    return pcv_rope(C, ldc, M, rope_cols, T, head_dim, cos_tab, sin_tab, 0, stream);
+  }
+  BigArgs g{};
+  g.A = (const bf16*)A; g.B = (const bf16*)B; g.C = (bf16*)C;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.alpha = 1.f; g.res_scale = 0.f;
+  g.rcos = rope_cols ? cos_tab : nullptr; g.rsin = sin_tab;
+  g.rope_cols = rope_cols; g.rope_T = T; g.rope_half = head_dim / 2;
+  const int bn = big_bn(M, N) == 192 ? 192 : 256;
+  g.tiles_m = (int)((M + GB_T - 1) / GB_T);
+  g.tiles_n = (int)((N + bn - 1) / bn);
+  const int e = bn == 192 ? launch_big<192>(g, (hipStream_t)stream) : launch_big<256>(g, (hipStream_t)stream);
+  return e ? e : pcv_launch_status();
+}
+
+// dgu = SwiGLU-VJP(dh = A . B^T, gu): the LM's fc2 data gradient and the GLU backward
+// (models/LM/transformer.py:110-134: dh = dx W2^T, then d(silu(gate) * up)) in one pass -- dh never
+// reaches HBM.  Same values as pcv_gemm_bf16 into dh followed by pcv_swiglu_bwd (the VJP runs on the
+// bf16-rounded dh); products the 256-wide kernel does not take run as those two launches through the
+// caller's dh buffer.
+extern "C" int pcv_swiglu_bwd(const void* dh, int64_t lddh, const void* gu, int64_t ldgu, void* dgu, int64_t lddgu,
+                              int64_t R, int F, int Fp, void* stream);
+extern "C" int pcv_gemm_swiglu_bwd(const void* A, const void* B, int64_t M, int64_t F, int64_t K, int64_t lda,
+                                   int64_t ldb, const void* gu, int64_t ldgu, void* dgu, int64_t lddgu, void* dh,
+                                   int64_t lddh, void* stream) {
+  const int64_t Fp = (F + 7) / 8 * 8;
+  if (!gu || !dgu || F <= 0 || M <= 0 || ldgu < 2 * Fp || lddgu < 2 * Fp) return PCV_EINVAL;
+  if ((ldgu & 7) || (lddgu & 7) || !pcv_aligned16(gu) || !pcv_aligned16(dgu)) return PCV_EALIGN;
+  if (!pcv_gemm_big_ok(M, F, K, A, lda, B, ldb)) {
+    if (!dh || lddh < Fp) return PCV_EINVAL;
+    const int e = pcv_gemm_bf16(A, B, dh, M, F, K, lda, ldb, lddh, 0, 1, 1, 0, 0, 0, 1.f, 0.f, 0, nullptr, nullptr, 0,
+                                0, 0, 1.f, nullptr, 0, 0, 0.f, nullptr, 0, nullptr, 0, nullptr, 0, nullptr, nullptr, 0,
+                                0, 1, stream);
+    return e ? e : pcv_swiglu_bwd(dh, lddh, gu, ldgu, dgu, lddgu, M, (int)F, (int)Fp, stream);
+  }
+  BigArgs g{};
+  g.A = (const bf16*)A; g.B = (const bf16*)B; g.C = nullptr;
+  g.lda = lda; g.ldb = ldb; g.ldc = 0;
+  g.M = (int)M; g.N = (int)F; g.K = (int)K;
+  g.alpha = 1.f; g.res_scale = 0.f;
+  g.sw_gu = (const bf16*)gu; g.sw_dgu = (bf16*)dgu; g.sw_ldgu = ldgu; g.sw_lddgu = lddgu; g.sw_Fp = (int)Fp;
+  const int bn = big_bn(M, F) == 192 ? 192 : 256;
+  g.tiles_m = (int)((M + GB_T - 1) / GB_T);
+  g.tiles_n = (int)((F + bn - 1) / bn);
   const int e = bn == 192 ? launch_big<192>(g, (hipStream_t)stream) : launch_big<256>(g, (hipStream_t)stream);
   return e ? e : pcv_launch_status();
 }

@@ -35,6 +35,8 @@ SIGNATURES = {
     "pcv_attn_fwd": [P, P, P, I64, P, I64, P, I32, I32, I32, I32, I32, F32, P, P, P, P, P],
     "pcv_attn_bwd": [P, P, P, I64, P, I64, P, I64, P, P, P, P, P, I64, I32, I32, I32, I32, I32,
                      F32, P, I32, P, P, P, P],
+    "pcv_attn_bwd_rope": [P, P, P, I64, P, I64, P, I64, P, P, P, P, P, I64, I32, I32, I32, I32, I32,
+                          F32, P, I32, P, P, P, P, P],
     "pcv_attn_short_ok": [I32, I32, I32],
     "pcv_attn_mask_words": [I32],
     "pcv_attn_drop_mask": [P, U32, U32, I32, I32, F32, P, P],
@@ -151,6 +153,8 @@ SIGNATURES = {
     "pcv_gemm_big_enable": [I32],
     "pcv_gemm_big_ok": [I64, I64, I64, P, I64, P, I64],
     "pcv_gemm_big": [P, P, P, I64, I64, I64, I64, I64, I64, F32, P, I64, F32, P],
+    "pcv_gemm_rope": [P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, I32, P, P, P],
+    "pcv_gemm_swiglu_bwd": [P, P, I64, I64, I64, I64, I64, P, I64, P, I64, P, I64, P],
     "pcv_gemm_stream_enable": [I32],
     "pcv_gemm_stream_ok": [I64, I64, I64, P, I64, P, I64],
     "pcv_gemm_stream": [P, P, P, I64, I64, I64, I64, I64, I64, F32, P, I64, F32, P],

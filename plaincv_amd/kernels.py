@@ -359,7 +359,9 @@ def attn_fwd(qkv, out, lse2, B, T, H, Dh, causal, drop_rate=0.0, mask=None, q_of
 
 
 def attn_bwd(qkv, o, dout, lse2, delta_ws, dqkv, B, T, H, Dh, causal, drop_rate=0.0, mask=None, delta_ready=False,
-             doc=None, o_lo=None):
+             doc=None, o_lo=None, rope=None):
+    """rope=(cos, sin) fp32 [T, Dh/2]: also the inverse RoPE of the q and k heads of dqkv (as rope(...,
+    backward=True, ncols=2 D) after it), in the dq / dk stores."""
     D = H * Dh
     _chk(qkv.dtype == BF16 and dqkv.dtype == BF16 and dout.dtype == BF16 and o.dtype == BF16, "attn bwd dtypes")
     _chk(dqkv.shape[0] == B * T and dqkv.shape[1] >= 3 * D and delta_ws.numel() >= B * H * T, "attn bwd shapes")
@@ -371,6 +373,17 @@ def attn_bwd(qkv, o, dout, lse2, delta_ws, dqkv, B, T, H, Dh, causal, drop_rate=
     ds, de = _doc_arrays(doc, B, T, causal)
     base, es = qkv.data_ptr(), qkv.element_size()
     dbase = dqkv.data_ptr()
+    if rope is not None:
+        cos_tab, sin_tab = rope
+        _chk(o_lo is None and cos_tab.dtype == F32 and sin_tab.dtype == F32 and cos_tab.is_contiguous() and
+             sin_tab.is_contiguous() and cos_tab.shape[0] >= T and cos_tab.shape[-1] == Dh // 2 and
+             sin_tab.shape == cos_tab.shape, "attn bwd rope tables")
+        _dev(cos_tab, sin_tab)
+        hip.call("pcv_attn_bwd_rope", base, base + D * es, base + 2 * D * es, _ld(qkv), ptr(o), _ld(o), ptr(dout),
+                 _ld(dout), ptr(lse2), ptr(delta_ws), dbase, dbase + D * es, dbase + 2 * D * es, _ld(dqkv),
+                 B, T, H, Dh, int(causal), float(drop_rate), ptr(mask), int(delta_ready), ptr(ds), ptr(de),
+                 ptr(cos_tab), ptr(sin_tab), stream_ptr())
+        return
     hip.call("pcv_attn_bwd", base, base + D * es, base + 2 * D * es, _ld(qkv), ptr(o), _ld(o), ptr(dout),
              _ld(dout), ptr(lse2), ptr(delta_ws), dbase, dbase + D * es, dbase + 2 * D * es, _ld(dqkv),
              B, T, H, Dh, int(causal), float(drop_rate), ptr(mask), int(delta_ready), ptr(ds), ptr(de),
@@ -535,6 +548,36 @@ def rmsnorm_bwd(dy, x, scale, rstd, dres, dx, dscale):
     _dev(dy, x, scale, rstd, dres, dx, dscale)
     hip.call("pcv_rmsnorm_bwd", ptr(dy), _ld(dy), ptr(x), _ld(x), ptr(scale), ptr(rstd), ptr(dres),
              _ld(dres) if dres is not None else 0, ptr(dx), _ld(dx), ptr(dscale), R, D, stream_ptr())
+
+
+def gemm_rope(a, b, out, T, Dh, cos_tab, sin_tab, rope_cols):
+    """out[M,N] (bf16) = a[M,K] . b[N,K]^T with the forward RoPE on columns [0, rope_cols) (heads of Dh,
+    row r at position r % T): gemm(a, b, out, tb=True) then rope(out, T, Dh, cos, sin, ncols=rope_cols),
+    fused into the GEMM's epilogue where the 256-wide kernel takes the product."""
+    M, Kd = a.shape
+    N, K2 = b.shape
+    _chk(Kd == K2 and tuple(out.shape) == (M, N) and a.dtype == BF16 and b.dtype == BF16 and out.dtype == BF16,
+         "gemm_rope shapes")
+    _chk(a.stride(1) == 1 and b.stride(1) == 1 and out.stride(1) == 1, "gemm_rope strides")
+    _chk(cos_tab.dtype == F32 and sin_tab.dtype == F32 and cos_tab.is_contiguous() and sin_tab.is_contiguous() and
+         cos_tab.shape[0] >= T and cos_tab.shape[-1] == Dh // 2 and sin_tab.shape == cos_tab.shape, "gemm_rope tables")
+    _dev(a, b, out, cos_tab, sin_tab)
+    hip.call("pcv_gemm_rope", ptr(a), ptr(b), ptr(out), M, N, Kd, _ld(a), _ld(b), _ld(out), int(rope_cols), int(T),
+             int(Dh), ptr(cos_tab), ptr(sin_tab), stream_ptr())
+
+
+def gemm_swiglu_bwd(dx, w2, gu, dgu, dh, F):
+    """dgu = swiglu_bwd(dx . w2^T, gu) without dh in HBM where the 256-wide kernel takes the product
+    (else gemm into dh, then swiglu_bwd).  dx [R, K], w2 [F, K] (K-contiguous), gu / dgu [R, 2 Fp]
+    ([gate | up] halves Fp = F rounded to 8 apart), dh [R, >= Fp] scratch for the fallback."""
+    R, Kd = dx.shape
+    Fp = (F + 7) // 8 * 8
+    _chk(w2.shape[0] == F and w2.shape[1] == Kd and gu.shape[0] == R and tuple(dgu.shape) == tuple(gu.shape) and
+         gu.shape[1] == 2 * Fp and dh.shape[0] == R and _ld(dh) >= Fp, "gemm_swiglu_bwd shapes")
+    _chk(all(t.dtype == BF16 and t.stride(1) == 1 for t in (dx, w2, gu, dgu, dh)), "gemm_swiglu_bwd dtypes")
+    _dev(dx, w2, gu, dgu, dh)
+    hip.call("pcv_gemm_swiglu_bwd", ptr(dx), ptr(w2), R, F, Kd, _ld(dx), _ld(w2), ptr(gu), _ld(gu), ptr(dgu),
+             _ld(dgu), ptr(dh), _ld(dh), stream_ptr())
 
 
 def rope(qk, T, Dh, cos_tab, sin_tab, backward=False, ncols=None):

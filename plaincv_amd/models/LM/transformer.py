@@ -156,7 +156,8 @@ class LMRunner:
         # glu: [gate | up] halves of Fp columns each (pads are zero after swiglu); else the fc1 output
         self.glu = c.mlp == "glu"
         nmlp = 2 * self.Fp if self.glu else self.Fp
-        self.gu = [e(R, nmlp) for _ in range(L)]
+        nml = (nmlp + 63) // 64 * 64   # 128-B aligned rows (see self.hm)
+        self.gu = [e(R, nml)[:, :nmlp] for _ in range(L)]
         # rows of the K = F operands (hm, and W2T below) start on 128-B lines (420M fc2 forward
         # 88.3 -> 81.6 us, profiles/r06q_gemm_lab_nt_pad64.txt)
         Fl = (self.F + 63) // 64 * 64
@@ -175,7 +176,7 @@ class LMRunner:
         self.dx = e(R, d)
         self.dy = e(R, d)
         self.dh = e(R, Fl)[:, : self.F]
-        self.dgu = e(R, nmlp)
+        self.dgu = e(R, nml)[:, :nmlp]
         self.do = e(R, d)
         self.dqkv = e(R, 3 * d)
         self.delta = e(b * self.H * T, dt=f32)
@@ -305,8 +306,7 @@ class LMRunner:
         for i in range(c.n_layers):
             w = self.w[i]
             K.rmsnorm_fwd(self.x[i], w["s0"], self.y0[i], self.r0[i], eps)
-            K.gemm(self.y0[i], w["WqkvT"], self.qkv[i], tb=True)
-            K.rope(self.qkv[i], T, Dh, self.cos, self.sin, ncols=2 * d)
+            K.gemm_rope(self.y0[i], w["WqkvT"], self.qkv[i], T, Dh, self.cos, self.sin, 2 * d)   # qkv + RoPE
             K.attn_fwd(self.qkv[i], self.o[i], self.lse[i], b, T, H, Dh, causal=True, doc=self.doc)
             K.gemm(self.o[i], w["WoT"], self.x1[i], tb=True, res=self.x[i])
             K.rmsnorm_fwd(self.x1[i], w["s1"], self.y1[i], self.r1[i], eps)
@@ -357,11 +357,11 @@ class LMRunner:
             else:
                 dx_in = dx_mid = dx_out = self.dxb[0]
                 K.gemm(self.hm[i], dx_in, w["gW2"], ta=True, beta=1.0)
-            K.gemm(dx_in, w["W2"], self.dh, tb=True)
-            if self.glu:
-                K.swiglu_bwd(self.dh, self.gu[i], self.dgu, F=self.F)
+            if self.glu:   # fc2 data gradient + GLU backward in one pass (dh stays on chip)
+                K.gemm_swiglu_bwd(dx_in, w["W2"], self.gu[i], self.dgu, self.dh, self.F)
                 dgu = self.dgu
             else:
+                K.gemm(dx_in, w["W2"], self.dh, tb=True)
                 K.mlp_act_bwd(self.dh, self.gu[i], self.dgu, self.F, c.mlp)
                 dgu = self.dgu[:, : self.F]
             if not grouped:
@@ -372,9 +372,7 @@ class LMRunner:
                 K.gemm(self.o[i], dx_mid, w["gWo"], ta=True, beta=1.0)
             K.gemm(dx_mid, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H))   # + delta
             K.attn_bwd(self.qkv[i], self.o[i], self.do, self.lse[i], self.delta, self.dqkv, b, T, H, Dh, causal=True,
-                       doc=self.doc,
-                       delta_ready=True)
-            K.rope(self.dqkv, T, Dh, self.cos, self.sin, backward=True, ncols=2 * d)
+                       doc=self.doc, delta_ready=True, rope=(self.cos, self.sin))   # + inverse RoPE of dq, dk
             if grouped:
                 self.wg_layers[i](beta=1.0)   # fc2, gate|up, out, qkv weight gradients: one launch
             else:

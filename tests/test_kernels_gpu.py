@@ -689,3 +689,86 @@ def test_attention_lm_geometry(dev, B, T, H):
     print(f"LMATTN B={B} T={T} H={H}: fwd rel {fwd_rel:.2e}  dq / dk / dv rel {rel[0]:.2e} {rel[1]:.2e} {rel[2]:.2e}")
     assert fwd_rel <= 1e-2, fwd_rel
     assert max(rel) <= 1e-2, rel
+
+
+@pytest.mark.parametrize("M,N,Kd,T,Dh", [(16384, 2304, 768, 1024, 64), (16384, 3072, 1024, 2048, 64),
+                                         (2048, 384, 256, 128, 32)])
+def test_gemm_rope_fused_matches_two_launches(dev, M, N, Kd, T, Dh):
+    """pcv_gemm_rope (RoPE in the 256-wide GEMM's epilogue; the last case takes the two-launch fallback)
+    against gemm + rope: the rotation runs on the same bf16-rounded product, so the values agree."""
+    from plaincv_amd import kernels as K
+    from plaincv_amd.models.LM.transformer import precompute_freqs_cis
+    torch.manual_seed(3)
+    a = (torch.randn(M, Kd, device=dev) * 0.5).to(torch.bfloat16)
+    b = (torch.randn(N, Kd, device=dev) * 0.05).to(torch.bfloat16)
+    cos, sin = precompute_freqs_cis(Dh, T, 500000.0)
+    cos, sin = cos.to(dev), sin.to(dev)
+    rc = 2 * (N // 3)
+    ref = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    K.gemm(a, b, ref, tb=True)
+    K.rope(ref, T, Dh, cos, sin, ncols=rc)
+    out = torch.empty_like(ref)
+    K.gemm_rope(a, b, out, T, Dh, cos, sin, rc)
+    torch.cuda.synchronize()
+    diff = (out.float() - ref.float()).abs()
+    print(f"GEMMROPE M={M} N={N}: max diff {diff.max().item():.3g}, differing {(diff > 0).float().mean().item():.2e}")
+    assert (diff > 0).float().mean().item() < 1e-4 and diff.max().item() <= 2e-2 * ref.float().abs().max().item()
+    assert torch.equal(out[:, rc:], ref[:, rc:])
+
+
+@pytest.mark.parametrize("B,T,H,Dh,doc", [(2, 1024, 4, 64, False), (1, 300, 2, 64, False), (2, 512, 2, 64, True),
+                                          (2, 257, 2, 32, False)])
+def test_attn_bwd_rope_fused_matches_two_launches(dev, B, T, H, Dh, doc):
+    """attn_bwd(..., rope=(cos, sin)) (inverse RoPE in the dq / dk stores) against attn_bwd + rope backward."""
+    from plaincv_amd import kernels as K
+    from plaincv_amd.models.LM.transformer import precompute_freqs_cis
+    torch.manual_seed(5)
+    D = H * Dh
+    qkv = torch.randn(B * T, 3 * D, device=dev).to(torch.bfloat16)
+    out = torch.empty(B * T, D, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * T, device=dev)
+    dd = None
+    if doc:
+        starts = torch.tensor([0, 100, 333], dtype=torch.int32)
+        pos = torch.arange(T)
+        st = starts[(pos[:, None] >= starts[None, :]).sum(1) - 1]
+        en = torch.cat([starts[1:], torch.tensor([T], dtype=torch.int32)])[(pos[:, None] >= starts[None, :]).sum(1) - 1]
+        dd = (st.repeat(B, 1).to(torch.int32).contiguous().to(dev), en.repeat(B, 1).to(torch.int32).contiguous().to(dev))
+    K.attn_fwd(qkv, out, lse, B, T, H, Dh, True, doc=dd)
+    do = torch.randn(B * T, D, device=dev).to(torch.bfloat16)
+    cos, sin = precompute_freqs_cis(Dh, T, 10000.0)
+    cos, sin = cos.to(dev), sin.to(dev)
+    delta = torch.empty(B * H * T, device=dev)
+    ref = torch.zeros(B * T, 3 * D, device=dev, dtype=torch.bfloat16)
+    K.attn_bwd(qkv, out, do, lse, delta, ref, B, T, H, Dh, True, doc=dd)
+    K.rope(ref, T, Dh, cos, sin, backward=True, ncols=2 * D)
+    got = torch.zeros_like(ref)
+    K.attn_bwd(qkv, out, do, lse, delta, got, B, T, H, Dh, True, doc=dd, rope=(cos, sin))
+    torch.cuda.synchronize()
+    diff = (got.float() - ref.float()).abs()
+    print(f"ATTNROPE B={B} T={T}: max diff {diff.max().item():.3g}, differing {(diff > 0).float().mean().item():.2e}")
+    assert (diff > 0).float().mean().item() < 1e-4 and diff.max().item() <= 2e-2 * ref.float().abs().max().item()
+    assert torch.equal(got[:, 2 * D:], ref[:, 2 * D:])
+
+
+@pytest.mark.parametrize("R,F,Kd", [(16384, 2048, 768), (16384, 2730, 1024), (1000, 300, 128)])
+def test_gemm_swiglu_bwd_fused_matches_two_launches(dev, R, F, Kd):
+    """pcv_gemm_swiglu_bwd (the GLU VJP in the 256-wide GEMM's epilogue, dh never stored; the last case
+    takes the two-launch fallback) against gemm into dh + swiglu_bwd, pad columns included."""
+    from plaincv_amd import kernels as K
+    torch.manual_seed(9)
+    Fp = (F + 7) // 8 * 8
+    dx = torch.randn(R, Kd, device=dev).to(torch.bfloat16)
+    w2 = (torch.randn(F, Kd, device=dev) * 0.05).to(torch.bfloat16)
+    gu = torch.randn(R, 2 * Fp, device=dev).to(torch.bfloat16)
+    dh = torch.empty(R, Fp, device=dev, dtype=torch.bfloat16)[:, :F]
+    ref = torch.full((R, 2 * Fp), 7.0, device=dev, dtype=torch.bfloat16)
+    K.gemm(dx, w2, dh, tb=True)
+    K.swiglu_bwd(dh, gu, ref, F=F)
+    got = torch.full_like(ref, 7.0)
+    K.gemm_swiglu_bwd(dx, w2, gu, got, torch.empty(R, Fp, device=dev, dtype=torch.bfloat16)[:, :F], F)
+    torch.cuda.synchronize()
+    diff = (got.float() - ref.float()).abs()
+    print(f"GEMMSWIGLU R={R} F={F}: max diff {diff.max().item():.3g}, differing {(diff > 0).float().mean().item():.2e}")
+    assert (diff > 0).float().mean().item() < 1e-4 and diff.max().item() <= 2e-2 * ref.float().abs().max().item()
+    assert torch.equal(got[:, F:Fp], torch.zeros_like(got[:, F:Fp]))
