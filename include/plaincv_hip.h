@@ -58,6 +58,14 @@ int pcv_gemm_big_enable(int on);
 int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb);
 int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                  int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale, void* stream);
+/* C[M,N] (bf16) = A[M,K] . B[N,K]^T and delta[(b H + h) T + t] = <C[row, head h], attn_o[row, head h]>
+ * (head width N / H in {32, 64}, row = b T + t): pcv_gemm_bf16's attn_delta epilogue on the 256-wide
+ * kernel, which pcv_gemm_bf16 takes by itself for eligible shapes (PCV_EINVAL otherwise).  Replaces the
+ * LM's out-projection data gradient and the attention VJP's row constant (transformer.py:246-253,
+ * 228-240). */
+int pcv_gemm_big_attn_delta(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                            int64_t ldb, int64_t ldc, const void* attn_o, int64_t ld_o, float* delta, int T, int H,
+                            void* stream);
 /* C[M,N] (bf16) = A[M,K] . B[N,K]^T with the forward RoPE on columns [0, rope_cols) (heads of head_dim,
  * row r at position r % T, cos/sin fp32 [T][head_dim/2]): the LM's qkv Dense product and the rotation
  * of its q | k heads (models/LM/transformer.py:194-201, embedding.py:29-66) -- pcv_gemm_bf16 + pcv_rope in

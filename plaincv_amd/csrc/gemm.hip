@@ -25,6 +25,9 @@ extern "C" int pcv_gemm_big_ok(int64_t M, int64_t N, int64_t K, const void* A, i
 extern "C" int pcv_gemm_big(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                             int64_t ldb, int64_t ldc, float alpha, const void* res, int64_t ldr, float res_scale,
                             void* stream);
+extern "C" int pcv_gemm_big_attn_delta(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
+                                       int64_t lda, int64_t ldb, int64_t ldc, const void* attn_o, int64_t ld_o,
+                                       float* delta, int T, int H, void* stream);
 extern "C" int pcv_gemm_stream_ok(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda, const void* B,
                                   int64_t ldb);
 extern "C" int pcv_gemm_stream(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
@@ -1281,6 +1284,11 @@ extern "C" int pcv_gemm_bf16(const void* A, const void* B, void* C,
     g.k_per_split = kps;
   }
   hipStream_t s = (hipStream_t)stream;
+  // the attention delta beside a large dO product: the 256-wide kernel's form of the same epilogue
+  if (attn_delta && !attn_o_lo && !trans_a && trans_b && alpha == 1.f && !res && !bias && !aux && act == EPI_NONE &&
+      g.drop_thresh == 0 && !colsum && pcv_gemm_big_ok(M, N, K, A, lda, B, ldb))
+    return pcv_gemm_big_attn_delta(A, B, C, M, N, K, lda, ldb, ldc, attn_o, ld_attn_o, attn_delta, attn_T, attn_H,
+                                   stream);
   // large products with both operands K-contiguous and a plain (or residual) bf16 epilogue:
   // the 256x256 8-wave ping-pong kernel (gemm_big.hip)
   // (the persistent continuous-ring form, gemm_stream.hip, first; gemm_big when it is switched off)

@@ -48,6 +48,11 @@ struct BigArgs {
   const bf16* sw_gu; bf16* sw_dgu;
   int64_t sw_ldgu, sw_lddgu;
   int sw_Fp;
+  // attention delta beside the store (pcv_gemm_big_attn_delta): the product is dO; delta[(b H + h) T +
+  // t] = <bf16 dO row, O row> over head h's dl_dh columns, summed as gemm.hip's epilogue sums it
+  const bf16* dl_o; float* dl_delta;
+  int64_t ld_dlo;
+  int dl_T, dl_H, dl_dh;
 };
 
 constexpr int GB_T = 256;                 // tile rows (M); the N width BN is a template parameter
@@ -297,6 +302,20 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
         const float x0 = bf2f(v[2 * j]), x1 = bf2f(v[2 * j + 1]);
         v[2 * j] = f2bf(x0 * c - x1 * sn);
         v[2 * j + 1] = f2bf(x1 * c + x0 * sn);
+      }
+    }
+    if (g.dl_delta) {   // 8 consecutive lanes hold one head's 8 chunks of this row (dh 64; 4 for dh 32)
+      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(g.dl_o + (int64_t)gr * g.ld_dlo + gc);
+      float d = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) d += bf2f(v[q]) * bf2f(ov[q]);
+      d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0xB1, 0xF, 0xF, false));
+      d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x4E, 0xF, 0xF, false));
+      if (g.dl_dh == 64)
+        d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x141, 0xF, 0xF, false));
+      if (gc % g.dl_dh == 0) {
+        const int64_t bb = gr / g.dl_T, t = gr % g.dl_T;
+        g.dl_delta[(bb * g.dl_H + gc / g.dl_dh) * g.dl_T + t] = d;
       }
     }
     if (vec && gc + 8 <= g.N) {
@@ -595,6 +614,31 @@ extern "C" int pcv_gemm_rope(const void* A, const void* B, void* C, int64_t M, i
   g.rcos = rope_cols ? cos_tab : nullptr; g.rsin = sin_tab;
   g.rope_cols = rope_cols; g.rope_T = T; g.rope_half = head_dim / 2;
   const int bn = big_bn(M, N) == 192 ? 192 : 256;
+  g.tiles_m = (int)((M + GB_T - 1) / GB_T);
+  g.tiles_n = (int)((N + bn - 1) / bn);
+  const int e = bn == 192 ? launch_big<192>(g, (hipStream_t)stream) : launch_big<256>(g, (hipStream_t)stream);
+  return e ? e : pcv_launch_status();
+}
+
+// C = A . B^T (bf16) and the attention backward's softmax row constant delta = <dO, O> per (row, head)
+// from the stored dO: the LM's out-projection data gradient (models/LM/transformer.py:246-253 VJP)
+// feeding the attention backward (pcv_attn_bwd with delta_ready) -- gemm.hip's attn_delta epilogue on
+// the 256-wide kernel.  Returns PCV_EINVAL when the shape is not the 256-wide kernel's (the caller then
+// takes pcv_gemm_bf16).
+extern "C" int pcv_gemm_big_attn_delta(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K,
+                                       int64_t lda, int64_t ldb, int64_t ldc, const void* attn_o, int64_t ld_o,
+                                       float* delta, int T, int H, void* stream) {
+  if (!C || !attn_o || !delta || T <= 0 || H <= 0 || N % H || M % T) return PCV_EINVAL;
+  const int64_t dh = N / H;
+  if ((dh != 32 && dh != 64) || !pcv_gemm_big_ok(M, N, K, A, lda, B, ldb)) return PCV_EINVAL;
+  if ((ldc & 7) || (ld_o & 7) || !pcv_aligned16(C) || !pcv_aligned16(attn_o)) return PCV_EALIGN;
+  BigArgs g{};
+  g.A = (const bf16*)A; g.B = (const bf16*)B; g.C = (bf16*)C;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.alpha = 1.f; g.res_scale = 0.f;
+  g.dl_o = (const bf16*)attn_o; g.ld_dlo = ld_o; g.dl_delta = delta; g.dl_T = T; g.dl_H = H; g.dl_dh = (int)dh;
+  const int bn = big_bn(M, N) == 192 ? 192 : 256;   // both multiples of dh: heads never straddle tiles
   g.tiles_m = (int)((M + GB_T - 1) / GB_T);
   g.tiles_n = (int)((N + bn - 1) / bn);
   const int e = bn == 192 ? launch_big<192>(g, (hipStream_t)stream) : launch_big<256>(g, (hipStream_t)stream);

@@ -153,6 +153,7 @@ SIGNATURES = {
     "pcv_gemm_big_enable": [I32],
     "pcv_gemm_big_ok": [I64, I64, I64, P, I64, P, I64],
     "pcv_gemm_big": [P, P, P, I64, I64, I64, I64, I64, I64, F32, P, I64, F32, P],
+    "pcv_gemm_big_attn_delta": [P, P, P, I64, I64, I64, I64, I64, I64, P, I64, P, I32, I32, P],
     "pcv_gemm_rope": [P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, I32, P, P, P],
     "pcv_gemm_swiglu_bwd": [P, P, I64, I64, I64, I64, I64, P, I64, P, I64, P, I64, P],
     "pcv_gemm_stream_enable": [I32],

@@ -481,9 +481,10 @@ def test_grouped_wgrad(dev, tile):
         assert (c - ref2).abs().max().item() < 2e-3 * max(1.0, ref2.abs().max().item())
 
 
-@pytest.mark.parametrize("B,T,H,Dh", [(4, 257, 4, 32), (2, 128, 12, 64)])
+@pytest.mark.parametrize("B,T,H,Dh", [(4, 257, 4, 32), (2, 128, 12, 64), (16, 1024, 12, 64), (8, 2048, 16, 64)])
 def test_gemm_attn_delta_epilogue(dev, B, T, H, Dh):
-    """dO GEMM epilogue computing the attention-backward delta = rowsum per head of dO * O."""
+    """dO GEMM epilogue computing the attention-backward delta = rowsum per head of dO * O (the last two:
+    the LM bench shapes, on the 256-wide kernel's form of the epilogue)."""
     from plaincv_amd import kernels as K_
     torch.manual_seed(12)
     R, D = B * T, H * Dh

@@ -21,7 +21,8 @@ LMBENCH lines):
       launches fold their partials in split order, the persistent forward / data-gradient kernel has no
       split; attention and cross-entropy are atomic-free).  Two leaf classes still sum with fp32
       atomics: the embedding table (a scatter-add over token ids, embed_bwd_kernel) and the RMSNorm
-      scales (column sums over 16 384 rows, norm_param_grad_kernel); they are held to 1e-6 relative.
+      scales (column sums over 16 384 rows, norm_param_grad_kernel); their gradients are held to 1e-6
+      relative across the two states, and the second state's update of them to check (4)'s bound.
 """
 import pytest
 import torch
@@ -108,13 +109,24 @@ def test_lm_bench_path_matches_oracle(dev, workload):
     p1 = outs[0][0].params.to_dict()
     p1b = outs[1][0].params.to_dict()
     # a matrix leaf's update depends on its own gradient and, under clipping, on the global norm, which
-    # sums the atomic leaves too: bitwise when the two clip factors agree, else within 1e-6
+    # sums the atomic leaves too: bitwise when the two clip factors agree.  The other leaves (the atomic
+    # classes, or every leaf when the clip factors differ) are checked for correctness instead: state 2's
+    # update against the oracle optimizer fed state 2's own gradients, as check (4) does for state 1 (an
+    # Adam first step g / (|g| + eps) turns the 1e-6 gradient differences of near-zero elements into
+    # larger update differences, so a cross-run bound on them would measure eps, not the kernels)
     same_scale = clip is None or outs[0][0].gscale.item() == outs[1][0].gscale.item()
+    loose = []
     for k in p1:
         if same_scale and not atomic(k):
             assert torch.equal(p1[k], p1b[k]), ("params not run-to-run identical", k)
         else:
-            assert rel(p1b[k] - p0[k], p1[k] - p0[k], 1e-30) <= 1e-5, k
+            loose.append(k)
+    if loose:
+        tx2 = oopt.get_optimizer(cfg)
+        u2, _ = tx2.update(clip_grads(g_hip2, clip), tx2.init(dict(init)), p0)
+        for k in loose:
+            e = step_rel(p0[k], p1b[k], u2[k])
+            assert e <= step_bound(cfg.optim, k, p0[k]), ("second state's update", workload, k, e)
     n_hip, n_or = global_norm(g_hip), global_norm(g_b)
     print(f"LMBENCH {workload} gnorm hip {n_hip:.5f} oracle {n_or:.5f}")
     assert abs(n_hip - n_or) <= 3e-2 * n_or, (n_hip, n_or)
