@@ -579,10 +579,11 @@ def lm_roofline(st, ms_per_micro):
             2.0 * R * r.V * d, 1)
         add("lm_head data gradient", nt, lambda: K.gemm(r.logits, r.WhK, r.dy, tb=True), 2.0 * R * r.V * d, 1)
     fl_fwd = 2.0 * R * d * (3 * d + d + gu_n + r.F)
-    add("layer forward products (qkv + RoPE, out + residual, gate|up, fc2 + residual)", nt,
+    add("layer forward products (qkv + RoPE, out + residual, gate|up + GLU, fc2 + residual)", nt,
         lambda: (K.gemm_rope(r.y0[0], w["WqkvT"], r.qkv[0], T, Dh, r.cos, r.sin, 2 * d),
                  K.gemm(r.o[0], w["WoT"], r.x1[0], tb=True, res=r.x[0]),
-                 K.gemm(r.y1[0], w["WguT"], r.gu[0], tb=True),
+                 (K.gemm_swiglu_fwd(r.y1[0], w["WguI"], r.gu[0], r.hm[0], r.F) if r.swiglu_fused else
+                  K.gemm(r.y1[0], w["WguT"], r.gu[0], tb=True)),
                  K.gemm(r.hm[0], w["W2T"], r.x[1], tb=True, res=r.x1[0])), fl_fwd, L)
     dgu = r.dgu if r.glu else r.dgu[:, : r.F]
     add("layer data-gradient products (fc2 + GLU backward, gate|up, qkv; out with the attention delta)", nt,

@@ -74,6 +74,15 @@ int pcv_gemm_big_attn_delta(const void* A, const void* B, void* C, int64_t M, in
 int pcv_gemm_rope(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                   int64_t ldc, int rope_cols, int T, int head_dim, const float* cos_tab, const float* sin_tab,
                   void* stream);
+/* gu = A[M,K] . W_gu^T ([gate | up] halves Fp = F rounded to 8 apart, pads 0) and h = silu(gate) * up
+ * ([M][ldh >= Fp], pads 0) in one pass: the LM's fc_gate / fc_up products and the GLU
+ * (models/LM/transformer.py:110-134).  Bi = the weight rows K-contiguous, interleaved in 128-row blocks
+ * ([gate rows 128j..128j+127 | up rows 128j..] per block j, zero rows past F; 256 ceil(F/128) rows).
+ * pcv_gemm_swiglu_fwd_ok(): whether the 256-wide kernel takes the product (otherwise run pcv_gemm_bf16 on
+ * the plain layout + pcv_swiglu_fwd). */
+int pcv_gemm_swiglu_fwd_ok(int64_t M, int64_t F, int64_t K, const void* A, int64_t lda, const void* Bi, int64_t ldb);
+int pcv_gemm_swiglu_fwd(const void* A, const void* Bi, int64_t M, int64_t F, int64_t K, int64_t lda, int64_t ldb,
+                        void* gu, int64_t ldgu, void* h, int64_t ldh, void* stream);
 /* dgu = SwiGLU VJP of dh = A[M,K] . B[F,K]^T against gu = [gate | up] (halves Fp = F rounded to 8
  * apart; pad columns of dgu written 0): the LM's fc2 data gradient and the GLU backward
  * (models/LM/transformer.py:110-134) in one pass, dh never stored; products the 256-wide kernel does

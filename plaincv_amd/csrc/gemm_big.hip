@@ -53,6 +53,13 @@ struct BigArgs {
   const bf16* dl_o; float* dl_delta;
   int64_t ld_dlo;
   int dl_T, dl_H, dl_dh;
+  // SwiGLU forward beside the store (pcv_gemm_swiglu_fwd; 256-wide tiles): B's rows are the [gate | up]
+  // weight rows interleaved in 128-row blocks (tile n = features 128n .. 128n+127: gate columns 0-127,
+  // up columns 128-255), so one tile holds both halves of its features; the epilogue writes gu in the
+  // standard layout (gate at feature f, up at gl_Fp + f of C) and h = silu(gate) * up (pads 0)
+  bf16* gl_h;
+  int64_t gl_ldh;
+  int gl_F, gl_Fp;
 };
 
 constexpr int GB_T = 256;                 // tile rows (M); the N width BN is a template parameter
@@ -264,6 +271,26 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
         *reinterpret_cast<bf16*>(smem + row * C::CLD + col * 2) = f2bf(g.alpha * acc[i][j][r]);
       }
   __syncthreads();
+  if (g.gl_h) {   // 16 gate chunks of 8 features per row; the up chunk sits 128 columns to the right
+    for (int e = tid; e < GB_T * 16; e += 512) {
+      const int row = e >> 4, cc = (e & 15) * 8;
+      const int gr = m0 + row, f0 = (n0 >> 1) + cc;
+      if (gr >= g.M || f0 >= g.gl_Fp) continue;
+      const bf16x8 vg = *reinterpret_cast<const bf16x8*>(smem + row * C::CLD + cc * 2);
+      const bf16x8 vu = *reinterpret_cast<const bf16x8*>(smem + row * C::CLD + (128 + cc) * 2);
+      bf16x8 hv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = bf2f(vg[j]);
+        hv[j] = f2bf(f0 + j < g.gl_F ? x / (1.f + __expf(-x)) * bf2f(vu[j]) : 0.f);
+      }
+      bf16* cp = g.C + (int64_t)gr * g.ldc + f0;
+      *reinterpret_cast<bf16x8*>(cp) = vg;
+      *reinterpret_cast<bf16x8*>(cp + g.gl_Fp) = vu;
+      *reinterpret_cast<bf16x8*>(g.gl_h + (int64_t)gr * g.gl_ldh + f0) = hv;
+    }
+    return;
+  }
   const bool vec = ((g.ldc & 7) == 0) && ((uintptr_t)g.C & 15) == 0 &&
                    (!g.res || (((g.ldr & 7) == 0) && ((uintptr_t)g.res & 15) == 0));
   constexpr int CPR = BN / 8;   // 8-column chunks per row
@@ -642,6 +669,36 @@ extern "C" int pcv_gemm_big_attn_delta(const void* A, const void* B, void* C, in
   g.tiles_m = (int)((M + GB_T - 1) / GB_T);
   g.tiles_n = (int)((N + bn - 1) / bn);
   const int e = bn == 192 ? launch_big<192>(g, (hipStream_t)stream) : launch_big<256>(g, (hipStream_t)stream);
+  return e ? e : pcv_launch_status();
+}
+
+// gu = A . W_gu (gate | up halves Fp = F rounded to 8 apart) and h = silu(gate) * up in one pass: the
+// LM's fc_gate / fc_up products and the GLU (models/LM/transformer.py:110-134) -- Bi holds the weight
+// rows (K-contiguous) interleaved in 128-row blocks, [gate 128 | up 128] per block (zero rows past F),
+// Ni = 256 * ceil(F / 128) rows.  Same values as pcv_gemm_bf16 into gu + pcv_swiglu_fwd.
+// pcv_gemm_swiglu_fwd_ok tells whether the 256-wide kernel takes the product; otherwise the caller runs
+// the two launches on the plain layout.
+static int gl_ni(int64_t F) { return (int)(256 * ((F + 127) / 128)); }
+extern "C" int pcv_gemm_swiglu_fwd_ok(int64_t M, int64_t F, int64_t K, const void* A, int64_t lda, const void* Bi,
+                                      int64_t ldb) {
+  if (F <= 0 || !g_big_enabled || !big_shape_ok(M, gl_ni(F), K, A, lda, Bi, ldb)) return 0;
+  const int64_t t = ((M + GB_T - 1) / GB_T) * (gl_ni(F) / 256);
+  return (t >= 512 || (t >= 256 && t % 256 == 0)) ? 1 : 0;
+}
+extern "C" int pcv_gemm_swiglu_fwd(const void* A, const void* Bi, int64_t M, int64_t F, int64_t K, int64_t lda,
+                                   int64_t ldb, void* gu, int64_t ldgu, void* h, int64_t ldh, void* stream) {
+  const int64_t Fp = (F + 7) / 8 * 8;
+  if (!pcv_gemm_swiglu_fwd_ok(M, F, K, A, lda, Bi, ldb) || !gu || !h || ldgu < 2 * Fp || ldh < Fp) return PCV_EINVAL;
+  if ((ldgu & 7) || (ldh & 7) || !pcv_aligned16(gu) || !pcv_aligned16(h)) return PCV_EALIGN;
+  BigArgs g{};
+  g.A = (const bf16*)A; g.B = (const bf16*)Bi; g.C = (bf16*)gu;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldgu;
+  g.M = (int)M; g.N = gl_ni(F); g.K = (int)K;
+  g.alpha = 1.f; g.res_scale = 0.f;
+  g.gl_h = (bf16*)h; g.gl_ldh = ldh; g.gl_F = (int)F; g.gl_Fp = (int)Fp;
+  g.tiles_m = (int)((M + GB_T - 1) / GB_T);
+  g.tiles_n = g.N / 256;
+  const int e = launch_big<256>(g, (hipStream_t)stream);
   return e ? e : pcv_launch_status();
 }
 

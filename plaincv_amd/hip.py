@@ -155,6 +155,8 @@ SIGNATURES = {
     "pcv_gemm_big": [P, P, P, I64, I64, I64, I64, I64, I64, F32, P, I64, F32, P],
     "pcv_gemm_big_attn_delta": [P, P, P, I64, I64, I64, I64, I64, I64, P, I64, P, I32, I32, P],
     "pcv_gemm_rope": [P, P, P, I64, I64, I64, I64, I64, I64, I32, I32, I32, P, P, P],
+    "pcv_gemm_swiglu_fwd_ok": [I64, I64, I64, P, I64, P, I64],
+    "pcv_gemm_swiglu_fwd": [P, P, I64, I64, I64, I64, I64, P, I64, P, I64, P],
     "pcv_gemm_swiglu_bwd": [P, P, I64, I64, I64, I64, I64, P, I64, P, I64, P, I64, P],
     "pcv_gemm_stream_enable": [I32],
     "pcv_gemm_stream_ok": [I64, I64, I64, P, I64, P, I64],

@@ -566,6 +566,28 @@ def gemm_rope(a, b, out, T, Dh, cos_tab, sin_tab, rope_cols):
              int(Dh), ptr(cos_tab), ptr(sin_tab), stream_ptr())
 
 
+def swiglu_interleaved_rows(F):
+    """Rows of the interleaved [gate | up] operand pcv_gemm_swiglu_fwd takes: 256 ceil(F / 128)."""
+    return 256 * ((F + 127) // 128)
+
+
+def gemm_swiglu_fwd_ok(y, wi, F):
+    return bool(hip.load().pcv_gemm_swiglu_fwd_ok(y.shape[0], int(F), y.shape[1], ptr(y), _ld(y), ptr(wi), _ld(wi)))
+
+
+def gemm_swiglu_fwd(y, wi, gu, h, F):
+    """gu = y . W_gu^T ([gate | up], halves Fp apart) and h = silu(gate) * up in one launch; wi = the weight
+    rows interleaved in 128-row blocks (swiglu_interleaved_rows(F) x K, zero rows past F)."""
+    R, Kd = y.shape
+    Fp = (F + 7) // 8 * 8
+    _chk(wi.shape[0] == swiglu_interleaved_rows(F) and wi.shape[1] == Kd and gu.shape[0] == R and
+         gu.shape[1] == 2 * Fp and h.shape[0] == R and _ld(h) >= Fp, "gemm_swiglu_fwd shapes")
+    _chk(all(t.dtype == BF16 and t.stride(1) == 1 for t in (y, wi, gu, h)), "gemm_swiglu_fwd dtypes")
+    _dev(y, wi, gu, h)
+    hip.call("pcv_gemm_swiglu_fwd", ptr(y), ptr(wi), R, int(F), Kd, _ld(y), _ld(wi), ptr(gu), _ld(gu), ptr(h),
+             _ld(h), stream_ptr())
+
+
 def gemm_swiglu_bwd(dx, w2, gu, dgu, dh, F):
     """dgu = swiglu_bwd(dx . w2^T, gu) without dh in HBM where the 256-wide kernel takes the product
     (else gemm into dh, then swiglu_bwd).  dx [R, K], w2 [F, K] (K-contiguous), gu / dgu [R, 2 Fp]

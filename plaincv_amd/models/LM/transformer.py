@@ -251,9 +251,25 @@ class LMRunner:
             ld = (cols + 63) // 64 * 64   # 128-B aligned rows (see self.hm)
             return torch.zeros(rows, ld, dtype=torch.bfloat16, device=dev)[:, :cols]
         pairs = []
-        for w in self.w:
+        # GLU: the [gate | up] rows interleaved in 128-row blocks, so the gate|up product's 256-wide
+        # tiles hold both halves of their 128 features and write h = silu(gate) * up beside gu
+        # (pcv_gemm_swiglu_fwd); shapes the 256-wide kernel does not take keep the plain copy
+        self.swiglu_fused = False
+        if self.glu:
+            Ni, F, Fp = K.swiglu_interleaved_rows(self.F), self.F, self.Fp
+            wi0 = t(Ni, self.d)
+            self.swiglu_fused = K.gemm_swiglu_fwd_ok(self.y1[0], wi0, F)
+        for li, w in enumerate(self.w):
             for k in ("Wqkv", "Wo", "Wgu", "W2"):
                 src = w[k]
+                if k == "Wgu" and self.swiglu_fused:
+                    wi = wi0 if li == 0 else t(Ni, self.d)
+                    w["WguI"] = wi
+                    for j in range(0, Fp, 128):
+                        n = min(128, Fp - j)
+                        pairs.append((src[:, j:j + n], wi[2 * j:2 * j + n]))
+                        pairs.append((src[:, Fp + j:Fp + j + n], wi[2 * j + 128:2 * j + 128 + n]))
+                    continue
                 dst = t(src.shape[1], src.shape[0])
                 w[k + "T"] = dst
                 pairs.append((src, dst))
@@ -310,7 +326,9 @@ class LMRunner:
             K.attn_fwd(self.qkv[i], self.o[i], self.lse[i], b, T, H, Dh, causal=True, doc=self.doc)
             K.gemm(self.o[i], w["WoT"], self.x1[i], tb=True, res=self.x[i])
             K.rmsnorm_fwd(self.x1[i], w["s1"], self.y1[i], self.r1[i], eps)
-            if self.glu:
+            if self.swiglu_fused:   # gate|up product + GLU in one pass
+                K.gemm_swiglu_fwd(self.y1[i], w["WguI"], self.gu[i], self.hm[i], self.F)
+            elif self.glu:
                 K.gemm(self.y1[i], w["WguT"], self.gu[i], tb=True)
                 K.swiglu_fwd(self.gu[i], self.hm[i], F=self.F)
             else:

@@ -1,7 +1,7 @@
 """Run-to-run bitwise reproducibility of the LM step's fused launches at the bench shapes (124M: B 16,
 T 1024, 12 heads; 420M: B 8, T 2048, 16 heads): the attention forward / backward (with and without the
 inverse RoPE in the dq / dk stores), the qkv product with the RoPE epilogue and the fc2 data gradient
-with the GLU backward epilogue.  Each launch runs four times on the same inputs with the outputs
+with the GLU backward epilogue, the gate|up product with the GLU epilogue.  Each launch runs four times on the same inputs with the outputs
 poisoned (NaN) in between; every run must equal the first bit for bit.  (The packed-fp32 code SLP
 vectorisation formed in the RoPE store gave different values in ~1 of 7000 elements from run to run on
 gfx950: csrc/Makefile NOSLP.)"""
@@ -54,3 +54,6 @@ def test_lm_launches_bitwise_reproducible(dev, B, T, H, d, F):
     dgu = torch.empty(R, 2 * Fp, device=dev, dtype=torch.bfloat16)
     dh = torch.empty(R, Fp, device=dev, dtype=torch.bfloat16)[:, :F]
     _same(lambda: K.gemm_swiglu_bwd(y, w2, gu, dgu, dh, F), [dgu])
+    wi = (torch.randn(K.swiglu_interleaved_rows(F), d, device=dev) * 0.05).to(torch.bfloat16)
+    hm = torch.empty(R, Fp, device=dev, dtype=torch.bfloat16)
+    _same(lambda: K.gemm_swiglu_fwd(y, wi, gu, hm, F), [gu, hm])

@@ -773,3 +773,36 @@ def test_gemm_swiglu_bwd_fused_matches_two_launches(dev, R, F, Kd):
     print(f"GEMMSWIGLU R={R} F={F}: max diff {diff.max().item():.3g}, differing {(diff > 0).float().mean().item():.2e}")
     assert (diff > 0).float().mean().item() < 1e-4 and diff.max().item() <= 2e-2 * ref.float().abs().max().item()
     assert torch.equal(got[:, F:Fp], torch.zeros_like(got[:, F:Fp]))
+
+
+@pytest.mark.parametrize("R,F,Kd", [(16384, 2048, 768), (16384, 2730, 1024)])
+def test_gemm_swiglu_fwd_fused_matches_two_launches(dev, R, F, Kd):
+    """pcv_gemm_swiglu_fwd (interleaved [gate | up] weight rows, GLU in the 256-wide GEMM's epilogue)
+    against gemm on the plain layout + swiglu_fwd: gu and h, pad columns included."""
+    from plaincv_amd import kernels as K
+    torch.manual_seed(11)
+    Fp = (F + 7) // 8 * 8
+    y = torch.randn(R, Kd, device=dev).to(torch.bfloat16)
+    wt = torch.zeros(2 * Fp, Kd, device=dev, dtype=torch.bfloat16)   # plain [gate | up] rows, pads 0
+    wt[:F] = (torch.randn(F, Kd, device=dev) * 0.05).to(torch.bfloat16)
+    wt[Fp:Fp + F] = (torch.randn(F, Kd, device=dev) * 0.05).to(torch.bfloat16)
+    wi = torch.zeros(K.swiglu_interleaved_rows(F), Kd, device=dev, dtype=torch.bfloat16)
+    for j in range(0, Fp, 128):
+        n = min(128, Fp - j)
+        wi[2 * j:2 * j + n] = wt[j:j + n]
+        wi[2 * j + 128:2 * j + 128 + n] = wt[Fp + j:Fp + j + n]
+    assert K.gemm_swiglu_fwd_ok(y, wi, F)
+    gu_ref = torch.empty(R, 2 * Fp, device=dev, dtype=torch.bfloat16)
+    h_ref = torch.full((R, Fp), 5.0, device=dev, dtype=torch.bfloat16)
+    K.gemm(y, wt, gu_ref, tb=True)
+    K.swiglu_fwd(gu_ref, h_ref, F=F)
+    gu = torch.full_like(gu_ref, 5.0)
+    h = torch.full_like(h_ref, 5.0)
+    K.gemm_swiglu_fwd(y, wi, gu, h, F)
+    torch.cuda.synchronize()
+    for name, a, b in (("gu", gu, gu_ref), ("h", h, h_ref)):
+        diff = (a.float() - b.float()).abs()
+        print(f"GEMMSWIGLUFWD R={R} F={F} {name}: max diff {diff.max().item():.3g}, "
+              f"differing {(diff > 0).float().mean().item():.2e}")
+        assert (diff > 0).float().mean().item() < 1e-4 and diff.max().item() <= 2e-2 * b.float().abs().max().item()
+    assert torch.equal(h[:, F:], torch.zeros_like(h[:, F:]))
