@@ -294,6 +294,28 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
   const bool vec = ((g.ldc & 7) == 0) && ((uintptr_t)g.C & 15) == 0 &&
                    (!g.res || (((g.ldr & 7) == 0) && ((uintptr_t)g.res & 15) == 0));
   constexpr int CPR = BN / 8;   // 8-column chunks per row
+  if (g.dl_delta) {   // the attention delta: its DPP row sums keep this loop rolled, so a loop of its own
+    for (int e = tid; e < GB_T * CPR; e += 512) {   // (no RoPE / residual / GLU with it: pcv_gemm_big_attn_delta)
+      const int row = e / CPR, cc = (e % CPR) * 8;
+      const int gr = m0 + row, gc = n0 + cc;
+      if (gr >= g.M || gc >= g.N) continue;   // whole heads (8 lanes) skip together
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + row * C::CLD + cc * 2);
+      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(g.dl_o + (int64_t)gr * g.ld_dlo + gc);
+      float d = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) d += bf2f(v[q]) * bf2f(ov[q]);
+      d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0xB1, 0xF, 0xF, false));
+      d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x4E, 0xF, 0xF, false));
+      if (g.dl_dh == 64)
+        d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x141, 0xF, 0xF, false));
+      if (gc % g.dl_dh == 0) {
+        const int64_t bb = gr / g.dl_T, t = gr % g.dl_T;
+        g.dl_delta[(bb * g.dl_H + gc / g.dl_dh) * g.dl_T + t] = d;
+      }
+      *reinterpret_cast<bf16x8*>(g.C + (int64_t)gr * g.ldc + gc) = v;
+    }
+    return;
+  }
 #pragma unroll 4
   for (int e = tid; e < GB_T * CPR; e += 512) {
     const int row = e / CPR, cc = (e % CPR) * 8;
@@ -329,20 +351,6 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(BigArgs g) {
         const float x0 = bf2f(v[2 * j]), x1 = bf2f(v[2 * j + 1]);
         v[2 * j] = f2bf(x0 * c - x1 * sn);
         v[2 * j + 1] = f2bf(x1 * c + x0 * sn);
-      }
-    }
-    if (g.dl_delta) {   // 8 consecutive lanes hold one head's 8 chunks of this row (dh 64; 4 for dh 32)
-      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(g.dl_o + (int64_t)gr * g.ld_dlo + gc);
-      float d = 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) d += bf2f(v[q]) * bf2f(ov[q]);
-      d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0xB1, 0xF, 0xF, false));
-      d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x4E, 0xF, 0xF, false));
-      if (g.dl_dh == 64)
-        d += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, d), 0x141, 0xF, 0xF, false));
-      if (gc % g.dl_dh == 0) {
-        const int64_t bb = gr / g.dl_T, t = gr % g.dl_T;
-        g.dl_delta[(bb * g.dl_H + gc / g.dl_dh) * g.dl_T + t] = d;
       }
     }
     if (vec && gc + 8 <= g.N) {
