@@ -1298,19 +1298,33 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_fwd_kernel(AttnArgs 
       }
     }
     const float inv = (DROP ? a.drop_scale : 1.f) / l;
+    // O (and its rounding residual) leave through this group's own Q rows in LDS -- read into qf above
+    // and by no other wave -- as one 16-B row chunk per lane (per-lane 2-B stores at a row stride cost
+    // as much as the rest of the store tail)
+    bf16* ot = Qs + gq * 16 * DH;   // [16][DH] plain
+    float ov[DT][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float iv = __shfl(inv, 4 * g + r, 64);
-      const int qq = gq * 16 + 4 * g + r;
-      if (qq < T) {
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        ov[d][r] = acc[d][r] * iv;
+        ot[(4 * g + r) * DH + 16 * d + (lane & 15)] = f2bf(ov[d][r]);
+      }
+    }
+    const int orow = lane / (DH / 8), oc = (lane % (DH / 8)) * 8, oq = gq * 16 + orow;
+    const bf16x8 hv = *reinterpret_cast<const bf16x8*>(ot + orow * DH + oc);
+    if (oq < T) *reinterpret_cast<bf16x8*>(a.out + (bT + oq) * a.ldout + h * DH + oc) = hv;
+    if (a.out_lo) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int d = 0; d < DT; ++d) {
-          const float o = acc[d][r] * iv;
-          const bf16 oh = f2bf(o);
-          a.out[(bT + qq) * a.ldout + h * DH + 16 * d + (lane & 15)] = oh;
-          if (a.out_lo) a.out_lo[(bT + qq) * a.ldout + h * DH + 16 * d + (lane & 15)] = f2bf(o - bf2f(oh));
+          const int e = (4 * g + r) * DH + 16 * d + (lane & 15);
+          ot[e] = f2bf(ov[d][r] - bf2f(ot[e]));
         }
-      }
+      const bf16x8 lv = *reinterpret_cast<const bf16x8*>(ot + orow * DH + oc);
+      if (oq < T) *reinterpret_cast<bf16x8*>(a.out_lo + (bT + oq) * a.ldout + h * DH + oc) = lv;
     }
     if (g == 0 && qv) a.lse2[((int64_t)b * a.H + h) * T + myq] = m2 + log2f(l);
   }
@@ -1524,15 +1538,18 @@ __global__ __launch_bounds__(SH_THREADS, 1) void attn_short_bwd_kernel(AttnArgs 
           tq[j] += dpp_row_sum16(dsb * bf2f(kf[j]));
         }
       }
-      if (mykey < T) {
+      if (mykey < T) {   // this lane's 4 consecutive dims of each 16-dim block: one 8-B store each
 #pragma unroll
-        for (int d = 0; d < DT; ++d)
+        for (int d = 0; d < DT; ++d) {
+          bf16x4 v4, k4;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int dd = 16 * d + 4 * g + r;
-            a.dv[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(DROP ? dv[d][r] * a.drop_scale : dv[d][r]);
-            a.dk[(bT + mykey) * a.lddq + h * DH + dd] = f2bf(dk[d][r] * a.scale);
+            v4[r] = f2bf(DROP ? dv[d][r] * a.drop_scale : dv[d][r]);
+            k4[r] = f2bf(dk[d][r] * a.scale);
           }
+          *reinterpret_cast<bf16x4*>(a.dv + (bT + mykey) * a.lddq + h * DH + 16 * d + 4 * g) = v4;
+          *reinterpret_cast<bf16x4*>(a.dk + (bT + mykey) * a.lddq + h * DH + 16 * d + 4 * g) = k4;
+        }
       }
     }
   }
@@ -1774,6 +1791,10 @@ static int dispatch(AttnArgs a, int dh, int causal, int drop, hipStream_t s) {
   if ((a.out_lo || a.o_lo) && !short_ok(a, dh, causal, FWD)) return PCV_EINVAL;   // short path only
   if (a.o_lo && a.delta_ready) return PCV_EINVAL;                                 // delta is formed here
   if (short_ok(a, dh, causal, FWD)) {
+    // O / O_lo leave as 16-B row chunks, dK / dV as 8-B pieces
+    if (FWD ? (!pcv_aligned16(a.out) || (a.ldout & 7) || (a.out_lo && !pcv_aligned16(a.out_lo)))
+            : (((uintptr_t)a.dk & 7) || ((uintptr_t)a.dv & 7) || (a.lddq & 3)))
+      return PCV_EALIGN;
     // batch b's heads on the XCD that wrote its rows (C2: step 0.778 -> 0.768 ms)
     a.xcd_map = a.B % 8 == 0 ? 1 : 0;
     const int e = FWD ? (drop ? launch_short_fwd<true>(a, s) : launch_short_fwd<false>(a, s))

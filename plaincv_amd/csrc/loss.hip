@@ -248,20 +248,32 @@ __global__ __launch_bounds__(1024, 1) void xent_reg_kernel(const bf16* logits, i
     const int c = tid + 1024 * i;
     if (c < nv) x[i] = *reinterpret_cast<const bf16x8*>(z + (int64_t)c * 8);
   }
-  // tail elements (V % 8) belong to thread 0
+  // tail elements (V % 8) belong to thread 0.
+  // VALU per element kept low (the kernel was as much VALU- as HBM-bound): the max as v_max3 trees per
+  // chunk with the first index recovered once from the winning chunk; exp(z - c) as exp2(z log2e - c log2e)
+  // by one fma; the label's -1 applied to its one chunk.
   const int tail0 = nv * 8;
+  constexpr float L2E = 1.4426950408889634f;
   float m = -3.0e38f;
-  int am = 0x7fffffff;
+  int mc = -1;
 #pragma unroll
   for (int i = 0; i < XR_CH; ++i) {
     const int c = tid + 1024 * i;
     if (c < nv) {
+      float f[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float v = bf2f(x[i][q]);
-        if (v > m) { m = v; am = c * 8 + q; }   // increasing index order: strict > keeps the first
-      }
+      for (int q = 0; q < 8; ++q) f[q] = bf2f(x[i][q]);
+      const float cm = fmaxf(fmaxf(fmaxf(f[0], f[1]), fmaxf(f[2], f[3])), fmaxf(fmaxf(f[4], f[5]), fmaxf(f[6], f[7])));
+      if (cm > m) { m = cm; mc = i; }   // increasing index order: strict > keeps the first chunk
     }
+  }
+  int am = 0x7fffffff;
+  if (mc >= 0) {
+    bf16x8 xc = x[0];
+#pragma unroll
+    for (int i = 1; i < XR_CH; ++i) xc = (i == mc) ? x[i] : xc;
+#pragma unroll
+    for (int q = 7; q >= 0; --q) am = bf2f(xc[q]) == m ? (tid + 1024 * mc) * 8 + q : am;
   }
   if (tid == 0)
     for (int j = tail0; j < V; ++j) {
@@ -281,13 +293,14 @@ __global__ __launch_bounds__(1024, 1) void xent_reg_kernel(const bf16* logits, i
 #pragma unroll
   for (int i = 1; i < 16; ++i)
     if (rm[i] > M || (rm[i] == M && ri[i] < A)) { M = rm[i]; A = ri[i]; }
+  const float nml = -M * L2E;
   float sum = 0.f;
 #pragma unroll
   for (int i = 0; i < XR_CH; ++i) {
     const int c = tid + 1024 * i;
     if (c < nv) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) sum += __expf(bf2f(x[i][q]) - M);
+      for (int q = 0; q < 8; ++q) sum += __builtin_amdgcn_exp2f(fmaf(bf2f(x[i][q]), L2E, nml));
     }
   }
   if (tid == 0)
@@ -308,16 +321,25 @@ __global__ __launch_bounds__(1024, 1) void xent_reg_kernel(const bf16* logits, i
   if (!dlogits) return;
   __syncthreads();   // z[y] and the tail read above before an in-place overwrite
   bf16* d = dlogits + row * ldd;
+  // p * grad_scale = exp2(z log2e - (lse log2e - log2(grad_scale)))  (grad_scale > 0)
+  const bool fast = grad_scale > 0.f;
+  const float nlg = fast ? -(lse * L2E - __log2f(grad_scale)) : 0.f;
+  const int yc = yok ? y >> 3 : -1;
 #pragma unroll
   for (int i = 0; i < XR_CH; ++i) {
     const int c = tid + 1024 * i;
     if (c < nv) {
       bf16x8 o;
+      if (fast && c != yc) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float p = __expf(bf2f(x[i][q]) - lse);
-        if (c * 8 + q == y) p -= 1.f;
-        o[q] = f2bf(p * grad_scale);
+        for (int q = 0; q < 8; ++q) o[q] = f2bf(__builtin_amdgcn_exp2f(fmaf(bf2f(x[i][q]), L2E, nlg)));
+      } else {   // the label's chunk (and grad_scale <= 0): softmax - onehot, as the reference forms it
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float p = __expf(bf2f(x[i][q]) - lse);
+          if (c * 8 + q == y) p -= 1.f;
+          o[q] = f2bf(p * grad_scale);
+        }
       }
       *reinterpret_cast<bf16x8*>(d + (int64_t)c * 8) = o;
     }

@@ -259,6 +259,16 @@ def test_rope_swiglu_xent_embed(dev):
     assert torch.equal(rc3, (rows % 2 == 0).float())
     assert torch.allclose(rl3, torch.nn.functional.cross_entropy(lg3.float(), lab3.long(), reduction="none"),
                           atol=1e-3, rtol=1e-4)
+    # ties inside one 16-B chunk (the kernel recovers the first index from the winning chunk)
+    buf4 = torch.randn(R, 50264, device=dev).to(torch.bfloat16)
+    lg4 = buf4[:, :V]
+    k8 = torch.randint(0, V // 8 - 1, (R,), device=dev) * 8
+    lg4[rows, k8 + 2] = 9.0
+    lg4[rows, k8 + 5] = 9.0
+    lab4 = torch.where(rows % 2 == 0, k8 + 2, k8 + 5).to(torch.int32)
+    rl4, rc4 = torch.empty(R, device=dev), torch.empty(R, device=dev)
+    K.xent(lg4, lab4, rl4, rc4, None, grad_scale=1.0)
+    assert torch.equal(rc4, (rows % 2 == 0).float())
     # embedding
     Vv, Dd = 1000, 64
     tab = torch.randn(Vv, Dd, device=dev).to(torch.bfloat16)
