@@ -175,6 +175,13 @@ class LMRunner:
         # backward workspaces
         self.dx = e(R, d)
         self.dy = e(R, d)
+        # RMSNorm scale gradients (column sums over the token rows, HBM-bound) run on a side stream beside
+        # the next launches; the norm inputs dy alternate between two buffers so a GEMM writing the next dy
+        # never waits on the column sums of the previous one
+        self.dys = [self.dy, e(R, d)]
+        self._pg = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        self._pg_ev = [None, None]
+        self._nk = 0
         self.dh = e(R, Fl)[:, : self.F]
         self.dgu = e(R, nml)[:, :nmlp]
         self.do = e(R, d)
@@ -345,6 +352,32 @@ class LMRunner:
         K.mean2(self.row_loss, self.row_correct, self.R, 1.0 / self.R, self.metrics)
         return self.metrics
 
+    def _next_dy(self):
+        """The dy buffer the next norm VJP reads; the compute stream waits until the side stream has
+        finished the column sums that last read it."""
+        k = self._nk % 2
+        self._nk += 1
+        if self._pg_ev[k] is not None:
+            torch.cuda.current_stream().wait_event(self._pg_ev[k])
+        return k, self.dys[k]
+
+    def _norm_bwd(self, k, dy, x, scale, rstd, dres, dx, dscale):
+        """RMSNorm VJP on the compute stream, its scale gradient on the side stream after it."""
+        if self._pg is None:
+            K.rmsnorm_bwd(dy, x, scale, rstd, dres, dx, dscale)
+            return
+        K.rmsnorm_bwd(dy, x, scale, rstd, dres, dx, None)
+        self._pg.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self._pg):
+            K.rmsnorm_param_grad(dy, x, rstd, dscale)
+            ev = torch.cuda.Event()
+            ev.record(self._pg)
+        self._pg_ev[k] = ev
+
+    def _join_side(self):
+        if self._pg is not None:
+            torch.cuda.current_stream().wait_stream(self._pg)
+
     def backward(self, on_ready=None):
         """on_ready(offset): called (host side, in stream order) whenever the flat gradient above
         `offset` is final -- after the head, after each layer, after the embedding -- so a data-
@@ -359,12 +392,14 @@ class LMRunner:
             K.gemm(dl, self.yf, self.gWemb, ta=True, beta=1.0)
         else:
             K.gemm(self.yf, dl, self.gWh, ta=True, beta=1.0)
+        k, dy = self._next_dy()
         if c.tie_embeddings:
-            K.gemm(dl, self.Wemb, self.dy, tb=False)
+            K.gemm(dl, self.Wemb, dy, tb=False)
         else:
-            K.gemm(dl, self.WhK, self.dy, tb=True)
-        K.rmsnorm_bwd(self.dy, self.x[-1], self.sf, self.rf, None, self.dxb[0], self.gsf)
+            K.gemm(dl, self.WhK, dy, tb=True)
+        self._norm_bwd(k, dy, self.x[-1], self.sf, self.rf, None, self.dxb[0], self.gsf)
         if on_ready is not None:
+            self._join_side()
             on_ready(self._ready_off["head"])
         L = c.n_layers
         for i in reversed(range(L)):
@@ -384,8 +419,9 @@ class LMRunner:
                 dgu = self.dgu[:, : self.F]
             if not grouped:
                 K.gemm(self.y1[i], dgu, w["gWgu"], ta=True, beta=1.0)
-            K.gemm(dgu, w["Wgu"], self.dy, tb=True)
-            K.rmsnorm_bwd(self.dy, self.x1[i], w["s1"], self.r1[i], dx_in, dx_mid, w["gs1"])
+            k, dy = self._next_dy()
+            K.gemm(dgu, w["Wgu"], dy, tb=True)
+            self._norm_bwd(k, dy, self.x1[i], w["s1"], self.r1[i], dx_in, dx_mid, w["gs1"])
             if not grouped:
                 K.gemm(self.o[i], dx_mid, w["gWo"], ta=True, beta=1.0)
             K.gemm(dx_mid, w["Wo"], self.do, tb=True, attn_delta=(self.o[i], self.delta, T, H))   # + delta
@@ -395,11 +431,15 @@ class LMRunner:
                 self.wg_layers[i](beta=1.0)   # fc2, gate|up, out, qkv weight gradients: one launch
             else:
                 K.gemm(self.y0[i], self.dqkv, w["gWqkv"], ta=True, beta=1.0)
-            K.gemm(self.dqkv, w["Wqkv"], self.dy, tb=True)
-            K.rmsnorm_bwd(self.dy, self.x[i], w["s0"], self.r0[i], dx_mid, dx_out, w["gs0"])
+            k, dy = self._next_dy()
+            K.gemm(self.dqkv, w["Wqkv"], dy, tb=True)
+            self._norm_bwd(k, dy, self.x[i], w["s0"], self.r0[i], dx_mid, dx_out, w["gs0"])
             if on_ready is not None and i > 0:
+                self._join_side()
                 on_ready(self._ready_off[i])
         dx_fin = self.dxb[(2 * L) % 3] if grouped else self.dxb[0]
         K.embed_bwd(self.inputs, dx_fin, self.gWemb)
+        # the next forward rewrites the norm inputs the side stream reads; every gradient final here
+        self._join_side()
         if on_ready is not None:
             on_ready(0)
