@@ -4,7 +4,10 @@
 // every LM forward GEMM (activations x K-contiguous weight copies: qkv, out, gate|up, fc2,
 // lm_head) and the data-gradient GEMMs (dY x W^T) of models/LM/transformer.py:194-201,
 // 246-253, 110-134, 393-405.  Dispatched from pcv_gemm_bf16 when the product has enough
-// 256x256 tiles to fill the chip and no fused epilogue beyond a residual.
+// 256x256 tiles to fill the chip and no fused epilogue beyond a residual (or the attention delta);
+// the LM's fused forms enter through their own entries below: pcv_gemm_rope (qkv + RoPE),
+// pcv_gemm_swiglu_fwd (gate|up + GLU), pcv_gemm_swiglu_bwd (fc2 data gradient + GLU backward),
+// pcv_gemm_big_attn_delta (out-projection data gradient + the attention delta).
 //
 // Structure (MI355X: 2 waves per SIMD, the two halves of the workgroup ping-pong):
 //   * 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns a 128 x 64 output block,
@@ -26,7 +29,8 @@
 //            were retired by their lgkmcnt(0) before a barrier the issuer has passed.
 //     No __syncthreads() in the loop (it would add vmcnt(0) and drain the prefetch).
 //   * a ragged K tail (K % 32) goes through registers with zero fill after the ring drains;
-//   * the bf16 tile is staged through LDS and stored as 16-byte rows (+ residual).
+//   * the bf16 tile is staged through LDS and stored as 16-byte rows (+ residual, or one of the
+//     fused epilogues, each applied to the bf16-rounded tile exactly as its standalone kernel would).
 #include "common.h"
 #include <cstdlib>
 #include <type_traits>
