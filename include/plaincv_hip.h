@@ -444,6 +444,19 @@ int pcv_gemm_f32_rows_lnout(const float* A, int64_t lda, const float* B, int64_t
                             int64_t ws_floats, void* stream);
 /* floats of pcv_gemm_f32_rows_lnout's split-tail workspace at (M, K) (0: none; zeroed, one launch at a time) */
 int64_t pcv_gemm_f32_rows_lnout_ws_floats(int64_t M, int64_t K);
+/* dy = A B^T (B stored [N][K], N = 128; dy is not stored), then the LayerNorm VJP of every dy row: dx = dres +
+ * rstd (g - mean(g) - xhat mean(g xhat)), g = dy scale, xhat = (x - mean) rstd (pcv_layernorm_bwd_f32's
+ * arithmetic); dxd (optional) = dropout_vjp(dx) (rate, seed, site, index row * N + col); the column sums of
+ * dy xhat / dy of each 32-row tile -> part[tile][0, N) / [N, 2 N) for pcv_layernorm_part_reduce (nblk =
+ * ceil(M / 32); part_floats >= pcv_gemm_f32_rows_lnbwd_part_floats).  The ViT's MLP Dense_0 data gradient ->
+ * LayerNorm_1 VJP and qkv data gradient -> LayerNorm_0 VJP (models/vit_small.py:46-56, :38) in one launch.
+ * ws (optional, pcv_gemm_f32_rows_lnout_ws_floats(M, K)): the split tail, as pcv_gemm_f32_rows_lnout. */
+int pcv_gemm_f32_rows_lnbwd(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
+                            const float* x, int64_t ldx, const float* scale, const float* mean, const float* rstd,
+                            const float* dres, int64_t ldres, float* dx, int64_t lddx, float* part,
+                            int64_t part_floats, float* dxd, int64_t lddxd, float rate, const uint32_t* seed,
+                            uint32_t site, float* ws, int64_t ws_floats, void* stream);
+int64_t pcv_gemm_f32_rows_lnbwd_part_floats(int64_t M, int64_t N);
 /* pcv_gemm_f32_rows with a workspace for the split tail of its tiled form (data-gradient products, no
  * epilogue: the few tiles past a whole number of 4-per-CU rounds run as K slices beside the first round, the
  * tile's last slice adding the slabs in order); pcv_gemm_f32_rows_ws_floats gives the floats needed (0: no

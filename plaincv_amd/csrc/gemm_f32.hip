@@ -44,6 +44,11 @@ struct GrArgs {
   // in slice order and runs the epilogue; the other workgroups are the row tiles of [0, tail_m0)
   float* tail_ws; unsigned* tail_cnt;
   int tail_blocks, tail_split, tail_m0;
+  // LNB (pcv_gemm_f32_rows_lnbwd): C = dy is not stored; the LayerNorm VJP of each finished row instead --
+  // x rows lb_x, scale ln_s, statistics ln_mean / ln_rstd, residual gradient res (ldr), dx -> ln_y (ldy),
+  // dropout_vjp(dx) -> lb_dxd, the tile's column sums of dy xhat / dy -> lb_part row m0 / BM
+  const float* lb_x; float* lb_part; float* lb_dxd;
+  int64_t lb_ldx, lb_lddxd;
 };
 
 // GELU (tanh form): 0.5 x (1 + tanh(u)) = x / (1 + exp(-2u)), u = sqrt(2/pi) (x + 0.044715 x^3) --
@@ -224,8 +229,8 @@ __device__ __forceinline__ f32x4 gr_epi_apply(const GrArgs& g, f32x4 v, const Gr
   return v;
 }
 
-template <bool TB, bool EPI, int BN, int BM, bool LNO = false, int NT = 256>
-__global__ __launch_bounds__(NT, LNO ? 6 : 1) void gemm_f32_rows_kernel(GrArgs g) {
+template <bool TB, bool EPI, int BN, int BM, bool LNO = false, int NT = 256, bool LNB = false>
+__global__ __launch_bounds__(NT, (LNO || LNB) ? 6 : 1) void gemm_f32_rows_kernel(GrArgs g) {
   // operand images during the main loop; the C tile [BM][BN + 4] for the epilogue afterwards
   __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * GR_LDK];
   static_assert(BM * (BN + 4) <= (BM + BN) * GR_LDK, "C tile fits the operand images");
@@ -266,7 +271,7 @@ __global__ __launch_bounds__(NT, LNO ? 6 : 1) void gemm_f32_rows_kernel(GrArgs g
       pin[it] = gr_epi_load(g, min(m0 + idx / Q, g.M - 1), n0 + (idx % Q) * 4);
     }
   }
-  const uint32_t seed = (EPI && g.thresh) ? *g.seed : 0u;
+  const uint32_t seed = ((EPI || LNB) && g.thresh) ? *g.seed : 0u;
   gr_mainloop<false, TB, BN, BM, NT>(g.A, g.lda, g.B, g.ldb, g.M, m0, n0, kb, ke, As, Bs, acc);
   if (tail) {
     // the slice's partial tile -> its slab (thread-major register order), published with one agent-scope
@@ -315,6 +320,7 @@ __global__ __launch_bounds__(NT, LNO ? 6 : 1) void gemm_f32_rows_kernel(GrArgs g
 #pragma unroll
       for (int j = 0; j < NJ; ++j) smem[(wm * 32 + i * 16 + 4 * g4 + r) * LDC + wn * WN + j * 16 + c16] = acc[i][j][r];
   __syncthreads();
+  f32x4 pa{0.f, 0.f, 0.f, 0.f}, pb{0.f, 0.f, 0.f, 0.f};   // (LNB: this thread's column partials)
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int idx = threadIdx.x + NT * it, rl = idx / Q, cl = (idx % Q) * 4;
@@ -322,6 +328,37 @@ __global__ __launch_bounds__(NT, LNO ? 6 : 1) void gemm_f32_rows_kernel(GrArgs g
     if (row >= g.M) continue;
     f32x4 v = *reinterpret_cast<const f32x4*>(&smem[rl * LDC + cl]);
     if (EPI) v = gr_epi_apply(g, v, PRE ? pin[PRE ? it : 0] : gr_epi_load(g, row, col), row, col, seed);
+    if constexpr (LNB) {   // the row's LayerNorm VJP (pcv_layernorm_bwd_f32's arithmetic): its Q = 32 float4
+      static_assert(BN == 128 && !EPI && !LNO, "a whole dy row per tile");   // in 32 consecutive lanes
+      const float mu = g.ln_mean[row], rs = g.ln_rstd[row];
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(g.lb_x + (int64_t)row * g.lb_ldx + cl);
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(g.ln_s + cl);
+      const f32x4 r = g.res ? *reinterpret_cast<const f32x4*>(g.res + (int64_t)row * g.ldr + cl) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 xh = (xv - mu) * rs, gg = v * sc;
+      float sg = gg[0] + gg[1] + gg[2] + gg[3];
+      float sgx = gg[0] * xh[0] + gg[1] * xh[1] + gg[2] * xh[2] + gg[3] * xh[3];
+#pragma unroll
+      for (int o = 1; o < Q; o <<= 1) {
+        sg += __shfl_xor(sg, o, Q);
+        sgx += __shfl_xor(sgx, o, Q);
+      }
+      sg /= BN;
+      sgx /= BN;
+      const f32x4 dx = r + rs * (gg - sg - xh * sgx);
+      *reinterpret_cast<f32x4*>(g.ln_y + (int64_t)row * g.ldy + cl) = dx;
+      if (g.lb_dxd) {   // the next consumer's dropout VJP (flat index row * D + col, as ln16_bwd_f32_kernel)
+        f32x4 od = dx;
+        if (g.thresh) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            od[e] = hash3(seed, (uint32_t)g.site, (uint32_t)((int64_t)row * BN + cl + e)) >= g.thresh ? dx[e] * g.dscale : 0.f;
+        }
+        *reinterpret_cast<f32x4*>(g.lb_dxd + (int64_t)row * g.lb_lddxd + cl) = od;
+      }
+      pa += v * xh;
+      pb += v;
+      continue;
+    }
     *reinterpret_cast<f32x4*>(g.C + (int64_t)row * g.ldc + col) = v;
     if constexpr (LNO) {   // the row's LayerNorm: its Q = 32 float4 sit in 32 consecutive lanes (BN = N = 128)
       static_assert(BN == 128, "a whole row per tile");
@@ -335,6 +372,21 @@ __global__ __launch_bounds__(NT, LNO ? 6 : 1) void gemm_f32_rows_kernel(GrArgs g
       const f32x4 sc = *reinterpret_cast<const f32x4*>(g.ln_s + cl), bi = *reinterpret_cast<const f32x4*>(g.ln_c + cl);
       *reinterpret_cast<f32x4*>(g.ln_y + (int64_t)row * g.ldy + cl) = (v - mu) * rs * sc + bi;
       if (cl == 0) { g.ln_mean[row] = mu; g.ln_rstd[row] = rs; }
+    }
+  }
+  if constexpr (LNB) {   // the tile's column sums: 16 row groups per column, added in row-group order
+    static_assert(NT == 16 * Q && BM * LDC + 2 * 16 * BN <= (BM + BN) * GR_LDK, "partials beside the C tile");
+    float* red = smem + BM * LDC;   // [2][16][BN]
+    const int rg = threadIdx.x / Q, cl = (threadIdx.x % Q) * 4;
+    *reinterpret_cast<f32x4*>(&red[rg * BN + cl]) = pa;
+    *reinterpret_cast<f32x4*>(&red[(16 + rg) * BN + cl]) = pb;
+    __syncthreads();
+    if (threadIdx.x < 2 * BN) {
+      const int k = threadIdx.x / BN, c = threadIdx.x % BN;
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) t += red[(16 * k + q) * BN + c];
+      g.lb_part[(int64_t)(m0 / BM) * 2 * BN + threadIdx.x] = t;
     }
   }
 }
@@ -1004,6 +1056,54 @@ extern "C" int pcv_gemm_f32_rows_lnout(const float* A, int64_t lda, const float*
   // 514 of C2 start together -- at two per CU the two tail tiles ran as a second round, 16.3 / 25.8 vs
   // 14.7 / 23.5 us, tools/lnout_probe.py)
   hipLaunchKernelGGL((gemm_f32_rows_kernel<false, true, 128, 32, true, 512>), dim3(blocks), dim3(512), 0,
+                     (hipStream_t)stream, g);
+  return pcv_launch_status();
+}
+
+// dy = A B^T (B stored [N][K], N = 128), then the LayerNorm VJP of every dy row from the tile still in LDS
+// (dy itself is not stored): dx = dres + rstd (g - mean(g) - xhat mean(g xhat)), g = dy scale, xhat =
+// (x - mean) rstd; dxd (optional) = dropout_vjp(dx) (rate, seed, site, index row * N + col); the column
+// sums of dy xhat / dy of each 32-row tile -> part[tile][0, N) / [N, 2 N) (tiles = ceil(M / 32), for
+// pcv_layernorm_part_reduce).  ws: the split tail, as pcv_gemm_f32_rows_lnout (its _ws_floats).
+extern "C" int64_t pcv_gemm_f32_rows_lnbwd_part_floats(int64_t M, int64_t N) { return (M + 31) / 32 * 2 * N; }
+
+extern "C" int pcv_gemm_f32_rows_lnbwd(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N,
+                                       int64_t K, const float* x, int64_t ldx, const float* scale, const float* mean,
+                                       const float* rstd, const float* dres, int64_t ldres, float* dx, int64_t lddx,
+                                       float* part, int64_t part_floats, float* dxd, int64_t lddxd, float rate,
+                                       const uint32_t* seed, uint32_t site, float* ws, int64_t ws_floats, void* stream) {
+  if (N != 128 || M <= 0 || K <= 0 || K % GR_BK || !A || !B || !x || !scale || !mean || !rstd || !dx || !part ||
+      part_floats < pcv_gemm_f32_rows_lnbwd_part_floats(M, N) || rate < 0.f || rate >= 1.f || (rate > 0.f && !seed) ||
+      lda < K || ldb < K || ldx < N || lddx < N || (dres && ldres < N) || (dxd && lddxd < N) ||
+      ((lda | ldb | ldx | lddx | (dres ? ldres : 0) | (dxd ? lddxd : 0)) & 3) || M * N >= (1ll << 32))
+    return PCV_EINVAL;
+  if (!gr_al(A) || !gr_al(B) || !gr_al(x) || !gr_al(scale) || !gr_al(dx) || (dres && !gr_al(dres)) ||
+      (dxd && !gr_al(dxd)))
+    return PCV_EALIGN;
+  GrArgs g = {};
+  g.A = A; g.B = B; g.seed = seed;
+  g.lda = lda; g.ldb = ldb; g.res = dres; g.ldr = ldres;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K; g.site = (int)site; g.rstep = 1; g.tiles_n = 1;
+  g.dscale = 1.f;
+  if (rate > 0.f && dxd) {   // as drop_params (elementwise.hip)
+    const double t = (double)rate * 4294967296.0;
+    g.thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+    g.dscale = 1.f / (1.f - rate);
+  }
+  g.ln_s = scale; g.ln_mean = const_cast<float*>(mean); g.ln_rstd = const_cast<float*>(rstd);
+  g.ln_y = dx; g.ldy = lddx;
+  g.lb_x = x; g.lb_ldx = ldx; g.lb_part = part; g.lb_dxd = dxd; g.lb_lddxd = lddxd;
+  unsigned blocks = (unsigned)((M + 31) / 32);
+  const GrSplit sp = ln_split_plan(M, K);
+  if (ws && sp.tiles && ws_floats >= pcv_gemm_f32_rows_lnout_ws_floats(M, K) && gr_al(ws)) {
+    g.tail_ws = ws;
+    g.tail_cnt = reinterpret_cast<unsigned*>(ws + (int64_t)sp.tiles * sp.split * 32 * 128);
+    g.tail_blocks = sp.tiles * sp.split;
+    g.tail_split = sp.split;
+    g.tail_m0 = sp.m0;
+    blocks = blocks - sp.tiles + g.tail_blocks;
+  }
+  hipLaunchKernelGGL((gemm_f32_rows_kernel<true, false, 128, 32, false, 512, true>), dim3(blocks), dim3(512), 0,
                      (hipStream_t)stream, g);
   return pcv_launch_status();
 }

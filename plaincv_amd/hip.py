@@ -106,6 +106,9 @@ SIGNATURES = {
     "pcv_gemm_f32_rows_lnout": [P, I64, P, I64, P, I64, I64, I64, I64, P, P, I64, F32, F32, P, U32, P, P, P, I64, P, P,
                                 F32, P, I64, P],
     "pcv_gemm_f32_rows_lnout_ws_floats": [I64, I64],
+    "pcv_gemm_f32_rows_lnbwd_part_floats": [I64, I64],
+    "pcv_gemm_f32_rows_lnbwd": [P, I64, P, I64, I64, I64, I64, P, I64, P, P, P, P, I64, P, I64, P, I64, P, I64, F32, P,
+                                U32, P, I64, P],
     "pcv_gemm_f32_rows_ws_floats": [I64, I64, I64, I32, I32],
     "pcv_gemm_f32_rows_ws": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32, P, I64,
                              P],
@@ -194,7 +197,8 @@ SIGNATURES = {
 # non-status return types (everything else returns an int status)
 RESTYPES = {"pcv_gemm_wgrad_ws_bytes": I64, "pcv_attn_mask_words": I64, "pcv_batchnorm_workspace_size": SZ, "pcv_qrb_panel_lds": SZ, "pcv_gemm_grouped_plan_size": I64, "pcv_gemm_grouped_ws_floats": I64, "pcv_eigh_log_floats": I64,
             "pcv_layernorm_bwd_f32_ws": I64, "pcv_colsum_ws_floats": I64, "pcv_vit_patch_embed_bwd_f32_ws": I64,
-            "pcv_gemm_f32_rows_ws_floats": I64, "pcv_gemm_f32_rows_lnout_ws_floats": I64}
+            "pcv_gemm_f32_rows_ws_floats": I64, "pcv_gemm_f32_rows_lnout_ws_floats": I64,
+            "pcv_gemm_f32_rows_lnbwd_part_floats": I64}
 
 _lib = None
 _err = None

@@ -78,7 +78,7 @@ class _Dense:
             raise ValueError("a strided-row Dense needs the fused row GEMM's shapes")
         self.plan = None if self.fused else GemmF32().add(a, b, c, tb=tb).finalize(c.device)
         self.epi = bias is not None or res is not None or act or dropout
-        self.ln = None
+        self.ln = self.lnb = None
         # the split tail of the tiled form (pcv_gemm_f32_rows_ws: the data-gradient products at C2's rows)
         nws = int(hip.load().pcv_gemm_f32_rows_ws_floats(M, self.N, K, int(tb), int(bool(self.epi)))) \
             if self.fused and self.rstep == 1 else 0
@@ -96,7 +96,33 @@ class _Dense:
             self.ws = torch.zeros(nws, dtype=torch.float32, device=y.device) if nws else None
         return ok
 
+    def fuse_layernorm_vjp(self, x, scale, st, dres, dx, part, dxd=None, site=0):
+        """Take the LayerNorm VJP of this product's output rows (dy = this product, not stored) into the
+        launch (pcv_gemm_f32_rows_lnbwd: N = 128, B stored [N][K]): dx = LN_vjp(dy) + dres, dxd =
+        dropout_vjp(dx) (site; the rate given to run), the parameter-gradient partials of every 32-row tile
+        -> part (for the deferred LayerNormParamReduce, nblk = lnbwd_blocks); False: keep the VJP launch."""
+        ok = self.fused and self.entry == "pcv_gemm_f32_rows" and self.rstep == 1 and self.tb and not self.epi and \
+            self.N == 128 and self.K % 64 == 0 and \
+            all(t is None or (t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 and
+                              tuple(t.shape) == (self.M, self.N)) for t in (x, dres, dx, dxd)) and \
+            scale.is_contiguous() and scale.data_ptr() % 16 == 0 and part.is_contiguous() and \
+            part.numel() >= int(hip.load().pcv_gemm_f32_rows_lnbwd_part_floats(self.M, self.N))
+        if ok:
+            self.lnb = (x, scale, st, dres, dx, part, dxd, int(site))
+            nws = int(hip.load().pcv_gemm_f32_rows_lnout_ws_floats(self.M, self.K))
+            self.ws = torch.zeros(nws, dtype=torch.float32, device=dx.device) if nws else None
+        return ok
+
     def run(self, rate=0.0, seed=None):
+        if self.lnb is not None:
+            x, sc, st, dres, dx, part, dxd, site = self.lnb
+            rate = rate if dxd is not None else 0.0
+            hip.call("pcv_gemm_f32_rows_lnbwd", ptr(self.a), self.a.stride(0), ptr(self.b), self.b.stride(0), self.M,
+                     self.N, self.K, ptr(x), x.stride(0), ptr(sc), ptr(st[0]), ptr(st[1]), ptr(dres),
+                     dres.stride(0) if dres is not None else 0, ptr(dx), dx.stride(0), ptr(part), part.numel(),
+                     ptr(dxd), dxd.stride(0) if dxd is not None else 0, float(rate), ptr(seed), site, ptr(self.ws),
+                     self.ws.numel() if self.ws is not None else 0, stream_ptr())
+            return
         rate = rate if self.dropout else 0.0
         if self.ln is not None:
             sc, bi, y, st = self.ln
@@ -134,6 +160,8 @@ class ViTRunnerF32:
     # forward leaves the loss / accuracy metrics to backward(), which computes them in the launch of
     # the LayerNorm parameter reduction instead of a launch of their own
     metrics_in_backward = False
+    # False: the LayerNorm VJPs as launches of their own after the data-gradient products (A/B, tests)
+    fuse_ln_vjp = True
 
     def __init__(self, model, store, image_shape, device, batch_stats=None, fused_attn=True):
         """fused_attn False: the per-(batch, head) GEMM path around a materialised softmax (also taken
@@ -407,18 +435,36 @@ class ViTRunnerF32:
         # LayerNorm dscale / dbias: every VJP leaves per-block column sums in its ws row, one launch
         # at the end of backward adds them all (instead of a small reduction launch per LayerNorm)
         self.ln_red = None
+        self.lnb_fused = set()   # (block, 0 | 1): that block's LayerNorm_0 / _1 VJP runs in a data-gradient product
         xcls, dxc = self.xs[-1].view(B, T * D)[:, :D], self.dx.view(B, T * D)[:, :D]
         if self.m.use_layernorm and \
                 K.layernorm_bwd_f32_fits(D, self.dyf, xcls, None, dxc) and \
                 K.layernorm_bwd_f32_fits(D, self.dy1, self.x1s[0], self.dx, self.dx1):
+            # the data-gradient products whose output feeds a LayerNorm VJP (MLP Dense_0 -> LayerNorm_1, qkv ->
+            # LayerNorm_0 + the previous block's MLP-out dropout VJP) take it into their epilogue
+            # (pcv_gemm_f32_rows_lnbwd); the residual gradient they read is the one the backward hands them
+            # (dx_in: the next block's LayerNorm_0 VJP output, or the head VJP's dx; dx1)
+            for i in range(L):
+                w, gb = self.w[i], self.gb[i]
+                if not (self.cls_last and i == L - 1) and self.fuse_ln_vjp:
+                    dres = self.dx if i == L - 1 else self.dxo[i + 1]
+                    if gb["fc1_d"].fuse_layernorm_vjp(self.x1s[i], w["s1"], self.st1[i], dres, self.dx1_l[i],
+                                                      self.ln_ws[1 + 2 * i]):
+                        self.lnb_fused.add((i, 1))
+                dxd = self.dmo_l[i - 1] if i > 0 else None
+                if self.fuse_ln_vjp and gb["qkv_d"].fuse_layernorm_vjp(self.xs[i], w["s0"], self.st0[i], self.dx1_l[i],
+                                                                  self.dxo[i], self.ln_ws[2 + 2 * i], dxd=dxd,
+                                                                  site=site_mlp_out(i - 1) if i > 0 else 0):
+                    self.lnb_fused.add((i, 0))
+            lb = lambda i, j: -(-B * T // 32) if (i, j) in self.lnb_fused else None  # noqa: E731  (32-row tiles)
             red = K.LayerNormParamReduce().add(self.ln_ws[0], B, D, self.gsf, self.gcf,
                                                nblk=B if self.head_fused else None)
             for i in range(L):
                 w = self.w[i]
                 last = self.cls_last and i == L - 1   # (cls rows: B; the fused chain leaves one partial per row)
                 red.add(self.ln_ws[1 + 2 * i], B if last else B * T, D, w["gs1"], w["gc1"],
-                        nblk=B if (last and self.cls_chain) else None)
-                red.add(self.ln_ws[2 + 2 * i], B * T, D, w["gs0"], w["gc0"])
+                        nblk=B if (last and self.cls_chain) else lb(i, 1))
+                red.add(self.ln_ws[2 + 2 * i], B * T, D, w["gs0"], w["gc0"], nblk=lb(i, 0))
             self.ln_red = red.finalize(dev)
 
     def _ln_bwd(self, slot, dy, x, scale, st, dres, dx, gs, gc, **drop):
@@ -624,8 +670,10 @@ class ViTRunnerF32:
             self._colsum(dmo, w["gb1"])
             g["fc2_d"].run(rate, seed)                        # da = dropout_vjp(dmo W1^T) * gelu'(pre)
             self._colsum(da, w["gb0"])
-            g["fc1_d"].run()                                                           # self.dy1 = da W0^T
-            if m.use_layernorm:
+            g["fc1_d"].run()                            # self.dy1 = da W0^T (fused: its LayerNorm_1 VJP -> dx1)
+            if (i, 1) in self.lnb_fused:
+                pass
+            elif m.use_layernorm:
                 self._ln_bwd(1 + 2 * i, self.dy1, self.x1s[i], w["s1"], self.st1[i], dx_in, dx1, w["gs1"], w["gc1"])
             elif self.bn:
                 K.batchnorm_bwd(self.dy1, self.x1s[i], *self.bst1[i], w["s1"], dx_in, dx1, None, w["gs1"], w["gc1"],
@@ -661,8 +709,10 @@ class ViTRunnerF32:
         """Block i's qkv-product VJP and LayerNorm_0 VJP (with the residual gradient dx1) into dxo[i]."""
         m, w = self.m, self.w[i]
         self._colsum(self.dqkv_l[i], w["gbqkv"])
-        self.gb[i]["qkv_d"].run()                                                      # self.dy0 = dqkv Wqkv^T
-        if m.use_layernorm:
+        self.gb[i]["qkv_d"].run(rate, seed)         # self.dy0 = dqkv Wqkv^T (fused: its LayerNorm_0 VJP -> dxo[i])
+        if (i, 0) in self.lnb_fused:
+            pass
+        elif m.use_layernorm:
             drop = dict(dxd=self.dmo_l[i - 1], rate=rate, seed=seed, site=site_mlp_out(i - 1)) if i > 0 else {}
             self._ln_bwd(2 + 2 * i, self.dy0, self.xs[i], w["s0"], self.st0[i], dx1, self.dxo[i], w["gs0"], w["gc0"],
                          **drop)

@@ -154,6 +154,64 @@ def test_gemm_f32_rows_layernorm_of_output_rejects_other_widths(dev):
 
 
 
+# the LayerNorm VJP of the product's rows (pcv_gemm_f32_rows_lnbwd): MLP Dense_0's data gradient -> LayerNorm_1
+# (K = 256) and the qkv data gradient -> LayerNorm_0 with the previous block's dropout VJP (K = 384); vs an fp64
+# product through the fp64 LayerNorm VJP, the partial rows summed against the parameter gradients
+@pytest.mark.parametrize("M,K,rate", [(16448, 256, 0.0), (16448, 384, 0.1), (1000, 256, 0.1), (77, 384, 0.0),
+                                      (64, 128, 0.3)])
+def test_gemm_f32_rows_layernorm_vjp(dev, M, K, rate):
+    from plaincv_amd import hip
+    from plaincv_amd.hip import ptr, stream_ptr
+    from plaincv_amd.models.vit_f32 import _epi_bwd
+    N = 128
+    g = torch.Generator().manual_seed(M + K + 1)
+    a = torch.randn(M, K, generator=g).to(dev)
+    b = (torch.randn(N, K, generator=g) * K ** -0.5).to(dev)      # [N][K]: dy = a b^T
+    x = (torch.randn(M, N, generator=g) * 1.5 + 0.3).to(dev)
+    sc = (1 + 0.3 * torch.randn(N, generator=g)).to(dev)
+    mean = x.double().mean(1)
+    rstd = (1.0 / torch.sqrt(((x.double() - mean[:, None]) ** 2).mean(1) + 1e-6))
+    mean, rstd = mean.float(), rstd.float()
+    dres = torch.randn(M, N, generator=g).to(dev)
+    seed = torch.tensor([777], dtype=torch.int32, device=dev)
+    lib = hip.load()
+    npart = int(lib.pcv_gemm_f32_rows_lnbwd_part_floats(M, N))
+    assert npart == (M + 31) // 32 * 2 * N
+    part = torch.full((npart,), float("nan"), device=dev)
+    dx = torch.full((M, N + 4), float("nan"), device=dev)[:, :N]   # (a strided dx)
+    dxd = torch.full((M, N), float("nan"), device=dev) if rate > 0 else None
+    nws = lib.pcv_gemm_f32_rows_lnout_ws_floats(M, K)
+    ws = torch.zeros(max(nws, 1), device=dev)
+
+    def run(out, outd):
+        hip.call("pcv_gemm_f32_rows_lnbwd", ptr(a), K, ptr(b), K, M, N, K, ptr(x), N, ptr(sc), ptr(mean), ptr(rstd),
+                 ptr(dres), N, ptr(out), out.stride(0), ptr(part), npart, ptr(outd), N if outd is not None else 0,
+                 float(rate), ptr(seed), 11, ptr(ws), nws, stream_ptr())
+    run(dx, dxd)
+    dy = a.double() @ b.double().t()
+    xh = (x.double() - mean.double()[:, None]) * rstd.double()[:, None]
+    gg = dy * sc.double()
+    ref = dres.double() + rstd.double()[:, None] * (gg - gg.mean(1, keepdim=True) - xh * (gg * xh).mean(1, keepdim=True))
+    torch.cuda.synchronize()
+    err = (dx.double() - ref).abs()
+    assert (err <= 2e-5 * (1 + ref.abs())).all(), err.max().item()
+    pr = part.view(-1, 2 * N).double().sum(0)
+    ds, db = (dy * xh).sum(0), dy.sum(0)
+    assert ((pr[:N] - ds).abs() <= 1e-4 * (1 + ds.abs())).all(), (pr[:N] - ds).abs().max().item()
+    assert ((pr[N:] - db).abs() <= 1e-4 * (1 + db.abs())).all(), (pr[N:] - db).abs().max().item()
+    if dxd is not None:   # the dropout VJP of the kernel's own dx (same index and bits as the stand-alone VJP)
+        dref = torch.empty_like(dxd)
+        _epi_bwd(dx.contiguous(), dref, rate=rate, seed=seed, site=11)
+        torch.cuda.synchronize()
+        assert torch.equal(dxd, dref)
+    # repeated launches bit-identical (the split tail's counters back at zero)
+    dx2 = torch.empty(M, N, device=dev)
+    p1 = part.clone()
+    run(dx2, dxd)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx2) and torch.equal(part, p1)
+
+
 # the split tail (pcv_gemm_f32_rows_ws): C2's data-gradient products, whose last 4 tiles run as K slices beside
 # the first round and meet in the workspace; checked against fp64, repeated launches bit-identical, the tile
 # counters back at zero after every launch

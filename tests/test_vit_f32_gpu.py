@@ -164,6 +164,38 @@ def test_vit_f32_unfused_attention_matches_fused(dev):
     assert rel(out[0][1], out[1][1]) < 1e-5
 
 
+def test_vit_f32_fused_layernorm_vjp_matches_separate(dev, monkeypatch):
+    """The LayerNorm VJPs taken into the data-gradient products' epilogue (pcv_gemm_f32_rows_lnbwd: MLP
+    Dense_0 -> LayerNorm_1, qkv -> LayerNorm_0 + the MLP-out dropout VJP; D = 128) and the stand-alone VJP
+    launches give the same step (loss, every gradient leaf rel 1e-5), on C2's geometry at B = 4."""
+    from plaincv_amd.engine import create_train_state
+    from plaincv_amd.models.vit_f32 import ViTRunnerF32
+    m = _model(0.1, 200, 128, 256, 4, 4)
+    shape = (4, 64, 64, 3)
+    init = m.init(7, shape)
+    g = torch.Generator().manual_seed(2)
+    images = torch.randint(0, 256, shape, generator=g, dtype=torch.uint8).to(dev)
+    labels = torch.randint(0, 200, (4,), generator=g, dtype=torch.int32).to(dev)
+    out = []
+    for fused in (True, False):
+        monkeypatch.setattr(ViTRunnerF32, "fuse_ln_vjp", fused)
+        st = create_train_state(0, m, 1e-3, shape, 200, init_params=init)
+        r = ViTRunnerF32(m, st.params, shape, dev)
+        st.runners[tuple(shape)] = r
+        # every full-height LayerNorm VJP (the cls-sparse last block's LayerNorm_1 stays in its chain)
+        assert len(r.lnb_fused) == (2 * m.num_layers - 1 if fused else 0), sorted(r.lnb_fused)
+        r.seed.fill_(5)
+        st.params.zero_grad()
+        met = r.forward(images, labels, train=True)
+        r.backward(train=True)
+        torch.cuda.synchronize()
+        out.append((met[0].item(), st.params.grads_dict()))
+    assert abs(out[0][0] - out[1][0]) <= 1e-6 * abs(out[1][0])
+    bad = [(k, rel(out[0][1][k], out[1][1][k])) for k in out[1][1]
+           if not k.endswith("key/bias") and rel(out[0][1][k], out[1][1][k]) > 1e-5]
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("optim,mlp", [("soap+schedule_free", 128), ("shampoo", 320)])
 def test_graphed_step_matches_eager_host_driven(dev, optim, mlp):
     """GraphedTrainStep == eager steps where the optimizer keeps host state:
