@@ -83,11 +83,14 @@ struct GrShape {
   static constexpr int WNW = (NT / 64) / (BM / 32), WN = BN / WNW, NJ = WN / 16;
 };
 
-template <bool TA, bool TB, int BN, int BM = GR_BM, int NT = 256, int BK = GR_BK>
+// DB: two image sets (As / Bs and As2 / Bs2) alternate per chunk, so one barrier per chunk remains (the
+// next chunk is stored to the set nobody reads while this chunk's MFMAs run)
+template <bool TA, bool TB, int BN, int BM = GR_BM, int NT = 256, int BK = GR_BK, bool DB = false>
 __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
                                             int64_t ldb, int M, int m0, int n0, int kbeg, int kend, float* As,
                                             float* Bs, f32x4 (&acc)[2][GrShape<BM, BN, NT>::NJ],
-                                            bool colsum = false, float* cs_out = nullptr) {
+                                            bool colsum = false, float* cs_out = nullptr, float* As2 = nullptr,
+                                            float* Bs2 = nullptr) {
   constexpr int C4 = BK / 4, LDK = BK + 4;               // float4 per k row; k-contiguous image stride
   constexpr int NA = BM * C4 / NT, NB = BN * C4 / NT;
   static_assert(NA * NT == BM * C4 && NB * NT == BN * C4, "whole float4 loads per thread");
@@ -118,38 +121,40 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
       rb[i] = *reinterpret_cast<const f32x4*>(bp[i] + (TB ? (int64_t)kc * BK : (int64_t)kc * BK * ldb));
   };
   constexpr int LDA_K = BM + 4, LDB_K = BN + 4;   // row strides of the k-major images
-  auto lstore = [&]() {
+  auto lstore = [&](float* Ad, float* Bd) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int idx = tid + NT * i;
-      if (TA) *reinterpret_cast<f32x4*>(&As[(idx / (BM / 4)) * LDA_K + (idx % (BM / 4)) * 4]) = ra[i];
-      else *reinterpret_cast<f32x4*>(&As[(idx / C4) * LDK + (idx % C4) * 4]) = ra[i];
+      if (TA) *reinterpret_cast<f32x4*>(&Ad[(idx / (BM / 4)) * LDA_K + (idx % (BM / 4)) * 4]) = ra[i];
+      else *reinterpret_cast<f32x4*>(&Ad[(idx / C4) * LDK + (idx % C4) * 4]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int idx = tid + NT * i;
-      if (TB) *reinterpret_cast<f32x4*>(&Bs[(idx / C4) * LDK + (idx % C4) * 4]) = rb[i];
-      else *reinterpret_cast<f32x4*>(&Bs[(idx / (BN / 4)) * LDB_K + (idx % (BN / 4)) * 4]) = rb[i];
+      if (TB) *reinterpret_cast<f32x4*>(&Bd[(idx / C4) * LDK + (idx % C4) * 4]) = rb[i];
+      else *reinterpret_cast<f32x4*>(&Bd[(idx / (BN / 4)) * LDB_K + (idx % (BN / 4)) * 4]) = rb[i];
     }
   };
+  float* Ac = As;   // the image set this chunk's MFMAs read
+  float* Bc = Bs;
   auto fload = [&](int kk, f32x4 (&fa)[2], f32x4 (&fb)[NJ]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int x = wm * 32 + i * 16 + c16;
       if (TA) {
-        const float* p = &As[(kk + 4 * g4) * LDA_K + x];
+        const float* p = &Ac[(kk + 4 * g4) * LDA_K + x];
         fa[i] = f32x4{p[0], p[LDA_K], p[2 * LDA_K], p[3 * LDA_K]};
       } else {
-        fa[i] = *reinterpret_cast<const f32x4*>(&As[x * LDK + kk + 4 * g4]);
+        fa[i] = *reinterpret_cast<const f32x4*>(&Ac[x * LDK + kk + 4 * g4]);
       }
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int x = wn * WN + j * 16 + c16;
       if (TB) {
-        fb[j] = *reinterpret_cast<const f32x4*>(&Bs[x * LDK + kk + 4 * g4]);
+        fb[j] = *reinterpret_cast<const f32x4*>(&Bc[x * LDK + kk + 4 * g4]);
       } else {
-        const float* p = &Bs[(kk + 4 * g4) * LDB_K + x];
+        const float* p = &Bc[(kk + 4 * g4) * LDB_K + x];
         fb[j] = f32x4{p[0], p[LDB_K], p[2 * LDB_K], p[3 * LDB_K]};
       }
     }
@@ -161,12 +166,16 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
   const int cs_n = tid % BN, cs_k = (tid / BN) * CS_SEG;
   float cs = 0.f;
   gload(0);
-  lstore();
+  lstore(As, Bs);
   __syncthreads();
   for (int kc = 0; kc < nk; ++kc) {
+    if (DB) {
+      Ac = (kc & 1) ? As2 : As;
+      Bc = (kc & 1) ? Bs2 : Bs;
+    }
     if (colsum) {
 #pragma unroll
-      for (int e = 0; e < CS_SEG; ++e) cs += Bs[(cs_k + e) * LDB_K + cs_n];
+      for (int e = 0; e < CS_SEG; ++e) cs += Bc[(cs_k + e) * LDB_K + cs_n];
     }
     if (kc + 1 < nk) gload(kc + 1);
     f32x4 fa[2][2], fb[2][NJ];
@@ -184,8 +193,12 @@ __device__ __forceinline__ void gr_mainloop(const float* __restrict__ A, int64_t
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[cur][i][s], fb[cur][j][s], acc[i][j], 0, 0, 0);
     }
     if (kc + 1 < nk) {
-      __syncthreads();
-      lstore();
+      if (DB) {
+        lstore((kc & 1) ? As : As2, (kc & 1) ? Bs : Bs2);
+      } else {
+        __syncthreads();
+        lstore(As, Bs);
+      }
       __syncthreads();
     }
   }
@@ -412,9 +425,10 @@ static_assert(sizeof(WgJob) == 8 * 8 + 10 * 4, "WgJob layout");
 
 constexpr int WG_BK = 32;   // (k chunk of the weight-gradient main loop)
 template <int BN>
-__global__ __launch_bounds__(256, 4) void gemm_f32_wgrad_kernel(const WgJob* __restrict__ jobs, int njobs, int total) {
-  __shared__ __attribute__((aligned(16))) float As[WG_BK * (GR_BM + 4)];   // [k][m] images
-  __shared__ __attribute__((aligned(16))) float Bs[WG_BK * (BN + 4)];      // [k][n]
+__global__ __launch_bounds__(256, 3) void gemm_f32_wgrad_kernel(const WgJob* __restrict__ jobs, int njobs, int total) {
+  // [k][m] / [k][n] images, two sets (one barrier per chunk; 3 workgroups per CU still fit the LDS)
+  __shared__ __attribute__((aligned(16))) float As[2][WG_BK * (GR_BM + 4)];
+  __shared__ __attribute__((aligned(16))) float Bs[2][WG_BK * (BN + 4)];
   constexpr int WN = BN / 2, NJ = WN / 16;
   __shared__ int ft[256];
   // XCD-aware order: the tiles of one K slice (which share its A and B rows) and the job's next
@@ -438,18 +452,18 @@ __global__ __launch_bounds__(256, 4) void gemm_f32_wgrad_kernel(const WgJob* __r
     for (int q = 0; q < NJ; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bool cs_on = m0 == 0 && jb.colsum;
   float cs = 0.f;
-  gr_mainloop<true, false, BN, GR_BM, 256, WG_BK>(jb.A, jb.lda, jb.B, jb.ldb, jb.M, m0, n0, kbeg, kend, As, Bs, acc, cs_on,
-                                                 &cs);
+  gr_mainloop<true, false, BN, GR_BM, 256, WG_BK, true>(jb.A, jb.lda, jb.B, jb.ldb, jb.M, m0, n0, kbeg, kend, As[0], Bs[0],
+                                                       acc, cs_on, &cs, As[1], Bs[1]);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
   const int g4 = lane >> 4, c16 = lane & 15;
   if (cs_on) {   // (block-uniform) the column's 256 / BN thread partials in thread order
     __syncthreads();   // the main loop's last LDS reads are done: As is free
-    As[threadIdx.x] = cs;
+    As[0][threadIdx.x] = cs;
     __syncthreads();
     if (threadIdx.x < BN) {
       float v = 0.f;
 #pragma unroll
-      for (int q = 0; q < 256 / BN; ++q) v += As[q * BN + threadIdx.x];
+      for (int q = 0; q < 256 / BN; ++q) v += As[0][q * BN + threadIdx.x];
       if (jb.ws && jb.ksplit > 1)
         jb.ws[(int64_t)jb.tiles * jb.ksplit * (GR_BM * BN) + ((int64_t)(n0 / BN) * jb.ksplit + sl) * BN + threadIdx.x] = v;
       else
