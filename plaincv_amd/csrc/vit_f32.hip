@@ -187,17 +187,19 @@ struct LnPartJob {
 };
 static_assert(sizeof(LnPartJob) == 40, "LnPartJob layout");
 
-// dscale[c] += sum_b part[b][c], dbias[c] += sum_b part[b][D + c]: workgroup (x, z) sums 64 columns
-// of job z (jobs == nullptr: the single job `one`) over all of its nblk partial rows -- 16 row lanes
-// of 64 columns, the lanes' sums added in lane order through LDS and ONE add per column: the result is
+// dscale[c] += sum_b part[b][c], dbias[c] += sum_b part[b][D + c]: workgroup (x, z) sums LNR_COLS columns
+// of job z (jobs == nullptr: the single job `one`) over all of its nblk partial rows -- LNR_LANES row lanes
+// of LNR_COLS columns, the lanes' sums added in lane order through LDS and ONE add per column: the result is
 // run-to-run identical (no float atomics whose order varies)
-constexpr int LNR_THREADS = 1024, LNR_LANES = LNR_THREADS / 64;
+// (32 columns x 32 row lanes per workgroup: 80 workgroups for the ViT's ten jobs, one masked batch of loads per
+// lane; 64 columns x 16 lanes took 13 us at 514 partial rows)
+constexpr int LNR_THREADS = 1024, LNR_COLS = 32, LNR_LANES = LNR_THREADS / LNR_COLS;
 // (metrics != nullptr: the z-slice past the jobs is mean2_kernel's work -- the step's mean loss / accuracy,
 // moved off its own launch; the same block_sum, so the same values)
 __global__ __launch_bounds__(LNR_THREADS) void ln_part_reduce_kernel(const LnPartJob* jobs, LnPartJob one,
                                                                      const float* m_loss, const float* m_correct,
                                                                      int64_t m_n, float m_scale, float* metrics) {
-  __shared__ float red[LNR_LANES][64];
+  __shared__ float red[LNR_LANES][LNR_COLS];
   if (metrics && (int)blockIdx.z == (int)gridDim.z - 1) {
     if (blockIdx.x != 0) return;
     float* r16 = &red[0][0];
@@ -212,7 +214,7 @@ __global__ __launch_bounds__(LNR_THREADS) void ln_part_reduce_kernel(const LnPar
   const float* part = j.part;
   const int nblk = (int)j.nblk, D = (int)j.D;
   float *dscale = j.dscale, *dbias = j.dbias;
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63), sl = threadIdx.x >> 6;
+  const int col = blockIdx.x * LNR_COLS + (threadIdx.x % LNR_COLS), sl = threadIdx.x / LNR_COLS;
   float sum = 0.f;
   if (col < 2 * D) {   // rows sl, sl + LNR_LANES, ... added in order, 64 loads in flight per batch
     int b = sl;
@@ -224,7 +226,7 @@ __global__ __launch_bounds__(LNR_THREADS) void ln_part_reduce_kernel(const LnPar
       for (int j = 0; j < 64; ++j) sum += v[j];
     }
     // the rest in masked batches of 32 (+ 0 past the end), not a serial loop: 514 partial rows of 32-row
-    // tiles took 18 us as one dependent load after another (12.8 us in batches of 16)
+    // tiles took 18 us as one dependent load after another
     for (; b < nblk; b += 32 * LNR_LANES) {
       float v[32];
 #pragma unroll
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(LNR_THREADS) void ln_part_reduce_kernel(const LnPar
       for (int j = 0; j < 32; ++j) sum += v[j];
     }
   }
-  red[sl][threadIdx.x & 63] = sum;
+  red[sl][threadIdx.x % LNR_COLS] = sum;
   __syncthreads();
   if (sl == 0 && col < 2 * D) {
     float t = 0.f;
@@ -2084,7 +2086,7 @@ extern "C" int pcv_layernorm_bwd_f32(const float* dy, int64_t lddy, const float*
                                           (hipStream_t)stream, dy, lddy, x, ldx, scale, mean, rstd, dres, ldres, dx,
                                           lddx, ws, R, dxd, lddxd, th, sc, seed, site));
   if (!dscale) return pcv_launch_status();   // partials stay in ws for pcv_layernorm_part_reduce
-  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * D + 63) / 64)), dim3(LNR_THREADS), 0,
+  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * D + LNR_COLS - 1) / LNR_COLS)), dim3(LNR_THREADS), 0,
                      (hipStream_t)stream, nullptr, LnPartJob{ws, dscale, dbias, blocks, D}, nullptr, nullptr, 0, 0.f,
                      nullptr);
   return pcv_launch_status();
@@ -2096,7 +2098,7 @@ extern "C" int pcv_layernorm_part_job_size() { return (int)sizeof(LnPartJob); }
 // table of LnPartJob; max_D / max_nblk bound the table's entries)
 extern "C" int pcv_layernorm_part_reduce(const void* jobs, int njobs, int max_D, int64_t max_nblk, void* stream) {
   if (!jobs || njobs <= 0 || njobs > 65535 || max_D <= 0 || max_D > 512 || max_nblk <= 0) return PCV_EINVAL;
-  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * max_D + 63) / 64), 1, njobs), dim3(LNR_THREADS), 0,
+  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * max_D + LNR_COLS - 1) / LNR_COLS), 1, njobs), dim3(LNR_THREADS), 0,
                      (hipStream_t)stream, (const LnPartJob*)jobs, LnPartJob{}, nullptr, nullptr, 0, 0.f, nullptr);
   return pcv_launch_status();
 }
@@ -2108,7 +2110,7 @@ extern "C" int pcv_layernorm_part_reduce_metrics(const void* jobs, int njobs, in
   if (!jobs || njobs <= 0 || njobs >= 65535 || max_D <= 0 || max_D > 512 || max_nblk <= 0 || !loss || !correct ||
       !metrics || n <= 0)
     return PCV_EINVAL;
-  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * max_D + 63) / 64), 1, njobs + 1), dim3(LNR_THREADS),
+  hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((unsigned)((2 * max_D + LNR_COLS - 1) / LNR_COLS), 1, njobs + 1), dim3(LNR_THREADS),
                      0, (hipStream_t)stream, (const LnPartJob*)jobs, LnPartJob{}, loss, correct, n, scale, metrics);
   return pcv_launch_status();
 }
