@@ -450,12 +450,15 @@ int64_t pcv_gemm_f32_rows_lnout_ws_floats(int64_t M, int64_t K);
  * dy xhat / dy of each 32-row tile -> part[tile][0, N) / [N, 2 N) for pcv_layernorm_part_reduce (nblk =
  * ceil(M / 32); part_floats >= pcv_gemm_f32_rows_lnbwd_part_floats).  The ViT's MLP Dense_0 data gradient ->
  * LayerNorm_1 VJP and qkv data gradient -> LayerNorm_0 VJP (models/vit_small.py:46-56, :38) in one launch.
+ * B2 / C2 (optional, both or neither): C2 = dx B2^T (B2 stored [N][N]) from the same rows in the same launch
+ * (the attention out projection's data gradient after LayerNorm_1's VJP).
  * ws (optional, pcv_gemm_f32_rows_lnout_ws_floats(M, K)): the split tail, as pcv_gemm_f32_rows_lnout. */
 int pcv_gemm_f32_rows_lnbwd(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                             const float* x, int64_t ldx, const float* scale, const float* mean, const float* rstd,
                             const float* dres, int64_t ldres, float* dx, int64_t lddx, float* part,
                             int64_t part_floats, float* dxd, int64_t lddxd, float rate, const uint32_t* seed,
-                            uint32_t site, float* ws, int64_t ws_floats, void* stream);
+                            uint32_t site, const float* B2, int64_t ldb2, float* C2, int64_t ldc2, float* ws,
+                            int64_t ws_floats, void* stream);
 int64_t pcv_gemm_f32_rows_lnbwd_part_floats(int64_t M, int64_t N);
 /* pcv_gemm_f32_rows with a workspace for the split tail of its tiled form (data-gradient products, no
  * epilogue: the few tiles past a whole number of 4-per-CU rounds run as K slices beside the first round, the

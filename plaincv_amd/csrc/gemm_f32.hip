@@ -49,6 +49,9 @@ struct GrArgs {
   // dropout_vjp(dx) -> lb_dxd, the tile's column sums of dy xhat / dy -> lb_part row m0 / BM
   const float* lb_x; float* lb_part; float* lb_dxd;
   int64_t lb_ldx, lb_lddxd;
+  // LNB second product (optional): C2 = dx B2^T (B2 stored [N][N], N = 128) from the dx rows just stored
+  const float* lb_B2; float* lb_C2;
+  int64_t lb_ldb2, lb_ldc2;
 };
 
 // GELU (tanh form): 0.5 x (1 + tanh(u)) = x / (1 + exp(-2u)), u = sqrt(2/pi) (x + 0.044715 x^3) --
@@ -400,6 +403,32 @@ __global__ __launch_bounds__(NT, (LNO || LNB) ? 6 : 1) void gemm_f32_rows_kernel
 #pragma unroll
       for (int q = 0; q < 16; ++q) t += red[(16 * k + q) * BN + c];
       g.lb_part[(int64_t)(m0 / BM) * 2 * BN + threadIdx.x] = t;
+    }
+    if (g.lb_C2) {   // (block-uniform) the next data-gradient product of the same rows, K = N = 128: its A
+      // rows are the dx rows this workgroup just stored (ordered by the barrier at workgroup scope, read
+      // back through L2), one launch less than the stand-alone product
+      __syncthreads();   // every dx row stored; the partial sums read out of LDS
+      f32x4 acc2[2][NJ];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      gr_mainloop<false, true, BN, BM, NT>(g.ln_y, g.ldy, g.lb_B2, g.lb_ldb2, g.M, m0, 0, 0, BN, As, Bs, acc2);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) smem[(wm * 32 + i * 16 + 4 * g4 + r) * LDC + wn * WN + j * 16 + c16] = acc2[i][j][r];
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int idx = threadIdx.x + NT * it, rl = idx / Q, cl2 = (idx % Q) * 4;
+        const int row = m0 + rl;
+        if (row < g.M)
+          *reinterpret_cast<f32x4*>(g.lb_C2 + (int64_t)row * g.lb_ldc2 + cl2) = *reinterpret_cast<const f32x4*>(&smem[rl * LDC + cl2]);
+      }
     }
   }
 }
@@ -1078,14 +1107,19 @@ extern "C" int pcv_gemm_f32_rows_lnout(const float* A, int64_t lda, const float*
 // (dy itself is not stored): dx = dres + rstd (g - mean(g) - xhat mean(g xhat)), g = dy scale, xhat =
 // (x - mean) rstd; dxd (optional) = dropout_vjp(dx) (rate, seed, site, index row * N + col); the column
 // sums of dy xhat / dy of each 32-row tile -> part[tile][0, N) / [N, 2 N) (tiles = ceil(M / 32), for
-// pcv_layernorm_part_reduce).  ws: the split tail, as pcv_gemm_f32_rows_lnout (its _ws_floats).
+// pcv_layernorm_part_reduce); B2 / C2 (optional, both or neither): C2 = dx B2^T (B2 stored [N][N]) in the
+// same launch.  ws: the split tail, as pcv_gemm_f32_rows_lnout (its _ws_floats).
 extern "C" int64_t pcv_gemm_f32_rows_lnbwd_part_floats(int64_t M, int64_t N) { return (M + 31) / 32 * 2 * N; }
 
 extern "C" int pcv_gemm_f32_rows_lnbwd(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N,
                                        int64_t K, const float* x, int64_t ldx, const float* scale, const float* mean,
                                        const float* rstd, const float* dres, int64_t ldres, float* dx, int64_t lddx,
                                        float* part, int64_t part_floats, float* dxd, int64_t lddxd, float rate,
-                                       const uint32_t* seed, uint32_t site, float* ws, int64_t ws_floats, void* stream) {
+                                       const uint32_t* seed, uint32_t site, const float* B2, int64_t ldb2, float* C2,
+                                       int64_t ldc2, float* ws, int64_t ws_floats, void* stream) {
+  if ((B2 != nullptr) != (C2 != nullptr) || (B2 && (ldb2 < N || ldc2 < N || ((ldb2 | ldc2) & 3) || !gr_al(B2) ||
+                                                    !gr_al(C2))))
+    return PCV_EINVAL;
   if (N != 128 || M <= 0 || K <= 0 || K % GR_BK || !A || !B || !x || !scale || !mean || !rstd || !dx || !part ||
       part_floats < pcv_gemm_f32_rows_lnbwd_part_floats(M, N) || rate < 0.f || rate >= 1.f || (rate > 0.f && !seed) ||
       lda < K || ldb < K || ldx < N || lddx < N || (dres && ldres < N) || (dxd && lddxd < N) ||
@@ -1107,6 +1141,7 @@ extern "C" int pcv_gemm_f32_rows_lnbwd(const float* A, int64_t lda, const float*
   g.ln_s = scale; g.ln_mean = const_cast<float*>(mean); g.ln_rstd = const_cast<float*>(rstd);
   g.ln_y = dx; g.ldy = lddx;
   g.lb_x = x; g.lb_ldx = ldx; g.lb_part = part; g.lb_dxd = dxd; g.lb_lddxd = lddxd;
+  g.lb_B2 = B2; g.lb_ldb2 = ldb2; g.lb_C2 = C2; g.lb_ldc2 = ldc2;
   unsigned blocks = (unsigned)((M + 31) / 32);
   const GrSplit sp = ln_split_plan(M, K);
   if (ws && sp.tiles && ws_floats >= pcv_gemm_f32_rows_lnout_ws_floats(M, K) && gr_al(ws)) {

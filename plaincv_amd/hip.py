@@ -108,7 +108,7 @@ SIGNATURES = {
     "pcv_gemm_f32_rows_lnout_ws_floats": [I64, I64],
     "pcv_gemm_f32_rows_lnbwd_part_floats": [I64, I64],
     "pcv_gemm_f32_rows_lnbwd": [P, I64, P, I64, I64, I64, I64, P, I64, P, P, P, P, I64, P, I64, P, I64, P, I64, F32, P,
-                                U32, P, I64, P],
+                                U32, P, I64, P, I64, P, I64, P],
     "pcv_gemm_f32_rows_ws_floats": [I64, I64, I64, I32, I32],
     "pcv_gemm_f32_rows_ws": [P, I64, P, I64, I32, P, I64, I64, I64, I64, P, P, I64, P, I64, F32, I32, F32, P, U32, P, I64,
                              P],

@@ -96,32 +96,39 @@ class _Dense:
             self.ws = torch.zeros(nws, dtype=torch.float32, device=y.device) if nws else None
         return ok
 
-    def fuse_layernorm_vjp(self, x, scale, st, dres, dx, part, dxd=None, site=0):
+    def fuse_layernorm_vjp(self, x, scale, st, dres, dx, part, dxd=None, site=0, then=None):
         """Take the LayerNorm VJP of this product's output rows (dy = this product, not stored) into the
         launch (pcv_gemm_f32_rows_lnbwd: N = 128, B stored [N][K]): dx = LN_vjp(dy) + dres, dxd =
         dropout_vjp(dx) (site; the rate given to run), the parameter-gradient partials of every 32-row tile
-        -> part (for the deferred LayerNormParamReduce, nblk = lnbwd_blocks); False: keep the VJP launch."""
+        -> part (for the deferred LayerNormParamReduce, nblk = lnbwd_blocks); then = (B2, C2): also C2 = dx
+        B2^T in the launch (a plain product of dx with a [128][128] weight); False: keep the VJP launch."""
         ok = self.fused and self.entry == "pcv_gemm_f32_rows" and self.rstep == 1 and self.tb and not self.epi and \
             self.N == 128 and self.K % 64 == 0 and \
             all(t is None or (t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 and
                               tuple(t.shape) == (self.M, self.N)) for t in (x, dres, dx, dxd)) and \
             scale.is_contiguous() and scale.data_ptr() % 16 == 0 and part.is_contiguous() and \
             part.numel() >= int(hip.load().pcv_gemm_f32_rows_lnbwd_part_floats(self.M, self.N))
+        if ok and then is not None:
+            b2, c2 = then
+            ok = tuple(b2.shape) == (self.N, self.N) and tuple(c2.shape) == (self.M, self.N) and \
+                all(t.stride(1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0 for t in (b2, c2))
         if ok:
-            self.lnb = (x, scale, st, dres, dx, part, dxd, int(site))
+            self.lnb = (x, scale, st, dres, dx, part, dxd, int(site), then)
             nws = int(hip.load().pcv_gemm_f32_rows_lnout_ws_floats(self.M, self.K))
             self.ws = torch.zeros(nws, dtype=torch.float32, device=dx.device) if nws else None
         return ok
 
     def run(self, rate=0.0, seed=None):
         if self.lnb is not None:
-            x, sc, st, dres, dx, part, dxd, site = self.lnb
+            x, sc, st, dres, dx, part, dxd, site, then = self.lnb
             rate = rate if dxd is not None else 0.0
+            b2, c2 = then if then is not None else (None, None)
             hip.call("pcv_gemm_f32_rows_lnbwd", ptr(self.a), self.a.stride(0), ptr(self.b), self.b.stride(0), self.M,
                      self.N, self.K, ptr(x), x.stride(0), ptr(sc), ptr(st[0]), ptr(st[1]), ptr(dres),
                      dres.stride(0) if dres is not None else 0, ptr(dx), dx.stride(0), ptr(part), part.numel(),
-                     ptr(dxd), dxd.stride(0) if dxd is not None else 0, float(rate), ptr(seed), site, ptr(self.ws),
-                     self.ws.numel() if self.ws is not None else 0, stream_ptr())
+                     ptr(dxd), dxd.stride(0) if dxd is not None else 0, float(rate), ptr(seed), site,
+                     ptr(b2), b2.stride(0) if b2 is not None else 0, ptr(c2), c2.stride(0) if c2 is not None else 0,
+                     ptr(self.ws), self.ws.numel() if self.ws is not None else 0, stream_ptr())
             return
         rate = rate if self.dropout else 0.0
         if self.ln is not None:
@@ -436,6 +443,7 @@ class ViTRunnerF32:
         # at the end of backward adds them all (instead of a small reduction launch per LayerNorm)
         self.ln_red = None
         self.lnb_fused = set()   # (block, 0 | 1): that block's LayerNorm_0 / _1 VJP runs in a data-gradient product
+        self.out_d_fused = set()   # blocks whose out-projection data gradient runs in that launch too
         xcls, dxc = self.xs[-1].view(B, T * D)[:, :D], self.dx.view(B, T * D)[:, :D]
         if self.m.use_layernorm and \
                 K.layernorm_bwd_f32_fits(D, self.dyf, xcls, None, dxc) and \
@@ -448,9 +456,19 @@ class ViTRunnerF32:
                 w, gb = self.w[i], self.gb[i]
                 if not (self.cls_last and i == L - 1) and self.fuse_ln_vjp:
                     dres = self.dx if i == L - 1 else self.dxo[i + 1]
+                    # (+ the out projection's data gradient dO = dx1 Wo^T from the same rows, when out_d is
+                    # that plain product)
+                    od = gb["out_d"]
+                    then = (w["Wo"], self.dO) if (od.fused and od.tb and not od.epi and od.rstep == 1 and
+                                                  od.a.data_ptr() == self.dx1_l[i].data_ptr() and
+                                                  od.c.data_ptr() == self.dO.data_ptr()) else None
                     if gb["fc1_d"].fuse_layernorm_vjp(self.x1s[i], w["s1"], self.st1[i], dres, self.dx1_l[i],
-                                                      self.ln_ws[1 + 2 * i]):
+                                                      self.ln_ws[1 + 2 * i], then=then) or \
+                            gb["fc1_d"].fuse_layernorm_vjp(self.x1s[i], w["s1"], self.st1[i], dres, self.dx1_l[i],
+                                                           self.ln_ws[1 + 2 * i]):
                         self.lnb_fused.add((i, 1))
+                        if gb["fc1_d"].lnb[8] is not None:
+                            self.out_d_fused.add(i)
                 dxd = self.dmo_l[i - 1] if i > 0 else None
                 if self.fuse_ln_vjp and gb["qkv_d"].fuse_layernorm_vjp(self.xs[i], w["s0"], self.st0[i], self.dx1_l[i],
                                                                   self.dxo[i], self.ln_ws[2 + 2 * i], dxd=dxd,
@@ -681,7 +699,8 @@ class ViTRunnerF32:
             else:
                 _epi(self.dy1, dx1, res=dx_in)
             self._colsum(dx1, w["gbo"])
-            g["out_d"].run()                                                           # self.dO = dx1 Wo^T
+            if i not in self.out_d_fused:
+                g["out_d"].run()                                                       # self.dO = dx1 Wo^T
             if self.fused_attn:                                                        # dQ, dK, dV
                 self.attn_bwd(i, rate)
             else:

@@ -157,9 +157,11 @@ def test_gemm_f32_rows_layernorm_of_output_rejects_other_widths(dev):
 # the LayerNorm VJP of the product's rows (pcv_gemm_f32_rows_lnbwd): MLP Dense_0's data gradient -> LayerNorm_1
 # (K = 256) and the qkv data gradient -> LayerNorm_0 with the previous block's dropout VJP (K = 384); vs an fp64
 # product through the fp64 LayerNorm VJP, the partial rows summed against the parameter gradients
-@pytest.mark.parametrize("M,K,rate", [(16448, 256, 0.0), (16448, 384, 0.1), (1000, 256, 0.1), (77, 384, 0.0),
-                                      (64, 128, 0.3)])
-def test_gemm_f32_rows_layernorm_vjp(dev, M, K, rate):
+@pytest.mark.parametrize("M,K,rate,then", [(16448, 256, 0.0, True), (16448, 384, 0.1, False), (1000, 256, 0.1, True),
+                                           (77, 384, 0.0, False), (64, 128, 0.3, True), (16448, 256, 0.0, False)])
+def test_gemm_f32_rows_layernorm_vjp(dev, M, K, rate, then):
+    """then: also the next product of the same rows, C2 = dx B2^T (the out projection's data gradient), in
+    the launch -- checked against fp64 from the kernel's own dx"""
     from plaincv_amd import hip
     from plaincv_amd.hip import ptr, stream_ptr
     from plaincv_amd.models.vit_f32 import _epi_bwd
@@ -183,10 +185,14 @@ def test_gemm_f32_rows_layernorm_vjp(dev, M, K, rate):
     nws = lib.pcv_gemm_f32_rows_lnout_ws_floats(M, K)
     ws = torch.zeros(max(nws, 1), device=dev)
 
+    b2 = (torch.randn(N, N, generator=g) * N ** -0.5).to(dev) if then else None
+    c2 = torch.full((M, N + 8), float("nan"), device=dev)[:, :N] if then else None
+
     def run(out, outd):
         hip.call("pcv_gemm_f32_rows_lnbwd", ptr(a), K, ptr(b), K, M, N, K, ptr(x), N, ptr(sc), ptr(mean), ptr(rstd),
                  ptr(dres), N, ptr(out), out.stride(0), ptr(part), npart, ptr(outd), N if outd is not None else 0,
-                 float(rate), ptr(seed), 11, ptr(ws), nws, stream_ptr())
+                 float(rate), ptr(seed), 11, ptr(b2), N if then else 0, ptr(c2), c2.stride(0) if then else 0, ptr(ws),
+                 nws, stream_ptr())
     run(dx, dxd)
     dy = a.double() @ b.double().t()
     xh = (x.double() - mean.double()[:, None]) * rstd.double()[:, None]
@@ -199,6 +205,10 @@ def test_gemm_f32_rows_layernorm_vjp(dev, M, K, rate):
     ds, db = (dy * xh).sum(0), dy.sum(0)
     assert ((pr[:N] - ds).abs() <= 1e-4 * (1 + ds.abs())).all(), (pr[:N] - ds).abs().max().item()
     assert ((pr[N:] - db).abs() <= 1e-4 * (1 + db.abs())).all(), (pr[N:] - db).abs().max().item()
+    if then:   # the second product from the kernel's own dx rows
+        r2 = dx.double() @ b2.double().t()
+        e2 = (c2.double() - r2).abs()
+        assert (e2 <= 2e-5 * (1 + r2.abs())).all(), e2.max().item()
     if dxd is not None:   # the dropout VJP of the kernel's own dx (same index and bits as the stand-alone VJP)
         dref = torch.empty_like(dxd)
         _epi_bwd(dx.contiguous(), dref, rate=rate, seed=seed, site=11)

@@ -184,6 +184,8 @@ def test_vit_f32_fused_layernorm_vjp_matches_separate(dev, monkeypatch):
         st.runners[tuple(shape)] = r
         # every full-height LayerNorm VJP (the cls-sparse last block's LayerNorm_1 stays in its chain)
         assert len(r.lnb_fused) == (2 * m.num_layers - 1 if fused else 0), sorted(r.lnb_fused)
+        # (+ the out projection's data gradient in the LayerNorm_1 launch of every full-height block)
+        assert len(r.out_d_fused) == (m.num_layers - 1 if fused else 0), sorted(r.out_d_fused)
         r.seed.fill_(5)
         st.params.zero_grad()
         met = r.forward(images, labels, train=True)

@@ -47,9 +47,26 @@ def main():
         def fused():
             hip.call("pcv_gemm_f32_rows_lnbwd", ptr(a), K, ptr(b), K, M, N, K, ptr(x), N, ptr(sc), ptr(mean),
                      ptr(rstd), ptr(dres), N, ptr(dx), N, ptr(part), npart, ptr(dd), N if dd is not None else 0,
-                     float(rate), ptr(seed), 5, ptr(lw), nlw, stream_ptr())
+                     float(rate), ptr(seed), 5, None, 0, None, 0, ptr(lw), nlw, stream_ptr())
         t2, tf = bench.timed_kernel(two, iters=40), bench.timed_kernel(fused, iters=40)
         print(f"K={K} rate={rate}: product + LayerNorm VJP {t2 * 1e6:6.2f} us, fused {tf * 1e6:6.2f} us", flush=True)
+        if K == 256:   # + the out projection's data gradient dO = dx Wo^T: its own launch vs the second product
+            wo = (torch.randn(N, N, generator=g) * N ** -0.5).to(dev)
+            dO = torch.empty(M, N, device=dev)
+            nw2 = int(lib.pcv_gemm_f32_rows_ws_floats(M, N, N, 1, 0))
+            ws2 = torch.zeros(max(nw2, 4), device=dev)
+
+            def fused_then_out():
+                fused()
+                hip.call("pcv_gemm_f32_rows_ws", ptr(dx), N, ptr(wo), N, 1, ptr(dO), N, M, N, N, None, None, 0, None,
+                         0, 1.0, 0, 0.0, None, 0, ptr(ws2), nw2, stream_ptr())
+
+            def fused_out():
+                hip.call("pcv_gemm_f32_rows_lnbwd", ptr(a), K, ptr(b), K, M, N, K, ptr(x), N, ptr(sc), ptr(mean),
+                         ptr(rstd), ptr(dres), N, ptr(dx), N, ptr(part), npart, None, 0, 0.0, ptr(seed), 5, ptr(wo), N,
+                         ptr(dO), N, ptr(lw), nlw, stream_ptr())
+            ta, tb = bench.timed_kernel(fused_then_out, iters=40), bench.timed_kernel(fused_out, iters=40)
+            print(f"  + out-projection dgrad: two launches {ta * 1e6:6.2f} us, one {tb * 1e6:6.2f} us", flush=True)
 
 
 if __name__ == "__main__":
