@@ -94,3 +94,22 @@ def test_python_wrapper_raises_with_entry_point_name(lib):
     from plaincv_amd import hip
     with pytest.raises(RuntimeError, match=r"pcv_cast_f32_bf16 failed: invalid argument \(rc=-1\)"):
         hip.call("pcv_cast_f32_bf16", P(A16), P(A16), -1, None)
+
+
+def _lnbwd(lib, N=128, K=256, A=A16, dx=A16, part_floats=1 << 20, B2=None, C2=None, ldb2=128, rate=0.0, seed=None):
+    return lib.pcv_gemm_f32_rows_lnbwd(P(A), K, P(A16), K, 1000, N, K, P(A16), 128, P(A16), P(A16), P(A16), None, 0,
+                                       P(dx), 128, P(A16), part_floats, None, 0, rate, P(seed) if seed else None, 0,
+                                       P(B2) if B2 else None, ldb2, P(C2) if C2 else None, 128, None, 0, None)
+
+
+def test_fp32_layernorm_vjp_product_entry_point(lib):
+    """pcv_gemm_f32_rows_lnbwd: the width, the partial buffer, the optional second product (both or neither)"""
+    assert lib.pcv_gemm_f32_rows_lnbwd_part_floats(1000, 128) == 32 * 2 * 128
+    assert _lnbwd(lib, N=256) == EINVAL                       # a whole row per 128-wide tile
+    assert _lnbwd(lib, K=96) == EINVAL                        # K % 64
+    assert _lnbwd(lib, part_floats=100) == EINVAL             # fewer partial rows than 32-row tiles
+    assert _lnbwd(lib, B2=A16) == EINVAL                      # B2 without C2
+    assert _lnbwd(lib, B2=A16, C2=A16, ldb2=64) == EINVAL      # B2 rows shorter than N
+    assert _lnbwd(lib, rate=0.1) == EINVAL                    # dropout without a seed (it has no dxd either)
+    assert _lnbwd(lib, A=A2) == EALIGN
+    assert _lnbwd(lib, dx=A2) == EALIGN
