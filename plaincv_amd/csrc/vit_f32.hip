@@ -583,15 +583,16 @@ __global__ __launch_bounds__(256) void patch_embed_fold_kernel(const float* __re
     const int k = o / D4, d = (o % D4) * 4;
     const float* p = ws + (int64_t)k * D + d;
     const int64_t st = (int64_t)(Kp + 1) * D;
-    int t = q;
-    for (; t + 32 * 3 < NT; t += 32 * 4) {
-      const f32x4 a0 = *reinterpret_cast<const f32x4*>(p + t * st);
-      const f32x4 a1 = *reinterpret_cast<const f32x4*>(p + (t + 32) * st);
-      const f32x4 a2 = *reinterpret_cast<const f32x4*>(p + (t + 64) * st);
-      const f32x4 a3 = *reinterpret_cast<const f32x4*>(p + (t + 96) * st);
-      acc += a0; acc += a1; acc += a2; acc += a3;
+    // batches of 8 tokens with every load in flight (the ViT's 256 tokens: one batch), masked to + 0 past
+    // NT; added in token order
+    for (int t = q; t < NT; t += 32 * 8) {
+      f32x4 a[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        a[j] = t + 32 * j < NT ? *reinterpret_cast<const f32x4*>(p + (t + 32 * j) * st) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += a[j];
     }
-    for (; t < NT; t += 32) acc += *reinterpret_cast<const f32x4*>(p + t * st);
   }
   part[q][threadIdx.x & 7] = acc;
   __syncthreads();
