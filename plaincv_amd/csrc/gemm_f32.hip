@@ -528,12 +528,10 @@ template <int BN>
 __global__ __launch_bounds__(256) void wgrad_fold_kernel(const WgJob* __restrict__ jobs, int njobs) {
   constexpr int CPR = BN / 4, RPB = 256 / CPR, BPT = GR_BM / RPB;
   const int b = blockIdx.x / BPT, rg = blockIdx.x % BPT;
-  int lo = 0, hi = njobs - 1;   // last job whose first fold tile <= b (jobs without a fold hold 0 tiles)
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (jobs[mid].ffirst <= b) lo = mid; else hi = mid - 1;
-  }
-  const WgJob& jb = jobs[lo];
+  // last job whose first fold tile <= b (jobs without a fold hold 0 tiles), searched in LDS: the table's
+  // ffirst column loaded in one round trip instead of a chain of dependent global loads
+  __shared__ int ft[256];
+  const WgJob& jb = jobs[pcv_find_job<int32_t>(jobs, njobs, (int)sizeof(WgJob), (int)offsetof(WgJob, ffirst), ft, 256, b)];
   const int t = b - jb.ffirst;
   const int m0 = (t / jb.tiles_n) * GR_BM, n0 = (t % jb.tiles_n) * BN;
   const int rr = rg * RPB + threadIdx.x / CPR, c = (threadIdx.x % CPR) * 4;
@@ -556,15 +554,13 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(const WgJob* __restrict
   if (jb.colsum && m0 == 0 && rg == 0 && threadIdx.x < BN) {   // the first panel's column partials
     const float* qp = jb.ws + (int64_t)jb.tiles * S * (GR_BM * BN) + (int64_t)(n0 / BN) * S * BN + threadIdx.x;
     float v = 0.f;
-    int u = 0;
-    for (; u + 8 <= S; u += 8) {   // 8 loads in flight, added in slice order
-      float x[8];
+    for (int u = 0; u < S; u += 16) {   // 16 loads in flight (masked to + 0 past S), added in slice order
+      float x[16];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) x[e] = qp[(int64_t)(u + e) * BN];
+      for (int e = 0; e < 16; ++e) x[e] = u + e < S ? qp[(int64_t)(u + e) * BN] : 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v += x[e];
+      for (int e = 0; e < 16; ++e) v += x[e];
     }
-    for (; u < S; ++u) v += qp[(int64_t)u * BN];
     jb.colsum[n0 + threadIdx.x] += v;
   }
 }
